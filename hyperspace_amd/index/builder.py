@@ -1,0 +1,98 @@
+"""Index data builder: the build hot path (SURVEY §3.1 "HOT LOOP", kernels K1-K6).
+
+``build_from_source``  scan source files (K1) -> attach lineage ids (K2, a per-file constant —
+                       no broadcast join needed) -> Murmur3 bucket + partition (K3) ->
+                       sort within bucket (K4) -> one Parquet file per bucket.
+``rewrite_buckets``    per-bucket merge of existing index files, optionally dropping rows whose
+                       ``_data_file_id`` was deleted (K5, incremental refresh) — used by optimize
+                       (K6) as well.  The bucket is known from the file name, so no re-hash.
+
+Each function dispatches to the MI355X device pipeline (``exec.device_build``) when the session
+executes on GPU, or to the host oracle below.  Under ``torch.distributed`` the device pipeline
+shuffles rows with RCCL all-to-all so that bucket ``b`` is written by rank ``b % world``.
+"""
+from __future__ import annotations
+
+import uuid
+from typing import Dict, List, Optional
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.compute as pc
+
+from ..io.reader import read_files
+from ..io.writer import get_bucket_id, sort_indices_by, write_bucket_file, write_bucketed_table
+from ..utils import path_utils as P
+from ..utils.conf import HyperspaceConf
+from . import constants as C
+
+
+def source_format(rel) -> str:
+    return "parquet" if rel.file_format == "delta" or rel.is_index() else rel.file_format
+
+
+def read_index_input(rel, files: List[str], columns: List[str], lineage_ids: Optional[Dict[str, int]]):
+    """Read the index columns of ``files`` (+ ``_data_file_id`` when lineage is on)."""
+    t, fidx = read_files(source_format(rel), files, rel.data_schema, rel.options,
+                         rel.location.partition_spec, columns, with_file_index=True)
+    if lineage_ids is not None:
+        ids = np.array([lineage_ids[f] for f in files], dtype=np.int64)
+        fi = fidx.to_numpy() if hasattr(fidx, "to_numpy") else np.asarray(fidx)
+        t = t.append_column(pa.field(C.DATA_FILE_NAME_ID, pa.int64(), False),
+                            pa.array(ids[np.asarray(fi, dtype=np.int64)] if len(fi) else
+                                     np.zeros(0, np.int64)))
+    return t
+
+
+def build_from_source(session, rel, files: List[str], columns: List[str], indexed: List[str],
+                      num_buckets: int, out_path: str, lineage_ids: Optional[Dict[str, int]],
+                      mode: str = "overwrite") -> List[str]:
+    if session.device_kind() == "gpu":
+        from ..exec.device_build import device_build_from_source
+        return device_build_from_source(session, rel, files, columns, indexed, num_buckets,
+                                        out_path, lineage_ids, mode)
+    t = read_index_input(rel, files, columns, lineage_ids)
+    return write_bucketed_table(t, out_path, num_buckets, indexed, mode,
+                                HyperspaceConf.index_file_codec(session.conf),
+                                HyperspaceConf.index_row_group_rows(session.conf),
+                                job_uuid=str(uuid.uuid4()))
+
+
+def group_by_bucket(files: List[str]) -> Dict[int, List[str]]:
+    out: Dict[int, List[str]] = {}
+    for f in files:
+        b = get_bucket_id(P.get_name(f))
+        out.setdefault(-1 if b is None else b, []).append(f)
+    return out
+
+
+def rewrite_buckets(session, files: List[str], indexed: List[str], out_path: str,
+                    deleted_ids: Optional[List[int]] = None, num_buckets: int = None) -> List[str]:
+    """Merge every bucket's files into one sorted file, optionally dropping deleted lineage ids."""
+    if session.device_kind() == "gpu":
+        from ..exec.device_build import device_rewrite_buckets
+        return device_rewrite_buckets(session, files, indexed, out_path, deleted_ids, num_buckets)
+    import pyarrow.parquet as pq
+    codec = HyperspaceConf.index_file_codec(session.conf)
+    rg = HyperspaceConf.index_row_group_rows(session.conf)
+    job = str(uuid.uuid4())
+    out = []
+    dist = getattr(session, "dist", None)
+    for b, fs in sorted(group_by_bucket(files).items()):
+        if dist is not None and b % dist.world != dist.rank:
+            continue
+        t = pa.concat_tables([pq.read_table(P.to_local(f)) for f in fs])
+        if deleted_ids:
+            mask = pc.invert(pc.is_in(t.column(C.DATA_FILE_NAME_ID),
+                                      value_set=pa.array(deleted_ids, pa.int64())))
+            t = t.filter(mask)
+        if t.num_rows == 0:
+            continue
+        if len(fs) > 1:
+            t = t.take(pa.array(sort_indices_by(t, indexed)))
+        if b < 0:
+            out += write_bucketed_table(t, out_path, num_buckets, indexed, "append", codec, rg,
+                                        job_uuid=job)
+        else:
+            out.append(write_bucket_file(t, out_path, 0, job, b, codec, rg))
+    return out

@@ -1,0 +1,95 @@
+"""All configuration keys and on-disk constants (reference ``index/IndexConstants.scala:21-107``).
+
+Key strings are identical to the reference so existing configurations keep working.  Keys under
+``spark.hyperspace.mi.*`` are MI355X-specific additions (device executor, HBM budget, ...).
+"""
+
+INDEXES_DIR = "indexes"
+INDEX_SYSTEM_PATH = "spark.hyperspace.system.path"
+WAREHOUSE_DIR = "spark.sql.warehouse.dir"
+
+INDEX_NUM_BUCKETS_LEGACY = "spark.hyperspace.index.num.buckets"
+INDEX_NUM_BUCKETS = "spark.hyperspace.index.numBuckets"
+# Compiled default of spark.sql.shuffle.partitions (Appendix B quirk 8): NOT the runtime value.
+INDEX_NUM_BUCKETS_DEFAULT = 200
+
+INDEX_HYBRID_SCAN_ENABLED = "spark.hyperspace.index.hybridscan.enabled"
+INDEX_HYBRID_SCAN_ENABLED_DEFAULT = "false"
+INDEX_HYBRID_SCAN_DELETED_RATIO_THRESHOLD = "spark.hyperspace.index.hybridscan.maxDeletedRatio"
+INDEX_HYBRID_SCAN_DELETED_RATIO_THRESHOLD_DEFAULT = "0.2"
+INDEX_HYBRID_SCAN_APPENDED_RATIO_THRESHOLD = "spark.hyperspace.index.hybridscan.maxAppendedRatio"
+INDEX_HYBRID_SCAN_APPENDED_RATIO_THRESHOLD_DEFAULT = "0.3"
+
+INDEX_RELATION_IDENTIFIER = ("indexRelation", "true")
+
+INDEX_CACHE_EXPIRY_DURATION_SECONDS = "spark.hyperspace.index.cache.expiryDurationInSeconds"
+INDEX_CACHE_EXPIRY_DURATION_SECONDS_DEFAULT = "300"
+
+HYPERSPACE_LOG = "_hyperspace_log"
+INDEX_VERSION_DIRECTORY_PREFIX = "v__"
+LATEST_STABLE_LOG_NAME = "latestStable"
+
+DISPLAY_MODE = "spark.hyperspace.explain.displayMode"
+HIGHLIGHT_BEGIN_TAG = "spark.hyperspace.explain.displayMode.highlight.beginTag"
+HIGHLIGHT_END_TAG = "spark.hyperspace.explain.displayMode.highlight.endTag"
+
+
+class DisplayMode:
+    CONSOLE = "console"
+    PLAIN_TEXT = "plaintext"
+    HTML = "html"
+
+
+DATA_FILE_NAME_ID = "_data_file_id"
+INDEX_LINEAGE_ENABLED = "spark.hyperspace.index.lineage.enabled"
+INDEX_LINEAGE_ENABLED_DEFAULT = "false"
+
+REFRESH_MODE_INCREMENTAL = "incremental"
+REFRESH_MODE_FULL = "full"
+REFRESH_MODE_QUICK = "quick"
+
+OPTIMIZE_FILE_SIZE_THRESHOLD = "spark.hyperspace.index.optimize.fileSizeThreshold"
+OPTIMIZE_FILE_SIZE_THRESHOLD_DEFAULT = 256 * 1024 * 1024
+OPTIMIZE_MODE_QUICK = "quick"
+OPTIMIZE_MODE_FULL = "full"
+OPTIMIZE_MODES = (OPTIMIZE_MODE_QUICK, OPTIMIZE_MODE_FULL)
+
+UNKNOWN_FILE_ID = -1
+
+LINEAGE_PROPERTY = "lineage"
+HAS_PARQUET_AS_SOURCE_FORMAT_PROPERTY = "hasParquetAsSourceFormat"
+
+GLOBBING_PATTERN_KEY = "spark.hyperspace.source.globbingPattern"
+
+EVENT_LOGGER_CLASS_KEY = "spark.hyperspace.eventLoggerClass"
+FILE_BASED_SOURCE_BUILDERS = "spark.hyperspace.index.sources.fileBasedBuilders"
+FILE_BASED_SOURCE_BUILDERS_DEFAULT = "hyperspace_amd.sources.default.DefaultFileBasedSourceBuilder"
+DEFAULT_SOURCE_SUPPORTED_FORMATS = \
+    "spark.hyperspace.index.sources.defaultFileBasedSource.supportedFileFormats"
+DEFAULT_SOURCE_SUPPORTED_FORMATS_DEFAULT = "avro,csv,json,orc,parquet,text"
+
+# Spark SQL keys the engine honours.
+SQL_CASE_SENSITIVE = "spark.sql.caseSensitive"
+SQL_SHUFFLE_PARTITIONS = "spark.sql.shuffle.partitions"
+SQL_AUTO_BROADCAST_JOIN_THRESHOLD = "spark.sql.autoBroadcastJoinThreshold"
+SQL_IN_SET_CONVERSION_THRESHOLD = "spark.sql.optimizer.inSetConversionThreshold"
+
+# ---- MI355X-native additions -------------------------------------------------------------
+# Execution device for physical plans: "auto" (GPU when available), "gpu", "cpu".
+EXEC_DEVICE = "spark.hyperspace.mi.execution.device"
+EXEC_DEVICE_DEFAULT = "auto"
+# Per-GPU HBM budget for the resident index-column cache (bytes); 0 = disabled.
+DEVICE_CACHE_BYTES = "spark.hyperspace.mi.deviceCacheBytes"
+DEVICE_CACHE_BYTES_DEFAULT = str(160 * 1024 ** 3)
+# Index data file encoding written by the build: "plain" (GPU-decodable, uncompressed) or
+# "snappy" (pyarrow default, host decode).
+INDEX_FILE_CODEC = "spark.hyperspace.mi.index.codec"
+INDEX_FILE_CODEC_DEFAULT = "none"
+# Rows per Parquet row group in index files (row-group stats drive pruning).
+INDEX_ROW_GROUP_ROWS = "spark.hyperspace.mi.index.rowGroupRows"
+INDEX_ROW_GROUP_ROWS_DEFAULT = "1048576"
+# Capture the steady-state query pipeline in a hipGraph.
+HIPGRAPH_ENABLED = "spark.hyperspace.mi.hipGraph.enabled"
+HIPGRAPH_ENABLED_DEFAULT = "true"
+# Fault-injection hook for action crash tests: after_begin | mid_op | before_end.
+FAULT_INJECTION = "spark.hyperspace.mi.faultInjection"

@@ -1,0 +1,56 @@
+"""QueryExecution: analyzed -> optimized -> physical -> executed plan, then run on a backend."""
+from __future__ import annotations
+
+import pyarrow as pa
+
+from .optimizer import Optimizer
+from .physical import Planner, ensure_requirements
+
+
+class QueryExecution:
+    def __init__(self, session, logical):
+        self.session = session
+        self.logical = logical
+        self._optimized = None
+        self._spark_plan = None
+        self._executed = None
+
+    @property
+    def analyzed(self):
+        return self.logical
+
+    @property
+    def optimized_plan(self):
+        if self._optimized is None:
+            self._optimized = Optimizer(self.session).execute(self.logical)
+        return self._optimized
+
+    optimizedPlan = optimized_plan
+
+    @property
+    def spark_plan(self):
+        if self._spark_plan is None:
+            self._spark_plan = Planner(self.session).plan(self.optimized_plan)
+        return self._spark_plan
+
+    sparkPlan = spark_plan
+
+    @property
+    def executed_plan(self):
+        if self._executed is None:
+            self._executed = ensure_requirements(self.spark_plan, self.session)
+        return self._executed
+
+    executedPlan = executed_plan
+
+    def to_arrow(self) -> pa.Table:
+        backend = self.session.backend()
+        return backend.collect(self.executed_plan)
+
+    def explain_string(self, extended: bool = False) -> str:
+        parts = []
+        if extended:
+            parts += ["== Analyzed Logical Plan ==", self.logical.tree_string(),
+                      "== Optimized Logical Plan ==", self.optimized_plan.tree_string()]
+        parts += ["== Physical Plan ==", self.executed_plan.tree_string()]
+        return "\n".join(parts)
