@@ -1,0 +1,162 @@
+"""ctypes binding to ``libhs_kernels.so`` (the HIP/CDNA4 kernels in ``csrc/kernels``).
+
+The C structs are mirrored with ``ctypes.Structure`` and their sizes are checked against the
+library at load time, so an ABI drift fails loudly instead of corrupting kernel arguments.
+On a machine with a GPU a missing library is an error (never a silent host fallback).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_HERE, "_native", "libhs_kernels.so")
+
+MAX_COLS = 16
+MAX_PREDS = 16
+MAX_AGGS = 8
+MAX_TERMS = 3
+HASH_MAX_COLS = 8
+GATHER_MAX_COLS = 32
+
+# HsType
+I8, I16, I32, I64, F32, F64, BOOL, U32, U64 = range(9)
+STR = 100
+# PredKind
+PK_INT_LIT, PK_FLT_LIT, PK_INT_COL, PK_FLT_COL, PK_IS_NULL, PK_NOT_NULL, PK_IN_SET, PK_BITMAP, \
+    PK_TRUE = range(9)
+# CmpOp
+OP_EQ, OP_NE, OP_LT, OP_LE, OP_GT, OP_GE = range(6)
+# AggKind
+AK_SUM, AK_COUNT, AK_MIN, AK_MAX, AK_COUNT_STAR = range(5)
+
+
+class ColDesc(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("valid", C.c_void_p), ("type", C.c_int32),
+                ("pad", C.c_int32)]
+
+
+class HashCol(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("valid", C.c_void_p), ("offsets", C.c_void_p),
+                ("type", C.c_int32), ("pad", C.c_int32)]
+
+
+class HashParams(C.Structure):
+    _fields_ = [("cols", HashCol * HASH_MAX_COLS), ("ncols", C.c_int32),
+                ("num_buckets", C.c_int32), ("seed", C.c_uint32), ("pad", C.c_int32)]
+
+
+class Pred(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("op", C.c_int32), ("col", C.c_int32), ("col2", C.c_int32),
+                ("group", C.c_int32), ("set_len", C.c_int32), ("ilit", C.c_int64),
+                ("flit", C.c_double), ("set", C.c_void_p)]
+
+
+class AggSpec(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("nterms", C.c_int32), ("col", C.c_int32 * MAX_TERMS),
+                ("pad", C.c_int32), ("alpha", C.c_double * MAX_TERMS),
+                ("beta", C.c_double * MAX_TERMS)]
+
+
+class ScanParams(C.Structure):
+    _fields_ = [("cols", ColDesc * MAX_COLS), ("preds", Pred * MAX_PREDS),
+                ("aggs", AggSpec * MAX_AGGS), ("npreds", C.c_int32), ("naggs", C.c_int32),
+                ("group_col", C.c_int32), ("num_groups", C.c_int32), ("group_base", C.c_int64)]
+
+
+class JoinParams(C.Structure):
+    _fields_ = [("cols", ColDesc * MAX_COLS), ("preds", Pred * MAX_PREDS),
+                ("aggs", AggSpec * MAX_AGGS), ("npreds", C.c_int32), ("nlp", C.c_int32),
+                ("naggs", C.c_int32), ("lkey", C.c_int32), ("rkey", C.c_int32),
+                ("group_col", C.c_int32), ("num_groups", C.c_int32), ("key_is_float", C.c_int32),
+                ("group_base", C.c_int64)]
+
+
+class SortKeySpec(C.Structure):
+    _fields_ = [("col", ColDesc), ("kmin", C.c_uint64), ("bits", C.c_int32),
+                ("has_nulls", C.c_int32)]
+
+
+class GatherCol(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("src_valid", C.c_void_p),
+                ("dst_valid", C.c_void_p), ("elem_bytes", C.c_int32), ("pad", C.c_int32)]
+
+
+class GatherParams(C.Structure):
+    _fields_ = [("cols", GatherCol * GATHER_MAX_COLS), ("ncols", C.c_int32),
+                ("idx_is_u32", C.c_int32)]
+
+
+_lib = None
+
+
+class NativeMissing(RuntimeError):
+    pass
+
+
+def _sig(fn, restype, *args):
+    fn.restype = restype
+    fn.argtypes = list(args)
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeMissing(f"{LIB_PATH} not built; run `python -m hyperspace_amd._native.build`")
+    L = C.CDLL(LIB_PATH)
+    P, I, I64, U64 = C.c_void_p, C.c_int, C.c_int64, C.c_uint64
+    for name, st in (("hs_hash_params_size", HashParams), ("hs_scan_params_size", ScanParams),
+                     ("hs_join_params_size", JoinParams), ("hs_sort_key_spec_size", SortKeySpec),
+                     ("hs_gather_params_size", GatherParams)):
+        f = getattr(L, name)
+        f.restype = C.c_int
+        if f() != C.sizeof(st):
+            raise RuntimeError(f"ABI mismatch for {st.__name__}: lib {f()} vs ctypes {C.sizeof(st)}")
+    _sig(L.hs_murmur3_bucket, I, P, I64, P, P, P)
+    _sig(L.hs_murmur3_hash, I, P, I64, P, P)
+    _sig(L.hs_sort_workspace_bytes, I64, I64)
+    _sig(L.hs_sort_columns, I, P, I, I64, P, I, P, I64, P)
+    _sig(L.hs_scan_tmp_elems, I64, I64)
+    _sig(L.hs_exclusive_scan_i64, I, P, P, I64, P, I64, P)
+    _sig(L.hs_exclusive_scan_u32, I, P, P, I64, P, I64, P)
+    _sig(L.hs_gather, I, P, P, I64, P)
+    _sig(L.hs_bucket_offsets, I, P, I64, I, P, P)
+    _sig(L.hs_scan_tile_rows, I)
+    _sig(L.hs_scan_grid, I)
+    _sig(L.hs_join_tile_rows, I)
+    _sig(L.hs_range_search, I, P, P, P, I, I, U64, I, I, U64, I, P, P, P, P)
+    _sig(L.hs_ranges_to_tiles, I, P, I, P, P)
+    _sig(L.hs_scan_agg, I, P, P, P, I, P, I, P, P, P, P, P, P, P, P, P)
+    _sig(L.hs_scan_count, I, P, P, P, I, P, I, P, P)
+    _sig(L.hs_scan_select, I, P, P, P, I, P, P, I, P, P)
+    _sig(L.hs_join_agg, I, P, P, P, P, P, I, P, I, P, P, P, P, P)
+    _sig(L.hs_join_count, I, P, P, P, P, P, I, P, I, P, P)
+    _sig(L.hs_join_emit, I, P, P, P, P, P, I, P, I, P, P, P, P)
+    if L.hs_scan_tile_rows() != L.hs_join_tile_rows():
+        raise RuntimeError("scan/join tile sizes differ")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with code {rc}")
+
+
+def stream_ptr():
+    import torch
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except (NativeMissing, OSError):
+        return False

@@ -1,0 +1,308 @@
+"""Python entry points for the HIP kernels.  All buffers are torch tensors on the current device;
+every launch goes on the current torch stream (so it composes with torch ops, RCCL collectives and
+hipGraph capture).  Kernels never allocate; workspaces are torch allocations made here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib as NL
+
+
+def _torch():
+    import torch
+    return torch
+
+
+# ------------------------------------------------------------------------------------------------
+# K3: Spark Murmur3 bucketing
+# ------------------------------------------------------------------------------------------------
+def _hash_params(cols, num_buckets: int, seed: int = 42) -> NL.HashParams:
+    if len(cols) > NL.HASH_MAX_COLS:
+        raise ValueError("too many bucket columns")
+    p = NL.HashParams()
+    for i, c in enumerate(cols):
+        if c.dictionary is not None:
+            if c.offsets is None:
+                raise ValueError("string bucket column needs raw bytes (raw_strings=True)")
+            p.cols[i] = NL.HashCol(c.chars.data_ptr(), c.valid.data_ptr() if c.valid is not None else 0,
+                                   c.offsets.data_ptr(), NL.STR, 0)
+        else:
+            p.cols[i] = NL.HashCol(c.data.data_ptr(),
+                                   c.valid.data_ptr() if c.valid is not None else 0, 0, c.hs_type, 0)
+    p.ncols = len(cols)
+    p.num_buckets = int(num_buckets)
+    p.seed = seed
+    return p
+
+
+def murmur3_bucket(cols, num_buckets: int, with_counts: bool = True):
+    """Returns (bucket int32 [n], counts int64 [num_buckets] or None)."""
+    torch = _torch()
+    n = len(cols[0])
+    dev = cols[0].data.device
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    counts = torch.zeros(num_buckets, dtype=torch.int64, device=dev) if with_counts else None
+    p = _hash_params(cols, num_buckets)
+    NL.check(NL.lib().hs_murmur3_bucket(C.byref(p), n, NL.ptr(out), NL.ptr(counts), NL.stream_ptr()),
+             "hs_murmur3_bucket")
+    return out, counts
+
+
+def murmur3_hash(cols):
+    torch = _torch()
+    n = len(cols[0])
+    out = torch.empty(n, dtype=torch.int32, device=cols[0].data.device)
+    p = _hash_params(cols, 1)
+    NL.check(NL.lib().hs_murmur3_hash(C.byref(p), n, NL.ptr(out), NL.stream_ptr()), "hs_murmur3_hash")
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# K4: radix sort -> permutation
+# ------------------------------------------------------------------------------------------------
+def _sortable_range(col) -> tuple:
+    """(kmin, bits) of the order-preserving image over valid rows (host sync: one small D2H)."""
+    torch = _torch()
+    d = col.data
+    if col.valid is not None:
+        vm = col.valid.bool()
+        if not bool(vm.any()):
+            return 0, 0
+        d = d[vm]
+    if d.numel() == 0:
+        return 0, 0
+    lo, hi = torch.aminmax(d)
+    lo, hi = lo.item(), hi.item()
+    t = col.hs_type
+    if t in (NL.F32, NL.F64):
+        return 0, 32 if t == NL.F32 else 64
+    width = {NL.I8: 8, NL.I16: 16, NL.I32: 32, NL.I64: 64, NL.BOOL: 8, NL.U32: 32, NL.U64: 64}[t]
+    if t in (NL.BOOL, NL.U32, NL.U64):
+        kmin = int(lo)
+    else:
+        kmin = (int(lo) + (1 << (width - 1))) & ((1 << width) - 1)
+    span = int(hi) - int(lo)
+    bits = max(1, span.bit_length()) if span > 0 else 0
+    return kmin, bits
+
+
+def sort_permutation(key_cols: Sequence, init_perm=None, extra_leading=None):
+    """Stable ascending (NULLS FIRST) permutation over ``key_cols`` (most significant first).
+
+    ``extra_leading`` is an optional (int32 tensor, bits) most-significant key (e.g. bucket ids).
+    """
+    torch = _torch()
+    from ..exec.device_table import DeviceColumn
+    import pyarrow as pa
+    cols = list(key_cols)
+    if extra_leading is not None:
+        t, _bits = extra_leading
+        cols = [DeviceColumn(t, None, pa.int32())] + cols
+    n = len(cols[0])
+    dev = cols[0].data.device
+    specs = (NL.SortKeySpec * len(cols))()
+    for i, c in enumerate(cols):
+        kmin, bits = _sortable_range(c)
+        specs[i] = NL.SortKeySpec(c.desc(), kmin, bits, 1 if c.valid is not None else 0)
+    L = NL.lib()
+    ws = torch.empty(int(L.hs_sort_workspace_bytes(n)), dtype=torch.uint8, device=dev)
+    if init_perm is None:
+        perm = torch.empty(n, dtype=torch.int32, device=dev)
+        init = 0
+    else:
+        perm = init_perm.clone()
+        init = 1
+    NL.check(L.hs_sort_columns(specs, len(cols), n, NL.ptr(perm), init, NL.ptr(ws), ws.numel(),
+                               NL.stream_ptr()), "hs_sort_columns")
+    return perm
+
+
+def exclusive_scan_i64(x):
+    torch = _torch()
+    n = x.numel()
+    out = torch.empty_like(x)
+    L = NL.lib()
+    tmp = torch.empty(max(1, int(L.hs_scan_tmp_elems(n))), dtype=torch.int64, device=x.device)
+    NL.check(L.hs_exclusive_scan_i64(NL.ptr(x), NL.ptr(out), n, NL.ptr(tmp), tmp.numel(),
+                                     NL.stream_ptr()), "hs_exclusive_scan_i64")
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# Gather
+# ------------------------------------------------------------------------------------------------
+def gather_columns(cols: list, idx, want_valid: bool = True) -> list:
+    """Gather a list of DeviceColumns by ``idx`` (int32 or int64 tensor) in one launch."""
+    torch = _torch()
+    from ..exec.device_table import DeviceColumn
+    n = idx.numel()
+    out = []
+    for i in range(0, len(cols), NL.GATHER_MAX_COLS):
+        chunk = cols[i:i + NL.GATHER_MAX_COLS]
+        p = NL.GatherParams()
+        res = []
+        for j, c in enumerate(chunk):
+            dst = torch.empty(n, dtype=c.data.dtype, device=c.data.device)
+            dv = torch.empty(n, dtype=torch.uint8, device=c.data.device) \
+                if (c.valid is not None and want_valid) else None
+            p.cols[j] = NL.GatherCol(c.data.data_ptr(), dst.data_ptr(),
+                                     c.valid.data_ptr() if c.valid is not None else 0,
+                                     dv.data_ptr() if dv is not None else 0,
+                                     c.data.element_size(), 0)
+            res.append(DeviceColumn(dst, dv, c.atype, c.dictionary))
+        p.ncols = len(chunk)
+        p.idx_is_u32 = 1 if idx.dtype == torch.int32 else 0
+        NL.check(NL.lib().hs_gather(C.byref(p), NL.ptr(idx), n, NL.stream_ptr()), "hs_gather")
+        out.extend(res)
+    return out
+
+
+def bucket_offsets_from_sorted(sorted_bucket, num_buckets: int):
+    torch = _torch()
+    off = torch.empty(num_buckets + 1, dtype=torch.int64, device=sorted_bucket.device)
+    NL.check(NL.lib().hs_bucket_offsets(NL.ptr(sorted_bucket), sorted_bucket.numel(), num_buckets,
+                                        NL.ptr(off), NL.stream_ptr()), "hs_bucket_offsets")
+    return off
+
+
+# ------------------------------------------------------------------------------------------------
+# Scan: ranges, filter+aggregate, filter+select
+# ------------------------------------------------------------------------------------------------
+def range_search(key_col, bucket_off, buckets=None, lo=None, lo_incl=True, hi=None, hi_incl=True):
+    """Per-bucket [start, len) of rows whose sorted key lies in the bound interval.
+
+    ``lo``/``hi`` are sortable uint64 images (see ``sortable_image``); None = unbounded.
+    Returns (rstart, rlen, rbucket) int64/int64/int32 device tensors of length nb.
+    """
+    torch = _torch()
+    dev = bucket_off.device
+    nb = (buckets.numel() if buckets is not None else bucket_off.numel() - 1)
+    rstart = torch.empty(nb, dtype=torch.int64, device=dev)
+    rlen = torch.empty(nb, dtype=torch.int64, device=dev)
+    rbucket = torch.empty(nb, dtype=torch.int32, device=dev)
+    kd = key_col.desc()
+    NL.check(NL.lib().hs_range_search(C.byref(kd), NL.ptr(bucket_off), NL.ptr(buckets), nb,
+                                      1 if lo is not None else 0, int(lo or 0), 1 if lo_incl else 0,
+                                      1 if hi is not None else 0, int(hi or 0), 1 if hi_incl else 0,
+                                      NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket), NL.stream_ptr()),
+             "hs_range_search")
+    return rstart, rlen, rbucket
+
+
+def full_ranges(bucket_off_host: np.ndarray, device, buckets: Optional[List[int]] = None):
+    torch = _torch()
+    off = bucket_off_host
+    bs = np.arange(len(off) - 1) if buckets is None else np.asarray(buckets, dtype=np.int64)
+    rstart = torch.from_numpy(off[bs].astype(np.int64)).to(device)
+    rlen = torch.from_numpy((off[bs + 1] - off[bs]).astype(np.int64)).to(device)
+    rbucket = torch.from_numpy(bs.astype(np.int32)).to(device)
+    return rstart, rlen, rbucket
+
+
+def ranges_to_tiles(rlen):
+    torch = _torch()
+    R = rlen.numel()
+    tp = torch.empty(R + 1, dtype=torch.int64, device=rlen.device)
+    NL.check(NL.lib().hs_ranges_to_tiles(NL.ptr(rlen), R, NL.ptr(tp), NL.stream_ptr()),
+             "hs_ranges_to_tiles")
+    return tp
+
+
+def sortable_image(value, hs_type: int) -> int:
+    """Host mirror of hs_sortable for a literal."""
+    import struct
+    if hs_type == NL.F64:
+        b = struct.unpack("<Q", struct.pack("<d", float(value)))[0]
+        return (~b) & 0xFFFFFFFFFFFFFFFF if b >> 63 else b | (1 << 63)
+    if hs_type == NL.F32:
+        b = struct.unpack("<I", struct.pack("<f", float(value)))[0]
+        return ((~b) & 0xFFFFFFFF) if b >> 31 else (b | 0x80000000)
+    width = {NL.I8: 8, NL.I16: 16, NL.I32: 32, NL.I64: 64}.get(hs_type)
+    if width is None:
+        return int(value)
+    return (int(value) + (1 << (width - 1))) & ((1 << width) - 1)
+
+
+def scan_agg(params: NL.ScanParams, rstart, rlen, tile_prefix, grid: int = None):
+    """Returns (sum f64 [GA], count i64 [GA], min f64 [GA], max f64 [GA]) device tensors."""
+    torch = _torch()
+    L = NL.lib()
+    grid = grid or L.hs_scan_grid()
+    GA = params.naggs * (params.num_groups if params.group_col >= 0 else 1)
+    dev = rstart.device
+    ps = torch.empty(grid * GA, dtype=torch.float64, device=dev)
+    pc_ = torch.empty(grid * GA, dtype=torch.int64, device=dev)
+    pmn = torch.empty(grid * GA, dtype=torch.float64, device=dev)
+    pmx = torch.empty(grid * GA, dtype=torch.float64, device=dev)
+    os_ = torch.empty(GA, dtype=torch.float64, device=dev)
+    oc = torch.empty(GA, dtype=torch.int64, device=dev)
+    omn = torch.empty(GA, dtype=torch.float64, device=dev)
+    omx = torch.empty(GA, dtype=torch.float64, device=dev)
+    NL.check(L.hs_scan_agg(C.byref(params), NL.ptr(rstart), NL.ptr(rlen), rstart.numel(),
+                           NL.ptr(tile_prefix), grid, NL.ptr(ps), NL.ptr(pc_), NL.ptr(pmn),
+                           NL.ptr(pmx), NL.ptr(os_), NL.ptr(oc), NL.ptr(omn), NL.ptr(omx),
+                           NL.stream_ptr()), "hs_scan_agg")
+    return os_, oc, omn, omx
+
+
+def scan_select(params: NL.ScanParams, rstart, rlen, tile_prefix, max_tiles: int):
+    """Row ids (int64, ascending within each range) of rows passing the predicate."""
+    torch = _torch()
+    L = NL.lib()
+    grid = L.hs_scan_grid()
+    dev = rstart.device
+    counts = torch.zeros(max_tiles + 1, dtype=torch.int64, device=dev)
+    NL.check(L.hs_scan_count(C.byref(params), NL.ptr(rstart), NL.ptr(rlen), rstart.numel(),
+                             NL.ptr(tile_prefix), grid, NL.ptr(counts), NL.stream_ptr()),
+             "hs_scan_count")
+    offs = exclusive_scan_i64(counts)
+    total = int(offs[-1].item())
+    out = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
+    NL.check(L.hs_scan_select(C.byref(params), NL.ptr(rstart), NL.ptr(rlen), rstart.numel(),
+                              NL.ptr(tile_prefix), NL.ptr(offs), grid, NL.ptr(out),
+                              NL.stream_ptr()), "hs_scan_select")
+    return out[:total]
+
+
+# ------------------------------------------------------------------------------------------------
+# Join
+# ------------------------------------------------------------------------------------------------
+def join_agg(params: NL.JoinParams, rstart, rlen, rbucket, roff, tile_prefix, grid: int = None):
+    torch = _torch()
+    L = NL.lib()
+    grid = grid or L.hs_scan_grid()
+    GA = params.naggs * (params.num_groups if params.group_col >= 0 else 1)
+    dev = rstart.device
+    ps = torch.empty(grid * GA, dtype=torch.float64, device=dev)
+    pc_ = torch.empty(grid * GA, dtype=torch.int64, device=dev)
+    pmn = torch.empty(grid * GA, dtype=torch.float64, device=dev)
+    pmx = torch.empty(grid * GA, dtype=torch.float64, device=dev)
+    NL.check(L.hs_join_agg(C.byref(params), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
+                           NL.ptr(roff), rstart.numel(), NL.ptr(tile_prefix), grid, NL.ptr(ps),
+                           NL.ptr(pc_), NL.ptr(pmn), NL.ptr(pmx), NL.stream_ptr()), "hs_join_agg")
+    ps = ps.view(grid, GA)
+    pc_ = pc_.view(grid, GA)
+    return ps.sum(0), pc_.sum(0), pmn.view(grid, GA).amin(0), pmx.view(grid, GA).amax(0)
+
+
+def join_pairs(params: NL.JoinParams, rstart, rlen, rbucket, roff, tile_prefix, max_tiles: int):
+    torch = _torch()
+    L = NL.lib()
+    grid = L.hs_scan_grid()
+    dev = rstart.device
+    counts = torch.zeros(max_tiles + 1, dtype=torch.int64, device=dev)
+    NL.check(L.hs_join_count(C.byref(params), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
+                             NL.ptr(roff), rstart.numel(), NL.ptr(tile_prefix), grid, NL.ptr(counts),
+                             NL.stream_ptr()), "hs_join_count")
+    offs = exclusive_scan_i64(counts)
+    total = int(offs[-1].item())
+    ol = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
+    orr = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
+    NL.check(L.hs_join_emit(C.byref(params), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
+                            NL.ptr(roff), rstart.numel(), NL.ptr(tile_prefix), grid, NL.ptr(offs),
+                            NL.ptr(ol), NL.ptr(orr), NL.stream_ptr()), "hs_join_emit")
+    return ol[:total], orr[:total]

@@ -1,0 +1,190 @@
+"""Numerics of every HIP kernel against a host reference (pyarrow / numpy / the Spark-compatible
+Murmur3 oracle).  GPU-only."""
+import numpy as np
+import pyarrow as pa
+import pyarrow.compute as pc
+import pytest
+
+from hyperspace_amd.utils import murmur3
+
+pytestmark = pytest.mark.gpu
+
+
+def _col(arr, device, raw=False):
+    from hyperspace_amd.exec.device_table import DeviceColumn
+    return DeviceColumn.from_arrow(arr, device, raw_strings=raw)
+
+
+def test_murmur3_bucket_matches_spark_oracle(device):
+    from hyperspace_amd.ops import kernels as K
+    rng = np.random.default_rng(1)
+    n = 100_003
+    i32 = pa.array(rng.integers(-2**31, 2**31 - 1, n).astype(np.int32),
+                   mask=rng.random(n) < 0.05)
+    i64 = pa.array(rng.integers(-2**62, 2**62, n).astype(np.int64))
+    f64 = pa.array(np.where(rng.random(n) < 0.01, -0.0, rng.normal(size=n)))
+    f32 = pa.array(rng.normal(size=n).astype(np.float32))
+    s = pa.array([("k%d" % v) * (v % 5) for v in rng.integers(0, 1000, n)],
+                 mask=rng.random(n) < 0.03)
+    d = pa.array(rng.integers(0, 20000, n).astype(np.int32)).view(pa.date32())
+    for cols in ([i32], [i64], [f64], [f32], [s], [d], [i64, s, f64], [s, i32]):
+        dcols = [_col(c, device, raw=True) for c in cols]
+        for nb in (1, 7, 200, 20000):
+            b, counts = K.murmur3_bucket(dcols, nb)
+            ref = murmur3.bucket_ids(cols, nb)
+            got = b.cpu().numpy()
+            assert np.array_equal(got, ref), (cols[0].type, nb)
+            assert np.array_equal(counts.cpu().numpy(), np.bincount(ref, minlength=nb))
+    # golden vectors (BucketUnionTest.scala:101-122)
+    b, _ = K.murmur3_bucket([_col(pa.array([2, 3], pa.int32()), device)], 10)
+    assert b.cpu().tolist() == [4, 1]
+
+
+def test_sort_permutation_stable_nulls_first(device):
+    import torch
+    from hyperspace_amd.ops import kernels as K
+    rng = np.random.default_rng(2)
+    n = 300_001
+    a = rng.integers(-50, 50, n).astype(np.int64)
+    amask = rng.random(n) < 0.02
+    b = rng.normal(size=n)
+    c = rng.integers(0, 2**31 - 1, n).astype(np.int32)
+    bucket = rng.integers(0, 200, n).astype(np.int32)
+    ca = _col(pa.array(a, mask=amask), device)
+    cb = _col(pa.array(b), device)
+    cc = _col(pa.array(c), device)
+    perm = K.sort_permutation([ca, cb, cc],
+                              extra_leading=(torch.from_numpy(bucket).to(device), 8)).cpu().numpy()
+    # reference: lexsort (last key primary) - nulls first encoded via flag
+    a_key = np.where(amask, np.iinfo(np.int64).min, a)
+    a_flag = (~amask).astype(np.int8)
+    ref = np.lexsort((np.arange(n), c, b, a_key, a_flag, bucket))
+    assert np.array_equal(perm, ref)
+
+
+def test_gather_and_scan_agg_q6_shape(device):
+    import torch
+    from hyperspace_amd.ops import _lib as NL, kernels as K
+    rng = np.random.default_rng(3)
+    B = 16
+    per = rng.integers(1000, 40000, B)
+    n = int(per.sum())
+    ship = np.concatenate([np.sort(rng.integers(8000, 10500, k)) for k in per]).astype(np.int32)
+    disc = rng.integers(0, 11, n) / 100.0
+    qty = rng.integers(1, 51, n).astype(np.float64)
+    price = rng.random(n) * 1e5
+    off = np.concatenate([[0], np.cumsum(per)]).astype(np.int64)
+    cs, cd, cq, cp = (_col(pa.array(x), device) for x in (ship, disc, qty, price))
+    boff = torch.from_numpy(off).to(device)
+    lo, hi = 8766, 9131
+    rstart, rlen, rb = K.range_search(cs, boff, lo=K.sortable_image(lo, NL.I32), lo_incl=True,
+                                      hi=K.sortable_image(hi, NL.I32), hi_incl=False)
+    tp = K.ranges_to_tiles(rlen)
+    p = NL.ScanParams()
+    for i, c in enumerate((cs, cd, cq, cp)):
+        p.cols[i] = c.desc()
+    p.preds[0] = NL.Pred(NL.PK_FLT_LIT, NL.OP_GE, 1, 0, 0, 0, 0, 0.05, None)
+    p.preds[1] = NL.Pred(NL.PK_FLT_LIT, NL.OP_LE, 1, 0, 1, 0, 0, 0.07, None)
+    p.preds[2] = NL.Pred(NL.PK_FLT_LIT, NL.OP_LT, 2, 0, 2, 0, 0, 24.0, None)
+    p.npreds = 3
+    a = NL.AggSpec()
+    a.kind, a.nterms = NL.AK_SUM, 2
+    a.col[0], a.col[1] = 3, 1
+    a.alpha[0], a.alpha[1] = 0.0, 0.0
+    a.beta[0], a.beta[1] = 1.0, 1.0
+    p.aggs[0] = a
+    p.naggs = 1
+    p.group_col = -1
+    s, c, mn, mx = K.scan_agg(p, rstart, rlen, tp)
+    m = (ship >= lo) & (ship < hi) & (disc >= 0.05) & (disc <= 0.07) & (qty < 24)
+    ref = float((price[m] * disc[m]).sum())
+    assert int(c[0].item()) == int(m.sum())
+    assert abs(float(s[0].item()) - ref) <= 1e-9 * max(1.0, abs(ref))
+    # selection path
+    rows = K.scan_select(p, rstart, rlen, tp, max_tiles=n // 2048 + B + 1).cpu().numpy()
+    assert np.array_equal(rows, np.nonzero(m)[0])
+    g = K.gather_columns([cp, cd], torch.from_numpy(rows).to(device))
+    assert np.allclose(g[0].data.cpu().numpy(), price[rows])
+
+
+def test_grouped_scan_agg(device):
+    from hyperspace_amd.ops import _lib as NL, kernels as K
+    rng = np.random.default_rng(4)
+    n = 200_000
+    g = rng.integers(0, 37, n).astype(np.int32)
+    v = rng.random(n)
+    cg, cv = _col(pa.array(g), device), _col(pa.array(v), device)
+    rstart, rlen, _ = K.full_ranges(np.array([0, n], np.int64), device)
+    tp = K.ranges_to_tiles(rlen)
+    p = NL.ScanParams()
+    p.cols[0], p.cols[1] = cg.desc(), cv.desc()
+    p.npreds = 0
+    for k, kind in enumerate((NL.AK_SUM, NL.AK_MIN, NL.AK_MAX, NL.AK_COUNT_STAR)):
+        a = NL.AggSpec()
+        a.kind = kind
+        a.nterms = 0 if kind == NL.AK_COUNT_STAR else 1
+        a.col[0], a.alpha[0], a.beta[0] = 1, 0.0, 1.0
+        p.aggs[k] = a
+    p.naggs = 4
+    p.group_col, p.num_groups, p.group_base = 0, 37, 0
+    s, c, mn, mx = K.scan_agg(p, rstart, rlen, tp)
+    s, c, mn, mx = (x.cpu().numpy().reshape(37, 4) for x in (s, c, mn, mx))
+    for grp in range(37):
+        sel = v[g == grp]
+        assert abs(s[grp, 0] - sel.sum()) < 1e-9 * max(1, sel.sum())
+        assert mn[grp, 1] == sel.min() and mx[grp, 2] == sel.max()
+        assert c[grp, 3] == len(sel)
+
+
+def test_join_agg_and_pairs(device):
+    import torch
+    from hyperspace_amd.ops import _lib as NL, kernels as K
+    rng = np.random.default_rng(5)
+    B = 8
+    # right: unique keys per bucket (orders), left: ~4 rows per key (lineitem)
+    rk = np.arange(0, 60_000, dtype=np.int64) * 3
+    rb = murmur3.bucket_ids([pa.array(rk)], B)
+    lk = np.repeat(rk, rng.integers(1, 7, len(rk)))
+    lk = np.concatenate([lk, rng.integers(0, 180_000, 5000)])  # some keys without a match
+    lb = murmur3.bucket_ids([pa.array(lk)], B)
+    ro = np.lexsort((rk, rb)); rk, rb = rk[ro], rb[ro]
+    lo_ = np.lexsort((lk, lb)); lk, lb = lk[lo_], lb[lo_]
+    rdate = rng.integers(0, 1000, len(rk)).astype(np.int32)
+    lprice = rng.random(len(lk)) * 100
+    ldisc = rng.integers(0, 11, len(lk)) / 100.0
+    loff = np.searchsorted(lb, np.arange(B + 1)).astype(np.int64)
+    roff = np.searchsorted(rb, np.arange(B + 1)).astype(np.int64)
+    clk, clp, cld = (_col(pa.array(x), device) for x in (lk, lprice, ldisc))
+    crk, crd = _col(pa.array(rk), device), _col(pa.array(rdate), device)
+    p = NL.JoinParams()
+    p.cols[0], p.cols[1], p.cols[2] = clk.desc(), clp.desc(), cld.desc()
+    p.cols[8], p.cols[9] = crk.desc(), crd.desc()
+    p.lkey, p.rkey = 0, 8
+    p.preds[0] = NL.Pred(NL.PK_FLT_LIT, NL.OP_GT, 2, 0, 0, 0, 0, 0.02, None)   # left pred
+    p.preds[1] = NL.Pred(NL.PK_INT_LIT, NL.OP_LT, 9, 0, 1, 0, 500, 0.0, None)  # right pred
+    p.nlp, p.npreds = 1, 2
+    a = NL.AggSpec()
+    a.kind, a.nterms = NL.AK_SUM, 2
+    a.col[0], a.alpha[0], a.beta[0] = 1, 0.0, 1.0
+    a.col[1], a.alpha[1], a.beta[1] = 2, 1.0, -1.0
+    p.aggs[0] = a
+    p.naggs, p.group_col, p.key_is_float = 1, -1, 0
+    rstart, rlen, rbk = K.full_ranges(loff, device)
+    tp = K.ranges_to_tiles(rlen)
+    s, c, _, _ = K.join_agg(p, rstart, rlen, rbk, torch.from_numpy(roff).to(device), tp)
+    # reference
+    rmap = {int(k): i for i, k in enumerate(rk)}
+    tot, cnt, pairs = 0.0, 0, []
+    for i, k in enumerate(lk):
+        j = rmap.get(int(k))
+        if j is None or not (ldisc[i] > 0.02) or not (rdate[j] < 500):
+            continue
+        tot += lprice[i] * (1 - ldisc[i])
+        cnt += 1
+        pairs.append((i, j))
+    assert int(c[0].item()) == cnt
+    assert abs(float(s[0].item()) - tot) < 1e-9 * tot
+    ol, orr = K.join_pairs(p, rstart, rlen, rbk, torch.from_numpy(roff).to(device), tp,
+                           max_tiles=len(lk) // 2048 + B + 1)
+    got = sorted(zip(ol.cpu().tolist(), orr.cpu().tolist()))
+    assert got == sorted(pairs)
