@@ -1,0 +1,203 @@
+"""Index build on MI355X (SURVEY §3.1 hot loop, kernels K1-K4; §7.2 steps 3-4).
+
+1. scan: this rank's share of the source files is decoded on the host (pyarrow, thread pool)
+   and streamed to HBM through pinned staging (K1); lineage ids are a per-file constant (K2);
+2. ``hs_murmur3_bucket``: Spark-compatible bucket id per row (K3);
+3. multi-GPU: rows move to their owner rank (bucket % world) with one RCCL all-to-all per column;
+4. ``hs_sort_columns``: one stable LSD radix sort by (bucket, indexed columns...) (K4);
+5. ``hs_gather``: all columns permuted in one launch; bucket offsets from the histogram;
+6. one Parquet file per owned bucket, written by a host thread pool while the GPU is idle.
+String columns use a job-global sorted dictionary so their codes sort and exchange consistently.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import time
+import uuid
+from typing import Dict, List, Optional
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.compute as pc
+
+from ..index import constants as C
+from ..index.builder import group_by_bucket, read_index_input
+from ..io.writer import write_bucket_file
+from ..ops import kernels as K
+from ..utils import path_utils as P
+from ..utils.conf import HyperspaceConf
+from .device_table import DeviceColumn, DeviceTable, is_string
+
+_WRITE_POOL = None
+LAST_BUILD_STATS: Dict[str, float] = {}
+
+
+def _writer_pool():
+    global _WRITE_POOL
+    if _WRITE_POOL is None:
+        _WRITE_POOL = cf.ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4))
+    return _WRITE_POOL
+
+
+def _global_dicts(t: pa.Table, dist) -> Dict[str, pa.Array]:
+    out = {}
+    for name in t.column_names:
+        if is_string(t.schema.field(name).type):
+            u = pc.unique(t.column(name).combine_chunks().drop_null())
+            if dist is not None and dist.world > 1:
+                parts = dist.all_gather_object(u.to_pylist())
+                u = pa.array(sorted(set(x for p in parts for x in p)), pa.string())
+            out[name] = u.sort()
+    return out
+
+
+def _prepare_out_dir(out_path: str, mode: str, dist) -> None:
+    import shutil
+    local = P.to_local(out_path)
+    if dist is None or dist.rank == 0:
+        if mode == "overwrite" and os.path.exists(local):
+            shutil.rmtree(local)
+        os.makedirs(local, exist_ok=True)
+    if dist is not None:
+        dist.barrier()
+
+
+def _sort_and_write(session, table: Dict[str, DeviceColumn], names: List[str], bucket,
+                    indexed: List[str], num_buckets: int, out_path: str, schema: pa.Schema,
+                    task_id: int) -> List[str]:
+    import torch
+    n = int(bucket.numel())
+    if n == 0:
+        return []
+    t0 = time.perf_counter()
+    perm = K.sort_permutation([table[c] for c in indexed], extra_leading=(bucket, 16))
+    gathered = K.gather_columns([table[c] for c in names], perm)
+    counts = torch.bincount(bucket.long(), minlength=num_buckets)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    off = np.concatenate([[0], np.cumsum(counts.cpu().numpy())]).astype(np.int64)
+    host_cols = [g.to_arrow() for g in gathered]
+    full = pa.Table.from_arrays(host_cols, names=names)
+    full = full.cast(schema) if not full.schema.equals(schema) else full
+    t2 = time.perf_counter()
+    codec = HyperspaceConf.index_file_codec(session.conf)
+    rg = HyperspaceConf.index_row_group_rows(session.conf)
+    job = str(uuid.uuid4())
+    futs = []
+    for b in range(num_buckets):
+        lo, hi = int(off[b]), int(off[b + 1])
+        if hi > lo:
+            futs.append(_writer_pool().submit(write_bucket_file, full.slice(lo, hi - lo), out_path,
+                                              task_id, job, b, codec, rg))
+    paths = [f.result() for f in futs]
+    LAST_BUILD_STATS.update({"sort_gather_s": t1 - t0, "d2h_s": t2 - t1,
+                             "write_s": time.perf_counter() - t2})
+    return paths
+
+
+def device_build_from_source(session, rel, files: List[str], columns: List[str], indexed: List[str],
+                             num_buckets: int, out_path: str, lineage_ids: Optional[Dict[str, int]],
+                             mode: str = "overwrite") -> List[str]:
+    import torch
+    dist = getattr(session, "dist", None)
+    rank, world = (dist.rank, dist.world) if dist is not None else (0, 1)
+    device = torch.device("cuda", torch.cuda.current_device())
+    _prepare_out_dir(out_path, mode, dist)
+    t0 = time.perf_counter()
+    my_files = files[rank::world]
+    t = read_index_input(rel, my_files, columns, lineage_ids) if my_files else None
+    if t is None:
+        from ..io.reader import read_files
+        t = read_files("parquet" if rel.file_format == "delta" else rel.file_format, files[:1],
+                       rel.data_schema, rel.options, rel.location.partition_spec, columns).slice(0, 0)
+        if lineage_ids is not None:
+            t = t.append_column(pa.field(C.DATA_FILE_NAME_ID, pa.int64(), False),
+                                pa.array([], pa.int64()))
+    schema = t.schema
+    names = t.column_names
+    dicts = _global_dicts(t, dist)
+    t1 = time.perf_counter()
+    cols = {n: DeviceColumn.from_arrow(t.column(n), device, dicts.get(n),
+                                       raw_strings=(n in indexed and n in dicts))
+            for n in names}
+    source_bytes = sum(c.nbytes() for c in cols.values())
+    del t
+    bucket, _ = K.murmur3_bucket([cols[c] for c in indexed], num_buckets, with_counts=False)
+    if world > 1:
+        from ..parallel.shuffle import exchange
+        dest = torch.remainder(bucket, world).to(torch.int32)
+        flat = []
+        for n in names:
+            flat.append(cols[n].data)
+            flat.append(cols[n].valid)
+        flat.append(bucket)
+        recv, _ = exchange(flat, dest, world)
+        bucket = recv[-1]
+        new = {}
+        for i, n in enumerate(names):
+            new[n] = DeviceColumn(recv[2 * i], recv[2 * i + 1], cols[n].atype, cols[n].dictionary)
+        cols = new
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    paths = _sort_and_write(session, cols, names, bucket, indexed, num_buckets, out_path, schema,
+                            rank)
+    if dist is not None:
+        dist.barrier()
+    LAST_BUILD_STATS.update({"read_s": t1 - t0, "h2d_hash_exchange_s": t2 - t1,
+                             "total_s": time.perf_counter() - t0, "source_bytes": source_bytes})
+    return paths
+
+
+def device_rewrite_buckets(session, files: List[str], indexed: List[str], out_path: str,
+                           deleted_ids: Optional[List[int]], num_buckets: Optional[int]) -> List[str]:
+    """K5/K6 on the device: per-bucket merge (+ lineage bitmap filter) of existing index files."""
+    import pyarrow.parquet as pq
+    import torch
+    dist = getattr(session, "dist", None)
+    rank, world = (dist.rank, dist.world) if dist is not None else (0, 1)
+    device = torch.device("cuda", torch.cuda.current_device())
+    groups = group_by_bucket(files)
+    mine = sorted(b for b in groups if b >= 0 and b % world == rank)
+    paths_in = [f for b in mine for f in groups[b]]
+    if -1 in groups:
+        raise ValueError("index files without bucket ids")
+    if not paths_in:
+        return []
+    tables, bucket_parts = [], []
+    for b in mine:
+        for f in groups[b]:
+            tt = pq.read_table(P.to_local(f))
+            tables.append(tt)
+            bucket_parts.append(np.full(tt.num_rows, b, np.int32))
+    bucket_np = np.concatenate(bucket_parts)
+    t = pa.concat_tables(tables)
+    schema = t.schema
+    names = t.column_names
+    dicts = _global_dicts(t, None)
+    cols = {n: DeviceColumn.from_arrow(t.column(n), device, dicts.get(n)) for n in names}
+    bucket = torch.from_numpy(bucket_np).to(device)
+    if deleted_ids:
+        # K5: lineage NOT IN deleted -> bitmap probe + stable compaction, fused in one scan kernel
+        from ..ops import _lib as NL
+        ids = sorted(set(int(i) for i in deleted_ids))
+        words = np.zeros(ids[-1] // 64 + 1, dtype=np.uint64)
+        for i in ids:
+            words[i >> 6] |= np.uint64(1) << np.uint64(i & 63)
+        wt = torch.from_numpy(words.view(np.int64)).to(device)
+        lin = cols[C.DATA_FILE_NAME_ID]
+        p = NL.ScanParams()
+        p.cols[0] = lin.desc()
+        p.preds[0] = NL.Pred(NL.PK_BITMAP, NL.OP_NE, 0, 0, 0, len(words), 0, 0.0, wt.data_ptr())
+        p.npreds, p.naggs, p.group_col = 1, 0, -1
+        n = t.num_rows
+        rstart, rlen, _ = K.full_ranges(np.array([0, n], np.int64), device)
+        tp = K.ranges_to_tiles(rlen)
+        rows = K.scan_select(p, rstart, rlen, tp, n // NL.lib().hs_scan_tile_rows() + 2)
+        kept = K.gather_columns([cols[c] for c in names] +
+                                [DeviceColumn(bucket, None, pa.int32())], rows)
+        cols = dict(zip(names, kept[:-1]))
+        bucket = kept[-1].data
+    out = _sort_and_write(session, cols, names, bucket, indexed,
+                          num_buckets or (max(mine) + 1), out_path, schema, rank)
+    return out

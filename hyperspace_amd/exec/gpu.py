@@ -1,0 +1,641 @@
+"""MI355X executor: runs physical plans on HIP kernels over HBM-resident tables.
+
+Plans are evaluated into lazy device relations (``DRel``): a device table, an attribute -> column
+map, pending filter conjuncts and optional row ranges.  Nothing is materialized until a consumer
+needs rows, so the hot shapes compile into single fused launches:
+
+* ``Aggregate <- Filter <- IndexScan``            -> range search + ``hs_scan_agg`` (Q6 shape)
+* ``Aggregate <- SortMergeJoin(IndexScan, IndexScan)`` -> ``hs_join_agg`` (co-located, no shuffle)
+* ``Filter/Project <- Scan``                       -> ``hs_scan_select`` + ``hs_gather``
+* ``SortMergeJoin``                                 -> ``hs_join_count/emit`` + gathers
+* ``Exchange(hashpartitioning) <- Scan``           -> Murmur3 + radix sort on the device
+
+Under ``torch.distributed`` each rank owns buckets ``b % world == rank`` (co-partitioned, so a
+bucketed join needs no data movement); partial aggregates are combined with one RCCL all-reduce
+and row results with an all-gather.  Shapes outside the kernel templates raise ``Unsupported``
+and the whole query runs on the host oracle (recorded in ``last_path``).
+"""
+from __future__ import annotations
+
+import logging
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import pyarrow as pa
+
+from ..index import constants as C
+from ..ops import _lib as NL
+from ..ops import kernels as K
+from ..plan import expressions as E
+from ..plan import physical as X
+from ..utils import murmur3
+from ..utils.conf import HyperspaceConf
+from . import compile as CP
+from .arrow_eval import key
+from .device_cache import DeviceTableCache, load_bucketed_index, load_flat
+from .device_table import DeviceColumn, DeviceTable
+
+log = logging.getLogger(__name__)
+Unsupported = CP.Unsupported
+MAX_GROUPS_SCAN = 3000
+MAX_GROUPS_JOIN = 2400
+
+
+class DRel:
+    def __init__(self, table: DeviceTable, colmap: Dict[int, str], attrs: List[E.Attribute],
+                 conds: Optional[list] = None, bucketed: bool = False,
+                 sort_attrs: Optional[List[E.Attribute]] = None,
+                 bucket_attrs: Optional[List[E.Attribute]] = None, num_buckets: int = 0):
+        self.table = table
+        self.colmap = colmap
+        self.attrs = attrs
+        self.conds = list(conds or [])
+        self.bucketed = bucketed
+        self.sort_attrs = list(sort_attrs or [])
+        self.bucket_attrs = list(bucket_attrs or [])
+        self.num_buckets = num_buckets
+
+    def col(self, a: E.Attribute) -> DeviceColumn:
+        name = self.colmap.get(a.expr_id)
+        if name is None:
+            raise Unsupported(f"attribute {a.sql()} not available on device")
+        return self.table.columns[name]
+
+    def copy(self, **kw) -> "DRel":
+        d = DRel(self.table, dict(self.colmap), list(self.attrs), list(self.conds), self.bucketed,
+                 self.sort_attrs, self.bucket_attrs, self.num_buckets)
+        for k, v in kw.items():
+            setattr(d, k, v)
+        return d
+
+
+class GpuBackend:
+    name = "gpu"
+
+    def __init__(self, session):
+        import torch
+        NL.lib()  # fail loudly if the kernels are not built
+        self.session = session
+        self.device = torch.device("cuda", torch.cuda.current_device())
+        self.cache = DeviceTableCache(HyperspaceConf.device_cache_bytes(session.conf))
+        self.last_path = None
+        self.fallback_reason = None
+        self.metrics: Dict[str, float] = {}
+        self._cpu = None
+
+    # ------------------------------------------------------------------------------------------
+    @property
+    def cpu(self):
+        if self._cpu is None:
+            from .cpu import CpuBackend
+            self._cpu = CpuBackend(self.session)
+        return self._cpu
+
+    def _dist(self):
+        return getattr(self.session, "dist", None)
+
+    def collect(self, plan: X.SparkPlan) -> pa.Table:
+        t0 = time.perf_counter()
+        try:
+            out = self._collect_native(plan)
+            self.last_path = "native"
+            self.fallback_reason = None
+        except Unsupported as e:
+            log.info("device executor fallback: %s", e)
+            self.last_path = "fallback"
+            self.fallback_reason = str(e)
+            out = self.cpu.collect(plan)
+        self.metrics["last_query_s"] = time.perf_counter() - t0
+        return out
+
+    def _collect_native(self, plan: X.SparkPlan) -> pa.Table:
+        limit = None
+        if isinstance(plan, X.CollectLimitExec):
+            limit = plan.n
+            plan = plan.child
+        agg = self._match_agg(plan)
+        if agg is not None:
+            t = self._exec_agg(*agg)
+        else:
+            rel = self._rel(plan)
+            t = self._to_arrow(rel, plan.output)
+            t = self._gather_ranks(t)
+        if limit is not None:
+            t = t.slice(0, limit)
+        return t
+
+    # ------------------------------------------------------------------------------------------
+    # Relations
+    # ------------------------------------------------------------------------------------------
+    def _rel(self, p: X.SparkPlan) -> DRel:
+        if isinstance(p, X.FileSourceScanExec):
+            return self._scan(p)
+        if isinstance(p, X.FilterExec):
+            r = self._rel(p.child)
+            return r.copy(conds=r.conds + E.split_conjuncts(p.condition))
+        if isinstance(p, X.ProjectExec):
+            r = self._rel(p.child)
+            colmap = dict(r.colmap)
+            attrs = []
+            for e in p.project_list:
+                if isinstance(e, E.Attribute):
+                    attrs.append(e)
+                elif isinstance(e, E.Alias) and isinstance(e.child, E.Attribute):
+                    if e.child.expr_id not in colmap:
+                        raise Unsupported("alias of unknown column")
+                    colmap[e.expr_id] = colmap[e.child.expr_id]
+                    attrs.append(e.to_attribute())
+                else:
+                    raise Unsupported("computed projection")
+            return r.copy(colmap=colmap, attrs=attrs)
+        if isinstance(p, X.SortExec):
+            r = self._rel(p.child)
+            if not p.global_sort and r.bucketed and _prefix_sorted(r, [o.child for o in p.order]):
+                return r
+            raise Unsupported("device sort of unsorted input")
+        if isinstance(p, X.ShuffleExchangeExec) and isinstance(p.partitioning, X.HashPartitioning):
+            return self._repartition(self._rel(p.child), p.partitioning)
+        if isinstance(p, X.SortMergeJoinExec):
+            return self._join_rel(p)
+        raise Unsupported(f"operator {p.node_name}")
+
+    def _scan(self, p: X.FileSourceScanExec) -> DRel:
+        rel = p.relation
+        files = rel.location.all_files()
+        d = self._dist()
+        rank, world = (d.rank, d.world) if d is not None else (0, 1)
+        names = [a.name for a in p.output]
+        if rel.is_index() and self._all_bucket_files(files, rel.index.num_buckets):
+            idx = rel.index
+            ncol = {n.lower(): n for n in idx.schema.names}
+            cols = [ncol[a.name.lower()] for a in p.output]
+            sort_cols = [ncol[c.lower()] for c in idx.indexed_columns]
+            load_cols = list(dict.fromkeys(cols + sort_cols))
+            table = self.cache.get(files, load_cols, ("bucketed", rank, world),
+                                   lambda: load_bucketed_index(files, load_cols, idx.num_buckets,
+                                                               sort_cols, self.device, rank, world))
+            colmap = {a.expr_id: c for a, c in zip(p.output, cols)}
+            sort_attrs = []
+            for c in sort_cols:
+                a = next((x for x in p.output if x.name.lower() == c.lower()), None)
+                if a is None:
+                    a = E.Attribute(c, idx.schema.field(c).type)
+                    colmap[a.expr_id] = c
+                sort_attrs.append(a)
+            return DRel(table, colmap, list(p.output), [], True, sort_attrs, sort_attrs,
+                        idx.num_buckets)
+        if world > 1:
+            raise Unsupported("distributed scan of non-index data")
+        fmt = "parquet" if (rel.is_index() or rel.file_format == "delta") else rel.file_format
+        table = self.cache.get(files, names, ("flat", fmt),
+                               lambda: load_flat(files, fmt, names, rel.data_schema, rel.options,
+                                                 rel.location.partition_spec, self.device))
+        return DRel(table, {a.expr_id: a.name for a in p.output}, list(p.output))
+
+    @staticmethod
+    def _all_bucket_files(files, nb) -> bool:
+        from ..io.writer import get_bucket_id
+        from ..utils import path_utils as P
+        for f in files:
+            b = get_bucket_id(P.get_name(f.path))
+            if b is None or b >= nb:
+                return False
+        return True
+
+    # -- lowering helpers ----------------------------------------------------------------------
+    def _ranges(self, r: DRel, conds: list):
+        """Row ranges after bucket / sort-key pruning on the leading indexed column."""
+        t = r.table
+        if not (r.bucketed and r.sort_attrs):
+            return K.full_ranges(t.bucket_offsets_host, self.device)
+        lead = r.sort_attrs[0]
+        kc = r.col(lead)
+        lo = hi = None
+        lo_incl = hi_incl = True
+        eq_bucket = None
+        for c in conds:
+            if not isinstance(c, E.BinaryComparison) or isinstance(c, E.NotEqual):
+                continue
+            leaf = None
+            try:
+                leaf = CP._leaf(c)
+            except Unsupported:
+                continue
+            if leaf.kind != "cmp_lit" or leaf.attr.expr_id != lead.expr_id or leaf.value is None:
+                continue
+            v = leaf.value
+            if kc.dictionary is not None or isinstance(v, str):
+                continue
+            if kc.is_float:
+                v = float(v)
+            elif isinstance(v, float):
+                if not float(v).is_integer():
+                    continue
+                v = int(v)
+            img = K.sortable_image(v, kc.hs_type)
+            if leaf.op in (NL.OP_GT, NL.OP_GE, NL.OP_EQ):
+                inc = leaf.op != NL.OP_GT
+                if lo is None or img > lo or (img == lo and not inc):
+                    lo, lo_incl = img, inc
+            if leaf.op in (NL.OP_LT, NL.OP_LE, NL.OP_EQ):
+                inc = leaf.op != NL.OP_LT
+                if hi is None or img < hi or (img == hi and not inc):
+                    hi, hi_incl = img, inc
+            if leaf.op == NL.OP_EQ and len(r.bucket_attrs) == 1 and not kc.is_float:
+                eq_bucket = self._bucket_of_literal(leaf.value, lead.data_type, r.num_buckets)
+        buckets = None
+        if eq_bucket is not None:
+            import torch
+            buckets = torch.tensor([eq_bucket], dtype=torch.int32, device=self.device)
+        if lo is None and hi is None and buckets is None:
+            return K.full_ranges(t.bucket_offsets_host, self.device)
+        return K.range_search(kc, t.bucket_offsets, buckets, lo, lo_incl, hi, hi_incl)
+
+    @staticmethod
+    def _bucket_of_literal(v, dtype, nb) -> int:
+        arr = pa.array([v], type=dtype)
+        return int(murmur3.bucket_ids([arr], nb)[0])
+
+    def _column_infos(self, rels_slots):
+        """rels_slots: list of (DRel, slot_base). Returns col_info(attr) and the ColDesc list."""
+        slot_map: Dict[int, int] = {}
+        descs: Dict[int, DeviceColumn] = {}
+        counters = {base: 0 for _, base in rels_slots}
+
+        def col_info(a: E.Attribute) -> CP.ColumnInfo:
+            if a.expr_id not in slot_map:
+                for rel, base in rels_slots:
+                    if a.expr_id in rel.colmap:
+                        i = counters[base]
+                        limit = 8 if len(rels_slots) > 1 else NL.MAX_COLS
+                        if i >= limit:
+                            raise Unsupported("too many columns for one kernel")
+                        counters[base] = i + 1
+                        slot_map[a.expr_id] = base + i
+                        descs[base + i] = rel.col(a)
+                        break
+                else:
+                    raise Unsupported(f"unknown column {a.sql()}")
+            s = slot_map[a.expr_id]
+            c = descs[s]
+            return CP.ColumnInfo(s, c.hs_type, c.atype, c.dictionary)
+        return col_info, descs
+
+    # ------------------------------------------------------------------------------------------
+    # Materialization
+    # ------------------------------------------------------------------------------------------
+    def _materialize(self, r: DRel, attrs: List[E.Attribute]) -> Dict[int, DeviceColumn]:
+        """Apply pending predicates; return expr_id -> gathered DeviceColumn."""
+        if not r.conds:
+            t = r.table
+            full = t.num_rows
+            return {a.expr_id: r.col(a) for a in attrs} if full is not None else {}
+        rstart, rlen, _ = self._ranges(r, r.conds)
+        col_info, descs = self._column_infos([(r, 0)])
+        bound = CP.bind(CP.to_cnf(r.conds), col_info, self.device)
+        for a in attrs:
+            col_info(a)
+        p = NL.ScanParams()
+        for s, c in descs.items():
+            p.cols[s] = c.desc()
+        for i, pr in enumerate(bound.preds):
+            p.preds[i] = pr
+        p.npreds = len(bound.preds)
+        p.naggs, p.group_col = 0, -1
+        import torch
+        if bound.always_false:
+            rows = torch.empty(0, dtype=torch.int64, device=self.device)
+        else:
+            tp = K.ranges_to_tiles(rlen)
+            max_tiles = r.table.num_rows // NL.lib().hs_scan_tile_rows() + rlen.numel() + 1
+            rows = K.scan_select(p, rstart, rlen, tp, max_tiles)
+        cols = [r.col(a) for a in attrs]
+        g = K.gather_columns(cols, rows)
+        return {a.expr_id: c for a, c in zip(attrs, g)}
+
+    def _to_arrow(self, r: DRel, out_attrs: List[E.Attribute]) -> pa.Table:
+        cols = self._materialize(r, out_attrs)
+        arrays = [cols[a.expr_id].to_arrow() for a in out_attrs]
+        fixed = []
+        for a, arr in zip(out_attrs, arrays):
+            if not arr.type.equals(a.data_type):
+                try:
+                    arr = arr.cast(a.data_type)
+                except (pa.ArrowInvalid, pa.ArrowNotImplementedError):
+                    pass
+            fixed.append(arr)
+        return pa.Table.from_arrays(fixed, names=[a.name for a in out_attrs])
+
+    def _gather_ranks(self, t: pa.Table) -> pa.Table:
+        d = self._dist()
+        if d is None or d.world == 1:
+            return t
+        parts = d.all_gather_object(t)
+        return pa.concat_tables(parts)
+
+    # ------------------------------------------------------------------------------------------
+    # Repartition (device shuffle for non-index inputs)
+    # ------------------------------------------------------------------------------------------
+    def _repartition(self, r: DRel, part: X.HashPartitioning) -> DRel:
+        d = self._dist()
+        if d is not None and d.world > 1:
+            raise Unsupported("distributed device shuffle of non-index data")
+        if not all(isinstance(e, E.Attribute) for e in part.expressions):
+            raise Unsupported("hash partitioning on expressions")
+        keys = list(part.expressions)
+        cols = self._materialize(r, list(dict.fromkeys(r.attrs + keys)))
+        kcols = [cols[k.expr_id] for k in keys]
+        for c in kcols:
+            if c.dictionary is not None:
+                raise Unsupported("device shuffle on string keys")
+        n = len(next(iter(cols.values()))) if cols else 0
+        import torch
+        B = part.num_partitions
+        bucket, counts = K.murmur3_bucket(kcols, B)
+        perm = K.sort_permutation(kcols, extra_leading=(bucket, 16))
+        names = list(cols.keys())
+        gathered = K.gather_columns([cols[i] for i in names], perm)
+        off_host = np.concatenate([[0], np.cumsum(counts.cpu().numpy())]).astype(np.int64)
+        table = DeviceTable({f"c{i}": c for i, c in zip(names, gathered)}, n,
+                            torch.from_numpy(off_host).to(self.device), off_host)
+        colmap = {i: f"c{i}" for i in names}
+        return DRel(table, colmap, list(r.attrs), [], True, keys, keys, B)
+
+    # ------------------------------------------------------------------------------------------
+    # Joins
+    # ------------------------------------------------------------------------------------------
+    def _join_inputs(self, p: X.SortMergeJoinExec):
+        if p.join_type != "inner":
+            raise Unsupported(f"{p.join_type} join on device")
+        if len(p.left_keys) != 1 or not isinstance(p.left_keys[0], E.Attribute) or \
+                not isinstance(p.right_keys[0], E.Attribute):
+            raise Unsupported("multi-key / expression join keys")
+        left, right = self._rel(p.left), self._rel(p.right)
+        if not (left.bucketed and right.bucketed) or left.num_buckets != right.num_buckets:
+            raise Unsupported("join inputs not co-partitioned on device")
+        lk, rk = p.left_keys[0], p.right_keys[0]
+        if not _prefix_sorted(left, [lk]):
+            raise Unsupported("left not sorted by join key")
+        if not _prefix_sorted(right, [rk]):
+            raise Unsupported("right not sorted by join key")
+        lc, rc = left.col(lk), right.col(rk)
+        if lc.dictionary is not None or rc.dictionary is not None:
+            raise Unsupported("string join keys on device")
+        if lc.is_float != rc.is_float:
+            raise Unsupported("mixed int/float join keys")
+        return left, right, lk, rk
+
+    def _join_params(self, left: DRel, right: DRel, lk, rk, residual, extra_attrs=()):
+        col_info, descs = self._column_infos([(left, 0), (right, 8)])
+        lslot = col_info(lk).slot
+        rslot = col_info(rk).slot
+        lb = CP.bind(CP.to_cnf(left.conds), col_info, self.device, 0)
+        rconds = list(right.conds) + ([residual] if residual is not None else [])
+        rb = CP.bind(CP.to_cnf(rconds), col_info, self.device, 1000)
+        for a in extra_attrs:
+            col_info(a)
+        p = NL.JoinParams()
+        preds = lb.preds + rb.preds
+        if len(preds) > NL.MAX_PREDS:
+            raise Unsupported("too many join predicates")
+        for i, pr in enumerate(preds):
+            p.preds[i] = pr
+        p.nlp, p.npreds = len(lb.preds), len(preds)
+        p.lkey, p.rkey = lslot, rslot
+        p.key_is_float = 1 if left.col(lk).is_float else 0
+        p.group_col = -1
+        return p, col_info, descs, (lb, rb)
+
+    def _join_rel(self, p: X.SortMergeJoinExec) -> DRel:
+        left, right, lk, rk = self._join_inputs(p)
+        out_attrs = list(p.output)
+        jp, col_info, descs, keep = self._join_params(left, right, lk, rk, p.condition)
+        for s, c in descs.items():
+            jp.cols[s] = c.desc()
+        if keep[0].always_false or keep[1].always_false:
+            import torch
+            ol = orr = torch.empty(0, dtype=torch.int64, device=self.device)
+        else:
+            rstart, rlen, rbk = self._ranges(left, left.conds)
+            tp = K.ranges_to_tiles(rlen)
+            max_tiles = left.table.num_rows // NL.lib().hs_join_tile_rows() + rlen.numel() + 1
+            ol, orr = K.join_pairs(jp, rstart, rlen, rbk, right.table.bucket_offsets, tp, max_tiles)
+        lset = {a.expr_id for a in p.left.output}
+        lattrs = [a for a in out_attrs if a.expr_id in lset]
+        rattrs = [a for a in out_attrs if a.expr_id not in lset]
+        lg = K.gather_columns([left.col(a) for a in lattrs], ol)
+        rg = K.gather_columns([right.col(a) for a in rattrs], orr)
+        cols = {}
+        for a, c in list(zip(lattrs, lg)) + list(zip(rattrs, rg)):
+            cols[key(a)] = c
+        n = int(ol.numel())
+        import torch
+        off = np.array([0, n], dtype=np.int64)
+        table = DeviceTable(cols, n, torch.from_numpy(off).to(self.device), off)
+        return DRel(table, {a.expr_id: key(a) for a in out_attrs}, out_attrs)
+
+    # ------------------------------------------------------------------------------------------
+    # Aggregation
+    # ------------------------------------------------------------------------------------------
+    def _match_agg(self, plan):
+        if not (isinstance(plan, X.HashAggregateExec) and plan.mode == "final"):
+            return None
+        ex = plan.child
+        if not isinstance(ex, X.ShuffleExchangeExec):
+            return None
+        partial = ex.child
+        if not (isinstance(partial, X.HashAggregateExec) and partial.mode == "partial"):
+            return None
+        return plan, partial.child
+
+    def _exec_agg(self, final: X.HashAggregateExec, child: X.SparkPlan) -> pa.Table:
+        fns = [fn for _, fn in X.agg_functions(final.aggregates)]
+        if len(final.grouping) > 1:
+            raise Unsupported("multi-column group by")
+        group = final.grouping[0] if final.grouping else None
+        if group is not None and not isinstance(group, E.Attribute):
+            raise Unsupported("group by expression")
+        node = child
+        while isinstance(node, X.ProjectExec) and all(isinstance(e, E.Attribute) for e in node.project_list):
+            node = node.child
+        import torch
+        if isinstance(node, X.SortMergeJoinExec):
+            res = self._join_agg(node, fns, group)
+        else:
+            res = self._scan_agg(self._rel(child), fns, group)
+        sums, cnts, mins, maxs, G, gbase, gdict, gtype = res
+        d = self._dist()
+        if d is not None and d.world > 1:
+            sums, cnts, mins, maxs = d.all_reduce_agg(sums, cnts, mins, maxs)
+        A = len(fns) + 1  # + implicit count(*)
+        s = sums.cpu().numpy().reshape(G, A)
+        c = cnts.cpu().numpy().reshape(G, A)
+        mn = mins.cpu().numpy().reshape(G, A)
+        mx = maxs.cpu().numpy().reshape(G, A)
+        rows = [g for g in range(G) if c[g, A - 1] > 0] if group is not None else [0]
+        vals = {}
+        for i, fn in enumerate(fns):
+            vals[id(fn)] = [CP.finalize_value(fn, s[g, i], c[g, i], mn[g, i], mx[g, i]) for g in rows]
+        gvals = None
+        if group is not None:
+            raw = [gbase + g for g in rows]
+            if gdict is not None:
+                gvals = [gdict[int(v)].as_py() for v in raw]
+            elif pa.types.is_date32(gtype):
+                gvals = pa.array(np.array(raw, dtype=np.int32)).view(pa.date32()).to_pylist()
+            else:
+                gvals = raw
+        out_cols = []
+        for e in final.aggregates:
+            out_cols.append(self._agg_output(e, group, gvals, vals, len(rows)))
+        arrays = []
+        for a, vlist in zip(final.output, out_cols):
+            try:
+                arrays.append(pa.array(vlist, type=a.data_type))
+            except (pa.ArrowInvalid, pa.ArrowTypeError):
+                arrays.append(pa.array(vlist))
+        return pa.Table.from_arrays(arrays, names=[a.name for a in final.output])
+
+    def _agg_output(self, e, group, gvals, vals, nrows):
+        inner = e.child if isinstance(e, E.Alias) else e
+        if isinstance(inner, E.AggregateFunction):
+            return vals[id(inner)]
+        if group is not None and isinstance(inner, E.Attribute) and inner.expr_id == group.expr_id:
+            return gvals
+        # arithmetic over aggregates (e.g. sum(a)/count(b)) evaluated on the host
+        out = []
+        for r in range(nrows):
+            out.append(_eval_scalar(inner, lambda fn: vals[id(fn)][r],
+                                    lambda a: gvals[r] if group is not None and a.expr_id == group.expr_id
+                                    else None))
+        return out
+
+    def _group_spec(self, r: DRel, group, limit):
+        if group is None:
+            return -1, 1, 0, None, None
+        c = r.col(group)
+        if c.is_float:
+            raise Unsupported("float group key")
+        if c.dictionary is not None:
+            G = len(c.dictionary)
+            base = 0
+        else:
+            import torch
+            vals = c.data if c.valid is None else c.data[c.valid.bool()]
+            if vals.numel() == 0:
+                return None
+            lo, hi = torch.aminmax(vals)
+            base, G = int(lo.item()), int(hi.item()) - int(lo.item()) + 1
+        if G > limit:
+            raise Unsupported("group domain too large for LDS aggregation")
+        return None, max(G, 1), base, c.dictionary, c.atype
+
+    def _agg_specs(self, fns, col_info):
+        specs = [CP.agg_spec(fn, lambda a: col_info(a).slot) for fn in fns]
+        star = NL.AggSpec()
+        star.kind, star.nterms = NL.AK_COUNT_STAR, 0
+        specs.append(star)
+        if len(specs) > NL.MAX_AGGS:
+            raise Unsupported("too many aggregates")
+        return specs
+
+    def _scan_agg(self, r: DRel, fns, group):
+        col_info, descs = self._column_infos([(r, 0)])
+        bound = CP.bind(CP.to_cnf(r.conds), col_info, self.device)
+        specs = self._agg_specs(fns, col_info)
+        gs = self._group_spec(r, group, MAX_GROUPS_SCAN)
+        p = NL.ScanParams()
+        if gs is None:  # empty group column
+            return (*self._empty_agg(len(specs)), 1, 0, None, None)
+        _, G, gbase, gdict, gtype = gs
+        p.group_col = col_info(group).slot if group is not None else -1
+        p.num_groups, p.group_base = G, gbase
+        for s, c in descs.items():
+            p.cols[s] = c.desc()
+        for i, pr in enumerate(bound.preds):
+            p.preds[i] = pr
+        p.npreds = len(bound.preds)
+        for i, a in enumerate(specs):
+            p.aggs[i] = a
+        p.naggs = len(specs)
+        if bound.always_false:
+            out = self._empty_agg(len(specs), G)
+        else:
+            rstart, rlen, _ = self._ranges(r, r.conds)
+            tp = K.ranges_to_tiles(rlen)
+            out = K.scan_agg(p, rstart, rlen, tp)
+        return (*out, G, gbase, gdict, gtype)
+
+    def _empty_agg(self, A, G=1):
+        import torch
+        z = torch.zeros(G * A, dtype=torch.float64, device=self.device)
+        zc = torch.zeros(G * A, dtype=torch.int64, device=self.device)
+        return z, zc, torch.full_like(z, float("inf")), torch.full_like(z, float("-inf"))
+
+    def _join_agg(self, node: X.SortMergeJoinExec, fns, group):
+        left, right, lk, rk = self._join_inputs(node)
+        jp, col_info, descs, keep = self._join_params(left, right, lk, rk, node.condition)
+        specs = self._agg_specs(fns, col_info)
+        gs = None
+        if group is not None:
+            side = left if group.expr_id in left.colmap else right
+            gs = self._group_spec(side, group, MAX_GROUPS_JOIN)
+            if gs is None:
+                return (*self._empty_agg(len(specs)), 1, 0, None, None)
+            _, G, gbase, gdict, gtype = gs
+            jp.group_col = col_info(group).slot
+            jp.num_groups, jp.group_base = G, gbase
+        else:
+            G, gbase, gdict, gtype = 1, 0, None, None
+        for s, c in descs.items():
+            jp.cols[s] = c.desc()
+        for i, a in enumerate(specs):
+            jp.aggs[i] = a
+        jp.naggs = len(specs)
+        if keep[0].always_false or keep[1].always_false:
+            return (*self._empty_agg(len(specs), G), G, gbase, gdict, gtype)
+        rstart, rlen, rbk = self._ranges(left, left.conds)
+        tp = K.ranges_to_tiles(rlen)
+        out = K.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, tp)
+        return (*out, G, gbase, gdict, gtype)
+
+
+def _prefix_sorted(r: DRel, exprs) -> bool:
+    if len(exprs) > len(r.sort_attrs):
+        return False
+    for e, s in zip(exprs, r.sort_attrs):
+        if not isinstance(e, E.Attribute):
+            return False
+        if r.colmap.get(e.expr_id) != r.colmap.get(s.expr_id):
+            return False
+    return True
+
+
+def _eval_scalar(e, agg_val, attr_val):
+    if isinstance(e, E.AggregateFunction):
+        return agg_val(e)
+    if isinstance(e, E.Attribute):
+        return attr_val(e)
+    if isinstance(e, E.Literal):
+        return e.value
+    if isinstance(e, E.Alias):
+        return _eval_scalar(e.child, agg_val, attr_val)
+    if isinstance(e, E.Cast):
+        return _eval_scalar(e.child, agg_val, attr_val)
+    if isinstance(e, E.BinaryArithmetic):
+        a = _eval_scalar(e.left, agg_val, attr_val)
+        b = _eval_scalar(e.right, agg_val, attr_val)
+        if a is None or b is None:
+            return None
+        if isinstance(e, E.Add):
+            return a + b
+        if isinstance(e, E.Subtract):
+            return a - b
+        if isinstance(e, E.Multiply):
+            return a * b
+        return None if b == 0 else a / b
+    raise Unsupported(f"result expression {type(e).__name__}")
+
+
+__all__ = ["GpuBackend", "C"]

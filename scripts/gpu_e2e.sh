@@ -1,0 +1,12 @@
+#!/bin/bash
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests/ -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> gpurun_out/gpu_tests.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?
+echo "smoke rc=$rc" >> gpurun_out/smoke.log
+exit $rc
