@@ -1,0 +1,232 @@
+#!/usr/bin/env python
+"""Headline benchmark (BASELINE.json): queries/sec + index-build GB/s on TPC-H SF100-shaped data,
+filter (FilterIndexRule, TPC-H Q6) + join (JoinIndexRule, TPC-H Q3-style) on 1/2/4/8 MI355X.
+
+    python bench.py --gpus N --steps K --warmup W [--sf 100]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One step = one Q6 filter query + one Q3-style join query, each with fresh literals, run through
+the full engine path every time (optimizer + Hyperspace rules + signature validation + execution
+on the HIP kernels + cross-rank combine).  ``value`` = whole-job queries/sec.  Data is synthetic
+TPC-H-shaped (``hyperspace_amd.models.tpch``) and generated once per data dir.  Index build is
+timed separately (three covering indexes: lineitem(l_shipdate), lineitem(l_orderkey),
+orders(o_orderkey)); ``index_build_gbps`` = decoded indexed-column bytes / build wall time.
+Total work is fixed as N grows (strong scaling): buckets are owned by rank ``b % N``.
+"""
+import argparse
+import datetime
+import json
+import os
+import shutil
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "queries/sec + index-build GB/s, TPC-H SF100 filter+join at 1/2/4/8 MI355X"
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--sf", type=float, default=100.0)
+    ap.add_argument("--buckets", type=int, default=200)
+    ap.add_argument("--files", type=int, default=0, help="source files per table (0=auto)")
+    ap.add_argument("--data-dir", default=os.environ.get("HS_BENCH_DIR", "/tmp/hs_bench"))
+    ap.add_argument("--workers", type=int, default=int(os.environ.get("HS_BENCH_WORKERS", "0")))
+    ap.add_argument("--no-crosscheck", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    from hyperspace_amd import Hyperspace, IndexConfig, Session, col, count, sum_
+    from hyperspace_amd.exec import device_build
+    from hyperspace_amd.models import tpch
+    from hyperspace_amd.parallel.dist import DistContext
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    dist = DistContext.from_env() if world_env > 1 else None
+    rank, world = (dist.rank, dist.world) if dist else (0, 1)
+    if dist is None:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    barrier = dist.barrier if dist else (lambda: None)
+
+    sf = args.sf
+    nfiles = args.files or max(8, int(round(sf * 1.28)))
+    data = os.path.join(args.data_dir, f"tpch_sf{sf:g}_f{nfiles}")
+    cpus = os.cpu_count() or 8
+    workers = args.workers or max(1, min(16, cpus // max(world, 1)))
+    # ---------------------------------------------------------------- data generation (once)
+    t0 = time.perf_counter()
+    mine = [i for i in range(nfiles) if i % world == rank]
+    tpch.generate(data, sf, nfiles, mine, workers=workers)
+    barrier()
+    gen_s = time.perf_counter() - t0
+    log(rank, f"[bench] data ready sf={sf} files={nfiles} in {gen_s:.1f}s ({data})")
+
+    idx_root = os.path.join(args.data_dir, f"indexes_sf{sf:g}_b{args.buckets}_w{world}")
+    if rank == 0 and os.path.exists(idx_root):
+        shutil.rmtree(idx_root)
+    barrier()
+    s = Session(conf={"spark.hyperspace.system.path": idx_root,
+                      "spark.hyperspace.index.numBuckets": str(args.buckets),
+                      "spark.sql.autoBroadcastJoinThreshold": "-1",
+                      "spark.sql.shuffle.partitions": str(args.buckets),
+                      "spark.hyperspace.mi.execution.device": "gpu",
+                      "spark.hyperspace.mi.index.codec": "snappy"},
+                warehouse_dir=os.path.join(args.data_dir, "wh"))
+    s.dist = dist
+    hs = Hyperspace(s)
+    li = s.read.parquet(os.path.join(data, "lineitem"))
+    od = s.read.parquet(os.path.join(data, "orders"))
+
+    # ---------------------------------------------------------------- index build (timed)
+    builds = [(li, IndexConfig("li_shipdate", ["l_shipdate"],
+                               ["l_discount", "l_quantity", "l_extendedprice"])),
+              (li, IndexConfig("li_orderkey", ["l_orderkey"],
+                               ["l_extendedprice", "l_discount", "l_shipdate"])),
+              (od, IndexConfig("ord_orderkey", ["o_orderkey"], ["o_orderdate", "o_shippriority"]))]
+    build_s, build_bytes = 0.0, 0
+    per_index = {}
+    for df, cfg in builds:
+        barrier()
+        torch.cuda.synchronize()
+        tb = time.perf_counter()
+        hs.createIndex(df, cfg)
+        torch.cuda.synchronize()
+        barrier()
+        dt = time.perf_counter() - tb
+        local_bytes = float(device_build.LAST_BUILD_STATS.get("source_bytes", 0))
+        if dist:
+            t = torch.tensor([local_bytes], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(t)
+            local_bytes = float(t.item())
+            dt = dist.all_reduce_max_float(dt)
+        build_s += dt
+        build_bytes += local_bytes
+        per_index[cfg.indexName] = {"s": round(dt, 3), "gbps": round(local_bytes / dt / 1e9, 3)}
+        log(rank, f"[bench] built {cfg.indexName} in {dt:.2f}s "
+                  f"({local_bytes / 1e9:.2f} GB decoded) {device_build.LAST_BUILD_STATS}")
+    build_gbps = build_bytes / build_s / 1e9
+
+    Hyperspace.enable(s)
+    backend = s.backend()
+
+    # ---------------------------------------------------------------- queries
+    def d(days):
+        return datetime.date(1970, 1, 1) + datetime.timedelta(days=int(days))
+
+    def q6(i):
+        year = 1993 + i % 5
+        disc = 0.02 + (i % 8) * 0.01
+        qty = 24 + (i % 2)
+        lo = datetime.date(year, 1, 1)
+        hi = datetime.date(year + 1, 1, 1)
+        return li.filter((col("l_shipdate") >= lo) & (col("l_shipdate") < hi) &
+                         (col("l_discount") >= round(disc - 0.01, 2)) &
+                         (col("l_discount") <= round(disc + 0.01, 2)) & (col("l_quantity") < qty)) \
+            .agg(sum_(col("l_extendedprice") * col("l_discount")).alias("revenue"))
+
+    def q3(i):
+        dd = datetime.date(1995, 3, 1) + datetime.timedelta(days=(i * 7) % 30)
+        j = li.join(od, li["l_orderkey"] == od["o_orderkey"]) \
+            .filter((col("o_orderdate") < dd) & (col("l_shipdate") > dd))
+        return j.groupBy("o_shippriority").agg(
+            sum_(col("l_extendedprice") * (1 - col("l_discount"))).alias("revenue"),
+            count("*").alias("lines"))
+
+    def step(i):
+        r1 = q6(i).collect()
+        p1 = backend.last_path
+        r2 = q3(i).collect()
+        p2 = backend.last_path
+        if p1 != "native" or p2 != "native":
+            raise RuntimeError(f"query fell back to host: {backend.fallback_reason}")
+        return r1, r2
+
+    tl = time.perf_counter()
+    for i in range(args.warmup):
+        step(1000 + i)
+    torch.cuda.synchronize()
+    barrier()
+    warm_s = time.perf_counter() - tl
+    log(rank, f"[bench] warmup {args.warmup} steps in {warm_s:.2f}s "
+              f"(includes first HBM load of the indexes)")
+
+    barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    results = []
+    for i in range(args.steps):
+        results.append(step(i))
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist:
+        elapsed = dist.all_reduce_max_float(elapsed)
+    nq = 2 * args.steps
+    qps = nq / elapsed
+    ms_step = elapsed / args.steps * 1000.0
+
+    # ---------------------------------------------------------------- per-query latency
+    lat = {}
+    for name, fn in (("q6_filter_ms", q6), ("q3_join_ms", q3)):
+        barrier()
+        torch.cuda.synchronize()
+        tq = time.perf_counter()
+        for i in range(5):
+            fn(i).collect()
+        torch.cuda.synchronize()
+        dtq = (time.perf_counter() - tq) / 5
+        lat[name] = round((dist.all_reduce_max_float(dtq) if dist else dtq) * 1000, 3)
+
+    # ---------------------------------------------------------------- cross-check
+    check = None
+    if not args.no_crosscheck and world == 1:
+        s.disableHyperspace()
+        tc = time.perf_counter()
+        n6 = q6(0).collect()[0][0]
+        n3 = sorted(q3(0).collect())
+        noidx_s = time.perf_counter() - tc
+        s.enableHyperspace()
+        i6 = results[0][0][0][0]
+        i3 = sorted(results[0][1])
+        ok6 = abs(n6 - i6) <= 1e-9 * abs(n6)
+        ok3 = len(n3) == len(i3) and all(a[2] == b[2] and abs(a[1] - b[1]) <= 1e-9 * abs(b[1])
+                                         for a, b in zip(i3, n3))
+        check = {"index_vs_full_scan_match": bool(ok6 and ok3),
+                 "no_index_q6_plus_q3_s": round(noidx_s, 3)}
+        if not (ok6 and ok3):
+            raise RuntimeError(f"cross-check failed: {i6} vs {n6}; {i3} vs {n3}")
+
+    if rank == 0:
+        out = {"metric": METRIC, "value": round(qps, 3), "unit": "queries/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
+               "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+               "dtype": "fp64", "data": "synthetic",
+               "config": {"model": f"tpch-sf{sf:g} lineitem/orders covering indexes",
+                          "global_batch": 2, "seq_len": 0,
+                          "parallelism": f"bucket-dp{world}", "num_buckets": args.buckets,
+                          "source_files": nfiles},
+               "index_build_gbps": round(build_gbps, 3), "index_build_s": round(build_s, 3),
+               "index_build": per_index, "latency": lat, "warmup_s": round(warm_s, 3),
+               "datagen_s": round(gen_s, 2), "crosscheck": check,
+               "device_cache": {"hits": backend.cache.hits, "misses": backend.cache.misses}}
+        print(json.dumps(out), flush=True)
+    if dist:
+        barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

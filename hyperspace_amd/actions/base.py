@@ -107,7 +107,9 @@ class Action:
     def run(self) -> None:
         try:
             self._log_event("Operation started.")
+            self._barrier()   # every rank has pinned base_id / target paths
             self.validate()
+            self._barrier()   # nobody writes the log before every rank validated
             self._begin()
             self._fault("after_begin")
             self.op()

@@ -30,6 +30,9 @@ class CreateActionBase:
         self.data_manager = data_manager
         self.file_id_tracker = FileIdTracker()
         self._index_data_path = None
+        # Pin the target version now: under SPMD every rank must agree on it before any rank
+        # creates the directory.
+        _ = self.index_data_path
 
     @property
     def index_data_path(self) -> str:

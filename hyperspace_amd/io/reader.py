@@ -22,6 +22,17 @@ from ..utils import path_utils as P
 
 SUPPORTED_FORMATS = ("parquet", "csv", "json", "orc", "text", "avro", "delta")
 
+_POOL = None
+
+
+def _io_pool():
+    """Shared host decode pool (files are decoded concurrently; pyarrow releases the GIL)."""
+    global _POOL
+    if _POOL is None:
+        import concurrent.futures as cf
+        _POOL = cf.ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4))
+    return _POOL
+
 
 def _infer_partition_value(v: str):
     if v == "__HIVE_DEFAULT_PARTITION__":
@@ -182,25 +193,31 @@ def read_files(fmt: str, files: List[str], data_schema: pa.Schema, options: dict
     part_cols = [f for f in pspec.columns if (need is None or f.name in need)
                  and f.name not in data_schema.names]
     out_schema = pa.schema(data_cols + part_cols)
-    tables = []
     file_idx = []
     read_schema = pa.schema(data_cols)
-    for i, fq in enumerate(files):
+
+    def one(fq):
         local = P.to_local(fq)
         if fmt == "parquet" and not data_cols:
             import pyarrow.parquet as pq
             t = pq.read_table(local, columns=[])
         else:
             t = read_one(fmt, local, read_schema, options)
-        nrows = t.num_rows
         if part_cols:
+            nrows = t.num_rows
             pdir = P.qualify(os.path.dirname(local))
             vals = pspec.partitions.get(pdir, {})
             for f in part_cols:
                 t = t.append_column(f, pa.array([vals.get(f.name)] * nrows, f.type))
-        tables.append(t)
-        if with_file_index:
-            file_idx.append(pa.array(np.full(nrows, i, dtype=np.int32)))
+        return t
+
+    if len(files) > 1:
+        tables = list(_io_pool().map(one, files))
+    else:
+        tables = [one(f) for f in files]
+    if with_file_index:
+        for i, t in enumerate(tables):
+            file_idx.append(pa.array(np.full(t.num_rows, i, dtype=np.int32)))
     if not tables:
         t = out_schema.empty_table()
     else:
