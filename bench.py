@@ -108,9 +108,7 @@ def main():
         dt = time.perf_counter() - tb
         local_bytes = float(device_build.LAST_BUILD_STATS.get("source_bytes", 0))
         if dist:
-            t = torch.tensor([local_bytes], dtype=torch.float64, device=dev)
-            torch.distributed.all_reduce(t)
-            local_bytes = float(t.item())
+            local_bytes = dist.all_reduce_sum_float(local_bytes)
             dt = dist.all_reduce_max_float(dt)
         build_s += dt
         build_bytes += local_bytes
@@ -163,15 +161,28 @@ def main():
     log(rank, f"[bench] warmup {args.warmup} steps in {warm_s:.2f}s "
               f"(includes first HBM load of the indexes)")
 
+    prof = None
+    if os.environ.get("HS_BENCH_PROFILE") and rank == 0:
+        import cProfile
+        prof = cProfile.Profile()
     barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
+    if prof is not None:
+        prof.enable()
     results = []
     for i in range(args.steps):
         results.append(step(i))
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t_start
+    if prof is not None:
+        import io
+        import pstats
+        prof.disable()
+        buf = io.StringIO()
+        pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(40)
+        log(rank, buf.getvalue())
     if dist:
         elapsed = dist.all_reduce_max_float(elapsed)
     nq = 2 * args.steps

@@ -12,7 +12,7 @@
 #define JN_BLOCK 256
 #define JN_ITEMS 8
 #define JN_TILE (JN_BLOCK * JN_ITEMS)
-#define JN_LDS_KEYS 6144
+#define JN_LDS_KEYS 4096
 #define JN_SPLIT 8   // column slots < 8: left side, >= 8: right side
 
 struct JoinParams {
@@ -142,100 +142,56 @@ __global__ __launch_bounds__(JN_BLOCK) void hs_join_agg_kernel(
   extern __shared__ __attribute__((aligned(16))) double glds[];
   const int A = p.naggs;
   const int GA = GROUPED ? p.num_groups * A : A;
-  double* g_sum = glds;
-  double* g_min = glds + GA;
-  double* g_max = glds + 2 * GA;
-  unsigned long long* g_cnt = (unsigned long long*)(glds + 3 * GA);
-  if (GROUPED) {
-    for (int i = threadIdx.x; i < GA; i += JN_BLOCK) {
-      g_sum[i] = 0.0;
-      g_min[i] = __builtin_inf();
-      g_max[i] = -__builtin_inf();
-      g_cnt[i] = 0ull;
-    }
-  }
-  double s[HS_MAX_AGGS], mn[HS_MAX_AGGS], mx[HS_MAX_AGGS];
-  int64_t c[HS_MAX_AGGS];
-#pragma unroll
-  for (int a = 0; a < HS_MAX_AGGS; ++a) {
-    s[a] = 0.0; c[a] = 0; mn[a] = __builtin_inf(); mx[a] = -__builtin_inf();
-  }
+  GroupLds gl = group_lds(glds, GROUPED ? GA : 0);
+  if (GROUPED) group_lds_init(gl, GA, JN_BLOCK);  // visible after the tile setup barrier
+  AggAcc acc;
+  acc_init(acc);
   const bool fl = p.key_is_float != 0;
+  const ColDesc& lk = p.cols[p.lkey];
   const int64_t ntiles = tile_prefix[R];
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     TileCtx ctx = join_tile_setup(p, rstart, rlen, rbucket, roff, R, tile_prefix, t, skeys, sh);
     for (int it = 0; it < JN_ITEMS; ++it) {
       const int64_t k = (int64_t)it * JN_BLOCK + threadIdx.x;
-      if (k >= ctx.rows) break;
       const int64_t lrow = ctx.row0 + k;
-      const ColDesc& lk = p.cols[p.lkey];
-      if (!col_valid(lk, lrow)) continue;
       RowRef rr{lrow, 0};
-      if (!hs_eval_cnf(p.preds, 0, p.nlp, p.cols, JN_SPLIT, rr)) continue;
-      const uint64_t key = join_key(lk, lrow, fl);
-      for (int64_t j = span_lower(ctx, skeys, p, key); j < ctx.re && span_key(ctx, skeys, p, j) == key; ++j) {
-        rr.r1 = j;
-        if (!hs_eval_cnf(p.preds, p.nlp, p.npreds, p.cols, JN_SPLIT, rr)) continue;
+      bool lok = k < ctx.rows && col_valid(lk, lrow) &&
+                 hs_eval_cnf(p.preds, 0, p.nlp, p.cols, JN_SPLIT, rr);
+      uint64_t key = 0;
+      int64_t j = 0;
+      if (lok) {
+        key = join_key(lk, lrow, fl);
+        j = span_lower(ctx, skeys, p, key);
+        lok = j < ctx.re && span_key(ctx, skeys, p, j) == key;
+      }
+      // one match per lane per round; rounds are wave-uniform so acc_row sees a converged wave
+      while (__any(lok)) {
+        bool pass = false;
         int gidx = 0;
-        if (GROUPED) {
-          const ColDesc& gc = p.cols[p.group_col];
-          const int64_t grow = p.group_col >= JN_SPLIT ? j : lrow;
-          if (!col_valid(gc, grow)) continue;
-          gidx = (int)(load_i64(gc, grow) - p.group_base);
-          if (gidx < 0 || gidx >= p.num_groups) continue;
-        }
-#pragma unroll
-        for (int a = 0; a < HS_MAX_AGGS; ++a) {
-          if (a >= A) break;
-          const AggSpec& ag = p.aggs[a];
-          double v = 0.0;
-          if (ag.kind != AK_COUNT_STAR && !hs_agg_value(ag, p.cols, JN_SPLIT, rr, v)) continue;
-          if (GROUPED) {
-            const int slot = gidx * A + a;
-            if (ag.kind == AK_SUM) atomicAdd(&g_sum[slot], v);
-            else if (ag.kind == AK_MIN) hs_lds_atomic_min(&g_min[slot], v);
-            else if (ag.kind == AK_MAX) hs_lds_atomic_max(&g_max[slot], v);
-            atomicAdd(&g_cnt[slot], 1ull);
-          } else {
-            s[a] += v; c[a] += 1; mn[a] = fmin(mn[a], v); mx[a] = fmax(mx[a], v);
+        if (lok) {
+          rr.r1 = j;
+          pass = hs_eval_cnf(p.preds, p.nlp, p.npreds, p.cols, JN_SPLIT, rr);
+          if (GROUPED && pass) {
+            const ColDesc& gc = p.cols[p.group_col];
+            const int64_t grow = p.group_col >= JN_SPLIT ? j : lrow;
+            if (!col_valid(gc, grow)) {
+              pass = false;
+            } else {
+              gidx = (int)(load_i64(gc, grow) - p.group_base);
+              if (gidx < 0 || gidx >= p.num_groups) pass = false;
+            }
           }
+        }
+        acc_row<GROUPED>(acc, p.aggs, A, pass, gidx, p.cols, JN_SPLIT, rr, gl);
+        if (lok) {
+          ++j;
+          lok = j < ctx.re && span_key(ctx, skeys, p, j) == key;
         }
       }
     }
     __syncthreads();  // skeys reuse
   }
-  if (GROUPED) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < GA; i += JN_BLOCK) {
-      const int64_t o = (int64_t)blockIdx.x * GA + i;
-      psum[o] = g_sum[i]; pcnt[o] = (int64_t)g_cnt[i]; pmin[o] = g_min[i]; pmax[o] = g_max[i];
-    }
-    return;
-  }
-  __shared__ double r_s[JN_BLOCK / 64][HS_MAX_AGGS], r_mn[JN_BLOCK / 64][HS_MAX_AGGS],
-      r_mx[JN_BLOCK / 64][HS_MAX_AGGS];
-  __shared__ int64_t r_c[JN_BLOCK / 64][HS_MAX_AGGS];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int a = 0; a < HS_MAX_AGGS; ++a) {
-    if (a >= A) break;
-    const double ws = hs_wave_sum(s[a]);
-    const int64_t wc = hs_wave_sum(c[a]);
-    const double wmn = hs_wave_min(mn[a]);
-    const double wmx = hs_wave_max(mx[a]);
-    if (lane == 0) { r_s[w][a] = ws; r_c[w][a] = wc; r_mn[w][a] = wmn; r_mx[w][a] = wmx; }
-  }
-  __syncthreads();
-  if (threadIdx.x < A) {
-    const int a = threadIdx.x;
-    double ts = 0.0, tmn = __builtin_inf(), tmx = -__builtin_inf();
-    int64_t tc = 0;
-    for (int ww = 0; ww < JN_BLOCK / 64; ++ww) {
-      ts += r_s[ww][a]; tc += r_c[ww][a]; tmn = fmin(tmn, r_mn[ww][a]); tmx = fmax(tmx, r_mx[ww][a]);
-    }
-    const int64_t o = (int64_t)blockIdx.x * A + a;
-    psum[o] = ts; pcnt[o] = tc; pmin[o] = tmn; pmax[o] = tmx;
-  }
+  acc_flush<GROUPED, JN_BLOCK>(acc, A, GA, gl, psum, pcnt, pmin, pmax);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -334,9 +290,14 @@ extern "C" {
 int hs_join_params_size() { return (int)sizeof(JoinParams); }
 int hs_join_tile_rows() { return JN_TILE; }
 
+int hs_agg_final(const double* psum, const int64_t* pcnt, const double* pmin, const double* pmax,
+                 int nblk, int GA, double* osum, int64_t* ocnt, double* omin, double* omax,
+                 void* stream);
+
 int hs_join_agg(const JoinParams* p, const int64_t* rstart, const int64_t* rlen,
                 const int32_t* rbucket, const int64_t* roff, int R, const int64_t* tile_prefix,
-                int grid, double* psum, int64_t* pcnt, double* pmin, double* pmax, void* stream) {
+                int grid, double* psum, int64_t* pcnt, double* pmin, double* pmax, double* osum,
+                int64_t* ocnt, double* omin, double* omax, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool grouped = p->group_col >= 0;
   if (grouped) {
@@ -349,7 +310,8 @@ int hs_join_agg(const JoinParams* p, const int64_t* rstart, const int64_t* rlen,
     hipLaunchKernelGGL(hs_join_agg_kernel<false>, dim3(grid), dim3(JN_BLOCK), 0, s, *p, rstart,
                        rlen, rbucket, roff, R, tile_prefix, psum, pcnt, pmin, pmax);
   }
-  return (int)hipGetLastError();
+  const int GA = grouped ? p->num_groups * p->naggs : p->naggs;
+  return hs_agg_final(psum, pcnt, pmin, pmax, grid, GA, osum, ocnt, omin, omax, stream);
 }
 
 int hs_join_count(const JoinParams* p, const int64_t* rstart, const int64_t* rlen,

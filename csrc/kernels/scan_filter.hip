@@ -13,6 +13,7 @@
 #define SF_ITEMS 8
 #define SF_TILE (SF_BLOCK * SF_ITEMS)
 #define SF_GRID 2048
+#define FIN_BLOCK 256
 
 struct ScanParams {
   ColDesc cols[HS_MAX_COLS];
@@ -31,7 +32,6 @@ struct ScanParams {
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int64_t lb_sorted(const ColDesc& c, int64_t lo, int64_t hi, uint64_t key,
                                              bool upper) {
-  // first index in [lo,hi) whose (valid, sortable) > key (upper) or >= key (lower); null < all.
   while (lo < hi) {
     const int64_t mid = lo + ((hi - lo) >> 1);
     bool less;
@@ -55,7 +55,6 @@ __global__ void hs_range_search_kernel(ColDesc key, const int64_t* __restrict__ 
   if (i >= nb) return;
   const int b = buckets ? buckets[i] : i;
   const int64_t s = bucket_off[b], e = bucket_off[b + 1];
-  // skip nulls (NULLS FIRST): first valid row
   int64_t first_valid = s;
   if (key.valid != nullptr) {
     int64_t lo = s, hi = e;
@@ -85,7 +84,6 @@ __global__ __launch_bounds__(1024) void hs_ranges_to_tiles_kernel(const int64_t*
   for (int base = 0; base < R; base += blockDim.x) {
     const int i = base + threadIdx.x;
     const int64_t t = i < R ? (rlen[i] + tile_rows - 1) / tile_rows : 0;
-    // block inclusive scan
     int64_t x = t;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int off = 1; off < 64; off <<= 1) {
@@ -132,28 +130,13 @@ __global__ __launch_bounds__(SF_BLOCK) void hs_scan_agg_kernel(
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int A = p.naggs;
   const int GA = GROUPED ? p.num_groups * A : A;
-  double* g_sum = lds;
-  double* g_min = lds + GA;
-  double* g_max = lds + 2 * GA;
-  unsigned long long* g_cnt = (unsigned long long*)(lds + 3 * GA);
+  GroupLds gl = group_lds(lds, GROUPED ? GA : 0);
   if (GROUPED) {
-    for (int i = threadIdx.x; i < GA; i += SF_BLOCK) {
-      g_sum[i] = 0.0;
-      g_min[i] = __builtin_inf();
-      g_max[i] = -__builtin_inf();
-      g_cnt[i] = 0ull;
-    }
+    group_lds_init(gl, GA, SF_BLOCK);
     __syncthreads();
   }
-  double s[HS_MAX_AGGS], mn[HS_MAX_AGGS], mx[HS_MAX_AGGS];
-  int64_t c[HS_MAX_AGGS];
-#pragma unroll
-  for (int a = 0; a < HS_MAX_AGGS; ++a) {
-    s[a] = 0.0;
-    c[a] = 0;
-    mn[a] = __builtin_inf();
-    mx[a] = -__builtin_inf();
-  }
+  AggAcc acc;
+  acc_init(acc);
   const int64_t ntiles = tile_prefix[R];
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int r = find_range(tile_prefix, R, t);
@@ -163,109 +146,69 @@ __global__ __launch_bounds__(SF_BLOCK) void hs_scan_agg_kernel(
 #pragma unroll 2
     for (int it = 0; it < SF_ITEMS; ++it) {
       const int64_t k = (int64_t)it * SF_BLOCK + threadIdx.x;
-      if (k >= rows) break;
       const int64_t row = row0 + k;
       RowRef rr{row, row};
-      if (!hs_eval_cnf(p.preds, 0, p.npreds, p.cols, HS_MAX_COLS, rr)) continue;
+      bool pass = k < rows && hs_eval_cnf(p.preds, 0, p.npreds, p.cols, HS_MAX_COLS, rr);
       int gidx = 0;
-      if (GROUPED) {
+      if (GROUPED && pass) {
         const ColDesc& gc = p.cols[p.group_col];
-        if (!col_valid(gc, row)) continue;  // null group handled on host (not supported here)
-        gidx = (int)(load_i64(gc, row) - p.group_base);
-        if (gidx < 0 || gidx >= p.num_groups) continue;
-      }
-#pragma unroll
-      for (int a = 0; a < HS_MAX_AGGS; ++a) {
-        if (a >= A) break;
-        const AggSpec& ag = p.aggs[a];
-        double v = 0.0;
-        bool ok = true;
-        if (ag.kind != AK_COUNT_STAR) ok = hs_agg_value(ag, p.cols, HS_MAX_COLS, rr, v);
-        if (!ok) continue;
-        if (GROUPED) {
-          const int slot = gidx * A + a;
-          if (ag.kind == AK_SUM) atomicAdd(&g_sum[slot], v);
-          else if (ag.kind == AK_MIN) hs_lds_atomic_min(&g_min[slot], v);
-          else if (ag.kind == AK_MAX) hs_lds_atomic_max(&g_max[slot], v);
-          atomicAdd(&g_cnt[slot], 1ull);
+        if (!col_valid(gc, row)) {
+          pass = false;
         } else {
-          s[a] += v;
-          c[a] += 1;
-          mn[a] = fmin(mn[a], v);
-          mx[a] = fmax(mx[a], v);
+          gidx = (int)(load_i64(gc, row) - p.group_base);
+          if (gidx < 0 || gidx >= p.num_groups) pass = false;
         }
       }
+      acc_row<GROUPED>(acc, p.aggs, A, pass, gidx, p.cols, HS_MAX_COLS, rr, gl);
     }
   }
-  if (GROUPED) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < GA; i += SF_BLOCK) {
-      const int64_t o = (int64_t)blockIdx.x * GA + i;
-      psum[o] = g_sum[i];
-      pcnt[o] = (int64_t)g_cnt[i];
-      pmin[o] = g_min[i];
-      pmax[o] = g_max[i];
-    }
-    return;
-  }
-  // global aggregate: deterministic wave + block reduction
-  __shared__ double r_s[SF_BLOCK / 64][HS_MAX_AGGS], r_mn[SF_BLOCK / 64][HS_MAX_AGGS],
-      r_mx[SF_BLOCK / 64][HS_MAX_AGGS];
-  __shared__ int64_t r_c[SF_BLOCK / 64][HS_MAX_AGGS];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int a = 0; a < HS_MAX_AGGS; ++a) {
-    if (a >= A) break;
-    const double ws = hs_wave_sum(s[a]);
-    const int64_t wc = hs_wave_sum(c[a]);
-    const double wmn = hs_wave_min(mn[a]);
-    const double wmx = hs_wave_max(mx[a]);
-    if (lane == 0) {
-      r_s[w][a] = ws;
-      r_c[w][a] = wc;
-      r_mn[w][a] = wmn;
-      r_mx[w][a] = wmx;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < A) {
-    const int a = threadIdx.x;
-    double ts = 0.0, tmn = __builtin_inf(), tmx = -__builtin_inf();
-    int64_t tc = 0;
-    for (int ww = 0; ww < SF_BLOCK / 64; ++ww) {
-      ts += r_s[ww][a];
-      tc += r_c[ww][a];
-      tmn = fmin(tmn, r_mn[ww][a]);
-      tmx = fmax(tmx, r_mx[ww][a]);
-    }
-    const int64_t o = (int64_t)blockIdx.x * A + a;
-    psum[o] = ts;
-    pcnt[o] = tc;
-    pmin[o] = tmn;
-    pmax[o] = tmx;
-  }
+  acc_flush<GROUPED, SF_BLOCK>(acc, A, GA, gl, psum, pcnt, pmin, pmax);
 }
 
-__global__ void hs_agg_final_kernel(const double* __restrict__ psum, const int64_t* __restrict__ pcnt,
-                                    const double* __restrict__ pmin, const double* __restrict__ pmax,
-                                    int nblk, int GA, double* __restrict__ osum,
-                                    int64_t* __restrict__ ocnt, double* __restrict__ omin,
-                                    double* __restrict__ omax) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= GA) return;
+// Deterministic final reduction: one workgroup per output slot, fixed-order tree.
+__global__ __launch_bounds__(FIN_BLOCK) void hs_agg_final_kernel(
+    const double* __restrict__ psum, const int64_t* __restrict__ pcnt,
+    const double* __restrict__ pmin, const double* __restrict__ pmax, int nblk, int GA,
+    double* __restrict__ osum, int64_t* __restrict__ ocnt, double* __restrict__ omin,
+    double* __restrict__ omax) {
+  __shared__ double rs[FIN_BLOCK / 64], rmn[FIN_BLOCK / 64], rmx[FIN_BLOCK / 64];
+  __shared__ int64_t rc[FIN_BLOCK / 64];
+  const int i = blockIdx.x;
   double s = 0.0, mn = __builtin_inf(), mx = -__builtin_inf();
   int64_t c = 0;
-  for (int b = 0; b < nblk; ++b) {
+  for (int b = threadIdx.x; b < nblk; b += FIN_BLOCK) {
     const int64_t o = (int64_t)b * GA + i;
     s += psum[o];
     c += pcnt[o];
     mn = fmin(mn, pmin[o]);
     mx = fmax(mx, pmax[o]);
   }
-  osum[i] = s;
-  ocnt[i] = c;
-  omin[i] = mn;
-  omax[i] = mx;
+  s = hs_wave_sum(s);
+  c = hs_wave_sum(c);
+  mn = hs_wave_min(mn);
+  mx = hs_wave_max(mx);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    rs[w] = s;
+    rc[w] = c;
+    rmn[w] = mn;
+    rmx[w] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double ts = 0.0, tmn = __builtin_inf(), tmx = -__builtin_inf();
+    int64_t tc = 0;
+    for (int k = 0; k < FIN_BLOCK / 64; ++k) {
+      ts += rs[k];
+      tc += rc[k];
+      tmn = fmin(tmn, rmn[k]);
+      tmx = fmax(tmx, rmx[k]);
+    }
+    osum[i] = ts;
+    ocnt[i] = tc;
+    omin[i] = tmn;
+    omax[i] = tmx;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -365,6 +308,15 @@ int hs_ranges_to_tiles(const int64_t* rlen, int R, int64_t* tile_prefix, void* s
   return (int)hipGetLastError();
 }
 
+int hs_agg_final(const double* psum, const int64_t* pcnt, const double* pmin, const double* pmax,
+                 int nblk, int GA, double* osum, int64_t* ocnt, double* omin, double* omax,
+                 void* stream) {
+  if (GA <= 0) return 0;
+  hipLaunchKernelGGL(hs_agg_final_kernel, dim3(GA), dim3(FIN_BLOCK), 0, (hipStream_t)stream, psum,
+                     pcnt, pmin, pmax, nblk, GA, osum, ocnt, omin, omax);
+  return (int)hipGetLastError();
+}
+
 // Partials: 4 arrays of grid*GA. Outputs: 4 arrays of GA.
 int hs_scan_agg(const ScanParams* p, const int64_t* rstart, const int64_t* rlen, int R,
                 const int64_t* tile_prefix, int grid, double* psum, int64_t* pcnt, double* pmin,
@@ -383,9 +335,7 @@ int hs_scan_agg(const ScanParams* p, const int64_t* rstart, const int64_t* rlen,
     hipLaunchKernelGGL(hs_scan_agg_kernel<false>, dim3(grid), dim3(SF_BLOCK), 0, s, *p, rstart,
                        rlen, R, tile_prefix, psum, pcnt, pmin, pmax);
   }
-  hipLaunchKernelGGL(hs_agg_final_kernel, dim3((GA + 255) / 256), dim3(256), 0, s, psum, pcnt, pmin,
-                     pmax, grid, GA, osum, ocnt, omin, omax);
-  return (int)hipGetLastError();
+  return hs_agg_final(psum, pcnt, pmin, pmax, grid, GA, osum, ocnt, omin, omax, stream);
 }
 
 int hs_scan_count(const ScanParams* p, const int64_t* rstart, const int64_t* rlen, int R,

@@ -132,7 +132,7 @@ def device_build_from_source(session, rel, files: List[str], columns: List[str],
             flat.append(cols[n].data)
             flat.append(cols[n].valid)
         flat.append(bucket)
-        recv, _ = exchange(flat, dest, world)
+        recv, _ = exchange(flat, dest, world, dist)
         bucket = recv[-1]
         new = {}
         for i, n in enumerate(names):

@@ -52,6 +52,21 @@ def read_parquet_columns(paths: List[str], columns: List[str]) -> List[pa.Table]
     return list(_pool().map(one, paths))
 
 
+_FILES_KEYS: Dict[int, tuple] = {}
+
+
+def _files_key(files) -> tuple:
+    """Identity of a file list (path, size, mtime); memoized per list object."""
+    hit = _FILES_KEYS.get(id(files))
+    if hit is not None and hit[0] is files:
+        return hit[1]
+    k = tuple((f.path, f.length, f.modification_time) for f in files)
+    if len(_FILES_KEYS) > 4096:
+        _FILES_KEYS.clear()
+    _FILES_KEYS[id(files)] = (files, k)
+    return k
+
+
 class DeviceTableCache:
     def __init__(self, budget_bytes: int):
         self.budget = int(budget_bytes)
@@ -62,7 +77,8 @@ class DeviceTableCache:
         self.misses = 0
 
     def _key(self, files, columns, extra):
-        return (tuple((f.path, f.length, f.modification_time) for f in files), tuple(columns), extra)
+        fk = _files_key(files)
+        return (fk, tuple(columns), extra)
 
     def get(self, files, columns, extra, loader) -> DeviceTable:
         key = self._key(files, columns, extra)

@@ -83,6 +83,7 @@ class GpuBackend:
         self.fallback_reason = None
         self.metrics: Dict[str, float] = {}
         self._cpu = None
+        self._domains: Dict[tuple, tuple] = {}
 
     # ------------------------------------------------------------------------------------------
     @property
@@ -166,7 +167,7 @@ class GpuBackend:
         d = self._dist()
         rank, world = (d.rank, d.world) if d is not None else (0, 1)
         names = [a.name for a in p.output]
-        if rel.is_index() and self._all_bucket_files(files, rel.index.num_buckets):
+        if rel.is_index() and self._all_bucket_files(rel.location, files, rel.index.num_buckets):
             idx = rel.index
             ncol = {n.lower(): n for n in idx.schema.names}
             cols = [ncol[a.name.lower()] for a in p.output]
@@ -194,21 +195,27 @@ class GpuBackend:
         return DRel(table, {a.expr_id: a.name for a in p.output}, list(p.output))
 
     @staticmethod
-    def _all_bucket_files(files, nb) -> bool:
-        from ..io.writer import get_bucket_id
-        from ..utils import path_utils as P
-        for f in files:
-            b = get_bucket_id(P.get_name(f.path))
-            if b is None or b >= nb:
-                return False
-        return True
+    def _all_bucket_files(location, files, nb) -> bool:
+        v = getattr(location, "_hs_all_bucket_files", None)
+        if v is None or v[0] != nb:
+            from ..io.writer import get_bucket_id
+            from ..utils import path_utils as P
+            ok = True
+            for f in files:
+                b = get_bucket_id(P.get_name(f.path))
+                if b is None or b >= nb:
+                    ok = False
+                    break
+            v = (nb, ok)
+            location._hs_all_bucket_files = v
+        return v[1]
 
     # -- lowering helpers ----------------------------------------------------------------------
     def _ranges(self, r: DRel, conds: list):
         """Row ranges after bucket / sort-key pruning on the leading indexed column."""
         t = r.table
         if not (r.bucketed and r.sort_attrs):
-            return K.full_ranges(t.bucket_offsets_host, self.device)
+            return self._full_ranges(t)
         lead = r.sort_attrs[0]
         kc = r.col(lead)
         lo = hi = None
@@ -249,8 +256,15 @@ class GpuBackend:
             import torch
             buckets = torch.tensor([eq_bucket], dtype=torch.int32, device=self.device)
         if lo is None and hi is None and buckets is None:
-            return K.full_ranges(t.bucket_offsets_host, self.device)
+            return self._full_ranges(t)
         return K.range_search(kc, t.bucket_offsets, buckets, lo, lo_incl, hi, hi_incl)
+
+    def _full_ranges(self, t: DeviceTable):
+        fr = getattr(t, "_full_ranges", None)
+        if fr is None:
+            fr = K.full_ranges(t.bucket_offsets_host, self.device)
+            t._full_ranges = fr
+        return fr
 
     @staticmethod
     def _bucket_of_literal(v, dtype, nb) -> int:
@@ -521,12 +535,22 @@ class GpuBackend:
             G = len(c.dictionary)
             base = 0
         else:
-            import torch
-            vals = c.data if c.valid is None else c.data[c.valid.bool()]
-            if vals.numel() == 0:
+            # tables are immutable: the group domain is computed once per column
+            ck = id(c)
+            hit = self._domains.get(ck)
+            dom = hit[1] if hit is not None and hit[0] is c else None
+            if dom is None:
+                import torch
+                vals = c.data if c.valid is None else c.data[c.valid.bool()]
+                if vals.numel() == 0:
+                    dom = (0, 0)
+                else:
+                    lo, hi = torch.aminmax(vals)
+                    dom = (int(lo.item()), int(hi.item()) - int(lo.item()) + 1)
+                self._domains[ck] = (c, dom)
+            base, G = dom
+            if G == 0:
                 return None
-            lo, hi = torch.aminmax(vals)
-            base, G = int(lo.item()), int(hi.item()) - int(lo.item()) + 1
         if G > limit:
             raise Unsupported("group domain too large for LDS aggregation")
         return None, max(G, 1), base, c.dictionary, c.atype
@@ -549,7 +573,8 @@ class GpuBackend:
         if gs is None:  # empty group column
             return (*self._empty_agg(len(specs)), 1, 0, None, None)
         _, G, gbase, gdict, gtype = gs
-        p.group_col = col_info(group).slot if group is not None else -1
+        # a single-valued group key runs the register-accumulating (ungrouped) kernel
+        p.group_col = col_info(group).slot if (group is not None and G > 1) else -1
         p.num_groups, p.group_base = G, gbase
         for s, c in descs.items():
             p.cols[s] = c.desc()
@@ -584,7 +609,8 @@ class GpuBackend:
             if gs is None:
                 return (*self._empty_agg(len(specs)), 1, 0, None, None)
             _, G, gbase, gdict, gtype = gs
-            jp.group_col = col_info(group).slot
+            col_info(group)
+            jp.group_col = col_info(group).slot if G > 1 else -1
             jp.num_groups, jp.group_base = G, gbase
         else:
             G, gbase, gdict, gtype = 1, 0, None, None

@@ -281,12 +281,15 @@ def join_agg(params: NL.JoinParams, rstart, rlen, rbucket, roff, tile_prefix, gr
     pc_ = torch.empty(grid * GA, dtype=torch.int64, device=dev)
     pmn = torch.empty(grid * GA, dtype=torch.float64, device=dev)
     pmx = torch.empty(grid * GA, dtype=torch.float64, device=dev)
+    os_ = torch.empty(GA, dtype=torch.float64, device=dev)
+    oc = torch.empty(GA, dtype=torch.int64, device=dev)
+    omn = torch.empty(GA, dtype=torch.float64, device=dev)
+    omx = torch.empty(GA, dtype=torch.float64, device=dev)
     NL.check(L.hs_join_agg(C.byref(params), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
                            NL.ptr(roff), rstart.numel(), NL.ptr(tile_prefix), grid, NL.ptr(ps),
-                           NL.ptr(pc_), NL.ptr(pmn), NL.ptr(pmx), NL.stream_ptr()), "hs_join_agg")
-    ps = ps.view(grid, GA)
-    pc_ = pc_.view(grid, GA)
-    return ps.sum(0), pc_.sum(0), pmn.view(grid, GA).amin(0), pmx.view(grid, GA).amax(0)
+                           NL.ptr(pc_), NL.ptr(pmn), NL.ptr(pmx), NL.ptr(os_), NL.ptr(oc),
+                           NL.ptr(omn), NL.ptr(omx), NL.stream_ptr()), "hs_join_agg")
+    return os_, oc, omn, omx
 
 
 def join_pairs(params: NL.JoinParams, rstart, rlen, rbucket, roff, tile_prefix, max_tiles: int):

@@ -27,10 +27,17 @@ class DistContext:
             return None
         rank = int(os.environ.get("RANK", "0"))
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("HS_DIST_BACKEND") or (
+                "nccl" if torch.cuda.is_available() else "gloo")
         device = None
         if backend == "nccl":
             local = int(os.environ.get("LOCAL_RANK", "0"))
+            torch.cuda.set_device(local)
+            device = torch.device("cuda", local)
+        elif torch.cuda.is_available():
+            # gloo + GPU: ranks may share one device (multi-rank rehearsal on a 1-GPU box);
+            # collectives are staged through host memory.
+            local = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
             torch.cuda.set_device(local)
             device = torch.device("cuda", local)
         if init and not dist.is_initialized():
@@ -60,21 +67,54 @@ class DistContext:
         dist.broadcast_object_list(box, src=src)
         return box[0]
 
+    def _staged(self, t) -> bool:
+        return self.backend != "nccl" and t is not None and t.is_cuda
+
+    def all_reduce(self, t, op: str = "sum"):
+        """In-place all-reduce (RCCL on device; host-staged for gloo + CUDA tensors)."""
+        import torch.distributed as dist
+        rop = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN,
+               "max": dist.ReduceOp.MAX}[op]
+        if self._staged(t):
+            h = t.cpu()
+            dist.all_reduce(h, op=rop)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=rop)
+        return t
+
+    def all_to_all_single(self, out, inp, out_splits=None, in_splits=None):
+        import torch.distributed as dist
+        if self._staged(inp):
+            ho = out.new_empty(out.shape, device="cpu")
+            dist.all_to_all_single(ho, inp.cpu(), output_split_sizes=out_splits,
+                                   input_split_sizes=in_splits)
+            out.copy_(ho)
+        else:
+            dist.all_to_all_single(out, inp, output_split_sizes=out_splits,
+                                   input_split_sizes=in_splits)
+        return out
+
     def all_reduce_agg(self, sums, cnts, mins, maxs):
         """Combine partial aggregates (sum, count, min, max) across ranks — 4 small RCCL calls."""
-        import torch.distributed as dist
-        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-        dist.all_reduce(cnts, op=dist.ReduceOp.SUM)
-        dist.all_reduce(mins, op=dist.ReduceOp.MIN)
-        dist.all_reduce(maxs, op=dist.ReduceOp.MAX)
+        self.all_reduce(sums, "sum")
+        self.all_reduce(cnts, "sum")
+        self.all_reduce(mins, "min")
+        self.all_reduce(maxs, "max")
         return sums, cnts, mins, maxs
 
     def all_reduce_max_float(self, x: float) -> float:
         import torch
-        import torch.distributed as dist
         dev = self.device if self.backend == "nccl" else "cpu"
         t = torch.tensor([x], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        self.all_reduce(t, "max")
+        return float(t.item())
+
+    def all_reduce_sum_float(self, x: float) -> float:
+        import torch
+        dev = self.device if self.backend == "nccl" else "cpu"
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        self.all_reduce(t, "sum")
         return float(t.item())
 
     def owns(self, bucket: int) -> bool:

@@ -24,13 +24,18 @@ def order_by_dest(dest, world: int):
     return perm, counts
 
 
-def exchange(columns: List, dest, world: int, group=None) -> Tuple[List, "object"]:
-    """Send row i of every column to rank ``dest[i]``.  Returns (received columns, recv counts)."""
+def exchange(columns: List, dest, world: int, ctx=None) -> Tuple[List, "object"]:
+    """Send row i of every column to rank ``dest[i]``.  Returns (received columns, recv counts).
+
+    ``ctx`` is the session's DistContext (RCCL, or host-staged gloo for CPU rehearsals)."""
     import torch
     import torch.distributed as dist
+    a2a = ctx.all_to_all_single if ctx is not None else (
+        lambda o, i, os_=None, is_=None: dist.all_to_all_single(o, i, output_split_sizes=os_,
+                                                                  input_split_sizes=is_))
     perm, send_counts = order_by_dest(dest, world)
     recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts, group=group)
+    a2a(recv_counts, send_counts)
     send = send_counts.cpu().tolist()
     recv = recv_counts.cpu().tolist()
     total = int(sum(recv))
@@ -47,8 +52,7 @@ def exchange(columns: List, dest, world: int, group=None) -> Tuple[List, "object
         else:
             src = c.index_select(0, perm.long())
         dst = torch.empty((total,) + tuple(c.shape[1:]), dtype=c.dtype, device=c.device)
-        dist.all_to_all_single(dst, src.contiguous(), output_split_sizes=recv,
-                               input_split_sizes=send, group=group)
+        a2a(dst, src.contiguous(), recv, send)
         out.append(dst)
     return out, recv_counts
 

@@ -65,6 +65,17 @@ class FileIndex:
     def size_in_bytes(self) -> int:
         return sum(f.length for f in self.all_files())
 
+    def one_file_per_bucket(self) -> bool:
+        """True iff no two files carry the same bucket id (cached; the file list is fixed)."""
+        v = getattr(self, "_one_per_bucket", None)
+        if v is None:
+            from ..io.writer import get_bucket_id
+            from ..utils import path_utils as P
+            ids = [get_bucket_id(P.get_name(f.path)) for f in self.all_files()]
+            v = len(ids) == len(set(ids))
+            self._one_per_bucket = v
+        return v
+
     def __repr__(self):
         return f"{self.kind}[{', '.join(self.root_paths)}]"
 

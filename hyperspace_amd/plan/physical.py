@@ -179,13 +179,8 @@ class FileSourceScanExec(SparkPlan):
         if bs is None or not bs.sort_column_names:
             return []
         # Sorted output only when every bucket has at most one file (E2EHyperspaceRulesTest:455-479).
-        from ..io.writer import get_bucket_id
-        seen = set()
-        for f in self.relation.location.all_files():
-            b = get_bucket_id(f.name)
-            if b in seen:
-                return []
-            seen.add(b)
+        if not self.relation.location.one_file_per_bucket():
+            return []
         out = []
         for n in bs.sort_column_names:
             a = next((x for x in self._output if x.name.lower() == n.lower()), None)
