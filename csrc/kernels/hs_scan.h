@@ -151,24 +151,35 @@ __device__ __forceinline__ void hs_lds_atomic_max(double* addr, double v) {
 // ------------------------------------------------------------------------------------------------
 // Block accumulator shared by the scan and join aggregate kernels.
 //
-// Global aggregates accumulate in registers (no atomics).  Grouped aggregates are first reduced
-// across the wave per distinct group (ballot / readfirstlane peeling, so a wave with k distinct
-// groups issues k LDS atomics instead of 64) — low-cardinality GROUP BYs no longer serialize on
-// one LDS address.  Callers must invoke acc_row with the whole wave converged.
+// Global aggregates accumulate in registers (no atomics), one value per aggregate whose meaning
+// follows its kind (sum / min / max) plus a 32-bit valid-row count: 3 VGPRs per aggregate instead
+// of a full (sum, min, max, count) quad, which is what keeps the fused kernels at >= 4 waves/SIMD.
+// Grouped aggregates are first reduced across the wave per distinct group (ballot / readfirstlane
+// peeling, so a wave with k distinct groups issues k LDS atomics instead of 64) — low-cardinality
+// GROUP BYs no longer serialize on one LDS address.
 // ------------------------------------------------------------------------------------------------
 struct AggAcc {
-  double s[HS_MAX_AGGS], mn[HS_MAX_AGGS], mx[HS_MAX_AGGS];
-  int64_t c[HS_MAX_AGGS];
+  double v[HS_MAX_AGGS];
+  uint32_t c[HS_MAX_AGGS];
 };
 
-__device__ __forceinline__ void acc_init(AggAcc& acc) {
+__device__ __forceinline__ double agg_identity(int kind) {
+  return kind == AK_MIN ? __builtin_inf() : (kind == AK_MAX ? -__builtin_inf() : 0.0);
+}
+
+__device__ __forceinline__ void acc_init(AggAcc& acc, const AggSpec* aggs, int A) {
 #pragma unroll
   for (int a = 0; a < HS_MAX_AGGS; ++a) {
-    acc.s[a] = 0.0;
-    acc.c[a] = 0;
-    acc.mn[a] = __builtin_inf();
-    acc.mx[a] = -__builtin_inf();
+    acc.v[a] = a < A ? agg_identity(aggs[a].kind) : 0.0;
+    acc.c[a] = 0u;
   }
+}
+
+__device__ __forceinline__ void acc_add(AggAcc& acc, int a, int kind, double x) {
+  if (kind == AK_MIN) acc.v[a] = fmin(acc.v[a], x);
+  else if (kind == AK_MAX) acc.v[a] = fmax(acc.v[a], x);
+  else acc.v[a] += x;
+  acc.c[a] += 1u;
 }
 
 struct GroupLds {
@@ -191,66 +202,10 @@ __device__ __forceinline__ void group_lds_init(GroupLds g, int GA, int nthreads)
   }
 }
 
-template <bool GROUPED>
-__device__ __forceinline__ void acc_row(AggAcc& acc, const AggSpec* aggs, int A, bool pass, int g,
-                                        const ColDesc* cols, int split, RowRef rr, GroupLds gl) {
-  double v[HS_MAX_AGGS];
-  bool ok[HS_MAX_AGGS];
-#pragma unroll
-  for (int a = 0; a < HS_MAX_AGGS; ++a) {
-    v[a] = 0.0;
-    ok[a] = false;
-    if (a < A && pass) {
-      const AggSpec& ag = aggs[a];
-      ok[a] = ag.kind == AK_COUNT_STAR ? true : hs_agg_value(ag, cols, split, rr, v[a]);
-    }
-  }
-  if (!GROUPED) {
-#pragma unroll
-    for (int a = 0; a < HS_MAX_AGGS; ++a) {
-      if (a < A && ok[a]) {
-        acc.s[a] += v[a];
-        acc.c[a] += 1;
-        acc.mn[a] = fmin(acc.mn[a], v[a]);
-        acc.mx[a] = fmax(acc.mx[a], v[a]);
-      }
-    }
-    return;
-  }
-  const int lane = threadIdx.x & 63;
-  bool todo = pass;
-  while (true) {
-    const uint64_t act = __ballot(todo);
-    if (act == 0ull) break;
-    const int leader = __ffsll((unsigned long long)act) - 1;
-    const int g0 = __shfl(g, leader, 64);
-    const bool mine = todo && g == g0;
-#pragma unroll
-    for (int a = 0; a < HS_MAX_AGGS; ++a) {
-      if (a >= A) break;
-      const bool m = mine && ok[a];
-      const uint64_t cm = __ballot(m);
-      if (cm == 0ull) continue;
-      const double sv = hs_wave_sum(m ? v[a] : 0.0);
-      const double mnv = hs_wave_min(m ? v[a] : __builtin_inf());
-      const double mxv = hs_wave_max(m ? v[a] : -__builtin_inf());
-      if (lane == leader) {
-        const int slot = g0 * A + a;
-        const int kind = aggs[a].kind;
-        if (kind == AK_SUM) atomicAdd(&gl.sum[slot], sv);
-        else if (kind == AK_MIN) hs_lds_atomic_min(&gl.mn[slot], mnv);
-        else if (kind == AK_MAX) hs_lds_atomic_max(&gl.mx[slot], mxv);
-        atomicAdd(&gl.cnt[slot], (unsigned long long)__popcll(cm));
-      }
-    }
-    todo = todo && !mine;
-  }
-}
-
 // Write this block's partials: global -> [blockIdx][A]; grouped -> [blockIdx][G*A].
 template <bool GROUPED, int NT>
-__device__ __forceinline__ void acc_flush(const AggAcc& acc, int A, int GA, GroupLds gl,
-                                          double* psum, int64_t* pcnt, double* pmin,
+__device__ __forceinline__ void acc_flush(const AggAcc& acc, const AggSpec* aggs, int A, int GA,
+                                          GroupLds gl, double* psum, int64_t* pcnt, double* pmin,
                                           double* pmax) {
   if (GROUPED) {
     __syncthreads();
@@ -263,38 +218,38 @@ __device__ __forceinline__ void acc_flush(const AggAcc& acc, int A, int GA, Grou
     }
     return;
   }
-  __shared__ double r_s[NT / 64][HS_MAX_AGGS], r_mn[NT / 64][HS_MAX_AGGS], r_mx[NT / 64][HS_MAX_AGGS];
+  __shared__ double r_v[NT / 64][HS_MAX_AGGS];
   __shared__ int64_t r_c[NT / 64][HS_MAX_AGGS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int a = 0; a < HS_MAX_AGGS; ++a) {
     if (a >= A) break;
-    const double ws = hs_wave_sum(acc.s[a]);
-    const int64_t wc = hs_wave_sum(acc.c[a]);
-    const double wmn = hs_wave_min(acc.mn[a]);
-    const double wmx = hs_wave_max(acc.mx[a]);
+    const int kind = aggs[a].kind;
+    double wv;
+    if (kind == AK_MIN) wv = hs_wave_min(acc.v[a]);
+    else if (kind == AK_MAX) wv = hs_wave_max(acc.v[a]);
+    else wv = hs_wave_sum(acc.v[a]);
+    const int64_t wc = hs_wave_sum((int64_t)acc.c[a]);
     if (lane == 0) {
-      r_s[w][a] = ws;
+      r_v[w][a] = wv;
       r_c[w][a] = wc;
-      r_mn[w][a] = wmn;
-      r_mx[w][a] = wmx;
     }
   }
   __syncthreads();
   if (threadIdx.x < A) {
     const int a = threadIdx.x;
-    double ts = 0.0, tmn = __builtin_inf(), tmx = -__builtin_inf();
+    const int kind = aggs[a].kind;
+    double tv = agg_identity(kind);
     int64_t tc = 0;
     for (int ww = 0; ww < NT / 64; ++ww) {
-      ts += r_s[ww][a];
+      const double x = r_v[ww][a];
+      tv = kind == AK_MIN ? fmin(tv, x) : (kind == AK_MAX ? fmax(tv, x) : tv + x);
       tc += r_c[ww][a];
-      tmn = fmin(tmn, r_mn[ww][a]);
-      tmx = fmax(tmx, r_mx[ww][a]);
     }
     const int64_t o = (int64_t)blockIdx.x * A + a;
-    psum[o] = ts;
+    psum[o] = (kind == AK_MIN || kind == AK_MAX) ? 0.0 : tv;
     pcnt[o] = tc;
-    pmin[o] = tmn;
-    pmax[o] = tmx;
+    pmin[o] = kind == AK_MIN ? tv : __builtin_inf();
+    pmax[o] = kind == AK_MAX ? tv : -__builtin_inf();
   }
 }

@@ -1,18 +1,24 @@
 // K8: co-located per-bucket sort-merge join of two bucketed covering indexes.
 //
 // Both sides are sorted by the join key inside every bucket and bucket b of the left index joins
-// only bucket b of the right one (equal numBuckets => zero inter-GPU traffic).  A workgroup takes
-// a 2048-row tile of one left bucket range; lane 0 binary-searches the right bucket for the
-// tile's [first key, last key] span, the whole span of right keys is staged in LDS, and every
-// lane then binary-searches its key in LDS (falls back to the global bucket when the span does
-// not fit).  Modes: fused aggregate (filters on both sides + product-of-affine aggregates, the
-// TPC-H Q3-style hot path) or count/emit of (left_row, right_row) pairs for general joins.
-#include "hs_scan.h"
+// only bucket b of the right one (equal numBuckets => zero inter-GPU traffic).
+//
+//  1. hs_join_spans_kernel — one *thread* per 2048-row left tile binary-searches the right
+//     bucket for the tile's [first key, last key] span.  All tiles search concurrently, so the
+//     ~40 dependent HBM round trips of a search are paid once for the whole join instead of once
+//     per tile on a block's critical path.
+//  2. the join kernels — each block takes a contiguous chunk of tiles, stages the tile's right
+//     key span in LDS (coalesced), and every lane looks its SF_ITEMS left keys up in LDS; the
+//     match rounds evaluate right-side predicates / aggregates predicate-major (hs_vec.h).
+//
+// Modes: fused aggregate (filters on both sides + product-of-affine aggregates, the TPC-H
+// Q3-style hot path) or count/emit of (left_row, right_row) pairs for general joins.
+#include "hs_vec.h"
 
 #define JN_BLOCK 256
-#define JN_ITEMS 8
+#define JN_ITEMS 4
 #define JN_TILE (JN_BLOCK * JN_ITEMS)
-#define JN_LDS_KEYS 4096
+#define JN_LDS_KEYS 2048
 #define JN_SPLIT 8   // column slots < 8: left side, >= 8: right side
 
 struct JoinParams {
@@ -40,15 +46,6 @@ __device__ __forceinline__ uint64_t join_key(const ColDesc& c, int64_t row, bool
   return (uint64_t)load_i64(c, row) ^ 0x8000000000000000ull;
 }
 
-__device__ __forceinline__ int64_t find_range_j(const int64_t* tile_prefix, int R, int64_t t) {
-  int lo = 0, hi = R;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (tile_prefix[mid] <= t) lo = mid; else hi = mid;
-  }
-  return lo;
-}
-
 // global lower/upper bound over [lo,hi) of the right key column (nulls first, never equal)
 __device__ __forceinline__ int64_t rkey_bound(const ColDesc& c, int64_t lo, int64_t hi, uint64_t k,
                                               bool upper, bool is_float) {
@@ -65,67 +62,130 @@ __device__ __forceinline__ int64_t rkey_bound(const ColDesc& c, int64_t lo, int6
   return lo;
 }
 
-struct TileCtx {
+// Per tile: left rows [row0, row0+rows) and the right key span [rs, re).
+__global__ __launch_bounds__(256) void hs_join_spans_kernel(
+    JoinParams p, const int64_t* __restrict__ rstart, const int64_t* __restrict__ rlen,
+    const int32_t* __restrict__ rbucket, const int64_t* __restrict__ roff, int R,
+    const int64_t* __restrict__ tile_prefix, int64_t* __restrict__ spans) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= tile_prefix[R]) return;
+  const int r = tile_range_of(tile_prefix, R, t);
+  const int64_t off = (t - tile_prefix[r]) * JN_TILE;
+  const int64_t row0 = rstart[r] + off;
+  const int64_t rows = min((int64_t)JN_TILE, rlen[r] - off);
+  const bool fl = p.key_is_float != 0;
+  const int b = rbucket[r];
+  const int64_t bs = roff[b], be = roff[b + 1];
+  const ColDesc& lk = p.cols[p.lkey];
+  // first valid left key of the tile (left is sorted, nulls first) -> binary search
+  int64_t f = row0, l = row0 + rows - 1;
+  if (lk.valid != nullptr) {
+    int64_t lo = row0, hi = row0 + rows;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (!col_valid(lk, mid)) lo = mid + 1; else hi = mid;
+    }
+    f = lo;
+  }
+  int64_t rs = bs, re = bs;
+  if (f <= l) {
+    const uint64_t kmin = join_key(lk, f, fl), kmax = join_key(lk, l, fl);
+    rs = rkey_bound(p.cols[p.rkey], bs, be, kmin, false, fl);
+    re = rkey_bound(p.cols[p.rkey], rs, be, kmax, true, fl);
+  }
+  spans[4 * t + 0] = row0;
+  spans[4 * t + 1] = rows;
+  spans[4 * t + 2] = rs;
+  spans[4 * t + 3] = re;
+}
+
+struct JTile {
   int64_t row0, rows, rs, re;
   bool staged;
 };
 
-// Sets up the tile: left row span and the right key span [rs, re) staged into LDS when it fits.
-__device__ __forceinline__ TileCtx join_tile_setup(const JoinParams& p, const int64_t* rstart,
-                                                   const int64_t* rlen, const int32_t* rbucket,
-                                                   const int64_t* roff, int R,
-                                                   const int64_t* tile_prefix, int64_t t,
-                                                   uint64_t* skeys, int64_t* sh) {
-  const int r = (int)find_range_j(tile_prefix, R, t);
-  const int64_t off = (t - tile_prefix[r]) * JN_TILE;
-  TileCtx ctx;
-  ctx.row0 = rstart[r] + off;
-  ctx.rows = min((int64_t)JN_TILE, rlen[r] - off);
-  const bool fl = p.key_is_float != 0;
-  if (threadIdx.x == 0) {
-    const int b = rbucket[r];
-    const int64_t bs = roff[b], be = roff[b + 1];
-    // first / last valid left key of the tile (left is sorted, nulls first)
-    const ColDesc& lk = p.cols[p.lkey];
-    int64_t f = ctx.row0, l = ctx.row0 + ctx.rows - 1;
-    while (f <= l && !col_valid(lk, f)) ++f;
-    int64_t rs = bs, re = bs;
-    if (f <= l && col_valid(lk, l)) {
-      const uint64_t kmin = join_key(lk, f, fl), kmax = join_key(lk, l, fl);
-      rs = rkey_bound(p.cols[p.rkey], bs, be, kmin, false, fl);
-      re = rkey_bound(p.cols[p.rkey], rs, be, kmax, true, fl);
-    }
-    sh[0] = rs;
-    sh[1] = re;
+__device__ __forceinline__ JTile jtile_load(const JoinParams& p, const int64_t* spans, int64_t t,
+                                            uint64_t* skeys) {
+  JTile c;
+  c.row0 = spans[4 * t + 0];
+  c.rows = spans[4 * t + 1];
+  c.rs = spans[4 * t + 2];
+  c.re = spans[4 * t + 3];
+  c.staged = (c.re - c.rs) <= JN_LDS_KEYS;
+  if (c.staged) {
+    const bool fl = p.key_is_float != 0;
+    for (int64_t j = threadIdx.x; j < c.re - c.rs; j += JN_BLOCK)
+      skeys[j] = join_key(p.cols[p.rkey], c.rs + j, fl);  // right keys in span are non-null
   }
   __syncthreads();
-  ctx.rs = sh[0];
-  ctx.re = sh[1];
-  ctx.staged = (ctx.re - ctx.rs) <= JN_LDS_KEYS;
-  if (ctx.staged) {
-    for (int64_t j = threadIdx.x; j < ctx.re - ctx.rs; j += JN_BLOCK)
-      skeys[j] = join_key(p.cols[p.rkey], ctx.rs + j, fl);  // right keys in span are non-null
-  }
-  __syncthreads();
-  return ctx;
+  return c;
 }
 
-__device__ __forceinline__ int64_t span_lower(const TileCtx& ctx, const uint64_t* skeys,
+__device__ __forceinline__ int64_t span_lower(const JTile& c, const uint64_t* skeys,
                                               const JoinParams& p, uint64_t k) {
-  if (ctx.staged) {
-    int64_t lo = 0, hi = ctx.re - ctx.rs;
+  if (c.staged) {
+    int64_t lo = 0, hi = c.re - c.rs;
     while (lo < hi) {
       const int64_t mid = (lo + hi) >> 1;
       if (skeys[mid] < k) lo = mid + 1; else hi = mid;
     }
-    return ctx.rs + lo;
+    return c.rs + lo;
   }
-  return rkey_bound(p.cols[p.rkey], ctx.rs, ctx.re, k, false, p.key_is_float != 0);
+  return rkey_bound(p.cols[p.rkey], c.rs, c.re, k, false, p.key_is_float != 0);
 }
 
-__device__ __forceinline__ uint64_t span_key(const TileCtx& ctx, const uint64_t* skeys,
+__device__ __forceinline__ uint64_t span_key(const JTile& c, const uint64_t* skeys,
                                              const JoinParams& p, int64_t j) {
-  return ctx.staged ? skeys[j - ctx.rs] : join_key(p.cols[p.rkey], j, p.key_is_float != 0);
+  return c.staged ? skeys[j - c.rs] : join_key(p.cols[p.rkey], j, p.key_is_float != 0);
+}
+
+// Left batch of a tile: rows, left predicates, key lookup.  m[i]: row i has a first match at j[i].
+__device__ __forceinline__ void jbatch_probe(const JoinParams& p, const JTile& c,
+                                             const uint64_t* skeys, int64_t (&r0)[JN_ITEMS],
+                                             uint64_t (&key)[JN_ITEMS], int64_t (&j)[JN_ITEMS],
+                                             bool (&m)[JN_ITEMS]) {
+  bool act[JN_ITEMS];
+#pragma unroll
+  for (int i = 0; i < JN_ITEMS; ++i) {
+    const int64_t k = (int64_t)i * JN_BLOCK + threadIdx.x;
+    act[i] = k < c.rows;
+    r0[i] = act[i] ? c.row0 + k : c.row0;
+  }
+  const ColDesc& lk = p.cols[p.lkey];
+  bool lv[JN_ITEMS];
+  vvalid(lk, r0, act, lv);
+  veval_cnf(p.preds, 0, p.nlp, p.cols, JN_SPLIT, r0, r0, lv, m);
+  const bool fl = p.key_is_float != 0;
+  if (fl) {
+    double x[JN_ITEMS];
+    vload_f64(lk, r0, m, x);
+#pragma unroll
+    for (int i = 0; i < JN_ITEMS; ++i) {
+      double d = x[i] == 0.0 ? 0.0 : x[i];
+      const uint64_t b = (uint64_t)__double_as_longlong(d);
+      key[i] = (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
+    }
+  } else {
+    int64_t x[JN_ITEMS];
+    vload_i64(lk, r0, m, x);
+#pragma unroll
+    for (int i = 0; i < JN_ITEMS; ++i) key[i] = (uint64_t)x[i] ^ 0x8000000000000000ull;
+  }
+#pragma unroll
+  for (int i = 0; i < JN_ITEMS; ++i) {
+    j[i] = c.rs;
+    if (m[i]) {
+      j[i] = span_lower(c, skeys, p, key[i]);
+      m[i] = j[i] < c.re && span_key(c, skeys, p, j[i]) == key[i];
+    }
+  }
+}
+
+__device__ __forceinline__ bool any_of(const bool (&m)[JN_ITEMS]) {
+  bool a = false;
+#pragma unroll
+  for (int i = 0; i < JN_ITEMS; ++i) a = a || m[i];
+  return a;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -133,156 +193,163 @@ __device__ __forceinline__ uint64_t span_key(const TileCtx& ctx, const uint64_t*
 // ------------------------------------------------------------------------------------------------
 template <bool GROUPED>
 __global__ __launch_bounds__(JN_BLOCK) void hs_join_agg_kernel(
-    JoinParams p, const int64_t* __restrict__ rstart, const int64_t* __restrict__ rlen,
-    const int32_t* __restrict__ rbucket, const int64_t* __restrict__ roff, int R,
-    const int64_t* __restrict__ tile_prefix, double* __restrict__ psum, int64_t* __restrict__ pcnt,
+    JoinParams p, const int64_t* __restrict__ tile_prefix, int R,
+    const int64_t* __restrict__ spans, double* __restrict__ psum, int64_t* __restrict__ pcnt,
     double* __restrict__ pmin, double* __restrict__ pmax) {
   __shared__ uint64_t skeys[JN_LDS_KEYS];
-  __shared__ int64_t sh[2];
   extern __shared__ __attribute__((aligned(16))) double glds[];
   const int A = p.naggs;
   const int GA = GROUPED ? p.num_groups * A : A;
   GroupLds gl = group_lds(glds, GROUPED ? GA : 0);
-  if (GROUPED) group_lds_init(gl, GA, JN_BLOCK);  // visible after the tile setup barrier
+  if (GROUPED) group_lds_init(gl, GA, JN_BLOCK);  // visible after the first tile barrier
   AggAcc acc;
-  acc_init(acc);
-  const bool fl = p.key_is_float != 0;
-  const ColDesc& lk = p.cols[p.lkey];
-  const int64_t ntiles = tile_prefix[R];
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    TileCtx ctx = join_tile_setup(p, rstart, rlen, rbucket, roff, R, tile_prefix, t, skeys, sh);
-    for (int it = 0; it < JN_ITEMS; ++it) {
-      const int64_t k = (int64_t)it * JN_BLOCK + threadIdx.x;
-      const int64_t lrow = ctx.row0 + k;
-      RowRef rr{lrow, 0};
-      bool lok = k < ctx.rows && col_valid(lk, lrow) &&
-                 hs_eval_cnf(p.preds, 0, p.nlp, p.cols, JN_SPLIT, rr);
-      uint64_t key = 0;
-      int64_t j = 0;
-      if (lok) {
-        key = join_key(lk, lrow, fl);
-        j = span_lower(ctx, skeys, p, key);
-        lok = j < ctx.re && span_key(ctx, skeys, p, j) == key;
-      }
-      // one match per lane per round; rounds are wave-uniform so acc_row sees a converged wave
-      while (__any(lok)) {
-        bool pass = false;
-        int gidx = 0;
-        if (lok) {
-          rr.r1 = j;
-          pass = hs_eval_cnf(p.preds, p.nlp, p.npreds, p.cols, JN_SPLIT, rr);
-          if (GROUPED && pass) {
-            const ColDesc& gc = p.cols[p.group_col];
-            const int64_t grow = p.group_col >= JN_SPLIT ? j : lrow;
-            if (!col_valid(gc, grow)) {
-              pass = false;
-            } else {
-              gidx = (int)(load_i64(gc, grow) - p.group_base);
-              if (gidx < 0 || gidx >= p.num_groups) pass = false;
-            }
-          }
-        }
-        acc_row<GROUPED>(acc, p.aggs, A, pass, gidx, p.cols, JN_SPLIT, rr, gl);
-        if (lok) {
-          ++j;
-          lok = j < ctx.re && span_key(ctx, skeys, p, j) == key;
+  acc_init(acc, p.aggs, A);
+  int64_t t0, t1;
+  block_tile_chunk(tile_prefix[R], t0, t1);
+  if (GROUPED) __syncthreads();
+  for (int64_t t = t0; t < t1; ++t) {
+    const JTile c = jtile_load(p, spans, t, skeys);
+    int64_t r0[JN_ITEMS], j[JN_ITEMS];
+    uint64_t key[JN_ITEMS];
+    bool m[JN_ITEMS];
+    jbatch_probe(p, c, skeys, r0, key, j, m);
+    // match rounds: every row advances one right match per round (wave-uniform trip count)
+    while (__any(any_of(m))) {
+      bool pass[JN_ITEMS];
+      veval_cnf(p.preds, p.nlp, p.npreds, p.cols, JN_SPLIT, r0, j, m, pass);
+      int g[JN_ITEMS];
+#pragma unroll
+      for (int i = 0; i < JN_ITEMS; ++i) g[i] = 0;
+      if (GROUPED)
+        vgroup(p.cols, p.group_col, JN_SPLIT, p.group_base, p.num_groups, r0, j, pass, g);
+      vaccumulate<GROUPED, JN_ITEMS>(acc, p.aggs, A, p.cols, JN_SPLIT, r0, j, pass, g, gl);
+#pragma unroll
+      for (int i = 0; i < JN_ITEMS; ++i) {
+        if (m[i]) {
+          ++j[i];
+          m[i] = j[i] < c.re && span_key(c, skeys, p, j[i]) == key[i];
         }
       }
     }
     __syncthreads();  // skeys reuse
   }
-  acc_flush<GROUPED, JN_BLOCK>(acc, A, GA, gl, psum, pcnt, pmin, pmax);
+  acc_flush<GROUPED, JN_BLOCK>(acc, p.aggs, A, GA, gl, psum, pcnt, pmin, pmax);
 }
 
 // ------------------------------------------------------------------------------------------------
-// Pair count / emit (general inner join)
+// Pair count / emit (general inner join).  Output order: tile, then left row, then right row.
 // ------------------------------------------------------------------------------------------------
 template <bool EMIT>
 __global__ __launch_bounds__(JN_BLOCK) void hs_join_pairs_kernel(
-    JoinParams p, const int64_t* __restrict__ rstart, const int64_t* __restrict__ rlen,
-    const int32_t* __restrict__ rbucket, const int64_t* __restrict__ roff, int R,
-    const int64_t* __restrict__ tile_prefix, int64_t* __restrict__ tile_counts,
+    JoinParams p, const int64_t* __restrict__ tile_prefix, int R,
+    const int64_t* __restrict__ spans, int64_t* __restrict__ tile_counts,
     const int64_t* __restrict__ tile_offsets, int64_t* __restrict__ out_l,
     int64_t* __restrict__ out_r) {
   __shared__ uint64_t skeys[JN_LDS_KEYS];
-  __shared__ int64_t sh[2];
-  __shared__ int64_t wtot[JN_BLOCK / 64];
-  __shared__ int64_t run;
-  const bool fl = p.key_is_float != 0;
+  __shared__ int64_t wtot[JN_ITEMS][JN_BLOCK / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t ntiles = tile_prefix[R];
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    TileCtx ctx = join_tile_setup(p, rstart, rlen, rbucket, roff, R, tile_prefix, t, skeys, sh);
-    if (EMIT && threadIdx.x == 0) run = tile_offsets[t];
-    int64_t total = 0;
-    for (int it = 0; it < JN_ITEMS; ++it) {
-      const int64_t k = (int64_t)it * JN_BLOCK + threadIdx.x;
-      int64_t cnt = 0, first = 0;
-      uint64_t key = 0;
-      int64_t lrow = 0;
-      bool ok = false;
-      if (k < ctx.rows) {
-        lrow = ctx.row0 + k;
-        const ColDesc& lk = p.cols[p.lkey];
-        RowRef rr{lrow, 0};
-        if (col_valid(lk, lrow) && hs_eval_cnf(p.preds, 0, p.nlp, p.cols, JN_SPLIT, rr)) {
-          ok = true;
-          key = join_key(lk, lrow, fl);
-          first = span_lower(ctx, skeys, p, key);
-          for (int64_t j = first; j < ctx.re && span_key(ctx, skeys, p, j) == key; ++j) {
-            rr.r1 = j;
-            if (hs_eval_cnf(p.preds, p.nlp, p.npreds, p.cols, JN_SPLIT, rr)) ++cnt;
-          }
+  int64_t t0, t1;
+  block_tile_chunk(tile_prefix[R], t0, t1);
+  for (int64_t t = t0; t < t1; ++t) {
+    const JTile c = jtile_load(p, spans, t, skeys);
+    int64_t r0[JN_ITEMS], j0[JN_ITEMS];
+    uint64_t key[JN_ITEMS];
+    bool m0[JN_ITEMS];
+    jbatch_probe(p, c, skeys, r0, key, j0, m0);
+    // count matches per row (right predicates evaluated per match round)
+    int64_t cnt[JN_ITEMS], j[JN_ITEMS];
+    bool m[JN_ITEMS];
+#pragma unroll
+    for (int i = 0; i < JN_ITEMS; ++i) {
+      cnt[i] = 0;
+      j[i] = j0[i];
+      m[i] = m0[i];
+    }
+    while (__any(any_of(m))) {
+      bool pass[JN_ITEMS];
+      veval_cnf(p.preds, p.nlp, p.npreds, p.cols, JN_SPLIT, r0, j, m, pass);
+#pragma unroll
+      for (int i = 0; i < JN_ITEMS; ++i) {
+        cnt[i] += pass[i] ? 1 : 0;
+        if (m[i]) {
+          ++j[i];
+          m[i] = j[i] < c.re && span_key(c, skeys, p, j[i]) == key[i];
         }
       }
-      if (!EMIT) {
-        total += cnt;
-        continue;
-      }
-      // stable exclusive prefix of cnt across the block (wave scan + wave totals)
-      int64_t x = cnt;
-      for (int off = 1; off < 64; off <<= 1) {
-        int64_t y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-      }
-      if (lane == 63) wtot[w] = x;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        int64_t acc = run;
-        for (int ww = 0; ww < JN_BLOCK / 64; ++ww) {
-          const int64_t v = wtot[ww];
-          wtot[ww] = acc;
-          acc += v;
-        }
-        run = acc;
-      }
-      __syncthreads();
-      int64_t pos = wtot[w] + x - cnt;
-      if (ok && cnt) {
-        RowRef rr{lrow, 0};
-        for (int64_t j = first; j < ctx.re && span_key(ctx, skeys, p, j) == key; ++j) {
-          rr.r1 = j;
-          if (hs_eval_cnf(p.preds, p.nlp, p.npreds, p.cols, JN_SPLIT, rr)) {
-            out_l[pos] = lrow;
-            out_r[pos] = j;
-            ++pos;
-          }
-        }
-      }
-      __syncthreads();
     }
     if (!EMIT) {
-      total = hs_wave_sum(total);
-      if (lane == 0) wtot[w] = total;
+      int64_t tot = 0;
+#pragma unroll
+      for (int i = 0; i < JN_ITEMS; ++i) tot += cnt[i];
+      tot = hs_wave_sum(tot);
+      if (lane == 0) wtot[0][w] = tot;
       __syncthreads();
       if (threadIdx.x == 0) {
         int64_t tt = 0;
-        for (int ww = 0; ww < JN_BLOCK / 64; ++ww) tt += wtot[ww];
+        for (int ww = 0; ww < JN_BLOCK / 64; ++ww) tt += wtot[0][ww];
         tile_counts[t] = tt;
+      }
+      __syncthreads();
+      continue;
+    }
+    // exclusive position of each row's run: order (item, wave, lane) == left row order
+    int64_t x[JN_ITEMS];
+#pragma unroll
+    for (int i = 0; i < JN_ITEMS; ++i) {
+      int64_t v = cnt[i];
+      for (int off = 1; off < 64; off <<= 1) {
+        const int64_t y = __shfl_up(v, off, 64);
+        if (lane >= off) v += y;
+      }
+      x[i] = v - cnt[i];
+      if (lane == 63) wtot[i][w] = v;
+    }
+    __syncthreads();
+    int64_t base = tile_offsets[t];
+#pragma unroll
+    for (int i = 0; i < JN_ITEMS; ++i) {
+      int64_t mine = base;
+      for (int ww = 0; ww < JN_BLOCK / 64; ++ww) {
+        if (ww < w) mine += wtot[i][ww];
+        base += wtot[i][ww];
+      }
+      x[i] += mine;
+    }
+    // emit rounds
+#pragma unroll
+    for (int i = 0; i < JN_ITEMS; ++i) {
+      j[i] = j0[i];
+      m[i] = m0[i];
+    }
+    while (__any(any_of(m))) {
+      bool pass[JN_ITEMS];
+      veval_cnf(p.preds, p.nlp, p.npreds, p.cols, JN_SPLIT, r0, j, m, pass);
+#pragma unroll
+      for (int i = 0; i < JN_ITEMS; ++i) {
+        if (pass[i]) {
+          out_l[x[i]] = r0[i];
+          out_r[x[i]] = j[i];
+          ++x[i];
+        }
+        if (m[i]) {
+          ++j[i];
+          m[i] = j[i] < c.re && span_key(c, skeys, p, j[i]) == key[i];
+        }
       }
     }
     __syncthreads();
   }
+}
+
+static int launch_spans(const JoinParams* p, const int64_t* rstart, const int64_t* rlen,
+                        const int32_t* rbucket, const int64_t* roff, int R,
+                        const int64_t* tile_prefix, int64_t max_tiles, int64_t* spans,
+                        hipStream_t s) {
+  if (max_tiles <= 0) return 0;
+  const int64_t blocks = (max_tiles + 255) / 256;
+  hipLaunchKernelGGL(hs_join_spans_kernel, dim3((unsigned)blocks), dim3(256), 0, s, *p, rstart,
+                     rlen, rbucket, roff, R, tile_prefix, spans);
+  return (int)hipGetLastError();
 }
 
 extern "C" {
@@ -294,21 +361,25 @@ int hs_agg_final(const double* psum, const int64_t* pcnt, const double* pmin, co
                  int nblk, int GA, double* osum, int64_t* ocnt, double* omin, double* omax,
                  void* stream);
 
+// spans: scratch of 4 * max_tiles int64 (max_tiles >= tile_prefix[R]).
 int hs_join_agg(const JoinParams* p, const int64_t* rstart, const int64_t* rlen,
                 const int32_t* rbucket, const int64_t* roff, int R, const int64_t* tile_prefix,
-                int grid, double* psum, int64_t* pcnt, double* pmin, double* pmax, double* osum,
-                int64_t* ocnt, double* omin, double* omax, void* stream) {
+                int64_t max_tiles, int64_t* spans, int grid, double* psum, int64_t* pcnt,
+                double* pmin, double* pmax, double* osum, int64_t* ocnt, double* omin,
+                double* omax, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  HS_CHECK((hipError_t)launch_spans(p, rstart, rlen, rbucket, roff, R, tile_prefix, max_tiles,
+                                    spans, s));
   const bool grouped = p->group_col >= 0;
   if (grouped) {
     const int GA = p->num_groups * p->naggs;
     const size_t lds = (size_t)GA * 32;
     if (lds > 96 * 1024) return -5;
-    hipLaunchKernelGGL(hs_join_agg_kernel<true>, dim3(grid), dim3(JN_BLOCK), lds, s, *p, rstart,
-                       rlen, rbucket, roff, R, tile_prefix, psum, pcnt, pmin, pmax);
+    hipLaunchKernelGGL(hs_join_agg_kernel<true>, dim3(grid), dim3(JN_BLOCK), lds, s, *p,
+                       tile_prefix, R, spans, psum, pcnt, pmin, pmax);
   } else {
-    hipLaunchKernelGGL(hs_join_agg_kernel<false>, dim3(grid), dim3(JN_BLOCK), 0, s, *p, rstart,
-                       rlen, rbucket, roff, R, tile_prefix, psum, pcnt, pmin, pmax);
+    hipLaunchKernelGGL(hs_join_agg_kernel<false>, dim3(grid), dim3(JN_BLOCK), 0, s, *p,
+                       tile_prefix, R, spans, psum, pcnt, pmin, pmax);
   }
   const int GA = grouped ? p->num_groups * p->naggs : p->naggs;
   return hs_agg_final(psum, pcnt, pmin, pmax, grid, GA, osum, ocnt, omin, omax, stream);
@@ -316,20 +387,24 @@ int hs_join_agg(const JoinParams* p, const int64_t* rstart, const int64_t* rlen,
 
 int hs_join_count(const JoinParams* p, const int64_t* rstart, const int64_t* rlen,
                   const int32_t* rbucket, const int64_t* roff, int R, const int64_t* tile_prefix,
-                  int grid, int64_t* tile_counts, void* stream) {
-  hipLaunchKernelGGL(hs_join_pairs_kernel<false>, dim3(grid), dim3(JN_BLOCK), 0,
-                     (hipStream_t)stream, *p, rstart, rlen, rbucket, roff, R, tile_prefix,
-                     tile_counts, (const int64_t*)nullptr, (int64_t*)nullptr, (int64_t*)nullptr);
+                  int64_t max_tiles, int64_t* spans, int grid, int64_t* tile_counts,
+                  void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  HS_CHECK((hipError_t)launch_spans(p, rstart, rlen, rbucket, roff, R, tile_prefix, max_tiles,
+                                    spans, s));
+  hipLaunchKernelGGL(hs_join_pairs_kernel<false>, dim3(grid), dim3(JN_BLOCK), 0, s, *p,
+                     tile_prefix, R, (const int64_t*)spans, tile_counts, (const int64_t*)nullptr,
+                     (int64_t*)nullptr, (int64_t*)nullptr);
   return (int)hipGetLastError();
 }
 
-int hs_join_emit(const JoinParams* p, const int64_t* rstart, const int64_t* rlen,
-                 const int32_t* rbucket, const int64_t* roff, int R, const int64_t* tile_prefix,
+// Reuses the spans computed by hs_join_count.
+int hs_join_emit(const JoinParams* p, int R, const int64_t* tile_prefix, const int64_t* spans,
                  int grid, const int64_t* tile_offsets, int64_t* out_l, int64_t* out_r,
                  void* stream) {
   hipLaunchKernelGGL(hs_join_pairs_kernel<true>, dim3(grid), dim3(JN_BLOCK), 0,
-                     (hipStream_t)stream, *p, rstart, rlen, rbucket, roff, R, tile_prefix,
-                     (int64_t*)nullptr, tile_offsets, out_l, out_r);
+                     (hipStream_t)stream, *p, tile_prefix, R, spans, (int64_t*)nullptr,
+                     tile_offsets, out_l, out_r);
   return (int)hipGetLastError();
 }
 

@@ -4,10 +4,14 @@
 // indexed column inside each bucket, so a range predicate on that column becomes one binary search
 // per bucket (hs_range_search) — row-level zone pruning that is strictly finer than Parquet
 // row-group stats.  An equality predicate on all bucket columns additionally prunes to a single
-// bucket (the literal is Murmur3-hashed on the host).  Ranges are cut into 2048-row tiles; a
-// fixed grid walks the tile list (its length lives in device memory, so no host round trip and
-// the launch sequence is hipGraph-capturable).
-#include "hs_scan.h"
+// bucket (the literal is Murmur3-hashed on the host).  Ranges are cut into 2048-row tiles; each
+// block of a fixed grid takes a contiguous chunk of the tile list (its length lives in device
+// memory, so no host round trip and the launch sequence is hipGraph-capturable).
+//
+// Inside a tile every lane owns SF_ITEMS rows (stride SF_BLOCK, so each wave load is one
+// coalesced 64-row segment) and evaluates them predicate-major (hs_vec.h): SF_ITEMS independent
+// loads in flight per lane per column.
+#include "hs_vec.h"
 
 #define SF_BLOCK 256
 #define SF_ITEMS 8
@@ -110,13 +114,30 @@ __global__ __launch_bounds__(1024) void hs_ranges_to_tiles_kernel(const int64_t*
   if (threadIdx.x == 0) tile_prefix[R] = carry;
 }
 
-__device__ __forceinline__ int find_range(const int64_t* tile_prefix, int R, int64_t t) {
-  int lo = 0, hi = R;  // largest r with tile_prefix[r] <= t
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (tile_prefix[mid] <= t) lo = mid; else hi = mid;
+// Walks a block's contiguous tile chunk, yielding (row0, rows) per tile.
+struct TileWalker {
+  const int64_t* tile_prefix;
+  const int64_t* rstart;
+  const int64_t* rlen;
+  int R;
+  int r;
+  __device__ __forceinline__ void init(int64_t t0) { r = tile_range_of(tile_prefix, R, t0); }
+  __device__ __forceinline__ void at(int64_t t, int64_t& row0, int64_t& rows) {
+    while (r + 1 < R && tile_prefix[r + 1] <= t) ++r;
+    const int64_t off = (t - tile_prefix[r]) * SF_TILE;
+    row0 = rstart[r] + off;
+    rows = min((int64_t)SF_TILE, rlen[r] - off);
   }
-  return lo;
+};
+
+__device__ __forceinline__ void tile_rows(int64_t row0, int64_t rows, int64_t (&r)[SF_ITEMS],
+                                          bool (&act)[SF_ITEMS]) {
+#pragma unroll
+  for (int i = 0; i < SF_ITEMS; ++i) {
+    const int64_t k = (int64_t)i * SF_BLOCK + threadIdx.x;
+    act[i] = k < rows;
+    r[i] = act[i] ? row0 + k : row0;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -136,33 +157,28 @@ __global__ __launch_bounds__(SF_BLOCK) void hs_scan_agg_kernel(
     __syncthreads();
   }
   AggAcc acc;
-  acc_init(acc);
-  const int64_t ntiles = tile_prefix[R];
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int r = find_range(tile_prefix, R, t);
-    const int64_t off = (t - tile_prefix[r]) * SF_TILE;
-    const int64_t row0 = rstart[r] + off;
-    const int64_t rows = min((int64_t)SF_TILE, rlen[r] - off);
-#pragma unroll 2
-    for (int it = 0; it < SF_ITEMS; ++it) {
-      const int64_t k = (int64_t)it * SF_BLOCK + threadIdx.x;
-      const int64_t row = row0 + k;
-      RowRef rr{row, row};
-      bool pass = k < rows && hs_eval_cnf(p.preds, 0, p.npreds, p.cols, HS_MAX_COLS, rr);
-      int gidx = 0;
-      if (GROUPED && pass) {
-        const ColDesc& gc = p.cols[p.group_col];
-        if (!col_valid(gc, row)) {
-          pass = false;
-        } else {
-          gidx = (int)(load_i64(gc, row) - p.group_base);
-          if (gidx < 0 || gidx >= p.num_groups) pass = false;
-        }
-      }
-      acc_row<GROUPED>(acc, p.aggs, A, pass, gidx, p.cols, HS_MAX_COLS, rr, gl);
+  acc_init(acc, p.aggs, A);
+  int64_t t0, t1;
+  block_tile_chunk(tile_prefix[R], t0, t1);
+  if (t0 < t1) {
+    TileWalker tw{tile_prefix, rstart, rlen, R, 0};
+    tw.init(t0);
+    for (int64_t t = t0; t < t1; ++t) {
+      int64_t row0, rows;
+      tw.at(t, row0, rows);
+      int64_t r[SF_ITEMS];
+      bool act[SF_ITEMS], pass[SF_ITEMS];
+      tile_rows(row0, rows, r, act);
+      veval_cnf(p.preds, 0, p.npreds, p.cols, HS_MAX_COLS, r, r, act, pass);
+      int g[SF_ITEMS];
+#pragma unroll
+      for (int i = 0; i < SF_ITEMS; ++i) g[i] = 0;
+      if (GROUPED)
+        vgroup(p.cols, p.group_col, HS_MAX_COLS, p.group_base, p.num_groups, r, r, pass, g);
+      vaccumulate<GROUPED, SF_ITEMS>(acc, p.aggs, A, p.cols, HS_MAX_COLS, r, r, pass, g, gl);
     }
   }
-  acc_flush<GROUPED, SF_BLOCK>(acc, A, GA, gl, psum, pcnt, pmin, pmax);
+  acc_flush<GROUPED, SF_BLOCK>(acc, p.aggs, A, GA, gl, psum, pcnt, pmin, pmax);
 }
 
 // Deterministic final reduction: one workgroup per output slot, fixed-order tree.
@@ -212,26 +228,27 @@ __global__ __launch_bounds__(FIN_BLOCK) void hs_agg_final_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
-// Filter -> stable compaction of row ids.
+// Filter -> stable compaction of row ids (count pass, then emit pass at the scanned offsets).
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(SF_BLOCK) void hs_scan_count_kernel(
     ScanParams p, const int64_t* __restrict__ rstart, const int64_t* __restrict__ rlen, int R,
     const int64_t* __restrict__ tile_prefix, int64_t* __restrict__ tile_counts) {
   __shared__ int64_t red[SF_BLOCK / 64];
-  const int64_t ntiles = tile_prefix[R];
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int r = find_range(tile_prefix, R, t);
-    const int64_t off = (t - tile_prefix[r]) * SF_TILE;
-    const int64_t row0 = rstart[r] + off;
-    const int64_t rows = min((int64_t)SF_TILE, rlen[r] - off);
+  int64_t t0, t1;
+  block_tile_chunk(tile_prefix[R], t0, t1);
+  if (t0 >= t1) return;
+  TileWalker tw{tile_prefix, rstart, rlen, R, 0};
+  tw.init(t0);
+  for (int64_t t = t0; t < t1; ++t) {
+    int64_t row0, rows;
+    tw.at(t, row0, rows);
+    int64_t r[SF_ITEMS];
+    bool act[SF_ITEMS], pass[SF_ITEMS];
+    tile_rows(row0, rows, r, act);
+    veval_cnf(p.preds, 0, p.npreds, p.cols, HS_MAX_COLS, r, r, act, pass);
     int64_t cnt = 0;
-    for (int it = 0; it < SF_ITEMS; ++it) {
-      const int64_t k = (int64_t)it * SF_BLOCK + threadIdx.x;
-      if (k < rows) {
-        RowRef rr{row0 + k, row0 + k};
-        cnt += hs_eval_cnf(p.preds, 0, p.npreds, p.cols, HS_MAX_COLS, rr) ? 1 : 0;
-      }
-    }
+#pragma unroll
+    for (int i = 0; i < SF_ITEMS; ++i) cnt += pass[i] ? 1 : 0;
     cnt = hs_wave_sum(cnt);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
     __syncthreads();
@@ -248,41 +265,40 @@ __global__ __launch_bounds__(SF_BLOCK) void hs_scan_select_kernel(
     ScanParams p, const int64_t* __restrict__ rstart, const int64_t* __restrict__ rlen, int R,
     const int64_t* __restrict__ tile_prefix, const int64_t* __restrict__ tile_offsets,
     int64_t* __restrict__ out_rows) {
-  __shared__ int64_t wbase[SF_BLOCK / 64];
-  __shared__ int64_t run;
+  __shared__ int64_t wcnt[SF_ITEMS][SF_BLOCK / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = hs_lanemask_lt();
-  const int64_t ntiles = tile_prefix[R];
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int r = find_range(tile_prefix, R, t);
-    const int64_t off = (t - tile_prefix[r]) * SF_TILE;
-    const int64_t row0 = rstart[r] + off;
-    const int64_t rows = min((int64_t)SF_TILE, rlen[r] - off);
-    if (threadIdx.x == 0) run = tile_offsets[t];
-    __syncthreads();
-    for (int it = 0; it < SF_ITEMS; ++it) {
-      const int64_t k = (int64_t)it * SF_BLOCK + threadIdx.x;
-      bool pass = false;
-      if (k < rows) {
-        RowRef rr{row0 + k, row0 + k};
-        pass = hs_eval_cnf(p.preds, 0, p.npreds, p.cols, HS_MAX_COLS, rr);
-      }
-      const uint64_t m = __ballot(pass);
-      if (lane == 0) wbase[w] = (int64_t)__popcll(m);
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        int64_t acc = run;
-        for (int ww = 0; ww < SF_BLOCK / 64; ++ww) {
-          const int64_t c = wbase[ww];
-          wbase[ww] = acc;
-          acc += c;
-        }
-        run = acc;
-      }
-      __syncthreads();
-      if (pass) out_rows[wbase[w] + __popcll(m & lt)] = row0 + k;
-      __syncthreads();
+  int64_t t0, t1;
+  block_tile_chunk(tile_prefix[R], t0, t1);
+  if (t0 >= t1) return;
+  TileWalker tw{tile_prefix, rstart, rlen, R, 0};
+  tw.init(t0);
+  for (int64_t t = t0; t < t1; ++t) {
+    int64_t row0, rows;
+    tw.at(t, row0, rows);
+    int64_t r[SF_ITEMS];
+    bool act[SF_ITEMS], pass[SF_ITEMS];
+    tile_rows(row0, rows, r, act);
+    veval_cnf(p.preds, 0, p.npreds, p.cols, HS_MAX_COLS, r, r, act, pass);
+    uint64_t m[SF_ITEMS];
+#pragma unroll
+    for (int i = 0; i < SF_ITEMS; ++i) {
+      m[i] = __ballot(pass[i]);
+      if (lane == 0) wcnt[i][w] = (int64_t)__popcll(m[i]);
     }
+    __syncthreads();
+    // output order = row order = (item, wave, lane)
+    int64_t base = tile_offsets[t];
+#pragma unroll
+    for (int i = 0; i < SF_ITEMS; ++i) {
+      int64_t mine = base;
+      for (int ww = 0; ww < SF_BLOCK / 64; ++ww) {
+        if (ww < w) mine += wcnt[i][ww];
+        base += wcnt[i][ww];
+      }
+      if (pass[i]) out_rows[mine + __popcll(m[i] & lt)] = r[i];
+    }
+    __syncthreads();
   }
 }
 

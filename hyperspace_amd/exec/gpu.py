@@ -211,8 +211,12 @@ class GpuBackend:
         return v[1]
 
     # -- lowering helpers ----------------------------------------------------------------------
-    def _ranges(self, r: DRel, conds: list):
-        """Row ranges after bucket / sort-key pruning on the leading indexed column."""
+    def _ranges(self, r: DRel, conds: list, implied: Optional[set] = None):
+        """Row ranges after bucket / sort-key pruning on the leading indexed column.
+
+        When ``implied`` is given it receives ``id(c)`` of every conjunct the ranges already
+        guarantee (comparisons of the sort key with literals, and ``isnotnull(key)`` since range
+        search skips the null prefix), so kernels do not re-evaluate them per row."""
         t = r.table
         if not (r.bucketed and r.sort_attrs):
             return self._full_ranges(t)
@@ -221,6 +225,9 @@ class GpuBackend:
         lo = hi = None
         lo_incl = hi_incl = True
         eq_bucket = None
+        used = []
+        notnull = [c for c in conds if isinstance(c, E.IsNotNull) and
+                   isinstance(c.child, E.Attribute) and c.child.expr_id == lead.expr_id]
         for c in conds:
             if not isinstance(c, E.BinaryComparison) or isinstance(c, E.NotEqual):
                 continue
@@ -241,6 +248,7 @@ class GpuBackend:
                     continue
                 v = int(v)
             img = K.sortable_image(v, kc.hs_type)
+            used.append(c)
             if leaf.op in (NL.OP_GT, NL.OP_GE, NL.OP_EQ):
                 inc = leaf.op != NL.OP_GT
                 if lo is None or img > lo or (img == lo and not inc):
@@ -255,8 +263,10 @@ class GpuBackend:
         if eq_bucket is not None:
             import torch
             buckets = torch.tensor([eq_bucket], dtype=torch.int32, device=self.device)
-        if lo is None and hi is None and buckets is None:
+        if lo is None and hi is None and buckets is None and not notnull:
             return self._full_ranges(t)
+        if implied is not None:
+            implied.update(id(c) for c in used + notnull)
         return K.range_search(kc, t.bucket_offsets, buckets, lo, lo_incl, hi, hi_incl)
 
     def _full_ranges(self, t: DeviceTable):
@@ -305,9 +315,11 @@ class GpuBackend:
             t = r.table
             full = t.num_rows
             return {a.expr_id: r.col(a) for a in attrs} if full is not None else {}
-        rstart, rlen, _ = self._ranges(r, r.conds)
+        implied: set = set()
+        rstart, rlen, _ = self._ranges(r, r.conds, implied)
         col_info, descs = self._column_infos([(r, 0)])
-        bound = CP.bind(CP.to_cnf(r.conds), col_info, self.device)
+        bound = CP.bind(CP.to_cnf([c for c in r.conds if id(c) not in implied]), col_info,
+                        self.device)
         for a in attrs:
             col_info(a)
         p = NL.ScanParams()
@@ -400,11 +412,12 @@ class GpuBackend:
             raise Unsupported("mixed int/float join keys")
         return left, right, lk, rk
 
-    def _join_params(self, left: DRel, right: DRel, lk, rk, residual, extra_attrs=()):
+    def _join_params(self, left: DRel, right: DRel, lk, rk, residual, extra_attrs=(),
+                     lconds=None):
         col_info, descs = self._column_infos([(left, 0), (right, 8)])
         lslot = col_info(lk).slot
         rslot = col_info(rk).slot
-        lb = CP.bind(CP.to_cnf(left.conds), col_info, self.device, 0)
+        lb = CP.bind(CP.to_cnf(left.conds if lconds is None else lconds), col_info, self.device, 0)
         rconds = list(right.conds) + ([residual] if residual is not None else [])
         rb = CP.bind(CP.to_cnf(rconds), col_info, self.device, 1000)
         for a in extra_attrs:
@@ -424,14 +437,17 @@ class GpuBackend:
     def _join_rel(self, p: X.SortMergeJoinExec) -> DRel:
         left, right, lk, rk = self._join_inputs(p)
         out_attrs = list(p.output)
-        jp, col_info, descs, keep = self._join_params(left, right, lk, rk, p.condition)
+        implied: set = set()
+        rstart, rlen, rbk = self._ranges(left, left.conds, implied)
+        jp, col_info, descs, keep = self._join_params(
+            left, right, lk, rk, p.condition,
+            lconds=[c for c in left.conds if id(c) not in implied])
         for s, c in descs.items():
             jp.cols[s] = c.desc()
         if keep[0].always_false or keep[1].always_false:
             import torch
             ol = orr = torch.empty(0, dtype=torch.int64, device=self.device)
         else:
-            rstart, rlen, rbk = self._ranges(left, left.conds)
             tp = K.ranges_to_tiles(rlen)
             max_tiles = left.table.num_rows // NL.lib().hs_join_tile_rows() + rlen.numel() + 1
             ol, orr = K.join_pairs(jp, rstart, rlen, rbk, right.table.bucket_offsets, tp, max_tiles)
@@ -566,7 +582,10 @@ class GpuBackend:
 
     def _scan_agg(self, r: DRel, fns, group):
         col_info, descs = self._column_infos([(r, 0)])
-        bound = CP.bind(CP.to_cnf(r.conds), col_info, self.device)
+        implied: set = set()
+        rstart, rlen, _ = self._ranges(r, r.conds, implied)
+        bound = CP.bind(CP.to_cnf([c for c in r.conds if id(c) not in implied]), col_info,
+                        self.device)
         specs = self._agg_specs(fns, col_info)
         gs = self._group_spec(r, group, MAX_GROUPS_SCAN)
         p = NL.ScanParams()
@@ -587,7 +606,6 @@ class GpuBackend:
         if bound.always_false:
             out = self._empty_agg(len(specs), G)
         else:
-            rstart, rlen, _ = self._ranges(r, r.conds)
             tp = K.ranges_to_tiles(rlen)
             out = K.scan_agg(p, rstart, rlen, tp)
         return (*out, G, gbase, gdict, gtype)
@@ -600,7 +618,11 @@ class GpuBackend:
 
     def _join_agg(self, node: X.SortMergeJoinExec, fns, group):
         left, right, lk, rk = self._join_inputs(node)
-        jp, col_info, descs, keep = self._join_params(left, right, lk, rk, node.condition)
+        implied: set = set()
+        rstart, rlen, rbk = self._ranges(left, left.conds, implied)
+        jp, col_info, descs, keep = self._join_params(
+            left, right, lk, rk, node.condition,
+            lconds=[c for c in left.conds if id(c) not in implied])
         specs = self._agg_specs(fns, col_info)
         gs = None
         if group is not None:
@@ -621,9 +643,9 @@ class GpuBackend:
         jp.naggs = len(specs)
         if keep[0].always_false or keep[1].always_false:
             return (*self._empty_agg(len(specs), G), G, gbase, gdict, gtype)
-        rstart, rlen, rbk = self._ranges(left, left.conds)
         tp = K.ranges_to_tiles(rlen)
-        out = K.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, tp)
+        max_tiles = left.table.num_rows // NL.lib().hs_join_tile_rows() + rlen.numel() + 1
+        out = K.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, tp, max_tiles)
         return (*out, G, gbase, gdict, gtype)
 
 

@@ -271,7 +271,10 @@ def scan_select(params: NL.ScanParams, rstart, rlen, tile_prefix, max_tiles: int
 # ------------------------------------------------------------------------------------------------
 # Join
 # ------------------------------------------------------------------------------------------------
-def join_agg(params: NL.JoinParams, rstart, rlen, rbucket, roff, tile_prefix, grid: int = None):
+def join_agg(params: NL.JoinParams, rstart, rlen, rbucket, roff, tile_prefix, max_tiles: int,
+             grid: int = None):
+    """``max_tiles`` bounds ``tile_prefix[-1]`` (left rows / tile + #ranges); sizes the per-tile
+    span scratch."""
     torch = _torch()
     L = NL.lib()
     grid = grid or L.hs_scan_grid()
@@ -285,10 +288,12 @@ def join_agg(params: NL.JoinParams, rstart, rlen, rbucket, roff, tile_prefix, gr
     oc = torch.empty(GA, dtype=torch.int64, device=dev)
     omn = torch.empty(GA, dtype=torch.float64, device=dev)
     omx = torch.empty(GA, dtype=torch.float64, device=dev)
+    spans = torch.empty(4 * max(max_tiles, 1), dtype=torch.int64, device=dev)
     NL.check(L.hs_join_agg(C.byref(params), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
-                           NL.ptr(roff), rstart.numel(), NL.ptr(tile_prefix), grid, NL.ptr(ps),
-                           NL.ptr(pc_), NL.ptr(pmn), NL.ptr(pmx), NL.ptr(os_), NL.ptr(oc),
-                           NL.ptr(omn), NL.ptr(omx), NL.stream_ptr()), "hs_join_agg")
+                           NL.ptr(roff), rstart.numel(), NL.ptr(tile_prefix), int(max_tiles),
+                           NL.ptr(spans), grid, NL.ptr(ps), NL.ptr(pc_), NL.ptr(pmn), NL.ptr(pmx),
+                           NL.ptr(os_), NL.ptr(oc), NL.ptr(omn), NL.ptr(omx), NL.stream_ptr()),
+             "hs_join_agg")
     return os_, oc, omn, omx
 
 
@@ -298,14 +303,15 @@ def join_pairs(params: NL.JoinParams, rstart, rlen, rbucket, roff, tile_prefix, 
     grid = L.hs_scan_grid()
     dev = rstart.device
     counts = torch.zeros(max_tiles + 1, dtype=torch.int64, device=dev)
+    spans = torch.empty(4 * max(max_tiles, 1), dtype=torch.int64, device=dev)
     NL.check(L.hs_join_count(C.byref(params), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
-                             NL.ptr(roff), rstart.numel(), NL.ptr(tile_prefix), grid, NL.ptr(counts),
-                             NL.stream_ptr()), "hs_join_count")
+                             NL.ptr(roff), rstart.numel(), NL.ptr(tile_prefix), int(max_tiles),
+                             NL.ptr(spans), grid, NL.ptr(counts), NL.stream_ptr()), "hs_join_count")
     offs = exclusive_scan_i64(counts)
     total = int(offs[-1].item())
     ol = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
     orr = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
-    NL.check(L.hs_join_emit(C.byref(params), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
-                            NL.ptr(roff), rstart.numel(), NL.ptr(tile_prefix), grid, NL.ptr(offs),
-                            NL.ptr(ol), NL.ptr(orr), NL.stream_ptr()), "hs_join_emit")
+    NL.check(L.hs_join_emit(C.byref(params), rstart.numel(), NL.ptr(tile_prefix), NL.ptr(spans),
+                            grid, NL.ptr(offs), NL.ptr(ol), NL.ptr(orr), NL.stream_ptr()),
+             "hs_join_emit")
     return ol[:total], orr[:total]

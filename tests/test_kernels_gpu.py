@@ -171,7 +171,8 @@ def test_join_agg_and_pairs(device):
     p.naggs, p.group_col, p.key_is_float = 1, -1, 0
     rstart, rlen, rbk = K.full_ranges(loff, device)
     tp = K.ranges_to_tiles(rlen)
-    s, c, _, _ = K.join_agg(p, rstart, rlen, rbk, torch.from_numpy(roff).to(device), tp)
+    mt = len(lk) // NL.lib().hs_join_tile_rows() + B + 1
+    s, c, _, _ = K.join_agg(p, rstart, rlen, rbk, torch.from_numpy(roff).to(device), tp, mt)
     # reference
     rmap = {int(k): i for i, k in enumerate(rk)}
     tot, cnt, pairs = 0.0, 0, []
@@ -185,6 +186,65 @@ def test_join_agg_and_pairs(device):
     assert int(c[0].item()) == cnt
     assert abs(float(s[0].item()) - tot) < 1e-9 * tot
     ol, orr = K.join_pairs(p, rstart, rlen, rbk, torch.from_numpy(roff).to(device), tp,
-                           max_tiles=len(lk) // 2048 + B + 1)
+                           max_tiles=mt)
     got = sorted(zip(ol.cpu().tolist(), orr.cpu().tolist()))
     assert got == sorted(pairs)
+
+
+def test_join_many_to_many_with_nulls_and_wide_spans(device):
+    """Duplicate right keys (match rounds > 1), null left keys (sorted first), a right span wider
+    than the LDS stage (global binary-search fallback) and a grouped aggregate on a right column."""
+    import torch
+    from hyperspace_amd.ops import _lib as NL, kernels as K
+    rng = np.random.default_rng(11)
+    B = 4
+    rk = np.concatenate([np.repeat(np.arange(0, 3000, dtype=np.int64), 3),   # 3 dups per key
+                         np.arange(10_000, 100_000, dtype=np.int64)])          # dense: wide spans
+    rb = murmur3.bucket_ids([pa.array(rk)], B)
+    lk = np.concatenate([rng.integers(0, 3000, 20_000), rng.integers(10_000, 100_000, 20_000)])
+    lb = murmur3.bucket_ids([pa.array(lk)], B)
+    ro = np.lexsort((rk, rb)); rk, rb = rk[ro], rb[ro]
+    lo_ = np.lexsort((lk, lb)); lk, lb = lk[lo_], lb[lo_]
+    lnull = np.zeros(len(lk), bool)
+    # null keys must sit at the start of each bucket (nulls-first sort); null out the first 5
+    loff = np.searchsorted(lb, np.arange(B + 1)).astype(np.int64)
+    for b in range(B):
+        lnull[loff[b]:loff[b] + 5] = True
+    roff = np.searchsorted(rb, np.arange(B + 1)).astype(np.int64)
+    rgrp = rng.integers(0, 5, len(rk)).astype(np.int32)
+    lval = rng.random(len(lk))
+    clk = _col(pa.array(lk, mask=lnull), device)
+    clv = _col(pa.array(lval), device)
+    crk, crg = _col(pa.array(rk), device), _col(pa.array(rgrp), device)
+    p = NL.JoinParams()
+    p.cols[0], p.cols[1] = clk.desc(), clv.desc()
+    p.cols[8], p.cols[9] = crk.desc(), crg.desc()
+    p.lkey, p.rkey = 0, 8
+    p.nlp, p.npreds = 0, 0
+    a = NL.AggSpec()
+    a.kind, a.nterms = NL.AK_SUM, 1
+    a.col[0], a.alpha[0], a.beta[0] = 1, 0.0, 1.0
+    p.aggs[0] = a
+    p.naggs, p.key_is_float = 1, 0
+    p.group_col, p.num_groups, p.group_base = 9, 5, 0
+    rstart, rlen, rbk = K.full_ranges(loff, device)
+    tp = K.ranges_to_tiles(rlen)
+    mt = len(lk) // NL.lib().hs_join_tile_rows() + B + 1
+    roff_t = torch.from_numpy(roff).to(device)
+    s, c, _, _ = K.join_agg(p, rstart, rlen, rbk, roff_t, tp, mt)
+    from collections import defaultdict
+    rpos = defaultdict(list)
+    for j, k in enumerate(rk):
+        rpos[int(k)].append(j)
+    exp_s, exp_c, pairs = np.zeros(5), np.zeros(5, np.int64), []
+    for i, k in enumerate(lk):
+        if lnull[i]:
+            continue
+        for j in rpos.get(int(k), []):
+            exp_s[rgrp[j]] += lval[i]
+            exp_c[rgrp[j]] += 1
+            pairs.append((i, j))
+    assert c.cpu().numpy().tolist() == exp_c.tolist()
+    np.testing.assert_allclose(s.cpu().numpy(), exp_s, rtol=1e-9)
+    ol, orr = K.join_pairs(p, rstart, rlen, rbk, roff_t, tp, mt)
+    assert sorted(zip(ol.cpu().tolist(), orr.cpu().tolist())) == sorted(pairs)

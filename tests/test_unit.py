@@ -1,0 +1,310 @@
+"""Pure unit tests (no data): IndexConfig, JSON/hash utils, Murmur3 golden vectors, display
+buffers, conf accessors, caches, event logger wiring.
+
+Mirrors the reference's pure-unit tier: ``IndexConfigTest``, ``JsonUtilsTest``,
+``HashingUtilsTest``, ``BufferStreamTest``, ``DisplayModeTest``, ``HyperspaceConfTest``,
+``IndexCacheTest`` (mock clock) and ``BucketUnionTest.scala:101-122`` (Murmur3 vectors).
+"""
+import numpy as np
+import pyarrow as pa
+import pytest
+
+from hyperspace_amd import IndexConfig
+from hyperspace_amd.index import constants as C
+from hyperspace_amd.index.cache import Clock, CreationTimeBasedIndexCache, IndexCacheFactoryImpl
+from hyperspace_amd.plananalysis.display import (BufferStream, ConsoleMode, HTMLMode, PlainTextMode,
+                                                 Tag, get_display_mode)
+from hyperspace_amd.utils import hashing, json_utils, murmur3
+from hyperspace_amd.utils import path_utils as P
+from hyperspace_amd.utils.cache import CacheWithTransform
+from hyperspace_amd.utils.conf import HyperspaceConf, RuntimeConf
+
+
+# ------------------------------------------------------------------------------------------------
+# IndexConfig (IndexConfigTest)
+# ------------------------------------------------------------------------------------------------
+def test_index_config_validation():
+    with pytest.raises(ValueError):
+        IndexConfig("", ["a"])
+    with pytest.raises(ValueError):
+        IndexConfig("i", [])
+    with pytest.raises(ValueError):
+        IndexConfig("i", ["a", "A"])
+    with pytest.raises(ValueError):
+        IndexConfig("i", ["a"], ["b", "B"])
+    with pytest.raises(ValueError):
+        IndexConfig("i", ["a"], ["A"])
+
+
+def test_index_config_equality_ignores_case_and_included_order():
+    a = IndexConfig("Idx", ["A", "b"], ["c", "D"])
+    b = IndexConfig("idx", ["a", "B"], ["d", "C"])
+    assert a == b and hash(a) == hash(b)
+    # indexed order matters
+    assert IndexConfig("i", ["a", "b"]) != IndexConfig("i", ["b", "a"])
+    assert IndexConfig("i", ["a"]) != IndexConfig("j", ["a"])
+
+
+def test_index_config_builder_guards():
+    cfg = IndexConfig.builder().indexName("n").indexBy("a", "b").include("c").create()
+    assert cfg == IndexConfig("n", ["a", "b"], ["c"])
+    with pytest.raises(RuntimeError):
+        IndexConfig.builder().indexName("n").indexName("m")
+    with pytest.raises(RuntimeError):
+        IndexConfig.builder().indexBy("a").indexBy("b")
+    with pytest.raises(RuntimeError):
+        IndexConfig.builder().include("a").include("b")
+    with pytest.raises(ValueError):
+        IndexConfig.builder().indexName("")
+    with pytest.raises(ValueError):
+        IndexConfig.builder().indexName("n").create()
+
+
+# ------------------------------------------------------------------------------------------------
+# JSON / hashing (JsonUtilsTest, HashingUtilsTest)
+# ------------------------------------------------------------------------------------------------
+def test_json_pretty_jackson_style():
+    s = json_utils.to_json({"a": 1, "b": [1, 2], "c": {}, "d": [], "e": None, "f": "x"})
+    assert s == ('{\n  "a" : 1,\n  "b" : [ 1, 2 ],\n  "c" : { },\n  "d" : [ ],\n'
+                 '  "e" : null,\n  "f" : "x"\n}')
+    assert json_utils.from_json(s) == {"a": 1, "b": [1, 2], "c": {}, "d": [], "e": None, "f": "x"}
+
+
+def test_json_round_trip_nested():
+    obj = {"x": [{"name": "f1", "size": 1}, {"name": "f2", "size": 2}], "y": {"z": True}}
+    assert json_utils.from_json(json_utils.to_json(obj)) == obj
+
+
+def test_md5_hex():
+    assert hashing.md5_hex("") == "d41d8cd98f00b204e9800998ecf8427e"
+    assert hashing.md5_hex("abc") == "900150983cd24fb0d6963f7d28e17f72"
+
+
+# ------------------------------------------------------------------------------------------------
+# Spark Murmur3 (Appendix D golden vectors)
+# ------------------------------------------------------------------------------------------------
+def test_murmur3_golden_ints():
+    h = murmur3.hash_columns([pa.array([2, 3], pa.int32())])
+    assert list(h) == [1765031574, -1823081949]
+    assert list(murmur3.bucket_ids([pa.array([2, 3], pa.int32())], 10)) == [4, 1]
+
+
+M32 = 0xFFFFFFFF
+
+
+def _py_mix_k1(k):
+    k = (k * 0xCC9E2D51) & M32
+    k = ((k << 15) | (k >> 17)) & M32
+    return (k * 0x1B873593) & M32
+
+
+def _py_mix_h1(h, k):
+    h ^= k
+    h = ((h << 13) | (h >> 19)) & M32
+    return (h * 5 + 0xE6546B64) & M32
+
+
+def _py_fmix(h, n):
+    h ^= n
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & M32
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & M32
+    return h ^ (h >> 16)
+
+
+def _signed(u):
+    return u - (1 << 32) if u & 0x80000000 else u
+
+
+def _py_hash_int(v, seed):
+    return _signed(_py_fmix(_py_mix_h1(seed & M32, _py_mix_k1(v & M32)), 4))
+
+
+def _py_hash_long(v, seed):
+    v &= (1 << 64) - 1
+    h = _py_mix_h1(seed & M32, _py_mix_k1(v & M32))
+    h = _py_mix_h1(h, _py_mix_k1(v >> 32))
+    return _signed(_py_fmix(h, 8))
+
+
+def _py_hash_bytes(b, seed):
+    """Spark ``hashUnsafeBytes``: 4-byte LE words, then each tail byte mixed on its own."""
+    h = seed & M32
+    n4 = len(b) // 4 * 4
+    for i in range(0, n4, 4):
+        h = _py_mix_h1(h, _py_mix_k1(int.from_bytes(b[i:i + 4], "little")))
+    for i in range(n4, len(b)):
+        sb = b[i] - 256 if b[i] >= 128 else b[i]
+        h = _py_mix_h1(h, _py_mix_k1(sb & M32))
+    return _signed(_py_fmix(h, len(b)))
+
+
+def test_murmur3_spark_known_values():
+    # Spark: SELECT hash(1) == -559580957
+    assert murmur3.hash_columns([pa.array([1], pa.int32())])[0] == -559580957
+
+
+def test_murmur3_matches_scalar_oracle():
+    rng = np.random.default_rng(3)
+    ints = rng.integers(-2**31, 2**31 - 1, 200).astype(np.int32)
+    longs = rng.integers(-2**63, 2**63 - 1, 200, dtype=np.int64)
+    strs = ["", "a", "ab", "abc", "abcd", "abcde", "héllo wörld", "x" * 37]
+    assert list(murmur3.hash_columns([pa.array(ints)])) == [_py_hash_int(int(v), 42) for v in ints]
+    assert list(murmur3.hash_columns([pa.array(longs)])) == [_py_hash_long(int(v), 42) for v in longs]
+    assert list(murmur3.hash_columns([pa.array(strs)])) == \
+        [_py_hash_bytes(s.encode(), 42) for s in strs]
+    # dates hash as int, doubles as their long bits (with -0.0 normalised to 0.0)
+    assert murmur3.hash_columns([pa.array([19000], pa.date32())])[0] == _py_hash_int(19000, 42)
+    bits = int(np.array([1.5]).view(np.int64)[0])
+    assert murmur3.hash_columns([pa.array([1.5])])[0] == _py_hash_long(bits, 42)
+    assert murmur3.hash_columns([pa.array([-0.0])])[0] == murmur3.hash_columns([pa.array([0.0])])[0]
+
+
+def test_murmur3_null_keeps_seed_and_chaining():
+    # A null contributes nothing: hash(null) == seed.
+    assert murmur3.hash_columns([pa.array([None], pa.int32())])[0] == 42
+    # Chaining: hash(a, b) == hash_b(seed=hash_a(42)).
+    a = pa.array([5, 6], pa.int32())
+    b = pa.array([7, 8], pa.int64())
+    ha = murmur3.hash_columns([a])
+    hab = murmur3.hash_columns([a, b])
+    assert list(hab) == [_py_hash_long(bv, int(s)) for bv, s in zip(b.to_pylist(), ha)]
+
+
+def test_murmur3_pmod_non_negative():
+    h = np.array([-7, -1, 0, 5], dtype=np.int32)
+    assert list(murmur3.pmod(h, 4)) == [1, 3, 0, 1]
+
+
+# ------------------------------------------------------------------------------------------------
+# Paths (PathUtilsTest / DataPathFilter)
+# ------------------------------------------------------------------------------------------------
+def test_data_path_filter():
+    assert P.data_path_filter("part-0.parquet")
+    assert not P.data_path_filter("_SUCCESS")
+    assert not P.data_path_filter(".hidden")
+    assert P.data_path_filter("_col=1")  # partition dir with '='
+
+
+def test_path_helpers(tmp_path):
+    q = P.make_absolute(str(tmp_path))
+    assert P.is_qualified(q) and q.startswith("file:/")
+    assert P.to_local(q) == str(tmp_path)
+    assert P.get_name(P.join(q, "x")) == "x"
+    assert P.get_parent(P.join(q, "x")) == q
+
+
+# ------------------------------------------------------------------------------------------------
+# Display / BufferStream (DisplayModeTest, BufferStreamTest)
+# ------------------------------------------------------------------------------------------------
+def test_buffer_stream_highlight_preserves_whitespace():
+    b = BufferStream(PlainTextMode())
+    b.write("  ").highlight("  abc  ").write_line("x")
+    assert str(b) == "    <----abc---->  x\n"
+    b2 = BufferStream(PlainTextMode())
+    b2.highlight("   ")
+    assert str(b2) == "   "
+
+
+def test_display_modes_and_conf_override():
+    assert HTMLMode().new_line == "<br>"
+    h = BufferStream(HTMLMode()).write_line("a")
+    assert h.with_tag() == "<pre>a<br></pre>"
+    assert ConsoleMode().highlight_tag.open == "\u001b[42m"
+    conf = RuntimeConf({C.DISPLAY_MODE: "html", C.HIGHLIGHT_BEGIN_TAG: "<<",
+                        C.HIGHLIGHT_END_TAG: ">>"})
+    m = get_display_mode(conf)
+    assert isinstance(m, HTMLMode) and m.highlight_tag.open == "<<"
+    assert isinstance(get_display_mode(RuntimeConf({})), PlainTextMode)
+    assert PlainTextMode(Tag("", "")).highlight_tag.open == "<----"
+
+
+# ------------------------------------------------------------------------------------------------
+# Conf (HyperspaceConfTest: legacy numBuckets key precedence)
+# ------------------------------------------------------------------------------------------------
+def test_num_buckets_legacy_key_precedence():
+    assert HyperspaceConf.num_buckets_for_index(RuntimeConf({})) == 200
+    assert HyperspaceConf.num_buckets_for_index(RuntimeConf({C.INDEX_NUM_BUCKETS_LEGACY: "7"})) == 7
+    assert HyperspaceConf.num_buckets_for_index(
+        RuntimeConf({C.INDEX_NUM_BUCKETS_LEGACY: "7", C.INDEX_NUM_BUCKETS: "9"})) == 9
+
+
+def test_hybrid_scan_delete_enabled_follows_ratio():
+    c = RuntimeConf({C.INDEX_HYBRID_SCAN_DELETED_RATIO_THRESHOLD: "0"})
+    assert not HyperspaceConf.hybrid_scan_delete_enabled(c)
+    c.set(C.INDEX_HYBRID_SCAN_DELETED_RATIO_THRESHOLD, "0.2")
+    assert HyperspaceConf.hybrid_scan_delete_enabled(c)
+
+
+def test_runtime_conf_basic():
+    c = RuntimeConf({"a": 1})
+    assert c.get("a") == "1" and c.contains("a")
+    c.unset("a")
+    assert c.get("a", "d") == "d" and not c.contains("a")
+
+
+# ------------------------------------------------------------------------------------------------
+# Caches (IndexCacheTest with a mock clock)
+# ------------------------------------------------------------------------------------------------
+class MockClock(Clock):
+    def __init__(self):
+        self.t = 1000
+
+    def get_time(self):
+        return self.t
+
+
+class _S:
+    def __init__(self, conf):
+        self.conf = conf
+
+
+def test_creation_time_cache_expiry():
+    clock = MockClock()
+    s = _S(RuntimeConf({C.INDEX_CACHE_EXPIRY_DURATION_SECONDS: "10"}))
+    cache = CreationTimeBasedIndexCache(s, clock)
+    assert cache.get() is None
+    cache.set(["e1"])
+    assert cache.get() == ["e1"]
+    clock.t += 9_999
+    assert cache.get() == ["e1"]
+    clock.t += 1
+    assert cache.get() is None
+    cache.set(["e2"])
+    cache.clear()
+    assert cache.get() is None
+    with pytest.raises(ValueError):
+        IndexCacheFactoryImpl().create(s, "nope")
+
+
+def test_cache_with_transform_recomputes_on_change():
+    state = {"v": "a", "n": 0}
+
+    def transform(v):
+        state["n"] += 1
+        return v.upper()
+    c = CacheWithTransform(lambda: state["v"], transform)
+    assert c.load() == "A" and c.load() == "A" and state["n"] == 1
+    state["v"] = "b"
+    assert c.load() == "B" and state["n"] == 2
+
+
+# ------------------------------------------------------------------------------------------------
+# Event logger reflection (SparkInvolvedSuite MockEventLogger wiring)
+# ------------------------------------------------------------------------------------------------
+class RecordingLogger:
+    events = []
+
+    def log_event(self, e):
+        RecordingLogger.events.append(e)
+
+
+def test_event_logger_by_class_name():
+    from hyperspace_amd.exceptions import HyperspaceException
+    from hyperspace_amd.telemetry.events import NoOpEventLogger, get_event_logger
+    assert isinstance(get_event_logger(RuntimeConf({})), NoOpEventLogger)
+    lg = get_event_logger(RuntimeConf({C.EVENT_LOGGER_CLASS_KEY: f"{__name__}.RecordingLogger"}))
+    assert isinstance(lg, RecordingLogger)
+    with pytest.raises(HyperspaceException):
+        get_event_logger(RuntimeConf({C.EVENT_LOGGER_CLASS_KEY: "no.such.Logger"}))
