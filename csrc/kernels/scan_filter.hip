@@ -318,9 +318,10 @@ int hs_range_search(const ColDesc* key, const int64_t* bucket_off, const int32_t
   return (int)hipGetLastError();
 }
 
-int hs_ranges_to_tiles(const int64_t* rlen, int R, int64_t* tile_prefix, void* stream) {
+int hs_ranges_to_tiles(const int64_t* rlen, int R, int tile_rows, int64_t* tile_prefix,
+                       void* stream) {
   hipLaunchKernelGGL(hs_ranges_to_tiles_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rlen,
-                     R, SF_TILE, tile_prefix);
+                     R, tile_rows, tile_prefix);
   return (int)hipGetLastError();
 }
 

@@ -78,10 +78,14 @@ class Action:
             self._save_entry(self.base_id + 1, entry)
         self._barrier()
 
+    def end_log_entry(self):
+        """Entry committed by ``end`` (the same as ``begin``'s unless an action overrides it)."""
+        return self.log_entry()
+
     def _end(self) -> None:
         self._barrier()
         if self._is_coordinator():
-            entry = self.log_entry()
+            entry = self.end_log_entry()
             entry.state = self.final_state
             entry.id = self.base_id + 2
             if not self.log_manager.delete_latest_stable_log():

@@ -86,11 +86,22 @@ class VacuumAction(_ExistingEntryAction):
 
 
 class CancelAction(_ExistingEntryAction):
-    """Roll a crashed action back to the last stable state."""
+    """Roll a crashed action back to the last stable state.
+
+    The reference documents "save the next log entry with the contents of the last active state
+    log entry" but commits the *crashed* entry with the stable state (``CancelAction.scala:36-40``),
+    so cancelling a crashed refresh leaves an ACTIVE entry pointing at a half-written ``v__=n``.
+    Here the final entry carries the last stable entry's content, as documented."""
     what = "cancel"
     transient_state = states.CANCELLING
 
     _final = None
+
+    def end_log_entry(self):
+        stable = self.log_manager.get_latest_stable_log()
+        if self.final_state == states.DOESNOTEXIST or stable is None:
+            return self.log_entry()
+        return stable
 
     @property
     def final_state(self):

@@ -448,9 +448,8 @@ class GpuBackend:
             import torch
             ol = orr = torch.empty(0, dtype=torch.int64, device=self.device)
         else:
-            tp = K.ranges_to_tiles(rlen)
-            max_tiles = left.table.num_rows // NL.lib().hs_join_tile_rows() + rlen.numel() + 1
-            ol, orr = K.join_pairs(jp, rstart, rlen, rbk, right.table.bucket_offsets, tp, max_tiles)
+            max_tiles = K.join_max_tiles(left.table.num_rows, rlen.numel())
+            ol, orr = K.join_pairs(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles)
         lset = {a.expr_id for a in p.left.output}
         lattrs = [a for a in out_attrs if a.expr_id in lset]
         rattrs = [a for a in out_attrs if a.expr_id not in lset]
@@ -643,9 +642,8 @@ class GpuBackend:
         jp.naggs = len(specs)
         if keep[0].always_false or keep[1].always_false:
             return (*self._empty_agg(len(specs), G), G, gbase, gdict, gtype)
-        tp = K.ranges_to_tiles(rlen)
-        max_tiles = left.table.num_rows // NL.lib().hs_join_tile_rows() + rlen.numel() + 1
-        out = K.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, tp, max_tiles)
+        max_tiles = K.join_max_tiles(left.table.num_rows, rlen.numel())
+        out = K.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles)
         return (*out, G, gbase, gdict, gtype)
 
 

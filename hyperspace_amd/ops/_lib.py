@@ -127,7 +127,7 @@ def lib():
     _sig(L.hs_scan_grid, I)
     _sig(L.hs_join_tile_rows, I)
     _sig(L.hs_range_search, I, P, P, P, I, I, U64, I, I, U64, I, P, P, P, P)
-    _sig(L.hs_ranges_to_tiles, I, P, I, P, P)
+    _sig(L.hs_ranges_to_tiles, I, P, I, I, P, P)
     _sig(L.hs_scan_agg, I, P, P, P, I, P, I, P, P, P, P, P, P, P, P, P)
     _sig(L.hs_scan_count, I, P, P, P, I, P, I, P, P)
     _sig(L.hs_scan_select, I, P, P, P, I, P, P, I, P, P)
@@ -135,8 +135,6 @@ def lib():
     _sig(L.hs_agg_final, I, P, P, P, P, I, I, P, P, P, P, P)
     _sig(L.hs_join_count, I, P, P, P, P, P, I, P, I64, P, I, P, P)
     _sig(L.hs_join_emit, I, P, I, P, P, I, P, P, P, P)
-    if L.hs_scan_tile_rows() != L.hs_join_tile_rows():
-        raise RuntimeError("scan/join tile sizes differ")
     _lib = L
     return L
 

@@ -203,11 +203,14 @@ def full_ranges(bucket_off_host: np.ndarray, device, buckets: Optional[List[int]
     return rstart, rlen, rbucket
 
 
-def ranges_to_tiles(rlen):
+def ranges_to_tiles(rlen, tile_rows: int = None):
+    """Exclusive prefix of per-range tile counts (``tp[R]`` = total).  Scan kernels use the scan
+    tile; the join wrappers below compute their own prefix with the join tile."""
     torch = _torch()
     R = rlen.numel()
     tp = torch.empty(R + 1, dtype=torch.int64, device=rlen.device)
-    NL.check(NL.lib().hs_ranges_to_tiles(NL.ptr(rlen), R, NL.ptr(tp), NL.stream_ptr()),
+    tr = int(tile_rows or NL.lib().hs_scan_tile_rows())
+    NL.check(NL.lib().hs_ranges_to_tiles(NL.ptr(rlen), R, tr, NL.ptr(tp), NL.stream_ptr()),
              "hs_ranges_to_tiles")
     return tp
 
@@ -271,12 +274,17 @@ def scan_select(params: NL.ScanParams, rstart, rlen, tile_prefix, max_tiles: int
 # ------------------------------------------------------------------------------------------------
 # Join
 # ------------------------------------------------------------------------------------------------
-def join_agg(params: NL.JoinParams, rstart, rlen, rbucket, roff, tile_prefix, max_tiles: int,
+def join_max_tiles(left_rows: int, num_ranges: int) -> int:
+    """Upper bound of the join tile count over ``num_ranges`` ranges of ``left_rows`` rows."""
+    return left_rows // NL.lib().hs_join_tile_rows() + num_ranges + 1
+
+
+def join_agg(params: NL.JoinParams, rstart, rlen, rbucket, roff, max_tiles: int,
              grid: int = None):
-    """``max_tiles`` bounds ``tile_prefix[-1]`` (left rows / tile + #ranges); sizes the per-tile
-    span scratch."""
+    """``max_tiles`` (see ``join_max_tiles``) sizes the per-tile span scratch."""
     torch = _torch()
     L = NL.lib()
+    tile_prefix = ranges_to_tiles(rlen, L.hs_join_tile_rows())
     grid = grid or L.hs_scan_grid()
     GA = params.naggs * (params.num_groups if params.group_col >= 0 else 1)
     dev = rstart.device
@@ -297,9 +305,10 @@ def join_agg(params: NL.JoinParams, rstart, rlen, rbucket, roff, tile_prefix, ma
     return os_, oc, omn, omx
 
 
-def join_pairs(params: NL.JoinParams, rstart, rlen, rbucket, roff, tile_prefix, max_tiles: int):
+def join_pairs(params: NL.JoinParams, rstart, rlen, rbucket, roff, max_tiles: int):
     torch = _torch()
     L = NL.lib()
+    tile_prefix = ranges_to_tiles(rlen, L.hs_join_tile_rows())
     grid = L.hs_scan_grid()
     dev = rstart.device
     counts = torch.zeros(max_tiles + 1, dtype=torch.int64, device=dev)

@@ -170,9 +170,8 @@ def test_join_agg_and_pairs(device):
     p.aggs[0] = a
     p.naggs, p.group_col, p.key_is_float = 1, -1, 0
     rstart, rlen, rbk = K.full_ranges(loff, device)
-    tp = K.ranges_to_tiles(rlen)
-    mt = len(lk) // NL.lib().hs_join_tile_rows() + B + 1
-    s, c, _, _ = K.join_agg(p, rstart, rlen, rbk, torch.from_numpy(roff).to(device), tp, mt)
+    mt = K.join_max_tiles(len(lk), B)
+    s, c, _, _ = K.join_agg(p, rstart, rlen, rbk, torch.from_numpy(roff).to(device), mt)
     # reference
     rmap = {int(k): i for i, k in enumerate(rk)}
     tot, cnt, pairs = 0.0, 0, []
@@ -185,8 +184,7 @@ def test_join_agg_and_pairs(device):
         pairs.append((i, j))
     assert int(c[0].item()) == cnt
     assert abs(float(s[0].item()) - tot) < 1e-9 * tot
-    ol, orr = K.join_pairs(p, rstart, rlen, rbk, torch.from_numpy(roff).to(device), tp,
-                           max_tiles=mt)
+    ol, orr = K.join_pairs(p, rstart, rlen, rbk, torch.from_numpy(roff).to(device), mt)
     got = sorted(zip(ol.cpu().tolist(), orr.cpu().tolist()))
     assert got == sorted(pairs)
 
@@ -228,10 +226,9 @@ def test_join_many_to_many_with_nulls_and_wide_spans(device):
     p.naggs, p.key_is_float = 1, 0
     p.group_col, p.num_groups, p.group_base = 9, 5, 0
     rstart, rlen, rbk = K.full_ranges(loff, device)
-    tp = K.ranges_to_tiles(rlen)
-    mt = len(lk) // NL.lib().hs_join_tile_rows() + B + 1
+    mt = K.join_max_tiles(len(lk), B)
     roff_t = torch.from_numpy(roff).to(device)
-    s, c, _, _ = K.join_agg(p, rstart, rlen, rbk, roff_t, tp, mt)
+    s, c, _, _ = K.join_agg(p, rstart, rlen, rbk, roff_t, mt)
     from collections import defaultdict
     rpos = defaultdict(list)
     for j, k in enumerate(rk):
@@ -246,5 +243,5 @@ def test_join_many_to_many_with_nulls_and_wide_spans(device):
             pairs.append((i, j))
     assert c.cpu().numpy().tolist() == exp_c.tolist()
     np.testing.assert_allclose(s.cpu().numpy(), exp_s, rtol=1e-9)
-    ol, orr = K.join_pairs(p, rstart, rlen, rbk, roff_t, tp, mt)
+    ol, orr = K.join_pairs(p, rstart, rlen, rbk, roff_t, mt)
     assert sorted(zip(ol.cpu().tolist(), orr.cpu().tolist())) == sorted(pairs)
