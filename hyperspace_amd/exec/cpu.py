@@ -58,7 +58,8 @@ class CpuBackend:
     def _read(self, p: X.FileSourceScanExec, files: List[str]) -> pa.Table:
         rel = p.relation
         cols = [a.name for a in p.output]
-        fmt = "parquet" if rel.is_index() else rel.file_format
+        # index data and Delta data files are parquet
+        fmt = "parquet" if rel.is_index() or rel.file_format == "delta" else rel.file_format
         data_schema = rel.data_schema
         t = read_files(fmt, files, data_schema, rel.options, rel.location.partition_spec, cols)
         arrays = []
