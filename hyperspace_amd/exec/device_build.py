@@ -22,22 +22,14 @@ import pyarrow as pa
 import pyarrow.compute as pc
 
 from ..index import constants as C
-from ..index.builder import group_by_bucket, read_index_input
+from ..index.builder import group_by_bucket, read_index_input, source_format
 from ..io.writer import write_bucket_file
 from ..ops import kernels as K
 from ..utils import path_utils as P
 from ..utils.conf import HyperspaceConf
 from .device_table import DeviceColumn, DeviceTable, is_string
 
-_WRITE_POOL = None
 LAST_BUILD_STATS: Dict[str, float] = {}
-
-
-def _writer_pool():
-    global _WRITE_POOL
-    if _WRITE_POOL is None:
-        _WRITE_POOL = cf.ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4))
-    return _WRITE_POOL
 
 
 def _global_dicts(t: pa.Table, dist) -> Dict[str, pa.Array]:
@@ -77,22 +69,16 @@ def _sort_and_write(session, table: Dict[str, DeviceColumn], names: List[str], b
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     off = np.concatenate([[0], np.cumsum(counts.cpu().numpy())]).astype(np.int64)
-    host_cols = [g.to_arrow() for g in gathered]
-    full = pa.Table.from_arrays(host_cols, names=names)
-    full = full.cast(schema) if not full.schema.equals(schema) else full
-    t2 = time.perf_counter()
     codec = HyperspaceConf.index_file_codec(session.conf)
     rg = HyperspaceConf.index_row_group_rows(session.conf)
     job = str(uuid.uuid4())
-    futs = []
-    for b in range(num_buckets):
-        lo, hi = int(off[b]), int(off[b + 1])
-        if hi > lo:
-            futs.append(_writer_pool().submit(write_bucket_file, full.slice(lo, hi - lo), out_path,
-                                              task_id, job, b, codec, rg))
-    paths = [f.result() for f in futs]
-    LAST_BUILD_STATS.update({"sort_gather_s": t1 - t0, "d2h_s": t2 - t1,
-                             "write_s": time.perf_counter() - t2})
+    from . import staging
+    paths = staging.download_buckets(
+        gathered, names, schema, off,
+        lambda t, b: write_bucket_file(t, out_path, task_id, job, b, codec, rg),
+        bucket.device)
+    LAST_BUILD_STATS.update({"sort_gather_s": t1 - t0,
+                             "d2h_write_s": time.perf_counter() - t1})
     return paths
 
 
@@ -106,29 +92,26 @@ def device_build_from_source(session, rel, files: List[str], columns: List[str],
     _prepare_out_dir(out_path, mode, dist)
     t0 = time.perf_counter()
     my_files = files[rank::world]
-    t = read_index_input(rel, my_files, columns, lineage_ids) if my_files else None
-    if t is None:
-        from ..io.reader import read_files
-        t = read_files("parquet" if rel.file_format == "delta" else rel.file_format, files[:1],
-                       rel.data_schema, rel.options, rel.location.partition_spec, columns).slice(0, 0)
-        if lineage_ids is not None:
-            t = t.append_column(pa.field(C.DATA_FILE_NAME_ID, pa.int64(), False),
-                                pa.array([], pa.int64()))
-    schema = t.schema
-    names = t.column_names
-    dicts = _global_dicts(t, dist)
+    fmt = source_format(rel)
+    if fmt == "parquet":
+        cols, names, schema = _upload_parquet(rel, my_files, columns, indexed, lineage_ids,
+                                              device, dist)
+    else:
+        cols, names, schema = _upload_generic(rel, files, my_files, columns, indexed, lineage_ids,
+                                              device, dist)
     t1 = time.perf_counter()
-    cols = {n: DeviceColumn.from_arrow(t.column(n), device, dicts.get(n),
-                                       raw_strings=(n in indexed and n in dicts))
-            for n in names}
     source_bytes = sum(c.nbytes() for c in cols.values())
-    del t
     bucket, _ = K.murmur3_bucket([cols[c] for c in indexed], num_buckets, with_counts=False)
     if world > 1:
         from ..parallel.shuffle import exchange
+        # every rank must send the same column list: agree on which columns carry validity
+        has_valid = dist.all_gather_object([cols[n].valid is not None for n in names])
+        need_valid = [any(v[i] for v in has_valid) for i in range(len(names))]
         dest = torch.remainder(bucket, world).to(torch.int32)
         flat = []
-        for n in names:
+        for n, nv in zip(names, need_valid):
+            if nv and cols[n].valid is None:
+                cols[n].valid = torch.ones(len(cols[n]), dtype=torch.uint8, device=device)
             flat.append(cols[n].data)
             flat.append(cols[n].valid)
         flat.append(bucket)
@@ -144,9 +127,61 @@ def device_build_from_source(session, rel, files: List[str], columns: List[str],
                             rank)
     if dist is not None:
         dist.barrier()
-    LAST_BUILD_STATS.update({"read_s": t1 - t0, "h2d_hash_exchange_s": t2 - t1,
+    LAST_BUILD_STATS.update({"read_h2d_s": t1 - t0, "hash_exchange_s": t2 - t1,
                              "total_s": time.perf_counter() - t0, "source_bytes": source_bytes})
     return paths
+
+
+def _finish_strings(host_strings: Dict[str, list], cols: Dict[str, DeviceColumn], indexed,
+                    device, dist) -> None:
+    """Dictionary-encode string columns with a job-global sorted dictionary and upload codes."""
+    for name, chunks in host_strings.items():
+        chunks = [c for c in chunks if c is not None]
+        arr = pa.chunked_array(chunks, type=chunks[0].type) if chunks else pa.chunked_array([], pa.string())
+        d = _global_dicts(pa.table({name: arr}), dist)[name]
+        cols[name] = DeviceColumn.from_arrow(arr, device, d, raw_strings=name in indexed)
+
+
+def _upload_parquet(rel, my_files, columns, indexed, lineage_ids, device, dist):
+    """Pipelined decode -> pinned -> HBM upload of this rank's Parquet files (staging.py)."""
+    import pyarrow.parquet as pq
+    from ..io.reader import output_schema, read_files
+    from . import staging
+    schema = output_schema(rel.data_schema, rel.location.partition_spec, columns)
+    counts = list(staging.io_pool().map(
+        lambda f: pq.ParquetFile(P.to_local(f)).metadata.num_rows, my_files))
+
+    def read_file(f):
+        return read_files("parquet", [f], rel.data_schema, rel.options,
+                          rel.location.partition_spec, columns)
+    lin = [lineage_ids[f] for f in my_files] if lineage_ids is not None else None
+    up = staging.upload_files(read_file, my_files, counts, schema, device, lin,
+                              C.DATA_FILE_NAME_ID)
+    cols = dict(up.columns)
+    _finish_strings(up.host_strings, cols, indexed, device, dist)
+    names = list(schema.names)
+    fields = list(schema)
+    if lineage_ids is not None:
+        names.append(C.DATA_FILE_NAME_ID)
+        fields.append(pa.field(C.DATA_FILE_NAME_ID, pa.int64(), False))
+    return {n: cols[n] for n in names}, names, pa.schema(fields)
+
+
+def _upload_generic(rel, files, my_files, columns, indexed, lineage_ids, device, dist):
+    """Non-Parquet sources (CSV/JSON/ORC/text): host decode of the whole share, then upload."""
+    from ..io.reader import read_files
+    t = read_index_input(rel, my_files, columns, lineage_ids) if my_files else None
+    if t is None:
+        t = read_files(source_format(rel), files[:1], rel.data_schema, rel.options,
+                       rel.location.partition_spec, columns).slice(0, 0)
+        if lineage_ids is not None:
+            t = t.append_column(pa.field(C.DATA_FILE_NAME_ID, pa.int64(), False),
+                                pa.array([], pa.int64()))
+    dicts = _global_dicts(t, dist)
+    cols = {n: DeviceColumn.from_arrow(t.column(n), device, dicts.get(n),
+                                       raw_strings=(n in indexed and n in dicts))
+            for n in t.column_names}
+    return cols, list(t.column_names), t.schema
 
 
 def device_rewrite_buckets(session, files: List[str], indexed: List[str], out_path: str,

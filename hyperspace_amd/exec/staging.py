@@ -1,0 +1,255 @@
+"""Pipelined host <-> HBM staging for index builds (SURVEY §2.3 K1/K4 I/O, §2.4 "pipeline").
+
+Upload (``upload_files``): a thread pool decodes source files (pyarrow, one file per task) and
+each worker immediately copies its fixed-width columns into pinned host memory and issues the
+H2D copy on a dedicated HIP copy stream into a pre-sized device column, at the file's row
+offset.  Decode of file i+1 overlaps the PCIe transfer of file i, and no concatenated host copy
+of the whole table is ever built.  Row offsets come from the Parquet footers, so every file's
+destination slice is known before any data is read.  Lineage ids (K2) are a per-file constant
+written with a device fill — no host array at all.
+
+Download (``download_buckets``): buckets are grouped into ~``chunk_bytes`` chunks; each chunk's
+columns are copied D2H into pinned memory asynchronously, and a writer task waits on that
+chunk's event and encodes/writes its Parquet files while the next chunk is still in flight.
+
+Pinned buffers come from torch's caching host allocator, which keeps a block alive until the
+copies recorded on it have completed, so buffer reuse is race-free by construction.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import threading
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import pyarrow as pa
+
+from .device_table import DeviceColumn, is_string, storage_numpy_dtype
+
+_POOL = None
+_COPY_STREAMS: Dict[int, object] = {}
+
+
+def io_pool() -> cf.ThreadPoolExecutor:
+    global _POOL
+    if _POOL is None:
+        _POOL = cf.ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4),
+                                      thread_name_prefix="hs-stage")
+    return _POOL
+
+
+def copy_stream(device):
+    import torch
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _COPY_STREAMS.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _COPY_STREAMS[idx] = s
+    return s
+
+
+_TORCH_OF_NP = None
+
+
+def _torch_dtype(nd: np.dtype):
+    global _TORCH_OF_NP
+    import torch
+    if _TORCH_OF_NP is None:
+        _TORCH_OF_NP = {np.dtype(np.int8): torch.int8, np.dtype(np.int16): torch.int16,
+                        np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64,
+                        np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
+                        np.dtype(np.uint8): torch.uint8}
+    if nd == np.dtype(np.uint32):
+        return torch.int32
+    if nd == np.dtype(np.uint64):
+        return torch.int64
+    return _TORCH_OF_NP[nd]
+
+
+def fixed_width_numpy(arr) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+    """(values in storage dtype, validity uint8 or None) of a non-string arrow column."""
+    if isinstance(arr, pa.ChunkedArray):
+        arr = arr.combine_chunks() if arr.num_chunks != 1 else arr.chunk(0)
+    t = arr.type
+    nd = storage_numpy_dtype(t)
+    valid = None
+    if arr.null_count:
+        valid = np.asarray(arr.is_valid().to_numpy(zero_copy_only=False), dtype=np.uint8)
+    if pa.types.is_boolean(t):
+        vals = np.asarray(arr.fill_null(False).to_numpy(zero_copy_only=False), dtype=np.uint8)
+    elif pa.types.is_decimal(t):
+        vals = np.asarray(arr.cast(pa.float64()).fill_null(0).to_numpy(), dtype=np.float64)
+    elif pa.types.is_date32(t) or pa.types.is_timestamp(t) or pa.types.is_date64(t) or \
+            pa.types.is_duration(t):
+        st = pa.int32() if pa.types.is_date32(t) else pa.int64()
+        a = arr.view(st)
+        vals = np.asarray((a.fill_null(0) if arr.null_count else a).to_numpy(zero_copy_only=False),
+                          dtype=nd)
+    else:
+        a = arr.fill_null(0) if arr.null_count else arr
+        vals = np.asarray(a.to_numpy(zero_copy_only=False), dtype=nd)
+    return vals, valid
+
+
+def _h2d_async(dst, src: np.ndarray, stream) -> None:
+    """Copy ``src`` into device tensor slice ``dst`` via a pinned bounce buffer on ``stream``."""
+    import torch
+    n = src.shape[0]
+    if n == 0:
+        return
+    pinned = torch.empty(n, dtype=dst.dtype, pin_memory=True)
+    np.copyto(pinned.numpy().view(src.dtype), src, casting="no")
+    with torch.cuda.stream(stream):
+        # torch's caching host allocator records an event for this copy and will not hand the
+        # pinned block out again before it completes
+        dst.copy_(pinned, non_blocking=True)
+
+
+class UploadResult:
+    def __init__(self, columns: Dict[str, DeviceColumn], num_rows: int, host_strings: dict):
+        self.columns = columns
+        self.num_rows = num_rows
+        self.host_strings = host_strings  # name -> list of per-file arrow chunks (in file order)
+
+
+def upload_files(read_file: Callable[[str], pa.Table], files: Sequence[str],
+                 row_counts: Sequence[int], schema: pa.Schema, device,
+                 lineage_ids: Optional[Sequence[int]] = None,
+                 lineage_name: Optional[str] = None) -> UploadResult:
+    """Decode ``files`` in parallel and stream their fixed-width columns into HBM.
+
+    ``row_counts[i]`` must equal the row count ``read_file(files[i])`` returns (Parquet footer);
+    string columns are returned as host arrow chunks for dictionary encoding by the caller.
+    """
+    import torch
+    offs = np.concatenate([[0], np.cumsum(np.asarray(row_counts, dtype=np.int64))])
+    n = int(offs[-1])
+    stream = copy_stream(device)
+    cols: Dict[str, DeviceColumn] = {}
+    strings: Dict[str, list] = {}
+    for f in schema:
+        if is_string(f.type):
+            strings[f.name] = [None] * len(files)
+            continue
+        nd = storage_numpy_dtype(f.type)
+        cols[f.name] = DeviceColumn(torch.empty(n, dtype=_torch_dtype(nd), device=device), None,
+                                    f.type)
+    if lineage_ids is not None:
+        cols[lineage_name] = DeviceColumn(torch.empty(n, dtype=torch.int64, device=device), None,
+                                          pa.int64())
+    lock = threading.Lock()
+    main = torch.cuda.current_stream(device)
+    stream.wait_stream(main)  # allocations above happen-before the copies
+
+    def work(i: int):
+        torch.cuda.set_device(device)
+        t = read_file(files[i])
+        lo, hi = int(offs[i]), int(offs[i + 1])
+        if t.num_rows != hi - lo:
+            raise RuntimeError(f"row count mismatch for {files[i]}: footer {hi - lo}, read "
+                               f"{t.num_rows}")
+        for f in schema:
+            c = t.column(f.name)
+            if f.name in strings:
+                strings[f.name][i] = c
+                continue
+            vals, valid = fixed_width_numpy(c)
+            dc = cols[f.name]
+            _h2d_async(dc.data[lo:hi], vals, stream)
+            if valid is not None:
+                with lock:
+                    if dc.valid is None:
+                        with torch.cuda.stream(stream):
+                            dc.valid = torch.ones(n, dtype=torch.uint8, device=device)
+                _h2d_async(dc.valid[lo:hi], valid, stream)
+        if lineage_ids is not None:
+            with torch.cuda.stream(stream):
+                cols[lineage_name].data[lo:hi].fill_(int(lineage_ids[i]))
+        return t.num_rows
+
+    futs = [io_pool().submit(work, i) for i in range(len(files))]
+    for fu in futs:
+        fu.result()
+    main.wait_stream(stream)
+    return UploadResult(cols, n, strings)
+
+
+def download_buckets(columns: List[DeviceColumn], names: List[str], schema: pa.Schema,
+                     bucket_off: np.ndarray, write_bucket: Callable[[pa.Table, int], str],
+                     device, chunk_bytes: int = 512 << 20) -> List[str]:
+    """D2H the bucket-major ``columns`` chunk by chunk and write each bucket as it lands."""
+    import torch
+    B = len(bucket_off) - 1
+    row_bytes = sum(c.data.element_size() + (1 if c.valid is not None else 0) for c in columns)
+    stream = copy_stream(device)
+    stream.wait_stream(torch.cuda.current_stream(device))
+    chunks: List[Tuple[int, int]] = []
+    b = 0
+    while b < B:
+        e = b
+        rows = 0
+        while e < B and (e == b or (rows + int(bucket_off[e + 1] - bucket_off[e])) * row_bytes
+                         <= chunk_bytes):
+            rows += int(bucket_off[e + 1] - bucket_off[e])
+            e += 1
+        chunks.append((b, e))
+        b = e
+    futs = []
+    max_inflight = 2 * min(16, os.cpu_count() or 4)
+    for b0, b1 in chunks:
+        lo, hi = int(bucket_off[b0]), int(bucket_off[b1])
+        if hi <= lo:
+            continue
+        if len(futs) >= max_inflight:
+            futs[len(futs) - max_inflight].result()  # bound pinned memory in flight
+        host = []
+        with torch.cuda.stream(stream):
+            for c in columns:
+                hv = torch.empty(hi - lo, dtype=c.data.dtype, pin_memory=True)
+                hv.copy_(c.data[lo:hi], non_blocking=True)
+                hm = None
+                if c.valid is not None:
+                    hm = torch.empty(hi - lo, dtype=torch.uint8, pin_memory=True)
+                    hm.copy_(c.valid[lo:hi], non_blocking=True)
+                host.append((hv, hm))
+            ev = torch.cuda.Event()
+            ev.record(stream)
+
+        def write_chunk(b0=b0, b1=b1, lo=lo, host=host, ev=ev):
+            ev.synchronize()
+            arrays = []
+            for c, (hv, hm) in zip(columns, host):
+                arrays.append(host_to_arrow(c, hv.numpy(), None if hm is None else hm.numpy()))
+            full = pa.Table.from_arrays(arrays, names=names)
+            if not full.schema.equals(schema):
+                full = full.cast(schema)
+            out = []
+            for bb in range(b0, b1):
+                s, e = int(bucket_off[bb]) - lo, int(bucket_off[bb + 1]) - lo
+                if e > s:
+                    out.append(write_bucket(full.slice(s, e - s), bb))
+            return out
+        futs.append(io_pool().submit(write_chunk))
+    paths = []
+    for fu in futs:
+        paths.extend(fu.result())
+    return paths
+
+
+def host_to_arrow(c: DeviceColumn, vals: np.ndarray, valid: Optional[np.ndarray]) -> pa.Array:
+    """Arrow array over host numpy values (zero-copy for plain fixed-width columns)."""
+    mask = None if valid is None else (valid == 0)
+    t = c.atype
+    if c.dictionary is not None:
+        idx = pa.array(vals.view(np.int32), pa.int32(), mask=mask)
+        return c.dictionary.take(idx).cast(t) if len(c.dictionary) else pa.nulls(len(vals), t)
+    if pa.types.is_boolean(t):
+        return pa.array(vals.astype(bool), pa.bool_(), mask=mask)
+    if pa.types.is_date32(t):
+        return pa.array(vals.view(np.int32), pa.int32(), mask=mask).view(pa.date32())
+    if pa.types.is_timestamp(t) or pa.types.is_date64(t) or pa.types.is_duration(t):
+        return pa.array(vals.view(np.int64), pa.int64(), mask=mask).view(t)
+    if pa.types.is_decimal(t):
+        return pa.array(vals, pa.float64(), mask=mask).cast(t)
+    return pa.array(vals, t, mask=mask)

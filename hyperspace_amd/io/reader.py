@@ -183,6 +183,16 @@ def read_one(fmt: str, local_path: str, schema: Optional[pa.Schema], options: di
     return t
 
 
+def output_schema(data_schema: pa.Schema, partition_spec: Optional[L.PartitionSpec] = None,
+                  columns: Optional[List[str]] = None) -> pa.Schema:
+    """Schema ``read_files`` returns: requested data columns, then partition columns."""
+    pspec = partition_spec or L.PartitionSpec()
+    data_cols = [f for f in data_schema if columns is None or f.name in columns]
+    part_cols = [f for f in pspec.columns if (columns is None or f.name in columns)
+                 and f.name not in data_schema.names]
+    return pa.schema(data_cols + part_cols)
+
+
 def read_files(fmt: str, files: List[str], data_schema: pa.Schema, options: dict,
                partition_spec: Optional[L.PartitionSpec] = None,
                columns: Optional[List[str]] = None, with_file_index: bool = False) -> pa.Table:
@@ -220,6 +230,9 @@ def read_files(fmt: str, files: List[str], data_schema: pa.Schema, options: dict
             file_idx.append(pa.array(np.full(t.num_rows, i, dtype=np.int32)))
     if not tables:
         t = out_schema.empty_table()
+    elif len(tables) == 1:
+        t = tables[0].select(out_schema.names)
+        t = t if t.schema.equals(out_schema) else t.cast(out_schema)
     else:
         t = pa.concat_tables([x.select(out_schema.names).cast(out_schema) for x in tables])
     if with_file_index:
