@@ -354,6 +354,14 @@ static int launch_spans(const JoinParams* p, const int64_t* rstart, const int64_
 
 extern "C" {
 
+// Per-tile (row0, rows, rs, re) only — consumed by the generated join kernels (exec/jit.py).
+int hs_join_spans(const JoinParams* p, const int64_t* rstart, const int64_t* rlen,
+                  const int32_t* rbucket, const int64_t* roff, int R, const int64_t* tile_prefix,
+                  int64_t max_tiles, int64_t* spans, void* stream) {
+  return launch_spans(p, rstart, rlen, rbucket, roff, R, tile_prefix, max_tiles, spans,
+                      (hipStream_t)stream);
+}
+
 int hs_join_params_size() { return (int)sizeof(JoinParams); }
 int hs_join_tile_rows() { return JN_TILE; }
 

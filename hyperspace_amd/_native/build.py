@@ -81,7 +81,11 @@ def build_runtime(force: bool = False) -> str:
     if not force and not _newer(RUNTIME_LIB, srcs + hdrs):
         return RUNTIME_LIB
     tmp = RUNTIME_LIB + ".tmp"
-    _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", tmp] + srcs)
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    # host-only C++ against the HIP runtime + hipRTC (whole-stage codegen); hipcc supplies the
+    # platform defines and include paths
+    _run([_hipcc(), "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", tmp] + srcs +
+         [f"-L{rocm}/lib", "-lhiprtc", "-lamdhip64", f"-Wl,-rpath,{rocm}/lib"])
     os.replace(tmp, RUNTIME_LIB)
     return RUNTIME_LIB
 

@@ -32,6 +32,7 @@ from ..plan import physical as X
 from ..utils import murmur3
 from ..utils.conf import HyperspaceConf
 from . import compile as CP
+from . import jit
 from .arrow_eval import key
 from .device_cache import DeviceTableCache, load_bucketed_index, load_flat
 from .device_table import DeviceColumn, DeviceTable
@@ -606,7 +607,10 @@ class GpuBackend:
             out = self._empty_agg(len(specs), G)
         else:
             tp = K.ranges_to_tiles(rlen)
-            out = K.scan_agg(p, rstart, rlen, tp)
+            if HyperspaceConf.codegen_enabled(self.session.conf):
+                out = jit.scan_agg(p, rstart, rlen, tp)
+            else:
+                out = K.scan_agg(p, rstart, rlen, tp)
         return (*out, G, gbase, gdict, gtype)
 
     def _empty_agg(self, A, G=1):
@@ -643,7 +647,8 @@ class GpuBackend:
         if keep[0].always_false or keep[1].always_false:
             return (*self._empty_agg(len(specs), G), G, gbase, gdict, gtype)
         max_tiles = K.join_max_tiles(left.table.num_rows, rlen.numel())
-        out = K.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles)
+        run = jit.join_agg if HyperspaceConf.codegen_enabled(self.session.conf) else K.join_agg
+        out = run(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles)
         return (*out, G, gbase, gdict, gtype)
 
 

@@ -1,0 +1,712 @@
+"""Whole-stage code generation for the MI355X executor (hipRTC; ``csrc/runtime/hs_jit.cpp``).
+
+The AOT kernels in ``csrc/kernels`` interpret a predicate/aggregate *description* (``Pred`` /
+``AggSpec`` structs) per row batch.  That keeps one binary for every query, but the compiler
+cannot see which columns a query touches: each predicate is a separate, serialized load round
+trip, and the interpreter's register footprint caps occupancy.  This module emits one
+straight-line HIP kernel per query *shape* instead — exact column types, the CNF as a boolean
+expression, every load visible to the scheduler so all predicate columns of a row batch are in
+flight at once — and compiles it with hipRTC for gfx950.  Literals (filter constants, affine
+coefficients, IN-set pointers) are kernel arguments, so a shape compiles once and every later
+query of that shape (e.g. TPC-H Q6 with new dates) reuses the code object.
+
+The generated kernels write the same per-block partials as the AOT ones and share the AOT
+deterministic final reduction (``hs_agg_final``), and the join kernel reuses the AOT per-tile span
+search (``hs_join_spans_kernel``): codegen only replaces the per-row inner loops.
+
+Kernel arguments are one by-value struct whose fields are all 8 bytes wide, packed here with
+``struct``; the runtime passes it with ``HIP_LAUNCH_PARAM_BUFFER_POINTER``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import struct
+import threading
+from typing import Dict, List, Optional, Tuple
+
+from ..ops import _lib as NL
+
+ARCH = os.environ.get("HS_OFFLOAD_ARCH", "gfx950")
+_HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RUNTIME_PATH = os.path.join(_HERE, "_native", "libhs_runtime.so")
+# in-tree cache travels with the repo snapshot; override with HS_JIT_CACHE
+CACHE_DIR = os.environ.get("HS_JIT_CACHE", os.path.join(_HERE, "_native", "jitcache"))
+
+BLOCK = 256
+SCAN_ITEMS = 8
+JOIN_ITEMS = 4
+JOIN_LDS_KEYS = 2048
+
+_CTYPE = {NL.I8: "signed char", NL.I16: "short", NL.I32: "int", NL.I64: "long long",
+          NL.F32: "float", NL.F64: "double", NL.BOOL: "unsigned char", NL.U32: "unsigned int",
+          NL.U64: "unsigned long long"}
+_OPSTR = {NL.OP_EQ: "==", NL.OP_NE: "!=", NL.OP_LT: "<", NL.OP_LE: "<=", NL.OP_GT: ">",
+          NL.OP_GE: ">="}
+
+_rt = None
+_rt_lock = threading.Lock()
+
+
+def runtime():
+    global _rt
+    if _rt is None:
+        with _rt_lock:
+            if _rt is None:
+                if not os.path.exists(RUNTIME_PATH):
+                    raise RuntimeError(f"{RUNTIME_PATH} missing: run python -m hyperspace_amd._native.build")
+                L = C.CDLL(RUNTIME_PATH)
+                L.hs_jit_get.restype = C.c_void_p
+                L.hs_jit_get.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
+                                         C.POINTER(C.c_int)]
+                L.hs_jit_launch.restype = C.c_int
+                L.hs_jit_launch.argtypes = [C.c_void_p, C.c_uint, C.c_uint, C.c_uint, C.c_void_p,
+                                            C.c_void_p, C.c_size_t]
+                L.hs_jit_compile_to_cache.restype = C.c_int
+                L.hs_jit_compile_to_cache.argtypes = [C.c_char_p] * 4
+                L.hs_jit_last_error.restype = C.c_char_p
+                _rt = L
+    return _rt
+
+
+# ------------------------------------------------------------------------------------------------
+# Argument struct
+# ------------------------------------------------------------------------------------------------
+class Args:
+    """Ordered 8-byte kernel argument slots: ('p'|'q'|'d', name, C type)."""
+
+    def __init__(self):
+        self.slots: List[Tuple[str, str, str]] = []
+        self._index: Dict[str, int] = {}
+
+    def add(self, kind: str, name: str, ctype: str) -> str:
+        if name not in self._index:
+            self._index[name] = len(self.slots)
+            self.slots.append((kind, name, ctype))
+        return f"a.{name}"
+
+    def struct_src(self) -> str:
+        body = "".join(f"  {ct} {n};\n" for _, n, ct in self.slots)
+        return "struct Args {\n" + body + "};\n"
+
+    def pack(self, values: Dict[str, object]) -> bytes:
+        fmt = "<" + "".join("q" if k in ("p", "q") else "d" for k, _, _ in self.slots)
+        vals = []
+        for k, n, _ in self.slots:
+            v = values[n]
+            vals.append(float(v) if k == "d" else int(v or 0))
+        return struct.pack(fmt, *vals)
+
+
+class Kernel:
+    def __init__(self, src: str, name: str, args: Args, lds_bytes: int = 0):
+        self.src = src
+        self.name = name
+        self.args = args
+        self.lds_bytes = lds_bytes
+        self._fn = None
+
+    def function(self):
+        if self._fn is None:
+            L = runtime()
+            compiled = C.c_int(0)
+            fn = L.hs_jit_get(self.src.encode(), self.name.encode(), ARCH.encode(),
+                              CACHE_DIR.encode(), C.byref(compiled))
+            if not fn:
+                raise RuntimeError(f"JIT compile/load failed: {L.hs_jit_last_error().decode()}")
+            self._fn = fn
+        return self._fn
+
+    def launch(self, grid: int, values: Dict[str, object], stream_ptr: int, shmem: int = 0) -> None:
+        buf = self.args.pack(values)
+        cbuf = C.create_string_buffer(buf, len(buf))
+        rc = runtime().hs_jit_launch(self.function(), grid, BLOCK, shmem or self.lds_bytes,
+                                     stream_ptr, cbuf, len(buf))
+        if rc != 0:
+            raise RuntimeError(f"JIT launch failed: {runtime().hs_jit_last_error().decode()}")
+
+
+# ------------------------------------------------------------------------------------------------
+# Shared source fragments
+# ------------------------------------------------------------------------------------------------
+_PRELUDE = r"""
+typedef long long i64;
+typedef unsigned long long u64;
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ i64 wsumi(i64 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wmin(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wmax(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ bool in_set(const i64* s, int n, i64 x) {
+  int lo = 0, hi = n;
+  while (lo < hi) { const int m = (lo + hi) >> 1; if (s[m] < x) lo = m + 1; else hi = m; }
+  return lo < n && s[lo] == x;
+}
+__device__ __forceinline__ bool bit_test(const u64* w, i64 nbits, i64 x) {
+  return x >= 0 && x < nbits && ((w[x >> 6] >> (x & 63)) & 1ull);
+}
+__device__ __forceinline__ void lds_min(double* p, double v) {
+  u64* a = (u64*)p; u64 old = *a, as;
+  do { as = old; if (__longlong_as_double((i64)as) <= v) break;
+       old = atomicCAS(a, as, (u64)__double_as_longlong(v)); } while (as != old);
+}
+__device__ __forceinline__ void lds_max(double* p, double v) {
+  u64* a = (u64*)p; u64 old = *a, as;
+  do { as = old; if (__longlong_as_double((i64)as) >= v) break;
+       old = atomicCAS(a, as, (u64)__double_as_longlong(v)); } while (as != old);
+}
+"""
+
+
+def _ident(kind: int) -> str:
+    return "__builtin_inf()" if kind == NL.AK_MIN else (
+        "-__builtin_inf()" if kind == NL.AK_MAX else "0.0")
+
+
+class _Gen:
+    """Expression builder over column slots of one or two row variables."""
+
+    def __init__(self, args: Args, cols: Dict[int, Tuple[int, bool]], split: int,
+                 rows: Tuple[str, str]):
+        self.a = args
+        self.cols = cols          # slot -> (hs_type, has_valid)
+        self.split = split
+        self.rows = rows          # row variable for slot < split / >= split
+
+    def row(self, slot: int) -> str:
+        return self.rows[1] if slot >= self.split else self.rows[0]
+
+    def ptr(self, slot: int) -> str:
+        t, _ = self.cols[slot]
+        return self.a.add("p", f"c{slot}", f"const {_CTYPE[t]}*")
+
+    def vptr(self, slot: int) -> Optional[str]:
+        _, hv = self.cols[slot]
+        return self.a.add("p", f"v{slot}", "const unsigned char*") if hv else None
+
+    def val(self, slot: int) -> str:
+        return f"x{slot}"
+
+    def ok(self, slot: int) -> str:
+        return f"n{slot}" if self.cols[slot][1] else "true"
+
+    def load(self, slot: int, guard: str, out: List[str], ind: str) -> None:
+        t, hv = self.cols[slot]
+        ct = _CTYPE[t]
+        r = self.row(slot)
+        out.append(f"{ind}const {ct} x{slot} = ({guard}) ? {self.ptr(slot)}[{r}] : ({ct})0;")
+        if hv:
+            out.append(f"{ind}const bool n{slot} = ({guard}) && {self.vptr(slot)}[{r}] != 0;")
+
+    def leaf(self, k: int, p: NL.Pred) -> str:
+        kind, op = p.kind, p.op
+        if kind == NL.PK_TRUE:
+            return "true"
+        c = p.col
+        if kind == NL.PK_IS_NULL:
+            return f"(!{self.ok(c)})"
+        if kind == NL.PK_NOT_NULL:
+            return f"({self.ok(c)})"
+        if kind == NL.PK_INT_LIT:
+            lit = self.a.add("q", f"L{k}", "long long")
+            return f"({self.ok(c)} && ((i64)x{c} {_OPSTR[op]} {lit}))"
+        if kind == NL.PK_FLT_LIT:
+            lit = self.a.add("d", f"F{k}", "double")
+            return f"({self.ok(c)} && ((double)x{c} {_OPSTR[op]} {lit}))"
+        if kind in (NL.PK_INT_COL, NL.PK_FLT_COL):
+            c2 = p.col2
+            cast = "i64" if kind == NL.PK_INT_COL else "double"
+            return (f"({self.ok(c)} && {self.ok(c2)} && "
+                    f"(({cast})x{c} {_OPSTR[op]} ({cast})x{c2}))")
+        if kind == NL.PK_IN_SET:
+            sp = self.a.add("p", f"S{k}", "const long long*")
+            sn = self.a.add("q", f"N{k}", "long long")
+            neg = "" if op == NL.OP_EQ else "!"
+            return f"({self.ok(c)} && {neg}in_set({sp}, (int){sn}, (i64)x{c}))"
+        if kind == NL.PK_BITMAP:
+            sp = self.a.add("p", f"S{k}", "const unsigned long long*")
+            sn = self.a.add("q", f"N{k}", "long long")
+            neg = "" if op == NL.OP_EQ else "!"
+            return f"({self.ok(c)} && {neg}bit_test({sp}, {sn} * 64, (i64)x{c}))"
+        raise ValueError(f"pred kind {kind}")
+
+    def cnf(self, preds: List[Tuple[int, NL.Pred]]) -> str:
+        if not preds:
+            return "true"
+        groups: Dict[int, List[str]] = {}
+        order: List[int] = []
+        for k, p in preds:
+            if p.group not in groups:
+                groups[p.group] = []
+                order.append(p.group)
+            groups[p.group].append(self.leaf(k, p))
+        return " && ".join("(" + " || ".join(groups[g]) + ")" for g in order)
+
+    def agg_value(self, i: int, a: NL.AggSpec) -> Tuple[str, str]:
+        """(value expr, validity expr) of aggregate i."""
+        if a.kind == NL.AK_COUNT_STAR:
+            return "1.0", "true"
+        terms, oks = [], []
+        for t in range(a.nterms):
+            c = a.col[t]
+            al = self.a.add("d", f"A{i}_{t}", "double")
+            be = self.a.add("d", f"B{i}_{t}", "double")
+            terms.append(f"({al} + {be} * (double)x{c})")
+            if self.cols[c][1]:
+                oks.append(f"n{c}")
+        return " * ".join(terms) or "1.0", " && ".join(oks) or "true"
+
+
+def _pred_slots(preds) -> List[int]:
+    s = []
+    for _, p in preds:
+        if p.kind == NL.PK_TRUE:
+            continue
+        s.append(p.col)
+        if p.kind in (NL.PK_INT_COL, NL.PK_FLT_COL):
+            s.append(p.col2)
+    return list(dict.fromkeys(s))
+
+
+def _agg_slots(aggs) -> List[int]:
+    s = []
+    for a in aggs:
+        if a.kind != NL.AK_COUNT_STAR:
+            s += [a.col[t] for t in range(a.nterms)]
+    return list(dict.fromkeys(s))
+
+
+def _accumulate(gen: _Gen, aggs, grouped: bool, pass_var: str, gvar: str, ind: str) -> List[str]:
+    out = []
+    for i, a in enumerate(aggs):
+        v, ok = gen.agg_value(i, a)
+        out.append(f"{ind}{{ const bool ok = {pass_var} && {ok}; const double v = ok ? {v} : 0.0;")
+        if not grouped:
+            if a.kind == NL.AK_MIN:
+                out.append(f"{ind}  if (ok) {{ acc{i} = fmin(acc{i}, v); cnt{i} += 1u; }} }}")
+            elif a.kind == NL.AK_MAX:
+                out.append(f"{ind}  if (ok) {{ acc{i} = fmax(acc{i}, v); cnt{i} += 1u; }} }}")
+            else:
+                out.append(f"{ind}  if (ok) {{ acc{i} += v; cnt{i} += 1u; }} }}")
+            continue
+        # wave-peeled grouped accumulation into LDS (one atomic per distinct group per wave)
+        out.append(f"{ind}  bool todo = ok;")
+        out.append(f"{ind}  while (true) {{")
+        out.append(f"{ind}    const u64 act = __ballot(todo); if (act == 0ull) break;")
+        out.append(f"{ind}    const int ld = __ffsll((unsigned long long)act) - 1;")
+        out.append(f"{ind}    const int g0 = __shfl({gvar}, ld, 64);")
+        out.append(f"{ind}    const bool mine = todo && {gvar} == g0;")
+        out.append(f"{ind}    const u64 cm = __ballot(mine);")
+        if a.kind == NL.AK_MIN:
+            out.append(f"{ind}    const double r = wmin(mine ? v : __builtin_inf());")
+        elif a.kind == NL.AK_MAX:
+            out.append(f"{ind}    const double r = wmax(mine ? v : -__builtin_inf());")
+        else:
+            out.append(f"{ind}    const double r = wsum(mine ? v : 0.0);")
+        out.append(f"{ind}    if ((int)(threadIdx.x & 63) == ld) {{")
+        out.append(f"{ind}      const int s = g0 * NA + {i};")
+        if a.kind == NL.AK_MIN:
+            out.append(f"{ind}      lds_min(&gmn[s], r);")
+        elif a.kind == NL.AK_MAX:
+            out.append(f"{ind}      lds_max(&gmx[s], r);")
+        else:
+            out.append(f"{ind}      atomicAdd(&gsum[s], r);")
+        out.append(f"{ind}      atomicAdd(&gcnt[s], (unsigned long long)__popcll(cm));")
+        out.append(f"{ind}    }}")
+        out.append(f"{ind}    todo = todo && !mine;")
+        out.append(f"{ind}  }} }}")
+    return out
+
+
+def _acc_decls(aggs, grouped: bool, args: Args) -> List[str]:
+    out = [f"  constexpr int NA = {len(aggs)};"]
+    if grouped:
+        out += ["  extern __shared__ __attribute__((aligned(16))) double glds[];",
+                "  const int GA = (int)a.num_groups * NA;",
+                "  double* gsum = glds; double* gmn = glds + GA; double* gmx = glds + 2 * GA;",
+                "  unsigned long long* gcnt = (unsigned long long*)(glds + 3 * GA);",
+                "  for (int i = threadIdx.x; i < GA; i += blockDim.x) {",
+                "    gsum[i] = 0.0; gmn[i] = __builtin_inf(); gmx[i] = -__builtin_inf(); gcnt[i] = 0ull; }",
+                "  __syncthreads();"]
+        args.add("q", "num_groups", "long long")
+        args.add("q", "group_base", "long long")
+    else:
+        for i, a in enumerate(aggs):
+            out.append(f"  double acc{i} = {_ident(a.kind)}; unsigned cnt{i} = 0u;")
+    return out
+
+
+def _flush(aggs, grouped: bool) -> List[str]:
+    out = []
+    if grouped:
+        out += ["  __syncthreads();",
+                "  for (int i = threadIdx.x; i < GA; i += blockDim.x) {",
+                "    const i64 o = (i64)blockIdx.x * GA + i;",
+                "    a.psum[o] = gsum[i]; a.pcnt[o] = (i64)gcnt[i]; a.pmin[o] = gmn[i]; a.pmax[o] = gmx[i];",
+                "  }"]
+        return out
+    out += [f"  __shared__ double rv[{BLOCK // 64}][NA]; __shared__ i64 rc[{BLOCK // 64}][NA];",
+            "  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;"]
+    for i, a in enumerate(aggs):
+        red = "wmin" if a.kind == NL.AK_MIN else ("wmax" if a.kind == NL.AK_MAX else "wsum")
+        out.append(f"  {{ const double r = {red}(acc{i}); const i64 c = wsumi((i64)cnt{i});"
+                   f" if (lane == 0) {{ rv[w][{i}] = r; rc[w][{i}] = c; }} }}")
+    out.append("  __syncthreads();")
+    out.append("  if (threadIdx.x == 0) {")
+    for i, a in enumerate(aggs):
+        comb = "fmin(t, rv[k][{i}])" if a.kind == NL.AK_MIN else (
+            "fmax(t, rv[k][{i}])" if a.kind == NL.AK_MAX else "t + rv[k][{i}]")
+        comb = comb.format(i=i)
+        out.append(f"    {{ double t = {_ident(a.kind)}; i64 c = 0;")
+        out.append(f"      for (int k = 0; k < {BLOCK // 64}; ++k) {{ t = {comb}; c += rc[k][{i}]; }}")
+        out.append(f"      const i64 o = (i64)blockIdx.x * NA + {i};")
+        is_mm = a.kind in (NL.AK_MIN, NL.AK_MAX)
+        out.append(f"      a.psum[o] = {'0.0' if is_mm else 't'}; a.pcnt[o] = c;")
+        out.append(f"      a.pmin[o] = {'t' if a.kind == NL.AK_MIN else '__builtin_inf()'};"
+                   f" a.pmax[o] = {'t' if a.kind == NL.AK_MAX else '-__builtin_inf()'}; }}")
+    out.append("  }")
+    return out
+
+
+def _common_args(args: Args) -> None:
+    for n in ("psum", "pmin", "pmax"):
+        args.add("p", n, "double*")
+    args.add("p", "pcnt", "long long*")
+
+
+# ------------------------------------------------------------------------------------------------
+# Scan + filter + aggregate
+# ------------------------------------------------------------------------------------------------
+def scan_agg_shape(p: NL.ScanParams) -> tuple:
+    cols = tuple((s, p.cols[s].type, bool(p.cols[s].valid)) for s in range(NL.MAX_COLS)
+                 if p.cols[s].data)
+    preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
+                   p.preds[k].group) for k in range(p.npreds))
+    aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
+                 for i in range(p.naggs))
+    return ("scan_agg", cols, preds, aggs, p.group_col)
+
+
+def gen_scan_agg(p: NL.ScanParams) -> Kernel:
+    args = Args()
+    for n, ct in (("rstart", "const long long*"), ("rlen", "const long long*"),
+                  ("tile_prefix", "const long long*")):
+        args.add("p", n, ct)
+    args.add("q", "R", "long long")
+    _common_args(args)
+    cols = {s: (p.cols[s].type, bool(p.cols[s].valid)) for s in range(NL.MAX_COLS)
+            if p.cols[s].data}
+    gen = _Gen(args, cols, NL.MAX_COLS, ("row", "row"))
+    preds = [(k, p.preds[k]) for k in range(p.npreds)]
+    aggs = [p.aggs[i] for i in range(p.naggs)]
+    grouped = p.group_col >= 0
+    pslots = _pred_slots(preds)
+    aslots = [s for s in _agg_slots(aggs) if s not in pslots]
+    if grouped and p.group_col not in pslots and p.group_col not in aslots:
+        aslots.append(p.group_col)
+    T = BLOCK * SCAN_ITEMS
+    b: List[str] = []
+    b += _acc_decls(aggs, grouped, args)
+    b += ["  const i64 ntiles = a.tile_prefix[a.R];",
+          "  const i64 per = (ntiles + gridDim.x - 1) / gridDim.x;",
+          "  const i64 t0 = (i64)blockIdx.x * per;",
+          "  const i64 t1 = ntiles < t0 + per ? ntiles : t0 + per;",
+          "  int r = 0;",
+          "  if (t0 < t1) { int lo = 0, hi = (int)a.R;",
+          "    while (hi - lo > 1) { const int m = (lo + hi) >> 1; if (a.tile_prefix[m] <= t0) lo = m; else hi = m; }",
+          "    r = lo; }",
+          "  for (i64 t = t0; t < t1; ++t) {",
+          "    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;",
+          f"    const i64 off = (t - a.tile_prefix[r]) * {T};",
+          "    const i64 row0 = a.rstart[r] + off;",
+          f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};",
+          "#pragma unroll",
+          f"    for (int it = 0; it < {SCAN_ITEMS}; ++it) {{",
+          f"      const i64 k = (i64)it * {BLOCK} + threadIdx.x;",
+          "      const bool act = k < rows;",
+          "      const i64 row = row0 + (act ? k : 0);"]
+    ind = "      "
+    for s in pslots:
+        gen.load(s, "act", b, ind)
+    b.append(f"{ind}bool pass = act && {gen.cnf(preds)};")
+    for s in aslots:
+        gen.load(s, "pass", b, ind)
+    gvar = "gi"
+    if grouped:
+        g = p.group_col
+        base = args.add("q", "group_base", "long long")
+        ng = args.add("q", "num_groups", "long long")
+        b.append(f"{ind}const i64 gl = (i64)x{g} - {base};")
+        b.append(f"{ind}pass = pass && {gen.ok(g)} && gl >= 0 && gl < {ng};")
+        b.append(f"{ind}const int {gvar} = pass ? (int)gl : 0;")
+    b += _accumulate(gen, aggs, grouped, "pass", gvar, ind)
+    b += ["    }", "  }"]
+    b += _flush(aggs, grouped)
+    src = (_PRELUDE + args.struct_src() +
+           f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_scan_agg(Args a) {{\n' +
+           "\n".join(b) + "\n}\n")
+    lds = (len(aggs) * p.num_groups * 32) if grouped else 0
+    return Kernel(src, "hs_jit_scan_agg", args, lds)
+
+
+def scan_agg_values(p: NL.ScanParams, rstart, rlen, tile_prefix, parts) -> Dict[str, object]:
+    v = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tile_prefix.data_ptr(),
+         "R": rstart.numel(), "psum": parts[0].data_ptr(), "pcnt": parts[1].data_ptr(),
+         "pmin": parts[2].data_ptr(), "pmax": parts[3].data_ptr(),
+         "num_groups": p.num_groups, "group_base": p.group_base}
+    _fill_common(v, p.cols, [(k, p.preds[k]) for k in range(p.npreds)],
+                 [p.aggs[i] for i in range(p.naggs)])
+    return v
+
+
+def _fill_common(v: Dict[str, object], cols, preds, aggs) -> None:
+    for s in range(NL.MAX_COLS):
+        if cols[s].data:
+            v[f"c{s}"] = cols[s].data
+            v[f"v{s}"] = cols[s].valid or 0
+    for k, p in preds:
+        v[f"L{k}"] = p.ilit
+        v[f"F{k}"] = p.flit
+        v[f"S{k}"] = p.set or 0
+        v[f"N{k}"] = p.set_len
+    for i, a in enumerate(aggs):
+        for t in range(a.nterms):
+            v[f"A{i}_{t}"] = a.alpha[t]
+            v[f"B{i}_{t}"] = a.beta[t]
+
+
+# ------------------------------------------------------------------------------------------------
+# Co-located join + aggregate
+# ------------------------------------------------------------------------------------------------
+def join_agg_shape(p: NL.JoinParams) -> tuple:
+    cols = tuple((s, p.cols[s].type, bool(p.cols[s].valid)) for s in range(NL.MAX_COLS)
+                 if p.cols[s].data)
+    preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
+                   p.preds[k].group) for k in range(p.npreds))
+    aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
+                 for i in range(p.naggs))
+    return ("join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey, p.key_is_float)
+
+
+def _key_expr(var: str, is_float: bool) -> str:
+    if is_float:
+        return (f"({{ double d_ = (double){var}; d_ = d_ == 0.0 ? 0.0 : d_; "
+                f"const u64 b_ = (u64)__double_as_longlong(d_); "
+                f"(b_ & 0x8000000000000000ull) ? ~b_ : (b_ | 0x8000000000000000ull); }})")
+    return f"((u64)(i64){var} ^ 0x8000000000000000ull)"
+
+
+def gen_join_agg(p: NL.JoinParams) -> Kernel:
+    args = Args()
+    args.add("p", "tile_prefix", "const long long*")
+    args.add("q", "R", "long long")
+    args.add("p", "spans", "const long long*")
+    _common_args(args)
+    cols = {s: (p.cols[s].type, bool(p.cols[s].valid)) for s in range(NL.MAX_COLS)
+            if p.cols[s].data}
+    split = 8
+    gen = _Gen(args, cols, split, ("lrow", "j"))
+    lpreds = [(k, p.preds[k]) for k in range(p.nlp)]
+    rpreds = [(k, p.preds[k]) for k in range(p.nlp, p.npreds)]
+    aggs = [p.aggs[i] for i in range(p.naggs)]
+    grouped = p.group_col >= 0
+    fl = bool(p.key_is_float)
+    lk, rk = p.lkey, p.rkey
+    lslots = [s for s in _pred_slots(lpreds) if s < split]
+    lslots = list(dict.fromkeys([lk] + lslots))
+    rslots = [s for s in _pred_slots(rpreds) if s >= split]
+    lpost = [s for s in _pred_slots(rpreds) if s < split and s not in lslots]
+    aslots = [s for s in _agg_slots(aggs) if s not in lslots + rslots + lpost]
+    if grouped and p.group_col not in lslots + rslots + lpost + aslots:
+        aslots.append(p.group_col)
+    NI = JOIN_ITEMS
+    T = BLOCK * NI
+    rkt = _CTYPE[cols[rk][0]]
+    b: List[str] = []
+    b += _acc_decls(aggs, grouped, args)
+    b += [f"  __shared__ u64 skeys[{JOIN_LDS_KEYS}];",
+          "  const i64 ntiles = a.tile_prefix[a.R];",
+          "  const i64 per = (ntiles + gridDim.x - 1) / gridDim.x;",
+          "  const i64 t0 = (i64)blockIdx.x * per;",
+          "  const i64 t1 = ntiles < t0 + per ? ntiles : t0 + per;",
+          "  for (i64 t = t0; t < t1; ++t) {",
+          "    const i64 row0 = a.spans[4 * t], rows = a.spans[4 * t + 1];",
+          "    const i64 rs = a.spans[4 * t + 2], re = a.spans[4 * t + 3];",
+          f"    const bool staged = re - rs <= {JOIN_LDS_KEYS};"]
+    # left batch loads first (independent of the LDS stage)
+    for it in range(NI):
+        b.append(f"    const i64 lr{it} = row0 + {it * BLOCK} + threadIdx.x;")
+        b.append(f"    const bool la{it} = {it * BLOCK} + (i64)threadIdx.x < rows;")
+    ind = "    "
+    for it in range(NI):
+        g2 = _Gen(args, cols, split, (f"lr{it}", "j"))
+        blk: List[str] = []
+        for s in lslots:
+            g2.load(s, f"la{it}", blk, ind)
+        b += [_rename(x, lslots, it) for x in blk]
+        cond = _rename(g2.cnf(lpreds), lslots, it)
+        okk = _rename(gen.ok(lk), [lk], it) if cols[lk][1] else "true"
+        b.append(f"{ind}bool m{it} = la{it} && {okk} && {cond};")
+        b.append(f"{ind}const u64 k{it} = {_key_expr(f'x{lk}_{it}', fl)};")
+    # stage right keys
+    b += ["    if (staged) {",
+          f"      for (i64 q = threadIdx.x; q < re - rs; q += {BLOCK})",
+          f"        skeys[q] = {_key_expr(f'{gen.ptr(rk)}[rs + q]', fl)};",
+          "    }",
+          "    __syncthreads();"]
+    # probe: first match per row
+    for it in range(NI):
+        b += [f"    i64 j{it} = rs;",
+              f"    if (m{it}) {{",
+              "      if (staged) { i64 lo = 0, hi = re - rs;",
+              f"        while (lo < hi) {{ const i64 md = (lo + hi) >> 1; if (skeys[md] < k{it}) lo = md + 1; else hi = md; }}",
+              f"        j{it} = rs + lo; m{it} = j{it} < re && skeys[lo] == k{it};",
+              "      } else { i64 lo = rs, hi = re;",
+              f"        while (lo < hi) {{ const i64 md = (lo + hi) >> 1; const bool nv = {_valid_expr(gen, rk, 'md')};",
+              f"          if (nv || {_key_expr(f'{gen.ptr(rk)}[md]', fl)} < k{it}) lo = md + 1; else hi = md; }}",
+              f"        j{it} = lo; m{it} = lo < re && {_key_expr(f'{gen.ptr(rk)}[lo]', fl)} == k{it}; }}",
+              "    }"]
+    # match rounds
+    anym = " || ".join(f"m{it}" for it in range(NI))
+    b.append(f"    while (__any({anym})) {{")
+    for it in range(NI):
+        g2 = _Gen(args, cols, split, (f"lr{it}", f"j{it}"))
+        blk = []
+        for s in rslots:
+            g2.load(s, f"m{it}", blk, "      ")
+        for s in lpost:
+            g2.load(s, f"m{it}", blk, "      ")
+        b += [_rename(x, rslots + lpost + lslots, it) for x in blk]
+        cond = _rename(g2.cnf(rpreds), rslots + lpost + lslots, it)
+        b.append(f"      bool ps{it} = m{it} && {cond};")
+        blk = []
+        for s in aslots:
+            g2.load(s, f"ps{it}", blk, "      ")
+        b += [_rename(x, aslots, it) for x in blk]
+        allslots = lslots + rslots + lpost + aslots
+        gvar = f"gi{it}"
+        if grouped:
+            g = p.group_col
+            base = args.add("q", "group_base", "long long")
+            ng = args.add("q", "num_groups", "long long")
+            b.append(f"      const i64 gl{it} = (i64)x{g}_{it} - {base};")
+            okg = f"n{g}_{it}" if cols[g][1] else "true"
+            b.append(f"      ps{it} = ps{it} && {okg} && gl{it} >= 0 && gl{it} < {ng};")
+            b.append(f"      const int {gvar} = ps{it} ? (int)gl{it} : 0;")
+        acc = _accumulate(g2, aggs, grouped, f"ps{it}", gvar, "      ")
+        b += [_rename(x, allslots, it) for x in acc]
+        b += [f"      if (m{it}) {{ ++j{it};",
+              f"        m{it} = j{it} < re && (staged ? skeys[j{it} - rs] : "
+              f"{_key_expr(f'{gen.ptr(rk)}[j{it}]', fl)}) == k{it}; }}"]
+    b += ["    }", "    __syncthreads();", "  }"]
+    b += _flush(aggs, grouped)
+    src = (_PRELUDE + args.struct_src() +
+           f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_join_agg(Args a) {{\n' +
+           "\n".join(b) + "\n}\n")
+    lds = (len(aggs) * p.num_groups * 32) if grouped else 0
+    return Kernel(src, "hs_jit_join_agg", args, lds)
+
+
+def _valid_expr(gen: _Gen, slot: int, row: str) -> str:
+    vp = gen.vptr(slot)
+    return f"({vp}[{row}] == 0)" if vp else "false"
+
+
+def _rename(line: str, slots, it: int) -> str:
+    """Suffix per-row-slot variables x<s>/n<s> with the batch item index."""
+    import re
+    for s in sorted(set(slots), reverse=True):
+        line = re.sub(rf"\b([xn]){s}\b", rf"\g<1>{s}_{it}", line)
+    return line
+
+
+def join_agg_values(p: NL.JoinParams, tile_prefix, spans, parts) -> Dict[str, object]:
+    v = {"tile_prefix": tile_prefix.data_ptr(), "R": tile_prefix.numel() - 1,
+         "spans": spans.data_ptr(), "psum": parts[0].data_ptr(), "pcnt": parts[1].data_ptr(),
+         "pmin": parts[2].data_ptr(), "pmax": parts[3].data_ptr(),
+         "num_groups": p.num_groups, "group_base": p.group_base}
+    _fill_common(v, p.cols, [(k, p.preds[k]) for k in range(p.npreds)],
+                 [p.aggs[i] for i in range(p.naggs)])
+    return v
+
+
+# ------------------------------------------------------------------------------------------------
+# Shape cache
+# ------------------------------------------------------------------------------------------------
+_KERNELS: Dict[tuple, Kernel] = {}
+
+
+def kernel_for(shape: tuple, make) -> Kernel:
+    k = _KERNELS.get(shape)
+    if k is None:
+        k = make()
+        _KERNELS[shape] = k
+    return k
+
+
+# ------------------------------------------------------------------------------------------------
+# Entry points (same outputs as ops.kernels.scan_agg / join_agg)
+# ------------------------------------------------------------------------------------------------
+def _partials(grid: int, GA: int, dev):
+    import torch
+    return (torch.empty(grid * GA, dtype=torch.float64, device=dev),
+            torch.empty(grid * GA, dtype=torch.int64, device=dev),
+            torch.empty(grid * GA, dtype=torch.float64, device=dev),
+            torch.empty(grid * GA, dtype=torch.float64, device=dev))
+
+
+def _final(parts, grid: int, GA: int, dev):
+    import torch
+    out = (torch.empty(GA, dtype=torch.float64, device=dev),
+           torch.empty(GA, dtype=torch.int64, device=dev),
+           torch.empty(GA, dtype=torch.float64, device=dev),
+           torch.empty(GA, dtype=torch.float64, device=dev))
+    NL.check(NL.lib().hs_agg_final(NL.ptr(parts[0]), NL.ptr(parts[1]), NL.ptr(parts[2]),
+                                   NL.ptr(parts[3]), grid, GA, NL.ptr(out[0]), NL.ptr(out[1]),
+                                   NL.ptr(out[2]), NL.ptr(out[3]), NL.stream_ptr()),
+             "hs_agg_final")
+    return out
+
+
+def scan_agg(p: NL.ScanParams, rstart, rlen, tile_prefix):
+    grid = NL.lib().hs_scan_grid()
+    GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
+    k = kernel_for(scan_agg_shape(p), lambda: gen_scan_agg(p))
+    parts = _partials(grid, GA, rstart.device)
+    k.launch(grid, scan_agg_values(p, rstart, rlen, tile_prefix, parts), NL.stream_ptr(),
+             GA * 32 if p.group_col >= 0 else 0)
+    return _final(parts, grid, GA, rstart.device)
+
+
+def join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, max_tiles: int):
+    import torch
+    from ..ops import kernels as K
+    L = NL.lib()
+    grid = L.hs_scan_grid()
+    GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
+    dev = rstart.device
+    tp = K.ranges_to_tiles(rlen, L.hs_join_tile_rows())
+    spans = torch.empty(4 * max(max_tiles, 1), dtype=torch.int64, device=dev)
+    NL.check(L.hs_join_spans(C.byref(p), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
+                             NL.ptr(roff), rstart.numel(), NL.ptr(tp), int(max_tiles),
+                             NL.ptr(spans), NL.stream_ptr()), "hs_join_spans")
+    k = kernel_for(join_agg_shape(p), lambda: gen_join_agg(p))
+    parts = _partials(grid, GA, dev)
+    k.launch(grid, join_agg_values(p, tp, spans, parts), NL.stream_ptr(),
+             GA * 32 if p.group_col >= 0 else 0)
+    return _final(parts, grid, GA, dev)

@@ -92,4 +92,7 @@ INDEX_ROW_GROUP_ROWS_DEFAULT = "1048576"
 HIPGRAPH_ENABLED = "spark.hyperspace.mi.hipGraph.enabled"
 HIPGRAPH_ENABLED_DEFAULT = "true"
 # Fault-injection hook for action crash tests: after_begin | mid_op | before_end.
+# whole-stage code generation (hipRTC) for the fused scan/join aggregate kernels
+CODEGEN_ENABLED = "spark.hyperspace.mi.codegen.enabled"
+CODEGEN_ENABLED_DEFAULT = "true"
 FAULT_INJECTION = "spark.hyperspace.mi.faultInjection"

@@ -112,3 +112,7 @@ class HyperspaceConf:
     @staticmethod
     def hipgraph_enabled(conf) -> bool:
         return _b(conf.get(C.HIPGRAPH_ENABLED, C.HIPGRAPH_ENABLED_DEFAULT))
+
+    @staticmethod
+    def codegen_enabled(conf) -> bool:
+        return _b(conf.get(C.CODEGEN_ENABLED, C.CODEGEN_ENABLED_DEFAULT))
