@@ -324,7 +324,7 @@ def _accumulate(gen: _Gen, aggs, grouped: bool, pass_var: str, gvar: str, ind: s
             out.append(f"{ind}      lds_min(&gmn[s], r);")
         elif a.kind == NL.AK_MAX:
             out.append(f"{ind}      lds_max(&gmx[s], r);")
-        else:
+        elif a.kind == NL.AK_SUM:
             out.append(f"{ind}      atomicAdd(&gsum[s], r);")
         out.append(f"{ind}      atomicAdd(&gcnt[s], (unsigned long long)__popcll(cm));")
         out.append(f"{ind}    }}")
