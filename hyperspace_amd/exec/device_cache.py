@@ -12,8 +12,6 @@ several files through incremental refresh are re-sorted on the device at load ti
 """
 from __future__ import annotations
 
-import concurrent.futures as cf
-import os
 import threading
 from collections import OrderedDict
 from typing import Dict, List, Optional
@@ -25,31 +23,7 @@ import pyarrow.parquet as pq
 
 from ..io.writer import get_bucket_id
 from ..utils import path_utils as P
-from .device_table import DeviceColumn, DeviceTable, h2d, is_string
-
-_POOL = None
-
-
-def _pool():
-    global _POOL
-    if _POOL is None:
-        _POOL = cf.ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4))
-    return _POOL
-
-
-def read_parquet_columns(paths: List[str], columns: List[str]) -> List[pa.Table]:
-    def one(p):
-        local = P.to_local(p)
-        avail = pq.read_schema(local).names
-        cols = [c for c in columns if c in avail]
-        t = pq.read_table(local, columns=cols, use_threads=False)
-        for c in columns:
-            if c not in t.column_names:
-                raise KeyError(f"column {c} missing in {p}")
-        return t.select(columns)
-    if len(paths) <= 1:
-        return [one(p) for p in paths]
-    return list(_pool().map(one, paths))
+from .device_table import DeviceColumn, DeviceTable
 
 
 _FILES_KEYS: Dict[int, tuple] = {}
@@ -106,15 +80,6 @@ class DeviceTableCache:
             self._bytes = 0
 
 
-def _dict_encode_tables(tables: List[pa.Table], columns: List[str]) -> Dict[str, pa.Array]:
-    out = {}
-    for c in columns:
-        if tables and is_string(tables[0].schema.field(c).type):
-            u = pc.unique(pa.chunked_array([t.column(c) for t in tables]).combine_chunks().drop_null())
-            out[c] = u.sort()
-    return out
-
-
 def load_bucketed_index(files, columns: List[str], num_buckets: int, sort_cols: List[str], device,
                         rank: int = 0, world: int = 1) -> DeviceTable:
     """Load index files bucket-major for the buckets this rank owns (b % world == rank)."""
@@ -128,22 +93,35 @@ def load_bucketed_index(files, columns: List[str], num_buckets: int, sort_cols: 
         by_bucket.setdefault(b, []).append(f.path)
     owned = [b for b in range(num_buckets) if b % world == rank and b in by_bucket]
     ordered = [(b, p) for b in owned for p in sorted(by_bucket[b])]
-    tables = read_parquet_columns([p for _, p in ordered], columns)
+    paths = [p for _, p in ordered]
     counts = np.zeros(num_buckets, dtype=np.int64)
     multi = False
-    for (b, _), t in zip(ordered, tables):
-        multi = multi or counts[b] > 0
-        counts[b] += t.num_rows
+    if paths:
+        # footers give every file's row count up front, so files stream straight into their
+        # slice of presized HBM columns (staging.upload_files) with no host-side concatenation
+        from . import staging
+        rows = list(staging.io_pool().map(
+            lambda p: pq.ParquetFile(P.to_local(p)).metadata.num_rows, paths))
+        for (b, _), r in zip(ordered, rows):
+            multi = multi or counts[b] > 0
+            counts[b] += r
+        schema = pq.read_schema(P.to_local(paths[0]))
+        schema = pa.schema([schema.field(c) for c in columns])
+
+        def read_file(p):
+            return pq.read_table(P.to_local(p), columns=columns, use_threads=False)
+        up = staging.upload_files(read_file, paths, rows, schema, device)
+        cols = dict(up.columns)
+        for name, chunks in up.host_strings.items():
+            arr = pa.chunked_array(chunks, type=chunks[0].type)
+            d = pc.unique(arr.combine_chunks().drop_null()).sort()
+            cols[name] = DeviceColumn.from_arrow(arr, device, d)
+        cols = {c: cols[c] for c in columns}
     off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
     n = int(off[-1])
-    dicts = _dict_encode_tables(tables, columns)
-    if tables:
-        full = pa.concat_tables(tables)
-    else:
-        full = pa.schema([(c, pa.null()) for c in columns]).empty_table()
-    cols = {c: DeviceColumn.from_arrow(full.column(c), device, dicts.get(c)) for c in columns} if n else \
-        {c: DeviceColumn(torch.empty(0, dtype=torch.int64, device=device), None, pa.int64())
-         for c in columns}
+    if not n:
+        cols = {c: DeviceColumn(torch.empty(0, dtype=torch.int64, device=device), None, pa.int64())
+                for c in columns}
     table = DeviceTable(cols, n, torch.from_numpy(off).to(device), off)
     if multi and n:
         # re-establish (bucket, sort cols) order on the device

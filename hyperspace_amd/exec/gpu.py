@@ -499,10 +499,7 @@ class GpuBackend:
         if d is not None and d.world > 1:
             sums, cnts, mins, maxs = d.all_reduce_agg(sums, cnts, mins, maxs)
         A = len(fns) + 1  # + implicit count(*)
-        s = sums.cpu().numpy().reshape(G, A)
-        c = cnts.cpu().numpy().reshape(G, A)
-        mn = mins.cpu().numpy().reshape(G, A)
-        mx = maxs.cpu().numpy().reshape(G, A)
+        s, c, mn, mx = (x.reshape(G, A) for x in K.agg_to_host(sums, cnts, mins, maxs))
         rows = [g for g in range(G) if c[g, A - 1] > 0] if group is not None else [0]
         vals = {}
         for i, fn in enumerate(fns):

@@ -672,10 +672,8 @@ def _partials(grid: int, GA: int, dev):
 
 def _final(parts, grid: int, GA: int, dev):
     import torch
-    out = (torch.empty(GA, dtype=torch.float64, device=dev),
-           torch.empty(GA, dtype=torch.int64, device=dev),
-           torch.empty(GA, dtype=torch.float64, device=dev),
-           torch.empty(GA, dtype=torch.float64, device=dev))
+    from ..ops import kernels as K
+    out = K.agg_outputs(GA, dev)
     NL.check(NL.lib().hs_agg_final(NL.ptr(parts[0]), NL.ptr(parts[1]), NL.ptr(parts[2]),
                                    NL.ptr(parts[3]), grid, GA, NL.ptr(out[0]), NL.ptr(out[1]),
                                    NL.ptr(out[2]), NL.ptr(out[3]), NL.stream_ptr()),

@@ -230,6 +230,31 @@ def sortable_image(value, hs_type: int) -> int:
     return (int(value) + (1 << (width - 1))) & ((1 << width) - 1)
 
 
+def agg_outputs(GA: int, dev):
+    """(sum f64, count i64, min f64, max f64) [GA] as views of ONE device buffer, so the host
+    reads a query's aggregate result with a single D2H copy (``sum.hs_buf``)."""
+    torch = _torch()
+    buf = torch.empty(32 * max(GA, 1), dtype=torch.uint8, device=dev)
+    n = 8 * GA
+    s = buf[0:n].view(torch.float64)
+    c = buf[n:2 * n].view(torch.int64)
+    mn = buf[2 * n:3 * n].view(torch.float64)
+    mx = buf[3 * n:4 * n].view(torch.float64)
+    s.hs_buf = buf
+    return s, c, mn, mx
+
+
+def agg_to_host(sums, cnts, mins, maxs):
+    """numpy views of the four aggregate outputs with one D2H copy when they share a buffer."""
+    buf = getattr(sums, "hs_buf", None)
+    if buf is None:
+        return sums.cpu().numpy(), cnts.cpu().numpy(), mins.cpu().numpy(), maxs.cpu().numpy()
+    h = buf.cpu().numpy()
+    n = sums.numel() * 8
+    return (h[0:n].view(np.float64), h[n:2 * n].view(np.int64), h[2 * n:3 * n].view(np.float64),
+            h[3 * n:4 * n].view(np.float64))
+
+
 def scan_agg(params: NL.ScanParams, rstart, rlen, tile_prefix, grid: int = None):
     """Returns (sum f64 [GA], count i64 [GA], min f64 [GA], max f64 [GA]) device tensors."""
     torch = _torch()
@@ -241,10 +266,7 @@ def scan_agg(params: NL.ScanParams, rstart, rlen, tile_prefix, grid: int = None)
     pc_ = torch.empty(grid * GA, dtype=torch.int64, device=dev)
     pmn = torch.empty(grid * GA, dtype=torch.float64, device=dev)
     pmx = torch.empty(grid * GA, dtype=torch.float64, device=dev)
-    os_ = torch.empty(GA, dtype=torch.float64, device=dev)
-    oc = torch.empty(GA, dtype=torch.int64, device=dev)
-    omn = torch.empty(GA, dtype=torch.float64, device=dev)
-    omx = torch.empty(GA, dtype=torch.float64, device=dev)
+    os_, oc, omn, omx = agg_outputs(GA, dev)
     NL.check(L.hs_scan_agg(C.byref(params), NL.ptr(rstart), NL.ptr(rlen), rstart.numel(),
                            NL.ptr(tile_prefix), grid, NL.ptr(ps), NL.ptr(pc_), NL.ptr(pmn),
                            NL.ptr(pmx), NL.ptr(os_), NL.ptr(oc), NL.ptr(omn), NL.ptr(omx),
@@ -292,10 +314,7 @@ def join_agg(params: NL.JoinParams, rstart, rlen, rbucket, roff, max_tiles: int,
     pc_ = torch.empty(grid * GA, dtype=torch.int64, device=dev)
     pmn = torch.empty(grid * GA, dtype=torch.float64, device=dev)
     pmx = torch.empty(grid * GA, dtype=torch.float64, device=dev)
-    os_ = torch.empty(GA, dtype=torch.float64, device=dev)
-    oc = torch.empty(GA, dtype=torch.int64, device=dev)
-    omn = torch.empty(GA, dtype=torch.float64, device=dev)
-    omx = torch.empty(GA, dtype=torch.float64, device=dev)
+    os_, oc, omn, omx = agg_outputs(GA, dev)
     spans = torch.empty(4 * max(max_tiles, 1), dtype=torch.int64, device=dev)
     NL.check(L.hs_join_agg(C.byref(params), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
                            NL.ptr(roff), rstart.numel(), NL.ptr(tile_prefix), int(max_tiles),
