@@ -66,13 +66,13 @@ __device__ __forceinline__ int64_t rkey_bound(const ColDesc& c, int64_t lo, int6
 __global__ __launch_bounds__(256) void hs_join_spans_kernel(
     JoinParams p, const int64_t* __restrict__ rstart, const int64_t* __restrict__ rlen,
     const int32_t* __restrict__ rbucket, const int64_t* __restrict__ roff, int R,
-    const int64_t* __restrict__ tile_prefix, int64_t* __restrict__ spans) {
+    const int64_t* __restrict__ tile_prefix, int64_t* __restrict__ spans, int tile_rows) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= tile_prefix[R]) return;
   const int r = tile_range_of(tile_prefix, R, t);
-  const int64_t off = (t - tile_prefix[r]) * JN_TILE;
+  const int64_t off = (t - tile_prefix[r]) * tile_rows;
   const int64_t row0 = rstart[r] + off;
-  const int64_t rows = min((int64_t)JN_TILE, rlen[r] - off);
+  const int64_t rows = min((int64_t)tile_rows, rlen[r] - off);
   const bool fl = p.key_is_float != 0;
   const int b = rbucket[r];
   const int64_t bs = roff[b], be = roff[b + 1];
@@ -344,22 +344,23 @@ __global__ __launch_bounds__(JN_BLOCK) void hs_join_pairs_kernel(
 static int launch_spans(const JoinParams* p, const int64_t* rstart, const int64_t* rlen,
                         const int32_t* rbucket, const int64_t* roff, int R,
                         const int64_t* tile_prefix, int64_t max_tiles, int64_t* spans,
-                        hipStream_t s) {
+                        hipStream_t s, int tile_rows = JN_TILE) {
   if (max_tiles <= 0) return 0;
   const int64_t blocks = (max_tiles + 255) / 256;
   hipLaunchKernelGGL(hs_join_spans_kernel, dim3((unsigned)blocks), dim3(256), 0, s, *p, rstart,
-                     rlen, rbucket, roff, R, tile_prefix, spans);
+                     rlen, rbucket, roff, R, tile_prefix, spans, tile_rows);
   return (int)hipGetLastError();
 }
 
 extern "C" {
 
-// Per-tile (row0, rows, rs, re) only — consumed by the generated join kernels (exec/jit.py).
+// Per-tile (row0, rows, rs, re) only — consumed by the generated join kernels (exec/jit.py),
+// whose tile size is a codegen parameter (tile_prefix must be built with the same tile_rows).
 int hs_join_spans(const JoinParams* p, const int64_t* rstart, const int64_t* rlen,
                   const int32_t* rbucket, const int64_t* roff, int R, const int64_t* tile_prefix,
-                  int64_t max_tiles, int64_t* spans, void* stream) {
+                  int64_t max_tiles, int64_t* spans, int tile_rows, void* stream) {
   return launch_spans(p, rstart, rlen, rbucket, roff, R, tile_prefix, max_tiles, spans,
-                      (hipStream_t)stream);
+                      (hipStream_t)stream, tile_rows);
 }
 
 int hs_join_params_size() { return (int)sizeof(JoinParams); }

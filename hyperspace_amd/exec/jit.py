@@ -34,9 +34,11 @@ RUNTIME_PATH = os.path.join(_HERE, "_native", "libhs_runtime.so")
 CACHE_DIR = os.environ.get("HS_JIT_CACHE", os.path.join(_HERE, "_native", "jitcache"))
 
 BLOCK = 256
-SCAN_ITEMS = 8
-JOIN_ITEMS = 4
-JOIN_LDS_KEYS = 2048
+SCAN_ITEMS = int(os.environ.get("HS_JIT_SCAN_ITEMS", "8"))
+JOIN_ITEMS = int(os.environ.get("HS_JIT_JOIN_ITEMS", "4"))
+JOIN_LDS_KEYS = int(os.environ.get("HS_JIT_JOIN_LDS_KEYS", "2048"))
+SCAN_GRID = int(os.environ.get("HS_JIT_SCAN_GRID", "0"))   # 0: library default (2048)
+JOIN_GRID = int(os.environ.get("HS_JIT_JOIN_GRID", "0"))
 
 _CTYPE = {NL.I8: "signed char", NL.I16: "short", NL.I32: "int", NL.I64: "long long",
           NL.F32: "float", NL.F64: "double", NL.BOOL: "unsigned char", NL.U32: "unsigned int",
@@ -399,7 +401,7 @@ def scan_agg_shape(p: NL.ScanParams) -> tuple:
                    p.preds[k].group) for k in range(p.npreds))
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
-    return ("scan_agg", cols, preds, aggs, p.group_col)
+    return ("scan_agg", cols, preds, aggs, p.group_col, SCAN_ITEMS)
 
 
 def gen_scan_agg(p: NL.ScanParams) -> Kernel:
@@ -500,7 +502,8 @@ def join_agg_shape(p: NL.JoinParams) -> tuple:
                    p.preds[k].group) for k in range(p.npreds))
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
-    return ("join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey, p.key_is_float)
+    return ("join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey, p.key_is_float,
+            JOIN_ITEMS, JOIN_LDS_KEYS)
 
 
 def _key_expr(var: str, is_float: bool) -> str:
@@ -681,8 +684,12 @@ def _final(parts, grid: int, GA: int, dev):
     return out
 
 
-def scan_agg(p: NL.ScanParams, rstart, rlen, tile_prefix):
-    grid = NL.lib().hs_scan_grid()
+def scan_agg(p: NL.ScanParams, rstart, rlen, tile_prefix=None):
+    """``tile_prefix`` must use this kernel's tile (BLOCK * SCAN_ITEMS); None computes it."""
+    from ..ops import kernels as K
+    if tile_prefix is None or BLOCK * SCAN_ITEMS != NL.lib().hs_scan_tile_rows():
+        tile_prefix = K.ranges_to_tiles(rlen, BLOCK * SCAN_ITEMS)
+    grid = SCAN_GRID or NL.lib().hs_scan_grid()
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
     k = kernel_for(scan_agg_shape(p), lambda: gen_scan_agg(p))
     parts = _partials(grid, GA, rstart.device)
@@ -692,17 +699,20 @@ def scan_agg(p: NL.ScanParams, rstart, rlen, tile_prefix):
 
 
 def join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, max_tiles: int):
+    """``max_tiles`` = ``ops.kernels.join_max_tiles`` (AOT tile); rescaled to this kernel's tile."""
     import torch
     from ..ops import kernels as K
     L = NL.lib()
-    grid = L.hs_scan_grid()
+    grid = JOIN_GRID or L.hs_scan_grid()
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
     dev = rstart.device
-    tp = K.ranges_to_tiles(rlen, L.hs_join_tile_rows())
-    spans = torch.empty(4 * max(max_tiles, 1), dtype=torch.int64, device=dev)
+    tile = BLOCK * JOIN_ITEMS
+    tp = K.ranges_to_tiles(rlen, tile)
+    mt = (max_tiles * L.hs_join_tile_rows()) // tile + rlen.numel() + 1
+    spans = torch.empty(4 * mt, dtype=torch.int64, device=dev)
     NL.check(L.hs_join_spans(C.byref(p), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
-                             NL.ptr(roff), rstart.numel(), NL.ptr(tp), int(max_tiles),
-                             NL.ptr(spans), NL.stream_ptr()), "hs_join_spans")
+                             NL.ptr(roff), rstart.numel(), NL.ptr(tp), int(mt),
+                             NL.ptr(spans), tile, NL.stream_ptr()), "hs_join_spans")
     k = kernel_for(join_agg_shape(p), lambda: gen_join_agg(p))
     parts = _partials(grid, GA, dev)
     k.launch(grid, join_agg_values(p, tp, spans, parts), NL.stream_ptr(),

@@ -135,7 +135,7 @@ def lib():
     _sig(L.hs_agg_final, I, P, P, P, P, I, I, P, P, P, P, P)
     _sig(L.hs_join_count, I, P, P, P, P, P, I, P, I64, P, I, P, P)
     _sig(L.hs_join_emit, I, P, I, P, P, I, P, P, P, P)
-    _sig(L.hs_join_spans, I, P, P, P, P, P, I, P, I64, P, P)
+    _sig(L.hs_join_spans, I, P, P, P, P, P, I, P, I64, P, I, P)
     _lib = L
     return L
 

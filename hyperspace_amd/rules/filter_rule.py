@@ -11,7 +11,8 @@ import logging
 
 from ..actions import states
 from ..plan import logical as L
-from ..telemetry.events import AppInfo, HyperspaceIndexUsageEvent, get_event_logger
+from ..telemetry.events import (AppInfo, HyperspaceIndexUsageEvent, NoOpEventLogger,
+                                get_event_logger)
 from ..utils.resolver import resolve, resolve_one
 from . import rule_utils as RU
 from .rankers import rank_filter
@@ -64,9 +65,11 @@ def FilterIndexRule(session, plan):
             if index is None:
                 return None
             transformed = RU.transform_plan_to_use_index(session, index, original, False)
-            get_event_logger(session.conf).log_event(HyperspaceIndexUsageEvent(
-                AppInfo(session.user, session.app_id, session.app_name), [index],
-                filt.tree_string(), transformed.tree_string(), "Filter index rule applied."))
+            logger = get_event_logger(session.conf)
+            if not isinstance(logger, NoOpEventLogger):  # plan strings only when someone listens
+                logger.log_event(HyperspaceIndexUsageEvent(
+                    AppInfo(session.user, session.app_id, session.app_name), [index],
+                    filt.tree_string(), transformed.tree_string(), "Filter index rule applied."))
             return _Done(transformed)
         except Exception as e:  # noqa: BLE001
             log.warning("Non fatal exception in running filter index rule: %s", e)

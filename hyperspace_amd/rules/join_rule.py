@@ -15,7 +15,8 @@ from typing import Dict, List, Optional
 from ..actions import states
 from ..plan import expressions as E
 from ..plan import logical as L
-from ..telemetry.events import AppInfo, HyperspaceIndexUsageEvent, get_event_logger
+from ..telemetry.events import (AppInfo, HyperspaceIndexUsageEvent, NoOpEventLogger,
+                                get_event_logger)
 from ..utils.resolver import resolve, resolve_one
 from . import rule_utils as RU
 from .rankers import rank_join
@@ -154,9 +155,11 @@ def JoinIndexRule(session, plan):
             li, ri = pair
             updated = p.copy(left=RU.transform_plan_to_use_index(session, li, p.left, True),
                              right=RU.transform_plan_to_use_index(session, ri, p.right, True))
-            get_event_logger(session.conf).log_event(HyperspaceIndexUsageEvent(
-                AppInfo(session.user, session.app_id, session.app_name), [li, ri],
-                p.tree_string(), updated.tree_string(), "Join index rule applied."))
+            logger = get_event_logger(session.conf)
+            if not isinstance(logger, NoOpEventLogger):  # plan strings only when someone listens
+                logger.log_event(HyperspaceIndexUsageEvent(
+                    AppInfo(session.user, session.app_id, session.app_name), [li, ri],
+                    p.tree_string(), updated.tree_string(), "Join index rule applied."))
             return updated
         except Exception as e:  # noqa: BLE001
             log.warning("Non fatal exception in running join index rule: %s", e)
