@@ -60,7 +60,7 @@ def h2d(a: np.ndarray, device):
 
 
 class DeviceColumn:
-    __slots__ = ("data", "valid", "atype", "dictionary", "offsets", "chars")
+    __slots__ = ("data", "valid", "atype", "dictionary", "offsets", "chars", "compact")
 
     def __init__(self, data, valid, atype: pa.DataType, dictionary: Optional[pa.Array] = None,
                  offsets=None, chars=None):
@@ -70,6 +70,7 @@ class DeviceColumn:
         self.dictionary = dictionary
         self.offsets = offsets
         self.chars = chars
+        self.compact = False  # exec.encoding.compact_of: False = not computed, None = n/a
 
     def __len__(self):
         return int(self.data.shape[0])

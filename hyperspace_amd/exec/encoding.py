@@ -1,0 +1,114 @@
+"""Lossless lightweight compression of HBM-resident index columns (frame-of-reference, with an
+optional exact decimal scale for floating-point columns).
+
+The fused query kernels are HBM-bandwidth bound, so the bytes per row they stream are the cost
+model.  Index columns are immutable once loaded, so the executor derives a compact copy per
+column once and the generated kernels (``exec/jit.py``) decode it in registers:
+
+    value = base + code                  (integers, dates, timestamps, dictionary codes)
+    value = (double)(base + code) / 10^k (floats that are exact k-digit decimals, e.g. prices)
+
+``code`` is a signed 8/16/32-bit integer chosen from the value range.  An encoding is kept only if
+decoding reproduces every valid row *bit for bit* (checked on the device), so results are exact —
+e.g. TPC-H ``l_discount`` becomes 1 byte/row instead of 8, ``l_orderkey`` 4 instead of 8.  Columns
+that do not qualify simply have no compact form and are read at full width.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+from ..ops import _lib as NL
+
+_INT_TYPES = (NL.I8, NL.I16, NL.I32, NL.I64, NL.U32, NL.BOOL)
+_FLOAT_TYPES = (NL.F64,)
+_MAX_SCALE_DIGITS = 4
+
+
+class Compact:
+    __slots__ = ("codes", "width", "base", "scale", "logical_type")
+
+    def __init__(self, codes, width: int, base: int, scale: Optional[float], logical_type: int):
+        self.codes = codes          # torch int8/int16/int32 tensor (biased: code = v - base)
+        self.width = width          # bytes per row
+        self.base = int(base)
+        self.scale = scale          # None for integers, 10**k for decimals
+        self.logical_type = logical_type
+
+    def nbytes(self) -> int:
+        return self.codes.numel() * self.width
+
+    def signature(self) -> tuple:
+        """Shape-relevant part (codegen key): literals like base/scale are kernel arguments."""
+        return (self.width, self.scale is not None)
+
+
+def _width_for(span: int):
+    for w, bits in ((1, 8), (2, 16), (4, 32)):
+        if span < (1 << bits):
+            return w, 1 << (bits - 1)
+    return None, None
+
+
+def _codes(v, lo: int, w: int, bias: int):
+    import torch
+    dt = {1: torch.int8, 2: torch.int16, 4: torch.int32}[w]
+    return (v - (lo + bias)).to(dt)
+
+
+def encode(col) -> Optional[Compact]:
+    """Compact form of a DeviceColumn, or None when no encoding is narrower and exact."""
+    import torch
+    t = col.hs_type
+    d = col.data
+    n = d.numel()
+    if n == 0 or col.offsets is not None:
+        return None
+    vm = col.valid.bool() if col.valid is not None else None
+    if t in _INT_TYPES:
+        v = d.long()
+        if vm is not None:
+            if not bool(vm.any()):
+                return None
+            lo = int(torch.where(vm, v, torch.iinfo(torch.int64).max).min().item())
+            hi = int(torch.where(vm, v, torch.iinfo(torch.int64).min).max().item())
+            v = torch.where(vm, v, lo)
+        else:
+            lo, hi = (int(x.item()) for x in torch.aminmax(v))
+        w, bias = _width_for(hi - lo)
+        if w is None or w >= d.element_size():
+            return None
+        return Compact(_codes(v, lo, w, bias), w, lo + bias, None, t)
+    if t in _FLOAT_TYPES:
+        x = d.double()
+        if vm is not None:
+            if not bool(vm.any()):
+                return None
+            x = torch.where(vm, x, x[vm][0])
+        if not bool(torch.isfinite(x).all()):
+            return None
+        for k in range(_MAX_SCALE_DIGITS + 1):
+            s = float(10 ** k)
+            q = torch.round(x * s)
+            if float(q.abs().max().item()) >= 2.0 ** 52:
+                return None
+            back = (q / s).view(torch.int64)
+            same = bool((back == x.view(torch.int64)).all())  # bit-exact (also keeps -0.0 out)
+            if not same:
+                continue
+            qi = q.long()
+            lo, hi = (int(a.item()) for a in torch.aminmax(qi))
+            w, bias = _width_for(hi - lo)
+            if w is None or w >= d.element_size():
+                return None
+            return Compact(_codes(qi, lo, w, bias), w, lo + bias, s, t)
+        return None
+    return None
+
+
+def compact_of(col) -> Optional[Compact]:
+    """Cached compact form (computed on first use; tables are immutable)."""
+    c = getattr(col, "compact", False)
+    if c is False:
+        c = encode(col)
+        col.compact = c
+    return c

@@ -605,10 +605,22 @@ class GpuBackend:
         else:
             tp = K.ranges_to_tiles(rlen)
             if HyperspaceConf.codegen_enabled(self.session.conf):
-                out = jit.scan_agg(p, rstart, rlen, tp)
+                out = jit.scan_agg(p, rstart, rlen, tp, self._compacts(descs))
             else:
                 out = K.scan_agg(p, rstart, rlen, tp)
         return (*out, G, gbase, gdict, gtype)
+
+    def _compacts(self, descs: Dict[int, DeviceColumn]) -> Optional[dict]:
+        """Compact HBM encodings (exec/encoding.py) the generated kernels read instead."""
+        if not HyperspaceConf.hbm_compression_enabled(self.session.conf):
+            return None
+        from .encoding import compact_of
+        out = {}
+        for s, c in descs.items():
+            enc = compact_of(c)
+            if enc is not None:
+                out[s] = enc
+        return out
 
     def _empty_agg(self, A, G=1):
         import torch
@@ -644,8 +656,11 @@ class GpuBackend:
         if keep[0].always_false or keep[1].always_false:
             return (*self._empty_agg(len(specs), G), G, gbase, gdict, gtype)
         max_tiles = K.join_max_tiles(left.table.num_rows, rlen.numel())
-        run = jit.join_agg if HyperspaceConf.codegen_enabled(self.session.conf) else K.join_agg
-        out = run(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles)
+        if HyperspaceConf.codegen_enabled(self.session.conf):
+            out = jit.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles,
+                               self._compacts(descs))
+        else:
+            out = K.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles)
         return (*out, G, gbase, gdict, gtype)
 
 

@@ -35,16 +35,19 @@ CACHE_DIR = os.environ.get("HS_JIT_CACHE", os.path.join(_HERE, "_native", "jitca
 
 BLOCK = 256
 SCAN_ITEMS = int(os.environ.get("HS_JIT_SCAN_ITEMS", "8"))
-JOIN_ITEMS = int(os.environ.get("HS_JIT_JOIN_ITEMS", "4"))
+# 512-row join tiles on a 4096-block grid measured best on MI355X (scripts/microbench_join.py,
+# profiles/microbench_join_r1.jsonl): short per-tile latency chains, 16 blocks/CU in flight
+JOIN_ITEMS = int(os.environ.get("HS_JIT_JOIN_ITEMS", "2"))
 JOIN_LDS_KEYS = int(os.environ.get("HS_JIT_JOIN_LDS_KEYS", "2048"))
 SCAN_GRID = int(os.environ.get("HS_JIT_SCAN_GRID", "0"))   # 0: library default (2048)
-JOIN_GRID = int(os.environ.get("HS_JIT_JOIN_GRID", "0"))
+JOIN_GRID = int(os.environ.get("HS_JIT_JOIN_GRID", "4096"))
 
 _CTYPE = {NL.I8: "signed char", NL.I16: "short", NL.I32: "int", NL.I64: "long long",
           NL.F32: "float", NL.F64: "double", NL.BOOL: "unsigned char", NL.U32: "unsigned int",
           NL.U64: "unsigned long long"}
 _OPSTR = {NL.OP_EQ: "==", NL.OP_NE: "!=", NL.OP_LT: "<", NL.OP_LE: "<=", NL.OP_GT: ">",
           NL.OP_GE: ">="}
+_CODE_T = {1: "signed char", 2: "short", 4: "int"}   # exec.encoding code widths
 
 _rt = None
 _rt_lock = threading.Lock()
@@ -183,10 +186,9 @@ def _ident(kind: int) -> str:
 class _Gen:
     """Expression builder over column slots of one or two row variables."""
 
-    def __init__(self, args: Args, cols: Dict[int, Tuple[int, bool]], split: int,
-                 rows: Tuple[str, str]):
+    def __init__(self, args: Args, cols: Dict[int, tuple], split: int, rows: Tuple[str, str]):
         self.a = args
-        self.cols = cols          # slot -> (hs_type, has_valid)
+        self.cols = cols          # slot -> (hs_type, has_valid, compact signature or None)
         self.split = split
         self.rows = rows          # row variable for slot < split / >= split
 
@@ -194,25 +196,36 @@ class _Gen:
         return self.rows[1] if slot >= self.split else self.rows[0]
 
     def ptr(self, slot: int) -> str:
-        t, _ = self.cols[slot]
-        return self.a.add("p", f"c{slot}", f"const {_CTYPE[t]}*")
+        t, _, enc = self.cols[slot]
+        ct = _CODE_T[enc[0]] if enc else _CTYPE[t]
+        return self.a.add("p", f"c{slot}", f"const {ct}*")
 
     def vptr(self, slot: int) -> Optional[str]:
-        _, hv = self.cols[slot]
+        hv = self.cols[slot][1]
         return self.a.add("p", f"v{slot}", "const unsigned char*") if hv else None
 
-    def val(self, slot: int) -> str:
-        return f"x{slot}"
+    def value(self, slot: int, row: str) -> str:
+        """Logical value of column ``slot`` at ``row`` (decodes compact columns in registers)."""
+        t, _, enc = self.cols[slot]
+        raw = f"{self.ptr(slot)}[{row}]"
+        if not enc:
+            return raw
+        ct = _CTYPE[t]
+        base = self.a.add("q", f"B{slot}", "long long")
+        if enc[1]:
+            scale = self.a.add("d", f"Q{slot}", "double")
+            return f"({ct})((double)({base} + (i64){raw}) / {scale})"
+        return f"({ct})({base} + (i64){raw})"
 
     def ok(self, slot: int) -> str:
         return f"n{slot}" if self.cols[slot][1] else "true"
 
     def load(self, slot: int, guard: str, out: List[str], ind: str) -> None:
-        t, hv = self.cols[slot]
+        t = self.cols[slot][0]
         ct = _CTYPE[t]
         r = self.row(slot)
-        out.append(f"{ind}const {ct} x{slot} = ({guard}) ? {self.ptr(slot)}[{r}] : ({ct})0;")
-        if hv:
+        out.append(f"{ind}const {ct} x{slot} = ({guard}) ? {self.value(slot, r)} : ({ct})0;")
+        if self.cols[slot][1]:
             out.append(f"{ind}const bool n{slot} = ({guard}) && {self.vptr(slot)}[{r}] != 0;")
 
     def leaf(self, k: int, p: NL.Pred) -> str:
@@ -394,9 +407,18 @@ def _common_args(args: Args) -> None:
 # ------------------------------------------------------------------------------------------------
 # Scan + filter + aggregate
 # ------------------------------------------------------------------------------------------------
-def scan_agg_shape(p: NL.ScanParams) -> tuple:
-    cols = tuple((s, p.cols[s].type, bool(p.cols[s].valid)) for s in range(NL.MAX_COLS)
-                 if p.cols[s].data)
+def _col_specs(p, compacts) -> Dict[int, tuple]:
+    """slot -> (hs_type, has_valid, compact signature | None)."""
+    out = {}
+    for s in range(NL.MAX_COLS):
+        if p.cols[s].data:
+            c = (compacts or {}).get(s)
+            out[s] = (p.cols[s].type, bool(p.cols[s].valid), c.signature() if c else None)
+    return out
+
+
+def scan_agg_shape(p: NL.ScanParams, compacts=None) -> tuple:
+    cols = tuple(sorted(_col_specs(p, compacts).items()))
     preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
                    p.preds[k].group) for k in range(p.npreds))
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
@@ -404,15 +426,14 @@ def scan_agg_shape(p: NL.ScanParams) -> tuple:
     return ("scan_agg", cols, preds, aggs, p.group_col, SCAN_ITEMS)
 
 
-def gen_scan_agg(p: NL.ScanParams) -> Kernel:
+def gen_scan_agg(p: NL.ScanParams, compacts=None) -> Kernel:
     args = Args()
     for n, ct in (("rstart", "const long long*"), ("rlen", "const long long*"),
                   ("tile_prefix", "const long long*")):
         args.add("p", n, ct)
     args.add("q", "R", "long long")
     _common_args(args)
-    cols = {s: (p.cols[s].type, bool(p.cols[s].valid)) for s in range(NL.MAX_COLS)
-            if p.cols[s].data}
+    cols = _col_specs(p, compacts)
     gen = _Gen(args, cols, NL.MAX_COLS, ("row", "row"))
     preds = [(k, p.preds[k]) for k in range(p.npreds)]
     aggs = [p.aggs[i] for i in range(p.naggs)]
@@ -466,21 +487,26 @@ def gen_scan_agg(p: NL.ScanParams) -> Kernel:
     return Kernel(src, "hs_jit_scan_agg", args, lds)
 
 
-def scan_agg_values(p: NL.ScanParams, rstart, rlen, tile_prefix, parts) -> Dict[str, object]:
+def scan_agg_values(p: NL.ScanParams, rstart, rlen, tile_prefix, parts,
+                    compacts=None) -> Dict[str, object]:
     v = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tile_prefix.data_ptr(),
          "R": rstart.numel(), "psum": parts[0].data_ptr(), "pcnt": parts[1].data_ptr(),
          "pmin": parts[2].data_ptr(), "pmax": parts[3].data_ptr(),
          "num_groups": p.num_groups, "group_base": p.group_base}
     _fill_common(v, p.cols, [(k, p.preds[k]) for k in range(p.npreds)],
-                 [p.aggs[i] for i in range(p.naggs)])
+                 [p.aggs[i] for i in range(p.naggs)], compacts)
     return v
 
 
-def _fill_common(v: Dict[str, object], cols, preds, aggs) -> None:
+def _fill_common(v: Dict[str, object], cols, preds, aggs, compacts=None) -> None:
     for s in range(NL.MAX_COLS):
         if cols[s].data:
-            v[f"c{s}"] = cols[s].data
+            c = (compacts or {}).get(s)
+            v[f"c{s}"] = c.codes.data_ptr() if c else cols[s].data
             v[f"v{s}"] = cols[s].valid or 0
+            if c:
+                v[f"B{s}"] = c.base
+                v[f"Q{s}"] = c.scale or 1.0
     for k, p in preds:
         v[f"L{k}"] = p.ilit
         v[f"F{k}"] = p.flit
@@ -495,9 +521,8 @@ def _fill_common(v: Dict[str, object], cols, preds, aggs) -> None:
 # ------------------------------------------------------------------------------------------------
 # Co-located join + aggregate
 # ------------------------------------------------------------------------------------------------
-def join_agg_shape(p: NL.JoinParams) -> tuple:
-    cols = tuple((s, p.cols[s].type, bool(p.cols[s].valid)) for s in range(NL.MAX_COLS)
-                 if p.cols[s].data)
+def join_agg_shape(p: NL.JoinParams, compacts=None) -> tuple:
+    cols = tuple(sorted(_col_specs(p, compacts).items()))
     preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
                    p.preds[k].group) for k in range(p.npreds))
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
@@ -514,14 +539,13 @@ def _key_expr(var: str, is_float: bool) -> str:
     return f"((u64)(i64){var} ^ 0x8000000000000000ull)"
 
 
-def gen_join_agg(p: NL.JoinParams) -> Kernel:
+def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
     args = Args()
     args.add("p", "tile_prefix", "const long long*")
     args.add("q", "R", "long long")
     args.add("p", "spans", "const long long*")
     _common_args(args)
-    cols = {s: (p.cols[s].type, bool(p.cols[s].valid)) for s in range(NL.MAX_COLS)
-            if p.cols[s].data}
+    cols = _col_specs(p, compacts)
     split = 8
     gen = _Gen(args, cols, split, ("lrow", "j"))
     lpreds = [(k, p.preds[k]) for k in range(p.nlp)]
@@ -569,7 +593,7 @@ def gen_join_agg(p: NL.JoinParams) -> Kernel:
     # stage right keys
     b += ["    if (staged) {",
           f"      for (i64 q = threadIdx.x; q < re - rs; q += {BLOCK})",
-          f"        skeys[q] = {_key_expr(f'{gen.ptr(rk)}[rs + q]', fl)};",
+          f"        skeys[q] = {_key_expr(gen.value(rk, 'rs + q'), fl)};",
           "    }",
           "    __syncthreads();"]
     # probe: first match per row
@@ -581,8 +605,8 @@ def gen_join_agg(p: NL.JoinParams) -> Kernel:
               f"        j{it} = rs + lo; m{it} = j{it} < re && skeys[lo] == k{it};",
               "      } else { i64 lo = rs, hi = re;",
               f"        while (lo < hi) {{ const i64 md = (lo + hi) >> 1; const bool nv = {_valid_expr(gen, rk, 'md')};",
-              f"          if (nv || {_key_expr(f'{gen.ptr(rk)}[md]', fl)} < k{it}) lo = md + 1; else hi = md; }}",
-              f"        j{it} = lo; m{it} = lo < re && {_key_expr(f'{gen.ptr(rk)}[lo]', fl)} == k{it}; }}",
+              f"          if (nv || {_key_expr(gen.value(rk, 'md'), fl)} < k{it}) lo = md + 1; else hi = md; }}",
+              f"        j{it} = lo; m{it} = lo < re && {_key_expr(gen.value(rk, 'lo'), fl)} == k{it}; }}",
               "    }"]
     # match rounds
     anym = " || ".join(f"m{it}" for it in range(NI))
@@ -615,7 +639,7 @@ def gen_join_agg(p: NL.JoinParams) -> Kernel:
         b += [_rename(x, allslots, it) for x in acc]
         b += [f"      if (m{it}) {{ ++j{it};",
               f"        m{it} = j{it} < re && (staged ? skeys[j{it} - rs] : "
-              f"{_key_expr(f'{gen.ptr(rk)}[j{it}]', fl)}) == k{it}; }}"]
+              f"{_key_expr(gen.value(rk, f'j{it}'), fl)}) == k{it}; }}"]
     b += ["    }", "    __syncthreads();", "  }"]
     b += _flush(aggs, grouped)
     src = (_PRELUDE + args.struct_src() +
@@ -638,13 +662,14 @@ def _rename(line: str, slots, it: int) -> str:
     return line
 
 
-def join_agg_values(p: NL.JoinParams, tile_prefix, spans, parts) -> Dict[str, object]:
+def join_agg_values(p: NL.JoinParams, tile_prefix, spans, parts,
+                    compacts=None) -> Dict[str, object]:
     v = {"tile_prefix": tile_prefix.data_ptr(), "R": tile_prefix.numel() - 1,
          "spans": spans.data_ptr(), "psum": parts[0].data_ptr(), "pcnt": parts[1].data_ptr(),
          "pmin": parts[2].data_ptr(), "pmax": parts[3].data_ptr(),
          "num_groups": p.num_groups, "group_base": p.group_base}
     _fill_common(v, p.cols, [(k, p.preds[k]) for k in range(p.npreds)],
-                 [p.aggs[i] for i in range(p.naggs)])
+                 [p.aggs[i] for i in range(p.naggs)], compacts)
     return v
 
 
@@ -684,21 +709,22 @@ def _final(parts, grid: int, GA: int, dev):
     return out
 
 
-def scan_agg(p: NL.ScanParams, rstart, rlen, tile_prefix=None):
-    """``tile_prefix`` must use this kernel's tile (BLOCK * SCAN_ITEMS); None computes it."""
+def scan_agg(p: NL.ScanParams, rstart, rlen, tile_prefix=None, compacts=None):
+    """``tile_prefix`` must use this kernel's tile (BLOCK * SCAN_ITEMS); None computes it.
+    ``compacts``: slot -> ``encoding.Compact`` read instead of the full-width column."""
     from ..ops import kernels as K
     if tile_prefix is None or BLOCK * SCAN_ITEMS != NL.lib().hs_scan_tile_rows():
         tile_prefix = K.ranges_to_tiles(rlen, BLOCK * SCAN_ITEMS)
     grid = SCAN_GRID or NL.lib().hs_scan_grid()
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
-    k = kernel_for(scan_agg_shape(p), lambda: gen_scan_agg(p))
+    k = kernel_for(scan_agg_shape(p, compacts), lambda: gen_scan_agg(p, compacts))
     parts = _partials(grid, GA, rstart.device)
-    k.launch(grid, scan_agg_values(p, rstart, rlen, tile_prefix, parts), NL.stream_ptr(),
-             GA * 32 if p.group_col >= 0 else 0)
+    k.launch(grid, scan_agg_values(p, rstart, rlen, tile_prefix, parts, compacts),
+             NL.stream_ptr(), GA * 32 if p.group_col >= 0 else 0)
     return _final(parts, grid, GA, rstart.device)
 
 
-def join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, max_tiles: int):
+def join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, max_tiles: int, compacts=None):
     """``max_tiles`` = ``ops.kernels.join_max_tiles`` (AOT tile); rescaled to this kernel's tile."""
     import torch
     from ..ops import kernels as K
@@ -713,8 +739,8 @@ def join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, max_tiles: int):
     NL.check(L.hs_join_spans(C.byref(p), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
                              NL.ptr(roff), rstart.numel(), NL.ptr(tp), int(mt),
                              NL.ptr(spans), tile, NL.stream_ptr()), "hs_join_spans")
-    k = kernel_for(join_agg_shape(p), lambda: gen_join_agg(p))
+    k = kernel_for(join_agg_shape(p, compacts), lambda: gen_join_agg(p, compacts))
     parts = _partials(grid, GA, dev)
-    k.launch(grid, join_agg_values(p, tp, spans, parts), NL.stream_ptr(),
+    k.launch(grid, join_agg_values(p, tp, spans, parts, compacts), NL.stream_ptr(),
              GA * 32 if p.group_col >= 0 else 0)
     return _final(parts, grid, GA, dev)

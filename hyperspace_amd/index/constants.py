@@ -95,4 +95,7 @@ HIPGRAPH_ENABLED_DEFAULT = "true"
 # whole-stage code generation (hipRTC) for the fused scan/join aggregate kernels
 CODEGEN_ENABLED = "spark.hyperspace.mi.codegen.enabled"
 CODEGEN_ENABLED_DEFAULT = "true"
+# lossless frame-of-reference / decimal-scale compaction of HBM columns read by generated kernels
+HBM_COMPRESSION_ENABLED = "spark.hyperspace.mi.hbmCompression.enabled"
+HBM_COMPRESSION_ENABLED_DEFAULT = "true"
 FAULT_INJECTION = "spark.hyperspace.mi.faultInjection"

@@ -116,3 +116,7 @@ class HyperspaceConf:
     @staticmethod
     def codegen_enabled(conf) -> bool:
         return _b(conf.get(C.CODEGEN_ENABLED, C.CODEGEN_ENABLED_DEFAULT))
+
+    @staticmethod
+    def hbm_compression_enabled(conf) -> bool:
+        return _b(conf.get(C.HBM_COMPRESSION_ENABLED, C.HBM_COMPRESSION_ENABLED_DEFAULT))

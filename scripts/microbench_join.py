@@ -53,7 +53,8 @@ def main():
     loff = np.concatenate([[0], np.cumsum(lcounts.cpu().numpy())]).astype(np.int64)
     roff = torch.from_numpy(np.concatenate([[0], np.cumsum(ocounts.cpu().numpy())]).astype(np.int64)).to(dev)
     ship = torch.randint(8000, 10600, (n_li,), dtype=torch.int32, device=dev, generator=g)
-    price = torch.rand(n_li, dtype=torch.float64, device=dev, generator=g) * 1e5
+    # TPC-H prices are DECIMAL(15,2): doubles that are exact 2-digit decimals
+    price = torch.round(torch.rand(n_li, dtype=torch.float64, device=dev, generator=g) * 1e7) / 100
     disc = torch.randint(0, 11, (n_li,), device=dev, generator=g).double() / 100
     odate = torch.randint(8000, 10500, (n_ord,), dtype=torch.int32, device=dev, generator=g)
     del per, lb
@@ -90,18 +91,24 @@ def main():
         return e0.elapsed_time(e1) / args.iters, out
 
     ms, out = timed(lambda: K.join_agg(p, rstart, rlen, rbk, roff, mt))
-    ref = out[0].item()
+    ref = out[0][0].item()
     print(json.dumps({"kernel": "aot_join", "ms": round(ms, 3), "GBps": round(nbytes / ms / 1e6, 1),
                       "rows": n_li}), flush=True)
-    for lds in [int(x) for x in args.lds.split(",")]:
-        for items in [int(x) for x in args.items.split(",")]:
-            for grid in [int(x) for x in args.grids.split(",")]:
-                jit.JOIN_ITEMS, jit.JOIN_GRID, jit.JOIN_LDS_KEYS = items, grid, lds
-                ms, out = timed(lambda: jit.join_agg(p, rstart, rlen, rbk, roff, mt))
-                ok = abs(out[0].item() - ref) <= 1e-9 * abs(ref)
-                print(json.dumps({"kernel": "jit_join", "items": items, "grid": grid, "lds": lds,
-                                  "ms": round(ms, 3), "GBps": round(nbytes / ms / 1e6, 1),
-                                  "match": ok}), flush=True)
+    from hyperspace_amd.exec.encoding import encode
+    comp = {s: e for s, e in ((s, encode(cc)) for s, cc in cols.items()) if e is not None}
+    print(json.dumps({"compact_widths": {s: e.width for s, e in comp.items()}}), flush=True)
+    for cmode in ("raw", "compact"):
+        cm = comp if cmode == "compact" else None
+        for lds in [int(x) for x in args.lds.split(",")]:
+            for items in [int(x) for x in args.items.split(",")]:
+                for grid in [int(x) for x in args.grids.split(",")]:
+                    jit.JOIN_ITEMS, jit.JOIN_GRID, jit.JOIN_LDS_KEYS = items, grid, lds
+                    ms, out = timed(lambda: jit.join_agg(p, rstart, rlen, rbk, roff, mt, cm))
+                    ok = abs(out[0][0].item() - ref) <= 1e-9 * abs(ref)
+                    print(json.dumps({"kernel": "jit_join", "enc": cmode, "items": items,
+                                      "grid": grid, "lds": lds, "ms": round(ms, 3),
+                                      "GBps_logical": round(nbytes / ms / 1e6, 1),
+                                      "match": ok}), flush=True)
     # scan (Q6 shape) over a shipdate-sorted copy: 1/7 of the rows in range
     order = torch.argsort(ship.view(-1), stable=True)
     s_ship, s_disc, s_price = ship[order], disc[order], price[order]
@@ -129,17 +136,21 @@ def main():
     sbytes = (hi - lo) * 24
     tp = K.ranges_to_tiles(rl_)
     ms, out = timed(lambda: K.scan_agg(sp, rs_, rl_, tp))
-    ref = out[0].item()
+    ref = out[0][0].item()
     print(json.dumps({"kernel": "aot_scan", "ms": round(ms, 3), "GBps": round(sbytes / ms / 1e6, 1),
                       "rows": hi - lo}), flush=True)
-    for items in (4, 8, 16):
-        for grid in [int(x) for x in args.grids.split(",")]:
-            jit.SCAN_ITEMS, jit.SCAN_GRID = items, grid
-            ms, out = timed(lambda: jit.scan_agg(sp, rs_, rl_, None))
-            ok = abs(out[0].item() - ref) <= 1e-9 * abs(ref)
-            print(json.dumps({"kernel": "jit_scan", "items": items, "grid": grid,
-                              "ms": round(ms, 3), "GBps": round(sbytes / ms / 1e6, 1),
-                              "match": ok}), flush=True)
+    scomp = {s: e for s, e in ((s, encode(cc)) for s, cc in scols.items()) if e is not None}
+    for cmode in ("raw", "compact"):
+        cm = scomp if cmode == "compact" else None
+        for items in (4, 8):
+            for grid in [int(x) for x in args.grids.split(",")]:
+                jit.SCAN_ITEMS, jit.SCAN_GRID = items, grid
+                ms, out = timed(lambda: jit.scan_agg(sp, rs_, rl_, None, cm))
+                ok = abs(out[0][0].item() - ref) <= 1e-9 * abs(ref)
+                print(json.dumps({"kernel": "jit_scan", "enc": cmode, "items": items,
+                                  "grid": grid, "ms": round(ms, 3),
+                                  "GBps_logical": round(sbytes / ms / 1e6, 1), "match": ok}),
+                      flush=True)
 
 
 if __name__ == "__main__":

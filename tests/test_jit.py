@@ -87,6 +87,77 @@ def test_generated_sources_compile(rt, tmp_path):
         assert rc == 0, jit.runtime().hs_jit_last_error().decode()
 
 
+def _decode(c):
+    import torch
+    v = c.codes.long() + c.base
+    return v.double() / c.scale if c.scale else v
+
+
+def test_hbm_encoding_round_trip_cpu():
+    import torch
+    from hyperspace_amd.exec.device_table import DeviceColumn
+    from hyperspace_amd.exec.encoding import encode
+    rng = np.random.default_rng(2)
+    # int64 keys with a large base -> 4-byte FOR
+    k = torch.from_numpy(rng.integers(10**12, 10**12 + 3_000_000_000, 5000))
+    c = encode(DeviceColumn(k, None, pa.int64()))
+    assert c.width == 4 and c.scale is None and torch.equal(_decode(c), k)
+    # dates -> 2 bytes
+    d = torch.from_numpy(rng.integers(8000, 10600, 5000).astype(np.int32))
+    c = encode(DeviceColumn(d, None, pa.date32()))
+    assert c.width == 2 and torch.equal(_decode(c), d.long())
+    # TPC-H style decimals: discount 0.00..0.10 -> 1 byte, prices (2 digits) -> 4 bytes
+    disc = torch.from_numpy(rng.integers(0, 11, 5000) / 100.0)
+    c = encode(DeviceColumn(disc, None, pa.float64()))
+    assert c.width == 1 and c.scale == 100.0
+    assert torch.equal(_decode(c).view(torch.int64), disc.view(torch.int64))
+    price = torch.from_numpy(np.round(rng.random(5000) * 1e5, 2))
+    c = encode(DeviceColumn(price, None, pa.float64()))
+    assert c.width == 4 and torch.equal(_decode(c).view(torch.int64), price.view(torch.int64))
+    # arbitrary doubles and wide ranges stay uncompressed
+    assert encode(DeviceColumn(torch.from_numpy(rng.random(100)), None, pa.float64())) is None
+    assert encode(DeviceColumn(torch.tensor([0, 2**40], dtype=torch.int64), None, pa.int64())) is None
+    # nulls: masked slots do not widen the range
+    vals = torch.tensor([5, 0, 7, 6], dtype=torch.int64)
+    valid = torch.tensor([1, 0, 1, 1], dtype=torch.uint8)
+    c = encode(DeviceColumn(vals, valid, pa.int64()))
+    assert c.width == 1
+    dec = _decode(c)
+    assert dec[0] == 5 and dec[2] == 7 and dec[3] == 6
+    # -0.0 is not representable as a scaled integer bit-exactly
+    assert encode(DeviceColumn(torch.tensor([-0.0, 1.0]), None, pa.float64())) is None
+
+
+def test_generated_sources_compile_with_compact_columns(rt, tmp_path):
+    from hyperspace_amd.exec.encoding import Compact
+    jit = rt
+    p = _scan_params({0: _fake(NL.F64), 1: _fake(NL.F64), 2: _fake(NL.I64, True)},
+                     [NL.Pred(NL.PK_FLT_LIT, NL.OP_GE, 0, 0, 0, 0, 0, 0.05, None),
+                      NL.Pred(NL.PK_INT_LIT, NL.OP_LT, 2, 0, 1, 0, 9, 0.0, None)],
+                     [_agg(NL.AK_SUM, [(1, 0.0, 1.0), (0, 1.0, -1.0)])])
+    comp = {0: Compact(None, 1, 0, 100.0, NL.F64), 1: Compact(None, 4, 0, 100.0, NL.F64),
+            2: Compact(None, 2, 5, None, NL.I64)}
+    k = jit.gen_scan_agg(p, comp)
+    assert "a.Q0" in k.src and "const signed char* c0" in k.src
+    rc = jit.runtime().hs_jit_compile_to_cache(k.src.encode(), k.name.encode(), b"gfx950",
+                                               str(tmp_path).encode())
+    assert rc == 0, jit.runtime().hs_jit_last_error().decode()
+    assert jit.scan_agg_shape(p, comp) != jit.scan_agg_shape(p, None)
+    j = NL.JoinParams()
+    j.cols[0], j.cols[1] = _fake(NL.I64), _fake(NL.F64)
+    j.cols[8], j.cols[9] = _fake(NL.I64), _fake(NL.I32)
+    j.preds[0] = NL.Pred(NL.PK_INT_LIT, NL.OP_LT, 9, 0, 1000, 0, 9000, 0.0, None)
+    j.nlp, j.npreds = 0, 1
+    j.aggs[0] = _agg(NL.AK_SUM, [(1, 0.0, 1.0)])
+    j.naggs, j.lkey, j.rkey, j.group_col = 1, 0, 8, -1
+    comp = {0: Compact(None, 4, 1, None, NL.I64), 8: Compact(None, 4, 1, None, NL.I64),
+            9: Compact(None, 2, 8000, None, NL.I32), 1: Compact(None, 4, 0, 100.0, NL.F64)}
+    k = jit.gen_join_agg(j, comp)
+    rc = jit.runtime().hs_jit_compile_to_cache(k.src.encode(), k.name.encode(), b"gfx950",
+                                               str(tmp_path).encode())
+    assert rc == 0, jit.runtime().hs_jit_last_error().decode()
+
+
 def test_shape_key_ignores_literals():
     from hyperspace_amd.exec import jit
     a = _scan_params({0: _fake(NL.F64)}, [NL.Pred(NL.PK_FLT_LIT, NL.OP_LT, 0, 0, 0, 0, 0, 1.0, None)],
@@ -151,6 +222,14 @@ def test_jit_scan_agg_matches_aot_and_numpy(device):
                 assert got[3][base + 2] == price[m].max()
         np.testing.assert_allclose(got[0], aot[0], rtol=1e-12)
         assert np.array_equal(got[1], aot[1])
+        # compact HBM encodings give bit-identical inputs, hence identical results
+        from hyperspace_amd.exec.encoding import encode
+        comp = {s: e for s, e in ((s, encode(c)) for s, c in cols.items()) if e is not None}
+        assert {1, 2, 4} <= set(comp)  # discount (dec2/u8), quantity (int/u8), group (u8)
+        cg = [t.cpu().numpy() for t in jit.scan_agg(p, rstart, rlen, None, comp)]
+        np.testing.assert_allclose(cg[0], got[0], rtol=1e-12)
+        assert np.array_equal(cg[1], got[1])
+        assert np.array_equal(cg[2], got[2]) and np.array_equal(cg[3], got[3])
 
 
 @pytest.mark.gpu
@@ -197,3 +276,11 @@ def test_jit_join_agg_matches_aot(device):
         np.testing.assert_allclose(got[0], aot[0], rtol=1e-12)
         assert np.array_equal(got[1], aot[1])
         assert got[1].sum() > 0
+        from hyperspace_amd.exec.encoding import encode
+        allc = dict(enumerate(cl))
+        allc.update({8 + i: c for i, c in enumerate(cr)})
+        comp = {s: e for s, e in ((s, encode(c)) for s, c in allc.items()) if e is not None}
+        assert 0 in comp and 8 in comp  # both join keys FOR-encoded
+        cg = [t.cpu().numpy() for t in jit.join_agg(p, rstart, rlen, rbk, roff_t, mt, comp)]
+        np.testing.assert_allclose(cg[0], got[0], rtol=1e-12)
+        assert np.array_equal(cg[1], got[1])
