@@ -47,7 +47,8 @@ class DRel:
     def __init__(self, table: DeviceTable, colmap: Dict[int, str], attrs: List[E.Attribute],
                  conds: Optional[list] = None, bucketed: bool = False,
                  sort_attrs: Optional[List[E.Attribute]] = None,
-                 bucket_attrs: Optional[List[E.Attribute]] = None, num_buckets: int = 0):
+                 bucket_attrs: Optional[List[E.Attribute]] = None, num_buckets: int = 0,
+                 parts: Optional[List["DRel"]] = None):
         self.table = table
         self.colmap = colmap
         self.attrs = attrs
@@ -56,8 +57,12 @@ class DRel:
         self.sort_attrs = list(sort_attrs or [])
         self.bucket_attrs = list(bucket_attrs or [])
         self.num_buckets = num_buckets
+        # BucketUnion: co-partitioned parts (each sorted within its buckets); table is None
+        self.parts = parts
 
     def col(self, a: E.Attribute) -> DeviceColumn:
+        if self.parts:
+            raise Unsupported("column access on a bucket union")
         name = self.colmap.get(a.expr_id)
         if name is None:
             raise Unsupported(f"attribute {a.sql()} not available on device")
@@ -65,7 +70,7 @@ class DRel:
 
     def copy(self, **kw) -> "DRel":
         d = DRel(self.table, dict(self.colmap), list(self.attrs), list(self.conds), self.bucketed,
-                 self.sort_attrs, self.bucket_attrs, self.num_buckets)
+                 self.sort_attrs, self.bucket_attrs, self.num_buckets, self.parts)
         for k, v in kw.items():
             setattr(d, k, v)
         return d
@@ -133,11 +138,45 @@ class GpuBackend:
     def _rel(self, p: X.SparkPlan) -> DRel:
         if isinstance(p, X.FileSourceScanExec):
             return self._scan(p)
-        if isinstance(p, X.FilterExec):
+        if isinstance(p, X.BucketUnionExec):
+            return self._bucket_union(p)
+        if isinstance(p, (X.FilterExec, X.ProjectExec)):
             r = self._rel(p.child)
+            if r.parts:
+                parts = [self._unary(p, x) for x in r.parts]
+                return r.copy(parts=parts, attrs=list(p.output), colmap=dict(parts[0].colmap))
+            return self._unary(p, r)
+        if isinstance(p, X.SortExec):
+            r = self._rel(p.child)
+            if not p.global_sort and r.bucketed and _prefix_sorted(r, [o.child for o in p.order]):
+                return r
+            raise Unsupported("device sort of unsorted input")
+        if isinstance(p, X.ShuffleExchangeExec) and isinstance(p.partitioning, X.HashPartitioning):
+            return self._repartition(self._rel(p.child), p.partitioning)
+        if isinstance(p, X.SortMergeJoinExec):
+            return self._join_rel(p)
+        raise Unsupported(f"operator {p.node_name}")
+
+    def _bucket_union(self, p: X.BucketUnionExec) -> DRel:
+        nb = p.bucket_spec.num_buckets
+        parts = []
+        for child in p.children:
+            r = self._rel(child)
+            if r.parts or not r.bucketed or r.num_buckets != nb:
+                raise Unsupported("bucket union of non co-partitioned inputs")
+            colmap = dict(r.colmap)
+            for u, c in zip(p.output, child.output):   # BucketUnion output = child 0's attrs
+                if c.expr_id in r.colmap:
+                    colmap[u.expr_id] = r.colmap[c.expr_id]
+            parts.append(r.copy(colmap=colmap))
+        first = parts[0]
+        return DRel(None, dict(first.colmap), list(p.output), [], True, first.sort_attrs,
+                    first.bucket_attrs, nb, parts)
+
+    def _unary(self, p: X.SparkPlan, r: DRel) -> DRel:
+        if isinstance(p, X.FilterExec):
             return r.copy(conds=r.conds + E.split_conjuncts(p.condition))
         if isinstance(p, X.ProjectExec):
-            r = self._rel(p.child)
             colmap = dict(r.colmap)
             attrs = []
             for e in p.project_list:
@@ -151,15 +190,6 @@ class GpuBackend:
                 else:
                     raise Unsupported("computed projection")
             return r.copy(colmap=colmap, attrs=attrs)
-        if isinstance(p, X.SortExec):
-            r = self._rel(p.child)
-            if not p.global_sort and r.bucketed and _prefix_sorted(r, [o.child for o in p.order]):
-                return r
-            raise Unsupported("device sort of unsorted input")
-        if isinstance(p, X.ShuffleExchangeExec) and isinstance(p.partitioning, X.HashPartitioning):
-            return self._repartition(self._rel(p.child), p.partitioning)
-        if isinstance(p, X.SortMergeJoinExec):
-            return self._join_rel(p)
         raise Unsupported(f"operator {p.node_name}")
 
     def _scan(self, p: X.FileSourceScanExec) -> DRel:
@@ -312,6 +342,8 @@ class GpuBackend:
     # ------------------------------------------------------------------------------------------
     def _materialize(self, r: DRel, attrs: List[E.Attribute]) -> Dict[int, DeviceColumn]:
         """Apply pending predicates; return expr_id -> gathered DeviceColumn."""
+        if r.parts:
+            raise Unsupported("materialize a bucket union")
         if not r.conds:
             t = r.table
             full = t.num_rows
@@ -342,6 +374,8 @@ class GpuBackend:
         return {a.expr_id: c for a, c in zip(attrs, g)}
 
     def _to_arrow(self, r: DRel, out_attrs: List[E.Attribute]) -> pa.Table:
+        if r.parts:  # rows of a bucket union: each part's rows, concatenated
+            return pa.concat_tables([self._to_arrow(x, out_attrs) for x in r.parts])
         cols = self._materialize(r, out_attrs)
         arrays = [cols[a.expr_id].to_arrow() for a in out_attrs]
         fixed = []
@@ -406,10 +440,14 @@ class GpuBackend:
             raise Unsupported("left not sorted by join key")
         if not _prefix_sorted(right, [rk]):
             raise Unsupported("right not sorted by join key")
-        lc, rc = left.col(lk), right.col(rk)
-        if lc.dictionary is not None or rc.dictionary is not None:
-            raise Unsupported("string join keys on device")
-        if lc.is_float != rc.is_float:
+        kinds = set()
+        for side, k in ((left, lk), (right, rk)):
+            for part in side.parts or [side]:
+                c = part.col(k)
+                if c.dictionary is not None:
+                    raise Unsupported("string join keys on device")
+                kinds.add(c.is_float)
+        if len(kinds) > 1:
             raise Unsupported("mixed int/float join keys")
         return left, right, lk, rk
 
@@ -437,6 +475,8 @@ class GpuBackend:
 
     def _join_rel(self, p: X.SortMergeJoinExec) -> DRel:
         left, right, lk, rk = self._join_inputs(p)
+        if left.parts or right.parts:
+            raise Unsupported("row-producing join over a bucket union")
         out_attrs = list(p.output)
         implied: set = set()
         rstart, rlen, rbk = self._ranges(left, left.conds, implied)
@@ -629,42 +669,84 @@ class GpuBackend:
         return z, zc, torch.full_like(z, float("inf")), torch.full_like(z, float("-inf"))
 
     def _join_agg(self, node: X.SortMergeJoinExec, fns, group):
+        """Fused join + aggregate.  A side that is a BucketUnion (Hybrid Scan: index buckets plus
+        appended rows shuffled by the index bucket spec) is a list of co-partitioned sorted parts;
+        an inner join distributes over union, so every (left part, right part) pair runs as its
+        own co-located join and the partial aggregates combine — the index side is never
+        re-sorted together with the appended rows."""
         left, right, lk, rk = self._join_inputs(node)
+        lparts, rparts = left.parts or [left], right.parts or [right]
+        gs = (None, 1, 0, None, None)
+        if group is not None:
+            side = lparts if any(group.expr_id in x.colmap for x in lparts) else rparts
+            gs = self._group_spec_parts(side, group, MAX_GROUPS_JOIN)
+            if gs is None:
+                return (*self._empty_agg(len(fns) + 1), 1, 0, None, None)
+        _, G, gbase, gdict, gtype = gs
+        out = None
+        for lp in lparts:
+            for rp in rparts:
+                part = self._join_agg_pair(node, lp, rp, lk, rk, fns, group, G, gbase)
+                out = part if out is None else _combine_aggs(out, part)
+        return (*out, G, gbase, gdict, gtype)
+
+    def _group_spec_parts(self, parts, group, limit):
+        specs = [self._group_spec(x, group, limit) for x in parts if group.expr_id in x.colmap]
+        specs = [s for s in specs if s is not None]
+        if not specs:
+            return None
+        if len(specs) == 1:
+            return specs[0]
+        if any(s[3] is not None for s in specs):
+            raise Unsupported("string group key over a bucket union")
+        lo = min(s[2] for s in specs)
+        hi = max(s[2] + s[1] for s in specs)
+        if hi - lo > limit:
+            raise Unsupported("group domain too large for LDS aggregation")
+        return None, hi - lo, lo, None, specs[0][4]
+
+    def _join_agg_pair(self, node, left: DRel, right: DRel, lk, rk, fns, group, G, gbase):
+        # drive the kernel from the smaller side (the appended part of a hybrid scan is small)
+        if right.table.num_rows * 4 < left.table.num_rows:
+            left, right, lk, rk = right, left, rk, lk
         implied: set = set()
         rstart, rlen, rbk = self._ranges(left, left.conds, implied)
         jp, col_info, descs, keep = self._join_params(
             left, right, lk, rk, node.condition,
             lconds=[c for c in left.conds if id(c) not in implied])
         specs = self._agg_specs(fns, col_info)
-        gs = None
         if group is not None:
-            side = left if group.expr_id in left.colmap else right
-            gs = self._group_spec(side, group, MAX_GROUPS_JOIN)
-            if gs is None:
-                return (*self._empty_agg(len(specs)), 1, 0, None, None)
-            _, G, gbase, gdict, gtype = gs
             col_info(group)
             jp.group_col = col_info(group).slot if G > 1 else -1
             jp.num_groups, jp.group_base = G, gbase
-        else:
-            G, gbase, gdict, gtype = 1, 0, None, None
         for s, c in descs.items():
             jp.cols[s] = c.desc()
         for i, a in enumerate(specs):
             jp.aggs[i] = a
         jp.naggs = len(specs)
-        if keep[0].always_false or keep[1].always_false:
-            return (*self._empty_agg(len(specs), G), G, gbase, gdict, gtype)
+        if keep[0].always_false or keep[1].always_false or left.table.num_rows == 0 or \
+                right.table.num_rows == 0:
+            return self._empty_agg(len(specs), G)
         max_tiles = K.join_max_tiles(left.table.num_rows, rlen.numel())
         if HyperspaceConf.codegen_enabled(self.session.conf):
-            out = jit.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles,
-                               self._compacts(descs))
-        else:
-            out = K.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles)
-        return (*out, G, gbase, gdict, gtype)
+            return jit.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles,
+                                self._compacts(descs))
+        return K.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles)
+
+
+def _combine_aggs(a, b):
+    """Merge two (sum, count, min, max) partial aggregate tuples in place of ``a``."""
+    import torch
+    a[0].add_(b[0])
+    a[1].add_(b[1])
+    torch.minimum(a[2], b[2], out=a[2])
+    torch.maximum(a[3], b[3], out=a[3])
+    return a
 
 
 def _prefix_sorted(r: DRel, exprs) -> bool:
+    if r.parts:
+        return all(_prefix_sorted(x, exprs) for x in r.parts)
     if len(exprs) > len(r.sort_attrs):
         return False
     for e, s in zip(exprs, r.sort_attrs):

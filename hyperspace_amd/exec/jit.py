@@ -41,6 +41,9 @@ JOIN_ITEMS = int(os.environ.get("HS_JIT_JOIN_ITEMS", "2"))
 JOIN_LDS_KEYS = int(os.environ.get("HS_JIT_JOIN_LDS_KEYS", "2048"))
 SCAN_GRID = int(os.environ.get("HS_JIT_SCAN_GRID", "0"))   # 0: library default (2048)
 JOIN_GRID = int(os.environ.get("HS_JIT_JOIN_GRID", "4096"))
+# latency-bound kernels: load every needed column in the first batch (more bytes, fewer trips)
+JOIN_EAGER = os.environ.get("HS_JIT_JOIN_EAGER", "1") == "1"
+SCAN_EAGER = os.environ.get("HS_JIT_SCAN_EAGER", "1") == "1"
 
 _CTYPE = {NL.I8: "signed char", NL.I16: "short", NL.I32: "int", NL.I64: "long long",
           NL.F32: "float", NL.F64: "double", NL.BOOL: "unsigned char", NL.U32: "unsigned int",
@@ -423,7 +426,7 @@ def scan_agg_shape(p: NL.ScanParams, compacts=None) -> tuple:
                    p.preds[k].group) for k in range(p.npreds))
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
-    return ("scan_agg", cols, preds, aggs, p.group_col, SCAN_ITEMS)
+    return ("scan_agg", cols, preds, aggs, p.group_col, SCAN_ITEMS, SCAN_EAGER)
 
 
 def gen_scan_agg(p: NL.ScanParams, compacts=None) -> Kernel:
@@ -464,11 +467,12 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None) -> Kernel:
           "      const bool act = k < rows;",
           "      const i64 row = row0 + (act ? k : 0);"]
     ind = "      "
-    for s in pslots:
+    for s in pslots + (aslots if SCAN_EAGER else []):
         gen.load(s, "act", b, ind)
     b.append(f"{ind}bool pass = act && {gen.cnf(preds)};")
-    for s in aslots:
-        gen.load(s, "pass", b, ind)
+    if not SCAN_EAGER:
+        for s in aslots:
+            gen.load(s, "pass", b, ind)
     gvar = "gi"
     if grouped:
         g = p.group_col
@@ -528,7 +532,7 @@ def join_agg_shape(p: NL.JoinParams, compacts=None) -> tuple:
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
     return ("join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey, p.key_is_float,
-            JOIN_ITEMS, JOIN_LDS_KEYS)
+            JOIN_ITEMS, JOIN_LDS_KEYS, JOIN_EAGER)
 
 
 def _key_expr(var: str, is_float: bool) -> str:
@@ -540,6 +544,19 @@ def _key_expr(var: str, is_float: bool) -> str:
 
 
 def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
+    """Co-located join + aggregate over 512-row left tiles (see module docstring).
+
+    The kernel is latency-bound (rows in flight per CU x dependent HBM round trips per tile), so
+    the code is scheduled to minimise round trips on each tile's critical path:
+
+    1. the next tile's span record is prefetched while the current tile runs;
+    2. every left column the query needs (key, left predicates, left aggregate inputs, group) and
+       this thread's share of the right key span are loaded in ONE batch;
+    3. LDS stage + barrier + LDS binary search of the keys;
+    4. one batch of right-column loads at the matched rows, then accumulate.
+
+    With ``JOIN_EAGER`` off, left aggregate inputs are loaded only for matched rows instead
+    (fewer bytes, one more round trip)."""
     args = Args()
     args.add("p", "tile_prefix", "const long long*")
     args.add("q", "R", "long long")
@@ -554,16 +571,18 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
     grouped = p.group_col >= 0
     fl = bool(p.key_is_float)
     lk, rk = p.lkey, p.rkey
-    lslots = [s for s in _pred_slots(lpreds) if s < split]
-    lslots = list(dict.fromkeys([lk] + lslots))
-    rslots = [s for s in _pred_slots(rpreds) if s >= split]
-    lpost = [s for s in _pred_slots(rpreds) if s < split and s not in lslots]
-    aslots = [s for s in _agg_slots(aggs) if s not in lslots + rslots + lpost]
-    if grouped and p.group_col not in lslots + rslots + lpost + aslots:
-        aslots.append(p.group_col)
+    need = _pred_slots(lpreds) + _pred_slots(rpreds) + _agg_slots(aggs) + \
+        ([p.group_col] if grouped else [])
+    left_all = list(dict.fromkeys([lk] + [s for s in need if s < split]))
+    right_all = list(dict.fromkeys([s for s in need if s >= split]))
+    lpred_slots = list(dict.fromkeys([lk] + [s for s in _pred_slots(lpreds) if s < split]))
+    if JOIN_EAGER:
+        left_first, left_late = left_all, []
+    else:
+        left_first = lpred_slots
+        left_late = [s for s in left_all if s not in lpred_slots]
     NI = JOIN_ITEMS
-    T = BLOCK * NI
-    rkt = _CTYPE[cols[rk][0]]
+    KEYS_PER_THREAD = 1   # typical spans (~4 right rows per 16 left rows) fit one key per thread
     b: List[str] = []
     b += _acc_decls(aggs, grouped, args)
     b += [f"  __shared__ u64 skeys[{JOIN_LDS_KEYS}];",
@@ -571,32 +590,43 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
           "  const i64 per = (ntiles + gridDim.x - 1) / gridDim.x;",
           "  const i64 t0 = (i64)blockIdx.x * per;",
           "  const i64 t1 = ntiles < t0 + per ? ntiles : t0 + per;",
+          "  i64 n_row0 = 0, n_rows = 0, n_rs = 0, n_re = 0;",
+          "  if (t0 < t1) { n_row0 = a.spans[4 * t0]; n_rows = a.spans[4 * t0 + 1];",
+          "                 n_rs = a.spans[4 * t0 + 2]; n_re = a.spans[4 * t0 + 3]; }",
           "  for (i64 t = t0; t < t1; ++t) {",
-          "    const i64 row0 = a.spans[4 * t], rows = a.spans[4 * t + 1];",
-          "    const i64 rs = a.spans[4 * t + 2], re = a.spans[4 * t + 3];",
+          "    const i64 row0 = n_row0, rows = n_rows, rs = n_rs, re = n_re;",
+          "    if (t + 1 < t1) { n_row0 = a.spans[4 * t + 4]; n_rows = a.spans[4 * t + 5];",
+          "                      n_rs = a.spans[4 * t + 6]; n_re = a.spans[4 * t + 7]; }",
           f"    const bool staged = re - rs <= {JOIN_LDS_KEYS};"]
-    # left batch loads first (independent of the LDS stage)
-    for it in range(NI):
-        b.append(f"    const i64 lr{it} = row0 + {it * BLOCK} + threadIdx.x;")
-        b.append(f"    const bool la{it} = {it * BLOCK} + (i64)threadIdx.x < rows;")
     ind = "    "
+    for it in range(NI):
+        b.append(f"{ind}const i64 lr{it} = row0 + {it * BLOCK} + threadIdx.x;")
+        b.append(f"{ind}const bool la{it} = {it * BLOCK} + (i64)threadIdx.x < rows;")
+    # (1) left batch + this thread's right keys, issued together
     for it in range(NI):
         g2 = _Gen(args, cols, split, (f"lr{it}", "j"))
         blk: List[str] = []
-        for s in lslots:
+        for s in left_first:
             g2.load(s, f"la{it}", blk, ind)
-        b += [_rename(x, lslots, it) for x in blk]
-        cond = _rename(g2.cnf(lpreds), lslots, it)
-        okk = _rename(gen.ok(lk), [lk], it) if cols[lk][1] else "true"
+        b += [_rename(x, left_first, it) for x in blk]
+    for q in range(KEYS_PER_THREAD):
+        off = f"{q * BLOCK} + (i64)threadIdx.x"
+        b.append(f"{ind}const u64 sk{q} = (staged && {off} < re - rs) ? "
+                 f"{_key_expr(gen.value(rk, f'rs + {off}'), fl)} : 0ull;")
+    for it in range(NI):
+        g2 = _Gen(args, cols, split, (f"lr{it}", "j"))
+        cond = _rename(g2.cnf(lpreds), left_first, it)
+        okk = f"n{lk}_{it}" if cols[lk][1] else "true"
         b.append(f"{ind}bool m{it} = la{it} && {okk} && {cond};")
         b.append(f"{ind}const u64 k{it} = {_key_expr(f'x{lk}_{it}', fl)};")
-    # stage right keys
-    b += ["    if (staged) {",
-          f"      for (i64 q = threadIdx.x; q < re - rs; q += {BLOCK})",
-          f"        skeys[q] = {_key_expr(gen.value(rk, 'rs + q'), fl)};",
-          "    }",
-          "    __syncthreads();"]
-    # probe: first match per row
+    for q in range(KEYS_PER_THREAD):
+        b.append(f"{ind}if ({q * BLOCK} + (i64)threadIdx.x < re - rs) skeys[{q * BLOCK} + threadIdx.x] = sk{q};")
+    b += [f"{ind}if (staged) {{",
+          f"{ind}  for (i64 q = {KEYS_PER_THREAD * BLOCK} + threadIdx.x; q < re - rs; q += {BLOCK})",
+          f"{ind}    skeys[q] = {_key_expr(gen.value(rk, 'rs + q'), fl)};",
+          f"{ind}}}",
+          f"{ind}__syncthreads();"]
+    # (2) first match per row (LDS binary search; global search for oversized spans)
     for it in range(NI):
         b += [f"    i64 j{it} = rs;",
               f"    if (m{it}) {{",
@@ -608,24 +638,23 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
               f"          if (nv || {_key_expr(gen.value(rk, 'md'), fl)} < k{it}) lo = md + 1; else hi = md; }}",
               f"        j{it} = lo; m{it} = lo < re && {_key_expr(gen.value(rk, 'lo'), fl)} == k{it}; }}",
               "    }"]
-    # match rounds
+    # (3) match rounds: right columns at j, residual predicates, accumulate
     anym = " || ".join(f"m{it}" for it in range(NI))
     b.append(f"    while (__any({anym})) {{")
+    allslots = left_all + right_all
     for it in range(NI):
         g2 = _Gen(args, cols, split, (f"lr{it}", f"j{it}"))
         blk = []
-        for s in rslots:
+        for s in right_all:
             g2.load(s, f"m{it}", blk, "      ")
-        for s in lpost:
-            g2.load(s, f"m{it}", blk, "      ")
-        b += [_rename(x, rslots + lpost + lslots, it) for x in blk]
-        cond = _rename(g2.cnf(rpreds), rslots + lpost + lslots, it)
+        b += [_rename(x, right_all, it) for x in blk]
+        cond = _rename(g2.cnf(rpreds), allslots, it)
         b.append(f"      bool ps{it} = m{it} && {cond};")
-        blk = []
-        for s in aslots:
-            g2.load(s, f"ps{it}", blk, "      ")
-        b += [_rename(x, aslots, it) for x in blk]
-        allslots = lslots + rslots + lpost + aslots
+        if left_late:
+            blk = []
+            for s in left_late:
+                g2.load(s, f"ps{it}", blk, "      ")
+            b += [_rename(x, left_late, it) for x in blk]
         gvar = f"gi{it}"
         if grouped:
             g = p.group_col

@@ -97,5 +97,7 @@ CODEGEN_ENABLED = "spark.hyperspace.mi.codegen.enabled"
 CODEGEN_ENABLED_DEFAULT = "true"
 # lossless frame-of-reference / decimal-scale compaction of HBM columns read by generated kernels
 HBM_COMPRESSION_ENABLED = "spark.hyperspace.mi.hbmCompression.enabled"
-HBM_COMPRESSION_ENABLED_DEFAULT = "true"
+# off by default: the fused kernels measured latency-bound, not bandwidth-bound, on MI355X
+# (profiles/microbench_join_r1*.jsonl), so narrower columns did not pay for the decode
+HBM_COMPRESSION_ENABLED_DEFAULT = "false"
 FAULT_INJECTION = "spark.hyperspace.mi.faultInjection"

@@ -99,16 +99,17 @@ def main():
     print(json.dumps({"compact_widths": {s: e.width for s, e in comp.items()}}), flush=True)
     for cmode in ("raw", "compact"):
         cm = comp if cmode == "compact" else None
-        for lds in [int(x) for x in args.lds.split(",")]:
+        for eager in (True, False):
             for items in [int(x) for x in args.items.split(",")]:
                 for grid in [int(x) for x in args.grids.split(",")]:
-                    jit.JOIN_ITEMS, jit.JOIN_GRID, jit.JOIN_LDS_KEYS = items, grid, lds
+                    jit.JOIN_ITEMS, jit.JOIN_GRID, jit.JOIN_EAGER = items, grid, eager
                     ms, out = timed(lambda: jit.join_agg(p, rstart, rlen, rbk, roff, mt, cm))
                     ok = abs(out[0][0].item() - ref) <= 1e-9 * abs(ref)
-                    print(json.dumps({"kernel": "jit_join", "enc": cmode, "items": items,
-                                      "grid": grid, "lds": lds, "ms": round(ms, 3),
+                    print(json.dumps({"kernel": "jit_join", "enc": cmode, "eager": eager,
+                                      "items": items, "grid": grid, "ms": round(ms, 3),
                                       "GBps_logical": round(nbytes / ms / 1e6, 1),
                                       "match": ok}), flush=True)
+    jit.JOIN_EAGER = True
     # scan (Q6 shape) over a shipdate-sorted copy: 1/7 of the rows in range
     order = torch.argsort(ship.view(-1), stable=True)
     s_ship, s_disc, s_price = ship[order], disc[order], price[order]
@@ -142,15 +143,16 @@ def main():
     scomp = {s: e for s, e in ((s, encode(cc)) for s, cc in scols.items()) if e is not None}
     for cmode in ("raw", "compact"):
         cm = scomp if cmode == "compact" else None
-        for items in (4, 8):
-            for grid in [int(x) for x in args.grids.split(",")]:
-                jit.SCAN_ITEMS, jit.SCAN_GRID = items, grid
-                ms, out = timed(lambda: jit.scan_agg(sp, rs_, rl_, None, cm))
-                ok = abs(out[0][0].item() - ref) <= 1e-9 * abs(ref)
-                print(json.dumps({"kernel": "jit_scan", "enc": cmode, "items": items,
-                                  "grid": grid, "ms": round(ms, 3),
-                                  "GBps_logical": round(sbytes / ms / 1e6, 1), "match": ok}),
-                      flush=True)
+        for eager in (True, False):
+            for items in (4, 8):
+                for grid in [int(x) for x in args.grids.split(",")]:
+                    jit.SCAN_ITEMS, jit.SCAN_GRID, jit.SCAN_EAGER = items, grid, eager
+                    ms, out = timed(lambda: jit.scan_agg(sp, rs_, rl_, None, cm))
+                    ok = abs(out[0][0].item() - ref) <= 1e-9 * abs(ref)
+                    print(json.dumps({"kernel": "jit_scan", "enc": cmode, "eager": eager,
+                                      "items": items, "grid": grid, "ms": round(ms, 3),
+                                      "GBps_logical": round(sbytes / ms / 1e6, 1), "match": ok}),
+                          flush=True)
 
 
 if __name__ == "__main__":
