@@ -34,16 +34,18 @@ RUNTIME_PATH = os.path.join(_HERE, "_native", "libhs_runtime.so")
 CACHE_DIR = os.environ.get("HS_JIT_CACHE", os.path.join(_HERE, "_native", "jitcache"))
 
 BLOCK = 256
-SCAN_ITEMS = int(os.environ.get("HS_JIT_SCAN_ITEMS", "8"))
+SCAN_ITEMS = int(os.environ.get("HS_JIT_SCAN_ITEMS", "4"))
 # 512-row join tiles on a 4096-block grid measured best on MI355X (scripts/microbench_join.py,
 # profiles/microbench_join_r1.jsonl): short per-tile latency chains, 16 blocks/CU in flight
 JOIN_ITEMS = int(os.environ.get("HS_JIT_JOIN_ITEMS", "2"))
+JOIN_BLOCK = int(os.environ.get("HS_JIT_JOIN_BLOCK", "256"))
 JOIN_LDS_KEYS = int(os.environ.get("HS_JIT_JOIN_LDS_KEYS", "2048"))
-SCAN_GRID = int(os.environ.get("HS_JIT_SCAN_GRID", "0"))   # 0: library default (2048)
-JOIN_GRID = int(os.environ.get("HS_JIT_JOIN_GRID", "4096"))
-# latency-bound kernels: load every needed column in the first batch (more bytes, fewer trips)
-JOIN_EAGER = os.environ.get("HS_JIT_JOIN_EAGER", "1") == "1"
-SCAN_EAGER = os.environ.get("HS_JIT_SCAN_EAGER", "1") == "1"
+SCAN_GRID = int(os.environ.get("HS_JIT_SCAN_GRID", "8192"))
+JOIN_GRID = int(os.environ.get("HS_JIT_JOIN_GRID", "8192"))
+# eager = load every needed column in the first batch (more bytes, one round trip fewer); the
+# sweep (profiles/microbench_join_r1c.jsonl) favoured lazy loads for both kernels
+JOIN_EAGER = os.environ.get("HS_JIT_JOIN_EAGER", "0") == "1"
+SCAN_EAGER = os.environ.get("HS_JIT_SCAN_EAGER", "0") == "1"
 
 _CTYPE = {NL.I8: "signed char", NL.I16: "short", NL.I32: "int", NL.I64: "long long",
           NL.F32: "float", NL.F64: "double", NL.BOOL: "unsigned char", NL.U32: "unsigned int",
@@ -107,11 +109,12 @@ class Args:
 
 
 class Kernel:
-    def __init__(self, src: str, name: str, args: Args, lds_bytes: int = 0):
+    def __init__(self, src: str, name: str, args: Args, lds_bytes: int = 0, block: int = 256):
         self.src = src
         self.name = name
         self.args = args
         self.lds_bytes = lds_bytes
+        self.block = block
         self._fn = None
 
     def function(self):
@@ -128,7 +131,7 @@ class Kernel:
     def launch(self, grid: int, values: Dict[str, object], stream_ptr: int, shmem: int = 0) -> None:
         buf = self.args.pack(values)
         cbuf = C.create_string_buffer(buf, len(buf))
-        rc = runtime().hs_jit_launch(self.function(), grid, BLOCK, shmem or self.lds_bytes,
+        rc = runtime().hs_jit_launch(self.function(), grid, self.block, shmem or self.lds_bytes,
                                      stream_ptr, cbuf, len(buf))
         if rc != 0:
             raise RuntimeError(f"JIT launch failed: {runtime().hs_jit_last_error().decode()}")
@@ -369,7 +372,8 @@ def _acc_decls(aggs, grouped: bool, args: Args) -> List[str]:
     return out
 
 
-def _flush(aggs, grouped: bool) -> List[str]:
+def _flush(aggs, grouped: bool, block: int = None) -> List[str]:
+    BLOCK = block or globals()["BLOCK"]  # noqa: N806 — waves per block of this kernel
     out = []
     if grouped:
         out += ["  __syncthreads();",
@@ -532,7 +536,7 @@ def join_agg_shape(p: NL.JoinParams, compacts=None) -> tuple:
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
     return ("join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey, p.key_is_float,
-            JOIN_ITEMS, JOIN_LDS_KEYS, JOIN_EAGER)
+            JOIN_ITEMS, JOIN_LDS_KEYS, JOIN_EAGER, JOIN_BLOCK)
 
 
 def _key_expr(var: str, is_float: bool) -> str:
@@ -557,6 +561,8 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
 
     With ``JOIN_EAGER`` off, left aggregate inputs are loaded only for matched rows instead
     (fewer bytes, one more round trip)."""
+    BLOCK = JOIN_BLOCK  # noqa: N806 — workgroup size of this kernel
+    LDS_KEYS = join_lds_keys()  # noqa: N806
     args = Args()
     args.add("p", "tile_prefix", "const long long*")
     args.add("q", "R", "long long")
@@ -585,7 +591,7 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
     KEYS_PER_THREAD = 1   # typical spans (~4 right rows per 16 left rows) fit one key per thread
     b: List[str] = []
     b += _acc_decls(aggs, grouped, args)
-    b += [f"  __shared__ u64 skeys[{JOIN_LDS_KEYS}];",
+    b += [f"  __shared__ u64 skeys[{LDS_KEYS}];",
           "  const i64 ntiles = a.tile_prefix[a.R];",
           "  const i64 per = (ntiles + gridDim.x - 1) / gridDim.x;",
           "  const i64 t0 = (i64)blockIdx.x * per;",
@@ -597,7 +603,7 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
           "    const i64 row0 = n_row0, rows = n_rows, rs = n_rs, re = n_re;",
           "    if (t + 1 < t1) { n_row0 = a.spans[4 * t + 4]; n_rows = a.spans[4 * t + 5];",
           "                      n_rs = a.spans[4 * t + 6]; n_re = a.spans[4 * t + 7]; }",
-          f"    const bool staged = re - rs <= {JOIN_LDS_KEYS};"]
+          f"    const bool staged = re - rs <= {LDS_KEYS};"]
     ind = "    "
     for it in range(NI):
         b.append(f"{ind}const i64 lr{it} = row0 + {it * BLOCK} + threadIdx.x;")
@@ -670,12 +676,17 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
               f"        m{it} = j{it} < re && (staged ? skeys[j{it} - rs] : "
               f"{_key_expr(gen.value(rk, f'j{it}'), fl)}) == k{it}; }}"]
     b += ["    }", "    __syncthreads();", "  }"]
-    b += _flush(aggs, grouped)
+    b += _flush(aggs, grouped, BLOCK)
     src = (_PRELUDE + args.struct_src() +
            f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_join_agg(Args a) {{\n' +
            "\n".join(b) + "\n}\n")
     lds = (len(aggs) * p.num_groups * 32) if grouped else 0
-    return Kernel(src, "hs_jit_join_agg", args, lds)
+    return Kernel(src, "hs_jit_join_agg", args, lds, BLOCK)
+
+
+def join_lds_keys() -> int:
+    """LDS key slots per join workgroup: 2x the tile (FK joins stage ~tile/4 keys), capped."""
+    return max(256, min(JOIN_LDS_KEYS, 2 * JOIN_BLOCK * JOIN_ITEMS))
 
 
 def _valid_expr(gen: _Gen, slot: int, row: str) -> str:
@@ -761,7 +772,7 @@ def join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, max_tiles: int, comp
     grid = JOIN_GRID or L.hs_scan_grid()
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
     dev = rstart.device
-    tile = BLOCK * JOIN_ITEMS
+    tile = JOIN_BLOCK * JOIN_ITEMS
     tp = K.ranges_to_tiles(rlen, tile)
     mt = (max_tiles * L.hs_join_tile_rows()) // tile + rlen.numel() + 1
     spans = torch.empty(4 * mt, dtype=torch.int64, device=dev)

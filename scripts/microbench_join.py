@@ -24,7 +24,9 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--items", default="2,4,8")
     ap.add_argument("--grids", default="1024,2048,4096")
-    ap.add_argument("--lds", default="2048")
+    ap.add_argument("--blocks", default="256")
+    ap.add_argument("--quick", action="store_true", help="raw/lazy join variants only")
+    ap.add_argument("--no-scan", action="store_true")
     args = ap.parse_args()
     import numpy as np
     import pyarrow as pa
@@ -97,19 +99,24 @@ def main():
     from hyperspace_amd.exec.encoding import encode
     comp = {s: e for s, e in ((s, encode(cc)) for s, cc in cols.items()) if e is not None}
     print(json.dumps({"compact_widths": {s: e.width for s, e in comp.items()}}), flush=True)
-    for cmode in ("raw", "compact"):
+    modes = [("raw", False)] if args.quick else [("raw", False), ("raw", True), ("compact", False)]
+    for cmode, eager in modes:
         cm = comp if cmode == "compact" else None
-        for eager in (True, False):
+        for block in [int(x) for x in args.blocks.split(",")]:
             for items in [int(x) for x in args.items.split(",")]:
                 for grid in [int(x) for x in args.grids.split(",")]:
                     jit.JOIN_ITEMS, jit.JOIN_GRID, jit.JOIN_EAGER = items, grid, eager
+                    jit.JOIN_BLOCK = block
                     ms, out = timed(lambda: jit.join_agg(p, rstart, rlen, rbk, roff, mt, cm))
                     ok = abs(out[0][0].item() - ref) <= 1e-9 * abs(ref)
                     print(json.dumps({"kernel": "jit_join", "enc": cmode, "eager": eager,
-                                      "items": items, "grid": grid, "ms": round(ms, 3),
+                                      "block": block, "items": items, "grid": grid,
+                                      "ms": round(ms, 3),
                                       "GBps_logical": round(nbytes / ms / 1e6, 1),
                                       "match": ok}), flush=True)
-    jit.JOIN_EAGER = True
+    jit.JOIN_EAGER, jit.JOIN_BLOCK = False, 256
+    if args.no_scan:
+        return
     # scan (Q6 shape) over a shipdate-sorted copy: 1/7 of the rows in range
     order = torch.argsort(ship.view(-1), stable=True)
     s_ship, s_disc, s_price = ship[order], disc[order], price[order]

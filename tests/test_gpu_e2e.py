@@ -162,6 +162,42 @@ def test_non_index_join_device_shuffle(tpch):
     _close(g, c)
 
 
+def test_hybrid_scan_join_and_filter_on_device(tpch, tmp_path):
+    """BASELINE config #4 shape: indexes + appended Parquet files, served by Hybrid Scan on
+    the device (BucketUnion parts joined pairwise; appended rows shuffled on the GPU)."""
+    s, lpath, opath = tpch
+    for k, v in (("lineage.enabled", "true"), ("hybridscan.enabled", "true"),
+                 ("hybridscan.maxAppendedRatio", "0.5"), ("hybridscan.maxDeletedRatio", "0.5")):
+        s.conf.set(f"spark.hyperspace.index.{k}", v)
+    hs = Hyperspace(s)
+    li, od = s.read.parquet(lpath), s.read.parquet(opath)
+    hs.createIndex(li, IndexConfig("li_ok", ["l_orderkey"], ["l_extendedprice", "l_discount"]))
+    hs.createIndex(od, IndexConfig("ord_ok", ["o_orderkey"], ["o_orderdate"]))
+    hs.createIndex(li, IndexConfig("li_ship", ["l_shipdate"], ["l_discount", "l_quantity"]))
+    # append ~10% new rows to both tables (fresh order keys so the join has new matches)
+    t_li = pq.read_table(os.path.join(lpath, "part-0.parquet")).slice(0, 20_000)
+    t_od = pq.read_table(os.path.join(opath, "part-0.parquet")).slice(0, 4_000)
+    shift = 10_000_000
+    t_od = t_od.set_column(0, "o_orderkey", pa.compute.add(t_od.column("o_orderkey"), shift))
+    t_li = t_li.set_column(0, "l_orderkey", pa.compute.add(t_li.column("l_orderkey"), shift))
+    pq.write_table(t_li, os.path.join(lpath, "part-app.parquet"))
+    pq.write_table(t_od, os.path.join(opath, "part-app.parquet"))
+    Hyperspace.enable(s)
+    li, od = s.read.parquet(lpath), s.read.parquet(opath)
+    q = li.join(od, li["l_orderkey"] == od["o_orderkey"]).filter("o_orderdate < DATE '1996-01-01'") \
+        .agg(sum_(col("l_extendedprice") * (1 - col("l_discount"))).alias("rev"), count("*").alias("n"))
+    plan = q.queryExecution.executed_plan.tree_string()
+    assert "BucketUnion" in plan
+    g, c, path = _both(s, q, sort=False)
+    assert path == "native", s.backend().fallback_reason
+    _close(g, c)
+    q2 = li.filter("l_shipdate >= DATE '1994-01-01' AND l_shipdate < DATE '1995-01-01'") \
+        .agg(sum_(col("l_quantity") * col("l_discount")).alias("r"))
+    g, c, path = _both(s, q2, sort=False)
+    assert path == "native", s.backend().fallback_reason
+    _close(g, c)
+
+
 def test_incremental_refresh_with_deletes_on_device(tpch, tmp_path):
     s, lpath, _ = tpch
     s.conf.set("spark.hyperspace.index.lineage.enabled", "true")
