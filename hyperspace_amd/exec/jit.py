@@ -45,6 +45,8 @@ JOIN_GRID = int(os.environ.get("HS_JIT_JOIN_GRID", "8192"))
 # eager = load every needed column in the first batch (more bytes, one round trip fewer); the
 # sweep (profiles/microbench_join_r1c.jsonl) favoured lazy loads for both kernels
 JOIN_EAGER = os.environ.get("HS_JIT_JOIN_EAGER", "0") == "1"
+# stage the right side's columns of each tile's key span in LDS with the keys
+JOIN_STAGE_RIGHT = os.environ.get("HS_JIT_JOIN_STAGE_RIGHT", "1") == "1"
 SCAN_EAGER = os.environ.get("HS_JIT_SCAN_EAGER", "0") == "1"
 
 _CTYPE = {NL.I8: "signed char", NL.I16: "short", NL.I32: "int", NL.I64: "long long",
@@ -536,7 +538,7 @@ def join_agg_shape(p: NL.JoinParams, compacts=None) -> tuple:
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
     return ("join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey, p.key_is_float,
-            JOIN_ITEMS, JOIN_LDS_KEYS, JOIN_EAGER, JOIN_BLOCK)
+            JOIN_ITEMS, JOIN_LDS_KEYS, JOIN_EAGER, JOIN_BLOCK, JOIN_STAGE_RIGHT)
 
 
 def _key_expr(var: str, is_float: bool) -> str:
@@ -615,10 +617,24 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
         for s in left_first:
             g2.load(s, f"la{it}", blk, ind)
         b += [_rename(x, left_first, it) for x in blk]
+    # right columns of the span are staged in LDS with the keys (one coalesced batch), so the
+    # match rounds read them from LDS instead of a dependent HBM gather at j
+    staged_cols = right_all if JOIN_STAGE_RIGHT else []
+    for s in staged_cols:
+        ct = _CTYPE[cols[s][0]]
+        b.insert(1, f"  __shared__ {ct} sv{s}[{LDS_KEYS}];")
+        if cols[s][1]:
+            b.insert(1, f"  __shared__ unsigned char sn{s}[{LDS_KEYS}];")
     for q in range(KEYS_PER_THREAD):
         off = f"{q * BLOCK} + (i64)threadIdx.x"
-        b.append(f"{ind}const u64 sk{q} = (staged && {off} < re - rs) ? "
+        b.append(f"{ind}const bool sa{q} = staged && {off} < re - rs;")
+        b.append(f"{ind}const u64 sk{q} = sa{q} ? "
                  f"{_key_expr(gen.value(rk, f'rs + {off}'), fl)} : 0ull;")
+        for s in staged_cols:
+            ct = _CTYPE[cols[s][0]]
+            b.append(f"{ind}const {ct} svv{s}_{q} = sa{q} ? {gen.value(s, f'rs + {off}')} : ({ct})0;")
+            if cols[s][1]:
+                b.append(f"{ind}const unsigned char snv{s}_{q} = sa{q} ? {gen.vptr(s)}[rs + {off}] : 0;")
     for it in range(NI):
         g2 = _Gen(args, cols, split, (f"lr{it}", "j"))
         cond = _rename(g2.cnf(lpreds), left_first, it)
@@ -626,12 +642,21 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
         b.append(f"{ind}bool m{it} = la{it} && {okk} && {cond};")
         b.append(f"{ind}const u64 k{it} = {_key_expr(f'x{lk}_{it}', fl)};")
     for q in range(KEYS_PER_THREAD):
-        b.append(f"{ind}if ({q * BLOCK} + (i64)threadIdx.x < re - rs) skeys[{q * BLOCK} + threadIdx.x] = sk{q};")
+        idx = f"{q * BLOCK} + threadIdx.x"
+        b.append(f"{ind}if (sa{q}) {{ skeys[{idx}] = sk{q};")
+        for s in staged_cols:
+            b.append(f"{ind}  sv{s}[{idx}] = svv{s}_{q};")
+            if cols[s][1]:
+                b.append(f"{ind}  sn{s}[{idx}] = snv{s}_{q};")
+        b.append(f"{ind}}}")
     b += [f"{ind}if (staged) {{",
-          f"{ind}  for (i64 q = {KEYS_PER_THREAD * BLOCK} + threadIdx.x; q < re - rs; q += {BLOCK})",
-          f"{ind}    skeys[q] = {_key_expr(gen.value(rk, 'rs + q'), fl)};",
-          f"{ind}}}",
-          f"{ind}__syncthreads();"]
+          f"{ind}  for (i64 q = {KEYS_PER_THREAD * BLOCK} + threadIdx.x; q < re - rs; q += {BLOCK}) {{",
+          f"{ind}    skeys[q] = {_key_expr(gen.value(rk, 'rs + q'), fl)};"]
+    for s in staged_cols:
+        b.append(f"{ind}    sv{s}[q] = {gen.value(s, 'rs + q')};")
+        if cols[s][1]:
+            b.append(f"{ind}    sn{s}[q] = {gen.vptr(s)}[rs + q];")
+    b += [f"{ind}  }}", f"{ind}}}", f"{ind}__syncthreads();"]
     # (2) first match per row (LDS binary search; global search for oversized spans)
     for it in range(NI):
         b += [f"    i64 j{it} = rs;",
@@ -652,7 +677,15 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
         g2 = _Gen(args, cols, split, (f"lr{it}", f"j{it}"))
         blk = []
         for s in right_all:
-            g2.load(s, f"m{it}", blk, "      ")
+            if s in staged_cols:
+                ct = _CTYPE[cols[s][0]]
+                blk.append(f"      const {ct} x{s} = m{it} ? (staged ? sv{s}[j{it} - rs] : "
+                           f"{g2.value(s, f'j{it}')}) : ({ct})0;")
+                if cols[s][1]:
+                    blk.append(f"      const bool n{s} = m{it} && (staged ? sn{s}[j{it} - rs] : "
+                               f"{g2.vptr(s)}[j{it}]) != 0;")
+            else:
+                g2.load(s, f"m{it}", blk, "      ")
         b += [_rename(x, right_all, it) for x in blk]
         cond = _rename(g2.cnf(rpreds), allslots, it)
         b.append(f"      bool ps{it} = m{it} && {cond};")

@@ -235,7 +235,8 @@ def optimize_in(plan, threshold: int = IN_SET_THRESHOLD_DEFAULT):
 
     def fn(p):
         if isinstance(p, L.Filter):
-            return L.Filter(p.condition.transform_up(efn), p.child)
+            c2 = p.condition.transform_up(efn)
+            return None if c2 is p.condition else L.Filter(c2, p.child)
         return None
     return plan.transform_up(fn)
 
@@ -251,12 +252,9 @@ class Optimizer:
     def base_batches(self, plan):
         from ..index import constants as C
         thr = int(self.session.conf.get(C.SQL_IN_SET_CONVERSION_THRESHOLD, "10"))
-        prev = None
+        # fixed point by identity: every rule returns the very same tree when it changes nothing
         for _ in range(10):
-            s = plan.tree_string()
-            if s == prev:
-                break
-            prev = s
+            before = plan
             plan = combine_filters(plan)
             plan = push_down_predicates(plan)
             plan = push_join_condition(plan)
@@ -264,6 +262,8 @@ class Optimizer:
             plan = collapse_project(plan)
             plan = remove_redundant_project(plan)
             plan = optimize_in(plan, thr)
+            if plan is before:
+                break
         plan = infer_filters(plan)
         plan = column_pruning(plan)
         plan = collapse_project(plan)
