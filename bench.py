@@ -32,6 +32,21 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def _decoded_bytes(df, cfg) -> int:
+    """Decoded (in-memory, fixed-width) bytes of an index's columns over all source rows — the
+    byte count the device build reports as ``source_bytes``."""
+    import pyarrow.parquet as pq
+    from hyperspace_amd.exec.device_table import storage_numpy_dtype
+    from hyperspace_amd.plan import logical as L
+    from hyperspace_amd.utils import path_utils as P
+    rel = df.queryExecution.analyzed.collect(lambda p: isinstance(p, L.LogicalRelation))[0].relation
+    rows = sum(pq.ParquetFile(P.to_local(f.path)).metadata.num_rows
+               for f in rel.location.all_files())
+    width = sum(storage_numpy_dtype(rel.schema.field(c).type).itemsize
+                for c in cfg.indexedColumns + cfg.includedColumns)
+    return rows * width
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -43,6 +58,8 @@ def main():
     ap.add_argument("--data-dir", default=os.environ.get("HS_BENCH_DIR", "/tmp/hs_bench"))
     ap.add_argument("--workers", type=int, default=int(os.environ.get("HS_BENCH_WORKERS", "0")))
     ap.add_argument("--no-crosscheck", action="store_true")
+    ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
+                    help="cpu = the pyarrow host engine (measured baseline, BASELINE.md)")
     args = ap.parse_args()
 
     import numpy as np
@@ -54,11 +71,15 @@ def main():
     from hyperspace_amd.parallel.dist import DistContext
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    on_gpu = args.device == "gpu"
     dist = DistContext.from_env() if world_env > 1 else None
     rank, world = (dist.rank, dist.world) if dist else (0, 1)
-    if dist is None:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+    if on_gpu:
+        if dist is None:
+            torch.cuda.set_device(0)
+        sync = torch.cuda.synchronize
+    else:
+        sync = (lambda: None)
     barrier = dist.barrier if dist else (lambda: None)
 
     sf = args.sf
@@ -82,7 +103,7 @@ def main():
                       "spark.hyperspace.index.numBuckets": str(args.buckets),
                       "spark.sql.autoBroadcastJoinThreshold": "-1",
                       "spark.sql.shuffle.partitions": str(args.buckets),
-                      "spark.hyperspace.mi.execution.device": "gpu",
+                      "spark.hyperspace.mi.execution.device": args.device,
                       "spark.hyperspace.mi.index.codec": "snappy"},
                 warehouse_dir=os.path.join(args.data_dir, "wh"))
     s.dist = dist
@@ -100,13 +121,16 @@ def main():
     per_index = {}
     for df, cfg in builds:
         barrier()
-        torch.cuda.synchronize()
+        sync()
         tb = time.perf_counter()
         hs.createIndex(df, cfg)
-        torch.cuda.synchronize()
+        sync()
         barrier()
         dt = time.perf_counter() - tb
-        local_bytes = float(device_build.LAST_BUILD_STATS.get("source_bytes", 0))
+        if on_gpu:
+            local_bytes = float(device_build.LAST_BUILD_STATS.get("source_bytes", 0))
+        else:  # same definition as the device build: decoded bytes of the indexed columns
+            local_bytes = float(_decoded_bytes(df, cfg))
         if dist:
             local_bytes = dist.all_reduce_sum_float(local_bytes)
             dt = dist.all_reduce_max_float(dt)
@@ -145,17 +169,17 @@ def main():
 
     def step(i):
         r1 = q6(i).collect()
-        p1 = backend.last_path
+        p1 = getattr(backend, "last_path", "native")
         r2 = q3(i).collect()
-        p2 = backend.last_path
-        if p1 != "native" or p2 != "native":
+        p2 = getattr(backend, "last_path", "native")
+        if on_gpu and (p1 != "native" or p2 != "native"):
             raise RuntimeError(f"query fell back to host: {backend.fallback_reason}")
         return r1, r2
 
     tl = time.perf_counter()
     for i in range(args.warmup):
         step(1000 + i)
-    torch.cuda.synchronize()
+    sync()
     barrier()
     warm_s = time.perf_counter() - tl
     log(rank, f"[bench] warmup {args.warmup} steps in {warm_s:.2f}s "
@@ -166,14 +190,14 @@ def main():
         import cProfile
         prof = cProfile.Profile()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t_start = time.perf_counter()
     if prof is not None:
         prof.enable()
     results = []
     for i in range(args.steps):
         results.append(step(i))
-    torch.cuda.synchronize()
+    sync()
     barrier()
     elapsed = time.perf_counter() - t_start
     if prof is not None:
@@ -193,11 +217,11 @@ def main():
     lat = {}
     for name, fn in (("q6_filter_ms", q6), ("q3_join_ms", q3)):
         barrier()
-        torch.cuda.synchronize()
+        sync()
         tq = time.perf_counter()
         for i in range(5):
             fn(i).collect()
-        torch.cuda.synchronize()
+        sync()
         dtq = (time.perf_counter() - tq) / 5
         lat[name] = round((dist.all_reduce_max_float(dtq) if dist else dtq) * 1000, 3)
 
@@ -229,12 +253,16 @@ def main():
                "dtype": "fp64", "data": "synthetic",
                "config": {"model": f"tpch-sf{sf:g} lineitem/orders covering indexes",
                           "global_batch": 2, "seq_len": 0,
-                          "parallelism": f"bucket-dp{world}", "num_buckets": args.buckets,
-                          "source_files": nfiles},
+                          "parallelism": f"bucket-dp{world}" if on_gpu else "cpu-host",
+                          "num_buckets": args.buckets, "source_files": nfiles,
+                          "device": args.device},
                "index_build_gbps": round(build_gbps, 3), "index_build_s": round(build_s, 3),
                "index_build": per_index, "latency": lat, "warmup_s": round(warm_s, 3),
-               "datagen_s": round(gen_s, 2), "crosscheck": check,
-               "device_cache": {"hits": backend.cache.hits, "misses": backend.cache.misses}}
+               "datagen_s": round(gen_s, 2), "crosscheck": check}
+        if on_gpu:
+            out["device_cache"] = {"hits": backend.cache.hits, "misses": backend.cache.misses}
+        if not on_gpu:
+            out["n_gpus"] = 0
         print(json.dumps(out), flush=True)
     if dist:
         barrier()

@@ -41,12 +41,12 @@ JOIN_ITEMS = int(os.environ.get("HS_JIT_JOIN_ITEMS", "2"))
 JOIN_BLOCK = int(os.environ.get("HS_JIT_JOIN_BLOCK", "256"))
 JOIN_LDS_KEYS = int(os.environ.get("HS_JIT_JOIN_LDS_KEYS", "2048"))
 SCAN_GRID = int(os.environ.get("HS_JIT_SCAN_GRID", "8192"))
-JOIN_GRID = int(os.environ.get("HS_JIT_JOIN_GRID", "8192"))
+JOIN_GRID = int(os.environ.get("HS_JIT_JOIN_GRID", "16384"))
 # eager = load every needed column in the first batch (more bytes, one round trip fewer); the
 # sweep (profiles/microbench_join_r1c.jsonl) favoured lazy loads for both kernels
 JOIN_EAGER = os.environ.get("HS_JIT_JOIN_EAGER", "0") == "1"
 # stage the right side's columns of each tile's key span in LDS with the keys
-JOIN_STAGE_RIGHT = os.environ.get("HS_JIT_JOIN_STAGE_RIGHT", "1") == "1"
+JOIN_STAGE_RIGHT = os.environ.get("HS_JIT_JOIN_STAGE_RIGHT", "0") == "1"
 SCAN_EAGER = os.environ.get("HS_JIT_SCAN_EAGER", "0") == "1"
 
 _CTYPE = {NL.I8: "signed char", NL.I16: "short", NL.I32: "int", NL.I64: "long long",
