@@ -185,6 +185,8 @@ def main():
     log(rank, f"[bench] warmup {args.warmup} steps in {warm_s:.2f}s "
               f"(includes first HBM load of the indexes)")
 
+    from hyperspace_amd.utils.tracing import TRACER, format_report
+    TRACER.reset()  # HS_PROFILE=1: per-stage host/device times of the timed steps only
     prof = None
     if os.environ.get("HS_BENCH_PROFILE") and rank == 0:
         import cProfile
@@ -207,6 +209,8 @@ def main():
         buf = io.StringIO()
         pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(40)
         log(rank, buf.getvalue())
+    if TRACER.profile:
+        log(rank, "[bench] stage profile (timed steps)\n" + format_report(TRACER.report()))
     if dist:
         elapsed = dist.all_reduce_max_float(elapsed)
     nq = 2 * args.steps

@@ -3,8 +3,9 @@ snapshot to the GPU box):
 
 * ``libhs_kernels.so`` — HIP/CDNA4 kernels for gfx950 (``csrc/kernels/*.hip``), compiled with
   ``hipcc --offload-arch=gfx950``; C ABI launchers called through ctypes.
-* ``libhs_runtime.so`` — host C++ runtime (``csrc/runtime/*.cpp``): Parquet page writer/reader,
-  thread pool, pinned staging.  Built with g++.
+* ``libhs_runtime.so`` — host C++ runtime (``csrc/runtime/*.cpp``): hipRTC whole-stage codegen
+  (compile, code-object cache, module launch) and roctx pipeline-stage markers.  Host-only C++
+  against the HIP runtime, built with hipcc.
 
 Usage: ``python -m hyperspace_amd._native.build [--force]``.
 """
@@ -85,7 +86,7 @@ def build_runtime(force: bool = False) -> str:
     # host-only C++ against the HIP runtime + hipRTC (whole-stage codegen); hipcc supplies the
     # platform defines and include paths
     _run([_hipcc(), "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", tmp] + srcs +
-         [f"-L{rocm}/lib", "-lhiprtc", "-lamdhip64", f"-Wl,-rpath,{rocm}/lib"])
+         [f"-L{rocm}/lib", "-lhiprtc", "-lamdhip64", "-ldl", f"-Wl,-rpath,{rocm}/lib"])
     os.replace(tmp, RUNTIME_LIB)
     return RUNTIME_LIB
 

@@ -62,29 +62,67 @@ class Action:
             d.barrier()
 
     def _fault(self, point: str) -> None:
-        if self.session is not None and self.session.conf.get(C.FAULT_INJECTION) == point:
-            raise FaultInjected(f"fault injected at {point}")
+        """Raise at ``point`` if the fault-injection conf names it.  ``point@r`` limits the fault
+        to rank ``r`` (SPMD failure tests: one rank fails, every rank must observe it)."""
+        spec = self.session.conf.get(C.FAULT_INJECTION) if self.session is not None else None
+        if not spec:
+            return
+        name, _, rank = str(spec).partition("@")
+        if name != point:
+            return
+        d = self._dist()
+        if rank and int(rank) != (d.rank if d is not None else 0):
+            return
+        raise FaultInjected(f"fault injected at {point}")
+
+    def _op_with_faults(self) -> None:
+        self.op()
+        self._fault("mid_op")
 
     def _save_entry(self, id: int, entry) -> None:
         entry.timestamp = int(time.time() * 1000)
         if not self.log_manager.write_log(id, entry):
             raise HyperspaceException("Could not acquire proper state")
 
+    def _agreed(self, fn, coordinator_only: bool = False) -> None:
+        """Run ``fn`` (on every rank, or on the coordinator only) and make its outcome unanimous:
+        under SPMD a failure on any rank is re-raised on every rank — the same exception kind,
+        so a ``NoChangesException`` stays a no-op everywhere — instead of leaving the other ranks
+        blocked in the next barrier.  Doubles as that barrier."""
+        d = self._dist()
+        if d is None:
+            fn()
+            return
+        err = None
+        try:
+            if not coordinator_only or d.rank == 0:
+                fn()
+        except Exception as e:  # noqa: BLE001 — shared with the other ranks below
+            err = e
+        outcomes = d.all_gather_object(
+            None if err is None else (isinstance(err, NoChangesException), str(err)))
+        if err is not None:
+            raise err
+        failed = [o for o in outcomes if o is not None]
+        if failed:
+            no_change, msg = failed[0]
+            raise NoChangesException(msg) if no_change else HyperspaceException(
+                f"failed on another rank: {msg}")
+
     def _begin(self) -> None:
-        if self._is_coordinator():
+        def write():
             entry = self.log_entry()
             entry.state = self.transient_state
             entry.id = self.base_id + 1
             self._save_entry(self.base_id + 1, entry)
-        self._barrier()
+        self._agreed(write, coordinator_only=True)
 
     def end_log_entry(self):
         """Entry committed by ``end`` (the same as ``begin``'s unless an action overrides it)."""
         return self.log_entry()
 
     def _end(self) -> None:
-        self._barrier()
-        if self._is_coordinator():
+        def commit():
             entry = self.end_log_entry()
             entry.state = self.final_state
             entry.id = self.base_id + 2
@@ -93,7 +131,7 @@ class Action:
             self._save_entry(self.base_id + 2, entry)
             if not self.log_manager.create_latest_stable_log(self.base_id + 2):
                 log.warning("Unable to recreate latest stable log")
-        self._barrier()
+        self._agreed(commit, coordinator_only=True)
 
     def _app_info(self) -> AppInfo:
         s = self.session
@@ -112,11 +150,12 @@ class Action:
         try:
             self._log_event("Operation started.")
             self._barrier()   # every rank has pinned base_id / target paths
-            self.validate()
-            self._barrier()   # nobody writes the log before every rank validated
+            # nobody writes the log before every rank validated
+            self._agreed(self.validate)
             self._begin()
             self._fault("after_begin")
-            self.op()
+            # every rank's share of the build finished before the coordinator commits
+            self._agreed(self._op_with_faults)
             self._fault("before_end")
             self._end()
             self._log_event("Operation succeeded.")

@@ -31,6 +31,7 @@ from ..plan import expressions as E
 from ..plan import physical as X
 from ..utils import murmur3
 from ..utils.conf import HyperspaceConf
+from ..utils.tracing import TRACER, stage
 from . import compile as CP
 from . import jit
 from .arrow_eval import key
@@ -48,7 +49,7 @@ class DRel:
                  conds: Optional[list] = None, bucketed: bool = False,
                  sort_attrs: Optional[List[E.Attribute]] = None,
                  bucket_attrs: Optional[List[E.Attribute]] = None, num_buckets: int = 0,
-                 parts: Optional[List["DRel"]] = None):
+                 parts: Optional[List["DRel"]] = None, split: bool = False):
         self.table = table
         self.colmap = colmap
         self.attrs = attrs
@@ -59,6 +60,9 @@ class DRel:
         self.num_buckets = num_buckets
         # BucketUnion: co-partitioned parts (each sorted within its buckets); table is None
         self.parts = parts
+        # distributed: this rank holds a file split of a non-index relation (rows not yet routed
+        # to their bucket owners)
+        self.split = split
 
     def col(self, a: E.Attribute) -> DeviceColumn:
         if self.parts:
@@ -70,7 +74,7 @@ class DRel:
 
     def copy(self, **kw) -> "DRel":
         d = DRel(self.table, dict(self.colmap), list(self.attrs), list(self.conds), self.bucketed,
-                 self.sort_attrs, self.bucket_attrs, self.num_buckets, self.parts)
+                 self.sort_attrs, self.bucket_attrs, self.num_buckets, self.parts, self.split)
         for k, v in kw.items():
             setattr(d, k, v)
         return d
@@ -104,8 +108,10 @@ class GpuBackend:
 
     def collect(self, plan: X.SparkPlan) -> pa.Table:
         t0 = time.perf_counter()
+        TRACER.configure(self.session.conf)
         try:
-            out = self._collect_native(plan)
+            with stage("query"):
+                out = self._collect_native(plan)
             self.last_path = "native"
             self.fallback_reason = None
         except Unsupported as e:
@@ -217,13 +223,16 @@ class GpuBackend:
                 sort_attrs.append(a)
             return DRel(table, colmap, list(p.output), [], True, sort_attrs, sort_attrs,
                         idx.num_buckets)
-        if world > 1:
-            raise Unsupported("distributed scan of non-index data")
         fmt = "parquet" if (rel.is_index() or rel.file_format == "delta") else rel.file_format
-        table = self.cache.get(files, names, ("flat", fmt),
+        if world > 1:
+            # a file split per rank, like Spark's scan tasks; a following hash Exchange moves rows
+            # to their owners with an all-to-all (_repartition), aggregates all-reduce
+            files = sorted(files, key=lambda f: f.path)[rank::world]
+        table = self.cache.get(files, names, ("flat", fmt, rank, world),
                                lambda: load_flat(files, fmt, names, rel.data_schema, rel.options,
                                                  rel.location.partition_spec, self.device))
-        return DRel(table, {a.expr_id: a.name for a in p.output}, list(p.output))
+        return DRel(table, {a.expr_id: a.name for a in p.output}, list(p.output),
+                    split=world > 1)
 
     @staticmethod
     def _all_bucket_files(location, files, nb) -> bool:
@@ -399,9 +408,11 @@ class GpuBackend:
     # Repartition (device shuffle for non-index inputs)
     # ------------------------------------------------------------------------------------------
     def _repartition(self, r: DRel, part: X.HashPartitioning) -> DRel:
+        """Hash Exchange (K3) on the device: Spark-compatible Murmur3 bucket ids, then one
+        (bucket, keys) sort so the result is bucketed and sorted like an index.  With several
+        ranks, rows first move to their bucket's owner (``b % world``) with RCCL all-to-all, so
+        the output is co-partitioned with the index tables of the same bucket count."""
         d = self._dist()
-        if d is not None and d.world > 1:
-            raise Unsupported("distributed device shuffle of non-index data")
         if not all(isinstance(e, E.Attribute) for e in part.expressions):
             raise Unsupported("hash partitioning on expressions")
         keys = list(part.expressions)
@@ -410,11 +421,18 @@ class GpuBackend:
         for c in kcols:
             if c.dictionary is not None:
                 raise Unsupported("device shuffle on string keys")
-        n = len(next(iter(cols.values()))) if cols else 0
         import torch
         B = part.num_partitions
-        bucket, counts = K.murmur3_bucket(kcols, B)
-        perm = K.sort_permutation(kcols, extra_leading=(bucket, 16))
+        with stage("shuffle.hash"):
+            bucket, counts = K.murmur3_bucket(kcols, B)
+        if d is not None and d.world > 1:
+            with stage("shuffle.all_to_all"):
+                cols, bucket = self._exchange_rows(d, cols, bucket)
+            kcols = [cols[k.expr_id] for k in keys]
+            counts = torch.bincount(bucket.long(), minlength=B)
+        n = int(bucket.numel())
+        with stage("shuffle.sort"):
+            perm = K.sort_permutation(kcols, extra_leading=(bucket, 16))
         names = list(cols.keys())
         gathered = K.gather_columns([cols[i] for i in names], perm)
         off_host = np.concatenate([[0], np.cumsum(counts.cpu().numpy())]).astype(np.int64)
@@ -422,6 +440,47 @@ class GpuBackend:
                             torch.from_numpy(off_host).to(self.device), off_host)
         colmap = {i: f"c{i}" for i in names}
         return DRel(table, colmap, list(r.attrs), [], True, keys, keys, B)
+
+    def _exchange_rows(self, d, cols: Dict[int, DeviceColumn], bucket):
+        """Route every row to rank ``bucket % world`` (all-to-all per column).  Ranks first agree
+        on column layouts: string dictionaries are unified (codes remapped on the device) and a
+        validity mask exists on every rank if it exists on any."""
+        import torch
+        from ..parallel.shuffle import exchange
+        ids = list(cols)
+        lay = d.all_gather_object([(c.valid is not None,
+                                    c.dictionary.to_pylist() if c.dictionary is not None else None)
+                                   for c in (cols[i] for i in ids)])
+        datas, valids, dicts = [], [], []
+        for j, i in enumerate(ids):
+            c = cols[i]
+            data = c.data
+            gdict = None
+            if c.dictionary is not None:
+                values = sorted({v for rk in lay for v in (rk[j][1] or [])})
+                pos = {v: k for k, v in enumerate(values)}
+                local = c.dictionary.to_pylist()
+                if local and values != local:
+                    remap = torch.tensor([pos[v] for v in local], dtype=torch.int32,
+                                         device=self.device)
+                    data = remap[data.long()]
+                elif not local:
+                    data = torch.zeros_like(data)
+                gdict = pa.array(values, type=pa.string())
+            need_valid = any(rk[j][0] for rk in lay)
+            v = c.valid
+            if need_valid and v is None:
+                v = torch.ones(data.shape[0], dtype=torch.uint8, device=self.device)
+            datas.append(data)
+            valids.append(v if need_valid else None)
+            dicts.append(gdict)
+        dest = (bucket % d.world).to(torch.int32)
+        moved, _ = exchange(datas + valids + [bucket], dest, d.world, ctx=d)
+        k = len(ids)
+        out = {}
+        for j, i in enumerate(ids):
+            out[i] = DeviceColumn(moved[j], moved[k + j], cols[i].atype, dicts[j])
+        return out, moved[2 * k]
 
     # ------------------------------------------------------------------------------------------
     # Joins
@@ -479,7 +538,8 @@ class GpuBackend:
             raise Unsupported("row-producing join over a bucket union")
         out_attrs = list(p.output)
         implied: set = set()
-        rstart, rlen, rbk = self._ranges(left, left.conds, implied)
+        with stage("join.ranges"):
+            rstart, rlen, rbk = self._ranges(left, left.conds, implied)
         jp, col_info, descs, keep = self._join_params(
             left, right, lk, rk, p.condition,
             lconds=[c for c in left.conds if id(c) not in implied])
@@ -536,10 +596,16 @@ class GpuBackend:
             res = self._scan_agg(self._rel(child), fns, group)
         sums, cnts, mins, maxs, G, gbase, gdict, gtype = res
         d = self._dist()
-        if d is not None and d.world > 1:
-            sums, cnts, mins, maxs = d.all_reduce_agg(sums, cnts, mins, maxs)
         A = len(fns) + 1  # + implicit count(*)
-        s, c, mn, mx = (x.reshape(G, A) for x in K.agg_to_host(sums, cnts, mins, maxs))
+        if d is not None and d.world > 1:
+            with stage("agg.all_reduce"):
+                if group is not None:
+                    sums, cnts, mins, maxs, G, gbase, gdict, gtype = self._agree_groups(
+                        d, sums, cnts, mins, maxs, G, gbase, gdict, gtype, A)
+                sums, cnts, mins, maxs = d.all_reduce_agg(sums, cnts, mins, maxs)
+        with stage("agg.d2h"):
+            host = K.agg_to_host(sums, cnts, mins, maxs)
+        s, c, mn, mx = (x.reshape(G, A) for x in host)
         rows = [g for g in range(G) if c[g, A - 1] > 0] if group is not None else [0]
         vals = {}
         for i, fn in enumerate(fns):
@@ -563,6 +629,41 @@ class GpuBackend:
             except (pa.ArrowInvalid, pa.ArrowTypeError):
                 arrays.append(pa.array(vlist))
         return pa.Table.from_arrays(arrays, names=[a.name for a in final.output])
+
+    def _agree_groups(self, d, sums, cnts, mins, maxs, G, gbase, gdict, gtype, A):
+        """Re-key grouped partials onto the union group domain of all ranks.
+
+        Every rank aggregated only its own buckets (index) or files (non-index), so its [G, A]
+        partials are laid out over its *local* domain — integer range ``[gbase, gbase+G)`` or the
+        rank's own string dictionary.  The ranks exchange those domains (one small object
+        all-gather), scatter their rows into the union layout, and only then run the element-wise
+        all-reduce.  Ranks that saw no rows do not contribute a domain."""
+        import torch
+        live_here = bool(cnts.view(G, A)[:, A - 1].sum().item() > 0)
+        infos = d.all_gather_object((G, gbase, gdict.to_pylist() if gdict is not None else None,
+                                     gtype, live_here))
+        live = [x for x in infos if x[4]]
+        if not live:
+            z = self._empty_agg(A, 1)
+            return (*z, 1, 0, None, gtype)
+        if any(x[2] is not None for x in live):
+            values = sorted({v for x in live for v in (x[2] or [])})
+            pos = {v: i for i, v in enumerate(values)}
+            Gg, base, new_dict = len(values), 0, pa.array(values, type=pa.string())
+            idx = [pos[v] for v in gdict.to_pylist()] if (live_here and gdict is not None) else []
+        else:
+            base = min(x[1] for x in live)
+            Gg = max(x[1] + x[0] for x in live) - base
+            new_dict = None
+            idx = list(range(gbase - base, gbase - base + G)) if live_here else []
+        gt = next(x[3] for x in live if x[3] is not None) if any(x[3] is not None for x in live) \
+            else gtype
+        s2, c2, mn2, mx2 = self._empty_agg(A, Gg)
+        if idx:
+            it = torch.tensor(idx, dtype=torch.int64, device=self.device)
+            for dst, src in ((s2, sums), (c2, cnts), (mn2, mins), (mx2, maxs)):
+                dst.view(Gg, A)[it] = src.view(G, A)[:len(idx)]
+        return s2, c2, mn2, mx2, Gg, base, new_dict, gt
 
     def _agg_output(self, e, group, gvals, vals, nrows):
         inner = e.child if isinstance(e, E.Alias) else e
@@ -602,10 +703,15 @@ class GpuBackend:
                     dom = (int(lo.item()), int(hi.item()) - int(lo.item()) + 1)
                 self._domains[ck] = (c, dom)
             base, G = dom
-            if G == 0:
-                return None
-        if G > limit:
+        too_big = G > limit
+        d = self._dist()
+        if d is not None and d.world > 1:
+            # data-dependent fallbacks must be unanimous, or ranks diverge in their collectives
+            too_big = any(d.all_gather_object(too_big))
+        if too_big:
             raise Unsupported("group domain too large for LDS aggregation")
+        if G == 0:
+            return None
         return None, max(G, 1), base, c.dictionary, c.atype
 
     def _agg_specs(self, fns, col_info):
@@ -620,7 +726,8 @@ class GpuBackend:
     def _scan_agg(self, r: DRel, fns, group):
         col_info, descs = self._column_infos([(r, 0)])
         implied: set = set()
-        rstart, rlen, _ = self._ranges(r, r.conds, implied)
+        with stage("scan.ranges"):
+            rstart, rlen, _ = self._ranges(r, r.conds, implied)
         bound = CP.bind(CP.to_cnf([c for c in r.conds if id(c) not in implied]), col_info,
                         self.device)
         specs = self._agg_specs(fns, col_info)
@@ -643,11 +750,12 @@ class GpuBackend:
         if bound.always_false:
             out = self._empty_agg(len(specs), G)
         else:
-            tp = K.ranges_to_tiles(rlen)
-            if HyperspaceConf.codegen_enabled(self.session.conf):
-                out = jit.scan_agg(p, rstart, rlen, tp, self._compacts(descs))
-            else:
-                out = K.scan_agg(p, rstart, rlen, tp)
+            with stage("scan.agg_kernel"):
+                tp = K.ranges_to_tiles(rlen)
+                if HyperspaceConf.codegen_enabled(self.session.conf):
+                    out = jit.scan_agg(p, rstart, rlen, tp, self._compacts(descs))
+                else:
+                    out = K.scan_agg(p, rstart, rlen, tp)
         return (*out, G, gbase, gdict, gtype)
 
     def _compacts(self, descs: Dict[int, DeviceColumn]) -> Optional[dict]:
@@ -706,8 +814,11 @@ class GpuBackend:
         return None, hi - lo, lo, None, specs[0][4]
 
     def _join_agg_pair(self, node, left: DRel, right: DRel, lk, rk, fns, group, G, gbase):
-        # drive the kernel from the smaller side (the appended part of a hybrid scan is small)
-        if right.table.num_rows * 4 < left.table.num_rows:
+        # drive the kernel from a much smaller side (the appended part of a hybrid scan).  Only
+        # then: one work item per driving row is cheapest when each finds few matches, so a
+        # many-to-one pair like lineitem⋈orders (4:1) keeps the many side driving — swapping it
+        # made TPC-H Q3 2.5x slower on MI355X (profiles/bench_sf100_r1_v5.json)
+        if right.table.num_rows * 64 < left.table.num_rows:
             left, right, lk, rk = right, left, rk, lk
         implied: set = set()
         rstart, rlen, rbk = self._ranges(left, left.conds, implied)
@@ -728,10 +839,11 @@ class GpuBackend:
                 right.table.num_rows == 0:
             return self._empty_agg(len(specs), G)
         max_tiles = K.join_max_tiles(left.table.num_rows, rlen.numel())
-        if HyperspaceConf.codegen_enabled(self.session.conf):
-            return jit.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles,
-                                self._compacts(descs))
-        return K.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles)
+        with stage("join.agg_kernel"):
+            if HyperspaceConf.codegen_enabled(self.session.conf):
+                return jit.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles,
+                                    self._compacts(descs))
+            return K.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles)
 
 
 def _combine_aggs(a, b):

@@ -35,8 +35,8 @@ CACHE_DIR = os.environ.get("HS_JIT_CACHE", os.path.join(_HERE, "_native", "jitca
 
 BLOCK = 256
 SCAN_ITEMS = int(os.environ.get("HS_JIT_SCAN_ITEMS", "4"))
-# 512-row join tiles on a 4096-block grid measured best on MI355X (scripts/microbench_join.py,
-# profiles/microbench_join_r1.jsonl): short per-tile latency chains, 16 blocks/CU in flight
+# 512-row join tiles on a 16384-block grid measured best on MI355X (scripts/microbench_join.py,
+# profiles/microbench_join_r1*.jsonl): short per-tile latency chains, many blocks per CU in flight
 JOIN_ITEMS = int(os.environ.get("HS_JIT_JOIN_ITEMS", "2"))
 JOIN_BLOCK = int(os.environ.get("HS_JIT_JOIN_BLOCK", "256"))
 JOIN_LDS_KEYS = int(os.environ.get("HS_JIT_JOIN_LDS_KEYS", "2048"))

@@ -52,10 +52,44 @@ def build_from_source(session, rel, files: List[str], columns: List[str], indexe
         return device_build_from_source(session, rel, files, columns, indexed, num_buckets,
                                         out_path, lineage_ids, mode)
     t = read_index_input(rel, files, columns, lineage_ids)
+    dist = getattr(session, "dist", None)
+    if dist is not None and dist.world > 1:
+        return _spmd_host_write(session, dist, t, out_path, num_buckets, indexed, mode)
     return write_bucketed_table(t, out_path, num_buckets, indexed, mode,
                                 HyperspaceConf.index_file_codec(session.conf),
                                 HyperspaceConf.index_row_group_rows(session.conf),
                                 job_uuid=str(uuid.uuid4()))
+
+
+def _spmd_host_write(session, dist, t: pa.Table, out_path: str, num_buckets: int,
+                     indexed: List[str], mode: str) -> List[str]:
+    """Host oracle under ``torch.distributed``: every rank hashes the full input (it is the
+    correctness reference, not the fast path) and writes only the buckets it owns
+    (``b % world == rank``), as task ``rank`` of one job — one file per bucket overall, the layout
+    the device pipeline produces with its all-to-all."""
+    import os
+    err = None
+    if dist.rank == 0:
+        local = P.to_local(out_path)
+        if mode == "overwrite" and os.path.exists(local):
+            import shutil
+            shutil.rmtree(local)
+        elif mode == "errorifexists" and os.path.exists(local):
+            err = f"path {out_path} already exists"
+        os.makedirs(local, exist_ok=True)
+    # one collective carries the job id and the coordinator's verdict, so no rank is left
+    # waiting in a barrier the others never reach
+    job, err = dist.broadcast_object((str(uuid.uuid4()), err) if dist.rank == 0 else None)
+    if err is not None:
+        from ..exceptions import HyperspaceException
+        raise HyperspaceException(err)
+    owned = {b for b in range(num_buckets) if b % dist.world == dist.rank}
+    out = write_bucketed_table(t, out_path, num_buckets, indexed, "append",
+                               HyperspaceConf.index_file_codec(session.conf),
+                               HyperspaceConf.index_row_group_rows(session.conf),
+                               task_id=dist.rank, job_uuid=job, buckets_to_write=owned)
+    dist.barrier()
+    return out
 
 
 def group_by_bucket(files: List[str]) -> Dict[int, List[str]]:

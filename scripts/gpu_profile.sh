@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 cd /tmp && export TMPDIR=/tmp
 REPO="${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p "$REPO/gpurun_out/prof"
-export HS_BENCH_DIR=/tmp/hs_bench
+export HS_BENCH_DIR=/tmp/hs_bench HS_PROFILE=1
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$REPO/gpurun_out/prof" -o run -- \
   python3 "$REPO/bench.py" --steps 10 --warmup 2 --no-crosscheck > "$REPO/gpurun_out/prof/bench.json" 2> "$REPO/gpurun_out/prof/bench.log"
 rc=$?
