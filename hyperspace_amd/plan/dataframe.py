@@ -83,7 +83,10 @@ class DataFrame:
     def __getattr__(self, name):
         if name.startswith("_") or name in ("session", "plan"):
             raise AttributeError(name)
-        return self[name]
+        try:
+            return self[name]
+        except HyperspaceException as e:  # PySpark semantics: unknown attribute -> AttributeError
+            raise AttributeError(str(e)) from None
 
     def _resolve(self, e: E.Expression, plan: L.LogicalPlan = None) -> E.Expression:
         plan = plan or self.plan
@@ -147,6 +150,9 @@ class DataFrame:
     def drop(self, *names) -> "DataFrame":
         keep = [a for a in self.plan.output if a.name not in names]
         return DataFrame(self.session, L.Project(keep, self.plan))
+
+    def crossJoin(self, other: "DataFrame") -> "DataFrame":
+        return self.join(other, None, "cross")
 
     def join(self, other: "DataFrame", on=None, how: str = "inner") -> "DataFrame":
         how = {"left_outer": "left", "leftouter": "left", "right_outer": "right",

@@ -132,8 +132,8 @@ def test_spmd_device_executor(tmp_path, spmd_data, device):
 
     def oracle(key, aggs):
         g = j.group_by(key).aggregate(aggs)
-        return sorted(zip(*[g.column(c).to_pylist() for c in g.column_names[-1:] +
-                            g.column_names[:-1]]))
+        names = [key] + [f"{c}_{fn}" for c, fn in aggs]
+        return sorted(zip(*[g.column(c).to_pylist() for c in names]))
     exp_s = oracle("s", [("v", "sum"), ("v", "count")])
     exp_w = oracle("w", [("v", "sum"), ("v", "count")])
     exp_sm = oracle("s", [("v", "sum"), ("v", "min")])
