@@ -43,11 +43,14 @@ class CpuBackend:
     def __init__(self, session):
         self.session = session
         self.metrics: Dict[str, float] = {}
+        self.last_path = None         # "host" once a query ran (GpuBackend: native / fallback)
+        self.fallback_reason = None
 
     # -- public -------------------------------------------------------------------------------
     def collect(self, plan: X.SparkPlan) -> pa.Table:
         parts = self.execute(plan)
         t = _concat(parts, plan.output)
+        self.last_path = "host"
         return pa.Table.from_arrays(t.columns, names=[a.name for a in plan.output])
 
     def execute(self, p: X.SparkPlan) -> List[pa.Table]:

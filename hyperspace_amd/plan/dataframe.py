@@ -336,10 +336,21 @@ def _fix_self_join_condition(cond: E.Expression, remap: dict) -> E.Expression:
     return cond.transform_up(fn)
 
 
+def _cell(v) -> str:
+    """Spark's cell rendering: null, arrays as ``[a, b]``, booleans lower-case."""
+    if v is None:
+        return "null"
+    if isinstance(v, (list, tuple)):
+        return "[" + ", ".join(_cell(x) for x in v) + "]"
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    return str(v)
+
+
 def show_string(t: pa.Table, truncate: bool = True) -> str:
     """Spark ``Dataset.showString`` table layout (right-aligned cells)."""
     names = t.column_names
-    rows = [["null" if v is None else str(v) for v in r] for r in
+    rows = [[_cell(v) for v in r] for r in
             zip(*[c.to_pylist() for c in t.columns])] if t.num_columns else []
     if truncate:
         rows = [[v if len(v) <= 20 else v[:17] + "..." for v in r] for r in rows]
