@@ -48,6 +48,8 @@ JOIN_EAGER = os.environ.get("HS_JIT_JOIN_EAGER", "0") == "1"
 # stage the right side's columns of each tile's key span in LDS with the keys
 JOIN_STAGE_RIGHT = os.environ.get("HS_JIT_JOIN_STAGE_RIGHT", "0") == "1"
 SCAN_EAGER = os.environ.get("HS_JIT_SCAN_EAGER", "0") == "1"
+# software-pipeline the join's tile loop (next tile's batch loads overlap this tile's work)
+JOIN_PIPELINE = os.environ.get("HS_JIT_JOIN_PIPELINE", "1") == "1"
 
 _CTYPE = {NL.I8: "signed char", NL.I16: "short", NL.I32: "int", NL.I64: "long long",
           NL.F32: "float", NL.F64: "double", NL.BOOL: "unsigned char", NL.U32: "unsigned int",
@@ -538,7 +540,7 @@ def join_agg_shape(p: NL.JoinParams, compacts=None) -> tuple:
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
     return ("join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey, p.key_is_float,
-            JOIN_ITEMS, JOIN_LDS_KEYS, JOIN_EAGER, JOIN_BLOCK, JOIN_STAGE_RIGHT)
+            JOIN_ITEMS, JOIN_LDS_KEYS, JOIN_EAGER, JOIN_BLOCK, JOIN_STAGE_RIGHT, JOIN_PIPELINE)
 
 
 def _key_expr(var: str, is_float: bool) -> str:
@@ -610,13 +612,20 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
     for it in range(NI):
         b.append(f"{ind}const i64 lr{it} = row0 + {it * BLOCK} + threadIdx.x;")
         b.append(f"{ind}const bool la{it} = {it * BLOCK} + (i64)threadIdx.x < rows;")
-    # (1) left batch + this thread's right keys, issued together
+    # (1) left batch + this thread's right keys, issued together.  `batch` collects the loads
+    # and `fields` the registers they fill, so the pipelined variant can issue the NEXT tile's
+    # batch while this tile searches and gathers.
+    batch: List[str] = []
+    fields: List[Tuple[str, str]] = []
     for it in range(NI):
         g2 = _Gen(args, cols, split, (f"lr{it}", "j"))
         blk: List[str] = []
         for s in left_first:
             g2.load(s, f"la{it}", blk, ind)
-        b += [_rename(x, left_first, it) for x in blk]
+            fields.append((_CTYPE[cols[s][0]], f"x{s}_{it}"))
+            if cols[s][1]:
+                fields.append(("bool", f"n{s}_{it}"))
+        batch += [_rename(x, left_first, it) for x in blk]
     # right columns of the span are staged in LDS with the keys (one coalesced batch), so the
     # match rounds read them from LDS instead of a dependent HBM gather at j
     staged_cols = right_all if JOIN_STAGE_RIGHT else []
@@ -627,14 +636,22 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
             b.insert(1, f"  __shared__ unsigned char sn{s}[{LDS_KEYS}];")
     for q in range(KEYS_PER_THREAD):
         off = f"{q * BLOCK} + (i64)threadIdx.x"
-        b.append(f"{ind}const bool sa{q} = staged && {off} < re - rs;")
-        b.append(f"{ind}const u64 sk{q} = sa{q} ? "
-                 f"{_key_expr(gen.value(rk, f'rs + {off}'), fl)} : 0ull;")
+        batch.append(f"{ind}const bool sa{q} = staged && {off} < re - rs;")
+        batch.append(f"{ind}const u64 sk{q} = sa{q} ? "
+                     f"{_key_expr(gen.value(rk, f'rs + {off}'), fl)} : 0ull;")
+        fields += [("bool", f"sa{q}"), ("u64", f"sk{q}")]
         for s in staged_cols:
             ct = _CTYPE[cols[s][0]]
-            b.append(f"{ind}const {ct} svv{s}_{q} = sa{q} ? {gen.value(s, f'rs + {off}')} : ({ct})0;")
+            batch.append(f"{ind}const {ct} svv{s}_{q} = sa{q} ? {gen.value(s, f'rs + {off}')} : ({ct})0;")
+            fields.append((ct, f"svv{s}_{q}"))
             if cols[s][1]:
-                b.append(f"{ind}const unsigned char snv{s}_{q} = sa{q} ? {gen.vptr(s)}[rs + {off}] : 0;")
+                batch.append(f"{ind}const unsigned char snv{s}_{q} = sa{q} ? {gen.vptr(s)}[rs + {off}] : 0;")
+                fields.append(("unsigned char", f"snv{s}_{q}"))
+    pre: List[str] = []
+    if JOIN_PIPELINE:
+        b, pre = _pipeline_tiles(b, batch, fields, NI, BLOCK, LDS_KEYS)
+    else:
+        b += batch
     for it in range(NI):
         g2 = _Gen(args, cols, split, (f"lr{it}", "j"))
         cond = _rename(g2.cnf(lpreds), left_first, it)
@@ -710,11 +727,49 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
               f"{_key_expr(gen.value(rk, f'j{it}'), fl)}) == k{it}; }}"]
     b += ["    }", "    __syncthreads();", "  }"]
     b += _flush(aggs, grouped, BLOCK)
-    src = (_PRELUDE + args.struct_src() +
+    src = (_PRELUDE + args.struct_src() + "\n".join(pre) +
            f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_join_agg(Args a) {{\n' +
            "\n".join(b) + "\n}\n")
     lds = (len(aggs) * p.num_groups * 32) if grouped else 0
     return Kernel(src, "hs_jit_join_agg", args, lds, BLOCK)
+
+
+def _pipeline_tiles(b: List[str], batch: List[str], fields, NI: int, BLOCK: int,  # noqa: N803
+                    LDS_KEYS: int):  # noqa: N803
+    """Software-pipeline the tile loop: tile t+1's left batch and right keys are loaded while
+    tile t runs its LDS search and match rounds, which takes one dependent HBM round trip off
+    every tile's critical path.  Vector-memory loads retire in issue order, so the prefetch
+    (issued first) never delays the current tile's own gathers.
+
+    ``b`` holds the kernel prologue up to and including the per-tile ``lr/la`` lines; the
+    batch loads move into a device function returning a register struct, and the tile body
+    reads the current struct's fields under their usual names."""
+    head = b[:b.index("  for (i64 t = t0; t < t1; ++t) {")]
+    body_la = [x for x in b[len(head):] if x.lstrip().startswith(("const i64 lr",
+                                                                   "const bool la"))]
+    pre = ["struct Batch {"] + [f"  {ct} {n};" for ct, n in fields] + ["};",
+           "__device__ __forceinline__ Batch load_batch(const Args& a, i64 row0, i64 rows, "
+           "i64 rs, i64 re) {",
+           f"  const bool staged = re - rs <= {LDS_KEYS};"]
+    pre += [x.replace("    ", "  ", 1) for x in body_la + batch]
+    pre += ["  Batch B_;"] + [f"  B_.{n} = {n};" for _, n in fields] + ["  return B_;", "}", ""]
+    out = list(head)
+    out += ["  i64 c_row0 = n_row0, c_rows = n_rows, c_rs = n_rs, c_re = n_re;",
+            "  if (t0 + 1 < t1) { n_row0 = a.spans[4 * t0 + 4]; n_rows = a.spans[4 * t0 + 5];",
+            "                     n_rs = a.spans[4 * t0 + 6]; n_re = a.spans[4 * t0 + 7]; }",
+            "  Batch cur = load_batch(a, c_row0, c_rows, c_rs, c_re);",
+            "  for (i64 t = t0; t < t1; ++t) {",
+            "    const i64 row0 = c_row0, rows = c_rows, rs = c_rs, re = c_re;",
+            f"    const bool staged = re - rs <= {LDS_KEYS};",
+            "    Batch nxt = cur;",
+            "    if (t + 1 < t1) nxt = load_batch(a, n_row0, n_rows, n_rs, n_re);",
+            "    c_row0 = n_row0; c_rows = n_rows; c_rs = n_rs; c_re = n_re;",
+            "    if (t + 2 < t1) { n_row0 = a.spans[4 * t + 8]; n_rows = a.spans[4 * t + 9];",
+            "                      n_rs = a.spans[4 * t + 10]; n_re = a.spans[4 * t + 11]; }"]
+    out += body_la
+    out += [f"    const {ct} {n} = cur.{n};" for ct, n in fields]
+    out += ["    cur = nxt;"]
+    return out, pre
 
 
 def join_lds_keys() -> int:
