@@ -99,6 +99,94 @@ __global__ __launch_bounds__(256) void hs_join_spans_kernel(
   spans[4 * t + 3] = re;
 }
 
+// ---- sampled span search (generated-kernel path) ------------------------------------------
+// A sparse index over the right side — every JN_SAMPLE-th key of each bucket, built per join in
+// one strided pass (~1/64 of the right keys) — is small enough to stay in L2 / Infinity Cache.
+// A tile's span start is then a search of the cached samples plus one <=64-key window in HBM,
+// and the span end gallops forward from the start (spans are short for FK joins): ~9 HBM
+// transactions per tile instead of ~40 dependent random reads for two full binary searches.
+#define JN_SAMPLE 64
+
+__global__ __launch_bounds__(256) void hs_join_sample_kernel(
+    ColDesc rk, const int64_t* __restrict__ roff, const int64_t* __restrict__ soff, int B,
+    int64_t nsamples, uint64_t* __restrict__ samples, int is_float) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsamples || i >= soff[B]) return;  // nsamples: host-side bound of soff[B]
+  int lo = 0, hi = B;  // bucket b with soff[b] <= i < soff[b+1]
+  while (hi - lo > 1) {
+    const int md = (lo + hi) >> 1;
+    if (soff[md] <= i) lo = md; else hi = md;
+  }
+  const int64_t row = roff[lo] + (i - soff[lo]) * JN_SAMPLE;
+  // nulls sort first and never match: the minimum image keeps the samples ordered
+  samples[i] = col_valid(rk, row) ? join_key(rk, row, is_float != 0) : 0ull;
+}
+
+// first row in [bs, be) whose key is >= k (nulls count as smaller), via the bucket's samples
+__device__ __forceinline__ int64_t sampled_lower(const ColDesc& c, const uint64_t* smp, int64_t ns,
+                                                 int64_t bs, int64_t be, uint64_t k, bool fl) {
+  int64_t lo = 0, hi = ns;  // first sample >= k
+  while (lo < hi) {
+    const int64_t md = (lo + hi) >> 1;
+    if (smp[md] < k) lo = md + 1; else hi = md;
+  }
+  const int64_t wlo = lo == 0 ? bs : bs + (lo - 1) * JN_SAMPLE + 1;
+  const int64_t whi = lo == ns ? be : min(be, bs + lo * JN_SAMPLE);
+  return rkey_bound(c, wlo, whi, k, false, fl);
+}
+
+// first row in [from, be) whose key is > k, galloping forward from `from`
+__device__ __forceinline__ int64_t gallop_upper(const ColDesc& c, int64_t from, int64_t be,
+                                                uint64_t k, bool fl) {
+  int64_t lo = from, step = 1;
+  while (lo < be) {
+    const int64_t probe = min(be - 1, lo + step - 1);
+    const bool le = !col_valid(c, probe) || join_key(c, probe, fl) <= k;
+    if (!le) return rkey_bound(c, lo, probe, k, true, fl);
+    lo = probe + 1;
+    step <<= 1;
+  }
+  return be;
+}
+
+__global__ __launch_bounds__(256) void hs_join_spans_sampled_kernel(
+    JoinParams p, const int64_t* __restrict__ rstart, const int64_t* __restrict__ rlen,
+    const int32_t* __restrict__ rbucket, const int64_t* __restrict__ roff,
+    const int64_t* __restrict__ soff, const uint64_t* __restrict__ samples, int R,
+    const int64_t* __restrict__ tile_prefix, int64_t* __restrict__ spans, int tile_rows) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= tile_prefix[R]) return;
+  const int r = tile_range_of(tile_prefix, R, t);
+  const int64_t off = (t - tile_prefix[r]) * tile_rows;
+  const int64_t row0 = rstart[r] + off;
+  const int64_t rows = min((int64_t)tile_rows, rlen[r] - off);
+  const bool fl = p.key_is_float != 0;
+  const int b = rbucket[r];
+  const int64_t bs = roff[b], be = roff[b + 1];
+  const ColDesc& lk = p.cols[p.lkey];
+  int64_t f = row0;
+  const int64_t l = row0 + rows - 1;
+  if (lk.valid != nullptr) {
+    int64_t lo = row0, hi = row0 + rows;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (!col_valid(lk, mid)) lo = mid + 1; else hi = mid;
+    }
+    f = lo;
+  }
+  int64_t rs = bs, re = bs;
+  if (f <= l) {
+    const uint64_t kmin = join_key(lk, f, fl), kmax = join_key(lk, l, fl);
+    const ColDesc& rk = p.cols[p.rkey];
+    rs = sampled_lower(rk, samples + soff[b], soff[b + 1] - soff[b], bs, be, kmin, fl);
+    re = gallop_upper(rk, rs, be, kmax, fl);
+  }
+  spans[4 * t + 0] = row0;
+  spans[4 * t + 1] = rows;
+  spans[4 * t + 2] = rs;
+  spans[4 * t + 3] = re;
+}
+
 struct JTile {
   int64_t row0, rows, rs, re;
   bool staged;
@@ -362,6 +450,25 @@ int hs_join_spans(const JoinParams* p, const int64_t* rstart, const int64_t* rle
   return launch_spans(p, rstart, rlen, rbucket, roff, R, tile_prefix, max_tiles, spans,
                       (hipStream_t)stream, tile_rows);
 }
+
+// Sampled variant: soff (B+1, device) = per-bucket sample offsets, soff[b+1]-soff[b] =
+// ceil(rows_b / JN_SAMPLE); samples = scratch of nsamples >= soff[B] uint64 (filled here).
+int hs_join_spans_sampled(const JoinParams* p, const int64_t* rstart, const int64_t* rlen,
+                          const int32_t* rbucket, const int64_t* roff, const int64_t* soff, int B,
+                          int64_t nsamples, uint64_t* samples, int R, const int64_t* tile_prefix,
+                          int64_t max_tiles, int64_t* spans, int tile_rows, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (nsamples > 0)
+    hipLaunchKernelGGL(hs_join_sample_kernel, dim3((unsigned)((nsamples + 255) / 256)), dim3(256),
+                       0, s, p->cols[p->rkey], roff, soff, B, nsamples, samples, p->key_is_float);
+  if (max_tiles > 0)
+    hipLaunchKernelGGL(hs_join_spans_sampled_kernel, dim3((unsigned)((max_tiles + 255) / 256)),
+                       dim3(256), 0, s, *p, rstart, rlen, rbucket, roff, soff, samples, R,
+                       tile_prefix, spans, tile_rows);
+  return (int)hipGetLastError();
+}
+
+int hs_join_sample_stride() { return JN_SAMPLE; }
 
 int hs_join_params_size() { return (int)sizeof(JoinParams); }
 int hs_join_tile_rows() { return JN_TILE; }

@@ -11,8 +11,9 @@ coefficients, IN-set pointers) are kernel arguments, so a shape compiles once an
 query of that shape (e.g. TPC-H Q6 with new dates) reuses the code object.
 
 The generated kernels write the same per-block partials as the AOT ones and share the AOT
-deterministic final reduction (``hs_agg_final``), and the join kernel reuses the AOT per-tile span
-search (``hs_join_spans_kernel``): codegen only replaces the per-row inner loops.
+deterministic final reduction (``hs_agg_final``), and the join kernel consumes the AOT per-tile
+span records (``hs_join_spans_sampled``: cached sparse samples + galloping): codegen only
+replaces the per-row inner loops.
 
 Kernel arguments are one by-value struct whose fields are all 8 bytes wide, packed here with
 ``struct``; the runtime passes it with ``HIP_LAUNCH_PARAM_BUFFER_POINTER``.
@@ -46,7 +47,7 @@ JOIN_GRID = int(os.environ.get("HS_JIT_JOIN_GRID", "16384"))
 # sweep (profiles/microbench_join_r1c.jsonl) favoured lazy loads for both kernels
 JOIN_EAGER = os.environ.get("HS_JIT_JOIN_EAGER", "0") == "1"
 # stage the right side's columns of each tile's key span in LDS with the keys
-JOIN_STAGE_RIGHT = os.environ.get("HS_JIT_JOIN_STAGE_RIGHT", "0") == "1"
+JOIN_STAGE_RIGHT = os.environ.get("HS_JIT_JOIN_STAGE_RIGHT", "1") == "1"
 SCAN_EAGER = os.environ.get("HS_JIT_SCAN_EAGER", "0") == "1"
 # software-pipeline the join's tile loop (next tile's batch loads overlap this tile's work)
 JOIN_PIPELINE = os.environ.get("HS_JIT_JOIN_PIPELINE", "1") == "1"
@@ -790,6 +791,29 @@ def _rename(line: str, slots, it: int) -> str:
     return line
 
 
+_SOFF: Dict[int, tuple] = {}
+
+
+def _sample_offsets(roff):
+    """Per-bucket offsets of the right side's sparse key samples (every ``hs_join_sample_stride``
+    -th key) and a host bound on their count.  Bucket offsets of a device table never change, so
+    this is computed once per right table (keyed by tensor identity, holding a reference)."""
+    import torch
+    hit = _SOFF.get(id(roff))
+    if hit is not None and hit[0] is roff:
+        return hit[1], hit[2]
+    stride = NL.lib().hs_join_sample_stride()
+    n = roff[1:] - roff[:-1]
+    soff = torch.zeros(roff.numel(), dtype=torch.int64, device=roff.device)
+    torch.cumsum((n + stride - 1) // stride, 0, out=soff[1:])
+    B = roff.numel() - 1
+    bound = int(roff[-1].item()) // stride + B  # one sync per right table, then cached
+    if len(_SOFF) > 64:
+        _SOFF.clear()
+    _SOFF[id(roff)] = (roff, soff, bound)
+    return soff, bound
+
+
 def join_agg_values(p: NL.JoinParams, tile_prefix, spans, parts,
                     compacts=None) -> Dict[str, object]:
     v = {"tile_prefix": tile_prefix.data_ptr(), "R": tile_prefix.numel() - 1,
@@ -864,9 +888,13 @@ def join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, max_tiles: int, comp
     tp = K.ranges_to_tiles(rlen, tile)
     mt = (max_tiles * L.hs_join_tile_rows()) // tile + rlen.numel() + 1
     spans = torch.empty(4 * mt, dtype=torch.int64, device=dev)
-    NL.check(L.hs_join_spans(C.byref(p), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
-                             NL.ptr(roff), rstart.numel(), NL.ptr(tp), int(mt),
-                             NL.ptr(spans), tile, NL.stream_ptr()), "hs_join_spans")
+    soff, bound = _sample_offsets(roff)
+    samples = torch.empty(max(bound, 1), dtype=torch.int64, device=dev)
+    NL.check(L.hs_join_spans_sampled(C.byref(p), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
+                                     NL.ptr(roff), NL.ptr(soff), roff.numel() - 1, bound,
+                                     NL.ptr(samples), rstart.numel(), NL.ptr(tp), int(mt),
+                                     NL.ptr(spans), tile, NL.stream_ptr()),
+             "hs_join_spans_sampled")
     k = kernel_for(join_agg_shape(p, compacts), lambda: gen_join_agg(p, compacts))
     parts = _partials(grid, GA, dev)
     k.launch(grid, join_agg_values(p, tp, spans, parts, compacts), NL.stream_ptr(),
