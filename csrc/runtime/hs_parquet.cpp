@@ -1,0 +1,661 @@
+// Native Parquet page layer for the MI355X decode path (SURVEY.md §2.3 K1, §7.1 "Parquet
+// reader/writer page layer, thrift metadata parsed on the host in C++").
+//
+// Host side only: footer + page headers (Thrift compact protocol), page decompression
+// (UNCOMPRESSED / SNAPPY; other codecs are reported as unsupported so the caller falls back),
+// and a pre-parse of every RLE/bit-packed hybrid stream (definition levels, dictionary indices)
+// into a flat *run table*.  The decompressed page bytes and the run table are what travel to the
+// GPU; expanding runs into values (dictionary gather, bit unpacking, PLAIN copies) happens in
+// csrc/kernels/parquet_decode.hip.  Dictionary-encoded data therefore crosses PCIe at its
+// encoded width (e.g. 6 bits per TPC-H l_quantity instead of 64).
+//
+// Scope: flat schemas (no repetition), physical types INT32 / INT64 / FLOAT / DOUBLE,
+// encodings PLAIN and PLAIN_DICTIONARY / RLE_DICTIONARY, data pages V1 and V2.  Anything else
+// returns HS_PQ_UNSUPPORTED and the Python side reads that column with pyarrow instead.
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+enum : int {
+  HS_PQ_OK = 0,
+  HS_PQ_IO = -1,
+  HS_PQ_CORRUPT = -2,
+  HS_PQ_UNSUPPORTED = -3,
+  HS_PQ_CAPACITY = -4,
+};
+
+// ------------------------------------------------------------------ Thrift compact protocol
+struct TReader {
+  const uint8_t* p;
+  const uint8_t* end;
+  bool bad = false;
+
+  uint8_t byte() {
+    if (p >= end) { bad = true; return 0; }
+    return *p++;
+  }
+  uint64_t varint() {
+    uint64_t v = 0;
+    for (int shift = 0; shift < 64; shift += 7) {
+      const uint8_t b = byte();
+      v |= (uint64_t)(b & 0x7f) << shift;
+      if (!(b & 0x80)) return v;
+    }
+    bad = true;
+    return 0;
+  }
+  int64_t zigzag() {
+    const uint64_t v = varint();
+    return (int64_t)(v >> 1) ^ -(int64_t)(v & 1);
+  }
+  std::string binary() {
+    const uint64_t n = varint();
+    if ((uint64_t)(end - p) < n) { bad = true; return {}; }
+    std::string s((const char*)p, n);
+    p += n;
+    return s;
+  }
+  // field header: returns type (0 = stop); id updated from the delta or an explicit i16
+  int field(int16_t& id) {
+    const uint8_t b = byte();
+    if (b == 0) return 0;
+    const int type = b & 0x0f;
+    const int delta = b >> 4;
+    id = delta ? (int16_t)(id + delta) : (int16_t)zigzag();
+    return type;
+  }
+  void list_header(int& elem_type, int64_t& size) {
+    const uint8_t b = byte();
+    elem_type = b & 0x0f;
+    size = b >> 4;
+    if (size == 15) size = (int64_t)varint();
+  }
+  void skip(int type) {
+    switch (type) {
+      case 1: case 2: return;                       // bool (value in the type nibble)
+      case 3: byte(); return;
+      case 4: case 5: case 6: zigzag(); return;
+      case 7: p += 8; if (p > end) bad = true; return;
+      case 8: binary(); return;
+      case 9: case 10: {
+        int et; int64_t n; list_header(et, n);
+        for (int64_t i = 0; i < n && !bad; ++i) skip_elem(et);
+        return;
+      }
+      case 11: {
+        const uint64_t n = varint();
+        if (n == 0) return;
+        const uint8_t kv = byte();
+        for (uint64_t i = 0; i < n && !bad; ++i) { skip_elem(kv >> 4); skip_elem(kv & 0x0f); }
+        return;
+      }
+      case 12: skip_struct(); return;
+      default: bad = true;
+    }
+  }
+  void skip_elem(int type) {
+    if (type == 1 || type == 2) { byte(); return; }  // bools inside containers take a byte
+    skip(type);
+  }
+  void skip_struct() {
+    int16_t id = 0;
+    for (int t; (t = field(id)) != 0 && !bad;) skip(t);
+  }
+};
+
+struct SchemaEl {
+  int type = -1, type_length = 0, repetition = 0, num_children = 0;
+  std::string name;
+};
+
+struct ChunkMeta {
+  int type = -1, codec = 0;
+  int64_t num_values = 0, total_compressed = 0, total_uncompressed = 0;
+  int64_t data_page_offset = 0, dict_page_offset = -1;
+  std::vector<std::string> path;
+};
+
+struct RowGroupMeta {
+  int64_t num_rows = 0;
+  std::vector<ChunkMeta> cols;
+};
+
+struct File {
+  int fd = -1;
+  int64_t size = 0;
+  int64_t num_rows = 0;
+  std::vector<SchemaEl> schema;      // flattened, as stored
+  std::vector<int> leaves;           // schema index of each leaf column
+  std::vector<RowGroupMeta> rgs;
+  std::string error;
+};
+
+void parse_schema_el(TReader& r, SchemaEl& s) {
+  int16_t id = 0;
+  for (int t; (t = r.field(id)) != 0 && !r.bad;) {
+    switch (id) {
+      case 1: s.type = (int)r.zigzag(); break;
+      case 2: s.type_length = (int)r.zigzag(); break;
+      case 3: s.repetition = (int)r.zigzag(); break;
+      case 4: s.name = r.binary(); break;
+      case 5: s.num_children = (int)r.zigzag(); break;
+      default: r.skip(t);
+    }
+  }
+}
+
+void parse_col_meta(TReader& r, ChunkMeta& m) {
+  int16_t id = 0;
+  for (int t; (t = r.field(id)) != 0 && !r.bad;) {
+    switch (id) {
+      case 1: m.type = (int)r.zigzag(); break;
+      case 3: {
+        int et; int64_t n; r.list_header(et, n);
+        for (int64_t i = 0; i < n && !r.bad; ++i) m.path.push_back(r.binary());
+        break;
+      }
+      case 4: m.codec = (int)r.zigzag(); break;
+      case 5: m.num_values = r.zigzag(); break;
+      case 6: m.total_uncompressed = r.zigzag(); break;
+      case 7: m.total_compressed = r.zigzag(); break;
+      case 9: m.data_page_offset = r.zigzag(); break;
+      case 11: m.dict_page_offset = r.zigzag(); break;
+      default: r.skip(t);
+    }
+  }
+}
+
+void parse_row_group(TReader& r, RowGroupMeta& g) {
+  int16_t id = 0;
+  for (int t; (t = r.field(id)) != 0 && !r.bad;) {
+    if (id == 1) {
+      int et; int64_t n; r.list_header(et, n);
+      g.cols.resize((size_t)n);
+      for (int64_t i = 0; i < n && !r.bad; ++i) {
+        int16_t cid = 0;  // ColumnChunk
+        for (int ct; (ct = r.field(cid)) != 0 && !r.bad;) {
+          if (cid == 3) parse_col_meta(r, g.cols[(size_t)i]);
+          else r.skip(ct);
+        }
+      }
+    } else if (id == 3) {
+      g.num_rows = r.zigzag();
+    } else {
+      r.skip(t);
+    }
+  }
+}
+
+bool pread_all(int fd, void* buf, size_t n, int64_t off) {
+  uint8_t* d = (uint8_t*)buf;
+  while (n) {
+    const ssize_t k = pread(fd, d, n, off);
+    if (k <= 0) return false;
+    d += k; n -= (size_t)k; off += k;
+  }
+  return true;
+}
+
+int open_file(const char* path, File& f) {
+  f.fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (f.fd < 0) { f.error = "open failed"; return HS_PQ_IO; }
+  struct stat st;
+  if (fstat(f.fd, &st) != 0 || st.st_size < 12) { f.error = "not a parquet file"; return HS_PQ_IO; }
+  f.size = st.st_size;
+  uint8_t tail[8];
+  if (!pread_all(f.fd, tail, 8, f.size - 8) || memcmp(tail + 4, "PAR1", 4) != 0) {
+    f.error = "missing PAR1 footer";
+    return HS_PQ_CORRUPT;
+  }
+  uint32_t flen;
+  memcpy(&flen, tail, 4);
+  if ((int64_t)flen + 12 > f.size) { f.error = "bad footer length"; return HS_PQ_CORRUPT; }
+  std::vector<uint8_t> meta(flen);
+  if (!pread_all(f.fd, meta.data(), flen, f.size - 8 - flen)) { f.error = "read"; return HS_PQ_IO; }
+  TReader r{meta.data(), meta.data() + meta.size()};
+  int16_t id = 0;
+  for (int t; (t = r.field(id)) != 0 && !r.bad;) {
+    if (id == 2) {
+      int et; int64_t n; r.list_header(et, n);
+      f.schema.resize((size_t)n);
+      for (int64_t i = 0; i < n && !r.bad; ++i) parse_schema_el(r, f.schema[(size_t)i]);
+    } else if (id == 3) {
+      f.num_rows = r.zigzag();
+    } else if (id == 4) {
+      int et; int64_t n; r.list_header(et, n);
+      f.rgs.resize((size_t)n);
+      for (int64_t i = 0; i < n && !r.bad; ++i) parse_row_group(r, f.rgs[(size_t)i]);
+    } else {
+      r.skip(t);
+    }
+  }
+  if (r.bad) { f.error = "corrupt footer"; return HS_PQ_CORRUPT; }
+  for (size_t i = 1; i < f.schema.size(); ++i)
+    if (f.schema[i].num_children == 0) f.leaves.push_back((int)i);
+  return HS_PQ_OK;
+}
+
+// ------------------------------------------------------------------ Snappy (raw block format)
+bool snappy_decompress(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
+  const uint8_t* ip = in;
+  const uint8_t* iend = in + n;
+  uint64_t len = 0;
+  for (int shift = 0; ip < iend; shift += 7) {
+    const uint8_t b = *ip++;
+    len |= (uint64_t)(b & 0x7f) << shift;
+    if (!(b & 0x80)) break;
+    if (shift > 28) return false;
+  }
+  if (len > cap) return false;
+  uint8_t* op = out;
+  uint8_t* oend = out + len;
+  while (ip < iend) {
+    const uint8_t tag = *ip++;
+    const int kind = tag & 3;
+    if (kind == 0) {  // literal
+      size_t l = tag >> 2;
+      if (l >= 60) {
+        const int nb = (int)l - 59;
+        if (ip + nb > iend) return false;
+        l = 0;
+        for (int i = 0; i < nb; ++i) l |= (size_t)ip[i] << (8 * i);
+        ip += nb;
+      }
+      l += 1;
+      if (ip + l > iend || op + l > oend) return false;
+      memcpy(op, ip, l);
+      ip += l; op += l;
+      continue;
+    }
+    size_t l, off;
+    if (kind == 1) {
+      if (ip >= iend) return false;
+      l = 4 + ((tag >> 2) & 7);
+      off = ((size_t)(tag >> 5) << 8) | *ip++;
+    } else if (kind == 2) {
+      if (ip + 2 > iend) return false;
+      l = 1 + (tag >> 2);
+      off = (size_t)ip[0] | ((size_t)ip[1] << 8);
+      ip += 2;
+    } else {
+      if (ip + 4 > iend) return false;
+      l = 1 + (tag >> 2);
+      off = (size_t)ip[0] | ((size_t)ip[1] << 8) | ((size_t)ip[2] << 16) | ((size_t)ip[3] << 24);
+      ip += 4;
+    }
+    if (off == 0 || off > (size_t)(op - out) || op + l > oend) return false;
+    const uint8_t* src = op - off;
+    if (off >= l) {
+      memcpy(op, src, l);
+      op += l;
+    } else {
+      for (size_t i = 0; i < l; ++i) *op++ = src[i];  // overlapping copy (run extension)
+    }
+  }
+  if (op != oend) return false;
+  *out_len = len;
+  return true;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ run table (shared with GPU)
+// One entry per RLE run or (chunk of a) bit-packed run / PLAIN page.  Values are written to
+// out[dst .. dst+count) (dense index space: non-null values for value runs, rows for levels).
+struct HsPqRun {
+  int64_t dst;        // first output index
+  int64_t count;      // values in this run
+  int64_t src;        // byte offset in the page buffer (bit-packed / PLAIN data); RLE: value
+  int32_t kind;       // 0 RLE, 1 bit-packed, 2 PLAIN
+  int32_t bit_width;  // bits per value (bit-packed / RLE); PLAIN: element bytes
+};
+
+struct HsPqChunkInfo {
+  int64_t num_values;     // rows in the chunk
+  int64_t num_nonnull;    // non-null values
+  int64_t dict_off;       // byte offset of the PLAIN dictionary in the buffer (-1: none)
+  int64_t dict_count;
+  int64_t bytes_used;     // bytes of the buffer written
+  int32_t nvalue_runs, nlevel_runs;
+  int32_t dict_encoded;   // 1 if any data page is dictionary-encoded
+  int32_t plain_pages;    // pages stored PLAIN
+};
+
+namespace {
+
+struct Out {
+  uint8_t* buf; int64_t cap; int64_t used = 0;
+  HsPqRun* vruns; int64_t vcap; int64_t nv = 0;
+  HsPqRun* lruns; int64_t lcap; int64_t nl = 0;
+};
+
+constexpr int64_t kChunk = 4096;  // split long runs so each GPU work item stays short
+
+bool push(HsPqRun* runs, int64_t cap, int64_t& n, const HsPqRun& r) {
+  if (n >= cap) return false;
+  runs[n++] = r;
+  return true;
+}
+
+// Parse an RLE/bit-packed hybrid stream of `count` values into runs (dst starts at `dst0`).
+// `base` is the stream's byte offset in the output buffer.  Returns values that are non-zero
+// (only meaningful for def levels, bit width 1) or -1 on error.
+int64_t parse_hybrid(const uint8_t* s, int64_t len, int64_t base, int bw, int64_t count,
+                     int64_t dst0, HsPqRun* runs, int64_t cap, int64_t& n, bool count_ones) {
+  TReader r{s, s + len};
+  int64_t done = 0, ones = 0;
+  const int vbytes = (bw + 7) / 8;
+  while (done < count) {
+    if (r.p >= r.end) return -1;
+    const uint64_t h = r.varint();
+    if (r.bad) return -1;
+    if (h & 1) {  // bit-packed: (h>>1) groups of 8
+      const int64_t groups = (int64_t)(h >> 1);
+      const int64_t nvals = groups * 8;
+      const int64_t nbytes = groups * bw;
+      if (r.end - r.p < nbytes) return -1;
+      const int64_t take = nvals < count - done ? nvals : count - done;
+      const int64_t off = base + (r.p - s);
+      for (int64_t c = 0; c < take; c += kChunk) {   // kChunk is a multiple of 8: byte aligned
+        const int64_t k = take - c < kChunk ? take - c : kChunk;
+        if (!push(runs, cap, n, {dst0 + done + c, k, off + c * bw / 8, 1, bw})) return -2;
+      }
+      if (count_ones) {
+        for (int64_t i = 0; i < take; ++i) ones += (r.p[i >> 3] >> (i & 7)) & 1;
+      }
+      r.p += nbytes;
+      done += take;
+    } else {
+      const int64_t nvals = (int64_t)(h >> 1);
+      uint64_t v = 0;
+      if (r.end - r.p < vbytes) return -1;
+      for (int i = 0; i < vbytes; ++i) v |= (uint64_t)r.p[i] << (8 * i);
+      r.p += vbytes;
+      const int64_t take = nvals < count - done ? nvals : count - done;
+      for (int64_t c = 0; c < take; c += kChunk) {
+        const int64_t k = take - c < kChunk ? take - c : kChunk;
+        if (!push(runs, cap, n, {dst0 + done + c, k, (int64_t)v, 0, bw})) return -2;
+      }
+      if (count_ones && v) ones += take;
+      done += take;
+    }
+  }
+  return ones;
+}
+
+struct PageHdr {
+  int type = -1, usize = 0, csize = 0;
+  int nvals = 0, enc = 0, def_enc = 3, v2_nulls = 0, v2_def_len = 0, v2_rep_len = 0;
+  bool v2 = false, v2_compressed = true;
+  int dict_nvals = 0;
+};
+
+bool parse_page_header(TReader& r, PageHdr& h) {
+  int16_t id = 0;
+  for (int t; (t = r.field(id)) != 0 && !r.bad;) {
+    switch (id) {
+      case 1: h.type = (int)r.zigzag(); break;
+      case 2: h.usize = (int)r.zigzag(); break;
+      case 3: h.csize = (int)r.zigzag(); break;
+      case 5: {  // DataPageHeader
+        int16_t d = 0;
+        for (int dt; (dt = r.field(d)) != 0 && !r.bad;) {
+          if (d == 1) h.nvals = (int)r.zigzag();
+          else if (d == 2) h.enc = (int)r.zigzag();
+          else if (d == 3) h.def_enc = (int)r.zigzag();
+          else r.skip(dt);
+        }
+        break;
+      }
+      case 7: {  // DictionaryPageHeader
+        int16_t d = 0;
+        for (int dt; (dt = r.field(d)) != 0 && !r.bad;) {
+          if (d == 1) h.dict_nvals = (int)r.zigzag();
+          else if (d == 2) h.enc = (int)r.zigzag();
+          else r.skip(dt);
+        }
+        break;
+      }
+      case 8: {  // DataPageHeaderV2
+        h.v2 = true;
+        int16_t d = 0;
+        for (int dt; (dt = r.field(d)) != 0 && !r.bad;) {
+          if (d == 1) h.nvals = (int)r.zigzag();
+          else if (d == 2) h.v2_nulls = (int)r.zigzag();
+          else if (d == 4) h.enc = (int)r.zigzag();
+          else if (d == 5) h.v2_def_len = (int)r.zigzag();
+          else if (d == 6) h.v2_rep_len = (int)r.zigzag();
+          else if (d == 7) h.v2_compressed = (dt == 1);
+          else r.skip(dt);
+        }
+        break;
+      }
+      default: r.skip(t);
+    }
+  }
+  return !r.bad;
+}
+
+int elem_bytes(int type) {
+  switch (type) {
+    case 1: case 4: return 4;   // INT32, FLOAT
+    case 2: case 5: return 8;   // INT64, DOUBLE
+    default: return 0;
+  }
+}
+
+// decompress `csize` bytes at `src` into dst (capacity cap); returns bytes or -1
+int64_t inflate(int codec, const uint8_t* src, int64_t csize, uint8_t* dst, int64_t cap) {
+  if (codec == 0) {
+    if (csize > cap) return -1;
+    memcpy(dst, src, (size_t)csize);
+    return csize;
+  }
+  if (codec == 1) {
+    size_t n = 0;
+    if (!snappy_decompress(src, (size_t)csize, dst, (size_t)cap, &n)) return -1;
+    return (int64_t)n;
+  }
+  return -2;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* hs_pq_error(void* h) { return h ? ((File*)h)->error.c_str() : "null handle"; }
+
+void* hs_pq_open(const char* path) {
+  File* f = new File();
+  if (open_file(path, *f) != HS_PQ_OK) {
+    // keep the handle so the caller can read the error, then close it
+  }
+  return f;
+}
+
+int hs_pq_ok(void* h) { return ((File*)h)->fd >= 0 && ((File*)h)->error.empty() ? 1 : 0; }
+
+void hs_pq_close(void* h) {
+  File* f = (File*)h;
+  if (!f) return;
+  if (f->fd >= 0) close(f->fd);
+  delete f;
+}
+
+int64_t hs_pq_num_rows(void* h) { return ((File*)h)->num_rows; }
+int hs_pq_num_row_groups(void* h) { return (int)((File*)h)->rgs.size(); }
+int64_t hs_pq_row_group_rows(void* h, int rg) { return ((File*)h)->rgs[(size_t)rg].num_rows; }
+int hs_pq_num_columns(void* h) { return (int)((File*)h)->leaves.size(); }
+
+// Leaf column by (top-level) name; -1 if absent or nested.
+int hs_pq_find_column(void* h, const char* name) {
+  File* f = (File*)h;
+  for (size_t i = 0; i < f->leaves.size(); ++i) {
+    if (f->schema[(size_t)f->leaves[i]].name == name) {
+      // flat schema only: root's direct child
+      if (f->schema.size() == f->leaves.size() + 1) return (int)i;
+      return -1;
+    }
+  }
+  return -1;
+}
+
+// physical type, max definition level (0 required / 1 optional), element bytes (0: unsupported)
+int hs_pq_column_info(void* h, int col, int* type, int* max_def, int* ebytes) {
+  File* f = (File*)h;
+  const SchemaEl& s = f->schema[(size_t)f->leaves[(size_t)col]];
+  *type = s.type;
+  *max_def = s.repetition == 1 ? 1 : 0;
+  *ebytes = s.repetition == 2 ? 0 : elem_bytes(s.type);
+  return HS_PQ_OK;
+}
+
+// Upper bounds for one column chunk: buffer bytes, value runs, level runs.
+int hs_pq_chunk_bounds(void* h, int rg, int col, int64_t* buf_bytes, int64_t* vruns,
+                       int64_t* lruns) {
+  File* f = (File*)h;
+  const ChunkMeta& m = f->rgs[(size_t)rg].cols[(size_t)col];
+  const int64_t nv = m.num_values;
+  *buf_bytes = m.total_uncompressed + 64;
+  // a bit-packed header covers >= 8 values; every page may add a partial run per stream
+  *vruns = nv / 8 + nv / kChunk + 1024;
+  *lruns = nv / 8 + nv / kChunk + 1024;
+  return HS_PQ_OK;
+}
+
+// Read, decompress and pre-parse one column chunk.  Data pages land back to back in `buf`
+// (after the dictionary page, if any); vruns/lruns receive the run tables.  Value runs address
+// the dense non-null value index; level runs (optional columns only) address rows.
+int hs_pq_read_chunk(void* h, int rg, int col, uint8_t* buf, int64_t cap, HsPqRun* vruns,
+                     int64_t vcap, HsPqRun* lruns, int64_t lcap, HsPqChunkInfo* info) {
+  File* f = (File*)h;
+  memset(info, 0, sizeof(*info));
+  info->dict_off = -1;
+  const ChunkMeta& m = f->rgs[(size_t)rg].cols[(size_t)col];
+  const SchemaEl& s = f->schema[(size_t)f->leaves[(size_t)col]];
+  if (s.repetition == 2) return HS_PQ_UNSUPPORTED;
+  const int eb = elem_bytes(m.type);
+  if (!eb) return HS_PQ_UNSUPPORTED;
+  if (m.codec != 0 && m.codec != 1) return HS_PQ_UNSUPPORTED;
+  const bool optional = s.repetition == 1;
+  const int64_t start = m.dict_page_offset >= 0 && m.dict_page_offset < m.data_page_offset
+                            ? m.dict_page_offset : m.data_page_offset;
+  const int64_t len = m.total_compressed;
+  if (start < 0 || start + len > f->size) return HS_PQ_CORRUPT;
+  std::vector<uint8_t> raw((size_t)len);
+  if (!pread_all(f->fd, raw.data(), (size_t)len, start)) return HS_PQ_IO;
+  Out o{buf, cap, 0, vruns, vcap, 0, lruns, lcap, 0};
+  int64_t rows = 0, dense = 0;
+  TReader r{raw.data(), raw.data() + raw.size()};
+  while (rows < m.num_values) {
+    PageHdr ph;
+    if (!parse_page_header(r, ph)) return HS_PQ_CORRUPT;
+    if (r.end - r.p < ph.csize || ph.csize < 0 || ph.usize < 0) return HS_PQ_CORRUPT;
+    const uint8_t* payload = r.p;
+    r.p += ph.csize;
+    if (ph.type == 2) {  // dictionary page: PLAIN values
+      if (ph.enc != 0 && ph.enc != 2) return HS_PQ_UNSUPPORTED;
+      const int64_t at = (o.used + 15) & ~(int64_t)15;
+      if (at + ph.usize > cap) return HS_PQ_CAPACITY;
+      const int64_t got = inflate(m.codec, payload, ph.csize, buf + at, cap - at);
+      if (got < 0) return got == -2 ? HS_PQ_UNSUPPORTED : HS_PQ_CORRUPT;
+      info->dict_off = at;
+      info->dict_count = ph.dict_nvals;
+      o.used = at + got;
+      continue;
+    }
+    if (ph.type != 0 && ph.type != 3) continue;  // index pages etc.
+    const bool dict = ph.enc == 2 || ph.enc == 8;
+    if (!dict && ph.enc != 0) return HS_PQ_UNSUPPORTED;
+    const int64_t at = (o.used + 15) & ~(int64_t)15;
+    if (at + ph.usize > cap) return HS_PQ_CAPACITY;
+    uint8_t* page = buf + at;
+    int64_t plen;
+    const uint8_t* levels = nullptr;
+    int64_t levels_len = 0, vbase;
+    if (ph.v2) {  // levels are stored uncompressed ahead of the (maybe compressed) values
+      const int64_t lv = (int64_t)ph.v2_def_len + ph.v2_rep_len;
+      if (ph.v2_rep_len) return HS_PQ_UNSUPPORTED;
+      if (lv > ph.csize) return HS_PQ_CORRUPT;
+      memcpy(page, payload, (size_t)lv);
+      int64_t got;
+      if (ph.v2_compressed) got = inflate(m.codec, payload + lv, ph.csize - lv, page + lv,
+                                          cap - at - lv);
+      else got = inflate(0, payload + lv, ph.csize - lv, page + lv, cap - at - lv);
+      if (got < 0) return got == -2 ? HS_PQ_UNSUPPORTED : HS_PQ_CORRUPT;
+      plen = lv + got;
+      levels = page;
+      levels_len = ph.v2_def_len;
+      vbase = lv;
+    } else {
+      plen = inflate(m.codec, payload, ph.csize, page, cap - at);
+      if (plen < 0) return plen == -2 ? HS_PQ_UNSUPPORTED : HS_PQ_CORRUPT;
+      vbase = 0;
+      if (optional) {
+        if (ph.def_enc != 3) return HS_PQ_UNSUPPORTED;  // BIT_PACKED levels: deprecated
+        if (plen < 4) return HS_PQ_CORRUPT;
+        uint32_t l32;
+        memcpy(&l32, page, 4);
+        levels = page + 4;
+        levels_len = l32;
+        vbase = 4 + (int64_t)l32;
+        if (vbase > plen) return HS_PQ_CORRUPT;
+      }
+    }
+    int64_t nonnull = ph.nvals;
+    if (optional) {
+      const int64_t ones = parse_hybrid(levels, levels_len, at + (levels - page), 1, ph.nvals,
+                                        rows, o.lruns, o.lcap, o.nl, true);
+      if (ones == -2) return HS_PQ_CAPACITY;
+      if (ones < 0) return HS_PQ_CORRUPT;
+      nonnull = ones;
+    }
+    const uint8_t* vals = page + vbase;
+    const int64_t vlen = plen - vbase;
+    if (dict) {
+      if (info->dict_off < 0) return HS_PQ_CORRUPT;
+      if (nonnull > 0) {
+        if (vlen < 1) return HS_PQ_CORRUPT;
+        const int bw = vals[0];
+        if (bw > 32) return HS_PQ_CORRUPT;
+        const int64_t rc = parse_hybrid(vals + 1, vlen - 1, at + vbase + 1, bw, nonnull, dense,
+                                        o.vruns, o.vcap, o.nv, false);
+        if (rc == -2) return HS_PQ_CAPACITY;
+        if (rc < 0) return HS_PQ_CORRUPT;
+      }
+      info->dict_encoded = 1;
+    } else {
+      if (vlen < nonnull * eb) return HS_PQ_CORRUPT;
+      for (int64_t c = 0; c < nonnull; c += kChunk) {
+        const int64_t k = nonnull - c < kChunk ? nonnull - c : kChunk;
+        if (!push(o.vruns, o.vcap, o.nv, {dense + c, k, at + vbase + c * eb, 2, eb}))
+          return HS_PQ_CAPACITY;
+      }
+      info->plain_pages += 1;
+    }
+    rows += ph.nvals;
+    dense += nonnull;
+    o.used = at + plen;
+  }
+  info->num_values = rows;
+  info->num_nonnull = dense;
+  info->bytes_used = o.used;
+  info->nvalue_runs = (int32_t)o.nv;
+  info->nlevel_runs = (int32_t)o.nl;
+  return HS_PQ_OK;
+}
+
+// Snappy round-trip hook for tests (decompress only).
+int64_t hs_pq_snappy_decompress(const uint8_t* in, int64_t n, uint8_t* out, int64_t cap) {
+  size_t got = 0;
+  return snappy_decompress(in, (size_t)n, out, (size_t)cap, &got) ? (int64_t)got : -1;
+}
+
+}  // extern "C"
