@@ -127,8 +127,35 @@ struct RowGroupMeta {
   std::vector<ChunkMeta> cols;
 };
 
+}  // namespace
+
+// One entry per RLE run or (chunk of a) bit-packed run / PLAIN page — the GPU's work items
+// (layout shared with csrc/kernels/parquet_decode.hip).  Values are written to
+// out[dst .. dst+count): the dense non-null value index for value runs, rows for level runs.
+struct HsPqRun {
+  int64_t dst;        // first output index
+  int64_t count;      // values in this run
+  int64_t src;        // byte offset of the data in the chunk buffer; RLE runs: the value
+  int32_t kind;       // 0 RLE, 1 bit-packed, 2 PLAIN
+  int32_t bit_width;  // bits per value (RLE / bit-packed); PLAIN: element bytes
+};
+
+struct HsPqChunkInfo {
+  int64_t num_values;     // rows in the chunk
+  int64_t num_nonnull;    // non-null values
+  int64_t dict_off;       // byte offset of the PLAIN dictionary in the buffer (-1: none)
+  int64_t dict_count;
+  int64_t bytes_used;     // bytes of the buffer written
+  int64_t nvalue_runs, nlevel_runs;
+  int32_t dict_encoded;   // 1 if any data page is dictionary-encoded
+  int32_t plain_pages;    // pages stored PLAIN
+};
+
+namespace {
+
 struct File {
   int fd = -1;
+  std::vector<HsPqRun> vruns, lruns;  // run tables of the last hs_pq_read_chunk
   int64_t size = 0;
   int64_t num_rows = 0;
   std::vector<SchemaEl> schema;      // flattened, as stored
@@ -306,49 +333,15 @@ bool snappy_decompress(const uint8_t* in, size_t n, uint8_t* out, size_t cap, si
 
 }  // namespace
 
-// ------------------------------------------------------------------ run table (shared with GPU)
-// One entry per RLE run or (chunk of a) bit-packed run / PLAIN page.  Values are written to
-// out[dst .. dst+count) (dense index space: non-null values for value runs, rows for levels).
-struct HsPqRun {
-  int64_t dst;        // first output index
-  int64_t count;      // values in this run
-  int64_t src;        // byte offset in the page buffer (bit-packed / PLAIN data); RLE: value
-  int32_t kind;       // 0 RLE, 1 bit-packed, 2 PLAIN
-  int32_t bit_width;  // bits per value (bit-packed / RLE); PLAIN: element bytes
-};
-
-struct HsPqChunkInfo {
-  int64_t num_values;     // rows in the chunk
-  int64_t num_nonnull;    // non-null values
-  int64_t dict_off;       // byte offset of the PLAIN dictionary in the buffer (-1: none)
-  int64_t dict_count;
-  int64_t bytes_used;     // bytes of the buffer written
-  int32_t nvalue_runs, nlevel_runs;
-  int32_t dict_encoded;   // 1 if any data page is dictionary-encoded
-  int32_t plain_pages;    // pages stored PLAIN
-};
-
 namespace {
-
-struct Out {
-  uint8_t* buf; int64_t cap; int64_t used = 0;
-  HsPqRun* vruns; int64_t vcap; int64_t nv = 0;
-  HsPqRun* lruns; int64_t lcap; int64_t nl = 0;
-};
 
 constexpr int64_t kChunk = 4096;  // split long runs so each GPU work item stays short
 
-bool push(HsPqRun* runs, int64_t cap, int64_t& n, const HsPqRun& r) {
-  if (n >= cap) return false;
-  runs[n++] = r;
-  return true;
-}
-
 // Parse an RLE/bit-packed hybrid stream of `count` values into runs (dst starts at `dst0`).
-// `base` is the stream's byte offset in the output buffer.  Returns values that are non-zero
-// (only meaningful for def levels, bit width 1) or -1 on error.
+// `base` is the stream's byte offset in the chunk buffer.  Returns the number of non-zero
+// values when `count_ones` (definition levels, bit width 1), 0 otherwise; -1 on corruption.
 int64_t parse_hybrid(const uint8_t* s, int64_t len, int64_t base, int bw, int64_t count,
-                     int64_t dst0, HsPqRun* runs, int64_t cap, int64_t& n, bool count_ones) {
+                     int64_t dst0, std::vector<HsPqRun>& runs, bool count_ones) {
   TReader r{s, s + len};
   int64_t done = 0, ones = 0;
   const int vbytes = (bw + 7) / 8;
@@ -356,43 +349,40 @@ int64_t parse_hybrid(const uint8_t* s, int64_t len, int64_t base, int bw, int64_
     if (r.p >= r.end) return -1;
     const uint64_t h = r.varint();
     if (r.bad) return -1;
-    if (h & 1) {  // bit-packed: (h>>1) groups of 8
+    if (h & 1) {  // bit-packed: (h>>1) groups of 8 values, bw bytes per group
       const int64_t groups = (int64_t)(h >> 1);
-      const int64_t nvals = groups * 8;
       const int64_t nbytes = groups * bw;
       if (r.end - r.p < nbytes) return -1;
-      const int64_t take = nvals < count - done ? nvals : count - done;
+      const int64_t take = groups * 8 < count - done ? groups * 8 : count - done;
       const int64_t off = base + (r.p - s);
-      for (int64_t c = 0; c < take; c += kChunk) {   // kChunk is a multiple of 8: byte aligned
-        const int64_t k = take - c < kChunk ? take - c : kChunk;
-        if (!push(runs, cap, n, {dst0 + done + c, k, off + c * bw / 8, 1, bw})) return -2;
-      }
-      if (count_ones) {
+      for (int64_t c = 0; c < take; c += kChunk)   // kChunk % 8 == 0: chunks stay byte aligned
+        runs.push_back({dst0 + done + c, take - c < kChunk ? take - c : kChunk,
+                        off + c * bw / 8, 1, bw});
+      if (count_ones)
         for (int64_t i = 0; i < take; ++i) ones += (r.p[i >> 3] >> (i & 7)) & 1;
-      }
       r.p += nbytes;
       done += take;
-    } else {
+    } else {  // RLE: (h>>1) repeats of one value stored in ceil(bw/8) bytes
       const int64_t nvals = (int64_t)(h >> 1);
-      uint64_t v = 0;
       if (r.end - r.p < vbytes) return -1;
+      uint64_t v = 0;
       for (int i = 0; i < vbytes; ++i) v |= (uint64_t)r.p[i] << (8 * i);
       r.p += vbytes;
+      if (nvals == 0) continue;
       const int64_t take = nvals < count - done ? nvals : count - done;
-      for (int64_t c = 0; c < take; c += kChunk) {
-        const int64_t k = take - c < kChunk ? take - c : kChunk;
-        if (!push(runs, cap, n, {dst0 + done + c, k, (int64_t)v, 0, bw})) return -2;
-      }
+      for (int64_t c = 0; c < take; c += kChunk)
+        runs.push_back({dst0 + done + c, take - c < kChunk ? take - c : kChunk, (int64_t)v, 0,
+                        bw});
       if (count_ones && v) ones += take;
       done += take;
     }
   }
-  return ones;
+  return count_ones ? ones : 0;
 }
 
 struct PageHdr {
   int type = -1, usize = 0, csize = 0;
-  int nvals = 0, enc = 0, def_enc = 3, v2_nulls = 0, v2_def_len = 0, v2_rep_len = 0;
+  int nvals = 0, enc = 0, def_enc = 3, v2_def_len = 0, v2_rep_len = 0;
   bool v2 = false, v2_compressed = true;
   int dict_nvals = 0;
 };
@@ -428,7 +418,6 @@ bool parse_page_header(TReader& r, PageHdr& h) {
         int16_t d = 0;
         for (int dt; (dt = r.field(d)) != 0 && !r.bad;) {
           if (d == 1) h.nvals = (int)r.zigzag();
-          else if (d == 2) h.v2_nulls = (int)r.zigzag();
           else if (d == 4) h.enc = (int)r.zigzag();
           else if (d == 5) h.v2_def_len = (int)r.zigzag();
           else if (d == 6) h.v2_rep_len = (int)r.zigzag();
@@ -451,7 +440,7 @@ int elem_bytes(int type) {
   }
 }
 
-// decompress `csize` bytes at `src` into dst (capacity cap); returns bytes or -1
+// decompress `csize` bytes into dst (capacity cap): bytes written, -1 corrupt, -2 unsupported
 int64_t inflate(int codec, const uint8_t* src, int64_t csize, uint8_t* dst, int64_t cap) {
   if (codec == 0) {
     if (csize > cap) return -1;
@@ -466,17 +455,129 @@ int64_t inflate(int codec, const uint8_t* src, int64_t csize, uint8_t* dst, int6
   return -2;
 }
 
+int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
+
+int read_chunk(File* f, int rg, int col, uint8_t* buf, int64_t cap, HsPqChunkInfo* info) {
+  memset(info, 0, sizeof(*info));
+  info->dict_off = -1;
+  f->vruns.clear();
+  f->lruns.clear();
+  const ChunkMeta& m = f->rgs[(size_t)rg].cols[(size_t)col];
+  const SchemaEl& s = f->schema[(size_t)f->leaves[(size_t)col]];
+  if (s.repetition == 2) return HS_PQ_UNSUPPORTED;
+  const int eb = elem_bytes(m.type);
+  if (!eb) return HS_PQ_UNSUPPORTED;
+  if (m.codec != 0 && m.codec != 1) return HS_PQ_UNSUPPORTED;
+  const bool optional = s.repetition == 1;
+  const int64_t start = m.dict_page_offset > 0 && m.dict_page_offset < m.data_page_offset
+                            ? m.dict_page_offset : m.data_page_offset;
+  const int64_t len = m.total_compressed;
+  if (start < 4 || len < 0 || start + len > f->size) return HS_PQ_CORRUPT;
+  std::vector<uint8_t> raw((size_t)len);
+  if (!pread_all(f->fd, raw.data(), (size_t)len, start)) return HS_PQ_IO;
+  int64_t used = 0, rows = 0, dense = 0;
+  TReader r{raw.data(), raw.data() + raw.size()};
+  while (rows < m.num_values) {
+    PageHdr ph;
+    if (!parse_page_header(r, ph)) return HS_PQ_CORRUPT;
+    if (ph.csize < 0 || ph.usize < 0 || r.end - r.p < ph.csize) return HS_PQ_CORRUPT;
+    const uint8_t* payload = r.p;
+    r.p += ph.csize;
+    const int64_t at = align16(used);
+    if (ph.type == 2) {  // dictionary page: PLAIN values
+      if (ph.enc != 0 && ph.enc != 2) return HS_PQ_UNSUPPORTED;
+      if (at + ph.usize > cap) return HS_PQ_CAPACITY;
+      const int64_t got = inflate(m.codec, payload, ph.csize, buf + at, cap - at);
+      if (got < 0) return got == -2 ? HS_PQ_UNSUPPORTED : HS_PQ_CORRUPT;
+      if (got < (int64_t)ph.dict_nvals * eb) return HS_PQ_CORRUPT;
+      info->dict_off = at;
+      info->dict_count = ph.dict_nvals;
+      used = at + got;
+      continue;
+    }
+    if (ph.type != 0 && ph.type != 3) continue;  // index pages and the like carry no rows
+    const bool dict = ph.enc == 2 || ph.enc == 8;
+    if (!dict && ph.enc != 0) return HS_PQ_UNSUPPORTED;
+    if (at + ph.usize + 8 > cap) return HS_PQ_CAPACITY;
+    uint8_t* page = buf + at;
+    int64_t plen, vbase = 0, levels_len = 0;
+    const uint8_t* levels = nullptr;
+    if (ph.v2) {  // levels stay uncompressed ahead of the (optionally compressed) values
+      if (ph.v2_rep_len) return HS_PQ_UNSUPPORTED;
+      const int64_t lv = ph.v2_def_len;
+      if (lv > ph.csize) return HS_PQ_CORRUPT;
+      memcpy(page, payload, (size_t)lv);
+      const int64_t got = inflate(ph.v2_compressed ? m.codec : 0, payload + lv, ph.csize - lv,
+                                  page + lv, cap - at - lv);
+      if (got < 0) return got == -2 ? HS_PQ_UNSUPPORTED : HS_PQ_CORRUPT;
+      plen = lv + got;
+      levels = page;
+      levels_len = lv;
+      vbase = lv;
+    } else {
+      plen = inflate(m.codec, payload, ph.csize, page, cap - at);
+      if (plen < 0) return plen == -2 ? HS_PQ_UNSUPPORTED : HS_PQ_CORRUPT;
+      if (optional) {
+        if (ph.def_enc != 3) return HS_PQ_UNSUPPORTED;  // deprecated BIT_PACKED levels
+        if (plen < 4) return HS_PQ_CORRUPT;
+        uint32_t l32;
+        memcpy(&l32, page, 4);
+        levels = page + 4;
+        levels_len = l32;
+        vbase = 4 + (int64_t)l32;
+        if (vbase > plen) return HS_PQ_CORRUPT;
+      }
+    }
+    int64_t nonnull = ph.nvals;
+    if (optional) {
+      const int64_t ones = parse_hybrid(levels, levels_len, at + (levels - page), 1, ph.nvals,
+                                        rows, f->lruns, true);
+      if (ones < 0) return HS_PQ_CORRUPT;
+      nonnull = ones;
+    }
+    const uint8_t* vals = page + vbase;
+    const int64_t vlen = plen - vbase;
+    if (dict) {
+      if (info->dict_off < 0) return HS_PQ_CORRUPT;
+      if (nonnull > 0) {
+        if (vlen < 1) return HS_PQ_CORRUPT;
+        const int bw = vals[0];
+        if (bw > 32) return HS_PQ_CORRUPT;
+        if (parse_hybrid(vals + 1, vlen - 1, at + vbase + 1, bw, nonnull, dense, f->vruns,
+                         false) < 0)
+          return HS_PQ_CORRUPT;
+      }
+      info->dict_encoded = 1;
+    } else {
+      if (vlen < nonnull * eb) return HS_PQ_CORRUPT;
+      for (int64_t c = 0; c < nonnull; c += kChunk)
+        f->vruns.push_back({dense + c, nonnull - c < kChunk ? nonnull - c : kChunk,
+                            at + vbase + c * eb, 2, eb});
+      info->plain_pages += 1;
+    }
+    rows += ph.nvals;
+    dense += nonnull;
+    used = at + plen;
+  }
+  info->num_values = rows;
+  info->num_nonnull = dense;
+  info->bytes_used = used;
+  info->nvalue_runs = (int64_t)f->vruns.size();
+  info->nlevel_runs = (int64_t)f->lruns.size();
+  return HS_PQ_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 const char* hs_pq_error(void* h) { return h ? ((File*)h)->error.c_str() : "null handle"; }
 
+// Opens a file and parses its footer.  Always returns a handle (check hs_pq_ok / hs_pq_error;
+// release with hs_pq_close).
 void* hs_pq_open(const char* path) {
   File* f = new File();
-  if (open_file(path, *f) != HS_PQ_OK) {
-    // keep the handle so the caller can read the error, then close it
-  }
+  open_file(path, *f);
   return f;
 }
 
@@ -494,20 +595,17 @@ int hs_pq_num_row_groups(void* h) { return (int)((File*)h)->rgs.size(); }
 int64_t hs_pq_row_group_rows(void* h, int rg) { return ((File*)h)->rgs[(size_t)rg].num_rows; }
 int hs_pq_num_columns(void* h) { return (int)((File*)h)->leaves.size(); }
 
-// Leaf column by (top-level) name; -1 if absent or nested.
+// Leaf column by top-level name in a flat schema; -1 if absent (or the schema is nested).
 int hs_pq_find_column(void* h, const char* name) {
   File* f = (File*)h;
-  for (size_t i = 0; i < f->leaves.size(); ++i) {
-    if (f->schema[(size_t)f->leaves[i]].name == name) {
-      // flat schema only: root's direct child
-      if (f->schema.size() == f->leaves.size() + 1) return (int)i;
-      return -1;
-    }
-  }
+  if (f->schema.size() != f->leaves.size() + 1) return -1;
+  for (size_t i = 0; i < f->leaves.size(); ++i)
+    if (f->schema[(size_t)f->leaves[i]].name == name) return (int)i;
   return -1;
 }
 
-// physical type, max definition level (0 required / 1 optional), element bytes (0: unsupported)
+// physical type, max definition level (0 required / 1 optional), element bytes (0: the native
+// path does not decode this column)
 int hs_pq_column_info(void* h, int col, int* type, int* max_def, int* ebytes) {
   File* f = (File*)h;
   const SchemaEl& s = f->schema[(size_t)f->leaves[(size_t)col]];
@@ -517,142 +615,42 @@ int hs_pq_column_info(void* h, int col, int* type, int* max_def, int* ebytes) {
   return HS_PQ_OK;
 }
 
-// Upper bounds for one column chunk: buffer bytes, value runs, level runs.
-int hs_pq_chunk_bounds(void* h, int rg, int col, int64_t* buf_bytes, int64_t* vruns,
-                       int64_t* lruns) {
-  File* f = (File*)h;
-  const ChunkMeta& m = f->rgs[(size_t)rg].cols[(size_t)col];
-  const int64_t nv = m.num_values;
-  *buf_bytes = m.total_uncompressed + 64;
-  // a bit-packed header covers >= 8 values; every page may add a partial run per stream
-  *vruns = nv / 8 + nv / kChunk + 1024;
-  *lruns = nv / 8 + nv / kChunk + 1024;
-  return HS_PQ_OK;
+// Buffer bytes that suffice for hs_pq_read_chunk of this column chunk.
+int64_t hs_pq_chunk_bound(void* h, int rg, int col) {
+  const ChunkMeta& m = ((File*)h)->rgs[(size_t)rg].cols[(size_t)col];
+  return m.total_uncompressed + 16 * 64 + 64;  // + per-page alignment / slack
 }
 
-// Read, decompress and pre-parse one column chunk.  Data pages land back to back in `buf`
-// (after the dictionary page, if any); vruns/lruns receive the run tables.  Value runs address
-// the dense non-null value index; level runs (optional columns only) address rows.
-int hs_pq_read_chunk(void* h, int rg, int col, uint8_t* buf, int64_t cap, HsPqRun* vruns,
-                     int64_t vcap, HsPqRun* lruns, int64_t lcap, HsPqChunkInfo* info) {
+// Read, decompress and pre-parse one column chunk into `buf` (dictionary page first, then the
+// data pages back to back, each 16-byte aligned).  The run tables stay in the handle until the
+// next call; fetch them with hs_pq_copy_runs.
+int hs_pq_read_chunk(void* h, int rg, int col, uint8_t* buf, int64_t cap, HsPqChunkInfo* info) {
+  return read_chunk((File*)h, rg, col, buf, cap, info);
+}
+
+// Copy the last chunk's run tables out, adding `src_base` to every buffer offset (so several
+// chunks can share one device buffer) and `dst_base` to every output index.
+int hs_pq_copy_runs(void* h, HsPqRun* vdst, HsPqRun* ldst, int64_t src_base, int64_t dst_base) {
   File* f = (File*)h;
-  memset(info, 0, sizeof(*info));
-  info->dict_off = -1;
-  const ChunkMeta& m = f->rgs[(size_t)rg].cols[(size_t)col];
-  const SchemaEl& s = f->schema[(size_t)f->leaves[(size_t)col]];
-  if (s.repetition == 2) return HS_PQ_UNSUPPORTED;
-  const int eb = elem_bytes(m.type);
-  if (!eb) return HS_PQ_UNSUPPORTED;
-  if (m.codec != 0 && m.codec != 1) return HS_PQ_UNSUPPORTED;
-  const bool optional = s.repetition == 1;
-  const int64_t start = m.dict_page_offset >= 0 && m.dict_page_offset < m.data_page_offset
-                            ? m.dict_page_offset : m.data_page_offset;
-  const int64_t len = m.total_compressed;
-  if (start < 0 || start + len > f->size) return HS_PQ_CORRUPT;
-  std::vector<uint8_t> raw((size_t)len);
-  if (!pread_all(f->fd, raw.data(), (size_t)len, start)) return HS_PQ_IO;
-  Out o{buf, cap, 0, vruns, vcap, 0, lruns, lcap, 0};
-  int64_t rows = 0, dense = 0;
-  TReader r{raw.data(), raw.data() + raw.size()};
-  while (rows < m.num_values) {
-    PageHdr ph;
-    if (!parse_page_header(r, ph)) return HS_PQ_CORRUPT;
-    if (r.end - r.p < ph.csize || ph.csize < 0 || ph.usize < 0) return HS_PQ_CORRUPT;
-    const uint8_t* payload = r.p;
-    r.p += ph.csize;
-    if (ph.type == 2) {  // dictionary page: PLAIN values
-      if (ph.enc != 0 && ph.enc != 2) return HS_PQ_UNSUPPORTED;
-      const int64_t at = (o.used + 15) & ~(int64_t)15;
-      if (at + ph.usize > cap) return HS_PQ_CAPACITY;
-      const int64_t got = inflate(m.codec, payload, ph.csize, buf + at, cap - at);
-      if (got < 0) return got == -2 ? HS_PQ_UNSUPPORTED : HS_PQ_CORRUPT;
-      info->dict_off = at;
-      info->dict_count = ph.dict_nvals;
-      o.used = at + got;
-      continue;
-    }
-    if (ph.type != 0 && ph.type != 3) continue;  // index pages etc.
-    const bool dict = ph.enc == 2 || ph.enc == 8;
-    if (!dict && ph.enc != 0) return HS_PQ_UNSUPPORTED;
-    const int64_t at = (o.used + 15) & ~(int64_t)15;
-    if (at + ph.usize > cap) return HS_PQ_CAPACITY;
-    uint8_t* page = buf + at;
-    int64_t plen;
-    const uint8_t* levels = nullptr;
-    int64_t levels_len = 0, vbase;
-    if (ph.v2) {  // levels are stored uncompressed ahead of the (maybe compressed) values
-      const int64_t lv = (int64_t)ph.v2_def_len + ph.v2_rep_len;
-      if (ph.v2_rep_len) return HS_PQ_UNSUPPORTED;
-      if (lv > ph.csize) return HS_PQ_CORRUPT;
-      memcpy(page, payload, (size_t)lv);
-      int64_t got;
-      if (ph.v2_compressed) got = inflate(m.codec, payload + lv, ph.csize - lv, page + lv,
-                                          cap - at - lv);
-      else got = inflate(0, payload + lv, ph.csize - lv, page + lv, cap - at - lv);
-      if (got < 0) return got == -2 ? HS_PQ_UNSUPPORTED : HS_PQ_CORRUPT;
-      plen = lv + got;
-      levels = page;
-      levels_len = ph.v2_def_len;
-      vbase = lv;
-    } else {
-      plen = inflate(m.codec, payload, ph.csize, page, cap - at);
-      if (plen < 0) return plen == -2 ? HS_PQ_UNSUPPORTED : HS_PQ_CORRUPT;
-      vbase = 0;
-      if (optional) {
-        if (ph.def_enc != 3) return HS_PQ_UNSUPPORTED;  // BIT_PACKED levels: deprecated
-        if (plen < 4) return HS_PQ_CORRUPT;
-        uint32_t l32;
-        memcpy(&l32, page, 4);
-        levels = page + 4;
-        levels_len = l32;
-        vbase = 4 + (int64_t)l32;
-        if (vbase > plen) return HS_PQ_CORRUPT;
-      }
-    }
-    int64_t nonnull = ph.nvals;
-    if (optional) {
-      const int64_t ones = parse_hybrid(levels, levels_len, at + (levels - page), 1, ph.nvals,
-                                        rows, o.lruns, o.lcap, o.nl, true);
-      if (ones == -2) return HS_PQ_CAPACITY;
-      if (ones < 0) return HS_PQ_CORRUPT;
-      nonnull = ones;
-    }
-    const uint8_t* vals = page + vbase;
-    const int64_t vlen = plen - vbase;
-    if (dict) {
-      if (info->dict_off < 0) return HS_PQ_CORRUPT;
-      if (nonnull > 0) {
-        if (vlen < 1) return HS_PQ_CORRUPT;
-        const int bw = vals[0];
-        if (bw > 32) return HS_PQ_CORRUPT;
-        const int64_t rc = parse_hybrid(vals + 1, vlen - 1, at + vbase + 1, bw, nonnull, dense,
-                                        o.vruns, o.vcap, o.nv, false);
-        if (rc == -2) return HS_PQ_CAPACITY;
-        if (rc < 0) return HS_PQ_CORRUPT;
-      }
-      info->dict_encoded = 1;
-    } else {
-      if (vlen < nonnull * eb) return HS_PQ_CORRUPT;
-      for (int64_t c = 0; c < nonnull; c += kChunk) {
-        const int64_t k = nonnull - c < kChunk ? nonnull - c : kChunk;
-        if (!push(o.vruns, o.vcap, o.nv, {dense + c, k, at + vbase + c * eb, 2, eb}))
-          return HS_PQ_CAPACITY;
-      }
-      info->plain_pages += 1;
-    }
-    rows += ph.nvals;
-    dense += nonnull;
-    o.used = at + plen;
+  for (size_t i = 0; i < f->vruns.size(); ++i) {
+    HsPqRun r = f->vruns[i];
+    if (r.kind != 0) r.src += src_base;
+    r.dst += dst_base;
+    vdst[i] = r;
   }
-  info->num_values = rows;
-  info->num_nonnull = dense;
-  info->bytes_used = o.used;
-  info->nvalue_runs = (int32_t)o.nv;
-  info->nlevel_runs = (int32_t)o.nl;
+  for (size_t i = 0; i < f->lruns.size(); ++i) {
+    HsPqRun r = f->lruns[i];
+    if (r.kind != 0) r.src += src_base;
+    r.dst += dst_base;
+    ldst[i] = r;
+  }
   return HS_PQ_OK;
 }
 
-// Snappy round-trip hook for tests (decompress only).
+int hs_pq_run_size() { return (int)sizeof(HsPqRun); }
+int hs_pq_info_size() { return (int)sizeof(HsPqChunkInfo); }
+
+// Snappy decompression hook for tests.
 int64_t hs_pq_snappy_decompress(const uint8_t* in, int64_t n, uint8_t* out, int64_t cap) {
   size_t got = 0;
   return snappy_decompress(in, (size_t)n, out, (size_t)cap, &got) ? (int64_t)got : -1;

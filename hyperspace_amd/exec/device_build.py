@@ -151,12 +151,13 @@ def _upload_parquet(rel, my_files, columns, indexed, lineage_ids, device, dist):
     counts = list(staging.io_pool().map(
         lambda f: pq.ParquetFile(P.to_local(f)).metadata.num_rows, my_files))
 
-    def read_file(f):
+    def read_file(f, cols=None):
         return read_files("parquet", [f], rel.data_schema, rel.options,
-                          rel.location.partition_spec, columns)
+                          rel.location.partition_spec, columns if cols is None else cols)
     lin = [lineage_ids[f] for f in my_files] if lineage_ids is not None else None
     up = staging.upload_files(read_file, my_files, counts, schema, device, lin,
-                              C.DATA_FILE_NAME_ID)
+                              C.DATA_FILE_NAME_ID,
+                              parquet_local=[P.to_local(f) for f in my_files])
     cols = dict(up.columns)
     _finish_strings(up.host_strings, cols, indexed, device, dist)
     names = list(schema.names)

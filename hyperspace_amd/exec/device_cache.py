@@ -108,9 +108,11 @@ def load_bucketed_index(files, columns: List[str], num_buckets: int, sort_cols: 
         schema = pq.read_schema(P.to_local(paths[0]))
         schema = pa.schema([schema.field(c) for c in columns])
 
-        def read_file(p):
-            return pq.read_table(P.to_local(p), columns=columns, use_threads=False)
-        up = staging.upload_files(read_file, paths, rows, schema, device)
+        def read_file(p, cols=None):
+            return pq.read_table(P.to_local(p), columns=columns if cols is None else cols,
+                                 use_threads=False)
+        up = staging.upload_files(read_file, paths, rows, schema, device,
+                                  parquet_local=[P.to_local(p) for p in paths])
         cols = dict(up.columns)
         for name, chunks in up.host_strings.items():
             arr = pa.chunked_array(chunks, type=chunks[0].type)

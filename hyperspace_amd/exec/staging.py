@@ -92,6 +92,11 @@ def fixed_width_numpy(arr) -> Tuple[np.ndarray, Optional[np.ndarray]]:
     return vals, valid
 
 
+def native_decode_enabled() -> bool:
+    """Native Parquet page decode (HIP) for staging; ``HS_NATIVE_PARQUET=0`` forces pyarrow."""
+    return os.environ.get("HS_NATIVE_PARQUET", "1") == "1"
+
+
 def _h2d_async(dst, src: np.ndarray, stream) -> None:
     """Copy ``src`` into device tensor slice ``dst`` via a pinned bounce buffer on ``stream``."""
     import torch
@@ -113,14 +118,19 @@ class UploadResult:
         self.host_strings = host_strings  # name -> list of per-file arrow chunks (in file order)
 
 
-def upload_files(read_file: Callable[[str], pa.Table], files: Sequence[str],
+def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
                  row_counts: Sequence[int], schema: pa.Schema, device,
                  lineage_ids: Optional[Sequence[int]] = None,
-                 lineage_name: Optional[str] = None) -> UploadResult:
+                 lineage_name: Optional[str] = None,
+                 parquet_local: Optional[Sequence[str]] = None) -> UploadResult:
     """Decode ``files`` in parallel and stream their fixed-width columns into HBM.
 
     ``row_counts[i]`` must equal the row count ``read_file(files[i])`` returns (Parquet footer);
     string columns are returned as host arrow chunks for dictionary encoding by the caller.
+
+    With ``parquet_local`` (local paths of Parquet ``files``) fixed-width columns go through the
+    native page layer + HIP decode (``io/native_parquet.py``); ``read_file(path, columns)`` then
+    reads only the columns that path does not cover.
     """
     import torch
     offs = np.concatenate([[0], np.cumsum(np.asarray(row_counts, dtype=np.int64))])
@@ -142,14 +152,28 @@ def upload_files(read_file: Callable[[str], pa.Table], files: Sequence[str],
     main = torch.cuda.current_stream(device)
     stream.wait_stream(main)  # allocations above happen-before the copies
 
+    native = parquet_local is not None and native_decode_enabled()
+
     def work(i: int):
         torch.cuda.set_device(device)
-        t = read_file(files[i])
         lo, hi = int(offs[i]), int(offs[i + 1])
+        done = set()
+        if native:
+            from ..io import native_parquet
+            done = native_parquet.upload_file(parquet_local[i], [f for f in schema
+                                                                 if f.name in cols],
+                                              cols, lo, n, stream, device, lock)
+        rest = [f for f in schema if f.name not in done]
+        if not rest:
+            if lineage_ids is not None:
+                with torch.cuda.stream(stream):
+                    cols[lineage_name].data[lo:hi].fill_(int(lineage_ids[i]))
+            return hi - lo
+        t = read_file(files[i], [f.name for f in rest]) if native else read_file(files[i])
         if t.num_rows != hi - lo:
             raise RuntimeError(f"row count mismatch for {files[i]}: footer {hi - lo}, read "
                                f"{t.num_rows}")
-        for f in schema:
+        for f in rest:
             c = t.column(f.name)
             if f.name in strings:
                 strings[f.name][i] = c
