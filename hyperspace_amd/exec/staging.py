@@ -40,13 +40,31 @@ def io_pool() -> cf.ThreadPoolExecutor:
 
 
 def copy_stream(device):
+    return copy_streams(device)[0]
+
+
+def copy_streams(device, k: int = 4) -> list:
+    """``k`` staging streams per device (the box exposes 4 hardware queues per process):
+    uploads of different files run their H2D copies and decode kernels concurrently."""
     import torch
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _COPY_STREAMS.get(idx)
     if s is None:
-        s = torch.cuda.Stream(device=device)
+        s = [torch.cuda.Stream(device=device) for _ in range(k)]
         _COPY_STREAMS[idx] = s
     return s
+
+
+def ensure_valid(dc: DeviceColumn, n: int, device, lock: threading.Lock):
+    """The column's validity mask, created all-valid on first use.  The fill completes before
+    any thread can see the mask, so concurrent streams writing their own slices never race it."""
+    import torch
+    with lock:
+        if dc.valid is None:
+            v = torch.ones(n, dtype=torch.uint8, device=device)
+            torch.cuda.current_stream(device).synchronize()
+            dc.valid = v
+    return dc.valid
 
 
 _TORCH_OF_NP = None
@@ -135,7 +153,7 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
     import torch
     offs = np.concatenate([[0], np.cumsum(np.asarray(row_counts, dtype=np.int64))])
     n = int(offs[-1])
-    stream = copy_stream(device)
+    streams = copy_streams(device)
     cols: Dict[str, DeviceColumn] = {}
     strings: Dict[str, list] = {}
     for f in schema:
@@ -150,12 +168,14 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
                                           pa.int64())
     lock = threading.Lock()
     main = torch.cuda.current_stream(device)
-    stream.wait_stream(main)  # allocations above happen-before the copies
+    for st in streams:
+        st.wait_stream(main)  # allocations above happen-before the copies
 
     native = parquet_local is not None and native_decode_enabled()
 
     def work(i: int):
         torch.cuda.set_device(device)
+        stream = streams[i % len(streams)]
         lo, hi = int(offs[i]), int(offs[i + 1])
         done = set()
         if native:
@@ -182,11 +202,7 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
             dc = cols[f.name]
             _h2d_async(dc.data[lo:hi], vals, stream)
             if valid is not None:
-                with lock:
-                    if dc.valid is None:
-                        with torch.cuda.stream(stream):
-                            dc.valid = torch.ones(n, dtype=torch.uint8, device=device)
-                _h2d_async(dc.valid[lo:hi], valid, stream)
+                _h2d_async(ensure_valid(dc, n, device, lock)[lo:hi], valid, stream)
         if lineage_ids is not None:
             with torch.cuda.stream(stream):
                 cols[lineage_name].data[lo:hi].fill_(int(lineage_ids[i]))
@@ -195,7 +211,8 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
     futs = [io_pool().submit(work, i) for i in range(len(files))]
     for fu in futs:
         fu.result()
-    main.wait_stream(stream)
+    for st in streams:
+        main.wait_stream(st)
     return UploadResult(cols, n, strings)
 
 

@@ -88,9 +88,6 @@ INDEX_FILE_CODEC_DEFAULT = "none"
 # Rows per Parquet row group in index files (row-group stats drive pruning).
 INDEX_ROW_GROUP_ROWS = "spark.hyperspace.mi.index.rowGroupRows"
 INDEX_ROW_GROUP_ROWS_DEFAULT = "1048576"
-# Capture the steady-state query pipeline in a hipGraph.
-HIPGRAPH_ENABLED = "spark.hyperspace.mi.hipGraph.enabled"
-HIPGRAPH_ENABLED_DEFAULT = "true"
 # Fault-injection hook for action crash tests: after_begin | mid_op | before_end.
 # whole-stage code generation (hipRTC) for the fused scan/join aggregate kernels
 CODEGEN_ENABLED = "spark.hyperspace.mi.codegen.enabled"

@@ -274,10 +274,8 @@ def upload_file(path: str, fields: Sequence[pa.Field], cols: Dict[str, object], 
                 NL.check(NL.lib().hs_pq_decode_values(
                     dbuf.data_ptr(), druns.data_ptr() + v0 * rsz, vn, dict_off, info.dict_count,
                     eb, dense.data_ptr(), sp), "hs_pq_decode_values")
-                with valid_lock:
-                    if dc.valid is None:
-                        dc.valid = torch.ones(n_all, dtype=torch.uint8, device=device)
-                vslice = dc.valid[row0:row0 + rows]
+                from ..exec.staging import ensure_valid
+                vslice = ensure_valid(dc, n_all, device, valid_lock)[row0:row0 + rows]
                 NL.check(NL.lib().hs_pq_decode_levels(
                     dbuf.data_ptr(), druns.data_ptr() + (nv + l0) * rsz, ln,
                     vslice.data_ptr(), sp), "hs_pq_decode_levels")

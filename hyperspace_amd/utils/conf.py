@@ -110,10 +110,6 @@ class HyperspaceConf:
         return int(conf.get(C.INDEX_ROW_GROUP_ROWS, C.INDEX_ROW_GROUP_ROWS_DEFAULT))
 
     @staticmethod
-    def hipgraph_enabled(conf) -> bool:
-        return _b(conf.get(C.HIPGRAPH_ENABLED, C.HIPGRAPH_ENABLED_DEFAULT))
-
-    @staticmethod
     def codegen_enabled(conf) -> bool:
         return _b(conf.get(C.CODEGEN_ENABLED, C.CODEGEN_ENABLED_DEFAULT))
 
