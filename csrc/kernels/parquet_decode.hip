@@ -109,6 +109,9 @@ extern "C" {
 int hs_pq_decode_values(const uint8_t* buf, const HsPqRun* runs, int64_t nruns, int64_t dict_off,
                         int64_t dict_count, int elem_bytes, void* out, void* stream) {
   if (nruns <= 0) return 0;
+  // staging worker threads share the thread-local HIP error slot with torch; clear anything
+  // stale so the check below reports this launch only
+  (void)hipGetLastError();
   const dim3 grid((unsigned)((nruns + 3) / 4));
   hipStream_t s = (hipStream_t)stream;
   if (elem_bytes == 4)
@@ -126,6 +129,7 @@ int hs_pq_decode_values(const uint8_t* buf, const HsPqRun* runs, int64_t nruns, 
 int hs_pq_decode_levels(const uint8_t* buf, const HsPqRun* runs, int64_t nruns, uint8_t* valid,
                         void* stream) {
   if (nruns <= 0) return 0;
+  (void)hipGetLastError();
   hipLaunchKernelGGL(hs_pq_levels_kernel, dim3((unsigned)((nruns + 3) / 4)), dim3(256), 0,
                      (hipStream_t)stream, buf, runs, nruns, valid);
   return (int)hipGetLastError();
