@@ -50,13 +50,11 @@ __device__ __forceinline__ int64_t lb_sorted(const ColDesc& c, int64_t lo, int64
   return lo;
 }
 
-__global__ void hs_range_search_kernel(ColDesc key, const int64_t* __restrict__ bucket_off,
-                                       const int32_t* __restrict__ buckets, int nb, int has_lo,
-                                       uint64_t lo_key, int lo_incl, int has_hi, uint64_t hi_key,
-                                       int hi_incl, int64_t* __restrict__ rstart,
-                                       int64_t* __restrict__ rlen, int32_t* __restrict__ rbucket) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nb) return;
+__device__ __forceinline__ void range_one(const ColDesc& key, const int64_t* __restrict__ bucket_off,
+                                          const int32_t* __restrict__ buckets, int i, int has_lo,
+                                          uint64_t lo_key, int lo_incl, int has_hi,
+                                          uint64_t hi_key, int hi_incl, int64_t* __restrict__ rstart,
+                                          int64_t* __restrict__ rlen, int32_t* __restrict__ rbucket) {
   const int b = buckets ? buckets[i] : i;
   const int64_t s = bucket_off[b], e = bucket_off[b + 1];
   int64_t first_valid = s;
@@ -75,6 +73,30 @@ __global__ void hs_range_search_kernel(ColDesc key, const int64_t* __restrict__ 
   rstart[i] = a;
   rlen[i] = z - a;
   if (rbucket) rbucket[i] = b;
+}
+
+__global__ void hs_range_search_kernel(ColDesc key, const int64_t* __restrict__ bucket_off,
+                                       const int32_t* __restrict__ buckets, int nb, int has_lo,
+                                       uint64_t lo_key, int lo_incl, int has_hi, uint64_t hi_key,
+                                       int hi_incl, int64_t* __restrict__ rstart,
+                                       int64_t* __restrict__ rlen, int32_t* __restrict__ rbucket) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb) return;
+  range_one(key, bucket_off, buckets, i, has_lo, lo_key, lo_incl, has_hi, hi_key, hi_incl, rstart,
+            rlen, rbucket);
+}
+
+// Bounds read from device memory (int64 x6: has_lo, lo, lo_incl, has_hi, hi, hi_incl), so a
+// captured hipGraph replays with new literals after one H2D of the parameter block.
+__global__ void hs_range_search_dev_kernel(ColDesc key, const int64_t* __restrict__ bucket_off,
+                                           const int32_t* __restrict__ buckets, int nb,
+                                           const int64_t* __restrict__ bp,
+                                           int64_t* __restrict__ rstart,
+                                           int64_t* __restrict__ rlen, int32_t* __restrict__ rbucket) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb) return;
+  range_one(key, bucket_off, buckets, i, (int)bp[0], (uint64_t)bp[1], (int)bp[2], (int)bp[3],
+            (uint64_t)bp[4], (int)bp[5], rstart, rlen, rbucket);
 }
 
 // ranges -> tile prefix (single block, R arbitrary): tile_prefix[R] = total tiles.
@@ -307,6 +329,16 @@ extern "C" {
 int hs_scan_params_size() { return (int)sizeof(ScanParams); }
 int hs_scan_tile_rows() { return SF_TILE; }
 int hs_scan_grid() { return SF_GRID; }
+
+int hs_range_search_dev(const ColDesc* key, const int64_t* bucket_off, const int32_t* buckets,
+                        int nb, const int64_t* dparams, int64_t* rstart, int64_t* rlen,
+                        int32_t* rbucket, void* stream) {
+  if (nb <= 0) return 0;
+  hipLaunchKernelGGL(hs_range_search_dev_kernel, dim3((nb + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, *key, bucket_off, buckets, nb, dparams, rstart, rlen,
+                     rbucket);
+  return (int)hipGetLastError();
+}
 
 int hs_range_search(const ColDesc* key, const int64_t* bucket_off, const int32_t* buckets, int nb,
                     int has_lo, uint64_t lo_key, int lo_incl, int has_hi, uint64_t hi_key,

@@ -37,6 +37,7 @@ from . import jit
 from .arrow_eval import key
 from .device_cache import DeviceTableCache, load_bucketed_index, load_flat
 from .device_table import DeviceColumn, DeviceTable
+from .graphs import GraphCache, ScanAggGraph, range_bounds
 
 log = logging.getLogger(__name__)
 Unsupported = CP.Unsupported
@@ -94,6 +95,7 @@ class GpuBackend:
         self.metrics: Dict[str, float] = {}
         self._cpu = None
         self._domains: Dict[tuple, tuple] = {}
+        self.graphs = GraphCache()
 
     # ------------------------------------------------------------------------------------------
     @property
@@ -257,9 +259,18 @@ class GpuBackend:
         When ``implied`` is given it receives ``id(c)`` of every conjunct the ranges already
         guarantee (comparisons of the sort key with literals, and ``isnotnull(key)`` since range
         search skips the null prefix), so kernels do not re-evaluate them per row."""
+        spec = self._range_spec(r, conds, implied)
+        if spec is None:
+            return self._full_ranges(r.table)
+        kc, lo, lo_incl, hi, hi_incl, buckets = spec
+        return K.range_search(kc, r.table.bucket_offsets, buckets, lo, lo_incl, hi, hi_incl)
+
+    def _range_spec(self, r: DRel, conds: list, implied: Optional[set] = None):
+        """(key column, lo, lo_incl, hi, hi_incl, buckets) of the range search ``_ranges``
+        runs, or None when every row of every bucket is in range."""
         t = r.table
         if not (r.bucketed and r.sort_attrs):
-            return self._full_ranges(t)
+            return None
         lead = r.sort_attrs[0]
         kc = r.col(lead)
         lo = hi = None
@@ -304,10 +315,10 @@ class GpuBackend:
             import torch
             buckets = torch.tensor([eq_bucket], dtype=torch.int32, device=self.device)
         if lo is None and hi is None and buckets is None and not notnull:
-            return self._full_ranges(t)
+            return None
         if implied is not None:
             implied.update(id(c) for c in used + notnull)
-        return K.range_search(kc, t.bucket_offsets, buckets, lo, lo_incl, hi, hi_incl)
+        return kc, lo, lo_incl, hi, hi_incl, buckets
 
     def _full_ranges(self, t: DeviceTable):
         fr = getattr(t, "_full_ranges", None)
@@ -604,7 +615,8 @@ class GpuBackend:
                         d, sums, cnts, mins, maxs, G, gbase, gdict, gtype, A)
                 sums, cnts, mins, maxs = d.all_reduce_agg(sums, cnts, mins, maxs)
         with stage("agg.d2h"):
-            host = K.agg_to_host(sums, cnts, mins, maxs)
+            host = (sums, cnts, mins, maxs) if isinstance(sums, np.ndarray) else \
+                K.agg_to_host(sums, cnts, mins, maxs)
         s, c, mn, mx = (x.reshape(G, A) for x in host)
         rows = [g for g in range(G) if c[g, A - 1] > 0] if group is not None else [0]
         vals = {}
@@ -726,8 +738,12 @@ class GpuBackend:
     def _scan_agg(self, r: DRel, fns, group):
         col_info, descs = self._column_infos([(r, 0)])
         implied: set = set()
-        with stage("scan.ranges"):
-            rstart, rlen, _ = self._ranges(r, r.conds, implied)
+        spec = self._range_spec(r, r.conds, implied)
+        graph = self._graph_eligible(spec, descs)
+        if not graph:
+            with stage("scan.ranges"):
+                rstart, rlen, _ = self._ranges(r, r.conds) if spec is not None else \
+                    self._full_ranges(r.table)
         bound = CP.bind(CP.to_cnf([c for c in r.conds if id(c) not in implied]), col_info,
                         self.device)
         specs = self._agg_specs(fns, col_info)
@@ -749,6 +765,10 @@ class GpuBackend:
         p.naggs = len(specs)
         if bound.always_false:
             out = self._empty_agg(len(specs), G)
+        elif graph:
+            with stage("scan.graph"):
+                out = self._scan_agg_graph(r, p, spec,
+                                           p.naggs * (p.num_groups if p.group_col >= 0 else 1))
         else:
             with stage("scan.agg_kernel"):
                 tp = K.ranges_to_tiles(rlen)
@@ -757,6 +777,37 @@ class GpuBackend:
                 else:
                     out = K.scan_agg(p, rstart, rlen, tp)
         return (*out, G, gbase, gdict, gtype)
+
+    def _graph_eligible(self, spec, descs) -> bool:
+        """Replay a captured hipGraph for this scan (exec/graphs.py): single rank, generated
+        kernels, a range search over all buckets (equality bucket pruning changes the launch
+        shape), and no compacted columns."""
+        if spec is None or spec[5] is not None:
+            return False
+        d = self._dist()
+        if d is not None and d.world > 1:
+            return False
+        conf = self.session.conf
+        return (HyperspaceConf.codegen_enabled(conf) and HyperspaceConf.hipgraph_enabled(conf)
+                and self._compacts(descs) is None)
+
+    def _scan_agg_graph(self, r: DRel, p: NL.ScanParams, spec, GA: int):
+        kc, lo, lo_incl, hi, hi_incl, _ = spec
+        t = r.table
+        nb = t.num_buckets
+        grid = jit.SCAN_GRID or NL.lib().hs_scan_grid()
+        shape = jit.scan_agg_shape(p)
+        k = jit.kernel_for(shape, lambda: jit.gen_scan_agg(p))
+        key = (shape, kc.data.data_ptr(), kc.valid.data_ptr() if kc.valid is not None else 0,
+               kc.hs_type, t.bucket_offsets.data_ptr(), nb, grid, GA)
+        shmem = GA * 32 if p.group_col >= 0 else 0
+        g = self.graphs.get(key, lambda: ScanAggGraph(k, kc.desc(), t.bucket_offsets, nb, grid,
+                                                      GA, shmem, self.device))
+        values = g.values_template()
+        values.update({"num_groups": p.num_groups, "group_base": p.group_base})
+        jit._fill_common(values, p.cols, [(i, p.preds[i]) for i in range(p.npreds)],
+                         [p.aggs[i] for i in range(p.naggs)])
+        return g.run(range_bounds(lo, lo_incl, hi, hi_incl), k.args.pack(values))
 
     def _compacts(self, descs: Dict[int, DeviceColumn]) -> Optional[dict]:
         """Compact HBM encodings (exec/encoding.py) the generated kernels read instead."""

@@ -1,0 +1,169 @@
+"""hipGraph-captured scan pipelines (BASELINE.json north star; SURVEY.md §2.3 K7 "kernel chain
+captured in a hipGraph", §7.4 item 6).
+
+An indexed filter + aggregate (TPC-H Q6 shape) is five device steps on the device-resident index
+table:
+
+1. per-bucket range search of the leading indexed column (``hs_range_search_dev``);
+2. ranges -> tile prefix (``hs_ranges_to_tiles``);
+3. the query's generated scan kernel (``exec/jit.py``);
+4. the deterministic final reduction (``hs_agg_final``);
+5. the D2H copy of the result block.
+
+Every size in that chain is fixed by the table (one range per bucket, a fixed grid), so it is
+captured ONCE per (query shape, table) into a HIP graph.  The graph's only input is a pinned
+parameter block: the range bounds plus the generated kernel's argument block (its literals),
+which the kernel reads through a device pointer.  A query of a known shape writes the block and
+replays the graph: one launch instead of five, and none of the per-kernel host work.
+
+The first execution of a key runs the same sequence eagerly (that also loads the kernel module)
+and then captures; later executions replay.  Graph mode is single-rank only: with several ranks
+the partial aggregates go through an all-reduce on the device tensors instead.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import struct
+import threading
+from collections import OrderedDict
+from typing import Optional, Tuple
+
+import numpy as np
+
+from ..ops import _lib as NL
+from . import jit
+
+PARAM_HEAD = 64   # 6 x int64 range bounds, padded to a cache line
+
+
+class _Pinned:
+    """A hipHostMalloc block (capture-safe: no allocator bookkeeping on the copies)."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = nbytes
+        self.ptr = jit.runtime().hs_host_alloc(nbytes)
+        if not self.ptr:
+            raise MemoryError(f"hipHostMalloc({nbytes}) failed")
+
+    def view(self) -> np.ndarray:
+        return np.ctypeslib.as_array((C.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            jit.runtime().hs_host_free(self.ptr)
+            self.ptr = None
+
+
+class ScanAggGraph:
+    def __init__(self, kernel: jit.Kernel, kd: NL.ColDesc, bucket_off, nb: int, grid: int,
+                 GA: int, shmem: int, device):
+        import torch
+        from ..ops import kernels as K
+        self.kernel = kernel.by_pointer()
+        self.kd = kd
+        self.bucket_off = bucket_off
+        self.nb, self.grid, self.GA, self.shmem = nb, grid, GA, shmem
+        self.tile = jit.BLOCK * jit.SCAN_ITEMS
+        self.args_size = 8 * len(kernel.args.slots)
+        self.h_params = _Pinned(PARAM_HEAD + self.args_size)
+        self.d_params = torch.empty(PARAM_HEAD + self.args_size, dtype=torch.uint8, device=device)
+        self.rstart = torch.empty(nb, dtype=torch.int64, device=device)
+        self.rlen = torch.empty(nb, dtype=torch.int64, device=device)
+        self.rbk = torch.empty(nb, dtype=torch.int32, device=device)
+        self.tp = torch.empty(nb + 1, dtype=torch.int64, device=device)
+        self.parts = jit._partials(grid, GA, device)
+        self.out = K.agg_outputs(GA, device)
+        self.h_out = _Pinned(self.out[0].hs_buf.numel())
+        self.graph = None
+        self.replays = 0
+
+    def _enqueue(self, stream: int) -> None:
+        L = jit.runtime()
+        K = NL.lib()
+        NL.check(L.hs_memcpy_async(self.d_params.data_ptr(), self.h_params.ptr,
+                                   self.h_params.nbytes, 1, stream), "param H2D")
+        NL.check(K.hs_range_search_dev(C.byref(self.kd), NL.ptr(self.bucket_off), None, self.nb,
+                                       self.d_params.data_ptr(), NL.ptr(self.rstart),
+                                       NL.ptr(self.rlen), NL.ptr(self.rbk), stream),
+                 "hs_range_search_dev")
+        NL.check(K.hs_ranges_to_tiles(NL.ptr(self.rlen), self.nb, self.tile, NL.ptr(self.tp),
+                                      stream), "hs_ranges_to_tiles")
+        self.kernel.launch_ptr(self.grid, self.d_params.data_ptr() + PARAM_HEAD, stream,
+                               self.shmem)
+        p = self.parts
+        o = self.out
+        NL.check(K.hs_agg_final(NL.ptr(p[0]), NL.ptr(p[1]), NL.ptr(p[2]), NL.ptr(p[3]),
+                                self.grid, self.GA, NL.ptr(o[0]), NL.ptr(o[1]), NL.ptr(o[2]),
+                                NL.ptr(o[3]), stream), "hs_agg_final")
+        NL.check(L.hs_memcpy_async(self.h_out.ptr, o[0].hs_buf.data_ptr(), self.h_out.nbytes, 2,
+                                   stream), "result D2H")
+
+    def values_template(self) -> dict:
+        return {"rstart": self.rstart.data_ptr(), "rlen": self.rlen.data_ptr(),
+                "tile_prefix": self.tp.data_ptr(), "R": self.nb,
+                "psum": self.parts[0].data_ptr(), "pcnt": self.parts[1].data_ptr(),
+                "pmin": self.parts[2].data_ptr(), "pmax": self.parts[3].data_ptr()}
+
+    def run(self, bounds: Tuple[int, int, int, int, int, int], args_block: bytes):
+        """(sum, count, min, max) numpy arrays for one query."""
+        import torch
+        hp = self.h_params.view()
+        hp[:48] = np.frombuffer(struct.pack("<6q", *bounds), dtype=np.uint8)
+        hp[PARAM_HEAD:PARAM_HEAD + len(args_block)] = np.frombuffer(args_block, dtype=np.uint8)
+        cur = torch.cuda.current_stream()
+        if self.graph is None:
+            self._enqueue(cur.cuda_stream)         # eager first run (loads the module)
+            cur.synchronize()
+            res = self._results()
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream()
+            side.wait_stream(cur)
+            with torch.cuda.graph(g, stream=side):
+                self._enqueue(torch.cuda.current_stream().cuda_stream)
+            cur.wait_stream(side)
+            self.graph = g
+            return res
+        self.graph.replay()
+        cur.synchronize()
+        self.replays += 1
+        return self._results()
+
+    def _results(self):
+        h = self.h_out.view()
+        n = 8 * self.GA
+        return (h[0:n].view(np.float64).copy(), h[n:2 * n].view(np.int64).copy(),
+                h[2 * n:3 * n].view(np.float64).copy(), h[3 * n:4 * n].view(np.float64).copy())
+
+
+class GraphCache:
+    """Per-backend LRU of captured pipelines (graphs pin their buffers)."""
+
+    def __init__(self, capacity: int = 64):
+        self.capacity = capacity
+        self._lru: "OrderedDict[tuple, ScanAggGraph]" = OrderedDict()
+        self._lock = threading.Lock()
+
+    def get(self, key: tuple, make) -> ScanAggGraph:
+        with self._lock:
+            g = self._lru.get(key)
+            if g is not None:
+                self._lru.move_to_end(key)
+                return g
+        g = make()
+        with self._lock:
+            self._lru[key] = g
+            while len(self._lru) > self.capacity:
+                self._lru.popitem(last=False)
+        return g
+
+    def __len__(self):
+        return len(self._lru)
+
+
+def range_bounds(lo: Optional[int], lo_incl: bool, hi: Optional[int], hi_incl: bool):
+    """The 6-int64 bound block read by ``hs_range_search_dev`` (images as signed int64 bits)."""
+    def s64(v):
+        v = int(v or 0) & 0xFFFFFFFFFFFFFFFF
+        return v - (1 << 64) if v >= (1 << 63) else v
+    return (1 if lo is not None else 0, s64(lo), 1 if lo_incl else 0,
+            1 if hi is not None else 0, s64(hi), 1 if hi_incl else 0)

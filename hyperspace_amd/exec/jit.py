@@ -80,6 +80,15 @@ def runtime():
                 L.hs_jit_compile_to_cache.restype = C.c_int
                 L.hs_jit_compile_to_cache.argtypes = [C.c_char_p] * 4
                 L.hs_jit_last_error.restype = C.c_char_p
+                L.hs_host_alloc.restype = C.c_void_p
+                L.hs_host_alloc.argtypes = [C.c_size_t]
+                L.hs_host_free.restype = None
+                L.hs_host_free.argtypes = [C.c_void_p]
+                L.hs_memcpy_async.restype = C.c_int
+                L.hs_memcpy_async.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int,
+                                              C.c_void_p]
+                L.hs_stream_sync.restype = C.c_int
+                L.hs_stream_sync.argtypes = [C.c_void_p]
                 _rt = L
     return _rt
 
@@ -121,6 +130,23 @@ class Kernel:
         self.lds_bytes = lds_bytes
         self.block = block
         self._fn = None
+
+    def by_pointer(self) -> "Kernel":
+        """The same kernel taking ``const Args*`` (argument block in device memory): a captured
+        hipGraph replays it with new literals after one H2D of the block."""
+        sig = f"void {self.name}(Args a) {{"
+        assert sig in self.src
+        src = self.src.replace(sig, f"void {self.name}(const Args* __restrict__ ap) {{\n"
+                                    f"  const Args& a = *ap;")
+        return Kernel(src, self.name, self.args, self.lds_bytes, self.block)
+
+    def launch_ptr(self, grid: int, dev_args: int, stream_ptr: int, shmem: int = 0) -> None:
+        buf = struct.pack("<q", dev_args)
+        cbuf = C.create_string_buffer(buf, len(buf))
+        rc = runtime().hs_jit_launch(self.function(), grid, self.block, shmem or self.lds_bytes,
+                                     stream_ptr, cbuf, len(buf))
+        if rc != 0:
+            raise RuntimeError(f"JIT launch failed: {runtime().hs_jit_last_error().decode()}")
 
     def function(self):
         if self._fn is None:

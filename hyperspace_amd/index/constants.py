@@ -97,4 +97,7 @@ HBM_COMPRESSION_ENABLED = "spark.hyperspace.mi.hbmCompression.enabled"
 # off by default: the fused kernels measured latency-bound, not bandwidth-bound, on MI355X
 # (profiles/microbench_join_r1*.jsonl), so narrower columns did not pay for the decode
 HBM_COMPRESSION_ENABLED_DEFAULT = "false"
+# replay captured hipGraphs of the scan pipeline (exec/graphs.py)
+HIPGRAPH_ENABLED = "spark.hyperspace.mi.hipGraph.enabled"
+HIPGRAPH_ENABLED_DEFAULT = "true"
 FAULT_INJECTION = "spark.hyperspace.mi.faultInjection"

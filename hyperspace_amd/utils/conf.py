@@ -114,5 +114,9 @@ class HyperspaceConf:
         return _b(conf.get(C.CODEGEN_ENABLED, C.CODEGEN_ENABLED_DEFAULT))
 
     @staticmethod
+    def hipgraph_enabled(conf) -> bool:
+        return _b(conf.get(C.HIPGRAPH_ENABLED, C.HIPGRAPH_ENABLED_DEFAULT))
+
+    @staticmethod
     def hbm_compression_enabled(conf) -> bool:
         return _b(conf.get(C.HBM_COMPRESSION_ENABLED, C.HBM_COMPRESSION_ENABLED_DEFAULT))

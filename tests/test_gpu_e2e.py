@@ -108,6 +108,35 @@ def test_q6_filter_aggregate_native(tpch):
     assert "Hyperspace(Type: CI, Name: li_ship" in q.queryExecution.executed_plan.tree_string()
 
 
+def test_q6_graph_replays_with_new_literals(tpch):
+    """The captured hipGraph of the scan pipeline replays with each query's literals."""
+    s, lpath, _ = tpch
+    hs = Hyperspace(s)
+    li = s.read.parquet(lpath)
+    hs.createIndex(li, IndexConfig("li_ship", ["l_shipdate"],
+                                   ["l_discount", "l_quantity", "l_extendedprice"]))
+    Hyperspace.enable(s)
+    backend = s.backend()
+    for year, disc, qty in ((1994, 0.06, 24), (1995, 0.03, 25), (1993, 0.09, 24),
+                            (1994, 0.06, 24), (1997, 0.05, 30)):
+        q = li.filter(f"l_shipdate >= DATE '{year}-01-01' AND l_shipdate < DATE '{year + 1}-01-01'"
+                      f" AND l_discount >= {disc - 0.01:.2f} AND l_discount <= {disc + 0.01:.2f}"
+                      f" AND l_quantity < {qty}") \
+            .agg(sum_(col("l_extendedprice") * col("l_discount")).alias("revenue"),
+                 count("*").alias("n"), max_("l_quantity").alias("mq"))
+        g, c, path = _both(s, q, sort=False)
+        assert path == "native", s.backend().fallback_reason
+        _close(g, c)
+    assert len(backend.graphs) == 1
+    graph = next(iter(backend.graphs._lru.values()))
+    assert graph.replays >= 3
+    # disabling graphs runs the eager launch sequence with identical results
+    s.conf.set("spark.hyperspace.mi.hipGraph.enabled", "false")
+    g2, c2, _ = _both(s, q, sort=False)
+    _close(g2, c2)
+    _close(g2, g)
+
+
 def test_filter_rows_and_group_by_native(tpch):
     s, lpath, _ = tpch
     hs = Hyperspace(s)
