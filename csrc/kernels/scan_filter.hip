@@ -17,7 +17,7 @@
 #define SF_ITEMS 8
 #define SF_TILE (SF_BLOCK * SF_ITEMS)
 #define SF_GRID 2048
-#define FIN_BLOCK 256
+#define FIN_BLOCK 1024  // final reduction: 16 waves, so each lane sums only grid/1024 partials
 
 struct ScanParams {
   ColDesc cols[HS_MAX_COLS];
@@ -214,6 +214,7 @@ __global__ __launch_bounds__(FIN_BLOCK) void hs_agg_final_kernel(
   const int i = blockIdx.x;
   double s = 0.0, mn = __builtin_inf(), mx = -__builtin_inf();
   int64_t c = 0;
+#pragma unroll 4
   for (int b = threadIdx.x; b < nblk; b += FIN_BLOCK) {
     const int64_t o = (int64_t)b * GA + i;
     s += psum[o];

@@ -1,0 +1,264 @@
+// Native Parquet writer for index bucket files (SURVEY.md §2.3 K4 "Parquet encode").
+//
+// The MI355X does the encoding work — dictionary build, code assignment and bit-packing run in
+// HIP kernels (exec/pq_encode.py + csrc/kernels/parquet_encode.hip) — so a column chunk arrives
+// here as ready page payload in pinned host memory: PLAIN values, or bit-packed dictionary codes.
+// This file only frames it: Thrift-compact page headers, definition levels (all valid: one RLE
+// run), the dictionary page, and the footer; payload bytes go to the file with pwritev straight
+// from the pinned buffers (no host-side copy or re-encode).
+//
+// Output: Parquet format 1 files with data page V1, codec UNCOMPRESSED, optional flat columns,
+// readable by Spark, pyarrow and the native reader in hs_parquet.cpp.
+#include <fcntl.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+// ------------------------------------------------------------------ Thrift compact writer
+struct TWriter {
+  std::vector<uint8_t> b;
+  std::vector<int16_t> last{0};
+
+  void byte(uint8_t v) { b.push_back(v); }
+  void varint(uint64_t v) {
+    while (v >= 0x80) { b.push_back((uint8_t)(v | 0x80)); v >>= 7; }
+    b.push_back((uint8_t)v);
+  }
+  void zz(int64_t v) { varint(((uint64_t)v << 1) ^ (uint64_t)(v >> 63)); }
+  void field(int16_t id, int type) {
+    const int16_t d = (int16_t)(id - last.back());
+    if (d > 0 && d <= 15) byte((uint8_t)((d << 4) | type));
+    else { byte((uint8_t)type); zz(id); }
+    last.back() = id;
+  }
+  void i32(int16_t id, int64_t v) { field(id, 5); zz(v); }
+  void i64(int16_t id, int64_t v) { field(id, 6); zz(v); }
+  void str(int16_t id, const std::string& s) { field(id, 8); varint(s.size()); bin(s); }
+  void bin(const std::string& s) { b.insert(b.end(), s.begin(), s.end()); }
+  void begin_struct(int16_t id) { field(id, 12); last.push_back(0); }
+  void begin_anon_struct() { last.push_back(0); }  // list element
+  void end_struct() { byte(0); last.pop_back(); }
+  void list(int16_t id, int elem_type, int64_t n) {
+    field(id, 9);
+    if (n < 15) byte((uint8_t)((n << 4) | elem_type));
+    else { byte((uint8_t)(0xf0 | elem_type)); varint((uint64_t)n); }
+  }
+};
+
+}  // namespace
+
+// Per column chunk (one row group) handed over by Python.
+struct HsPqWCol {
+  const char* name;
+  int32_t ptype;          // 1 INT32, 2 INT64, 4 FLOAT, 5 DOUBLE, 6 BYTE_ARRAY
+  int32_t logical;        // 0 none, 1 DATE, 2 STRING
+  int32_t dict;           // 1: payload is bit-packed dictionary codes
+  int32_t bit_width;      // dict code width
+  const uint8_t* dict_page;  // PLAIN dictionary values (fixed width, or BYTE_ARRAY len+bytes)
+  int64_t dict_bytes;
+  int64_t dict_count;
+  const uint8_t* payload;    // PLAIN values or packed codes (ceil(n/8)*bit_width bytes)
+  int64_t payload_bytes;
+};
+
+namespace {
+
+struct ColPos {
+  int64_t dict_off = -1, data_off = 0, total = 0;
+};
+
+void def_levels_all_valid(std::vector<uint8_t>& v, int64_t n) {
+  // 4-byte length prefix + one RLE run (header (n << 1), value 1 in one byte)
+  std::vector<uint8_t> run;
+  uint64_t h = (uint64_t)n << 1;
+  while (h >= 0x80) { run.push_back((uint8_t)(h | 0x80)); h >>= 7; }
+  run.push_back((uint8_t)h);
+  run.push_back(1);
+  const uint32_t len = (uint32_t)run.size();
+  v.insert(v.end(), (const uint8_t*)&len, (const uint8_t*)&len + 4);
+  v.insert(v.end(), run.begin(), run.end());
+}
+
+std::vector<uint8_t> page_header(int type, int64_t size, int64_t nvals, int enc) {
+  TWriter w;
+  w.i32(1, type);
+  w.i32(2, size);
+  w.i32(3, size);
+  if (type == 2) {
+    w.begin_struct(7);
+    w.i32(1, nvals);
+    w.i32(2, enc);
+    w.end_struct();
+  } else {
+    w.begin_struct(5);
+    w.i32(1, nvals);
+    w.i32(2, enc);
+    w.i32(3, 3);  // definition levels: RLE
+    w.i32(4, 3);  // repetition levels: RLE
+    w.end_struct();
+  }
+  w.byte(0);
+  return w.b;
+}
+
+bool write_all(int fd, std::vector<iovec>& iov, int64_t& pos) {
+  size_t i = 0;
+  while (i < iov.size()) {
+    const int cnt = (int)std::min<size_t>(iov.size() - i, 512);
+    ssize_t k = pwritev(fd, iov.data() + i, cnt, pos);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    pos += k;
+    while (k > 0 && i < iov.size()) {   // advance past fully written vectors
+      if ((size_t)k >= iov[i].iov_len) { k -= (ssize_t)iov[i].iov_len; ++i; }
+      else {
+        iov[i].iov_base = (uint8_t*)iov[i].iov_base + k;
+        iov[i].iov_len -= (size_t)k;
+        k = 0;
+      }
+    }
+  }
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Write one Parquet file: `ncols` columns x `nrg` row groups (cols[rg * ncols + c]),
+// rg_rows[rg] rows each, no nulls.  Returns 0 or -errno.
+int hs_pq_write_file(const char* path, int ncols, int nrg, const int64_t* rg_rows,
+                     const HsPqWCol* cols, const char* created_by) {
+  const std::string tmp = std::string(path);
+  const int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd < 0) return -errno;
+  int64_t pos = 0;
+  std::vector<std::vector<uint8_t>> keep;   // header bytes referenced by iovecs
+  keep.reserve((size_t)ncols * nrg * 4 + 4);
+  std::vector<iovec> iov;
+  static const char magic[4] = {'P', 'A', 'R', '1'};
+  iov.push_back({(void*)magic, 4});
+  int64_t off = 4;
+  std::vector<ColPos> posv((size_t)ncols * nrg);
+  for (int g = 0; g < nrg; ++g) {
+    const int64_t n = rg_rows[g];
+    for (int c = 0; c < ncols; ++c) {
+      const HsPqWCol& col = cols[(size_t)g * ncols + c];
+      ColPos& p = posv[(size_t)g * ncols + c];
+      const int64_t start = off;
+      if (col.dict) {
+        keep.push_back(page_header(2, col.dict_bytes, col.dict_count, 0));
+        p.dict_off = off;
+        iov.push_back({keep.back().data(), keep.back().size()});
+        iov.push_back({(void*)col.dict_page, (size_t)col.dict_bytes});
+        off += (int64_t)keep.back().size() + col.dict_bytes;
+      }
+      std::vector<uint8_t> pre;
+      def_levels_all_valid(pre, n);
+      if (col.dict) {
+        pre.push_back((uint8_t)col.bit_width);
+        uint64_t h = ((uint64_t)((n + 7) / 8) << 1) | 1;  // one bit-packed run
+        while (h >= 0x80) { pre.push_back((uint8_t)(h | 0x80)); h >>= 7; }
+        pre.push_back((uint8_t)h);
+      }
+      const int64_t psize = (int64_t)pre.size() + col.payload_bytes;
+      keep.push_back(page_header(0, psize, n, col.dict ? 8 : 0));
+      p.data_off = off;
+      iov.push_back({keep.back().data(), keep.back().size()});
+      off += (int64_t)keep.back().size();
+      keep.push_back(std::move(pre));
+      iov.push_back({keep.back().data(), keep.back().size()});
+      if (col.payload_bytes) iov.push_back({(void*)col.payload, (size_t)col.payload_bytes});
+      off += psize;
+      p.total = off - start;
+    }
+  }
+  // footer
+  TWriter w;
+  w.i32(1, 1);
+  w.list(2, 12, ncols + 1);
+  w.begin_anon_struct();
+  w.str(4, "schema");
+  w.i32(5, ncols);
+  w.end_struct();
+  for (int c = 0; c < ncols; ++c) {
+    const HsPqWCol& col = cols[c];
+    w.begin_anon_struct();
+    w.i32(1, col.ptype);
+    w.i32(3, 1);  // OPTIONAL
+    w.str(4, col.name);
+    if (col.logical == 1) w.i32(6, 6);        // converted type DATE
+    else if (col.logical == 2) w.i32(6, 0);   // UTF8
+    if (col.logical) {
+      w.begin_struct(10);                       // LogicalType union
+      w.begin_struct(col.logical == 1 ? 6 : 1);  // DateType / StringType
+      w.end_struct();
+      w.end_struct();
+    }
+    w.end_struct();
+  }
+  int64_t total_rows = 0;
+  for (int g = 0; g < nrg; ++g) total_rows += rg_rows[g];
+  w.i64(3, total_rows);
+  w.list(4, 12, nrg);
+  for (int g = 0; g < nrg; ++g) {
+    w.begin_anon_struct();
+    w.list(1, 12, ncols);
+    int64_t rg_bytes = 0;
+    for (int c = 0; c < ncols; ++c) {
+      const HsPqWCol& col = cols[(size_t)g * ncols + c];
+      const ColPos& p = posv[(size_t)g * ncols + c];
+      rg_bytes += p.total;
+      w.begin_anon_struct();                   // ColumnChunk
+      w.i64(2, p.dict_off >= 0 ? p.dict_off : p.data_off);
+      w.begin_struct(3);                       // ColumnMetaData
+      w.i32(1, col.ptype);
+      if (col.dict) {
+        w.list(2, 5, 3);
+        w.zz(0); w.zz(3); w.zz(8);              // PLAIN, RLE, RLE_DICTIONARY
+      } else {
+        w.list(2, 5, 2);
+        w.zz(0); w.zz(3);                       // PLAIN, RLE
+      }
+      w.list(3, 8, 1);
+      w.varint(strlen(col.name));
+      w.bin(col.name);
+      w.i32(4, 0);                              // UNCOMPRESSED
+      w.i64(5, rg_rows[g]);
+      w.i64(6, p.total);
+      w.i64(7, p.total);
+      w.i64(9, p.data_off);
+      if (p.dict_off >= 0) w.i64(11, p.dict_off);
+      w.end_struct();
+      w.end_struct();
+    }
+    w.i64(2, rg_bytes);
+    w.i64(3, rg_rows[g]);
+    w.end_struct();
+  }
+  w.str(6, created_by ? created_by : "hyperspace_amd");
+  w.byte(0);
+  keep.push_back(std::move(w.b));
+  const uint32_t flen = (uint32_t)keep.back().size();
+  iov.push_back({keep.back().data(), keep.back().size()});
+  std::vector<uint8_t> tail(8);
+  memcpy(tail.data(), &flen, 4);
+  memcpy(tail.data() + 4, magic, 4);
+  keep.push_back(std::move(tail));
+  iov.push_back({keep.back().data(), 8});
+  const bool ok = write_all(fd, iov, pos);
+  const int err = ok ? 0 : -errno;
+  if (close(fd) != 0 && ok) return -errno;
+  return err;
+}
+
+}  // extern "C"

@@ -73,10 +73,22 @@ def _sort_and_write(session, table: Dict[str, DeviceColumn], names: List[str], b
     rg = HyperspaceConf.index_row_group_rows(session.conf)
     job = str(uuid.uuid4())
     from . import staging
-    paths = staging.download_buckets(
-        gathered, names, schema, off,
-        lambda t, b: write_bucket_file(t, out_path, task_id, job, b, codec, rg),
-        bucket.device)
+    paths = None
+    if codec in ("none", "uncompressed") and os.environ.get("HS_NATIVE_PQ_WRITE", "1") == "1":
+        # K4 on the device: dictionary build + bit-packing in HIP, host only frames pages
+        from . import pq_encode
+        from ..io.writer import bucket_file_name
+        local = P.to_local(out_path)
+        os.makedirs(local, exist_ok=True)
+        paths = pq_encode.write_buckets(
+            dict(zip(names, gathered)), names, schema, off,
+            lambda b: os.path.join(local, bucket_file_name(task_id, job, b, "none")), rg,
+            bucket.device)
+    if paths is None:
+        paths = staging.download_buckets(
+            gathered, names, schema, off,
+            lambda t, b: write_bucket_file(t, out_path, task_id, job, b, codec, rg),
+            bucket.device)
     LAST_BUILD_STATS.update({"sort_gather_s": t1 - t0,
                              "d2h_write_s": time.perf_counter() - t1})
     return paths

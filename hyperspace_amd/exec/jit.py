@@ -136,8 +136,10 @@ class Kernel:
         hipGraph replays it with new literals after one H2D of the block."""
         sig = f"void {self.name}(Args a) {{"
         assert sig in self.src
+        # copy the block once: a reference would make every field access a memory load the
+        # compiler cannot hoist across the kernel's own stores
         src = self.src.replace(sig, f"void {self.name}(const Args* __restrict__ ap) {{\n"
-                                    f"  const Args& a = *ap;")
+                                    f"  const Args a = *ap;")
         return Kernel(src, self.name, self.args, self.lds_bytes, self.block)
 
     def launch_ptr(self, grid: int, dev_args: int, stream_ptr: int, shmem: int = 0) -> None:

@@ -1,0 +1,279 @@
+"""Device-side Parquet encoding of index bucket files (SURVEY.md §2.3 K4 "Parquet encode
+kernels"; host framing in ``csrc/runtime/hs_parquet_write.cpp``).
+
+The sorted, bucket-major index columns are still in HBM when the build writes them, so the
+encoding happens there:
+
+* **dictionary build** — a strided sample of each fixed-width column is uniqued on the device;
+  if it is small (``DICT_MAX``) every value is looked up in it by bit pattern
+  (``hs_pq_dict_codes``; a miss falls back to a full device unique), giving int32 codes.
+  String columns are already codes into a sorted host dictionary.
+* **bit-packing** — ``hs_pq_pack`` writes one bit-packed run per data page (one page per bucket
+  file row group).
+* PLAIN columns (high cardinality) are their own payload.
+
+Only the encoded bytes cross PCIe: for the TPC-H ``l_shipdate`` index (``l_discount`` 11
+values, ``l_quantity`` 50, ``l_shipdate`` 2.5k) that is ~12 B/row instead of 28.  The host
+writes each bucket file with ``pwritev`` straight from the pinned D2H buffers.
+
+Files are Parquet v1 (data page V1, UNCOMPRESSED, optional flat columns); anything outside that
+(nulls, booleans, decimals, timestamps, a requested codec) returns ``None`` so the caller writes
+with pyarrow instead.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import pyarrow as pa
+
+from ..ops import _lib as NL
+from .device_table import DeviceColumn, is_string
+
+DICT_MAX = 4096          # fixed-width dictionaries (repeated in every row group's chunk)
+DICT_MAX_STRINGS = 1 << 16
+SAMPLE = 1 << 16
+
+PAGE_DTYPE = np.dtype([("row0", "<i8"), ("n", "<i8"), ("out_off", "<i8"), ("gpre", "<i8")])
+
+
+class WCol(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("ptype", C.c_int32), ("logical", C.c_int32),
+                ("dict", C.c_int32), ("bit_width", C.c_int32), ("dict_page", C.c_void_p),
+                ("dict_bytes", C.c_int64), ("dict_count", C.c_int64), ("payload", C.c_void_p),
+                ("payload_bytes", C.c_int64)]
+
+
+def _writer():
+    from .jit import runtime
+    L = runtime()
+    if not getattr(L, "_hs_pqw", False):
+        L.hs_pq_write_file.restype = C.c_int
+        L.hs_pq_write_file.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_int64),
+                                       C.POINTER(WCol), C.c_char_p]
+        L._hs_pqw = True
+    return L
+
+
+def _physical(t: pa.DataType):
+    """(Parquet physical type, logical 0/1 DATE/2 STRING, element bytes) or None."""
+    if pa.types.is_date32(t):
+        return 1, 1, 4
+    if pa.types.is_int32(t):
+        return 1, 0, 4
+    if pa.types.is_int64(t):
+        return 2, 0, 8
+    if pa.types.is_float32(t):
+        return 4, 0, 4
+    if pa.types.is_float64(t):
+        return 5, 0, 8
+    if is_string(t):
+        return 6, 2, 0
+    return None
+
+
+class ColPlan:
+    def __init__(self, name: str, ptype: int, logical: int, eb: int):
+        self.name = name
+        self.bname = name.encode()
+        self.ptype, self.logical, self.eb = ptype, logical, eb
+        self.dict = False
+        self.bw = 0
+        self.dict_page: Optional[np.ndarray] = None
+        self.dict_count = 0
+        self.payload = None          # device uint8
+        self.page_off: Optional[np.ndarray] = None   # byte offset of every page (+ end)
+
+    @property
+    def encoded_bytes(self) -> int:
+        return int(self.page_off[-1])
+
+
+def _bit_width(n: int) -> int:
+    return max(1, math.ceil(math.log2(max(n, 2))))
+
+
+def _string_dict_page(d: pa.Array) -> np.ndarray:
+    """PLAIN BYTE_ARRAY encoding of a string dictionary: (u32 length, bytes) per entry."""
+    a = d.cast(pa.large_string()).combine_chunks() if isinstance(d, pa.ChunkedArray) else \
+        d.cast(pa.large_string())
+    bufs = a.buffers()
+    offs = np.frombuffer(bufs[1], dtype=np.int64)[a.offset:a.offset + len(a) + 1]
+    data = np.frombuffer(bufs[2], dtype=np.uint8) if bufs[2] is not None else np.zeros(0, np.uint8)
+    lens = np.diff(offs)
+    out = np.empty(int(lens.sum()) + 4 * len(a), dtype=np.uint8)
+    pos = 0
+    for i in range(len(a)):   # dictionaries are small (<= DICT_MAX_STRINGS)
+        ln = int(lens[i])
+        out[pos:pos + 4] = np.frombuffer(np.uint32(ln).tobytes(), dtype=np.uint8)
+        out[pos + 4:pos + 4 + ln] = data[offs[i]:offs[i] + ln]
+        pos += 4 + ln
+    return out
+
+
+def _dict_codes(v, eb: int, dbits, device):
+    import torch
+    codes = torch.empty(v.numel(), dtype=torch.int32, device=device)
+    miss = torch.zeros(1, dtype=torch.int32, device=device)
+    NL.check(NL.lib().hs_pq_dict_codes(v.data_ptr(), v.numel(), eb, dbits.data_ptr(),
+                                       dbits.numel(), codes.data_ptr(), miss.data_ptr(),
+                                       NL.stream_ptr()), "hs_pq_dict_codes")
+    return codes, bool(miss.item())
+
+
+def plan_columns(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: pa.Schema,
+                 pages: np.ndarray, device) -> Optional[List[ColPlan]]:
+    """Encode every column on the device; None if some column needs the pyarrow writer."""
+    import torch
+    plans = []
+    np_pages = pages
+    gpre = np.concatenate([[0], np.cumsum((np_pages["n"] + 7) // 8)]).astype(np.int64)
+    for name in names:
+        dc = cols[name]
+        phys = _physical(schema.field(name).type)
+        if phys is None:
+            return None
+        if dc.valid is not None and bool((dc.valid == 0).any().item()):
+            return None
+        ptype, logical, eb = phys
+        cp = ColPlan(name, ptype, logical, eb)
+        codes = None
+        if ptype == 6:
+            d = dc.dictionary
+            if d is None or len(d) == 0 or len(d) > DICT_MAX_STRINGS:
+                return None
+            codes = dc.data
+            cp.dict_page = _string_dict_page(d)
+            cp.dict_count = len(d)
+        else:
+            v = dc.data.view(torch.int32 if eb == 4 else torch.int64)
+            n = v.numel()
+            step = max(1, n // SAMPLE)
+            u = torch.unique(v[::step])
+            if 0 < u.numel() <= DICT_MAX // 2:
+                codes, missed = _dict_codes(v, eb, u, device)
+                if missed:
+                    u = torch.unique(v)
+                    codes = None
+                    if u.numel() <= DICT_MAX:
+                        codes, _ = _dict_codes(v, eb, u, device)
+            if codes is not None:
+                cp.dict_page = u.cpu().numpy().view(np.uint8)
+                cp.dict_count = int(u.numel())
+        if codes is not None:
+            cp.dict = True
+            cp.bw = _bit_width(cp.dict_count)
+            sizes = ((np_pages["n"] + 7) // 8) * cp.bw
+            cp.page_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+            tab = np_pages.copy()
+            tab["out_off"] = cp.page_off[:-1]
+            tab["gpre"] = gpre[:-1]
+            dtab = torch.from_numpy(tab.view(np.uint8).copy()).to(device)
+            cp.payload = torch.empty(int(cp.page_off[-1]) + 16, dtype=torch.uint8, device=device)
+            NL.check(NL.lib().hs_pq_pack(codes.data_ptr(), dtab.data_ptr(), len(tab),
+                                         int(gpre[-1]), cp.bw, cp.payload.data_ptr(),
+                                         NL.stream_ptr()), "hs_pq_pack")
+        else:
+            cp.payload = dc.data.view(torch.uint8)
+            cp.page_off = np.concatenate([np_pages["row0"], [np_pages["row0"][-1] +
+                                                              np_pages["n"][-1]]]) * eb
+        plans.append(cp)
+    return plans
+
+
+def page_table(bucket_off: np.ndarray, rg_rows: int) -> Tuple[np.ndarray, List[Tuple[int, int, int]]]:
+    """Pages (= row groups) of every non-empty bucket and, per bucket, (bucket, first page,
+    page count)."""
+    rows, files = [], []
+    for b in range(len(bucket_off) - 1):
+        lo, hi = int(bucket_off[b]), int(bucket_off[b + 1])
+        if hi <= lo:
+            continue
+        first = len(rows)
+        for r0 in range(lo, hi, rg_rows):
+            rows.append((r0, min(rg_rows, hi - r0), 0, 0))
+        files.append((b, first, len(rows) - first))
+    return np.array(rows, dtype=PAGE_DTYPE), files
+
+
+def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: pa.Schema,
+                  bucket_off: np.ndarray, path_of: Callable[[int], str], rg_rows: int, device,
+                  chunk_bytes: int = 512 << 20) -> Optional[List[str]]:
+    """Encode on the device and write one Parquet file per non-empty bucket; None when the
+    columns need the pyarrow writer."""
+    import torch
+    from .staging import copy_stream, io_pool
+    pages, files = page_table(bucket_off, rg_rows)
+    if not files:
+        return []
+    plans = plan_columns(cols, names, schema, pages, device)
+    if plans is None:
+        return None
+    L = _writer()
+    stream = copy_stream(device)
+    stream.wait_stream(torch.cuda.current_stream(device))
+    # group files into ~chunk_bytes of encoded data per D2H batch
+    batches, cur, cur_bytes = [], [], 0
+    for f in files:
+        _, p0, pn = f
+        nb = sum(int(cp.page_off[p0 + pn] - cp.page_off[p0]) for cp in plans)
+        if cur and cur_bytes + nb > chunk_bytes:
+            batches.append(cur)
+            cur, cur_bytes = [], 0
+        cur.append(f)
+        cur_bytes += nb
+    if cur:
+        batches.append(cur)
+    futs = []
+    max_inflight = 2 * min(16, os.cpu_count() or 4)
+    created_by = b"hyperspace_amd (MI355X device-encoded)"
+    for batch in batches:
+        if len(futs) >= max_inflight:
+            futs[len(futs) - max_inflight].result()
+        p_first = batch[0][1]
+        p_end = batch[-1][1] + batch[-1][2]
+        host = []
+        with torch.cuda.stream(stream):
+            for cp in plans:
+                lo, hi = int(cp.page_off[p_first]), int(cp.page_off[p_end])
+                h = torch.empty(max(hi - lo, 1), dtype=torch.uint8, pin_memory=True)
+                if hi > lo:
+                    h[:hi - lo].copy_(cp.payload[lo:hi], non_blocking=True)
+                host.append((h, lo))
+            ev = torch.cuda.Event()
+            ev.record(stream)
+
+        def write_batch(batch=batch, host=host, ev=ev):
+            ev.synchronize()
+            out = []
+            for b, p0, pn in batch:
+                arr = (WCol * (pn * len(plans)))()
+                rg = (C.c_int64 * pn)()
+                for g in range(pn):
+                    rg[g] = int(pages["n"][p0 + g])
+                    for c, (cp, (h, base)) in enumerate(zip(plans, host)):
+                        w = arr[g * len(plans) + c]
+                        lo = int(cp.page_off[p0 + g]) - base
+                        w.name = cp.bname
+                        w.ptype, w.logical = cp.ptype, cp.logical
+                        w.dict, w.bit_width = int(cp.dict), cp.bw
+                        if cp.dict:
+                            w.dict_page = cp.dict_page.ctypes.data
+                            w.dict_bytes = cp.dict_page.nbytes
+                            w.dict_count = cp.dict_count
+                        w.payload = h.data_ptr() + lo
+                        w.payload_bytes = int(cp.page_off[p0 + g + 1] - cp.page_off[p0 + g])
+                path = path_of(b)
+                rc = L.hs_pq_write_file(path.encode(), len(plans), pn, rg, arr, created_by)
+                if rc != 0:
+                    raise OSError(-rc, f"native Parquet write failed: {path}")
+                out.append(path)
+            return out
+        futs.append(io_pool().submit(write_batch))
+    paths = []
+    for fu in futs:
+        paths.extend(fu.result())
+    return paths

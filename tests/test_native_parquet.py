@@ -181,3 +181,123 @@ def test_native_parquet_gpu_decode_matches_pyarrow(tmp_path, device):
             np.testing.assert_array_equal(col.valid.cpu().numpy().astype(bool), valid)
         np.testing.assert_array_equal(vals[valid], ref.drop_null().to_numpy())
     assert "s" in up.host_strings  # strings still come back through pyarrow
+
+
+# ------------------------------------------------------------------------------------------------
+# Writer framing (csrc/runtime/hs_parquet_write.cpp) with host-packed payloads
+def _pack_host(codes: np.ndarray, bw: int) -> bytes:
+    """LSB-first bit-packing in groups of 8 (the contract of the hs_pq_pack kernel)."""
+    n = len(codes)
+    pad = (-n) % 8
+    c = np.concatenate([codes.astype(np.uint64), np.zeros(pad, np.uint64)])
+    bits = ((c[:, None] >> np.arange(bw, dtype=np.uint64)) & 1).astype(np.uint8).reshape(-1)
+    return np.packbits(bits, bitorder="little").tobytes()
+
+
+def test_native_writer_round_trips_through_pyarrow_and_native_reader(tmp_path):
+    import ctypes as C
+    from hyperspace_amd.exec import pq_encode as PE
+    rng = np.random.default_rng(4)
+    rgs = [1000, 777]
+    n = sum(rgs)
+    plain = rng.integers(-10**12, 10**12, n).astype(np.int64)
+    dvals = np.array([0.0, -0.0, 0.05, 0.1, np.nan], dtype=np.float64)
+    dcodes = rng.integers(0, len(dvals), n)
+    dates = np.sort(rng.integers(8000, 8050, n)).astype(np.int32)
+    ddict = np.unique(dates)
+    date_codes = np.searchsorted(ddict, dates)
+    sdict = pa.array(["A", "N", "R", "long string value"])
+    scodes = rng.integers(0, len(sdict), n)
+    sd_page = PE._string_dict_page(sdict)
+    keep = []
+
+    def buf(b: bytes):
+        a = np.frombuffer(b, dtype=np.uint8).copy()
+        keep.append(a)
+        return a.ctypes.data, a.nbytes
+
+    L = PE._writer()
+    cols = (PE.WCol * (4 * len(rgs)))()
+    start = 0
+    for g, rows in enumerate(rgs):
+        sl = slice(start, start + rows)
+        specs = [("k", 2, 0, 0, 0, None, 0, plain[sl].tobytes()),
+                 ("d", 5, 0, 1, 3, dvals.tobytes(), len(dvals), _pack_host(dcodes[sl], 3)),
+                 ("t", 1, 1, 1, 6, ddict.tobytes(), len(ddict), _pack_host(date_codes[sl], 6)),
+                 ("s", 6, 2, 1, 2, sd_page.tobytes(), len(sdict), _pack_host(scodes[sl], 2))]
+        for c, (name, pt, lg, dic, bw, dpage, dcount, payload) in enumerate(specs):
+            w = cols[g * 4 + c]
+            w.name, w.ptype, w.logical, w.dict, w.bit_width = name.encode(), pt, lg, dic, bw
+            if dic:
+                w.dict_page, w.dict_bytes = buf(dpage)
+                w.dict_count = dcount
+            w.payload, w.payload_bytes = buf(payload)
+        start += rows
+    path = tmp_path / "native.parquet"
+    rg = (C.c_int64 * len(rgs))(*rgs)
+    assert L.hs_pq_write_file(str(path).encode(), 4, len(rgs), rg, cols, b"test") == 0
+    t = pq.read_table(path)
+    assert t.schema.field("t").type == pa.date32() and t.schema.field("s").type == pa.string()
+    np.testing.assert_array_equal(t.column("k").to_numpy(), plain)
+    got_d = t.column("d").to_numpy()
+    np.testing.assert_array_equal(got_d.view(np.int64), dvals[dcodes].view(np.int64))  # bit-exact
+    np.testing.assert_array_equal(t.column("t").cast(pa.int32()).to_numpy(), dates)
+    assert t.column("s").to_pylist() == sdict.take(pa.array(scodes)).to_pylist()
+    assert pq.ParquetFile(path).metadata.num_row_groups == 2
+    # the native reader decodes the same file (dictionary + bit-packed pages)
+    with NP.PqFile(str(path)) as f:
+        rc, b, info, vr, lr = f.read_chunk_host(1, f.column("d"))
+        assert rc == NP.OK and info.dict_encoded
+        dense, _ = NP.expand_host(b, info, vr, lr, np.dtype(np.float64))
+        np.testing.assert_array_equal(dense.view(np.int64), dvals[dcodes[1000:]].view(np.int64))
+
+
+@pytest.mark.gpu
+def test_device_encoded_bucket_files(tmp_path, device):
+    """pq_encode: device dictionary build (sample + full-unique fallback), HIP bit-packing and
+    the native writer produce bucket files pyarrow reads back bit-exactly."""
+    import torch
+    from hyperspace_amd.exec import pq_encode as PE
+    from hyperspace_amd.exec.device_table import DeviceColumn
+    rng = np.random.default_rng(12)
+    n = 300_000
+    dvals = np.array([0.0, -0.0, 0.05, 0.1, np.nan, 1e300], dtype=np.float64)
+    data = {"plain": rng.integers(-10**15, 10**15, n).astype(np.int64),
+            "lowcard": dvals[rng.integers(0, len(dvals), n)],
+            # rare values the sample misses: forces the full device unique
+            "rare": np.where(rng.random(n) < 0.0005, rng.integers(100, 2000, n),
+                             rng.integers(0, 8, n)).astype(np.int32),
+            "date": rng.integers(8000, 8100, n).astype(np.int32)}
+    sdict = pa.array(sorted({f"s{i}" for i in range(37)}))
+    scodes = rng.integers(0, len(sdict), n).astype(np.int32)
+    cols = {k: DeviceColumn(torch.from_numpy(v).to(device), None,
+                            pa.date32() if k == "date" else pa.from_numpy_dtype(v.dtype))
+            for k, v in data.items()}
+    cols["str"] = DeviceColumn(torch.from_numpy(scodes).to(device), None, pa.string(), sdict)
+    names = list(cols)
+    schema = pa.schema([pa.field(k, cols[k].atype) for k in names])
+    counts = rng.multinomial(n, np.ones(16) / 16)
+    counts[3] = 0
+    counts[0] += n - counts.sum()
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    paths = PE.write_buckets(cols, names, schema, off,
+                             lambda b: str(tmp_path / f"b{b:03d}.parquet"), 7_000, device)
+    assert paths is not None and len(paths) == 15
+    for b in range(16):
+        lo, hi = int(off[b]), int(off[b + 1])
+        p = tmp_path / f"b{b:03d}.parquet"
+        if hi == lo:
+            assert not p.exists()
+            continue
+        t = pq.read_table(p)
+        assert t.num_rows == hi - lo
+        np.testing.assert_array_equal(t.column("plain").to_numpy(), data["plain"][lo:hi])
+        np.testing.assert_array_equal(t.column("lowcard").to_numpy().view(np.int64),
+                                      data["lowcard"][lo:hi].view(np.int64))
+        np.testing.assert_array_equal(t.column("rare").to_numpy(), data["rare"][lo:hi])
+        np.testing.assert_array_equal(t.column("date").cast(pa.int32()).to_numpy(),
+                                      data["date"][lo:hi])
+        assert t.column("str").to_pylist() == sdict.take(pa.array(scodes[lo:hi])).to_pylist()
+        md = pq.ParquetFile(p).metadata
+        assert md.num_row_groups == (hi - lo + 6_999) // 7_000
+        assert "RLE_DICTIONARY" in md.row_group(0).column(1).encodings
