@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--data-dir", default=os.environ.get("HS_BENCH_DIR", "/tmp/hs_bench"))
     ap.add_argument("--workers", type=int, default=int(os.environ.get("HS_BENCH_WORKERS", "0")))
     ap.add_argument("--no-crosscheck", action="store_true")
+    ap.add_argument("--codec", default="none",
+                    help="index file codec; 'none' = device dictionary/bit-packed encoding "
+                         "(exec/pq_encode.py), otherwise pyarrow with that codec")
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
                     help="cpu = the pyarrow host engine (measured baseline, BASELINE.md)")
     args = ap.parse_args()
@@ -104,7 +107,7 @@ def main():
                       "spark.sql.autoBroadcastJoinThreshold": "-1",
                       "spark.sql.shuffle.partitions": str(args.buckets),
                       "spark.hyperspace.mi.execution.device": args.device,
-                      "spark.hyperspace.mi.index.codec": "snappy"},
+                      "spark.hyperspace.mi.index.codec": args.codec},
                 warehouse_dir=os.path.join(args.data_dir, "wh"))
     s.dist = dist
     hs = Hyperspace(s)

@@ -125,6 +125,20 @@ int hs_pq_decode_values(const uint8_t* buf, const HsPqRun* runs, int64_t nruns, 
   return (int)hipGetLastError();
 }
 
+// Load the decode kernels' code objects from the calling thread (empty launches).  HIP loads a
+// library's kernels lazily on first launch; doing that once from the main thread keeps the
+// first launches of the staging worker threads from racing the load.
+int hs_pq_warmup(void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(hs_pq_values_kernel<uint32_t>, dim3(1), dim3(256), 0, s, nullptr, nullptr,
+                     (int64_t)0, (int64_t)0, (int64_t)0, (uint32_t*)nullptr);
+  hipLaunchKernelGGL(hs_pq_values_kernel<uint64_t>, dim3(1), dim3(256), 0, s, nullptr, nullptr,
+                     (int64_t)0, (int64_t)0, (int64_t)0, (uint64_t*)nullptr);
+  hipLaunchKernelGGL(hs_pq_levels_kernel, dim3(1), dim3(256), 0, s, nullptr, nullptr, (int64_t)0,
+                     (uint8_t*)nullptr);
+  return (int)hipStreamSynchronize(s);
+}
+
 // Expand definition-level runs (max level 1) into one validity byte per row.
 int hs_pq_decode_levels(const uint8_t* buf, const HsPqRun* runs, int64_t nruns, uint8_t* valid,
                         void* stream) {

@@ -110,6 +110,18 @@ def fixed_width_numpy(arr) -> Tuple[np.ndarray, Optional[np.ndarray]]:
     return vals, valid
 
 
+_WARM = False
+
+
+def _warm_decode_kernels() -> None:
+    """Load the page-decode kernels from this (main) thread before workers launch them."""
+    global _WARM
+    if not _WARM:
+        from ..ops import _lib as NL
+        NL.check(NL.lib().hs_pq_warmup(NL.stream_ptr()), "hs_pq_warmup")
+        _WARM = True
+
+
 def native_decode_enabled() -> bool:
     """Native Parquet page decode (HIP) for staging; ``HS_NATIVE_PARQUET=0`` forces pyarrow."""
     return os.environ.get("HS_NATIVE_PARQUET", "1") == "1"
@@ -172,6 +184,8 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
         st.wait_stream(main)  # allocations above happen-before the copies
 
     native = parquet_local is not None and native_decode_enabled()
+    if native:
+        _warm_decode_kernels()
 
     def work(i: int):
         torch.cuda.set_device(device)

@@ -142,6 +142,7 @@ def lib():
     _sig(L.hs_pq_decode_values, I, P, P, I64, I64, I64, I, P, P)
     _sig(L.hs_pq_decode_levels, I, P, P, I64, P, P)
     _sig(L.hs_pq_pack, I, P, P, I, I64, I, P, P)
+    _sig(L.hs_pq_warmup, I, P)
     _sig(L.hs_pq_dict_codes, I, P, I64, I, P, I, P, P, P)
     _lib = L
     return L
