@@ -1,0 +1,327 @@
+#!/usr/bin/env python
+"""The BASELINE.json configurations next to the headline benchmark (``bench.py``).
+
+    python benchmarks/configs.py --config csv10k            # CPU plumbing, no GPU
+    python benchmarks/configs.py --config sf10_filter       # 1 MI355X
+    python benchmarks/configs.py --config hybrid --sf 100   # SF100 index + 10% appended files
+    python benchmarks/configs.py --config q3_3way --sf 100  # three-way join
+    python benchmarks/configs.py --config all
+
+One JSON line per configuration on stdout.  Every configuration checks its indexed results
+against the same query with Hyperspace disabled (the reference's correctness oracle,
+``E2EHyperspaceRulesTest.scala:1004-1019``) and reports which executor path ran.
+
+* ``csv10k`` — 10k-row CSV covering index + equality lookups on the host executor.
+* ``sf10_filter`` — TPC-H SF10 ``lineitem`` FilterIndexRule (``l_shipdate`` range, Q6).
+* ``hybrid`` — SF-N indexes, then +10% appended Parquet files in both tables: Q6 + Q3 through
+  Hybrid Scan (BucketUnion on the device), an incremental refresh, and the same queries on the
+  refreshed index.
+* ``q3_3way`` — the TPC-H Q3 three-way join customer ⋈ orders ⋈ lineitem (JoinIndexRule on the
+  customer/orders join, device shuffle of the intermediate onto the lineitem index layout).
+  This stands in for BASELINE config #5 (TPC-DS SF300 three-way join): no TPC-DS generator is
+  available offline, and Q3 has the same shape — fact ⋈ dimension ⋈ dimension with an
+  intermediate re-partition.
+"""
+import argparse
+import datetime
+import json
+import os
+import shutil
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _session(root, device, buckets, **extra):
+    from hyperspace_amd import Session
+    conf = {"spark.hyperspace.system.path": os.path.join(root, "indexes"),
+            "spark.hyperspace.index.numBuckets": str(buckets),
+            "spark.sql.autoBroadcastJoinThreshold": "-1",
+            "spark.sql.shuffle.partitions": str(buckets),
+            "spark.hyperspace.mi.execution.device": device}
+    conf.update(extra)
+    return Session(conf=conf, warehouse_dir=os.path.join(root, "wh"))
+
+
+def _sync(device):
+    if device == "gpu":
+        import torch
+        torch.cuda.synchronize()
+
+
+def _timed_loop(fn, n, device):
+    _sync(device)
+    t0 = time.perf_counter()
+    for i in range(n):
+        fn(i)
+    _sync(device)
+    return time.perf_counter() - t0
+
+
+def _rows(df):
+    return sorted(tuple(r) for r in df.collect())
+
+
+def _close(a, b):
+    if len(a) != len(b):
+        return False
+    for x, y in zip(a, b):
+        for u, v in zip(x, y):
+            if isinstance(u, float) or isinstance(v, float):
+                if abs(u - v) > 1e-9 * max(1.0, abs(v)):
+                    return False
+            elif u != v:
+                return False
+    return True
+
+
+# ------------------------------------------------------------------------------------ csv10k
+def config_csv10k(args):
+    import numpy as np
+    import pyarrow as pa
+    import pyarrow.csv as pacsv
+    from hyperspace_amd import Hyperspace, IndexConfig, col
+    root = os.path.join(args.data_dir, "csv10k")
+    shutil.rmtree(root, ignore_errors=True)
+    os.makedirs(os.path.join(root, "src"))
+    rng = np.random.default_rng(7)
+    n = 10_000
+    queries = np.array(["donde", "facebook", "ibraco", "miperro", "google", "bing", "yahoo"])
+    t = pa.table({"Date": pa.array([f"2019-10-{d:02d}" for d in rng.integers(1, 29, n)]),
+                  "RGUID": pa.array([f"{x:08x}" for x in rng.integers(0, 2**32, n)]),
+                  "Query": pa.array(queries[rng.integers(0, len(queries), n)]),
+                  "imprs": pa.array(rng.integers(1, 1000, n).astype(np.int32)),
+                  "clicks": pa.array(rng.integers(0, 100, n).astype(np.int64))})
+    for i in range(4):
+        pacsv.write_csv(t.slice(i * n // 4, n // 4), os.path.join(root, "src", f"part-{i}.csv"))
+    s = _session(root, "cpu", 8)
+    hs = Hyperspace(s)
+    df = s.read.option("header", "true").csv(os.path.join(root, "src"))
+    tb = time.perf_counter()
+    hs.createIndex(df, IndexConfig("csvIdx", ["Query"], ["clicks", "imprs"]))
+    build_s = time.perf_counter() - tb
+
+    def q(i):
+        return df.filter(col("Query") == str(queries[i % len(queries)])).select("Query", "clicks")
+    Hyperspace.enable(s)
+    used = "csvIdx" in q(0).queryExecution.executed_plan.tree_string()
+    on = [_rows(q(i)) for i in range(len(queries))]
+    dt_on = _timed_loop(lambda i: q(i).collect(), 50, "cpu")
+    s.disableHyperspace()
+    off = [_rows(q(i)) for i in range(len(queries))]
+    dt_off = _timed_loop(lambda i: q(i).collect(), 50, "cpu")
+    return {"config": "csv10k", "device": "cpu", "rows": n, "index_build_s": round(build_s, 4),
+            "lookups_per_s_indexed": round(50 / dt_on, 2),
+            "lookups_per_s_no_index": round(50 / dt_off, 2),
+            "index_used": used, "match": all(_close(a, b) for a, b in zip(on, off))}
+
+
+# ------------------------------------------------------------------------------------ TPC-H
+def _tpch(args, sf, with_customer=False):
+    from hyperspace_amd.models import tpch
+    nfiles = max(8, int(round(sf * 1.28)))
+    data = os.path.join(args.data_dir, f"tpch_sf{sf:g}_f{nfiles}")
+    tpch.generate(data, sf, nfiles, workers=min(16, os.cpu_count() or 8))
+    if with_customer:
+        tpch.write_customers(data, sf, max(4, nfiles // 8))
+    return data, nfiles
+
+
+def _build(hs, df, cfg, device):
+    from hyperspace_amd.exec import device_build
+    _sync(device)
+    t0 = time.perf_counter()
+    hs.createIndex(df, cfg)
+    _sync(device)
+    dt = time.perf_counter() - t0
+    nbytes = device_build.LAST_BUILD_STATS.get("source_bytes", 0) if device == "gpu" else 0
+    return dt, nbytes
+
+
+def _q6(li, i):
+    from hyperspace_amd import col, sum_
+    year = 1993 + i % 5
+    disc = 0.02 + (i % 8) * 0.01
+    lo, hi = datetime.date(year, 1, 1), datetime.date(year + 1, 1, 1)
+    return li.filter((col("l_shipdate") >= lo) & (col("l_shipdate") < hi) &
+                     (col("l_discount") >= round(disc - 0.01, 2)) &
+                     (col("l_discount") <= round(disc + 0.01, 2)) &
+                     (col("l_quantity") < 24 + (i % 2))) \
+        .agg(sum_(col("l_extendedprice") * col("l_discount")).alias("revenue"))
+
+
+def _q3(li, od, i):
+    from hyperspace_amd import col, count, sum_
+    dd = datetime.date(1995, 3, 1) + datetime.timedelta(days=(i * 7) % 30)
+    j = li.join(od, li["l_orderkey"] == od["o_orderkey"]) \
+        .filter((col("o_orderdate") < dd) & (col("l_shipdate") > dd))
+    return j.groupBy("o_shippriority").agg(
+        sum_(col("l_extendedprice") * (1 - col("l_discount"))).alias("revenue"),
+        count("*").alias("lines"))
+
+
+def config_sf10_filter(args):
+    from hyperspace_amd import Hyperspace, IndexConfig
+    sf = 10.0
+    data, _ = _tpch(args, sf)
+    root = os.path.join(args.data_dir, "cfg_sf10")
+    shutil.rmtree(root, ignore_errors=True)
+    s = _session(root, args.device, args.buckets)
+    hs = Hyperspace(s)
+    li = s.read.parquet(os.path.join(data, "lineitem"))
+    dt, nbytes = _build(hs, li, IndexConfig("li_shipdate", ["l_shipdate"],
+                                            ["l_discount", "l_quantity", "l_extendedprice"]),
+                        args.device)
+    Hyperspace.enable(s)
+    for i in range(3):
+        _q6(li, 1000 + i).collect()
+    k = args.steps * 5
+    el = _timed_loop(lambda i: _q6(li, i).collect(), k, args.device)
+    path = getattr(s.backend(), "last_path", None)
+    got = _q6(li, 0).collect()[0][0]
+    s.disableHyperspace()
+    ref = _q6(li, 0).collect()[0][0]
+    return {"config": "sf10_filter", "device": args.device, "queries_per_s": round(k / el, 2),
+            "q6_ms": round(el / k * 1e3, 3), "index_build_s": round(dt, 3),
+            "index_build_gbps": round(nbytes / dt / 1e9, 3) if nbytes else None,
+            "path": path, "match": abs(got - ref) <= 1e-9 * abs(ref)}
+
+
+def config_hybrid(args):
+    import pyarrow.parquet as pq  # noqa: F401
+    from hyperspace_amd import Hyperspace, IndexConfig
+    from hyperspace_amd.models import tpch
+    sf = args.sf
+    data, nfiles = _tpch(args, sf)
+    # a private copy: appending files must not disturb the shared generated data set
+    work = os.path.join(args.data_dir, f"cfg_hybrid_sf{sf:g}")
+    shutil.rmtree(work, ignore_errors=True)
+    for t in ("lineitem", "orders"):
+        os.makedirs(os.path.join(work, "data", t))
+        for f in os.listdir(os.path.join(data, t)):
+            os.link(os.path.join(data, t, f), os.path.join(work, "data", t, f))
+    s = _session(work, args.device, args.buckets,
+                 **{"spark.hyperspace.index.lineage.enabled": "true",
+                    "spark.hyperspace.index.hybridscan.enabled": "true",
+                    "spark.hyperspace.index.hybridscan.maxAppendedRatio": "0.3"})
+    hs = Hyperspace(s)
+    lpath, opath = os.path.join(work, "data", "lineitem"), os.path.join(work, "data", "orders")
+    li, od = s.read.parquet(lpath), s.read.parquet(opath)
+    builds = {}
+    for df, cfg in ((li, IndexConfig("li_orderkey", ["l_orderkey"],
+                                     ["l_extendedprice", "l_discount", "l_shipdate"])),
+                    (od, IndexConfig("ord_orderkey", ["o_orderkey"],
+                                     ["o_orderdate", "o_shippriority"])),
+                    (li, IndexConfig("li_shipdate", ["l_shipdate"],
+                                     ["l_discount", "l_quantity", "l_extendedprice"]))):
+        builds[cfg.indexName] = round(_build(hs, df, cfg, args.device)[0], 3)
+    # +10%: chunks nfiles.. extend the key domain (fresh orders and their lineitems)
+    extra = max(1, nfiles // 10)
+    for i in range(nfiles, nfiles + extra):
+        tpch.write_chunk(os.path.join(work, "data"), sf, nfiles, i)
+    Hyperspace.enable(s)
+    li, od = s.read.parquet(lpath), s.read.parquet(opath)
+
+    def step(i):
+        _q6(li, i).collect()
+        _q3(li, od, i).collect()
+    plan = _q3(li, od, 0).queryExecution.executed_plan.tree_string()
+    for i in range(2):
+        step(1000 + i)
+    el_h = _timed_loop(step, args.steps, args.device)
+    path_h = getattr(s.backend(), "last_path", None)
+    hyb = (_q6(li, 0).collect()[0][0], _rows(_q3(li, od, 0)))
+    tr = time.perf_counter()
+    for name in ("li_orderkey", "ord_orderkey", "li_shipdate"):
+        hs.refreshIndex(name, "incremental")
+    _sync(args.device)
+    refresh_s = time.perf_counter() - tr
+    li, od = s.read.parquet(lpath), s.read.parquet(opath)
+    for i in range(2):
+        step(2000 + i)
+    el_r = _timed_loop(step, args.steps, args.device)
+    ref = (_q6(li, 0).collect()[0][0], _rows(_q3(li, od, 0)))
+    match = abs(hyb[0] - ref[0]) <= 1e-9 * abs(ref[0]) and _close(hyb[1], ref[1])
+    return {"config": "hybrid", "device": args.device, "sf": sf, "appended_files": extra,
+            "hybrid_queries_per_s": round(2 * args.steps / el_h, 2),
+            "refreshed_queries_per_s": round(2 * args.steps / el_r, 2),
+            "incremental_refresh_s": round(refresh_s, 3), "index_build_s": builds,
+            "bucket_union_in_plan": "BucketUnion" in plan, "path": path_h,
+            "hybrid_matches_refreshed": bool(match)}
+
+
+def config_q3_3way(args):
+    from hyperspace_amd import Hyperspace, IndexConfig, col, count, sum_
+    sf = args.sf
+    data, _ = _tpch(args, sf, with_customer=True)
+    root = os.path.join(args.data_dir, f"cfg_q3_sf{sf:g}")
+    shutil.rmtree(root, ignore_errors=True)
+    s = _session(root, args.device, args.buckets)
+    hs = Hyperspace(s)
+    c = s.read.parquet(os.path.join(data, "customer"))
+    o = s.read.parquet(os.path.join(data, "orders"))
+    li = s.read.parquet(os.path.join(data, "lineitem"))
+    builds = {}
+    for df, cfg in ((c, IndexConfig("cust", ["c_custkey"], ["c_mktsegment"])),
+                    (o, IndexConfig("ord_cust", ["o_custkey"],
+                                    ["o_orderkey", "o_orderdate", "o_shippriority"])),
+                    (li, IndexConfig("li_orderkey", ["l_orderkey"],
+                                     ["l_extendedprice", "l_discount", "l_shipdate"]))):
+        builds[cfg.indexName] = round(_build(hs, df, cfg, args.device)[0], 3)
+    segs = ["BUILDING", "AUTOMOBILE", "MACHINERY", "HOUSEHOLD", "FURNITURE"]
+
+    def q(i):
+        d = datetime.date(1995, 3, 1) + datetime.timedelta(days=(i * 7) % 30)
+        co = c.join(o, c["c_custkey"] == o["o_custkey"]) \
+            .filter((col("c_mktsegment") == segs[i % 5]) & (col("o_orderdate") < d))
+        return co.join(li, co["o_orderkey"] == li["l_orderkey"]).filter(col("l_shipdate") > d) \
+            .agg(sum_(col("l_extendedprice") * (1 - col("l_discount"))).alias("revenue"),
+                 count("*").alias("lines"))
+    Hyperspace.enable(s)
+    plan = q(0).queryExecution.executed_plan.tree_string()
+    for i in range(2):
+        q(1000 + i).collect()
+    k = max(3, args.steps // 2)
+    el = _timed_loop(lambda i: q(i).collect(), k, args.device)
+    path = getattr(s.backend(), "last_path", None)
+    reason = getattr(s.backend(), "fallback_reason", None)
+    got = _rows(q(0))
+    s.disableHyperspace()
+    t0 = time.perf_counter()
+    ref = _rows(q(0))
+    noidx_s = time.perf_counter() - t0
+    return {"config": "q3_3way", "device": args.device, "sf": sf,
+            "queries_per_s": round(k / el, 3), "q3_3way_ms": round(el / k * 1e3, 2),
+            "no_index_query_s": round(noidx_s, 3), "index_build_s": builds,
+            "indexes_in_plan": [n for n in ("cust", "ord_cust", "li_orderkey") if n in plan],
+            "path": path, "fallback_reason": reason, "match": _close(got, ref)}
+
+
+CONFIGS = {"csv10k": config_csv10k, "sf10_filter": config_sf10_filter, "hybrid": config_hybrid,
+           "q3_3way": config_q3_3way}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="all", choices=["all"] + list(CONFIGS))
+    ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
+    ap.add_argument("--sf", type=float, default=100.0)
+    ap.add_argument("--buckets", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--data-dir", default=os.environ.get("HS_BENCH_DIR", "/tmp/hs_bench"))
+    args = ap.parse_args()
+    if args.device == "gpu":
+        import torch
+        torch.cuda.set_device(0)
+    names = list(CONFIGS) if args.config == "all" else [args.config]
+    for name in names:
+        t0 = time.perf_counter()
+        res = CONFIGS[name](args)
+        res["wall_s"] = round(time.perf_counter() - t0, 2)
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -427,6 +427,13 @@ class GpuBackend:
         if not all(isinstance(e, E.Attribute) for e in part.expressions):
             raise Unsupported("hash partitioning on expressions")
         keys = list(part.expressions)
+        if (r.bucketed and not r.parts and not r.split and r.num_buckets == part.num_partitions
+                and [a.expr_id for a in r.bucket_attrs] == [k.expr_id for k in keys]
+                and _prefix_sorted(r, keys)):
+            # an index table loaded bucket-major is already hash-partitioned by these keys into
+            # this many buckets (same Murmur3 + pmod) and sorted inside each bucket — the
+            # exchange the planner asked for would reproduce exactly this layout
+            return r
         cols = self._materialize(r, list(dict.fromkeys(r.attrs + keys)))
         kcols = [cols[k.expr_id] for k in keys]
         for c in kcols:

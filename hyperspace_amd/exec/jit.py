@@ -70,6 +70,7 @@ def runtime():
             if _rt is None:
                 if not os.path.exists(RUNTIME_PATH):
                     raise RuntimeError(f"{RUNTIME_PATH} missing: run python -m hyperspace_amd._native.build")
+                NL.bind_hip_runtime()
                 L = C.CDLL(RUNTIME_PATH)
                 L.hs_jit_get.restype = C.c_void_p
                 L.hs_jit_get.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,

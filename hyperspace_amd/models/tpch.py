@@ -120,3 +120,34 @@ def generate(root: str, sf: float, nfiles: int, files: Optional[list] = None,
     ctx = mp.get_context("fork")
     with ctx.Pool(processes=min(workers, len(todo))) as pool:
         return sum(pool.map(_write_chunk_args, todo, chunksize=1))
+
+
+CUSTOMERS_PER_SF = 150_000
+SEGMENTS = np.array(["AUTOMOBILE", "BUILDING", "FURNITURE", "HOUSEHOLD", "MACHINERY"])
+
+CUSTOMER_SCHEMA = pa.schema([("c_custkey", pa.int64()), ("c_nationkey", pa.int32()),
+                             ("c_acctbal", pa.float64()), ("c_mktsegment", pa.string())])
+
+
+def write_customers(root: str, sf: float, nfiles: int = 4, seed: int = 42) -> int:
+    """``customer`` (c_custkey 1..150k*SF, the domain of o_custkey) in ``nfiles`` files —
+    the third table of the TPC-H Q3 three-way join."""
+    n = int(CUSTOMERS_PER_SF * sf)
+    out_dir = os.path.join(root, "customer")
+    os.makedirs(out_dir, exist_ok=True)
+    for i in range(nfiles):
+        path = os.path.join(out_dir, f"part-{i:05d}.parquet")
+        if os.path.exists(path):
+            continue
+        lo, hi = n * i // nfiles, n * (i + 1) // nfiles
+        rng = np.random.default_rng([seed, 10_000 + i])
+        m = hi - lo
+        t = pa.Table.from_arrays([
+            pa.array(np.arange(lo + 1, hi + 1, dtype=np.int64)),
+            pa.array(rng.integers(0, 25, m).astype(np.int32)),
+            pa.array(np.round(rng.random(m) * 10_999 - 999, 2)),
+            pa.array(SEGMENTS[rng.integers(0, 5, m)])], schema=CUSTOMER_SCHEMA)
+        tmp = os.path.join(out_dir, f".tmp-{os.getpid()}-part-{i:05d}.parquet")
+        pq.write_table(t, tmp, compression="snappy", row_group_size=1 << 20)
+        os.replace(tmp, path)
+    return n

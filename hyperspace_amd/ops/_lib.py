@@ -99,12 +99,23 @@ def _sig(fn, restype, *args):
     fn.argtypes = list(args)
 
 
+def bind_hip_runtime() -> None:
+    """Load torch (and with it the HIP runtime torch ships) before any of our libraries.
+
+    Our .so files need ``libamdhip64.so.7``; torch bundles its own copy with the same SONAME.
+    Whichever loads first is the one the process uses, and two HIP runtimes must never be
+    mixed (torch's streams, allocations and contexts belong to its copy): loading ours first
+    made a later torch share /opt/rocm's runtime and launches failed with hipErrorNoDevice."""
+    import torch  # noqa: F401
+
+
 def lib():
     global _lib
     if _lib is not None:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise NativeMissing(f"{LIB_PATH} not built; run `python -m hyperspace_amd._native.build`")
+    bind_hip_runtime()
     L = C.CDLL(LIB_PATH)
     P, I, I64, U64 = C.c_void_p, C.c_int, C.c_int64, C.c_uint64
     for name, st in (("hs_hash_params_size", HashParams), ("hs_scan_params_size", ScanParams),
