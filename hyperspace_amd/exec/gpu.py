@@ -96,6 +96,10 @@ class GpuBackend:
         self._cpu = None
         self._domains: Dict[tuple, tuple] = {}
         self.graphs = GraphCache()
+        # engine start: size the pinned staging pool once (pinning GBs is the slow part of a
+        # cold build), as the HBM side is sized by the device table cache
+        from .staging import pinned_pool
+        pinned_pool().reserve()
 
     # ------------------------------------------------------------------------------------------
     @property

@@ -201,11 +201,11 @@ def page_table(bucket_off: np.ndarray, rg_rows: int) -> Tuple[np.ndarray, List[T
 
 def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: pa.Schema,
                   bucket_off: np.ndarray, path_of: Callable[[int], str], rg_rows: int, device,
-                  chunk_bytes: int = 512 << 20) -> Optional[List[str]]:
+                  chunk_bytes: int = 96 << 20) -> Optional[List[str]]:
     """Encode on the device and write one Parquet file per non-empty bucket; None when the
     columns need the pyarrow writer."""
     import torch
-    from .staging import copy_stream, io_pool
+    from .staging import copy_stream, io_pool, pinned_pool
     pages, files = page_table(bucket_off, rg_rows)
     if not files:
         return []
@@ -239,7 +239,7 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
         with torch.cuda.stream(stream):
             for cp in plans:
                 lo, hi = int(cp.page_off[p_first]), int(cp.page_off[p_end])
-                h = torch.empty(max(hi - lo, 1), dtype=torch.uint8, pin_memory=True)
+                h = pinned_pool().acquire(hi - lo)
                 if hi > lo:
                     h[:hi - lo].copy_(cp.payload[lo:hi], non_blocking=True)
                 host.append((h, lo))
@@ -271,6 +271,8 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
                 if rc != 0:
                     raise OSError(-rc, f"native Parquet write failed: {path}")
                 out.append(path)
+            for h, _ in host:   # written: the blocks can serve the next batch
+                pinned_pool().release(h, torch.cuda.current_stream(device))
             return out
         futs.append(io_pool().submit(write_batch))
     paths = []

@@ -67,6 +67,87 @@ def ensure_valid(dc: DeviceColumn, n: int, device, lock: threading.Lock):
     return dc.valid
 
 
+RESERVE_BLOCK = 128 << 20
+
+
+class PinnedPool:
+    """Reusable pinned host blocks for staging (decode buffers, D2H encode buffers).
+
+    Pinning is the slow part of a cold build (hipHostMalloc of GBs), so blocks are kept and
+    handed out best-fit; a released block returns to the free list only after the copy recorded
+    on its stream has completed.  ``reserve`` pre-pins blocks at engine start (the GPU backend
+    does this), like any engine sizing its staging pool up front."""
+
+    def __init__(self, limit_bytes: int = 8 << 30):
+        self.limit = limit_bytes
+        self._free: list = []
+        self._pending: list = []
+        self._held = 0
+        self._lock = threading.Lock()
+
+    def _reclaim(self) -> None:
+        keep = []
+        for t, ev in self._pending:
+            if ev.query():
+                self._free.append(t)
+            else:
+                keep.append((t, ev))
+        self._pending = keep
+
+    def acquire(self, nbytes: int):
+        import torch
+        nbytes = max(int(nbytes), 1)
+        with self._lock:
+            self._reclaim()
+            best = None
+            for i, t in enumerate(self._free):
+                if nbytes <= t.numel() <= max(4 * nbytes, RESERVE_BLOCK) and \
+                        (best is None or t.numel() < self._free[best].numel()):
+                    best = i
+            if best is not None:
+                return self._free.pop(best)
+            size = (nbytes + (8 << 20) - 1) // (8 << 20) * (8 << 20)
+            pooled = self._held + size <= self.limit
+            if pooled:
+                self._held += size
+        t = torch.empty(size if pooled else nbytes, dtype=torch.uint8, pin_memory=True)
+        t.hs_pooled = pooled
+        return t
+
+    def release(self, t, stream) -> None:
+        """Return ``t`` once the work queued on ``stream`` (its copies) has finished."""
+        import torch
+        if not getattr(t, "hs_pooled", False):
+            return
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        with self._lock:
+            self._pending.append((t, ev))
+
+    def reserve(self, count: int = 32, nbytes: int = None) -> None:
+        """Pre-pin ``count`` blocks once per process (idempotent)."""
+        import torch
+        nbytes = nbytes or RESERVE_BLOCK
+        with self._lock:
+            if self._held:
+                return
+        blocks = [self.acquire(nbytes) for _ in range(count)]
+        with self._lock:
+            self._free.extend(b for b in blocks if getattr(b, "hs_pooled", False))
+        del blocks
+        torch.cuda.synchronize()
+
+
+_PINNED: Optional[PinnedPool] = None
+
+
+def pinned_pool() -> PinnedPool:
+    global _PINNED
+    if _PINNED is None:
+        _PINNED = PinnedPool()
+    return _PINNED
+
+
 _TORCH_OF_NP = None
 
 

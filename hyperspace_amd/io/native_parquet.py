@@ -209,7 +209,9 @@ def upload_file(path: str, fields: Sequence[pa.Field], cols: Dict[str, object], 
         rg_off = np.concatenate([[0], np.cumsum([f.row_group_rows(g) for g in range(nrg)])])
         bounds = [[int(L.hs_pq_chunk_bound(f.h, g, c)) for g in range(nrg)] for _, c, _ in plan]
         total = sum(sum((b + 15) // 16 * 16 for b in bl) for bl in bounds) + 64
-        pinned = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+        from ..exec.staging import pinned_pool
+        pool = pinned_pool()
+        pinned = pool.acquire(total)
         base = pinned.data_ptr()
         off = 0
         chunks = []
@@ -248,16 +250,19 @@ def upload_file(path: str, fields: Sequence[pa.Field], cols: Dict[str, object], 
                 nl += len(lv)
             done.add(fld.name)
         if not done:
+            pool.release(pinned, stream)
             return set()
         runs = np.concatenate(vparts + lparts) if (nv + nl) else np.empty(0, RUN_DTYPE)
-        pruns = torch.empty(max(runs.nbytes, 8), dtype=torch.uint8, pin_memory=True)
+        pruns = pool.acquire(max(runs.nbytes, 8))
         pruns.numpy()[:runs.nbytes] = runs.view(np.uint8)
         sp = stream.cuda_stream
         with torch.cuda.stream(stream):
             dbuf = torch.empty(off + 64, dtype=torch.uint8, device=device)
             dbuf[:off].copy_(pinned[:off], non_blocking=True)
             druns = torch.empty(max(runs.nbytes, 8), dtype=torch.uint8, device=device)
-            druns.copy_(pruns, non_blocking=True)
+            druns.copy_(pruns[:druns.numel()], non_blocking=True)
+            pool.release(pinned, stream)
+            pool.release(pruns, stream)
             rsz = RUN_DTYPE.itemsize
             for fld, eb, g, info, boff, v0, vn, l0, ln in chunks:
                 dc = cols[fld.name]

@@ -46,6 +46,10 @@ class Session:
         self._backends: dict = {}
         self.dist = None  # parallel.dist.DistContext when running under torch.distributed
         Session.set_active(self)
+        if str(self.conf.get(C.EXEC_DEVICE, "")).lower() == "gpu":
+            # engine start: HIP context, kernel libraries and the pinned staging pool come up
+            # with the session, not inside its first index build or query
+            self.backend()
 
     # -- active session --------------------------------------------------------------------------
     @staticmethod
