@@ -51,6 +51,10 @@ JOIN_STAGE_RIGHT = os.environ.get("HS_JIT_JOIN_STAGE_RIGHT", "1") == "1"
 SCAN_EAGER = os.environ.get("HS_JIT_SCAN_EAGER", "0") == "1"
 # software-pipeline the join's tile loop (next tile's batch loads overlap this tile's work)
 JOIN_PIPELINE = os.environ.get("HS_JIT_JOIN_PIPELINE", "1") == "1"
+# direct-address LDS table for dense integer key spans (one verified lookup instead of a
+# binary search); slots = key values a tile's right span may cover
+JOIN_DIRECT = os.environ.get("HS_JIT_JOIN_DIRECT", "1") == "1"
+JOIN_DIRECT_SLOTS = int(os.environ.get("HS_JIT_JOIN_DIRECT_SLOTS", "2048"))
 
 _CTYPE = {NL.I8: "signed char", NL.I16: "short", NL.I32: "int", NL.I64: "long long",
           NL.F32: "float", NL.F64: "double", NL.BOOL: "unsigned char", NL.U32: "unsigned int",
@@ -570,7 +574,8 @@ def join_agg_shape(p: NL.JoinParams, compacts=None) -> tuple:
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
     return ("join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey, p.key_is_float,
-            JOIN_ITEMS, JOIN_LDS_KEYS, JOIN_EAGER, JOIN_BLOCK, JOIN_STAGE_RIGHT, JOIN_PIPELINE)
+            JOIN_ITEMS, JOIN_LDS_KEYS, JOIN_EAGER, JOIN_BLOCK, JOIN_STAGE_RIGHT, JOIN_PIPELINE,
+            JOIN_DIRECT, JOIN_DIRECT_SLOTS)
 
 
 def _key_expr(var: str, is_float: bool) -> str:
@@ -677,6 +682,16 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
             if cols[s][1]:
                 batch.append(f"{ind}const unsigned char snv{s}_{q} = sa{q} ? {gen.vptr(s)}[rs + {off}] : 0;")
                 fields.append(("unsigned char", f"snv{s}_{q}"))
+    direct = JOIN_DIRECT and not fl
+    if direct:
+        # first / last right key of the span (uniform loads): a span of integer keys whose
+        # value range fits DT slots gets a direct-address LDS table instead of a binary search
+        batch.append(f"{ind}const u64 dbk = (staged && re > rs) ? "
+                     f"{_key_expr(gen.value(rk, 'rs'), fl)} : 0ull;")
+        batch.append(f"{ind}const u64 dek = (staged && re > rs) ? "
+                     f"{_key_expr(gen.value(rk, 're - 1'), fl)} : 0ull;")
+        fields += [("u64", "dbk"), ("u64", "dek")]
+        b.insert(1, f"  __shared__ short dtab[{JOIN_DIRECT_SLOTS}];")
     pre: List[str] = []
     if JOIN_PIPELINE:
         b, pre = _pipeline_tiles(b, batch, fields, NI, BLOCK, LDS_KEYS)
@@ -688,9 +703,13 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
         okk = f"n{lk}_{it}" if cols[lk][1] else "true"
         b.append(f"{ind}bool m{it} = la{it} && {okk} && {cond};")
         b.append(f"{ind}const u64 k{it} = {_key_expr(f'x{lk}_{it}', fl)};")
+    if direct:
+        b.append(f"{ind}const bool dense = staged && re > rs && dek - dbk < {JOIN_DIRECT_SLOTS}ull;")
     for q in range(KEYS_PER_THREAD):
         idx = f"{q * BLOCK} + threadIdx.x"
         b.append(f"{ind}if (sa{q}) {{ skeys[{idx}] = sk{q};")
+        if direct:
+            b.append(f"{ind}  if (dense) dtab[sk{q} - dbk] = (short)({idx});")
         for s in staged_cols:
             b.append(f"{ind}  sv{s}[{idx}] = svv{s}_{q};")
             if cols[s][1]:
@@ -698,7 +717,10 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
         b.append(f"{ind}}}")
     b += [f"{ind}if (staged) {{",
           f"{ind}  for (i64 q = {KEYS_PER_THREAD * BLOCK} + threadIdx.x; q < re - rs; q += {BLOCK}) {{",
-          f"{ind}    skeys[q] = {_key_expr(gen.value(rk, 'rs + q'), fl)};"]
+          f"{ind}    const u64 kq = {_key_expr(gen.value(rk, 'rs + q'), fl)};",
+          f"{ind}    skeys[q] = kq;"]
+    if direct:
+        b.append(f"{ind}    if (dense) dtab[kq - dbk] = (short)q;")
     for s in staged_cols:
         b.append(f"{ind}    sv{s}[q] = {gen.value(s, 'rs + q')};")
         if cols[s][1]:
@@ -707,8 +729,18 @@ def gen_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
     # (2) first match per row (LDS binary search; global search for oversized spans)
     for it in range(NI):
         b += [f"    i64 j{it} = rs;",
-              f"    if (m{it}) {{",
-              "      if (staged) { i64 lo = 0, hi = re - rs;",
+              f"    if (m{it}) {{"]
+        if direct:
+            # slot hit verified against the staged key (stale slots from earlier tiles fail the
+            # check); duplicates walk back to their first occurrence
+            b += ["      if (dense) {",
+                  f"        const u64 d = k{it} - dbk; m{it} = false;",
+                  f"        if (d < {JOIN_DIRECT_SLOTS}ull) {{ i64 q = dtab[d];",
+                  f"          if (q >= 0 && q < re - rs && skeys[q] == k{it}) {{",
+                  f"            while (q > 0 && skeys[q - 1] == k{it}) --q;",
+                  f"            j{it} = rs + q; m{it} = true; }} }}",
+                  "      } else"]
+        b += ["      if (staged) { i64 lo = 0, hi = re - rs;",
               f"        while (lo < hi) {{ const i64 md = (lo + hi) >> 1; if (skeys[md] < k{it}) lo = md + 1; else hi = md; }}",
               f"        j{it} = rs + lo; m{it} = j{it} < re && skeys[lo] == k{it};",
               "      } else { i64 lo = rs, hi = re;",

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--blocks", default="256")
     ap.add_argument("--stage", default="1,0", help="stage right columns in LDS (1/0)")
     ap.add_argument("--pipe", default="1,0", help="software-pipelined tile loop (1/0)")
+    ap.add_argument("--direct", default="1,0", help="direct-address LDS key table (1/0)")
     ap.add_argument("--quick", action="store_true", help="raw/lazy join variants only")
     ap.add_argument("--no-scan", action="store_true")
     args = ap.parse_args()
@@ -104,18 +105,20 @@ def main():
     modes = [("raw", False)] if args.quick else [("raw", False), ("raw", True), ("compact", False)]
     for cmode, eager in modes:
         cm = comp if cmode == "compact" else None
-        for pipe in [x == "1" for x in args.pipe.split(",")]:
+        for pipe, direct in [(p_ == "1", d_ == "1") for p_ in args.pipe.split(",")
+                             for d_ in args.direct.split(",")]:
           for stage in [x == "1" for x in args.stage.split(",")]:
             for block in [int(x) for x in args.blocks.split(",")]:
                 for items in [int(x) for x in args.items.split(",")]:
                     for grid in [int(x) for x in args.grids.split(",")]:
                         jit.JOIN_ITEMS, jit.JOIN_GRID, jit.JOIN_EAGER = items, grid, eager
                         jit.JOIN_BLOCK, jit.JOIN_STAGE_RIGHT = block, stage
-                        jit.JOIN_PIPELINE = pipe
+                        jit.JOIN_PIPELINE, jit.JOIN_DIRECT = pipe, direct
                         ms, out = timed(lambda: jit.join_agg(p, rstart, rlen, rbk, roff, mt, cm))
                         ok = abs(out[0][0].item() - ref) <= 1e-9 * abs(ref)
                         print(json.dumps({"kernel": "jit_join", "enc": cmode, "eager": eager,
-                                          "pipeline": pipe, "stage_right": stage,
+                                          "pipeline": pipe, "direct": direct,
+                                          "stage_right": stage,
                                           "block": block, "items": items,
                                           "grid": grid, "ms": round(ms, 3),
                                           "GBps_logical": round(nbytes / ms / 1e6, 1),
