@@ -52,8 +52,10 @@ SCAN_EAGER = os.environ.get("HS_JIT_SCAN_EAGER", "0") == "1"
 # software-pipeline the join's tile loop (next tile's batch loads overlap this tile's work)
 JOIN_PIPELINE = os.environ.get("HS_JIT_JOIN_PIPELINE", "1") == "1"
 # direct-address LDS table for dense integer key spans (one verified lookup instead of a
-# binary search); slots = key values a tile's right span may cover
-JOIN_DIRECT = os.environ.get("HS_JIT_JOIN_DIRECT", "1") == "1"
+# binary search); slots = key values a tile's right span may cover.  Off by default: it measured
+# 5.18 vs 3.98 ms on the SF100 Q3 shape (profiles/microbench_join_r1f_direct.jsonl) — the LDS
+# search is not on this kernel's critical path, the extra table writes and loads are
+JOIN_DIRECT = os.environ.get("HS_JIT_JOIN_DIRECT", "0") == "1"
 JOIN_DIRECT_SLOTS = int(os.environ.get("HS_JIT_JOIN_DIRECT_SLOTS", "2048"))
 
 _CTYPE = {NL.I8: "signed char", NL.I16: "short", NL.I32: "int", NL.I64: "long long",
