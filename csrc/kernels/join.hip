@@ -429,6 +429,34 @@ __global__ __launch_bounds__(JN_BLOCK) void hs_join_pairs_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Join index (exec/join_index.py): the first matching right row of every left row (-1 = none) for
+// a pair of device-resident index tables.  Built ONCE per table pair with the same span + LDS
+// search the join kernels use; the tables are immutable, so every later join of the pair is a
+// streaming scan of the left table plus a gather of the right columns (exec/jit.py
+// gen_join_index_agg) — no span search, no LDS staging, no binary search per query.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(JN_BLOCK) void hs_join_index_kernel(
+    JoinParams p, const int64_t* __restrict__ tile_prefix, int R,
+    const int64_t* __restrict__ spans, int32_t* __restrict__ jidx) {
+  __shared__ uint64_t skeys[JN_LDS_KEYS];
+  int64_t t0, t1;
+  block_tile_chunk(tile_prefix[R], t0, t1);
+  for (int64_t t = t0; t < t1; ++t) {
+    const JTile c = jtile_load(p, spans, t, skeys);
+    int64_t r0[JN_ITEMS], j0[JN_ITEMS];
+    uint64_t key[JN_ITEMS];
+    bool m0[JN_ITEMS];
+    jbatch_probe(p, c, skeys, r0, key, j0, m0);  // p.nlp == 0: key validity only
+#pragma unroll
+    for (int i = 0; i < JN_ITEMS; ++i) {
+      const int64_t k = (int64_t)i * JN_BLOCK + threadIdx.x;
+      if (k < c.rows) jidx[r0[i]] = m0[i] ? (int32_t)j0[i] : -1;
+    }
+    __syncthreads();  // skeys is restaged by the next tile
+  }
+}
+
 static int launch_spans(const JoinParams* p, const int64_t* rstart, const int64_t* rlen,
                         const int32_t* rbucket, const int64_t* roff, int R,
                         const int64_t* tile_prefix, int64_t max_tiles, int64_t* spans,
@@ -465,6 +493,18 @@ int hs_join_spans_sampled(const JoinParams* p, const int64_t* rstart, const int6
     hipLaunchKernelGGL(hs_join_spans_sampled_kernel, dim3((unsigned)((max_tiles + 255) / 256)),
                        dim3(256), 0, s, *p, rstart, rlen, rbucket, roff, soff, samples, R,
                        tile_prefix, spans, tile_rows);
+  return (int)hipGetLastError();
+}
+
+// spans: per-tile records from hs_join_spans_sampled built with tile_rows = JN_TILE;
+// jidx: one int32 per left row (rows outside the ranges are left untouched).
+int hs_join_index(const JoinParams* p, int R, const int64_t* tile_prefix, const int64_t* spans,
+                  int grid, int32_t* jidx, void* stream) {
+  JoinParams q = *p;
+  q.npreds = 0;
+  q.nlp = 0;
+  hipLaunchKernelGGL(hs_join_index_kernel, dim3(grid), dim3(JN_BLOCK), 0, (hipStream_t)stream, q,
+                     tile_prefix, R, spans, jidx);
   return (int)hipGetLastError();
 }
 

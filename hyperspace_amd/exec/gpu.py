@@ -33,9 +33,9 @@ from ..utils import murmur3
 from ..utils.conf import HyperspaceConf
 from ..utils.tracing import TRACER, stage
 from . import compile as CP
-from . import jit
+from . import jit, join_index
 from .arrow_eval import key
-from .device_cache import DeviceTableCache, load_bucketed_index, load_flat
+from .device_cache import DeviceTableCache, _files_key, load_bucketed_index, load_flat
 from .device_table import DeviceColumn, DeviceTable
 from .graphs import GraphCache, ScanAggGraph, range_bounds
 
@@ -95,6 +95,8 @@ class GpuBackend:
         self.metrics: Dict[str, float] = {}
         self._cpu = None
         self._domains: Dict[tuple, tuple] = {}
+        self._gdomains: Dict[tuple, tuple] = {}   # (table global key, column) -> all-rank domain
+        self._groups_agreed = False
         self.graphs = GraphCache()
         # engine start: size the pinned staging pool once (pinning GBs is the slow part of a
         # cold build), as the HBM side is sized by the device table cache
@@ -219,6 +221,8 @@ class GpuBackend:
             table = self.cache.get(files, load_cols, ("bucketed", rank, world),
                                    lambda: load_bucketed_index(files, load_cols, idx.num_buckets,
                                                                sort_cols, self.device, rank, world))
+            # rank-independent identity (every rank scans the same file list)
+            table.global_key = ("bucketed", _files_key(files), tuple(load_cols), world)
             colmap = {a.expr_id: c for a, c in zip(p.output, cols)}
             sort_attrs = []
             for c in sort_cols:
@@ -230,6 +234,7 @@ class GpuBackend:
             return DRel(table, colmap, list(p.output), [], True, sort_attrs, sort_attrs,
                         idx.num_buckets)
         fmt = "parquet" if (rel.is_index() or rel.file_format == "delta") else rel.file_format
+        gkey = ("flat", _files_key(files), tuple(names), world)
         if world > 1:
             # a file split per rank, like Spark's scan tasks; a following hash Exchange moves rows
             # to their owners with an all-to-all (_repartition), aggregates all-reduce
@@ -237,6 +242,7 @@ class GpuBackend:
         table = self.cache.get(files, names, ("flat", fmt, rank, world),
                                lambda: load_flat(files, fmt, names, rel.data_schema, rel.options,
                                                  rel.location.partition_spec, self.device))
+        table.global_key = gkey
         return DRel(table, {a.expr_id: a.name for a in p.output}, list(p.output),
                     split=world > 1)
 
@@ -612,6 +618,7 @@ class GpuBackend:
         while isinstance(node, X.ProjectExec) and all(isinstance(e, E.Attribute) for e in node.project_list):
             node = node.child
         import torch
+        self._groups_agreed = False
         if isinstance(node, X.SortMergeJoinExec):
             res = self._join_agg(node, fns, group)
         else:
@@ -619,15 +626,17 @@ class GpuBackend:
         sums, cnts, mins, maxs, G, gbase, gdict, gtype = res
         d = self._dist()
         A = len(fns) + 1  # + implicit count(*)
+        host = None
         if d is not None and d.world > 1:
-            with stage("agg.all_reduce"):
-                if group is not None:
+            with stage("agg.combine_ranks"):
+                if group is not None and not self._groups_agreed:
                     sums, cnts, mins, maxs, G, gbase, gdict, gtype = self._agree_groups(
                         d, sums, cnts, mins, maxs, G, gbase, gdict, gtype, A)
-                sums, cnts, mins, maxs = d.all_reduce_agg(sums, cnts, mins, maxs)
-        with stage("agg.d2h"):
-            host = (sums, cnts, mins, maxs) if isinstance(sums, np.ndarray) else \
-                K.agg_to_host(sums, cnts, mins, maxs)
+                host = d.combine_aggs_host(sums, cnts, mins, maxs)
+        if host is None:
+            with stage("agg.d2h"):
+                host = (sums, cnts, mins, maxs) if isinstance(sums, np.ndarray) else \
+                    K.agg_to_host(sums, cnts, mins, maxs)
         s, c, mn, mx = (x.reshape(G, A) for x in host)
         rows = [g for g in range(G) if c[g, A - 1] > 0] if group is not None else [0]
         vals = {}
@@ -703,32 +712,41 @@ class GpuBackend:
         return out
 
     def _group_spec(self, r: DRel, group, limit):
+        """(agreed, G, base, dictionary, arrow type) of a group column, or None when empty.
+
+        ``agreed`` is True when ``[base, base+G)`` is the domain over ALL ranks: partials laid
+        out over it combine with a plain element-wise reduction, no per-query domain exchange.
+        It is agreed once per (table identity, column) — a key every rank computes identically,
+        unlike device-cache residency — and cached, so steady-state queries run no collective
+        here."""
         if group is None:
             return -1, 1, 0, None, None
         c = r.col(group)
         if c.is_float:
             raise Unsupported("float group key")
+        d = self._dist()
+        multi = d is not None and d.world > 1
+        gkey = getattr(r.table, "global_key", None) if r.table is not None else None
         if c.dictionary is not None:
             G = len(c.dictionary)
             base = 0
         else:
-            # tables are immutable: the group domain is computed once per column
-            ck = id(c)
-            hit = self._domains.get(ck)
-            dom = hit[1] if hit is not None and hit[0] is c else None
-            if dom is None:
-                import torch
-                vals = c.data if c.valid is None else c.data[c.valid.bool()]
-                if vals.numel() == 0:
-                    dom = (0, 0)
-                else:
-                    lo, hi = torch.aminmax(vals)
-                    dom = (int(lo.item()), int(hi.item()) - int(lo.item()) + 1)
-                self._domains[ck] = (c, dom)
-            base, G = dom
+            base, G = self._local_domain(c)
+            if multi and gkey is not None:
+                k = (gkey, r.colmap.get(group.expr_id))
+                dom = self._gdomains.get(k)
+                if dom is None:
+                    live = [x for x in d.all_gather_object((base, G)) if x[1] > 0]
+                    lo = min((x[0] for x in live), default=0)
+                    dom = (lo, max((x[0] + x[1] for x in live), default=lo) - lo)
+                    self._gdomains[k] = dom
+                base, G = dom
+                # identical on every rank, so the fallback decision is unanimous by construction
+                if G > limit:
+                    raise Unsupported("group domain too large for LDS aggregation")
+                return (True, G, base, None, c.atype) if G > 0 else None
         too_big = G > limit
-        d = self._dist()
-        if d is not None and d.world > 1:
+        if multi:
             # data-dependent fallbacks must be unanimous, or ranks diverge in their collectives
             too_big = any(d.all_gather_object(too_big))
         if too_big:
@@ -736,6 +754,23 @@ class GpuBackend:
         if G == 0:
             return None
         return None, max(G, 1), base, c.dictionary, c.atype
+
+    def _local_domain(self, c: DeviceColumn):
+        """(min, max - min + 1) of an integer column on this rank; tables are immutable, so it
+        is computed once per column."""
+        ck = id(c)
+        hit = self._domains.get(ck)
+        if hit is not None and hit[0] is c:
+            return hit[1]
+        import torch
+        vals = c.data if c.valid is None else c.data[c.valid.bool()]
+        if vals.numel() == 0:
+            dom = (0, 0)
+        else:
+            lo, hi = torch.aminmax(vals)
+            dom = (int(lo.item()), int(hi.item()) - int(lo.item()) + 1)
+        self._domains[ck] = (c, dom)
+        return dom
 
     def _agg_specs(self, fns, col_info):
         specs = [CP.agg_spec(fn, lambda a: col_info(a).slot) for fn in fns]
@@ -762,7 +797,8 @@ class GpuBackend:
         p = NL.ScanParams()
         if gs is None:  # empty group column
             return (*self._empty_agg(len(specs)), 1, 0, None, None)
-        _, G, gbase, gdict, gtype = gs
+        agreed, G, gbase, gdict, gtype = gs
+        self._groups_agreed = agreed is True
         # a single-valued group key runs the register-accumulating (ungrouped) kernel
         p.group_col = col_info(group).slot if (group is not None and G > 1) else -1
         p.num_groups, p.group_base = G, gbase
@@ -852,7 +888,8 @@ class GpuBackend:
             gs = self._group_spec_parts(side, group, MAX_GROUPS_JOIN)
             if gs is None:
                 return (*self._empty_agg(len(fns) + 1), 1, 0, None, None)
-        _, G, gbase, gdict, gtype = gs
+        agreed, G, gbase, gdict, gtype = gs
+        self._groups_agreed = agreed is True
         out = None
         for lp in lparts:
             for rp in rparts:
@@ -873,7 +910,7 @@ class GpuBackend:
         hi = max(s[2] + s[1] for s in specs)
         if hi - lo > limit:
             raise Unsupported("group domain too large for LDS aggregation")
-        return None, hi - lo, lo, None, specs[0][4]
+        return (True if all(s[0] is True for s in specs) else None), hi - lo, lo, None, specs[0][4]
 
     def _join_agg_pair(self, node, left: DRel, right: DRel, lk, rk, fns, group, G, gbase):
         # drive the kernel from a much smaller side (the appended part of a hybrid scan).  Only
@@ -901,10 +938,24 @@ class GpuBackend:
                 right.table.num_rows == 0:
             return self._empty_agg(len(specs), G)
         max_tiles = K.join_max_tiles(left.table.num_rows, rlen.numel())
+        conf = self.session.conf
+        if HyperspaceConf.codegen_enabled(conf) and HyperspaceConf.join_index_enabled(conf) and \
+                getattr(left.table, "global_key", None) is not None and \
+                getattr(right.table, "global_key", None) is not None and \
+                join_index.eligible(left.table, right.table, left.col(lk), right.col(rk)):
+            # both sides are resident index tables: join through the cached join index
+            with stage("join.index"):
+                fs, fl, fb = self._full_ranges(left.table)
+                jidx = join_index.get_join_index(jp, left.table, right.table, left.col(lk),
+                                                 right.col(rk), fs, fl, fb)
+            with stage("join.index_agg_kernel"):
+                return jit.join_index_agg(jp, rstart, rlen, jidx, self._compacts(descs))
         with stage("join.agg_kernel"):
             if HyperspaceConf.codegen_enabled(self.session.conf):
+                fr = getattr(left.table, "_full_ranges", None)
                 return jit.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles,
-                                    self._compacts(descs))
+                                    self._compacts(descs),
+                                    cache_spans=fr is not None and rstart is fr[0])
             return K.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles)
 
 

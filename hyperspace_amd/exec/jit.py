@@ -876,6 +876,41 @@ def _sample_offsets(roff):
     _SOFF[id(roff)] = (roff, soff, bound)
     return soff, bound
 
+# (identity key) -> (refs..., tile_prefix, spans): span records of full-range joins.  Holding the
+# range / offset tensors keeps their ids from being reused while the entry lives.
+_SPANS: Dict[tuple, tuple] = {}
+
+
+def _join_spans(p: NL.JoinParams, rstart, rlen, rbucket, roff, max_tiles: int, tile: int,
+                cache: bool):
+    import torch
+    from ..ops import kernels as K
+    L = NL.lib()
+    lk, rk = p.cols[p.lkey], p.cols[p.rkey]
+    key = (id(rstart), id(rlen), id(rbucket), id(roff), lk.data, lk.valid, rk.data, rk.valid,
+           int(p.key_is_float), tile)
+    if cache:
+        hit = _SPANS.get(key)
+        if hit is not None and hit[0] is rstart and hit[1] is rlen and hit[2] is rbucket \
+                and hit[3] is roff:
+            return hit[4], hit[5]
+    dev = rstart.device
+    tp = K.ranges_to_tiles(rlen, tile)
+    mt = (max_tiles * L.hs_join_tile_rows()) // tile + rlen.numel() + 1
+    spans = torch.empty(4 * mt, dtype=torch.int64, device=dev)
+    soff, bound = _sample_offsets(roff)
+    samples = torch.empty(max(bound, 1), dtype=torch.int64, device=dev)
+    NL.check(L.hs_join_spans_sampled(C.byref(p), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
+                                     NL.ptr(roff), NL.ptr(soff), roff.numel() - 1, bound,
+                                     NL.ptr(samples), rstart.numel(), NL.ptr(tp), int(mt),
+                                     NL.ptr(spans), tile, NL.stream_ptr()),
+             "hs_join_spans_sampled")
+    if cache:
+        if len(_SPANS) >= 16:
+            _SPANS.pop(next(iter(_SPANS)))
+        _SPANS[key] = (rstart, rlen, rbucket, roff, tp, spans)
+    return tp, spans
+
 
 def join_agg_values(p: NL.JoinParams, tile_prefix, spans, parts,
                     compacts=None) -> Dict[str, object]:
@@ -887,6 +922,114 @@ def join_agg_values(p: NL.JoinParams, tile_prefix, spans, parts,
                  [p.aggs[i] for i in range(p.naggs)], compacts)
     return v
 
+
+# ------------------------------------------------------------------------------------------------
+# Join through a cached join index (exec/join_index.py)
+# ------------------------------------------------------------------------------------------------
+def join_index_agg_shape(p: NL.JoinParams, compacts=None) -> tuple:
+    cols = tuple(sorted(_col_specs(p, compacts).items()))
+    preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
+                   p.preds[k].group) for k in range(p.npreds))
+    aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
+                 for i in range(p.naggs))
+    return ("join_index_agg", cols, preds, p.nlp, aggs, p.group_col, SCAN_ITEMS, BLOCK)
+
+
+def gen_join_index_agg(p: NL.JoinParams, compacts=None) -> Kernel:
+    """Fused join + aggregate as a streaming scan of the left table's row ranges (the scan
+    kernel's tiling) that reads ``jidx[row]`` — the matching right row from the cached join
+    index — and gathers right-side columns there.  Per row, in three dependent load batches:
+
+    1. ``jidx`` and the left predicate columns;
+    2. (rows passing the left CNF with a match) right predicate columns at ``j``;
+    3. (rows passing both) the aggregate inputs and the group column.
+
+    Right rows of consecutive left rows are monotone (both sides sorted by key per bucket), so
+    the gathers of a wavefront hit a few adjacent cache lines."""
+    args = Args()
+    for n, ct in (("rstart", "const long long*"), ("rlen", "const long long*"),
+                  ("tile_prefix", "const long long*"), ("jidx", "const int*")):
+        args.add("p", n, ct)
+    args.add("q", "R", "long long")
+    _common_args(args)
+    cols = _col_specs(p, compacts)
+    split = 8
+    gen = _Gen(args, cols, split, ("row", "j"))
+    lpreds = [(k, p.preds[k]) for k in range(p.nlp)]
+    rpreds = [(k, p.preds[k]) for k in range(p.nlp, p.npreds)]
+    aggs = [p.aggs[i] for i in range(p.naggs)]
+    grouped = p.group_col >= 0
+    first = _pred_slots(lpreds)
+    second = [s for s in _pred_slots(rpreds) if s not in first]
+    third = [s for s in _agg_slots(aggs) + ([p.group_col] if grouped else [])
+             if s not in first and s not in second]
+    third = list(dict.fromkeys(third))
+    T = BLOCK * SCAN_ITEMS
+    b: List[str] = []
+    b += _acc_decls(aggs, grouped, args)
+    b += ["  const i64 ntiles = a.tile_prefix[a.R];",
+          "  const i64 per = (ntiles + gridDim.x - 1) / gridDim.x;",
+          "  const i64 t0 = (i64)blockIdx.x * per;",
+          "  const i64 t1 = ntiles < t0 + per ? ntiles : t0 + per;",
+          "  int r = 0;",
+          "  if (t0 < t1) { int lo = 0, hi = (int)a.R;",
+          "    while (hi - lo > 1) { const int m = (lo + hi) >> 1; if (a.tile_prefix[m] <= t0) lo = m; else hi = m; }",
+          "    r = lo; }",
+          "  for (i64 t = t0; t < t1; ++t) {",
+          "    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;",
+          f"    const i64 off = (t - a.tile_prefix[r]) * {T};",
+          "    const i64 row0 = a.rstart[r] + off;",
+          f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};",
+          "#pragma unroll",
+          f"    for (int it = 0; it < {SCAN_ITEMS}; ++it) {{",
+          f"      const i64 k = (i64)it * {BLOCK} + threadIdx.x;",
+          "      const bool act = k < rows;",
+          "      const i64 row = row0 + (act ? k : 0);",
+          "      const int jr = act ? a.jidx[row] : -1;",
+          "      const i64 j = jr < 0 ? 0 : (i64)jr;"]
+    ind = "      "
+    for s in first:
+        gen.load(s, "act", b, ind)
+    b.append(f"{ind}bool pass = jr >= 0 && {gen.cnf(lpreds)};")
+    for s in second:
+        gen.load(s, "pass", b, ind)
+    b.append(f"{ind}pass = pass && {gen.cnf(rpreds)};")
+    for s in third:
+        gen.load(s, "pass", b, ind)
+    gvar = "gi"
+    if grouped:
+        g = p.group_col
+        base = args.add("q", "group_base", "long long")
+        ng = args.add("q", "num_groups", "long long")
+        b.append(f"{ind}const i64 gl = (i64)x{g} - {base};")
+        b.append(f"{ind}pass = pass && {gen.ok(g)} && gl >= 0 && gl < {ng};")
+        b.append(f"{ind}const int {gvar} = pass ? (int)gl : 0;")
+    b += _accumulate(gen, aggs, grouped, "pass", gvar, ind)
+    b += ["    }", "  }"]
+    b += _flush(aggs, grouped)
+    src = (_PRELUDE + args.struct_src() +
+           f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_join_index_agg(Args a) {{\n' +
+           "\n".join(b) + "\n}\n")
+    lds = (len(aggs) * p.num_groups * 32) if grouped else 0
+    return Kernel(src, "hs_jit_join_index_agg", args, lds)
+
+
+def join_index_agg(p: NL.JoinParams, rstart, rlen, jidx, compacts=None):
+    """Same outputs as ``join_agg``; ``jidx`` from ``join_index.get_join_index``."""
+    from ..ops import kernels as K
+    tp = K.ranges_to_tiles(rlen, BLOCK * SCAN_ITEMS)
+    grid = SCAN_GRID or NL.lib().hs_scan_grid()
+    GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
+    k = kernel_for(join_index_agg_shape(p, compacts), lambda: gen_join_index_agg(p, compacts))
+    parts = _partials(grid, GA, rstart.device)
+    v = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
+         "jidx": jidx.data_ptr(), "R": rstart.numel(), "psum": parts[0].data_ptr(),
+         "pcnt": parts[1].data_ptr(), "pmin": parts[2].data_ptr(), "pmax": parts[3].data_ptr(),
+         "num_groups": p.num_groups, "group_base": p.group_base}
+    _fill_common(v, p.cols, [(k_, p.preds[k_]) for k_ in range(p.npreds)],
+                 [p.aggs[i] for i in range(p.naggs)], compacts)
+    k.launch(grid, v, NL.stream_ptr(), GA * 32 if p.group_col >= 0 else 0)
+    return _final(parts, grid, GA, rstart.device)
 
 # ------------------------------------------------------------------------------------------------
 # Shape cache
@@ -939,8 +1082,12 @@ def scan_agg(p: NL.ScanParams, rstart, rlen, tile_prefix=None, compacts=None):
     return _final(parts, grid, GA, rstart.device)
 
 
-def join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, max_tiles: int, compacts=None):
-    """``max_tiles`` = ``ops.kernels.join_max_tiles`` (AOT tile); rescaled to this kernel's tile."""
+def join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, max_tiles: int, compacts=None,
+             cache_spans: bool = False):
+    """``max_tiles`` = ``ops.kernels.join_max_tiles`` (AOT tile); rescaled to this kernel's tile.
+    ``cache_spans``: the row ranges are the left table's cached full ranges, so the tile span
+    records (a function of the two key columns and the layouts only, not of the query's
+    literals) are reused across queries instead of re-searched."""
     import torch
     from ..ops import kernels as K
     L = NL.lib()
@@ -948,16 +1095,7 @@ def join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, max_tiles: int, comp
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
     dev = rstart.device
     tile = JOIN_BLOCK * JOIN_ITEMS
-    tp = K.ranges_to_tiles(rlen, tile)
-    mt = (max_tiles * L.hs_join_tile_rows()) // tile + rlen.numel() + 1
-    spans = torch.empty(4 * mt, dtype=torch.int64, device=dev)
-    soff, bound = _sample_offsets(roff)
-    samples = torch.empty(max(bound, 1), dtype=torch.int64, device=dev)
-    NL.check(L.hs_join_spans_sampled(C.byref(p), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
-                                     NL.ptr(roff), NL.ptr(soff), roff.numel() - 1, bound,
-                                     NL.ptr(samples), rstart.numel(), NL.ptr(tp), int(mt),
-                                     NL.ptr(spans), tile, NL.stream_ptr()),
-             "hs_join_spans_sampled")
+    tp, spans = _join_spans(p, rstart, rlen, rbucket, roff, max_tiles, tile, cache_spans)
     k = kernel_for(join_agg_shape(p, compacts), lambda: gen_join_agg(p, compacts))
     parts = _partials(grid, GA, dev)
     k.launch(grid, join_agg_values(p, tp, spans, parts, compacts), NL.stream_ptr(),

@@ -100,4 +100,9 @@ HBM_COMPRESSION_ENABLED_DEFAULT = "false"
 # replay captured hipGraphs of the scan pipeline (exec/graphs.py)
 HIPGRAPH_ENABLED = "spark.hyperspace.mi.hipGraph.enabled"
 HIPGRAPH_ENABLED_DEFAULT = "true"
+# cached join index (left row -> first matching right row, int32 in HBM) for joins of two
+# device-resident index tables with unique integer right keys: the fused join aggregate becomes a
+# streaming scan of the left table plus a gather, no per-tile span search (exec/join_index.py)
+JOIN_INDEX_ENABLED = "spark.hyperspace.mi.joinIndex.enabled"
+JOIN_INDEX_ENABLED_DEFAULT = "true"
 FAULT_INJECTION = "spark.hyperspace.mi.faultInjection"

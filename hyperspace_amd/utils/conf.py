@@ -118,5 +118,9 @@ class HyperspaceConf:
         return _b(conf.get(C.HIPGRAPH_ENABLED, C.HIPGRAPH_ENABLED_DEFAULT))
 
     @staticmethod
+    def join_index_enabled(conf) -> bool:
+        return _b(conf.get(C.JOIN_INDEX_ENABLED, C.JOIN_INDEX_ENABLED_DEFAULT))
+
+    @staticmethod
     def hbm_compression_enabled(conf) -> bool:
         return _b(conf.get(C.HBM_COMPRESSION_ENABLED, C.HBM_COMPRESSION_ENABLED_DEFAULT))

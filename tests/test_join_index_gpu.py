@@ -1,0 +1,145 @@
+"""Cached join index (exec/join_index.py): joins of two resident index tables run as a streaming
+scan + gather.  Results are checked against the host oracle and against the merge-join kernels
+(join index disabled); the index itself is checked row by row against a numpy merge."""
+import os
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.parquet as pq
+import pytest
+
+from hyperspace_amd import Hyperspace, IndexConfig, Session, col, count, max_, min_, sum_
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def data(tmp_path, device):
+    rng = np.random.default_rng(11)
+    n_ord = 30_000
+    okeys = rng.permutation(np.arange(1, n_ord + 1, dtype=np.int64) * 4)
+    od = pa.table({"o_orderkey": okeys,
+                   "o_orderdate": pa.array(rng.integers(8000, 10500, n_ord).astype(np.int32)),
+                   "o_shippriority": rng.integers(0, 5, n_ord).astype(np.int32)})
+    # lineitem keys: FK into orders plus keys with no order (no match) and nulls
+    lk = np.concatenate([np.repeat(okeys, rng.integers(1, 8, n_ord)),
+                         rng.integers(0, n_ord, 3000) * 4 + 2])
+    n = len(lk)
+    valid = rng.random(n) > 0.01
+    li = pa.table({"l_orderkey": pa.array(lk, mask=~valid),
+                   "l_extendedprice": np.round(rng.random(n) * 1e5, 2),
+                   "l_discount": rng.integers(0, 11, n) / 100.0,
+                   "l_shipdate": pa.array(rng.integers(8000, 10600, n).astype(np.int32))})
+    # a right side with duplicate keys (not eligible: merge-join kernels)
+    dup = pa.table({"d_key": np.repeat(okeys[:5000], 2),
+                    "d_val": rng.integers(0, 100, 10000).astype(np.int32)})
+    for name, t, parts in (("lineitem", li, 4), ("orders", od, 2), ("dup", dup, 1)):
+        os.makedirs(tmp_path / name)
+        step = (t.num_rows + parts - 1) // parts
+        for i in range(parts):
+            pq.write_table(t.slice(i * step, step), tmp_path / name / f"part-{i}.parquet")
+    s = Session(conf={"spark.hyperspace.system.path": str(tmp_path / "idx"),
+                      "spark.hyperspace.index.numBuckets": "16",
+                      "spark.sql.autoBroadcastJoinThreshold": "-1",
+                      "spark.hyperspace.mi.execution.device": "gpu"},
+                warehouse_dir=str(tmp_path / "wh"))
+    hs = Hyperspace(s)
+    li_df = s.read.parquet(str(tmp_path / "lineitem"))
+    od_df = s.read.parquet(str(tmp_path / "orders"))
+    dup_df = s.read.parquet(str(tmp_path / "dup"))
+    hs.createIndex(li_df, IndexConfig("li_ok", ["l_orderkey"],
+                                      ["l_extendedprice", "l_discount", "l_shipdate"]))
+    hs.createIndex(od_df, IndexConfig("od_ok", ["o_orderkey"], ["o_orderdate", "o_shippriority"]))
+    hs.createIndex(dup_df, IndexConfig("dup_k", ["d_key"], ["d_val"]))
+    Hyperspace.enable(s)
+    return s, li_df, od_df, dup_df
+
+
+def _run(s, df, device="gpu", join_index=True):
+    s.conf.set("spark.hyperspace.mi.execution.device", device)
+    s.conf.set("spark.hyperspace.mi.joinIndex.enabled", "true" if join_index else "false")
+    t = df.to_arrow()
+    path = s.backend().last_path if device == "gpu" else "cpu"
+    s.conf.set("spark.hyperspace.mi.execution.device", "gpu")
+    s.conf.set("spark.hyperspace.mi.joinIndex.enabled", "true")
+    return t.sort_by([(n, "ascending") for n in t.column_names]) if t.num_rows else t, path
+
+
+def _close(a: pa.Table, b: pa.Table):
+    assert a.num_rows == b.num_rows
+    for x, y in zip(a.columns, b.columns):
+        for u, v in zip(x.to_pylist(), y.to_pylist()):
+            if isinstance(u, float):
+                assert abs(u - v) <= 1e-9 * max(1.0, abs(v)), (u, v)
+            else:
+                assert u == v, (u, v)
+
+
+def _q3(li, od, dd):
+    return li.join(od, li["l_orderkey"] == od["o_orderkey"]) \
+        .filter((col("o_orderdate") < dd) & (col("l_shipdate") > dd)) \
+        .groupBy("o_shippriority") \
+        .agg(sum_(col("l_extendedprice") * (1 - col("l_discount"))).alias("rev"),
+             count("*").alias("n"), min_(col("o_orderdate")).alias("mn"),
+             max_(col("l_shipdate")).alias("mx"))
+
+
+def test_join_index_q3_matches_oracle_and_merge_join(data):
+    s, li, od, _ = data
+    from hyperspace_amd.exec.jit import _KERNELS
+    for dd in (9000, 9300, 10000):
+        q = _q3(li, od, dd)
+        g, p = _run(s, q)
+        assert p == "native", s.backend().fallback_reason
+        m, p2 = _run(s, q, join_index=False)
+        assert p2 == "native"
+        c, _ = _run(s, q, device="cpu")
+        _close(g, c)
+        _close(m, c)
+    assert any(k[0] == "join_index_agg" for k in _KERNELS), "join-index kernel did not run"
+
+
+def test_join_index_ungrouped_and_left_range_pruned(data):
+    s, li, od, _ = data
+    j = li.join(od, li["l_orderkey"] == od["o_orderkey"])
+    for q in (j.filter(col("o_orderdate") < 9500).agg(sum_(col("l_extendedprice")).alias("s")),
+              j.filter((col("l_orderkey") > 20000) & (col("l_orderkey") <= 80000))
+               .agg(count("*").alias("n"), sum_(col("o_shippriority")).alias("p"))):
+        g, p = _run(s, q)
+        assert p == "native", s.backend().fallback_reason
+        c, _ = _run(s, q, device="cpu")
+        _close(g, c)
+
+
+def test_join_index_matches_numpy_merge(data):
+    """Every left row's index entry is the first right row with an equal key, or -1."""
+    s, li, od, _ = data
+    q = li.join(od, li["l_orderkey"] == od["o_orderkey"]).agg(count("*").alias("n"))
+    _run(s, q)
+    be = s.backend()
+    tables = [t for t in be.cache._lru.values() if "_join_index" in t.__dict__]
+    assert tables, "no join index was built"
+    lt = tables[0]
+    (rref, lcol, rcol, jidx), = lt._join_index.values()
+    lk = lcol.data.cpu().numpy()
+    lv = lcol.valid.cpu().numpy().astype(bool) if lcol.valid is not None else np.ones(len(lk), bool)
+    rk = rcol.data.cpu().numpy()
+    rt = rref()
+    j = jidx.cpu().numpy()[:lt.num_rows]
+    loff, roff = lt.bucket_offsets_host, rt.bucket_offsets_host
+    for b in range(len(loff) - 1):
+        seg = rk[roff[b]:roff[b + 1]]
+        for i in range(loff[b], loff[b + 1]):
+            pos = np.searchsorted(seg, lk[i])
+            want = roff[b] + pos if lv[i] and pos < len(seg) and seg[pos] == lk[i] else -1
+            assert j[i] == want, (b, i, j[i], want)
+
+
+def test_duplicate_right_keys_keep_merge_join(data):
+    s, li, _, dup = data
+    q = li.join(dup, li["l_orderkey"] == dup["d_key"]).groupBy("d_val") \
+        .agg(count("*").alias("n"), sum_(col("l_discount")).alias("d"))
+    g, p = _run(s, q)
+    assert p == "native", s.backend().fallback_reason
+    c, _ = _run(s, q, device="cpu")
+    _close(g, c)
