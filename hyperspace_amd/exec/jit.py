@@ -49,6 +49,8 @@ JOIN_EAGER = os.environ.get("HS_JIT_JOIN_EAGER", "0") == "1"
 # stage the right side's columns of each tile's key span in LDS with the keys
 JOIN_STAGE_RIGHT = os.environ.get("HS_JIT_JOIN_STAGE_RIGHT", "1") == "1"
 SCAN_EAGER = os.environ.get("HS_JIT_SCAN_EAGER", "0") == "1"
+# rows per thread of the join-index kernel (phase-major: each phase's loads of all items in flight)
+JI_ITEMS = int(os.environ.get("HS_JIT_JI_ITEMS", "4"))
 # software-pipeline the join's tile loop (next tile's batch loads overlap this tile's work)
 JOIN_PIPELINE = os.environ.get("HS_JIT_JOIN_PIPELINE", "1") == "1"
 # direct-address LDS table for dense integer key spans (one verified lookup instead of a
@@ -932,17 +934,33 @@ def join_index_agg_shape(p: NL.JoinParams, compacts=None) -> tuple:
                    p.preds[k].group) for k in range(p.npreds))
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
-    return ("join_index_agg", cols, preds, p.nlp, aggs, p.group_col, SCAN_ITEMS, BLOCK)
+    return ("join_index_agg", cols, preds, p.nlp, aggs, p.group_col, JI_ITEMS, BLOCK)
+
+
+def _uload(gen: _Gen, slot: int, it: int, out: List[str], ind: str) -> None:
+    """Unconditional load of column ``slot`` for batch item ``it`` at the generator's row
+    variable (callers redirect rows that do not need the value to an always-valid shared row, so
+    the load needs no branch and the wavefront's redirected lanes coalesce into one line)."""
+    ct = _CTYPE[gen.cols[slot][0]]
+    r = gen.row(slot)
+    out.append(f"{ind}const {ct} x{slot}_{it} = {gen.value(slot, r)};")
+    if gen.cols[slot][1]:
+        out.append(f"{ind}const bool n{slot}_{it} = {gen.vptr(slot)}[{r}] != 0;")
 
 
 def gen_join_index_agg(p: NL.JoinParams, compacts=None) -> Kernel:
-    """Fused join + aggregate as a streaming scan of the left table's row ranges (the scan
-    kernel's tiling) that reads ``jidx[row]`` — the matching right row from the cached join
-    index — and gathers right-side columns there.  Per row, in three dependent load batches:
+    """Fused join + aggregate as a streaming scan of the left table's row ranges that reads
+    ``jidx[row]`` — the matching right row from the cached join index (exec/join_index.py) — and
+    gathers right-side columns there.
 
-    1. ``jidx`` and the left predicate columns;
-    2. (rows passing the left CNF with a match) right predicate columns at ``j``;
-    3. (rows passing both) the aggregate inputs and the group column.
+    The kernel is latency-bound on its chain of dependent loads, so the code is phase-major over
+    the JI_ITEMS rows of each thread (every row's loads of one phase are in flight together) and
+    branch-free (rows that do not need a value load it from a shared, always-valid row instead
+    of branching around the load):
+
+    1. ``jidx`` and the left predicate columns of all items;
+    2. right predicate columns at ``j`` (non-matching rows read right row 0);
+    3. aggregate inputs and the group column (failing rows read the tile's first row).
 
     Right rows of consecutive left rows are monotone (both sides sorted by key per bucket), so
     the gathers of a wavefront hit a few adjacent cache lines."""
@@ -954,7 +972,6 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None) -> Kernel:
     _common_args(args)
     cols = _col_specs(p, compacts)
     split = 8
-    gen = _Gen(args, cols, split, ("row", "j"))
     lpreds = [(k, p.preds[k]) for k in range(p.nlp)]
     rpreds = [(k, p.preds[k]) for k in range(p.nlp, p.npreds)]
     aggs = [p.aggs[i] for i in range(p.naggs)]
@@ -964,9 +981,14 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None) -> Kernel:
     third = [s for s in _agg_slots(aggs) + ([p.group_col] if grouped else [])
              if s not in first and s not in second]
     third = list(dict.fromkeys(third))
-    T = BLOCK * SCAN_ITEMS
+    allslots = first + second + third
+    NI = JI_ITEMS
+    T = BLOCK * NI
     b: List[str] = []
     b += _acc_decls(aggs, grouped, args)
+    if grouped:
+        base = args.add("q", "group_base", "long long")
+        ng = args.add("q", "num_groups", "long long")
     b += ["  const i64 ntiles = a.tile_prefix[a.R];",
           "  const i64 per = (ntiles + gridDim.x - 1) / gridDim.x;",
           "  const i64 t0 = (i64)blockIdx.x * per;",
@@ -978,34 +1000,53 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None) -> Kernel:
           "  for (i64 t = t0; t < t1; ++t) {",
           "    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;",
           f"    const i64 off = (t - a.tile_prefix[r]) * {T};",
-          "    const i64 row0 = a.rstart[r] + off;",
-          f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};",
-          "#pragma unroll",
-          f"    for (int it = 0; it < {SCAN_ITEMS}; ++it) {{",
-          f"      const i64 k = (i64)it * {BLOCK} + threadIdx.x;",
-          "      const bool act = k < rows;",
-          "      const i64 row = row0 + (act ? k : 0);",
-          "      const int jr = act ? a.jidx[row] : -1;",
-          "      const i64 j = jr < 0 ? 0 : (i64)jr;"]
-    ind = "      "
-    for s in first:
-        gen.load(s, "act", b, ind)
-    b.append(f"{ind}bool pass = jr >= 0 && {gen.cnf(lpreds)};")
-    for s in second:
-        gen.load(s, "pass", b, ind)
-    b.append(f"{ind}pass = pass && {gen.cnf(rpreds)};")
-    for s in third:
-        gen.load(s, "pass", b, ind)
-    gvar = "gi"
-    if grouped:
-        g = p.group_col
-        base = args.add("q", "group_base", "long long")
-        ng = args.add("q", "num_groups", "long long")
-        b.append(f"{ind}const i64 gl = (i64)x{g} - {base};")
-        b.append(f"{ind}pass = pass && {gen.ok(g)} && gl >= 0 && gl < {ng};")
-        b.append(f"{ind}const int {gvar} = pass ? (int)gl : 0;")
-    b += _accumulate(gen, aggs, grouped, "pass", gvar, ind)
-    b += ["    }", "  }"]
+          "    const i64 tb0 = a.rstart[r] + off;",
+          f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};"]
+    ind = "    "
+    # phase 1: join index + left predicate columns of every item
+    for it in range(NI):
+        b += [f"{ind}const bool act{it} = {it * BLOCK} + (i64)threadIdx.x < rows;",
+              f"{ind}const i64 row{it} = tb0 + (act{it} ? {it * BLOCK} + (i64)threadIdx.x : 0);"]
+    for it in range(NI):
+        b.append(f"{ind}const int jr{it} = a.jidx[row{it}];")
+        g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"))
+        for s in first:
+            _uload(g1, s, it, b, ind)
+    for it in range(NI):
+        g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"))
+        cond = _rename(g1.cnf(lpreds), allslots, it)
+        b.append(f"{ind}bool pass{it} = act{it} && jr{it} >= 0 && {cond};")
+        b.append(f"{ind}const i64 j{it} = pass{it} ? (i64)jr{it} : 0;")
+    # phase 2: right predicate columns at the matched rows
+    for it in range(NI):
+        g2 = _Gen(args, cols, split, (f"row{it}", f"j{it}"))
+        for s in second:
+            _uload(g2, s, it, b, ind)
+    for it in range(NI):
+        g2 = _Gen(args, cols, split, (f"row{it}", f"j{it}"))
+        b.append(f"{ind}pass{it} = pass{it} && {_rename(g2.cnf(rpreds), allslots, it)};")
+    # phase 3: aggregate inputs (rows that failed read the tile's first row / right row 0)
+    if third:
+        for it in range(NI):
+            b += [f"{ind}const i64 lq{it} = pass{it} ? row{it} : tb0;",
+                  f"{ind}const i64 jq{it} = pass{it} ? j{it} : 0;"]
+        for it in range(NI):
+            g3 = _Gen(args, cols, split, (f"lq{it}", f"jq{it}"))
+            for s in third:
+                _uload(g3, s, it, b, ind)
+    for it in range(NI):
+        g3 = _Gen(args, cols, split, (f"lq{it}", f"jq{it}"))
+        gvar = f"gi{it}"
+        if grouped:
+            g = p.group_col
+            gx = _rename(f"x{g}", allslots, it)
+            ok = _rename(g3.ok(g), allslots, it)
+            b.append(f"{ind}const i64 gl{it} = (i64){gx} - {base};")
+            b.append(f"{ind}pass{it} = pass{it} && {ok} && gl{it} >= 0 && gl{it} < {ng};")
+            b.append(f"{ind}const int {gvar} = pass{it} ? (int)gl{it} : 0;")
+        b += [_rename(x, allslots, it) for x in
+              _accumulate(g3, aggs, grouped, f"pass{it}", gvar, ind)]
+    b += ["  }"]
     b += _flush(aggs, grouped)
     src = (_PRELUDE + args.struct_src() +
            f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_join_index_agg(Args a) {{\n' +
@@ -1017,7 +1058,7 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None) -> Kernel:
 def join_index_agg(p: NL.JoinParams, rstart, rlen, jidx, compacts=None):
     """Same outputs as ``join_agg``; ``jidx`` from ``join_index.get_join_index``."""
     from ..ops import kernels as K
-    tp = K.ranges_to_tiles(rlen, BLOCK * SCAN_ITEMS)
+    tp = K.ranges_to_tiles(rlen, BLOCK * JI_ITEMS)
     grid = SCAN_GRID or NL.lib().hs_scan_grid()
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
     k = kernel_for(join_index_agg_shape(p, compacts), lambda: gen_join_index_agg(p, compacts))
