@@ -11,7 +11,14 @@ on the HIP kernels + cross-rank combine).  ``value`` = whole-job queries/sec.  D
 TPC-H-shaped (``hyperspace_amd.models.tpch``) and generated once per data dir.  Index build is
 timed separately (three covering indexes: lineitem(l_shipdate), lineitem(l_orderkey),
 orders(o_orderkey)); ``index_build_gbps`` = decoded indexed-column bytes / build wall time.
-Total work is fixed as N grows (strong scaling): buckets are owned by rank ``b % N``.
+Index builds shard buckets over ranks (bucket ``b`` -> rank ``b % N``, RCCL all-to-all).  Queries
+run with two placements (``--placement``, default both; the JSON reports the last):
+
+* ``sharded``: each rank holds its buckets only; every query runs on all ranks and partial
+  aggregates combine with one all-gather — strong scaling of a single query stream;
+* ``replicated``: every rank loads all buckets into its HBM (the SF100 index set is ~36 GB of a
+  288 GB MI355X) and serves its own query stream with no collective — read replicas, weak
+  scaling (``value`` = total queries/s of all ranks; the sharded numbers are in ``sharded``).
 """
 import argparse
 import datetime
@@ -61,6 +68,11 @@ def main():
     ap.add_argument("--codec", default="none",
                     help="index file codec; 'none' = device dictionary/bit-packed encoding "
                          "(exec/pq_encode.py), otherwise pyarrow with that codec")
+    ap.add_argument("--placement", default="both", choices=["both", "sharded", "replicated"],
+                    help="multi-GPU query placement (spark.hyperspace.mi.index.placement): "
+                         "sharded = buckets b %% N per rank, every query on all ranks + one "
+                         "all-gather; replicated = every rank holds all buckets and serves its "
+                         "own query stream; both = time sharded, then replicated (reported)")
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
                     help="cpu = the pyarrow host engine (measured baseline, BASELINE.md)")
     args = ap.parse_args()
@@ -179,46 +191,60 @@ def main():
             raise RuntimeError(f"query fell back to host: {backend.fallback_reason}")
         return r1, r2
 
-    tl = time.perf_counter()
-    for i in range(args.warmup):
-        step(1000 + i)
-    sync()
-    barrier()
-    warm_s = time.perf_counter() - tl
-    log(rank, f"[bench] warmup {args.warmup} steps in {warm_s:.2f}s "
-              f"(includes first HBM load of the indexes)")
+    def timed(mode):
+        """Warm up, then time exactly ``args.steps`` steps bracketed by barrier + sync."""
+        s.conf.set("spark.hyperspace.mi.index.placement", mode)
+        off = rank * 100000 if mode == "replicated" else 0   # replicas serve distinct queries
+        tl = time.perf_counter()
+        for i in range(args.warmup):
+            step(1000 + off + i)
+        sync()
+        barrier()
+        warm = time.perf_counter() - tl
+        log(rank, f"[bench] {mode}: warmup {args.warmup} steps in {warm:.2f}s "
+                  f"(includes first HBM load of the indexes)")
+        TRACER.reset()  # HS_PROFILE=1: per-stage host/device times of the timed steps only
+        prof = None
+        if os.environ.get("HS_BENCH_PROFILE") and rank == 0:
+            import cProfile
+            prof = cProfile.Profile()
+        barrier()
+        sync()
+        t_start = time.perf_counter()
+        if prof is not None:
+            prof.enable()
+        res = []
+        for i in range(args.steps):
+            res.append(step(off + i))
+        sync()
+        barrier()
+        el = time.perf_counter() - t_start
+        if prof is not None:
+            import io
+            import pstats
+            prof.disable()
+            buf = io.StringIO()
+            pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(40)
+            log(rank, buf.getvalue())
+        if TRACER.profile:
+            log(rank, f"[bench] {mode} stage profile (timed steps)\n" +
+                format_report(TRACER.report()))
+        if dist:
+            el = dist.all_reduce_max_float(el)
+        # sharded: every query runs on all ranks; replicated: each rank runs its own stream
+        nq = 2 * args.steps * (world if mode == "replicated" else 1)
+        return {"qps": nq / el, "ms_per_step": el / args.steps * 1000.0, "warmup_s": warm,
+                "results": res, "first": off}
 
     from hyperspace_amd.utils.tracing import TRACER, format_report
-    TRACER.reset()  # HS_PROFILE=1: per-stage host/device times of the timed steps only
-    prof = None
-    if os.environ.get("HS_BENCH_PROFILE") and rank == 0:
-        import cProfile
-        prof = cProfile.Profile()
-    barrier()
-    sync()
-    t_start = time.perf_counter()
-    if prof is not None:
-        prof.enable()
-    results = []
-    for i in range(args.steps):
-        results.append(step(i))
-    sync()
-    barrier()
-    elapsed = time.perf_counter() - t_start
-    if prof is not None:
-        import io
-        import pstats
-        prof.disable()
-        buf = io.StringIO()
-        pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(40)
-        log(rank, buf.getvalue())
-    if TRACER.profile:
-        log(rank, "[bench] stage profile (timed steps)\n" + format_report(TRACER.report()))
-    if dist:
-        elapsed = dist.all_reduce_max_float(elapsed)
-    nq = 2 * args.steps
-    qps = nq / elapsed
-    ms_step = elapsed / args.steps * 1000.0
+    modes = ["sharded", "replicated"] if world > 1 and args.placement == "both" else \
+        [args.placement if world > 1 else "sharded"]
+    runs = {m: timed(m) for m in modes}
+    final = modes[-1]
+    qps = runs[final]["qps"]
+    ms_step = runs[final]["ms_per_step"]
+    warm_s = runs[final]["warmup_s"]
+    results = runs[final]["results"]
 
     # ---------------------------------------------------------------- per-query latency
     lat = {}
@@ -239,8 +265,9 @@ def main():
     if not args.no_crosscheck and (world == 1 or sf <= 10):
         s.disableHyperspace()
         tc = time.perf_counter()
-        n6 = q6(0).collect()[0][0]
-        n3 = sorted(q3(0).collect())
+        first = runs[final]["first"]   # the literals of this rank's first timed step
+        n6 = q6(first).collect()[0][0]
+        n3 = sorted(q3(first).collect())
         noidx_s = time.perf_counter() - tc
         s.enableHyperspace()
         i6 = results[0][0][0][0]
@@ -256,16 +283,23 @@ def main():
     if rank == 0:
         out = {"metric": METRIC, "value": round(qps, 3), "unit": "queries/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
-               "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+               "higher_is_better": True,
+               "scaling": "weak" if final == "replicated" else "strong", "vs_baseline": None,
                "dtype": "fp64", "data": "synthetic",
                "config": {"model": f"tpch-sf{sf:g} lineitem/orders covering indexes",
                           "global_batch": 2, "seq_len": 0,
-                          "parallelism": f"bucket-dp{world}" if on_gpu else "cpu-host",
+                          "parallelism": (f"replicated-dp{world}" if final == "replicated" else
+                                          f"bucket-dp{world}") if on_gpu else "cpu-host",
+                          "placement": final,
                           "num_buckets": args.buckets, "source_files": nfiles,
                           "device": args.device},
                "index_build_gbps": round(build_gbps, 3), "index_build_s": round(build_s, 3),
                "index_build": per_index, "latency": lat, "warmup_s": round(warm_s, 3),
                "datagen_s": round(gen_s, 2), "crosscheck": check}
+        if "sharded" in runs and final != "sharded":
+            out["sharded"] = {"value": round(runs["sharded"]["qps"], 3),
+                              "ms_per_step": round(runs["sharded"]["ms_per_step"], 3),
+                              "scaling": "strong"}
         if on_gpu:
             out["device_cache"] = {"hits": backend.cache.hits, "misses": backend.cache.misses}
         if not on_gpu:

@@ -112,7 +112,13 @@ class GpuBackend:
         return self._cpu
 
     def _dist(self):
-        return getattr(self.session, "dist", None)
+        """The process group queries run over, or None when this rank answers alone: single
+        process, or replicated placement (every rank holds every bucket; builds still shard
+        through ``session.dist`` in exec/device_build.py)."""
+        d = getattr(self.session, "dist", None)
+        if d is not None and HyperspaceConf.index_placement(self.session.conf) == "replicated":
+            return None
+        return d
 
     def collect(self, plan: X.SparkPlan) -> pa.Table:
         t0 = time.perf_counter()

@@ -476,6 +476,12 @@ def scan_agg_shape(p: NL.ScanParams, compacts=None) -> tuple:
 
 
 def gen_scan_agg(p: NL.ScanParams, compacts=None) -> Kernel:
+    """Filter + aggregate over row ranges, phase-major over the SCAN_ITEMS rows of each thread
+    and branch-free: (1) the predicate columns of every item are loaded together; (2) the
+    aggregate inputs (and group column) of every item, where rows that failed the predicates
+    read the tile's first row instead of branching around the load — their lanes coalesce into
+    one line, so only passing rows cost HBM bytes; (3) accumulate.  SCAN_EAGER loads every
+    column in phase 1."""
     args = Args()
     for n, ct in (("rstart", "const long long*"), ("rlen", "const long long*"),
                   ("tile_prefix", "const long long*")):
@@ -483,7 +489,6 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None) -> Kernel:
     args.add("q", "R", "long long")
     _common_args(args)
     cols = _col_specs(p, compacts)
-    gen = _Gen(args, cols, NL.MAX_COLS, ("row", "row"))
     preds = [(k, p.preds[k]) for k in range(p.npreds)]
     aggs = [p.aggs[i] for i in range(p.naggs)]
     grouped = p.group_col >= 0
@@ -491,9 +496,16 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None) -> Kernel:
     aslots = [s for s in _agg_slots(aggs) if s not in pslots]
     if grouped and p.group_col not in pslots and p.group_col not in aslots:
         aslots.append(p.group_col)
-    T = BLOCK * SCAN_ITEMS
+    if SCAN_EAGER:
+        pslots, aslots = pslots + aslots, []
+    allslots = pslots + aslots
+    NI = SCAN_ITEMS
+    T = BLOCK * NI
     b: List[str] = []
     b += _acc_decls(aggs, grouped, args)
+    if grouped:
+        base = args.add("q", "group_base", "long long")
+        ng = args.add("q", "num_groups", "long long")
     b += ["  const i64 ntiles = a.tile_prefix[a.R];",
           "  const i64 per = (ntiles + gridDim.x - 1) / gridDim.x;",
           "  const i64 t0 = (i64)blockIdx.x * per;",
@@ -505,30 +517,38 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None) -> Kernel:
           "  for (i64 t = t0; t < t1; ++t) {",
           "    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;",
           f"    const i64 off = (t - a.tile_prefix[r]) * {T};",
-          "    const i64 row0 = a.rstart[r] + off;",
-          f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};",
-          "#pragma unroll",
-          f"    for (int it = 0; it < {SCAN_ITEMS}; ++it) {{",
-          f"      const i64 k = (i64)it * {BLOCK} + threadIdx.x;",
-          "      const bool act = k < rows;",
-          "      const i64 row = row0 + (act ? k : 0);"]
-    ind = "      "
-    for s in pslots + (aslots if SCAN_EAGER else []):
-        gen.load(s, "act", b, ind)
-    b.append(f"{ind}bool pass = act && {gen.cnf(preds)};")
-    if not SCAN_EAGER:
-        for s in aslots:
-            gen.load(s, "pass", b, ind)
-    gvar = "gi"
-    if grouped:
-        g = p.group_col
-        base = args.add("q", "group_base", "long long")
-        ng = args.add("q", "num_groups", "long long")
-        b.append(f"{ind}const i64 gl = (i64)x{g} - {base};")
-        b.append(f"{ind}pass = pass && {gen.ok(g)} && gl >= 0 && gl < {ng};")
-        b.append(f"{ind}const int {gvar} = pass ? (int)gl : 0;")
-    b += _accumulate(gen, aggs, grouped, "pass", gvar, ind)
-    b += ["    }", "  }"]
+          "    const i64 tb0 = a.rstart[r] + off;",
+          f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};"]
+    ind = "    "
+    for it in range(NI):
+        b += [f"{ind}const bool act{it} = {it * BLOCK} + (i64)threadIdx.x < rows;",
+              f"{ind}const i64 row{it} = tb0 + (act{it} ? {it * BLOCK} + (i64)threadIdx.x : 0);"]
+    for it in range(NI):
+        g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"))
+        for s in pslots:
+            _uload(g1, s, it, b, ind)
+    for it in range(NI):
+        g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"))
+        b.append(f"{ind}bool pass{it} = act{it} && {_rename(g1.cnf(preds), allslots, it)};")
+    if aslots:
+        for it in range(NI):
+            b.append(f"{ind}const i64 lq{it} = pass{it} ? row{it} : tb0;")
+        for it in range(NI):
+            g2 = _Gen(args, cols, NL.MAX_COLS, (f"lq{it}", f"lq{it}"))
+            for s in aslots:
+                _uload(g2, s, it, b, ind)
+    for it in range(NI):
+        g2 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"))
+        gvar = f"gi{it}"
+        if grouped:
+            g = p.group_col
+            b.append(f"{ind}const i64 gl{it} = (i64){_rename(f'x{g}', allslots, it)} - {base};")
+            b.append(f"{ind}pass{it} = pass{it} && {_rename(g2.ok(g), allslots, it)} && "
+                     f"gl{it} >= 0 && gl{it} < {ng};")
+            b.append(f"{ind}const int {gvar} = pass{it} ? (int)gl{it} : 0;")
+        b += [_rename(x, allslots, it) for x in
+              _accumulate(g2, aggs, grouped, f"pass{it}", gvar, ind)]
+    b += ["  }"]
     b += _flush(aggs, grouped)
     src = (_PRELUDE + args.struct_src() +
            f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_scan_agg(Args a) {{\n' +

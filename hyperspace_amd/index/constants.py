@@ -105,4 +105,12 @@ HIPGRAPH_ENABLED_DEFAULT = "true"
 # streaming scan of the left table plus a gather, no per-tile span search (exec/join_index.py)
 JOIN_INDEX_ENABLED = "spark.hyperspace.mi.joinIndex.enabled"
 JOIN_INDEX_ENABLED_DEFAULT = "true"
+# Query-time placement of index buckets across the ranks of a torch.distributed job:
+#  "sharded"    bucket b is resident on rank b % world only; every query runs on all ranks and
+#               partial results combine with one RCCL all-gather (strong scaling of one query);
+#  "replicated" every rank holds all buckets in its HBM (an SF100 index set is ~36 GB of a
+#               288 GB MI355X) and answers queries alone, with no collective (read replicas:
+#               query throughput scales with ranks).  Index builds are sharded either way.
+INDEX_PLACEMENT = "spark.hyperspace.mi.index.placement"
+INDEX_PLACEMENT_DEFAULT = "sharded"
 FAULT_INJECTION = "spark.hyperspace.mi.faultInjection"

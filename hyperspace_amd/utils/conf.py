@@ -118,6 +118,13 @@ class HyperspaceConf:
         return _b(conf.get(C.HIPGRAPH_ENABLED, C.HIPGRAPH_ENABLED_DEFAULT))
 
     @staticmethod
+    def index_placement(conf) -> str:
+        v = str(conf.get(C.INDEX_PLACEMENT, C.INDEX_PLACEMENT_DEFAULT)).lower()
+        if v not in ("sharded", "replicated"):
+            raise ValueError(f"{C.INDEX_PLACEMENT} must be sharded or replicated, got {v}")
+        return v
+
+    @staticmethod
     def join_index_enabled(conf) -> bool:
         return _b(conf.get(C.JOIN_INDEX_ENABLED, C.JOIN_INDEX_ENABLED_DEFAULT))
 
