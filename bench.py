@@ -73,6 +73,9 @@ def main():
                          "sharded = buckets b %% N per rank, every query on all ranks + one "
                          "all-gather; replicated = every rank holds all buckets and serves its "
                          "own query stream; both = time sharded, then replicated (reported)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="query steps kept in flight (DataFrame.collect_async): 1 = each query "
+                         "finishes before the next is planned")
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
                     help="cpu = the pyarrow host engine (measured baseline, BASELINE.md)")
     args = ap.parse_args()
@@ -182,22 +185,35 @@ def main():
             sum_(col("l_extendedprice") * (1 - col("l_discount"))).alias("revenue"),
             count("*").alias("lines"))
 
-    def step(i):
-        r1 = q6(i).collect()
-        p1 = getattr(backend, "last_path", "native")
-        r2 = q3(i).collect()
-        p2 = getattr(backend, "last_path", "native")
-        if on_gpu and (p1 != "native" or p2 != "native"):
-            raise RuntimeError(f"query fell back to host: {backend.fallback_reason}")
-        return r1, r2
+    def submit(i):
+        """One step = one Q6 + one Q3, each planned and submitted through the full engine."""
+        return q6(i).collect_async(), q3(i).collect_async()
+
+    def finish(fs):
+        out = tuple(f.result() for f in fs)
+        if on_gpu and any(f.path != "native" for f in fs):
+            raise RuntimeError(f"query fell back to host: {[f.reason for f in fs]}")
+        return out
+
+    def run_steps(idx):
+        """Steps ``idx`` with up to ``args.inflight`` steps submitted ahead of the one being
+        finished: the host plans and submits step i+1 while the device runs step i."""
+        from collections import deque
+        pending, out = deque(), []
+        for i in idx:
+            pending.append(submit(i))
+            while len(pending) > max(args.inflight - 1, 0):
+                out.append(finish(pending.popleft()))
+        while pending:
+            out.append(finish(pending.popleft()))
+        return out
 
     def timed(mode):
         """Warm up, then time exactly ``args.steps`` steps bracketed by barrier + sync."""
         s.conf.set("spark.hyperspace.mi.index.placement", mode)
         off = rank * 100000 if mode == "replicated" else 0   # replicas serve distinct queries
         tl = time.perf_counter()
-        for i in range(args.warmup):
-            step(1000 + off + i)
+        run_steps(range(1000 + off, 1000 + off + args.warmup))
         sync()
         barrier()
         warm = time.perf_counter() - tl
@@ -213,9 +229,7 @@ def main():
         t_start = time.perf_counter()
         if prof is not None:
             prof.enable()
-        res = []
-        for i in range(args.steps):
-            res.append(step(off + i))
+        res = run_steps(range(off, off + args.steps))
         sync()
         barrier()
         el = time.perf_counter() - t_start
@@ -295,7 +309,7 @@ def main():
                           "device": args.device},
                "index_build_gbps": round(build_gbps, 3), "index_build_s": round(build_s, 3),
                "index_build": per_index, "latency": lat, "warmup_s": round(warm_s, 3),
-               "datagen_s": round(gen_s, 2), "crosscheck": check}
+               "datagen_s": round(gen_s, 2), "crosscheck": check, "inflight": args.inflight}
         if "sharded" in runs and final != "sharded":
             out["sharded"] = {"value": round(runs["sharded"]["qps"], 3),
                               "ms_per_step": round(runs["sharded"]["ms_per_step"], 3),

@@ -121,36 +121,46 @@ class GpuBackend:
         return d
 
     def collect(self, plan: X.SparkPlan) -> pa.Table:
+        return self.collect_async(plan).result()
+
+    def collect_async(self, plan: X.SparkPlan) -> "QueryFuture":
+        """Submit a query; ``.result()`` returns its table.  Fused aggregates (the indexed
+        filter / join hot paths) return before the device finishes, so a caller that keeps
+        several queries in flight overlaps host planning with device execution.  A shape the
+        device cannot run falls back to the host oracle (recorded in ``path``)."""
         t0 = time.perf_counter()
         TRACER.configure(self.session.conf)
         try:
             with stage("query"):
-                out = self._collect_native(plan)
-            self.last_path = "native"
-            self.fallback_reason = None
+                finish = self._collect_native(plan)
+            fut = QueryFuture(self, plan, finish, "native", None, t0)
         except Unsupported as e:
-            log.info("device executor fallback: %s", e)
-            self.last_path = "fallback"
-            self.fallback_reason = str(e)
-            out = self.cpu.collect(plan)
-        self.metrics["last_query_s"] = time.perf_counter() - t0
-        return out
+            fut = self._fallback(plan, e, t0)
+        self.last_path, self.fallback_reason = fut.path, fut.reason
+        return fut
 
-    def _collect_native(self, plan: X.SparkPlan) -> pa.Table:
+    def _fallback(self, plan, e, t0) -> "QueryFuture":
+        log.info("device executor fallback: %s", e)
+        out = self.cpu.collect(plan)
+        return QueryFuture(self, plan, lambda: out, "fallback", str(e), t0)
+
+    def _collect_native(self, plan: X.SparkPlan):
+        """``finish() -> pa.Table`` of a plan (aggregates deferred, row results computed now)."""
         limit = None
         if isinstance(plan, X.CollectLimitExec):
             limit = plan.n
             plan = plan.child
         agg = self._match_agg(plan)
         if agg is not None:
-            t = self._exec_agg(*agg)
+            finish = self._exec_agg(*agg)
         else:
             rel = self._rel(plan)
             t = self._to_arrow(rel, plan.output)
             t = self._gather_ranks(t)
-        if limit is not None:
-            t = t.slice(0, limit)
-        return t
+            finish = (lambda: t)
+        if limit is None:
+            return finish
+        return lambda: finish().slice(0, limit)
 
     # ------------------------------------------------------------------------------------------
     # Relations
@@ -613,7 +623,11 @@ class GpuBackend:
             return None
         return plan, partial.child
 
-    def _exec_agg(self, final: X.HashAggregateExec, child: X.SparkPlan) -> pa.Table:
+    def _exec_agg(self, final: X.HashAggregateExec, child: X.SparkPlan):
+        """Queue a fused aggregate and return ``finish() -> pa.Table``.  Nothing here waits on
+        the device: kernels, the cross-rank combine and the D2H of the tiny result block are
+        stream-ordered, so the host can plan and submit the next query while this one runs
+        (``collect_async``)."""
         fns = [fn for _, fn in X.agg_functions(final.aggregates)]
         if len(final.grouping) > 1:
             raise Unsupported("multi-column group by")
@@ -623,7 +637,6 @@ class GpuBackend:
         node = child
         while isinstance(node, X.ProjectExec) and all(isinstance(e, E.Attribute) for e in node.project_list):
             node = node.child
-        import torch
         self._groups_agreed = False
         if isinstance(node, X.SortMergeJoinExec):
             res = self._join_agg(node, fns, group)
@@ -632,17 +645,27 @@ class GpuBackend:
         sums, cnts, mins, maxs, G, gbase, gdict, gtype = res
         d = self._dist()
         A = len(fns) + 1  # + implicit count(*)
-        host = None
-        if d is not None and d.world > 1:
+        if isinstance(sums, _GraphPending):
+            fetch = sums.result
+        elif d is not None and d.world > 1:
             with stage("agg.combine_ranks"):
                 if group is not None and not self._groups_agreed:
                     sums, cnts, mins, maxs, G, gbase, gdict, gtype = self._agree_groups(
                         d, sums, cnts, mins, maxs, G, gbase, gdict, gtype, A)
-                host = d.combine_aggs_host(sums, cnts, mins, maxs)
-        if host is None:
-            with stage("agg.d2h"):
-                host = (sums, cnts, mins, maxs) if isinstance(sums, np.ndarray) else \
-                    K.agg_to_host(sums, cnts, mins, maxs)
+                fetch = d.combine_aggs_async(sums, cnts, mins, maxs)
+        elif isinstance(sums, np.ndarray):
+            host = (sums, cnts, mins, maxs)
+            fetch = (lambda: host)
+        else:
+            fetch = K.agg_to_host_async(sums, cnts, mins, maxs)
+
+        def finish() -> pa.Table:
+            with stage("agg.result"):
+                host = fetch()
+            return self._agg_table(final, fns, group, host, G, A, gbase, gdict, gtype)
+        return finish
+
+    def _agg_table(self, final, fns, group, host, G, A, gbase, gdict, gtype) -> pa.Table:
         s, c, mn, mx = (x.reshape(G, A) for x in host)
         rows = [g for g in range(G) if c[g, A - 1] > 0] if group is not None else [0]
         vals = {}
@@ -860,7 +883,8 @@ class GpuBackend:
         values.update({"num_groups": p.num_groups, "group_base": p.group_base})
         jit._fill_common(values, p.cols, [(i, p.preds[i]) for i in range(p.npreds)],
                          [p.aggs[i] for i in range(p.naggs)])
-        return g.run(range_bounds(lo, lo_incl, hi, hi_incl), k.args.pack(values))
+        slot = g.launch(range_bounds(lo, lo_incl, hi, hi_incl), k.args.pack(values))
+        return (_GraphPending(g, slot), None, None, None)
 
     def _compacts(self, descs: Dict[int, DeviceColumn]) -> Optional[dict]:
         """Compact HBM encodings (exec/encoding.py) the generated kernels read instead."""
@@ -1014,4 +1038,39 @@ def _eval_scalar(e, agg_val, attr_val):
     raise Unsupported(f"result expression {type(e).__name__}")
 
 
-__all__ = ["GpuBackend", "C"]
+class _GraphPending:
+    """A replayed scan pipeline whose result block is still in flight (exec/graphs.py)."""
+
+    def __init__(self, graph, slot):
+        self.graph, self.slot = graph, slot
+
+    def result(self):
+        return self.graph.result(self.slot)
+
+
+class QueryFuture:
+    """Handle of a submitted query (``GpuBackend.collect_async``)."""
+
+    def __init__(self, backend, plan, finish, path: str, reason, t0: float):
+        self.backend, self.plan = backend, plan
+        self._finish = finish
+        self.path, self.reason = path, reason
+        self._t0 = t0
+        self._value = None
+        self._done = False
+
+    def result(self) -> pa.Table:
+        if not self._done:
+            try:
+                self._value = self._finish()
+            except Unsupported as e:   # e.g. a result expression the device path cannot finish
+                f = self.backend._fallback(self.plan, e, self._t0)
+                self._value, self.path, self.reason = f.result(), f.path, f.reason
+                self.backend.last_path, self.backend.fallback_reason = self.path, self.reason
+            self._done = True
+            self._finish = None
+            self.backend.metrics["last_query_s"] = time.perf_counter() - self._t0
+        return self._value
+
+
+__all__ = ["GpuBackend", "QueryFuture", "C"]

@@ -54,7 +54,26 @@ class _Pinned:
             self.ptr = None
 
 
+class _Slot:
+    """One in-flight instance of a captured pipeline: its own pinned parameter and result
+    blocks (the graph's H2D reads the first and its D2H writes the second when the graph
+    EXECUTES, so a query queued behind another must not share them), its own graph, and the
+    event that marks its result ready."""
+
+    def __init__(self, params_bytes: int, out_bytes: int):
+        import torch
+        self.h_params = _Pinned(params_bytes)
+        self.h_out = _Pinned(out_bytes)
+        self.graph = None
+        self.event = torch.cuda.Event()
+        self.busy = False
+
+
 class ScanAggGraph:
+    # in-flight instances per captured shape: a pipelined query stream (exec/gpu.py
+    # collect_async) keeps a few replays of the same shape queued at once
+    RING = 4
+
     def __init__(self, kernel: jit.Kernel, kd: NL.ColDesc, bucket_off, nb: int, grid: int,
                  GA: int, shmem: int, device):
         import torch
@@ -65,7 +84,7 @@ class ScanAggGraph:
         self.nb, self.grid, self.GA, self.shmem = nb, grid, GA, shmem
         self.tile = jit.BLOCK * jit.SCAN_ITEMS
         self.args_size = 8 * len(kernel.args.slots)
-        self.h_params = _Pinned(PARAM_HEAD + self.args_size)
+        # device intermediates are shared: replays on one stream execute in order
         self.d_params = torch.empty(PARAM_HEAD + self.args_size, dtype=torch.uint8, device=device)
         self.rstart = torch.empty(nb, dtype=torch.int64, device=device)
         self.rlen = torch.empty(nb, dtype=torch.int64, device=device)
@@ -73,15 +92,21 @@ class ScanAggGraph:
         self.tp = torch.empty(nb + 1, dtype=torch.int64, device=device)
         self.parts = jit._partials(grid, GA, device)
         self.out = K.agg_outputs(GA, device)
-        self.h_out = _Pinned(self.out[0].hs_buf.numel())
-        self.graph = None
+        self.slots = [_Slot(PARAM_HEAD + self.args_size, self.out[0].hs_buf.numel())
+                      for _ in range(self.RING)]
+        self._next = 0
+        self._warm = False
         self.replays = 0
 
-    def _enqueue(self, stream: int) -> None:
+    @property
+    def graph(self):
+        return self.slots[0].graph
+
+    def _enqueue(self, slot: _Slot, stream: int) -> None:
         L = jit.runtime()
         K = NL.lib()
-        NL.check(L.hs_memcpy_async(self.d_params.data_ptr(), self.h_params.ptr,
-                                   self.h_params.nbytes, 1, stream), "param H2D")
+        NL.check(L.hs_memcpy_async(self.d_params.data_ptr(), slot.h_params.ptr,
+                                   slot.h_params.nbytes, 1, stream), "param H2D")
         NL.check(K.hs_range_search_dev(C.byref(self.kd), NL.ptr(self.bucket_off), None, self.nb,
                                        self.d_params.data_ptr(), NL.ptr(self.rstart),
                                        NL.ptr(self.rlen), NL.ptr(self.rbk), stream),
@@ -95,7 +120,7 @@ class ScanAggGraph:
         NL.check(K.hs_agg_final(NL.ptr(p[0]), NL.ptr(p[1]), NL.ptr(p[2]), NL.ptr(p[3]),
                                 self.grid, self.GA, NL.ptr(o[0]), NL.ptr(o[1]), NL.ptr(o[2]),
                                 NL.ptr(o[3]), stream), "hs_agg_final")
-        NL.check(L.hs_memcpy_async(self.h_out.ptr, o[0].hs_buf.data_ptr(), self.h_out.nbytes, 2,
+        NL.check(L.hs_memcpy_async(slot.h_out.ptr, o[0].hs_buf.data_ptr(), slot.h_out.nbytes, 2,
                                    stream), "result D2H")
 
     def values_template(self) -> dict:
@@ -104,35 +129,49 @@ class ScanAggGraph:
                 "psum": self.parts[0].data_ptr(), "pcnt": self.parts[1].data_ptr(),
                 "pmin": self.parts[2].data_ptr(), "pmax": self.parts[3].data_ptr()}
 
-    def run(self, bounds: Tuple[int, int, int, int, int, int], args_block: bytes):
-        """(sum, count, min, max) numpy arrays for one query."""
+    def launch(self, bounds: Tuple[int, int, int, int, int, int], args_block: bytes) -> _Slot:
+        """Queue one query on the current stream and return its slot; ``result(slot)`` waits.
+        A slot still in flight from an earlier launch is waited for first (back-pressure)."""
         import torch
-        hp = self.h_params.view()
+        slot = self.slots[self._next]
+        self._next = (self._next + 1) % len(self.slots)
+        if slot.busy:
+            slot.event.synchronize()
+        hp = slot.h_params.view()
         hp[:48] = np.frombuffer(struct.pack("<6q", *bounds), dtype=np.uint8)
         hp[PARAM_HEAD:PARAM_HEAD + len(args_block)] = np.frombuffer(args_block, dtype=np.uint8)
         cur = torch.cuda.current_stream()
-        if self.graph is None:
-            self._enqueue(cur.cuda_stream)         # eager first run (loads the module)
-            cur.synchronize()
-            res = self._results()
+        eager = not self._warm
+        if eager:
+            self._enqueue(slot, cur.cuda_stream)   # first run of the shape: eager (loads the module)
+            self._warm = True
+        if slot.graph is None:
             g = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream()
             side.wait_stream(cur)
             with torch.cuda.graph(g, stream=side):
-                self._enqueue(torch.cuda.current_stream().cuda_stream)
+                self._enqueue(slot, torch.cuda.current_stream().cuda_stream)
             cur.wait_stream(side)
-            self.graph = g
-            return res
-        self.graph.replay()
-        cur.synchronize()
-        self.replays += 1
-        return self._results()
+            slot.graph = g
+        if not eager:
+            slot.graph.replay()
+            self.replays += 1
+        slot.event.record(cur)
+        slot.busy = True
+        return slot
 
-    def _results(self):
-        h = self.h_out.view()
+    def result(self, slot: _Slot):
+        """(sum, count, min, max) numpy arrays of the query launched into ``slot``."""
+        slot.event.synchronize()
+        slot.busy = False
+        h = slot.h_out.view()
         n = 8 * self.GA
         return (h[0:n].view(np.float64).copy(), h[n:2 * n].view(np.int64).copy(),
                 h[2 * n:3 * n].view(np.float64).copy(), h[3 * n:4 * n].view(np.float64).copy())
+
+    def run(self, bounds: Tuple[int, int, int, int, int, int], args_block: bytes):
+        """(sum, count, min, max) numpy arrays for one query (launch + wait)."""
+        return self.result(self.launch(bounds, args_block))
 
 
 class GraphCache:

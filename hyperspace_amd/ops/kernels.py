@@ -255,6 +255,27 @@ def agg_to_host(sums, cnts, mins, maxs):
             h[3 * n:4 * n].view(np.float64))
 
 
+def agg_to_host_async(sums, cnts, mins, maxs):
+    """Queue the D2H of the four aggregate outputs into pinned memory and return ``fetch()``,
+    which waits for that copy only (not for the whole device) and returns numpy views."""
+    torch = _torch()
+    buf = getattr(sums, "hs_buf", None)
+    if buf is None or buf.numel() != 32 * sums.numel():
+        buf = torch.cat([x.contiguous().view(torch.uint8) for x in (sums, cnts, mins, maxs)])
+    h = torch.empty(buf.numel(), dtype=torch.uint8, pin_memory=True)
+    h.copy_(buf, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    n = sums.numel() * 8
+
+    def fetch():
+        ev.synchronize()
+        a = h.numpy()
+        return (a[0:n].view(np.float64), a[n:2 * n].view(np.int64),
+                a[2 * n:3 * n].view(np.float64), a[3 * n:4 * n].view(np.float64))
+    return fetch
+
+
 def scan_agg(params: NL.ScanParams, rstart, rlen, tile_prefix, grid: int = None):
     """Returns (sum f64 [GA], count i64 [GA], min f64 [GA], max f64 [GA]) device tensors."""
     torch = _torch()

@@ -104,11 +104,17 @@ class DistContext:
         return sums, cnts, mins, maxs
 
     def combine_aggs_host(self, sums, cnts, mins, maxs):
+        """``combine_aggs_async(...)()``: the combined partials as numpy arrays."""
+        return self.combine_aggs_async(sums, cnts, mins, maxs)()
+
+    def combine_aggs_async(self, sums, cnts, mins, maxs):
         """Cross-rank combine of partial aggregates in ONE collective: the four [GA] partials
         (already one contiguous device block when they come from the kernels' output buffer)
-        are all-gathered as raw bytes, copied to the host once, and reduced there in rank order
-        — deterministic sums, and one small RCCL call instead of four all-reduces plus a D2H.
-        Returns numpy (sum f64, count i64, min f64, max f64)."""
+        are all-gathered as raw bytes and copied to pinned host memory, all stream-ordered;
+        the returned ``fetch()`` waits for that copy and reduces in rank order on the host —
+        deterministic sums, one small RCCL call instead of four all-reduces plus a D2H, and
+        nothing blocks the host before the caller asks for the result.
+        ``fetch()`` returns numpy (sum f64, count i64, min f64, max f64)."""
         import numpy as np
         import torch
         import torch.distributed as dist
@@ -124,17 +130,25 @@ class DistContext:
             packed = packed.to(self.device, non_blocking=True)
             out = torch.empty(self.world * packed.numel(), dtype=torch.uint8, device=self.device)
             dist.all_gather_into_tensor(out, packed)
-            h = out.cpu().numpy()
+            h = torch.empty(out.numel(), dtype=torch.uint8, pin_memory=True)
+            h.copy_(out, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
         else:
             parts = [torch.empty_like(packed, device="cpu") for _ in range(self.world)]
             dist.all_gather(parts, packed.cpu())
-            h = torch.cat(parts).numpy()
-        h = h.reshape(self.world, 4, GA * 8)
-        s = h[:, 0].copy().view(np.float64).sum(axis=0)
-        c = h[:, 1].copy().view(np.int64).sum(axis=0)
-        mn = h[:, 2].copy().view(np.float64).min(axis=0)
-        mx = h[:, 3].copy().view(np.float64).max(axis=0)
-        return s, c, mn, mx
+            h, ev = torch.cat(parts), None
+
+        def fetch():
+            if ev is not None:
+                ev.synchronize()
+            x = h.numpy().reshape(self.world, 4, GA * 8)
+            s = x[:, 0].copy().view(np.float64).sum(axis=0)
+            c = x[:, 1].copy().view(np.int64).sum(axis=0)
+            mn = x[:, 2].copy().view(np.float64).min(axis=0)
+            mx = x[:, 3].copy().view(np.float64).max(axis=0)
+            return s, c, mn, mx
+        return fetch
 
     def all_reduce_max_float(self, x: float) -> float:
         import torch

@@ -224,10 +224,13 @@ class DataFrame:
     toArrow = to_arrow
 
     def collect(self) -> List[Row]:
-        t = self.to_arrow()
-        names = t.column_names
-        cols = [c.to_pylist() for c in t.columns]
-        return [Row(vals, names) for vals in zip(*cols)] if cols else []
+        return _rows(self.to_arrow())
+
+    def collect_async(self) -> "RowsFuture":
+        """Submit this query and return at once; ``.result()`` gives ``collect()``'s rows.
+        Keeping several queries in flight lets the MI355X executor run one query's kernels
+        while the host plans the next (``GpuBackend.collect_async``)."""
+        return RowsFuture(self.queryExecution.to_arrow_async())
 
     def count(self) -> int:
         return self.to_arrow().num_rows
@@ -361,3 +364,27 @@ def show_string(t: pa.Table, truncate: bool = True) -> str:
         lines.append("|" + "|".join(v.rjust(w) for v, w in zip(r, widths)) + "|")
     lines.append(sep)
     return "\n".join(lines) + "\n"
+
+
+def _rows(t: pa.Table) -> List[Row]:
+    names = t.column_names
+    cols = [c.to_pylist() for c in t.columns]
+    return [Row(vals, names) for vals in zip(*cols)] if cols else []
+
+
+class RowsFuture:
+    """Pending ``collect()`` of a submitted query; ``path`` is the executor path that ran."""
+
+    def __init__(self, fut):
+        self._fut = fut
+
+    @property
+    def path(self) -> str:
+        return self._fut.path
+
+    @property
+    def reason(self):
+        return self._fut.reason
+
+    def result(self) -> List[Row]:
+        return _rows(self._fut.result())

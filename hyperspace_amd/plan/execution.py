@@ -47,6 +47,24 @@ class QueryExecution:
         backend = self.session.backend()
         return backend.collect(self.executed_plan)
 
+    def to_arrow_async(self):
+        """Plan now, execute asynchronously: an object whose ``result()`` is the table.  The
+        device backend returns before its kernels finish (``GpuBackend.collect_async``); the
+        host backend runs the query here."""
+        backend = self.session.backend()
+        plan = self.executed_plan
+        if hasattr(backend, "collect_async"):
+            return backend.collect_async(plan)
+        return _Done(backend.collect(plan), getattr(backend, "last_path", "host"))
+
+
+class _Done:
+    def __init__(self, table: pa.Table, path: str):
+        self._t, self.path, self.reason = table, path, None
+
+    def result(self) -> pa.Table:
+        return self._t
+
     def explain_string(self, extended: bool = False) -> str:
         parts = []
         if extended:
