@@ -124,6 +124,10 @@ def main():
                       "spark.hyperspace.mi.execution.device": args.device,
                       "spark.hyperspace.mi.index.codec": args.codec},
                 warehouse_dir=os.path.join(args.data_dir, "wh"))
+    # extra session conf for sweeps: HS_BENCH_CONF="key=value,key=value"
+    for kv in filter(None, os.environ.get("HS_BENCH_CONF", "").split(",")):
+        k, v = kv.split("=", 1)
+        s.conf.set(k.strip(), v.strip())
     s.dist = dist
     hs = Hyperspace(s)
     li = s.read.parquet(os.path.join(data, "lineitem"))

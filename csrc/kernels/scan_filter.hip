@@ -100,16 +100,21 @@ __global__ void hs_range_search_dev_kernel(ColDesc key, const int64_t* __restric
 }
 
 // ranges -> tile prefix (single block, R arbitrary): tile_prefix[R] = total tiles.
+// rstart != nullptr: each range is widened down to a multiple of `align` rows first (the tiling of
+// the vectorized generated kernels, which load `align` consecutive rows per thread).
 __global__ __launch_bounds__(1024) void hs_ranges_to_tiles_kernel(const int64_t* __restrict__ rlen,
                                                                   int R, int tile_rows,
-                                                                  int64_t* __restrict__ tile_prefix) {
+                                                                  int64_t* __restrict__ tile_prefix,
+                                                                  const int64_t* __restrict__ rstart,
+                                                                  int64_t align) {
   __shared__ int64_t wsum[16];
   __shared__ int64_t carry;
   if (threadIdx.x == 0) carry = 0;
   __syncthreads();
   for (int base = 0; base < R; base += blockDim.x) {
     const int i = base + threadIdx.x;
-    const int64_t t = i < R ? (rlen[i] + tile_rows - 1) / tile_rows : 0;
+    const int64_t len = i < R ? rlen[i] + (rstart != nullptr ? (rstart[i] & (align - 1)) : 0) : 0;
+    const int64_t t = (len + tile_rows - 1) / tile_rows;
     int64_t x = t;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int off = 1; off < 64; off <<= 1) {
@@ -354,7 +359,14 @@ int hs_range_search(const ColDesc* key, const int64_t* bucket_off, const int32_t
 int hs_ranges_to_tiles(const int64_t* rlen, int R, int tile_rows, int64_t* tile_prefix,
                        void* stream) {
   hipLaunchKernelGGL(hs_ranges_to_tiles_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rlen,
-                     R, tile_rows, tile_prefix);
+                     R, tile_rows, tile_prefix, (const int64_t*)nullptr, (int64_t)1);
+  return (int)hipGetLastError();
+}
+
+int hs_ranges_to_tiles_aligned(const int64_t* rstart, const int64_t* rlen, int R, int tile_rows,
+                               int64_t align, int64_t* tile_prefix, void* stream) {
+  hipLaunchKernelGGL(hs_ranges_to_tiles_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rlen,
+                     R, tile_rows, tile_prefix, rstart, align);
   return (int)hipGetLastError();
 }
 

@@ -844,12 +844,14 @@ class GpuBackend:
         elif graph:
             with stage("scan.graph"):
                 out = self._scan_agg_graph(r, p, spec,
-                                           p.naggs * (p.num_groups if p.group_col >= 0 else 1))
+                                           p.naggs * (p.num_groups if p.group_col >= 0 else 1),
+                                           descs)
         else:
             with stage("scan.agg_kernel"):
                 tp = K.ranges_to_tiles(rlen)
                 if HyperspaceConf.codegen_enabled(self.session.conf):
-                    out = jit.scan_agg(p, rstart, rlen, tp, self._compacts(descs))
+                    out = jit.scan_agg(p, rstart, rlen, tp, self._compacts(descs),
+                                       nrows=r.table.num_rows)
                 else:
                     out = K.scan_agg(p, rstart, rlen, tp)
         return (*out, G, gbase, gdict, gtype)
@@ -864,27 +866,29 @@ class GpuBackend:
         if d is not None and d.world > 1:
             return False
         conf = self.session.conf
-        return (HyperspaceConf.codegen_enabled(conf) and HyperspaceConf.hipgraph_enabled(conf)
-                and self._compacts(descs) is None)
+        return HyperspaceConf.codegen_enabled(conf) and HyperspaceConf.hipgraph_enabled(conf)
 
-    def _scan_agg_graph(self, r: DRel, p: NL.ScanParams, spec, GA: int):
+    def _scan_agg_graph(self, r: DRel, p: NL.ScanParams, spec, GA: int, descs=None):
         kc, lo, lo_incl, hi, hi_incl, _ = spec
         t = r.table
         nb = t.num_buckets
         grid = jit.SCAN_GRID or NL.lib().hs_scan_grid()
-        shape = jit.scan_agg_shape(p)
-        k = jit.kernel_for(shape, lambda: jit.gen_scan_agg(p))
+        compacts = self._compacts(descs or {})
+        vec = jit.scan_vec(p, compacts, t.num_rows)
+        shape = jit.scan_agg_shape(p, compacts, vec)
+        k = jit.kernel_for(shape, lambda: jit.gen_scan_agg(p, compacts, vec))
         key = (shape, kc.data.data_ptr(), kc.valid.data_ptr() if kc.valid is not None else 0,
                kc.hs_type, t.bucket_offsets.data_ptr(), nb, grid, GA)
         shmem = GA * 32 if p.group_col >= 0 else 0
         g = self.graphs.get(key, lambda: ScanAggGraph(k, kc.desc(), t.bucket_offsets, nb, grid,
-                                                      GA, shmem, self.device))
+                                                      GA, shmem, self.device, vec))
         values = g.values_template()
-        values.update({"num_groups": p.num_groups, "group_base": p.group_base})
+        values.update({"num_groups": p.num_groups, "group_base": p.group_base,
+                       "nrows": t.num_rows})
         jit._fill_common(values, p.cols, [(i, p.preds[i]) for i in range(p.npreds)],
-                         [p.aggs[i] for i in range(p.naggs)])
-        slot = g.launch(range_bounds(lo, lo_incl, hi, hi_incl), k.args.pack(values))
-        return (_GraphPending(g, slot), None, None, None)
+                         [p.aggs[i] for i in range(p.naggs)], compacts)
+        handle = g.launch(range_bounds(lo, lo_incl, hi, hi_incl), k.args.pack(values))
+        return (_GraphPending(g, handle), None, None, None)
 
     def _compacts(self, descs: Dict[int, DeviceColumn]) -> Optional[dict]:
         """Compact HBM encodings (exec/encoding.py) the generated kernels read instead."""
@@ -979,7 +983,8 @@ class GpuBackend:
                 jidx = join_index.get_join_index(jp, left.table, right.table, left.col(lk),
                                                  right.col(rk), fs, fl, fb)
             with stage("join.index_agg_kernel"):
-                return jit.join_index_agg(jp, rstart, rlen, jidx, self._compacts(descs))
+                return jit.join_index_agg(jp, rstart, rlen, jidx, self._compacts(descs),
+                                          nrows=left.table.num_rows)
         with stage("join.agg_kernel"):
             if HyperspaceConf.codegen_enabled(self.session.conf):
                 fr = getattr(left.table, "_full_ranges", None)
@@ -1041,11 +1046,11 @@ def _eval_scalar(e, agg_val, attr_val):
 class _GraphPending:
     """A replayed scan pipeline whose result block is still in flight (exec/graphs.py)."""
 
-    def __init__(self, graph, slot):
-        self.graph, self.slot = graph, slot
+    def __init__(self, graph, handle):
+        self.graph, self.handle = graph, handle
 
     def result(self):
-        return self.graph.result(self.slot)
+        return self.graph.result(self.handle)
 
 
 class QueryFuture:

@@ -66,7 +66,18 @@ class _Slot:
         self.h_out = _Pinned(out_bytes)
         self.graph = None
         self.event = torch.cuda.Event()
-        self.busy = False
+        self.current = None   # _Launch whose result the slot's h_out holds / will hold
+
+
+class _Launch:
+    """One query launched into a slot; ``value`` is filled when it is read (by the caller, or
+    by the next launch that needs the slot first)."""
+
+    __slots__ = ("slot", "value")
+
+    def __init__(self, slot: _Slot):
+        self.slot = slot
+        self.value = None
 
 
 class ScanAggGraph:
@@ -75,14 +86,15 @@ class ScanAggGraph:
     RING = 4
 
     def __init__(self, kernel: jit.Kernel, kd: NL.ColDesc, bucket_off, nb: int, grid: int,
-                 GA: int, shmem: int, device):
+                 GA: int, shmem: int, device, vec: int = 0):
         import torch
         from ..ops import kernels as K
         self.kernel = kernel.by_pointer()
         self.kd = kd
         self.bucket_off = bucket_off
         self.nb, self.grid, self.GA, self.shmem = nb, grid, GA, shmem
-        self.tile = jit.BLOCK * jit.SCAN_ITEMS
+        self.vec = vec   # rows per thread of a vectorized kernel (tiles over aligned ranges)
+        self.tile = jit.BLOCK * (vec or jit.SCAN_ITEMS)
         self.args_size = 8 * len(kernel.args.slots)
         # device intermediates are shared: replays on one stream execute in order
         self.d_params = torch.empty(PARAM_HEAD + self.args_size, dtype=torch.uint8, device=device)
@@ -111,8 +123,13 @@ class ScanAggGraph:
                                        self.d_params.data_ptr(), NL.ptr(self.rstart),
                                        NL.ptr(self.rlen), NL.ptr(self.rbk), stream),
                  "hs_range_search_dev")
-        NL.check(K.hs_ranges_to_tiles(NL.ptr(self.rlen), self.nb, self.tile, NL.ptr(self.tp),
-                                      stream), "hs_ranges_to_tiles")
+        if self.vec:
+            NL.check(K.hs_ranges_to_tiles_aligned(NL.ptr(self.rstart), NL.ptr(self.rlen), self.nb,
+                                                  self.tile, self.vec, NL.ptr(self.tp), stream),
+                     "hs_ranges_to_tiles_aligned")
+        else:
+            NL.check(K.hs_ranges_to_tiles(NL.ptr(self.rlen), self.nb, self.tile,
+                                          NL.ptr(self.tp), stream), "hs_ranges_to_tiles")
         self.kernel.launch_ptr(self.grid, self.d_params.data_ptr() + PARAM_HEAD, stream,
                                self.shmem)
         p = self.parts
@@ -129,14 +146,16 @@ class ScanAggGraph:
                 "psum": self.parts[0].data_ptr(), "pcnt": self.parts[1].data_ptr(),
                 "pmin": self.parts[2].data_ptr(), "pmax": self.parts[3].data_ptr()}
 
-    def launch(self, bounds: Tuple[int, int, int, int, int, int], args_block: bytes) -> _Slot:
-        """Queue one query on the current stream and return its slot; ``result(slot)`` waits.
-        A slot still in flight from an earlier launch is waited for first (back-pressure)."""
+    def launch(self, bounds: Tuple[int, int, int, int, int, int], args_block: bytes) -> _Launch:
+        """Queue one query on the current stream; ``result(handle)`` waits for it.  A slot
+        still holding an unread earlier result is drained first: wait for it and keep its
+        result on the earlier handle (back-pressure, no lost results)."""
         import torch
         slot = self.slots[self._next]
         self._next = (self._next + 1) % len(self.slots)
-        if slot.busy:
-            slot.event.synchronize()
+        prev = slot.current
+        if prev is not None and prev.value is None:
+            prev.value = self._read(slot)
         hp = slot.h_params.view()
         hp[:48] = np.frombuffer(struct.pack("<6q", *bounds), dtype=np.uint8)
         hp[PARAM_HEAD:PARAM_HEAD + len(args_block)] = np.frombuffer(args_block, dtype=np.uint8)
@@ -157,13 +176,18 @@ class ScanAggGraph:
             slot.graph.replay()
             self.replays += 1
         slot.event.record(cur)
-        slot.busy = True
-        return slot
+        h = _Launch(slot)
+        slot.current = h
+        return h
 
-    def result(self, slot: _Slot):
-        """(sum, count, min, max) numpy arrays of the query launched into ``slot``."""
+    def result(self, h: _Launch):
+        """(sum, count, min, max) numpy arrays of the launched query ``h``."""
+        if h.value is None:
+            h.value = self._read(h.slot)
+        return h.value
+
+    def _read(self, slot: _Slot):
         slot.event.synchronize()
-        slot.busy = False
         h = slot.h_out.view()
         n = 8 * self.GA
         return (h[0:n].view(np.float64).copy(), h[n:2 * n].view(np.int64).copy(),

@@ -51,6 +51,11 @@ JOIN_STAGE_RIGHT = os.environ.get("HS_JIT_JOIN_STAGE_RIGHT", "1") == "1"
 SCAN_EAGER = os.environ.get("HS_JIT_SCAN_EAGER", "0") == "1"
 # rows per thread of the join-index kernel (phase-major: each phase's loads of all items in flight)
 JI_ITEMS = int(os.environ.get("HS_JIT_JI_ITEMS", "4"))
+# > 0: each thread of the join-index kernel owns JI_VEC consecutive rows and loads the streamed
+# left columns (join index, predicate columns) as aligned vectors (dwordx4 for 4 int32 rows)
+JI_VEC = int(os.environ.get("HS_JIT_JI_VEC", "8"))
+# > 0: rows per thread of the vectorized scan kernel (aligned vector loads of predicate columns)
+SCAN_VEC = int(os.environ.get("HS_JIT_SCAN_VEC", "8"))
 # software-pipeline the join's tile loop (next tile's batch loads overlap this tile's work)
 JOIN_PIPELINE = os.environ.get("HS_JIT_JOIN_PIPELINE", "1") == "1"
 # direct-address LDS table for dense integer key spans (one verified lookup instead of a
@@ -213,6 +218,24 @@ __device__ __forceinline__ bool in_set(const i64* s, int n, i64 x) {
 __device__ __forceinline__ bool bit_test(const u64* w, i64 nbits, i64 x) {
   return x >= 0 && x < nbits && ((w[x >> 6] >> (x & 63)) & 1ull);
 }
+// V consecutive elements starting at an index that is a multiple of V (so the address is
+// aligned to V * sizeof(T) for a 16-byte aligned base): one dwordx4 per 16 bytes
+template <typename T, int V>
+__device__ __forceinline__ void vload(const T* __restrict__ p, long long i, T (&x)[V]) {
+  constexpr int B = (int)sizeof(T) * V;
+  if constexpr (B % 16 == 0) {
+    const uint4* q = reinterpret_cast<const uint4*>(p + i);
+#pragma unroll
+    for (int k = 0; k < B / 16; ++k) reinterpret_cast<uint4*>(x)[k] = q[k];
+  } else if constexpr (B == 8) {
+    *reinterpret_cast<uint2*>(x) = *reinterpret_cast<const uint2*>(p + i);
+  } else if constexpr (B == 4) {
+    *reinterpret_cast<unsigned*>(x) = *reinterpret_cast<const unsigned*>(p + i);
+  } else {
+#pragma unroll
+    for (int k = 0; k < V; ++k) x[k] = p[i + k];
+  }
+}
 __device__ __forceinline__ void lds_min(double* p, double v) {
   u64* a = (u64*)p; u64 old = *a, as;
   do { as = old; if (__longlong_as_double((i64)as) <= v) break;
@@ -254,8 +277,16 @@ class _Gen:
 
     def value(self, slot: int, row: str) -> str:
         """Logical value of column ``slot`` at ``row`` (decodes compact columns in registers)."""
+        return self.decode(slot, f"{self.ptr(slot)}[{row}]")
+
+    def raw_type(self, slot: int) -> str:
+        """C type of the stored element (the code type for compact columns)."""
         t, _, enc = self.cols[slot]
-        raw = f"{self.ptr(slot)}[{row}]"
+        return _CODE_T[enc[0]] if enc else _CTYPE[t]
+
+    def decode(self, slot: int, raw: str) -> str:
+        """Logical value of a stored element expression ``raw`` of column ``slot``."""
+        t, _, enc = self.cols[slot]
         if not enc:
             return raw
         ct = _CTYPE[t]
@@ -466,16 +497,16 @@ def _col_specs(p, compacts) -> Dict[int, tuple]:
     return out
 
 
-def scan_agg_shape(p: NL.ScanParams, compacts=None) -> tuple:
+def scan_agg_shape(p: NL.ScanParams, compacts=None, vec: int = 0) -> tuple:
     cols = tuple(sorted(_col_specs(p, compacts).items()))
     preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
                    p.preds[k].group) for k in range(p.npreds))
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
-    return ("scan_agg", cols, preds, aggs, p.group_col, SCAN_ITEMS, SCAN_EAGER)
+    return ("scan_agg", cols, preds, aggs, p.group_col, SCAN_ITEMS, SCAN_EAGER, vec)
 
 
-def gen_scan_agg(p: NL.ScanParams, compacts=None) -> Kernel:
+def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
     """Filter + aggregate over row ranges, phase-major over the SCAN_ITEMS rows of each thread
     and branch-free: (1) the predicate columns of every item are loaded together; (2) the
     aggregate inputs (and group column) of every item, where rows that failed the predicates
@@ -499,8 +530,10 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None) -> Kernel:
     if SCAN_EAGER:
         pslots, aslots = pslots + aslots, []
     allslots = pslots + aslots
-    NI = SCAN_ITEMS
+    NI = vec or SCAN_ITEMS
     T = BLOCK * NI
+    if vec:
+        args.add("q", "nrows", "long long")
     b: List[str] = []
     b += _acc_decls(aggs, grouped, args)
     if grouped:
@@ -516,17 +549,21 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None) -> Kernel:
           "    r = lo; }",
           "  for (i64 t = t0; t < t1; ++t) {",
           "    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;",
-          f"    const i64 off = (t - a.tile_prefix[r]) * {T};",
-          "    const i64 tb0 = a.rstart[r] + off;",
-          f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};"]
+          f"    const i64 off = (t - a.tile_prefix[r]) * {T};"]
     ind = "    "
-    for it in range(NI):
-        b += [f"{ind}const bool act{it} = {it * BLOCK} + (i64)threadIdx.x < rows;",
-              f"{ind}const i64 row{it} = tb0 + (act{it} ? {it * BLOCK} + (i64)threadIdx.x : 0);"]
-    for it in range(NI):
-        g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"))
-        for s in pslots:
-            _uload(g1, s, it, b, ind)
+    if vec:
+        _vec_rows(b, NI, ind)
+        _vec_load_slots(b, _Gen(args, cols, NL.MAX_COLS, ("row0", "row0")), pslots, NI, ind)
+    else:
+        b += ["    const i64 tb0 = a.rstart[r] + off;",
+              f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};"]
+        for it in range(NI):
+            b += [f"{ind}const bool act{it} = {it * BLOCK} + (i64)threadIdx.x < rows;",
+                  f"{ind}const i64 row{it} = tb0 + (act{it} ? {it * BLOCK} + (i64)threadIdx.x : 0);"]
+        for it in range(NI):
+            g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"))
+            for s in pslots:
+                _uload(g1, s, it, b, ind)
     for it in range(NI):
         g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"))
         b.append(f"{ind}bool pass{it} = act{it} && {_rename(g1.cnf(preds), allslots, it)};")
@@ -948,13 +985,13 @@ def join_agg_values(p: NL.JoinParams, tile_prefix, spans, parts,
 # ------------------------------------------------------------------------------------------------
 # Join through a cached join index (exec/join_index.py)
 # ------------------------------------------------------------------------------------------------
-def join_index_agg_shape(p: NL.JoinParams, compacts=None) -> tuple:
+def join_index_agg_shape(p: NL.JoinParams, compacts=None, vec: int = 0) -> tuple:
     cols = tuple(sorted(_col_specs(p, compacts).items()))
     preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
                    p.preds[k].group) for k in range(p.npreds))
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
-    return ("join_index_agg", cols, preds, p.nlp, aggs, p.group_col, JI_ITEMS, BLOCK)
+    return ("join_index_agg", cols, preds, p.nlp, aggs, p.group_col, JI_ITEMS, vec, BLOCK)
 
 
 def _uload(gen: _Gen, slot: int, it: int, out: List[str], ind: str) -> None:
@@ -968,7 +1005,45 @@ def _uload(gen: _Gen, slot: int, it: int, out: List[str], ind: str) -> None:
         out.append(f"{ind}const bool n{slot}_{it} = {gen.vptr(slot)}[{r}] != 0;")
 
 
-def gen_join_index_agg(p: NL.JoinParams, compacts=None) -> Kernel:
+def _vec_rows(b: List[str], NI: int, ind: str) -> None:
+    """Row mapping of a vectorized tile: the tile covers range r from its start rounded down to
+    a multiple of NI, each thread owns NI consecutive rows at an aligned index ``g0``; rows
+    outside [rs, re) are inactive and point at an in-range row."""
+    b += ["    const i64 rs = a.rstart[r], re = rs + a.rlen[r];",
+          f"    const i64 tb0 = (rs & ~(i64){NI - 1}) + off;",
+          f"    const i64 g0 = tb0 + (i64)threadIdx.x * {NI};",
+          f"    const bool vok = g0 + {NI} <= a.nrows;"]
+    for it in range(NI):
+        b += [f"{ind}const bool act{it} = g0 + {it} >= rs && g0 + {it} < re;",
+              f"{ind}const i64 row{it} = act{it} ? g0 + {it} : tb0 > rs ? tb0 : rs;"]
+
+
+def _vec_load_slots(b: List[str], gen: "_Gen", slots, NI: int, ind: str, extra=()) -> None:
+    """Aligned vector loads of NI consecutive rows for every column in ``slots`` (plus
+    ``extra`` = (name, C type, pointer) raw arrays), then per-item registers x<s>_<k> /
+    n<s>_<k>.  The last partial vector of a column (``!vok``) loads element-wise."""
+    loads = list(extra) + [(f"x{s}", gen.raw_type(s), gen.ptr(s)) for s in slots]
+    for s in slots:
+        if gen.cols[s][1]:
+            loads.append((f"n{s}", "unsigned char", gen.vptr(s)))
+    for name, ct, ptr in loads:
+        b.append(f"{ind}{ct} {name}v[{NI}];")
+        b.append(f"{ind}if (vok) vload<{ct}, {NI}>({ptr}, g0, {name}v);")
+        b.append(f"{ind}else {{ " + " ".join(
+            f"{name}v[{k}] = act{k} ? {ptr}[g0 + {k}] : ({ct})0;" for k in range(NI)) + " }")
+    for it in range(NI):
+        for s in slots:
+            ct = _CTYPE[gen.cols[s][0]]
+            b.append(f"{ind}const {ct} x{s}_{it} = {gen.decode(s, f'x{s}v[{it}]')};")
+            if gen.cols[s][1]:
+                b.append(f"{ind}const bool n{s}_{it} = n{s}v[{it}] != 0;")
+
+
+def _vec_aligned_ptrs(ptrs) -> bool:
+    return all(int(x) % 16 == 0 for x in ptrs if x)
+
+
+def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0) -> Kernel:
     """Fused join + aggregate as a streaming scan of the left table's row ranges that reads
     ``jidx[row]`` — the matching right row from the cached join index (exec/join_index.py) — and
     gathers right-side columns there.
@@ -1002,8 +1077,10 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None) -> Kernel:
              if s not in first and s not in second]
     third = list(dict.fromkeys(third))
     allslots = first + second + third
-    NI = JI_ITEMS
+    NI = vec or JI_ITEMS
     T = BLOCK * NI
+    if vec:
+        args.add("q", "nrows", "long long")
     b: List[str] = []
     b += _acc_decls(aggs, grouped, args)
     if grouped:
@@ -1019,19 +1096,26 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None) -> Kernel:
           "    r = lo; }",
           "  for (i64 t = t0; t < t1; ++t) {",
           "    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;",
-          f"    const i64 off = (t - a.tile_prefix[r]) * {T};",
-          "    const i64 tb0 = a.rstart[r] + off;",
-          f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};"]
+          f"    const i64 off = (t - a.tile_prefix[r]) * {T};"]
     ind = "    "
-    # phase 1: join index + left predicate columns of every item
-    for it in range(NI):
-        b += [f"{ind}const bool act{it} = {it * BLOCK} + (i64)threadIdx.x < rows;",
-              f"{ind}const i64 row{it} = tb0 + (act{it} ? {it * BLOCK} + (i64)threadIdx.x : 0);"]
-    for it in range(NI):
-        b.append(f"{ind}const int jr{it} = a.jidx[row{it}];")
-        g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"))
-        for s in first:
-            _uload(g1, s, it, b, ind)
+    if vec:
+        _vec_rows(b, NI, ind)
+        g1 = _Gen(args, cols, split, ("row0", "row0"))
+        _vec_load_slots(b, g1, first, NI, ind, extra=[("jr", "int", "a.jidx")])
+        for it in range(NI):
+            b.append(f"{ind}const int jr{it} = act{it} ? jrv[{it}] : -1;")
+    else:
+        b += ["    const i64 tb0 = a.rstart[r] + off;",
+              f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};"]
+        for it in range(NI):
+            b += [f"{ind}const bool act{it} = {it * BLOCK} + (i64)threadIdx.x < rows;",
+                  f"{ind}const i64 row{it} = tb0 + (act{it} ? {it * BLOCK} + (i64)threadIdx.x : 0);"]
+        # phase 1: join index + left predicate columns of every item
+        for it in range(NI):
+            b.append(f"{ind}const int jr{it} = a.jidx[row{it}];")
+            g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"))
+            for s in first:
+                _uload(g1, s, it, b, ind)
     for it in range(NI):
         g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"))
         cond = _rename(g1.cnf(lpreds), allslots, it)
@@ -1075,16 +1159,34 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None) -> Kernel:
     return Kernel(src, "hs_jit_join_index_agg", args, lds)
 
 
-def join_index_agg(p: NL.JoinParams, rstart, rlen, jidx, compacts=None):
-    """Same outputs as ``join_agg``; ``jidx`` from ``join_index.get_join_index``."""
+def _vec_aligned(p: NL.JoinParams, compacts, jidx) -> bool:
+    """Vector loads need 16-byte aligned bases for every streamed left column."""
+    ptrs = [jidx.data_ptr()]
+    for s in _pred_slots([(k, p.preds[k]) for k in range(p.nlp)]):
+        c = (compacts or {}).get(s)
+        ptrs.append(c.codes.data_ptr() if c else p.cols[s].data)
+        if p.cols[s].valid:
+            ptrs.append(p.cols[s].valid)
+    return all(int(x) % 16 == 0 for x in ptrs)
+
+
+def join_index_agg(p: NL.JoinParams, rstart, rlen, jidx, compacts=None, nrows: int = 0):
+    """Same outputs as ``join_agg``; ``jidx`` from ``join_index.get_join_index``; ``nrows`` =
+    left table rows (vectorized loads stay inside the columns)."""
     from ..ops import kernels as K
-    tp = K.ranges_to_tiles(rlen, BLOCK * JI_ITEMS)
+    vec = JI_VEC if JI_VEC > 0 and _vec_aligned(p, compacts, jidx) else 0
+    if vec:
+        # tiles over the ranges widened down to a multiple of vec rows (the kernel masks them)
+        tp = K.ranges_to_tiles(rlen + (rstart & (vec - 1)), BLOCK * vec)
+    else:
+        tp = K.ranges_to_tiles(rlen, BLOCK * JI_ITEMS)
     grid = SCAN_GRID or NL.lib().hs_scan_grid()
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
-    k = kernel_for(join_index_agg_shape(p, compacts), lambda: gen_join_index_agg(p, compacts))
+    k = kernel_for(join_index_agg_shape(p, compacts, vec),
+                   lambda: gen_join_index_agg(p, compacts, vec))
     parts = _partials(grid, GA, rstart.device)
     v = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
-         "jidx": jidx.data_ptr(), "R": rstart.numel(), "psum": parts[0].data_ptr(),
+         "jidx": jidx.data_ptr(), "R": rstart.numel(), "nrows": nrows, "psum": parts[0].data_ptr(),
          "pcnt": parts[1].data_ptr(), "pmin": parts[2].data_ptr(), "pmax": parts[3].data_ptr(),
          "num_groups": p.num_groups, "group_base": p.group_base}
     _fill_common(v, p.cols, [(k_, p.preds[k_]) for k_ in range(p.npreds)],
@@ -1128,18 +1230,36 @@ def _final(parts, grid: int, GA: int, dev):
     return out
 
 
-def scan_agg(p: NL.ScanParams, rstart, rlen, tile_prefix=None, compacts=None):
+def scan_vec(p: NL.ScanParams, compacts=None, nrows: int = 0) -> int:
+    """Rows per thread of the vectorized scan kernel for this query (0 = strided kernel): the
+    predicate columns must have 16-byte aligned bases."""
+    if SCAN_VEC <= 0 or nrows <= 0:
+        return 0
+    ptrs = []
+    for s in _pred_slots([(k, p.preds[k]) for k in range(p.npreds)]):
+        c = (compacts or {}).get(s)
+        ptrs.append(c.codes.data_ptr() if c else p.cols[s].data)
+        ptrs.append(p.cols[s].valid)
+    return SCAN_VEC if _vec_aligned_ptrs(ptrs) else 0
+
+
+def scan_agg(p: NL.ScanParams, rstart, rlen, tile_prefix=None, compacts=None, nrows: int = 0):
     """``tile_prefix`` must use this kernel's tile (BLOCK * SCAN_ITEMS); None computes it.
-    ``compacts``: slot -> ``encoding.Compact`` read instead of the full-width column."""
+    ``compacts``: slot -> ``encoding.Compact`` read instead of the full-width column.
+    ``nrows``: rows of the scanned table (enables the vectorized kernel)."""
     from ..ops import kernels as K
-    if tile_prefix is None or BLOCK * SCAN_ITEMS != NL.lib().hs_scan_tile_rows():
+    vec = scan_vec(p, compacts, nrows)
+    if vec:
+        tile_prefix = K.ranges_to_tiles(rlen + (rstart & (vec - 1)), BLOCK * vec)
+    elif tile_prefix is None or BLOCK * SCAN_ITEMS != NL.lib().hs_scan_tile_rows():
         tile_prefix = K.ranges_to_tiles(rlen, BLOCK * SCAN_ITEMS)
     grid = SCAN_GRID or NL.lib().hs_scan_grid()
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
-    k = kernel_for(scan_agg_shape(p, compacts), lambda: gen_scan_agg(p, compacts))
+    k = kernel_for(scan_agg_shape(p, compacts, vec), lambda: gen_scan_agg(p, compacts, vec))
     parts = _partials(grid, GA, rstart.device)
-    k.launch(grid, scan_agg_values(p, rstart, rlen, tile_prefix, parts, compacts),
-             NL.stream_ptr(), GA * 32 if p.group_col >= 0 else 0)
+    v = scan_agg_values(p, rstart, rlen, tile_prefix, parts, compacts)
+    v["nrows"] = nrows
+    k.launch(grid, v, NL.stream_ptr(), GA * 32 if p.group_col >= 0 else 0)
     return _final(parts, grid, GA, rstart.device)
 
 

@@ -94,9 +94,10 @@ CODEGEN_ENABLED = "spark.hyperspace.mi.codegen.enabled"
 CODEGEN_ENABLED_DEFAULT = "true"
 # lossless frame-of-reference / decimal-scale compaction of HBM columns read by generated kernels
 HBM_COMPRESSION_ENABLED = "spark.hyperspace.mi.hbmCompression.enabled"
-# off by default: the fused kernels measured latency-bound, not bandwidth-bound, on MI355X
-# (profiles/microbench_join_r1*.jsonl), so narrower columns did not pay for the decode
-HBM_COMPRESSION_ENABLED_DEFAULT = "false"
+# on by default since the generated kernels load each thread's rows as aligned vectors
+# (jit.SCAN_VEC / JI_VEC): narrow codes then cut HBM bytes instead of only adding decode work
+# (SF100 Q6+Q3: 988 -> 1133 q/s, profiles/sweep_r1_compaction_vec.txt)
+HBM_COMPRESSION_ENABLED_DEFAULT = "true"
 # replay captured hipGraphs of the scan pipeline (exec/graphs.py)
 HIPGRAPH_ENABLED = "spark.hyperspace.mi.hipGraph.enabled"
 HIPGRAPH_ENABLED_DEFAULT = "true"

@@ -409,8 +409,14 @@ class IndexLogEntry(LogEntry):
     # -- accessors -------------------------------------------------------------------------------
     @property
     def schema(self):
+        """The index data schema (parsed once per schema string: rules ask on every query)."""
         from ..plan.types import schema_from_json
-        return schema_from_json(self.derived_dataset.schema_string)
+        ss = self.derived_dataset.schema_string
+        hit = self.__dict__.get("_schema_cache")
+        if hit is None or hit[0] != ss:
+            hit = (ss, schema_from_json(ss))
+            self.__dict__["_schema_cache"] = hit
+        return hit[1]
 
     @property
     def created(self) -> bool:

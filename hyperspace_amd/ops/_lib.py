@@ -140,6 +140,7 @@ def lib():
     _sig(L.hs_range_search, I, P, P, P, I, I, U64, I, I, U64, I, P, P, P, P)
     _sig(L.hs_range_search_dev, I, P, P, P, I, P, P, P, P, P)
     _sig(L.hs_ranges_to_tiles, I, P, I, I, P, P)
+    _sig(L.hs_ranges_to_tiles_aligned, I, P, P, I, I, I64, P, P)
     _sig(L.hs_scan_agg, I, P, P, P, I, P, I, P, P, P, P, P, P, P, P, P)
     _sig(L.hs_scan_count, I, P, P, P, I, P, I, P, P)
     _sig(L.hs_scan_select, I, P, P, P, I, P, P, I, P, P)

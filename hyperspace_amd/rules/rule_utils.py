@@ -101,13 +101,27 @@ def _index_file_index(index, extra: list = ()) -> L.FileIndex:
     return L.FileIndex([f.path for f in files], files)
 
 
+_SCHEMA_FOR: dict = {}
+
+
 def _index_schema_for(index, base: L.LogicalRelation, with_lineage: bool):
+    """Index columns that exist in the base relation (+ lineage); memoized on the (immutable)
+    schema objects since rules evaluate it for every candidate of every query."""
     import pyarrow as pa
-    base_fields = {(f.name, str(f.type)) for f in base.relation.schema}
-    fields = [f for f in index.schema
+    ischema, bschema = index.schema, base.relation.schema
+    k = (id(ischema), id(bschema), with_lineage)
+    hit = _SCHEMA_FOR.get(k)
+    if hit is not None and hit[0] is ischema and hit[1] is bschema:
+        return hit[2]
+    base_fields = {(f.name, str(f.type)) for f in bschema}
+    fields = [f for f in ischema
               if (f.name, str(f.type)) in base_fields or
               (with_lineage and f.name == C.DATA_FILE_NAME_ID)]
-    return pa.schema(fields)
+    out = pa.schema(fields)
+    if len(_SCHEMA_FOR) > 1024:
+        _SCHEMA_FOR.clear()
+    _SCHEMA_FOR[k] = (ischema, bschema, out)
+    return out
 
 
 def _index_relation(session, index, base: L.LogicalRelation, location, schema, use_bucket_spec):

@@ -81,7 +81,10 @@ def test_generated_sources_compile(rt, tmp_path):
     j.naggs, j.lkey, j.rkey = 2, 0, 8
     for g, fl in ((-1, 0), (10, 0), (-1, 1)):
         j.group_col, j.num_groups, j.key_is_float = g, 3, fl
-        for k in [jit.gen_join_agg(j)] + ([jit.gen_join_index_agg(j)] if not fl else []):
+        ks = [jit.gen_join_agg(j)]
+        if not fl:
+            ks += [jit.gen_join_index_agg(j), jit.gen_join_index_agg(j, vec=4)]
+        for k in ks:
             rc = jit.runtime().hs_jit_compile_to_cache(k.src.encode(), k.name.encode(),
                                                        b"gfx950", str(tmp_path).encode())
             assert rc == 0, jit.runtime().hs_jit_last_error().decode()
