@@ -985,13 +985,15 @@ def join_agg_values(p: NL.JoinParams, tile_prefix, spans, parts,
 # ------------------------------------------------------------------------------------------------
 # Join through a cached join index (exec/join_index.py)
 # ------------------------------------------------------------------------------------------------
-def join_index_agg_shape(p: NL.JoinParams, compacts=None, vec: int = 0) -> tuple:
+def join_index_agg_shape(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int = 4,
+                         jlog: int = 0) -> tuple:
     cols = tuple(sorted(_col_specs(p, compacts).items()))
     preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
                    p.preds[k].group) for k in range(p.npreds))
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
-    return ("join_index_agg", cols, preds, p.nlp, aggs, p.group_col, JI_ITEMS, vec, BLOCK)
+    return ("join_index_agg", cols, preds, p.nlp, aggs, p.group_col, JI_ITEMS, vec, BLOCK, jw,
+            jlog)
 
 
 def _uload(gen: _Gen, slot: int, it: int, out: List[str], ind: str) -> None:
@@ -1043,7 +1045,8 @@ def _vec_aligned_ptrs(ptrs) -> bool:
     return all(int(x) % 16 == 0 for x in ptrs if x)
 
 
-def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0) -> Kernel:
+def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int = 4,
+                       jlog: int = 0) -> Kernel:
     """Fused join + aggregate as a streaming scan of the left table's row ranges that reads
     ``jidx[row]`` — the matching right row from the cached join index (exec/join_index.py) — and
     gathers right-side columns there.
@@ -1060,9 +1063,14 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0) -> Kernel:
     Right rows of consecutive left rows are monotone (both sides sorted by key per bucket), so
     the gathers of a wavefront hit a few adjacent cache lines."""
     args = Args()
+    jct = {4: "int", 2: "unsigned short", 1: "unsigned char"}[jw]
+    sent = {2: "0xFFFF", 1: "0xFF"}.get(jw)
     for n, ct in (("rstart", "const long long*"), ("rlen", "const long long*"),
-                  ("tile_prefix", "const long long*"), ("jidx", "const int*")):
+                  ("tile_prefix", "const long long*"), ("jidx", f"const {jct}*")):
         args.add("p", n, ct)
+    if jw < 4:
+        # block-coded join index (exec/join_index.py): j = jbase[row >> jlog] + code
+        args.add("p", "jbase", "const int*")
     args.add("q", "R", "long long")
     _common_args(args)
     cols = _col_specs(p, compacts)
@@ -1101,9 +1109,15 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0) -> Kernel:
     if vec:
         _vec_rows(b, NI, ind)
         g1 = _Gen(args, cols, split, ("row0", "row0"))
-        _vec_load_slots(b, g1, first, NI, ind, extra=[("jr", "int", "a.jidx")])
+        _vec_load_slots(b, g1, first, NI, ind, extra=[("jr", jct, "a.jidx")])
+        if jw < 4:   # NI | block size and g0 % NI == 0: the thread's rows share one block
+            b.append(f"{ind}const int jb = a.jbase[g0 >> {jlog}];")
         for it in range(NI):
-            b.append(f"{ind}const int jr{it} = act{it} ? jrv[{it}] : -1;")
+            if jw < 4:
+                b.append(f"{ind}const int jr{it} = act{it} && jrv[{it}] != {sent} ? "
+                         f"jb + (int)jrv[{it}] : -1;")
+            else:
+                b.append(f"{ind}const int jr{it} = act{it} ? jrv[{it}] : -1;")
     else:
         b += ["    const i64 tb0 = a.rstart[r] + off;",
               f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};"]
@@ -1112,7 +1126,12 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0) -> Kernel:
                   f"{ind}const i64 row{it} = tb0 + (act{it} ? {it * BLOCK} + (i64)threadIdx.x : 0);"]
         # phase 1: join index + left predicate columns of every item
         for it in range(NI):
-            b.append(f"{ind}const int jr{it} = a.jidx[row{it}];")
+            if jw < 4:
+                b.append(f"{ind}const {jct} jc{it} = a.jidx[row{it}];")
+                b.append(f"{ind}const int jr{it} = jc{it} != {sent} ? "
+                         f"a.jbase[row{it} >> {jlog}] + (int)jc{it} : -1;")
+            else:
+                b.append(f"{ind}const int jr{it} = a.jidx[row{it}];")
             g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"))
             for s in first:
                 _uload(g1, s, it, b, ind)
@@ -1165,16 +1184,20 @@ def _vec_aligned(p: NL.JoinParams, compacts, jidx) -> bool:
     for s in _pred_slots([(k, p.preds[k]) for k in range(p.nlp)]):
         c = (compacts or {}).get(s)
         ptrs.append(c.codes.data_ptr() if c else p.cols[s].data)
-        if p.cols[s].valid:
-            ptrs.append(p.cols[s].valid)
-    return all(int(x) % 16 == 0 for x in ptrs)
+        ptrs.append(p.cols[s].valid)
+    return _vec_aligned_ptrs(ptrs)
 
 
-def join_index_agg(p: NL.JoinParams, rstart, rlen, jidx, compacts=None, nrows: int = 0):
-    """Same outputs as ``join_agg``; ``jidx`` from ``join_index.get_join_index``; ``nrows`` =
-    left table rows (vectorized loads stay inside the columns)."""
+def join_index_agg(p: NL.JoinParams, rstart, rlen, jx, compacts=None, nrows: int = 0):
+    """Same outputs as ``join_agg``.  ``jx``: the join index from ``join_index.get_join_index``
+    (``codes`` int32 rows, or uint8/uint16 block-coded with ``base`` / ``log_blk``);
+    ``nrows`` = left table rows (vectorized loads stay inside the columns)."""
     from ..ops import kernels as K
-    vec = JI_VEC if JI_VEC > 0 and _vec_aligned(p, compacts, jidx) else 0
+    jw = jx.width
+    jlog = jx.log_blk if jw < 4 else 0
+    vec = JI_VEC if JI_VEC > 0 and _vec_aligned(p, compacts, jx.codes) else 0
+    if vec and jw < 4 and (1 << jlog) % vec:
+        vec = 0
     if vec:
         # tiles over the ranges widened down to a multiple of vec rows (the kernel masks them)
         tp = K.ranges_to_tiles(rlen + (rstart & (vec - 1)), BLOCK * vec)
@@ -1182,17 +1205,19 @@ def join_index_agg(p: NL.JoinParams, rstart, rlen, jidx, compacts=None, nrows: i
         tp = K.ranges_to_tiles(rlen, BLOCK * JI_ITEMS)
     grid = SCAN_GRID or NL.lib().hs_scan_grid()
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
-    k = kernel_for(join_index_agg_shape(p, compacts, vec),
-                   lambda: gen_join_index_agg(p, compacts, vec))
+    k = kernel_for(join_index_agg_shape(p, compacts, vec, jw, jlog),
+                   lambda: gen_join_index_agg(p, compacts, vec, jw, jlog))
     parts = _partials(grid, GA, rstart.device)
     v = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
-         "jidx": jidx.data_ptr(), "R": rstart.numel(), "nrows": nrows, "psum": parts[0].data_ptr(),
+         "jidx": jx.codes.data_ptr(), "jbase": jx.base.data_ptr() if jw < 4 else 0,
+         "R": rstart.numel(), "nrows": nrows, "psum": parts[0].data_ptr(),
          "pcnt": parts[1].data_ptr(), "pmin": parts[2].data_ptr(), "pmax": parts[3].data_ptr(),
          "num_groups": p.num_groups, "group_base": p.group_base}
     _fill_common(v, p.cols, [(k_, p.preds[k_]) for k_ in range(p.npreds)],
                  [p.aggs[i] for i in range(p.naggs)], compacts)
     k.launch(grid, v, NL.stream_ptr(), GA * 32 if p.group_col >= 0 else 0)
     return _final(parts, grid, GA, rstart.device)
+
 
 # ------------------------------------------------------------------------------------------------
 # Shape cache

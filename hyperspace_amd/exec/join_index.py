@@ -23,6 +23,7 @@ invalidates the entry.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import weakref
 from typing import Optional
 
@@ -62,9 +63,66 @@ def eligible(left_table: DeviceTable, right_table: DeviceTable, lcol: DeviceColu
     return right_keys_unique(right_table, rcol)
 
 
+class JoinIndex:
+    """A join index in HBM.  ``width`` 4: ``codes`` is int32 [left rows] (j or -1).  ``width``
+    1 / 2: block-coded — ``codes`` uint8 / uint16 per row, ``base`` int32 per block of
+    ``2**log_blk`` rows, ``j = base[row >> log_blk] + code`` and the all-ones code = no match.
+    Right rows of a block of left rows are a short monotone span for FK joins (lineitem ->
+    orders: ~32 orders per 128 lines), so one byte per row usually suffices: the join kernel
+    streams 1 byte per left row instead of 4."""
+
+    def __init__(self, codes, width: int, base=None, log_blk: int = 0):
+        self.codes, self.width, self.base, self.log_blk = codes, width, base, log_blk
+
+    def nbytes(self) -> int:
+        n = self.codes.numel() * self.codes.element_size()
+        return n + (self.base.numel() * 4 if self.base is not None else 0)
+
+    def decoded(self, n: int):
+        """int32 [n] j-or--1 view (tests / debugging)."""
+        import torch
+        if self.width == 4:
+            return self.codes[:n]
+        c = self.codes[:n].to(torch.int64)
+        if self.width == 2:
+            c = c & 0xFFFF
+        sent = (1 << (8 * self.width)) - 1
+        b = self.base.to(torch.int64).repeat_interleave(1 << self.log_blk)[:n]
+        return torch.where(c == sent, torch.full_like(c, -1), b + c).to(torch.int32)
+
+
+# block-coded join indexes (HS_JOIN_INDEX_CODED=0 keeps int32 rows)
+CODED = os.environ.get("HS_JOIN_INDEX_CODED", "1") == "1"
+# (code width, log2 block rows) tried in order; the first that fits every block wins
+CODINGS = ((1, 7), (2, 8))
+
+
+def _block_code(jidx, width: int, log_blk: int) -> Optional[JoinIndex]:
+    import torch
+    n = jidx.numel()
+    B = 1 << log_blk
+    nb = (n + B - 1) // B
+    j = torch.full((nb * B,), -1, dtype=torch.int64, device=jidx.device)
+    j[:n] = jidx
+    j = j.view(nb, B)
+    big = 1 << 62
+    base = torch.where(j >= 0, j, torch.full_like(j, big)).min(dim=1).values
+    base = torch.where(base == big, torch.zeros_like(base), base)
+    off = j - base[:, None]
+    sent = (1 << (8 * width)) - 1
+    if not bool(((j < 0) | (off < sent)).all().item()):
+        return None
+    code = torch.where(j >= 0, off, torch.full_like(off, sent)).to(torch.int32).reshape(-1)
+    if width == 1:
+        codes = code.to(torch.uint8)
+    else:   # low 16 bits of each int32 (little-endian), stored as int16
+        codes = code.view(torch.uint8).view(-1, 4)[:, :2].contiguous().view(torch.int16).reshape(-1)
+    return JoinIndex(codes, width, base.to(torch.int32), log_blk)
+
+
 def get_join_index(jp: NL.JoinParams, left_table: DeviceTable, right_table: DeviceTable,
-                   lcol: DeviceColumn, rcol: DeviceColumn, rstart, rlen, rbucket) -> Optional[object]:
-    """int32 [left rows] device tensor: first matching right row of every left row, or -1.
+                   lcol: DeviceColumn, rcol: DeviceColumn, rstart, rlen, rbucket) -> JoinIndex:
+    """The join index of the pair: first matching right row of every left row (or none).
 
     ``rstart/rlen/rbucket`` must be the left table's full ranges (every row of every bucket).
     ``jp`` supplies the key column descriptors (slots ``jp.lkey`` / ``jp.rkey``)."""
@@ -72,9 +130,9 @@ def get_join_index(jp: NL.JoinParams, left_table: DeviceTable, right_table: Devi
     key = (id(lcol), id(rcol))
     hit = cache.get(key)
     if hit is not None:
-        rref, lc, rc, jidx = hit
+        rref, lc, rc, ji = hit
         if rref() is right_table and lc is lcol and rc is rcol:
-            return jidx
+            return ji
     import torch
     from . import jit
     dev = rstart.device
@@ -86,5 +144,13 @@ def get_join_index(jp: NL.JoinParams, left_table: DeviceTable, right_table: Devi
     grid = NL.lib().hs_scan_grid()
     NL.check(NL.lib().hs_join_index(C.byref(jp), rlen.numel(), NL.ptr(tp), NL.ptr(spans), grid,
                                     NL.ptr(jidx), NL.stream_ptr()), "hs_join_index")
-    cache[key] = (weakref.ref(right_table), lcol, rcol, jidx)
-    return jidx
+    ji = None
+    if CODED:
+        for width, log_blk in CODINGS:
+            ji = _block_code(jidx[:left_table.num_rows], width, log_blk)
+            if ji is not None:
+                break
+    if ji is None:
+        ji = JoinIndex(jidx, 4)
+    cache[key] = (weakref.ref(right_table), lcol, rcol, ji)
+    return ji

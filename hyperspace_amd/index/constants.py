@@ -114,4 +114,8 @@ JOIN_INDEX_ENABLED_DEFAULT = "true"
 #               query throughput scales with ranks).  Index builds are sharded either way.
 INDEX_PLACEMENT = "spark.hyperspace.mi.index.placement"
 INDEX_PLACEMENT_DEFAULT = "sharded"
+# parameterized plan cache: queries that differ only in literal values reuse one planning
+# (plan/plan_cache.py)
+PLAN_CACHE_ENABLED = "spark.hyperspace.mi.planCache.enabled"
+PLAN_CACHE_ENABLED_DEFAULT = "true"
 FAULT_INJECTION = "spark.hyperspace.mi.faultInjection"

@@ -156,6 +156,15 @@ class CachingIndexCollectionManager(IndexCollectionManager):
             self.cache.set(cached)
         return [e for e in cached if not states_ or e.state in states_]
 
+    def snapshot(self):
+        """The cached index-metadata list the rules read (a new object after every refill:
+        mutating API calls and TTL expiry), so its identity versions cached plans."""
+        cached = self.cache.get()
+        if cached is None:
+            cached = super().get_indexes(())
+            self.cache.set(cached)
+        return cached
+
     def clear_cache(self) -> None:
         self.cache.clear()
 

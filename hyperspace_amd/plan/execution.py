@@ -38,7 +38,18 @@ class QueryExecution:
     @property
     def executed_plan(self):
         if self._executed is None:
+            from ..utils.conf import HyperspaceConf
+            pc = None
+            if HyperspaceConf.plan_cache_enabled(self.session.conf):
+                from .plan_cache import plan_cache
+                pc = plan_cache(self.session)
+                plan, key, ctx = pc.lookup(self.session, self.logical)
+                if plan is not None:
+                    self._executed = plan
+                    return plan
             self._executed = ensure_requirements(self.spark_plan, self.session)
+            if pc is not None:
+                pc.store(key, self._executed, ctx)
         return self._executed
 
     executedPlan = executed_plan

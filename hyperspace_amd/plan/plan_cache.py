@@ -1,0 +1,250 @@
+"""Parameterized plan cache: queries that differ only in literal values share one planning.
+
+Planning a query — optimizer batches, the Hyperspace rules (candidate indexes, signatures,
+rankers), physical planning and ``EnsureRequirements`` — costs 0.2-0.5 ms of Python per query,
+which is a large share of an indexed query that runs 0.3-1.5 ms on an MI355X.  A serving
+workload repeats a handful of query *shapes* with new literals (TPC-H Q6 with another year,
+Q3 with another date), and nothing in planning depends on literal values:
+
+* the optimizer rules used here are structural, except ``OptimizeIn`` (it deduplicates IN-list
+  values), so plans containing ``In``/``InSet`` are not parameterized;
+* the Hyperspace rules decide from referenced columns, index metadata and file signatures;
+* physical planning decides from sizes and partitioning, not from literals.
+
+So the analyzed plan is fingerprinted with every literal replaced by a typed placeholder (its
+type and null-ness stay in the key), attribute ids canonicalized by first appearance, and
+relations by identity.  The key also carries the session state planning reads: the conf
+version, the installed optimizer rules (Hyperspace enabled or not) and the identity of the
+index-metadata snapshot the rules see (a refresh / create / delete or the TTL expiry of the
+index cache produces a new snapshot, so a new key).
+
+On a miss the query is planned normally and cached only if every literal object of the
+analyzed plan survived, by identity, into the executed plan.  On a hit the cached executed plan
+is copied with each old literal object replaced by the new query's literal in the same position.
+Only the objects on paths from the plan root to those literals (recorded when the entry is
+stored) are copied; everything else is shared with the cached plan.
+"""
+from __future__ import annotations
+
+import copy
+import threading
+from collections import OrderedDict
+from typing import Dict, List, Optional, Tuple
+
+import pyarrow as pa
+
+from . import expressions as E
+from . import logical as L
+
+_PLAN_MODULES = ("hyperspace_amd.plan",)
+_SCALARS = (str, int, float, bool, type(None), pa.DataType, pa.Schema, pa.Field)
+CAPACITY = 256
+
+
+class _NotCacheable(Exception):
+    pass
+
+
+class _Ctx:
+    __slots__ = ("ids", "lits", "refs")
+
+    def __init__(self):
+        self.ids: Dict[int, int] = {}
+        self.lits: List[E.Literal] = []
+        self.refs: list = []
+
+    def eid(self, x: int) -> int:
+        v = self.ids.get(x)
+        if v is None:
+            v = len(self.ids)
+            self.ids[x] = v
+        return v
+
+
+def _own(obj) -> bool:
+    return type(obj).__module__.startswith(_PLAN_MODULES)
+
+
+def _fp(v, ctx: _Ctx):
+    if isinstance(v, E.Literal):
+        ctx.lits.append(v)
+        return ("L", str(v.dtype), v.value is None)
+    if isinstance(v, (E.In, E.InSet)):
+        raise _NotCacheable("IN list (OptimizeIn depends on its values)")
+    if isinstance(v, E.Attribute):
+        return ("A", v.name, str(v.dtype), v.nullable, ctx.eid(v.expr_id), v.qualifier)
+    if v is None or isinstance(v, (str, int, float, bool)):
+        return v
+    if isinstance(v, (list, tuple)):
+        return tuple(_fp(x, ctx) for x in v)
+    if isinstance(v, (set, frozenset)):
+        raise _NotCacheable("set-valued node field")
+    if isinstance(v, dict):
+        return tuple(sorted((str(k), _fp(x, ctx)) for k, x in v.items()))
+    if isinstance(v, (pa.DataType, pa.Schema, pa.Field)):
+        return str(v)
+    if isinstance(v, L.HadoopFsRelation) or not _own(v):
+        # relations, file indexes, tables: by identity (the entry keeps them alive)
+        ctx.refs.append(v)
+        return ("O", id(v))
+    items = []
+    for k, x in sorted(vars(v).items()):
+        if k == "expr_id":
+            items.append((k, ctx.eid(x)))
+        elif k.startswith("_cache") or k.startswith("_hs_"):
+            continue   # memoized derived state, not part of the node's meaning
+        else:
+            items.append((k, _fp(x, ctx)))
+    return (type(v).__name__, tuple(items))
+
+
+def _iter_literals(v, out: List[E.Literal], seen: set):
+    """Every Literal object reachable from a plan (through our own node/container types)."""
+    if isinstance(v, E.Literal):
+        out.append(v)
+        return
+    if isinstance(v, _SCALARS):
+        return
+    if isinstance(v, (list, tuple, set, frozenset)):
+        for x in v:
+            _iter_literals(x, out, seen)
+        return
+    if isinstance(v, dict):
+        for x in v.values():
+            _iter_literals(x, out, seen)
+        return
+    if not _own(v) or isinstance(v, L.HadoopFsRelation) or id(v) in seen:
+        return
+    seen.add(id(v))
+    for x in vars(v).values():
+        _iter_literals(x, out, seen)
+
+
+def _hot_paths(v, lit_ids: set, hot: set, seen: Dict[int, bool]) -> bool:
+    """Mark (in ``hot``) every object/container on a path from ``v`` to a literal in
+    ``lit_ids``; returns whether ``v`` leads to one."""
+    if isinstance(v, E.Literal):
+        return id(v) in lit_ids
+    if isinstance(v, _SCALARS):
+        return False
+    k = id(v)
+    if k in seen:
+        return seen[k]
+    seen[k] = False
+    found = False
+    if isinstance(v, (list, tuple)):
+        for x in v:
+            found = _hot_paths(x, lit_ids, hot, seen) or found
+    elif isinstance(v, dict):
+        for x in v.values():
+            found = _hot_paths(x, lit_ids, hot, seen) or found
+    elif _own(v) and not isinstance(v, (L.HadoopFsRelation, L.LogicalPlan)):
+        for x in vars(v).values():
+            found = _hot_paths(x, lit_ids, hot, seen) or found
+    seen[k] = found
+    if found:
+        hot.add(k)
+    return found
+
+
+def _subst(v, m: Dict[int, E.Literal], hot: set, memo: Dict[int, object]):
+    """Copy of ``v`` with literal objects replaced via ``m`` (id -> new literal), rebuilding only
+    the objects on ``hot`` paths; everything else is shared with the cached plan."""
+    if isinstance(v, E.Literal):
+        return m.get(id(v), v)
+    k = id(v)
+    if k not in hot:
+        return v
+    hit = memo.get(k)
+    if hit is not None:
+        return hit
+    if isinstance(v, list):
+        out = [_subst(x, m, hot, memo) for x in v]
+    elif isinstance(v, tuple):
+        out = tuple(_subst(x, m, hot, memo) for x in v)
+    elif isinstance(v, dict):
+        out = {kk: _subst(x, m, hot, memo) for kk, x in v.items()}
+    else:
+        out = copy.copy(v)
+        for kk, x in vars(v).items():
+            nx = _subst(x, m, hot, memo)
+            if nx is not x:
+                object.__setattr__(out, kk, nx)
+    memo[k] = out
+    return out
+
+
+class PlanCache:
+    def __init__(self, capacity: int = CAPACITY):
+        self.capacity = capacity
+        self._lru: "OrderedDict[tuple, tuple]" = OrderedDict()
+        self._lock = threading.Lock()
+        self.hits = 0
+        self.misses = 0
+        self.uncacheable = 0
+
+    @staticmethod
+    def _session_key(session, ctx: _Ctx) -> tuple:
+        rules = tuple(id(r) for r in session.extra_optimizations)
+        ctx.refs.extend(session.extra_optimizations)
+        snap = 0
+        if session.extra_optimizations:
+            from ..hyperspace import get_context
+            snap_obj = get_context(session).index_collection_manager.snapshot()
+            ctx.refs.append(snap_obj)
+            snap = id(snap_obj)
+        return (id(session), session.conf.version, rules, snap)
+
+    def lookup(self, session, logical) -> Tuple[Optional[object], Optional[tuple], _Ctx]:
+        """(executed plan or None, key, fingerprint context) of ``logical``."""
+        ctx = _Ctx()
+        try:
+            key = (self._session_key(session, ctx), _fp(logical, ctx))
+        except _NotCacheable:
+            self.uncacheable += 1
+            return None, None, ctx
+        with self._lock:
+            hit = self._lru.get(key)
+            if hit is not None:
+                self._lru.move_to_end(key)
+        if hit is None:
+            self.misses += 1
+            return None, key, ctx
+        plan, old_lits, hot, _refs = hit
+        if len(old_lits) != len(ctx.lits):
+            self.misses += 1
+            return None, key, ctx
+        m = {id(o): n for o, n in zip(old_lits, ctx.lits) if o is not n}
+        new_plan = _subst(plan, m, hot, {}) if m else plan
+        self.hits += 1
+        return new_plan, key, ctx
+
+    def store(self, key, executed, ctx: _Ctx) -> bool:
+        """Cache ``executed`` for ``key`` if every literal of the analyzed plan reached it."""
+        if key is None:
+            return False
+        present: List[E.Literal] = []
+        _iter_literals(executed, present, set())
+        ids = {id(x) for x in present}
+        if not all(id(x) in ids for x in ctx.lits):
+            self.uncacheable += 1
+            return False
+        hot: set = set()
+        _hot_paths(executed, {id(x) for x in ctx.lits}, hot, {})
+        with self._lock:
+            self._lru[key] = (executed, list(ctx.lits), hot, list(ctx.refs))
+            while len(self._lru) > self.capacity:
+                self._lru.popitem(last=False)
+        return True
+
+    def clear(self):
+        with self._lock:
+            self._lru.clear()
+
+
+def plan_cache(session) -> PlanCache:
+    pc = getattr(session, "_plan_cache", None)
+    if pc is None:
+        pc = PlanCache()
+        session._plan_cache = pc
+    return pc

@@ -11,13 +11,17 @@ from ..index import constants as C
 class RuntimeConf:
     def __init__(self, initial=None):
         self._m = {}
+        self.version = 0   # bumped on every change (plan-cache key, plan/plan_cache.py)
         for k, v in (initial or {}).items():
             self.set(k, v)
 
     def set(self, key: str, value) -> None:
         if isinstance(value, bool):
             value = "true" if value else "false"
-        self._m[key] = str(value)
+        value = str(value)
+        if self._m.get(key) != value:
+            self._m[key] = value
+            self.version += 1
 
     def get(self, key: str, default=None):
         return self._m.get(key, default)
@@ -26,7 +30,8 @@ class RuntimeConf:
         return self._m.get(key)
 
     def unset(self, key: str) -> None:
-        self._m.pop(key, None)
+        if self._m.pop(key, None) is not None:
+            self.version += 1
 
     def contains(self, key: str) -> bool:
         return key in self._m
@@ -123,6 +128,10 @@ class HyperspaceConf:
         if v not in ("sharded", "replicated"):
             raise ValueError(f"{C.INDEX_PLACEMENT} must be sharded or replicated, got {v}")
         return v
+
+    @staticmethod
+    def plan_cache_enabled(conf) -> bool:
+        return _b(conf.get(C.PLAN_CACHE_ENABLED, C.PLAN_CACHE_ENABLED_DEFAULT))
 
     @staticmethod
     def join_index_enabled(conf) -> bool:

@@ -83,7 +83,9 @@ def test_generated_sources_compile(rt, tmp_path):
         j.group_col, j.num_groups, j.key_is_float = g, 3, fl
         ks = [jit.gen_join_agg(j)]
         if not fl:
-            ks += [jit.gen_join_index_agg(j), jit.gen_join_index_agg(j, vec=4)]
+            ks += [jit.gen_join_index_agg(j), jit.gen_join_index_agg(j, vec=4),
+                   jit.gen_join_index_agg(j, vec=8, jw=1, jlog=7),
+                   jit.gen_join_index_agg(j, jw=2, jlog=8)]
         for k in ks:
             rc = jit.runtime().hs_jit_compile_to_cache(k.src.encode(), k.name.encode(),
                                                        b"gfx950", str(tmp_path).encode())

@@ -120,7 +120,8 @@ def test_join_index_matches_numpy_merge(data):
     tables = [t for t in be.cache._lru.values() if "_join_index" in t.__dict__]
     assert tables, "no join index was built"
     lt = tables[0]
-    (rref, lcol, rcol, jidx), = lt._join_index.values()
+    (rref, lcol, rcol, ji), = lt._join_index.values()
+    jidx = ji.decoded(lt.num_rows)
     lk = lcol.data.cpu().numpy()
     lv = lcol.valid.cpu().numpy().astype(bool) if lcol.valid is not None else np.ones(len(lk), bool)
     rk = rcol.data.cpu().numpy()
@@ -143,3 +144,22 @@ def test_duplicate_right_keys_keep_merge_join(data):
     assert p == "native", s.backend().fallback_reason
     c, _ = _run(s, q, device="cpu")
     _close(g, c)
+
+
+@pytest.mark.parametrize("coded,codings", [(True, ((1, 7),)), (True, ((2, 8),)), (False, ())])
+def test_join_index_encodings(data, monkeypatch, coded, codings):
+    """uint8 / uint16 block-coded and plain int32 join indexes give the oracle's answer."""
+    from hyperspace_amd.exec import join_index
+    s, li, od, _ = data
+    monkeypatch.setattr(join_index, "CODED", coded)
+    monkeypatch.setattr(join_index, "CODINGS", codings)
+    for t in s.backend().cache._lru.values():
+        t.__dict__.pop("_join_index", None)
+    q = _q3(li, od, 9400)
+    g, p = _run(s, q)
+    assert p == "native", s.backend().fallback_reason
+    c, _ = _run(s, q, device="cpu")
+    _close(g, c)
+    widths = {ji.width for t in s.backend().cache._lru.values()
+              for (_, _, _, ji) in t.__dict__.get("_join_index", {}).values()}
+    assert widths == {codings[0][0] if coded else 4}

@@ -1,0 +1,115 @@
+"""Parameterized plan cache (plan/plan_cache.py): a query that differs from a cached one only in
+its literals reuses the cached executed plan with the new literals substituted, and gives the
+same rows as planning from scratch; conf changes, Hyperspace on/off and index changes re-plan;
+IN lists are never parameterized."""
+import datetime
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.parquet as pq
+import pytest
+
+from hyperspace_amd import Hyperspace, IndexConfig, col, count, sum_
+from hyperspace_amd.plan.plan_cache import plan_cache
+
+
+@pytest.fixture
+def data(session, tmp_path):
+    rng = np.random.default_rng(3)
+    n = 4000
+    t = pa.table({"k": rng.integers(0, 500, n).astype(np.int64),
+                  "d": pa.array(rng.integers(8000, 9000, n).astype(np.int32)).view(pa.date32()),
+                  "v": rng.random(n),
+                  "s": pa.array([f"s{x}" for x in rng.integers(0, 20, n)])})
+    o = pa.table({"ok": np.arange(500, dtype=np.int64), "od": rng.integers(0, 100, 500).astype(np.int32)})
+    (tmp_path / "t").mkdir()
+    (tmp_path / "o").mkdir()
+    pq.write_table(t, tmp_path / "t" / "p0.parquet")
+    pq.write_table(o, tmp_path / "o" / "p0.parquet")
+    s = session
+    hs = Hyperspace(s)
+    df = s.read.parquet(str(tmp_path / "t"))
+    od = s.read.parquet(str(tmp_path / "o"))
+    hs.createIndex(df, IndexConfig("by_d", ["d"], ["v", "k"]))
+    hs.createIndex(df, IndexConfig("by_k", ["k"], ["v", "d"]))
+    hs.createIndex(od, IndexConfig("by_ok", ["ok"], ["od"]))
+    Hyperspace.enable(s)
+    return s, hs, df, od
+
+
+def _filter_q(df, i):
+    lo = datetime.date(1991, 12, 1) + datetime.timedelta(days=20 * i)
+    return df.filter((col("d") >= lo) & (col("d") < lo + datetime.timedelta(days=90)) &
+                     (col("v") > 0.1 * (i % 5))).agg(sum_(col("v")).alias("sv"),
+                                                     count("*").alias("n"))
+
+
+def _join_q(df, od, i):
+    return df.join(od, df["k"] == od["ok"]).filter(col("od") < 10 + 7 * i) \
+        .groupBy("od").agg(sum_(col("v") * (1 - col("v"))).alias("x"), count("*").alias("n"))
+
+
+def _rows(df):
+    return sorted(tuple(r) for r in df.collect())
+
+
+def test_literal_variants_hit_and_match_fresh_planning(data):
+    s, _, df, od = data
+    pc = plan_cache(s)
+    got = [(_rows(_filter_q(df, i)), _rows(_join_q(df, od, i))) for i in range(8)]
+    assert pc.hits >= 12, (pc.hits, pc.misses)
+    s.conf.set("spark.hyperspace.mi.planCache.enabled", "false")
+    want = [(_rows(_filter_q(df, i)), _rows(_join_q(df, od, i))) for i in range(8)]
+    assert got == want
+    # the cached plan keeps using the index with new literals
+    s.conf.set("spark.hyperspace.mi.planCache.enabled", "true")
+    q = _filter_q(df, 5)
+    assert "Name: by_d" in q.queryExecution.executed_plan.tree_string()
+
+
+def test_hit_substitutes_literals_in_plan(data):
+    s, _, df, _ = data
+    q1, q2 = _filter_q(df, 1), _filter_q(df, 2)
+    p1 = q1.queryExecution.executed_plan.tree_string()
+    p2 = q2.queryExecution.executed_plan.tree_string()
+    assert plan_cache(s).hits >= 1
+    assert p1 != p2
+    lo2 = (datetime.date(1991, 12, 1) + datetime.timedelta(days=40)).isoformat()
+    assert lo2 in p2 and lo2 not in p1
+
+
+def test_conf_and_hyperspace_toggle_replan(data):
+    s, _, df, _ = data
+    pc = plan_cache(s)
+    _rows(_filter_q(df, 0))
+    m = pc.misses
+    s.conf.set("spark.sql.shuffle.partitions", "7")
+    _rows(_filter_q(df, 1))
+    assert pc.misses == m + 1
+    s.disableHyperspace()
+    q = _filter_q(df, 2)
+    assert "Hyperspace" not in q.queryExecution.executed_plan.tree_string()
+    s.enableHyperspace()
+    assert "Hyperspace" in _filter_q(df, 3).queryExecution.executed_plan.tree_string()
+
+
+def test_index_changes_replan(data):
+    s, hs, df, _ = data
+    assert "Name: by_d" in _filter_q(df, 0).queryExecution.executed_plan.tree_string()
+    hs.deleteIndex("by_d")
+    p = _filter_q(df, 1).queryExecution.executed_plan.tree_string()
+    assert "Name: by_d" not in p
+    hs.restoreIndex("by_d")
+    assert "Name: by_d" in _filter_q(df, 2).queryExecution.executed_plan.tree_string()
+
+
+def test_in_lists_are_not_parameterized(data):
+    s, _, df, _ = data
+    pc = plan_cache(s)
+    u = pc.uncacheable
+    a = _rows(df.filter(col("s").isin("s1", "s2", "s1")).agg(count("*").alias("n")))
+    b = _rows(df.filter(col("s").isin("s3")).agg(count("*").alias("n")))
+    assert pc.uncacheable >= u + 2
+    t = df.to_arrow()
+    assert a[0][0] == sum(1 for x in t.column("s").to_pylist() if x in ("s1", "s2"))
+    assert b[0][0] == sum(1 for x in t.column("s").to_pylist() if x == "s3")
