@@ -96,6 +96,7 @@ class GpuBackend:
         self._cpu = None
         self._domains: Dict[tuple, tuple] = {}
         self._gdomains: Dict[tuple, tuple] = {}   # (table global key, column) -> all-rank domain
+        self._unions: Dict[tuple, tuple] = {}     # string join keys: dictionary pair -> union
         self._groups_agreed = False
         self.graphs = GraphCache()
         # engine start: size the pinned staging pool once (pinning GBs is the slow part of a
@@ -544,15 +545,64 @@ class GpuBackend:
         if not _prefix_sorted(right, [rk]):
             raise Unsupported("right not sorted by join key")
         kinds = set()
+        strings = []
         for side, k in ((left, lk), (right, rk)):
             for part in side.parts or [side]:
                 c = part.col(k)
-                if c.dictionary is not None:
-                    raise Unsupported("string join keys on device")
+                strings.append(c.dictionary is not None)
                 kinds.add(c.is_float)
-        if len(kinds) > 1:
+        if any(strings):
+            if not all(strings) or left.parts or right.parts:
+                raise Unsupported("string join keys over a bucket union / mixed key types")
+            left, right = self._string_join_keys(left, right, lk, rk)
+        elif len(kinds) > 1:
             raise Unsupported("mixed int/float join keys")
         return left, right, lk, rk
+
+    def _string_join_keys(self, left: DRel, right: DRel, lk, rk):
+        """Join on string keys.  Strings live in HBM as codes into per-table *sorted*
+        dictionaries, so codes of the two sides are not comparable — but codes into the sorted
+        union of both dictionaries are, and they keep each bucket's sort order (code order ==
+        string order).  Each side's key column is remapped once (one int32 gather) into the
+        union's code space; the remapped tables are cached on the originals, so the join index
+        and span caches see stable tables across queries."""
+        lc, rc = left.col(lk), right.col(rk)
+        ld, rd = lc.dictionary, rc.dictionary
+        if ld is rd or ld.equals(rd):
+            return left, right
+        ukey = (id(ld), id(rd))
+        hit = self._unions.get(ukey)
+        if hit is None or hit[0] is not ld or hit[1] is not rd:
+            import pyarrow.compute as pc
+            union = pc.unique(pa.concat_arrays([ld.cast(pa.string()), rd.cast(pa.string())]))
+            union = union.sort()
+            hit = (ld, rd, union)
+            self._unions[ukey] = hit
+        union = hit[2]
+        return (self._remapped(left, lk, union), self._remapped(right, rk, union))
+
+    def _remapped(self, r: DRel, attr, union) -> DRel:
+        import pyarrow.compute as pc
+        import torch
+        name = r.colmap[attr.expr_id]
+        t = r.table
+        cache = t.__dict__.setdefault("_remap", {})
+        hit = cache.get((name, id(union)))
+        if hit is None or hit[0] is not union:
+            c = t.columns[name]
+            pos = pc.index_in(c.dictionary.cast(pa.string()), value_set=union)
+            remap = torch.from_numpy(pos.to_numpy(zero_copy_only=False).astype(np.int32)) \
+                .to(self.device)
+            data = remap[c.data.long()] if len(pos) else torch.zeros_like(c.data)
+            cols = dict(t.columns)
+            cols[name] = DeviceColumn(data, c.valid, c.atype, union)
+            nt = DeviceTable(cols, t.num_rows, t.bucket_offsets, t.bucket_offsets_host)
+            for a in ("global_key", "_full_ranges"):
+                if a in t.__dict__:
+                    nt.__dict__[a] = t.__dict__[a]
+            hit = (union, nt)
+            cache[(name, id(union))] = hit
+        return r.copy(table=hit[1])
 
     def _join_params(self, left: DRel, right: DRel, lk, rk, residual, extra_attrs=(),
                      lconds=None):

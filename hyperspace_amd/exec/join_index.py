@@ -55,9 +55,11 @@ def right_keys_unique(table: DeviceTable, col: DeviceColumn) -> bool:
 
 def eligible(left_table: DeviceTable, right_table: DeviceTable, lcol: DeviceColumn,
              rcol: DeviceColumn) -> bool:
-    if lcol.is_float or rcol.is_float or lcol.dictionary is not None or \
-            rcol.dictionary is not None:
+    if lcol.is_float or rcol.is_float:
         return False
+    if (lcol.dictionary is None) != (rcol.dictionary is None) or \
+            (lcol.dictionary is not None and lcol.dictionary is not rcol.dictionary):
+        return False   # string keys: only codes into one shared (unified) dictionary compare
     if right_table.num_rows >= 2 ** 31 - 1:
         return False
     return right_keys_unique(right_table, rcol)

@@ -163,3 +163,37 @@ def test_join_index_encodings(data, monkeypatch, coded, codings):
     widths = {ji.width for t in s.backend().cache._lru.values()
               for (_, _, _, ji) in t.__dict__.get("_join_index", {}).values()}
     assert widths == {codings[0][0] if coded else 4}
+
+
+def test_string_join_keys_on_device(tmp_path, device):
+    """Joins on string keys run natively: both sides' dictionary codes are remapped into the
+    sorted union of the two dictionaries (order-preserving), then the join index applies."""
+    rng = np.random.default_rng(2)
+    names = np.array([f"cust#{i:06d}" for i in rng.permutation(5000)])
+    cust = pa.table({"c_name": names, "c_seg": pa.array(rng.choice(["AUTO", "BUILD", "MACH"], 5000))})
+    on = rng.choice(names, 20000)
+    on[:300] = [f"ghost#{i}" for i in range(300)]              # keys with no customer
+    valid = rng.random(20000) > 0.02
+    ords = pa.table({"o_cname": pa.array(on, mask=~valid),
+                     "o_total": np.round(rng.random(20000) * 1e4, 2)})
+    for name, t in (("cust", cust), ("ords", ords)):
+        os.makedirs(tmp_path / name)
+        pq.write_table(t, tmp_path / name / "p0.parquet")
+    s = Session(conf={"spark.hyperspace.system.path": str(tmp_path / "idx"),
+                      "spark.hyperspace.index.numBuckets": "8",
+                      "spark.sql.autoBroadcastJoinThreshold": "-1",
+                      "spark.hyperspace.mi.execution.device": "gpu"},
+                warehouse_dir=str(tmp_path / "wh"))
+    hs = Hyperspace(s)
+    c = s.read.parquet(str(tmp_path / "cust"))
+    o = s.read.parquet(str(tmp_path / "ords"))
+    hs.createIndex(c, IndexConfig("c_name_idx", ["c_name"], ["c_seg"]))
+    hs.createIndex(o, IndexConfig("o_cname_idx", ["o_cname"], ["o_total"]))
+    Hyperspace.enable(s)
+    for lim in (2000.0, 7000.0):
+        q = o.join(c, o["o_cname"] == c["c_name"]).filter(col("o_total") < lim) \
+            .groupBy("c_seg").agg(sum_(col("o_total")).alias("t"), count("*").alias("n"))
+        g, p = _run(s, q)
+        assert p == "native", s.backend().fallback_reason
+        cpu, _ = _run(s, q, device="cpu")
+        _close(g, cpu)
