@@ -241,7 +241,14 @@ def config_hybrid(args):
     li, od = s.read.parquet(lpath), s.read.parquet(opath)
     for i in range(2):
         step(2000 + i)
+    from hyperspace_amd.utils.tracing import TRACER, format_report
+    TRACER.reset()
     el_r = _timed_loop(step, args.steps, args.device)
+    if TRACER.profile:   # HS_PROFILE=1: where the refreshed-index steps spend their time
+        print("[hybrid] refreshed stage profile\n" + format_report(TRACER.report()),
+              file=sys.stderr, flush=True)
+        for q in (_q6(li, 0), _q3(li, od, 0)):
+            print(q.queryExecution.executed_plan.tree_string(), file=sys.stderr, flush=True)
     ref = (_q6(li, 0).collect()[0][0], _rows(_q3(li, od, 0)))
     match = abs(hyb[0] - ref[0]) <= 1e-9 * abs(ref[0]) and _close(hyb[1], ref[1])
     return {"config": "hybrid", "device": args.device, "sf": sf, "appended_files": extra,

@@ -146,3 +146,26 @@ def test_spmd_device_executor(tmp_path, spmd_data, device):
         assert [tuple(x) for x in d["join_s"]] == exp_sm
         assert [tuple(x) for x in d["filter"]] == flt
         assert "Name: i1" in d["join_w_plan"]
+
+
+def test_bench_two_ranks_reports_both_placements(tmp_path):
+    """bench.py under torch.distributed (2 gloo ranks, host engine, tiny scale factor): one JSON
+    line from rank 0 with the replicated (weak-scaling) value and the sharded numbers, and the
+    indexed results cross-checked against the un-indexed plan."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(29000 + os.getpid() % 2000),
+           os.path.join(root, "bench.py"), "--gpus", "2", "--device", "cpu", "--sf", "0.02",
+           "--steps", "2", "--warmup", "1", "--buckets", "4", "--data-dir", str(tmp_path)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["config"]["placement"] == "replicated" and out["scaling"] == "weak"
+    assert out["sharded"]["scaling"] == "strong" and out["sharded"]["value"] > 0
+    assert out["steps"] == 2 and out["crosscheck"]["index_vs_full_scan_match"]
