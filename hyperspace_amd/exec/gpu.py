@@ -533,17 +533,18 @@ class GpuBackend:
     def _join_inputs(self, p: X.SortMergeJoinExec):
         if p.join_type != "inner":
             raise Unsupported(f"{p.join_type} join on device")
-        if len(p.left_keys) != 1 or not isinstance(p.left_keys[0], E.Attribute) or \
-                not isinstance(p.right_keys[0], E.Attribute):
-            raise Unsupported("multi-key / expression join keys")
+        if not all(isinstance(k, E.Attribute) for k in list(p.left_keys) + list(p.right_keys)):
+            raise Unsupported("expression join keys")
         left, right = self._rel(p.left), self._rel(p.right)
         if not (left.bucketed and right.bucketed) or left.num_buckets != right.num_buckets:
             raise Unsupported("join inputs not co-partitioned on device")
-        lk, rk = p.left_keys[0], p.right_keys[0]
-        if not _prefix_sorted(left, [lk]):
+        if not _prefix_sorted(left, list(p.left_keys)):
             raise Unsupported("left not sorted by join key")
-        if not _prefix_sorted(right, [rk]):
+        if not _prefix_sorted(right, list(p.right_keys)):
             raise Unsupported("right not sorted by join key")
+        if len(p.left_keys) > 1:
+            return self._packed_join_keys(left, right, list(p.left_keys), list(p.right_keys))
+        lk, rk = p.left_keys[0], p.right_keys[0]
         kinds = set()
         strings = []
         for side, k in ((left, lk), (right, rk)):
@@ -558,6 +559,58 @@ class GpuBackend:
         elif len(kinds) > 1:
             raise Unsupported("mixed int/float join keys")
         return left, right, lk, rk
+
+    def _packed_join_keys(self, left: DRel, right: DRel, lks, rks):
+        """Multi-column equi-join (e.g. ``(l_partkey, l_suppkey) = (ps_partkey, ps_suppkey)``):
+        both sides are sorted by the key columns inside every bucket, so packing the integer
+        keys into one 64-bit value — ``(k1 - lo1) << bits2 | (k2 - lo2)`` with the SAME bases
+        and widths on both sides — preserves the lexicographic order and equality.  The packed
+        column (null if any component is null) is cached on each table, and the single-key join
+        machinery (merge join or join index) runs on it."""
+        if left.parts or right.parts:
+            raise Unsupported("multi-key join over a bucket union")
+        lcs, rcs = [left.col(k) for k in lks], [right.col(k) for k in rks]
+        if any(c.is_float or c.dictionary is not None for c in lcs + rcs):
+            raise Unsupported("multi-key join on float / string keys")
+        spans = []
+        for lc, rc in zip(lcs, rcs):
+            doms = [d for d in (self._local_domain(lc), self._local_domain(rc)) if d[1] > 0]
+            lo = min((d[0] for d in doms), default=0)
+            hi = max((d[0] + d[1] - 1 for d in doms), default=0)
+            spans.append((lo, max(1, int(hi - lo).bit_length())))
+        if sum(b for _, b in spans) > 62:
+            raise Unsupported("multi-key join keys do not pack into 64 bits")
+        spec = tuple(spans)
+        nl = self._packed(left, lks, spec)
+        nr = self._packed(right, rks, spec)
+        la = E.Attribute("__hs_jkey", pa.int64(), True)
+        ra = E.Attribute("__hs_jkey", pa.int64(), True)
+        nl.colmap[la.expr_id] = "__hs_jkey"
+        nr.colmap[ra.expr_id] = "__hs_jkey"
+        return nl, nr, la, ra
+
+    def _packed(self, r: DRel, keys, spec) -> DRel:
+        import torch
+        t = r.table
+        names = tuple(r.colmap[k.expr_id] for k in keys)
+        cache = t.__dict__.setdefault("_packed_keys", {})
+        nt = cache.get((names, spec))
+        if nt is None:
+            packed = torch.zeros(t.num_rows, dtype=torch.int64, device=self.device)
+            valid = None
+            for name, (lo, bits) in zip(names, spec):
+                c = t.columns[name]
+                packed = (packed << bits) | (c.data.long() - lo)
+                if c.valid is not None:
+                    valid = c.valid.clone() if valid is None else valid & c.valid
+            cols = dict(t.columns)
+            cols["__hs_jkey"] = DeviceColumn(packed, valid, pa.int64())
+            nt = DeviceTable(cols, t.num_rows, t.bucket_offsets, t.bucket_offsets_host)
+            for a in ("global_key", "_full_ranges"):
+                if a in t.__dict__:
+                    nt.__dict__[a] = t.__dict__[a]
+            cache[(names, spec)] = nt
+        return r.copy(table=nt, colmap=dict(r.colmap))
 
     def _string_join_keys(self, left: DRel, right: DRel, lk, rk):
         """Join on string keys.  Strings live in HBM as codes into per-table *sorted*

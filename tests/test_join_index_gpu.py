@@ -197,3 +197,42 @@ def test_string_join_keys_on_device(tmp_path, device):
         assert p == "native", s.backend().fallback_reason
         cpu, _ = _run(s, q, device="cpu")
         _close(g, cpu)
+
+
+def test_multi_key_join_on_device(tmp_path, device):
+    """(k1, k2) equi-joins of two indexes bucketed and sorted by (k1, k2) run natively on a packed
+    order-preserving 64-bit key (here through the join index: the right pairs are unique)."""
+    rng = np.random.default_rng(4)
+    n_ps = 20000
+    pk = rng.integers(1, 3000, n_ps).astype(np.int64)
+    sk = rng.integers(1, 50, n_ps).astype(np.int32)
+    pairs = np.unique(np.stack([pk, sk.astype(np.int64)], 1), axis=0)
+    ps = pa.table({"ps_partkey": pairs[:, 0], "ps_suppkey": pairs[:, 1].astype(np.int32),
+                   "ps_cost": np.round(rng.random(len(pairs)) * 100, 2)})
+    pick = rng.integers(0, len(pairs), 60000)
+    lpk, lsk = pairs[pick, 0].copy(), pairs[pick, 1].astype(np.int32)
+    lsk[:500] = 99                                        # pairs with no partsupp row
+    li = pa.table({"l_partkey": lpk, "l_suppkey": pa.array(lsk, mask=rng.random(60000) < 0.01),
+                   "l_qty": rng.integers(1, 50, 60000).astype(np.float64)})
+    for name, t in (("ps", ps), ("li", li)):
+        os.makedirs(tmp_path / name)
+        pq.write_table(t, tmp_path / name / "p0.parquet")
+    s = Session(conf={"spark.hyperspace.system.path": str(tmp_path / "idx"),
+                      "spark.hyperspace.index.numBuckets": "8",
+                      "spark.sql.autoBroadcastJoinThreshold": "-1",
+                      "spark.hyperspace.mi.execution.device": "gpu"},
+                warehouse_dir=str(tmp_path / "wh"))
+    hs = Hyperspace(s)
+    a = s.read.parquet(str(tmp_path / "li"))
+    b = s.read.parquet(str(tmp_path / "ps"))
+    hs.createIndex(a, IndexConfig("li_ps", ["l_partkey", "l_suppkey"], ["l_qty"]))
+    hs.createIndex(b, IndexConfig("ps_ps", ["ps_partkey", "ps_suppkey"], ["ps_cost"]))
+    Hyperspace.enable(s)
+    j = a.join(b, (a["l_partkey"] == b["ps_partkey"]) & (a["l_suppkey"] == b["ps_suppkey"]))
+    for q in (j.filter(col("ps_cost") < 50).agg(sum_(col("l_qty") * col("ps_cost")).alias("v"),
+                                                 count("*").alias("n")),
+              j.filter(col("l_qty") > 25).select("l_partkey", "l_suppkey", "ps_cost")):
+        g, p = _run(s, q)
+        assert p == "native", s.backend().fallback_reason
+        c, _ = _run(s, q, device="cpu")
+        _close(g, c)
