@@ -42,9 +42,15 @@ def _files_key(files) -> tuple:
 
 
 class DeviceTableCache:
+    """LRU of resident tables under an HBM byte budget.  A table's footprint includes what
+    queries derive from it and keep on it (compacted column copies, join indexes, packed /
+    remapped key tables — ``DeviceTable.resident_bytes``), re-measured on every hit, so the
+    budget bounds what is really resident, not just the columns as loaded."""
+
     def __init__(self, budget_bytes: int):
         self.budget = int(budget_bytes)
         self._lru: "OrderedDict[tuple, DeviceTable]" = OrderedDict()
+        self._size: Dict[tuple, int] = {}
         self._bytes = 0
         self._lock = threading.Lock()
         self.hits = 0
@@ -54,6 +60,17 @@ class DeviceTableCache:
         fk = _files_key(files)
         return (fk, tuple(columns), extra)
 
+    def _evict(self, keep) -> None:
+        while self._bytes > self.budget and len(self._lru) > 1:
+            k, _ = next(iter(self._lru.items()))
+            if k == keep:
+                self._lru.move_to_end(k)
+                k, _ = next(iter(self._lru.items()))
+                if k == keep:
+                    break
+            self._lru.pop(k)
+            self._bytes -= self._size.pop(k, 0)
+
     def get(self, files, columns, extra, loader) -> DeviceTable:
         key = self._key(files, columns, extra)
         with self._lock:
@@ -61,22 +78,30 @@ class DeviceTableCache:
             if t is not None:
                 self._lru.move_to_end(key)
                 self.hits += 1
+                nb = t.resident_bytes()
+                self._bytes += nb - self._size.get(key, nb)
+                self._size[key] = nb
+                self._evict(key)
                 return t
         self.misses += 1
         t = loader()
-        nb = t.nbytes()
+        nb = t.resident_bytes()
         with self._lock:
             if self.budget > 0 and nb <= self.budget:
                 self._lru[key] = t
+                self._size[key] = nb
                 self._bytes += nb
-                while self._bytes > self.budget and len(self._lru) > 1:
-                    _, old = self._lru.popitem(last=False)
-                    self._bytes -= old.nbytes()
+                self._evict(key)
         return t
+
+    @property
+    def resident_bytes(self) -> int:
+        return self._bytes
 
     def clear(self):
         with self._lock:
             self._lru.clear()
+            self._size.clear()
             self._bytes = 0
 
 

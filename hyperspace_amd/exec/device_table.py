@@ -172,6 +172,27 @@ class DeviceTable:
     def nbytes(self) -> int:
         return sum(c.nbytes() for c in self.columns.values())
 
+    def resident_bytes(self) -> int:
+        """Columns plus the structures queries derive from this table and keep on it:
+        compacted copies (exec/encoding.py), join indexes (exec/join_index.py), packed
+        multi-key and remapped string-key tables (exec/gpu.py) — what stays in HBM with it."""
+        n = 0
+        for c in self.columns.values():
+            n += c.nbytes()
+            comp = getattr(c, "compact", None)
+            if comp:
+                n += comp.nbytes()
+        d = self.__dict__
+        for (_, _, _, ji) in d.get("_join_index", {}).values():
+            n += ji.nbytes()
+        for t in d.get("_packed_keys", {}).values():
+            n += t.columns["__hs_jkey"].nbytes() + sum(
+                ji.nbytes() for (_, _, _, ji) in t.__dict__.get("_join_index", {}).values())
+        for (_, t) in d.get("_remap", {}).values():
+            n += sum(c.nbytes() for k, c in t.columns.items() if c is not self.columns.get(k))
+            n += sum(ji.nbytes() for (_, _, _, ji) in t.__dict__.get("_join_index", {}).values())
+        return n
+
     @staticmethod
     def from_arrow(t: pa.Table, device, dictionaries: Optional[dict] = None) -> "DeviceTable":
         cols = {}

@@ -577,39 +577,43 @@ class GpuBackend:
             doms = [d for d in (self._local_domain(lc), self._local_domain(rc)) if d[1] > 0]
             lo = min((d[0] for d in doms), default=0)
             hi = max((d[0] + d[1] - 1 for d in doms), default=0)
-            spans.append((lo, max(1, int(hi - lo).bit_length())))
+            # codes: 0 = null on the left, 1 = null on the right, 2 + (v - lo) = value
+            spans.append((lo, max(1, int(hi - lo + 2).bit_length())))
         if sum(b for _, b in spans) > 62:
             raise Unsupported("multi-key join keys do not pack into 64 bits")
         spec = tuple(spans)
-        nl = self._packed(left, lks, spec)
-        nr = self._packed(right, rks, spec)
+        nl = self._packed(left, lks, spec, 0)
+        nr = self._packed(right, rks, spec, 1)
         la = E.Attribute("__hs_jkey", pa.int64(), True)
         ra = E.Attribute("__hs_jkey", pa.int64(), True)
         nl.colmap[la.expr_id] = "__hs_jkey"
         nr.colmap[ra.expr_id] = "__hs_jkey"
         return nl, nr, la, ra
 
-    def _packed(self, r: DRel, keys, spec) -> DRel:
+    def _packed(self, r: DRel, keys, spec, side: int) -> DRel:
+        """``side`` 0/1 = the code of a null component on this side: nulls sort first within
+        their prefix (the index order, NULLS FIRST) and never equal anything on the other side,
+        so the packed column is sorted per bucket and needs no validity mask."""
         import torch
         t = r.table
         names = tuple(r.colmap[k.expr_id] for k in keys)
         cache = t.__dict__.setdefault("_packed_keys", {})
-        nt = cache.get((names, spec))
+        nt = cache.get((names, spec, side))
         if nt is None:
             packed = torch.zeros(t.num_rows, dtype=torch.int64, device=self.device)
-            valid = None
             for name, (lo, bits) in zip(names, spec):
                 c = t.columns[name]
-                packed = (packed << bits) | (c.data.long() - lo)
+                code = c.data.long() - (lo - 2)
                 if c.valid is not None:
-                    valid = c.valid.clone() if valid is None else valid & c.valid
+                    code = torch.where(c.valid.bool(), code, torch.full_like(code, side))
+                packed = (packed << bits) | code
             cols = dict(t.columns)
-            cols["__hs_jkey"] = DeviceColumn(packed, valid, pa.int64())
+            cols["__hs_jkey"] = DeviceColumn(packed, None, pa.int64())
             nt = DeviceTable(cols, t.num_rows, t.bucket_offsets, t.bucket_offsets_host)
             for a in ("global_key", "_full_ranges"):
                 if a in t.__dict__:
                     nt.__dict__[a] = t.__dict__[a]
-            cache[(names, spec)] = nt
+            cache[(names, spec, side)] = nt
         return r.copy(table=nt, colmap=dict(r.colmap))
 
     def _string_join_keys(self, left: DRel, right: DRel, lk, rk):
