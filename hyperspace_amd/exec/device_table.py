@@ -188,6 +188,8 @@ class DeviceTable:
         for t in d.get("_packed_keys", {}).values():
             n += t.columns["__hs_jkey"].nbytes() + sum(
                 ji.nbytes() for (_, _, _, ji) in t.__dict__.get("_join_index", {}).values())
+        for t in d.get("_repart", {}).values():
+            n += t.resident_bytes()
         for (_, t) in d.get("_remap", {}).values():
             n += sum(c.nbytes() for k, c in t.columns.items() if c is not self.columns.get(k))
             n += sum(ji.nbytes() for (_, _, _, ji) in t.__dict__.get("_join_index", {}).values())

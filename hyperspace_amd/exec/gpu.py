@@ -461,6 +461,11 @@ class GpuBackend:
             # this many buckets (same Murmur3 + pmod) and sorted inside each bucket — the
             # exchange the planner asked for would reproduce exactly this layout
             return r
+        if (d is None or d.world == 1) and not r.parts and not r.split and \
+                getattr(r.table, "global_key", None) is not None:
+            cached = self._repartition_cached(r, keys, part.num_partitions)
+            if cached is not None:
+                return cached
         cols = self._materialize(r, list(dict.fromkeys(r.attrs + keys)))
         kcols = [cols[k.expr_id] for k in keys]
         for c in kcols:
@@ -485,6 +490,39 @@ class GpuBackend:
                             torch.from_numpy(off_host).to(self.device), off_host)
         colmap = {i: f"c{i}" for i in names}
         return DRel(table, colmap, list(r.attrs), [], True, keys, keys, B)
+
+    def _repartition_cached(self, r: DRel, keys, B: int) -> Optional[DRel]:
+        """Single rank, resident source table (e.g. the appended files of a Hybrid Scan): the
+        bucketed + sorted layout of the *unfiltered* rows depends only on the table, so it is
+        built once and cached on the table; the query's filters stay pending on the result
+        and run inside the consuming kernel.  Queries with new literals reuse the layout."""
+        need = list(dict.fromkeys(list(r.attrs) + list(keys) +
+                                  [a for c in r.conds for a in c.references()]))
+        if any(a.expr_id not in r.colmap for a in need):
+            return None
+        names = sorted({r.colmap[a.expr_id] for a in need})
+        knames = tuple(r.colmap[k.expr_id] for k in keys)
+        t = r.table
+        if any(t.columns[n].dictionary is not None for n in knames):
+            return None
+        cache = t.__dict__.setdefault("_repart", {})
+        ck = (tuple(names), knames, B)
+        nt = cache.get(ck)
+        if nt is None:
+            import torch
+            kcols = [t.columns[n] for n in knames]
+            with stage("shuffle.hash"):
+                bucket, counts = K.murmur3_bucket(kcols, B)
+            with stage("shuffle.sort"):
+                perm = K.sort_permutation(kcols, extra_leading=(bucket, 16))
+            gathered = K.gather_columns([t.columns[n] for n in names], perm)
+            off_host = np.concatenate([[0], np.cumsum(counts.cpu().numpy())]).astype(np.int64)
+            nt = DeviceTable(dict(zip(names, gathered)), t.num_rows,
+                             torch.from_numpy(off_host).to(self.device), off_host)
+            nt.global_key = ("repartition", t.global_key, ck)
+            cache[ck] = nt
+        colmap = {a.expr_id: r.colmap[a.expr_id] for a in need}
+        return DRel(nt, colmap, list(r.attrs), list(r.conds), True, list(keys), list(keys), B)
 
     def _exchange_rows(self, d, cols: Dict[int, DeviceColumn], bucket):
         """Route every row to rank ``bucket % world`` (all-to-all per column).  Ranks first agree

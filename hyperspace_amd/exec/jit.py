@@ -257,11 +257,15 @@ def _ident(kind: int) -> str:
 class _Gen:
     """Expression builder over column slots of one or two row variables."""
 
-    def __init__(self, args: Args, cols: Dict[int, tuple], split: int, rows: Tuple[str, str]):
+    def __init__(self, args: Args, cols: Dict[int, tuple], split: int, rows: Tuple[str, str],
+                 approx=frozenset()):
         self.a = args
         self.cols = cols          # slot -> (hs_type, has_valid, compact signature or None)
         self.split = split
         self.rows = rows          # row variable for slot < split / >= split
+        # decimal-scaled compact slots read only by SUM/COUNT: decode with a reciprocal
+        # multiply (<= 1 ulp) instead of an exact f64 division (~12 VALU instructions)
+        self.approx = approx
 
     def row(self, slot: int) -> str:
         return self.rows[1] if slot >= self.split else self.rows[0]
@@ -292,6 +296,9 @@ class _Gen:
         ct = _CTYPE[t]
         base = self.a.add("q", f"B{slot}", "long long")
         if enc[1]:
+            if slot in self.approx:
+                inv = self.a.add("d", f"R{slot}", "double")
+                return f"({ct})((double)({base} + (i64){raw}) * {inv})"
             scale = self.a.add("d", f"Q{slot}", "double")
             return f"({ct})((double)({base} + (i64){raw}) / {scale})"
         return f"({ct})({base} + (i64){raw})"
@@ -366,6 +373,23 @@ class _Gen:
         return " * ".join(terms) or "1.0", " && ".join(oks) or "true"
 
 
+def _sum_only_slots(preds, aggs, group_col: int = -1) -> frozenset:
+    """Slots read only as terms of SUM / COUNT aggregates (not by a predicate, MIN/MAX or the
+    group key): their values may carry a 1-ulp decode error, which a floating-point sum's own
+    rounding already dominates.  Predicates and MIN/MAX keep exact decoding."""
+    exact = set(_pred_slots(preds))
+    if group_col >= 0:
+        exact.add(group_col)
+    summed = set()
+    for a in aggs:
+        cols = [a.col[t] for t in range(a.nterms)]
+        if a.kind in (NL.AK_SUM, NL.AK_COUNT):
+            summed.update(cols)
+        elif a.kind != NL.AK_COUNT_STAR:
+            exact.update(cols)
+    return frozenset(summed - exact)
+
+
 def _pred_slots(preds) -> List[int]:
     s = []
     for _, p in preds:
@@ -395,8 +419,8 @@ def _accumulate(gen: _Gen, aggs, grouped: bool, pass_var: str, gvar: str, ind: s
                 out.append(f"{ind}  if (ok) {{ acc{i} = fmin(acc{i}, v); cnt{i} += 1u; }} }}")
             elif a.kind == NL.AK_MAX:
                 out.append(f"{ind}  if (ok) {{ acc{i} = fmax(acc{i}, v); cnt{i} += 1u; }} }}")
-            else:
-                out.append(f"{ind}  if (ok) {{ acc{i} += v; cnt{i} += 1u; }} }}")
+            else:   # v is 0.0 when !ok: no branch
+                out.append(f"{ind}  acc{i} += v; cnt{i} += ok ? 1u : 0u; }}")
             continue
         # wave-peeled grouped accumulation into LDS (one atomic per distinct group per wave)
         out.append(f"{ind}  bool todo = ok;")
@@ -530,6 +554,7 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
     if SCAN_EAGER:
         pslots, aslots = pslots + aslots, []
     allslots = pslots + aslots
+    approx = _sum_only_slots(preds, aggs, p.group_col)
     NI = vec or SCAN_ITEMS
     T = BLOCK * NI
     if vec:
@@ -553,7 +578,7 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
     ind = "    "
     if vec:
         _vec_rows(b, NI, ind)
-        _vec_load_slots(b, _Gen(args, cols, NL.MAX_COLS, ("row0", "row0")), pslots, NI, ind)
+        _vec_load_slots(b, _Gen(args, cols, NL.MAX_COLS, ("row0", "row0"), approx), pslots, NI, ind)
     else:
         b += ["    const i64 tb0 = a.rstart[r] + off;",
               f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};"]
@@ -561,21 +586,21 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
             b += [f"{ind}const bool act{it} = {it * BLOCK} + (i64)threadIdx.x < rows;",
                   f"{ind}const i64 row{it} = tb0 + (act{it} ? {it * BLOCK} + (i64)threadIdx.x : 0);"]
         for it in range(NI):
-            g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"))
+            g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"), approx)
             for s in pslots:
                 _uload(g1, s, it, b, ind)
     for it in range(NI):
-        g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"))
+        g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"), approx)
         b.append(f"{ind}bool pass{it} = act{it} && {_rename(g1.cnf(preds), allslots, it)};")
     if aslots:
         for it in range(NI):
             b.append(f"{ind}const i64 lq{it} = pass{it} ? row{it} : tb0;")
         for it in range(NI):
-            g2 = _Gen(args, cols, NL.MAX_COLS, (f"lq{it}", f"lq{it}"))
+            g2 = _Gen(args, cols, NL.MAX_COLS, (f"lq{it}", f"lq{it}"), approx)
             for s in aslots:
                 _uload(g2, s, it, b, ind)
     for it in range(NI):
-        g2 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"))
+        g2 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"), approx)
         gvar = f"gi{it}"
         if grouped:
             g = p.group_col
@@ -614,6 +639,7 @@ def _fill_common(v: Dict[str, object], cols, preds, aggs, compacts=None) -> None
             if c:
                 v[f"B{s}"] = c.base
                 v[f"Q{s}"] = c.scale or 1.0
+                v[f"R{s}"] = 1.0 / (c.scale or 1.0)
     for k, p in preds:
         v[f"L{k}"] = p.ilit
         v[f"F{k}"] = p.flit
@@ -1085,6 +1111,7 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int = 
              if s not in first and s not in second]
     third = list(dict.fromkeys(third))
     allslots = first + second + third
+    approx = _sum_only_slots(lpreds + rpreds, aggs, p.group_col)
     NI = vec or JI_ITEMS
     T = BLOCK * NI
     if vec:
@@ -1108,7 +1135,7 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int = 
     ind = "    "
     if vec:
         _vec_rows(b, NI, ind)
-        g1 = _Gen(args, cols, split, ("row0", "row0"))
+        g1 = _Gen(args, cols, split, ("row0", "row0"), approx)
         _vec_load_slots(b, g1, first, NI, ind, extra=[("jr", jct, "a.jidx")])
         if jw < 4:   # NI | block size and g0 % NI == 0: the thread's rows share one block
             b.append(f"{ind}const int jb = a.jbase[g0 >> {jlog}];")
@@ -1132,21 +1159,21 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int = 
                          f"a.jbase[row{it} >> {jlog}] + (int)jc{it} : -1;")
             else:
                 b.append(f"{ind}const int jr{it} = a.jidx[row{it}];")
-            g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"))
+            g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"), approx)
             for s in first:
                 _uload(g1, s, it, b, ind)
     for it in range(NI):
-        g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"))
+        g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"), approx)
         cond = _rename(g1.cnf(lpreds), allslots, it)
         b.append(f"{ind}bool pass{it} = act{it} && jr{it} >= 0 && {cond};")
         b.append(f"{ind}const i64 j{it} = pass{it} ? (i64)jr{it} : 0;")
     # phase 2: right predicate columns at the matched rows
     for it in range(NI):
-        g2 = _Gen(args, cols, split, (f"row{it}", f"j{it}"))
+        g2 = _Gen(args, cols, split, (f"row{it}", f"j{it}"), approx)
         for s in second:
             _uload(g2, s, it, b, ind)
     for it in range(NI):
-        g2 = _Gen(args, cols, split, (f"row{it}", f"j{it}"))
+        g2 = _Gen(args, cols, split, (f"row{it}", f"j{it}"), approx)
         b.append(f"{ind}pass{it} = pass{it} && {_rename(g2.cnf(rpreds), allslots, it)};")
     # phase 3: aggregate inputs (rows that failed read the tile's first row / right row 0)
     if third:
@@ -1154,11 +1181,11 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int = 
             b += [f"{ind}const i64 lq{it} = pass{it} ? row{it} : tb0;",
                   f"{ind}const i64 jq{it} = pass{it} ? j{it} : 0;"]
         for it in range(NI):
-            g3 = _Gen(args, cols, split, (f"lq{it}", f"jq{it}"))
+            g3 = _Gen(args, cols, split, (f"lq{it}", f"jq{it}"), approx)
             for s in third:
                 _uload(g3, s, it, b, ind)
     for it in range(NI):
-        g3 = _Gen(args, cols, split, (f"lq{it}", f"jq{it}"))
+        g3 = _Gen(args, cols, split, (f"lq{it}", f"jq{it}"), approx)
         gvar = f"gi{it}"
         if grouped:
             g = p.group_col
