@@ -258,7 +258,7 @@ class _Gen:
     """Expression builder over column slots of one or two row variables."""
 
     def __init__(self, args: Args, cols: Dict[int, tuple], split: int, rows: Tuple[str, str],
-                 approx=frozenset()):
+                 approx=frozenset(), intpred: bool = False):
         self.a = args
         self.cols = cols          # slot -> (hs_type, has_valid, compact signature or None)
         self.split = split
@@ -266,6 +266,10 @@ class _Gen:
         # decimal-scaled compact slots read only by SUM/COUNT: decode with a reciprocal
         # multiply (<= 1 ulp) instead of an exact f64 division (~12 VALU instructions)
         self.approx = approx
+        # predicates on decimal-scaled compact columns compare the integer q = base + code with
+        # host-computed integer bounds (exact, no f64 division); needs the q<s> registers the
+        # phase-major generators emit
+        self.intpred = intpred
 
     def row(self, slot: int) -> str:
         return self.rows[1] if slot >= self.split else self.rows[0]
@@ -327,6 +331,12 @@ class _Gen:
             lit = self.a.add("q", f"L{k}", "long long")
             return f"({self.ok(c)} && ((i64)x{c} {_OPSTR[op]} {lit}))"
         if kind == NL.PK_FLT_LIT:
+            enc = self.cols[c][2]
+            if self.intpred and enc and enc[1]:
+                lo = self.a.add("q", f"T{k}", "long long")
+                hi = self.a.add("q", f"U{k}", "long long")
+                inside = f"(q{c} >= {lo} && q{c} <= {hi})"
+                return f"({self.ok(c)} && {'!' if op == NL.OP_NE else ''}{inside})"
             lit = self.a.add("d", f"F{k}", "double")
             return f"({self.ok(c)} && ((double)x{c} {_OPSTR[op]} {lit}))"
         if kind in (NL.PK_INT_COL, NL.PK_FLT_COL):
@@ -373,11 +383,21 @@ class _Gen:
         return " * ".join(terms) or "1.0", " && ".join(oks) or "true"
 
 
-def _sum_only_slots(preds, aggs, group_col: int = -1) -> frozenset:
-    """Slots read only as terms of SUM / COUNT aggregates (not by a predicate, MIN/MAX or the
-    group key): their values may carry a 1-ulp decode error, which a floating-point sum's own
-    rounding already dominates.  Predicates and MIN/MAX keep exact decoding."""
-    exact = set(_pred_slots(preds))
+def _sum_only_slots(preds, aggs, group_col: int = -1, cols=None) -> frozenset:
+    """Slots whose decoded value is read only as a term of SUM / COUNT aggregates: it may carry
+    a 1-ulp decode error, which a floating-point sum's own rounding already dominates.
+    Predicates (except literal compares on decimal-scaled compact columns, which run on the
+    integer codes), MIN/MAX and the group key keep exact decoding."""
+    exact = set()
+    for _, p in preds:
+        enc = (cols or {}).get(p.col, (None, None, None))[2]
+        if p.kind in (NL.PK_IS_NULL, NL.PK_NOT_NULL, NL.PK_TRUE):
+            continue
+        if p.kind == NL.PK_FLT_LIT and enc and enc[1]:
+            continue
+        exact.add(p.col)
+        if p.kind in (NL.PK_INT_COL, NL.PK_FLT_COL):
+            exact.add(p.col2)
     if group_col >= 0:
         exact.add(group_col)
     summed = set()
@@ -554,7 +574,7 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
     if SCAN_EAGER:
         pslots, aslots = pslots + aslots, []
     allslots = pslots + aslots
-    approx = _sum_only_slots(preds, aggs, p.group_col)
+    approx = _sum_only_slots(preds, aggs, p.group_col, cols)
     NI = vec or SCAN_ITEMS
     T = BLOCK * NI
     if vec:
@@ -578,7 +598,7 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
     ind = "    "
     if vec:
         _vec_rows(b, NI, ind)
-        _vec_load_slots(b, _Gen(args, cols, NL.MAX_COLS, ("row0", "row0"), approx), pslots, NI, ind)
+        _vec_load_slots(b, _Gen(args, cols, NL.MAX_COLS, ("row0", "row0"), approx, True), pslots, NI, ind)
     else:
         b += ["    const i64 tb0 = a.rstart[r] + off;",
               f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};"]
@@ -586,21 +606,21 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
             b += [f"{ind}const bool act{it} = {it * BLOCK} + (i64)threadIdx.x < rows;",
                   f"{ind}const i64 row{it} = tb0 + (act{it} ? {it * BLOCK} + (i64)threadIdx.x : 0);"]
         for it in range(NI):
-            g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"), approx)
+            g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"), approx, True)
             for s in pslots:
                 _uload(g1, s, it, b, ind)
     for it in range(NI):
-        g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"), approx)
+        g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"), approx, True)
         b.append(f"{ind}bool pass{it} = act{it} && {_rename(g1.cnf(preds), allslots, it)};")
     if aslots:
         for it in range(NI):
             b.append(f"{ind}const i64 lq{it} = pass{it} ? row{it} : tb0;")
         for it in range(NI):
-            g2 = _Gen(args, cols, NL.MAX_COLS, (f"lq{it}", f"lq{it}"), approx)
+            g2 = _Gen(args, cols, NL.MAX_COLS, (f"lq{it}", f"lq{it}"), approx, True)
             for s in aslots:
                 _uload(g2, s, it, b, ind)
     for it in range(NI):
-        g2 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"), approx)
+        g2 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"), approx, True)
         gvar = f"gi{it}"
         if grouped:
             g = p.group_col
@@ -630,6 +650,42 @@ def scan_agg_values(p: NL.ScanParams, rstart, rlen, tile_prefix, parts,
     return v
 
 
+_BIG = 1 << 62
+
+
+def int_bounds(op: int, lit: float, scale: float) -> Tuple[int, int]:
+    """[T, U] such that, for every integer q of a decimal-scaled column (value = q / scale,
+    correctly rounded), ``q / scale OP lit`` holds iff ``T <= q <= U`` (``NE``: iff not).
+    Exact: thresholds are found with the same IEEE double division the decode uses."""
+    import math
+    if lit != lit:                                   # NaN compares false (NE: true)
+        return (_BIG, -_BIG)
+    if math.isinf(lit):
+        below = lit > 0                              # every finite value is below +inf
+        if op in (NL.OP_LT, NL.OP_LE):
+            return (-_BIG, _BIG) if below else (_BIG, -_BIG)
+        if op in (NL.OP_GT, NL.OP_GE):
+            return (_BIG, -_BIG) if below else (-_BIG, _BIG)
+        return (_BIG, -_BIG)
+
+    def first(pred) -> int:                          # smallest integer t with pred(t / scale)
+        t = math.floor(lit * scale) - 4
+        while not pred(t / scale):
+            t += 1
+        return t
+    ge = first(lambda x: x >= lit)
+    gt = first(lambda x: x > lit)
+    if op == NL.OP_GE:
+        return (ge, _BIG)
+    if op == NL.OP_GT:
+        return (gt, _BIG)
+    if op == NL.OP_LE:
+        return (-_BIG, gt - 1)
+    if op == NL.OP_LT:
+        return (-_BIG, ge - 1)
+    return (ge, gt - 1)                              # EQ / NE
+
+
 def _fill_common(v: Dict[str, object], cols, preds, aggs, compacts=None) -> None:
     for s in range(NL.MAX_COLS):
         if cols[s].data:
@@ -643,6 +699,9 @@ def _fill_common(v: Dict[str, object], cols, preds, aggs, compacts=None) -> None
     for k, p in preds:
         v[f"L{k}"] = p.ilit
         v[f"F{k}"] = p.flit
+        c = (compacts or {}).get(p.col)
+        if p.kind == NL.PK_FLT_LIT and c is not None and c.scale:
+            v[f"T{k}"], v[f"U{k}"] = int_bounds(p.op, p.flit, c.scale)
         v[f"S{k}"] = p.set or 0
         v[f"N{k}"] = p.set_len
     for i, a in enumerate(aggs):
@@ -935,7 +994,7 @@ def _rename(line: str, slots, it: int) -> str:
     """Suffix per-row-slot variables x<s>/n<s> with the batch item index."""
     import re
     for s in sorted(set(slots), reverse=True):
-        line = re.sub(rf"\b([xn]){s}\b", rf"\g<1>{s}_{it}", line)
+        line = re.sub(rf"\b([xnq]){s}\b", rf"\g<1>{s}_{it}", line)
     return line
 
 
@@ -1028,7 +1087,14 @@ def _uload(gen: _Gen, slot: int, it: int, out: List[str], ind: str) -> None:
     the load needs no branch and the wavefront's redirected lanes coalesce into one line)."""
     ct = _CTYPE[gen.cols[slot][0]]
     r = gen.row(slot)
-    out.append(f"{ind}const {ct} x{slot}_{it} = {gen.value(slot, r)};")
+    enc = gen.cols[slot][2]
+    if enc and enc[1]:
+        base = gen.a.add("q", f"B{slot}", "long long")
+        out.append(f"{ind}const {gen.raw_type(slot)} w{slot}_{it} = {gen.ptr(slot)}[{r}];")
+        out.append(f"{ind}const i64 q{slot}_{it} = {base} + (i64)w{slot}_{it};")
+        out.append(f"{ind}const {ct} x{slot}_{it} = {gen.decode(slot, f'w{slot}_{it}')};")
+    else:
+        out.append(f"{ind}const {ct} x{slot}_{it} = {gen.value(slot, r)};")
     if gen.cols[slot][1]:
         out.append(f"{ind}const bool n{slot}_{it} = {gen.vptr(slot)}[{r}] != 0;")
 
@@ -1062,6 +1128,10 @@ def _vec_load_slots(b: List[str], gen: "_Gen", slots, NI: int, ind: str, extra=(
     for it in range(NI):
         for s in slots:
             ct = _CTYPE[gen.cols[s][0]]
+            enc = gen.cols[s][2]
+            if enc and enc[1]:
+                base = gen.a.add("q", f"B{s}", "long long")
+                b.append(f"{ind}const i64 q{s}_{it} = {base} + (i64)x{s}v[{it}];")
             b.append(f"{ind}const {ct} x{s}_{it} = {gen.decode(s, f'x{s}v[{it}]')};")
             if gen.cols[s][1]:
                 b.append(f"{ind}const bool n{s}_{it} = n{s}v[{it}] != 0;")
@@ -1111,7 +1181,7 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int = 
              if s not in first and s not in second]
     third = list(dict.fromkeys(third))
     allslots = first + second + third
-    approx = _sum_only_slots(lpreds + rpreds, aggs, p.group_col)
+    approx = _sum_only_slots(lpreds + rpreds, aggs, p.group_col, cols)
     NI = vec or JI_ITEMS
     T = BLOCK * NI
     if vec:
@@ -1135,7 +1205,7 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int = 
     ind = "    "
     if vec:
         _vec_rows(b, NI, ind)
-        g1 = _Gen(args, cols, split, ("row0", "row0"), approx)
+        g1 = _Gen(args, cols, split, ("row0", "row0"), approx, True)
         _vec_load_slots(b, g1, first, NI, ind, extra=[("jr", jct, "a.jidx")])
         if jw < 4:   # NI | block size and g0 % NI == 0: the thread's rows share one block
             b.append(f"{ind}const int jb = a.jbase[g0 >> {jlog}];")
@@ -1159,21 +1229,21 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int = 
                          f"a.jbase[row{it} >> {jlog}] + (int)jc{it} : -1;")
             else:
                 b.append(f"{ind}const int jr{it} = a.jidx[row{it}];")
-            g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"), approx)
+            g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"), approx, True)
             for s in first:
                 _uload(g1, s, it, b, ind)
     for it in range(NI):
-        g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"), approx)
+        g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"), approx, True)
         cond = _rename(g1.cnf(lpreds), allslots, it)
         b.append(f"{ind}bool pass{it} = act{it} && jr{it} >= 0 && {cond};")
         b.append(f"{ind}const i64 j{it} = pass{it} ? (i64)jr{it} : 0;")
     # phase 2: right predicate columns at the matched rows
     for it in range(NI):
-        g2 = _Gen(args, cols, split, (f"row{it}", f"j{it}"), approx)
+        g2 = _Gen(args, cols, split, (f"row{it}", f"j{it}"), approx, True)
         for s in second:
             _uload(g2, s, it, b, ind)
     for it in range(NI):
-        g2 = _Gen(args, cols, split, (f"row{it}", f"j{it}"), approx)
+        g2 = _Gen(args, cols, split, (f"row{it}", f"j{it}"), approx, True)
         b.append(f"{ind}pass{it} = pass{it} && {_rename(g2.cnf(rpreds), allslots, it)};")
     # phase 3: aggregate inputs (rows that failed read the tile's first row / right row 0)
     if third:
@@ -1181,11 +1251,11 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int = 
             b += [f"{ind}const i64 lq{it} = pass{it} ? row{it} : tb0;",
                   f"{ind}const i64 jq{it} = pass{it} ? j{it} : 0;"]
         for it in range(NI):
-            g3 = _Gen(args, cols, split, (f"lq{it}", f"jq{it}"), approx)
+            g3 = _Gen(args, cols, split, (f"lq{it}", f"jq{it}"), approx, True)
             for s in third:
                 _uload(g3, s, it, b, ind)
     for it in range(NI):
-        g3 = _Gen(args, cols, split, (f"lq{it}", f"jq{it}"), approx)
+        g3 = _Gen(args, cols, split, (f"lq{it}", f"jq{it}"), approx, True)
         gvar = f"gi{it}"
         if grouped:
             g = p.group_col

@@ -143,7 +143,10 @@ def test_generated_sources_compile_with_compact_columns(rt, tmp_path):
     comp = {0: Compact(None, 1, 0, 100.0, NL.F64), 1: Compact(None, 4, 0, 100.0, NL.F64),
             2: Compact(None, 2, 5, None, NL.I64)}
     k = jit.gen_scan_agg(p, comp)
-    assert "a.Q0" in k.src and "const signed char* c0" in k.src
+    # slot 0: its literal predicate runs on the integer codes (T0/U0), its SUM term decodes with
+    # a reciprocal (R0); no exact division left for it
+    assert "a.T0" in k.src and "a.R0" in k.src and "a.Q0" not in k.src
+    assert "const signed char* c0" in k.src
     rc = jit.runtime().hs_jit_compile_to_cache(k.src.encode(), k.name.encode(), b"gfx950",
                                                str(tmp_path).encode())
     assert rc == 0, jit.runtime().hs_jit_last_error().decode()
@@ -289,3 +292,25 @@ def test_jit_join_agg_matches_aot(device):
         cg = [t.cpu().numpy() for t in jit.join_agg(p, rstart, rlen, rbk, roff_t, mt, comp)]
         np.testing.assert_allclose(cg[0], got[0], rtol=1e-12)
         assert np.array_equal(cg[1], got[1])
+
+
+def test_int_bounds_match_decoded_double_compares():
+    """Integer-code predicates on decimal-scaled compact columns select exactly the rows the
+    decoded double comparison selects (all ops, literals on and between grid points)."""
+    import random
+    from hyperspace_amd.exec.jit import int_bounds
+    rng = random.Random(7)
+    ops = {NL.OP_EQ: lambda a, b: a == b, NL.OP_NE: lambda a, b: a != b,
+           NL.OP_LT: lambda a, b: a < b, NL.OP_LE: lambda a, b: a <= b,
+           NL.OP_GT: lambda a, b: a > b, NL.OP_GE: lambda a, b: a >= b}
+    for scale in (1.0, 10.0, 100.0, 1000.0, 10000.0):
+        qs = list(range(-3000, 3000))
+        lits = [q / scale for q in rng.sample(qs, 40)] + [rng.uniform(-30, 30) for _ in range(40)]
+        lits += [0.05, 0.07, -0.0, float("inf"), float("-inf"), float("nan")]
+        for lit in lits:
+            for op, f in ops.items():
+                lo, hi = int_bounds(op, lit, scale)
+                for q in qs[::7]:
+                    inside = lo <= q <= hi
+                    got = (not inside) if op == NL.OP_NE else inside
+                    assert got == f(q / scale, lit), (scale, lit, op, q)
