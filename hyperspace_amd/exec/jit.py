@@ -54,6 +54,10 @@ JI_ITEMS = int(os.environ.get("HS_JIT_JI_ITEMS", "4"))
 # > 0: each thread of the join-index kernel owns JI_VEC consecutive rows and loads the streamed
 # left columns (join index, predicate columns) as aligned vectors (dwordx4 for 4 int32 rows)
 JI_VEC = int(os.environ.get("HS_JIT_JI_VEC", "8"))
+# join-index kernel: run the aggregate phase over a per-wavefront list of passing rows only
+JI_COMPACT = os.environ.get("HS_JIT_JI_COMPACT", "1") == "1"
+# scan kernel: same, for the aggregate inputs loaded after the predicates
+SCAN_COMPACT = os.environ.get("HS_JIT_SCAN_COMPACT", "1") == "1"
 # > 0: rows per thread of the vectorized scan kernel (aligned vector loads of predicate columns)
 SCAN_VEC = int(os.environ.get("HS_JIT_SCAN_VEC", "8"))
 # software-pipeline the join's tile loop (next tile's batch loads overlap this tile's work)
@@ -547,7 +551,8 @@ def scan_agg_shape(p: NL.ScanParams, compacts=None, vec: int = 0) -> tuple:
                    p.preds[k].group) for k in range(p.npreds))
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
-    return ("scan_agg", cols, preds, aggs, p.group_col, SCAN_ITEMS, SCAN_EAGER, vec)
+    return ("scan_agg", cols, preds, aggs, p.group_col, SCAN_ITEMS, SCAN_EAGER, vec,
+            SCAN_COMPACT)
 
 
 def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
@@ -612,6 +617,19 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
     for it in range(NI):
         g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"), approx, True)
         b.append(f"{ind}bool pass{it} = act{it} && {_rename(g1.cnf(preds), allslots, it)};")
+    if SCAN_COMPACT and aslots:
+        b += _compacted_tail(args, cols, NL.MAX_COLS, approx, aggs, grouped, p.group_col, aslots,
+                             allslots, NI, ind, with_j=False)
+        b += ["  }"]
+        b += _flush(aggs, grouped)
+        W = BLOCK // 64
+        b.insert(0, f"  __shared__ int crow_s[{W}][{64 * NI}];")
+        b.insert(1, "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;")
+        src = (_PRELUDE + args.struct_src() +
+               f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_scan_agg(Args a) {{\n' +
+               "\n".join(b) + "\n}\n")
+        lds = (len(aggs) * p.num_groups * 32) if grouped else 0
+        return Kernel(src, "hs_jit_scan_agg", args, lds)
     if aslots:
         for it in range(NI):
             b.append(f"{ind}const i64 lq{it} = pass{it} ? row{it} : tb0;")
@@ -1078,7 +1096,7 @@ def join_index_agg_shape(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int 
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
     return ("join_index_agg", cols, preds, p.nlp, aggs, p.group_col, JI_ITEMS, vec, BLOCK, jw,
-            jlog)
+            jlog, JI_COMPACT)
 
 
 def _uload(gen: _Gen, slot: int, it: int, out: List[str], ind: str) -> None:
@@ -1139,6 +1157,50 @@ def _vec_load_slots(b: List[str], gen: "_Gen", slots, NI: int, ind: str, extra=(
 
 def _vec_aligned_ptrs(ptrs) -> bool:
     return all(int(x) % 16 == 0 for x in ptrs if x)
+
+
+def _compacted_tail(args, cols, split, approx, aggs, grouped, group_col, third, allslots,
+                    NI: int, ind: str, with_j: bool = True) -> List[str]:
+    """Phase 3 over the passing rows only.  A join like TPC-H Q3 keeps a few percent of its
+    rows, so decoding and accumulating all NI x 64 rows of a wavefront (branch-free) is mostly
+    wasted VALU work: instead each lane appends its passing (row, j) pairs to a per-wavefront
+    LDS list (wavefront prefix sum of the per-lane counts), and the wavefront walks the list 64
+    entries at a time — aggregate loads, decode and accumulation run once per passing row."""
+    b = [f"{ind}int pc = " + " + ".join(f"(int)pass{it}" for it in range(NI)) + ";",
+         f"{ind}int incl = pc;",
+         "#pragma unroll",
+         f"{ind}for (int o = 1; o < 64; o <<= 1) {{ const int y = __shfl_up(incl, o, 64); "
+         "if (cln >= o) incl += y; }",
+         f"{ind}const int wtot = __shfl(incl, 63, 64);",
+         f"{ind}int pos = incl - pc;"]
+    for it in range(NI):
+        cj = f"cj_s[wv][pos] = (int)j{it}; " if with_j else ""
+        b.append(f"{ind}if (pass{it}) {{ crow_s[wv][pos] = (int)(row{it} - tb0); {cj}++pos; }}")
+    b += [f"{ind}__syncthreads();",
+          f"{ind}for (int cb = 0; cb < wtot; cb += 64) {{",
+          f"{ind}  const int ce = cb + cln;",
+          f"{ind}  bool cok = ce < wtot;",
+          f"{ind}  const i64 crow = tb0 + (cok ? crow_s[wv][ce] : 0);",
+          f"{ind}  const i64 cj = cok ? (i64)cj_s[wv][ce] : 0;" if with_j else
+          f"{ind}  const i64 cj = crow;"]
+    ind2 = ind + "  "
+    g = _Gen(args, cols, split, ("crow", "cj"), approx, True)
+    # every slot the aggregates and the group key read, re-loaded at the listed rows (the
+    # phase-1/2 registers belong to the original, uncompacted rows)
+    tail = list(dict.fromkeys(_agg_slots(aggs) + ([group_col] if grouped else [])))
+    for sl in tail:
+        _uload(g, sl, "c", b, ind2)
+    gvar = "gic"
+    if grouped:
+        base = args.add("q", "group_base", "long long")
+        ng = args.add("q", "num_groups", "long long")
+        b.append(f"{ind2}const i64 glc = (i64){_rename(f'x{group_col}', allslots, 'c')} - {base};")
+        b.append(f"{ind2}cok = cok && {_rename(g.ok(group_col), allslots, 'c')} && "
+                 f"glc >= 0 && glc < {ng};")
+        b.append(f"{ind2}const int {gvar} = cok ? (int)glc : 0;")
+    b += [_rename(x, allslots, "c") for x in _accumulate(g, aggs, grouped, "cok", gvar, ind2)]
+    b += [f"{ind}}}", f"{ind}__syncthreads();"]
+    return b
 
 
 def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int = 4,
@@ -1245,6 +1307,19 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int = 
     for it in range(NI):
         g2 = _Gen(args, cols, split, (f"row{it}", f"j{it}"), approx, True)
         b.append(f"{ind}pass{it} = pass{it} && {_rename(g2.cnf(rpreds), allslots, it)};")
+    if JI_COMPACT and third:
+        b += _compacted_tail(args, cols, split, approx, aggs, grouped, p.group_col, third,
+                             allslots, NI, ind)
+        b += ["  }"]
+        b += _flush(aggs, grouped)
+        W = BLOCK // 64
+        b.insert(0, f"  __shared__ int crow_s[{W}][{64 * NI}]; __shared__ int cj_s[{W}][{64 * NI}];")
+        b.insert(1, "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;")
+        src = (_PRELUDE + args.struct_src() +
+               f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_join_index_agg(Args a) {{\n' +
+               "\n".join(b) + "\n}\n")
+        lds = (len(aggs) * p.num_groups * 32) if grouped else 0
+        return Kernel(src, "hs_jit_join_index_agg", args, lds)
     # phase 3: aggregate inputs (rows that failed read the tile's first row / right row 0)
     if third:
         for it in range(NI):
