@@ -174,6 +174,11 @@ def _subst(v, m: Dict[int, E.Literal], hot: set, memo: Dict[int, object]):
     return out
 
 
+def _same(a: E.Literal, b: E.Literal) -> bool:
+    """Same value and type (so the cached plan's literal object can stay)."""
+    return type(a.value) is type(b.value) and a.value == b.value and a.dtype == b.dtype
+
+
 class PlanCache:
     def __init__(self, capacity: int = CAPACITY):
         self.capacity = capacity
@@ -210,12 +215,16 @@ class PlanCache:
         if hit is None:
             self.misses += 1
             return None, key, ctx
-        plan, old_lits, hot, _refs = hit
+        plan, old_lits, paths, _refs = hit
         if len(old_lits) != len(ctx.lits):
             self.misses += 1
             return None, key, ctx
-        m = {id(o): n for o, n in zip(old_lits, ctx.lits) if o is not n}
-        new_plan = _subst(plan, m, hot, {}) if m else plan
+        # only literals whose value changed are substituted, along their own paths
+        m = {id(o): n for o, n in zip(old_lits, ctx.lits) if o is not n and not _same(o, n)}
+        new_plan = plan
+        if m:
+            hot = set().union(*(paths[k] for k in m))
+            new_plan = _subst(plan, m, hot, {})
         self.hits += 1
         return new_plan, key, ctx
 
@@ -229,10 +238,14 @@ class PlanCache:
         if not all(id(x) in ids for x in ctx.lits):
             self.uncacheable += 1
             return False
-        hot: set = set()
-        _hot_paths(executed, {id(x) for x in ctx.lits}, hot, {})
+        paths = {}
+        for x in ctx.lits:
+            if id(x) not in paths:
+                hot: set = set()
+                _hot_paths(executed, {id(x)}, hot, {})
+                paths[id(x)] = hot
         with self._lock:
-            self._lru[key] = (executed, list(ctx.lits), hot, list(ctx.refs))
+            self._lru[key] = (executed, list(ctx.lits), paths, list(ctx.refs))
             while len(self._lru) > self.capacity:
                 self._lru.popitem(last=False)
         return True
