@@ -243,7 +243,13 @@ def config_hybrid(args):
         step(2000 + i)
     from hyperspace_amd.utils.tracing import TRACER, format_report
     TRACER.reset()
+    be = s.backend()
+    cache0 = (be.cache.hits, be.cache.misses) if hasattr(be, "cache") else (0, 0)
     el_r = _timed_loop(step, args.steps, args.device)
+    cache1 = (be.cache.hits, be.cache.misses, round(be.cache.resident_bytes / 1e9, 1)) \
+        if hasattr(be, "cache") else (0, 0, 0)
+    print(f"[hybrid] refreshed loop device cache hits/misses {cache0} -> {cache1}",
+          file=sys.stderr, flush=True)
     if TRACER.profile:   # HS_PROFILE=1: where the refreshed-index steps spend their time
         print("[hybrid] refreshed stage profile\n" + format_report(TRACER.report()),
               file=sys.stderr, flush=True)

@@ -149,9 +149,50 @@ def _finish_strings(host_strings: Dict[str, list], cols: Dict[str, DeviceColumn]
     """Dictionary-encode string columns with a job-global sorted dictionary and upload codes."""
     for name, chunks in host_strings.items():
         chunks = [c for c in chunks if c is not None]
+        if name not in indexed and chunks and \
+                all(pa.types.is_dictionary(c.type) for c in chunks):
+            cols[name] = _dictionary_codes(chunks, device, dist)
+            continue
         arr = pa.chunked_array(chunks, type=chunks[0].type) if chunks else pa.chunked_array([], pa.string())
+        if pa.types.is_dictionary(arr.type):
+            arr = arr.cast(pa.string())
         d = _global_dicts(pa.table({name: arr}), dist)[name]
         cols[name] = DeviceColumn.from_arrow(arr, device, d, raw_strings=name in indexed)
+
+
+def _dictionary_codes(chunks, device, dist) -> DeviceColumn:
+    """String column read as Parquet dictionary pages + indices (never materialised as strings
+    on the host): the job-global sorted dictionary is the union of the (small) per-chunk
+    dictionaries; each chunk's indices cross PCIe as int32 and are remapped to global codes
+    on the device with one gather through that chunk's local -> global table."""
+    import torch
+    parts = [ch for c in chunks for ch in c.chunks]
+    local = [ch.dictionary.cast(pa.string()) for ch in parts]
+    u = pc.unique(pa.concat_arrays(local)) if local else pa.array([], pa.string())
+    if dist is not None and dist.world > 1:
+        all_vals = dist.all_gather_object(u.to_pylist())
+        u = pa.array(sorted(set(x for p in all_vals for x in p)), pa.string())
+    gdict = u.sort()
+    n = sum(len(ch) for ch in parts)
+    codes = torch.empty(n, dtype=torch.int32, device=device)
+    valid = None
+    if any(ch.null_count for ch in parts):
+        valid = torch.ones(n, dtype=torch.uint8, device=device)
+    off = 0
+    for ch, d in zip(parts, local):
+        m = len(ch)
+        if m:
+            remap = pc.index_in(d, value_set=gdict).to_numpy(zero_copy_only=False)
+            remap_d = torch.from_numpy(np.asarray(remap, dtype=np.int32)).to(device)
+            idx = np.asarray(ch.indices.fill_null(0).to_numpy(zero_copy_only=False),
+                             dtype=np.int64)
+            idx_d = torch.from_numpy(idx).to(device, non_blocking=False)
+            codes[off:off + m] = remap_d[idx_d] if len(d) else 0
+            if ch.null_count:
+                vm = np.asarray(ch.is_valid().to_numpy(zero_copy_only=False), dtype=np.uint8)
+                valid[off:off + m] = torch.from_numpy(vm).to(device)
+        off += m
+    return DeviceColumn(codes, valid, pa.string(), gdict)
 
 
 def _upload_parquet(rel, my_files, columns, indexed, lineage_ids, device, dist):
@@ -163,9 +204,25 @@ def _upload_parquet(rel, my_files, columns, indexed, lineage_ids, device, dist):
     counts = list(staging.io_pool().map(
         lambda f: pq.ParquetFile(P.to_local(f)).metadata.num_rows, my_files))
 
+    want = columns
+    part_names = {f.name for f in rel.location.partition_spec.columns} \
+        if rel.location.partition_spec is not None else set()
+    # included string columns are read as dictionary pages + indices (_dictionary_codes)
+    dict_cols = [c for c in want if c not in indexed and c not in part_names and
+                 c in rel.data_schema.names and is_string(rel.data_schema.field(c).type)]
+
     def read_file(f, cols=None):
-        return read_files("parquet", [f], rel.data_schema, rel.options,
-                          rel.location.partition_spec, columns if cols is None else cols)
+        cols = want if cols is None else cols
+        dcols = [c for c in cols if c in dict_cols]
+        rest = [c for c in cols if c not in dcols]
+        t = read_files("parquet", [f], rel.data_schema, rel.options,
+                       rel.location.partition_spec, rest)
+        if dcols:
+            d = pq.read_table(P.to_local(f), columns=dcols, read_dictionary=dcols)
+            for c in dcols:
+                t = t.append_column(c, d.column(c))
+            t = t.select(cols)
+        return t
     lin = [lineage_ids[f] for f in my_files] if lineage_ids is not None else None
     up = staging.upload_files(read_file, my_files, counts, schema, device, lin,
                               C.DATA_FILE_NAME_ID,

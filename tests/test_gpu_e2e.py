@@ -73,10 +73,10 @@ def test_device_build_matches_host_build(tpch, tmp_path):
     s, lpath, _ = tpch
     hs = Hyperspace(s)
     li = s.read.parquet(lpath)
-    hs.createIndex(li, IndexConfig("li_ok", ["l_orderkey"], ["l_extendedprice"]))
+    hs.createIndex(li, IndexConfig("li_ok", ["l_orderkey"], ["l_extendedprice", "l_returnflag"]))
     s.conf.set("spark.hyperspace.mi.execution.device", "cpu")
     s.conf.set("spark.hyperspace.system.path", str(tmp_path / "idx_cpu"))
-    hs.createIndex(li, IndexConfig("li_ok", ["l_orderkey"], ["l_extendedprice"]))
+    hs.createIndex(li, IndexConfig("li_ok", ["l_orderkey"], ["l_extendedprice", "l_returnflag"]))
     from hyperspace_amd.io.writer import get_bucket_id
     def load(root):
         out = {}
@@ -90,6 +90,9 @@ def test_device_build_matches_host_build(tpch, tmp_path):
         assert g[b].column("l_orderkey").to_pylist() == c[b].column("l_orderkey").to_pylist()
         assert np.allclose(g[b].column("l_extendedprice").to_numpy(),
                            c[b].column("l_extendedprice").to_numpy())
+        # included string column: dictionary pages + device remap (device_build._dictionary_codes)
+        assert g[b].column("l_returnflag").cast(pa.string()).to_pylist() == \
+            c[b].column("l_returnflag").cast(pa.string()).to_pylist()
 
 
 def test_q6_filter_aggregate_native(tpch):
