@@ -103,6 +103,27 @@ class GpuBackend:
         # cold build), as the HBM side is sized by the device table cache
         from .staging import pinned_pool
         pinned_pool().reserve()
+        self._engine_start()
+
+    def _engine_start(self) -> None:
+        """Bring the engine up once, outside any query or build: the HBM arena (one large
+        allocation handed back to torch's caching allocator, which later builds and queries
+        carve up instead of calling hipMalloc per multi-GB column), the staging threads and
+        copy streams, and the kernel code objects."""
+        import torch
+        from . import staging
+        reserve = HyperspaceConf.hbm_reserve_bytes(self.session.conf)
+        if reserve > 0:
+            free, _ = torch.cuda.mem_get_info(self.device)
+            reserve = min(reserve, int(free * 0.8))
+            if reserve > (1 << 30):
+                block = torch.empty(reserve, dtype=torch.uint8, device=self.device)
+                del block   # stays cached in the allocator as one segment
+        pool = staging.io_pool()
+        list(pool.map(lambda _: None, range(pool._max_workers)))   # spawn the workers now
+        staging.copy_streams(self.device)
+        if staging.native_decode_enabled():
+            staging._warm_decode_kernels()
 
     # ------------------------------------------------------------------------------------------
     @property

@@ -118,4 +118,8 @@ INDEX_PLACEMENT_DEFAULT = "sharded"
 # (plan/plan_cache.py)
 PLAN_CACHE_ENABLED = "spark.hyperspace.mi.planCache.enabled"
 PLAN_CACHE_ENABLED_DEFAULT = "true"
+# HBM arena reserved at engine start (bytes; capped at 80% of free HBM): allocated once and
+# kept in torch's caching allocator so builds and queries do not hipMalloc multi-GB columns
+HBM_RESERVE_BYTES = "spark.hyperspace.mi.hbmReserveBytes"
+HBM_RESERVE_BYTES_DEFAULT = str(64 * 1024 ** 3)
 FAULT_INJECTION = "spark.hyperspace.mi.faultInjection"

@@ -130,6 +130,10 @@ class HyperspaceConf:
         return v
 
     @staticmethod
+    def hbm_reserve_bytes(conf) -> int:
+        return int(conf.get(C.HBM_RESERVE_BYTES, C.HBM_RESERVE_BYTES_DEFAULT))
+
+    @staticmethod
     def plan_cache_enabled(conf) -> bool:
         return _b(conf.get(C.PLAN_CACHE_ENABLED, C.PLAN_CACHE_ENABLED_DEFAULT))
 
