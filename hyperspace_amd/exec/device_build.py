@@ -105,6 +105,8 @@ def device_build_from_source(session, rel, files: List[str], columns: List[str],
     t0 = time.perf_counter()
     my_files = files[rank::world]
     fmt = source_format(rel)
+    from . import staging
+    staging.HOST_DECODED.clear()
     if fmt == "parquet":
         cols, names, schema = _upload_parquet(rel, my_files, columns, indexed, lineage_ids,
                                               device, dist)
@@ -140,7 +142,8 @@ def device_build_from_source(session, rel, files: List[str], columns: List[str],
     if dist is not None:
         dist.barrier()
     LAST_BUILD_STATS.update({"read_h2d_s": t1 - t0, "hash_exchange_s": t2 - t1,
-                             "total_s": time.perf_counter() - t0, "source_bytes": source_bytes})
+                             "total_s": time.perf_counter() - t0, "source_bytes": source_bytes,
+                             "host_decoded": sorted(staging.HOST_DECODED)})
     return paths
 
 

@@ -192,6 +192,8 @@ def fixed_width_numpy(arr) -> Tuple[np.ndarray, Optional[np.ndarray]]:
 
 
 _WARM = False
+# columns the last uploads had to decode on the host (pyarrow) instead of the native page layer
+HOST_DECODED: set = set()
 
 
 def _warm_decode_kernels() -> None:
@@ -279,6 +281,8 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
                                                                  if f.name in cols],
                                               cols, lo, n, stream, device, lock)
         rest = [f for f in schema if f.name not in done]
+        for f in rest:
+            HOST_DECODED.add(f.name)
         if not rest:
             if lineage_ids is not None:
                 with torch.cuda.stream(stream):
