@@ -811,6 +811,10 @@ class GpuBackend:
         sums, cnts, mins, maxs, G, gbase, gdict, gtype = res
         d = self._dist()
         A = len(fns) + 1  # + implicit count(*)
+        if isinstance(sums, _GraphPending) and d is not None and d.world > 1:
+            # sharded: combine this rank's partials straight from the graph's device output
+            # (stream-ordered after the replay; the next replay is ordered after the collective)
+            sums, cnts, mins, maxs = sums.graph.out
         if isinstance(sums, _GraphPending):
             fetch = sums.result
         elif d is not None and d.world > 1:
@@ -1023,13 +1027,10 @@ class GpuBackend:
         return (*out, G, gbase, gdict, gtype)
 
     def _graph_eligible(self, spec, descs) -> bool:
-        """Replay a captured hipGraph for this scan (exec/graphs.py): single rank, generated
-        kernels, a range search over all buckets (equality bucket pruning changes the launch
-        shape), and no compacted columns."""
+        """Replay a captured hipGraph for this scan (exec/graphs.py): generated kernels and a
+        range search over all of this rank's buckets (equality bucket pruning changes the
+        launch shape)."""
         if spec is None or spec[5] is not None:
-            return False
-        d = self._dist()
-        if d is not None and d.world > 1:
             return False
         conf = self.session.conf
         return HyperspaceConf.codegen_enabled(conf) and HyperspaceConf.hipgraph_enabled(conf)

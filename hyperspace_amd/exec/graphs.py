@@ -17,8 +17,9 @@ which the kernel reads through a device pointer.  A query of a known shape write
 replays the graph: one launch instead of five, and none of the per-kernel host work.
 
 The first execution of a key runs the same sequence eagerly (that also loads the kernel module)
-and then captures; later executions replay.  Graph mode is single-rank only: with several ranks
-the partial aggregates go through an all-reduce on the device tensors instead.
+and then captures; later executions replay.  With several ranks (sharded placement) the
+replay's device output block is all-gathered across ranks right after it (exec/gpu.py); the
+graph's own D2H then only feeds single-rank callers.
 """
 from __future__ import annotations
 
