@@ -297,7 +297,13 @@ def config_q3_3way(args):
     for i in range(2):
         q(1000 + i).collect()
     k = max(3, args.steps // 2)
+    from hyperspace_amd.utils.tracing import TRACER, format_report
+    TRACER.reset()
     el = _timed_loop(lambda i: q(i).collect(), k, args.device)
+    if TRACER.profile:   # HS_PROFILE=1: where the 3-way join's time goes
+        print("[q3_3way] stage profile\n" + format_report(TRACER.report()), file=sys.stderr,
+              flush=True)
+        print(plan, file=sys.stderr, flush=True)
     path = getattr(s.backend(), "last_path", None)
     reason = getattr(s.backend(), "fallback_reason", None)
     got = _rows(q(0))
