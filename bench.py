@@ -12,13 +12,21 @@ TPC-H-shaped (``hyperspace_amd.models.tpch``) and generated once per data dir.  
 timed separately (three covering indexes: lineitem(l_shipdate), lineitem(l_orderkey),
 orders(o_orderkey)); ``index_build_gbps`` = decoded indexed-column bytes / build wall time.
 Index builds shard buckets over ranks (bucket ``b`` -> rank ``b % N``, RCCL all-to-all).  Queries
-run with two placements (``--placement``, default both; the JSON reports the last):
+run with two placements (``--placement``, default both; ``value`` is the sharded one):
 
-* ``sharded``: each rank holds its buckets only; every query runs on all ranks and partial
-  aggregates combine with one all-gather — strong scaling of a single query stream;
-* ``replicated``: every rank loads all buckets into its HBM (the SF100 index set is ~36 GB of a
-  288 GB MI355X) and serves its own query stream with no collective — read replicas, weak
-  scaling (``value`` = total queries/s of all ranks; the sharded numbers are in ``sharded``).
+* ``sharded`` (headline): each rank holds its buckets only; every query runs on all ranks and
+  partial aggregates combine with one all-gather — strong scaling of a single query stream;
+* ``replicated`` (side key ``replicated``): every rank loads all buckets into its HBM (the SF100
+  index set is ~36 GB of a 288 GB MI355X) and serves its own query stream with no collective —
+  read replicas, weak scaling (total queries/s of all ranks).
+
+Extra keys: ``latency`` has single-query latencies, incl. ``q3_merge_join_ms`` (the JoinIndexRule
+join re-matched by the merge-join kernel every query, join index off) and the cold first
+queries after ``createIndex`` (``q6_cold_ms`` / ``q3_cold_ms``: HBM load of the index, kernel
+compile when the code-object cache is empty, join-index build); ``index_build_src_gbps`` is the
+compressed source-Parquet bytes of the read columns per second of build.  ``vs_baseline`` divides
+by the CPU engine's q/s on the same data (``profiles/cpu_baseline_sf<SF>.json``, written by
+``bench.py --device cpu``) when one was recorded.
 """
 import argparse
 import datetime
@@ -54,6 +62,33 @@ def _decoded_bytes(df, cfg) -> int:
     return rows * width
 
 
+def _source_parquet_bytes(df, cfg) -> int:
+    """Compressed on-disk bytes of the column chunks an index build reads (footer metadata)."""
+    import pyarrow.parquet as pq
+    from hyperspace_amd.plan import logical as L
+    from hyperspace_amd.utils import path_utils as P
+    rel = df.queryExecution.analyzed.collect(lambda p: isinstance(p, L.LogicalRelation))[0].relation
+    want = set(cfg.indexedColumns + cfg.includedColumns)
+    total = 0
+    for f in rel.location.all_files():
+        md = pq.ParquetFile(P.to_local(f.path)).metadata
+        for g in range(md.num_row_groups):
+            rg = md.row_group(g)
+            for c in range(rg.num_columns):
+                cc = rg.column(c)
+                if cc.path_in_schema in want:
+                    total += cc.total_compressed_size
+    return total
+
+
+def _cpu_baseline(sf: float):
+    p = os.path.join(ROOT, "profiles", f"cpu_baseline_sf{sf:g}.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -78,6 +113,9 @@ def main():
                          "finishes before the next is planned")
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
                     help="cpu = the pyarrow host engine (measured baseline, BASELINE.md)")
+    ap.add_argument("--record-baseline", action="store_true",
+                    help="with --device cpu: save the JSON line as profiles/cpu_baseline_sf<SF>.json "
+                         "(the vs_baseline denominator of later GPU runs)")
     args = ap.parse_args()
 
     import numpy as np
@@ -139,7 +177,7 @@ def main():
               (li, IndexConfig("li_orderkey", ["l_orderkey"],
                                ["l_extendedprice", "l_discount", "l_shipdate"])),
               (od, IndexConfig("ord_orderkey", ["o_orderkey"], ["o_orderdate", "o_shippriority"]))]
-    build_s, build_bytes = 0.0, 0
+    build_s, build_bytes, src_bytes = 0.0, 0, 0
     per_index = {}
     for df, cfg in builds:
         barrier()
@@ -156,12 +194,16 @@ def main():
         if dist:
             local_bytes = dist.all_reduce_sum_float(local_bytes)
             dt = dist.all_reduce_max_float(dt)
+        sb = _source_parquet_bytes(df, cfg) if rank == 0 else 0
         build_s += dt
         build_bytes += local_bytes
-        per_index[cfg.indexName] = {"s": round(dt, 3), "gbps": round(local_bytes / dt / 1e9, 3)}
+        src_bytes += sb
+        per_index[cfg.indexName] = {"s": round(dt, 3), "gbps": round(local_bytes / dt / 1e9, 3),
+                                    "src_gbps": round(sb / dt / 1e9, 3)}
         log(rank, f"[bench] built {cfg.indexName} in {dt:.2f}s "
                   f"({local_bytes / 1e9:.2f} GB decoded) {device_build.LAST_BUILD_STATS}")
     build_gbps = build_bytes / build_s / 1e9
+    src_gbps = src_bytes / build_s / 1e9
 
     Hyperspace.enable(s)
     backend = s.backend()
@@ -254,8 +296,23 @@ def main():
         return {"qps": nq / el, "ms_per_step": el / args.steps * 1000.0, "warmup_s": warm,
                 "results": res, "first": off}
 
+    def one_query_ms(fn, i):
+        barrier()
+        sync()
+        tq = time.perf_counter()
+        fn(i).collect()
+        sync()
+        dtq = time.perf_counter() - tq
+        return round((dist.all_reduce_max_float(dtq) if dist else dtq) * 1000, 3)
+
+    # cold: the first query of each kind after createIndex (index HBM load, kernel compile when
+    # the on-disk code-object cache is empty, join-index build) — not part of the timed steps
+    s.conf.set("spark.hyperspace.mi.index.placement", "sharded")
+    cold = {"q6_cold_ms": one_query_ms(q6, 999), "q3_cold_ms": one_query_ms(q3, 999)}
+    log(rank, f"[bench] cold first queries {cold}")
+
     from hyperspace_amd.utils.tracing import TRACER, format_report
-    modes = ["sharded", "replicated"] if world > 1 and args.placement == "both" else \
+    modes = ["replicated", "sharded"] if world > 1 and args.placement == "both" else \
         [args.placement if world > 1 else "sharded"]
     runs = {m: timed(m) for m in modes}
     final = modes[-1]
@@ -266,15 +323,27 @@ def main():
 
     # ---------------------------------------------------------------- per-query latency
     lat = {}
-    for name, fn in (("q6_filter_ms", q6), ("q3_join_ms", q3)):
+
+    def latency(name, fn, reps=5):
         barrier()
         sync()
         tq = time.perf_counter()
-        for i in range(5):
+        for i in range(reps):
             fn(i).collect()
         sync()
-        dtq = (time.perf_counter() - tq) / 5
+        dtq = (time.perf_counter() - tq) / reps
         lat[name] = round((dist.all_reduce_max_float(dtq) if dist else dtq) * 1000, 3)
+
+    latency("q6_filter_ms", q6)
+    latency("q3_join_ms", q3)
+    if on_gpu:
+        # the same JoinIndexRule join with the cached join index off: every query re-matches
+        # keys with the co-located merge-join kernel (one untimed query compiles it)
+        s.conf.set("spark.hyperspace.mi.joinIndex.enabled", "false")
+        q3(0).collect()
+        latency("q3_merge_join_ms", q3)
+        s.conf.set("spark.hyperspace.mi.joinIndex.enabled", "true")
+    lat.update(cold)
 
     # ---------------------------------------------------------------- cross-check
     check = None
@@ -298,11 +367,13 @@ def main():
         if not (ok6 and ok3):
             raise RuntimeError(f"cross-check failed: {i6} vs {n6}; {i3} vs {n3}")
 
+    base = _cpu_baseline(sf) if on_gpu else None
+    vs = round(qps / base["value"], 2) if base and base.get("value") else None
     if rank == 0:
         out = {"metric": METRIC, "value": round(qps, 3), "unit": "queries/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
                "higher_is_better": True,
-               "scaling": "weak" if final == "replicated" else "strong", "vs_baseline": None,
+               "scaling": "weak" if final == "replicated" else "strong", "vs_baseline": vs,
                "dtype": "fp64", "data": "synthetic",
                "config": {"model": f"tpch-sf{sf:g} lineitem/orders covering indexes",
                           "global_batch": 2, "seq_len": 0,
@@ -311,18 +382,25 @@ def main():
                           "placement": final,
                           "num_buckets": args.buckets, "source_files": nfiles,
                           "device": args.device},
-               "index_build_gbps": round(build_gbps, 3), "index_build_s": round(build_s, 3),
+               "index_build_gbps": round(build_gbps, 3),
+               "index_build_src_gbps": round(src_gbps, 3), "index_build_s": round(build_s, 3),
                "index_build": per_index, "latency": lat, "warmup_s": round(warm_s, 3),
                "datagen_s": round(gen_s, 2), "crosscheck": check, "inflight": args.inflight}
-        if "sharded" in runs and final != "sharded":
-            out["sharded"] = {"value": round(runs["sharded"]["qps"], 3),
-                              "ms_per_step": round(runs["sharded"]["ms_per_step"], 3),
-                              "scaling": "strong"}
+        if "replicated" in runs and final != "replicated":
+            out["replicated"] = {"value": round(runs["replicated"]["qps"], 3),
+                                 "ms_per_step": round(runs["replicated"]["ms_per_step"], 3),
+                                 "scaling": "weak"}
+        if base:
+            out["cpu_baseline"] = {"value": base["value"], "source": base.get("source")}
         if on_gpu:
             out["device_cache"] = {"hits": backend.cache.hits, "misses": backend.cache.misses}
         if not on_gpu:
             out["n_gpus"] = 0
         print(json.dumps(out), flush=True)
+        if args.record_baseline and not on_gpu:
+            out["source"] = f"bench.py --device cpu --sf {sf:g} (this repo's pyarrow host engine)"
+            with open(os.path.join(ROOT, "profiles", f"cpu_baseline_sf{sf:g}.json"), "w") as f:
+                json.dump(out, f, indent=1)
     if dist:
         barrier()
         torch.distributed.destroy_process_group()

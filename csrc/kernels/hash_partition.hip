@@ -9,13 +9,28 @@
 #define HS_HASH_MAX_COLS 8
 #define HS_STR 100
 
+// Value transform applied before hashing, so a device column hashes like Spark's logical value:
+//   HS_XF_DECIMAL | s : float64 storage of decimal(p<=15, s) -> unscaled long llrint(d * 10^s)
+//   HS_XF_MUL | k     : int64 * 10^k   (timestamp[s]/[ms] -> microseconds)
+//   HS_XF_FDIV | k    : floor(int64 / 10^k)  (timestamp[ns] -> microseconds)
+#define HS_XF_NONE 0
+#define HS_XF_DECIMAL 0x100
+#define HS_XF_MUL 0x200
+#define HS_XF_FDIV 0x300
+
 struct HashCol {
   const void* data;        // values, or chars for strings
   const uint8_t* valid;    // nullable
   const int64_t* offsets;  // strings only (n+1 int64 offsets)
   int32_t type;            // HsType or HS_STR
-  int32_t pad;
+  int32_t xform;           // HS_XF_* | argument
 };
+
+__device__ __forceinline__ int64_t hs_pow10(int k) {
+  int64_t p = 1;
+  for (int i = 0; i < k; ++i) p *= 10;
+  return p;
+}
 
 struct HashParams {
   HashCol cols[HS_HASH_MAX_COLS];
@@ -50,21 +65,32 @@ __device__ __forceinline__ uint32_t hash_value(const HashCol& c, int64_t row, ui
     case HS_I16: return hs_hash_int((uint32_t)(int32_t)((const int16_t*)c.data)[row], h);
     case HS_I32: return hs_hash_int((uint32_t)((const int32_t*)c.data)[row], h);
     case HS_BOOL: return hs_hash_int((uint32_t)(((const uint8_t*)c.data)[row] != 0), h);
-    case HS_I64: return hs_hash_long((uint64_t)((const int64_t*)c.data)[row], h);
+    case HS_I64: {
+      int64_t v = ((const int64_t*)c.data)[row];
+      const int xk = c.xform & 0xff;
+      if ((c.xform & 0xf00) == HS_XF_MUL) {
+        v *= hs_pow10(xk);
+      } else if ((c.xform & 0xf00) == HS_XF_FDIV) {
+        const int64_t d = hs_pow10(xk);
+        int64_t q = v / d;
+        if ((v % d) != 0 && v < 0) --q;  // floor, like Math.floorDiv
+        v = q;
+      }
+      return hs_hash_long((uint64_t)v, h);
+    }
+    // Spark 2.4.2 (the reference's pin, build.sbt:19) hashes floatToIntBits / doubleToLongBits:
+    // NaN is canonicalised, -0.0 keeps its sign bit (the -0.0 -> 0.0 rewrite is Spark 3.x).
     case HS_F32: {
       float f = ((const float*)c.data)[row];
-      uint32_t bits;
-      if (f == 0.0f) bits = 0u;                 // -0.0 -> 0.0
-      else if (f != f) bits = 0x7fc00000u;      // canonical NaN (floatToIntBits)
-      else bits = __float_as_uint(f);
+      const uint32_t bits = (f != f) ? 0x7fc00000u : __float_as_uint(f);
       return hs_hash_int(bits, h);
     }
     case HS_F64: {
       double d = ((const double*)c.data)[row];
-      uint64_t bits;
-      if (d == 0.0) bits = 0ull;
-      else if (d != d) bits = 0x7ff8000000000000ull;
-      else bits = (uint64_t)__double_as_longlong(d);
+      if ((c.xform & 0xf00) == HS_XF_DECIMAL) {  // decimal: Spark hashes the unscaled long
+        return hs_hash_long((uint64_t)__double2ll_rn(d * (double)hs_pow10(c.xform & 0xff)), h);
+      }
+      const uint64_t bits = (d != d) ? 0x7ff8000000000000ull : (uint64_t)__double_as_longlong(d);
       return hs_hash_long(bits, h);
     }
     case HS_STR:

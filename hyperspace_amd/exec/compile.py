@@ -53,11 +53,36 @@ class Leaf:
         raise Unsupported("negate")
 
 
-def _lit_value(v):
+_EPOCH = datetime.datetime(1970, 1, 1)
+_UNIT_PER_US = {"us": (1, 1), "ns": (1000, 1), "ms": (1, 1000), "s": (1, 1_000_000)}
+
+
+def _lit_value(v, dtype=None):
+    """A literal in the device storage of the column it is compared with: dates as days,
+    timestamps as integers in the column's own unit (exact integer arithmetic; tz-aware values
+    are converted to UTC).  A literal the column's unit cannot represent exactly is
+    ``Unsupported`` (the host path evaluates it)."""
     if isinstance(v, datetime.datetime):
-        return int((v - datetime.datetime(1970, 1, 1)).total_seconds() * 1_000_000)
+        if v.tzinfo is not None:
+            v = v.astimezone(datetime.timezone.utc).replace(tzinfo=None)
+        us = (v - _EPOCH) // datetime.timedelta(microseconds=1)
+        if dtype is not None and pa.types.is_date32(dtype):
+            days, rem = divmod(us, 86_400_000_000)
+            if rem:
+                raise Unsupported("timestamp literal compared with a date column")
+            return days
+        if dtype is not None and pa.types.is_timestamp(dtype):
+            mul, div = _UNIT_PER_US[dtype.unit]
+            if us % div:
+                raise Unsupported(f"timestamp literal finer than the column unit {dtype.unit}")
+            return us * mul // div
+        return us
     if isinstance(v, datetime.date):
-        return (v - datetime.date(1970, 1, 1)).days
+        days = (v - datetime.date(1970, 1, 1)).days
+        if dtype is not None and pa.types.is_timestamp(dtype):
+            mul, div = _UNIT_PER_US[dtype.unit]
+            return days * 86_400_000_000 * mul // div
+        return days
     return v
 
 
@@ -84,9 +109,9 @@ def _leaf(e: E.Expression) -> Leaf:
         if isinstance(r, E.Cast):
             r = r.child
         if isinstance(l, E.Attribute) and isinstance(r, E.Literal):
-            return Leaf("cmp_lit", op, l, value=_lit_value(r.value))
+            return Leaf("cmp_lit", op, l, value=_lit_value(r.value, l.data_type))
         if isinstance(r, E.Attribute) and isinstance(l, E.Literal):
-            return Leaf("cmp_lit", _FLIP[op], r, value=_lit_value(l.value))
+            return Leaf("cmp_lit", _FLIP[op], r, value=_lit_value(l.value, r.data_type))
         if isinstance(l, E.Attribute) and isinstance(r, E.Attribute):
             return Leaf("cmp_col", op, l, r)
         raise Unsupported(f"comparison {e.sql()}")
@@ -96,9 +121,9 @@ def _leaf(e: E.Expression) -> Leaf:
         return Leaf("notnull", 0, e.child)
     if isinstance(e, E.In) and isinstance(e.value, E.Attribute) and \
             all(isinstance(v, E.Literal) for v in e.values):
-        return Leaf("in", NL.OP_EQ, e.value, values=[_lit_value(v.value) for v in e.values])
+        return Leaf("in", NL.OP_EQ, e.value, values=[_lit_value(v.value, e.value.data_type) for v in e.values])
     if isinstance(e, E.InSet) and isinstance(e.value, E.Attribute):
-        return Leaf("in", NL.OP_EQ, e.value, values=[_lit_value(v) for v in e.hset])
+        return Leaf("in", NL.OP_EQ, e.value, values=[_lit_value(v, e.value.data_type) for v in e.hset])
     raise Unsupported(f"predicate {type(e).__name__}")
 
 

@@ -52,7 +52,8 @@ def is_string(t: pa.DataType) -> bool:
 
 def h2d(a: np.ndarray, device):
     torch = _torch()
-    t = torch.from_numpy(np.ascontiguousarray(a))
+    # arrow-backed numpy views are read-only: np.require copies those (torch needs writable)
+    t = torch.from_numpy(np.require(a, requirements=["C", "W"]))
     if t.numel() >= (1 << 20):
         t = t.pin_memory()
         return t.to(device, non_blocking=True)

@@ -86,13 +86,16 @@ def encode(col) -> Optional[Compact]:
             x = torch.where(vm, x, x[vm][0])
         if not bool(torch.isfinite(x).all()):
             return None
+        # -0.0 would decode as +0.0 (code 0): keep such columns uncompressed
+        if bool(((x == 0) & torch.signbit(x)).any()):
+            return None
         for k in range(_MAX_SCALE_DIGITS + 1):
             s = float(10 ** k)
             q = torch.round(x * s)
             if float(q.abs().max().item()) >= 2.0 ** 52:
                 return None
             back = (q / s).view(torch.int64)
-            same = bool((back == x.view(torch.int64)).all())  # bit-exact (also keeps -0.0 out)
+            same = bool((back == x.view(torch.int64)).all())  # bit-exact
             if not same:
                 continue
             qi = q.long()

@@ -47,7 +47,7 @@ def read_index_input(rel, files: List[str], columns: List[str], lineage_ids: Opt
 def build_from_source(session, rel, files: List[str], columns: List[str], indexed: List[str],
                       num_buckets: int, out_path: str, lineage_ids: Optional[Dict[str, int]],
                       mode: str = "overwrite") -> List[str]:
-    if session.device_kind() == "gpu":
+    if session.device_kind() == "gpu" and _device_hashable(rel, indexed):
         from ..exec.device_build import device_build_from_source
         return device_build_from_source(session, rel, files, columns, indexed, num_buckets,
                                         out_path, lineage_ids, mode)
@@ -59,6 +59,18 @@ def build_from_source(session, rel, files: List[str], columns: List[str], indexe
                                 HyperspaceConf.index_file_codec(session.conf),
                                 HyperspaceConf.index_row_group_rows(session.conf),
                                 job_uuid=str(uuid.uuid4()))
+
+
+def _device_hashable(rel, indexed: List[str]) -> bool:
+    """The device Murmur3 kernel hashes decimals from float64 storage, exact only up to
+    precision 15 (``ops.kernels.hash_xform``); wider decimal keys use the host build."""
+    names = set(rel.data_schema.names)
+    for c in indexed:
+        if c in names:
+            t = rel.data_schema.field(c).type
+            if pa.types.is_decimal(t) and t.precision > 15:
+                return False
+    return True
 
 
 def _spmd_host_write(session, dist, t: pa.Table, out_path: str, num_buckets: int,

@@ -38,7 +38,11 @@ class ColDesc(C.Structure):
 
 class HashCol(C.Structure):
     _fields_ = [("data", C.c_void_p), ("valid", C.c_void_p), ("offsets", C.c_void_p),
-                ("type", C.c_int32), ("pad", C.c_int32)]
+                ("type", C.c_int32), ("xform", C.c_int32)]
+
+
+# HashCol.xform (csrc/kernels/hash_partition.hip): value transform before hashing
+XF_NONE, XF_DECIMAL, XF_MUL, XF_FDIV = 0, 0x100, 0x200, 0x300
 
 
 class HashParams(C.Structure):

@@ -20,6 +20,25 @@ def _torch():
 # ------------------------------------------------------------------------------------------------
 # K3: Spark Murmur3 bucketing
 # ------------------------------------------------------------------------------------------------
+def hash_xform(atype) -> int:
+    """``HashCol.xform`` that makes a device column hash as Spark's logical value
+    (``utils/murmur3.py``): decimals (float64 storage) hash their unscaled long, timestamps hash
+    microseconds.  Raises for decimals too wide to round-trip exactly through float64."""
+    import pyarrow as pa
+    if pa.types.is_decimal(atype):
+        if atype.precision > 15:
+            raise ValueError(f"device hash of {atype}: precision > 15 is not exact in float64 "
+                             "storage")
+        return NL.XF_DECIMAL | int(atype.scale)
+    if pa.types.is_timestamp(atype):
+        k = {"s": 6, "ms": 3, "us": 0, "ns": -3}[atype.unit]
+        if k > 0:
+            return NL.XF_MUL | k
+        if k < 0:
+            return NL.XF_FDIV | -k
+    return NL.XF_NONE
+
+
 def _hash_params(cols, num_buckets: int, seed: int = 42) -> NL.HashParams:
     if len(cols) > NL.HASH_MAX_COLS:
         raise ValueError("too many bucket columns")
@@ -32,7 +51,8 @@ def _hash_params(cols, num_buckets: int, seed: int = 42) -> NL.HashParams:
                                    c.offsets.data_ptr(), NL.STR, 0)
         else:
             p.cols[i] = NL.HashCol(c.data.data_ptr(),
-                                   c.valid.data_ptr() if c.valid is not None else 0, 0, c.hs_type, 0)
+                                   c.valid.data_ptr() if c.valid is not None else 0, 0, c.hs_type,
+                                   hash_xform(c.atype))
     p.ncols = len(cols)
     p.num_buckets = int(num_buckets)
     p.seed = seed

@@ -68,14 +68,6 @@ class QueryExecution:
             return backend.collect_async(plan)
         return _Done(backend.collect(plan), getattr(backend, "last_path", "host"))
 
-
-class _Done:
-    def __init__(self, table: pa.Table, path: str):
-        self._t, self.path, self.reason = table, path, None
-
-    def result(self) -> pa.Table:
-        return self._t
-
     def explain_string(self, extended: bool = False) -> str:
         parts = []
         if extended:
@@ -83,3 +75,11 @@ class _Done:
                       "== Optimized Logical Plan ==", self.optimized_plan.tree_string()]
         parts += ["== Physical Plan ==", self.executed_plan.tree_string()]
         return "\n".join(parts)
+
+
+class _Done:
+    def __init__(self, table: pa.Table, path: str):
+        self._t, self.path, self.reason = table, path, None
+
+    def result(self) -> pa.Table:
+        return self._t

@@ -7,8 +7,10 @@ as used by ``HashPartitioning.partitionIdExpression = pmod(hash, numPartitions)`
 
 * columns chain: the running hash of column i is the seed of column i+1; a null leaves it as is;
 * int/short/byte/bool/date -> ``hashInt``; long/timestamp -> ``hashLong``;
-* float/double hash their IEEE bits (``floatToIntBits`` / ``doubleToLongBits``: canonical NaN);
-  -0.0 is normalised to 0.0 (Spark >= 3 behaviour, so equal keys always share a bucket);
+* float/double hash their IEEE bits (``floatToIntBits`` / ``doubleToLongBits``: canonical NaN,
+  -0.0 keeps its sign bit — Spark 2.4.2, the version the reference pins (``build.sbt:19``); the
+  -0.0 -> 0.0 rewrite inside hash expressions is Spark 3.x);
+* decimal(p <= 18) hashes its unscaled long; timestamps hash microseconds (floor for ns);
 * strings -> ``hashUnsafeBytes`` with Spark's non-standard tail (each trailing byte is mixed as
   its own sign-extended int).
 
@@ -124,17 +126,18 @@ def hash_column(arr, seed):
     elif pa.types.is_date32(t):
         h = hash_int(np.asarray(arr.cast(pa.int32()).fill_null(0).to_numpy()), seed)
     elif pa.types.is_timestamp(t):
-        micros = pc.cast(arr.cast(pa.timestamp("us", tz=t.tz)), pa.int64())
-        h = hash_long(np.asarray(micros.fill_null(0).to_numpy()), seed)
+        raw = np.asarray(arr.view(pa.int64()).fill_null(0).to_numpy(zero_copy_only=False),
+                         dtype=np.int64)
+        k = {"s": 6, "ms": 3, "us": 0, "ns": -3}[t.unit]
+        micros = raw * (10 ** k) if k >= 0 else np.floor_divide(raw, 10 ** -k)
+        h = hash_long(micros, seed)
     elif pa.types.is_float32(t):
         f = np.asarray(arr.fill_null(0).to_numpy(), dtype=np.float32).copy()
-        f[f == 0] = 0.0
         bits = f.view(np.int32).copy()
         bits[np.isnan(f)] = 0x7FC00000
         h = hash_int(bits, seed)
     elif pa.types.is_float64(t):
         f = np.asarray(arr.fill_null(0).to_numpy(), dtype=np.float64).copy()
-        f[f == 0] = 0.0
         bits = f.view(np.int64).copy()
         bits[np.isnan(f)] = 0x7FF8000000000000
         h = hash_long(bits, seed)

@@ -314,3 +314,25 @@ def test_int_bounds_match_decoded_double_compares():
                     inside = lo <= q <= hi
                     got = (not inside) if op == NL.OP_NE else inside
                     assert got == f(q / scale, lit), (scale, lit, op, q)
+
+
+def test_timestamp_literals_exact_in_column_unit():
+    import datetime
+    import random
+    from hyperspace_amd.exec.compile import Unsupported, _lit_value
+    rnd = random.Random(3)
+    epoch = datetime.datetime(1970, 1, 1)
+    for _ in range(20000):
+        us = rnd.randrange(-2**50, 2**50)
+        v = epoch + datetime.timedelta(microseconds=us)
+        assert _lit_value(v) == us
+        assert _lit_value(v, pa.timestamp("ns")) == us * 1000
+    tz = datetime.timezone(datetime.timedelta(hours=2))
+    assert _lit_value(datetime.datetime(1970, 1, 1, 2, 0, 1, tzinfo=tz)) == 1_000_000
+    assert _lit_value(datetime.datetime(1970, 1, 1, 0, 0, 5), pa.timestamp("s")) == 5
+    assert _lit_value(datetime.datetime(1970, 1, 2), pa.date32()) == 1
+    assert _lit_value(datetime.date(1970, 1, 2), pa.timestamp("ms")) == 86_400_000
+    with pytest.raises(Unsupported):
+        _lit_value(datetime.datetime(1970, 1, 1, 0, 0, 0, 5), pa.timestamp("ms"))
+    with pytest.raises(Unsupported):
+        _lit_value(datetime.datetime(1970, 1, 2, 1), pa.date32())

@@ -40,6 +40,26 @@ def test_murmur3_bucket_matches_spark_oracle(device):
     assert b.cpu().tolist() == [4, 1]
 
 
+def test_murmur3_bucket_decimal_and_timestamp_match_host(device):
+    """Device bucket ids equal the host/Spark hash for decimals (unscaled long from float64
+    storage) and timestamps in every unit (microseconds, floor for ns)."""
+    import decimal
+    from hyperspace_amd.ops import kernels as K
+    rng = np.random.default_rng(5)
+    n = 50_000
+    dec = pa.array([decimal.Decimal(int(v)).scaleb(-2) for v in rng.integers(-10**12, 10**12, n)],
+                   pa.decimal128(15, 2))
+    raw = rng.integers(-2**50, 2**50, n)
+    cols = [dec, pa.array([decimal.Decimal("1.50"), decimal.Decimal("2.25"),
+                           decimal.Decimal("100.00")], pa.decimal128(10, 2))]
+    for unit in ("s", "ms", "us", "ns"):
+        cols.append(pa.array(raw, pa.int64()).view(pa.timestamp(unit)))
+    for c in cols:
+        for nb in (200, 7):
+            got = K.murmur3_bucket([_col(c, device)], nb)[0].cpu().numpy()
+            assert np.array_equal(got, murmur3.bucket_ids([c], nb)), (c.type, nb)
+
+
 def test_sort_permutation_stable_nulls_first(device):
     import torch
     from hyperspace_amd.ops import kernels as K

@@ -275,3 +275,16 @@ def test_delta_source_index_refresh_and_time_travel(tmp_path):
     verify_index_usage(s, q, {"dIdx"})
     e = hs.index("dIdx").collect()[0]
     assert e.numSourceFiles == 1
+
+
+def test_dataframe_explain_extended_prints_all_plans(tmp_path, capsys):
+    from hyperspace_amd import Session, col
+    pq.write_table(pa.table({"a": [1, 2, 3], "b": [4.0, 5.0, 6.0]}), str(tmp_path / "t.parquet"))
+    s = Session(conf={"spark.hyperspace.system.path": str(tmp_path / "ix"),
+                      "spark.hyperspace.mi.execution.device": "cpu"})
+    df = s.read.parquet(str(tmp_path / "t.parquet")).filter(col("a") > 1)
+    text = df.queryExecution.explain_string(True)
+    for h in ("== Analyzed Logical Plan ==", "== Optimized Logical Plan ==", "== Physical Plan =="):
+        assert h in text
+    df.explain(True)
+    assert "== Physical Plan ==" in capsys.readouterr().out

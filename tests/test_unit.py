@@ -154,11 +154,47 @@ def test_murmur3_matches_scalar_oracle():
     assert list(murmur3.hash_columns([pa.array(longs)])) == [_py_hash_long(int(v), 42) for v in longs]
     assert list(murmur3.hash_columns([pa.array(strs)])) == \
         [_py_hash_bytes(s.encode(), 42) for s in strs]
-    # dates hash as int, doubles as their long bits (with -0.0 normalised to 0.0)
+    # dates hash as int, doubles as their long bits (Spark 2.4.2: -0.0 keeps its sign bit)
     assert murmur3.hash_columns([pa.array([19000], pa.date32())])[0] == _py_hash_int(19000, 42)
     bits = int(np.array([1.5]).view(np.int64)[0])
     assert murmur3.hash_columns([pa.array([1.5])])[0] == _py_hash_long(bits, 42)
-    assert murmur3.hash_columns([pa.array([-0.0])])[0] == murmur3.hash_columns([pa.array([0.0])])[0]
+    neg0 = int(np.array([-0.0]).view(np.int64)[0])
+    assert murmur3.hash_columns([pa.array([-0.0])])[0] == _py_hash_long(neg0, 42)
+    assert murmur3.hash_columns([pa.array([-0.0])])[0] != murmur3.hash_columns([pa.array([0.0])])[0]
+    nan_bits = 0x7FF8000000000000
+    assert murmur3.hash_columns([pa.array([float("nan")])])[0] == _py_hash_long(nan_bits, 42)
+
+
+def test_murmur3_decimal_and_timestamp_logical_values():
+    import datetime
+    import decimal
+    # decimal hashes its unscaled long (Spark Murmur3Hash on DecimalType(p<=18))
+    d = pa.array([decimal.Decimal("1.50"), decimal.Decimal("-2.25")], pa.decimal128(10, 2))
+    assert list(murmur3.hash_columns([d])) == [_py_hash_long(150, 42), _py_hash_long(-225, 42)]
+    # timestamps hash microseconds whatever the storage unit (floor for ns)
+    ts = datetime.datetime(2020, 1, 2, 3, 4, 5, 678901)
+    us = pa.array([ts], pa.timestamp("us"))
+    for unit in ("ms", "s"):
+        v = pa.array([ts.replace(microsecond=0)], pa.timestamp(unit))
+        ref = pa.array([ts.replace(microsecond=0)], pa.timestamp("us"))
+        assert murmur3.hash_columns([v])[0] == murmur3.hash_columns([ref])[0]
+    ns = pa.array([int(us.view(pa.int64())[0].as_py()) * 1000 + 999], pa.int64()).view(
+        pa.timestamp("ns"))
+    assert murmur3.hash_columns([ns])[0] == murmur3.hash_columns([us])[0]
+    neg_ns = pa.array([-1], pa.int64()).view(pa.timestamp("ns"))  # floor(-1 ns) = -1 us
+    assert murmur3.hash_columns([neg_ns])[0] == _py_hash_long(-1, 42)
+
+
+def test_device_hash_xform_codes():
+    from hyperspace_amd.ops import _lib as NL
+    from hyperspace_amd.ops.kernels import hash_xform
+    assert hash_xform(pa.decimal128(12, 2)) == NL.XF_DECIMAL | 2
+    assert hash_xform(pa.timestamp("ns")) == NL.XF_FDIV | 3
+    assert hash_xform(pa.timestamp("ms")) == NL.XF_MUL | 3
+    assert hash_xform(pa.timestamp("us")) == NL.XF_NONE
+    assert hash_xform(pa.float64()) == NL.XF_NONE
+    with pytest.raises(ValueError):
+        hash_xform(pa.decimal128(18, 2))
 
 
 def test_murmur3_null_keeps_seed_and_chaining():
