@@ -30,17 +30,21 @@ from ..utils.conf import HyperspaceConf
 from .device_table import DeviceColumn, DeviceTable, is_string
 
 LAST_BUILD_STATS: Dict[str, float] = {}
+# source files per exchange batch of a multi-GPU build (decode of batch k+1 overlaps the
+# all-to-all of batch k)
+FILES_PER_BATCH = 8
 
 
 def _global_dicts(t: pa.Table, dist) -> Dict[str, pa.Array]:
+    """Job-global sorted dictionary of every string column (``parallel/dictionary.py``)."""
+    from ..parallel.dictionary import union_sorted
     out = {}
     for name in t.column_names:
         if is_string(t.schema.field(name).type):
-            u = pc.unique(t.column(name).combine_chunks().drop_null())
-            if dist is not None and dist.world > 1:
-                parts = dist.all_gather_object(u.to_pylist())
-                u = pa.array(sorted(set(x for p in parts for x in p)), pa.string())
-            out[name] = u.sort()
+            c = t.column(name).combine_chunks()
+            if pa.types.is_dictionary(c.type):
+                c = c.cast(c.type.value_type)
+            out[name] = union_sorted(c, dist)
     return out
 
 
@@ -65,7 +69,7 @@ def _sort_and_write(session, table: Dict[str, DeviceColumn], names: List[str], b
     t0 = time.perf_counter()
     perm = K.sort_permutation([table[c] for c in indexed], extra_leading=(bucket, 16))
     gathered = K.gather_columns([table[c] for c in names], perm)
-    counts = torch.bincount(bucket.long(), minlength=num_buckets)
+    counts = K.histogram(bucket, num_buckets)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     off = np.concatenate([[0], np.cumsum(counts.cpu().numpy())]).astype(np.int64)
@@ -107,34 +111,21 @@ def device_build_from_source(session, rel, files: List[str], columns: List[str],
     fmt = source_format(rel)
     from . import staging
     staging.HOST_DECODED.clear()
+    xs = _BatchedExchange(dist, num_buckets, indexed) if world > 1 else None
     if fmt == "parquet":
         cols, names, schema = _upload_parquet(rel, my_files, columns, indexed, lineage_ids,
-                                              device, dist)
+                                              device, dist, xs)
     else:
         cols, names, schema = _upload_generic(rel, files, my_files, columns, indexed, lineage_ids,
                                               device, dist)
     t1 = time.perf_counter()
     source_bytes = sum(c.nbytes() for c in cols.values())
-    bucket, _ = K.murmur3_bucket([cols[c] for c in indexed], num_buckets, with_counts=False)
-    if world > 1:
-        from ..parallel.shuffle import exchange
-        # every rank must send the same column list: agree on which columns carry validity
-        has_valid = dist.all_gather_object([cols[n].valid is not None for n in names])
-        need_valid = [any(v[i] for v in has_valid) for i in range(len(names))]
-        dest = torch.remainder(bucket, world).to(torch.int32)
-        flat = []
-        for n, nv in zip(names, need_valid):
-            if nv and cols[n].valid is None:
-                cols[n].valid = torch.ones(len(cols[n]), dtype=torch.uint8, device=device)
-            flat.append(cols[n].data)
-            flat.append(cols[n].valid)
-        flat.append(bucket)
-        recv, _ = exchange(flat, dest, world, dist)
-        bucket = recv[-1]
-        new = {}
-        for i, n in enumerate(names):
-            new[n] = DeviceColumn(recv[2 * i], recv[2 * i + 1], cols[n].atype, cols[n].dictionary)
-        cols = new
+    if xs is None:
+        bucket, _ = K.murmur3_bucket([cols[c] for c in indexed], num_buckets, with_counts=False)
+    else:
+        if not xs.started:     # string columns: one batch once the global dictionaries exist
+            xs.batch_all(cols, names)
+        cols, bucket = xs.finish(cols, names)
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     paths = _sort_and_write(session, cols, names, bucket, indexed, num_buckets, out_path, schema,
@@ -144,7 +135,77 @@ def device_build_from_source(session, rel, files: List[str], columns: List[str],
     LAST_BUILD_STATS.update({"read_h2d_s": t1 - t0, "hash_exchange_s": t2 - t1,
                              "total_s": time.perf_counter() - t0, "source_bytes": source_bytes,
                              "host_decoded": sorted(staging.HOST_DECODED)})
+    if xs is not None:
+        LAST_BUILD_STATS.update({"exchange_batches": xs.nbatches,
+                                 "exchange_sent_bytes": xs.sent_bytes})
     return paths
+
+
+class _BatchedExchange:
+    """Multi-GPU build shuffle: every batch of decoded source rows is hashed (Spark Murmur3 on
+    the indexed columns) and sent to its owner ranks (bucket % world) with one packed
+    all-to-all while the staging pool decodes the next files (``parallel/exchange.py``).
+    Which columns carry a validity mask is agreed before the first batch, so every rank sends
+    the same column list."""
+
+    def __init__(self, dist, num_buckets: int, indexed: List[str]):
+        self.dist, self.num_buckets, self.indexed = dist, num_buckets, indexed
+        self.ex = None
+        self.started = False
+        self.nbatches = 0
+        self.sent_bytes = 0
+
+    def batch(self, cols: Dict[str, DeviceColumn], names: List[str], lo: int, hi: int) -> None:
+        from ..parallel.exchange import RowExchange
+        sl = {n: cols[n] for n in names}
+        part = [DeviceColumn(c.data[lo:hi], None if c.valid is None else c.valid[lo:hi],
+                             c.atype, c.dictionary, c.offsets, c.chars)
+                for c in (sl[n] for n in self.indexed)]
+        if any(c.offsets is not None for c in part):
+            raise ValueError("batched exchange over raw-string keys: hash the whole upload")
+        bucket, _ = K.murmur3_bucket(part, self.num_buckets, with_counts=False)
+        send = [sl[n].data[lo:hi] for n in names] + \
+            [sl[n].valid[lo:hi] for n in names if sl[n].valid is not None] + [bucket]
+        if self.ex is None:
+            self.ex = RowExchange(self.dist, [t.dtype for t in send], bucket.device)
+        self.ex.add(send, bucket)
+        self.started = True
+        self.nbatches += 1
+
+    def batch_all(self, cols, names) -> None:
+        """One whole-upload batch (string columns: their codes exist only once the job-global
+        dictionaries are built; indexed strings hash from raw bytes)."""
+        import torch
+        from ..parallel.exchange import RowExchange
+        need = self.dist.agree_any([cols[n].valid is not None for n in names])
+        for n, nv in zip(names, need):
+            if nv and cols[n].valid is None:
+                cols[n].valid = torch.ones(len(cols[n]), dtype=torch.uint8,
+                                           device=cols[n].data.device)
+        bucket, _ = K.murmur3_bucket([cols[c] for c in self.indexed], self.num_buckets,
+                                     with_counts=False)
+        send = [cols[n].data for n in names] + \
+            [cols[n].valid for n in names if cols[n].valid is not None] + [bucket]
+        self.ex = RowExchange(self.dist, [t.dtype for t in send], bucket.device)
+        self.ex.add(send, bucket)
+        self.started = True
+        self.nbatches += 1
+
+    def finish(self, cols: Dict[str, DeviceColumn], names: List[str]):
+        if not self.started:
+            raise RuntimeError("exchange finished before any batch")
+        got = self.ex.finish()
+        self.sent_bytes = self.ex.sent_bytes
+        out = {}
+        vi = len(names)
+        for j, n in enumerate(names):
+            c = cols[n]
+            v = None
+            if c.valid is not None:
+                v = got[vi]
+                vi += 1
+            out[n] = DeviceColumn(got[j], v, c.atype, c.dictionary)
+        return out, got[-1]
 
 
 def _finish_strings(host_strings: Dict[str, list], cols: Dict[str, DeviceColumn], indexed,
@@ -170,12 +231,10 @@ def _dictionary_codes(chunks, device, dist) -> DeviceColumn:
     on the device with one gather through that chunk's local -> global table."""
     import torch
     parts = [ch for c in chunks for ch in c.chunks]
+    from ..parallel.dictionary import union_sorted
     local = [ch.dictionary.cast(pa.string()) for ch in parts]
-    u = pc.unique(pa.concat_arrays(local)) if local else pa.array([], pa.string())
-    if dist is not None and dist.world > 1:
-        all_vals = dist.all_gather_object(u.to_pylist())
-        u = pa.array(sorted(set(x for p in all_vals for x in p)), pa.string())
-    gdict = u.sort()
+    u = pa.concat_arrays(local) if local else pa.array([], pa.string())
+    gdict = union_sorted(u, dist)
     n = sum(len(ch) for ch in parts)
     codes = torch.empty(n, dtype=torch.int32, device=device)
     valid = None
@@ -198,14 +257,34 @@ def _dictionary_codes(chunks, device, dist) -> DeviceColumn:
     return DeviceColumn(codes, valid, pa.string(), gdict)
 
 
-def _upload_parquet(rel, my_files, columns, indexed, lineage_ids, device, dist):
-    """Pipelined decode -> pinned -> HBM upload of this rank's Parquet files (staging.py)."""
+def _footer_info(path: str, names: List[str]):
+    """(rows, columns that may hold nulls) from one Parquet footer: a column counts as
+    nullable unless every row group's statistics say null_count == 0."""
     import pyarrow.parquet as pq
+    md = pq.ParquetFile(P.to_local(path)).metadata
+    want = set(names)
+    maybe = set()
+    for g in range(md.num_row_groups):
+        rg = md.row_group(g)
+        for c in range(rg.num_columns):
+            cc = rg.column(c)
+            nm = cc.path_in_schema
+            if nm in want:
+                st = cc.statistics
+                if st is None or not st.has_null_count or st.null_count > 0:
+                    maybe.add(nm)
+    return md.num_rows, maybe
+
+
+def _upload_parquet(rel, my_files, columns, indexed, lineage_ids, device, dist, xs=None):
+    """Pipelined decode -> pinned -> HBM upload of this rank's Parquet files (staging.py).
+    With a multi-GPU exchange ``xs`` and no string columns, every batch of files is hashed and
+    exchanged as soon as it is on the device, overlapping the decode of the next batch."""
     from ..io.reader import output_schema, read_files
     from . import staging
     schema = output_schema(rel.data_schema, rel.location.partition_spec, columns)
-    counts = list(staging.io_pool().map(
-        lambda f: pq.ParquetFile(P.to_local(f)).metadata.num_rows, my_files))
+    infos = list(staging.io_pool().map(lambda f: _footer_info(f, list(schema.names)), my_files))
+    counts = [r for r, _ in infos]
 
     want = columns
     part_names = {f.name for f in rel.location.partition_spec.columns} \
@@ -227,16 +306,29 @@ def _upload_parquet(rel, my_files, columns, indexed, lineage_ids, device, dist):
             t = t.select(cols)
         return t
     lin = [lineage_ids[f] for f in my_files] if lineage_ids is not None else None
-    up = staging.upload_files(read_file, my_files, counts, schema, device, lin,
-                              C.DATA_FILE_NAME_ID,
-                              parquet_local=[P.to_local(f) for f in my_files])
-    cols = dict(up.columns)
-    _finish_strings(up.host_strings, cols, indexed, device, dist)
     names = list(schema.names)
     fields = list(schema)
     if lineage_ids is not None:
         names.append(C.DATA_FILE_NAME_ID)
         fields.append(pa.field(C.DATA_FILE_NAME_ID, pa.int64(), False))
+    on_batch, nullable, batches = None, None, None
+    if xs is not None and not any(is_string(f.type) for f in schema):
+        fixed = [f.name for f in schema]
+        may = set().union(*[m for _, m in infos]) if infos else set()
+        agreed = dist.agree_any([n in may for n in fixed])
+        nullable = {n for n, a in zip(fixed, agreed) if a}
+        on_batch = (lambda cols, lo, hi: xs.batch(cols, names, lo, hi))
+        # every rank runs the same number of batches (each is a collective); ranks with fewer
+        # files send empty batches
+        k = int(dist.all_reduce_max_float(float(-(-len(my_files) // FILES_PER_BATCH))))
+        edges = np.linspace(0, len(my_files), max(k, 1) + 1).round().astype(int)
+        batches = [(int(a), int(b)) for a, b in zip(edges[:-1], edges[1:])]
+    up = staging.upload_files(read_file, my_files, counts, schema, device, lin,
+                              C.DATA_FILE_NAME_ID,
+                              parquet_local=[P.to_local(f) for f in my_files],
+                              nullable=nullable, on_batch=on_batch, file_batches=batches)
+    cols = dict(up.columns)
+    _finish_strings(up.host_strings, cols, indexed, device, dist)
     return {n: cols[n] for n in names}, names, pa.schema(fields)
 
 

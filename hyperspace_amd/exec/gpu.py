@@ -500,7 +500,7 @@ class GpuBackend:
             with stage("shuffle.all_to_all"):
                 cols, bucket = self._exchange_rows(d, cols, bucket)
             kcols = [cols[k.expr_id] for k in keys]
-            counts = torch.bincount(bucket.long(), minlength=B)
+            counts = K.histogram(bucket, B)
         n = int(bucket.numel())
         with stage("shuffle.sort"):
             perm = K.sort_permutation(kcols, extra_leading=(bucket, 16))
@@ -546,45 +546,47 @@ class GpuBackend:
         return DRel(nt, colmap, list(r.attrs), list(r.conds), True, list(keys), list(keys), B)
 
     def _exchange_rows(self, d, cols: Dict[int, DeviceColumn], bucket):
-        """Route every row to rank ``bucket % world`` (all-to-all per column).  Ranks first agree
-        on column layouts: string dictionaries are unified (codes remapped on the device) and a
-        validity mask exists on every rank if it exists on any."""
+        """Route every row to rank ``bucket % world`` with ONE packed all-to-all
+        (``parallel/exchange.py``).  Ranks first agree on column layouts: a validity mask exists
+        on every rank if it exists on any (one small all-reduce), and string dictionaries are
+        unified (raw-buffer all-gather, ``parallel/dictionary.py``) with codes remapped on the
+        device."""
         import torch
-        from ..parallel.shuffle import exchange
+        from ..parallel.dictionary import remap_table, union_sorted
+        from ..parallel.exchange import RowExchange
         ids = list(cols)
-        lay = d.all_gather_object([(c.valid is not None,
-                                    c.dictionary.to_pylist() if c.dictionary is not None else None)
-                                   for c in (cols[i] for i in ids)])
+        need_valid = d.agree_any([cols[i].valid is not None for i in ids])
         datas, valids, dicts = [], [], []
         for j, i in enumerate(ids):
             c = cols[i]
             data = c.data
             gdict = None
             if c.dictionary is not None:
-                values = sorted({v for rk in lay for v in (rk[j][1] or [])})
-                pos = {v: k for k, v in enumerate(values)}
-                local = c.dictionary.to_pylist()
-                if local and values != local:
-                    remap = torch.tensor([pos[v] for v in local], dtype=torch.int32,
-                                         device=self.device)
-                    data = remap[data.long()]
-                elif not local:
+                gdict = union_sorted(c.dictionary, d)
+                if len(c.dictionary) == 0:
                     data = torch.zeros_like(data)
-                gdict = pa.array(values, type=pa.string())
-            need_valid = any(rk[j][0] for rk in lay)
+                elif not c.dictionary.equals(gdict):
+                    remap = torch.from_numpy(remap_table(c.dictionary, gdict)).to(self.device)
+                    data = K.lookup_i32(remap, data)
             v = c.valid
-            if need_valid and v is None:
+            if need_valid[j] and v is None:
                 v = torch.ones(data.shape[0], dtype=torch.uint8, device=self.device)
             datas.append(data)
-            valids.append(v if need_valid else None)
+            valids.append(v if need_valid[j] else None)
             dicts.append(gdict)
-        dest = (bucket % d.world).to(torch.int32)
-        moved, _ = exchange(datas + valids + [bucket], dest, d.world, ctx=d)
-        k = len(ids)
+        send = datas + [v for v in valids if v is not None] + [bucket]
+        moved = RowExchange(d, [t.dtype for t in send], self.device)
+        moved.add(send, bucket)
+        got = moved.finish()
         out = {}
+        vi = len(ids)
         for j, i in enumerate(ids):
-            out[i] = DeviceColumn(moved[j], moved[k + j], cols[i].atype, dicts[j])
-        return out, moved[2 * k]
+            mv = None
+            if valids[j] is not None:
+                mv = got[vi]
+                vi += 1
+            out[i] = DeviceColumn(got[j], mv, cols[i].atype, dicts[j])
+        return out, got[-1]
 
     # ------------------------------------------------------------------------------------------
     # Joins

@@ -235,11 +235,21 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
                  row_counts: Sequence[int], schema: pa.Schema, device,
                  lineage_ids: Optional[Sequence[int]] = None,
                  lineage_name: Optional[str] = None,
-                 parquet_local: Optional[Sequence[str]] = None) -> UploadResult:
+                 parquet_local: Optional[Sequence[str]] = None,
+                 nullable: Optional[set] = None,
+                 on_batch: Optional[Callable[[Dict[str, DeviceColumn], int, int], None]] = None,
+                 file_batches: Optional[Sequence[Tuple[int, int]]] = None) -> UploadResult:
     """Decode ``files`` in parallel and stream their fixed-width columns into HBM.
 
     ``row_counts[i]`` must equal the row count ``read_file(files[i])`` returns (Parquet footer);
     string columns are returned as host arrow chunks for dictionary encoding by the caller.
+
+    ``nullable`` names fixed-width columns that get an all-valid mask up front (so every batch
+    has one).  ``on_batch(columns, lo, hi)`` is called on this thread, in order, for every
+    ``file_batches`` entry ``(first file, end file)`` — empty ones included — once the rows
+    ``[lo, hi)`` of those files are on the device and ordered before the current stream's next
+    work, while the pool keeps decoding later files (the multi-GPU build exchanges each batch as
+    it lands).
 
     With ``parquet_local`` (local paths of Parquet ``files``) fixed-width columns go through the
     native page layer + HIP decode (``io/native_parquet.py``); ``read_file(path, columns)`` then
@@ -261,6 +271,9 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
     if lineage_ids is not None:
         cols[lineage_name] = DeviceColumn(torch.empty(n, dtype=torch.int64, device=device), None,
                                           pa.int64())
+    for name in (nullable or ()):
+        if name in cols:
+            cols[name].valid = torch.ones(n, dtype=torch.uint8, device=device)
     lock = threading.Lock()
     main = torch.cuda.current_stream(device)
     for st in streams:
@@ -287,7 +300,7 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
             if lineage_ids is not None:
                 with torch.cuda.stream(stream):
                     cols[lineage_name].data[lo:hi].fill_(int(lineage_ids[i]))
-            return hi - lo
+            return _done_event(stream)
         t = read_file(files[i], [f.name for f in rest]) if native else read_file(files[i])
         if t.num_rows != hi - lo:
             raise RuntimeError(f"row count mismatch for {files[i]}: footer {hi - lo}, read "
@@ -305,9 +318,21 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
         if lineage_ids is not None:
             with torch.cuda.stream(stream):
                 cols[lineage_name].data[lo:hi].fill_(int(lineage_ids[i]))
-        return t.num_rows
+        return _done_event(stream)
+
+    def _done_event(stream):
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        return ev
 
     futs = [io_pool().submit(work, i) for i in range(len(files))]
+    if file_batches is None:
+        file_batches = [(0, len(files))]
+    for b0, b1 in file_batches:
+        for fu in futs[b0:b1]:
+            main.wait_event(fu.result())
+        if on_batch is not None:
+            on_batch(cols, int(offs[b0]), int(offs[b1]))
     for fu in futs:
         fu.result()
     for st in streams:

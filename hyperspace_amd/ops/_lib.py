@@ -91,6 +91,20 @@ class GatherParams(C.Structure):
                 ("idx_is_u32", C.c_int32)]
 
 
+XCH_MAX_COLS = 32
+XCH_MAX_DEST = 64
+
+
+class XchParams(C.Structure):
+    _fields_ = [("src", C.c_void_p * XCH_MAX_COLS), ("elem_bytes", C.c_int32 * XCH_MAX_COLS),
+                ("ncols", C.c_int32), ("world", C.c_int32)]
+
+
+class XchCopy(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("count", C.c_int64),
+                ("elem_bytes", C.c_int32), ("pad", C.c_int32)]
+
+
 _lib = None
 
 
@@ -124,7 +138,8 @@ def lib():
     P, I, I64, U64 = C.c_void_p, C.c_int, C.c_int64, C.c_uint64
     for name, st in (("hs_hash_params_size", HashParams), ("hs_scan_params_size", ScanParams),
                      ("hs_join_params_size", JoinParams), ("hs_sort_key_spec_size", SortKeySpec),
-                     ("hs_gather_params_size", GatherParams)):
+                     ("hs_gather_params_size", GatherParams), ("hs_xch_params_size", XchParams),
+                     ("hs_xch_copy_size", XchCopy)):
         f = getattr(L, name)
         f.restype = C.c_int
         if f() != C.sizeof(st):
@@ -161,6 +176,10 @@ def lib():
     _sig(L.hs_pq_pack, I, P, P, I, I64, I, P, P)
     _sig(L.hs_pq_warmup, I, P)
     _sig(L.hs_pq_dict_codes, I, P, I64, I, P, I, P, P, P)
+    _sig(L.hs_histogram, I, P, I64, I, P, P)
+    _sig(L.hs_xch_tile_rows, I)
+    _sig(L.hs_xch_pack, I, P, P, I64, P, P, P, P)
+    _sig(L.hs_xch_unpack, I, P, I, I64, P)
     _lib = L
     return L
 

@@ -181,6 +181,25 @@ def gather_columns(cols: list, idx, want_valid: bool = True) -> list:
     return out
 
 
+def histogram(ids, num_bins: int):
+    """int64 counts of int32 ``ids`` over ``[0, num_bins)`` (LDS-privatised HIP histogram;
+    replaces ``torch.bincount`` on the build path)."""
+    torch = _torch()
+    out = torch.empty(num_bins, dtype=torch.int64, device=ids.device)
+    if num_bins > 16384:
+        return torch.bincount(ids.long(), minlength=num_bins)
+    NL.check(NL.lib().hs_histogram(NL.ptr(ids), ids.numel(), num_bins, NL.ptr(out),
+                                   NL.stream_ptr()), "hs_histogram")
+    return out
+
+
+def lookup_i32(table, codes):
+    """``table[codes]`` for an int32 table and int32 codes, through the gather kernel."""
+    from ..exec.device_table import DeviceColumn
+    import pyarrow as pa
+    return gather_columns([DeviceColumn(table, None, pa.int32())], codes, want_valid=False)[0].data
+
+
 def bucket_offsets_from_sorted(sorted_bucket, num_buckets: int):
     torch = _torch()
     off = torch.empty(num_buckets + 1, dtype=torch.int64, device=sorted_bucket.device)

@@ -150,6 +150,15 @@ class DistContext:
             return s, c, mn, mx
         return fetch
 
+    def agree_any(self, flags) -> list:
+        """Element-wise OR of a list of booleans over all ranks (one small max all-reduce on a
+        tensor — used where every rank must take the same data-dependent decision)."""
+        import torch
+        dev = self.device if self.backend == "nccl" else "cpu"
+        t = torch.tensor([1 if f else 0 for f in flags] or [0], dtype=torch.int64, device=dev)
+        self.all_reduce(t, "max")
+        return [bool(v) for v in t.cpu().tolist()][:len(flags)]
+
     def all_reduce_max_float(self, x: float) -> float:
         import torch
         dev = self.device if self.backend == "nccl" else "cpu"

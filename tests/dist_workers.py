@@ -8,12 +8,20 @@ import os
 import traceback
 
 
-def _init(rank: int, world: int, port: int):
+def _init(rank: int, world: int, port: int, backend: str = "gloo"):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
                        "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
-                       "HS_DIST_BACKEND": "gloo"})
+                       "HS_DIST_BACKEND": backend})
+    if backend == "nccl":
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     from hyperspace_amd.parallel.dist import DistContext
-    return DistContext.from_env(backend="gloo")
+    if world == 1:
+        import torch.distributed as dist
+        import torch
+        torch.cuda.set_device(0)
+        dist.init_process_group(backend=backend, rank=0, world_size=1,
+                                device_id=torch.device("cuda", 0))
+    return DistContext.from_env(backend=backend)
 
 
 def _finish(out_dir: str, rank: int, result: dict) -> None:
@@ -24,10 +32,11 @@ def _finish(out_dir: str, rank: int, result: dict) -> None:
         dist.destroy_process_group()
 
 
-def run(rank: int, world: int, port: int, scenario: str, out_dir: str, data_dir: str) -> None:
+def run(rank: int, world: int, port: int, scenario: str, out_dir: str, data_dir: str,
+        backend: str = "gloo") -> None:
     result = {"rank": rank}
     try:
-        ctx = _init(rank, world, port)
+        ctx = _init(rank, world, port, backend)
         result.update(SCENARIOS[scenario](ctx, data_dir))
     except Exception as e:  # noqa: BLE001 — reported to the parent
         result["error"] = f"{type(e).__name__}: {e}\n{traceback.format_exc()}"
@@ -52,9 +61,13 @@ def collectives(ctx, data_dir):
     vals = torch.arange(n, dtype=torch.int64) + 1000 * r
     fl = vals.double() * 0.5
     (rv, rf), counts = exchange([vals, fl], dest, w, ctx=ctx)
+    import pyarrow as pa
+    from hyperspace_amd.parallel.dictionary import union_sorted
+    local = pa.array([f"s{r}_{i}" for i in range(r + 2)] + ["common", None])
+    gd = union_sorted(local, ctx)
     return {"sums": s.tolist(), "cnts": c.tolist(), "mins": mn.tolist(), "maxs": mx.tolist(),
             "objs": objs, "recv": rv.tolist(), "recv_f": rf.tolist(), "recv_counts": counts.tolist(),
-            "sent": {"dest": dest.tolist(), "vals": vals.tolist()}}
+            "sent": {"dest": dest.tolist(), "vals": vals.tolist()}, "dict": gd.to_pylist()}
 
 
 def _session(ctx, data_dir, **conf):
@@ -141,4 +154,52 @@ def spmd_gpu(ctx, data_dir):
     return out
 
 
-SCENARIOS = {"collectives": collectives, "spmd_index": spmd_index, "spmd_gpu": spmd_gpu}
+def nccl_paths(ctx, data_dir):
+    """Every RCCL branch of ``parallel/`` on the process group it was given (world 1 on a
+    1-GPU box, more ranks on a multi-GPU node): device all-reduce / all-gather / all-to-all,
+    the packed row exchange, the raw-buffer dictionary union and the one-collective aggregate
+    combine."""
+    import numpy as np
+    import pyarrow as pa
+    import torch
+    from hyperspace_amd.parallel.dictionary import union_sorted
+    from hyperspace_amd.parallel.exchange import RowExchange
+    assert ctx.backend == "nccl", ctx.backend
+    dev = ctx.device
+    r, w = ctx.rank, ctx.world
+    out = {}
+    t = torch.tensor([1.0 + r], dtype=torch.float64, device=dev)
+    ctx.all_reduce(t, "sum")
+    out["allreduce"] = t.item()
+    out["agree"] = ctx.agree_any([r == 0, False])
+    out["max"] = ctx.all_reduce_max_float(float(r))
+    g = torch.Generator().manual_seed(7 + r)
+    n = 100_000 + 1234 * r
+    bucket = torch.randint(0, 200, (n,), generator=g, dtype=torch.int32)
+    vals = torch.arange(n, dtype=torch.int64) + (r << 40)
+    f32 = (vals & ((1 << 40) - 1)).float() * 0.25
+    valid = (torch.arange(n) % 3 != 0).to(torch.uint8)
+    ex = RowExchange(ctx, [torch.int64, torch.float32, torch.uint8, torch.int32], dev)
+    half = n // 2
+    for lo, hi in ((0, half), (half, half), (half, n)):   # incl. an empty batch
+        ex.add([vals[lo:hi].to(dev), f32[lo:hi].to(dev), valid[lo:hi].to(dev),
+                bucket[lo:hi].to(dev)], bucket[lo:hi].to(dev))
+    gv, gf, gvalid, gb = (x.cpu() for x in ex.finish())
+    out["xch_rows"] = int(gv.numel())
+    out["xch_owner_ok"] = bool(((gb % w) == r).all())
+    out["xch_f_ok"] = bool(torch.equal(gf, (gv & ((1 << 40) - 1)).float() * 0.25))
+    out["xch_valid_ok"] = bool(torch.equal(gvalid, ((gv & ((1 << 40) - 1)) % 3 != 0).to(torch.uint8)))
+    out["xch_sum"] = int(gv.sum())
+    gd = union_sorted(pa.array([f"k{r}", "shared", f"x{r * 7}"]), ctx)
+    out["dict"] = gd.to_pylist()
+    sums = torch.tensor([1.5, 2.5], dtype=torch.float64, device=dev)
+    cnts = torch.tensor([1, 2], dtype=torch.int64, device=dev)
+    mins = torch.tensor([float(r), 0.0], dtype=torch.float64, device=dev)
+    maxs = torch.tensor([float(r), 9.0], dtype=torch.float64, device=dev)
+    s, c, mn, mx = ctx.combine_aggs_async(sums, cnts, mins, maxs)()
+    out["combine"] = [s.tolist(), c.tolist(), mn.tolist(), mx.tolist()]
+    ctx.barrier()
+    return out
+
+
+SCENARIOS = {"nccl_paths": nccl_paths, "collectives": collectives, "spmd_index": spmd_index, "spmd_gpu": spmd_gpu}

@@ -278,3 +278,62 @@ def test_join_many_to_many_with_nulls_and_wide_spans(device):
                 np.testing.assert_allclose(js.cpu().numpy(), exp_s, rtol=1e-9)
     finally:
         jit.JOIN_PIPELINE, jit.JOIN_STAGE_RIGHT = saved
+
+
+@pytest.mark.parametrize("world", [1, 3, 8, 64])
+def test_packed_exchange_kernel_matches_reference(device, world):
+    """hs_xch_pack writes the exact byte layout of the numpy oracle (stable per-destination
+    segments, 16-byte aligned column runs) and hs_xch_unpack restores the columns."""
+    import ctypes as C
+    import torch
+    from hyperspace_amd.ops import _lib as NL
+    from hyperspace_amd.parallel.exchange import pack_reference, segment_bytes
+    rng = np.random.default_rng(world)
+    n = 3 * 4096 + 77
+    bucket = rng.integers(0, 200, n).astype(np.int32)
+    cols = [rng.integers(-2**62, 2**62, n).astype(np.int64), rng.random(n).astype(np.float32),
+            rng.integers(0, 2, n).astype(np.uint8), rng.integers(0, 9, n).astype(np.int16), bucket]
+    ref, counts, lay = pack_reference(cols, bucket, world)
+    dcols = [torch.from_numpy(c).to(device) for c in cols]
+    L = NL.lib()
+    ntiles = (n + L.hs_xch_tile_rows() - 1) // L.hs_xch_tile_rows()
+    tile = torch.empty(ntiles * world, dtype=torch.int64, device=device)
+    meta = torch.zeros(2 * world + world * (len(cols) + 1), dtype=torch.int64, device=device)
+    send = torch.zeros(n * sum(c.dtype.itemsize for c in cols) + 16 * world * len(cols),
+                       dtype=torch.uint8, device=device)
+    p = NL.XchParams()
+    for i, c in enumerate(dcols):
+        p.src[i] = c.data_ptr()
+        p.elem_bytes[i] = c.element_size()
+    p.ncols, p.world = len(cols), world
+    NL.check(L.hs_xch_pack(C.byref(p), NL.ptr(dcols[-1]), n, NL.ptr(tile), NL.ptr(meta),
+                           NL.ptr(send), NL.stream_ptr()), "pack")
+    m = meta.cpu().numpy()
+    assert np.array_equal(m[:world], counts)
+    assert np.array_equal(m[2 * world:].reshape(world, -1), lay)
+    got = send.cpu().numpy()[:len(ref)]
+    # compare only the value bytes (alignment padding is unspecified)
+    for d in range(world):
+        for ci, c in enumerate(cols):
+            o, k = int(lay[d, ci]), int(counts[d]) * c.dtype.itemsize
+            assert np.array_equal(got[o:o + k], ref[o:o + k]), (d, ci)
+    # unpack through the exchange's copy table (world-1 local "exchange")
+    from hyperspace_amd.parallel.exchange import RowExchange
+    if world == 1:
+        ex = RowExchange(None, [c.dtype for c in dcols], device)
+        ex.add(dcols, dcols[-1])
+        outs = ex.finish()
+        for o, c in zip(outs, cols):
+            assert np.array_equal(o.cpu().numpy(), c)
+    assert segment_bytes(int(counts[0]), [c.dtype.itemsize for c in cols]) == \
+        int(lay[0, -1] - lay[0, 0])
+
+
+def test_histogram_kernel(device):
+    import torch
+    from hyperspace_amd.ops import kernels as K
+    rng = np.random.default_rng(2)
+    for B in (1, 200, 16384):
+        ids = rng.integers(0, B, 1_000_003).astype(np.int32)
+        got = K.histogram(torch.from_numpy(ids).to(device), B).cpu().numpy()
+        assert np.array_equal(got, np.bincount(ids, minlength=B))
