@@ -280,6 +280,7 @@ def _upload_parquet(rel, my_files, columns, indexed, lineage_ids, device, dist, 
     """Pipelined decode -> pinned -> HBM upload of this rank's Parquet files (staging.py).
     With a multi-GPU exchange ``xs`` and no string columns, every batch of files is hashed and
     exchanged as soon as it is on the device, overlapping the decode of the next batch."""
+    import pyarrow.parquet as pq
     from ..io.reader import output_schema, read_files
     from . import staging
     schema = output_schema(rel.data_schema, rel.location.partition_spec, columns)

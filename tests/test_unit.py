@@ -5,6 +5,8 @@ Mirrors the reference's pure-unit tier: ``IndexConfigTest``, ``Json
 ``HashingUtilsTest``, ``BufferStreamTest``, ``DisplayModeTest``, ``HyperspaceConfTest``,
 ``IndexCacheTest`` (mock clock) and ``BucketUnionTest.scala:101-122`` (Murmur3 vectors).
 """
+import os
+
 import numpy as np
 import pyarrow as pa
 import pytest
@@ -344,3 +346,13 @@ def test_event_logger_by_class_name():
     assert isinstance(lg, RecordingLogger)
     with pytest.raises(HyperspaceException):
         get_event_logger(RuntimeConf({C.EVENT_LOGGER_CLASS_KEY: "no.such.Logger"}))
+
+
+def test_lint_gate_no_undefined_names():
+    """scripts/lint_names.py: no function reads a name defined nowhere (dropped imports)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "lint_names.py")],
+                       cwd=root, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
