@@ -94,7 +94,10 @@ def encode(col) -> Optional[Compact]:
             q = torch.round(x * s)
             if float(q.abs().max().item()) >= 2.0 ** 52:
                 return None
-            back = (q / s).view(torch.int64)
+            # divide by a device tensor: torch implements division by a Python scalar as a
+            # multiply by its reciprocal on the GPU (not correctly rounded), while the kernels
+            # decode with an IEEE division
+            back = (q / torch.full((), s, dtype=torch.float64, device=q.device)).view(torch.int64)
             same = bool((back == x.view(torch.int64)).all())  # bit-exact
             if not same:
                 continue

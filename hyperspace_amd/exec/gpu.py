@@ -1153,7 +1153,8 @@ class GpuBackend:
                                                  right.col(rk), fs, fl, fb)
             with stage("join.index_agg_kernel"):
                 return jit.join_index_agg(jp, rstart, rlen, jidx, self._compacts(descs),
-                                          nrows=left.table.num_rows)
+                                          nrows=left.table.num_rows,
+                                          rnrows=right.table.num_rows)
         with stage("join.agg_kernel"):
             if HyperspaceConf.codegen_enabled(self.session.conf):
                 fr = getattr(left.table, "_full_ranges", None)

@@ -56,6 +56,15 @@ JI_ITEMS = int(os.environ.get("HS_JIT_JI_ITEMS", "4"))
 JI_VEC = int(os.environ.get("HS_JIT_JI_VEC", "8"))
 # join-index kernel: run the aggregate phase over a per-wavefront list of passing rows only
 JI_COMPACT = os.environ.get("HS_JIT_JI_COMPACT", "1") == "1"
+# join-index kernel phase 2 through a per-wavefront LDS copy of the matched right rows' run
+# (_ji_stage_phase2); measured slower than both alternatives on the Q3 shape, off by default
+JI_STAGE = os.environ.get("HS_JIT_JI_STAGE", "0") == "1"
+# join-index kernel phase 2 as a semi-join bitmap: the right side's predicates are evaluated
+# once per query over the right table into one bit per row (gen_pred_bitmap), and the join
+# kernel tests bits (cache-resident) instead of gathering right columns from HBM.  Off by
+# default: on the SF100 Q3 shape bitmap kernel + join measured no faster than the gathers
+# (profiles/qk_sweep_r2.jsonl)
+JI_BITMAP = os.environ.get("HS_JIT_JI_BITMAP", "0") == "1"
 # scan kernel: same, for the aggregate inputs loaded after the predicates
 SCAN_COMPACT = os.environ.get("HS_JIT_SCAN_COMPACT", "1") == "1"
 # > 0: rows per thread of the vectorized scan kernel (aligned vector loads of predicate columns)
@@ -68,6 +77,10 @@ JOIN_PIPELINE = os.environ.get("HS_JIT_JOIN_PIPELINE", "1") == "1"
 # search is not on this kernel's critical path, the extra table writes and loads are
 JOIN_DIRECT = os.environ.get("HS_JIT_JOIN_DIRECT", "0") == "1"
 JOIN_DIRECT_SLOTS = int(os.environ.get("HS_JIT_JOIN_DIRECT_SLOTS", "2048"))
+# software-pipelined full tiles in the vectorized kernels (_vec_tiles)
+VEC_PREFETCH = os.environ.get("HS_JIT_VEC_PREFETCH", "1") == "1"
+# per-wavefront compaction lists ordered by a wavefront barrier instead of __syncthreads
+WAVE_SYNC = os.environ.get("HS_JIT_WAVE_SYNC", "1") == "1"
 
 _CTYPE = {NL.I8: "signed char", NL.I16: "short", NL.I32: "int", NL.I64: "long long",
           NL.F32: "float", NL.F64: "double", NL.BOOL: "unsigned char", NL.U32: "unsigned int",
@@ -75,6 +88,8 @@ _CTYPE = {NL.I8: "signed char", NL.I16: "short", NL.I32: "int", NL.I64: "long lo
 _OPSTR = {NL.OP_EQ: "==", NL.OP_NE: "!=", NL.OP_LT: "<", NL.OP_LE: "<=", NL.OP_GT: ">",
           NL.OP_GE: ">="}
 _CODE_T = {1: "signed char", 2: "short", 4: "int"}   # exec.encoding code widths
+_SIZEOF = {"signed char": 1, "unsigned char": 1, "short": 2, "unsigned short": 2, "int": 4,
+           "unsigned int": 4, "float": 4, "long long": 8, "unsigned long long": 8, "double": 8}
 
 _rt = None
 _rt_lock = threading.Lock()
@@ -171,6 +186,13 @@ class Kernel:
     def function(self):
         if self._fn is None:
             L = runtime()
+            dump = os.environ.get("HS_JIT_DUMP")
+            if dump:   # generated sources for inspection / offline ISA (hipcc --save-temps)
+                import hashlib
+                os.makedirs(dump, exist_ok=True)
+                h = hashlib.md5(self.src.encode()).hexdigest()[:10]
+                with open(os.path.join(dump, f"{self.name}_{h}.hip"), "w") as f:
+                    f.write("#include <hip/hip_runtime.h>\n" + self.src)
             compiled = C.c_int(0)
             fn = L.hs_jit_get(self.src.encode(), self.name.encode(), ARCH.encode(),
                               CACHE_DIR.encode(), C.byref(compiled))
@@ -331,11 +353,19 @@ class _Gen:
             return f"(!{self.ok(c)})"
         if kind == NL.PK_NOT_NULL:
             return f"({self.ok(c)})"
+        enc = self.cols[c][2]
+        if self.intpred and enc and (kind == NL.PK_INT_LIT and not enc[1] or
+                                     kind == NL.PK_FLT_LIT and enc[1]):
+            # compact column: compare the stored code with host-computed 32-bit code bounds
+            # (exact: code_bounds), no decode and no 64-bit compare
+            lo = self.a.add("q", f"CL{k}", "long long")
+            hi = self.a.add("q", f"CH{k}", "long long")
+            inside = f"(r{c} >= (int){lo} && r{c} <= (int){hi})"
+            return f"({self.ok(c)} && {'!' if op == NL.OP_NE else ''}{inside})"
         if kind == NL.PK_INT_LIT:
             lit = self.a.add("q", f"L{k}", "long long")
             return f"({self.ok(c)} && ((i64)x{c} {_OPSTR[op]} {lit}))"
         if kind == NL.PK_FLT_LIT:
-            enc = self.cols[c][2]
             if self.intpred and enc and enc[1]:
                 lo = self.a.add("q", f"T{k}", "long long")
                 hi = self.a.add("q", f"U{k}", "long long")
@@ -552,7 +582,7 @@ def scan_agg_shape(p: NL.ScanParams, compacts=None, vec: int = 0) -> tuple:
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
     return ("scan_agg", cols, preds, aggs, p.group_col, SCAN_ITEMS, SCAN_EAGER, vec,
-            SCAN_COMPACT)
+            SCAN_COMPACT, WAVE_SYNC, VEC_PREFETCH)
 
 
 def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
@@ -589,67 +619,61 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
     if grouped:
         base = args.add("q", "group_base", "long long")
         ng = args.add("q", "num_groups", "long long")
-    b += ["  const i64 ntiles = a.tile_prefix[a.R];",
-          "  const i64 per = (ntiles + gridDim.x - 1) / gridDim.x;",
-          "  const i64 t0 = (i64)blockIdx.x * per;",
-          "  const i64 t1 = ntiles < t0 + per ? ntiles : t0 + per;",
-          "  int r = 0;",
-          "  if (t0 < t1) { int lo = 0, hi = (int)a.R;",
-          "    while (hi - lo > 1) { const int m = (lo + hi) >> 1; if (a.tile_prefix[m] <= t0) lo = m; else hi = m; }",
-          "    r = lo; }",
-          "  for (i64 t = t0; t < t1; ++t) {",
-          "    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;",
-          f"    const i64 off = (t - a.tile_prefix[r]) * {T};"]
     ind = "    "
-    if vec:
-        _vec_rows(b, NI, ind)
-        _vec_load_slots(b, _Gen(args, cols, NL.MAX_COLS, ("row0", "row0"), approx, True), pslots, NI, ind)
-    else:
-        b += ["    const i64 tb0 = a.rstart[r] + off;",
-              f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};"]
-        for it in range(NI):
-            b += [f"{ind}const bool act{it} = {it * BLOCK} + (i64)threadIdx.x < rows;",
-                  f"{ind}const i64 row{it} = tb0 + (act{it} ? {it * BLOCK} + (i64)threadIdx.x : 0);"]
+    g0_ = _Gen(args, cols, NL.MAX_COLS, ("row0", "row0"), approx, True)
+    compact = SCAN_COMPACT and bool(aslots)
+
+    def body(b: List[str], full: Optional[bool]) -> None:
+        """Tile body; ``full`` = vectorized full tile / vectorized last tile / None (scalar)."""
+        if full is not None:     # raw vector arrays come from the tile loop (_vec_tiles)
+            _vec_load_slots(b, g0_, pslots, NI, ind)
+        else:
+            b.extend(["    const i64 tb0 = a.rstart[r] + off;",
+                      f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};"])
+            for it in range(NI):
+                b.extend([f"{ind}const bool act{it} = {it * BLOCK} + (i64)threadIdx.x < rows;",
+                          f"{ind}const i64 row{it} = tb0 + (act{it} ? {it * BLOCK} + (i64)threadIdx.x : 0);"])
+            for it in range(NI):
+                g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"), approx, True)
+                for s in pslots:
+                    _uload(g1, s, it, b, ind)
         for it in range(NI):
             g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"), approx, True)
-            for s in pslots:
-                _uload(g1, s, it, b, ind)
-    for it in range(NI):
-        g1 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"), approx, True)
-        b.append(f"{ind}bool pass{it} = act{it} && {_rename(g1.cnf(preds), allslots, it)};")
-    if SCAN_COMPACT and aslots:
-        b += _compacted_tail(args, cols, NL.MAX_COLS, approx, aggs, grouped, p.group_col, aslots,
-                             allslots, NI, ind, with_j=False)
-        b += ["  }"]
-        b += _flush(aggs, grouped)
-        W = BLOCK // 64
-        b.insert(0, f"  __shared__ int crow_s[{W}][{64 * NI}];")
-        b.insert(1, "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;")
-        src = (_PRELUDE + args.struct_src() +
-               f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_scan_agg(Args a) {{\n' +
-               "\n".join(b) + "\n}\n")
-        lds = (len(aggs) * p.num_groups * 32) if grouped else 0
-        return Kernel(src, "hs_jit_scan_agg", args, lds)
-    if aslots:
+            b.append(f"{ind}bool pass{it} = act{it} && {_rename(g1.cnf(preds), allslots, it)};")
+        if compact:
+            b.extend(_compacted_tail(args, cols, NL.MAX_COLS, approx, aggs, grouped, p.group_col,
+                                     aslots, allslots, NI, ind, with_j=False))
+            return
+        if aslots:
+            for it in range(NI):
+                b.append(f"{ind}const i64 lq{it} = pass{it} ? row{it} : tb0;")
+            for it in range(NI):
+                g2 = _Gen(args, cols, NL.MAX_COLS, (f"lq{it}", f"lq{it}"), approx, True)
+                for s in aslots:
+                    _uload(g2, s, it, b, ind)
         for it in range(NI):
-            b.append(f"{ind}const i64 lq{it} = pass{it} ? row{it} : tb0;")
-        for it in range(NI):
-            g2 = _Gen(args, cols, NL.MAX_COLS, (f"lq{it}", f"lq{it}"), approx, True)
-            for s in aslots:
-                _uload(g2, s, it, b, ind)
-    for it in range(NI):
-        g2 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"), approx, True)
-        gvar = f"gi{it}"
-        if grouped:
-            g = p.group_col
-            b.append(f"{ind}const i64 gl{it} = (i64){_rename(f'x{g}', allslots, it)} - {base};")
-            b.append(f"{ind}pass{it} = pass{it} && {_rename(g2.ok(g), allslots, it)} && "
-                     f"gl{it} >= 0 && gl{it} < {ng};")
-            b.append(f"{ind}const int {gvar} = pass{it} ? (int)gl{it} : 0;")
-        b += [_rename(x, allslots, it) for x in
-              _accumulate(g2, aggs, grouped, f"pass{it}", gvar, ind)]
+            g2 = _Gen(args, cols, NL.MAX_COLS, (f"row{it}", f"row{it}"), approx, True)
+            gvar = f"gi{it}"
+            if grouped:
+                g = p.group_col
+                b.append(f"{ind}const i64 gl{it} = (i64){_rename(f'x{g}', allslots, it)} - {base};")
+                b.append(f"{ind}pass{it} = pass{it} && {_rename(g2.ok(g), allslots, it)} && "
+                         f"gl{it} >= 0 && gl{it} < {ng};")
+                b.append(f"{ind}const int {gvar} = pass{it} ? (int)gl{it} : 0;")
+            b.extend(_rename(x, allslots, it) for x in
+                     _accumulate(g2, aggs, grouped, f"pass{it}", gvar, ind))
+
+    if vec:
+        _vec_tiles(b, T, NI, ind, _vec_loads(g0_, pslots), [], body)
+    else:
+        _tile_loop(b, T, NI, 0)
+        body(b, None)
     b += ["  }"]
     b += _flush(aggs, grouped)
+    if compact:
+        W = BLOCK // 64
+        b.insert(0, f"  typedef {_crow_t(T)} crow_t; __shared__ crow_t crow_s[{W}][{64 * NI}];")
+        b.insert(1, "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;")
     src = (_PRELUDE + args.struct_src() +
            f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_scan_agg(Args a) {{\n' +
            "\n".join(b) + "\n}\n")
@@ -669,6 +693,29 @@ def scan_agg_values(p: NL.ScanParams, rstart, rlen, tile_prefix, parts,
 
 
 _BIG = 1 << 62
+
+
+def _int_lit_bounds(op: int, lit: int) -> Tuple[int, int]:
+    """Inclusive [lo, hi] of the integer values v with ``v OP lit`` (EQ and NE: [lit, lit])."""
+    lit = int(lit)
+    if op == NL.OP_LT:
+        return (-_BIG, lit - 1)
+    if op == NL.OP_LE:
+        return (-_BIG, lit)
+    if op == NL.OP_GT:
+        return (lit + 1, _BIG)
+    if op == NL.OP_GE:
+        return (lit, _BIG)
+    return (lit, lit)
+
+
+def code_bounds(lo: int, hi: int, base: int) -> Tuple[int, int]:
+    """Value bounds [lo, hi] mapped to the stored codes (value = base + code) of a compact
+    column and clamped to int32, the widest code: exact, since every code lies in int32; an
+    empty range stays empty ((1, 0))."""
+    clo = max(int(lo) - int(base), -(1 << 31))
+    chi = min(int(hi) - int(base), (1 << 31) - 1)
+    return (clo, chi) if clo <= chi else (1, 0)
 
 
 def int_bounds(op: int, lit: float, scale: float) -> Tuple[int, int]:
@@ -720,6 +767,9 @@ def _fill_common(v: Dict[str, object], cols, preds, aggs, compacts=None) -> None
         c = (compacts or {}).get(p.col)
         if p.kind == NL.PK_FLT_LIT and c is not None and c.scale:
             v[f"T{k}"], v[f"U{k}"] = int_bounds(p.op, p.flit, c.scale)
+            v[f"CL{k}"], v[f"CH{k}"] = code_bounds(v[f"T{k}"], v[f"U{k}"], c.base)
+        elif p.kind == NL.PK_INT_LIT and c is not None and not c.scale:
+            v[f"CL{k}"], v[f"CH{k}"] = code_bounds(*_int_lit_bounds(p.op, p.ilit), c.base)
         v[f"S{k}"] = p.set or 0
         v[f"N{k}"] = p.set_len
     for i, a in enumerate(aggs):
@@ -1012,7 +1062,7 @@ def _rename(line: str, slots, it: int) -> str:
     """Suffix per-row-slot variables x<s>/n<s> with the batch item index."""
     import re
     for s in sorted(set(slots), reverse=True):
-        line = re.sub(rf"\b([xnq]){s}\b", rf"\g<1>{s}_{it}", line)
+        line = re.sub(rf"\b([xnqr]){s}\b", rf"\g<1>{s}_{it}", line)
     return line
 
 
@@ -1089,14 +1139,14 @@ def join_agg_values(p: NL.JoinParams, tile_prefix, spans, parts,
 # Join through a cached join index (exec/join_index.py)
 # ------------------------------------------------------------------------------------------------
 def join_index_agg_shape(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int = 4,
-                         jlog: int = 0) -> tuple:
+                         jlog: int = 0, stage: bool = False, bitmap: bool = False) -> tuple:
     cols = tuple(sorted(_col_specs(p, compacts).items()))
     preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
                    p.preds[k].group) for k in range(p.npreds))
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
     return ("join_index_agg", cols, preds, p.nlp, aggs, p.group_col, JI_ITEMS, vec, BLOCK, jw,
-            jlog, JI_COMPACT)
+            jlog, JI_COMPACT, WAVE_SYNC, bool(stage and vec), bool(bitmap), VEC_PREFETCH)
 
 
 def _uload(gen: _Gen, slot: int, it: int, out: List[str], ind: str) -> None:
@@ -1106,10 +1156,12 @@ def _uload(gen: _Gen, slot: int, it: int, out: List[str], ind: str) -> None:
     ct = _CTYPE[gen.cols[slot][0]]
     r = gen.row(slot)
     enc = gen.cols[slot][2]
-    if enc and enc[1]:
-        base = gen.a.add("q", f"B{slot}", "long long")
+    if enc:
         out.append(f"{ind}const {gen.raw_type(slot)} w{slot}_{it} = {gen.ptr(slot)}[{r}];")
-        out.append(f"{ind}const i64 q{slot}_{it} = {base} + (i64)w{slot}_{it};")
+        out.append(f"{ind}const int r{slot}_{it} = (int)w{slot}_{it};")
+        if enc[1]:
+            base = gen.a.add("q", f"B{slot}", "long long")
+            out.append(f"{ind}const i64 q{slot}_{it} = {base} + (i64)w{slot}_{it};")
         out.append(f"{ind}const {ct} x{slot}_{it} = {gen.decode(slot, f'w{slot}_{it}')};")
     else:
         out.append(f"{ind}const {ct} x{slot}_{it} = {gen.value(slot, r)};")
@@ -1117,36 +1169,174 @@ def _uload(gen: _Gen, slot: int, it: int, out: List[str], ind: str) -> None:
         out.append(f"{ind}const bool n{slot}_{it} = {gen.vptr(slot)}[{r}] != 0;")
 
 
+def _crow_t(T: int) -> str:
+    """Element type of the compaction lists' tile-relative row offsets."""
+    return "unsigned short" if T + 8 <= 65536 else "int"
+
+
+def _wave_sync(force: bool = False) -> str:
+    """Barrier that orders the per-wavefront LDS compaction lists: each wavefront owns its own
+    list, and a wavefront's LDS operations execute in order, so only the compiler has to be kept
+    from moving accesses across (a block-wide barrier would make the block's wavefronts wait for
+    each other's memory round trips)."""
+    return ("__builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\"); "
+            "__builtin_amdgcn_wave_barrier(); "
+            "__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");") if (WAVE_SYNC or force) \
+        else "__syncthreads();"
+
+
 def _vec_rows(b: List[str], NI: int, ind: str) -> None:
     """Row mapping of a vectorized tile: the tile covers range r from its start rounded down to
     a multiple of NI, each thread owns NI consecutive rows at an aligned index ``g0``; rows
-    outside [rs, re) are inactive and point at an in-range row."""
+    outside [rs, re) are inactive (their ``row`` is never read: every use is guarded by the
+    item's ``act``/``pass``).  Activity is two 32-bit compares per item against the thread's
+    clamped item bounds [alo, ahi)."""
     b += ["    const i64 rs = a.rstart[r], re = rs + a.rlen[r];",
           f"    const i64 tb0 = (rs & ~(i64){NI - 1}) + off;",
-          f"    const i64 g0 = tb0 + (i64)threadIdx.x * {NI};",
-          f"    const bool vok = g0 + {NI} <= a.nrows;"]
+          f"    const i64 g0 = tb0 + (i64)threadIdx.x * {NI};"]
+    _vec_act(b, NI, ind)
+
+
+def _vec_act(b: List[str], NI: int, ind: str) -> None:
+    """Per-item activity and rows of a vectorized tile from its geometry ``rs re g0``."""
+    b += [f"    const i64 dlo_ = rs - g0, dhi_ = re - g0;",
+          f"    const int alo = dlo_ <= 0 ? 0 : (dlo_ >= {NI} ? {NI} : (int)dlo_);",
+          f"    const int ahi = dhi_ <= 0 ? 0 : (dhi_ >= {NI} ? {NI} : (int)dhi_);"]
     for it in range(NI):
-        b += [f"{ind}const bool act{it} = g0 + {it} >= rs && g0 + {it} < re;",
-              f"{ind}const i64 row{it} = act{it} ? g0 + {it} : tb0 > rs ? tb0 : rs;"]
+        b += [f"{ind}const bool act{it} = {it} >= alo && {it} < ahi;",
+              f"{ind}const i64 row{it} = g0 + {it};"]
 
 
-def _vec_load_slots(b: List[str], gen: "_Gen", slots, NI: int, ind: str, extra=()) -> None:
-    """Aligned vector loads of NI consecutive rows for every column in ``slots`` (plus
-    ``extra`` = (name, C type, pointer) raw arrays), then per-item registers x<s>_<k> /
-    n<s>_<k>.  The last partial vector of a column (``!vok``) loads element-wise."""
+def _vec_loads(gen: "_Gen", slots, extra=()) -> List[Tuple[str, str, str]]:
+    """(array name, C type, pointer) of every streamed vector load of a tile: ``extra`` raw
+    arrays, the stored elements of ``slots`` and their validity bytes."""
     loads = list(extra) + [(f"x{s}", gen.raw_type(s), gen.ptr(s)) for s in slots]
     for s in slots:
         if gen.cols[s][1]:
             loads.append((f"n{s}", "unsigned char", gen.vptr(s)))
+    return loads
+
+
+_TILE_HEAD = ["  const i64 ntiles = a.tile_prefix[a.R];",
+              "  const i64 per = (ntiles + gridDim.x - 1) / gridDim.x;",
+              "  const i64 t0 = (i64)blockIdx.x * per;",
+              "  const i64 t1 = ntiles < t0 + per ? ntiles : t0 + per;",
+              "  int r = 0;",
+              "  if (t0 < t1) { int lo = 0, hi = (int)a.R;",
+              "    while (hi - lo > 1) { const int m = (lo + hi) >> 1; if (a.tile_prefix[m] <= t0) lo = m; else hi = m; }",
+              "    r = lo; }"]
+
+
+def _tile_loop(b: List[str], T: int, NI: int, vec: int, ind: str = "    ") -> None:
+    """Header of the persistent tile loop of the streaming kernels: each block owns a contiguous
+    run of ``T``-row tiles and ``r`` tracks the row range of the tile.  Vectorized tiles
+    (``vec``) also get the row geometry ``rs re tb0 g0 act<k> row<k>``."""
+    b += _TILE_HEAD
+    b += ["  for (i64 t = t0; t < t1; ++t) {",
+          "    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;",
+          f"    const i64 off = (t - a.tile_prefix[r]) * {T};"]
+    if vec:
+        _vec_rows(b, NI, ind)
+
+
+def _vec_tiles(b: List[str], T: int, NI: int, ind: str, loads, scalars, body) -> None:
+    """Tile loops of a vectorized streaming kernel (``body(b, mode)`` emits one tile's work;
+    ``loads`` = (name, C type, pointer) vector arrays, ``scalars`` = (name, C type, expression
+    over ``G0``) per-thread values loaded with them).
+
+    Tiles that end inside the table (``tb0 + T <= nrows``: every tile but the table's last few)
+    read their columns with unconditional aligned vector loads, the rest element-wise, behind a
+    wavefront-uniform test — a per-thread ``if (vok) vector else elements`` merge makes the
+    compiler wait for each vector load before the merge, one round trip per column.
+
+    With VEC_PREFETCH the full tiles run software pipelined: tile t+1's vector loads are issued
+    at the top of tile t, before t's predicates, gathers and aggregate tail, so each wavefront
+    keeps the next tile's stream in flight across this tile's dependent round trips.  Full
+    tiles precede partial ones in a block's run, so the pipelined loop runs first and the
+    element-wise loop finishes the run."""
+    if not VEC_PREFETCH:
+        _tile_loop(b, T, NI, 1, ind)
+        b.append(f"{ind}if (tb0 + {T} <= a.nrows) {{")
+        _vec_issue(b, loads, NI, ind, True)
+        for name, ct, expr in scalars:
+            b.append(f"{ind}const {ct} {name} = {expr.replace('G0', 'g0')};")
+        body(b, True)
+        b.append(f"{ind}}} else {{")
+        _vec_issue(b, loads, NI, ind, False)
+        for name, ct, expr in scalars:
+            b.append(f"{ind}const {ct} {name} = {expr.replace('G0', 'g0')};")
+        body(b, False)
+        b.append(f"{ind}}}")
+        return
+    b += _TILE_HEAD
+
+    def geom(texpr: str, i2: str) -> None:
+        b.extend([f"{i2}while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= {texpr}) ++r;",
+                  f"{i2}{{ const i64 off_ = ({texpr} - a.tile_prefix[r]) * {T};",
+                  f"{i2}  rsP = a.rstart[r]; reP = rsP + a.rlen[r];",
+                  f"{i2}  tb0P = (rsP & ~(i64){NI - 1}) + off_;",
+                  f"{i2}  g0P = tb0P + (i64)threadIdx.x * {NI}; }}",
+                  f"{i2}fullP = tb0P + {T} <= a.nrows;",
+                  f"{i2}if (fullP) {{"])
+        for name, ct, ptr in loads:
+            b.append(f"{i2}  vload<{ct}, {NI}>({ptr}, g0P, {name}vP);")
+        for name, ct, expr in scalars:
+            b.append(f"{i2}  {name}P = {expr.replace('G0', 'g0P')};")
+        b.append(f"{i2}}}")
+
+    b.append("  i64 rsP = 0, reP = 0, tb0P = 0, g0P = 0; bool fullP = false;")
+    for name, ct, _ in loads:
+        b.append(f"  {ct} {name}vP[{NI}];")
+    for name, ct, _ in scalars:
+        b.append(f"  {ct} {name}P = ({ct})0;")
+    b.append("  i64 t = t0;")
+    b.append("  if (t < t1) {")
+    geom("t", "    ")
+    b.append("  }")
+    b += ["  for (; t < t1 && fullP; ++t) {",
+          "    const i64 rs = rsP, re = reP, tb0 = tb0P, g0 = g0P;"]
+    for name, ct, _ in loads:
+        b.append(f"{ind}{ct} {name}v[{NI}]; " +
+                 " ".join(f"{name}v[{k}] = {name}vP[{k}];" for k in range(NI)))
+    for name, ct, _ in scalars:
+        b.append(f"{ind}const {ct} {name} = {name}P;")
+    b.append(f"{ind}if (t + 1 < t1) {{")
+    geom("(t + 1)", ind + "  ")
+    b.append(f"{ind}}} else fullP = false;")
+    _vec_act(b, NI, ind)
+    body(b, True)
+    b.append("  }")
+    b += ["  for (; t < t1; ++t) {",
+          "    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;",
+          f"    const i64 off = (t - a.tile_prefix[r]) * {T};"]
+    _vec_rows(b, NI, ind)
+    _vec_issue(b, loads, NI, ind, False)
+    for name, ct, expr in scalars:
+        b.append(f"{ind}const {ct} {name} = {expr.replace('G0', 'g0')};")
+    body(b, False)
+
+
+def _vec_issue(b: List[str], loads, NI: int, ind: str, full: bool) -> None:
+    """Loads of the NI consecutive rows at ``g0`` into ``<name>v`` for every (name, C type,
+    pointer) of ``loads``: aligned vector loads in full tiles, guarded element loads otherwise."""
     for name, ct, ptr in loads:
         b.append(f"{ind}{ct} {name}v[{NI}];")
-        b.append(f"{ind}if (vok) vload<{ct}, {NI}>({ptr}, g0, {name}v);")
-        b.append(f"{ind}else {{ " + " ".join(
-            f"{name}v[{k}] = act{k} ? {ptr}[g0 + {k}] : ({ct})0;" for k in range(NI)) + " }")
+        if full:
+            b.append(f"{ind}vload<{ct}, {NI}>({ptr}, g0, {name}v);")
+        else:
+            b.append(f"{ind}" + " ".join(
+                f"{name}v[{k}] = act{k} ? {ptr}[g0 + {k}] : ({ct})0;" for k in range(NI)))
+
+
+def _vec_load_slots(b: List[str], gen: "_Gen", slots, NI: int, ind: str) -> None:
+    """Per-item registers x<s>_<k> / n<s>_<k> (decoded) of the raw vector arrays the tile loop
+    loaded for ``slots``."""
     for it in range(NI):
         for s in slots:
             ct = _CTYPE[gen.cols[s][0]]
             enc = gen.cols[s][2]
+            if enc:
+                b.append(f"{ind}const int r{s}_{it} = (int)x{s}v[{it}];")
             if enc and enc[1]:
                 base = gen.a.add("q", f"B{s}", "long long")
                 b.append(f"{ind}const i64 q{s}_{it} = {base} + (i64)x{s}v[{it}];")
@@ -1164,19 +1354,19 @@ def _compacted_tail(args, cols, split, approx, aggs, grouped, group_col, third, 
     """Phase 3 over the passing rows only.  A join like TPC-H Q3 keeps a few percent of its
     rows, so decoding and accumulating all NI x 64 rows of a wavefront (branch-free) is mostly
     wasted VALU work: instead each lane appends its passing (row, j) pairs to a per-wavefront
-    LDS list (wavefront prefix sum of the per-lane counts), and the wavefront walks the list 64
+    LDS list (positions from per-item ballots), and the wavefront walks the list 64
     entries at a time — aggregate loads, decode and accumulation run once per passing row."""
-    b = [f"{ind}int pc = " + " + ".join(f"(int)pass{it}" for it in range(NI)) + ";",
-         f"{ind}int incl = pc;",
-         "#pragma unroll",
-         f"{ind}for (int o = 1; o < 64; o <<= 1) {{ const int y = __shfl_up(incl, o, 64); "
-         "if (cln >= o) incl += y; }",
-         f"{ind}const int wtot = __shfl(incl, 63, 64);",
-         f"{ind}int pos = incl - pc;"]
+    # list position of a passing item: item-major order (all lanes' item 0, then item 1, ...),
+    # from one ballot + mbcnt per item instead of a 6-step cross-lane prefix sum
+    b = [f"{ind}int wtot = 0;"]
     for it in range(NI):
-        cj = f"cj_s[wv][pos] = (int)j{it}; " if with_j else ""
-        b.append(f"{ind}if (pass{it}) {{ crow_s[wv][pos] = (int)(row{it} - tb0); {cj}++pos; }}")
-    b += [f"{ind}__syncthreads();",
+        cj = f"cj_s[wv][pos{it}] = (int)j{it}; " if with_j else ""
+        b += [f"{ind}{{ const u64 bm = __ballot(pass{it});",
+              f"{ind}  const int pos{it} = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), "
+              f"__builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));",
+              f"{ind}  if (pass{it}) {{ crow_s[wv][pos{it}] = (crow_t)(row{it} - tb0); {cj}}}",
+              f"{ind}  wtot += __popcll(bm); }}"]
+    b += [f"{ind}{_wave_sync()}",
           f"{ind}for (int cb = 0; cb < wtot; cb += 64) {{",
           f"{ind}  const int ce = cb + cln;",
           f"{ind}  bool cok = ce < wtot;",
@@ -1199,12 +1389,13 @@ def _compacted_tail(args, cols, split, approx, aggs, grouped, group_col, third, 
                  f"glc >= 0 && glc < {ng};")
         b.append(f"{ind2}const int {gvar} = cok ? (int)glc : 0;")
     b += [_rename(x, allslots, "c") for x in _accumulate(g, aggs, grouped, "cok", gvar, ind2)]
-    b += [f"{ind}}}", f"{ind}__syncthreads();"]
+    b += [f"{ind}}}", f"{ind}{_wave_sync()}"]
     return b
 
 
 def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int = 4,
-                       jlog: int = 0) -> Kernel:
+                       jlog: int = 0, stage: Optional[bool] = None,
+                       bitmap: bool = False) -> Kernel:
     """Fused join + aggregate as a streaming scan of the left table's row ranges that reads
     ``jidx[row]`` — the matching right row from the cached join index (exec/join_index.py) — and
     gathers right-side columns there.
@@ -1253,101 +1444,298 @@ def gen_join_index_agg(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int = 
     if grouped:
         base = args.add("q", "group_base", "long long")
         ng = args.add("q", "num_groups", "long long")
-    b += ["  const i64 ntiles = a.tile_prefix[a.R];",
-          "  const i64 per = (ntiles + gridDim.x - 1) / gridDim.x;",
-          "  const i64 t0 = (i64)blockIdx.x * per;",
-          "  const i64 t1 = ntiles < t0 + per ? ntiles : t0 + per;",
-          "  int r = 0;",
-          "  if (t0 < t1) { int lo = 0, hi = (int)a.R;",
-          "    while (hi - lo > 1) { const int m = (lo + hi) >> 1; if (a.tile_prefix[m] <= t0) lo = m; else hi = m; }",
-          "    r = lo; }",
-          "  for (i64 t = t0; t < t1; ++t) {",
-          "    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;",
-          f"    const i64 off = (t - a.tile_prefix[r]) * {T};"]
     ind = "    "
-    if vec:
-        _vec_rows(b, NI, ind)
-        g1 = _Gen(args, cols, split, ("row0", "row0"), approx, True)
-        _vec_load_slots(b, g1, first, NI, ind, extra=[("jr", jct, "a.jidx")])
-        if jw < 4:   # NI | block size and g0 % NI == 0: the thread's rows share one block
-            b.append(f"{ind}const int jb = a.jbase[g0 >> {jlog}];")
+    g1 = _Gen(args, cols, split, ("row0", "row0"), approx, True)
+    compact = JI_COMPACT and bool(third)
+    # the bitmap replaces phase 2 only when the aggregate tail re-loads what it needs
+    bitmap = bool(bitmap and second and compact and _right_only(p, split))
+    stage = bool(vec and second and not bitmap and (JI_STAGE if stage is None else stage))
+
+    def phase2_global(b: List[str]) -> None:
         for it in range(NI):
-            if jw < 4:
-                b.append(f"{ind}const int jr{it} = act{it} && jrv[{it}] != {sent} ? "
-                         f"jb + (int)jrv[{it}] : -1;")
-            else:
-                b.append(f"{ind}const int jr{it} = act{it} ? jrv[{it}] : -1;")
-    else:
-        b += ["    const i64 tb0 = a.rstart[r] + off;",
-              f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};"]
+            g2 = _Gen(args, cols, split, (f"row{it}", f"j{it}"), approx, True)
+            for s in second:
+                _uload(g2, s, it, b, ind)
+
+    def body(b: List[str], full: Optional[bool]) -> None:
+        """Tile body; ``full`` = vectorized full tile / vectorized last tile / None (scalar)."""
+        if full is not None:     # raw vector arrays and jb come from the tile loop
+            _vec_load_slots(b, g1, first, NI, ind)
+            for it in range(NI):
+                if jw < 4:
+                    b.append(f"{ind}const int jr{it} = act{it} && jrv[{it}] != {sent} ? "
+                             f"jb + (int)jrv[{it}] : -1;")
+                else:
+                    b.append(f"{ind}const int jr{it} = act{it} ? jrv[{it}] : -1;")
+        else:
+            b.extend(["    const i64 tb0 = a.rstart[r] + off;",
+                      f"    const i64 rows = a.rlen[r] - off < {T} ? a.rlen[r] - off : {T};"])
+            for it in range(NI):
+                b.extend([f"{ind}const bool act{it} = {it * BLOCK} + (i64)threadIdx.x < rows;",
+                          f"{ind}const i64 row{it} = tb0 + (act{it} ? {it * BLOCK} + (i64)threadIdx.x : 0);"])
+            # phase 1: join index + left predicate columns of every item
+            for it in range(NI):
+                if jw < 4:
+                    b.append(f"{ind}const {jct} jc{it} = a.jidx[row{it}];")
+                    b.append(f"{ind}const int jr{it} = jc{it} != {sent} ? "
+                             f"a.jbase[row{it} >> {jlog}] + (int)jc{it} : -1;")
+                else:
+                    b.append(f"{ind}const int jr{it} = a.jidx[row{it}];")
+                g1i = _Gen(args, cols, split, (f"row{it}", f"row{it}"), approx, True)
+                for s in first:
+                    _uload(g1i, s, it, b, ind)
         for it in range(NI):
-            b += [f"{ind}const bool act{it} = {it * BLOCK} + (i64)threadIdx.x < rows;",
-                  f"{ind}const i64 row{it} = tb0 + (act{it} ? {it * BLOCK} + (i64)threadIdx.x : 0);"]
-        # phase 1: join index + left predicate columns of every item
+            g1i = _Gen(args, cols, split, (f"row{it}", f"row{it}"), approx, True)
+            cond = _rename(g1i.cnf(lpreds), allslots, it)
+            b.append(f"{ind}bool pass{it} = act{it} && jr{it} >= 0 && {cond};")
+            b.append(f"{ind}const i64 j{it} = pass{it} ? (i64)jr{it} : 0;")
+        # phase 2: right predicate columns at the matched rows
+        if bitmap:
+            _bitmap_phase2(b, args, NI, ind)
+            b.extend(_compacted_tail(args, cols, split, approx, aggs, grouped, p.group_col,
+                                     third, allslots, NI, ind))
+            return
+        if stage:
+            _ji_stage_phase2(b, g1, args, cols, split, approx, second, NI, stage, ind,
+                             phase2_global)
+        else:
+            phase2_global(b)
         for it in range(NI):
-            if jw < 4:
-                b.append(f"{ind}const {jct} jc{it} = a.jidx[row{it}];")
-                b.append(f"{ind}const int jr{it} = jc{it} != {sent} ? "
-                         f"a.jbase[row{it} >> {jlog}] + (int)jc{it} : -1;")
-            else:
-                b.append(f"{ind}const int jr{it} = a.jidx[row{it}];")
-            g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"), approx, True)
-            for s in first:
-                _uload(g1, s, it, b, ind)
-    for it in range(NI):
-        g1 = _Gen(args, cols, split, (f"row{it}", f"row{it}"), approx, True)
-        cond = _rename(g1.cnf(lpreds), allslots, it)
-        b.append(f"{ind}bool pass{it} = act{it} && jr{it} >= 0 && {cond};")
-        b.append(f"{ind}const i64 j{it} = pass{it} ? (i64)jr{it} : 0;")
-    # phase 2: right predicate columns at the matched rows
-    for it in range(NI):
-        g2 = _Gen(args, cols, split, (f"row{it}", f"j{it}"), approx, True)
-        for s in second:
-            _uload(g2, s, it, b, ind)
-    for it in range(NI):
-        g2 = _Gen(args, cols, split, (f"row{it}", f"j{it}"), approx, True)
-        b.append(f"{ind}pass{it} = pass{it} && {_rename(g2.cnf(rpreds), allslots, it)};")
-    if JI_COMPACT and third:
-        b += _compacted_tail(args, cols, split, approx, aggs, grouped, p.group_col, third,
-                             allslots, NI, ind)
-        b += ["  }"]
-        b += _flush(aggs, grouped)
-        W = BLOCK // 64
-        b.insert(0, f"  __shared__ int crow_s[{W}][{64 * NI}]; __shared__ int cj_s[{W}][{64 * NI}];")
-        b.insert(1, "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;")
-        src = (_PRELUDE + args.struct_src() +
-               f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_join_index_agg(Args a) {{\n' +
-               "\n".join(b) + "\n}\n")
-        lds = (len(aggs) * p.num_groups * 32) if grouped else 0
-        return Kernel(src, "hs_jit_join_index_agg", args, lds)
-    # phase 3: aggregate inputs (rows that failed read the tile's first row / right row 0)
-    if third:
-        for it in range(NI):
-            b += [f"{ind}const i64 lq{it} = pass{it} ? row{it} : tb0;",
-                  f"{ind}const i64 jq{it} = pass{it} ? j{it} : 0;"]
+            g2 = _Gen(args, cols, split, (f"row{it}", f"j{it}"), approx, True)
+            b.append(f"{ind}pass{it} = pass{it} && {_rename(g2.cnf(rpreds), allslots, it)};")
+        if compact:
+            b.extend(_compacted_tail(args, cols, split, approx, aggs, grouped, p.group_col,
+                                     third, allslots, NI, ind))
+            return
+        # phase 3: aggregate inputs (rows that failed read the tile's first row / right row 0)
+        if third:
+            for it in range(NI):
+                b.extend([f"{ind}const i64 lq{it} = pass{it} ? row{it} : tb0;",
+                          f"{ind}const i64 jq{it} = pass{it} ? j{it} : 0;"])
+            for it in range(NI):
+                g3 = _Gen(args, cols, split, (f"lq{it}", f"jq{it}"), approx, True)
+                for s in third:
+                    _uload(g3, s, it, b, ind)
         for it in range(NI):
             g3 = _Gen(args, cols, split, (f"lq{it}", f"jq{it}"), approx, True)
-            for s in third:
-                _uload(g3, s, it, b, ind)
-    for it in range(NI):
-        g3 = _Gen(args, cols, split, (f"lq{it}", f"jq{it}"), approx, True)
-        gvar = f"gi{it}"
-        if grouped:
-            g = p.group_col
-            gx = _rename(f"x{g}", allslots, it)
-            ok = _rename(g3.ok(g), allslots, it)
-            b.append(f"{ind}const i64 gl{it} = (i64){gx} - {base};")
-            b.append(f"{ind}pass{it} = pass{it} && {ok} && gl{it} >= 0 && gl{it} < {ng};")
-            b.append(f"{ind}const int {gvar} = pass{it} ? (int)gl{it} : 0;")
-        b += [_rename(x, allslots, it) for x in
-              _accumulate(g3, aggs, grouped, f"pass{it}", gvar, ind)]
+            gvar = f"gi{it}"
+            if grouped:
+                g = p.group_col
+                gx = _rename(f"x{g}", allslots, it)
+                ok = _rename(g3.ok(g), allslots, it)
+                b.append(f"{ind}const i64 gl{it} = (i64){gx} - {base};")
+                b.append(f"{ind}pass{it} = pass{it} && {ok} && gl{it} >= 0 && gl{it} < {ng};")
+                b.append(f"{ind}const int {gvar} = pass{it} ? (int)gl{it} : 0;")
+            b.extend(_rename(x, allslots, it) for x in
+                     _accumulate(g3, aggs, grouped, f"pass{it}", gvar, ind))
+
+    if vec:
+        # NI | block size and g0 % NI == 0: the thread's rows share one join-index block
+        sc = [("jb", "int", f"a.jbase[G0 >> {jlog}]")] if jw < 4 else []
+        _vec_tiles(b, T, NI, ind, _vec_loads(g1, first, extra=[("jr", jct, "a.jidx")]), sc, body)
+    else:
+        _tile_loop(b, T, NI, 0)
+        body(b, None)
     b += ["  }"]
     b += _flush(aggs, grouped)
+    W = BLOCK // 64
+    pre = []
+    if compact:
+        pre.append(f"  typedef {_crow_t(T)} crow_t; __shared__ crow_t crow_s[{W}][{64 * NI}]; "
+                   f"__shared__ int cj_s[{W}][{64 * NI}];")
+    if stage:
+        for s in second:
+            pre.append(f"  __shared__ __attribute__((aligned(16))) {g1.raw_type(s)} st{s}_s[{W}][512];")
+            if cols[s][1]:
+                pre.append(f"  __shared__ unsigned char sn{s}_s[{W}][512];")
+    if compact or stage:
+        pre.append("  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;")
+    b = pre + b
     src = (_PRELUDE + args.struct_src() +
            f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_join_index_agg(Args a) {{\n' +
            "\n".join(b) + "\n}\n")
     lds = (len(aggs) * p.num_groups * 32) if grouped else 0
     return Kernel(src, "hs_jit_join_index_agg", args, lds)
+
+
+def _bitmap_phase2(b: List[str], args: Args, NI: int, ind: str) -> None:
+    """Phase 2 of the join-index kernel as bit tests on the right side's predicate bitmap
+    (``gen_pred_bitmap``).  A thread's NI rows are consecutive and the join index is monotone
+    within a bucket, so the matched right rows of its passing items fall in at most two bitmap
+    words (loaded once each, unconditionally: word 0 stands in when nothing passes); an item
+    whose word is neither (a gap of over 64 right rows) loads its own."""
+    bm = args.add("p", "rbm", "const unsigned long long*")
+    lo = " ".join(f"if (pass{it} && (int)j{it} < mlo) mlo = (int)j{it};" for it in range(NI))
+    hi = " ".join(f"if (pass{it} && (int)j{it} > mhi) mhi = (int)j{it};" for it in range(NI))
+    b += [f"{ind}int mlo = 0x7fffffff, mhi = -1; {lo} {hi}",
+          f"{ind}const int wlo = mhi >= 0 ? (mlo >> 6) : 0, whi = mhi >= 0 ? (mhi >> 6) : 0;",
+          f"{ind}const u64 bw0 = {bm}[wlo], bw1 = {bm}[whi];"]
+    for it in range(NI):
+        b += [f"{ind}if (pass{it}) {{ const int wi = (int)j{it} >> 6;",
+              f"{ind}  const u64 w = wi == wlo ? bw0 : (wi == whi ? bw1 : {bm}[wi]);",
+              f"{ind}  pass{it} = ((w >> ((int)j{it} & 63)) & 1ull) != 0ull; }}"]
+
+
+def _right_only(p: NL.JoinParams, split: int = 8) -> bool:
+    """Every right-side predicate reads right columns only (no left/right column compares)."""
+    for k in range(p.nlp, p.npreds):
+        pr = p.preds[k]
+        if pr.kind == NL.PK_TRUE:
+            continue
+        if pr.col < split or (pr.kind in (NL.PK_INT_COL, NL.PK_FLT_COL) and pr.col2 < split):
+            return False
+    return True
+
+
+def pred_bitmap_shape(p: NL.JoinParams, compacts=None) -> tuple:
+    cols = tuple((s, c) for s, c in sorted(_col_specs(p, compacts).items()) if s >= 8)
+    preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
+                   p.preds[k].group) for k in range(p.nlp, p.npreds))
+    return ("pred_bitmap", cols, preds, p.nlp)
+
+
+BITMAP_ITEMS = 4
+
+
+def gen_pred_bitmap(p: NL.JoinParams, compacts=None) -> Kernel:
+    """Semi-join bitmap of the right side of a join: bit r of ``rbm`` = the right-side
+    predicates (``preds[nlp:]``) hold on right row r.  Each wavefront writes whole 64-bit words
+    (one ballot per word, BITMAP_ITEMS words in flight per wavefront); an SF100 orders table is
+    150M rows -> 18.75 MB of bitmap, resident in the Infinity Cache for the join kernel."""
+    args = Args()
+    args.add("p", "rbm", "unsigned long long*")
+    args.add("q", "rnrows", "long long")
+    cols = {s: c for s, c in _col_specs(p, compacts).items() if s >= 8}
+    rpreds = [(k, p.preds[k]) for k in range(p.nlp, p.npreds)]
+    slots = _pred_slots(rpreds)
+    NI = BITMAP_ITEMS
+    b = ["  const int lane = threadIdx.x & 63;",
+         "  const i64 nw = (a.rnrows + 63) >> 6;",
+         f"  const i64 wstep = (i64)gridDim.x * {BLOCK // 64 * NI};",
+         f"  for (i64 w0 = ((i64)blockIdx.x * {BLOCK // 64} + (threadIdx.x >> 6)) * {NI}; w0 < nw; "
+         "w0 += wstep) {"]
+    ind = "    "
+    for it in range(NI):
+        b += [f"{ind}const i64 row{it} = ((w0 + {it}) << 6) + lane;",
+              f"{ind}const bool act{it} = row{it} < a.rnrows;",
+              f"{ind}const i64 jr{it} = act{it} ? row{it} : 0;"]
+    for it in range(NI):
+        g = _Gen(args, cols, 8, (f"jr{it}", f"jr{it}"), frozenset(), True)
+        for sl in slots:
+            _uload(g, sl, it, b, ind)
+    for it in range(NI):
+        g = _Gen(args, cols, 8, (f"jr{it}", f"jr{it}"), frozenset(), True)
+        b += [f"{ind}{{ const u64 m = __ballot(act{it} && {_rename(g.cnf(rpreds), slots, it)});",
+              f"{ind}  if (lane == 0 && w0 + {it} < nw) a.rbm[w0 + {it}] = m; }}"]
+    b.append("  }")
+    src = (_PRELUDE + args.struct_src() +
+           f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_pred_bitmap(Args a) {{\n' +
+           "\n".join(b) + "\n}\n")
+    return Kernel(src, "hs_jit_pred_bitmap", args)
+
+
+def pred_bitmap(p: NL.JoinParams, compacts, rnrows: int, device):
+    """Launch the right side's predicate bitmap (``gen_pred_bitmap``) on the current stream."""
+    import torch
+    nw = (int(rnrows) + 63) // 64
+    bm = torch.empty(max(nw, 1), dtype=torch.int64, device=device)
+    k = kernel_for(pred_bitmap_shape(p, compacts), lambda: gen_pred_bitmap(p, compacts))
+    v = {"rbm": bm.data_ptr(), "rnrows": int(rnrows)}
+    _fill_common(v, p.cols, [(i, p.preds[i]) for i in range(p.npreds)], [], compacts)
+    per_block = BLOCK // 64 * BITMAP_ITEMS
+    grid = max(1, min((nw + per_block - 1) // per_block, 8192))
+    k.launch(grid, v, NL.stream_ptr())
+    return bm
+
+
+def _ji_stage_phase2(b: List[str], g1: "_Gen", args, cols, split, approx, second, NI: int,
+                     stage: int, ind: str, fallback) -> None:
+    """Phase 2 of the join-index kernel through LDS: the matched right rows of a wavefront's
+    passing items are one short, monotone run (both sides sorted by key within a bucket, the
+    wavefront's rows consecutive), so the wavefront copies the 8-byte aligned window of every
+    right predicate column that holds the run [jlo, jhi] into its own LDS slice — one coalesced
+    ``dwordx2`` per lane, i.e. one vector-memory instruction for the whole wavefront — and each
+    item then reads LDS, instead of NI divergent gathers per lane, which made vector-memory
+    instruction issue the kernel's limit.  Runs wider than the 512-byte window, or rows outside
+    the run (a non-monotone index), take the global gathers."""
+    lo_terms = " ".join(f"if (pass{it} && (int)j{it} < mlo) mlo = (int)j{it};" for it in range(NI))
+    hi_terms = " ".join(f"if (pass{it} && (int)j{it} > mhi) mhi = (int)j{it};" for it in range(NI))
+    # the window starts at jlo rounded down to 8 bytes of the widest staged element: every staged
+    # array holds STAGE_W elements (512 bytes of the widest, fewer bytes of narrower ones)
+    esz = max(_SIZEOF[g1.raw_type(s)] for s in second)
+    span = 512 // esz
+    b += [f"{ind}int mlo = 0x7fffffff, mhi = -1; {lo_terms} {hi_terms}",
+          f"{ind}const u64 anyp = __ballot(mhi >= 0);",
+          f"{ind}int jlo = 0, jhi = -1;",
+          f"{ind}if (anyp) {{ jlo = __builtin_amdgcn_readlane(mlo, __ffsll((long long)anyp) - 1);",
+          f"{ind}  jhi = __builtin_amdgcn_readlane(mhi, 63 - __clzll((long long)anyp)); }}",
+          f"{ind}const int jw0 = jlo & ~{8 // esz - 1 if esz < 8 else 0};",
+          f"{ind}const bool inrun = " + " && ".join(
+              f"(!pass{it} || ((int)j{it} >= jlo && (int)j{it} <= jhi))" for it in range(NI)) + ";",
+          f"{ind}const bool staged = anyp != 0ull && jhi - jw0 < {span} && __ballot(!inrun) == 0ull;"]
+    # phase-2 registers (S-prefixed here, renamed to x/n/q after the branch), filled from LDS
+    # or by the global gathers
+    outs = []
+    for it in range(NI):
+        for s in second:
+            outs.append((f"x{s}_{it}", _CTYPE[cols[s][0]]))
+            if cols[s][1]:
+                outs.append((f"n{s}_{it}", "bool"))
+            enc = cols[s][2]
+            if enc:
+                outs.append((f"r{s}_{it}", "int"))
+            if enc and enc[1]:
+                outs.append((f"q{s}_{it}", "i64"))
+    b.append(f"{ind}" + " ".join(f"{ct} S{n};" for n, ct in outs))
+    b.append(f"{ind}if (staged) {{")
+    i2 = ind + "  "
+    # lane l copies elements [jw0 + l*8/esz, +8/esz) of each column: 8 bytes of the widest,
+    # fewer of narrower ones; lanes whose piece starts past jhi stay idle (no read past the run's
+    # last 8-byte word, which lies inside the column's allocation)
+    for s in second:
+        es = _SIZEOF[g1.raw_type(s)]
+        per = 8 // esz * 1    # elements of the widest type per lane
+        b.append(f"{i2}if (jw0 + cln * {per} <= jhi) {{")
+        b.append(f"{i2}  " + " ".join(f"st{s}_s[wv][cln * {per} + {k}] = {g1.ptr(s)}[jw0 + cln * {per} + {k}];"
+                                      for k in range(per)) if es * per != 8 else
+                 f"{i2}  *reinterpret_cast<uint2*>(&st{s}_s[wv][cln * {per}]) = "
+                 f"*reinterpret_cast<const uint2*>({g1.ptr(s)} + jw0 + cln * {per});")
+        if cols[s][1]:
+            b.append(f"{i2}  " + " ".join(f"sn{s}_s[wv][cln * {per} + {k}] = {g1.vptr(s)}[jw0 + cln * {per} + {k}];"
+                                          for k in range(per)))
+        b.append(f"{i2}}}")
+    b.append(f"{i2}{_wave_sync(True)}")
+    for it in range(NI):
+        b.append(f"{i2}const int sj{it} = pass{it} ? (int)j{it} - jw0 : 0;")
+        for s in second:
+            enc = cols[s][2]
+            raw = f"st{s}_s[wv][sj{it}]"
+            if enc:
+                b.append(f"{i2}Sr{s}_{it} = (int){raw};")
+            if enc and enc[1]:
+                base = args.add("q", f"B{s}", "long long")
+                b.append(f"{i2}Sq{s}_{it} = {base} + (i64){raw};")
+            b.append(f"{i2}Sx{s}_{it} = {g1.decode(s, raw)};")
+            if cols[s][1]:
+                b.append(f"{i2}Sn{s}_{it} = sn{s}_s[wv][sj{it}] != 0;")
+    b.append(f"{i2}{_wave_sync(True)}")
+    b.append(f"{ind}}} else {{")
+    gl: List[str] = []
+    fallback(gl)
+    b += [f"{i2}{line.strip()}" for line in gl]
+    b.append(f"{i2}" + " ".join(f"S{n} = {n};" for n, _ in outs))
+    b.append(f"{ind}}}")
+    b.append(f"{ind}" + " ".join(f"const {ct} {n} = S{n};" for n, ct in outs))
+
+
+def _stage_aligned(p: NL.JoinParams, compacts) -> bool:
+    """LDS staging copies 8-byte words of the right predicate columns (and validity bytes)."""
+    ptrs = []
+    for s in _pred_slots([(k, p.preds[k]) for k in range(p.nlp, p.npreds)]):
+        c = (compacts or {}).get(s)
+        ptrs.append(c.codes.data_ptr() if c else p.cols[s].data)
+        ptrs.append(p.cols[s].valid)
+    return all(int(x) % 8 == 0 for x in ptrs if x)
 
 
 def _vec_aligned(p: NL.JoinParams, compacts, jidx) -> bool:
@@ -1360,7 +1748,8 @@ def _vec_aligned(p: NL.JoinParams, compacts, jidx) -> bool:
     return _vec_aligned_ptrs(ptrs)
 
 
-def join_index_agg(p: NL.JoinParams, rstart, rlen, jx, compacts=None, nrows: int = 0):
+def join_index_agg(p: NL.JoinParams, rstart, rlen, jx, compacts=None, nrows: int = 0,
+                   rnrows: int = 0):
     """Same outputs as ``join_agg``.  ``jx``: the join index from ``join_index.get_join_index``
     (``codes`` int32 rows, or uint8/uint16 block-coded with ``base`` / ``log_blk``);
     ``nrows`` = left table rows (vectorized loads stay inside the columns)."""
@@ -1377,14 +1766,19 @@ def join_index_agg(p: NL.JoinParams, rstart, rlen, jx, compacts=None, nrows: int
         tp = K.ranges_to_tiles(rlen, BLOCK * JI_ITEMS)
     grid = SCAN_GRID or NL.lib().hs_scan_grid()
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
-    k = kernel_for(join_index_agg_shape(p, compacts, vec, jw, jlog),
-                   lambda: gen_join_index_agg(p, compacts, vec, jw, jlog))
+    stage = bool(JI_STAGE and vec) and _stage_aligned(p, compacts)
+    bitmap = bool(JI_BITMAP and JI_COMPACT and rnrows > 0 and p.npreds > p.nlp and
+                  _right_only(p))
+    k = kernel_for(join_index_agg_shape(p, compacts, vec, jw, jlog, stage, bitmap),
+                   lambda: gen_join_index_agg(p, compacts, vec, jw, jlog, stage, bitmap))
+    bm = pred_bitmap(p, compacts, rnrows, rstart.device) if "rbm" in k.args._index else None
     parts = _partials(grid, GA, rstart.device)
     v = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
          "jidx": jx.codes.data_ptr(), "jbase": jx.base.data_ptr() if jw < 4 else 0,
          "R": rstart.numel(), "nrows": nrows, "psum": parts[0].data_ptr(),
          "pcnt": parts[1].data_ptr(), "pmin": parts[2].data_ptr(), "pmax": parts[3].data_ptr(),
-         "num_groups": p.num_groups, "group_base": p.group_base}
+         "num_groups": p.num_groups, "group_base": p.group_base,
+         "rbm": bm.data_ptr() if bm is not None else 0}
     _fill_common(v, p.cols, [(k_, p.preds[k_]) for k_ in range(p.npreds)],
                  [p.aggs[i] for i in range(p.naggs)], compacts)
     k.launch(grid, v, NL.stream_ptr(), GA * 32 if p.group_col >= 0 else 0)

@@ -65,10 +65,11 @@ def test_generated_sources_compile(rt, tmp_path):
         [_agg(NL.AK_MIN, [(1, 0.0, 1.0)]), _agg(NL.AK_MAX, [(1, 0.0, 2.0)]),
          _agg(NL.AK_COUNT, [(0, 0.0, 1.0)])], group_col=2, num_groups=2))
     for p in cases:
-        k = jit.gen_scan_agg(p)
-        rc = jit.runtime().hs_jit_compile_to_cache(k.src.encode(), k.name.encode(), b"gfx950",
-                                                   str(tmp_path).encode())
-        assert rc == 0, jit.runtime().hs_jit_last_error().decode()
+        for vec in (0, 8, 16):
+            k = jit.gen_scan_agg(p, vec=vec)
+            rc = jit.runtime().hs_jit_compile_to_cache(k.src.encode(), k.name.encode(),
+                                                       b"gfx950", str(tmp_path).encode())
+            assert rc == 0, jit.runtime().hs_jit_last_error().decode()
     j = NL.JoinParams()
     j.cols[0], j.cols[1], j.cols[2] = _fake(NL.I64), _fake(NL.I32), _fake(NL.F64, True)
     j.cols[8], j.cols[9], j.cols[10] = _fake(NL.I64), _fake(NL.I32), _fake(NL.I32, True)
@@ -85,6 +86,7 @@ def test_generated_sources_compile(rt, tmp_path):
         if not fl:
             ks += [jit.gen_join_index_agg(j), jit.gen_join_index_agg(j, vec=4),
                    jit.gen_join_index_agg(j, vec=8, jw=1, jlog=7),
+                   jit.gen_join_index_agg(j, vec=16, jw=1, jlog=7),
                    jit.gen_join_index_agg(j, jw=2, jlog=8)]
         for k in ks:
             rc = jit.runtime().hs_jit_compile_to_cache(k.src.encode(), k.name.encode(),
@@ -143,9 +145,10 @@ def test_generated_sources_compile_with_compact_columns(rt, tmp_path):
     comp = {0: Compact(None, 1, 0, 100.0, NL.F64), 1: Compact(None, 4, 0, 100.0, NL.F64),
             2: Compact(None, 2, 5, None, NL.I64)}
     k = jit.gen_scan_agg(p, comp)
-    # slot 0: its literal predicate runs on the integer codes (T0/U0), its SUM term decodes with
-    # a reciprocal (R0); no exact division left for it
-    assert "a.T0" in k.src and "a.R0" in k.src and "a.Q0" not in k.src
+    # slot 0: its literal predicate runs on the stored codes (CL0/CH0), its SUM term decodes
+    # with a reciprocal (R0); no exact division left for it
+    assert "a.CL0" in k.src and "a.R0" in k.src and "a.Q0" not in k.src
+    assert "a.CL1" in k.src and "a.L1" not in k.src    # integer compact column: code bounds
     assert "const signed char* c0" in k.src
     rc = jit.runtime().hs_jit_compile_to_cache(k.src.encode(), k.name.encode(), b"gfx950",
                                                str(tmp_path).encode())
@@ -164,6 +167,46 @@ def test_generated_sources_compile_with_compact_columns(rt, tmp_path):
     rc = jit.runtime().hs_jit_compile_to_cache(k.src.encode(), k.name.encode(), b"gfx950",
                                                str(tmp_path).encode())
     assert rc == 0, jit.runtime().hs_jit_last_error().decode()
+    ks = [q3_join_index_kernel(jit, stage=True), q3_join_index_kernel(jit, bitmap=True),
+          q3_join_index_kernel(jit, vec=0, bitmap=True), q3_bitmap_kernel(jit)]
+    assert "st9_s" in ks[0].src          # phase 2 staged through LDS
+    assert "a.rbm" in ks[1].src and "a.c9" not in ks[1].src   # phase 2 = bitmap tests
+    for k in ks:
+        rc = jit.runtime().hs_jit_compile_to_cache(k.src.encode(), k.name.encode(), b"gfx950",
+                                                   str(tmp_path).encode())
+        assert rc == 0, jit.runtime().hs_jit_last_error().decode()
+
+
+def q3_join_index_kernel(jit, vec=8, stage=False, bitmap=False):
+    """The TPC-H Q3 shape of the bench: left (lineitem) l_shipdate > d, right (orders)
+    o_orderdate < d, SUM(price * (1 - disc)) + COUNT(*), compact HBM columns, 1-byte join index."""
+    j = _q3_params()
+    return jit.gen_join_index_agg(j, _q3_compacts(), vec=vec, jw=1, jlog=7, stage=stage,
+                                  bitmap=bitmap)
+
+
+def _q3_params():
+    j = NL.JoinParams()
+    j.cols[0], j.cols[1] = _fake(NL.I64), _fake(NL.I32)
+    j.cols[2], j.cols[3] = _fake(NL.F64), _fake(NL.F64)
+    j.cols[8], j.cols[9] = _fake(NL.I64), _fake(NL.I32)
+    j.preds[0] = NL.Pred(NL.PK_INT_LIT, NL.OP_GT, 1, 0, 0, 0, 9000, 0.0, None)
+    j.preds[1] = NL.Pred(NL.PK_INT_LIT, NL.OP_LT, 9, 0, 1, 0, 9000, 0.0, None)
+    j.nlp, j.npreds = 1, 2
+    j.aggs[0] = _agg(NL.AK_SUM, [(2, 0.0, 1.0), (3, 1.0, -1.0)])
+    j.aggs[1] = _agg(NL.AK_COUNT_STAR)
+    j.naggs, j.lkey, j.rkey, j.group_col = 2, 0, 8, -1
+    return j
+
+
+def _q3_compacts():
+    from hyperspace_amd.exec.encoding import Compact
+    return {1: Compact(None, 2, 8000, None, NL.I32), 3: Compact(None, 1, 0, 100.0, NL.F64),
+            9: Compact(None, 2, 8000, None, NL.I32)}
+
+
+def q3_bitmap_kernel(jit):
+    return jit.gen_pred_bitmap(_q3_params(), _q3_compacts())
 
 
 def test_shape_key_ignores_literals():
@@ -292,6 +335,24 @@ def test_jit_join_agg_matches_aot(device):
         cg = [t.cpu().numpy() for t in jit.join_agg(p, rstart, rlen, rbk, roff_t, mt, comp)]
         np.testing.assert_allclose(cg[0], got[0], rtol=1e-12)
         assert np.array_equal(cg[1], got[1])
+
+
+def test_code_bounds_match_value_compares():
+    """Predicates on compact columns compare stored codes with host-computed int32 bounds; they
+    must agree with the compare on the decoded value for every code, op and literal."""
+    from hyperspace_amd.exec import jit
+    rng = np.random.default_rng(3)
+    codes = np.arange(-128, 128, dtype=np.int64)
+    ops = {NL.OP_EQ: np.equal, NL.OP_NE: np.not_equal, NL.OP_LT: np.less, NL.OP_LE: np.less_equal,
+           NL.OP_GT: np.greater, NL.OP_GE: np.greater_equal}
+    for base in (0, 1000, -5, 2**40):
+        for lit in list(base + rng.integers(-300, 300, 20)) + [2**62, -2**62]:
+            for op, fn in ops.items():
+                lo, hi = jit.code_bounds(*jit._int_lit_bounds(op, lit), base)
+                assert -2**31 <= lo and hi <= 2**31 - 1
+                inside = (codes >= lo) & (codes <= hi)
+                got = ~inside if op == NL.OP_NE else inside
+                assert (got == fn(base + codes, lit)).all(), (base, lit, op)
 
 
 def test_int_bounds_match_decoded_double_compares():
