@@ -1,6 +1,9 @@
-// K1: Parquet page decode on the MI355X.
+// K1: Parquet page decode on the MI355X.  Two paths:
+//   * device pages (hs_pq_decode_pages, below): raw compressed pages in, values out — Snappy,
+//     RLE/bit-packed parsing and dictionary expansion all on the GPU;
+//   * host run tables (hs_pq_decode_values / _levels): for chunks with nulls.
 //
-// The host page layer (csrc/runtime/hs_parquet.cpp) decompresses pages and cuts every
+// Host run tables: the host page layer (csrc/runtime/hs_parquet.cpp) decompresses pages and cuts every
 // RLE/bit-packed hybrid stream into a run table; the page bytes still hold dictionary indices
 // at their encoded bit width.  Here one wave expands one run:
 //   kind 0  RLE run         -> value (or dict[value]) repeated `count` times
@@ -102,7 +105,382 @@ __global__ __launch_bounds__(256) void hs_pq_levels_kernel(
     o[i] = (uint8_t)(unpack(buf, run.src, i, run.bit_width) != 0);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Device-resident page decode (no host decompression or run tables): the host preads the raw
+// column chunks and lists their pages (csrc/runtime/hs_parquet.cpp hs_pq_plan_chunk); here
+//   hs_pq_inflate_kernel  one wavefront per page: Snappy (or a copy) into the scratch buffer;
+//   hs_pq_expand_kernel   one workgroup per data page: RLE / bit-packed dictionary indices or
+//                         PLAIN values straight into the destination column.
+// Two launches per source file instead of one per run batch of every chunk.
+// dst: device address of the decompressed page (the caller turns the planner's scratch offsets
+// into addresses; host-inflated pages, codec 2, point at their own device copy)
+struct HsPqPage {
+  int64_t src, dst, out, dict, row;
+  int32_t csize, usize, nvals, codec, kind, enc, levels, eb, dict_page, pad;
+};
+
+enum : int { kErrCorrupt = 1, kErrDictRange = 2 };
+
+// Snappy raw-block decompression by one wavefront (input at byte offset `ib` of the 4-byte
+// aligned buffer `base`, `n` bytes; output `out`, `cap` bytes).
+//
+// Tag parsing is data-parallel.  Each batch looks at a 512-byte window of the input: every
+// lane speculatively decodes a tag at each of its 8 window offsets (length, source and the
+// offset of the following tag), then pointer-jumping tables over "next tag" (6 rounds) give
+// every lane j the position of the j-th tag after the window start, so up to 64 real tags
+// are found in O(log) LDS steps instead of one dependent step per tag.  Then
+//   1. literal bytes are copied byte-parallel over the batch (a batch that is one long literal,
+//      as on incompressible pages, with aligned dword stores: two aligned loads and a funnel
+//      shift per lane, four dwords in flight per lane);
+//   2. copy bytes are resolved byte-parallel from output that is already final: a byte whose
+//      source lies in an earlier batch or in a literal of this batch is read directly; a source
+//      inside another copy of this batch follows that copy back (a run of copies with one
+//      offset — RLE-like data — is one overlapping copy, left by a modulo), so every step moves
+//      to an earlier tag.
+// A fence between the passes and between batches makes the wavefront's stores visible to its
+// later loads.
+__device__ void snappy_wave(const uint8_t* __restrict__ base, int64_t ib, int n,
+                            uint8_t* __restrict__ out, int cap, int w, int lane,
+                            int* __restrict__ status) {
+  constexpr int WIN = 512, PER = WIN / 64, LOGT = 6;
+  __shared__ int s_next[4][LOGT][WIN];   // pointer-jumping tables: 2^k-th following tag
+  __shared__ int s_len[4][WIN];          // speculative tag at each window offset: output bytes
+  __shared__ int s_srcw[4][WIN];         //   and source (literal: input offset, copy: -offset)
+  __shared__ uint8_t s_win[4][WIN + 8];
+  __shared__ int s_start[4][65];
+  __shared__ int s_src[4][64];
+  __shared__ int s_root[4][64];          // output start of the tag's same-offset copy run
+  const uint8_t* in = base + ib;
+  int ip = 0;
+  uint32_t len = 0;
+  for (int shift = 0; ip < n && shift <= 28; shift += 7) {
+    const uint8_t b = in[ip++];
+    len |= (uint32_t)(b & 0x7f) << shift;
+    if (!(b & 0x80)) break;
+  }
+  if ((int)len != cap) { if (lane == 0) atomicOr(status, kErrCorrupt); return; }
+  auto wsync = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  int op = 0;
+  while (ip < n) {
+#pragma unroll
+    for (int k = 0; k < PER + 1; ++k) {
+      const int x = lane * PER + k;
+      if (x < WIN + 8) s_win[w][x] = ip + x < n ? in[ip + x] : 0;
+    }
+    wsync();
+    // speculative decode at every window offset
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = lane * PER + k;
+      const uint8_t* h = s_win[w] + i;
+      const int tag = h[0], kind = tag & 3;
+      int hl, l, src, ok = 1;
+      if (kind == 0) {
+        l = tag >> 2;
+        hl = 1;
+        if (l >= 60) {
+          const int nb = l - 59;
+          l = 0;
+          for (int b = 0; b < nb; ++b) l |= (int)h[1 + b] << (8 * b);
+          hl += nb;
+        }
+        l += 1;
+        src = ip + i + hl;
+        if (l <= 0) ok = 0;
+      } else if (kind == 1) {
+        l = 4 + ((tag >> 2) & 7); src = -(((tag >> 5) << 8) | h[1]); hl = 2;
+      } else if (kind == 2) {
+        l = 1 + (tag >> 2); src = -(h[1] | (h[2] << 8)); hl = 3;
+      } else {
+        l = 1 + (tag >> 2);
+        src = -(h[1] | (h[2] << 8) | (h[3] << 16) | ((int)h[4] << 24));
+        hl = 5;
+      }
+      // a header must lie inside the window (and the input): otherwise the offset absorbs
+      ok = ok && i + hl <= WIN && ip + i + hl <= n;
+      s_len[w][i] = l;
+      s_srcw[w][i] = src;
+      s_next[w][0][i] = ok ? i + hl + (kind == 0 ? l : 0) : i;
+    }
+    wsync();
+    for (int t = 1; t < LOGT; ++t) {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int i = lane * PER + k;
+        const int a = s_next[w][t - 1][i];
+        s_next[w][t][i] = a < WIN ? s_next[w][t - 1][a] : a;
+      }
+      wsync();
+    }
+    // lane j: position of the j-th tag of the batch
+    int pos = 0;
+#pragma unroll
+    for (int t = 0; t < LOGT; ++t)
+      if ((lane >> t) & 1) pos = pos < WIN ? s_next[w][t][pos] : pos;
+    const bool real = pos < WIN && s_next[w][0][pos] != pos && ip + pos < n;
+    const uint64_t rm = __ballot(real);
+    const int cnt = rm == ~0ull ? 64 : __ffsll((long long)~rm) - 1;   // leading decodable tags
+    if (cnt == 0) { if (lane == 0) atomicOr(status, kErrCorrupt); return; }
+    const bool mine = lane < cnt;
+    int l = mine ? s_len[w][pos] : 0;
+    const int src = mine ? s_srcw[w][pos] : 0;
+    // exclusive scan of the tag lengths -> output starts
+    int incl = l;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    const int st = incl - l;
+    const int total = __shfl(incl, cnt - 1, 64);
+    const int nextpos = __shfl(mine ? s_next[w][0][pos] : 0, cnt - 1, 64);
+    // a copy may not reach before the output start; literals must end inside the input
+    const bool bad = mine && (src < 0 ? (-src > op + st) : (src + l > n));
+    if (__ballot(bad) != 0ull || op + total > cap) {
+      if (lane == 0) atomicOr(status, kErrCorrupt);
+      return;
+    }
+    const int prev = __shfl_up(src, 1, 64);
+    const bool head = !(src < 0 && lane > 0 && prev == src);
+    const uint64_t heads = __ballot(mine && head);
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const int hl = 63 - __clzll((long long)(heads & upto));
+    const int root = __shfl(st, hl < 0 ? 0 : hl, 64);
+    if (mine) {
+      s_start[w][lane] = st;
+      s_src[w][lane] = src;
+      s_root[w][lane] = root;
+    }
+    if (lane == 0) s_start[w][cnt] = total;
+    wsync();
+    ip += nextpos;
+    // 1. literal bytes
+    if (cnt == 1 && s_src[w][0] >= 0) {
+      const int d0 = op, ll = total;
+      const int64_t sabs = ib + s_src[w][0];
+      const int mis = (int)((uintptr_t)out & 3);     // aligned in absolute address
+      const int wa = ((d0 + mis) & ~3) - mis;
+      const int nw = (d0 + ll - wa + 3) >> 2;
+#pragma unroll 4
+      for (int j = lane; j < nw; j += 64) {
+        const int x = wa + 4 * j;
+        if (x >= d0 && x + 4 <= d0 + ll) {
+          *(uint32_t*)(out + x) = load_u32_at(base, sabs + (x - d0));
+        } else {
+          for (int y = x; y < x + 4; ++y)
+            if (y >= d0 && y < d0 + ll) out[y] = base[sabs + (y - d0)];
+        }
+      }
+    } else {
+#pragma unroll 2
+      for (int b = lane; b < total; b += 64) {
+        int lo = 0, hi = cnt - 1;
+        while (lo < hi) {
+          const int m = (lo + hi + 1) >> 1;
+          if (s_start[w][m] <= b) lo = m; else hi = m - 1;
+        }
+        const int sr = s_src[w][lo];
+        if (sr >= 0) out[op + b] = base[ib + sr + (b - s_start[w][lo])];
+      }
+    }
+    __threadfence();
+    __builtin_amdgcn_wave_barrier();
+    // 2. copy bytes
+#pragma unroll 2
+    for (int b = lane; b < total; b += 64) {
+      int cur = 0, hi = cnt - 1;
+      while (cur < hi) {
+        const int m = (cur + hi + 1) >> 1;
+        if (s_start[w][m] <= b) cur = m; else hi = m - 1;
+      }
+      if (s_src[w][cur] >= 0) continue;
+      int p2 = b, q;
+      for (;;) {
+        const int off = -s_src[w][cur];
+        const int cst = s_root[w][cur];
+        q = p2 - off;
+        if (q >= cst) q = cst - off + (p2 - cst) % off;
+        if (q < 0) break;
+        int lo = 0, h2 = cur - 1;
+        while (lo < h2) {
+          const int m = (lo + h2 + 1) >> 1;
+          if (s_start[w][m] <= q) lo = m; else h2 = m - 1;
+        }
+        if (s_src[w][lo] >= 0) break;
+        p2 = q;
+        cur = lo;
+      }
+      out[op + b] = out[op + q];
+    }
+    __threadfence();
+    __builtin_amdgcn_wave_barrier();
+    op += total;
+  }
+  if (op != cap && lane == 0) atomicOr(status, kErrCorrupt);
+}
+
+__global__ __launch_bounds__(256) void hs_pq_inflate_kernel(
+    const uint8_t* __restrict__ raw, uint8_t* __restrict__ scratch,
+    const HsPqPage* __restrict__ pages, int npages, int* __restrict__ status) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int pi = blockIdx.x * 4 + w;
+  if (pi >= npages) return;               // wavefront-local from here on: no block barriers
+  const HsPqPage p = pages[pi];
+  if (p.codec == 2) return;               // inflated on the host (dst = its device copy)
+  const uint8_t* in = raw + p.src;
+  uint8_t* out = (uint8_t*)p.dst;
+  const int lv = p.kind == 1 ? p.levels : 0;   // v2: level streams stored uncompressed first
+  if (lv > p.csize || lv > p.usize) { if (lane == 0) atomicOr(status, kErrCorrupt); return; }
+  for (int i = lane; i < lv; i += 64) out[i] = in[i];
+  if (p.codec == 0) {
+    for (int i = lv + lane; i < p.csize; i += 64) out[i] = in[i];
+    return;
+  }
+  snappy_wave(raw, p.src + lv, p.csize - lv, out + lv, p.usize - lv, w, lane, status);
+}
+
+template <typename T>
+__device__ void expand_page(const HsPqPage& p, const uint8_t* __restrict__ pg,
+                            const HsPqPage* __restrict__ pages, int* __restrict__ status) {
+  __shared__ int r_start[129];
+  __shared__ int64_t r_src[128];
+  __shared__ int r_kind[128];
+  __shared__ int r_meta[3];           // runs, next stream position, error
+  T* out = (T*)p.out;
+  const int n = p.usize;
+  int voff = 0;
+  if (p.kind == 0 && p.levels) voff = 4 + (int)load_u32_at(pg, 0);
+  else if (p.kind == 1) voff = p.levels;
+  if (voff < 0 || voff > n) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
+  if (p.enc == 0) {                   // PLAIN
+    if ((int64_t)p.nvals * (int64_t)sizeof(T) > n - voff) {
+      if (threadIdx.x == 0) atomicOr(status, kErrCorrupt);
+      return;
+    }
+    for (int i = threadIdx.x; i < p.nvals; i += blockDim.x)
+      out[i] = load_elem<T>(pg, voff + (int64_t)i * (int64_t)sizeof(T));
+    return;
+  }
+  // dictionary indices: bit width byte, then the RLE / bit-packed hybrid stream
+  if (n - voff < 1 || p.dict_page < 0) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
+  const int bw = pg[voff];
+  if (bw > 32) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
+  const int64_t s0 = voff + 1, send = n;
+  const T* dict = (const T*)p.dict;
+  const int64_t dcount = pages[p.dict_page].nvals;
+  const int vbytes = (bw + 7) / 8;
+  int64_t pos = s0;
+  int done = 0;
+  while (done < p.nvals) {
+    if (threadIdx.x == 0) {
+      int k = 0, acc = 0, err = 0;
+      int64_t q = pos;
+      while (k < 128 && done + acc < p.nvals) {
+        uint64_t h = 0;
+        int shift = 0;
+        for (;;) {
+          if (q >= send || shift > 35) { err = 1; break; }
+          const uint8_t b = pg[q++];
+          h |= (uint64_t)(b & 0x7f) << shift;
+          if (!(b & 0x80)) break;
+          shift += 7;
+        }
+        if (err) break;
+        const int left = p.nvals - done - acc;
+        if (h & 1) {
+          const int64_t groups = (int64_t)(h >> 1);
+          const int64_t nbytes = groups * bw;
+          if (q + nbytes > send) { err = 1; break; }
+          const int64_t take = groups * 8 < left ? groups * 8 : left;
+          r_kind[k] = 1;
+          r_src[k] = q;
+          r_start[k] = acc;
+          acc += (int)take;
+          q += nbytes;
+        } else {
+          const int64_t cnt = (int64_t)(h >> 1);
+          if (q + vbytes > send) { err = 1; break; }
+          uint64_t v = 0;
+          for (int i = 0; i < vbytes; ++i) v |= (uint64_t)pg[q + i] << (8 * i);
+          q += vbytes;
+          if (cnt == 0) continue;
+          r_kind[k] = 0;
+          r_src[k] = (int64_t)v;
+          r_start[k] = acc;
+          acc += (int)(cnt < left ? cnt : left);
+        }
+        ++k;
+      }
+      r_start[k] = acc;
+      r_meta[0] = k;
+      r_meta[2] = err || (k == 0 && done < p.nvals);
+      pos = q;
+    }
+    __syncthreads();
+    const int k = r_meta[0];
+    const int err = r_meta[2];
+    const int total = r_start[k];
+    if (err) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
+    for (int i = threadIdx.x; i < total; i += blockDim.x) {
+      int lo = 0, hi = k - 1;
+      while (lo < hi) {
+        const int m = (lo + hi + 1) >> 1;
+        if (r_start[m] <= i) lo = m; else hi = m - 1;
+      }
+      uint32_t idx;
+      if (r_kind[lo] == 0) {
+        idx = (uint32_t)r_src[lo];
+      } else {
+        const int64_t bit = (int64_t)(i - r_start[lo]) * bw;
+        const uint64_t win = load_u64_at(pg, r_src[lo] + (bit >> 3));
+        const uint64_t mask = bw == 32 ? 0xffffffffull : ((1ull << bw) - 1);
+        idx = (uint32_t)((win >> (bit & 7)) & mask);
+      }
+      T v = (T)0;
+      if ((int64_t)idx < dcount) v = dict[idx];
+      else atomicOr(status, kErrDictRange);
+      out[done + i] = v;
+    }
+    __syncthreads();
+    done += total;
+  }
+}
+
+__global__ __launch_bounds__(256) void hs_pq_expand_kernel(
+    const uint8_t* __restrict__ scratch, const HsPqPage* __restrict__ pages, int npages,
+    int* __restrict__ status) {
+  const int pi = blockIdx.x;
+  if (pi >= npages) return;
+  const HsPqPage p = pages[pi];
+  if (p.kind == 2 || p.nvals == 0) return;     // dictionary pages are read by the data pages
+  const uint8_t* pg = (const uint8_t*)p.dst;
+  if (p.eb == 4) expand_page<uint32_t>(p, pg, pages, status);
+  else if (p.eb == 8) expand_page<uint64_t>(p, pg, pages, status);
+  else if (threadIdx.x == 0) atomicOr(status, kErrCorrupt);
+}
+
 extern "C" {
+
+// Decode the pages of one file planned by hs_pq_plan_chunk: inflate (one wavefront per page)
+// then expand (one workgroup per page) on `stream`.  `raw`, `scratch`, `pages` and `status`
+// are device pointers; errors accumulate as bits in *status.
+int hs_pq_decode_pages(const uint8_t* raw, uint8_t* scratch, const HsPqPage* pages, int npages,
+                       int* status, void* stream) {
+  if (npages <= 0) return 0;
+  (void)hipGetLastError();
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(hs_pq_inflate_kernel, dim3((unsigned)((npages + 3) / 4)), dim3(256), 0, s,
+                     raw, scratch, pages, npages, status);
+  hipLaunchKernelGGL(hs_pq_expand_kernel, dim3((unsigned)npages), dim3(256), 0, s, scratch,
+                     pages, npages, status);
+  return (int)hipGetLastError();
+}
+
+int hs_pq_page_struct_size() { return (int)sizeof(HsPqPage); }
 
 // Expand value runs into `out` (elem_bytes 4 or 8).  dict_off < 0: the chunk has no dictionary
 // (then every run must be PLAIN).  Returns a HIP error code.
@@ -136,6 +514,9 @@ int hs_pq_warmup(void* stream) {
                      (int64_t)0, (int64_t)0, (int64_t)0, (uint64_t*)nullptr);
   hipLaunchKernelGGL(hs_pq_levels_kernel, dim3(1), dim3(256), 0, s, nullptr, nullptr, (int64_t)0,
                      (uint8_t*)nullptr);
+  hipLaunchKernelGGL(hs_pq_inflate_kernel, dim3(1), dim3(256), 0, s, nullptr, nullptr, nullptr, 0,
+                     nullptr);
+  hipLaunchKernelGGL(hs_pq_expand_kernel, dim3(1), dim3(256), 0, s, nullptr, nullptr, 0, nullptr);
   return (int)hipStreamSynchronize(s);
 }
 

@@ -29,6 +29,7 @@ enum : int {
   HS_PQ_CORRUPT = -2,
   HS_PQ_UNSUPPORTED = -3,
   HS_PQ_CAPACITY = -4,
+  HS_PQ_NULLS = -5,        // the chunk may hold nulls: not decodable by the device-only path
 };
 
 // ------------------------------------------------------------------ Thrift compact protocol
@@ -119,6 +120,7 @@ struct ChunkMeta {
   int type = -1, codec = 0;
   int64_t num_values = 0, total_compressed = 0, total_uncompressed = 0;
   int64_t data_page_offset = 0, dict_page_offset = -1;
+  int64_t null_count = -1;   // from the chunk statistics; -1: not recorded
   std::vector<std::string> path;
 };
 
@@ -194,6 +196,14 @@ void parse_col_meta(TReader& r, ChunkMeta& m) {
       case 7: m.total_compressed = r.zigzag(); break;
       case 9: m.data_page_offset = r.zigzag(); break;
       case 11: m.dict_page_offset = r.zigzag(); break;
+      case 12: {  // Statistics: null_count is field 3
+        int16_t sid = 0;
+        for (int st; (st = r.field(sid)) != 0 && !r.bad;) {
+          if (sid == 3 && st == 6) m.null_count = r.zigzag();
+          else r.skip(st);
+        }
+        break;
+      }
       default: r.skip(t);
     }
   }
@@ -336,6 +346,8 @@ bool snappy_decompress(const uint8_t* in, size_t n, uint8_t* out, size_t cap, si
 namespace {
 
 constexpr int64_t kChunk = 4096;  // split long runs so each GPU work item stays short
+// device plans inflate Snappy dictionary pages larger than this on the host (plan_chunk)
+constexpr int kHostDictMin = 64 << 10;
 
 // Parse an RLE/bit-packed hybrid stream of `count` values into runs (dst starts at `dst0`).
 // `base` is the stream's byte offset in the chunk buffer.  Returns the number of non-zero
@@ -569,9 +581,177 @@ int read_chunk(File* f, int rg, int col, uint8_t* buf, int64_t cap, HsPqChunkInf
 
 }  // namespace
 
+// ------------------------------------------------------------------ device-decode page plan
+// One entry per page of a column chunk whose decompression, RLE/bit-packed parsing and value
+// expansion all run on the GPU (csrc/kernels/parquet_decode.hip: hs_pq_inflate /
+// hs_pq_expand).  The host only preads the raw (compressed) chunk and walks the page headers.
+// Layout shared with the kernels; `out` and `dict` are absolute device addresses the caller
+// fills in once the device buffers exist.
+struct HsPqPage {
+  int64_t src;      // payload offset in the raw (compressed) buffer
+  int64_t dst;      // offset of the decompressed page in the scratch buffer (16-byte aligned)
+  int64_t out;      // device address of the page's first output value (data pages)
+  int64_t dict;     // device address of the chunk's decompressed dictionary (0: none)
+  int64_t row;      // first row of the page within its chunk
+  int32_t csize;    // payload bytes as stored
+  int32_t usize;    // bytes after decompression (levels included)
+  int32_t nvals;    // rows of the page (data pages) / dictionary entries (dictionary page)
+  int32_t codec;    // 0 uncompressed, 1 snappy
+  int32_t kind;     // 0 data v1, 1 data v2, 2 dictionary
+  int32_t enc;      // 0 PLAIN, 2 / 8 dictionary indices
+  int32_t levels;   // v1: 1 if a length-prefixed definition-level stream precedes the values;
+                    // v2: byte length of the (never compressed) level streams
+  int32_t eb;       // element bytes (4 / 8)
+  int32_t dict_page;  // index (within the plan) of the chunk's dictionary page, -1: none
+  int32_t pad;
+};
+
+namespace {
+
+// Plan one chunk: pread its raw bytes to `raw + at` and describe every page.  `dst_at` is the
+// scratch offset where this chunk's first decompressed page goes; returns the scratch bytes
+// used via *dst_used.  Chunks with repetition, unsupported codecs or encodings are reported as
+// HS_PQ_UNSUPPORTED (the caller decodes them another way).
+int plan_chunk(File* f, int rg, int col, uint8_t* raw, int64_t raw_cap, int64_t raw_at,
+               int64_t dst_at, HsPqPage* pages, int max_pages, int* npages, int64_t* raw_used,
+               int64_t* dst_used, uint8_t* hbuf, int64_t hcap, int64_t h_at, int64_t* h_used) {
+  *npages = 0;
+  const ChunkMeta& m = f->rgs[(size_t)rg].cols[(size_t)col];
+  const SchemaEl& s = f->schema[(size_t)f->leaves[(size_t)col]];
+  if (s.repetition == 2) return HS_PQ_UNSUPPORTED;
+  const int eb = elem_bytes(m.type);
+  if (!eb) return HS_PQ_UNSUPPORTED;
+  if (m.codec != 0 && m.codec != 1) return HS_PQ_UNSUPPORTED;
+  const bool optional = s.repetition == 1;
+  // the device path writes values at their row index: every row must hold a value
+  if (optional && m.null_count != 0) return HS_PQ_NULLS;
+  const int64_t start = m.dict_page_offset > 0 && m.dict_page_offset < m.data_page_offset
+                            ? m.dict_page_offset : m.data_page_offset;
+  const int64_t len = m.total_compressed;
+  if (start < 4 || len < 0 || start + len > f->size) return HS_PQ_CORRUPT;
+  if (raw_at + len > raw_cap) return HS_PQ_CAPACITY;
+  uint8_t* base = raw + raw_at;
+  if (!pread_all(f->fd, base, (size_t)len, start)) return HS_PQ_IO;
+  TReader r{base, base + len};
+  int64_t rows = 0, dst = dst_at, hat = h_at;
+  int dict_idx = -1;
+  while (rows < m.num_values) {
+    PageHdr ph;
+    if (!parse_page_header(r, ph)) return HS_PQ_CORRUPT;
+    if (ph.csize < 0 || ph.usize < 0 || r.end - r.p < ph.csize) return HS_PQ_CORRUPT;
+    const int64_t payload = raw_at + (r.p - base);
+    r.p += ph.csize;
+    if (ph.type != 0 && ph.type != 2 && ph.type != 3) continue;   // index pages etc.
+    if (*npages >= max_pages) return HS_PQ_CAPACITY;
+    HsPqPage& p = pages[*npages];
+    memset(&p, 0, sizeof(p));
+    p.src = payload;
+    p.dst = (dst + 15) & ~(int64_t)15;
+    p.csize = ph.csize;
+    p.codec = m.codec;
+    p.eb = eb;
+    p.dict_page = -1;
+    if (ph.type == 2) {
+      if (ph.enc != 0 && ph.enc != 2) return HS_PQ_UNSUPPORTED;
+      p.kind = 2;
+      p.usize = ph.usize;
+      p.nvals = ph.dict_nvals;
+      if ((int64_t)ph.dict_nvals * eb > ph.usize) return HS_PQ_CORRUPT;
+      dict_idx = *npages;
+    } else {
+      const bool dict = ph.enc == 2 || ph.enc == 8;
+      if (!dict && ph.enc != 0) return HS_PQ_UNSUPPORTED;
+      if (dict && dict_idx < 0) return HS_PQ_CORRUPT;
+      p.enc = ph.enc;
+      p.nvals = ph.nvals;
+      p.row = rows;
+      p.dict_page = dict ? dict_idx : -1;
+      if (ph.v2) {
+        if (ph.v2_rep_len) return HS_PQ_UNSUPPORTED;
+        if (ph.v2_def_len > ph.csize) return HS_PQ_CORRUPT;
+        p.kind = 1;
+        p.levels = ph.v2_def_len;
+        if (!ph.v2_compressed) p.codec = 0;
+        p.usize = ph.usize;
+      } else {
+        if (optional && ph.def_enc != 3) return HS_PQ_UNSUPPORTED;
+        p.kind = 0;
+        p.levels = optional ? 1 : 0;
+        p.usize = ph.usize;
+      }
+      rows += ph.nvals;
+    }
+    if (p.codec == 0 && p.csize != p.usize) return HS_PQ_CORRUPT;
+    // Snappy pages that actually compressed are chains of short tags (a tag every few bytes),
+    // which a wavefront resolves at ~14 us per 64 tags; literal-dominated pages (bit-packed
+    // dictionary indices, random values) inflate on the device at copy speed.  Inflate the
+    // former here, like large dictionary pages (a dense chain of short copies): codec 2 =
+    // host-inflated, `src` = offset in the handle's host_pages buffer (levels included).
+    const bool dense = p.codec == 1 &&
+        ((int64_t)p.usize * 10 >= (int64_t)p.csize * 11 || (p.kind == 2 && p.usize > kHostDictMin));
+    if (dense && hbuf) {
+      const int lv = p.kind == 1 ? p.levels : 0;
+      const uint8_t* src = base + (payload - raw_at);
+      const int64_t at = (hat + 15) & ~(int64_t)15;
+      if (at + p.usize + 16 > hcap) return HS_PQ_CAPACITY;
+      memcpy(hbuf + at, src, (size_t)lv);
+      size_t got = 0;
+      if (!snappy_decompress(src + lv, (size_t)(p.csize - lv), hbuf + at + lv,
+                             (size_t)(p.usize - lv), &got) ||
+          got != (size_t)(p.usize - lv))
+        return HS_PQ_CORRUPT;
+      p.codec = 2;
+      p.src = at;
+      hat = at + p.usize + 16;
+      ++*npages;
+      continue;                      // occupies no device scratch
+    }
+    dst = p.dst + p.usize + 16;   // + slack: the kernels read 8-byte windows
+    ++*npages;
+  }
+  if (rows != m.num_values) return HS_PQ_CORRUPT;
+  *raw_used = len;
+  *dst_used = dst - dst_at;
+  *h_used = hat - h_at;
+  return HS_PQ_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 const char* hs_pq_error(void* h) { return h ? ((File*)h)->error.c_str() : "null handle"; }
+
+// Raw (compressed) bytes of a chunk as stored: the pread size of hs_pq_plan_chunk.
+int64_t hs_pq_chunk_raw_bytes(void* h, int rg, int col) {
+  return ((File*)h)->rgs[(size_t)rg].cols[(size_t)col].total_compressed;
+}
+
+// Upper bound of the pages of a chunk (uncompressed bytes / 1 KiB + 64): sizes the page table.
+int64_t hs_pq_chunk_max_pages(void* h, int rg, int col) {
+  const ChunkMeta& m = ((File*)h)->rgs[(size_t)rg].cols[(size_t)col];
+  return m.total_uncompressed / 1024 + m.num_values / 1024 + 64;
+}
+
+// `hbuf` (capacity `hcap`, next free offset `h_at`): where pages the host inflates go (codec 2,
+// `src` = offset in hbuf); null keeps every page for the device.  Sized by the caller from
+// hs_pq_chunk_host_bound.
+int hs_pq_plan_chunk(void* h, int rg, int col, uint8_t* raw, int64_t raw_cap, int64_t raw_at,
+                     int64_t dst_at, HsPqPage* pages, int max_pages, int* npages,
+                     int64_t* raw_used, int64_t* dst_used, uint8_t* hbuf, int64_t hcap,
+                     int64_t h_at, int64_t* h_used) {
+  return plan_chunk((File*)h, rg, col, raw, raw_cap, raw_at, dst_at, pages, max_pages, npages,
+                    raw_used, dst_used, hbuf, hcap, h_at, h_used);
+}
+
+// Bytes that bound what hs_pq_plan_chunk may inflate into the host buffer for this chunk.
+int64_t hs_pq_chunk_host_bound(void* h, int rg, int col) {
+  const ChunkMeta& m = ((File*)h)->rgs[(size_t)rg].cols[(size_t)col];
+  return m.total_uncompressed + 32 * hs_pq_chunk_max_pages(h, rg, col) + 64;
+}
+
+int hs_pq_page_size() { return (int)sizeof(HsPqPage); }
+
 
 // Opens a file and parses its footer.  Always returns a handle (check hs_pq_ok / hs_pq_error;
 // release with hs_pq_close).

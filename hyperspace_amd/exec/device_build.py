@@ -111,6 +111,9 @@ def device_build_from_source(session, rel, files: List[str], columns: List[str],
     fmt = source_format(rel)
     from . import staging
     staging.HOST_DECODED.clear()
+    staging.DEVICE_DECODED.clear()
+    from ..io import native_parquet
+    native_parquet.PHASES.clear()
     xs = _BatchedExchange(dist, num_buckets, indexed) if world > 1 else None
     if fmt == "parquet":
         cols, names, schema = _upload_parquet(rel, my_files, columns, indexed, lineage_ids,
@@ -134,7 +137,10 @@ def device_build_from_source(session, rel, files: List[str], columns: List[str],
         dist.barrier()
     LAST_BUILD_STATS.update({"read_h2d_s": t1 - t0, "hash_exchange_s": t2 - t1,
                              "total_s": time.perf_counter() - t0, "source_bytes": source_bytes,
-                             "host_decoded": sorted(staging.HOST_DECODED)})
+                             "host_decoded": sorted(staging.HOST_DECODED),
+                             "device_decoded": sorted(staging.DEVICE_DECODED),
+                             "decode_phases_s": {k: round(v, 4) for k, v in
+                                                 native_parquet.PHASES.items()}})
     if xs is not None:
         LAST_BUILD_STATS.update({"exchange_batches": xs.nbatches,
                                  "exchange_sent_bytes": xs.sent_bytes})

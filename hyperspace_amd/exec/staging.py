@@ -194,6 +194,8 @@ def fixed_width_numpy(arr) -> Tuple[np.ndarray, Optional[np.ndarray]]:
 _WARM = False
 # columns the last uploads had to decode on the host (pyarrow) instead of the native page layer
 HOST_DECODED: set = set()
+# columns the last uploads decoded entirely on the device (raw pages -> HIP inflate + expand)
+DEVICE_DECODED: set = set()
 
 
 def _warm_decode_kernels() -> None:
@@ -208,6 +210,13 @@ def _warm_decode_kernels() -> None:
 def native_decode_enabled() -> bool:
     """Native Parquet page decode (HIP) for staging; ``HS_NATIVE_PARQUET=0`` forces pyarrow."""
     return os.environ.get("HS_NATIVE_PARQUET", "1") == "1"
+
+
+def device_decode_enabled() -> bool:
+    """Device-only page decode (Snappy + hybrid RLE on the GPU, io/native_parquet
+    ``upload_file_device``); ``HS_DEVICE_PARQUET=0`` keeps decompression and run parsing on the
+    host page layer."""
+    return os.environ.get("HS_DEVICE_PARQUET", "1") == "1"
 
 
 def _h2d_async(dst, src: np.ndarray, stream) -> None:
@@ -280,8 +289,10 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
         st.wait_stream(main)  # allocations above happen-before the copies
 
     native = parquet_local is not None and native_decode_enabled()
+    status = None
     if native:
         _warm_decode_kernels()
+        status = torch.zeros(1, dtype=torch.int32, device=device)
 
     def work(i: int):
         torch.cuda.set_device(device)
@@ -290,9 +301,15 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
         done = set()
         if native:
             from ..io import native_parquet
-            done = native_parquet.upload_file(parquet_local[i], [f for f in schema
-                                                                 if f.name in cols],
-                                              cols, lo, n, stream, device, lock)
+            flds = [f for f in schema if f.name in cols]
+            if device_decode_enabled():
+                done = native_parquet.upload_file_device(parquet_local[i], flds, cols, lo,
+                                                         stream, device, status)
+                DEVICE_DECODED.update(done)
+            rest_native = [f for f in flds if f.name not in done]
+            if rest_native:
+                done = done | native_parquet.upload_file(parquet_local[i], rest_native, cols, lo,
+                                                         n, stream, device, lock)
         rest = [f for f in schema if f.name not in done]
         for f in rest:
             HOST_DECODED.add(f.name)
@@ -337,6 +354,11 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
         fu.result()
     for st in streams:
         main.wait_stream(st)
+    if status is not None:
+        code = int(status.item())
+        if code:
+            raise IOError(f"device Parquet decode failed (status {code}: 1 corrupt page, "
+                          f"2 dictionary index out of range) in {len(files)} files")
     return UploadResult(cols, n, strings)
 
 

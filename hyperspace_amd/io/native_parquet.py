@@ -1,8 +1,18 @@
 """Native Parquet decode into HBM: host page layer in C++
 (``csrc/runtime/hs_parquet.cpp``: footer/page-header Thrift parsing, Snappy, run tables) and
-HIP expansion kernels (``csrc/kernels/parquet_decode.hip``).
+HIP kernels (``csrc/kernels/parquet_decode.hip``).
 
-Per file: every natively decodable column chunk is decompressed straight into one pinned
+Device path (``upload_file_device``, default for chunks whose statistics say null-free): the
+host only preads the raw column chunks into one pinned block and walks the page headers; the
+compressed bytes cross PCIe and two launches per file decode them — ``hs_pq_inflate_kernel``
+(Snappy, one wavefront per page, data-parallel tag parsing) and ``hs_pq_expand_kernel`` (RLE /
+bit-packed hybrid parsing, dictionary gather or PLAIN copy, one workgroup per page).  Pages that
+Snappy actually compressed are chains of short tags that a wavefront resolves slowly; the
+planner inflates those (and large dictionary pages) on the host into the same pinned block, and
+the device still parses and expands them (measured: profiles/build_decode_r2.jsonl).
+
+Host-page-layer path (``upload_file``, chunks that may hold nulls):
+per file every natively decodable column chunk is decompressed straight into one pinned
 buffer, its RLE/bit-packed streams are cut into run tables, buffer and run tables cross PCIe
 in two copies on the HIP copy stream, and the expansion kernels write the values into the
 destination columns at the file's row offset.  Dictionary-encoded data crosses PCIe at its
@@ -24,6 +34,11 @@ OK, IO, CORRUPT, UNSUPPORTED, CAPACITY = 0, -1, -2, -3, -4
 
 RUN_DTYPE = np.dtype([("dst", "<i8"), ("count", "<i8"), ("src", "<i8"), ("kind", "<i4"),
                       ("bit_width", "<i4")])
+# HsPqPage (hs_parquet.cpp / parquet_decode.hip): one page of a device-decoded chunk
+PAGE_DTYPE = np.dtype([("src", "<i8"), ("dst", "<i8"), ("out", "<i8"), ("dict", "<i8"),
+                       ("row", "<i8"), ("csize", "<i4"), ("usize", "<i4"), ("nvals", "<i4"),
+                       ("codec", "<i4"), ("kind", "<i4"), ("enc", "<i4"), ("levels", "<i4"),
+                       ("eb", "<i4"), ("dict_page", "<i4"), ("pad", "<i4")])
 
 
 class ChunkInfo(C.Structure):
@@ -70,12 +85,21 @@ def lib():
                         ("hs_pq_read_chunk", I, [P, I, I, P, I64, C.POINTER(ChunkInfo)]),
                         ("hs_pq_copy_runs", I, [P, P, P, I64, I64]),
                         ("hs_pq_run_size", I, []), ("hs_pq_info_size", I, []),
+                        ("hs_pq_chunk_raw_bytes", I64, [P, I, I]),
+                        ("hs_pq_chunk_max_pages", I64, [P, I, I]),
+                        ("hs_pq_plan_chunk", I, [P, I, I, P, I64, I64, I64, P, I,
+                                                 C.POINTER(C.c_int), C.POINTER(C.c_int64),
+                                                 C.POINTER(C.c_int64), P, I64, I64,
+                                                 C.POINTER(C.c_int64)]),
+                        ("hs_pq_chunk_host_bound", I64, [P, I, I]),
+                        ("hs_pq_page_size", I, []),
                         ("hs_pq_snappy_decompress", I64, [P, I64, P, I64])):
                     fn = getattr(L, name)
                     fn.restype = res
                     fn.argtypes = args
                 if L.hs_pq_run_size() != RUN_DTYPE.itemsize or \
-                        L.hs_pq_info_size() != C.sizeof(ChunkInfo):
+                        L.hs_pq_info_size() != C.sizeof(ChunkInfo) or \
+                        L.hs_pq_page_size() != PAGE_DTYPE.itemsize:
                     raise RuntimeError("hs_parquet ABI mismatch: rebuild the native runtime")
                 _L = L
     return _L
@@ -292,3 +316,221 @@ def upload_file(path: str, fields: Sequence[pa.Field], cols: Dict[str, object], 
         return done
     finally:
         f.close()
+
+
+NULLS = -5
+# per-phase seconds summed over the staging threads (device decode path), reset per build
+PHASES: Dict[str, float] = {}
+_PH_LOCK = threading.Lock()
+
+
+def _phase(name: str, t0: float) -> float:
+    import time
+    t1 = time.perf_counter()
+    with _PH_LOCK:
+        PHASES[name] = PHASES.get(name, 0.0) + (t1 - t0)
+    return t1
+
+
+def plan_file(f: "PqFile", plan, raw_cap: int, raw_buf_ptr: int, host_cap: int = 0,
+              host_buf_ptr: int = 0):
+    """Plan every (field, column) of ``plan`` over all row groups of ``f``: pread raw chunks into
+    the buffer at ``raw_buf_ptr``, inflate tag-dense pages into the one at ``host_buf_ptr`` (0:
+    none, every page inflates on the device) and collect the page table.
+
+    Returns (pages, chunks, raw_used, scratch_used, host_used, skipped): ``chunks`` = (field,
+    row group, first page, npages); ``skipped`` = fields the device path cannot decode (possible
+    nulls, unsupported encodings), to be decoded another way."""
+    L = f.L
+    nrg = f.num_row_groups
+    maxp = sum(int(L.hs_pq_chunk_max_pages(f.h, g, c)) for _, c, _ in plan for g in range(nrg))
+    pages = np.zeros(max(maxp, 1), dtype=PAGE_DTYPE)
+    pbase = pages.ctypes.data
+    chunks, skipped = [], set()
+    raw_at = dst_at = h_at = npg = 0
+    n = C.c_int()
+    ru, du, hu = C.c_int64(), C.c_int64(), C.c_int64()
+    for fld, c, eb in plan:
+        mine, ok = [], True
+        raw0, dst0, h0, npg0 = raw_at, dst_at, h_at, npg
+        for g in range(nrg):
+            rc = L.hs_pq_plan_chunk(f.h, g, c, raw_buf_ptr, raw_cap, raw_at, dst_at,
+                                    pbase + npg * PAGE_DTYPE.itemsize, len(pages) - npg,
+                                    C.byref(n), C.byref(ru), C.byref(du), host_buf_ptr or None,
+                                    host_cap, h_at, C.byref(hu))
+            if rc in (UNSUPPORTED, NULLS):
+                ok = False
+                break
+            if rc != OK:
+                raise IOError(f"{f.path}: device page plan failed ({rc}) on column {fld.name}, "
+                              f"row group {g}")
+            seg = pages[npg:npg + n.value]
+            seg["dict_page"] = np.where(seg["dict_page"] >= 0, seg["dict_page"] + npg, -1)
+            mine.append((fld, g, npg, n.value))
+            npg += n.value
+            raw_at += (ru.value + 15) // 16 * 16
+            dst_at += (du.value + 15) // 16 * 16
+            h_at += (hu.value + 15) // 16 * 16
+        if ok:
+            chunks += mine
+        else:                                   # roll this column back
+            skipped.add(fld.name)
+            raw_at, dst_at, h_at, npg = raw0, dst0, h0, npg0
+    return pages[:npg], chunks, raw_at, dst_at, h_at, skipped
+
+
+def upload_file_device(path: str, fields: Sequence[pa.Field], cols: Dict[str, object], lo: int,
+                       stream, device, status) -> Set[str]:
+    """Decode the natively supported, null-free ``fields`` of ``path`` entirely on the GPU into
+    ``cols[name].data[lo:...]``: the host preads the raw column chunks into pinned memory and
+    lists their pages; one H2D copy moves the compressed bytes and the page table, and two
+    launches (``hs_pq_decode_pages``: Snappy inflate, then RLE / bit-packed / PLAIN expansion
+    with the dictionary gather) write the values.  Errors accumulate in the device int
+    ``status`` (checked once per build).  Returns the names decoded."""
+    import time
+    import torch
+    from ..ops import _lib as NL
+    from ..exec.staging import pinned_pool
+    t = time.perf_counter()
+    f = PqFile(path)
+    try:
+        if not f.ok:
+            return set()
+        t = _phase("open", t)
+        L = f.L
+        plan = []
+        for fld in fields:
+            kind = _native_kind(fld.type)
+            if kind is None:
+                continue
+            c = f.column(fld.name)
+            if c < 0:
+                continue
+            ptype, _, eb = f.column_info(c)
+            if eb == 0 or ptype != kind[0]:
+                continue
+            plan.append((fld, c, eb))
+        if not plan:
+            return set()
+        nrg = f.num_row_groups
+        raw_cap = sum((int(L.hs_pq_chunk_raw_bytes(f.h, g, c)) + 15) // 16 * 16
+                      for _, c, _ in plan for g in range(nrg)) + 64
+        host_cap = sum(int(L.hs_pq_chunk_host_bound(f.h, g, c)) + 16
+                       for _, c, _ in plan for g in range(nrg))
+        pool = pinned_pool()
+        # one pinned block: [raw chunks | pages the planner inflates]
+        pinned = pool.acquire(raw_cap + host_cap)
+        t = _phase("pinned", t)
+        pages, chunks, raw_used, scratch_bytes, host_used, skipped = plan_file(
+            f, plan, raw_cap, pinned.data_ptr(), host_cap, pinned.data_ptr() + raw_cap)
+        t = _phase("plan", t)
+        if not chunks:
+            pool.release(pinned, stream)
+            return set()
+        rg_off = np.concatenate([[0], np.cumsum([f.row_group_rows(g) for g in range(nrg)])])
+        with torch.cuda.stream(stream):
+            scratch = torch.empty(scratch_bytes + 64, dtype=torch.uint8, device=device)
+            sbase = scratch.data_ptr()
+            # device copy of the pinned block's used parts: raw chunks at 0, host-inflated
+            # pages (tag-dense pages, large dictionaries) at raw_cap
+            draw = torch.empty(raw_cap + host_used + 64, dtype=torch.uint8, device=device)
+            draw[:raw_used].copy_(pinned[:raw_used], non_blocking=True)
+            if host_used:
+                draw[raw_cap:raw_cap + host_used].copy_(pinned[raw_cap:raw_cap + host_used],
+                                                        non_blocking=True)
+            for fld, g, p0, np_ in chunks:
+                seg = pages[p0:p0 + np_]
+                dc = cols[fld.name]
+                eb = dc.data.element_size()
+                row0 = lo + int(rg_off[g])
+                seg["out"] = dc.data.data_ptr() + (row0 + seg["row"]) * eb
+            # device address of every decompressed page (scratch, or the host-inflated copy)
+            hbase = draw.data_ptr() + raw_cap
+            pages["dst"] = np.where(pages["codec"] == 2, hbase + pages["src"],
+                                    sbase + pages["dst"])
+            dp = pages["dict_page"]
+            pages["dict"] = np.where(dp >= 0, pages["dst"][np.maximum(dp, 0)], 0)
+            ppin = pool.acquire(pages.nbytes)
+            ppin.numpy()[:pages.nbytes] = pages.view(np.uint8)
+            dpages = torch.empty(pages.nbytes, dtype=torch.uint8, device=device)
+            dpages.copy_(ppin[:pages.nbytes], non_blocking=True)
+            pool.release(pinned, stream)
+            pool.release(ppin, stream)
+            t = _phase("h2d_enqueue", t)
+            NL.check(NL.lib().hs_pq_decode_pages(draw.data_ptr(), sbase, dpages.data_ptr(),
+                                                 len(pages), status.data_ptr(),
+                                                 stream.cuda_stream), "hs_pq_decode_pages")
+            for x in (draw, dpages, scratch):
+                x.record_stream(stream)
+            _phase("launch", t)
+        return {fld.name for fld, _, _, _ in chunks}
+    finally:
+        f.close()
+
+
+def decode_plan_host(raw: np.ndarray, pages: np.ndarray, outputs: Dict[int, np.ndarray],
+                     host_dicts: Optional[np.ndarray] = None) -> None:
+    """Reference (host) consumer of a device page plan — the oracle for hs_pq_decode_pages.
+    ``outputs`` maps a page's ``out`` value to a numpy array slice receiving its values (the
+    plan is built with ``out`` = synthetic keys here instead of device addresses)."""
+    L = lib()
+    scratch = {}
+    for i, p in enumerate(pages):
+        if p["codec"] == 2:
+            scratch[i] = host_dicts[p["src"]:p["src"] + p["usize"]]
+            continue
+        src = raw[p["src"]:p["src"] + p["csize"]]
+        lv = int(p["levels"]) if p["kind"] == 1 else 0
+        if p["codec"] == 0:
+            data = bytes(src)
+        else:
+            body = np.ascontiguousarray(src[lv:])
+            out = np.zeros(int(p["usize"]) - lv + 64, dtype=np.uint8)
+            got = L.hs_pq_snappy_decompress(body.ctypes.data, len(body), out.ctypes.data,
+                                            len(out))
+            assert got == p["usize"] - lv, (got, p["usize"])
+            data = bytes(src[:lv]) + out[:got].tobytes()
+        scratch[i] = np.frombuffer(data, dtype=np.uint8)
+    for i, p in enumerate(pages):
+        if p["kind"] == 2:
+            continue
+        pg = scratch[i]
+        dt = np.dtype(np.uint32 if p["eb"] == 4 else np.uint64)
+        voff = 0
+        if p["kind"] == 0 and p["levels"]:
+            voff = 4 + int(pg[:4].view(np.uint32)[0])
+        elif p["kind"] == 1:
+            voff = int(p["levels"])
+        nv = int(p["nvals"])
+        dst = outputs[int(p["out"])]
+        if p["enc"] == 0:
+            dst[:nv] = pg[voff:voff + nv * dt.itemsize].view(dt)
+            continue
+        d = scratch[int(p["dict_page"])]
+        dvals = d[:int(pages[int(p["dict_page"])]["nvals"]) * dt.itemsize].view(dt)
+        bw = int(pg[voff])
+        s = pg[voff + 1:]
+        q, done = 0, 0
+        while done < nv:
+            h, shift = 0, 0
+            while True:
+                b = int(s[q]); q += 1
+                h |= (b & 0x7F) << shift
+                if not b & 0x80:
+                    break
+                shift += 7
+            if h & 1:
+                groups = h >> 1
+                take = min(groups * 8, nv - done)
+                idx = _unpack(s, q, take, bw) if bw else np.zeros(take, np.int64)
+                dst[done:done + take] = dvals[idx]
+                q += groups * bw
+                done += take
+            else:
+                cnt = h >> 1
+                vb = (bw + 7) // 8
+                v = int.from_bytes(bytes(s[q:q + vb]), "little")
+                q += vb
+                take = min(cnt, nv - done)
+                dst[done:done + take] = dvals[v]
+                done += take

@@ -175,6 +175,8 @@ def lib():
     _sig(L.hs_pq_decode_levels, I, P, P, I64, P, P)
     _sig(L.hs_pq_pack, I, P, P, I, I64, I, P, P)
     _sig(L.hs_pq_warmup, I, P)
+    _sig(L.hs_pq_decode_pages, I, P, P, P, I, P, P)
+    _sig(L.hs_pq_page_struct_size, I)
     _sig(L.hs_pq_dict_codes, I, P, I64, I, P, I, P, P, P)
     _sig(L.hs_histogram, I, P, I64, I, P, P)
     _sig(L.hs_xch_tile_rows, I)

@@ -1,0 +1,69 @@
+#!/usr/bin/env python
+"""Index-build benchmark on the bench's TPC-H data: builds the bench's covering indexes (or
+those named by --index) and prints one JSON line per build with its wall time, decoded-bytes
+GB/s and the device build's stage breakdown (``LAST_BUILD_STATS``).
+
+    python scripts/build_bench.py --sf 100 [--index li_shipdate]
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sf", type=float, default=100)
+    ap.add_argument("--buckets", type=int, default=200)
+    ap.add_argument("--data-dir", default=os.environ.get("HS_BENCH_DIR", "/tmp/hs_bench"))
+    ap.add_argument("--index", action="append", default=None)
+    ap.add_argument("--codec", default="none")
+    ap.add_argument("--repeat", type=int, default=1)
+    args = ap.parse_args()
+    import torch
+    from hyperspace_amd import Hyperspace, IndexConfig, Session
+    from hyperspace_amd.exec import device_build
+    from hyperspace_amd.models import tpch
+    torch.cuda.set_device(0)
+    nfiles = max(8, int(round(args.sf * 1.28)))
+    data = os.path.join(args.data_dir, f"tpch_sf{args.sf:g}_f{nfiles}")
+    tpch.generate(data, args.sf, nfiles, workers=16)
+    idx_root = os.path.join(args.data_dir, f"bb_indexes_sf{args.sf:g}")
+    s = Session(conf={"spark.hyperspace.system.path": idx_root,
+                      "spark.hyperspace.index.numBuckets": str(args.buckets),
+                      "spark.hyperspace.mi.execution.device": "gpu",
+                      "spark.hyperspace.mi.index.codec": args.codec},
+                warehouse_dir=os.path.join(args.data_dir, "wh"))
+    hs = Hyperspace(s)
+    s.backend()             # engine start outside the timed builds (as bench.py)
+    li = s.read.parquet(os.path.join(data, "lineitem"))
+    od = s.read.parquet(os.path.join(data, "orders"))
+    builds = [(li, IndexConfig("li_shipdate", ["l_shipdate"],
+                               ["l_discount", "l_quantity", "l_extendedprice"])),
+              (li, IndexConfig("li_orderkey", ["l_orderkey"],
+                               ["l_extendedprice", "l_discount", "l_shipdate"])),
+              (od, IndexConfig("ord_orderkey", ["o_orderkey"], ["o_orderdate", "o_shippriority"]))]
+    for rep in range(args.repeat):
+        if os.path.exists(idx_root):
+            shutil.rmtree(idx_root)
+        for df, cfg in builds:
+            if args.index and cfg.indexName not in args.index:
+                continue
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            hs.createIndex(df, cfg)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+            st = dict(device_build.LAST_BUILD_STATS)
+            print(json.dumps({"index": cfg.indexName, "rep": rep, "s": round(dt, 3),
+                              "gbps": round(st.get("source_bytes", 0) / dt / 1e9, 3),
+                              "stats": st}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

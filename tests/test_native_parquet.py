@@ -145,6 +145,86 @@ def test_snappy_decompress_matches_pyarrow():
     assert L.hs_pq_snappy_decompress(src.ctypes.data, len(src), out.ctypes.data, len(out)) == -1
 
 
+def _plan_and_decode_host(path, names):
+    """Device page plan of ``names`` (hs_pq_plan_chunk) consumed by the host reference decoder
+    (NP.decode_plan_host): {name: values} plus the fields the plan refused."""
+    with NP.PqFile(str(path)) as f:
+        assert f.ok, f.error
+        plan = []
+        for name in names:
+            c = f.column(name)
+            _, _, eb = f.column_info(c)
+            plan.append((pa.field(name, pa.int64()), c, eb))
+        cap = sum(int(f.L.hs_pq_chunk_raw_bytes(f.h, g, c)) + 16
+                  for _, c, _ in plan for g in range(f.num_row_groups)) + 64
+        raw = np.zeros(cap, dtype=np.uint8)
+        hcap = sum(int(f.L.hs_pq_chunk_host_bound(f.h, g, c)) + 16
+                   for _, c, _ in plan for g in range(f.num_row_groups))
+        hd = np.zeros(hcap, dtype=np.uint8)
+        pages, chunks, raw_used, scratch, host_used, skipped = NP.plan_file(
+            f, plan, cap, raw.ctypes.data, hcap, hd.ctypes.data)
+        assert raw_used <= cap and host_used <= hcap
+        rg_off = np.concatenate([[0], np.cumsum([f.row_group_rows(g)
+                                                 for g in range(f.num_row_groups)])])
+        out = {fld.name: np.zeros(f.num_rows, dtype=np.uint32 if eb == 4 else np.uint64)
+               for fld, _, eb in plan}
+        targets = {}
+        for fld, g, p0, n in chunks:
+            for i in range(p0, p0 + n):
+                p = pages[i]
+                pages[i]["out"] = i + 1
+                r0 = int(rg_off[g] + p["row"])
+                targets[i + 1] = out[fld.name][r0:r0 + int(p["nvals"])]
+        NP.decode_plan_host(raw, pages, targets, hd)
+        # every data page starts at its row; pages tile the chunk
+        for fld, g, p0, n in chunks:
+            data = pages[p0:p0 + n][pages[p0:p0 + n]["kind"] != 2]
+            assert int(data["nvals"].sum()) == f.row_group_rows(g)
+            assert (data["dst"] % 16 == 0).all()
+        return {k: v for k, v in out.items() if k not in skipped}, skipped
+
+
+@pytest.mark.parametrize("compression", ["none", "snappy"])
+@pytest.mark.parametrize("dictionary", [True, False])
+@pytest.mark.parametrize("page_version", ["1.0", "2.0"])
+def test_device_page_plan_matches_pyarrow(tmp_path, compression, dictionary, page_version):
+    """The device-decode page plan (host pread + page headers only) decodes to pyarrow's values;
+    chunks that may hold nulls are refused (they take the host page layer)."""
+    rng = np.random.default_rng(8)
+    t = _table(23_000, rng, False)
+    t = t.append_column("n64", pa.array(np.where(rng.random(t.num_rows) < 0.05, None,
+                                                 rng.integers(0, 9, t.num_rows))))
+    path = tmp_path / "t.parquet"
+    pq.write_table(t, path, compression=compression, use_dictionary=dictionary,
+                   data_page_version=page_version, row_group_size=9_000, data_page_size=4096)
+    names = list(np_types) + ["sorted", "n64"]
+    vals, skipped = _plan_and_decode_host(path, names)
+    assert skipped == {"n64"}
+    for name in names[:-1]:
+        ref = t.column(name).combine_chunks()
+        if ref.type == pa.date32():
+            ref = ref.view(pa.int32())
+        nd = ref.to_numpy()
+        np.testing.assert_array_equal(vals[name].view(nd.dtype), nd)
+
+
+def test_device_page_plan_large_dictionary(tmp_path):
+    """Snappy dictionary pages over 64 KiB and pages Snappy compressed (tag-dense) are inflated
+    by the planner (codec 2) and still decode exactly."""
+    rng = np.random.default_rng(4)
+    n = 60_000
+    t = pa.table({"big": pa.array(rng.integers(0, 1 << 40, n)),
+                  "dbl": pa.array(np.round(rng.random(n) * 1e5, 2))})
+    path = tmp_path / "d.parquet"
+    pq.write_table(t, path, compression="snappy", row_group_size=40_000,
+                   dictionary_pagesize_limit=1 << 21)
+    vals, skipped = _plan_and_decode_host(path, ["big", "dbl"])
+    assert not skipped
+    for name in ("big", "dbl"):
+        nd = t.column(name).to_numpy()
+        np.testing.assert_array_equal(vals[name].view(nd.dtype), nd)
+
+
 @pytest.mark.gpu
 def test_native_parquet_gpu_decode_matches_pyarrow(tmp_path, device):
     """The HIP expansion kernels + staging path against pyarrow, incl. nulls and PLAIN pages."""
@@ -167,8 +247,11 @@ def test_native_parquet_gpu_decode_matches_pyarrow(tmp_path, device):
 
     def read_file(p, cols=None):
         return pq.read_table(p, columns=cols)
+    staging.DEVICE_DECODED.clear()
     up = staging.upload_files(read_file, files, counts, schema, device, parquet_local=files)
     torch.cuda.synchronize()
+    # null-free chunks were inflated and expanded on the device (file 0 has no nulls at all)
+    assert set(np_types) | {"sorted"} <= staging.DEVICE_DECODED
     for name in np_types:
         col = up.columns[name]
         ref = full.column(name).combine_chunks()
@@ -181,6 +264,37 @@ def test_native_parquet_gpu_decode_matches_pyarrow(tmp_path, device):
             np.testing.assert_array_equal(col.valid.cpu().numpy().astype(bool), valid)
         np.testing.assert_array_equal(vals[valid], ref.drop_null().to_numpy())
     assert "s" in up.host_strings  # strings still come back through pyarrow
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dictionary", [True, False])
+def test_device_inflate_expand_matches_pyarrow(tmp_path, device, dictionary):
+    """hs_pq_decode_pages (Snappy inflate + expand on the GPU) on streams with long overlapping
+    copies (repeated 8/16-byte patterns), literal-only pages, large pages and large (host
+    inflated) dictionaries."""
+    import torch
+    from hyperspace_amd.exec import staging
+    rng = np.random.default_rng(12)
+    n = 200_000
+    t = pa.table({"rep": pa.array(np.tile(np.array([7, 7, 7, 9], np.int64), n // 4)),
+                  "pat": pa.array(np.tile(rng.integers(0, 1 << 40, 37), n // 37 + 1)[:n]),
+                  "rnd": pa.array(rng.integers(-(1 << 62), 1 << 62, n)),
+                  "f": pa.array(rng.random(n).astype(np.float32)),
+                  "d": pa.array(np.repeat(rng.integers(0, 1000, n // 100), 100).astype(np.int32)),
+                  "const": pa.array(np.full(n, 123456789, np.int64)),
+                  "mix": pa.array(np.where(rng.random(n) < 0.9, 5, rng.integers(0, 1 << 30, n))),
+                  "hicard": pa.array(np.round(rng.random(n) * 1e6, 2))})
+    path = tmp_path / "r.parquet"
+    pq.write_table(t, path, compression="snappy", use_dictionary=dictionary,
+                   row_group_size=70_000, data_page_size=1 << 20)
+    staging.DEVICE_DECODED.clear()
+    up = staging.upload_files(lambda p, cols=None: pq.read_table(p, columns=cols), [str(path)],
+                              [n], t.schema, device, parquet_local=[str(path)])
+    torch.cuda.synchronize()
+    assert staging.DEVICE_DECODED == set(t.column_names)
+    for name in t.column_names:
+        np.testing.assert_array_equal(up.columns[name].data.cpu().numpy(),
+                                      t.column(name).to_numpy())
 
 
 # ------------------------------------------------------------------------------------------------
