@@ -153,13 +153,18 @@ __global__ __launch_bounds__(256) void hs_join_spans_sampled_kernel(
     JoinParams p, const int64_t* __restrict__ rstart, const int64_t* __restrict__ rlen,
     const int32_t* __restrict__ rbucket, const int64_t* __restrict__ roff,
     const int64_t* __restrict__ soff, const uint64_t* __restrict__ samples, int R,
-    const int64_t* __restrict__ tile_prefix, int64_t* __restrict__ spans, int tile_rows) {
+    const int64_t* __restrict__ tile_prefix, int64_t* __restrict__ spans, int tile_rows,
+    int align) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= tile_prefix[R]) return;
   const int r = tile_range_of(tile_prefix, R, t);
   const int64_t off = (t - tile_prefix[r]) * tile_rows;
-  const int64_t row0 = rstart[r] + off;
-  const int64_t rows = min((int64_t)tile_rows, rlen[r] - off);
+  // align > 1: tiles of range r start at rstart[r] rounded down to a multiple of `align` (the
+  // vectorized merge join loads each thread's rows as aligned vectors); the tile's own rows are
+  // its intersection with the range
+  const int64_t a0 = (rstart[r] & ~(int64_t)(align - 1)) + off;
+  const int64_t row0 = max(a0, rstart[r]);
+  const int64_t rows = min(a0 + (int64_t)tile_rows, rstart[r] + rlen[r]) - row0;
   const bool fl = p.key_is_float != 0;
   const int b = rbucket[r];
   const int64_t bs = roff[b], be = roff[b + 1];
@@ -481,18 +486,22 @@ int hs_join_spans(const JoinParams* p, const int64_t* rstart, const int64_t* rle
 
 // Sampled variant: soff (B+1, device) = per-bucket sample offsets, soff[b+1]-soff[b] =
 // ceil(rows_b / JN_SAMPLE); samples = scratch of nsamples >= soff[B] uint64 (filled here).
+// align: 1, or the power-of-two row alignment of the tiles (tile_prefix built from
+// rlen + (rstart & (align - 1)))
 int hs_join_spans_sampled(const JoinParams* p, const int64_t* rstart, const int64_t* rlen,
                           const int32_t* rbucket, const int64_t* roff, const int64_t* soff, int B,
                           int64_t nsamples, uint64_t* samples, int R, const int64_t* tile_prefix,
-                          int64_t max_tiles, int64_t* spans, int tile_rows, void* stream) {
+                          int64_t max_tiles, int64_t* spans, int tile_rows, int align,
+                          void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (align < 1 || (align & (align - 1)) != 0) return (int)hipErrorInvalidValue;
   if (nsamples > 0)
     hipLaunchKernelGGL(hs_join_sample_kernel, dim3((unsigned)((nsamples + 255) / 256)), dim3(256),
                        0, s, p->cols[p->rkey], roff, soff, B, nsamples, samples, p->key_is_float);
   if (max_tiles > 0)
     hipLaunchKernelGGL(hs_join_spans_sampled_kernel, dim3((unsigned)((max_tiles + 255) / 256)),
                        dim3(256), 0, s, *p, rstart, rlen, rbucket, roff, soff, samples, R,
-                       tile_prefix, spans, tile_rows);
+                       tile_prefix, spans, tile_rows, align);
   return (int)hipGetLastError();
 }
 

@@ -61,7 +61,7 @@ def h2d(a: np.ndarray, device):
 
 
 class DeviceColumn:
-    __slots__ = ("data", "valid", "atype", "dictionary", "offsets", "chars", "compact")
+    __slots__ = ("data", "valid", "atype", "dictionary", "offsets", "chars", "compact", "dupkeys")
 
     def __init__(self, data, valid, atype: pa.DataType, dictionary: Optional[pa.Array] = None,
                  offsets=None, chars=None):
@@ -72,6 +72,7 @@ class DeviceColumn:
         self.offsets = offsets
         self.chars = chars
         self.compact = False  # exec.encoding.compact_of: False = not computed, None = n/a
+        self.dupkeys = None   # exec.jit.key_has_dups: None = not computed
 
     def __len__(self):
         return int(self.data.shape[0])

@@ -25,14 +25,16 @@ _MAX_SCALE_DIGITS = 4
 
 
 class Compact:
-    __slots__ = ("codes", "width", "base", "scale", "logical_type")
+    __slots__ = ("codes", "width", "base", "scale", "logical_type", "lo", "hi")
 
-    def __init__(self, codes, width: int, base: int, scale: Optional[float], logical_type: int):
+    def __init__(self, codes, width: int, base: int, scale: Optional[float], logical_type: int,
+                 lo: Optional[int] = None, hi: Optional[int] = None):
         self.codes = codes          # torch int8/int16/int32 tensor (biased: code = v - base)
         self.width = width          # bytes per row
         self.base = int(base)
         self.scale = scale          # None for integers, 10**k for decimals
         self.logical_type = logical_type
+        self.lo, self.hi = lo, hi   # range of the (integer / scaled) values of valid rows
 
     def nbytes(self) -> int:
         return self.codes.numel() * self.width
@@ -77,7 +79,7 @@ def encode(col) -> Optional[Compact]:
         w, bias = _width_for(hi - lo)
         if w is None or w >= d.element_size():
             return None
-        return Compact(_codes(v, lo, w, bias), w, lo + bias, None, t)
+        return Compact(_codes(v, lo, w, bias), w, lo + bias, None, t, lo, hi)
     if t in _FLOAT_TYPES:
         x = d.double()
         if vm is not None:
@@ -106,7 +108,7 @@ def encode(col) -> Optional[Compact]:
             w, bias = _width_for(hi - lo)
             if w is None or w >= d.element_size():
                 return None
-            return Compact(_codes(qi, lo, w, bias), w, lo + bias, s, t)
+            return Compact(_codes(qi, lo, w, bias), w, lo + bias, s, t, lo, hi)
         return None
     return None
 

@@ -362,8 +362,15 @@ class GpuBackend:
         if eq_bucket is not None:
             import torch
             buckets = torch.tensor([eq_bucket], dtype=torch.int32, device=self.device)
-        if lo is None and hi is None and buckets is None and not notnull:
-            return None
+        if lo is None and hi is None and buckets is None:
+            if notnull and kc.valid is None:
+                # isnotnull(key) on a key column without nulls: the full ranges already satisfy
+                # it (and stay the cached full-range object, which keys cached join spans)
+                if implied is not None:
+                    implied.update(id(c) for c in notnull)
+                return None
+            if not notnull:
+                return None
         if implied is not None:
             implied.update(id(c) for c in used + notnull)
         return kc, lo, lo_incl, hi, hi_incl, buckets
@@ -1158,6 +1165,12 @@ class GpuBackend:
         with stage("join.agg_kernel"):
             if HyperspaceConf.codegen_enabled(self.session.conf):
                 fr = getattr(left.table, "_full_ranges", None)
+                comp = self._compacts(descs)
+                if jit.merge_join_ok(jp, comp, right.table.num_rows, left.table.num_rows):
+                    return jit.merge_join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets,
+                                              comp, nrows=left.table.num_rows,
+                                              cache_spans=fr is not None and rstart is fr[0],
+                                              rdup=jit.key_has_dups(right.col(rk)))
                 return jit.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles,
                                     self._compacts(descs),
                                     cache_spans=fr is not None and rstart is fr[0])

@@ -77,6 +77,15 @@ JOIN_PIPELINE = os.environ.get("HS_JIT_JOIN_PIPELINE", "1") == "1"
 # search is not on this kernel's critical path, the extra table writes and loads are
 JOIN_DIRECT = os.environ.get("HS_JIT_JOIN_DIRECT", "0") == "1"
 JOIN_DIRECT_SLOTS = int(os.environ.get("HS_JIT_JOIN_DIRECT_SLOTS", "2048"))
+# vectorized sort-merge join (gen_merge_join_agg): rows per thread (0 = the strided join_agg
+# kernel), LDS right-key slots per tile, grid
+MJ_ITEMS = int(os.environ.get("HS_JIT_MJ_ITEMS", "8"))
+MJ_LDS_KEYS = int(os.environ.get("HS_JIT_MJ_LDS_KEYS", "2048"))
+MJ_GRID = int(os.environ.get("HS_JIT_MJ_GRID", "8192"))
+MJ_STEPS = int(os.environ.get("HS_JIT_MJ_STEPS", "1"))   # branch-free walk steps per row
+MJ_KEY32 = os.environ.get("HS_JIT_MJ_KEY32", "1") == "1"  # 32-bit merge images (_key32_frame)
+# cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
+MJ_EXP = os.environ.get("HS_JIT_MJ_EXP", "")
 # software-pipelined full tiles in the vectorized kernels (_vec_tiles)
 VEC_PREFETCH = os.environ.get("HS_JIT_VEC_PREFETCH", "1") == "1"
 # per-wavefront compaction lists ordered by a wavefront barrier instead of __syncthreads
@@ -1069,6 +1078,373 @@ def _rename(line: str, slots, it: int) -> str:
 _SOFF: Dict[int, tuple] = {}
 
 
+def merge_join_shape(p: NL.JoinParams, compacts=None) -> tuple:
+    cols = tuple(sorted(_col_specs(p, compacts).items()))
+    preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
+                   p.preds[k].group) for k in range(p.npreds))
+    aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
+                 for i in range(p.naggs))
+    return ("merge_join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey,
+            p.key_is_float, MJ_ITEMS, MJ_LDS_KEYS, MJ_STEPS, BLOCK, WAVE_SYNC,
+            _key32_frame(p, compacts) is not None, MJ_EXP)
+
+
+def key_has_dups(col) -> bool:
+    """Whether a sorted key column (a join's right side) repeats a non-null key: equal keys hash
+    to one bucket, so they are adjacent.  Float keys are assumed to (NaN / -0.0 images).  Cached
+    on the column (one device sync per table)."""
+    d = getattr(col, "dupkeys", None)
+    if d is None:
+        x = col.data
+        if col.is_float:
+            d = True
+        elif x.numel() < 2:
+            d = False
+        else:
+            eq = x[1:] == x[:-1]
+            if col.valid is not None:
+                eq &= (col.valid[1:] != 0) & (col.valid[:-1] != 0)
+            d = bool(eq.any().item())
+        col.dupkeys = d
+    return d
+
+
+def _slots_of(pred) -> List[int]:
+    return _pred_slots([(0, pred)])
+
+
+def _key32_frame(p: NL.JoinParams, compacts) -> Optional[Tuple[int, int, int]]:
+    """32-bit merge keys: (lo, span, code offset) when the left key is an integer column with a
+    compact form whose value range [lo, lo + span] leaves room for the two out-of-range images
+    (span <= 2^32 - 3).  Left image = value - lo + 1 = code + (base - lo + 1), in [1, 2^32 - 2];
+    a right value maps to the same image, or to 0 / 2^32 - 1 outside the left range (never
+    equal to a left image, order kept), so merges compare 32-bit words."""
+    if p.key_is_float or not MJ_KEY32:
+        return None
+    c = (compacts or {}).get(p.lkey)
+    if c is None or c.scale is not None or getattr(c, "lo", None) is None:
+        return None
+    span = int(c.hi) - int(c.lo)
+    if span > (1 << 32) - 3:
+        return None
+    return int(c.lo), span, int(c.base) - int(c.lo) + 1
+
+
+def _deferred_append(NI: int, ind: str, pass_fmt: str, row_fmt: str, j_fmt: str) -> List[str]:
+    """Append this thread's passing (row, j) pairs to its wavefront's LDS list (absolute int32
+    rows); ``wcnt`` is the wave-uniform list length.  Failing lanes write a private dump slot,
+    so the appends are branch-free."""
+    b = []
+    for it in range(NI):
+        b += [f"{ind}{{ const bool pz = {pass_fmt.format(it=it)}; const u64 bm = __ballot(pz);",
+              f"{ind}  const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), "
+              f"__builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;",
+              f"{ind}  lrow_s[wv][wp] = (int)({row_fmt.format(it=it)}); "
+              f"lj_s[wv][wp] = (int)({j_fmt.format(it=it)});",
+              f"{ind}  wcnt += __popcll(bm); }}"]
+    return b
+
+
+def _deferred_drain(args, cols, split, approx, aggs, grouped, group_col, allslots, ind: str,
+                    final: bool) -> List[str]:
+    """Aggregate full 64-entry batches from the top of the wavefront's list (``final``: every
+    remaining entry): the aggregate inputs are gathered once per 64 passing rows, all lanes
+    active, instead of once per tile."""
+    cond = "wcnt > 0" if final else "wcnt >= 64"
+    b = [f"{ind}{_wave_sync()}",
+         f"{ind}while ({cond}) {{",
+         f"{ind}  const int cb = wcnt > 64 ? wcnt - 64 : 0;",
+         f"{ind}  const int ce = cb + cln;",
+         f"{ind}  bool cok = ce < wcnt;",
+         f"{ind}  const i64 crow = (i64)lrow_s[wv][cok ? ce : cb];",
+         f"{ind}  const i64 cj = (i64)lj_s[wv][cok ? ce : cb];"]
+    ind2 = ind + "  "
+    g = _Gen(args, cols, split, ("crow", "cj"), approx, True)
+    tail = list(dict.fromkeys(_agg_slots(aggs) + ([group_col] if grouped else [])))
+    for sl in tail:
+        _uload(g, sl, "c", b, ind2)
+    gvar = "gic"
+    if grouped:
+        base = args.add("q", "group_base", "long long")
+        ng = args.add("q", "num_groups", "long long")
+        b.append(f"{ind2}const i64 glc = (i64){_rename(f'x{group_col}', allslots, 'c')} - {base};")
+        b.append(f"{ind2}cok = cok && {_rename(g.ok(group_col), allslots, 'c')} && "
+                 f"glc >= 0 && glc < {ng};")
+        b.append(f"{ind2}const int {gvar} = cok ? (int)glc : 0;")
+    b += [_rename(x, allslots, "c") for x in _accumulate(g, aggs, grouped, "cok", gvar, ind2)]
+    b += [f"{ind2}wcnt = cb;",
+          f"{ind2}{_wave_sync()}",
+          f"{ind}}}"]
+    return b
+
+
+def gen_merge_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
+    """Co-located sort-merge join + aggregate, re-matching keys every query (no cached join
+    index).  Left tiles are ``BLOCK * MJ_ITEMS`` rows of one bucket range, aligned so each thread
+    owns ``MJ_ITEMS`` consecutive rows read with aligned vector loads; the tile's right key span
+    (``hs_join_spans_sampled``, align = MJ_ITEMS) is staged in LDS.  Per tile:
+
+    1. stage: right key images (32-bit in the left key's frame when ``_key32_frame`` allows,
+       else order-preserving u64; nulls as the minimum) and one pass byte per right row — the
+       right side's own predicates are evaluated once per right row here, not once per match;
+    2. stream: the left key + left predicate columns of the thread's rows (vector loads);
+    3. merge: one LDS binary search for the thread's first passing key, then a branch-free walk
+       of MJ_STEPS key steps per row (keys ascend through the thread's rows; an FK join moves 0
+       or 1 key per row); threads whose walk falls short take a general loop;
+    4. tail: passing (row, match) pairs go to per-wavefront LDS lists and the aggregate inputs
+       are loaded only for them (``_compacted_tail``); right tables with duplicate keys
+       (``a.rdup``) repeat 3-4 for the next equal key until no lane has one.
+
+    The kernel is VALU-issue bound, so the per-row work is kept to a few 32-bit operations
+    (profiles/pmc_merge_join_r2.txt).  Spans longer than MJ_LDS_KEYS (many right rows per left
+    tile) are searched in HBM.  Reference: the bucketed SortMergeJoin plans of JoinIndexRule
+    (JoinIndexRule.scala:63-69), which re-match keys on every query."""
+    NI = MJ_ITEMS  # noqa: N806
+    T = BLOCK * NI  # noqa: N806
+    LK = MJ_LDS_KEYS  # noqa: N806
+    args = Args()
+    for n, ct in (("rstart", "const long long*"), ("rlen", "const long long*"),
+                  ("tile_prefix", "const long long*"), ("spans", "const long long*")):
+        args.add("p", n, ct)
+    args.add("q", "R", "long long")
+    args.add("q", "nrows", "long long")
+    args.add("q", "rdup", "long long")
+    _common_args(args)
+    cols = _col_specs(p, compacts)
+    split = 8
+    fl = bool(p.key_is_float)
+    lk, rk = p.lkey, p.rkey
+    k32 = _key32_frame(p, compacts) is not None
+    KT = "unsigned" if k32 else "u64"  # noqa: N806
+    KMAX = "0xFFFFFFFFu" if k32 else "~0ull"  # noqa: N806
+    if k32:
+        args.add("q", "KLO", "long long")
+        args.add("q", "KSP", "long long")
+        args.add("q", "KOF", "long long")
+    lpreds = [(k, p.preds[k]) for k in range(p.nlp)]
+    rpreds = [(k, p.preds[k]) for k in range(p.nlp, p.npreds)]
+    ronly = [(k, q) for k, q in rpreds if all(x >= split for x in _slots_of(q))]
+    mixed = [(k, q) for k, q in rpreds if (k, q) not in ronly]
+    aggs = [p.aggs[i] for i in range(p.naggs)]
+    grouped = p.group_col >= 0
+    mixed_left = [x for x in _pred_slots(mixed) if x < split]
+    first = list(dict.fromkeys([lk] + _pred_slots(lpreds) + mixed_left))
+    ronly_slots = [x for x in _pred_slots(ronly)]
+    mixed_right = [x for x in _pred_slots(mixed) if x >= split]
+    stage_slots = list(dict.fromkeys([rk] + ronly_slots))
+    allslots = list(dict.fromkeys(first + stage_slots + mixed_right + _agg_slots(aggs) +
+                                  ([p.group_col] if grouped else [])))
+    approx = _sum_only_slots(lpreds + rpreds, aggs, p.group_col, cols) - {lk, rk}
+    ind = "    "
+    g1 = _Gen(args, cols, split, ("row0", "row0"), approx, True)
+    b: List[str] = []
+    b += _acc_decls(aggs, grouped, args)
+    W = BLOCK // 64  # noqa: N806
+    CAP = 64 * NI + 64  # noqa: N806 — list entries: < 64 carried over + one tile's appends
+    b += [f"  __shared__ {KT} skeys[{LK + 1}]; __shared__ unsigned char spass[{LK}];",
+          f"  constexpr int DUMP = {CAP};",
+          f"  __shared__ int lrow_s[{W}][{CAP + 64}]; __shared__ int lj_s[{W}][{CAP + 64}];",
+          "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;",
+          "  int wcnt = 0;   // wavefront-uniform length of this wavefront's (row, j) list"]
+    rkv = _valid_expr(g1, rk, "{r}")
+
+    def rimg(val: str) -> str:
+        """Merge image of a right key value."""
+        if not k32:
+            return _key_expr(val, fl)
+        return (f"({{ const i64 d_ = (i64)({val}) - a.KLO; "
+                f"d_ < 0 ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }})")
+
+    def limg(it: int) -> str:
+        """Merge image of left item ``it``."""
+        if not k32:
+            return _key_expr(f"x{lk}_{it}", fl)
+        return f"((unsigned)x{lk}v[{it}] + (unsigned)a.KOF)"
+
+    def body(b: List[str], full: bool) -> None:
+        b.extend([f"{ind}const i64 ss = a.spans[4 * t + 2], se = a.spans[4 * t + 3];",
+                  f"{ind}const int ns = (int)(se - ss);",
+                  f"{ind}const bool staged = ns <= {LK};"])
+        # (1) stage the right span: key images + right-only predicate pass bytes
+        stg = "staged && false" if "nostage" in MJ_EXP else "staged"
+        b.extend([f"{ind}if ({stg}) for (int sq = threadIdx.x; sq < ns; sq += {BLOCK}) {{",
+                  f"{ind}  const i64 jr = ss + sq;"])
+        gs = _Gen(args, cols, split, ("jr", "jr"), approx, True)
+        for sl in stage_slots:
+            _uload(gs, sl, "s", b, ind + "  ")
+        okk = f"n{rk}_s" if cols[rk][1] else "true"
+        cond = _rename(gs.cnf(ronly), allslots, "s")
+        b.extend([f"{ind}  const bool kv = {okk};",
+                  f"{ind}  skeys[sq] = kv ? {rimg(f'x{rk}_s')} : ({KT})0;",
+                  f"{ind}  spass[sq] = (kv && {cond}) ? 1 : 0;",
+                  f"{ind}}}",
+                  f"{ind}if (staged && threadIdx.x == 0) skeys[ns] = {KMAX};   // walk sentinel"])
+        # (2) left stream (raw vector arrays come from the tile loop).  Per-item flags live as
+        # bits of one VGPR word each (kvb: key valid, mb: left predicates, mtb: matched): a bool
+        # per item would hold a 64-bit SGPR lane mask, and 8 items x 4 flags exhaust the SGPRs
+        _vec_load_slots(b, g1, first, NI, ind)
+        b.append(f"{ind}unsigned kvb = 0u, mb = 0u;")
+        for it in range(NI):
+            gi = _Gen(args, cols, split, (f"row{it}", f"row{it}"), approx, True)
+            cond = _rename(gi.cnf(lpreds), allslots, it)
+            okl = f"n{lk}_{it}" if cols[lk][1] else "true"
+            b.append(f"{ind}{{ const bool kv = act{it} && {okl}; kvb |= kv ? {1 << it}u : 0u; "
+                     f"mb |= (kv && {cond}) ? {1 << it}u : 0u; }}")
+            b.append(f"{ind}const {KT} k{it} = {limg(it)};")
+        b.append(f"{ind}__syncthreads();")
+
+        def bit(word: str, it: int) -> str:
+            return f"(({word} >> {it}) & 1u)"
+        # (3) merge
+        b.append(f"{ind}{KT} kf = {KMAX};")
+        for it in reversed(range(NI)):
+            b.append(f"{ind}kf = {bit('mb', it)} ? k{it} : kf;")
+        b.append(f"{ind}unsigned mtb = 0u;")
+        for it in range(NI):
+            b.append(f"{ind}int jl{it} = 0;")
+        b.extend([f"{ind}bool slow = !staged;",
+                  f"{ind}int jw0 = 0;",
+                  f"{ind}if (staged) {{",
+                  f"{ind}  int lo = 0;",
+                  f"{ind}  for (int st = ns > 0 ? (1 << (31 - __builtin_clz(ns))) : 0; st > 0; st >>= 1) {{",
+                  f"{ind}    const int c = lo + st; const {KT} sv = skeys[c <= ns ? c - 1 : ns];",
+                  f"{ind}    lo = (c <= ns && sv < kf) ? c : lo; }}",
+                  f"{ind}  jw0 = lo; int jw = lo; {KT} v = skeys[jw];"])
+        for it in range(NI):
+            b.append(f"{ind}  {{ const {KT} ke = {bit('kvb', it)} ? k{it} : ({KT})0;")
+            for _ in range(MJ_STEPS):
+                b.append(f"{ind}    {{ const bool c = v < ke; jw += c ? 1 : 0; v = skeys[jw]; }}")
+            b.extend([f"{ind}    slow = slow || v < ke;",
+                      f"{ind}    mtb |= ({bit('mb', it)} && v == ke && jw < ns) ? {1 << it}u : 0u; "
+                      f"jl{it} = jw; }}"])
+        b.append(f"{ind}}}")
+        if "nowalk" in MJ_EXP:
+            b.append(f"{ind}mtb = mb; slow = false;")
+        b.extend([f"{ind}if (__any(slow)) {{",
+                  f"{ind}  if (slow) {{ int jw = jw0; mtb = 0u;"])
+        for it in range(NI):
+            b.extend([f"{ind}    if ({bit('mb', it)}) {{ bool hit;",
+                      f"{ind}      if (staged) {{ while (jw < ns && skeys[jw] < k{it}) ++jw;",
+                      f"{ind}        hit = jw < ns && skeys[jw] == k{it}; jl{it} = jw; }}",
+                      f"{ind}      else {{ i64 lo = ss, hi = se;",
+                      f"{ind}        while (lo < hi) {{ const i64 md = (lo + hi) >> 1; "
+                      f"const bool nv = {rkv.format(r='md')}; "
+                      f"if (nv || {rimg(g1.value(rk, 'md'))} < k{it}) lo = md + 1; else hi = md; }}",
+                      f"{ind}        hit = lo < se && !({rkv.format(r='lo')}) && "
+                      f"{rimg(g1.value(rk, 'lo'))} == k{it}; jl{it} = (int)(lo - ss); }}",
+                      f"{ind}      mtb |= hit ? {1 << it}u : 0u;",
+                      f"{ind}    }}"])
+        b.extend([f"{ind}  }}", f"{ind}}}"])
+
+        # (4) match rounds: right predicates at j, compacted aggregate tail; right tables with
+        # duplicate keys (a.rdup) repeat for the next equal key until no lane has one
+        def one_round(i2: str) -> None:
+            b.append(f"{i2}{{ unsigned pb = mtb;")
+            if ronly:
+                b.append(f"{i2}if (staged) {{")
+                for it in range(NI):
+                    b.append(f"{i2}  pb &= spass[{bit('mtb', it)} ? jl{it} : 0] != 0 ? ~0u : ~{1 << it}u;")
+                b.append(f"{i2}}} else {{")
+                for it in range(NI):
+                    b.append(f"{i2}  {{ const i64 jq{it} = ss + ({bit('mtb', it)} ? jl{it} : 0);")
+                    g2 = _Gen(args, cols, split, (f"row{it}", f"jq{it}"), approx, True)
+                    for sl in ronly_slots:
+                        _uload(g2, sl, it, b, i2 + "    ")
+                    b.append(f"{i2}    pb &= ({_rename(g2.cnf(ronly), allslots, it)}) ? ~0u : ~{1 << it}u; }}")
+                b.append(f"{i2}}}")
+            if mixed:
+                for it in range(NI):
+                    b.append(f"{i2}{{ const i64 jm{it} = ss + ({bit('pb', it)} ? jl{it} : 0);")
+                    g2 = _Gen(args, cols, split, (f"row{it}", f"jm{it}"), approx, True)
+                    for sl in mixed_right:
+                        _uload(g2, sl, f"{it}m", b, i2 + "  ")
+                    cond = _rename(_rename(g2.cnf(mixed), mixed_right, f"{it}m"), first, it)
+                    b.append(f"{i2}  pb &= ({cond}) ? ~0u : ~{1 << it}u; }}")
+            if "notail" in MJ_EXP:
+                b.append(f"{i2}cnt0 += __popc(pb);")
+            else:
+                b.extend(_deferred_append(NI, i2, "((pb >> {it}) & 1u)", "row{it}",
+                                          "ss + jl{it}"))
+                b.extend(_deferred_drain(args, cols, split, approx, aggs, grouped, p.group_col,
+                                         allslots, i2, final=False))
+            b.append(f"{i2}}}")
+
+        one_round(ind)
+        b.append(f"{ind}if (a.rdup) while (true) {{")
+        i2 = ind + "  "
+        for it in range(NI):
+            b.extend([f"{i2}if ({bit('mtb', it)}) {{ ++jl{it};",
+                      f"{i2}  const bool more = jl{it} < ns && (staged ? skeys[jl{it}] == k{it} : "
+                      f"(!({rkv.format(r=f'(ss + jl{it})')}) && "
+                      f"{rimg(g1.value(rk, f'(ss + jl{it})'))} == k{it}));",
+                      f"{i2}  if (!more) mtb &= ~{1 << it}u; }}"])
+        b.append(f"{i2}if (!__any(mtb != 0u)) break;")
+        one_round(i2)
+        b.append(f"{ind}}}")
+        b.append(f"{ind}__syncthreads();")
+
+    loads = _vec_loads(g1, first)
+    _tile_loop(b, T, NI, 1, ind)
+    b.append(f"{ind}if (tb0 + {T} <= a.nrows) {{")
+    _vec_issue(b, loads, NI, ind, True)
+    body(b, True)
+    b.append(f"{ind}}} else {{")
+    _vec_issue(b, loads, NI, ind, False)
+    body(b, False)
+    b.append(f"{ind}}}")
+    b += ["  }"]
+    b += _deferred_drain(args, cols, split, approx, aggs, grouped, p.group_col, allslots, "  ",
+                         final=True)
+    b += _flush(aggs, grouped)
+    src = (_PRELUDE + args.struct_src() +
+           f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_merge_join_agg(Args a) {{\n' +
+           "\n".join(b) + "\n}\n")
+    lds = (len(aggs) * p.num_groups * 32) if grouped else 0
+    return Kernel(src, "hs_jit_merge_join_agg", args, lds)
+
+
+def merge_join_ok(p: NL.JoinParams, compacts=None, rnrows: int = 0, lnrows: int = 0) -> bool:
+    """The vectorized merge join needs 16-byte aligned bases of the streamed left columns and
+    left / right row indices that fit its int32 aggregate lists."""
+    if MJ_ITEMS <= 0 or rnrows >= (1 << 31) or lnrows >= (1 << 31):
+        return False
+    ptrs = []
+    slots = [p.lkey] + _pred_slots([(k, p.preds[k]) for k in range(p.nlp)]) + \
+        [x for x in _pred_slots([(k, p.preds[k]) for k in range(p.nlp, p.npreds)]) if x < 8]
+    for s in dict.fromkeys(slots):
+        c = (compacts or {}).get(s)
+        ptrs.append(c.codes.data_ptr() if c else p.cols[s].data)
+        ptrs.append(p.cols[s].valid)
+    return _vec_aligned_ptrs(ptrs)
+
+
+def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None, nrows: int = 0,
+                   cache_spans: bool = False, rdup: bool = True):
+    """Sort-merge join + aggregate with ``gen_merge_join_agg`` (same outputs as ``join_agg``);
+    ``nrows`` = left table rows; ``rdup`` = the right key column may repeat a key
+    (``key_has_dups``)."""
+    NI = MJ_ITEMS  # noqa: N806
+    T = BLOCK * NI  # noqa: N806
+    GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
+    dev = rstart.device
+    max_tiles = nrows // T + 2 * rstart.numel() + 2
+    tp, spans = _join_spans(p, rstart, rlen, rbucket, roff, max_tiles, T, cache_spans, align=NI)
+    k = kernel_for(merge_join_shape(p, compacts), lambda: gen_merge_join_agg(p, compacts))
+    grid = MJ_GRID
+    parts = _partials(grid, GA, dev)
+    v = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
+         "spans": spans.data_ptr(), "R": rstart.numel(), "nrows": nrows, "rdup": int(rdup),
+         "psum": parts[0].data_ptr(), "pcnt": parts[1].data_ptr(), "pmin": parts[2].data_ptr(),
+         "pmax": parts[3].data_ptr(), "num_groups": p.num_groups, "group_base": p.group_base}
+    _fill_common(v, p.cols, [(k_, p.preds[k_]) for k_ in range(p.npreds)],
+                 [p.aggs[i] for i in range(p.naggs)], compacts)
+    frame = _key32_frame(p, compacts)
+    if frame is not None:
+        v["KLO"], v["KSP"], v["KOF"] = frame
+    k.launch(grid, v, NL.stream_ptr(), GA * 32 if p.group_col >= 0 else 0)
+    return _final(parts, grid, GA, dev)
+
+
 def _sample_offsets(roff):
     """Per-bucket offsets of the right side's sparse key samples (every ``hs_join_sample_stride``
     -th key) and a host bound on their count.  Bucket offsets of a device table never change, so
@@ -1094,28 +1470,35 @@ _SPANS: Dict[tuple, tuple] = {}
 
 
 def _join_spans(p: NL.JoinParams, rstart, rlen, rbucket, roff, max_tiles: int, tile: int,
-                cache: bool):
+                cache: bool, align: int = 1):
+    """(tile_prefix, spans) of the left ranges: per ``tile``-row tile its (row0, rows, rs, re).
+    ``align`` > 1: tiles start at each range's start rounded down to a multiple of ``align``
+    (the vectorized merge join), ``max_tiles`` is then a bound on the tile count itself."""
     import torch
     from ..ops import kernels as K
     L = NL.lib()
     lk, rk = p.cols[p.lkey], p.cols[p.rkey]
     key = (id(rstart), id(rlen), id(rbucket), id(roff), lk.data, lk.valid, rk.data, rk.valid,
-           int(p.key_is_float), tile)
+           int(p.key_is_float), tile, align)
     if cache:
         hit = _SPANS.get(key)
         if hit is not None and hit[0] is rstart and hit[1] is rlen and hit[2] is rbucket \
                 and hit[3] is roff:
             return hit[4], hit[5]
     dev = rstart.device
-    tp = K.ranges_to_tiles(rlen, tile)
-    mt = (max_tiles * L.hs_join_tile_rows()) // tile + rlen.numel() + 1
+    if align > 1:
+        tp = K.ranges_to_tiles(rlen + (rstart & (align - 1)), tile)
+        mt = int(max_tiles)
+    else:
+        tp = K.ranges_to_tiles(rlen, tile)
+        mt = (max_tiles * L.hs_join_tile_rows()) // tile + rlen.numel() + 1
     spans = torch.empty(4 * mt, dtype=torch.int64, device=dev)
     soff, bound = _sample_offsets(roff)
     samples = torch.empty(max(bound, 1), dtype=torch.int64, device=dev)
     NL.check(L.hs_join_spans_sampled(C.byref(p), NL.ptr(rstart), NL.ptr(rlen), NL.ptr(rbucket),
                                      NL.ptr(roff), NL.ptr(soff), roff.numel() - 1, bound,
                                      NL.ptr(samples), rstart.numel(), NL.ptr(tp), int(mt),
-                                     NL.ptr(spans), tile, NL.stream_ptr()),
+                                     NL.ptr(spans), tile, int(align), NL.stream_ptr()),
              "hs_join_spans_sampled")
     if cache:
         if len(_SPANS) >= 16:
@@ -1350,7 +1733,8 @@ def _vec_aligned_ptrs(ptrs) -> bool:
 
 
 def _compacted_tail(args, cols, split, approx, aggs, grouped, group_col, third, allslots,
-                    NI: int, ind: str, with_j: bool = True) -> List[str]:
+                    NI: int, ind: str, with_j: bool = True, pass_fmt: str = "pass{it}",
+                    j_fmt: str = "j{it}", dump: bool = False) -> List[str]:
     """Phase 3 over the passing rows only.  A join like TPC-H Q3 keeps a few percent of its
     rows, so decoding and accumulating all NI x 64 rows of a wavefront (branch-free) is mostly
     wasted VALU work: instead each lane appends its passing (row, j) pairs to a per-wavefront
@@ -1360,12 +1744,20 @@ def _compacted_tail(args, cols, split, approx, aggs, grouped, group_col, third, 
     # from one ballot + mbcnt per item instead of a 6-step cross-lane prefix sum
     b = [f"{ind}int wtot = 0;"]
     for it in range(NI):
-        cj = f"cj_s[wv][pos{it}] = (int)j{it}; " if with_j else ""
-        b += [f"{ind}{{ const u64 bm = __ballot(pass{it});",
+        pv = pass_fmt.format(it=it)
+        cj = f"cj_s[wv][pos{it}] = (int)({j_fmt.format(it=it)}); " if with_j else ""
+        b += [f"{ind}{{ const bool pz = {pv}; const u64 bm = __ballot(pz);",
               f"{ind}  const int pos{it} = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), "
-              f"__builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));",
-              f"{ind}  if (pass{it}) {{ crow_s[wv][pos{it}] = (crow_t)(row{it} - tb0); {cj}}}",
-              f"{ind}  wtot += __popcll(bm); }}"]
+              f"__builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));"]
+        if dump:
+            # branch-free: failing lanes write their own slot past the list (crow_s/cj_s carry
+            # 64 extra entries per wavefront), so no exec-mask save/restore per item
+            b += [f"{ind}  const int wp{it} = pz ? pos{it} : {64 * NI} + cln;",
+                  f"{ind}  crow_s[wv][wp{it}] = (crow_t)(row{it} - tb0); " +
+                  cj.replace(f"[pos{it}]", f"[wp{it}]")]
+        else:
+            b += [f"{ind}  if (pz) {{ crow_s[wv][pos{it}] = (crow_t)(row{it} - tb0); {cj}}}"]
+        b += [f"{ind}  wtot += __popcll(bm); }}"]
     b += [f"{ind}{_wave_sync()}",
           f"{ind}for (int cb = 0; cb < wtot; cb += 64) {{",
           f"{ind}  const int ce = cb + cln;",

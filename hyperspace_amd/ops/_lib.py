@@ -168,7 +168,7 @@ def lib():
     _sig(L.hs_join_count, I, P, P, P, P, P, I, P, I64, P, I, P, P)
     _sig(L.hs_join_emit, I, P, I, P, P, I, P, P, P, P)
     _sig(L.hs_join_spans, I, P, P, P, P, P, I, P, I64, P, I, P)
-    _sig(L.hs_join_spans_sampled, I, P, P, P, P, P, P, I, I64, P, I, P, I64, P, I, P)
+    _sig(L.hs_join_spans_sampled, I, P, P, P, P, P, P, I, I64, P, I, P, I64, P, I, I, P)
     _sig(L.hs_join_sample_stride, I)
     _sig(L.hs_join_index, I, P, I, P, P, I, P, P)
     _sig(L.hs_pq_decode_values, I, P, P, I64, I64, I64, I, P, P)

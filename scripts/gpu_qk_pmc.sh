@@ -16,9 +16,9 @@ i=0
 while IFS= read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-include-regex "${KREGEX:-hs_jit}" \
+  timeout -s KILL ${PMC_KILL:-120} rocprofv3 --pmc $grp --kernel-include-regex "${KREGEX:-hs_jit}" \
     --kernel-trace --output-format csv -d "$OUT/p$i" -o pmc -- \
-    python3 "$REPO/scripts/qk_sweep.py" --sf ${SF:-100} --reps 4 --configs "$CFGS" \
+    python3 "$REPO/scripts/qk_sweep.py" --sf ${SF:-100} --reps 4 --configs "$CFGS" ${SWEEP_EXTRA} \
     > "$OUT/p$i.jsonl" 2> "$OUT/p$i.log" || exit $?
   find "$OUT/p$i" -name "*counter_collection.csv" -exec cp {} "$OUT/counters$i.csv" \;
   rm -rf "$OUT/p$i"

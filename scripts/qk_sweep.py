@@ -123,6 +123,9 @@ def main():
         stages = {k: round(v["device_ms"] / max(v["calls"], 1), 4) for k, v in rep.items()}
         return {"wall_ms": round(wall, 4), "stages": stages, "res": str(res)[:120]}
 
+    if args.configs and args.configs.startswith("@"):   # @file: JSON list in a file
+        with open(args.configs[1:]) as f:
+            args.configs = f.read()
     configs = json.loads(args.configs) if args.configs else DEFAULT
     base = {k: getattr(jit, k) for c in configs for k in c}
     for cfg in configs:

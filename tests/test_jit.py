@@ -82,7 +82,7 @@ def test_generated_sources_compile(rt, tmp_path):
     j.naggs, j.lkey, j.rkey = 2, 0, 8
     for g, fl in ((-1, 0), (10, 0), (-1, 1)):
         j.group_col, j.num_groups, j.key_is_float = g, 3, fl
-        ks = [jit.gen_join_agg(j)]
+        ks = [jit.gen_join_agg(j), jit.gen_merge_join_agg(j)]
         if not fl:
             ks += [jit.gen_join_index_agg(j), jit.gen_join_index_agg(j, vec=4),
                    jit.gen_join_index_agg(j, vec=8, jw=1, jlog=7),
@@ -168,7 +168,15 @@ def test_generated_sources_compile_with_compact_columns(rt, tmp_path):
                                                str(tmp_path).encode())
     assert rc == 0, jit.runtime().hs_jit_last_error().decode()
     ks = [q3_join_index_kernel(jit, stage=True), q3_join_index_kernel(jit, bitmap=True),
-          q3_join_index_kernel(jit, vec=0, bitmap=True), q3_bitmap_kernel(jit)]
+          q3_join_index_kernel(jit, vec=0, bitmap=True), q3_bitmap_kernel(jit),
+          jit.gen_merge_join_agg(_q3_params(), _q3_compacts())]
+    c32 = dict(_q3_compacts())
+    c32[0] = Compact(None, 4, 1 + (1 << 31), None, NL.I64, 1, 600_000_000)
+    c32[8] = Compact(None, 4, 1 + (1 << 31), None, NL.I64, 1, 600_000_000)
+    k32 = jit.gen_merge_join_agg(_q3_params(), c32)
+    assert "unsigned skeys" in k32.src and "a.KOF" in k32.src    # 32-bit merge images
+    assert "u64 skeys" in ks[-1].src
+    ks.append(k32)
     assert "st9_s" in ks[0].src          # phase 2 staged through LDS
     assert "a.rbm" in ks[1].src and "a.c9" not in ks[1].src   # phase 2 = bitmap tests
     for k in ks:
@@ -335,6 +343,96 @@ def test_jit_join_agg_matches_aot(device):
         cg = [t.cpu().numpy() for t in jit.join_agg(p, rstart, rlen, rbk, roff_t, mt, comp)]
         np.testing.assert_allclose(cg[0], got[0], rtol=1e-12)
         assert np.array_equal(cg[1], got[1])
+        # vectorized sort-merge join: staged spans, and every span searched in HBM
+        lds_keys = jit.MJ_LDS_KEYS
+        try:
+            for keys in (lds_keys, 16):
+                jit.MJ_LDS_KEYS = keys
+                for cmp in (None, comp):
+                    mj = [t.cpu().numpy() for t in
+                          jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, cmp, nrows=len(lk))]
+                    np.testing.assert_allclose(mj[0], got[0], rtol=1e-12)
+                    assert np.array_equal(mj[1], got[1]), (keys, cmp is None)
+        finally:
+            jit.MJ_LDS_KEYS = lds_keys
+
+
+@pytest.mark.gpu
+def test_merge_join_agg_numpy_oracle(device):
+    """Merge join with right-only predicates, a left predicate, duplicate right keys, null keys
+    on both sides and sub-ranges (unaligned range starts) against a numpy fp64 oracle."""
+    import torch
+    from hyperspace_amd.exec import jit
+    from hyperspace_amd.ops import kernels as K
+    rng = np.random.default_rng(5)
+    B = 4
+    rk = rng.integers(0, 60_000, 50_000).astype(np.int64)
+    rnull = rng.random(len(rk)) < 0.01
+    lk = rng.integers(0, 60_000, 400_003).astype(np.int64)
+    lnull = rng.random(len(lk)) < 0.01
+    rb = murmur3.bucket_ids([pa.array(rk)], B)
+    lb = murmur3.bucket_ids([pa.array(lk)], B)
+    rb[rnull] = rng.integers(0, B, rnull.sum())
+    lb[lnull] = rng.integers(0, B, lnull.sum())
+    # sort: bucket, nulls first, key
+    ro = np.lexsort((rk, ~rnull, rb)); rk, rb, rnull = rk[ro], rb[ro], rnull[ro]
+    lo_ = np.lexsort((lk, ~lnull, lb)); lk, lb, lnull = lk[lo_], lb[lo_], lnull[lo_]
+    loff = np.searchsorted(lb, np.arange(B + 1)).astype(np.int64)
+    roff = np.searchsorted(rb, np.arange(B + 1)).astype(np.int64)
+    ldate = rng.integers(0, 1000, len(lk)).astype(np.int32)
+    lprice = np.round(rng.random(len(lk)) * 1000, 2)
+    rdate = rng.integers(0, 1000, len(rk)).astype(np.int32)
+    p = NL.JoinParams()
+    cl = [_col(pa.array(lk, mask=lnull), device), _col(pa.array(ldate), device),
+          _col(pa.array(lprice), device)]
+    cr = [_col(pa.array(rk, mask=rnull), device), _col(pa.array(rdate), device)]
+    for i, c in enumerate(cl):
+        p.cols[i] = c.desc()
+    for i, c in enumerate(cr):
+        p.cols[8 + i] = c.desc()
+    p.preds[0] = NL.Pred(NL.PK_INT_LIT, NL.OP_GT, 1, 0, 0, 0, 250, 0.0, None)
+    p.preds[1] = NL.Pred(NL.PK_INT_LIT, NL.OP_LT, 9, 0, 1, 0, 600, 0.0, None)
+    p.nlp, p.npreds = 1, 2
+    p.aggs[0] = _agg(NL.AK_SUM, [(2, 0.0, 1.0)])
+    p.aggs[1] = _agg(NL.AK_COUNT_STAR)
+    p.naggs, p.lkey, p.rkey, p.key_is_float = 2, 0, 8, 0
+    p.group_col, p.num_groups, p.group_base = -1, 1, 0
+    # oracle over sub-ranges of every bucket (unaligned starts)
+    starts = loff[:-1] + 3
+    lens = np.maximum(loff[1:] - starts - 5, 0)
+    exp_sum, exp_cnt = 0.0, 0
+    for b in range(B):
+        rows = np.arange(starts[b], starts[b] + lens[b])
+        rsel = np.arange(roff[b], roff[b + 1])
+        rsel = rsel[(~rnull[rsel]) & (rdate[rsel] < 600)]
+        cnt = {}
+        for k in rk[rsel]:
+            cnt[k] = cnt.get(k, 0) + 1
+        for i in rows:
+            if lnull[i] or ldate[i] <= 250:
+                continue
+            c = cnt.get(lk[i], 0)
+            exp_cnt += c
+            exp_sum += c * lprice[i]
+    rstart = torch.from_numpy(starts.astype(np.int64)).to(device)
+    rlen = torch.from_numpy(lens.astype(np.int64)).to(device)
+    rbk = torch.arange(B, dtype=torch.int32, device=device)
+    roff_t = torch.from_numpy(roff).to(device)
+    from hyperspace_amd.exec.encoding import encode
+    allc = dict(enumerate(cl))
+    allc.update({8 + i: c for i, c in enumerate(cr)})
+    comp = {s: e for s, e in ((s, encode(c)) for s, c in allc.items()) if e is not None}
+    lds_keys = jit.MJ_LDS_KEYS
+    try:
+        for keys in (lds_keys, 32):
+            jit.MJ_LDS_KEYS = keys
+            for cmp in (None, comp):
+                got = [t.cpu().numpy() for t in
+                       jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, cmp, nrows=len(lk))]
+                assert got[1][1] == exp_cnt and got[1][0] == exp_cnt, (keys, got[1], exp_cnt)
+                assert abs(got[0][0] - exp_sum) <= 1e-9 * max(1.0, exp_sum)
+    finally:
+        jit.MJ_LDS_KEYS = lds_keys
 
 
 def test_code_bounds_match_value_compares():
