@@ -86,7 +86,7 @@ def build_runtime(force: bool = False) -> str:
     # host-only C++ against the HIP runtime + hipRTC (whole-stage codegen); hipcc supplies the
     # platform defines and include paths
     _run([_hipcc(), "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", tmp] + srcs +
-         [f"-L{rocm}/lib", "-lhiprtc", "-lamdhip64", "-ldl", f"-Wl,-rpath,{rocm}/lib"])
+         [f"-L{rocm}/lib", "-lhiprtc", "-lamdhip64", "-ldl", "-lz", f"-Wl,-rpath,{rocm}/lib"])
     os.replace(tmp, RUNTIME_LIB)
     return RUNTIME_LIB
 

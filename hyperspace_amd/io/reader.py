@@ -166,7 +166,8 @@ def read_one(fmt: str, local_path: str, schema: Optional[pa.Schema], options: di
             lines = f.read().splitlines()
         t = pa.table({"value": pa.array(lines, pa.string())})
     elif fmt == "avro":
-        raise HyperspaceException("avro support requires fastavro, which is not installed")
+        from .avro import read_avro
+        t = read_avro(local_path)
     else:
         raise HyperspaceException(f"unsupported format {fmt}")
     if schema is not None:
@@ -308,6 +309,9 @@ class DataFrameReader:
 
     def orc(self, *paths):
         return self.format("orc").load(*paths)
+
+    def avro(self, *paths):
+        return self.format("avro").load(*paths)
 
     def text(self, *paths):
         return self.format("text").load(*paths)
