@@ -24,6 +24,7 @@ caller reads just those with pyarrow.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import threading
 from typing import Dict, List, Optional, Sequence, Set
 
@@ -93,10 +94,14 @@ def lib():
                                                  C.POINTER(C.c_int64)]),
                         ("hs_pq_chunk_host_bound", I64, [P, I, I]),
                         ("hs_pq_page_size", I, []),
-                        ("hs_pq_snappy_decompress", I64, [P, I64, P, I64])):
+                        ("hs_pq_snappy_decompress", I64, [P, I64, P, I64]),
+                        ("hs_pq_set_host_inflate", None, [I])):
                     fn = getattr(L, name)
                     fn.restype = res
                     fn.argtypes = args
+                # HS_PQ_HOST_INFLATE: which Snappy pages the planner inflates on the host
+                # (0 none, 1 large dictionaries, 2 + tag-dense data pages)
+                L.hs_pq_set_host_inflate(int(os.environ.get("HS_PQ_HOST_INFLATE", "2")))
                 if L.hs_pq_run_size() != RUN_DTYPE.itemsize or \
                         L.hs_pq_info_size() != C.sizeof(ChunkInfo) or \
                         L.hs_pq_page_size() != PAGE_DTYPE.itemsize:
