@@ -18,9 +18,11 @@ against the same query with Hyperspace disabled (the reference's correctness ora
   refreshed index.
 * ``q3_3way`` — the TPC-H Q3 three-way join customer ⋈ orders ⋈ lineitem (JoinIndexRule on the
   customer/orders join, device shuffle of the intermediate onto the lineitem index layout).
-  This stands in for BASELINE config #5 (TPC-DS SF300 three-way join): no TPC-DS generator is
-  available offline, and Q3 has the same shape — fact ⋈ dimension ⋈ dimension with an
-  intermediate re-partition.
+* ``tpcds_3way`` — BASELINE config #5: TPC-DS-shaped ``store_sales`` ⋈ ``item`` ⋈ ``date_dim``
+  (``hyperspace_amd.models.tpcds``, SF300 = 864M fact rows by default, ``--tpcds-sf``) with
+  covering indexes on all three tables; queries, then +10% appended fact files and an
+  incremental ``refreshIndex``, then the same queries on the refreshed index.  Results are
+  checked against an independent pyarrow-dataset computation (not this engine's host path).
 """
 import argparse
 import datetime
@@ -318,8 +320,95 @@ def config_q3_3way(args):
             "path": path, "fallback_reason": reason, "match": _close(got, ref)}
 
 
+# ------------------------------------------------------------------------------------ TPC-DS
+def _tpcds_query(ss, it, dd, i):
+    """TPC-DS Q3-shaped star join: one manufacturer's items sold in one month of the year."""
+    from hyperspace_amd import col, count, sum_
+    m, moy = 1 + (i * 37) % 1000, 1 + i % 12
+    items = it.filter(col("i_manufact_id") == m)
+    days = dd.filter(col("d_moy") == moy)
+    j = ss.join(items, ss["ss_item_sk"] == items["i_item_sk"])
+    j = j.join(days, j["ss_sold_date_sk"] == days["d_date_sk"])
+    return j.agg(sum_(col("ss_ext_sales_price")).alias("sales"), count("*").alias("lines"))
+
+
+def _tpcds_oracle(paths, i):
+    """The query computed independently with pyarrow datasets (filter pushdown, no join)."""
+    import pyarrow.compute as pc
+    import pyarrow.dataset as ds
+    import pyarrow.parquet as pq
+    m, moy = 1 + (i * 37) % 1000, 1 + i % 12
+    it = pq.read_table(paths["item"], columns=["i_item_sk", "i_manufact_id"])
+    items = it.filter(pc.equal(it["i_manufact_id"], m))["i_item_sk"]
+    dd = pq.read_table(paths["date_dim"], columns=["d_date_sk", "d_moy"])
+    days = dd.filter(pc.equal(dd["d_moy"], moy))["d_date_sk"]
+    t = ds.dataset(paths["store_sales"], format="parquet").to_table(
+        columns=["ss_ext_sales_price"],
+        filter=ds.field("ss_item_sk").isin(items) & ds.field("ss_sold_date_sk").isin(days))
+    return [(float(pc.sum(t["ss_ext_sales_price"]).as_py() or 0.0), t.num_rows)]
+
+
+def config_tpcds_3way(args):
+    from hyperspace_amd import Hyperspace, IndexConfig
+    from hyperspace_amd.models import tpcds
+    sf = args.tpcds_sf
+    nfiles = max(4, int(round(sf * 1.28)))
+    data = os.path.join(args.data_dir, f"tpcds_sf{sf:g}_f{nfiles}")
+    tg = time.perf_counter()
+    tpcds.generate(data, sf, nfiles, workers=min(16, os.cpu_count() or 8))
+    gen_s = time.perf_counter() - tg
+    work = os.path.join(args.data_dir, f"cfg_tpcds_sf{sf:g}")
+    shutil.rmtree(work, ignore_errors=True)
+    for t in ("store_sales", "item", "date_dim"):       # private links: appends stay local
+        os.makedirs(os.path.join(work, "data", t))
+        for f in os.listdir(os.path.join(data, t)):
+            os.link(os.path.join(data, t, f), os.path.join(work, "data", t, f))
+    paths = {t: os.path.join(work, "data", t) for t in ("store_sales", "item", "date_dim")}
+    s = _session(work, args.device, args.buckets)
+    hs = Hyperspace(s)
+    ss, it, dd = (s.read.parquet(paths[t]) for t in ("store_sales", "item", "date_dim"))
+    builds = {}
+    for df, cfg in ((ss, IndexConfig("ss_item", ["ss_item_sk"],
+                                     ["ss_sold_date_sk", "ss_ext_sales_price"])),
+                    (it, IndexConfig("item_idx", ["i_item_sk"], ["i_manufact_id"])),
+                    (dd, IndexConfig("date_idx", ["d_date_sk"], ["d_moy"]))):
+        builds[cfg.indexName] = round(_build(hs, df, cfg, args.device)[0], 3)
+    Hyperspace.enable(s)
+    k = max(3, args.steps)
+
+    def run_queries(tag):
+        ss_, it_, dd_ = (s.read.parquet(paths[t]) for t in ("store_sales", "item", "date_dim"))
+        plan = _tpcds_query(ss_, it_, dd_, 0).queryExecution.executed_plan.tree_string()
+        for i in range(2):
+            _tpcds_query(ss_, it_, dd_, 1000 + i).collect()
+        el = _timed_loop(lambda i: _tpcds_query(ss_, it_, dd_, i).collect(), k, args.device)
+        got = _rows(_tpcds_query(ss_, it_, dd_, 0))
+        ref = _tpcds_oracle(paths, 0)
+        return {f"{tag}_queries_per_s": round(k / el, 3), f"{tag}_query_ms": round(el / k * 1e3, 2),
+                f"{tag}_match": _close(got, ref), f"{tag}_lines": got[0][1] if got else None,
+                f"{tag}_indexes_in_plan": [n for n in ("ss_item", "item_idx", "date_idx")
+                                           if n in plan],
+                f"{tag}_path": getattr(s.backend(), "last_path", None)}
+    out = {"config": "tpcds_3way", "device": args.device, "sf": sf,
+           "store_sales_rows": tpcds.store_sales_rows(sf), "source_files": nfiles,
+           "datagen_s": round(gen_s, 2), "index_build_s": builds}
+    out.update(run_queries("base"))
+    # +10% fact rows: new files with the same domains, then an incremental refresh
+    extra = max(1, nfiles // 10)
+    tpcds.write_store_sales_files(os.path.join(work, "data"), sf, nfiles, first=nfiles,
+                                  count=extra, workers=min(16, os.cpu_count() or 8))
+    _sync(args.device)
+    tr = time.perf_counter()
+    hs.refreshIndex("ss_item", "incremental")
+    _sync(args.device)
+    out["appended_files"] = extra
+    out["incremental_refresh_s"] = round(time.perf_counter() - tr, 3)
+    out.update(run_queries("refreshed"))
+    return out
+
+
 CONFIGS = {"csv10k": config_csv10k, "sf10_filter": config_sf10_filter, "hybrid": config_hybrid,
-           "q3_3way": config_q3_3way}
+           "q3_3way": config_q3_3way, "tpcds_3way": config_tpcds_3way}
 
 
 def main():
@@ -330,6 +419,7 @@ def main():
     ap.add_argument("--buckets", type=int, default=200)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--data-dir", default=os.environ.get("HS_BENCH_DIR", "/tmp/hs_bench"))
+    ap.add_argument("--tpcds-sf", type=float, default=300.0)
     args = ap.parse_args()
     if args.device == "gpu":
         import torch
