@@ -98,6 +98,126 @@ def _sort_and_write(session, table: Dict[str, DeviceColumn], names: List[str], b
     return paths
 
 
+# decoded source bytes x this = HBM a one-pass build peaks at: source columns, bucket ids, sort
+# keys and permutation (radix_sort.hip), and the gathered bucket-major copy
+BUILD_SORT_FACTOR = 3.0
+
+
+def plan_passes(est_bytes: int, budget: int, num_buckets: int) -> List[tuple]:
+    """Bucket ranges [lo, hi) of a streaming build: one range when ``est_bytes`` fits the
+    budget, else ceil(est / budget) contiguous ranges of (near) equal bucket counts (Murmur3
+    spreads rows evenly over buckets), at most one bucket each."""
+    passes = 1 if budget <= 0 or est_bytes <= budget else -(-int(est_bytes) // int(budget))
+    passes = max(1, min(int(num_buckets), passes))
+    edges = np.linspace(0, num_buckets, passes + 1).round().astype(int)
+    return [(int(a), int(b)) for a, b in zip(edges[:-1], edges[1:]) if b > a]
+
+
+def plan_file_groups(rows: List[int], row_bytes: int, group_budget: int) -> List[tuple]:
+    """Consecutive file ranges [a, b) whose decoded bytes stay within ``group_budget`` (a
+    single file larger than that is a group of its own)."""
+    groups, a, acc = [], 0, 0
+    for i, r in enumerate(rows):
+        b = int(r) * int(row_bytes)
+        if i > a and acc + b > group_budget:
+            groups.append((a, i))
+            a, acc = i, 0
+        acc += b
+    if a < len(rows):
+        groups.append((a, len(rows)))
+    return groups
+
+
+def _build_budget(session, device) -> int:
+    b = HyperspaceConf.build_hbm_budget_bytes(session.conf)
+    if b > 0:
+        return b
+    import torch
+    free, _ = torch.cuda.mem_get_info(device)
+    return int(free * 0.6)
+
+
+def _streaming_plan(session, rel, my_files, columns, lineage_ids, num_buckets, device, world):
+    """(passes, file groups, row bytes) when this rank's build does not fit the HBM budget
+    (``spark.hyperspace.mi.build.hbmBudgetBytes``), else None.  Streaming covers single-rank
+    Parquet builds of fixed-width columns (string dictionaries are built over the whole input
+    in one pass)."""
+    if world > 1 or source_format(rel) != "parquet" or not my_files:
+        return None
+    from ..io.reader import output_schema
+    from .device_table import storage_numpy_dtype
+    schema = output_schema(rel.data_schema, rel.location.partition_spec, columns)
+    if any(is_string(f.type) for f in schema):
+        return None
+    from . import staging
+    infos = list(staging.io_pool().map(lambda f: _footer_info(f, list(schema.names)), my_files))
+    rows = [r for r, _ in infos]
+    row_bytes = sum(storage_numpy_dtype(f.type).itemsize + 1 for f in schema) + \
+        (8 if lineage_ids is not None else 0) + 4
+    est = int(sum(rows) * row_bytes * BUILD_SORT_FACTOR)
+    budget = _build_budget(session, device)
+    passes = plan_passes(est, budget, num_buckets)
+    if len(passes) <= 1:
+        return None
+    return passes, plan_file_groups(rows, row_bytes, max(budget // 4, 1)), row_bytes
+
+
+def _streaming_build(session, rel, my_files, columns, indexed, num_buckets, out_path,
+                     lineage_ids, device, plan, rank) -> List[str]:
+    """Build in bucket-range passes: each pass re-decodes the source file group by group,
+    hashes every row and keeps only its buckets' rows (in source order), then sorts and writes
+    those buckets.  Rows of a bucket meet the stable sort in the one-pass build's order, so the
+    bucket files are byte-identical to a one-pass build's; HBM holds one decoded file group plus
+    one pass's rows instead of the whole input."""
+    import torch
+    passes, groups, _ = plan
+    paths: List[str] = []
+    t0 = time.perf_counter()
+    decode_s = sort_s = 0.0
+    source_bytes = 0
+    schema = names = None
+    for pi, (lo, hi) in enumerate(passes):
+        parts: Dict[str, list] = {}
+        buckets = []
+        for a, b in groups:
+            td = time.perf_counter()
+            cols, names, schema = _upload_parquet(rel, my_files[a:b], columns, indexed,
+                                                  lineage_ids, device, None)
+            if pi == 0:
+                source_bytes += sum(c.nbytes() for c in cols.values())
+            bucket, _ = K.murmur3_bucket([cols[c] for c in indexed], num_buckets,
+                                         with_counts=False)
+            keep = torch.nonzero((bucket >= lo) & (bucket < hi)).squeeze(1)
+            got = K.gather_columns([cols[n] for n in names], keep)
+            for n, c in zip(names, got):
+                parts.setdefault(n, []).append(c)
+            buckets.append(bucket.index_select(0, keep))
+            del cols, bucket, keep, got
+            torch.cuda.synchronize()
+            decode_s += time.perf_counter() - td
+        ts = time.perf_counter()
+        table = {}
+        for n in names:
+            cs = parts[n]
+            data = torch.cat([c.data for c in cs])
+            valid = None
+            if any(c.valid is not None for c in cs):
+                valid = torch.cat([c.valid if c.valid is not None else
+                                   torch.ones(c.data.shape[0], dtype=torch.uint8, device=device)
+                                   for c in cs])
+            table[n] = DeviceColumn(data, valid, cs[0].atype, cs[0].dictionary)
+        del parts
+        paths += _sort_and_write(session, table, names, torch.cat(buckets), indexed,
+                                 num_buckets, out_path, schema, rank)
+        del table, buckets
+        sort_s += time.perf_counter() - ts
+    LAST_BUILD_STATS.update({"passes": len(passes), "file_groups": len(groups),
+                             "source_bytes": source_bytes,
+                             "pass_decode_s": decode_s, "pass_sort_write_s": sort_s,
+                             "total_s": time.perf_counter() - t0})
+    return paths
+
+
 def device_build_from_source(session, rel, files: List[str], columns: List[str], indexed: List[str],
                              num_buckets: int, out_path: str, lineage_ids: Optional[Dict[str, int]],
                              mode: str = "overwrite") -> List[str]:
@@ -115,6 +235,12 @@ def device_build_from_source(session, rel, files: List[str], columns: List[str],
     from ..io import native_parquet
     native_parquet.PHASES.clear()
     xs = _BatchedExchange(dist, num_buckets, indexed) if world > 1 else None
+    LAST_BUILD_STATS.clear()
+    splan = _streaming_plan(session, rel, my_files, columns, lineage_ids, num_buckets, device,
+                            world)
+    if splan is not None:
+        return _streaming_build(session, rel, my_files, columns, indexed, num_buckets, out_path,
+                                lineage_ids, device, splan, rank)
     if fmt == "parquet":
         cols, names, schema = _upload_parquet(rel, my_files, columns, indexed, lineage_ids,
                                               device, dist, xs)

@@ -122,4 +122,8 @@ PLAN_CACHE_ENABLED_DEFAULT = "true"
 # kept in torch's caching allocator so builds and queries do not hipMalloc multi-GB columns
 HBM_RESERVE_BYTES = "spark.hyperspace.mi.hbmReserveBytes"
 HBM_RESERVE_BYTES_DEFAULT = str(64 * 1024 ** 3)
+# HBM an index build may use (decoded source + sort workspace); a build whose estimate exceeds
+# it runs in bucket-range passes (exec/device_build.py).  0 = 60% of the free HBM at build time.
+BUILD_HBM_BUDGET_BYTES = "spark.hyperspace.mi.build.hbmBudgetBytes"
+BUILD_HBM_BUDGET_BYTES_DEFAULT = "0"
 FAULT_INJECTION = "spark.hyperspace.mi.faultInjection"

@@ -134,6 +134,10 @@ class HyperspaceConf:
         return int(conf.get(C.HBM_RESERVE_BYTES, C.HBM_RESERVE_BYTES_DEFAULT))
 
     @staticmethod
+    def build_hbm_budget_bytes(conf) -> int:
+        return int(conf.get(C.BUILD_HBM_BUDGET_BYTES, C.BUILD_HBM_BUDGET_BYTES_DEFAULT))
+
+    @staticmethod
     def plan_cache_enabled(conf) -> bool:
         return _b(conf.get(C.PLAN_CACHE_ENABLED, C.PLAN_CACHE_ENABLED_DEFAULT))
 

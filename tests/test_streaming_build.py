@@ -1,0 +1,71 @@
+"""HBM-budgeted streaming index build (the reference scales builds by bucket count
+and streaming tasks, docs/_docs/04-ug-faqs.md:107-132): the pass / file-group planner on the
+CPU, and on the GPU a build forced into many bucket-range passes whose bucket files are
+byte-identical to the one-pass build's."""
+import os
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.parquet as pq
+import pytest
+
+from hyperspace_amd.exec.device_build import plan_file_groups, plan_passes
+
+
+def test_plan_passes_cover_buckets_contiguously():
+    assert plan_passes(100, 1000, 200) == [(0, 200)]
+    assert plan_passes(100, 0, 200) == [(0, 200)]          # 0 = no budget
+    p = plan_passes(10_000, 1_000, 200)
+    assert len(p) == 10 and p[0][0] == 0 and p[-1][1] == 200
+    assert all(a[1] == b[0] for a, b in zip(p, p[1:]))
+    assert {hi - lo for lo, hi in p} == {20}
+    p = plan_passes(10 ** 12, 1, 7)                          # at most one bucket per pass
+    assert p == [(i, i + 1) for i in range(7)]
+    p = plan_passes(2_500, 1_000, 10)
+    assert len(p) == 3 and sum(hi - lo for lo, hi in p) == 10
+
+
+def test_plan_file_groups_respect_budget():
+    assert plan_file_groups([10, 10, 10], 4, 1_000) == [(0, 3)]
+    assert plan_file_groups([10, 10, 10, 10], 10, 250) == [(0, 2), (2, 4)]
+    assert plan_file_groups([100, 1, 1], 10, 50) == [(0, 1), (1, 3)]   # oversized file alone
+    assert plan_file_groups([], 8, 10) == []
+
+
+@pytest.mark.gpu
+def test_streaming_build_is_byte_identical(tmp_path, device):
+    from hyperspace_amd import Hyperspace, IndexConfig, Session
+    from hyperspace_amd.exec import device_build
+    rng = np.random.default_rng(3)
+    src = tmp_path / "src"
+    src.mkdir()
+    for i in range(5):
+        n = 40_000 + 1_000 * i
+        t = pa.table({"k": pa.array(rng.integers(0, 5_000, n)),           # many equal keys
+                      "d": pa.array(rng.integers(8000, 11000, n).astype(np.int32)),
+                      "p": pa.array(np.round(rng.random(n) * 1e4, 2)),
+                      "q": pa.array(np.where(rng.random(n) < 0.1, None,
+                                             rng.integers(0, 50, n)).tolist(), pa.int64())})
+        pq.write_table(t, src / f"part-{i}.parquet", row_group_size=16_000)
+
+    def build(name, budget):
+        s = Session(conf={"spark.hyperspace.system.path": str(tmp_path / "ix"),
+                          "spark.hyperspace.index.numBuckets": "16",
+                          "spark.hyperspace.mi.execution.device": "gpu",
+                          "spark.hyperspace.mi.build.hbmBudgetBytes": str(budget)},
+                    warehouse_dir=str(tmp_path / "wh"))
+        Hyperspace(s).createIndex(s.read.parquet(str(src)), IndexConfig(name, ["k"], ["d", "p", "q"]))
+        stats = dict(device_build.LAST_BUILD_STATS)
+        files = {}
+        for root, _, fs in os.walk(tmp_path / "ix" / name):
+            for f in fs:
+                if f.endswith(".parquet"):
+                    b = int(f.split("_")[-1].split(".")[0])
+                    files[b] = open(os.path.join(root, f), "rb").read()
+        return files, stats
+    one, s1 = build("one_pass", 1 << 40)
+    many, s2 = build("streamed", 600_000)
+    assert "passes" not in s1 and s2["passes"] >= 4 and s2["file_groups"] >= 2, s2
+    assert sorted(one) == sorted(many) and len(one) == 16
+    for b in one:
+        assert one[b] == many[b], f"bucket {b} differs"
