@@ -48,14 +48,24 @@ class CpuBackend:
 
     # -- public -------------------------------------------------------------------------------
     def collect(self, plan: X.SparkPlan) -> pa.Table:
-        parts = self.execute(plan)
+        self._reuse_memo = {}
+        try:
+            parts = self.execute(plan)
+        finally:
+            self._reuse_memo = {}
         t = _concat(parts, plan.output)
         self.last_path = "host"
         return pa.Table.from_arrays(t.columns, names=[a.name for a in plan.output])
 
     def execute(self, p: X.SparkPlan) -> List[pa.Table]:
         fn = getattr(self, "_exec_" + type(p).__name__)
-        return fn(p)
+        memo = getattr(self, "_reuse_memo", None)
+        if memo is None or not isinstance(p, (X.ShuffleExchangeExec, X.BroadcastExchangeExec)):
+            return fn(p)
+        hit = memo.get(id(p))
+        if hit is None or hit[0] is not p:
+            hit = memo[id(p)] = (p, fn(p))
+        return hit[1]
 
     # -- scans ----------------------------------------------------------------------------------
     def _read(self, p: X.FileSourceScanExec, files: List[str]) -> pa.Table:
@@ -140,6 +150,11 @@ class CpuBackend:
         if isinstance(part, X.HashPartitioning):
             return self._hash_partition(t, part.expressions, part.num_partitions)
         return [t]
+
+    def _exec_ReusedExchangeExec(self, p):
+        # the reused exchange runs once per query; its partitions are renamed positionally
+        names = [key(a) for a in p.output]
+        return [t.rename_columns(names) for t in self.execute(p.exchange)]
 
     def _exec_BroadcastExchangeExec(self, p):
         return [_concat(self.execute(p.child), p.child.output)]

@@ -207,6 +207,10 @@ class GpuBackend:
             return self._repartition(self._rel(p.child), p.partitioning)
         if isinstance(p, X.SortMergeJoinExec):
             return self._join_rel(p)
+        if isinstance(p, X.ReusedExchangeExec):
+            # the device repartition of a resident table is cached, so the original subtree
+            # replays the first exchange's result
+            return self._rel(p.equivalent)
         raise Unsupported(f"operator {p.node_name}")
 
     def _bucket_union(self, p: X.BucketUnionExec) -> DRel:

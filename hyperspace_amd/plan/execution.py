@@ -4,7 +4,7 @@ from __future__ import annotations
 import pyarrow as pa
 
 from .optimizer import Optimizer
-from .physical import Planner, ensure_requirements
+from .physical import Planner, ensure_requirements, reuse_exchanges
 
 
 class QueryExecution:
@@ -47,7 +47,8 @@ class QueryExecution:
                 if plan is not None:
                     self._executed = plan
                     return plan
-            self._executed = ensure_requirements(self.spark_plan, self.session)
+            self._executed = reuse_exchanges(ensure_requirements(self.spark_plan, self.session),
+                                             self.session)
             if pc is not None:
                 pc.store(key, self._executed, ctx)
         return self._executed

@@ -13,6 +13,7 @@ need neither (ExplainTest.scala:142-172: ShuffleExchange 1->0, Sort 2->0).
 """
 from __future__ import annotations
 
+import re
 from typing import List, Optional
 
 import pyarrow as pa
@@ -337,6 +338,44 @@ class ShuffleExchangeExec(UnaryExec):
         if isinstance(self.partitioning, HashPartitioning):
             return f"Exchange {self.partitioning.sql()}"
         return "Exchange SinglePartition"
+
+
+class ReusedExchangeExec(SparkPlan):
+    """Leaf standing for an exchange whose result another, identical exchange of the same plan
+    already produces (Spark's ``ReuseExchange`` rule; golden: ``ExplainTest.scala:142-172``,
+    ``ReusedExchange [Col1#21, Col2#22], Exchange hashpartitioning(Col1#11, 5)``).
+
+    ``exchange`` is the reused node (its output attributes map positionally onto ``output``);
+    ``equivalent`` is the original subtree this leaf replaced, for a backend that prefers to
+    execute it instead of sharing the result."""
+
+    def __init__(self, output: List[E.Attribute], exchange: SparkPlan, equivalent: SparkPlan):
+        self._output = list(output)
+        self.exchange = exchange
+        self.equivalent = equivalent
+
+    @property
+    def output(self):
+        return self._output
+
+    @property
+    def node_name(self):
+        return "ReusedExchange"
+
+    @property
+    def output_partitioning(self):
+        return self.equivalent.output_partitioning
+
+    @property
+    def output_ordering(self):
+        return self.equivalent.output_ordering
+
+    def with_children(self, children):
+        return self
+
+    def simple_string(self):
+        return (f"ReusedExchange [{', '.join(a.sql() for a in self._output)}], "
+                f"{self.exchange.simple_string()}")
 
 
 class BroadcastExchangeExec(UnaryExec):
@@ -753,6 +792,54 @@ def ensure_requirements(plan: SparkPlan, session) -> SparkPlan:
         if isinstance(p, BucketUnionExec):
             return None
         return None
+    return plan.transform_up(fn)
+
+
+_EXPR_ID = re.compile(r"#(\d+)")
+
+
+def canonical_string(plan: SparkPlan) -> str:
+    """Expression-id-free rendering of a subtree: ids are renumbered by first appearance, so
+    two subtrees that differ only in the ids of their (deduplicated self-join) attributes
+    render identically (the role of Spark's ``QueryPlan.canonicalized``)."""
+    seen: dict = {}
+
+    def sub(m):
+        return "#" + str(seen.setdefault(m.group(1), len(seen)))
+
+    lines = []
+    for prefix, node in plan.tree_lines():
+        s = prefix + node.simple_string()
+        # leaves carry their data identity: local rows by object, scans by their file list
+        if isinstance(node, LocalTableScanExec):
+            s += f" @{id(node.table)}"
+        elif isinstance(node, FileSourceScanExec):
+            s += f" @{hash(tuple(sorted(repr(f) for f in node.relation.location.all_files())))}"
+            s += f" {sorted(node.selected_buckets) if node.selected_buckets else ''}"
+        lines.append(s)
+    return _EXPR_ID.sub(sub, "\n".join(lines))
+
+
+def reuse_exchanges(plan: SparkPlan, session) -> SparkPlan:
+    """Spark's ``ReuseExchange``: the second and later exchanges whose canonical subtrees equal
+    an earlier one become ``ReusedExchange`` leaves (``spark.sql.exchange.reuse``, default
+    true).  Index scans of a bucketed self-join have no exchange left to reuse."""
+    v = str(session.conf.get("spark.sql.exchange.reuse", "true")).lower()
+    if v != "true":
+        return plan
+    seen: dict = {}
+
+    def fn(p):
+        if not isinstance(p, (ShuffleExchangeExec, BroadcastExchangeExec)):
+            return None
+        k = (type(p).__name__, canonical_string(p))
+        first = seen.get(k)
+        if first is None:
+            seen[k] = p
+            return None
+        if len(first.output) != len(p.output):
+            return None
+        return ReusedExchangeExec(p.output, first, p)
     return plan.transform_up(fn)
 
 

@@ -122,9 +122,29 @@ def test_explain_verbose_join_operator_stats(tmp_path):
         parts = [p.strip() for p in line.strip("|").split("|")]
         if len(parts) == 4 and parts[0] and parts[1].lstrip("-").isdigit():
             rows[parts[0]] = tuple(int(x) for x in parts[1:])
-    assert rows["ShuffleExchange"] == (2, 0, -2)
+    # ExplainTest.scala:142-172: the self-join's second exchange is a ReusedExchange
+    assert rows["ShuffleExchange"] == (1, 0, -1)
+    assert rows["ReusedExchange"] == (1, 0, -1)
     assert rows["Sort"] == (2, 0, -2)
     assert rows["SortMergeJoin"] == (1, 1, 0)
+    assert "ReusedExchange [RGUID#" in text and "], Exchange hashpartitioning(RGUID#" in text
+
+
+def test_reused_exchange_self_join_results(tmp_path):
+    s = make_session(tmp_path)
+    src = str(tmp_path / "src")
+    write_parquet_parts(sample_table(), src, 2)
+    a = s.read.parquet(src)
+    b = s.read.parquet(src)
+    q = a.join(b, a["RGUID"] == b["RGUID"]).select(a["clicks"], b["clicks"])
+    plan = q.queryExecution.executed_plan
+    assert len(plan.collect(lambda p: isinstance(p, X.ReusedExchangeExec))) == 1
+    got = sorted(tuple(r) for r in q.collect())
+    s.conf.set("spark.sql.exchange.reuse", "false")
+    q2 = a.join(b, a["RGUID"] == b["RGUID"]).select(a["clicks"], b["clicks"])
+    assert not q2.queryExecution.executed_plan.collect(
+        lambda p: isinstance(p, X.ReusedExchangeExec))
+    assert got == sorted(tuple(r) for r in q2.collect())
 
 
 def test_explain_html_mode(tmp_path):
