@@ -66,13 +66,25 @@ struct HsPqWCol {
   int64_t dict_count;
   const uint8_t* payload;    // PLAIN values or packed codes (ceil(n/8)*bit_width bytes)
   int64_t payload_bytes;
+  // codec 1 (SNAPPY): dict_page is a whole Snappy stream of dict_raw_bytes; payload holds the
+  // Snappy elements (no length preamble) of payload_raw_bytes encoded bytes, compressed on the
+  // device (csrc/kernels/snappy_encode.hip)
+  int64_t dict_raw_bytes;
+  int64_t payload_raw_bytes;
+  int32_t codec;             // 0 UNCOMPRESSED, 1 SNAPPY
+  int32_t pad;
 };
 
 namespace {
 
 struct ColPos {
-  int64_t dict_off = -1, data_off = 0, total = 0;
+  int64_t dict_off = -1, data_off = 0, total = 0, raw_total = 0;
 };
+
+void put_varint(std::vector<uint8_t>& v, uint64_t x) {
+  while (x >= 0x80) { v.push_back((uint8_t)(x | 0x80)); x >>= 7; }
+  v.push_back((uint8_t)x);
+}
 
 void def_levels_all_valid(std::vector<uint8_t>& v, int64_t n) {
   // 4-byte length prefix + one RLE run (header (n << 1), value 1 in one byte)
@@ -86,11 +98,12 @@ void def_levels_all_valid(std::vector<uint8_t>& v, int64_t n) {
   v.insert(v.end(), run.begin(), run.end());
 }
 
-std::vector<uint8_t> page_header(int type, int64_t size, int64_t nvals, int enc) {
+std::vector<uint8_t> page_header(int type, int64_t size, int64_t nvals, int enc,
+                                 int64_t raw_size = -1) {
   TWriter w;
   w.i32(1, type);
-  w.i32(2, size);
-  w.i32(3, size);
+  w.i32(2, raw_size < 0 ? size : raw_size);   // uncompressed_page_size
+  w.i32(3, size);                             // compressed_page_size
   if (type == 2) {
     w.begin_struct(7);
     w.i32(1, nvals);
@@ -155,12 +168,15 @@ int hs_pq_write_file(const char* path, int ncols, int nrg, const int64_t* rg_row
       const HsPqWCol& col = cols[(size_t)g * ncols + c];
       ColPos& p = posv[(size_t)g * ncols + c];
       const int64_t start = off;
+      const bool snappy = col.codec == 1;
       if (col.dict) {
-        keep.push_back(page_header(2, col.dict_bytes, col.dict_count, 0));
+        const int64_t raw = snappy ? col.dict_raw_bytes : col.dict_bytes;
+        keep.push_back(page_header(2, col.dict_bytes, col.dict_count, 0, raw));
         p.dict_off = off;
         iov.push_back({keep.back().data(), keep.back().size()});
         iov.push_back({(void*)col.dict_page, (size_t)col.dict_bytes});
         off += (int64_t)keep.back().size() + col.dict_bytes;
+        p.raw_total += (int64_t)keep.back().size() + raw;
       }
       std::vector<uint8_t> pre;
       def_levels_all_valid(pre, n);
@@ -170,11 +186,23 @@ int hs_pq_write_file(const char* path, int ncols, int nrg, const int64_t* rg_row
         while (h >= 0x80) { pre.push_back((uint8_t)(h | 0x80)); h >>= 7; }
         pre.push_back((uint8_t)h);
       }
+      int64_t raw_psize = (int64_t)pre.size() + col.payload_bytes;
+      if (snappy) {
+        // Snappy stream: varint(uncompressed size), the levels/width prefix as one literal
+        // element, then the device-compressed elements of the payload
+        raw_psize = (int64_t)pre.size() + col.payload_raw_bytes;
+        std::vector<uint8_t> z;
+        put_varint(z, (uint64_t)raw_psize);
+        z.push_back((uint8_t)((pre.size() - 1) << 2));   // prefix < 60 bytes
+        z.insert(z.end(), pre.begin(), pre.end());
+        pre.swap(z);
+      }
       const int64_t psize = (int64_t)pre.size() + col.payload_bytes;
-      keep.push_back(page_header(0, psize, n, col.dict ? 8 : 0));
+      keep.push_back(page_header(0, psize, n, col.dict ? 8 : 0, raw_psize));
       p.data_off = off;
       iov.push_back({keep.back().data(), keep.back().size()});
       off += (int64_t)keep.back().size();
+      p.raw_total += (int64_t)keep.back().size() + raw_psize;
       keep.push_back(std::move(pre));
       iov.push_back({keep.back().data(), keep.back().size()});
       if (col.payload_bytes) iov.push_back({(void*)col.payload, (size_t)col.payload_bytes});
@@ -217,7 +245,7 @@ int hs_pq_write_file(const char* path, int ncols, int nrg, const int64_t* rg_row
     for (int c = 0; c < ncols; ++c) {
       const HsPqWCol& col = cols[(size_t)g * ncols + c];
       const ColPos& p = posv[(size_t)g * ncols + c];
-      rg_bytes += p.total;
+      rg_bytes += p.raw_total;
       w.begin_anon_struct();                   // ColumnChunk
       w.i64(2, p.dict_off >= 0 ? p.dict_off : p.data_off);
       w.begin_struct(3);                       // ColumnMetaData
@@ -232,10 +260,10 @@ int hs_pq_write_file(const char* path, int ncols, int nrg, const int64_t* rg_row
       w.list(3, 8, 1);
       w.varint(strlen(col.name));
       w.bin(col.name);
-      w.i32(4, 0);                              // UNCOMPRESSED
+      w.i32(4, col.codec == 1 ? 1 : 0);         // SNAPPY / UNCOMPRESSED
       w.i64(5, rg_rows[g]);
-      w.i64(6, p.total);
-      w.i64(7, p.total);
+      w.i64(6, p.raw_total);                    // total_uncompressed_size
+      w.i64(7, p.total);                        // total_compressed_size
       w.i64(9, p.data_off);
       if (p.dict_off >= 0) w.i64(11, p.dict_off);
       w.end_struct();

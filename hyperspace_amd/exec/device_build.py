@@ -61,14 +61,20 @@ def _prepare_out_dir(out_path: str, mode: str, dist) -> None:
 
 def _sort_and_write(session, table: Dict[str, DeviceColumn], names: List[str], bucket,
                     indexed: List[str], num_buckets: int, out_path: str, schema: pa.Schema,
-                    task_id: int) -> List[str]:
+                    task_id: int, presorted: bool = False) -> List[str]:
+    """Sort rows by (bucket, indexed columns) and write one file per bucket.  ``presorted``:
+    the rows already are in that order (a rewrite of single sorted files per bucket), so no
+    sort or gather runs."""
     import torch
     n = int(bucket.numel())
     if n == 0:
         return []
     t0 = time.perf_counter()
-    perm = K.sort_permutation([table[c] for c in indexed], extra_leading=(bucket, 16))
-    gathered = K.gather_columns([table[c] for c in names], perm)
+    if presorted:
+        gathered = [table[c] for c in names]
+    else:
+        perm = K.sort_permutation([table[c] for c in indexed], extra_leading=(bucket, 16))
+        gathered = K.gather_columns([table[c] for c in names], perm)
     counts = K.histogram(bucket, num_buckets)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -78,7 +84,8 @@ def _sort_and_write(session, table: Dict[str, DeviceColumn], names: List[str], b
     job = str(uuid.uuid4())
     from . import staging
     paths = None
-    if codec in ("none", "uncompressed") and os.environ.get("HS_NATIVE_PQ_WRITE", "1") == "1":
+    if codec in ("none", "uncompressed", "snappy") and \
+            os.environ.get("HS_NATIVE_PQ_WRITE", "1") == "1":
         # K4 on the device: dictionary build + bit-packing in HIP, host only frames pages
         from . import pq_encode
         from ..io.writer import bucket_file_name
@@ -86,8 +93,8 @@ def _sort_and_write(session, table: Dict[str, DeviceColumn], names: List[str], b
         os.makedirs(local, exist_ok=True)
         paths = pq_encode.write_buckets(
             dict(zip(names, gathered)), names, schema, off,
-            lambda b: os.path.join(local, bucket_file_name(task_id, job, b, "none")), rg,
-            bucket.device)
+            lambda b: os.path.join(local, bucket_file_name(task_id, job, b, codec)), rg,
+            bucket.device, codec="none" if codec == "uncompressed" else codec)
     if paths is None:
         paths = staging.download_buckets(
             gathered, names, schema, off,
@@ -484,32 +491,49 @@ def _upload_generic(rel, files, my_files, columns, indexed, lineage_ids, device,
 
 def device_rewrite_buckets(session, files: List[str], indexed: List[str], out_path: str,
                            deleted_ids: Optional[List[int]], num_buckets: Optional[int]) -> List[str]:
-    """K5/K6 on the device: per-bucket merge (+ lineage bitmap filter) of existing index files."""
+    """K5/K6 on the device: rewrite this rank's buckets (``bucket % world == rank``) of existing
+    index files, dropping rows whose lineage id is deleted.
+
+    The files go through the same native page decode as a build (``staging.upload_files``); the
+    bucket id of every row is a per-file constant written by the lineage fill.  Rows arrive
+    bucket-major in file order.  When every bucket holds a single (sorted) file, a stable
+    compaction keeps that order, so the rows are written without any sort
+    (``RefreshIncrementalAction.scala:73-95``: deleted-file rows are filtered out of the old index
+    data); buckets with several files (``OptimizeAction.scala:85-99``) are merged by the stable
+    (bucket, indexed columns) radix sort."""
     import pyarrow.parquet as pq
     import torch
     dist = getattr(session, "dist", None)
     rank, world = (dist.rank, dist.world) if dist is not None else (0, 1)
     device = torch.device("cuda", torch.cuda.current_device())
     groups = group_by_bucket(files)
-    mine = sorted(b for b in groups if b >= 0 and b % world == rank)
-    paths_in = [f for b in mine for f in groups[b]]
     if -1 in groups:
         raise ValueError("index files without bucket ids")
+    mine = sorted(b for b in groups if b >= 0 and b % world == rank)
+    paths_in = [f for b in mine for f in groups[b]]
     if not paths_in:
         return []
-    tables, bucket_parts = [], []
-    for b in mine:
-        for f in groups[b]:
-            tt = pq.read_table(P.to_local(f))
-            tables.append(tt)
-            bucket_parts.append(np.full(tt.num_rows, b, np.int32))
-    bucket_np = np.concatenate(bucket_parts)
-    t = pa.concat_tables(tables)
-    schema = t.schema
-    names = t.column_names
-    dicts = _global_dicts(t, None)
-    cols = {n: DeviceColumn.from_arrow(t.column(n), device, dicts.get(n)) for n in names}
-    bucket = torch.from_numpy(bucket_np).to(device)
+    t0 = time.perf_counter()
+    file_bucket = [b for b in mine for _ in groups[b]]
+    schema = pq.read_schema(P.to_local(paths_in[0]))
+    schema = pa.schema([pa.field(f.name, f.type.value_type if pa.types.is_dictionary(f.type)
+                                 else f.type, f.nullable) for f in schema])
+    names = list(schema.names)
+    from . import staging
+    infos = list(staging.io_pool().map(lambda f: _footer_info(f, names), paths_in))
+    counts = [r for r, _ in infos]
+    nullable = set().union(*[m for _, m in infos]) if infos else set()
+
+    def read_file(f, cols=None):
+        return pq.read_table(P.to_local(f), columns=names if cols is None else cols)
+    bname = "__hs_bucket"
+    up = staging.upload_files(read_file, paths_in, counts, schema, device, file_bucket, bname,
+                              parquet_local=[P.to_local(f) for f in paths_in],
+                              nullable={n for n in nullable if not is_string(schema.field(n).type)})
+    cols = dict(up.columns)
+    bucket = cols.pop(bname).data.to(torch.int32)
+    _finish_strings(up.host_strings, cols, indexed, device, None)
+    n = up.num_rows
     if deleted_ids:
         # K5: lineage NOT IN deleted -> bitmap probe + stable compaction, fused in one scan kernel
         from ..ops import _lib as NL
@@ -523,7 +547,6 @@ def device_rewrite_buckets(session, files: List[str], indexed: List[str], out_pa
         p.cols[0] = lin.desc()
         p.preds[0] = NL.Pred(NL.PK_BITMAP, NL.OP_NE, 0, 0, 0, len(words), 0, 0.0, wt.data_ptr())
         p.npreds, p.naggs, p.group_col = 1, 0, -1
-        n = t.num_rows
         rstart, rlen, _ = K.full_ranges(np.array([0, n], np.int64), device)
         tp = K.ranges_to_tiles(rlen)
         rows = K.scan_select(p, rstart, rlen, tp, n // NL.lib().hs_scan_tile_rows() + 2)
@@ -531,6 +554,12 @@ def device_rewrite_buckets(session, files: List[str], indexed: List[str], out_pa
                                 [DeviceColumn(bucket, None, pa.int32())], rows)
         cols = dict(zip(names, kept[:-1]))
         bucket = kept[-1].data
+    presorted = all(len(groups[b]) == 1 for b in mine)
+    t1 = time.perf_counter()
     out = _sort_and_write(session, cols, names, bucket, indexed,
-                          num_buckets or (max(mine) + 1), out_path, schema, rank)
+                          num_buckets or (max(mine) + 1), out_path, schema, rank,
+                          presorted=presorted)
+    LAST_BUILD_STATS.update({"rewrite_read_h2d_s": t1 - t0, "rewrite_presorted": presorted,
+                             "rewrite_files": len(paths_in),
+                             "rewrite_total_s": time.perf_counter() - t0})
     return out

@@ -16,9 +16,13 @@ Only the encoded bytes cross PCIe: for the TPC-H ``l_shipdate`` index (``l_disco
 values, ``l_quantity`` 50, ``l_shipdate`` 2.5k) that is ~12 B/row instead of 28.  The host
 writes each bucket file with ``pwritev`` straight from the pinned D2H buffers.
 
-Files are Parquet v1 (data page V1, UNCOMPRESSED, optional flat columns); anything outside that
-(nulls, booleans, decimals, timestamps, a requested codec) returns ``None`` so the caller writes
-with pyarrow instead.
+* **Snappy** (the default index codec, as Spark writes) — data pages are compressed on the device
+  (``csrc/kernels/snappy_encode.hip``, ``snappy_pages``), so only compressed bytes cross PCIe;
+  the small dictionary pages with the host build of the same match finder.
+
+Files are Parquet v1 (data page V1, UNCOMPRESSED or SNAPPY, optional flat columns); anything
+outside that (nulls, booleans, decimals, timestamps, another codec) returns ``None`` so the
+caller writes with pyarrow instead.
 """
 from __future__ import annotations
 
@@ -44,7 +48,78 @@ class WCol(C.Structure):
     _fields_ = [("name", C.c_char_p), ("ptype", C.c_int32), ("logical", C.c_int32),
                 ("dict", C.c_int32), ("bit_width", C.c_int32), ("dict_page", C.c_void_p),
                 ("dict_bytes", C.c_int64), ("dict_count", C.c_int64), ("payload", C.c_void_p),
-                ("payload_bytes", C.c_int64)]
+                ("payload_bytes", C.c_int64), ("dict_raw_bytes", C.c_int64),
+                ("payload_raw_bytes", C.c_int64), ("codec", C.c_int32), ("pad", C.c_int32)]
+
+
+CODEC_IDS = {"none": 0, "uncompressed": 0, "snappy": 1}
+SNAPPY_CHUNK_DTYPE = np.dtype([("src", "<u8"), ("len", "<i8")])
+
+
+def _varint(n: int) -> bytes:
+    out = bytearray()
+    while n >= 0x80:
+        out.append((n & 0x7F) | 0x80)
+        n >>= 7
+    out.append(n)
+    return bytes(out)
+
+
+def snappy_stream_host(raw: np.ndarray) -> np.ndarray:
+    """Whole Snappy stream (length preamble + elements) of a small host buffer, e.g. a
+    dictionary page, with the host build of the device match finder."""
+    L = NL.lib()
+    raw = np.ascontiguousarray(raw, dtype=np.uint8)
+    ch = int(L.hs_snappy_chunk_bytes())
+    parts = [np.frombuffer(_varint(len(raw)), dtype=np.uint8)]
+    for s in range(0, len(raw), ch):
+        piece = raw[s:s + ch]
+        buf = np.empty(int(L.hs_snappy_max_compressed(len(piece))), dtype=np.uint8)
+        k = int(L.hs_snappy_compress_host(piece.ctypes.data, len(piece), buf.ctypes.data))
+        if k < 0:
+            raise RuntimeError("hs_snappy_compress_host failed")
+        parts.append(buf[:k])
+    return np.concatenate(parts)
+
+
+def snappy_pages(plans, p_first: int, p_end: int, device):
+    """Compress pages [p_first, p_end) of every column on the device (current stream):
+    returns (packed device buffer, offsets [col][page - p_first] into it, compressed sizes of
+    the same shape).  Pages are cut into 64 KiB chunks (one lane each,
+    csrc/kernels/snappy_encode.hip); the chunk sizes come back to the host once, then one pack
+    launch concatenates the used slot bytes page by page."""
+    import torch
+    L = NL.lib()
+    ch = int(L.hs_snappy_chunk_bytes())
+    npg = p_end - p_first
+    lo = np.stack([cp.page_off[p_first:p_end] for cp in plans]).astype(np.int64)
+    hi = np.stack([cp.page_off[p_first + 1:p_end + 1] for cp in plans]).astype(np.int64)
+    base = np.array([cp.payload.data_ptr() for cp in plans], dtype=np.uint64)
+    plen = (hi - lo).reshape(-1)
+    nchk = np.maximum(1, -(-plen // ch))
+    first = np.concatenate([[0], np.cumsum(nchk)]).astype(np.int64)
+    total = int(first[-1])
+    page_of = np.repeat(np.arange(plen.size), nchk)
+    k = np.arange(total, dtype=np.int64) - first[page_of]
+    tab = np.empty(total, dtype=SNAPPY_CHUNK_DTYPE)
+    src_page = (np.repeat(base, npg) + lo.reshape(-1).astype(np.uint64))
+    tab["src"] = src_page[page_of] + (k * ch).astype(np.uint64)
+    tab["len"] = np.minimum(ch, plen[page_of] - k * ch)
+    slot = int(L.hs_snappy_max_compressed(ch))
+    dtab = torch.from_numpy(tab.view(np.uint8)).to(device, non_blocking=False)
+    slots = torch.empty(total * slot, dtype=torch.uint8, device=device)
+    sizes = torch.empty(total, dtype=torch.int32, device=device)
+    NL.check(L.hs_snappy_compress(dtab.data_ptr(), total, slots.data_ptr(), slot,
+                                  sizes.data_ptr(), NL.stream_ptr()), "hs_snappy_compress")
+    hsz = sizes.cpu().numpy().astype(np.int64)
+    dst = np.concatenate([[0], np.cumsum(hsz)]).astype(np.int64)
+    zsize = np.add.reduceat(hsz, first[:-1]).reshape(len(plans), npg)
+    zoff = dst[first[:-1]].reshape(len(plans), npg)
+    out = torch.empty(max(1, int(dst[-1])), dtype=torch.uint8, device=device)
+    ddst = torch.from_numpy(dst[:-1].copy()).to(device)
+    NL.check(L.hs_snappy_pack(slots.data_ptr(), slot, sizes.data_ptr(), ddst.data_ptr(), total,
+                              out.data_ptr(), NL.stream_ptr()), "hs_snappy_pack")
+    return out, zoff, zsize
 
 
 def _writer():
@@ -201,17 +276,23 @@ def page_table(bucket_off: np.ndarray, rg_rows: int) -> Tuple[np.ndarray, List[T
 
 def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: pa.Schema,
                   bucket_off: np.ndarray, path_of: Callable[[int], str], rg_rows: int, device,
-                  chunk_bytes: int = 96 << 20) -> Optional[List[str]]:
+                  chunk_bytes: int = 96 << 20, codec: str = "none") -> Optional[List[str]]:
     """Encode on the device and write one Parquet file per non-empty bucket; None when the
-    columns need the pyarrow writer."""
+    columns need the pyarrow writer.  ``codec`` "snappy" compresses every data page on the
+    device (``snappy_pages``) and dictionary pages on the host."""
     import torch
     from .staging import copy_stream, io_pool, pinned_pool
+    if codec not in CODEC_IDS:
+        return None
+    cid = CODEC_IDS[codec]
     pages, files = page_table(bucket_off, rg_rows)
     if not files:
         return []
     plans = plan_columns(cols, names, schema, pages, device)
     if plans is None:
         return None
+    for cp in plans:
+        cp.dict_z = snappy_stream_host(cp.dict_page) if cid == 1 and cp.dict else None
     L = _writer()
     stream = copy_stream(device)
     stream.wait_stream(torch.cuda.current_stream(device))
@@ -236,17 +317,24 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
         p_first = batch[0][1]
         p_end = batch[-1][1] + batch[-1][2]
         host = []
+        zoff = zsize = None
         with torch.cuda.stream(stream):
-            for cp in plans:
-                lo, hi = int(cp.page_off[p_first]), int(cp.page_off[p_end])
-                h = pinned_pool().acquire(hi - lo)
-                if hi > lo:
-                    h[:hi - lo].copy_(cp.payload[lo:hi], non_blocking=True)
-                host.append((h, lo))
+            if cid == 1:
+                packed, zoff, zsize = snappy_pages(plans, p_first, p_end, device)
+                h = pinned_pool().acquire(packed.numel())
+                h[:packed.numel()].copy_(packed, non_blocking=True)
+                host = [(h, 0)]
+            else:
+                for cp in plans:
+                    lo, hi = int(cp.page_off[p_first]), int(cp.page_off[p_end])
+                    h = pinned_pool().acquire(hi - lo)
+                    if hi > lo:
+                        h[:hi - lo].copy_(cp.payload[lo:hi], non_blocking=True)
+                    host.append((h, lo))
             ev = torch.cuda.Event()
             ev.record(stream)
 
-        def write_batch(batch=batch, host=host, ev=ev):
+        def write_batch(batch=batch, host=host, ev=ev, zoff=zoff, zsize=zsize, p_first=p_first):
             ev.synchronize()
             out = []
             for b, p0, pn in batch:
@@ -254,18 +342,28 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
                 rg = (C.c_int64 * pn)()
                 for g in range(pn):
                     rg[g] = int(pages["n"][p0 + g])
-                    for c, (cp, (h, base)) in enumerate(zip(plans, host)):
+                    for c, cp in enumerate(plans):
                         w = arr[g * len(plans) + c]
-                        lo = int(cp.page_off[p0 + g]) - base
+                        raw = int(cp.page_off[p0 + g + 1] - cp.page_off[p0 + g])
                         w.name = cp.bname
                         w.ptype, w.logical = cp.ptype, cp.logical
                         w.dict, w.bit_width = int(cp.dict), cp.bw
+                        w.codec = cid
                         if cp.dict:
-                            w.dict_page = cp.dict_page.ctypes.data
-                            w.dict_bytes = cp.dict_page.nbytes
+                            dp = cp.dict_z if cid == 1 else cp.dict_page
+                            w.dict_page = dp.ctypes.data
+                            w.dict_bytes = dp.nbytes
+                            w.dict_raw_bytes = cp.dict_page.nbytes
                             w.dict_count = cp.dict_count
-                        w.payload = h.data_ptr() + lo
-                        w.payload_bytes = int(cp.page_off[p0 + g + 1] - cp.page_off[p0 + g])
+                        if cid == 1:
+                            j = p0 + g - p_first
+                            w.payload = host[0][0].data_ptr() + int(zoff[c][j])
+                            w.payload_bytes = int(zsize[c][j])
+                        else:
+                            h, base = host[c]
+                            w.payload = h.data_ptr() + int(cp.page_off[p0 + g]) - base
+                            w.payload_bytes = raw
+                        w.payload_raw_bytes = raw
                 path = path_of(b)
                 rc = L.hs_pq_write_file(path.encode(), len(plans), pn, rg, arr, created_by)
                 if rc != 0:

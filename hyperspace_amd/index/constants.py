@@ -81,10 +81,11 @@ EXEC_DEVICE_DEFAULT = "auto"
 # Per-GPU HBM budget for the resident index-column cache (bytes); 0 = disabled.
 DEVICE_CACHE_BYTES = "spark.hyperspace.mi.deviceCacheBytes"
 DEVICE_CACHE_BYTES_DEFAULT = str(160 * 1024 ** 3)
-# Index data file encoding written by the build: "plain" (GPU-decodable, uncompressed) or
-# "snappy" (pyarrow default, host decode).
+# Index data file codec written by the build: "snappy" (Spark's default Parquet codec, as the
+# reference writes; pages compressed on the device, decoded by the device Snappy inflate) or
+# "none" (uncompressed).
 INDEX_FILE_CODEC = "spark.hyperspace.mi.index.codec"
-INDEX_FILE_CODEC_DEFAULT = "none"
+INDEX_FILE_CODEC_DEFAULT = "snappy"
 # Rows per Parquet row group in index files (row-group stats drive pruning).
 INDEX_ROW_GROUP_ROWS = "spark.hyperspace.mi.index.rowGroupRows"
 INDEX_ROW_GROUP_ROWS_DEFAULT = "1048576"

@@ -182,6 +182,11 @@ def lib():
     _sig(L.hs_xch_tile_rows, I)
     _sig(L.hs_xch_pack, I, P, P, I64, P, P, P, P)
     _sig(L.hs_xch_unpack, I, P, I, I64, P)
+    _sig(L.hs_snappy_max_compressed, I64, I64)
+    _sig(L.hs_snappy_chunk_bytes, I)
+    _sig(L.hs_snappy_compress, I, P, I, P, I64, P, P)
+    _sig(L.hs_snappy_pack, I, P, I64, P, P, I, P, P)
+    _sig(L.hs_snappy_compress_host, I64, P, I64, P)
     _lib = L
     return L
 

@@ -308,7 +308,42 @@ def _pack_host(codes: np.ndarray, bw: int) -> bytes:
     return np.packbits(bits, bitorder="little").tobytes()
 
 
-def test_native_writer_round_trips_through_pyarrow_and_native_reader(tmp_path):
+def _snappy_elements_host(raw: bytes) -> bytes:
+    """Snappy elements (no preamble) of ``raw`` in 64 KiB chunks: the device kernel's output
+    contract, produced by the host build of the same match finder."""
+    from hyperspace_amd.ops import _lib as NL
+    L = NL.lib()
+    a = np.frombuffer(raw, dtype=np.uint8)
+    ch = L.hs_snappy_chunk_bytes()
+    out = []
+    for s in range(0, len(a), ch):
+        piece = np.ascontiguousarray(a[s:s + ch])
+        buf = np.empty(L.hs_snappy_max_compressed(len(piece)), dtype=np.uint8)
+        k = L.hs_snappy_compress_host(piece.ctypes.data, len(piece), buf.ctypes.data)
+        assert k >= 0
+        out.append(buf[:k].tobytes())
+    return b"".join(out)
+
+
+def test_snappy_compressor_round_trips_through_pyarrow():
+    from hyperspace_amd.exec import pq_encode as PE
+    rng = np.random.default_rng(9)
+    cases = [b"", b"abc", bytes(range(256)) * 300,
+             rng.integers(0, 256, 200_000).astype(np.uint8).tobytes(),       # incompressible
+             np.repeat(rng.integers(0, 5, 9000), 37).astype(np.uint8).tobytes(),
+             np.sort(rng.integers(0, 10**6, 50_000)).astype(np.int64).tobytes()]
+    for raw in cases:
+        z = PE.snappy_stream_host(np.frombuffer(raw, dtype=np.uint8))
+        got = pa.decompress(z.tobytes(), len(raw), codec="snappy", asbytes=True) if raw else b""
+        assert got == raw
+        # element streams of independently compressed chunks concatenate
+        el = _snappy_elements_host(raw)
+        assert PE._varint(len(raw)) + el == z.tobytes()
+    assert len(PE.snappy_stream_host(np.zeros(1 << 16, np.uint8))) < 4000
+
+
+@pytest.mark.parametrize("codec", ["none", "snappy"])
+def test_native_writer_round_trips_through_pyarrow_and_native_reader(tmp_path, codec):
     import ctypes as C
     from hyperspace_amd.exec import pq_encode as PE
     rng = np.random.default_rng(4)
@@ -342,9 +377,16 @@ def test_native_writer_round_trips_through_pyarrow_and_native_reader(tmp_path):
         for c, (name, pt, lg, dic, bw, dpage, dcount, payload) in enumerate(specs):
             w = cols[g * 4 + c]
             w.name, w.ptype, w.logical, w.dict, w.bit_width = name.encode(), pt, lg, dic, bw
+            w.codec = PE.CODEC_IDS[codec]
             if dic:
+                w.dict_raw_bytes = len(dpage)
+                if codec == "snappy":
+                    dpage = PE.snappy_stream_host(np.frombuffer(dpage, np.uint8)).tobytes()
                 w.dict_page, w.dict_bytes = buf(dpage)
                 w.dict_count = dcount
+            w.payload_raw_bytes = len(payload)
+            if codec == "snappy":
+                payload = _snappy_elements_host(payload)
             w.payload, w.payload_bytes = buf(payload)
         start += rows
     path = tmp_path / "native.parquet"
@@ -357,7 +399,10 @@ def test_native_writer_round_trips_through_pyarrow_and_native_reader(tmp_path):
     np.testing.assert_array_equal(got_d.view(np.int64), dvals[dcodes].view(np.int64))  # bit-exact
     np.testing.assert_array_equal(t.column("t").cast(pa.int32()).to_numpy(), dates)
     assert t.column("s").to_pylist() == sdict.take(pa.array(scodes)).to_pylist()
-    assert pq.ParquetFile(path).metadata.num_row_groups == 2
+    md = pq.ParquetFile(path).metadata
+    assert md.num_row_groups == 2
+    assert md.row_group(0).column(0).compression == ("SNAPPY" if codec == "snappy" else
+                                                     "UNCOMPRESSED")
     # the native reader decodes the same file (dictionary + bit-packed pages)
     with NP.PqFile(str(path)) as f:
         rc, b, info, vr, lr = f.read_chunk_host(1, f.column("d"))
@@ -367,7 +412,8 @@ def test_native_writer_round_trips_through_pyarrow_and_native_reader(tmp_path):
 
 
 @pytest.mark.gpu
-def test_device_encoded_bucket_files(tmp_path, device):
+@pytest.mark.parametrize("codec", ["none", "snappy"])
+def test_device_encoded_bucket_files(tmp_path, device, codec):
     """pq_encode: device dictionary build (sample + full-unique fallback), HIP bit-packing and
     the native writer produce bucket files pyarrow reads back bit-exactly."""
     import torch
@@ -395,7 +441,8 @@ def test_device_encoded_bucket_files(tmp_path, device):
     counts[0] += n - counts.sum()
     off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
     paths = PE.write_buckets(cols, names, schema, off,
-                             lambda b: str(tmp_path / f"b{b:03d}.parquet"), 7_000, device)
+                             lambda b: str(tmp_path / f"b{b:03d}.parquet"), 7_000, device,
+                             codec=codec)
     assert paths is not None and len(paths) == 15
     for b in range(16):
         lo, hi = int(off[b]), int(off[b + 1])
@@ -415,3 +462,12 @@ def test_device_encoded_bucket_files(tmp_path, device):
         md = pq.ParquetFile(p).metadata
         assert md.num_row_groups == (hi - lo + 6_999) // 7_000
         assert "RLE_DICTIONARY" in md.row_group(0).column(1).encodings
+        assert md.row_group(0).column(0).compression == ("SNAPPY" if codec == "snappy" else
+                                                         "UNCOMPRESSED")
+        # the native page layer + device decode read the same files back
+        with NP.PqFile(str(p)) as f:
+            rc, bb, info, vr, lr = f.read_chunk_host(0, f.column("date"))
+            assert rc == NP.OK
+            dense, _ = NP.expand_host(bb, info, vr, lr, np.dtype(np.int32))
+            np.testing.assert_array_equal(dense[:min(7_000, hi - lo)],
+                                          data["date"][lo:lo + min(7_000, hi - lo)])
