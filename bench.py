@@ -105,9 +105,10 @@ def main():
     ap.add_argument("--data-dir", default=os.environ.get("HS_BENCH_DIR", "/tmp/hs_bench"))
     ap.add_argument("--workers", type=int, default=int(os.environ.get("HS_BENCH_WORKERS", "0")))
     ap.add_argument("--no-crosscheck", action="store_true")
-    ap.add_argument("--codec", default="none",
-                    help="index file codec; 'none' = device dictionary/bit-packed encoding "
-                         "(exec/pq_encode.py), otherwise pyarrow with that codec")
+    ap.add_argument("--codec", default="snappy",
+                    help="index file codec: 'snappy' (Spark's default, as the reference writes; "
+                         "pages compressed on the device) or 'none'; both use the device "
+                         "dictionary/bit-packed encoding (exec/pq_encode.py)")
     ap.add_argument("--placement", default="both", choices=["both", "sharded", "replicated"],
                     help="multi-GPU query placement (spark.hyperspace.mi.index.placement): "
                          "sharded = buckets b %% N per rank, every query on all ranks + one "

@@ -58,7 +58,67 @@ def _codes(v, lo: int, w: int, bias: int):
 
 
 def encode(col) -> Optional[Compact]:
-    """Compact form of a DeviceColumn, or None when no encoding is narrower and exact."""
+    """Compact form of a DeviceColumn, or None when no encoding is narrower and exact.
+
+    Device columns: one ``hs_compact_probe`` pass decides the encoding and one
+    ``hs_compact_encode`` pass writes the codes (csrc/kernels/compact.hip); host tensors use
+    the PyTorch reference below (same decisions, same codes)."""
+    if col.data.is_cuda and col.offsets is None and col.hs_type in _INT_TYPES + _FLOAT_TYPES:
+        return _encode_device(col)
+    return _encode_torch(col)
+
+
+def _encode_device(col) -> Optional[Compact]:
+    import numpy as np
+    import torch
+    L = NL.lib()
+    t = col.hs_type
+    d = col.data.contiguous()
+    n = d.numel()
+    if n == 0:
+        return None
+    valid = col.valid.contiguous() if col.valid is not None else None
+    rs = int(L.hs_compact_result_size())
+    init = np.zeros(rs, dtype=np.int64)
+    imax, imin = np.iinfo(np.int64).max, np.iinfo(np.int64).min
+    init[3], init[4] = imax, imin
+    for k in range(_MAX_SCALE_DIGITS + 1):
+        init[5 + 4 * k + 2], init[5 + 4 * k + 3] = imax, imin
+    res = torch.from_numpy(init).to(d.device)
+    NL.check(L.hs_compact_probe(d.data_ptr(), valid.data_ptr() if valid is not None else None,
+                                n, t, _MAX_SCALE_DIGITS, res.data_ptr(), NL.stream_ptr()),
+             "hs_compact_probe")
+    r = res.cpu().numpy()
+    if not r[0]:
+        return None
+    k_used, scale = 0, None
+    if t in _INT_TYPES:
+        lo, hi = int(r[3]), int(r[4])
+    else:
+        if r[1] or r[2]:          # non-finite, or -0.0 (would decode as +0.0)
+            return None
+        for k in range(_MAX_SCALE_DIGITS + 1):
+            b = 5 + 4 * k
+            if r[b + 1]:          # |round(x * 10^k)| >= 2^52
+                return None
+            if not r[b]:
+                k_used, scale = k, float(10 ** k)
+                lo, hi = int(r[b + 2]), int(r[b + 3])
+                break
+        else:
+            return None
+    w, bias = _width_for(hi - lo)
+    if w is None or w >= d.element_size():
+        return None
+    dt = {1: torch.int8, 2: torch.int16, 4: torch.int32}[w]
+    codes = torch.empty(n, dtype=dt, device=d.device)
+    NL.check(L.hs_compact_encode(d.data_ptr(), valid.data_ptr() if valid is not None else None,
+                                 n, t, k_used, lo + bias, lo, w, codes.data_ptr(),
+                                 NL.stream_ptr()), "hs_compact_encode")
+    return Compact(codes, w, lo + bias, scale, t, lo, hi)
+
+
+def _encode_torch(col) -> Optional[Compact]:
     import torch
     t = col.hs_type
     d = col.data

@@ -84,22 +84,48 @@ def murmur3_hash(cols):
 # ------------------------------------------------------------------------------------------------
 # K4: radix sort -> permutation
 # ------------------------------------------------------------------------------------------------
+def _int_range(col):
+    """(any valid, min, max) of an integer column over valid rows: one hs_compact_probe launch
+    (csrc/kernels/compact.hip) and one 256-byte readback."""
+    torch = _torch()
+    import numpy as np
+    L = NL.lib()
+    init = np.zeros(int(L.hs_compact_result_size()), dtype=np.int64)
+    init[3], init[4] = np.iinfo(np.int64).max, np.iinfo(np.int64).min
+    res = torch.from_numpy(init).to(col.data.device)
+    d = col.data.contiguous()
+    v = col.valid.contiguous() if col.valid is not None else None
+    NL.check(L.hs_compact_probe(d.data_ptr(), v.data_ptr() if v is not None else None, d.numel(),
+                                col.hs_type, 0, res.data_ptr(), NL.stream_ptr()),
+             "hs_compact_probe")
+    r = res.cpu().numpy()
+    return bool(r[0]), int(r[3]), int(r[4])
+
+
 def _sortable_range(col) -> tuple:
     """(kmin, bits) of the order-preserving image over valid rows (host sync: one small D2H)."""
     torch = _torch()
     d = col.data
-    if col.valid is not None:
-        vm = col.valid.bool()
-        if not bool(vm.any()):
-            return 0, 0
-        d = d[vm]
+    t = col.hs_type
     if d.numel() == 0:
         return 0, 0
-    lo, hi = torch.aminmax(d)
-    lo, hi = lo.item(), hi.item()
-    t = col.hs_type
     if t in (NL.F32, NL.F64):
+        # full-width images; only "no valid row" needs a look at the data
+        if col.valid is not None and not bool(col.valid.any()):
+            return 0, 0
         return 0, 32 if t == NL.F32 else 64
+    if d.is_cuda and t in (NL.I8, NL.I16, NL.I32, NL.I64, NL.BOOL, NL.U32):
+        anyv, lo, hi = _int_range(col)
+        if not anyv:
+            return 0, 0
+    else:
+        if col.valid is not None:
+            vm = col.valid.bool()
+            if not bool(vm.any()):
+                return 0, 0
+            d = d[vm]
+        lo, hi = torch.aminmax(d)
+        lo, hi = lo.item(), hi.item()
     width = {NL.I8: 8, NL.I16: 16, NL.I32: 32, NL.I64: 64, NL.BOOL: 8, NL.U32: 32, NL.U64: 64}[t]
     if t in (NL.BOOL, NL.U32, NL.U64):
         kmin = int(lo)

@@ -495,3 +495,42 @@ def test_timestamp_literals_exact_in_column_unit():
         _lit_value(datetime.datetime(1970, 1, 1, 0, 0, 0, 5), pa.timestamp("ms"))
     with pytest.raises(Unsupported):
         _lit_value(datetime.datetime(1970, 1, 2, 1), pa.date32())
+
+
+@pytest.mark.gpu
+def test_hbm_encoding_device_matches_torch_reference(device):
+    """hs_compact_probe / hs_compact_encode (csrc/kernels/compact.hip) take the same decisions
+    and write the same codes as the PyTorch reference path on the host."""
+    import torch
+    from hyperspace_amd.exec.device_table import DeviceColumn
+    from hyperspace_amd.exec.encoding import _encode_device, _encode_torch
+    rng = np.random.default_rng(7)
+    n = 300_001
+    cases = [
+        (torch.from_numpy(rng.integers(10**12, 10**12 + 3_000_000_000, n)), None, pa.int64()),
+        (torch.from_numpy(rng.integers(8000, 10600, n).astype(np.int32)), None, pa.date32()),
+        (torch.from_numpy(rng.integers(-100, 100, n).astype(np.int32)),
+         torch.from_numpy((rng.random(n) < 0.9).astype(np.uint8)), pa.int32()),
+        (torch.from_numpy(rng.integers(0, 11, n) / 100.0), None, pa.float64()),
+        (torch.from_numpy(np.round(rng.random(n) * 1e5, 2)), None, pa.float64()),
+        (torch.from_numpy(np.round(rng.random(n) * 1e3, 3)),
+         torch.from_numpy((rng.random(n) < 0.5).astype(np.uint8)), pa.float64()),
+        (torch.from_numpy(rng.random(n)), None, pa.float64()),                  # no scale
+        (torch.tensor([-0.0, 1.0] * 100, dtype=torch.float64), None, pa.float64()),
+        (torch.tensor([np.nan, 1.0] * 100, dtype=torch.float64), None, pa.float64()),
+        (torch.tensor([1e17, 1.0] * 100, dtype=torch.float64), None, pa.float64()),
+        (torch.tensor([0, 2**40] * 100, dtype=torch.int64), None, pa.int64()),
+        (torch.tensor([3, 4], dtype=torch.int64), torch.tensor([0, 0], dtype=torch.uint8),
+         pa.int64()),
+    ]
+    for data, valid, at in cases:
+        ref = _encode_torch(DeviceColumn(data, valid, at))
+        got = _encode_device(DeviceColumn(data.to(device),
+                                          None if valid is None else valid.to(device), at))
+        assert (ref is None) == (got is None), (at, ref, got)
+        if ref is None:
+            continue
+        assert (got.width, got.base, got.scale, got.lo, got.hi) == \
+            (ref.width, ref.base, ref.scale, ref.lo, ref.hi)
+        vm = torch.ones(len(data), dtype=torch.bool) if valid is None else valid.bool()
+        assert torch.equal(got.codes.cpu()[vm], ref.codes[vm])
