@@ -5,27 +5,28 @@
 // The encoded pages (bit-packed dictionary codes or PLAIN values) are still in HBM after
 // hs_pq_pack, so they are compressed there and only the compressed bytes cross PCIe.
 //
-// Work split: every page is cut into chunks of <= 64 KiB; one lane compresses one chunk with the
-// greedy Snappy match finder (4-byte hash probe, skip acceleration over incompressible runs,
-// copy extension).  A chunk's elements only reference bytes of the same chunk, so the element
-// streams of consecutive chunks concatenate into one valid Snappy stream per page (the host
-// writer prepends the varint length and the definition-level literal).  Each lane's hash table
-// (512 x u16 positions) lives in LDS, interleaved by lane (entry h of lane l at h*64 + l), 64 KiB
-// per 64-lane workgroup: two workgroups per CU.  Chunks are written to fixed-size slots
-// (hs_snappy_max_compressed), then hs_snappy_pack concatenates the used bytes of every slot at
-// host-computed offsets (a workgroup per chunk, dword copies when aligned).
+// Work split: every page is cut into chunks of <= 64 KiB and one wavefront compresses one chunk
+// (hs_snappy_compress_kernel below: 64 positions hashed and probed per step, ballots pick the
+// greedy match, matches extend 64 bytes per step); its 4096-entry u16 hash table lives in LDS
+// (8 KiB per wave, 4 waves per workgroup).  A chunk's elements only reference bytes of the same
+// chunk, so the element streams of consecutive chunks concatenate into one valid Snappy stream
+// per page (the host writer prepends the varint length and the definition-level literal).
+// Chunks are written to fixed-size slots (hs_snappy_max_compressed), then hs_snappy_pack
+// concatenates the used bytes of every slot at host-computed offsets (a workgroup per chunk,
+// dword copies when aligned).
 //
-// The same match finder is compiled for the host (hs_snappy_compress_host) so CPU tests check
-// the element stream against an independent decoder.
+// A first version gave each lane its own chunk (serial greedy finder, 512-entry table per lane):
+// 64 KiB of LDS per 64 lanes left ~24 waves on the chip per 96 MB batch and ran at ~1.2 GB/s
+// (profiles/kernel_stats_sf100_r2_snappy_lane.csv).  That serial finder remains as the host
+// compressor (hs_snappy_compress_host: dictionary pages, CPU tests).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
 namespace {
 
-constexpr int kHashBits = 9;
+constexpr int kHashBits = 12;
 constexpr int kHashSize = 1 << kHashBits;
-constexpr int kLanes = 64;
 constexpr int kChunk = 1 << 16;
 constexpr int kInputMargin = 15;
 
@@ -131,22 +132,108 @@ done:
 
 struct HsSnappyChunk {
   const uint8_t* src;   // device pointer of the chunk's first input byte
-  int64_t len;          // 1 .. 65536
+  int64_t len;          // 0 .. 65536
 };
 
-__global__ __launch_bounds__(kLanes) void hs_snappy_compress_kernel(
+namespace {
+
+constexpr int kWaveHashBits = 12;
+constexpr int kWaveHashSize = 1 << kWaveHashBits;
+constexpr int kWavesPerBlock = 4;
+constexpr uint16_t kNone = 0xFFFF;
+
+__device__ inline uint32_t hash_wave(uint32_t v) { return (v * 0x1e35a7bdu) >> (32 - kWaveHashBits); }
+
+__device__ inline uint8_t* wave_literal(uint8_t* op, const uint8_t* src, int n, int lane) {
+  const uint32_t m = (uint32_t)n - 1;
+  const int h = m < 60 ? 1 : (m < (1u << 8) ? 2 : (m < (1u << 16) ? 3 : 4));
+  if (lane < h)   // tag (length in the tag, or 60..62 + 1..3 little-endian length bytes)
+    op[lane] = lane == 0 ? (uint8_t)((h == 1 ? m : (uint32_t)(58 + h)) << 2)
+                         : (uint8_t)(m >> (8 * (lane - 1)));
+  for (int i = lane; i < n; i += 64) op[h + i] = src[i];
+  return op + h + n;
+}
+
+__device__ inline uint8_t* wave_copy(uint8_t* op, int offset, int len, int lane) {
+  // uniform element sequence; lane 0 stores the tags
+  while (len > 0) {
+    const int piece = len >= 68 ? 64 : (len > 64 ? 60 : len);
+    if (lane == 0) emit_copy_le64(op, offset, piece);
+    op += (piece < 12 && offset < 2048) ? 2 : 3;
+    len -= piece;
+  }
+  return op;
+}
+
+}  // namespace
+
+// One wavefront per chunk.  Every step takes the 64 positions [ip, ip + 64): each lane hashes
+// its position's 4 bytes and probes the wave's LDS hash table (positions from earlier steps
+// only, so every candidate precedes it), a ballot picks the first lane with a verified 4-byte
+// match, the wave emits the pending literal and extends the match 64 bytes per step (ballot on
+// the first mismatching byte), and all probed positions up to the match enter the table.
+// Decisions are wave-uniform; lanes only parallelise hashing, probing, copying and comparing.
+__global__ __launch_bounds__(64 * kWavesPerBlock) void hs_snappy_compress_kernel(
     const HsSnappyChunk* __restrict__ chunks, int nchunks, uint8_t* __restrict__ slots,
     int64_t slot_bytes, int32_t* __restrict__ sizes) {
-  __shared__ uint16_t tab[kHashSize * kLanes];
-  const int lane = threadIdx.x;
-  const int c = blockIdx.x * kLanes + lane;
+  __shared__ uint16_t tabs[kWavesPerBlock][kWaveHashSize];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int c = blockIdx.x * kWavesPerBlock + w;
   if (c >= nchunks) return;
+  uint16_t* tab = tabs[w];
+  for (int i = lane; i < kWaveHashSize; i += 64) tab[i] = kNone;
+  __builtin_amdgcn_wave_barrier();
   const HsSnappyChunk ch = chunks[c];
-  uint8_t* out = slots + (int64_t)c * slot_bytes;
-  uint16_t* t = tab + lane;
-  uint8_t* end = compress_chunk(ch.src, (int)ch.len, out,
-                                [t](int h) -> uint16_t& { return t[h * kLanes]; });
-  sizes[c] = (int32_t)(end - out);
+  const uint8_t* in = ch.src;
+  const int n = (int)ch.len;
+  uint8_t* const out0 = slots + (int64_t)c * slot_bytes;
+  uint8_t* op = out0;
+  int next_emit = 0;
+  const int ip_limit = n - 4;       // last position with 4 readable bytes
+  int ip = 0;
+  while (ip <= ip_limit) {
+    const int pos = ip + lane;
+    const bool ok = pos <= ip_limit;
+    uint32_t v = 0, h = 0;
+    int cand = kNone;
+    if (ok) {
+      v = load32(in + pos);
+      h = hash_wave(v);
+      cand = tab[h];
+    }
+    const bool hit = ok && cand != kNone && load32(in + cand) == v;
+    const uint64_t mask = __ballot(hit);
+    __builtin_amdgcn_wave_barrier();
+    if (mask == 0) {
+      if (ok) tab[h] = (uint16_t)pos;
+      __builtin_amdgcn_wave_barrier();
+      ip += 64;
+      continue;
+    }
+    const int m = __ffsll((unsigned long long)mask) - 1;
+    if (ok && lane <= m) tab[h] = (uint16_t)pos;
+    __builtin_amdgcn_wave_barrier();
+    const int mpos = ip + m;
+    const int mcand = __shfl(cand, m);
+    if (mpos > next_emit) op = wave_literal(op, in + next_emit, mpos - next_emit, lane);
+    int len = 4;
+    for (;;) {                                // extend 64 bytes per step
+      const int a = mpos + len + lane;
+      const bool eq = a < n && in[mcand + len + lane] == in[a];
+      const uint64_t miss = __ballot(!eq);
+      if (miss) {
+        len += __ffsll((unsigned long long)miss) - 1;
+        break;
+      }
+      len += 64;
+    }
+    op = wave_copy(op, mpos - mcand, len, lane);
+    ip = mpos + len;
+    next_emit = ip;
+  }
+  if (next_emit < n) op = wave_literal(op, in + next_emit, n - next_emit, lane);
+  if (lane == 0) sizes[c] = (int32_t)(op - out0);
 }
 
 __global__ __launch_bounds__(256) void hs_snappy_pack_kernel(const uint8_t* __restrict__ slots,
@@ -182,9 +269,10 @@ int hs_snappy_compress(const HsSnappyChunk* chunks, int nchunks, uint8_t* slots,
   if (nchunks <= 0) return 0;
   if (slot_bytes < hs_snappy_max_compressed(kChunk)) return -1;
   (void)hipGetLastError();
-  hipLaunchKernelGGL(hs_snappy_compress_kernel, dim3((unsigned)((nchunks + kLanes - 1) / kLanes)),
-                     dim3(kLanes), 0, (hipStream_t)stream, chunks, nchunks, slots, slot_bytes,
-                     sizes);
+  hipLaunchKernelGGL(hs_snappy_compress_kernel,
+                     dim3((unsigned)((nchunks + kWavesPerBlock - 1) / kWavesPerBlock)),
+                     dim3(64 * kWavesPerBlock), 0, (hipStream_t)stream, chunks, nchunks, slots,
+                     slot_bytes, sizes);
   return (int)hipGetLastError();
 }
 

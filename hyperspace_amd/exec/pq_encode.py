@@ -53,6 +53,8 @@ class WCol(C.Structure):
 
 
 CODEC_IDS = {"none": 0, "uncompressed": 0, "snappy": 1}
+# raw encoded bytes compressed per Snappy launch (slots take ~1.17x that in HBM)
+SNAPPY_GROUP_BYTES = 2 << 30
 SNAPPY_CHUNK_DTYPE = np.dtype([("src", "<u8"), ("len", "<i8")])
 
 
@@ -311,19 +313,47 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
     futs = []
     max_inflight = 2 * min(16, os.cpu_count() or 4)
     created_by = b"hyperspace_amd (MI355X device-encoded)"
-    for batch in batches:
+    # Snappy: batches are compressed in groups of ~SNAPPY_GROUP_BYTES raw bytes, one launch each
+    # (tens of thousands of 64 KiB chunks keep every CU busy); each batch then copies its slice
+    # of the group's packed output
+    groups = []
+    if cid == 1:
+        g, gb = [], 0
+        for bi, batch in enumerate(batches):
+            nb = sum(int(cp.page_off[batch[-1][1] + batch[-1][2]] - cp.page_off[batch[0][1]])
+                     for cp in plans)
+            if g and gb + nb > SNAPPY_GROUP_BYTES:
+                groups.append(g)
+                g, gb = [], 0
+            g.append(bi)
+            gb += nb
+        if g:
+            groups.append(g)
+    group_of = {bi: gi for gi, g in enumerate(groups) for bi in g}
+    zgroup = (-1, None)
+    for bi, batch in enumerate(batches):
         if len(futs) >= max_inflight:
             futs[len(futs) - max_inflight].result()
         p_first = batch[0][1]
         p_end = batch[-1][1] + batch[-1][2]
         host = []
         zoff = zsize = None
+        gfirst = 0
         with torch.cuda.stream(stream):
             if cid == 1:
-                packed, zoff, zsize = snappy_pages(plans, p_first, p_end, device)
-                h = pinned_pool().acquire(packed.numel())
-                h[:packed.numel()].copy_(packed, non_blocking=True)
-                host = [(h, 0)]
+                gi = group_of[bi]
+                gb0, gb1 = batches[groups[gi][0]], batches[groups[gi][-1]]
+                gfirst, gend = gb0[0][1], gb1[-1][1] + gb1[-1][2]
+                if zgroup[0] != gi:
+                    zgroup = (gi, snappy_pages(plans, gfirst, gend, device))
+                packed, zoff, zsize = zgroup[1]
+                for c in range(len(plans)):
+                    lo = int(zoff[c][p_first - gfirst])
+                    hi = int(zoff[c][p_end - 1 - gfirst] + zsize[c][p_end - 1 - gfirst])
+                    h = pinned_pool().acquire(hi - lo)
+                    if hi > lo:
+                        h[:hi - lo].copy_(packed[lo:hi], non_blocking=True)
+                    host.append((h, lo))
             else:
                 for cp in plans:
                     lo, hi = int(cp.page_off[p_first]), int(cp.page_off[p_end])
@@ -334,7 +364,7 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
             ev = torch.cuda.Event()
             ev.record(stream)
 
-        def write_batch(batch=batch, host=host, ev=ev, zoff=zoff, zsize=zsize, p_first=p_first):
+        def write_batch(batch=batch, host=host, ev=ev, zoff=zoff, zsize=zsize, gfirst=gfirst):
             ev.synchronize()
             out = []
             for b, p0, pn in batch:
@@ -356,8 +386,9 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
                             w.dict_raw_bytes = cp.dict_page.nbytes
                             w.dict_count = cp.dict_count
                         if cid == 1:
-                            j = p0 + g - p_first
-                            w.payload = host[0][0].data_ptr() + int(zoff[c][j])
+                            j = p0 + g - gfirst
+                            h, base = host[c]
+                            w.payload = h.data_ptr() + int(zoff[c][j]) - base
                             w.payload_bytes = int(zsize[c][j])
                         else:
                             h, base = host[c]
