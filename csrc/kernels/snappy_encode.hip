@@ -7,8 +7,8 @@
 //
 // Work split: every page is cut into chunks of <= 64 KiB and one wavefront compresses one chunk
 // (hs_snappy_compress_kernel below: 64 positions hashed and probed per step, ballots pick the
-// greedy match, matches extend 64 bytes per step); its 4096-entry u16 hash table lives in LDS
-// (8 KiB per wave, 4 waves per workgroup).  A chunk's elements only reference bytes of the same
+// greedy match, matches extend 64 bytes per step); its 2048-entry u16 hash table lives in LDS
+// (4 KiB per wave, 4 waves per workgroup).  A chunk's elements only reference bytes of the same
 // chunk, so the element streams of consecutive chunks concatenate into one valid Snappy stream
 // per page (the host writer prepends the varint length and the definition-level literal).
 // Chunks are written to fixed-size slots (hs_snappy_max_compressed), then hs_snappy_pack
@@ -137,7 +137,7 @@ struct HsSnappyChunk {
 
 namespace {
 
-constexpr int kWaveHashBits = 12;
+constexpr int kWaveHashBits = 11;   // 4 KiB per wave: 10 waves per SIMD
 constexpr int kWaveHashSize = 1 << kWaveHashBits;
 constexpr int kWavesPerBlock = 4;
 constexpr uint16_t kNone = 0xFFFF;
@@ -167,12 +167,56 @@ __device__ inline uint8_t* wave_copy(uint8_t* op, int offset, int len, int lane)
 
 }  // namespace
 
-// One wavefront per chunk.  Every step takes the 64 positions [ip, ip + 64): each lane hashes
-// its position's 4 bytes and probes the wave's LDS hash table (positions from earlier steps
-// only, so every candidate precedes it), a ballot picks the first lane with a verified 4-byte
-// match, the wave emits the pending literal and extends the match 64 bytes per step (ballot on
-// the first mismatching byte), and all probed positions up to the match enter the table.
-// Decisions are wave-uniform; lanes only parallelise hashing, probing, copying and comparing.
+// 4 bytes at p from aligned dword loads (a funnel shift joins the two words); p's aligned
+// word is inside the buffer, and the second word is only read when p is unaligned, i.e. when
+// it holds bytes p..p+3 needs
+__device__ inline uint32_t load4(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t s = (uint32_t)(a & 3);
+  const uint32_t lo = w[0];
+  if (s == 0) return lo;
+  return (uint32_t)((((uint64_t)w[1] << 32) | lo) >> (8u * s));   // v_alignbit_b32
+}
+
+// bytes p .. p+19 as five little-endian words from six aligned dword loads (p + 24 must be
+// inside the buffer)
+__device__ inline void load20(const uint8_t* p, uint32_t r[5]) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t s = 8u * (uint32_t)(a & 3);
+  uint32_t x[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) x[k] = w[k];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) r[k] = (uint32_t)((((uint64_t)x[k + 1] << 32) | x[k]) >> s);
+}
+
+// literal of the window bytes [a, b) held one per lane (b - a <= 64)
+__device__ inline uint8_t* wave_literal_regs(uint8_t* op, uint32_t byte, int a, int b, int lane) {
+  const int m = b - a - 1;
+  const int h = m < 60 ? 1 : 2;
+  if (lane == 0) {
+    op[0] = (uint8_t)((m < 60 ? m : 60) << 2);
+    if (h == 2) op[1] = (uint8_t)m;
+  }
+  if (lane >= a && lane < b) op[h + lane - a] = (uint8_t)byte;
+  return op + h + (b - a);
+}
+
+// One wavefront per chunk, one window of 64 positions [ip, ip + 64) per step:
+//   1. every lane loads its position's 4 bytes (aligned dword loads), hashes them and probes the
+//      wave's LDS table (positions of earlier windows only, so candidates always precede);
+//   2. lanes with a candidate verify it and measure their own match length (dword compares,
+//      capped at 64 bytes) -- all in parallel, no serial dependence between positions;
+//   3. the greedy parse of the window runs on wave-uniform values only: first matching lane at or
+//      after the cursor -> literal of the bytes before it (straight from the lanes' registers) +
+//      copy, cursor jumps past the match, repeat; a match may run past the window;
+//   4. probed positions before the cursor enter the table and the next window starts there.
+// Literals are emitted per window (<= 64 bytes, 1-2 byte tag), so no byte is ever re-read for
+// output and each window costs two dependent memory round trips whatever its match count.
+// (The first wave design emitted one greedy match per step, with a literal copy and a serial
+// extension in between: 22 GB/s on sorted int64 keys, profiles/kernel_stats_build_r2_snappy_v2.csv.)
 __global__ __launch_bounds__(64 * kWavesPerBlock) void hs_snappy_compress_kernel(
     const HsSnappyChunk* __restrict__ chunks, int nchunks, uint8_t* __restrict__ slots,
     int64_t slot_bytes, int32_t* __restrict__ sizes) {
@@ -189,50 +233,76 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void hs_snappy_compress_kernel
   const int n = (int)ch.len;
   uint8_t* const out0 = slots + (int64_t)c * slot_bytes;
   uint8_t* op = out0;
-  int next_emit = 0;
-  const int ip_limit = n - 4;       // last position with 4 readable bytes
   int ip = 0;
-  while (ip <= ip_limit) {
+  while (ip < n) {
     const int pos = ip + lane;
-    const bool ok = pos <= ip_limit;
+    const bool probe = pos <= n - 4;
+    const bool fast = pos + 28 <= n;       // 20 bytes at pos and at any candidate < pos
+    uint32_t pv[5];
     uint32_t v = 0, h = 0;
-    int cand = kNone;
-    if (ok) {
-      v = load32(in + pos);
+    int cand = kNone, len = 0;
+    if (fast) {
+      load20(in + pos, pv);
+      v = pv[0];
+    } else if (probe) {
+      v = load4(in + pos);
+    } else if (pos < n) {
+      v = in[pos];
+    }
+    if (probe) {
       h = hash_wave(v);
       cand = tab[h];
     }
-    const bool hit = ok && cand != kNone && load32(in + cand) == v;
-    const uint64_t mask = __ballot(hit);
-    __builtin_amdgcn_wave_barrier();
-    if (mask == 0) {
-      if (ok) tab[h] = (uint16_t)pos;
-      __builtin_amdgcn_wave_barrier();
-      ip += 64;
-      continue;
+    if (cand != kNone) {
+      if (fast) {                          // verify + first 20 bytes in one round trip
+        uint32_t cv[5];
+        load20(in + cand, cv);
+        if (cv[0] == v) {
+          len = 20;
+#pragma unroll
+          for (int k = 4; k >= 1; --k) {
+            const uint32_t x = cv[k] ^ pv[k];
+            if (x) len = 4 * k + (__builtin_ctz(x) >> 3);
+          }
+        }
+      } else if (load4(in + cand) == v) {
+        len = 4;
+      }
+      if (len == 20 || (len == 4 && !fast)) {   // longer matches: 4 bytes per step
+        while (len < 64 && pos + len + 4 <= n) {
+          const uint32_t x = load4(in + pos + len) ^ load4(in + cand + len);
+          if (x) {
+            len += __builtin_ctz(x) >> 3;
+            break;
+          }
+          len += 4;
+        }
+        if (len > 64) len = 64;
+        while (len < 64 && pos + len < n && in[cand + len] == in[pos + len]) ++len;
+      }
     }
-    const int m = __ffsll((unsigned long long)mask) - 1;
-    if (ok && lane <= m) tab[h] = (uint16_t)pos;
-    __builtin_amdgcn_wave_barrier();
-    const int mpos = ip + m;
-    const int mcand = __shfl(cand, m);
-    if (mpos > next_emit) op = wave_literal(op, in + next_emit, mpos - next_emit, lane);
-    int len = 4;
-    for (;;) {                                // extend 64 bytes per step
-      const int a = mpos + len + lane;
-      const bool eq = a < n && in[mcand + len + lane] == in[a];
-      const uint64_t miss = __ballot(!eq);
-      if (miss) {
-        len += __ffsll((unsigned long long)miss) - 1;
+    const uint64_t hit = __ballot(len >= 4);
+    const int wv = n - ip < 64 ? n - ip : 64;
+    int cur = 0;
+    while (cur < wv) {
+      const uint64_t avail = hit & (~0ull << cur);
+      if (avail == 0) {
+        op = wave_literal_regs(op, v, cur, wv, lane);
+        cur = wv;
         break;
       }
-      len += 64;
+      const int m = __ffsll((unsigned long long)avail) - 1;
+      if (m > cur) op = wave_literal_regs(op, v, cur, m, lane);
+      const int ml = __shfl(len, m);
+      const int mc = __shfl(cand, m);
+      op = wave_copy(op, ip + m - mc, ml, lane);
+      cur = m + ml;
     }
-    op = wave_copy(op, mpos - mcand, len, lane);
-    ip = mpos + len;
-    next_emit = ip;
+    __builtin_amdgcn_wave_barrier();
+    if (probe && lane < cur) tab[h] = (uint16_t)pos;
+    __builtin_amdgcn_wave_barrier();
+    ip += cur;
   }
-  if (next_emit < n) op = wave_literal(op, in + next_emit, n - next_emit, lane);
   if (lane == 0) sizes[c] = (int32_t)(op - out0);
 }
 
