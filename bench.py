@@ -52,6 +52,15 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def _dir_bytes(root: str) -> int:
+    """Bytes of the index data files under ``root`` (all ranks' buckets: a shared file
+    system)."""
+    tot = 0
+    for dp, _, fs in os.walk(root):
+        tot += sum(os.path.getsize(os.path.join(dp, f)) for f in fs if f.endswith(".parquet"))
+    return tot
+
+
 def _decoded_bytes(df, cfg) -> int:
     """Decoded (in-memory, fixed-width) bytes of an index's columns over all source rows — the
     byte count the device build reports as ``source_bytes``."""
@@ -405,7 +414,8 @@ def main():
                           "device": args.device},
                "index_build_gbps": round(build_gbps, 3),
                "index_build_src_gbps": round(src_gbps, 3), "engine_start_s": round(engine_s, 3),
-               "index_build_s": round(build_s, 3),
+               "index_build_s": round(build_s, 3), "index_codec": args.codec,
+               "index_bytes_on_disk": _dir_bytes(idx_root),
                "index_build": per_index, "latency": lat, "warmup_s": round(warm_s, 3),
                "datagen_s": round(gen_s, 2), "crosscheck": check, "inflight": args.inflight}
         if ji_run is not None:

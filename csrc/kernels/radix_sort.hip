@@ -17,6 +17,7 @@
 #define RS_ITEMS 16
 #define RS_TILE (RS_BLOCK * RS_ITEMS)
 #define RS_BINS 256
+static_assert(RS_BINS == RS_BLOCK, "rs_scatter scans one digit per thread");
 #define SCAN_BLOCK 256
 #define SCAN_ITEMS 8
 #define SCAN_TILE (SCAN_BLOCK * SCAN_ITEMS)
@@ -75,6 +76,12 @@ __global__ __launch_bounds__(RS_BLOCK) void rs_hist(const KeyT* __restrict__ key
   for (int d = threadIdx.x; d < RS_BINS; d += RS_BLOCK) hist[(int64_t)d * ntiles + tile] = h[d];
 }
 
+// Stable scatter of one 4096-element tile.  Ranking: see the file comment.  Writing: instead of
+// storing every element straight to keys_out[global position] (256 digit runs per tile, each a
+// scattered partial line), the tile is first reordered in LDS by its local digit-major position
+// (tile digit start + per-wave prefix + rank), then threads walk the reordered tile in order and
+// element i goes to g_off[digit] + (i - tile_start[digit]): consecutive lanes write consecutive
+// addresses of one digit run, so global stores coalesce.
 template <typename KeyT>
 __global__ __launch_bounds__(RS_BLOCK) void rs_scatter(const KeyT* __restrict__ keys_in,
                                                        const uint32_t* __restrict__ vals_in,
@@ -84,6 +91,10 @@ __global__ __launch_bounds__(RS_BLOCK) void rs_scatter(const KeyT* __restrict__ 
                                                        const uint32_t* __restrict__ offsets) {
   __shared__ uint32_t wave_cnt[RS_WAVES][RS_BINS];
   __shared__ uint32_t g_off[RS_BINS];
+  __shared__ uint32_t t_start[RS_BINS];
+  __shared__ uint32_t scan_tmp[RS_WAVES];
+  __shared__ KeyT s_keys[RS_TILE];
+  __shared__ uint32_t s_vals[RS_TILE];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int64_t tile = blockIdx.x;
@@ -120,26 +131,48 @@ __global__ __launch_bounds__(RS_BLOCK) void rs_scatter(const KeyT* __restrict__ 
     rank[it] = pre + before;
   }
   __syncthreads();
-  // exclusive prefix of per-wave digit totals across waves
-  for (int d = threadIdx.x; d < RS_BINS; d += RS_BLOCK) {
-    uint32_t run = 0;
+  // per digit (one per thread: RS_BINS == RS_BLOCK): exclusive prefix of the per-wave totals
+  // across waves, and the digit's tile total
+  const int dd = threadIdx.x;
+  uint32_t total = 0;
 #pragma unroll
-    for (int ww = 0; ww < RS_WAVES; ++ww) {
-      const uint32_t t = wave_cnt[ww][d];
-      wave_cnt[ww][d] = run;
-      run += t;
-    }
+  for (int ww = 0; ww < RS_WAVES; ++ww) {
+    const uint32_t t = wave_cnt[ww][dd];
+    wave_cnt[ww][dd] = total;
+    total += t;
   }
+  // exclusive scan of the tile totals over digits -> digit start inside the reordered tile
+  uint32_t x = total;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) scan_tmp[w] = x;
+  __syncthreads();
+  uint32_t wpre = 0;
+  for (int ww = 0; ww < w; ++ww) wpre += scan_tmp[ww];
+  t_start[dd] = wpre + x - total;
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < RS_ITEMS; ++it) {
     const int64_t i = wbase + it * 64 + lane;
     if (i < n) {
       const uint32_t d = (uint32_t)(k[it] >> shift) & 0xFF;
-      const uint32_t pos = g_off[d] + wave_cnt[w][d] + rank[it];
-      keys_out[pos] = k[it];
-      vals_out[pos] = v[it];
+      const uint32_t lp = t_start[d] + wave_cnt[w][d] + rank[it];
+      s_keys[lp] = k[it];
+      s_vals[lp] = v[it];
     }
+  }
+  __syncthreads();
+  const int64_t rem = n - tile * RS_TILE;
+  const int cnt_tile = rem < RS_TILE ? (int)rem : RS_TILE;
+  for (int i = threadIdx.x; i < cnt_tile; i += RS_BLOCK) {
+    const KeyT kk = s_keys[i];
+    const uint32_t d = (uint32_t)(kk >> shift) & 0xFF;
+    const uint32_t pos = g_off[d] + (uint32_t)i - t_start[d];
+    keys_out[pos] = kk;
+    vals_out[pos] = s_vals[i];
   }
 }
 
