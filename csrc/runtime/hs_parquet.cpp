@@ -412,6 +412,7 @@ namespace {
 constexpr int64_t kChunk = 4096;  // split long runs so each GPU work item stays short
 // device plans inflate Snappy dictionary pages larger than this on the host (plan_chunk)
 constexpr int kHostDictMin = 64 << 10;
+constexpr int64_t kDeviceInflateMax = 2 << 20;   // largest page a wavefront inflates
 std::atomic<int> g_host_inflate{2};   // hs_pq_set_host_inflate
 
 // Parse an RLE/bit-packed hybrid stream of `count` values into runs (dst starts at `dst0`).
@@ -756,6 +757,10 @@ int plan_chunk(File* f, int rg, int col, uint8_t* raw, int64_t raw_cap, int64_t 
     const bool big_dict = p.kind == 2 && p.usize > kHostDictMin;
     const bool dense = p.codec == 1 && mode > 0 &&
         (big_dict || (mode > 1 && (int64_t)p.usize * 10 >= (int64_t)p.csize * 11));
+    // one wavefront inflates one page on the device: a multi-MB Snappy page left to it runs for
+    // seconds (profiles/cold_load_r2.jsonl: 58 s for an index of 1M-row pages), so such a
+    // column goes to the host page layer instead
+    if (p.codec == 1 && !(dense && hbuf) && p.usize > kDeviceInflateMax) return HS_PQ_UNSUPPORTED;
     if (dense && hbuf) {
       const int lv = p.kind == 1 ? p.levels : 0;
       const uint8_t* src = base + (payload - raw_at);

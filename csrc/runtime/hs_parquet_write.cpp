@@ -266,6 +266,12 @@ int hs_pq_write_file(const char* path, int ncols, int nrg, const int64_t* rg_row
       w.i64(7, p.total);                        // total_compressed_size
       w.i64(9, p.data_off);
       if (p.dict_off >= 0) w.i64(11, p.dict_off);
+      // Statistics { 3: null_count = 0 }: every index column the device encoder writes is
+      // null-free, and readers (our device page planner, hs_parquet.cpp) take the null-free
+      // decode path only when the footer says so
+      w.begin_struct(12);
+      w.i64(3, 0);
+      w.end_struct();
       w.end_struct();
       w.end_struct();
     }

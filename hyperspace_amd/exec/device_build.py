@@ -529,7 +529,8 @@ def device_rewrite_buckets(session, files: List[str], indexed: List[str], out_pa
     bname = "__hs_bucket"
     up = staging.upload_files(read_file, paths_in, counts, schema, device, file_bucket, bname,
                               parquet_local=[P.to_local(f) for f in paths_in],
-                              nullable={n for n in nullable if not is_string(schema.field(n).type)})
+                              nullable={n for n in nullable if not is_string(schema.field(n).type)},
+                              device_pages=False)
     cols = dict(up.columns)
     bucket = cols.pop(bname).data.to(torch.int32)
     _finish_strings(up.host_strings, cols, indexed, device, None)

@@ -137,7 +137,8 @@ def load_bucketed_index(files, columns: List[str], num_buckets: int, sort_cols: 
             return pq.read_table(P.to_local(p), columns=columns if cols is None else cols,
                                  use_threads=False)
         up = staging.upload_files(read_file, paths, rows, schema, device,
-                                  parquet_local=[P.to_local(p) for p in paths])
+                                  parquet_local=[P.to_local(p) for p in paths],
+                                  device_pages=False)
         cols = dict(up.columns)
         for name, chunks in up.host_strings.items():
             arr = pa.chunked_array(chunks, type=chunks[0].type)

@@ -403,6 +403,8 @@ def test_native_writer_round_trips_through_pyarrow_and_native_reader(tmp_path, c
     assert md.num_row_groups == 2
     assert md.row_group(0).column(0).compression == ("SNAPPY" if codec == "snappy" else
                                                      "UNCOMPRESSED")
+    st = md.row_group(0).column(0).statistics
+    assert st is not None and st.has_null_count and st.null_count == 0
     # the native reader decodes the same file (dictionary + bit-packed pages)
     with NP.PqFile(str(path)) as f:
         rc, b, info, vr, lr = f.read_chunk_host(1, f.column("d"))
