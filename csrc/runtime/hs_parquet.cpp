@@ -78,6 +78,11 @@ struct TReader {
     elem_type = b & 0x0f;
     size = b >> 4;
     if (size == 15) size = (int64_t)varint();
+    // every element takes at least one byte: a longer list is a damaged length
+    if (size < 0 || size > end - p) {
+      bad = true;
+      size = 0;
+    }
   }
   void skip(int type) {
     switch (type) {
@@ -277,6 +282,24 @@ int open_file(const char* path, File& f) {
   if (r.bad) { f.error = "corrupt footer"; return HS_PQ_CORRUPT; }
   for (size_t i = 1; i < f.schema.size(); ++i)
     if (f.schema[i].num_children == 0) f.leaves.push_back((int)i);
+  // every row group must describe every leaf column (callers index cols[] by leaf)
+  for (const RowGroupMeta& g : f.rgs) {
+    if (g.cols.size() != f.leaves.size() || g.num_rows < 0) {
+      f.error = "row group / schema mismatch";
+      return HS_PQ_CORRUPT;
+    }
+    // sizes the buffer bounds derive from (hs_pq_chunk_bound etc.) must be sane
+    for (const ChunkMeta& m : g.cols)
+      if (m.total_compressed < 0 || m.total_compressed > f.size || m.total_uncompressed < 0 ||
+          m.total_uncompressed > ((int64_t)1 << 40) || m.num_values < 0 ||
+          // Snappy expands at most ~22x (a 64-byte copy in 3 bytes); plain pages not at all
+          ((m.codec == 0 || m.codec == 1) &&
+           m.total_uncompressed > 24 * m.total_compressed + 4096) ||
+          m.data_page_offset < 0 || m.data_page_offset > f.size) {
+        f.error = "corrupt column chunk metadata";
+        return HS_PQ_CORRUPT;
+      }
+  }
   return HS_PQ_OK;
 }
 
@@ -428,10 +451,14 @@ int64_t parse_hybrid(const uint8_t* s, int64_t len, int64_t base, int bw, int64_
     const uint64_t h = r.varint();
     if (r.bad) return -1;
     if (h & 1) {  // bit-packed: (h>>1) groups of 8 values, bw bytes per group
-      const int64_t groups = (int64_t)(h >> 1);
+      const uint64_t g64 = h >> 1;
+      // a damaged header can claim ~2^63 groups: bound it by the bytes left before multiplying
+      if (bw > 0 && g64 > (uint64_t)(r.end - r.p) / (uint64_t)bw) return -1;
+      const int64_t left = count - done;
+      const int64_t groups = g64 > (uint64_t)((left + 7) / 8) && bw == 0 ? (left + 7) / 8
+                                                                           : (int64_t)g64;
       const int64_t nbytes = groups * bw;
-      if (r.end - r.p < nbytes) return -1;
-      const int64_t take = groups * 8 < count - done ? groups * 8 : count - done;
+      const int64_t take = groups < (left + 7) / 8 ? groups * 8 : left;
       const int64_t off = base + (r.p - s);
       for (int64_t c = 0; c < take; c += kChunk)   // kChunk % 8 == 0: chunks stay byte aligned
         runs.push_back({dst0 + done + c, take - c < kChunk ? take - c : kChunk,
@@ -507,6 +534,11 @@ bool parse_page_header(TReader& r, PageHdr& h) {
       default: r.skip(t);
     }
   }
+  // counts and lengths of a damaged header can decode negative (found by the ASan corpus run,
+  // scripts/sanitize_hostio.py): reject them here so no caller sizes a copy from them
+  if (h.usize < 0 || h.csize < 0 || h.nvals < 0 || h.dict_nvals < 0 || h.v2_def_len < 0 ||
+      h.v2_rep_len < 0 || h.v2_def_len > h.csize || h.v2_def_len > h.usize)
+    return false;
   return !r.bad;
 }
 
