@@ -30,6 +30,7 @@ from ..utils.conf import HyperspaceConf
 from .device_table import DeviceColumn, DeviceTable, is_string
 
 LAST_BUILD_STATS: Dict[str, float] = {}
+_T0 = [0.0]
 # source files per exchange batch of a multi-GPU build (decode of batch k+1 overlaps the
 # all-to-all of batch k)
 FILES_PER_BATCH = 8
@@ -157,12 +158,16 @@ def _streaming_plan(session, rel, my_files, columns, lineage_ids, num_buckets, d
     if any(is_string(f.type) for f in schema):
         return None
     from . import staging
+    tf = time.perf_counter()
     infos = list(staging.io_pool().map(lambda f: _footer_info(f, list(schema.names)), my_files))
+    LAST_BUILD_STATS["plan_footers_s"] = round(time.perf_counter() - tf, 4)
     rows = [r for r, _ in infos]
     row_bytes = sum(storage_numpy_dtype(f.type).itemsize + 1 for f in schema) + \
         (8 if lineage_ids is not None else 0) + 4
     est = int(sum(rows) * row_bytes * BUILD_SORT_FACTOR)
+    tb = time.perf_counter()
     budget = _build_budget(session, device)
+    LAST_BUILD_STATS["plan_budget_s"] = round(time.perf_counter() - tb, 4)
     passes = plan_passes(est, budget, num_buckets)
     if len(passes) <= 1:
         return None
@@ -234,6 +239,7 @@ def device_build_from_source(session, rel, files: List[str], columns: List[str],
     device = torch.device("cuda", torch.cuda.current_device())
     _prepare_out_dir(out_path, mode, dist)
     t0 = time.perf_counter()
+    _T0[0] = t0
     my_files = files[rank::world]
     fmt = source_format(rel)
     from . import staging
@@ -243,8 +249,10 @@ def device_build_from_source(session, rel, files: List[str], columns: List[str],
     native_parquet.PHASES.clear()
     xs = _BatchedExchange(dist, num_buckets, indexed) if world > 1 else None
     LAST_BUILD_STATS.clear()
+    tp = time.perf_counter()
     splan = _streaming_plan(session, rel, my_files, columns, lineage_ids, num_buckets, device,
                             world)
+    LAST_BUILD_STATS["pass_plan_s"] = round(time.perf_counter() - tp, 4)
     if splan is not None:
         return _streaming_build(session, rel, my_files, columns, indexed, num_buckets, out_path,
                                 lineage_ids, device, splan, rank)
@@ -272,6 +280,7 @@ def device_build_from_source(session, rel, files: List[str], columns: List[str],
                              "total_s": time.perf_counter() - t0, "source_bytes": source_bytes,
                              "host_decoded": sorted(staging.HOST_DECODED),
                              "device_decoded": sorted(staging.DEVICE_DECODED),
+                             "upload_wall_s": dict(staging.UPLOAD_TIMES),
                              "decode_phases_s": {k: round(v, 4) for k, v in
                                                  native_parquet.PHASES.items()}})
     if xs is not None:
@@ -423,8 +432,11 @@ def _upload_parquet(rel, my_files, columns, indexed, lineage_ids, device, dist, 
     from ..io.reader import output_schema, read_files
     from . import staging
     schema = output_schema(rel.data_schema, rel.location.partition_spec, columns)
+    LAST_BUILD_STATS["pre_upload_s"] = round(time.perf_counter() - _T0[0], 4)
+    tf = time.perf_counter()
     infos = list(staging.io_pool().map(lambda f: _footer_info(f, list(schema.names)), my_files))
     counts = [r for r, _ in infos]
+    LAST_BUILD_STATS["footers_s"] = round(time.perf_counter() - tf, 4)
 
     want = columns
     part_names = {f.name for f in rel.location.partition_spec.columns} \
@@ -463,10 +475,12 @@ def _upload_parquet(rel, my_files, columns, indexed, lineage_ids, device, dist, 
         k = int(dist.all_reduce_max_float(float(-(-len(my_files) // FILES_PER_BATCH))))
         edges = np.linspace(0, len(my_files), max(k, 1) + 1).round().astype(int)
         batches = [(int(a), int(b)) for a, b in zip(edges[:-1], edges[1:])]
+    tu = time.perf_counter()
     up = staging.upload_files(read_file, my_files, counts, schema, device, lin,
                               C.DATA_FILE_NAME_ID,
                               parquet_local=[P.to_local(f) for f in my_files],
                               nullable=nullable, on_batch=on_batch, file_batches=batches)
+    LAST_BUILD_STATS["upload_files_s"] = round(time.perf_counter() - tu, 4)
     cols = dict(up.columns)
     _finish_strings(up.host_strings, cols, indexed, device, dist)
     return {n: cols[n] for n in names}, names, pa.schema(fields)

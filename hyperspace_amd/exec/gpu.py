@@ -112,6 +112,11 @@ class GpuBackend:
         copy streams, and the kernel code objects."""
         import torch
         from . import staging
+        # pyarrow's lazily imported dataset layer (pulled in by the first Parquet read of a
+        # build) costs ~0.45 s of one-time import: pay it here, not inside the first build
+        import pyarrow.compute  # noqa: F401
+        import pyarrow.dataset  # noqa: F401
+        import pyarrow.parquet  # noqa: F401
         reserve = HyperspaceConf.hbm_reserve_bytes(self.session.conf)
         if reserve > 0:
             free, _ = torch.cuda.mem_get_info(self.device)

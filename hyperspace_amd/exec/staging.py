@@ -28,6 +28,7 @@ import pyarrow as pa
 from .device_table import DeviceColumn, is_string, storage_numpy_dtype
 
 _POOL = None
+UPLOAD_TIMES: Dict[str, float] = {}   # wall split of the last upload_files (build stats)
 _COPY_STREAMS: Dict[int, object] = {}
 
 
@@ -268,7 +269,9 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
     expansion; index bucket files pass False (profiles/cold_load_r2.jsonl: their row-group-sized
     Snappy pages load 0.39 s via the host page layer vs 2.2 s device-only at SF100).
     """
+    import time as _t
     import torch
+    t_in = _t.perf_counter()
     offs = np.concatenate([[0], np.cumsum(np.asarray(row_counts, dtype=np.int64))])
     n = int(offs[-1])
     streams = copy_streams(device)
@@ -292,6 +295,7 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
     for st in streams:
         st.wait_stream(main)  # allocations above happen-before the copies
 
+    t_alloc = _t.perf_counter()
     native = parquet_local is not None and native_decode_enabled()
     use_device_pages = device_decode_enabled() if device_pages is None else device_pages
     status = None
@@ -347,6 +351,9 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
         ev.record(stream)
         return ev
 
+    t_sub = _t.perf_counter()
+    UPLOAD_TIMES.clear()
+    UPLOAD_TIMES.update({"alloc_s": round(t_alloc - t_in, 4), "warm_s": round(t_sub - t_alloc, 4)})
     futs = [io_pool().submit(work, i) for i in range(len(files))]
     if file_batches is None:
         file_batches = [(0, len(files))]
@@ -357,10 +364,13 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
             on_batch(cols, int(offs[b0]), int(offs[b1]))
     for fu in futs:
         fu.result()
+    t_host = _t.perf_counter()
     for st in streams:
         main.wait_stream(st)
     if status is not None:
         code = int(status.item())
+        UPLOAD_TIMES.update({"files_s": round(t_host - t_sub, 4),
+                             "device_drain_s": round(_t.perf_counter() - t_host, 4)})
         if code:
             raise IOError(f"device Parquet decode failed (status {code}: 1 corrupt page, "
                           f"2 dictionary index out of range) in {len(files)} files")

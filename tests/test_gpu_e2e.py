@@ -245,3 +245,60 @@ def test_incremental_refresh_with_deletes_on_device(tpch, tmp_path):
     assert path == "native", s.backend().fallback_reason
     _close(g, c)
     assert "li_ok" in q.queryExecution.executed_plan.tree_string()
+
+
+def _bucket_files_sorted(index_dir: str, key: str) -> int:
+    """Every bucket file of the latest version is sorted by ``key``; returns the file count."""
+    vers = sorted(d for d in os.listdir(index_dir) if d.startswith("v__="))
+    vdir = os.path.join(index_dir, vers[-1])
+    files = [f for f in os.listdir(vdir) if f.endswith(".parquet")]
+    for f in files:
+        k = pq.read_table(os.path.join(vdir, f), columns=[key]).column(key).to_numpy()
+        assert np.all(k[:-1] <= k[1:]), f
+    return len(files)
+
+
+def test_delete_only_rewrite_is_sort_free_and_sorted(tpch, tmp_path):
+    from hyperspace_amd.exec import device_build
+    s, lpath, _ = tpch
+    s.conf.set("spark.hyperspace.index.lineage.enabled", "true")
+    hs = Hyperspace(s)
+    hs.createIndex(s.read.parquet(lpath), IndexConfig("li_ok", ["l_orderkey"], ["l_quantity"]))
+    os.remove(os.path.join(lpath, "part-3.parquet"))
+    hs.refreshIndex("li_ok", "incremental")
+    # one file per bucket + deletes only: the stable device compaction keeps the sorted order
+    assert device_build.LAST_BUILD_STATS.get("rewrite_presorted") is True
+    assert _bucket_files_sorted(str(tmp_path / "idx" / "li_ok"), "l_orderkey") <= 16
+    Hyperspace.enable(s)
+    q = s.read.parquet(lpath).filter("l_orderkey > 0").agg(sum_("l_quantity").alias("q"),
+                                                           count("*").alias("n"))
+    g, c, path = _both(s, q, sort=False)
+    assert path == "native", s.backend().fallback_reason
+    _close(g, c)
+
+
+def test_optimize_full_on_device_merges_bucket_files(tpch, tmp_path):
+    from hyperspace_amd.exec import device_build
+    s, lpath, _ = tpch
+    hs = Hyperspace(s)
+    hs.createIndex(s.read.parquet(lpath), IndexConfig("li_ok", ["l_orderkey"], ["l_quantity"]))
+    rng = np.random.default_rng(3)
+    extra = pa.table({"l_orderkey": rng.integers(1, 160_000, 3000).astype(np.int64),
+                      "l_quantity": rng.integers(1, 51, 3000).astype(np.float64),
+                      "l_extendedprice": np.round(rng.random(3000) * 1e5, 2),
+                      "l_discount": rng.integers(0, 11, 3000) / 100.0,
+                      "l_shipdate": pa.array(rng.integers(8000, 10600, 3000).astype(np.int32))
+                      .view(pa.date32()),
+                      "l_returnflag": pa.array(rng.choice(["A", "N", "R"], 3000))})
+    pq.write_table(extra, os.path.join(lpath, "part-9.parquet"))
+    hs.refreshIndex("li_ok", "incremental")       # appended rows: a second file per bucket
+    hs.optimizeIndex("li_ok", "full")
+    assert device_build.LAST_BUILD_STATS.get("rewrite_presorted") is False
+    assert _bucket_files_sorted(str(tmp_path / "idx" / "li_ok"), "l_orderkey") <= 16
+    Hyperspace.enable(s)
+    q = s.read.parquet(lpath).filter("l_orderkey > 0").agg(sum_("l_quantity").alias("q"),
+                                                           count("*").alias("n"))
+    g, c, path = _both(s, q, sort=False)
+    assert path == "native", s.backend().fallback_reason
+    _close(g, c)
+    assert "li_ok" in q.queryExecution.executed_plan.tree_string()
