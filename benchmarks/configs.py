@@ -381,7 +381,13 @@ def config_tpcds_3way(args):
         plan = _tpcds_query(ss_, it_, dd_, 0).queryExecution.executed_plan.tree_string()
         for i in range(2):
             _tpcds_query(ss_, it_, dd_, 1000 + i).collect()
+        from hyperspace_amd.utils.tracing import TRACER, format_report
+        TRACER.reset()
         el = _timed_loop(lambda i: _tpcds_query(ss_, it_, dd_, i).collect(), k, args.device)
+        if TRACER.profile:   # HS_PROFILE=1: where the star join's time goes
+            print(f"[tpcds_3way:{tag}] stage profile\n" + format_report(TRACER.report()),
+                  file=sys.stderr, flush=True)
+            print(plan, file=sys.stderr, flush=True)
         got = _rows(_tpcds_query(ss_, it_, dd_, 0))
         ref = _tpcds_oracle(paths, 0)
         return {f"{tag}_queries_per_s": round(k / el, 3), f"{tag}_query_ms": round(el / k * 1e3, 2),

@@ -86,6 +86,19 @@ __global__ void hs_range_search_kernel(ColDesc key, const int64_t* __restrict__ 
             rlen, rbucket);
 }
 
+// Key probes: for probe i, the rows of bucket pbucket[i] whose sorted key equals the sortable
+// image pkey[i] (one binary-search pair per probe).  Drives a join from a small, filtered side
+// into a large index sorted by the join key: only the matching key runs are scanned.
+__global__ void hs_probe_ranges_kernel(ColDesc key, const int64_t* __restrict__ bucket_off,
+                                       const int32_t* __restrict__ pbucket,
+                                       const uint64_t* __restrict__ pkey, int np,
+                                       int64_t* __restrict__ rstart, int64_t* __restrict__ rlen,
+                                       int32_t* __restrict__ rbucket) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= np) return;
+  range_one(key, bucket_off, pbucket, i, 1, pkey[i], 1, 1, pkey[i], 1, rstart, rlen, rbucket);
+}
+
 // Bounds read from device memory (int64 x6: has_lo, lo, lo_incl, has_hi, hi, hi_incl), so a
 // captured hipGraph replays with new literals after one H2D of the parameter block.
 __global__ void hs_range_search_dev_kernel(ColDesc key, const int64_t* __restrict__ bucket_off,
@@ -353,6 +366,16 @@ int hs_range_search(const ColDesc* key, const int64_t* bucket_off, const int32_t
   hipLaunchKernelGGL(hs_range_search_kernel, dim3((nb + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, *key, bucket_off, buckets, nb, has_lo, lo_key, lo_incl,
                      has_hi, hi_key, hi_incl, rstart, rlen, rbucket);
+  return (int)hipGetLastError();
+}
+
+int hs_probe_ranges(const ColDesc* key, const int64_t* bucket_off, const int32_t* pbucket,
+                    const uint64_t* pkey, int np, int64_t* rstart, int64_t* rlen, int32_t* rbucket,
+                    void* stream) {
+  if (np <= 0) return 0;
+  hipLaunchKernelGGL(hs_probe_ranges_kernel, dim3((np + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, *key, bucket_off, pbucket, pkey, np, rstart, rlen,
+                     rbucket);
   return (int)hipGetLastError();
 }
 

@@ -432,6 +432,13 @@ class GpuBackend:
             t = r.table
             full = t.num_rows
             return {a.expr_id: r.col(a) for a in attrs} if full is not None else {}
+        rows = self._selected_rows(r, attrs)
+        cols = [r.col(a) for a in attrs]
+        g = K.gather_columns(cols, rows)
+        return {a.expr_id: c for a, c in zip(attrs, g)}
+
+    def _selected_rows(self, r: DRel, attrs: List[E.Attribute] = ()):
+        """Row ids (int64, ascending) of ``r``'s rows that pass its pending predicates."""
         implied: set = set()
         rstart, rlen, _ = self._ranges(r, r.conds, implied)
         col_info, descs = self._column_infos([(r, 0)])
@@ -453,9 +460,64 @@ class GpuBackend:
             tp = K.ranges_to_tiles(rlen)
             max_tiles = r.table.num_rows // NL.lib().hs_scan_tile_rows() + rlen.numel() + 1
             rows = K.scan_select(p, rstart, rlen, tp, max_tiles)
-        cols = [r.col(a) for a in attrs]
-        g = K.gather_columns(cols, rows)
-        return {a.expr_id: c for a, c in zip(attrs, g)}
+        return rows
+
+    # a filtered right side drives the join when it keeps fewer than 1 / PROBE_RATIO of the left
+    # rows; only tried when the right table itself is this much smaller than the left
+    PROBE_RATIO = 64
+    PROBE_MAX = 1 << 20
+
+    def _probe_ranges(self, left: DRel, right: DRel, lk, rk):
+        """Key-probe ranges of ``left`` for a selective, filtered ``right`` (a dimension filtered
+        down to a few keys against a large fact index sorted by the join key): the right rows
+        passing their predicates are selected first, and each distinct (bucket, key) of them
+        becomes one equality range search in the left's bucket, so the join scans only the
+        matching key runs of the left instead of every left row.  None when the shape does not
+        qualify (then the left's own ranges drive the join).  Left-side predicates are not
+        applied by these ranges; the caller evaluates all of them per row."""
+        import torch
+        if left.parts or right.parts or not right.conds or not left.bucketed:
+            return None
+        nl, nr = left.table.num_rows or 0, right.table.num_rows or 0
+        if nl < (1 << 20) or nr * 8 > nl:
+            return None
+        lc, rc = left.col(lk), right.col(rk)
+        if lc.is_float or rc.is_float or lc.dictionary is not None or \
+                rc.dictionary is not None or lc.offsets is not None:
+            return None
+        width = {NL.I8: 8, NL.I16: 16, NL.I32: 32, NL.I64: 64}.get(lc.hs_type)
+        if width is None or rc.hs_type not in (NL.I8, NL.I16, NL.I32, NL.I64):
+            return None
+        with stage("join.probe_select"):
+            rows = self._selected_rows(right)
+            npass = int(rows.numel())
+        if npass * self.PROBE_RATIO > nl or npass > self.PROBE_MAX:
+            return None
+        with stage("join.probe_ranges"):
+            g = K.gather_columns([rc], rows)[0]
+            vals = g.data.to(torch.int64).cpu().numpy()
+            ok = np.ones(len(vals), dtype=bool)
+            if g.valid is not None:
+                ok &= g.valid.cpu().numpy().astype(bool)
+            rows_h = rows.cpu().numpy()
+            off = right.table.bucket_offsets_host
+            bk = np.searchsorted(off, rows_h, side="right") - 1
+            lo, hi = -(1 << (width - 1)), (1 << (width - 1)) - 1
+            ok &= (vals >= lo) & (vals <= hi)
+            vals, bk = vals[ok], bk[ok]
+            if width == 64:
+                u = (vals.view(np.uint64) ^ np.uint64(1 << 63))
+            else:
+                u = (vals + (1 << (width - 1))).astype(np.uint64)
+            probes = np.unique(np.stack([bk.astype(np.uint64), u], axis=1), axis=0) \
+                if len(u) else np.zeros((0, 2), np.uint64)
+            self.last_join_probes = len(probes)
+            pb = torch.from_numpy(probes[:, 0].astype(np.int32)).to(self.device)
+            pk = torch.from_numpy(probes[:, 1].view(np.int64).copy()).to(self.device)
+            if len(probes) == 0:
+                z = torch.zeros(0, dtype=torch.int64, device=self.device)
+                return z, z.clone(), torch.zeros(0, dtype=torch.int32, device=self.device)
+            return K.probe_ranges(lc, left.table.bucket_offsets, pb, pk)
 
     def _to_arrow(self, r: DRel, out_attrs: List[E.Attribute]) -> pa.Table:
         if r.parts:  # rows of a bucket union: each part's rows, concatenated
@@ -766,8 +828,12 @@ class GpuBackend:
             raise Unsupported("row-producing join over a bucket union")
         out_attrs = list(p.output)
         implied: set = set()
-        with stage("join.ranges"):
-            rstart, rlen, rbk = self._ranges(left, left.conds, implied)
+        probed = self._probe_ranges(left, right, lk, rk)
+        if probed is not None:
+            rstart, rlen, rbk = probed
+        else:
+            with stage("join.ranges"):
+                rstart, rlen, rbk = self._ranges(left, left.conds, implied)
         jp, col_info, descs, keep = self._join_params(
             left, right, lk, rk, p.condition,
             lconds=[c for c in left.conds if id(c) not in implied])
@@ -1139,7 +1205,11 @@ class GpuBackend:
         if right.table.num_rows * 64 < left.table.num_rows:
             left, right, lk, rk = right, left, rk, lk
         implied: set = set()
-        rstart, rlen, rbk = self._ranges(left, left.conds, implied)
+        probed = self._probe_ranges(left, right, lk, rk)
+        if probed is not None:
+            rstart, rlen, rbk = probed
+        else:
+            rstart, rlen, rbk = self._ranges(left, left.conds, implied)
         jp, col_info, descs, keep = self._join_params(
             left, right, lk, rk, node.condition,
             lconds=[c for c in left.conds if id(c) not in implied])

@@ -182,6 +182,7 @@ def lib():
     _sig(L.hs_xch_tile_rows, I)
     _sig(L.hs_xch_pack, I, P, P, I64, P, P, P, P)
     _sig(L.hs_xch_unpack, I, P, I, I64, P)
+    _sig(L.hs_probe_ranges, I, P, P, P, P, I, P, P, P, P)
     _sig(L.hs_compact_result_size, I)
     _sig(L.hs_compact_probe, I, P, P, I64, I, I, P, P)
     _sig(L.hs_compact_encode, I, P, P, I64, I, I, I64, I64, I, P, P)

@@ -258,6 +258,22 @@ def range_search(key_col, bucket_off, buckets=None, lo=None, lo_incl=True, hi=No
     return rstart, rlen, rbucket
 
 
+def probe_ranges(key_col, bucket_off, pbucket, pkey):
+    """Per probe (bucket int32, sortable key image as int64 bits), the [start, len) run of rows
+    of that bucket whose sorted key equals it.  Returns (rstart, rlen, rbucket)."""
+    torch = _torch()
+    n = int(pbucket.numel())
+    dev = bucket_off.device
+    rstart = torch.empty(n, dtype=torch.int64, device=dev)
+    rlen = torch.empty(n, dtype=torch.int64, device=dev)
+    rbucket = torch.empty(n, dtype=torch.int32, device=dev)
+    kd = key_col.desc()
+    NL.check(NL.lib().hs_probe_ranges(C.byref(kd), NL.ptr(bucket_off), NL.ptr(pbucket),
+                                      NL.ptr(pkey), n, NL.ptr(rstart), NL.ptr(rlen),
+                                      NL.ptr(rbucket), NL.stream_ptr()), "hs_probe_ranges")
+    return rstart, rlen, rbucket
+
+
 def full_ranges(bucket_off_host: np.ndarray, device, buckets: Optional[List[int]] = None):
     torch = _torch()
     off = bucket_off_host

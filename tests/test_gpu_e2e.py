@@ -302,3 +302,37 @@ def test_optimize_full_on_device_merges_bucket_files(tpch, tmp_path):
     assert path == "native", s.backend().fallback_reason
     _close(g, c)
     assert "li_ok" in q.queryExecution.executed_plan.tree_string()
+
+
+def test_selective_dimension_join_probes_key_runs(tmp_path, device):
+    """A fact index joined with a dimension filtered down to a few keys: the executor probes
+    the fact index's key runs (hs_probe_ranges) instead of scanning it, and the rows match the
+    host oracle."""
+    rng = np.random.default_rng(11)
+    n_item, n_fact = 20_000, 1_500_000
+    item = pa.table({"i_sk": np.arange(n_item, dtype=np.int64),
+                     "i_manu": rng.integers(0, 500, n_item).astype(np.int32)})
+    fact = pa.table({"s_item": rng.integers(0, n_item, n_fact).astype(np.int64),
+                     "s_date": rng.integers(0, 365, n_fact).astype(np.int32),
+                     "s_price": np.round(rng.random(n_fact) * 100, 2)})
+    for name, t, parts in (("item", item, 2), ("fact", fact, 4)):
+        os.makedirs(tmp_path / name)
+        step = (t.num_rows + parts - 1) // parts
+        for i in range(parts):
+            pq.write_table(t.slice(i * step, step), tmp_path / name / f"p{i}.parquet")
+    s = Session(conf={"spark.hyperspace.system.path": str(tmp_path / "idx"),
+                      "spark.hyperspace.index.numBuckets": "16",
+                      "spark.sql.autoBroadcastJoinThreshold": "-1",
+                      "spark.hyperspace.mi.execution.device": "gpu"})
+    hs = Hyperspace(s)
+    f, it = s.read.parquet(str(tmp_path / "fact")), s.read.parquet(str(tmp_path / "item"))
+    hs.createIndex(f, IndexConfig("f_item", ["s_item"], ["s_date", "s_price"]))
+    hs.createIndex(it, IndexConfig("i_idx", ["i_sk"], ["i_manu"]))
+    Hyperspace.enable(s)
+    sel = it.filter(col("i_manu") == 7)
+    q = f.join(sel, f["s_item"] == sel["i_sk"]).select(f["s_date"], f["s_price"], sel["i_sk"])
+    g, c, path = _both(s, q)
+    assert path == "native", s.backend().fallback_reason
+    assert 0 < getattr(s.backend(), "last_join_probes", 0) <= n_item
+    _close(g, c)
+    assert g.num_rows == c.num_rows > 0
