@@ -5,8 +5,8 @@
 //   float64:  any non-finite value, any -0.0, and for every decimal scale k = 0..4 whether
 //             q = rint(x * 10^k) reproduces x bit for bit under the IEEE division the generated
 //             kernels decode with (q / 10^k), whether |q| reaches 2^52, and min/max of q.
-// Per-wave reductions go through DPP/shuffles, then one atomic per wave into a small int64
-// result block.  This replaces the chain of PyTorch elementwise/reduce launches (mul, round,
+// Per-wave reductions go through shuffles, per-block ones through LDS; each block writes one
+// partial record and a one-block pass folds them (no global atomics).  This replaces the chain of PyTorch elementwise/reduce launches (mul, round,
 // div, abs, compare, all, aminmax per scale) and their host round trips with one launch and one
 // 256-byte readback.
 //
@@ -21,6 +21,7 @@ namespace {
 
 enum : int { T_I8 = 0, T_I16, T_I32, T_I64, T_F32, T_F64, T_BOOL, T_U32, T_U64 };
 constexpr int kMaxK = 4;
+constexpr int kProbeBlocks = 1024;   // stage-1 blocks (grid-stride over the column)
 // result block layout (int64)
 enum : int {
   R_ANY = 0, R_NONFINITE = 1, R_NEGZERO = 2, R_IMIN = 3, R_IMAX = 4,
@@ -39,99 +40,101 @@ __device__ inline int64_t load_int(const void* d, int t, int64_t i) {
   }
 }
 
-__device__ inline int64_t wave_min(int64_t v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    const int64_t w = __shfl_xor(v, o);
-    v = w < v ? w : v;
-  }
-  return v;
-}
-
-__device__ inline int64_t wave_max(int64_t v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    const int64_t w = __shfl_xor(v, o);
-    v = w > v ? w : v;
-  }
-  return v;
-}
-
 __constant__ double kPow10[kMaxK + 1] = {1.0, 10.0, 100.0, 1000.0, 10000.0};
 
+// per-field combine of the result block: 0 = or, 1 = min, 2 = max
+__host__ __device__ inline int field_kind(int f) {
+  if (f == R_IMIN) return 1;
+  if (f == R_IMAX) return 2;
+  if (f >= R_K) {
+    const int j = (f - R_K) & 3;
+    return j == 2 ? 1 : (j == 3 ? 2 : 0);
+  }
+  return 0;
+}
+
+__device__ inline int64_t field_init(int f) {
+  const int k = field_kind(f);
+  return k == 1 ? LLONG_MAX : (k == 2 ? LLONG_MIN : 0);
+}
+
+__device__ inline int64_t combine(int kind, int64_t a, int64_t b) {
+  return kind == 1 ? (a < b ? a : b) : (kind == 2 ? (a > b ? a : b) : (a | b));
+}
+
+// Stage 1: every block reduces its grid-stride share to one partial result record (wave
+// shuffles, then the block's waves through LDS) -- no global atomics: with thousands of waves
+// hammering one int64 the atomics serialised (~0.5 ms even for an 864K-row column).
 __global__ __launch_bounds__(256) void hs_compact_probe_kernel(const void* __restrict__ data,
                                                                const uint8_t* __restrict__ valid,
                                                                int64_t n, int type, int maxk,
-                                                               long long* __restrict__ res) {
+                                                               long long* __restrict__ partials) {
+  __shared__ int64_t red[4][R_SIZE];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int lane = threadIdx.x & 63;
-  int any = 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t r[R_SIZE];
+#pragma unroll
+  for (int f = 0; f < R_SIZE; ++f) r[f] = field_init(f);
   if (type != T_F64) {
-    int64_t mn = LLONG_MAX, mx = LLONG_MIN;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
       if (valid && !valid[i]) continue;
       const int64_t v = load_int(data, type, i);
-      mn = v < mn ? v : mn;
-      mx = v > mx ? v : mx;
-      any = 1;
+      r[R_IMIN] = v < r[R_IMIN] ? v : r[R_IMIN];
+      r[R_IMAX] = v > r[R_IMAX] ? v : r[R_IMAX];
+      r[R_ANY] = 1;
     }
-    mn = wave_min(mn);
-    mx = wave_max(mx);
-    const bool a = __any(any);
-    if (lane == 0 && a) {
-      atomicMin(&res[R_IMIN], (long long)mn);
-      atomicMax(&res[R_IMAX], (long long)mx);
-      atomicOr((unsigned long long*)&res[R_ANY], 1ull);
-    }
-    return;
-  }
-  const double* x = (const double*)data;
-  int nonfinite = 0, negzero = 0;
-  int inexact[kMaxK + 1] = {0}, over[kMaxK + 1] = {0};
-  int64_t qmin[kMaxK + 1], qmax[kMaxK + 1];
-#pragma unroll
-  for (int k = 0; k <= kMaxK; ++k) {
-    qmin[k] = LLONG_MAX;
-    qmax[k] = LLONG_MIN;
-  }
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    if (valid && !valid[i]) continue;
-    const double v = x[i];
-    any = 1;
-    if (!isfinite(v)) {
-      nonfinite = 1;
-      continue;
-    }
-    if (v == 0.0 && signbit(v)) negzero = 1;
-#pragma unroll
-    for (int k = 0; k <= kMaxK; ++k) {
-      if (k > maxk) break;
-      const double q = rint(v * kPow10[k]);
-      if (fabs(q) >= 4503599627370496.0) {   // 2^52
-        over[k] = 1;
+  } else {
+    const double* x = (const double*)data;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      if (valid && !valid[i]) continue;
+      const double v = x[i];
+      r[R_ANY] = 1;
+      if (!isfinite(v)) {
+        r[R_NONFINITE] = 1;
         continue;
       }
-      const double back = q / kPow10[k];   // IEEE division, as the kernels decode
-      if (__double_as_longlong(back) != __double_as_longlong(v)) inexact[k] = 1;
-      const int64_t qi = (int64_t)q;
-      qmin[k] = qi < qmin[k] ? qi : qmin[k];
-      qmax[k] = qi > qmax[k] ? qi : qmax[k];
-    }
-  }
-  const bool a = __any(any), nf = __any(nonfinite), nz = __any(negzero);
-  if (lane == 0 && a) atomicOr((unsigned long long*)&res[R_ANY], 1ull);
-  if (lane == 0 && nf) atomicOr((unsigned long long*)&res[R_NONFINITE], 1ull);
-  if (lane == 0 && nz) atomicOr((unsigned long long*)&res[R_NEGZERO], 1ull);
+      if (v == 0.0 && signbit(v)) r[R_NEGZERO] = 1;
 #pragma unroll
-  for (int k = 0; k <= kMaxK; ++k) {
-    if (k > maxk) break;
-    const bool ie = __any(inexact[k]), ov = __any(over[k]);
-    const int64_t mn = wave_min(qmin[k]), mx = wave_max(qmax[k]);
-    if (lane == 0) {
-      if (ie) atomicOr((unsigned long long*)&res[R_K + 4 * k], 1ull);
-      if (ov) atomicOr((unsigned long long*)&res[R_K + 4 * k + 1], 1ull);
-      if (mn != LLONG_MAX) atomicMin(&res[R_K + 4 * k + 2], (long long)mn);
-      if (mx != LLONG_MIN) atomicMax(&res[R_K + 4 * k + 3], (long long)mx);
+      for (int k = 0; k <= kMaxK; ++k) {
+        if (k > maxk) break;
+        const double q = rint(v * kPow10[k]);
+        if (fabs(q) >= 4503599627370496.0) {   // 2^52
+          r[R_K + 4 * k + 1] = 1;
+          continue;
+        }
+        const double back = q / kPow10[k];   // IEEE division, as the kernels decode
+        if (__double_as_longlong(back) != __double_as_longlong(v)) r[R_K + 4 * k] = 1;
+        const int64_t qi = (int64_t)q;
+        r[R_K + 4 * k + 2] = qi < r[R_K + 4 * k + 2] ? qi : r[R_K + 4 * k + 2];
+        r[R_K + 4 * k + 3] = qi > r[R_K + 4 * k + 3] ? qi : r[R_K + 4 * k + 3];
+      }
     }
   }
+#pragma unroll
+  for (int f = 0; f < R_SIZE; ++f) {
+    const int kind = field_kind(f);
+    int64_t v = r[f];
+    for (int o = 32; o > 0; o >>= 1) v = combine(kind, v, __shfl_xor(v, o));
+    if (lane == 0) red[w][f] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < R_SIZE) {
+    const int f = threadIdx.x, kind = field_kind(f);
+    int64_t v = red[0][f];
+    for (int ww = 1; ww < (int)(blockDim.x >> 6); ++ww) v = combine(kind, v, red[ww][f]);
+    partials[(int64_t)blockIdx.x * R_SIZE + f] = v;
+  }
+}
+
+// Stage 2: one thread per field folds the blocks' partial records into the result block.
+__global__ __launch_bounds__(64) void hs_compact_probe_final_kernel(
+    const long long* __restrict__ partials, int nblocks, long long* __restrict__ res) {
+  const int f = threadIdx.x;
+  if (f >= R_SIZE) return;
+  const int kind = field_kind(f);
+  int64_t v = field_init(f);
+  for (int b = 0; b < nblocks; ++b) v = combine(kind, v, partials[(int64_t)b * R_SIZE + f]);
+  res[f] = v;
 }
 
 template <typename C>
@@ -165,14 +168,20 @@ extern "C" {
 
 int hs_compact_result_size() { return R_SIZE; }
 
-// res: R_SIZE int64s, initialised by the caller (mins INT64_MAX, maxes INT64_MIN, flags 0)
+// partial records of stage 1 (int64 elements of the caller's workspace)
+int64_t hs_compact_probe_ws_elems() { return (int64_t)kProbeBlocks * R_SIZE; }
+
+// res: R_SIZE int64s (written entirely); ws: hs_compact_probe_ws_elems() int64s
 int hs_compact_probe(const void* data, const uint8_t* valid, int64_t n, int type, int maxk,
-                     int64_t* res, void* stream) {
-  if (n <= 0) return 0;
+                     int64_t* res, int64_t* ws, void* stream) {
   if (maxk < 0 || maxk > kMaxK) return -1;
   (void)hipGetLastError();
-  hipLaunchKernelGGL(hs_compact_probe_kernel, dim3(grid_for(n)), dim3(256), 0,
-                     (hipStream_t)stream, data, valid, n, type, maxk, (long long*)res);
+  int64_t b = (n + 255) / 256;
+  const int nb = (int)(b < 1 ? 1 : (b > kProbeBlocks ? kProbeBlocks : b));
+  hipLaunchKernelGGL(hs_compact_probe_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, data,
+                     valid, n, type, maxk, (long long*)ws);
+  hipLaunchKernelGGL(hs_compact_probe_final_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     (const long long*)ws, nb, (long long*)res);
   return (int)hipGetLastError();
 }
 

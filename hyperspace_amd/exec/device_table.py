@@ -61,7 +61,8 @@ def h2d(a: np.ndarray, device):
 
 
 class DeviceColumn:
-    __slots__ = ("data", "valid", "atype", "dictionary", "offsets", "chars", "compact", "dupkeys")
+    __slots__ = ("data", "valid", "atype", "dictionary", "offsets", "chars", "compact", "dupkeys",
+                 "hs_transient")
 
     def __init__(self, data, valid, atype: pa.DataType, dictionary: Optional[pa.Array] = None,
                  offsets=None, chars=None):
@@ -73,6 +74,7 @@ class DeviceColumn:
         self.chars = chars
         self.compact = False  # exec.encoding.compact_of: False = not computed, None = n/a
         self.dupkeys = None   # exec.jit.key_has_dups: None = not computed
+        self.hs_transient = False   # a per-query intermediate (never compacted)
 
     def __len__(self):
         return int(self.data.shape[0])

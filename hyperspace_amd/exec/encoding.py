@@ -68,8 +68,15 @@ def encode(col) -> Optional[Compact]:
     return _encode_torch(col)
 
 
+class DeviceColumnView:
+    """(data, valid, hs_type) triple in the shape ``kernels.compact_probe`` reads."""
+    __slots__ = ("data", "valid", "hs_type")
+
+    def __init__(self, data, valid, hs_type):
+        self.data, self.valid, self.hs_type = data, valid, hs_type
+
+
 def _encode_device(col) -> Optional[Compact]:
-    import numpy as np
     import torch
     L = NL.lib()
     t = col.hs_type
@@ -78,17 +85,8 @@ def _encode_device(col) -> Optional[Compact]:
     if n == 0:
         return None
     valid = col.valid.contiguous() if col.valid is not None else None
-    rs = int(L.hs_compact_result_size())
-    init = np.zeros(rs, dtype=np.int64)
-    imax, imin = np.iinfo(np.int64).max, np.iinfo(np.int64).min
-    init[3], init[4] = imax, imin
-    for k in range(_MAX_SCALE_DIGITS + 1):
-        init[5 + 4 * k + 2], init[5 + 4 * k + 3] = imax, imin
-    res = torch.from_numpy(init).to(d.device)
-    NL.check(L.hs_compact_probe(d.data_ptr(), valid.data_ptr() if valid is not None else None,
-                                n, t, _MAX_SCALE_DIGITS, res.data_ptr(), NL.stream_ptr()),
-             "hs_compact_probe")
-    r = res.cpu().numpy()
+    from ..ops import kernels as K
+    r = K.compact_probe(DeviceColumnView(d, valid, t), _MAX_SCALE_DIGITS)
     if not r[0]:
         return None
     k_used, scale = 0, None

@@ -584,6 +584,8 @@ class GpuBackend:
             perm = K.sort_permutation(kcols, extra_leading=(bucket, 16))
         names = list(cols.keys())
         gathered = K.gather_columns([cols[i] for i in names], perm)
+        for c in gathered:
+            c.hs_transient = True       # built for this query only (not the cached repartition)
         off_host = np.concatenate([[0], np.cumsum(counts.cpu().numpy())]).astype(np.int64)
         table = DeviceTable({f"c{i}": c for i, c in zip(names, gathered)}, n,
                             torch.from_numpy(off_host).to(self.device), off_host)
@@ -852,6 +854,7 @@ class GpuBackend:
         rg = K.gather_columns([right.col(a) for a in rattrs], orr)
         cols = {}
         for a, c in list(zip(lattrs, lg)) + list(zip(rattrs, rg)):
+            c.hs_transient = True
             cols[key(a)] = c
         n = int(ol.numel())
         import torch
@@ -1148,6 +1151,8 @@ class GpuBackend:
         from .encoding import compact_of
         out = {}
         for s, c in descs.items():
+            if getattr(c, "hs_transient", False):
+                continue    # a per-query intermediate: analysing it costs more than it saves
             enc = compact_of(c)
             if enc is not None:
                 out[s] = enc

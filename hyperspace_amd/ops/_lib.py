@@ -184,7 +184,8 @@ def lib():
     _sig(L.hs_xch_unpack, I, P, I, I64, P)
     _sig(L.hs_probe_ranges, I, P, P, P, P, I, P, P, P, P)
     _sig(L.hs_compact_result_size, I)
-    _sig(L.hs_compact_probe, I, P, P, I64, I, I, P, P)
+    _sig(L.hs_compact_probe, I, P, P, I64, I, I, P, P, P)
+    _sig(L.hs_compact_probe_ws_elems, I64)
     _sig(L.hs_compact_encode, I, P, P, I64, I, I, I64, I64, I, P, P)
     _sig(L.hs_snappy_max_compressed, I64, I64)
     _sig(L.hs_snappy_chunk_bytes, I)

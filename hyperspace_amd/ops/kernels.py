@@ -84,21 +84,25 @@ def murmur3_hash(cols):
 # ------------------------------------------------------------------------------------------------
 # K4: radix sort -> permutation
 # ------------------------------------------------------------------------------------------------
-def _int_range(col):
-    """(any valid, min, max) of an integer column over valid rows: one hs_compact_probe launch
-    (csrc/kernels/compact.hip) and one 256-byte readback."""
+def compact_probe(col, maxk: int):
+    """Result block of ``hs_compact_probe`` (csrc/kernels/compact.hip) for a device column, as
+    a host int64 array: one two-stage reduction launch pair and one small readback."""
     torch = _torch()
-    import numpy as np
     L = NL.lib()
-    init = np.zeros(int(L.hs_compact_result_size()), dtype=np.int64)
-    init[3], init[4] = np.iinfo(np.int64).max, np.iinfo(np.int64).min
-    res = torch.from_numpy(init).to(col.data.device)
+    dev = col.data.device
+    res = torch.empty(int(L.hs_compact_result_size()), dtype=torch.int64, device=dev)
+    ws = torch.empty(int(L.hs_compact_probe_ws_elems()), dtype=torch.int64, device=dev)
     d = col.data.contiguous()
     v = col.valid.contiguous() if col.valid is not None else None
     NL.check(L.hs_compact_probe(d.data_ptr(), v.data_ptr() if v is not None else None, d.numel(),
-                                col.hs_type, 0, res.data_ptr(), NL.stream_ptr()),
-             "hs_compact_probe")
-    r = res.cpu().numpy()
+                                col.hs_type, maxk, res.data_ptr(), ws.data_ptr(),
+                                NL.stream_ptr()), "hs_compact_probe")
+    return res.cpu().numpy()
+
+
+def _int_range(col):
+    """(any valid, min, max) of an integer column over valid rows (``compact_probe``)."""
+    r = compact_probe(col, 0)
     return bool(r[0]), int(r[3]), int(r[4])
 
 
