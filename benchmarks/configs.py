@@ -232,8 +232,14 @@ def config_hybrid(args):
     plan = _q3(li, od, 0).queryExecution.executed_plan.tree_string()
     for i in range(2):
         step(1000 + i)
+    from hyperspace_amd.utils.tracing import TRACER, format_report
+    TRACER.reset()
     el_h = _timed_loop(step, args.steps, args.device)
     path_h = getattr(s.backend(), "last_path", None)
+    if TRACER.profile:   # HS_PROFILE=1: where the Hybrid Scan steps spend their time
+        print("[hybrid] hybrid-scan stage profile\n" + format_report(TRACER.report()),
+              file=sys.stderr, flush=True)
+        print(plan, file=sys.stderr, flush=True)
     hyb = (_q6(li, 0).collect()[0][0], _rows(_q3(li, od, 0)))
     tr = time.perf_counter()
     for name in ("li_orderkey", "ord_orderkey", "li_shipdate"):
@@ -243,7 +249,6 @@ def config_hybrid(args):
     li, od = s.read.parquet(lpath), s.read.parquet(opath)
     for i in range(2):
         step(2000 + i)
-    from hyperspace_amd.utils.tracing import TRACER, format_report
     TRACER.reset()
     be = s.backend()
     cache0 = (be.cache.hits, be.cache.misses) if hasattr(be, "cache") else (0, 0)

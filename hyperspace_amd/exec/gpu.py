@@ -488,10 +488,19 @@ class GpuBackend:
         width = {NL.I8: 8, NL.I16: 16, NL.I32: 32, NL.I64: 64}.get(lc.hs_type)
         if width is None or rc.hs_type not in (NL.I8, NL.I16, NL.I32, NL.I64):
             return None
+        # a pair whose filtered side turned out not selective twice is not probed again (the
+        # selection costs a scan of the right side and a host sync per query)
+        pk_ = (id(left.table), id(right.table))
+        misses = self.__dict__.setdefault("_probe_misses", {})
+        if misses.get(pk_, 0) >= 2:
+            return None
         with stage("join.probe_select"):
             rows = self._selected_rows(right)
             npass = int(rows.numel())
         if npass * self.PROBE_RATIO > nl or npass > self.PROBE_MAX:
+            if len(misses) > 4096:
+                misses.clear()
+            misses[pk_] = misses.get(pk_, 0) + 1
             return None
         with stage("join.probe_ranges"):
             g = K.gather_columns([rc], rows)[0]
