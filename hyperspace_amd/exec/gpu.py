@@ -528,6 +528,40 @@ class GpuBackend:
                 return z, z.clone(), torch.zeros(0, dtype=torch.int32, device=self.device)
             return K.probe_ranges(lc, left.table.bucket_offsets, pb, pk)
 
+    def _domain_pruned_ranges(self, left: DRel, right: DRel, lk, rk):
+        """Left ranges restricted to the right join key's [min, max] when that domain is
+        narrower than the left's (a zone-map join filter on the sorted left key): e.g. the
+        Hybrid Scan pair (index lineitem, appended orders) whose keys are disjoint costs a range
+        search instead of a scan.  None when the left has its own key ranges, the shape is not
+        integer / resident, or the domains do not prune."""
+        if left.parts or right.parts or not left.bucketed or not left.sort_attrs:
+            return None
+        if self._range_spec(left, left.conds) is not None:
+            return None
+        lc, rc = left.col(lk), right.col(rk)
+        if lc.is_float or rc.is_float or lc.dictionary is not None or \
+                rc.dictionary is not None or lc.hs_transient or rc.hs_transient:
+            return None
+        width = {NL.I8: 8, NL.I16: 16, NL.I32: 32, NL.I64: 64}.get(lc.hs_type)
+        if width is None or rc.hs_type not in (NL.I8, NL.I16, NL.I32, NL.I64):
+            return None
+        llo, lspan = self._local_domain(lc)
+        rlo, rspan = self._local_domain(rc)
+        if lspan == 0:
+            return None
+        lhi, rhi = llo + lspan - 1, rlo + rspan - 1
+        if rspan > 0 and rlo <= llo and rhi >= lhi:
+            return None                     # the right covers the left's keys: nothing to prune
+        import torch
+        tmin, tmax = -(1 << (width - 1)), (1 << (width - 1)) - 1
+        if rspan == 0 or rlo > min(lhi, tmax) or rhi < max(llo, tmin):
+            z = torch.zeros(0, dtype=torch.int64, device=self.device)
+            return z, z.clone(), torch.zeros(0, dtype=torch.int32, device=self.device)
+        lo = K.sortable_image(max(rlo, tmin), lc.hs_type)
+        hi = K.sortable_image(min(rhi, tmax), lc.hs_type)
+        with stage("join.domain_prune"):
+            return K.range_search(lc, left.table.bucket_offsets, None, lo, True, hi, True)
+
     def _to_arrow(self, r: DRel, out_attrs: List[E.Attribute]) -> pa.Table:
         if r.parts:  # rows of a bucket union: each part's rows, concatenated
             return pa.concat_tables([self._to_arrow(x, out_attrs) for x in r.parts])
@@ -840,6 +874,8 @@ class GpuBackend:
         out_attrs = list(p.output)
         implied: set = set()
         probed = self._probe_ranges(left, right, lk, rk)
+        if probed is None:
+            probed = self._domain_pruned_ranges(left, right, lk, rk)
         if probed is not None:
             rstart, rlen, rbk = probed
         else:
@@ -1220,6 +1256,8 @@ class GpuBackend:
             left, right, lk, rk = right, left, rk, lk
         implied: set = set()
         probed = self._probe_ranges(left, right, lk, rk)
+        if probed is None:
+            probed = self._domain_pruned_ranges(left, right, lk, rk)
         if probed is not None:
             rstart, rlen, rbk = probed
         else:

@@ -336,3 +336,36 @@ def test_selective_dimension_join_probes_key_runs(tmp_path, device):
     assert 0 < getattr(s.backend(), "last_join_probes", 0) <= n_item
     _close(g, c)
     assert g.num_rows == c.num_rows > 0
+
+
+def test_join_key_domain_pruning_matches_oracle(tmp_path, device):
+    """The right side's join keys cover only the top of the left's key domain (as appended
+    orders do in a Hybrid Scan): the left ranges are cut to that domain before the join, and
+    the aggregate and the rows still match the host oracle."""
+    rng = np.random.default_rng(5)
+    n = 1_200_000
+    left = pa.table({"k": rng.integers(0, 1_000_000, n).astype(np.int64),
+                     "v": np.round(rng.random(n) * 10, 2)})
+    right = pa.table({"rk": np.arange(900_000, 1_100_000, dtype=np.int64),
+                      "w": rng.integers(0, 5, 200_000).astype(np.int32)})
+    for name, t in (("l", left), ("r", right)):
+        os.makedirs(tmp_path / name)
+        pq.write_table(t, tmp_path / name / "p0.parquet")
+    s = Session(conf={"spark.hyperspace.system.path": str(tmp_path / "idx"),
+                      "spark.hyperspace.index.numBuckets": "16",
+                      "spark.sql.autoBroadcastJoinThreshold": "-1",
+                      "spark.hyperspace.mi.execution.device": "gpu"})
+    hs = Hyperspace(s)
+    lt, rt = s.read.parquet(str(tmp_path / "l")), s.read.parquet(str(tmp_path / "r"))
+    hs.createIndex(lt, IndexConfig("l_k", ["k"], ["v"]))
+    hs.createIndex(rt, IndexConfig("r_k", ["rk"], ["w"]))
+    Hyperspace.enable(s)
+    j = lt.join(rt, lt["k"] == rt["rk"])
+    q = j.agg(sum_(col("v")).alias("s"), count("*").alias("n"))
+    g, c, path = _both(s, q, sort=False)
+    assert path == "native", s.backend().fallback_reason
+    _close(g, c)
+    rows = j.filter(col("w") == 3).select(lt["k"], lt["v"])
+    g, c, path = _both(s, rows)
+    assert path == "native", s.backend().fallback_reason
+    _close(g, c)
