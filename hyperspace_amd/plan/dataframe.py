@@ -6,6 +6,7 @@ rules when enabled) -> physical planner -> executor (HIP device executor or the 
 """
 from __future__ import annotations
 
+import weakref
 from typing import List, Sequence
 
 import pyarrow as pa
@@ -15,6 +16,8 @@ from . import expressions as E
 from . import logical as L
 from .column import Column, col
 from .parser import parse_expression
+
+_RESOLVED: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 
 
 class Row(tuple):
@@ -69,7 +72,21 @@ class DataFrame:
     def _resolve_name(self, name: str, plan: L.LogicalPlan = None) -> E.Attribute:
         plan = plan or self.plan
         cs = self.session.case_sensitive
-        matches = [a for a in plan.output if (a.name == name if cs else a.name.lower() == name.lower())]
+        # per-plan memo: a serving loop resolves the same names against the same base relation
+        # on every query (plans are immutable; the weak map dies with the plan)
+        memo = _RESOLVED.get(plan)
+        if memo is None:
+            memo = _RESOLVED[plan] = {}
+        hit = memo.get((name, cs))
+        if hit is not None:
+            return hit
+        if cs:
+            matches = [a for a in plan.output if a.name == name]
+        else:
+            lname = name.lower()
+            matches = [a for a in plan.output if a.name.lower() == lname]
+        if matches:
+            memo[(name, cs)] = matches[0]
         if not matches:
             raise HyperspaceException(
                 f"cannot resolve '{name}' given input columns: [{', '.join(a.name for a in plan.output)}]")

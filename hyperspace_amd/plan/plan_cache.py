@@ -65,7 +65,35 @@ def _own(obj) -> bool:
     return type(obj).__module__.startswith(_PLAN_MODULES)
 
 
+_PRIMS = (str, int, float, bool, type(None))
+_SKIP = ("_cache", "_hs_")
+_OWN: Dict[type, bool] = {}
+_FIELDS: Dict[tuple, tuple] = {}
+
+
+def _own_type(t: type) -> bool:
+    o = _OWN.get(t)
+    if o is None:
+        o = _OWN[t] = t.__module__.startswith(_PLAN_MODULES) and not issubclass(t, L.HadoopFsRelation)
+    return o
+
+
+def _fields(d: dict) -> tuple:
+    """Sorted fingerprinted field names of a node's ``__dict__`` (memoized by key set)."""
+    ks = tuple(d)
+    f = _FIELDS.get(ks)
+    if f is None:
+        # memoized derived state (_cache*, _hs_*) is not part of the node's meaning
+        f = _FIELDS[ks] = tuple(sorted(k for k in ks if not k.startswith(_SKIP)))
+    return f
+
+
 def _fp(v, ctx: _Ctx):
+    t = type(v)
+    if t in _PRIMS:
+        return v
+    if t is tuple or t is list:
+        return tuple([_fp(x, ctx) for x in v])
     if isinstance(v, E.Literal):
         ctx.lits.append(v)
         return ("L", str(v.dtype), v.value is None)
@@ -73,7 +101,7 @@ def _fp(v, ctx: _Ctx):
         raise _NotCacheable("IN list (OptimizeIn depends on its values)")
     if isinstance(v, E.Attribute):
         return ("A", v.name, str(v.dtype), v.nullable, ctx.eid(v.expr_id), v.qualifier)
-    if v is None or isinstance(v, (str, int, float, bool)):
+    if isinstance(v, _PRIMS):
         return v
     if isinstance(v, (list, tuple)):
         return tuple(_fp(x, ctx) for x in v)
@@ -83,19 +111,16 @@ def _fp(v, ctx: _Ctx):
         return tuple(sorted((str(k), _fp(x, ctx)) for k, x in v.items()))
     if isinstance(v, (pa.DataType, pa.Schema, pa.Field)):
         return str(v)
-    if isinstance(v, L.HadoopFsRelation) or not _own(v):
+    if not _own_type(t):
         # relations, file indexes, tables: by identity (the entry keeps them alive)
         ctx.refs.append(v)
         return ("O", id(v))
+    d = vars(v)
     items = []
-    for k, x in sorted(vars(v).items()):
-        if k == "expr_id":
-            items.append((k, ctx.eid(x)))
-        elif k.startswith("_cache") or k.startswith("_hs_"):
-            continue   # memoized derived state, not part of the node's meaning
-        else:
-            items.append((k, _fp(x, ctx)))
-    return (type(v).__name__, tuple(items))
+    for k in _fields(d):
+        x = d[k]
+        items.append((k, ctx.eid(x)) if k == "expr_id" else (k, _fp(x, ctx)))
+    return (t.__name__, tuple(items))
 
 
 def _iter_literals(v, out: List[E.Literal], seen: set):
@@ -165,11 +190,22 @@ def _subst(v, m: Dict[int, E.Literal], hot: set, memo: Dict[int, object]):
     elif isinstance(v, dict):
         out = {kk: _subst(x, m, hot, memo) for kk, x in v.items()}
     else:
-        out = copy.copy(v)
-        for kk, x in vars(v).items():
-            nx = _subst(x, m, hot, memo)
-            if nx is not x:
-                object.__setattr__(out, kk, nx)
+        d = vars(v)
+        if type(v).__reduce_ex__ is object.__reduce_ex__ and not hasattr(v, "__slots__"):
+            # plain node: shallow copy without copy.copy's reduce protocol (hot on cache hits)
+            out = object.__new__(type(v))
+            nd = out.__dict__
+            nd.update(d)
+            for kk, x in d.items():
+                nx = _subst(x, m, hot, memo)
+                if nx is not x:
+                    nd[kk] = nx
+        else:
+            out = copy.copy(v)
+            for kk, x in d.items():
+                nx = _subst(x, m, hot, memo)
+                if nx is not x:
+                    object.__setattr__(out, kk, nx)
     memo[k] = out
     return out
 
