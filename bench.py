@@ -311,6 +311,7 @@ def main():
             prof.disable()
             buf = io.StringIO()
             pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(40)
+            pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(30)
             log(rank, buf.getvalue())
         if TRACER.profile:
             log(rank, f"[bench] {mode} stage profile (timed steps)\n" +
