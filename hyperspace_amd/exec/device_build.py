@@ -393,7 +393,7 @@ def _dictionary_codes(chunks, device, dist) -> DeviceColumn:
         m = len(ch)
         if m:
             remap = pc.index_in(d, value_set=gdict).to_numpy(zero_copy_only=False)
-            remap_d = torch.from_numpy(np.asarray(remap, dtype=np.int32)).to(device)
+            remap_d = torch.from_numpy(np.array(remap, dtype=np.int32)).to(device)
             idx = np.asarray(ch.indices.fill_null(0).to_numpy(zero_copy_only=False),
                              dtype=np.int64)
             idx_d = torch.from_numpy(idx).to(device, non_blocking=False)
