@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import copy
 import threading
+import weakref
 from collections import OrderedDict
 from typing import Dict, List, Optional, Tuple
 
@@ -115,6 +116,32 @@ def _fp(v, ctx: _Ctx):
         # relations, file indexes, tables: by identity (the entry keeps them alive)
         ctx.refs.append(v)
         return ("O", id(v))
+    if t is L.LogicalRelation:
+        return _fp_leaf(v, ctx)
+    return _fp_node(v, t, ctx)
+
+
+# A serving loop builds every query over the same base relation objects: their fingerprint is
+# kept in local attribute numbering and re-mapped into the query's numbering on reuse.
+_LEAF_FP: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def _fp_leaf(v, ctx: _Ctx):
+    hit = _LEAF_FP.get(v)
+    if hit is None:
+        lctx = _Ctx()
+        lfp = _fp_node(v, type(v), lctx)
+        if lctx.lits:   # literals must reach the caller's list in order: no memo
+            ctx.lits.extend(lctx.lits)
+            ctx.refs.extend(lctx.refs)
+            return ("LR", lfp, tuple(ctx.eid(x) for x in lctx.ids))
+        hit = _LEAF_FP[v] = (lfp, tuple(lctx.ids), tuple(lctx.refs))
+    lfp, ids, refs = hit
+    ctx.refs.extend(refs)
+    return ("LR", lfp, tuple([ctx.eid(x) for x in ids]))
+
+
+def _fp_node(v, t: type, ctx: _Ctx):
     d = vars(v)
     items = []
     for k in _fields(d):
