@@ -113,3 +113,23 @@ def test_in_lists_are_not_parameterized(data):
     t = df.to_arrow()
     assert a[0][0] == sum(1 for x in t.column("s").to_pylist() if x in ("s1", "s2"))
     assert b[0][0] == sum(1 for x in t.column("s").to_pylist() if x == "s3")
+
+
+def test_base_relation_fingerprint_memo(data, tmp_path):
+    """Base-relation fingerprints are memoized in local attribute numbering: the same relation
+    with new literals keys the same entry, a join over two memoized relations keys its own
+    shape, and a second read of the same files (new attribute ids, new relation object) keys its own
+    entry."""
+    from hyperspace_amd.plan.plan_cache import _Ctx, _fp
+    s, _, df, od = data
+    k1, k2 = _fp(_filter_q(df, 1).plan, _Ctx()), _fp(_filter_q(df, 2).plan, _Ctx())
+    assert k1 == k2
+    again = s.read.parquet(str(tmp_path / "t"))
+    assert _fp(_filter_q(again, 1).plan, _Ctx()) != k1
+    j1 = _fp(_join_q(df, od, 1).plan, _Ctx())
+    j2 = _fp(_join_q(df, od, 3).plan, _Ctx())
+    assert j1 == j2 and j1 != k1
+    # cached plans still give the rows of planning from scratch
+    got = _filter_q(df, 4).collect()
+    s.conf.set("spark.hyperspace.mi.planCache.enabled", "false")
+    assert sorted(got) == sorted(_filter_q(df, 4).collect())
