@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <exception>
 #include <string>
 #include <vector>
 
@@ -136,12 +137,17 @@ bool inflate_raw(const uint8_t* in, size_t n, std::vector<uint8_t>& out) {
   z_stream zs;
   std::memset(&zs, 0, sizeof(zs));
   if (inflateInit2(&zs, -15) != Z_OK) return false;   // raw deflate (RFC 1951), as Avro writes
-  out.resize(std::max<size_t>(n * 4, 4096));
+  // DEFLATE expands at most ~1032:1: a larger output is a corrupt or hostile block, not data
+  const size_t cap = std::min<size_t>(n * 1032 + 4096, (size_t)1 << 32);
+  out.resize(std::min<size_t>(std::max<size_t>(n * 4, 4096), cap));
   zs.next_in = const_cast<Bytef*>(in);
   zs.avail_in = (uInt)n;
   int rc;
   do {
-    if (zs.total_out == out.size()) out.resize(out.size() * 2);
+    if (zs.total_out == out.size()) {
+      if (out.size() >= cap) { rc = Z_DATA_ERROR; break; }
+      out.resize(std::min(out.size() * 2, cap));
+    }
     zs.next_out = out.data() + zs.total_out;
     zs.avail_out = (uInt)(out.size() - zs.total_out);
     rc = inflate(&zs, Z_NO_FLUSH);
@@ -165,6 +171,9 @@ bool snappy_block(const uint8_t* in, size_t n, std::vector<uint8_t>& out) {
     if (!(b & 0x80)) break;
     shift += 7;
   }
+  // a Snappy tag of k bytes emits at most 64 bytes (copy-2: 3 bytes -> 64), so a preamble
+  // claiming more than ~32x the block is corrupt: never allocate from an untrusted length
+  if (len > (uint64_t)n * 32 + 64) return false;
   out.resize(len);
   if (hs_pq_snappy_decompress(in, (int64_t)n, out.data(), (int64_t)len) != (int64_t)len)
     return false;
@@ -182,6 +191,8 @@ extern "C" {
 void* hs_avro_decode(const uint8_t* buf, int64_t len, const uint8_t* sync, int32_t codec,
                      int32_t nfields, const int32_t* types, const int32_t* null_branch) {
   Result* res = new Result();
+  // no C++ exception may cross the C ABI (ctypes): allocation failures become res->err
+  try {
   res->cols.resize((size_t)nfields);
   for (int f = 0; f < nfields; ++f) {
     res->cols[f].type = types[f];
@@ -220,6 +231,11 @@ void* hs_avro_decode(const uint8_t* buf, int64_t len, const uint8_t* sync, int32
     }
     Reader r{data, data + dlen};
     if (!decode_records(r, count, *res)) break;
+  }
+  } catch (const std::exception& e) {
+    res->err = std::string("avro decode: ") + e.what();
+  } catch (...) {
+    res->err = "avro decode: unknown error";
   }
   return res;
 }

@@ -412,15 +412,19 @@ def _footer_info(path: str, names: List[str]):
     md = pq.ParquetFile(P.to_local(path)).metadata
     want = set(names)
     maybe = set()
+    seen = set()
     for g in range(md.num_row_groups):
         rg = md.row_group(g)
         for c in range(rg.num_columns):
             cc = rg.column(c)
             nm = cc.path_in_schema
             if nm in want:
+                seen.add(nm)
                 st = cc.statistics
                 if st is None or not st.has_null_count or st.null_count > 0:
                     maybe.add(nm)
+    # not covered by this footer (partition columns, columns missing from the file): unknown
+    maybe |= want - seen
     return md.num_rows, maybe
 
 
@@ -467,6 +471,10 @@ def _upload_parquet(rel, my_files, columns, indexed, lineage_ids, device, dist, 
     if xs is not None and not any(is_string(f.type) for f in schema):
         fixed = [f.name for f in schema]
         may = set().union(*[m for _, m in infos]) if infos else set()
+        # partition columns are not in the Parquet footers and may be null
+        # (__HIVE_DEFAULT_PARTITION__): a mask that appeared mid-upload on one rank would send
+        # one column more than its peers in the next collective batch
+        may |= {n for n in fixed if n in part_names or n not in rel.data_schema.names}
         agreed = dist.agree_any([n in may for n in fixed])
         nullable = {n for n, a in zip(fixed, agreed) if a}
         on_batch = (lambda cols, lo, hi: xs.batch(cols, names, lo, hi))

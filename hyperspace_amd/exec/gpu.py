@@ -43,6 +43,14 @@ log = logging.getLogger(__name__)
 Unsupported = CP.Unsupported
 MAX_GROUPS_SCAN = 3000
 MAX_GROUPS_JOIN = 2400
+# a grouped aggregate with more groups than this returns candidates of ORDER BY ... LIMIT from
+# the device top-k instead of copying every group to the host
+TOPK_MIN_GROUPS = 4096
+
+
+class _NeedHash(CP.Unsupported):
+    """The dense (LDS) grouped aggregate does not apply; run the hash-mode aggregate
+    (exec/hash_agg.py) instead of falling back to the host."""
 
 
 class DRel:
@@ -99,6 +107,8 @@ class GpuBackend:
         self._unions: Dict[tuple, tuple] = {}     # string join keys: dictionary pair -> union
         self._groups_agreed = False
         self.graphs = GraphCache()
+        from .hash_agg import TablePool
+        self.htables = TablePool()
         # engine start: size the pinned staging pool once (pinning GBs is the slow part of a
         # cold build), as the HBM side is sized by the device table cache
         from .staging import pinned_pool
@@ -172,22 +182,47 @@ class GpuBackend:
         return QueryFuture(self, plan, lambda: out, "fallback", str(e), t0)
 
     def _collect_native(self, plan: X.SparkPlan):
-        """``finish() -> pa.Table`` of a plan (aggregates deferred, row results computed now)."""
+        """``finish() -> pa.Table`` of a plan (aggregates deferred, row results computed now).
+        ``[CollectLimit] <- [Sort(global) <- Exchange(single)] <- plan``: a grouped aggregate
+        below takes the ORDER BY / LIMIT into its device top-k; the final ordering of the (few)
+        result rows runs on the host."""
         limit = None
+        order = None
         if isinstance(plan, X.CollectLimitExec):
             limit = plan.n
             plan = plan.child
+        if isinstance(plan, X.SortExec) and plan.global_sort:
+            order = plan.order
+            plan = plan.child
+            if isinstance(plan, X.ShuffleExchangeExec) and \
+                    isinstance(plan.partitioning, X.SinglePartition):
+                plan = plan.child
+        out_attrs = list(plan.output)
         agg = self._match_agg(plan)
         if agg is not None:
-            finish = self._exec_agg(*agg)
+            finish = self._exec_agg(*agg, order=order, limit=limit)
         else:
             rel = self._rel(plan)
             t = self._to_arrow(rel, plan.output)
             t = self._gather_ranks(t)
             finish = (lambda: t)
-        if limit is None:
+        if order is None and limit is None:
             return finish
-        return lambda: finish().slice(0, limit)
+
+        def ordered() -> pa.Table:
+            t = finish()
+            if order is not None:
+                t = self._sort_rows(t, out_attrs, order)
+            return t if limit is None else t.slice(0, limit)
+        return ordered
+
+    def _sort_rows(self, t: pa.Table, attrs, order) -> pa.Table:
+        """Host sort of a (small) result table by SortOrders over its output attributes."""
+        if t.num_rows <= 1:
+            return t
+        names = t.column_names
+        keyed = t.rename_columns([key(a) for a in attrs])
+        return self.cpu._sort_table(keyed, order).rename_columns(names)
 
     # ------------------------------------------------------------------------------------------
     # Relations
@@ -921,14 +956,25 @@ class GpuBackend:
             return None
         return plan, partial.child
 
-    def _exec_agg(self, final: X.HashAggregateExec, child: X.SparkPlan):
+    def _exec_agg(self, final: X.HashAggregateExec, child: X.SparkPlan, order=None,
+                  limit=None):
+        """Queue a fused aggregate and return ``finish() -> pa.Table``: the dense LDS
+        aggregate for one small integer group column, else the hash-mode aggregate
+        (``_hash_agg``)."""
+        try:
+            return self._dense_agg(final, child)
+        except _NeedHash as e:
+            log.debug("hash-mode aggregate: %s", e)
+        return self._hash_agg(final, child, order, limit)
+
+    def _dense_agg(self, final: X.HashAggregateExec, child: X.SparkPlan):
         """Queue a fused aggregate and return ``finish() -> pa.Table``.  Nothing here waits on
         the device: kernels, the cross-rank combine and the D2H of the tiny result block are
         stream-ordered, so the host can plan and submit the next query while this one runs
         (``collect_async``)."""
         fns = [fn for _, fn in X.agg_functions(final.aggregates)]
         if len(final.grouping) > 1:
-            raise Unsupported("multi-column group by")
+            raise _NeedHash("multi-column group by")
         group = final.grouping[0] if final.grouping else None
         if group is not None and not isinstance(group, E.Attribute):
             raise Unsupported("group by expression")
@@ -1054,7 +1100,7 @@ class GpuBackend:
             return -1, 1, 0, None, None
         c = r.col(group)
         if c.is_float:
-            raise Unsupported("float group key")
+            raise _NeedHash("float group key")
         d = self._dist()
         multi = d is not None and d.world > 1
         gkey = getattr(r.table, "global_key", None) if r.table is not None else None
@@ -1074,14 +1120,14 @@ class GpuBackend:
                 base, G = dom
                 # identical on every rank, so the fallback decision is unanimous by construction
                 if G > limit:
-                    raise Unsupported("group domain too large for LDS aggregation")
+                    raise _NeedHash("group domain too large for LDS aggregation")
                 return (True, G, base, None, c.atype) if G > 0 else None
         too_big = G > limit
         if multi:
             # data-dependent fallbacks must be unanimous, or ranks diverge in their collectives
             too_big = any(d.all_gather_object(too_big))
         if too_big:
-            raise Unsupported("group domain too large for LDS aggregation")
+            raise _NeedHash("group domain too large for LDS aggregation")
         if G == 0:
             return None
         return None, max(G, 1), base, c.dictionary, c.atype
@@ -1240,11 +1286,11 @@ class GpuBackend:
         if len(specs) == 1:
             return specs[0]
         if any(s[3] is not None for s in specs):
-            raise Unsupported("string group key over a bucket union")
+            raise _NeedHash("string group key over a bucket union")
         lo = min(s[2] for s in specs)
         hi = max(s[2] + s[1] for s in specs)
         if hi - lo > limit:
-            raise Unsupported("group domain too large for LDS aggregation")
+            raise _NeedHash("group domain too large for LDS aggregation")
         return (True if all(s[0] is True for s in specs) else None), hi - lo, lo, None, specs[0][4]
 
     def _join_agg_pair(self, node, left: DRel, right: DRel, lk, rk, fns, group, G, gbase):
@@ -1306,6 +1352,380 @@ class GpuBackend:
                                     self._compacts(descs),
                                     cache_spans=fr is not None and rstart is fr[0])
             return K.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles)
+
+    # ------------------------------------------------------------------------------------------
+    # Hash-mode aggregation (multi-column / high-cardinality / float keys; exec/hash_agg.py)
+    # ------------------------------------------------------------------------------------------
+    def _hash_agg(self, final: X.HashAggregateExec, child: X.SparkPlan, order, limit):
+        """GROUP BY through the device hash table: every (part) launch of the fused scan or
+        merge-join kernel inserts into one table, ``hs_hagg_extract`` compacts it, ranks merge
+        their groups, and ORDER BY ... LIMIT picks its candidates on the device.  Kernels and the
+        extract are queued now; ``finish`` reads the group count (re-running with a 4x table if
+        the size guess overflowed) and copies the result."""
+        from . import hash_agg as H
+        if not HyperspaceConf.codegen_enabled(self.session.conf):
+            raise Unsupported("hash aggregate needs code generation")
+        fns = [fn for _, fn in X.agg_functions(final.aggregates)]
+        grouping = list(final.grouping)
+        if not all(isinstance(g, E.Attribute) for g in grouping):
+            raise Unsupported("group by expression")
+        node = child
+        while isinstance(node, X.ProjectExec) and \
+                all(isinstance(e, E.Attribute) for e in node.project_list):
+            node = node.child
+        if isinstance(node, X.SortMergeJoinExec):
+            left, right, lk, rk = self._join_inputs(node)
+            lparts, rparts = left.parts or [left], right.parts or [right]
+            rels = lparts + rparts
+            launches = [("join", lp, rp) for lp in lparts for rp in rparts]
+        else:
+            r = self._rel(child)
+            rels = r.parts or [r]
+            launches = [("scan", x, None) for x in rels]
+        doms = {g.expr_id: self._union_domain(rels, g) for g in grouping}
+        A = len(fns) + 1
+        minmax = any(isinstance(fn, (E.Min, E.Max)) for fn in fns)
+        shape_key = (tuple(g.name for g in grouping), tuple(fn.sql() for fn in fns),
+                     tuple(id(x.table) for x in rels))
+        est = min(sum(x.table.num_rows or 0 for x in rels), 1 << 40)
+        span = 1
+        for g in grouping:
+            span *= max(1, doms[g.expr_id][1]) + 1 if doms[g.expr_id][1] else (1 << 32)
+        est = max(1, min(est, span))
+        hk_box: list = []
+
+        def run(M: int):
+            table = self.htables.get(M, A, minmax, self.device)
+            with stage("hagg.kernels"):
+                for kind, a, b in launches:
+                    if kind == "join":
+                        self._join_hash_pair(node, a, b, lk, rk, fns, grouping, doms, table, hk_box)
+                    else:
+                        self._scan_hash(a, fns, grouping, doms, table, hk_box)
+            with stage("hagg.extract"):
+                return table.extract(A - 1)
+
+        M = self.htables.slots_for(shape_key, est)
+        groups = run(M)
+        d = self._dist()
+
+        def finish() -> pa.Table:
+            nonlocal groups, M
+            with stage("hagg.result"):
+                G, over = groups.count()
+                while over:
+                    if M >= H.MAX_SLOTS:
+                        raise Unsupported("hash aggregate table too large")
+                    M *= 4
+                    groups = run(M)
+                    G, over = groups.count()
+                self.htables.record(shape_key, M, G)
+                hk = hk_box[0] if hk_box else None
+                if d is not None and d.world > 1:
+                    groups, G = self._hash_combine_ranks(d, groups, G, A, minmax)
+                if hk is None or G == 0:
+                    return self._hash_table_out(final, fns, grouping, hk, None, A)
+                src = self._topk_source(final, fns, grouping, hk, order, limit, G)
+                if src is not None:
+                    groups, G = H.topk_candidates(groups, G, src, int(limit))
+                return self._hash_table_out(final, fns, grouping, hk, groups.to_host(G), A)
+        return finish
+
+    def _union_domain(self, rels, g: E.Attribute):
+        """(lo, span, scale) of group column ``g`` over every part holding it and every rank.
+        Integer columns: their value range (scale None).  float64 columns: the range of the
+        exact decimal integers q = x * scale of their compact encoding (exec/encoding.py), so
+        such a column packs into a multi-column key; scale 0.0 = no usable encoding (a float
+        key then only runs alone, as raw bits).  Dictionary columns need none."""
+        from .encoding import compact_of
+        lo, hi, seen = None, None, False
+        dicts = []
+        scale = None
+        for x in rels:
+            if g.expr_id not in x.colmap:
+                continue
+            c = x.col(g)
+            if c.dictionary is not None:
+                dicts.append(c.dictionary)
+                continue
+            if c.is_float:
+                enc = compact_of(c) if c.hs_type == NL.F64 else None
+                if enc is None or enc.scale is None or enc.lo is None or \
+                        (scale is not None and enc.scale != scale):
+                    return (0, 0, 0.0)
+                scale = enc.scale
+                seen = True
+                l0, sp = int(enc.lo), int(enc.hi) - int(enc.lo) + 1
+            else:
+                seen = True
+                l0, sp = self._local_domain(c)
+            if sp == 0:
+                continue
+            lo = l0 if lo is None else min(lo, l0)
+            hi = l0 + sp - 1 if hi is None else max(hi, l0 + sp - 1)
+        if len(dicts) > 1 and not all(dd.equals(dicts[0]) for dd in dicts[1:]):
+            raise Unsupported("string group key with different dictionaries per part")
+        d = self._dist()
+        if seen and d is not None and d.world > 1:
+            import torch
+            dev = d.device if d.backend == "nccl" else "cpu"
+            big = 1 << 62
+            t = torch.tensor([-(lo if lo is not None else big), hi if hi is not None else -big],
+                             dtype=torch.int64, device=dev)
+            d.all_reduce(t, "max")
+            nlo, nhi = -int(t[0].item()), int(t[1].item())
+            if nhi < nlo:
+                return (0, 0, scale)
+            return (nlo, nhi - nlo + 1, scale)
+        if lo is None:
+            return (0, 0, scale)
+        return (lo, hi - lo + 1, scale)
+
+    def _hash_keyplan(self, grouping, col_info, rel_of, doms, specs, descs):
+        from . import hash_agg as H
+        items = []
+        for g in grouping:
+            ci = col_info(g)
+            items.append((ci.slot, g, descs[ci.slot], doms[g.expr_id]))
+        own = []
+        for a in specs:
+            own.append(a.kind != NL.AK_COUNT_STAR and
+                       any(descs[a.col[t]].valid is not None for t in range(a.nterms)))
+        return H.plan_keys(items, tuple(own))
+
+    def _scan_hash(self, r: DRel, fns, grouping, doms, table, hk_box) -> None:
+        col_info, descs = self._column_infos([(r, 0)])
+        implied: set = set()
+        spec = self._range_spec(r, r.conds, implied)
+        with stage("scan.ranges"):
+            rstart, rlen, _ = self._ranges(r, r.conds) if spec is not None else \
+                self._full_ranges(r.table)
+        bound = CP.bind(CP.to_cnf([c for c in r.conds if id(c) not in implied]), col_info,
+                        self.device)
+        specs = self._agg_specs(fns, col_info)
+        hk = self._hash_keyplan(grouping, col_info, None, doms, specs, descs)
+        if not hk_box:
+            hk_box.append(hk)
+        p = NL.ScanParams()
+        p.group_col, p.num_groups, p.group_base = -1, 1, 0
+        for s, c in descs.items():
+            p.cols[s] = c.desc()
+        for i, pr in enumerate(bound.preds):
+            p.preds[i] = pr
+        p.npreds = len(bound.preds)
+        for i, a in enumerate(specs):
+            p.aggs[i] = a
+        p.naggs = len(specs)
+        if bound.always_false or (r.table.num_rows or 0) == 0:
+            return
+        with stage("scan.hash_agg_kernel"):
+            tp = K.ranges_to_tiles(rlen)
+            jit.scan_agg(p, rstart, rlen, tp, self._compacts(descs), nrows=r.table.num_rows,
+                         hk=hk, htab=table)
+
+    def _join_hash_pair(self, node, left: DRel, right: DRel, lk, rk, fns, grouping, doms,
+                        table, hk_box) -> None:
+        if right.table.num_rows * 64 < left.table.num_rows:
+            left, right, lk, rk = right, left, rk, lk
+        implied: set = set()
+        probed = self._probe_ranges(left, right, lk, rk)
+        if probed is None:
+            probed = self._domain_pruned_ranges(left, right, lk, rk)
+        if probed is not None:
+            rstart, rlen, rbk = probed
+        else:
+            rstart, rlen, rbk = self._ranges(left, left.conds, implied)
+        jp, col_info, descs, keep = self._join_params(
+            left, right, lk, rk, node.condition,
+            lconds=[c for c in left.conds if id(c) not in implied])
+        specs = self._agg_specs(fns, col_info)
+        hk = self._hash_keyplan(grouping, col_info, None, doms, specs, descs)
+        if not hk_box:
+            hk_box.append(hk)
+        jp.group_col, jp.num_groups, jp.group_base = -1, 1, 0
+        for s, c in descs.items():
+            jp.cols[s] = c.desc()
+        for i, a in enumerate(specs):
+            jp.aggs[i] = a
+        jp.naggs = len(specs)
+        if keep[0].always_false or keep[1].always_false or left.table.num_rows == 0 or \
+                right.table.num_rows == 0:
+            return
+        comp = self._compacts(descs)
+        if not jit.merge_join_ok(jp, comp, right.table.num_rows, left.table.num_rows):
+            raise Unsupported("hash aggregate over a join the merge-join kernel cannot run")
+        fr = getattr(left.table, "_full_ranges", None)
+        with stage("join.hash_agg_kernel"):
+            jit.merge_join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, comp,
+                               nrows=left.table.num_rows,
+                               cache_spans=fr is not None and rstart is fr[0],
+                               rdup=jit.key_has_dups(right.col(rk)), hk=hk, htab=table)
+
+    def _hash_combine_ranks(self, d, groups, G: int, A: int, minmax: bool):
+        """Every rank's groups to every rank (one variable-size all-gather of packed rows),
+        merged in a device table: ranks may share groups (any key not led by the bucket key)."""
+        import torch
+        from . import hash_agg as H
+        with stage("hagg.combine_ranks"):
+            host = groups.to_host(G)
+            parts = [host["keys"].view(np.int64).reshape(G, 1),
+                     host["nulls"].astype(np.int64).reshape(G, 1),
+                     host["sums"].view(np.int64), host["cnts"],
+                     host["mins"].view(np.int64), host["maxs"].view(np.int64)]
+            rows = np.ascontiguousarray(np.concatenate(parts, axis=1)) if G else \
+                np.zeros((0, 2 + 4 * A), np.int64)
+            allr = d.all_gather_rows(rows)
+            n = allr.shape[0]
+            if n == 0:
+                return groups, 0
+            dev = self.device
+            cat = torch.from_numpy(allr).to(dev)
+            keys = cat[:, 0].contiguous()
+            nulls = cat[:, 1].to(torch.uint8).contiguous()
+
+            def col(j):
+                return cat[:, 2 + j * A: 2 + (j + 1) * A].contiguous().view(-1)
+            sums, cnts = col(0).view(torch.float64), col(1)
+            mins = col(2).view(torch.float64) if minmax else None
+            maxs = col(3).view(torch.float64) if minmax else None
+            M = H.next_pow2(max(H.MIN_SLOTS, 2 * n))
+            table = self.htables.get(M, A, minmax, dev)
+            NL.check(NL.lib().hs_hagg_merge(NL.ptr(keys), NL.ptr(nulls), NL.ptr(sums),
+                                            NL.ptr(cnts), NL.ptr(mins), NL.ptr(maxs), n,
+                                            NL.ptr(table.keys), NL.ptr(table.sums),
+                                            NL.ptr(table.cnts), NL.ptr(table.mins),
+                                            NL.ptr(table.maxs), M, A, NL.ptr(table.flag),
+                                            NL.stream_ptr()), "hs_hagg_merge")
+            merged = table.extract(A - 1)
+            Gm, over = merged.count()
+            if over:
+                raise Unsupported("rank merge table overflow")
+            return merged, Gm
+
+    def _topk_source(self, final, fns, grouping, hk, order, limit, G):
+        """The device top-k image of the primary ORDER BY key, or None (host sort of all)."""
+        from . import hash_agg as H
+        if not order or limit is None or G <= max(TOPK_MIN_GROUPS, 4 * int(limit)) or \
+                int(limit) > 1024 or int(limit) <= 0:
+            return None
+        o = order[0]
+        e = o.child
+        if not isinstance(e, E.Attribute):
+            return None
+        desc = not o.ascending
+        A = len(fns) + 1
+        for agg in final.aggregates:
+            a = agg if isinstance(agg, E.Attribute) else agg.to_attribute()
+            if a.expr_id != e.expr_id:
+                continue
+            inner = agg.child if isinstance(agg, E.Alias) else agg
+            if isinstance(inner, E.AggregateFunction):
+                i = next(k for k, fn in enumerate(fns) if fn is inner)
+                cs = i if hk.own_counts[i] else A - 1
+                src = {E.Sum: H.SRC_SUM, E.Count: H.SRC_COUNT, E.Min: H.SRC_MIN,
+                       E.Max: H.SRC_MAX, E.Avg: H.SRC_AVG}.get(type(inner))
+                if src is None:
+                    return None
+                if src == H.SRC_COUNT:
+                    cs = i if hk.own_counts[i] else A - 1
+                return H.OrderSource(src, i, cs, desc=desc)
+            if isinstance(inner, E.Attribute):
+                e = inner
+                break
+            return None
+        for j, g in enumerate(grouping):
+            if g.expr_id != e.expr_id:
+                continue
+            c = hk.cols[j]
+            if hk.mode == "raw_int":
+                return H.OrderSource(H.SRC_RAWINT, desc=desc)
+            if hk.mode == "raw_float":
+                return H.OrderSource(H.SRC_RAWFLT, desc=desc)
+            if c.kind == "f32":
+                return None
+            mask = (1 << c.bits) - 1 if c.bits < 64 else (1 << 64) - 1
+            return H.OrderSource(H.SRC_KEYFIELD, shift=c.shift, mask=mask,
+                                 nullable=c.nullable, desc=desc)
+        return None
+
+    def _hash_table_out(self, final, fns, grouping, hk, host, A) -> pa.Table:
+        """Result table of a hash-mode aggregate from its host group arrays (vectorized
+        finalize; arithmetic over aggregates with pyarrow.compute)."""
+        G = 0 if host is None else len(host["keys"])
+        gmap = {}
+        if hk is not None and G:
+            for g, arr in zip(grouping, hk.unpack(host["keys"], host["nulls"])):
+                gmap[g.expr_id] = arr
+        else:
+            for g in grouping:
+                gmap[g.expr_id] = pa.array([], type=g.data_type)
+        vals = {}
+        for i, fn in enumerate(fns):
+            if G:
+                cnt = host["cnts"][:, i] if (hk.own_counts[i]) else host["cnts"][:, A - 1]
+                vals[id(fn)] = _finalize_array(fn, host["sums"][:, i], cnt, host["mins"][:, i],
+                                               host["maxs"][:, i])
+            else:
+                vals[id(fn)] = pa.array([], type=fn.data_type)
+        arrays = []
+        for e, a in zip(final.aggregates, final.output):
+            arr = _eval_vec(e.child if isinstance(e, E.Alias) else e, vals, gmap, G)
+            if not arr.type.equals(a.data_type):
+                try:
+                    arr = arr.cast(a.data_type)
+                except (pa.ArrowInvalid, pa.ArrowNotImplementedError):
+                    pass
+            arrays.append(arr)
+        return pa.Table.from_arrays(arrays, names=[a.name for a in final.output])
+
+
+def _finalize_array(fn, s, c, mn, mx) -> pa.Array:
+    """Vectorized ``CP.finalize_value`` over the groups of a hash-mode aggregate."""
+    c = np.asarray(c, dtype=np.int64)
+    if isinstance(fn, E.Count):
+        return pa.array(c, type=pa.int64())
+    null = c == 0
+    if isinstance(fn, E.Avg):
+        with np.errstate(divide="ignore", invalid="ignore"):
+            return pa.array(np.where(null, 0.0, s / np.maximum(c, 1)), mask=null)
+    v = s if isinstance(fn, E.Sum) else (mn if isinstance(fn, E.Min) else mx)
+    v = np.where(null, 0.0, v)
+    if CP.int_result(fn):
+        return pa.array(np.rint(v).astype(np.int64), mask=null)
+    t = fn.child.data_type
+    if isinstance(fn, (E.Min, E.Max)) and pa.types.is_date32(t):
+        return pa.array(np.rint(v).astype(np.int32), mask=null).view(pa.date32())
+    return pa.array(v.astype(np.float64), mask=null)
+
+
+def _eval_vec(e, vals, gmap, n: int) -> pa.Array:
+    """Output expression of an aggregate over whole result columns."""
+    import pyarrow.compute as pc
+    if isinstance(e, E.AggregateFunction):
+        return vals[id(e)]
+    if isinstance(e, E.Attribute):
+        if e.expr_id in gmap:
+            return gmap[e.expr_id]
+        raise Unsupported(f"result column {e.sql()}")
+    if isinstance(e, E.Literal):
+        return pa.array([e.value] * n)
+    if isinstance(e, E.Alias):
+        return _eval_vec(e.child, vals, gmap, n)
+    if isinstance(e, E.Cast):
+        return _eval_vec(e.child, vals, gmap, n).cast(e.data_type)
+    if isinstance(e, E.BinaryArithmetic):
+        a = _eval_vec(e.left, vals, gmap, n)
+        b = _eval_vec(e.right, vals, gmap, n)
+        if isinstance(e, E.Add):
+            return pc.add(a, b)
+        if isinstance(e, E.Subtract):
+            return pc.subtract(a, b)
+        if isinstance(e, E.Multiply):
+            return pc.multiply(a, b)
+        a = pc.cast(a, pa.float64())
+        b = pc.cast(b, pa.float64())
+        return pc.if_else(pc.equal(b, 0.0), pa.scalar(None, pa.float64()), pc.divide(a, b))
+    raise Unsupported(f"result expression {type(e).__name__}")
 
 
 def _combine_aggs(a, b):

@@ -1,0 +1,376 @@
+"""High-cardinality and multi-column GROUP BY on the device, plus ORDER BY ... LIMIT (top-k).
+
+The dense path in ``exec/gpu.py`` aggregates into LDS, one slot per value of a single small
+integer group column.  Everything else — several group columns (TPC-H Q3 groups by
+``l_orderkey, o_orderdate, o_shippriority``), millions of groups, float or string keys — runs
+in *hash mode*:
+
+1. ``KeyPlan`` packs the group columns into one 64-bit key: each integer / dictionary-code
+   column contributes ``value - lo`` (+1 with a 0 code for NULL when nullable) in its own bit
+   field, with ``lo`` and the widths taken from the columns' value domains (the same domains on
+   every rank, so partial groups of different GPUs carry identical keys).  A single 64-bit
+   integer or float column is used raw (float images normalise -0.0 and NaN).
+2. The fused scan / merge-join kernels (``exec/jit.py``, ``_hash_accumulate``) insert the rows
+   into a global open-addressing table (``csrc/kernels/hash_agg.hip``); a wavefront reduces
+   runs of equal keys first, so sorted inputs cost about one probe per group and batch.
+3. ``hs_hagg_extract`` compacts occupied slots into dense arrays (and resets them, so tables are
+   reused without a memset).  With ``ORDER BY <expr> LIMIT k`` the top-k candidates are picked on
+   the device (order-preserving images, LDS bitonic top-k, ties at the k-th value kept) and only
+   those rows cross PCIe; the host finishes the exact multi-key sort over them.
+
+A table that overflows its probe budget (more groups than the size guess) sets a flag, is
+re-sized 4x and the query re-runs; the size that worked is remembered per query shape.
+Reference: the rules only swap scans (JoinIndexRule.scala:63-69, RuleUtils.scala:264-292), Spark
+runs every operator above them; ``E2EHyperspaceRulesTest.scala:1004-1019`` checks full results.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import pyarrow as pa
+
+from ..ops import _lib as NL
+from .compile import Unsupported
+
+EMPTY = (1 << 64) - 1
+MIN_SLOTS = 1 << 12
+MAX_SLOTS = 1 << 29
+_INT_TYPES = (NL.I8, NL.I16, NL.I32, NL.I64, NL.U32, NL.BOOL)
+
+
+@dataclass
+class KeyCol:
+    slot: int            # kernel column slot
+    attr: object         # the grouping attribute (output)
+    kind: str            # "int" | "f32" | "f64"
+    nullable: bool
+    lo: int = 0
+    bits: int = 0
+    shift: int = 0
+    dictionary: Optional[pa.Array] = None
+    atype: Optional[pa.DataType] = None
+    scale: float = 0.0   # kind "dec": value = (lo + code) / scale
+
+
+class KeyPlan:
+    """Packing of a query's group columns into the hash table's 64-bit key."""
+
+    def __init__(self, cols: List[KeyCol], mode: str, own_counts: Tuple[bool, ...]):
+        self.cols = cols
+        self.mode = mode                  # "packed" | "raw_int" | "raw_float"
+        self.own_counts = own_counts      # per aggregate: its own non-null count is kept
+        self.slots = [c.slot for c in cols]
+
+    def shape(self) -> tuple:
+        return (self.mode, tuple((c.slot, c.kind, c.nullable) for c in self.cols),
+                self.own_counts)
+
+    def values(self) -> Dict[str, int]:
+        v = {}
+        if self.mode == "packed":
+            for j, c in enumerate(self.cols):
+                v[f"HL{j}"] = c.lo
+                v[f"HS{j}"] = c.shift
+                if c.kind == "dec":
+                    v[f"HQ{j}"] = c.scale
+        return v
+
+    # -- host decode ---------------------------------------------------------------------------
+    def unpack(self, keys: np.ndarray, nulls: np.ndarray) -> List[pa.Array]:
+        out = []
+        if self.mode != "packed":
+            c = self.cols[0]
+            mask = nulls.astype(bool) if c.nullable else None
+            if self.mode == "raw_float":
+                vals = keys.view(np.float64)
+            else:
+                vals = keys.view(np.int64)
+            out.append(_to_arrow(c, vals, mask))
+            return out
+        for c in self.cols:
+            m = np.uint64((1 << c.bits) - 1) if c.bits < 64 else np.uint64(EMPTY)
+            code = (keys >> np.uint64(c.shift)) & m if c.bits else np.zeros_like(keys)
+            mask = None
+            if c.nullable:
+                mask = code == 0
+                code = code - np.uint64(1)
+            if c.kind == "f32":
+                vals = code.astype(np.uint32).view(np.float32).astype(np.float64)
+            elif c.kind == "dec":
+                # the decode the kernels and the encoder verified: (lo + code) / scale
+                vals = (code.astype(np.int64) + np.int64(c.lo)).astype(np.float64) / c.scale
+            else:
+                vals = code.astype(np.int64) + np.int64(c.lo)
+            if mask is not None:
+                vals = np.where(mask, 0, vals)
+            out.append(_to_arrow(c, vals, mask))
+        return out
+
+
+def _to_arrow(c: KeyCol, vals: np.ndarray, mask) -> pa.Array:
+    t = c.atype
+    if c.dictionary is not None:
+        codes = pa.array(vals.astype(np.int32), mask=mask)
+        return c.dictionary.take(codes)
+    if c.kind in ("f32", "f64", "dec"):
+        arr = pa.array(vals.astype(np.float64), mask=mask)
+        return arr.cast(t) if t is not None and not pa.types.is_float64(t) else arr
+    arr = pa.array(vals.astype(np.int64), mask=mask)
+    if t is None or pa.types.is_int64(t):
+        return arr
+    if pa.types.is_date32(t):
+        return pa.array(vals.astype(np.int32), mask=mask).view(pa.date32())
+    if pa.types.is_timestamp(t):
+        return arr.view(pa.int64()).cast(t)
+    if pa.types.is_boolean(t):
+        return pa.array(vals.astype(bool), mask=mask)
+    try:
+        return arr.cast(t)
+    except (pa.ArrowInvalid, pa.ArrowNotImplementedError):
+        return arr
+
+
+def plan_keys(items, own_counts) -> KeyPlan:
+    """``items``: (slot, attr, DeviceColumn, (lo, span)) per group column, in GROUP BY order;
+    the domain covers every part and rank (span 0 = no non-null values), so all launches of a
+    query (bucket-union parts, ranks) pack keys identically."""
+    cols: List[KeyCol] = []
+    for slot, attr, c, _ in items:
+        nullable = c.valid is not None
+        if c.offsets is not None:
+            raise Unsupported("raw string group key")
+        if c.dictionary is not None:
+            kind = "int"
+        elif c.hs_type == NL.F64:
+            kind = "f64"
+        elif c.hs_type == NL.F32:
+            kind = "f32"
+        elif c.hs_type in _INT_TYPES:
+            kind = "int"
+        else:
+            raise Unsupported(f"group key type {c.atype}")
+        cols.append(KeyCol(slot, attr, kind, nullable, dictionary=c.dictionary, atype=c.atype))
+    if len(cols) == 1 and cols[0].kind in ("f64", "f32"):
+        return KeyPlan(cols, "raw_float", own_counts)
+    shift = 0
+    for k, (_, _, c, dom) in zip(cols, items):
+        if k.kind == "f64":
+            # exact decimal column (exec/encoding.py): packs q = rint(x * scale) - lo
+            if len(dom) < 3 or not dom[2]:
+                raise Unsupported("float64 column without an exact decimal form in a "
+                                  "multi-column group key")
+            k.kind, k.scale = "dec", float(dom[2])
+            k.lo = int(dom[0])
+            k.bits = max(0, int(max(dom[1], 1) - 1 + (1 if k.nullable else 0)).bit_length())
+        elif k.kind == "f32":
+            k.lo, k.bits = 0, 32 + (1 if k.nullable else 0)
+        elif k.dictionary is not None:
+            k.lo, span = 0, max(len(k.dictionary), 1)
+            k.bits = max(0, int(span - 1 + (1 if k.nullable else 0)).bit_length())
+        else:
+            lo, span = dom
+            k.lo = int(lo)
+            k.bits = max(0, int(max(span, 1) - 1 + (1 if k.nullable else 0)).bit_length())
+        k.shift = shift
+        shift += k.bits
+    if shift > 64:
+        if len(cols) == 1 and cols[0].kind == "int":
+            return KeyPlan(cols, "raw_int", own_counts)
+        raise Unsupported("group key does not pack into 64 bits")
+    return KeyPlan(cols, "packed", own_counts)
+
+
+# ------------------------------------------------------------------------------------------------
+# Tables
+# ------------------------------------------------------------------------------------------------
+class HashTable:
+    """One device hash table (M probe slots + 2 direct slots, NA aggregates per group).  Tables
+    are pooled per (M, NA, min/max) and always left clean by ``extract(reset=True)``."""
+
+    def __init__(self, M: int, NA: int, minmax: bool, device):
+        import torch
+        self.M, self.NA, self.minmax, self.device = M, NA, minmax, device
+        n = (M + 2) * NA
+        self.keys = torch.empty(M + 2, dtype=torch.int64, device=device)
+        self.sums = torch.empty(n, dtype=torch.float64, device=device)
+        self.cnts = torch.empty(n, dtype=torch.int64, device=device)
+        self.mins = torch.empty(n, dtype=torch.float64, device=device) if minmax else None
+        self.maxs = torch.empty(n, dtype=torch.float64, device=device) if minmax else None
+        self.flag = torch.zeros(4, dtype=torch.int64, device=device)
+        NL.check(NL.lib().hs_hagg_init(NL.ptr(self.keys), NL.ptr(self.sums), NL.ptr(self.cnts),
+                                       NL.ptr(self.mins), NL.ptr(self.maxs), M, NA,
+                                       NL.stream_ptr()), "hs_hagg_init")
+
+    def kernel_values(self) -> Dict[str, int]:
+        return {"hkeys": self.keys.data_ptr(), "hsum": self.sums.data_ptr(),
+                "hcnt": self.cnts.data_ptr(),
+                "hmin": self.mins.data_ptr() if self.mins is not None else 0,
+                "hmax": self.maxs.data_ptr() if self.maxs is not None else 0,
+                "HM": self.M, "hflag": self.flag.data_ptr()}
+
+    def extract(self, star: int) -> "Groups":
+        """Stream-ordered: dense groups of this table (capacity M + 2 rows, the count ``G`` stays
+        on the device until ``Groups.count()``), the table reset for the next query."""
+        import torch
+        L = NL.lib()
+        cap = self.M + 2
+        dev = self.device
+        g = Groups(self.NA, dev)
+        g.keys = torch.empty(cap, dtype=torch.int64, device=dev)
+        g.nulls = torch.empty(cap, dtype=torch.uint8, device=dev)
+        g.sums = torch.empty(cap * self.NA, dtype=torch.float64, device=dev)
+        g.cnts = torch.empty(cap * self.NA, dtype=torch.int64, device=dev)
+        g.mins = torch.empty(cap * self.NA, dtype=torch.float64, device=dev) if self.minmax else None
+        g.maxs = torch.empty(cap * self.NA, dtype=torch.float64, device=dev) if self.minmax else None
+        ws = torch.empty(int(L.hs_hagg_extract_blocks(self.M)), dtype=torch.int64, device=dev)
+        g.total = torch.empty(2, dtype=torch.int64, device=dev)
+        NL.check(L.hs_hagg_extract(NL.ptr(self.keys), NL.ptr(self.sums), NL.ptr(self.cnts),
+                                   NL.ptr(self.mins), NL.ptr(self.maxs), self.M, self.NA, star, 1,
+                                   NL.ptr(ws), NL.ptr(g.total), NL.ptr(self.flag),
+                                   NL.ptr(g.keys), NL.ptr(g.nulls),
+                                   NL.ptr(g.sums), NL.ptr(g.cnts), NL.ptr(g.mins),
+                                   NL.ptr(g.maxs), NL.stream_ptr()), "hs_hagg_extract")
+        return g
+
+
+class Groups:
+    """Dense per-group arrays on the device: keys (u64 bits), nulls (raw single-column NULL
+    key), and NA (sum, count, min, max) partials per group."""
+
+    def __init__(self, NA: int, device):
+        self.NA, self.device = NA, device
+        self.keys = self.nulls = self.sums = self.cnts = self.mins = self.maxs = None
+        self.total = None
+        self._host_total = None
+
+    def count(self) -> Tuple[int, bool]:
+        if self._host_total is None:
+            h = self.total.cpu().numpy()
+            self._host_total = (int(h[0]), bool(h[1]))
+        return self._host_total
+
+    def set_count(self, n: int) -> None:
+        self._host_total = (n, False)
+
+    def to_host(self, n: Optional[int] = None) -> dict:
+        G = self.count()[0] if n is None else n
+        NA = self.NA
+        out = {"keys": self.keys[:G].cpu().numpy().view(np.uint64),
+               "nulls": self.nulls[:G].cpu().numpy(),
+               "sums": self.sums[:G * NA].cpu().numpy().reshape(G, NA),
+               "cnts": self.cnts[:G * NA].cpu().numpy().reshape(G, NA)}
+        out["mins"] = (self.mins[:G * NA].cpu().numpy().reshape(G, NA) if self.mins is not None
+                       else np.full((G, NA), np.inf))
+        out["maxs"] = (self.maxs[:G * NA].cpu().numpy().reshape(G, NA) if self.maxs is not None
+                       else np.full((G, NA), -np.inf))
+        return out
+
+    def take(self, rows, n: int) -> "Groups":
+        """Groups ``rows[:n]`` (uint32 device indices) as a new dense set."""
+        import torch
+        dev, NA = self.device, self.NA
+        g = Groups(NA, dev)
+        g.keys = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        g.nulls = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        g.sums = torch.empty(max(n, 1) * NA, dtype=torch.float64, device=dev)
+        g.cnts = torch.empty(max(n, 1) * NA, dtype=torch.int64, device=dev)
+        g.mins = torch.empty_like(g.sums) if self.mins is not None else None
+        g.maxs = torch.empty_like(g.sums) if self.maxs is not None else None
+        NL.check(NL.lib().hs_hagg_take(NL.ptr(rows), n, NL.ptr(self.keys), NL.ptr(self.nulls),
+                                       NL.ptr(self.sums), NL.ptr(self.cnts), NL.ptr(self.mins),
+                                       NL.ptr(self.maxs), NA, NL.ptr(g.keys), NL.ptr(g.nulls),
+                                       NL.ptr(g.sums), NL.ptr(g.cnts), NL.ptr(g.mins),
+                                       NL.ptr(g.maxs), NL.stream_ptr()), "hs_hagg_take")
+        g.set_count(n)
+        return g
+
+
+class TablePool:
+    def __init__(self):
+        self._tables: Dict[tuple, HashTable] = {}
+        self.sizes: Dict[tuple, int] = {}     # query shape -> slots that held its groups
+
+    def get(self, M: int, NA: int, minmax: bool, device) -> HashTable:
+        k = (M, NA, minmax)
+        t = self._tables.get(k)
+        if t is None:
+            # keep the pool bounded: tables of other sizes are dropped (re-created on demand)
+            big = [x for x in self._tables if x[0] >= (1 << 24)]
+            for x in big:
+                del self._tables[x]
+            t = HashTable(M, NA, minmax, device)
+            self._tables[k] = t
+        return t
+
+    def slots_for(self, shape_key, estimate: int) -> int:
+        M = self.sizes.get(shape_key)
+        if M is None:
+            M = next_pow2(max(MIN_SLOTS, min(2 * max(estimate, 1), 1 << 22)))
+        return M
+
+    def record(self, shape_key, M: int, groups: int) -> None:
+        # next time: at least 2x the groups seen (load <= 0.5), never below what worked
+        self.sizes[shape_key] = max(next_pow2(max(MIN_SLOTS, 2 * groups)),
+                                    min(M, next_pow2(max(MIN_SLOTS, 2 * groups)) * 2))
+
+
+def next_pow2(n: int) -> int:
+    return 1 << max(0, int(n - 1).bit_length())
+
+
+# ------------------------------------------------------------------------------------------------
+# Top-k
+# ------------------------------------------------------------------------------------------------
+# image sources (csrc/kernels/hash_agg.hip topk_images_kernel)
+SRC_SUM, SRC_COUNT, SRC_MIN, SRC_MAX, SRC_AVG, SRC_KEYFIELD, SRC_RAWINT, SRC_RAWFLT = range(8)
+
+
+@dataclass
+class OrderSource:
+    src: int
+    agg: int = 0
+    cnt_slot: int = 0
+    shift: int = 0
+    mask: int = 0
+    nullable: bool = False
+    desc: bool = False
+
+
+def topk_candidates(g: Groups, G: int, o: OrderSource, k: int) -> Tuple[Groups, int]:
+    """The groups whose primary ORDER BY image is <= the k-th smallest image: a superset of the
+    top k under the full ordering (ties at the k-th value are all kept)."""
+    import torch
+    L = NL.lib()
+    dev = g.device
+    if G <= k:
+        return g, G
+    img = torch.empty(G, dtype=torch.int64, device=dev)
+    NL.check(L.hs_topk_images(NL.ptr(g.keys), NL.ptr(g.nulls), NL.ptr(g.sums), NL.ptr(g.cnts),
+                              NL.ptr(g.mins), NL.ptr(g.maxs), G, g.NA, o.src, o.agg, o.cnt_slot,
+                              o.shift, C.c_uint64(o.mask), int(o.nullable), int(o.desc),
+                              NL.ptr(img), NL.stream_ptr()), "hs_topk_images")
+    chunk = int(L.hs_topk_chunk())
+    cur_img, cur_idx, n = img, None, G
+    while True:
+        nb = (n + chunk - 1) // chunk
+        oi = torch.empty(nb * k, dtype=torch.int64, device=dev)
+        ox = torch.empty(nb * k, dtype=torch.int32, device=dev)
+        NL.check(L.hs_topk_pass(NL.ptr(cur_img), NL.ptr(cur_idx), n, k, NL.ptr(oi), NL.ptr(ox),
+                                NL.stream_ptr()), "hs_topk_pass")
+        cur_img, cur_idx, n = oi, ox, nb * k
+        if nb == 1:
+            break
+    thr = cur_img[k - 1:k]
+    sel = torch.empty(G, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    NL.check(L.hs_topk_select(NL.ptr(img), G, NL.ptr(thr), NL.ptr(sel), NL.ptr(cnt),
+                              NL.stream_ptr()), "hs_topk_select")
+    n = int(cnt.item())
+    return g.take(sel, n), n
+
+
+__all__ = ["KeyPlan", "KeyCol", "plan_keys", "HashTable", "Groups", "TablePool",
+           "OrderSource", "topk_candidates", "Unsupported"]

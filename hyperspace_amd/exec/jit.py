@@ -281,6 +281,20 @@ __device__ __forceinline__ void lds_max(double* p, double v) {
   do { as = old; if (__longlong_as_double((i64)as) >= v) break;
        old = atomicCAS(a, as, (u64)__double_as_longlong(v)); } while (as != old);
 }
+// hash-mode grouping (exec/hash_agg.py, csrc/kernels/hash_agg.hip): probe hash and the bit
+// images of float group keys (-0.0 -> 0.0, one NaN)
+__device__ __forceinline__ u64 hs_mix64(u64 h) {
+  h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull;
+  return h ^ (h >> 33);
+}
+__device__ __forceinline__ u64 hs_f64key(double d) {
+  d = d == 0.0 ? 0.0 : d;
+  return d != d ? 0x7ff8000000000000ull : (u64)__double_as_longlong(d);
+}
+__device__ __forceinline__ u64 hs_f32key(float f) {
+  f = f == 0.0f ? 0.0f : f;
+  return f != f ? 0x7fc00000ull : (u64)(unsigned)__float_as_uint(f);
+}
 """
 
 
@@ -514,6 +528,115 @@ def _accumulate(gen: _Gen, aggs, grouped: bool, pass_var: str, gvar: str, ind: s
     return out
 
 
+HASH_MAX_PROBE = 512
+
+
+def _hash_accumulate(gen: _Gen, aggs, hk, pass_var: str, ind: str) -> List[str]:
+    """Hash-mode grouping (``hk``: an exec.hash_agg.KeyPlan): the wavefront's lanes, in row
+    order, are cut into runs of equal group keys (one ballot of the run heads); a segmented
+    shuffle scan sums each run's values into its last lane, and only that lane probes the
+    global table (linear probing, 64-bit key, atomicCAS insert) and adds the run's partials
+    with memory-side atomics.  Inputs sorted by a key prefix (index scans, merge-join output)
+    put a group's rows in adjacent lanes, so most groups cost one probe and one atomic per
+    aggregate per 64-row batch.  Variables are ``x<slot>`` / ``n<slot>`` (callers rename)."""
+    a = gen.a
+    kp = a.add("p", "hkeys", "unsigned long long*")
+    sp = a.add("p", "hsum", "double*")
+    cp = a.add("p", "hcnt", "long long*")
+    mm = any(x.kind in (NL.AK_MIN, NL.AK_MAX) for x in aggs)
+    mnp = a.add("p", "hmin", "double*") if mm else None
+    mxp = a.add("p", "hmax", "double*") if mm else None
+    hm = a.add("q", "HM", "long long")
+    fl = a.add("p", "hflag", "long long*")
+    na = len(aggs)
+    i2 = ind + "  "
+    b = [f"{ind}{{ const int hln = (int)(threadIdx.x & 63u); const bool hok = {pass_var};"]
+    if hk.mode == "packed":
+        b.append(f"{i2}u64 hk = 0ull; const bool hnul = false;")
+        for j, c in enumerate(hk.cols):
+            lo = a.add("q", f"HL{j}", "long long")
+            sh = a.add("q", f"HS{j}", "long long")
+            s = c.slot
+            if c.kind == "f32":
+                val = f"hs_f32key((float)x{s})"
+            elif c.kind == "dec":
+                sc = a.add("d", f"HQ{j}", "double")
+                val = f"(u64)((i64)__builtin_rint((double)x{s} * {sc}) - {lo})"
+            else:
+                val = f"(u64)((i64)x{s} - {lo})"
+            expr = f"({gen.ok(s)} ? {val} + 1ull : 0ull)" if c.nullable else val
+            b.append(f"{i2}hk |= {expr} << (unsigned){sh};")
+    else:
+        c = hk.cols[0]
+        s = c.slot
+        val = f"hs_f64key((double)x{s})" if hk.mode == "raw_float" else f"(u64)(i64)x{s}"
+        nul = f"!{gen.ok(s)}" if c.nullable else "false"
+        b.append(f"{i2}const bool hnul = {nul}; const u64 hk = hnul ? 0ull : {val};")
+    b += [f"{i2}const u64 hkp = __shfl_up(hk, 1u, 64);",
+          f"{i2}const int hfp = __shfl_up((hok ? 1 : 0) | (hnul ? 2 : 0), 1u, 64);",
+          f"{i2}const bool hsame = hln > 0 && hok && (hfp & 1) != 0 && "
+          f"((hfp >> 1) & 1) == (hnul ? 1 : 0) && hkp == hk;",
+          f"{i2}const u64 hH = __ballot(!hsame);",
+          f"{i2}const int hss = 63 - __builtin_clzll(hH & ((2ull << hln) - 1ull));",
+          f"{i2}const bool htl = hok && (hln == 63 || ((hH >> ((hln + 1) & 63)) & 1ull) != 0ull);"]
+    own = hk.own_counts
+    red = []
+    for i, ag in enumerate(aggs):
+        if ag.kind == NL.AK_COUNT_STAR:
+            continue
+        v, ok = gen.agg_value(i, ag)
+        b.append(f"{i2}const bool hq{i} = hok && {ok};")
+        if ag.kind != NL.AK_COUNT:
+            b.append(f"{i2}double hv{i} = hq{i} ? (double)({v}) : {_ident(ag.kind)};")
+            op = "fmin" if ag.kind == NL.AK_MIN else ("fmax" if ag.kind == NL.AK_MAX else None)
+            red.append((f"hv{i}", "double", op))
+        if own[i]:
+            b.append(f"{i2}long long hc{i} = hq{i} ? 1ll : 0ll;")
+            red.append((f"hc{i}", "long long", None))
+    if red:
+        b.append(f"{i2}#pragma unroll")
+        b.append(f"{i2}for (int hd = 1; hd < 64; hd <<= 1) {{")
+        for var, ct, _ in red:
+            b.append(f"{i2}  const {ct} u_{var} = __shfl_up({var}, (unsigned)hd, 64);")
+        b.append(f"{i2}  if (hln - hd >= hss) {{")
+        for var, _, op in red:
+            b.append(f"{i2}    {var} = " + (f"{op}({var}, u_{var});" if op else f"{var} + u_{var};"))
+        b.append(f"{i2}  }}")
+        b.append(f"{i2}}}")
+    b += [f"{i2}if (htl) {{",
+          f"{i2}  long long hs_ = -1;",
+          f"{i2}  if (hnul) hs_ = {hm} + 1; else if (hk == ~0ull) hs_ = {hm}; else {{",
+          f"{i2}    u64 hh = hs_mix64(hk) & (u64)({hm} - 1);",
+          f"{i2}    for (int pr_ = 0; pr_ < {HASH_MAX_PROBE}; ++pr_) {{",
+          f"{i2}      const u64 k_ = {kp}[hh];",
+          f"{i2}      if (k_ == hk) {{ hs_ = (long long)hh; break; }}",
+          f"{i2}      if (k_ == ~0ull) {{ const u64 pv_ = atomicCAS(&{kp}[hh], ~0ull, hk);",
+          f"{i2}        if (pv_ == ~0ull || pv_ == hk) {{ hs_ = (long long)hh; break; }} }}",
+          f"{i2}      hh = (hh + 1ull) & (u64)({hm} - 1);",
+          f"{i2}    }}",
+          f"{i2}    if (hs_ < 0) {fl}[0] = 1;",
+          f"{i2}  }}",
+          f"{i2}  if (hs_ >= 0) {{",
+          f"{i2}    const long long hb = hs_ * {na};",
+          f"{i2}    const unsigned long long hrn = (unsigned long long)(hln - hss + 1);"]
+    for i, ag in enumerate(aggs):
+        cnt = f"(unsigned long long)hc{i}" if own[i] else "hrn"
+        tgt = f"(unsigned long long*)&{cp}[hb + {i}]"
+        if ag.kind in (NL.AK_COUNT_STAR, NL.AK_COUNT):
+            b.append(f"{i2}    atomicAdd({tgt}, {cnt});")
+            continue
+        if ag.kind == NL.AK_SUM:
+            b.append(f"{i2}    unsafeAtomicAdd(&{sp}[hb + {i}], hv{i});")
+        elif ag.kind == NL.AK_MIN:
+            b.append(f"{i2}    atomicMin(&{mnp}[hb + {i}], hv{i});")
+        else:
+            b.append(f"{i2}    atomicMax(&{mxp}[hb + {i}], hv{i});")
+        if own[i]:
+            b.append(f"{i2}    atomicAdd({tgt}, {cnt});")
+    b += [f"{i2}  }}", f"{i2}}}", f"{ind}}}"]
+    return b
+
+
 def _acc_decls(aggs, grouped: bool, args: Args) -> List[str]:
     out = [f"  constexpr int NA = {len(aggs)};"]
     if grouped:
@@ -584,17 +707,17 @@ def _col_specs(p, compacts) -> Dict[int, tuple]:
     return out
 
 
-def scan_agg_shape(p: NL.ScanParams, compacts=None, vec: int = 0) -> tuple:
+def scan_agg_shape(p: NL.ScanParams, compacts=None, vec: int = 0, hk=None) -> tuple:
     cols = tuple(sorted(_col_specs(p, compacts).items()))
     preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
                    p.preds[k].group) for k in range(p.npreds))
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
     return ("scan_agg", cols, preds, aggs, p.group_col, SCAN_ITEMS, SCAN_EAGER, vec,
-            SCAN_COMPACT, WAVE_SYNC, VEC_PREFETCH)
+            SCAN_COMPACT, WAVE_SYNC, VEC_PREFETCH, hk.shape() if hk is not None else None)
 
 
-def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
+def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0, hk=None) -> Kernel:
     """Filter + aggregate over row ranges, phase-major over the SCAN_ITEMS rows of each thread
     and branch-free: (1) the predicate columns of every item are loaded together; (2) the
     aggregate inputs (and group column) of every item, where rows that failed the predicates
@@ -611,14 +734,18 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
     preds = [(k, p.preds[k]) for k in range(p.npreds)]
     aggs = [p.aggs[i] for i in range(p.naggs)]
     grouped = p.group_col >= 0
+    assert not (grouped and hk is not None)
     pslots = _pred_slots(preds)
     aslots = [s for s in _agg_slots(aggs) if s not in pslots]
     if grouped and p.group_col not in pslots and p.group_col not in aslots:
         aslots.append(p.group_col)
+    for s in (hk.slots if hk is not None else []):
+        if s not in pslots and s not in aslots:
+            aslots.append(s)
     if SCAN_EAGER:
         pslots, aslots = pslots + aslots, []
     allslots = pslots + aslots
-    approx = _sum_only_slots(preds, aggs, p.group_col, cols)
+    approx = _sum_only_slots(preds, aggs, p.group_col, cols) - set(hk.slots if hk else [])
     NI = vec or SCAN_ITEMS
     T = BLOCK * NI
     if vec:
@@ -651,7 +778,7 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
             b.append(f"{ind}bool pass{it} = act{it} && {_rename(g1.cnf(preds), allslots, it)};")
         if compact:
             b.extend(_compacted_tail(args, cols, NL.MAX_COLS, approx, aggs, grouped, p.group_col,
-                                     aslots, allslots, NI, ind, with_j=False))
+                                     aslots, allslots, NI, ind, with_j=False, hk=hk))
             return
         if aslots:
             for it in range(NI):
@@ -669,6 +796,10 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
                 b.append(f"{ind}pass{it} = pass{it} && {_rename(g2.ok(g), allslots, it)} && "
                          f"gl{it} >= 0 && gl{it} < {ng};")
                 b.append(f"{ind}const int {gvar} = pass{it} ? (int)gl{it} : 0;")
+            if hk is not None:
+                b.extend(_rename(x, allslots, it) for x in
+                         _hash_accumulate(g2, aggs, hk, f"pass{it}", ind))
+                continue
             b.extend(_rename(x, allslots, it) for x in
                      _accumulate(g2, aggs, grouped, f"pass{it}", gvar, ind))
 
@@ -678,7 +809,8 @@ def gen_scan_agg(p: NL.ScanParams, compacts=None, vec: int = 0) -> Kernel:
         _tile_loop(b, T, NI, 0)
         body(b, None)
     b += ["  }"]
-    b += _flush(aggs, grouped)
+    if hk is None:
+        b += _flush(aggs, grouped)
     if compact:
         W = BLOCK // 64
         b.insert(0, f"  typedef {_crow_t(T)} crow_t; __shared__ crow_t crow_s[{W}][{64 * NI}];")
@@ -1078,7 +1210,7 @@ def _rename(line: str, slots, it: int) -> str:
 _SOFF: Dict[int, tuple] = {}
 
 
-def merge_join_shape(p: NL.JoinParams, compacts=None) -> tuple:
+def merge_join_shape(p: NL.JoinParams, compacts=None, hk=None) -> tuple:
     cols = tuple(sorted(_col_specs(p, compacts).items()))
     preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
                    p.preds[k].group) for k in range(p.npreds))
@@ -1086,7 +1218,8 @@ def merge_join_shape(p: NL.JoinParams, compacts=None) -> tuple:
                  for i in range(p.naggs))
     return ("merge_join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey,
             p.key_is_float, MJ_ITEMS, MJ_LDS_KEYS, MJ_STEPS, BLOCK, WAVE_SYNC,
-            _key32_frame(p, compacts) is not None, MJ_EXP)
+            _key32_frame(p, compacts) is not None, MJ_EXP,
+            hk.shape() if hk is not None else None)
 
 
 def key_has_dups(col) -> bool:
@@ -1146,7 +1279,7 @@ def _deferred_append(NI: int, ind: str, pass_fmt: str, row_fmt: str, j_fmt: str)
 
 
 def _deferred_drain(args, cols, split, approx, aggs, grouped, group_col, allslots, ind: str,
-                    final: bool) -> List[str]:
+                    final: bool, hk=None) -> List[str]:
     """Aggregate full 64-entry batches from the top of the wavefront's list (``final``: every
     remaining entry): the aggregate inputs are gathered once per 64 passing rows, all lanes
     active, instead of once per tile."""
@@ -1160,7 +1293,8 @@ def _deferred_drain(args, cols, split, approx, aggs, grouped, group_col, allslot
          f"{ind}  const i64 cj = (i64)lj_s[wv][cok ? ce : cb];"]
     ind2 = ind + "  "
     g = _Gen(args, cols, split, ("crow", "cj"), approx, True)
-    tail = list(dict.fromkeys(_agg_slots(aggs) + ([group_col] if grouped else [])))
+    tail = list(dict.fromkeys(_agg_slots(aggs) + ([group_col] if grouped else []) +
+                              (hk.slots if hk is not None else [])))
     for sl in tail:
         _uload(g, sl, "c", b, ind2)
     gvar = "gic"
@@ -1171,14 +1305,17 @@ def _deferred_drain(args, cols, split, approx, aggs, grouped, group_col, allslot
         b.append(f"{ind2}cok = cok && {_rename(g.ok(group_col), allslots, 'c')} && "
                  f"glc >= 0 && glc < {ng};")
         b.append(f"{ind2}const int {gvar} = cok ? (int)glc : 0;")
-    b += [_rename(x, allslots, "c") for x in _accumulate(g, aggs, grouped, "cok", gvar, ind2)]
+    if hk is not None:
+        b += [_rename(x, allslots, "c") for x in _hash_accumulate(g, aggs, hk, "cok", ind2)]
+    else:
+        b += [_rename(x, allslots, "c") for x in _accumulate(g, aggs, grouped, "cok", gvar, ind2)]
     b += [f"{ind2}wcnt = cb;",
           f"{ind2}{_wave_sync()}",
           f"{ind}}}"]
     return b
 
 
-def gen_merge_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
+def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
     """Co-located sort-merge join + aggregate, re-matching keys every query (no cached join
     index).  Left tiles are ``BLOCK * MJ_ITEMS`` rows of one bucket range, aligned so each thread
     owns ``MJ_ITEMS`` consecutive rows read with aligned vector loads; the tile's right key span
@@ -1227,14 +1364,16 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
     mixed = [(k, q) for k, q in rpreds if (k, q) not in ronly]
     aggs = [p.aggs[i] for i in range(p.naggs)]
     grouped = p.group_col >= 0
+    assert not (grouped and hk is not None)
+    hslots = hk.slots if hk is not None else []
     mixed_left = [x for x in _pred_slots(mixed) if x < split]
     first = list(dict.fromkeys([lk] + _pred_slots(lpreds) + mixed_left))
     ronly_slots = [x for x in _pred_slots(ronly)]
     mixed_right = [x for x in _pred_slots(mixed) if x >= split]
     stage_slots = list(dict.fromkeys([rk] + ronly_slots))
     allslots = list(dict.fromkeys(first + stage_slots + mixed_right + _agg_slots(aggs) +
-                                  ([p.group_col] if grouped else [])))
-    approx = _sum_only_slots(lpreds + rpreds, aggs, p.group_col, cols) - {lk, rk}
+                                  ([p.group_col] if grouped else []) + hslots))
+    approx = _sum_only_slots(lpreds + rpreds, aggs, p.group_col, cols) - {lk, rk} - set(hslots)
     ind = "    "
     g1 = _Gen(args, cols, split, ("row0", "row0"), approx, True)
     b: List[str] = []
@@ -1366,7 +1505,7 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
                 b.extend(_deferred_append(NI, i2, "((pb >> {it}) & 1u)", "row{it}",
                                           "ss + jl{it}"))
                 b.extend(_deferred_drain(args, cols, split, approx, aggs, grouped, p.group_col,
-                                         allslots, i2, final=False))
+                                         allslots, i2, final=False, hk=hk))
             b.append(f"{i2}}}")
 
         one_round(ind)
@@ -1394,8 +1533,9 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None) -> Kernel:
     b.append(f"{ind}}}")
     b += ["  }"]
     b += _deferred_drain(args, cols, split, approx, aggs, grouped, p.group_col, allslots, "  ",
-                         final=True)
-    b += _flush(aggs, grouped)
+                         final=True, hk=hk)
+    if hk is None:
+        b += _flush(aggs, grouped)
     src = (_PRELUDE + args.struct_src() +
            f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_merge_join_agg(Args a) {{\n' +
            "\n".join(b) + "\n}\n")
@@ -1419,7 +1559,7 @@ def merge_join_ok(p: NL.JoinParams, compacts=None, rnrows: int = 0, lnrows: int 
 
 
 def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None, nrows: int = 0,
-                   cache_spans: bool = False, rdup: bool = True):
+                   cache_spans: bool = False, rdup: bool = True, hk=None, htab=None):
     """Sort-merge join + aggregate with ``gen_merge_join_agg`` (same outputs as ``join_agg``);
     ``nrows`` = left table rows; ``rdup`` = the right key column may repeat a key
     (``key_has_dups``)."""
@@ -1429,8 +1569,21 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
     dev = rstart.device
     max_tiles = nrows // T + 2 * rstart.numel() + 2
     tp, spans = _join_spans(p, rstart, rlen, rbucket, roff, max_tiles, T, cache_spans, align=NI)
-    k = kernel_for(merge_join_shape(p, compacts), lambda: gen_merge_join_agg(p, compacts))
+    k = kernel_for(merge_join_shape(p, compacts, hk), lambda: gen_merge_join_agg(p, compacts, hk))
     grid = MJ_GRID
+    if hk is not None:
+        v = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
+             "spans": spans.data_ptr(), "R": rstart.numel(), "nrows": nrows, "rdup": int(rdup),
+             "psum": 0, "pcnt": 0, "pmin": 0, "pmax": 0}
+        _fill_common(v, p.cols, [(k_, p.preds[k_]) for k_ in range(p.npreds)],
+                     [p.aggs[i] for i in range(p.naggs)], compacts)
+        frame = _key32_frame(p, compacts)
+        if frame is not None:
+            v["KLO"], v["KSP"], v["KOF"] = frame
+        v.update(htab.kernel_values())
+        v.update(hk.values())
+        k.launch(grid, v, NL.stream_ptr(), 0)
+        return None
     parts = _partials(grid, GA, dev)
     v = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
          "spans": spans.data_ptr(), "R": rstart.numel(), "nrows": nrows, "rdup": int(rdup),
@@ -1734,7 +1887,7 @@ def _vec_aligned_ptrs(ptrs) -> bool:
 
 def _compacted_tail(args, cols, split, approx, aggs, grouped, group_col, third, allslots,
                     NI: int, ind: str, with_j: bool = True, pass_fmt: str = "pass{it}",
-                    j_fmt: str = "j{it}", dump: bool = False) -> List[str]:
+                    j_fmt: str = "j{it}", dump: bool = False, hk=None) -> List[str]:
     """Phase 3 over the passing rows only.  A join like TPC-H Q3 keeps a few percent of its
     rows, so decoding and accumulating all NI x 64 rows of a wavefront (branch-free) is mostly
     wasted VALU work: instead each lane appends its passing (row, j) pairs to a per-wavefront
@@ -1769,7 +1922,8 @@ def _compacted_tail(args, cols, split, approx, aggs, grouped, group_col, third, 
     g = _Gen(args, cols, split, ("crow", "cj"), approx, True)
     # every slot the aggregates and the group key read, re-loaded at the listed rows (the
     # phase-1/2 registers belong to the original, uncompacted rows)
-    tail = list(dict.fromkeys(_agg_slots(aggs) + ([group_col] if grouped else [])))
+    tail = list(dict.fromkeys(_agg_slots(aggs) + ([group_col] if grouped else []) +
+                              (hk.slots if hk is not None else [])))
     for sl in tail:
         _uload(g, sl, "c", b, ind2)
     gvar = "gic"
@@ -1780,7 +1934,10 @@ def _compacted_tail(args, cols, split, approx, aggs, grouped, group_col, third, 
         b.append(f"{ind2}cok = cok && {_rename(g.ok(group_col), allslots, 'c')} && "
                  f"glc >= 0 && glc < {ng};")
         b.append(f"{ind2}const int {gvar} = cok ? (int)glc : 0;")
-    b += [_rename(x, allslots, "c") for x in _accumulate(g, aggs, grouped, "cok", gvar, ind2)]
+    if hk is not None:
+        b += [_rename(x, allslots, "c") for x in _hash_accumulate(g, aggs, hk, "cok", ind2)]
+    else:
+        b += [_rename(x, allslots, "c") for x in _accumulate(g, aggs, grouped, "cok", gvar, ind2)]
     b += [f"{ind}}}", f"{ind}{_wave_sync()}"]
     return b
 
@@ -2194,6 +2351,17 @@ def kernel_for(shape: tuple, make) -> Kernel:
 # ------------------------------------------------------------------------------------------------
 # Entry points (same outputs as ops.kernels.scan_agg / join_agg)
 # ------------------------------------------------------------------------------------------------
+class _NullTensor:
+    """Stand-in for the partials of a hash-mode launch (their kernel arguments are unused)."""
+
+    @staticmethod
+    def data_ptr() -> int:
+        return 0
+
+
+_NULLT = _NullTensor()
+
+
 def _partials(grid: int, GA: int, dev):
     import torch
     return (torch.empty(grid * GA, dtype=torch.float64, device=dev),
@@ -2226,7 +2394,8 @@ def scan_vec(p: NL.ScanParams, compacts=None, nrows: int = 0) -> int:
     return SCAN_VEC if _vec_aligned_ptrs(ptrs) else 0
 
 
-def scan_agg(p: NL.ScanParams, rstart, rlen, tile_prefix=None, compacts=None, nrows: int = 0):
+def scan_agg(p: NL.ScanParams, rstart, rlen, tile_prefix=None, compacts=None, nrows: int = 0,
+             hk=None, htab=None):
     """``tile_prefix`` must use this kernel's tile (BLOCK * SCAN_ITEMS); None computes it.
     ``compacts``: slot -> ``encoding.Compact`` read instead of the full-width column.
     ``nrows``: rows of the scanned table (enables the vectorized kernel)."""
@@ -2238,7 +2407,14 @@ def scan_agg(p: NL.ScanParams, rstart, rlen, tile_prefix=None, compacts=None, nr
         tile_prefix = K.ranges_to_tiles(rlen, BLOCK * SCAN_ITEMS)
     grid = SCAN_GRID or NL.lib().hs_scan_grid()
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
-    k = kernel_for(scan_agg_shape(p, compacts, vec), lambda: gen_scan_agg(p, compacts, vec))
+    k = kernel_for(scan_agg_shape(p, compacts, vec, hk), lambda: gen_scan_agg(p, compacts, vec, hk))
+    if hk is not None:
+        v = scan_agg_values(p, rstart, rlen, tile_prefix, (_NULLT,) * 4, compacts)
+        v["nrows"] = nrows
+        v.update(htab.kernel_values())
+        v.update(hk.values())
+        k.launch(grid, v, NL.stream_ptr(), 0)
+        return None
     parts = _partials(grid, GA, rstart.device)
     v = scan_agg_values(p, rstart, rlen, tile_prefix, parts, compacts)
     v["nrows"] = nrows

@@ -150,6 +150,30 @@ class DistContext:
             return s, c, mn, mx
         return fetch
 
+    def all_gather_rows(self, rows):
+        """Concatenation over ranks (in rank order) of each rank's int64 ``[n_r, w]`` numpy
+        rows: one all-gather of the counts, one of the rows padded to the largest count (RCCL
+        on device tensors; gloo on host tensors) — no pickling."""
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+        n, w = rows.shape
+        dev = self.device if self.backend == "nccl" else "cpu"
+        cnt = torch.tensor([n], dtype=torch.int64, device=dev)
+        counts = [torch.zeros_like(cnt) for _ in range(self.world)]
+        dist.all_gather(counts, cnt)
+        counts = [int(c.item()) for c in counts]
+        mx = max(counts)
+        if mx == 0:
+            return np.zeros((0, w), dtype=np.int64)
+        buf = torch.zeros((mx, w), dtype=torch.int64)
+        if n:
+            buf[:n] = torch.from_numpy(np.ascontiguousarray(rows))
+        buf = buf.to(dev)
+        outs = [torch.empty_like(buf) for _ in range(self.world)]
+        dist.all_gather(outs, buf)
+        return torch.cat([o[:c] for o, c in zip(outs, counts)]).cpu().numpy()
+
     def agree_any(self, flags) -> list:
         """Element-wise OR of a list of booleans over all ranks (one small max all-reduce on a
         tensor — used where every rank must take the same data-dependent decision)."""

@@ -86,6 +86,18 @@ class Column:
     def between(self, lo, hi):
         return (self >= lo) & (self <= hi)
 
+    def asc(self):
+        """Sort order for ``orderBy`` (ascending, nulls first — Spark's default)."""
+        c = Column(self.expr)
+        c.sort_ascending = True
+        return c
+
+    def desc(self):
+        """Sort order for ``orderBy`` (descending, nulls last)."""
+        c = Column(self.expr)
+        c.sort_ascending = False
+        return c
+
     def alias(self, name: str):
         return Column(E.Alias(self.expr, name))
 

@@ -216,7 +216,14 @@ class DataFrame:
     unionAll = union
 
     def orderBy(self, *cols, ascending=True) -> "DataFrame":
-        orders = [L.SortOrder(self._resolve(self._to_expr(c)), ascending) for c in cols]
+        """``ascending``: one flag or one per column; ``col(x).desc()`` / ``.asc()`` override it
+        per column (mixed orders such as TPC-H Q3's ``revenue DESC, o_orderdate``)."""
+        if len(cols) == 1 and isinstance(cols[0], (list, tuple)):
+            cols = tuple(cols[0])
+        flags = list(ascending) if isinstance(ascending, (list, tuple)) else [ascending] * len(cols)
+        orders = [L.SortOrder(self._resolve(self._to_expr(c)),
+                              bool(getattr(c, "sort_ascending", f)))
+                  for c, f in zip(cols, flags)]
         return DataFrame(self.session, L.Sort(orders, True, self.plan))
 
     sort = orderBy

@@ -45,12 +45,14 @@ class QueryExecution:
                 pc = plan_cache(self.session)
                 plan, key, ctx = pc.lookup(self.session, self.logical)
                 if plan is not None:
+                    if ctx.reuse:
+                        plan = reuse_exchanges(plan, self.session)
                     self._executed = plan
                     return plan
-            self._executed = reuse_exchanges(ensure_requirements(self.spark_plan, self.session),
-                                             self.session)
+            planned = ensure_requirements(self.spark_plan, self.session)
+            self._executed = reuse_exchanges(planned, self.session)
             if pc is not None:
-                pc.store(key, self._executed, ctx)
+                pc.store(key, planned, ctx)
         return self._executed
 
     executedPlan = executed_plan

@@ -817,7 +817,13 @@ def canonical_string(plan: SparkPlan) -> str:
             s += f" @{hash(tuple(sorted(repr(f) for f in node.relation.location.all_files())))}"
             s += f" {sorted(node.selected_buckets) if node.selected_buckets else ''}"
         lines.append(s)
-    return _EXPR_ID.sub(sub, "\n".join(lines))
+    # literal values verbatim (not renumbered): a string literal such as 'item#5' renders like
+    # an attribute id, so two subtrees differing only in such literals would otherwise match
+    from .plan_cache import _iter_literals
+    lits: list = []
+    _iter_literals(plan, lits, set())
+    tail = "\n#literals " + repr([(str(x.dtype), x.value) for x in lits])
+    return _EXPR_ID.sub(sub, "\n".join(lines)) + tail
 
 
 def reuse_exchanges(plan: SparkPlan, session) -> SparkPlan:

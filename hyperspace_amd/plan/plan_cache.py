@@ -47,12 +47,13 @@ class _NotCacheable(Exception):
 
 
 class _Ctx:
-    __slots__ = ("ids", "lits", "refs")
+    __slots__ = ("ids", "lits", "refs", "reuse")
 
     def __init__(self):
         self.ids: Dict[int, int] = {}
         self.lits: List[E.Literal] = []
         self.refs: list = []
+        self.reuse = False   # a hit must run exchange reuse on the substituted plan
 
     def eid(self, x: int) -> int:
         v = self.ids.get(x)
@@ -278,7 +279,8 @@ class PlanCache:
         if hit is None:
             self.misses += 1
             return None, key, ctx
-        plan, old_lits, paths, _refs = hit
+        plan, old_lits, paths, _refs, reuse = hit
+        ctx.reuse = reuse
         if len(old_lits) != len(ctx.lits):
             self.misses += 1
             return None, key, ctx
@@ -292,9 +294,21 @@ class PlanCache:
         return new_plan, key, ctx
 
     def store(self, key, executed, ctx: _Ctx) -> bool:
-        """Cache ``executed`` for ``key`` if every literal of the analyzed plan reached it."""
+        """Cache ``executed`` — the plan *before* exchange reuse — for ``key`` if every literal
+        of the analyzed plan reached it.  Exchange reuse compares canonical subtrees including
+        literal values (a self-join with equal filter literals shares one exchange, with unequal
+        ones it must not), so it is never part of a cached plan: entries whose plan has two
+        exchanges that could match are flagged and re-run ``reuse_exchanges`` after each
+        substitution."""
         if key is None:
             return False
+        from . import physical as X
+        exch = executed.collect(lambda n: isinstance(n, (X.ShuffleExchangeExec,
+                                                         X.BroadcastExchangeExec)))
+        shapes = [(type(e).__name__, len(e.output), type(getattr(e, "partitioning", None)).__name__,
+                   getattr(getattr(e, "partitioning", None), "num_partitions", None))
+                  for e in exch]
+        reuse = len(shapes) != len(set(shapes))
         present: List[E.Literal] = []
         _iter_literals(executed, present, set())
         ids = {id(x) for x in present}
@@ -308,7 +322,7 @@ class PlanCache:
                 _hot_paths(executed, {id(x)}, hot, {})
                 paths[id(x)] = hot
         with self._lock:
-            self._lru[key] = (executed, list(ctx.lits), paths, list(ctx.refs))
+            self._lru[key] = (executed, list(ctx.lits), paths, list(ctx.refs), reuse)
             while len(self._lru) > self.capacity:
                 self._lru.popitem(last=False)
         return True

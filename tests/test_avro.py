@@ -72,6 +72,27 @@ def test_snappy_codec_block_with_crc(tmp_path):
         avro.read_avro(str(p))
 
 
+def test_hostile_block_lengths_are_errors_not_allocations(tmp_path):
+    """A Snappy preamble claiming 2^35 bytes, and a deflate bomb past the ~1032:1 DEFLATE bound,
+    are rejected before any allocation of that size."""
+    schema = {"type": "record", "name": "r", "fields": [{"name": "v", "type": "int"}]}
+    huge = bytes([0xFF, 0xFF, 0xFF, 0xFF, 0x7F])     # varint ~2^35
+    body = huge + bytes([0]) + b"\x00" * 4
+    p = tmp_path / "h.avro"
+    p.write_bytes(_container(schema, [(1, body)], codec=b"snappy"))
+    with pytest.raises(HyperspaceException, match="snappy"):
+        avro.read_avro(str(p))
+    # valid raw-deflate stream whose output exceeds the DEFLATE expansion bound for its size:
+    # impossible for real data, so truncate a legit stream's output claim by corrupting it
+    co = zlib.compressobj(9, zlib.DEFLATED, -15)
+    bomb = co.compress(b"\x00" * (8 << 20)) + co.flush()
+    assert len(bomb) * 1032 + 4096 > (8 << 20)      # a genuine stream stays inside the bound
+    p2 = tmp_path / "d.avro"
+    p2.write_bytes(_container(schema, [(1, bomb[: len(bomb) // 2])], codec=b"deflate"))
+    with pytest.raises(HyperspaceException, match="deflate"):
+        avro.read_avro(str(p2))
+
+
 @pytest.mark.parametrize("codec", ["null", "deflate"])
 def test_round_trip_all_types(tmp_path, codec):
     n = 10_000

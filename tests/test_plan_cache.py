@@ -133,3 +133,38 @@ def test_base_relation_fingerprint_memo(data, tmp_path):
     got = _filter_q(df, 4).collect()
     s.conf.set("spark.hyperspace.mi.planCache.enabled", "false")
     assert sorted(got) == sorted(_filter_q(df, 4).collect())
+
+
+def test_self_join_exchange_reuse_is_not_parameterized(data):
+    """Exchange reuse compares subtrees including literal values, so a self-join planned with
+    equal literals (one exchange reused) must not serve a later query whose literals differ
+    (cached ReusedExchange replayed the first side's filter on both sides)."""
+    s, _, df, _ = data
+    s.disableHyperspace()
+
+    def q(x1, x2):
+        a = df.filter(col("v") > x1).select("k", "v")
+        b = df.filter(col("v") > x2).select("k", "v")
+        return a.join(b, a["k"] == b["k"])   # rows: both sides' columns
+
+    got = [_rows(q(0.5, 0.5)), _rows(q(0.5, 0.9)), _rows(q(0.2, 0.7))]
+    tree = q(0.5, 0.5).queryExecution.executed_plan.tree_string()
+    assert "ReusedExchange" in tree, tree
+    s.conf.set("spark.hyperspace.mi.planCache.enabled", "false")
+    want = [_rows(q(0.5, 0.5)), _rows(q(0.5, 0.9)), _rows(q(0.2, 0.7))]
+    assert got == want
+    assert got[0] != got[1]
+
+
+def test_canonical_string_keeps_literal_text():
+    """Literal strings that look like attribute ids do not canonicalize together."""
+    import pyarrow as pa
+    from hyperspace_amd.plan import expressions as E
+    from hyperspace_amd.plan import physical as X
+    a = E.Attribute("s", pa.string())
+    scan = X.LocalTableScanExec(pa.table({"s": ["x"]}), [a])
+    f1 = X.FilterExec(E.EqualTo(a, E.Literal("item#5")), scan)
+    f2 = X.FilterExec(E.EqualTo(a, E.Literal("item#7")), scan)
+    assert X.canonical_string(f1) != X.canonical_string(f2)
+    f3 = X.FilterExec(E.EqualTo(a, E.Literal("item#5")), scan)
+    assert X.canonical_string(f1) == X.canonical_string(f3)

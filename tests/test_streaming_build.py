@@ -69,3 +69,17 @@ def test_streaming_build_is_byte_identical(tmp_path, device):
     assert sorted(one) == sorted(many) and len(one) == 16
     for b in one:
         assert one[b] == many[b], f"bucket {b} differs"
+
+
+def test_footer_info_marks_uncovered_columns_nullable(tmp_path):
+    """Columns a Parquet footer does not cover (hive partition columns, columns missing from
+    the file) may hold nulls: the multi-GPU batched exchange agrees on validity masks from
+    this before its first collective batch (exec/device_build.py)."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from hyperspace_amd.exec.device_build import _footer_info
+    p = tmp_path / "f.parquet"
+    pq.write_table(pa.table({"a": [1, 2, 3], "b": [1.0, None, 2.0]}), p)
+    rows, maybe = _footer_info(str(p), ["a", "b", "part", "missing"])
+    assert rows == 3
+    assert maybe == {"b", "part", "missing"}

@@ -356,3 +356,13 @@ def test_lint_gate_no_undefined_names():
     r = subprocess.run([sys.executable, os.path.join(root, "scripts", "lint_names.py")],
                        cwd=root, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
+
+
+def test_negative_zero_float_keys_bucket_like_spark_2_4():
+    """Spark 2.4.2 (the reference's build.sbt:19) hashes a double's raw bits: 0.0 and -0.0 land
+    in different buckets (SPARK-26021, fixed only in Spark 3.0).  Kept on purpose for bucket-id
+    parity with reference-built indexes; documented in docs/user-guide.md."""
+    import pyarrow as pa
+    from hyperspace_amd.utils import murmur3
+    b = murmur3.bucket_ids([pa.array([0.0, -0.0])], 200)
+    assert int(b[0]) != int(b[1])
