@@ -749,8 +749,10 @@ class GpuBackend:
     # ------------------------------------------------------------------------------------------
     # Joins
     # ------------------------------------------------------------------------------------------
+    JOIN_TYPES = ("inner", "left", "right", "full", "leftsemi", "leftanti")
+
     def _join_inputs(self, p: X.SortMergeJoinExec):
-        if p.join_type != "inner":
+        if p.join_type not in self.JOIN_TYPES:
             raise Unsupported(f"{p.join_type} join on device")
         if not all(isinstance(k, E.Attribute) for k in list(p.left_keys) + list(p.right_keys)):
             raise Unsupported("expression join keys")
@@ -903,13 +905,21 @@ class GpuBackend:
         return p, col_info, descs, (lb, rb)
 
     def _join_rel(self, p: X.SortMergeJoinExec) -> DRel:
+        """Row-producing co-located join: matched (left row, right row) pairs from the join
+        kernels, then per join type — inner: the pairs; left/right/full outer: plus the
+        unmatched rows of the preserved side(s) (rows passing that side's own filters, marked
+        by a scatter of the matched ids and selected in order) padded with NULLs (gather index
+        -1); left semi / anti: the left rows that do / do not appear in a pair.  Reference: the
+        rule rewrites any join type (JoinIndexRule.scala:58), Spark's bucketed SortMergeJoin
+        runs it."""
         left, right, lk, rk = self._join_inputs(p)
         if left.parts or right.parts:
             raise Unsupported("row-producing join over a bucket union")
+        jt = p.join_type
         out_attrs = list(p.output)
         implied: set = set()
-        probed = self._probe_ranges(left, right, lk, rk)
-        if probed is None:
+        probed = self._probe_ranges(left, right, lk, rk) if jt in ("inner", "leftsemi") else None
+        if probed is None and jt in ("inner", "leftsemi", "right"):
             probed = self._domain_pruned_ranges(left, right, lk, rk)
         if probed is not None:
             rstart, rlen, rbk = probed
@@ -930,8 +940,35 @@ class GpuBackend:
         lset = {a.expr_id for a in p.left.output}
         lattrs = [a for a in out_attrs if a.expr_id in lset]
         rattrs = [a for a in out_attrs if a.expr_id not in lset]
-        lg = K.gather_columns([left.col(a) for a in lattrs], ol)
-        rg = K.gather_columns([right.col(a) for a in rattrs], orr)
+        padded = jt in ("left", "right", "full")
+        if jt != "inner":
+            import torch
+            with stage("join.outer_rows"):
+                if jt in ("left", "full", "leftsemi", "leftanti"):
+                    lsel = self._selected_rows(left)
+                    lmark = K.mark_rows(ol, int(left.table.num_rows or 0))
+                if jt in ("leftsemi", "leftanti"):
+                    ol = K.select_marked(lsel, lmark, 1 if jt == "leftsemi" else 0)
+                    orr = ol[:0]
+                    rattrs = []
+                else:
+                    extra_l, extra_r = [], []
+                    if jt in ("left", "full"):
+                        um = K.select_marked(lsel, lmark, 0)
+                        extra_l.append(um)
+                        extra_r.append(torch.full_like(um, -1))
+                    if jt in ("right", "full"):
+                        rsel = self._selected_rows(right)
+                        rmark = K.mark_rows(orr, int(right.table.num_rows or 0))
+                        um = K.select_marked(rsel, rmark, 0)
+                        extra_l.append(torch.full_like(um, -1))
+                        extra_r.append(um)
+                    ol = torch.cat([ol] + extra_l)
+                    orr = torch.cat([orr] + extra_r)
+        lg = K.gather_columns([left.col(a) for a in lattrs], ol,
+                              padded=padded and jt in ("right", "full"))
+        rg = K.gather_columns([right.col(a) for a in rattrs], orr,
+                              padded=padded and jt in ("left", "full"))
         cols = {}
         for a, c in list(zip(lattrs, lg)) + list(zip(rattrs, rg)):
             c.hs_transient = True
@@ -982,7 +1019,7 @@ class GpuBackend:
         while isinstance(node, X.ProjectExec) and all(isinstance(e, E.Attribute) for e in node.project_list):
             node = node.child
         self._groups_agreed = False
-        if isinstance(node, X.SortMergeJoinExec):
+        if isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner":
             res = self._join_agg(node, fns, group)
         else:
             res = self._scan_agg(self._rel(child), fns, group)
@@ -1373,7 +1410,7 @@ class GpuBackend:
         while isinstance(node, X.ProjectExec) and \
                 all(isinstance(e, E.Attribute) for e in node.project_list):
             node = node.child
-        if isinstance(node, X.SortMergeJoinExec):
+        if isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner":
             left, right, lk, rk = self._join_inputs(node)
             lparts, rparts = left.parts or [left], right.parts or [right]
             rels = lparts + rparts

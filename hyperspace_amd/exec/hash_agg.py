@@ -171,7 +171,7 @@ def plan_keys(items, own_counts) -> KeyPlan:
             k.lo, span = 0, max(len(k.dictionary), 1)
             k.bits = max(0, int(span - 1 + (1 if k.nullable else 0)).bit_length())
         else:
-            lo, span = dom
+            lo, span = dom[0], dom[1]
             k.lo = int(lo)
             k.bits = max(0, int(max(span, 1) - 1 + (1 if k.nullable else 0)).bit_length())
         k.shift = shift

@@ -192,6 +192,9 @@ def lib():
     _sig(L.hs_snappy_compress, I, P, I, P, I64, P, P)
     _sig(L.hs_snappy_pack, I, P, I64, P, P, I, P, P)
     _sig(L.hs_snappy_compress_host, I64, P, I64, P)
+    _sig(L.hs_mark_rows, I, P, I64, P, P)
+    _sig(L.hs_select_marked_blocks, I64, I64)
+    _sig(L.hs_select_marked, I, P, I64, P, I, P, P, P, P)
     _sig(L.hs_hagg_extract_chunk, I)
     _sig(L.hs_topk_chunk, I)
     _sig(L.hs_hagg_init, I, P, P, P, P, P, I64, I, P)

@@ -185,8 +185,10 @@ def exclusive_scan_i64(x):
 # ------------------------------------------------------------------------------------------------
 # Gather
 # ------------------------------------------------------------------------------------------------
-def gather_columns(cols: list, idx, want_valid: bool = True) -> list:
-    """Gather a list of DeviceColumns by ``idx`` (int32 or int64 tensor) in one launch."""
+def gather_columns(cols: list, idx, want_valid: bool = True, padded: bool = False) -> list:
+    """Gather a list of DeviceColumns by ``idx`` (int32 or int64 tensor) in one launch.
+    ``padded``: ``idx`` (int64) may hold -1 for outer-join padding rows, which come out NULL
+    (every output column then carries a validity mask)."""
     torch = _torch()
     from ..exec.device_table import DeviceColumn
     n = idx.numel()
@@ -198,7 +200,7 @@ def gather_columns(cols: list, idx, want_valid: bool = True) -> list:
         for j, c in enumerate(chunk):
             dst = torch.empty(n, dtype=c.data.dtype, device=c.data.device)
             dv = torch.empty(n, dtype=torch.uint8, device=c.data.device) \
-                if (c.valid is not None and want_valid) else None
+                if ((c.valid is not None and want_valid) or padded) else None
             p.cols[j] = NL.GatherCol(c.data.data_ptr(), dst.data_ptr(),
                                      c.valid.data_ptr() if c.valid is not None else 0,
                                      dv.data_ptr() if dv is not None else 0,
@@ -209,6 +211,29 @@ def gather_columns(cols: list, idx, want_valid: bool = True) -> list:
         NL.check(NL.lib().hs_gather(C.byref(p), NL.ptr(idx), n, NL.stream_ptr()), "hs_gather")
         out.extend(res)
     return out
+
+
+def mark_rows(idx, n: int):
+    """uint8 [n]: 1 at every row id of ``idx`` (int64; negative ids ignored)."""
+    torch = _torch()
+    mark = torch.zeros(max(n, 1), dtype=torch.uint8, device=idx.device)
+    NL.check(NL.lib().hs_mark_rows(NL.ptr(idx), idx.numel(), NL.ptr(mark), NL.stream_ptr()),
+             "hs_mark_rows")
+    return mark
+
+
+def select_marked(rows, mark, want: int):
+    """The row ids of ``rows`` (int64, order kept) whose ``mark`` byte equals ``want``."""
+    torch = _torch()
+    L = NL.lib()
+    n = rows.numel()
+    dev = rows.device
+    ws = torch.empty(max(int(L.hs_select_marked_blocks(n)), 1), dtype=torch.int64, device=dev)
+    total = torch.empty(1, dtype=torch.int64, device=dev)
+    out = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    NL.check(L.hs_select_marked(NL.ptr(rows), n, NL.ptr(mark), int(want), NL.ptr(ws),
+                                NL.ptr(total), NL.ptr(out), NL.stream_ptr()), "hs_select_marked")
+    return out[:int(total.item())]
 
 
 def histogram(ids, num_bins: int):
