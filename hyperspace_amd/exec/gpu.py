@@ -1518,7 +1518,7 @@ class GpuBackend:
             return (0, 0, scale)
         return (lo, hi - lo + 1, scale)
 
-    def _hash_keyplan(self, grouping, col_info, rel_of, doms, specs, descs):
+    def _hash_keyplan(self, grouping, col_info, fns, doms, specs, descs):
         from . import hash_agg as H
         items = []
         for g in grouping:
@@ -1528,7 +1528,8 @@ class GpuBackend:
         for a in specs:
             own.append(a.kind != NL.AK_COUNT_STAR and
                        any(descs[a.col[t]].valid is not None for t in range(a.nterms)))
-        return H.plan_keys(items, tuple(own))
+        need_star = any(isinstance(fn, (E.Count, E.Avg)) for fn in fns)
+        return H.plan_keys(items, tuple(own), need_star)
 
     def _scan_hash(self, r: DRel, fns, grouping, doms, table, hk_box) -> None:
         col_info, descs = self._column_infos([(r, 0)])
@@ -1540,7 +1541,7 @@ class GpuBackend:
         bound = CP.bind(CP.to_cnf([c for c in r.conds if id(c) not in implied]), col_info,
                         self.device)
         specs = self._agg_specs(fns, col_info)
-        hk = self._hash_keyplan(grouping, col_info, None, doms, specs, descs)
+        hk = self._hash_keyplan(grouping, col_info, fns, doms, specs, descs)
         if not hk_box:
             hk_box.append(hk)
         p = NL.ScanParams()
@@ -1576,7 +1577,7 @@ class GpuBackend:
             left, right, lk, rk, node.condition,
             lconds=[c for c in left.conds if id(c) not in implied])
         specs = self._agg_specs(fns, col_info)
-        hk = self._hash_keyplan(grouping, col_info, None, doms, specs, descs)
+        hk = self._hash_keyplan(grouping, col_info, fns, doms, specs, descs)
         if not hk_box:
             hk_box.append(hk)
         jp.group_col, jp.num_groups, jp.group_base = -1, 1, 0
@@ -1599,9 +1600,9 @@ class GpuBackend:
                                rdup=jit.key_has_dups(right.col(rk)), hk=hk, htab=table)
 
     def _hash_combine_ranks(self, d, groups, G: int, A: int, minmax: bool):
-        """Every rank's groups to every rank (one variable-size all-gather of packed rows),
-        merged in a device table: ranks may share groups (any key not led by the bucket key)."""
-        import torch
+        """Every rank's groups to every rank (one variable-size all-gather of packed rows, no
+        pickling), merged in a device table: ranks may share groups (any key not led by the
+        bucket key)."""
         from . import hash_agg as H
         with stage("hagg.combine_ranks"):
             host = groups.to_host(G)
@@ -1615,21 +1616,20 @@ class GpuBackend:
             n = allr.shape[0]
             if n == 0:
                 return groups, 0
-            dev = self.device
-            cat = torch.from_numpy(allr).to(dev)
-            keys = cat[:, 0].contiguous()
-            nulls = cat[:, 1].to(torch.uint8).contiguous()
 
             def col(j):
-                return cat[:, 2 + j * A: 2 + (j + 1) * A].contiguous().view(-1)
-            sums, cnts = col(0).view(torch.float64), col(1)
-            mins = col(2).view(torch.float64) if minmax else None
-            maxs = col(3).view(torch.float64) if minmax else None
+                return np.ascontiguousarray(allr[:, 2 + j * A: 2 + (j + 1) * A])
+            merged_in = H.Groups.from_host(
+                {"keys": allr[:, 0].copy().view(np.uint64), "nulls": allr[:, 1].astype(np.uint8),
+                 "sums": col(0).view(np.float64), "cnts": col(1),
+                 "mins": col(2).view(np.float64), "maxs": col(3).view(np.float64)},
+                A, minmax, self.device)
             M = H.next_pow2(max(H.MIN_SLOTS, 2 * n))
-            table = self.htables.get(M, A, minmax, dev)
-            NL.check(NL.lib().hs_hagg_merge(NL.ptr(keys), NL.ptr(nulls), NL.ptr(sums),
-                                            NL.ptr(cnts), NL.ptr(mins), NL.ptr(maxs), n,
-                                            NL.ptr(table.keys), NL.ptr(table.sums),
+            table = self.htables.get(M, A, minmax, self.device)
+            g = merged_in
+            NL.check(NL.lib().hs_hagg_merge(NL.ptr(g.keys), NL.ptr(g.nulls), NL.ptr(g.sums),
+                                            NL.ptr(g.cnts), NL.ptr(g.mins), NL.ptr(g.maxs), n,
+                                            g.cap, NL.ptr(table.keys), NL.ptr(table.sums),
                                             NL.ptr(table.cnts), NL.ptr(table.mins),
                                             NL.ptr(table.maxs), M, A, NL.ptr(table.flag),
                                             NL.stream_ptr()), "hs_hagg_merge")
@@ -1658,13 +1658,11 @@ class GpuBackend:
             inner = agg.child if isinstance(agg, E.Alias) else agg
             if isinstance(inner, E.AggregateFunction):
                 i = next(k for k, fn in enumerate(fns) if fn is inner)
-                cs = i if hk.own_counts[i] else A - 1
+                cs = i if hk.own_counts[i] else (A - 1 if hk.need_star else -1)
                 src = {E.Sum: H.SRC_SUM, E.Count: H.SRC_COUNT, E.Min: H.SRC_MIN,
                        E.Max: H.SRC_MAX, E.Avg: H.SRC_AVG}.get(type(inner))
                 if src is None:
                     return None
-                if src == H.SRC_COUNT:
-                    cs = i if hk.own_counts[i] else A - 1
                 return H.OrderSource(src, i, cs, desc=desc)
             if isinstance(inner, E.Attribute):
                 e = inner
@@ -1689,6 +1687,8 @@ class GpuBackend:
         """Result table of a hash-mode aggregate from its host group arrays (vectorized
         finalize; arithmetic over aggregates with pyarrow.compute)."""
         G = 0 if host is None else len(host["keys"])
+        if G and hk is not None and not hk.need_star:
+            host["cnts"][:, A - 1] = 1     # COUNT(*) not accumulated: every group has rows
         gmap = {}
         if hk is not None and G:
             for g, arr in zip(grouping, hk.unpack(host["keys"], host["nulls"])):

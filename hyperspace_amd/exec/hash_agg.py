@@ -58,15 +58,19 @@ class KeyCol:
 class KeyPlan:
     """Packing of a query's group columns into the hash table's 64-bit key."""
 
-    def __init__(self, cols: List[KeyCol], mode: str, own_counts: Tuple[bool, ...]):
+    def __init__(self, cols: List[KeyCol], mode: str, own_counts: Tuple[bool, ...],
+                 need_star: bool = True):
         self.cols = cols
         self.mode = mode                  # "packed" | "raw_int" | "raw_float"
         self.own_counts = own_counts      # per aggregate: its own non-null count is kept
+        # the implicit COUNT(*) is accumulated only when a result reads it (COUNT / AVG);
+        # otherwise every stored group counts as one row (groups exist only with rows)
+        self.need_star = need_star
         self.slots = [c.slot for c in cols]
 
     def shape(self) -> tuple:
         return (self.mode, tuple((c.slot, c.kind, c.nullable) for c in self.cols),
-                self.own_counts)
+                self.own_counts, self.need_star)
 
     def values(self) -> Dict[str, int]:
         v = {}
@@ -133,7 +137,7 @@ def _to_arrow(c: KeyCol, vals: np.ndarray, mask) -> pa.Array:
         return arr
 
 
-def plan_keys(items, own_counts) -> KeyPlan:
+def plan_keys(items, own_counts, need_star: bool = True) -> KeyPlan:
     """``items``: (slot, attr, DeviceColumn, (lo, span)) per group column, in GROUP BY order;
     the domain covers every part and rank (span 0 = no non-null values), so all launches of a
     query (bucket-union parts, ranks) pack keys identically."""
@@ -154,7 +158,7 @@ def plan_keys(items, own_counts) -> KeyPlan:
             raise Unsupported(f"group key type {c.atype}")
         cols.append(KeyCol(slot, attr, kind, nullable, dictionary=c.dictionary, atype=c.atype))
     if len(cols) == 1 and cols[0].kind in ("f64", "f32"):
-        return KeyPlan(cols, "raw_float", own_counts)
+        return KeyPlan(cols, "raw_float", own_counts, need_star)
     shift = 0
     for k, (_, _, c, dom) in zip(cols, items):
         if k.kind == "f64":
@@ -178,17 +182,17 @@ def plan_keys(items, own_counts) -> KeyPlan:
         shift += k.bits
     if shift > 64:
         if len(cols) == 1 and cols[0].kind == "int":
-            return KeyPlan(cols, "raw_int", own_counts)
+            return KeyPlan(cols, "raw_int", own_counts, need_star)
         raise Unsupported("group key does not pack into 64 bits")
-    return KeyPlan(cols, "packed", own_counts)
+    return KeyPlan(cols, "packed", own_counts, need_star)
 
 
 # ------------------------------------------------------------------------------------------------
 # Tables
 # ------------------------------------------------------------------------------------------------
 class HashTable:
-    """One device hash table (M probe slots + 2 direct slots, NA aggregates per group).  Tables
-    are pooled per (M, NA, min/max) and always left clean by ``extract(reset=True)``."""
+    """One device hash table (M probe slots + 2 direct slots, NA aggregates per group, SoA).
+    Tables are pooled per (M, NA, min/max) and always left clean by ``extract`` (reset)."""
 
     def __init__(self, M: int, NA: int, minmax: bool, device):
         import torch
@@ -212,39 +216,46 @@ class HashTable:
                 "HM": self.M, "hflag": self.flag.data_ptr()}
 
     def extract(self, star: int) -> "Groups":
-        """Stream-ordered: dense groups of this table (capacity M + 2 rows, the count ``G`` stays
-        on the device until ``Groups.count()``), the table reset for the next query."""
+        """Stream-ordered: dense groups of this table (SoA, capacity M + 2 rows; the count ``G``
+        stays on the device until ``Groups.count()``), the table reset for the next query."""
         import torch
         L = NL.lib()
         cap = self.M + 2
-        dev = self.device
-        g = Groups(self.NA, dev)
-        g.keys = torch.empty(cap, dtype=torch.int64, device=dev)
-        g.nulls = torch.empty(cap, dtype=torch.uint8, device=dev)
-        g.sums = torch.empty(cap * self.NA, dtype=torch.float64, device=dev)
-        g.cnts = torch.empty(cap * self.NA, dtype=torch.int64, device=dev)
-        g.mins = torch.empty(cap * self.NA, dtype=torch.float64, device=dev) if self.minmax else None
-        g.maxs = torch.empty(cap * self.NA, dtype=torch.float64, device=dev) if self.minmax else None
-        ws = torch.empty(int(L.hs_hagg_extract_blocks(self.M)), dtype=torch.int64, device=dev)
-        g.total = torch.empty(2, dtype=torch.int64, device=dev)
+        g = Groups.alloc(self.NA, cap, self.minmax, self.device)
+        ws = torch.empty(int(L.hs_hagg_extract_blocks(self.M)), dtype=torch.int64,
+                         device=self.device)
+        g.total = torch.empty(2, dtype=torch.int64, device=self.device)
         NL.check(L.hs_hagg_extract(NL.ptr(self.keys), NL.ptr(self.sums), NL.ptr(self.cnts),
                                    NL.ptr(self.mins), NL.ptr(self.maxs), self.M, self.NA, star, 1,
-                                   NL.ptr(ws), NL.ptr(g.total), NL.ptr(self.flag),
-                                   NL.ptr(g.keys), NL.ptr(g.nulls),
-                                   NL.ptr(g.sums), NL.ptr(g.cnts), NL.ptr(g.mins),
-                                   NL.ptr(g.maxs), NL.stream_ptr()), "hs_hagg_extract")
+                                   NL.ptr(ws), NL.ptr(g.total), NL.ptr(self.flag), cap,
+                                   NL.ptr(g.keys), NL.ptr(g.nulls), NL.ptr(g.sums),
+                                   NL.ptr(g.cnts), NL.ptr(g.mins), NL.ptr(g.maxs),
+                                   NL.stream_ptr()), "hs_hagg_extract")
         return g
 
 
 class Groups:
-    """Dense per-group arrays on the device: keys (u64 bits), nulls (raw single-column NULL
-    key), and NA (sum, count, min, max) partials per group."""
+    """Dense per-group arrays on the device (SoA, row stride ``cap``): keys (u64 bits), nulls
+    (raw single-column NULL key), and NA (sum, count, min, max) partials per group."""
 
-    def __init__(self, NA: int, device):
-        self.NA, self.device = NA, device
+    def __init__(self, NA: int, cap: int, device):
+        self.NA, self.cap, self.device = NA, cap, device
         self.keys = self.nulls = self.sums = self.cnts = self.mins = self.maxs = None
         self.total = None
         self._host_total = None
+
+    @staticmethod
+    def alloc(NA: int, cap: int, minmax: bool, device) -> "Groups":
+        import torch
+        g = Groups(NA, cap, device)
+        c = max(cap, 1)
+        g.keys = torch.empty(c, dtype=torch.int64, device=device)
+        g.nulls = torch.empty(c, dtype=torch.uint8, device=device)
+        g.sums = torch.empty(c * NA, dtype=torch.float64, device=device)
+        g.cnts = torch.empty(c * NA, dtype=torch.int64, device=device)
+        g.mins = torch.empty(c * NA, dtype=torch.float64, device=device) if minmax else None
+        g.maxs = torch.empty(c * NA, dtype=torch.float64, device=device) if minmax else None
+        return g
 
     def count(self) -> Tuple[int, bool]:
         if self._host_total is None:
@@ -255,36 +266,54 @@ class Groups:
     def set_count(self, n: int) -> None:
         self._host_total = (n, False)
 
+    def _cols(self, t, G: int):
+        """[G, NA] host array of a SoA device array (columns at stride cap)."""
+        if t is None:
+            return None
+        return t.view(self.NA, self.cap)[:, :G].cpu().numpy().T
+
     def to_host(self, n: Optional[int] = None) -> dict:
         G = self.count()[0] if n is None else n
-        NA = self.NA
         out = {"keys": self.keys[:G].cpu().numpy().view(np.uint64),
                "nulls": self.nulls[:G].cpu().numpy(),
-               "sums": self.sums[:G * NA].cpu().numpy().reshape(G, NA),
-               "cnts": self.cnts[:G * NA].cpu().numpy().reshape(G, NA)}
-        out["mins"] = (self.mins[:G * NA].cpu().numpy().reshape(G, NA) if self.mins is not None
-                       else np.full((G, NA), np.inf))
-        out["maxs"] = (self.maxs[:G * NA].cpu().numpy().reshape(G, NA) if self.maxs is not None
-                       else np.full((G, NA), -np.inf))
+               "sums": self._cols(self.sums, G), "cnts": self._cols(self.cnts, G)}
+        out["mins"] = self._cols(self.mins, G) if self.mins is not None else \
+            np.full((G, self.NA), np.inf)
+        out["maxs"] = self._cols(self.maxs, G) if self.maxs is not None else \
+            np.full((G, self.NA), -np.inf)
         return out
 
     def take(self, rows, n: int) -> "Groups":
         """Groups ``rows[:n]`` (uint32 device indices) as a new dense set."""
-        import torch
-        dev, NA = self.device, self.NA
-        g = Groups(NA, dev)
-        g.keys = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
-        g.nulls = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
-        g.sums = torch.empty(max(n, 1) * NA, dtype=torch.float64, device=dev)
-        g.cnts = torch.empty(max(n, 1) * NA, dtype=torch.int64, device=dev)
-        g.mins = torch.empty_like(g.sums) if self.mins is not None else None
-        g.maxs = torch.empty_like(g.sums) if self.maxs is not None else None
+        g = Groups.alloc(self.NA, max(n, 1), self.mins is not None, self.device)
         NL.check(NL.lib().hs_hagg_take(NL.ptr(rows), n, NL.ptr(self.keys), NL.ptr(self.nulls),
                                        NL.ptr(self.sums), NL.ptr(self.cnts), NL.ptr(self.mins),
-                                       NL.ptr(self.maxs), NA, NL.ptr(g.keys), NL.ptr(g.nulls),
-                                       NL.ptr(g.sums), NL.ptr(g.cnts), NL.ptr(g.mins),
-                                       NL.ptr(g.maxs), NL.stream_ptr()), "hs_hagg_take")
+                                       NL.ptr(self.maxs), self.NA, self.cap, g.cap,
+                                       NL.ptr(g.keys), NL.ptr(g.nulls), NL.ptr(g.sums),
+                                       NL.ptr(g.cnts), NL.ptr(g.mins), NL.ptr(g.maxs),
+                                       NL.stream_ptr()), "hs_hagg_take")
         g.set_count(n)
+        return g
+
+    @staticmethod
+    def from_host(host: dict, NA: int, minmax: bool, device) -> "Groups":
+        """Dense groups uploaded from host arrays (keys u64, nulls u8, [G, NA] aggregates)."""
+        import torch
+        G = len(host["keys"])
+        g = Groups(NA, max(G, 1), device)
+
+        def soa(a, dt):
+            return torch.from_numpy(np.ascontiguousarray(a.T).reshape(-1)).to(device) if G \
+                else torch.zeros(NA, dtype=dt, device=device)
+        g.keys = torch.from_numpy(host["keys"].view(np.int64).copy()).to(device) if G else \
+            torch.zeros(1, dtype=torch.int64, device=device)
+        g.nulls = torch.from_numpy(host["nulls"].astype(np.uint8)).to(device) if G else \
+            torch.zeros(1, dtype=torch.uint8, device=device)
+        g.sums = soa(host["sums"], torch.float64)
+        g.cnts = soa(host["cnts"], torch.int64)
+        g.mins = soa(host["mins"], torch.float64) if minmax else None
+        g.maxs = soa(host["maxs"], torch.float64) if minmax else None
+        g.set_count(G)
         return g
 
 
@@ -340,8 +369,8 @@ class OrderSource:
 
 
 def topk_candidates(g: Groups, G: int, o: OrderSource, k: int) -> Tuple[Groups, int]:
-    """The groups whose primary ORDER BY image is <= the k-th smallest image: a superset of the
-    top k under the full ordering (ties at the k-th value are all kept)."""
+    """The groups whose primary ORDER BY image is within the k smallest at 36-bit resolution (a
+    superset of the top k under the full ordering: ties at the k-th image are all kept)."""
     import torch
     L = NL.lib()
     dev = g.device
@@ -349,27 +378,30 @@ def topk_candidates(g: Groups, G: int, o: OrderSource, k: int) -> Tuple[Groups, 
         return g, G
     img = torch.empty(G, dtype=torch.int64, device=dev)
     NL.check(L.hs_topk_images(NL.ptr(g.keys), NL.ptr(g.nulls), NL.ptr(g.sums), NL.ptr(g.cnts),
-                              NL.ptr(g.mins), NL.ptr(g.maxs), G, g.NA, o.src, o.agg, o.cnt_slot,
+                              NL.ptr(g.mins), NL.ptr(g.maxs), G, g.cap, o.src, o.agg, o.cnt_slot,
                               o.shift, C.c_uint64(o.mask), int(o.nullable), int(o.desc),
                               NL.ptr(img), NL.stream_ptr()), "hs_topk_images")
-    chunk = int(L.hs_topk_chunk())
-    cur_img, cur_idx, n = img, None, G
-    while True:
-        nb = (n + chunk - 1) // chunk
-        oi = torch.empty(nb * k, dtype=torch.int64, device=dev)
-        ox = torch.empty(nb * k, dtype=torch.int32, device=dev)
-        NL.check(L.hs_topk_pass(NL.ptr(cur_img), NL.ptr(cur_idx), n, k, NL.ptr(oi), NL.ptr(ox),
-                                NL.stream_ptr()), "hs_topk_pass")
-        cur_img, cur_idx, n = oi, ox, nb * k
-        if nb == 1:
-            break
-    thr = cur_img[k - 1:k]
+    ws = _topk_ws(dev)
     sel = torch.empty(G, dtype=torch.int32, device=dev)
-    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
-    NL.check(L.hs_topk_select(NL.ptr(img), G, NL.ptr(thr), NL.ptr(sel), NL.ptr(cnt),
-                              NL.stream_ptr()), "hs_topk_select")
-    n = int(cnt.item())
+    NL.check(L.hs_topk_select(NL.ptr(img), G, k, NL.ptr(ws["st"]), NL.ptr(ws["hist"]),
+                              NL.ptr(sel), NL.ptr(ws["count"]), NL.stream_ptr()), "hs_topk_select")
+    n = int(ws["count"].item())
     return g.take(sel, n), n
+
+
+_TOPK_WS: Dict[object, dict] = {}
+
+
+def _topk_ws(dev) -> dict:
+    """Radix-select state + histogram (the kernels leave the histogram zeroed)."""
+    import torch
+    w = _TOPK_WS.get(dev)
+    if w is None:
+        w = {"st": torch.zeros(2, dtype=torch.int64, device=dev),
+             "hist": torch.zeros(int(NL.lib().hs_topk_bins()), dtype=torch.int32, device=dev),
+             "count": torch.zeros(1, dtype=torch.int64, device=dev)}
+        _TOPK_WS[dev] = w
+    return w
 
 
 __all__ = ["KeyPlan", "KeyCol", "plan_keys", "HashTable", "Groups", "TablePool",

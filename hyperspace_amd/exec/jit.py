@@ -603,34 +603,42 @@ def _hash_accumulate(gen: _Gen, aggs, hk, pass_var: str, ind: str) -> List[str]:
             b.append(f"{i2}    {var} = " + (f"{op}({var}, u_{var});" if op else f"{var} + u_{var};"))
         b.append(f"{i2}  }}")
         b.append(f"{i2}}}")
+    # CAS-first probe: a group's first run inserts with one returning atomic (no load first);
+    # later runs of the same group find it on the first CAS of their probe
     b += [f"{i2}if (htl) {{",
           f"{i2}  long long hs_ = -1;",
           f"{i2}  if (hnul) hs_ = {hm} + 1; else if (hk == ~0ull) hs_ = {hm}; else {{",
           f"{i2}    u64 hh = hs_mix64(hk) & (u64)({hm} - 1);",
           f"{i2}    for (int pr_ = 0; pr_ < {HASH_MAX_PROBE}; ++pr_) {{",
-          f"{i2}      const u64 k_ = {kp}[hh];",
-          f"{i2}      if (k_ == hk) {{ hs_ = (long long)hh; break; }}",
-          f"{i2}      if (k_ == ~0ull) {{ const u64 pv_ = atomicCAS(&{kp}[hh], ~0ull, hk);",
-          f"{i2}        if (pv_ == ~0ull || pv_ == hk) {{ hs_ = (long long)hh; break; }} }}",
+          f"{i2}      const u64 pv_ = atomicCAS(&{kp}[hh], ~0ull, hk);",
+          f"{i2}      if (pv_ == ~0ull || pv_ == hk) {{ hs_ = (long long)hh; break; }}",
           f"{i2}      hh = (hh + 1ull) & (u64)({hm} - 1);",
           f"{i2}    }}",
           f"{i2}    if (hs_ < 0) {fl}[0] = 1;",
           f"{i2}  }}",
           f"{i2}  if (hs_ >= 0) {{",
-          f"{i2}    const long long hb = hs_ * {na};",
+          f"{i2}    const long long hst = {hm} + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s",
           f"{i2}    const unsigned long long hrn = (unsigned long long)(hln - hss + 1);"]
     for i, ag in enumerate(aggs):
         cnt = f"(unsigned long long)hc{i}" if own[i] else "hrn"
-        tgt = f"(unsigned long long*)&{cp}[hb + {i}]"
-        if ag.kind in (NL.AK_COUNT_STAR, NL.AK_COUNT):
+        tgt = f"(unsigned long long*)&{cp}[{i} * hst + hs_]"
+        if ag.kind == NL.AK_COUNT_STAR:
+            # the implicit COUNT(*) is kept only when a result needs it (COUNT / AVG); group
+            # occupancy is the key word, except for the two direct slots
+            if hk.need_star:
+                b.append(f"{i2}    atomicAdd({tgt}, {cnt});")
+            else:
+                b.append(f"{i2}    if (hs_ >= {hm}) atomicAdd({tgt}, {cnt});")
+            continue
+        if ag.kind == NL.AK_COUNT:
             b.append(f"{i2}    atomicAdd({tgt}, {cnt});")
             continue
         if ag.kind == NL.AK_SUM:
-            b.append(f"{i2}    unsafeAtomicAdd(&{sp}[hb + {i}], hv{i});")
+            b.append(f"{i2}    unsafeAtomicAdd(&{sp}[{i} * hst + hs_], hv{i});")
         elif ag.kind == NL.AK_MIN:
-            b.append(f"{i2}    atomicMin(&{mnp}[hb + {i}], hv{i});")
+            b.append(f"{i2}    atomicMin(&{mnp}[{i} * hst + hs_], hv{i});")
         else:
-            b.append(f"{i2}    atomicMax(&{mxp}[hb + {i}], hv{i});")
+            b.append(f"{i2}    atomicMax(&{mxp}[{i} * hst + hs_], hv{i});")
         if own[i]:
             b.append(f"{i2}    atomicAdd({tgt}, {cnt});")
     b += [f"{i2}  }}", f"{i2}}}", f"{ind}}}"]

@@ -195,16 +195,15 @@ def lib():
     _sig(L.hs_mark_rows, I, P, I64, P, P)
     _sig(L.hs_select_marked_blocks, I64, I64)
     _sig(L.hs_select_marked, I, P, I64, P, I, P, P, P, P)
-    _sig(L.hs_hagg_extract_chunk, I)
-    _sig(L.hs_topk_chunk, I)
+    _sig(L.hs_topk_levels, I)
+    _sig(L.hs_topk_bins, I)
     _sig(L.hs_hagg_init, I, P, P, P, P, P, I64, I, P)
     _sig(L.hs_hagg_extract_blocks, I64, I64)
-    _sig(L.hs_hagg_extract, I, P, P, P, P, P, I64, I, I, I, P, P, P, P, P, P, P, P, P, P)
-    _sig(L.hs_hagg_merge, I, P, P, P, P, P, P, I64, P, P, P, P, P, I64, I, P, P)
-    _sig(L.hs_topk_images, I, P, P, P, P, P, P, I64, I, I, I, I, I, U64, I, I, P, P)
-    _sig(L.hs_topk_pass, I, P, P, I64, I, P, P, P)
-    _sig(L.hs_topk_select, I, P, I64, P, P, P, P)
-    _sig(L.hs_hagg_take, I, P, I64, P, P, P, P, P, P, I, P, P, P, P, P, P, P)
+    _sig(L.hs_hagg_extract, I, P, P, P, P, P, I64, I, I, I, P, P, P, I64, P, P, P, P, P, P, P)
+    _sig(L.hs_hagg_merge, I, P, P, P, P, P, P, I64, I64, P, P, P, P, P, I64, I, P, P)
+    _sig(L.hs_topk_images, I, P, P, P, P, P, P, I64, I64, I, I, I, I, U64, I, I, P, P)
+    _sig(L.hs_topk_select, I, P, I64, I64, P, P, P, P, P)
+    _sig(L.hs_hagg_take, I, P, I64, P, P, P, P, P, P, I, I64, I64, P, P, P, P, P, P, P)
     _lib = L
     return L
 

@@ -34,6 +34,10 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--configs", default=None)
     ap.add_argument("--merge-join", action="store_true")
+    ap.add_argument("--q3-full", action="store_true",
+                    help="also time TPC-H Q3's full shape (3-column group + top 10) via the "
+                         "merge join and the device hash aggregate")
+    ap.add_argument("--only-q3-full", action="store_true")
     ap.add_argument("--show-compact", action="store_true",
                     help="print every resident column's compact HBM encoding after the runs")
     ap.add_argument("--decompose", action="store_true",
@@ -108,6 +112,14 @@ def main():
                          (col("l_discount") <= round(disc + 0.01, 2)) &
                          (col("l_quantity") < 24 + i % 2)).agg(count("*").alias("n"))
 
+    def q3_full(i):
+        dd = datetime.date(1995, 3, 1) + datetime.timedelta(days=(i * 7) % 30)
+        j = li.join(od, li["l_orderkey"] == od["o_orderkey"]) \
+            .filter((col("o_orderdate") < dd) & (col("l_shipdate") > dd))
+        return j.groupBy("l_orderkey", "o_orderdate", "o_shippriority") \
+            .agg(sum_(col("l_extendedprice") * (1 - col("l_discount"))).alias("revenue")) \
+            .orderBy(col("revenue").desc(), col("o_orderdate")).limit(10)
+
     def timed(fn, reps):
         for i in range(3):
             fn(i).collect()
@@ -135,7 +147,17 @@ def main():
             setattr(jit, k, v)
         jit._KERNELS.clear()
         backend.graphs._lru.clear()
+        if args.only_q3_full:
+            s.conf.set("spark.hyperspace.mi.joinIndex.enabled", "false")
+            out = {"cfg": cfg, "q3_full": timed(q3_full, args.reps)}
+            s.conf.set("spark.hyperspace.mi.joinIndex.enabled", "true")
+            print(json.dumps(out), flush=True)
+            continue
         out = {"cfg": cfg, "q6": timed(q6, args.reps), "q3": timed(q3, args.reps)}
+        if args.q3_full:
+            s.conf.set("spark.hyperspace.mi.joinIndex.enabled", "false")
+            out["q3_full"] = timed(q3_full, args.reps)
+            s.conf.set("spark.hyperspace.mi.joinIndex.enabled", "true")
         if args.decompose:
             for name, fn in (("q3_left_count", q3_left_count), ("q3_count", q3_count),
                              ("q6_count", q6_count)):
