@@ -37,39 +37,78 @@ def _rt(name: str) -> str:
     return p if os.path.isabs(p) and os.path.exists(p) else ""
 
 
-def build(out_dir: str) -> str:
-    lib = os.path.join(out_dir, "libhs_hostio_asan.so")
-    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer",
-           "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-shared", "-fPIC",
+def build(out_dir: str, tsan: bool = False) -> str:
+    lib = os.path.join(out_dir, "libhs_hostio_tsan.so" if tsan else "libhs_hostio_asan.so")
+    san = ["-fsanitize=thread"] if tsan else \
+        ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", *san, "-shared", "-fPIC",
            *[os.path.join(ROOT, "csrc", "runtime", s) for s in SOURCES], "-lz", "-o", lib]
     subprocess.run(cmd, check=True)
     return lib
 
 
-def parent(iters: int, seed: int) -> int:
-    asan, ubsan = _rt("libasan.so"), _rt("libubsan.so")
-    if not asan or not ubsan:
-        print("sanitizer runtimes not found", file=sys.stderr)
-        return 2
+def parent(iters: int, seed: int, tsan: bool = False) -> int:
+    if tsan:
+        rt = _rt("libtsan.so")
+        if not rt:
+            print("sanitizer runtimes not found", file=sys.stderr)
+            return 2
+        preload = rt
+    else:
+        asan, ubsan = _rt("libasan.so"), _rt("libubsan.so")
+        if not asan or not ubsan:
+            print("sanitizer runtimes not found", file=sys.stderr)
+            return 2
+        preload = f"{asan}:{ubsan}"
     with tempfile.TemporaryDirectory() as d:
-        lib = build(d)
+        lib = build(d, tsan)
         env = dict(os.environ)
-        env["LD_PRELOAD"] = f"{asan}:{ubsan}"
+        env["LD_PRELOAD"] = preload
         env["ASAN_OPTIONS"] = "detect_leaks=0:abort_on_error=1:allocator_may_return_null=1"
         env["UBSAN_OPTIONS"] = "halt_on_error=1:print_stacktrace=1"
-        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", lib, d,
-                            "--iters", str(iters), "--seed", str(seed)], env=env)
+        # races are reported for the instrumented library only (CPython is not instrumented);
+        # any report fails the run
+        # pyarrow (used to write the test files) is not instrumented: its own thread pool's
+        # futures read as races to TSan, so reports whose stacks are inside Arrow are
+        # suppressed; the library under test is never on this list
+        supp = os.path.join(d, "tsan.supp")
+        with open(supp, "w") as f:
+            for lib_ in ("libarrow.so", "libarrow_dataset.so", "libparquet.so",
+                         "libarrow_acero.so", "libarrow_python.so", "libarrow_substrait.so"):
+                f.write(f"race:{lib_}\ncalled_from_lib:{lib_}\nmutex:{lib_}\n"
+                        f"deadlock:{lib_}\nthread:{lib_}\n")
+        env["TSAN_OPTIONS"] = (f"halt_on_error=1:exitcode=66:report_signal_unsafe=0:"
+                               f"suppressions={supp}")
+        cmd = [sys.executable, os.path.abspath(__file__), "--child", lib, d, "--iters",
+               str(iters), "--seed", str(seed)]
+        if tsan:
+            # the test files are written by an uninstrumented process first: pyarrow's own
+            # thread pool must not run inside the TSan process (it is not instrumented, its
+            # futures read as races); the TSan child only calls the native library
+            g = subprocess.run(cmd + ["--gen-only"], env=dict(os.environ))
+            if g.returncode != 0:
+                return g.returncode
+            cmd += ["--threads", "8", "--reuse"]
+        r = subprocess.run(cmd, env=env)
+        if r.returncode == 0 and tsan:
+            import pyarrow.parquet as pq
+            ws = [x for x in os.listdir(d) if x.startswith("w")]
+            for x in ws:   # the files the threads wrote concurrently are valid Parquet
+                assert pq.read_table(os.path.join(d, x, "native.parquet")).num_rows == 1331
+            print(f"verified {len(ws)} concurrently written files")
         return r.returncode
 
 
-def child(lib_path: str, work: str, iters: int, seed: int) -> int:
+def child(lib_path: str, work: str, iters: int, seed: int, threads: int = 0,
+          gen_only: bool = False, reuse: bool = False) -> int:
     sys.path.insert(0, ROOT)
     import numpy as np
     import pyarrow as pa
     import pyarrow.parquet as pq
 
     from hyperspace_amd.exec import jit
-    jit._rt = C.CDLL(lib_path)          # host I/O symbols only; bound by the modules below
+    if not gen_only:   # the generating process (no sanitizer runtime) uses the normal build
+        jit._rt = C.CDLL(lib_path)      # host I/O symbols only; bound by the modules below
     from hyperspace_amd.exec import pq_encode as PE
     from hyperspace_amd.io import avro
     from hyperspace_amd.io import native_parquet as NP
@@ -84,20 +123,31 @@ def child(lib_path: str, work: str, iters: int, seed: int) -> int:
         "d": pa.array(rng.integers(8000, 9000, n).astype(np.int32)).cast(pa.date32()),
         "s": pa.array([f"v{x}" for x in rng.integers(0, 50, n)]),
     })
-    nulls = tab.set_column(0, "i32", pa.array(
-        np.where(rng.random(n) < 0.2, None, rng.integers(0, 100, n)).tolist(), pa.int32()))
-    files = []
-    for comp in ("snappy", "none"):
-        for dic in (True, False):
-            for ver in ("1.0", "2.0"):
-                for t, tag in ((tab, "nn"), (nulls, "nu")):
-                    p = os.path.join(work, f"f_{comp}_{dic}_{ver}_{tag}.parquet")
-                    pq.write_table(t, p, compression=comp, use_dictionary=dic,
-                                   data_page_version=ver, row_group_size=1700,
-                                   data_page_size=4096)
-                    files.append(p)
-    # native writer file (device encoder contract, host-packed payloads)
-    files.append(_native_written(PE, work, rng))
+    manifest = os.path.join(work, "files.txt")
+    if reuse:
+        with open(manifest) as fh:
+            files = fh.read().split()
+    else:
+        nulls = tab.set_column(0, "i32", pa.array(
+            np.where(rng.random(n) < 0.2, None, rng.integers(0, 100, n)).tolist(), pa.int32()))
+        files = []
+        for comp in ("snappy", "none"):
+            for dic in (True, False):
+                for ver in ("1.0", "2.0"):
+                    for t, tag in ((tab, "nn"), (nulls, "nu")):
+                        p = os.path.join(work, f"f_{comp}_{dic}_{ver}_{tag}.parquet")
+                        pq.write_table(t, p, compression=comp, use_dictionary=dic,
+                                       data_page_version=ver, row_group_size=1700,
+                                       data_page_size=4096)
+                        files.append(p)
+        # native writer file (device encoder contract, host-packed payloads)
+        files.append(_native_written(PE, work, rng))
+        ap = os.path.join(work, "t.avro")
+        avro.write_avro(ap, tab.drop(["d"]), codec="deflate", block_rows=500)
+        with open(manifest, "w") as fh:
+            fh.write("\n".join(files))
+        if gen_only:
+            return 0
 
     def exercise(path: str) -> None:
         f = NP.PqFile(path)
@@ -132,6 +182,8 @@ def child(lib_path: str, work: str, iters: int, seed: int) -> int:
         finally:
             f.close()
 
+    if threads:
+        return _threaded(exercise, files, PE, avro, n, work, threads, iters)
     for p in files:
         exercise(p)
     blobs = [open(p, "rb").read() for p in files]
@@ -195,7 +247,64 @@ def child(lib_path: str, work: str, iters: int, seed: int) -> int:
     return 0
 
 
-def _native_written(PE, work: str, rng) -> str:
+def _threaded(exercise, files, PE, avro, nrows: int, work: str, threads: int, iters: int) -> int:
+    """TSan mode: the staging pool's access pattern (exec/staging.py) — many threads decoding
+    and planning chunks of the same and of different files at once (ctypes releases the GIL
+    for every native call), plus concurrent Snappy streams, Avro block decodes and native
+    Parquet writes, each thread with its own buffers."""
+    import concurrent.futures as cf
+
+    import numpy as np
+    ap = os.path.join(work, "t.avro")          # written by the generating process
+    abuf = open(ap, "rb").read()
+    meta, sync, start = avro.read_header(abuf)
+    fields, _ = avro.schema_of(meta)
+    AL = avro._lib()
+
+    def avro_native(rows_want: int) -> None:
+        """The native block decode of read_avro, without building Arrow arrays (pyarrow is not
+        instrumented; its internal atomics would read as races)."""
+        body = np.frombuffer(abuf, dtype=np.uint8)[start:]
+        types = np.array([f[1] for f in fields], dtype=np.int32)
+        nulls = np.array([f[2] for f in fields], dtype=np.int32)
+        syncb = np.frombuffer(sync, dtype=np.uint8)
+        h = AL.hs_avro_decode(body.ctypes.data, len(body), syncb.ctypes.data, 1, len(fields),
+                              types.ctypes.data, nulls.ctypes.data)
+        try:
+            assert not AL.hs_avro_error(h)
+            assert int(AL.hs_avro_rows(h)) == rows_want
+            for k in range(len(fields)):
+                for which in (0, 1, 2):
+                    avro._buf(AL, h, k, which)
+        finally:
+            AL.hs_avro_free(h)
+
+    def job(i: int) -> int:
+        rng = np.random.default_rng(1000 + i)
+        exercise(files[i % len(files)])
+        exercise(files[0])                      # every thread also shares one file
+        raw = rng.integers(0, 4, 4096).astype(np.uint8)
+        z = PE.snappy_stream_host(raw)
+        src = np.frombuffer(z.tobytes(), np.uint8).copy()
+        dst = np.zeros(len(raw), np.uint8)
+        from hyperspace_amd.io import native_parquet as NP
+        got = NP.lib().hs_pq_snappy_decompress(src.ctypes.data, len(src), dst.ctypes.data,
+                                                len(raw))
+        assert got == len(raw) and bytes(dst) == raw.tobytes()
+        avro_native(nrows)
+        d = os.path.join(work, f"w{i}")
+        os.makedirs(d, exist_ok=True)
+        _native_written(PE, d, rng, verify=False)
+        return i
+    n = max(threads * 4, min(iters, 64))
+    with cf.ThreadPoolExecutor(threads) as ex:
+        done = list(ex.map(job, range(n)))
+    assert done == list(range(n))
+    print(f"tsan host I/O: {n} jobs on {threads} threads over {len(files)} files: clean")
+    return 0
+
+
+def _native_written(PE, work: str, rng, verify: bool = True) -> str:
     import numpy as np
     L = PE._writer()
     rows = [900, 431]
@@ -227,8 +336,9 @@ def _native_written(PE, work: str, rng) -> str:
     path = os.path.join(work, "native.parquet")
     rg = (C.c_int64 * len(rows))(*rows)
     assert L.hs_pq_write_file(path.encode(), 2, len(rows), rg, cols, b"asan") == 0
-    import pyarrow.parquet as pq
-    assert pq.read_table(path).num_rows == sum(rows)
+    if verify:
+        import pyarrow.parquet as pq
+        assert pq.read_table(path).num_rows == sum(rows)
     return path
 
 
@@ -237,10 +347,16 @@ def main():
     ap.add_argument("--child", nargs=2, metavar=("LIB", "WORKDIR"))
     ap.add_argument("--iters", type=int, default=300)
     ap.add_argument("--seed", type=int, default=5)
+    ap.add_argument("--tsan", action="store_true",
+                    help="ThreadSanitizer build, concurrent calls from a thread pool")
+    ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--gen-only", action="store_true")
+    ap.add_argument("--reuse", action="store_true")
     a = ap.parse_args()
     if a.child:
-        sys.exit(child(a.child[0], a.child[1], a.iters, a.seed))
-    sys.exit(parent(a.iters, a.seed))
+        sys.exit(child(a.child[0], a.child[1], a.iters, a.seed, a.threads, a.gen_only,
+                       a.reuse))
+    sys.exit(parent(a.iters, a.seed, a.tsan))
 
 
 if __name__ == "__main__":

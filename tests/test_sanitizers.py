@@ -30,3 +30,23 @@ def test_host_io_layer_is_clean_under_asan_ubsan(tmp_path):
                        cwd=str(tmp_path), timeout=900)
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-6000:])
     assert "clean" in r.stdout
+
+
+def _have_tsan() -> bool:
+    if shutil.which("g++") is None:
+        return False
+    r = subprocess.run(["g++", "-print-file-name=libtsan.so"], capture_output=True, text=True)
+    return os.path.isabs(r.stdout.strip())
+
+
+@pytest.mark.skipif(not _have_tsan(), reason="g++ ThreadSanitizer runtime not installed")
+def test_host_io_layer_is_race_free_under_tsan(tmp_path):
+    """ThreadSanitizer build of the host runtime (csrc/runtime/hs_parquet.cpp,
+    hs_parquet_write.cpp, hs_avro.cpp) driven the way the staging pool drives it: 8 threads
+    decoding / planning chunks of shared and distinct files, Snappy streams, Avro blocks and
+    concurrent native Parquet writes."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "sanitize_hostio.py"),
+                        "--tsan", "--iters", "64", "--seed", "3"], capture_output=True,
+                       text=True, cwd=str(tmp_path), timeout=900)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-6000:])
+    assert "clean" in r.stdout and "verified" in r.stdout
