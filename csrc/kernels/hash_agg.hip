@@ -81,15 +81,29 @@ __device__ __forceinline__ int block_prefix(bool f, int* tot) {
   return base + __popcll(bm & ((1ull << lane) - 1ull));
 }
 
-// Per block (one slot per thread): number of occupied slots.
+constexpr int kSlotsPerThread = 4;
+constexpr int kChunk = kBlock * kSlotsPerThread;   // slots per extract block
+
+// Per block (kChunk slots, lane-consecutive slots per step): number of occupied slots.
 __global__ __launch_bounds__(kBlock) void hagg_count_kernel(
     const unsigned long long* __restrict__ keys, const long long* __restrict__ cnts, long long M,
     int star, long long* __restrict__ block_counts) {
-  const long long s = (long long)blockIdx.x * kBlock + threadIdx.x;
-  const bool f = s < M + 2 && occupied(keys, cnts, M, star, s);
-  int tot;
-  (void)block_prefix(f, &tot);
-  if (threadIdx.x == 0) block_counts[blockIdx.x] = tot;
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < kSlotsPerThread; ++k) {
+    const long long s = (long long)blockIdx.x * kChunk + k * kBlock + threadIdx.x;
+    c += (s < M + 2 && occupied(keys, cnts, M, star, s)) ? 1 : 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  __shared__ int ws[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < kBlock / 64; ++w) t += ws[w];
+    block_counts[blockIdx.x] = t;
+  }
 }
 
 // One block: exclusive scan of nb counts in place; total[0] = sum, total[1] = *flag (the
@@ -133,12 +147,16 @@ __global__ __launch_bounds__(kBlock) void hagg_emit_kernel(
     double* __restrict__ out_sums, long long* __restrict__ out_cnts, double* __restrict__ out_mins,
     double* __restrict__ out_maxs) {
   const long long st = M + 2;
-  const long long s = (long long)blockIdx.x * kBlock + threadIdx.x;
+  long long base = block_off[blockIdx.x];
+  for (int k = 0; k < kSlotsPerThread; ++k) {
+  const long long s = (long long)blockIdx.x * kChunk + k * kBlock + threadIdx.x;
   const bool f = s < st && occupied(keys, cnts, M, star, s);
   int tot;
   const int r = block_prefix(f, &tot);
-  if (!f) return;
-  const long long pos = block_off[blockIdx.x] + r;
+  __syncthreads();   // block_prefix's LDS words are reused by the next step
+  const long long pos = base + r;
+  base += tot;
+  if (!f) continue;
   out_keys[pos] = s == M ? kEmpty : keys[s];
   out_null[pos] = s == M + 1 ? 1 : 0;
   for (int i = 0; i < NA; ++i) {
@@ -155,6 +173,7 @@ __global__ __launch_bounds__(kBlock) void hagg_emit_kernel(
     }
   }
   if (reset && s < M) keys[s] = kEmpty;
+  }
 }
 
 // Slot of `key` (null: the NULL slot), inserting it if absent; -1 when the probe sequence
@@ -380,7 +399,7 @@ int hs_hagg_init(unsigned long long* keys, double* sums, long long* cnts, double
 }
 
 // Workspace int64s of hs_hagg_extract for a table of M slots.
-long long hs_hagg_extract_blocks(long long M) { return (M + 2 + kBlock - 1) / kBlock; }
+long long hs_hagg_extract_blocks(long long M) { return (M + 2 + kChunk - 1) / kChunk; }
 
 // total: two int64s (the group count G, and the table's overflow flag, which is cleared).
 // out_*: SoA with row stride `cap` >= G (M + 2 always suffices).

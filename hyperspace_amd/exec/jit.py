@@ -83,6 +83,10 @@ MJ_ITEMS = int(os.environ.get("HS_JIT_MJ_ITEMS", "8"))
 MJ_LDS_KEYS = int(os.environ.get("HS_JIT_MJ_LDS_KEYS", "2048"))
 MJ_GRID = int(os.environ.get("HS_JIT_MJ_GRID", "8192"))
 MJ_STEPS = int(os.environ.get("HS_JIT_MJ_STEPS", "1"))   # branch-free walk steps per row
+# right-span staging: per-thread rows loaded per round trip (all loads of a round issue before
+# any LDS store), and double-buffered LDS spans (no end-of-tile barrier)
+MJ_STAGE_UNROLL = int(os.environ.get("HS_JIT_MJ_STAGE_UNROLL", "4"))
+MJ_DBUF = os.environ.get("HS_JIT_MJ_DBUF", "1") == "1"
 MJ_KEY32 = os.environ.get("HS_JIT_MJ_KEY32", "1") == "1"  # 32-bit merge images (_key32_frame)
 # cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
 MJ_EXP = os.environ.get("HS_JIT_MJ_EXP", "")
@@ -1226,7 +1230,7 @@ def merge_join_shape(p: NL.JoinParams, compacts=None, hk=None) -> tuple:
                  for i in range(p.naggs))
     return ("merge_join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey,
             p.key_is_float, MJ_ITEMS, MJ_LDS_KEYS, MJ_STEPS, BLOCK, WAVE_SYNC,
-            _key32_frame(p, compacts) is not None, MJ_EXP,
+            _key32_frame(p, compacts) is not None, MJ_EXP, MJ_STAGE_UNROLL, MJ_DBUF,
             hk.shape() if hk is not None else None)
 
 
@@ -1388,7 +1392,8 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
     b += _acc_decls(aggs, grouped, args)
     W = BLOCK // 64  # noqa: N806
     CAP = 64 * NI + 64  # noqa: N806 — list entries: < 64 carried over + one tile's appends
-    b += [f"  __shared__ {KT} skeys[{LK + 1}]; __shared__ unsigned char spass[{LK}];",
+    NB = 2 if MJ_DBUF else 1  # noqa: N806
+    b += [f"  __shared__ {KT} skeys_[{NB}][{LK + 1}]; __shared__ unsigned char spass_[{NB}][{LK}];",
           f"  constexpr int DUMP = {CAP};",
           f"  __shared__ int lrow_s[{W}][{CAP + 64}]; __shared__ int lj_s[{W}][{CAP + 64}];",
           "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;",
@@ -1411,20 +1416,32 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
     def body(b: List[str], full: bool) -> None:
         b.extend([f"{ind}const i64 ss = a.spans[4 * t + 2], se = a.spans[4 * t + 3];",
                   f"{ind}const int ns = (int)(se - ss);",
-                  f"{ind}const bool staged = ns <= {LK};"])
-        # (1) stage the right span: key images + right-only predicate pass bytes
+                  f"{ind}const bool staged = ns <= {LK};",
+                  f"{ind}{KT}* const skeys = skeys_[{'(int)(t & 1)' if NB == 2 else '0'}];",
+                  f"{ind}unsigned char* const spass = spass_[{'(int)(t & 1)' if NB == 2 else '0'}];"])
+        # (1) stage the right span: key images + right-only predicate pass bytes; each round
+        # issues the loads of U rows per thread before any store (one HBM round trip per round
+        # instead of one per row)
         stg = "staged && false" if "nostage" in MJ_EXP else "staged"
-        b.extend([f"{ind}if ({stg}) for (int sq = threadIdx.x; sq < ns; sq += {BLOCK}) {{",
-                  f"{ind}  const i64 jr = ss + sq;"])
-        gs = _Gen(args, cols, split, ("jr", "jr"), approx, True)
-        for sl in stage_slots:
-            _uload(gs, sl, "s", b, ind + "  ")
-        okk = f"n{rk}_s" if cols[rk][1] else "true"
-        cond = _rename(gs.cnf(ronly), allslots, "s")
-        b.extend([f"{ind}  const bool kv = {okk};",
-                  f"{ind}  skeys[sq] = kv ? {rimg(f'x{rk}_s')} : ({KT})0;",
-                  f"{ind}  spass[sq] = (kv && {cond}) ? 1 : 0;",
-                  f"{ind}}}",
+        U = max(1, MJ_STAGE_UNROLL)  # noqa: N806
+        b.extend([f"{ind}if ({stg}) for (int sqb = 0; sqb < ns; sqb += {BLOCK * U}) {{"])
+        for u in range(U):
+            b.extend([f"{ind}  const int sq{u} = sqb + {u * BLOCK} + (int)threadIdx.x;",
+                      f"{ind}  const bool sv{u} = sq{u} < ns;",
+                      f"{ind}  const i64 jr{u} = ss + (sv{u} ? sq{u} : 0);"])
+        for u in range(U):
+            gs = _Gen(args, cols, split, (f"jr{u}", f"jr{u}"), approx, True)
+            for sl in stage_slots:
+                _uload(gs, sl, f"s{u}", b, ind + "  ")
+        okk_fmt = f"n{rk}_s{{u}}" if cols[rk][1] else "true"
+        for u in range(U):
+            gs = _Gen(args, cols, split, (f"jr{u}", f"jr{u}"), approx, True)
+            cond = _rename(gs.cnf(ronly), allslots, f"s{u}")
+            okk = okk_fmt.format(u=u)
+            b.extend([f"{ind}  if (sv{u}) {{ const bool kv = {okk};",
+                      f"{ind}    skeys[sq{u}] = kv ? {rimg(f'x{rk}_s{u}')} : ({KT})0;",
+                      f"{ind}    spass[sq{u}] = (kv && {cond}) ? 1 : 0; }}"])
+        b.extend([f"{ind}}}",
                   f"{ind}if (staged && threadIdx.x == 0) skeys[ns] = {KMAX};   // walk sentinel"])
         # (2) left stream (raw vector arrays come from the tile loop).  Per-item flags live as
         # bits of one VGPR word each (kvb: key valid, mb: left predicates, mtb: matched): a bool
@@ -1528,7 +1545,8 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
         b.append(f"{i2}if (!__any(mtb != 0u)) break;")
         one_round(i2)
         b.append(f"{ind}}}")
-        b.append(f"{ind}__syncthreads();")
+        if NB == 1:   # single span buffer: the next tile's staging must wait for this tile
+            b.append(f"{ind}__syncthreads();")
 
     loads = _vec_loads(g1, first)
     _tile_loop(b, T, NI, 1, ind)

@@ -185,6 +185,48 @@ def test_generated_sources_compile_with_compact_columns(rt, tmp_path):
         assert rc == 0, jit.runtime().hs_jit_last_error().decode()
 
 
+def test_hash_mode_sources_compile(rt, tmp_path):
+    """Hash-mode grouping (exec/hash_agg.py): the Q3 full-shape merge join (3-column packed key
+    over both sides), a scan with a nullable / exact-decimal / f32 packed key and MIN/MAX, and a
+    raw float key compile for gfx950."""
+    import types
+    from hyperspace_amd.exec import hash_agg as H
+    from hyperspace_amd.exec.encoding import Compact
+    jit = rt
+
+    def col(t, valid=False, dictionary=None):
+        return types.SimpleNamespace(hs_type=t, valid=1 if valid else None, dictionary=dictionary,
+                                     offsets=None, atype=pa.int64())
+    j = _q3_params()
+    j.cols[10] = _fake(NL.I32)
+    comp = dict(_q3_compacts())
+    comp[0] = Compact(None, 4, 1 + (1 << 31), None, NL.I64, 1, 600_000_000)
+    comp[8] = Compact(None, 4, 1 + (1 << 31), None, NL.I64, 1, 600_000_000)
+    hk = H.plan_keys([(0, None, col(NL.I64), (1, 600_000_000, None)),
+                      (9, None, col(NL.I32), (8000, 2500, None)),
+                      (10, None, col(NL.I32), (0, 1, None))], (False, False), False)
+    assert hk.mode == "packed" and [c.shift for c in hk.cols] == [0, 30, 42]
+    ks = [jit.gen_merge_join_agg(j, comp, hk), jit.gen_merge_join_agg(j, None, hk)]
+    assert "atomicCAS" in ks[0].src and "hs_mix64" in ks[0].src and "_flush" not in ks[0].src
+    p = _scan_params({0: _fake(NL.I64, True), 1: _fake(NL.F64), 2: _fake(NL.F32),
+                      3: _fake(NL.F64)},
+                     [NL.Pred(NL.PK_FLT_LIT, NL.OP_GE, 1, 0, 0, 0, 0, 0.05, None)],
+                     [_agg(NL.AK_SUM, [(3, 0.0, 1.0)]), _agg(NL.AK_MIN, [(3, 0.0, 1.0)]),
+                      _agg(NL.AK_MAX, [(3, 0.0, 1.0)]), _agg(NL.AK_COUNT_STAR)])
+    hk2 = H.plan_keys([(0, None, col(NL.I64, True), (-5, 100, None)),
+                       (1, None, col(NL.F64), (0, 11, 100.0)),
+                       (2, None, col(NL.F32), (0, 0, None))], (False, False, False, False), True)
+    assert [c.kind for c in hk2.cols] == ["int", "dec", "f32"]
+    hk3 = H.plan_keys([(3, None, col(NL.F64), (0, 0, 0.0))], (False, False, False, False))
+    assert hk3.mode == "raw_float"
+    for vec in (0, 8):
+        ks += [jit.gen_scan_agg(p, None, vec, hk2), jit.gen_scan_agg(p, None, vec, hk3)]
+    for k in ks:
+        rc = jit.runtime().hs_jit_compile_to_cache(k.src.encode(), k.name.encode(), b"gfx950",
+                                                   str(tmp_path).encode())
+        assert rc == 0, jit.runtime().hs_jit_last_error().decode()
+
+
 def q3_join_index_kernel(jit, vec=8, stage=False, bitmap=False):
     """The TPC-H Q3 shape of the bench: left (lineitem) l_shipdate > d, right (orders)
     o_orderdate < d, SUM(price * (1 - disc)) + COUNT(*), compact HBM columns, 1-byte join index."""
