@@ -62,7 +62,7 @@ def _prepare_out_dir(out_path: str, mode: str, dist) -> None:
 
 def _sort_and_write(session, table: Dict[str, DeviceColumn], names: List[str], bucket,
                     indexed: List[str], num_buckets: int, out_path: str, schema: pa.Schema,
-                    task_id: int, presorted: bool = False) -> List[str]:
+                    task_id: int, presorted: bool = False, seed=None) -> List[str]:
     """Sort rows by (bucket, indexed columns) and write one file per bucket.  ``presorted``:
     the rows already are in that order (a rewrite of single sorted files per bucket), so no
     sort or gather runs."""
@@ -103,6 +103,11 @@ def _sort_and_write(session, table: Dict[str, DeviceColumn], names: List[str], b
             bucket.device)
     LAST_BUILD_STATS.update({"sort_gather_s": t1 - t0,
                              "d2h_write_s": time.perf_counter() - t1})
+    if seed is not None and paths:
+        # the sorted bucket-major columns are exactly what a query would load back from these
+        # files: hand them to the device table cache instead of freeing them
+        from .device_cache import register_seed
+        register_seed(session, paths, dict(zip(names, gathered)), off, *seed)
     return paths
 
 
@@ -273,7 +278,7 @@ def device_build_from_source(session, rel, files: List[str], columns: List[str],
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     paths = _sort_and_write(session, cols, names, bucket, indexed, num_buckets, out_path, schema,
-                            rank)
+                            rank, seed=(rank, world, num_buckets))
     if dist is not None:
         dist.barrier()
     LAST_BUILD_STATS.update({"read_h2d_s": t1 - t0, "hash_exchange_s": t2 - t1,

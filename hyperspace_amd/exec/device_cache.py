@@ -105,6 +105,83 @@ class DeviceTableCache:
             self._bytes = 0
 
 
+# ------------------------------------------------------------------------------------------------
+# Build seeds: a device build ends with every index column sorted bucket-major in HBM — exactly
+# what load_bucketed_index would read back from the files it just wrote.  The build registers
+# those columns here and the first query of the new index takes them instead of re-reading,
+# re-decoding and re-sorting the files (cold-query latency).  A seed matches a query's file list
+# only if the owned files are the very files written, unchanged (path and size).
+# ------------------------------------------------------------------------------------------------
+_SEEDS: "OrderedDict[tuple, dict]" = OrderedDict()
+_SEED_LOCK = threading.Lock()
+SEED_STATS = {"registered": 0, "hits": 0}
+
+
+def _seed_budget(session) -> int:
+    from ..utils.conf import HyperspaceConf
+    return HyperspaceConf.device_cache_bytes(session.conf) // 2
+
+
+def register_seed(session, paths, cols: Dict[str, DeviceColumn], off, rank: int, world: int,
+                  num_buckets: int) -> None:
+    import os
+    import torch
+    keep = {}
+    for n, c in cols.items():
+        if c.offsets is not None:       # raw string bytes: queries read dictionary codes
+            continue
+        keep[n] = c
+    if not keep:
+        return
+    files = tuple(sorted((P.to_local(p), os.path.getsize(P.to_local(p))) for p in paths))
+    nbytes = sum(c.nbytes() for c in keep.values())
+    budget = _seed_budget(session)
+    if nbytes > budget:
+        return
+    dev = next(iter(keep.values())).data.device
+    off = np.asarray(off, dtype=np.int64)
+    entry = {"cols": keep, "off": off, "off_dev": torch.from_numpy(off).to(dev),
+             "bytes": nbytes, "num_buckets": num_buckets}
+    with _SEED_LOCK:
+        _SEEDS[(files, rank, world)] = entry
+        SEED_STATS["registered"] += 1
+        total = sum(e["bytes"] for e in _SEEDS.values())
+        while total > budget and len(_SEEDS) > 1:
+            _, old = _SEEDS.popitem(last=False)
+            total -= old["bytes"]
+
+
+def seeded_index(files, columns: List[str], num_buckets: int, rank: int,
+                 world: int) -> Optional[DeviceTable]:
+    """The build seed of exactly this rank's share of ``files`` holding ``columns``, as a
+    table view (shared tensors), or None."""
+    if not _SEEDS:
+        return None
+    owned = []
+    for f in files:
+        b = get_bucket_id(P.get_name(f.path))
+        if b is None or b >= num_buckets:
+            return None
+        if b % world == rank:
+            owned.append((P.to_local(f.path), int(f.length)))
+    key = (tuple(sorted(owned)), rank, world)
+    with _SEED_LOCK:
+        e = _SEEDS.get(key)
+        if e is not None:
+            _SEEDS.move_to_end(key)
+    if e is None or e["num_buckets"] != num_buckets or any(c not in e["cols"] for c in columns):
+        return None
+    off = e["off"]
+    cols = {c: e["cols"][c] for c in columns}
+    SEED_STATS["hits"] += 1
+    return DeviceTable(cols, int(off[-1]), e["off_dev"], off)
+
+
+def clear_seeds() -> None:
+    with _SEED_LOCK:
+        _SEEDS.clear()
+
+
 def load_bucketed_index(files, columns: List[str], num_buckets: int, sort_cols: List[str], device,
                         rank: int = 0, world: int = 1) -> DeviceTable:
     """Load index files bucket-major for the buckets this rank owns (b % world == rank)."""

@@ -35,7 +35,8 @@ from ..utils.tracing import TRACER, stage
 from . import compile as CP
 from . import jit, join_index
 from .arrow_eval import key
-from .device_cache import DeviceTableCache, _files_key, load_bucketed_index, load_flat
+from .device_cache import (DeviceTableCache, _files_key, load_bucketed_index, load_flat,
+                           seeded_index)
 from .device_table import DeviceColumn, DeviceTable
 from .graphs import GraphCache, ScanAggGraph, range_bounds
 
@@ -300,9 +301,11 @@ class GpuBackend:
             cols = [ncol[a.name.lower()] for a in p.output]
             sort_cols = [ncol[c.lower()] for c in idx.indexed_columns]
             load_cols = list(dict.fromkeys(cols + sort_cols))
-            table = self.cache.get(files, load_cols, ("bucketed", rank, world),
-                                   lambda: load_bucketed_index(files, load_cols, idx.num_buckets,
-                                                               sort_cols, self.device, rank, world))
+            table = self.cache.get(
+                files, load_cols, ("bucketed", rank, world),
+                lambda: seeded_index(files, load_cols, idx.num_buckets, rank, world) or
+                load_bucketed_index(files, load_cols, idx.num_buckets, sort_cols, self.device,
+                                    rank, world))
             # rank-independent identity (every rank scans the same file list)
             table.global_key = ("bucketed", _files_key(files), tuple(load_cols), world)
             colmap = {a.expr_id: c for a, c in zip(p.output, cols)}

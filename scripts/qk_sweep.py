@@ -38,6 +38,8 @@ def main():
                     help="also time TPC-H Q3's full shape (3-column group + top 10) via the "
                          "merge join and the device hash aggregate")
     ap.add_argument("--only-q3-full", action="store_true")
+    ap.add_argument("--only-merge", action="store_true",
+                    help="time only Q3 through the merge-join kernel")
     ap.add_argument("--show-compact", action="store_true",
                     help="print every resident column's compact HBM encoding after the runs")
     ap.add_argument("--decompose", action="store_true",
@@ -147,6 +149,12 @@ def main():
             setattr(jit, k, v)
         jit._KERNELS.clear()
         backend.graphs._lru.clear()
+        if args.only_merge:
+            s.conf.set("spark.hyperspace.mi.joinIndex.enabled", "false")
+            out = {"cfg": cfg, "q3_merge": timed(q3, args.reps)}
+            s.conf.set("spark.hyperspace.mi.joinIndex.enabled", "true")
+            print(json.dumps(out), flush=True)
+            continue
         if args.only_q3_full:
             s.conf.set("spark.hyperspace.mi.joinIndex.enabled", "false")
             out = {"cfg": cfg, "q3_full": timed(q3_full, args.reps)}

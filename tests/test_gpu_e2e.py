@@ -370,3 +370,22 @@ def test_join_key_domain_pruning_matches_oracle(tmp_path, device):
     g, c, path = _both(s, rows)
     assert path == "native", s.backend().fallback_reason
     _close(g, c)
+
+
+def test_first_query_after_build_uses_the_build_hbm_columns(tpch):
+    """The device build's sorted bucket-major columns seed the device table cache: the first
+    query of a new index reads no index file back (cold latency), and is exact."""
+    from hyperspace_amd.exec import device_cache as DC
+    s, lpath, _ = tpch
+    hs = Hyperspace(s)
+    li = s.read.parquet(lpath)
+    before = dict(DC.SEED_STATS)
+    hs.createIndex(li, IndexConfig("li_seed", ["l_shipdate"], ["l_discount", "l_quantity"]))
+    assert DC.SEED_STATS["registered"] == before["registered"] + 1
+    Hyperspace.enable(s)
+    q = li.filter("l_shipdate >= DATE '1994-01-01' AND l_shipdate < DATE '1995-01-01'") \
+        .agg(sum_("l_quantity").alias("q"), count("*").alias("n"))
+    g, c, path = _both(s, q, sort=False)
+    assert path == "native", s.backend().fallback_reason
+    assert DC.SEED_STATS["hits"] == before["hits"] + 1
+    _close(g, c)
