@@ -8,6 +8,7 @@
 
 #define HS_HASH_MAX_COLS 8
 #define HS_STR 100
+#define HS_STRDICT 101   // int32 codes into a dictionary held as (offsets, chars) on the device
 
 // Value transform applied before hashing, so a device column hashes like Spark's logical value:
 //   HS_XF_DECIMAL | s : float64 storage of decimal(p<=15, s) -> unscaled long llrint(d * 10^s)
@@ -19,10 +20,11 @@
 #define HS_XF_FDIV 0x300
 
 struct HashCol {
-  const void* data;        // values, or chars for strings
+  const void* data;        // values, chars for HS_STR, int32 codes for HS_STRDICT
   const uint8_t* valid;    // nullable
-  const int64_t* offsets;  // strings only (n+1 int64 offsets)
-  int32_t type;            // HsType or HS_STR
+  const int64_t* offsets;  // HS_STR: n+1 row offsets; HS_STRDICT: dictionary offsets
+  const void* aux;         // HS_STRDICT: dictionary chars
+  int32_t type;            // HsType, HS_STR or HS_STRDICT
   int32_t xform;           // HS_XF_* | argument
 };
 
@@ -95,6 +97,10 @@ __device__ __forceinline__ uint32_t hash_value(const HashCol& c, int64_t row, ui
     }
     case HS_STR:
       return hash_string((const uint8_t*)c.data, c.offsets[row], c.offsets[row + 1], h);
+    case HS_STRDICT: {   // the dictionary entry's bytes: same hash as the raw string
+      const int32_t code = ((const int32_t*)c.data)[row];
+      return hash_string((const uint8_t*)c.aux, c.offsets[code], c.offsets[code + 1], h);
+    }
     default:
       return hs_hash_long(((const uint64_t*)c.data)[row], h);
   }

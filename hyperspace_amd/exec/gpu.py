@@ -648,9 +648,6 @@ class GpuBackend:
                 return cached
         cols = self._materialize(r, list(dict.fromkeys(r.attrs + keys)))
         kcols = [cols[k.expr_id] for k in keys]
-        for c in kcols:
-            if c.dictionary is not None:
-                raise Unsupported("device shuffle on string keys")
         import torch
         B = part.num_partitions
         with stage("shuffle.hash"):
@@ -685,8 +682,6 @@ class GpuBackend:
         names = sorted({r.colmap[a.expr_id] for a in need})
         knames = tuple(r.colmap[k.expr_id] for k in keys)
         t = r.table
-        if any(t.columns[n].dictionary is not None for n in knames):
-            return None
         cache = t.__dict__.setdefault("_repart", {})
         ck = (tuple(names), knames, B)
         nt = cache.get(ck)
@@ -777,8 +772,8 @@ class GpuBackend:
                 strings.append(c.dictionary is not None)
                 kinds.add(c.is_float)
         if any(strings):
-            if not all(strings) or left.parts or right.parts:
-                raise Unsupported("string join keys over a bucket union / mixed key types")
+            if not all(strings):
+                raise Unsupported("mixed string / non-string join keys")
             left, right = self._string_join_keys(left, right, lk, rk)
         elif len(kinds) > 1:
             raise Unsupported("mixed int/float join keys")
@@ -842,25 +837,33 @@ class GpuBackend:
 
     def _string_join_keys(self, left: DRel, right: DRel, lk, rk):
         """Join on string keys.  Strings live in HBM as codes into per-table *sorted*
-        dictionaries, so codes of the two sides are not comparable — but codes into the sorted
-        union of both dictionaries are, and they keep each bucket's sort order (code order ==
-        string order).  Each side's key column is remapped once (one int32 gather) into the
-        union's code space; the remapped tables are cached on the originals, so the join index
-        and span caches see stable tables across queries."""
-        lc, rc = left.col(lk), right.col(rk)
-        ld, rd = lc.dictionary, rc.dictionary
-        if ld is rd or ld.equals(rd):
+        dictionaries, so codes of different tables are not comparable — but codes into the
+        sorted union of all their dictionaries are, and they keep each bucket's sort order
+        (code order == string order).  Every part's key column (both sides; a Hybrid Scan side
+        is a bucket union of the index and its shuffled appended rows) is remapped once (one
+        int32 gather) into the union's code space; the remapped tables are cached on the
+        originals, so the join index and span caches see stable tables across queries."""
+        sides = [(left, lk), (right, rk)]
+        dicts = []
+        for side, k in sides:
+            for part in side.parts or [side]:
+                dicts.append(part.col(k).dictionary)
+        if all(d is dicts[0] or d.equals(dicts[0]) for d in dicts[1:]):
             return left, right
-        ukey = (id(ld), id(rd))
+        ukey = tuple(id(d) for d in dicts)
         hit = self._unions.get(ukey)
-        if hit is None or hit[0] is not ld or hit[1] is not rd:
+        if hit is None or any(a is not b for a, b in zip(hit[0], dicts)):
             import pyarrow.compute as pc
-            union = pc.unique(pa.concat_arrays([ld.cast(pa.string()), rd.cast(pa.string())]))
-            union = union.sort()
-            hit = (ld, rd, union)
+            union = pc.unique(pa.concat_arrays([d.cast(pa.string()) for d in dicts])).sort()
+            hit = (tuple(dicts), union)
             self._unions[ukey] = hit
-        union = hit[2]
-        return (self._remapped(left, lk, union), self._remapped(right, rk, union))
+        union = hit[1]
+
+        def remap(side, k):
+            if side.parts:
+                return side.copy(parts=[self._remapped(x, k, union) for x in side.parts])
+            return self._remapped(side, k, union)
+        return remap(left, lk), remap(right, rk)
 
     def _remapped(self, r: DRel, attr, union) -> DRel:
         import pyarrow.compute as pc

@@ -22,6 +22,7 @@ GATHER_MAX_COLS = 32
 # HsType
 I8, I16, I32, I64, F32, F64, BOOL, U32, U64 = range(9)
 STR = 100
+STRDICT = 101   # int32 codes hashed through the dictionary's bytes (hash_partition.hip)
 # PredKind
 PK_INT_LIT, PK_FLT_LIT, PK_INT_COL, PK_FLT_COL, PK_IS_NULL, PK_NOT_NULL, PK_IN_SET, PK_BITMAP, \
     PK_TRUE = range(9)
@@ -38,7 +39,7 @@ class ColDesc(C.Structure):
 
 class HashCol(C.Structure):
     _fields_ = [("data", C.c_void_p), ("valid", C.c_void_p), ("offsets", C.c_void_p),
-                ("type", C.c_int32), ("xform", C.c_int32)]
+                ("aux", C.c_void_p), ("type", C.c_int32), ("xform", C.c_int32)]
 
 
 # HashCol.xform (csrc/kernels/hash_partition.hip): value transform before hashing

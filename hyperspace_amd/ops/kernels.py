@@ -39,20 +39,52 @@ def hash_xform(atype) -> int:
     return NL.XF_NONE
 
 
+_DICT_BYTES: dict = {}
+
+
+def dictionary_bytes(dictionary, device):
+    """(int64 offsets [n+1], uint8 chars) of a string dictionary on the device, uploaded once
+    per dictionary object (the entry keeps a reference, so its id is not reused)."""
+    import numpy as np
+    import pyarrow as pa
+    torch = _torch()
+    key = (id(dictionary), str(device))
+    hit = _DICT_BYTES.get(key)
+    if hit is not None and hit[0] is dictionary:
+        return hit[1], hit[2]
+    d = dictionary.cast(pa.large_binary()) if not pa.types.is_large_binary(dictionary.type) \
+        else dictionary
+    bufs = d.buffers()
+    n = len(d)
+    offs = np.frombuffer(bufs[1], dtype=np.int64, count=n + 1, offset=d.offset * 8) \
+        if n else np.zeros(1, np.int64)
+    base = int(offs[0])
+    chars = np.frombuffer(bufs[2], dtype=np.uint8)[base:int(offs[-1])] \
+        if n and bufs[2] is not None else np.zeros(1, np.uint8)
+    o = torch.from_numpy((offs - base).copy()).to(device)
+    ch = torch.from_numpy(np.ascontiguousarray(chars) if len(chars) else np.zeros(1, np.uint8)) \
+        .to(device)
+    if len(_DICT_BYTES) > 256:
+        _DICT_BYTES.clear()
+    _DICT_BYTES[key] = (dictionary, o, ch)
+    return o, ch
+
+
 def _hash_params(cols, num_buckets: int, seed: int = 42) -> NL.HashParams:
     if len(cols) > NL.HASH_MAX_COLS:
         raise ValueError("too many bucket columns")
     p = NL.HashParams()
     for i, c in enumerate(cols):
-        if c.dictionary is not None:
-            if c.offsets is None:
-                raise ValueError("string bucket column needs raw bytes (raw_strings=True)")
-            p.cols[i] = NL.HashCol(c.chars.data_ptr(), c.valid.data_ptr() if c.valid is not None else 0,
-                                   c.offsets.data_ptr(), NL.STR, 0)
+        vp = c.valid.data_ptr() if c.valid is not None else 0
+        if c.offsets is not None:
+            p.cols[i] = NL.HashCol(c.chars.data_ptr(), vp, c.offsets.data_ptr(), 0, NL.STR, 0)
+        elif c.dictionary is not None:
+            # dictionary codes: each row hashes its dictionary entry's bytes on the device
+            doff, dchars = dictionary_bytes(c.dictionary, c.data.device)
+            p.cols[i] = NL.HashCol(c.data.data_ptr(), vp, doff.data_ptr(), dchars.data_ptr(),
+                                   NL.STRDICT, 0)
         else:
-            p.cols[i] = NL.HashCol(c.data.data_ptr(),
-                                   c.valid.data_ptr() if c.valid is not None else 0, 0, c.hs_type,
-                                   hash_xform(c.atype))
+            p.cols[i] = NL.HashCol(c.data.data_ptr(), vp, 0, 0, c.hs_type, hash_xform(c.atype))
     p.ncols = len(cols)
     p.num_buckets = int(num_buckets)
     p.seed = seed

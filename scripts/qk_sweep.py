@@ -46,6 +46,15 @@ def main():
                     help="also time Q3 variants without the right predicate / aggregate tail")
     args = ap.parse_args()
     os.environ["HS_PROFILE"] = "1"
+    # heartbeat: long silent phases (data load under a profiler) must still show progress
+    import threading
+    t_start = time.time()
+
+    def beat():
+        while True:
+            time.sleep(30)
+            print(f"[qk_sweep] alive {time.time() - t_start:.0f}s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
     import torch
     from hyperspace_amd import Hyperspace, IndexConfig, Session, col, count, sum_
     from hyperspace_amd.exec import jit
