@@ -87,6 +87,7 @@ MJ_STEPS = int(os.environ.get("HS_JIT_MJ_STEPS", "1"))   # branch-free walk step
 # any LDS store), and double-buffered LDS spans (no end-of-tile barrier)
 MJ_STAGE_UNROLL = int(os.environ.get("HS_JIT_MJ_STAGE_UNROLL", "4"))
 MJ_DBUF = os.environ.get("HS_JIT_MJ_DBUF", "1") == "1"
+MJ_PREFETCH = os.environ.get("HS_JIT_MJ_PREFETCH", "1") == "1"
 MJ_KEY32 = os.environ.get("HS_JIT_MJ_KEY32", "1") == "1"  # 32-bit merge images (_key32_frame)
 # cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
 MJ_EXP = os.environ.get("HS_JIT_MJ_EXP", "")
@@ -1230,7 +1231,7 @@ def merge_join_shape(p: NL.JoinParams, compacts=None, hk=None) -> tuple:
                  for i in range(p.naggs))
     return ("merge_join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey,
             p.key_is_float, MJ_ITEMS, MJ_LDS_KEYS, MJ_STEPS, BLOCK, WAVE_SYNC,
-            _key32_frame(p, compacts) is not None, MJ_EXP, MJ_STAGE_UNROLL, MJ_DBUF,
+            _key32_frame(p, compacts) is not None, MJ_EXP, MJ_STAGE_UNROLL, MJ_DBUF, MJ_PREFETCH,
             hk.shape() if hk is not None else None)
 
 
@@ -1549,14 +1550,20 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
             b.append(f"{ind}__syncthreads();")
 
     loads = _vec_loads(g1, first)
-    _tile_loop(b, T, NI, 1, ind)
-    b.append(f"{ind}if (tb0 + {T} <= a.nrows) {{")
-    _vec_issue(b, loads, NI, ind, True)
-    body(b, True)
-    b.append(f"{ind}}} else {{")
-    _vec_issue(b, loads, NI, ind, False)
-    body(b, False)
-    b.append(f"{ind}}}")
+    if MJ_PREFETCH:
+        # software-pipelined: tile t+1's left vectors are in flight during tile t's staging,
+        # search and aggregate tail (the kernel waits on memory ~60% of its wave cycles:
+        # profiles/pmc_merge_join_r3.txt)
+        _vec_tiles(b, T, NI, ind, loads, [], body)
+    else:
+        _tile_loop(b, T, NI, 1, ind)
+        b.append(f"{ind}if (tb0 + {T} <= a.nrows) {{")
+        _vec_issue(b, loads, NI, ind, True)
+        body(b, True)
+        b.append(f"{ind}}} else {{")
+        _vec_issue(b, loads, NI, ind, False)
+        body(b, False)
+        b.append(f"{ind}}}")
     b += ["  }"]
     b += _deferred_drain(args, cols, split, approx, aggs, grouped, p.group_col, allslots, "  ",
                          final=True, hk=hk)
