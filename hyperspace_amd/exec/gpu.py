@@ -204,8 +204,7 @@ class GpuBackend:
             finish = self._exec_agg(*agg, order=order, limit=limit)
         else:
             rel = self._rel(plan)
-            t = self._to_arrow(rel, plan.output)
-            t = self._gather_ranks(t)
+            t = self._to_arrow_ranks(rel, plan.output)
             finish = (lambda: t)
         if order is None and limit is None:
             return finish
@@ -615,12 +614,55 @@ class GpuBackend:
             fixed.append(arr)
         return pa.Table.from_arrays(fixed, names=[a.name for a in out_attrs])
 
-    def _gather_ranks(self, t: pa.Table) -> pa.Table:
+    def _to_arrow_ranks(self, r: DRel, out_attrs: List[E.Attribute]) -> pa.Table:
+        """Rows of ``r`` from every rank (sharded placement): this rank's rows are materialized
+        as device columns (bucket-union parts concatenated, their string dictionaries unified)
+        and cross ranks with one packed device all-gather (``parallel/gather.py``) — no
+        pickled tables."""
         d = self._dist()
         if d is None or d.world == 1:
-            return t
-        parts = d.all_gather_object(t)
-        return pa.concat_tables(parts)
+            return self._to_arrow(r, out_attrs)
+        import torch
+        from ..parallel.gather import gather_device_columns
+        parts = r.parts or [r]
+        mats = [self._materialize(x, out_attrs) for x in parts]
+        cols = []
+        for a in out_attrs:
+            cs = [m[a.expr_id] for m in mats]
+            if len(cs) == 1:
+                cols.append(cs[0])
+                continue
+            dicts = [c.dictionary for c in cs]
+            if any(x is not None for x in dicts):
+                import pyarrow.compute as pc
+                from ..parallel.dictionary import remap_table
+                union = pc.unique(pa.concat_arrays([x.cast(pa.string()) for x in dicts])).sort()
+                datas = []
+                for c in cs:
+                    t_ = torch.from_numpy(remap_table(c.dictionary, union)).to(self.device)
+                    datas.append(K.lookup_i32(t_, c.data) if len(c.dictionary) and len(c)
+                                 else torch.zeros_like(c.data))
+            else:
+                union, datas = None, [c.data for c in cs]
+            valid = None
+            if any(c.valid is not None for c in cs):
+                valid = torch.cat([c.valid if c.valid is not None else
+                                   torch.ones(len(c), dtype=torch.uint8, device=self.device)
+                                   for c in cs])
+            cols.append(DeviceColumn(torch.cat(datas), valid, cs[0].atype, union))
+        n = len(cols[0]) if cols else 0
+        with stage("rows.gather_ranks"):
+            allc = gather_device_columns(d, cols, n)
+        arrays = []
+        for a, c in zip(out_attrs, allc):
+            arr = c.to_arrow()
+            if not arr.type.equals(a.data_type):
+                try:
+                    arr = arr.cast(a.data_type)
+                except (pa.ArrowInvalid, pa.ArrowNotImplementedError):
+                    pass
+            arrays.append(arr)
+        return pa.Table.from_arrays(arrays, names=[a.name for a in out_attrs])
 
     # ------------------------------------------------------------------------------------------
     # Repartition (device shuffle for non-index inputs)
@@ -1087,35 +1129,47 @@ class GpuBackend:
 
         Every rank aggregated only its own buckets (index) or files (non-index), so its [G, A]
         partials are laid out over its *local* domain — integer range ``[gbase, gbase+G)`` or the
-        rank's own string dictionary.  The ranks exchange those domains (one small object
-        all-gather), scatter their rows into the union layout, and only then run the element-wise
-        all-reduce.  Ranks that saw no rows do not contribute a domain."""
+        rank's own string dictionary.  The ranks exchange those domains with tensor collectives
+        (an all-gather of (G, base, live) and, for string keys, the raw-buffer dictionary union
+        of ``parallel/dictionary.py`` — nothing is pickled), scatter their rows into the union
+        layout, and only then run the element-wise all-reduce.  Ranks that saw no rows do not
+        contribute an integer domain."""
         import torch
+        from ..parallel.dictionary import union_sorted
+        from ..parallel.gather import _all_gather_flat
         live_here = bool(cnts.view(G, A)[:, A - 1].sum().item() > 0)
-        infos = d.all_gather_object((G, gbase, gdict.to_pylist() if gdict is not None else None,
-                                     gtype, live_here))
-        live = [x for x in infos if x[4]]
-        if not live:
-            z = self._empty_agg(A, 1)
-            return (*z, 1, 0, None, gtype)
-        if any(x[2] is not None for x in live):
-            values = sorted({v for x in live for v in (x[2] or [])})
-            pos = {v: i for i, v in enumerate(values)}
-            Gg, base, new_dict = len(values), 0, pa.array(values, type=pa.string())
-            idx = [pos[v] for v in gdict.to_pylist()] if (live_here and gdict is not None) else []
+        cdev = d.device if d.backend == "nccl" else torch.device("cpu")
+        info = torch.tensor([G, gbase, 1 if live_here else 0, 1 if gdict is not None else 0],
+                            dtype=torch.int64, device=cdev)
+        allinfo = _all_gather_flat(d, info).view(d.world, 4).cpu().numpy()
+        live = [x for x in allinfo if x[2]]
+        if any(x[3] for x in allinfo):
+            local = gdict if (live_here and gdict is not None) else pa.array([], pa.string())
+            new_dict = union_sorted(local, d)       # collective: every rank calls it
+            if not live:
+                z = self._empty_agg(A, 1)
+                return (*z, 1, 0, None, gtype)
+            Gg, base = max(len(new_dict), 1), 0
+            if live_here and gdict is not None and len(gdict):
+                import pyarrow.compute as pc
+                idx = pc.index_in(gdict.cast(pa.string()), value_set=new_dict).to_numpy(
+                    zero_copy_only=False).astype(np.int64).tolist()
+            else:
+                idx = []
         else:
-            base = min(x[1] for x in live)
-            Gg = max(x[1] + x[0] for x in live) - base
+            if not live:
+                z = self._empty_agg(A, 1)
+                return (*z, 1, 0, None, gtype)
+            base = int(min(x[1] for x in live))
+            Gg = int(max(x[1] + x[0] for x in live)) - base
             new_dict = None
             idx = list(range(gbase - base, gbase - base + G)) if live_here else []
-        gt = next(x[3] for x in live if x[3] is not None) if any(x[3] is not None for x in live) \
-            else gtype
         s2, c2, mn2, mx2 = self._empty_agg(A, Gg)
         if idx:
             it = torch.tensor(idx, dtype=torch.int64, device=self.device)
             for dst, src in ((s2, sums), (c2, cnts), (mn2, mins), (mx2, maxs)):
                 dst.view(Gg, A)[it] = src.view(G, A)[:len(idx)]
-        return s2, c2, mn2, mx2, Gg, base, new_dict, gt
+        return s2, c2, mn2, mx2, Gg, base, new_dict, gtype
 
     def _agg_output(self, e, group, gvals, vals, nrows):
         inner = e.child if isinstance(e, E.Alias) else e
@@ -1156,9 +1210,15 @@ class GpuBackend:
                 k = (gkey, r.colmap.get(group.expr_id))
                 dom = self._gdomains.get(k)
                 if dom is None:
-                    live = [x for x in d.all_gather_object((base, G)) if x[1] > 0]
-                    lo = min((x[0] for x in live), default=0)
-                    dom = (lo, max((x[0] + x[1] for x in live), default=lo) - lo)
+                    # (min, max) over ranks with one small all-reduce (no object collective)
+                    import torch
+                    cdev = d.device if d.backend == "nccl" else torch.device("cpu")
+                    big = 1 << 62
+                    t = torch.tensor([-base if G > 0 else -big, base + G - 1 if G > 0 else -big],
+                                     dtype=torch.int64, device=cdev)
+                    d.all_reduce(t, "max")
+                    lo, hi = -int(t[0].item()), int(t[1].item())
+                    dom = (lo, hi - lo + 1) if hi >= lo else (0, 0)
                     self._gdomains[k] = dom
                 base, G = dom
                 # identical on every rank, so the fallback decision is unanimous by construction
@@ -1168,7 +1228,7 @@ class GpuBackend:
         too_big = G > limit
         if multi:
             # data-dependent fallbacks must be unanimous, or ranks diverge in their collectives
-            too_big = any(d.all_gather_object(too_big))
+            too_big = d.agree_any([too_big])[0]
         if too_big:
             raise _NeedHash("group domain too large for LDS aggregation")
         if G == 0:

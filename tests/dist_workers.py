@@ -146,10 +146,32 @@ def spmd_gpu(ctx, data_dir):
     q = {"join_w": j.groupBy(t2["w"]).agg(sum_(col("v")).alias("sv"), count("*").alias("n")),
          "join_s": j.groupBy(t2["s"]).agg(sum_(col("v")).alias("sv"), min_(col("v")).alias("mv")),
          "filter": t1.filter(col("k") < 20).select("k", "v")}
+    q.update({
+        # row-producing join over sharded buckets: device row gather across ranks
+        "join_rows": j.select(t1["k"], t1["v"], t2["s"]),
+        # hash-mode aggregate (two group columns) + ORDER BY ... LIMIT
+        "join_multi": j.groupBy(t2["w"], t2["s"]).agg(sum_(col("v")).alias("sv")),
+        "topk": j.groupBy(t1["k"]).agg(sum_(col("v")).alias("sv"))
+                 .orderBy(col("sv").desc(), col("k")).limit(5),
+        "left_outer": t1.join(t2.filter(col("w") < 3), t1["k"] == t2["k"], "left")
+                        .select(t1["k"], t2["w"])})
     for name, df in q.items():
-        out[name] = sorted(tuple(r.values()) for r in df.to_arrow().to_pylist())
+        rows = [tuple(r.values()) for r in df.to_arrow().to_pylist()]
+        out[name] = rows if name == "topk" else sorted(rows, key=repr)
         out["paths"].append(s.backend().last_path)
         out[name + "_plan"] = df.queryExecution.executed_plan.tree_string()
+    # steady state: the same queries again make no pickled (object) collective
+    calls = {"n": 0}
+    orig = ctx.all_gather_object
+
+    def counting(obj):
+        calls["n"] += 1
+        return orig(obj)
+    ctx.all_gather_object = counting
+    for name, df in q.items():
+        df.to_arrow()
+    ctx.all_gather_object = orig
+    out["steady_object_collectives"] = calls["n"]
     ctx.barrier()
     return out
 

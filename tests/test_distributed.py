@@ -148,13 +148,35 @@ def test_spmd_device_executor(tmp_path, spmd_data, device):
     exp_sm = oracle("s", [("v", "sum"), ("v", "min")])
     flt = sorted((k, v) for k, v in zip(t1.column("k").to_pylist(), t1.column("v").to_pylist())
                  if k < 20)
+    rows = sorted(zip(j.column("k").to_pylist(), j.column("v").to_pylist(),
+                      j.column("s").to_pylist()), key=repr)
+    gm = j.group_by(["w", "s"]).aggregate([("v", "sum")])
+    exp_multi = sorted(zip(gm.column("w").to_pylist(), gm.column("s").to_pylist(),
+                           gm.column("v_sum").to_pylist()), key=repr)
+    gk = j.group_by("k").aggregate([("v", "sum")])
+    exp_topk = sorted(zip(gk.column("k").to_pylist(), gk.column("v_sum").to_pylist()),
+                      key=lambda x: (-x[1], x[0]))[:5]
+    t2f = t2.filter(pa.compute.less(t2.column("w"), 3))
+    lo = t1.join(t2f, "k", join_type="left outer")
+    exp_lo = sorted(zip(lo.column("k").to_pylist(), lo.column("w").to_pylist()), key=repr)
+
+    def close(a, b):
+        assert len(a) == len(b), (len(a), len(b))
+        for x, y in zip(a, b):
+            for u, v in zip(x, y):
+                assert (abs(u - v) <= 1e-9 * max(1.0, abs(v))) if isinstance(v, float) else u == v
     for d in res:
-        assert d["paths"] == ["native"] * 4, d["paths"]
+        assert d["paths"] == ["native"] * 8, d["paths"]
         assert [tuple(x) for x in d["nonindex_join"]] == exp_s
         assert [tuple(x) for x in d["join_w"]] == exp_w
         assert [tuple(x) for x in d["join_s"]] == exp_sm
         assert [tuple(x) for x in d["filter"]] == flt
         assert "Name: i1" in d["join_w_plan"]
+        close([tuple(x) for x in d["join_rows"]], rows)
+        close([tuple(x) for x in d["join_multi"]], exp_multi)
+        close([tuple(x) for x in d["topk"]], exp_topk)
+        assert [tuple(x) for x in d["left_outer"]] == exp_lo
+        assert d["steady_object_collectives"] == 0
 
 
 def test_bench_two_ranks_reports_both_placements(tmp_path):
