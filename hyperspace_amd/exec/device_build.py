@@ -155,13 +155,15 @@ def _streaming_plan(session, rel, my_files, columns, lineage_ids, num_buckets, d
     (``spark.hyperspace.mi.build.hbmBudgetBytes``), else None.  Streaming covers single-rank
     Parquet builds of fixed-width columns (string dictionaries are built over the whole input
     in one pass)."""
-    if world > 1 or source_format(rel) != "parquet" or not my_files:
-        return None
+    dist = getattr(session, "dist", None) if world > 1 else None
     from ..io.reader import output_schema
     from .device_table import storage_numpy_dtype
     schema = output_schema(rel.data_schema, rel.location.partition_spec, columns)
-    if any(is_string(f.type) for f in schema):
+    eligible = source_format(rel) == "parquet" and not any(is_string(f.type) for f in schema)
+    if dist is None and (not eligible or not my_files):
         return None
+    if dist is not None and dist.agree_any([not eligible])[0]:
+        return None                  # unanimous: every rank takes the same build path
     from . import staging
     tf = time.perf_counter()
     infos = list(staging.io_pool().map(lambda f: _footer_info(f, list(schema.names)), my_files))
@@ -169,14 +171,35 @@ def _streaming_plan(session, rel, my_files, columns, lineage_ids, num_buckets, d
     rows = [r for r, _ in infos]
     row_bytes = sum(storage_numpy_dtype(f.type).itemsize + 1 for f in schema) + \
         (8 if lineage_ids is not None else 0) + 4
+    # a rank holds its own decoded rows plus, after the exchange, its buckets' rows
     est = int(sum(rows) * row_bytes * BUILD_SORT_FACTOR)
     tb = time.perf_counter()
     budget = _build_budget(session, device)
     LAST_BUILD_STATS["plan_budget_s"] = round(time.perf_counter() - tb, 4)
     passes = plan_passes(est, budget, num_buckets)
+    if dist is not None:
+        # every rank runs the same passes and exchange batches (each batch is a collective)
+        npass = int(dist.all_reduce_max_float(float(len(passes))))
+        if npass <= 1:
+            return None
+        edges = np.linspace(0, num_buckets, min(npass, num_buckets) + 1).round().astype(int)
+        passes = [(int(a), int(b)) for a, b in zip(edges[:-1], edges[1:]) if b > a]
+        # the one-pass build's file batches (_upload_parquet), so rows of a bucket reach the
+        # stable sort in the same (batch, source rank, row) order: byte-identical files
+        k = int(dist.all_reduce_max_float(float(-(-len(my_files) // FILES_PER_BATCH))))
+        fe = np.linspace(0, len(my_files), max(k, 1) + 1).round().astype(int)
+        groups = [(int(a), int(b)) for a, b in zip(fe[:-1], fe[1:])]
+        fixed = list(schema.names)
+        may = set().union(*[m for _, m in infos]) if infos else set()
+        part_names = {f.name for f in rel.location.partition_spec.columns} \
+            if rel.location.partition_spec is not None else set()
+        may |= {n for n in fixed if n in part_names or n not in rel.data_schema.names}
+        agreed = dist.agree_any([n in may for n in fixed])
+        nullable = {n for n, a in zip(fixed, agreed) if a}
+        return passes, groups, row_bytes, nullable
     if len(passes) <= 1:
         return None
-    return passes, plan_file_groups(rows, row_bytes, max(budget // 4, 1)), row_bytes
+    return passes, plan_file_groups(rows, row_bytes, max(budget // 4, 1)), row_bytes, None
 
 
 def _streaming_build(session, rel, my_files, columns, indexed, num_buckets, out_path,
@@ -187,7 +210,9 @@ def _streaming_build(session, rel, my_files, columns, indexed, num_buckets, out_
     bucket files are byte-identical to a one-pass build's; HBM holds one decoded file group plus
     one pass's rows instead of the whole input."""
     import torch
-    passes, groups, _ = plan
+    passes, groups, _, nullable = plan
+    dist = getattr(session, "dist", None)
+    multi = dist is not None and dist.world > 1
     paths: List[str] = []
     t0 = time.perf_counter()
     decode_s = sort_s = 0.0
@@ -196,23 +221,60 @@ def _streaming_build(session, rel, my_files, columns, indexed, num_buckets, out_
     for pi, (lo, hi) in enumerate(passes):
         parts: Dict[str, list] = {}
         buckets = []
+        ex = None
         for a, b in groups:
             td = time.perf_counter()
             cols, names, schema = _upload_parquet(rel, my_files[a:b], columns, indexed,
-                                                  lineage_ids, device, None)
+                                                  lineage_ids, device, None,
+                                                  nullable_override=nullable)
             if pi == 0:
                 source_bytes += sum(c.nbytes() for c in cols.values())
-            bucket, _ = K.murmur3_bucket([cols[c] for c in indexed], num_buckets,
-                                         with_counts=False)
+            n_rows = len(cols[names[0]]) if names else 0
+            if n_rows:
+                bucket, _ = K.murmur3_bucket([cols[c] for c in indexed], num_buckets,
+                                             with_counts=False)
+            else:
+                bucket = torch.empty(0, dtype=torch.int32, device=device)
             keep = torch.nonzero((bucket >= lo) & (bucket < hi)).squeeze(1)
             got = K.gather_columns([cols[n] for n in names], keep)
-            for n, c in zip(names, got):
-                parts.setdefault(n, []).append(c)
-            buckets.append(bucket.index_select(0, keep))
-            del cols, bucket, keep, got
+            kb = bucket.index_select(0, keep)
+            if multi:
+                # rows of this pass's buckets go to their owner rank (b % world): one packed
+                # all-to-all per file batch, every rank the same number of batches
+                from ..parallel.exchange import RowExchange
+                vnames = [n for n in names if n in (nullable or set())]
+                send = [c.data for c in got] + \
+                    [(c.valid if c.valid is not None else
+                      torch.ones(c.data.shape[0], dtype=torch.uint8, device=device))
+                     for n, c in zip(names, got) if n in vnames] + [kb]
+                if ex is None:
+                    ex = RowExchange(dist, [t.dtype for t in send], device)
+                ex.add(send, kb)
+            else:
+                for n, c in zip(names, got):
+                    parts.setdefault(n, []).append(c)
+                buckets.append(kb)
+            del cols, bucket, keep, got, kb
             torch.cuda.synchronize()
             decode_s += time.perf_counter() - td
         ts = time.perf_counter()
+        if multi:
+            recv = ex.finish() if ex is not None else None
+            vnames = [n for n in names if n in (nullable or set())]
+            table = {}
+            vi = len(names)
+            for j, n in enumerate(names):
+                valid = None
+                if n in vnames:
+                    valid = recv[vi]
+                    vi += 1
+                atype = schema.field(n).type if n in schema.names else pa.int64()
+                table[n] = DeviceColumn(recv[j], valid, atype, None)
+            paths += _sort_and_write(session, table, names, recv[-1], indexed, num_buckets,
+                                     out_path, schema, rank)
+            del table, recv
+            sort_s += time.perf_counter() - ts
+            continue
         table = {}
         for n in names:
             cs = parts[n]
@@ -228,6 +290,8 @@ def _streaming_build(session, rel, my_files, columns, indexed, num_buckets, out_
                                  num_buckets, out_path, schema, rank)
         del table, buckets
         sort_s += time.perf_counter() - ts
+    if multi:
+        dist.barrier()
     LAST_BUILD_STATS.update({"passes": len(passes), "file_groups": len(groups),
                              "source_bytes": source_bytes,
                              "pass_decode_s": decode_s, "pass_sort_write_s": sort_s,
@@ -433,7 +497,8 @@ def _footer_info(path: str, names: List[str]):
     return md.num_rows, maybe
 
 
-def _upload_parquet(rel, my_files, columns, indexed, lineage_ids, device, dist, xs=None):
+def _upload_parquet(rel, my_files, columns, indexed, lineage_ids, device, dist, xs=None,
+                    nullable_override=None):
     """Pipelined decode -> pinned -> HBM upload of this rank's Parquet files (staging.py).
     With a multi-GPU exchange ``xs`` and no string columns, every batch of files is hashed and
     exchanged as soon as it is on the device, overlapping the decode of the next batch."""
@@ -488,6 +553,8 @@ def _upload_parquet(rel, my_files, columns, indexed, lineage_ids, device, dist, 
         k = int(dist.all_reduce_max_float(float(-(-len(my_files) // FILES_PER_BATCH))))
         edges = np.linspace(0, len(my_files), max(k, 1) + 1).round().astype(int)
         batches = [(int(a), int(b)) for a, b in zip(edges[:-1], edges[1:])]
+    if nullable_override is not None:
+        nullable = set(nullable_override)
     tu = time.perf_counter()
     up = staging.upload_files(read_file, my_files, counts, schema, device, lin,
                               C.DATA_FILE_NAME_ID,

@@ -71,6 +71,11 @@ class RowExchange:
         self.device = device
         self.batches: List[_Batch] = []
         self.sent_bytes = 0      # bytes this rank sent to other ranks (excludes its own slice)
+        # double-buffered counts: a batch's payload all-to-all is issued when the NEXT batch
+        # arrives (or at finish), by which time its counts / layout D2H has long completed, so
+        # add() never blocks the host on the device (decode of the next files keeps going)
+        self._pending = None
+        self.host_waits = 0      # add() calls that had to wait for a counts copy
         if len(self.dtypes) > 32:
             raise ValueError("RowExchange: at most 32 columns")
         if self.world > 64:
@@ -133,6 +138,17 @@ class RowExchange:
         host.copy_(meta, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
+        prev, self._pending = self._pending, (ev, host, send, tile, meta, cols, bucket, dev)
+        if prev is not None:
+            self._issue_payload(prev)
+
+    def _issue_payload(self, pend) -> None:
+        """Payload all-to-all of a packed batch whose counts copy was queued earlier."""
+        import torch
+        ev, host, send, tile, meta, cols, bucket, dev = pend
+        W, Cn = self.world, len(self.dtypes)
+        if not ev.query():
+            self.host_waits += 1
         ev.synchronize()
         h = host.numpy()
         sc, rc = h[:W].copy(), h[W:2 * W].copy()
@@ -175,11 +191,17 @@ class RowExchange:
 
     # -- receive side ----------------------------------------------------------------------------
     def received_rows(self) -> int:
+        if self._pending is not None:
+            pend, self._pending = self._pending, None
+            self._issue_payload(pend)
         return int(sum(int(b.counts.sum()) for b in self.batches))
 
     def finish(self) -> List:
         """Wait for every batch and unpack the received runs into one tensor per column."""
         import torch
+        if self._pending is not None:
+            pend, self._pending = self._pending, None
+            self._issue_payload(pend)
         total = self.received_rows()
         dev = self.batches[0].recv.device if self.batches else (self.device or "cpu")
         outs = [torch.empty(total, dtype=dt, device=dev) for dt in self.dtypes]

@@ -224,4 +224,24 @@ def nccl_paths(ctx, data_dir):
     return out
 
 
-SCENARIOS = {"nccl_paths": nccl_paths, "collectives": collectives, "spmd_index": spmd_index, "spmd_gpu": spmd_gpu}
+def spmd_stream_build(ctx, data_dir):
+    """Multi-rank device build twice: one pass, and under a tiny HBM budget (bucket-range passes,
+    every file batch exchanged per pass); the parent compares the bucket files byte for byte."""
+    from hyperspace_amd import Hyperspace, IndexConfig
+    from hyperspace_amd.exec import device_build
+    out = {}
+    for name, budget in (("one_pass", 1 << 40), ("streamed", 600_000)):
+        s = _session(ctx, data_dir, **{"spark.hyperspace.mi.execution.device": "gpu",
+                                       "spark.hyperspace.index.numBuckets": "16",
+                                       "spark.hyperspace.system.path":
+                                           os.path.join(data_dir, "ix"),
+                                       "spark.hyperspace.mi.build.hbmBudgetBytes": str(budget)})
+        Hyperspace(s).createIndex(s.read.parquet(os.path.join(data_dir, "src")),
+                                  IndexConfig(name, ["k"], ["d", "p", "q"]))
+        st = device_build.LAST_BUILD_STATS
+        out[name] = {"passes": st.get("passes"), "groups": st.get("file_groups")}
+    ctx.barrier()
+    return out
+
+
+SCENARIOS = {"spmd_stream_build": spmd_stream_build, "nccl_paths": nccl_paths, "collectives": collectives, "spmd_index": spmd_index, "spmd_gpu": spmd_gpu}
