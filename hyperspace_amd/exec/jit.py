@@ -86,8 +86,8 @@ MJ_STEPS = int(os.environ.get("HS_JIT_MJ_STEPS", "1"))   # branch-free walk step
 # right-span staging: per-thread rows loaded per round trip (all loads of a round issue before
 # any LDS store), and double-buffered LDS spans (no end-of-tile barrier)
 MJ_STAGE_UNROLL = int(os.environ.get("HS_JIT_MJ_STAGE_UNROLL", "4"))
-MJ_DBUF = os.environ.get("HS_JIT_MJ_DBUF", "1") == "1"
-MJ_PREFETCH = os.environ.get("HS_JIT_MJ_PREFETCH", "1") == "1"
+MJ_DBUF = os.environ.get("HS_JIT_MJ_DBUF", "0") == "1"
+MJ_PREFETCH = os.environ.get("HS_JIT_MJ_PREFETCH", "0") == "1"
 MJ_KEY32 = os.environ.get("HS_JIT_MJ_KEY32", "1") == "1"  # 32-bit merge images (_key32_frame)
 # cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
 MJ_EXP = os.environ.get("HS_JIT_MJ_EXP", "")
