@@ -717,8 +717,13 @@ int plan_chunk(File* f, int rg, int col, uint8_t* raw, int64_t raw_cap, int64_t 
   const ChunkMeta& m = f->rgs[(size_t)rg].cols[(size_t)col];
   const SchemaEl& s = f->schema[(size_t)f->leaves[(size_t)col]];
   if (s.repetition == 2) return HS_PQ_UNSUPPORTED;
-  const int eb = elem_bytes(m.type);
+  // BYTE_ARRAY: only dictionary-encoded chunks.  The dictionary page is inflated here (the
+  // caller parses its strings, hs_pq_plain_strings) and the data pages decode on the device to
+  // 4-byte dictionary codes through a code table the caller supplies in `dict`.
+  const bool strings = m.type == 6;
+  const int eb = strings ? 4 : elem_bytes(m.type);
   if (!eb) return HS_PQ_UNSUPPORTED;
+  if (strings && !hbuf) return HS_PQ_UNSUPPORTED;
   if (m.codec != 0 && m.codec != 1) return HS_PQ_UNSUPPORTED;
   const bool optional = s.repetition == 1;
   // the device path writes values at their row index: every row must hold a value
@@ -754,11 +759,13 @@ int plan_chunk(File* f, int rg, int col, uint8_t* raw, int64_t raw_cap, int64_t 
       p.kind = 2;
       p.usize = ph.usize;
       p.nvals = ph.dict_nvals;
-      if ((int64_t)ph.dict_nvals * eb > ph.usize) return HS_PQ_CORRUPT;
+      if ((int64_t)ph.dict_nvals * (strings ? 4 : eb) > ph.usize || ph.dict_nvals < 0)
+        return HS_PQ_CORRUPT;
       dict_idx = *npages;
     } else {
       const bool dict = ph.enc == 2 || ph.enc == 8;
       if (!dict && ph.enc != 0) return HS_PQ_UNSUPPORTED;
+      if (strings && !dict) return HS_PQ_UNSUPPORTED;   // PLAIN strings: decoded another way
       if (dict && dict_idx < 0) return HS_PQ_CORRUPT;
       p.enc = ph.enc;
       p.nvals = ph.nvals;
@@ -787,8 +794,9 @@ int plan_chunk(File* f, int rg, int col, uint8_t* raw, int64_t raw_cap, int64_t 
     // host-inflated, `src` = offset in the handle's host_pages buffer (levels included).
     const int mode = g_host_inflate.load(std::memory_order_relaxed);
     const bool big_dict = p.kind == 2 && p.usize > kHostDictMin;
-    const bool dense = p.codec == 1 && mode > 0 &&
-        (big_dict || (mode > 1 && (int64_t)p.usize * 10 >= (int64_t)p.csize * 11));
+    const bool str_dict = strings && p.kind == 2;
+    const bool dense = str_dict || (p.codec == 1 && mode > 0 &&
+        (big_dict || (mode > 1 && (int64_t)p.usize * 10 >= (int64_t)p.csize * 11)));
     // one wavefront inflates one page on the device: a multi-MB Snappy page left to it runs for
     // seconds (profiles/cold_load_r2.jsonl: 58 s for an index of 1M-row pages), so such a
     // column goes to the host page layer instead
@@ -799,11 +807,15 @@ int plan_chunk(File* f, int rg, int col, uint8_t* raw, int64_t raw_cap, int64_t 
       const int64_t at = (hat + 15) & ~(int64_t)15;
       if (at + p.usize + 16 > hcap) return HS_PQ_CAPACITY;
       memcpy(hbuf + at, src, (size_t)lv);
-      size_t got = 0;
-      if (!snappy_decompress(src + lv, (size_t)(p.csize - lv), hbuf + at + lv,
-                             (size_t)(p.usize - lv), &got) ||
-          got != (size_t)(p.usize - lv))
-        return HS_PQ_CORRUPT;
+      if (p.codec == 0) {
+        memcpy(hbuf + at, src, (size_t)p.usize);
+      } else {
+        size_t got = 0;
+        if (!snappy_decompress(src + lv, (size_t)(p.csize - lv), hbuf + at + lv,
+                               (size_t)(p.usize - lv), &got) ||
+            got != (size_t)(p.usize - lv))
+          return HS_PQ_CORRUPT;
+      }
       p.codec = 2;
       p.src = at;
       hat = at + p.usize + 16;
@@ -859,6 +871,29 @@ int64_t hs_pq_chunk_host_bound(void* h, int rg, int col) {
 }
 
 int hs_pq_page_size() { return (int)sizeof(HsPqPage); }
+
+// A PLAIN BYTE_ARRAY stream (`n` values of 4-byte little-endian length + bytes, as in a
+// dictionary page) to Arrow string layout: offsets[n + 1] (int32) and the concatenated bytes in
+// `chars` (capacity `cap`, at most `len`).  Returns the byte count, or -1 when the stream is
+// shorter than its lengths say.
+int64_t hs_pq_plain_strings(const uint8_t* src, int64_t len, int64_t n, int32_t* offsets,
+                            uint8_t* chars, int64_t cap) {
+  int64_t at = 0, out = 0;
+  offsets[0] = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    if (at + 4 > len) return -1;
+    uint32_t l;
+    memcpy(&l, src + at, 4);
+    at += 4;
+    if ((int64_t)l > len - at || out + (int64_t)l > cap || out + (int64_t)l > INT32_MAX)
+      return -1;
+    memcpy(chars + out, src + at, l);
+    at += l;
+    out += l;
+    offsets[i + 1] = (int32_t)out;
+  }
+  return out;
+}
 
 
 // Opens a file and parses its footer.  Always returns a handle (check hs_pq_ok / hs_pq_error;

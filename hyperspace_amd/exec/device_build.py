@@ -151,15 +151,16 @@ def _build_budget(session, device) -> int:
 
 
 def _streaming_plan(session, rel, my_files, columns, lineage_ids, num_buckets, device, world):
-    """(passes, file groups, row bytes) when this rank's build does not fit the HBM budget
-    (``spark.hyperspace.mi.build.hbmBudgetBytes``), else None.  Streaming covers single-rank
-    Parquet builds of fixed-width columns (string dictionaries are built over the whole input
-    in one pass)."""
+    """(passes, file groups, row bytes, nullable columns, string dictionaries) when this rank's
+    build does not fit the HBM budget (``spark.hyperspace.mi.build.hbmBudgetBytes``), else
+    None.  Covers Parquet builds on any number of ranks.  String columns get their job-global
+    sorted dictionary up front (``_string_dictionaries``), so every file group's codes map onto
+    one code space before they are kept, exchanged and sorted."""
     dist = getattr(session, "dist", None) if world > 1 else None
     from ..io.reader import output_schema
     from .device_table import storage_numpy_dtype
     schema = output_schema(rel.data_schema, rel.location.partition_spec, columns)
-    eligible = source_format(rel) == "parquet" and not any(is_string(f.type) for f in schema)
+    eligible = source_format(rel) == "parquet"
     if dist is None and (not eligible or not my_files):
         return None
     if dist is not None and dist.agree_any([not eligible])[0]:
@@ -196,10 +197,66 @@ def _streaming_plan(session, rel, my_files, columns, lineage_ids, num_buckets, d
         may |= {n for n in fixed if n in part_names or n not in rel.data_schema.names}
         agreed = dist.agree_any([n in may for n in fixed])
         nullable = {n for n, a in zip(fixed, agreed) if a}
-        return passes, groups, row_bytes, nullable
+        return passes, groups, row_bytes, nullable, _string_dictionaries(rel, my_files, schema,
+                                                                         dist)
     if len(passes) <= 1:
         return None
-    return passes, plan_file_groups(rows, row_bytes, max(budget // 4, 1)), row_bytes, None
+    return (passes, plan_file_groups(rows, row_bytes, max(budget // 4, 1)), row_bytes, None,
+            _string_dictionaries(rel, my_files, schema, None))
+
+
+def _string_dictionaries(rel, my_files, schema, dist) -> Dict[str, pa.Array]:
+    """Job-global sorted dictionary of every string column of a streaming build: the union of
+    the files' Parquet dictionary pages (read as dictionary arrays, no string materialised per
+    row; plain-encoded pages contribute their values) over all ranks."""
+    import pyarrow.parquet as pq
+    from ..parallel.dictionary import union_sorted
+    from . import staging
+    names = [f.name for f in schema if is_string(f.type)]
+    if not names:
+        return {}
+    part_names = {f.name for f in rel.location.partition_spec.columns} \
+        if rel.location.partition_spec is not None else set()
+    file_cols = [n for n in names if n not in part_names and n in rel.data_schema.names]
+
+    def values(f):
+        out = {}
+        if file_cols:
+            t = pq.read_table(P.to_local(f), columns=file_cols, read_dictionary=file_cols)
+            for n in file_cols:
+                vals = []
+                for ch in t.column(n).chunks:
+                    vals.append(ch.dictionary if pa.types.is_dictionary(ch.type)
+                                else pc.unique(ch))
+                out[n] = vals
+        rest = [n for n in names if n not in file_cols]
+        if rest:
+            from ..io.reader import read_files
+            t = read_files("parquet", [f], rel.data_schema, rel.options,
+                           rel.location.partition_spec, rest)
+            for n in rest:
+                out[n] = [pc.unique(t.column(n).combine_chunks())]
+        return out
+    per_file = list(staging.io_pool().map(values, my_files))
+    dicts = {}
+    for n in names:
+        parts = [a.cast(pa.string()) for v in per_file for a in v.get(n, [])]
+        local = pa.concat_arrays(parts) if parts else pa.array([], pa.string())
+        dicts[n] = union_sorted(local, dist)
+    return dicts
+
+
+def _to_dictionary(c: DeviceColumn, gd: pa.Array) -> DeviceColumn:
+    """``c``'s codes re-expressed over ``gd`` (a superset of its dictionary), on the device."""
+    import torch
+    from ..parallel.dictionary import remap_table
+    if c.dictionary is None or c.dictionary.equals(gd):
+        return DeviceColumn(c.data, c.valid, c.atype, gd)
+    data = c.data
+    if len(c.dictionary) and len(data):
+        tab = torch.from_numpy(remap_table(c.dictionary, gd)).to(data.device)
+        data = K.lookup_i32(tab, data)
+    return DeviceColumn(data, c.valid, c.atype, gd)
 
 
 def _streaming_build(session, rel, my_files, columns, indexed, num_buckets, out_path,
@@ -210,7 +267,7 @@ def _streaming_build(session, rel, my_files, columns, indexed, num_buckets, out_
     bucket files are byte-identical to a one-pass build's; HBM holds one decoded file group plus
     one pass's rows instead of the whole input."""
     import torch
-    passes, groups, _, nullable = plan
+    passes, groups, _, nullable, sdicts = plan
     dist = getattr(session, "dist", None)
     multi = dist is not None and dist.world > 1
     paths: List[str] = []
@@ -227,6 +284,8 @@ def _streaming_build(session, rel, my_files, columns, indexed, num_buckets, out_
             cols, names, schema = _upload_parquet(rel, my_files[a:b], columns, indexed,
                                                   lineage_ids, device, None,
                                                   nullable_override=nullable)
+            for n, gd in sdicts.items():
+                cols[n] = _to_dictionary(cols[n], gd)
             if pi == 0:
                 source_bytes += sum(c.nbytes() for c in cols.values())
             n_rows = len(cols[names[0]]) if names else 0
@@ -269,7 +328,7 @@ def _streaming_build(session, rel, my_files, columns, indexed, num_buckets, out_
                     valid = recv[vi]
                     vi += 1
                 atype = schema.field(n).type if n in schema.names else pa.int64()
-                table[n] = DeviceColumn(recv[j], valid, atype, None)
+                table[n] = DeviceColumn(recv[j], valid, atype, sdicts.get(n))
             paths += _sort_and_write(session, table, names, recv[-1], indexed, num_buckets,
                                      out_path, schema, rank)
             del table, recv
@@ -425,10 +484,15 @@ class _BatchedExchange:
         return out, got[-1]
 
 
-def _finish_strings(host_strings: Dict[str, list], cols: Dict[str, DeviceColumn], indexed,
-                    device, dist) -> None:
-    """Dictionary-encode string columns with a job-global sorted dictionary and upload codes."""
-    for name, chunks in host_strings.items():
+def _finish_strings(up, cols: Dict[str, DeviceColumn], indexed, device, dist) -> None:
+    """Dictionary-encode string columns with a job-global sorted dictionary and upload codes.
+    Columns whose dictionary pages the device decoded are remapped on the device
+    (``staging.finish_strings``); the rest come from the host chunks."""
+    from . import staging
+    staging.finish_strings(up, cols, device, dist, names=list(up.device_strings))
+    for name, chunks in up.host_strings.items():
+        if name in up.device_strings:
+            continue
         chunks = [c for c in chunks if c is not None]
         if name not in indexed and chunks and \
                 all(pa.types.is_dictionary(c.type) for c in chunks):
@@ -562,7 +626,7 @@ def _upload_parquet(rel, my_files, columns, indexed, lineage_ids, device, dist, 
                               nullable=nullable, on_batch=on_batch, file_batches=batches)
     LAST_BUILD_STATS["upload_files_s"] = round(time.perf_counter() - tu, 4)
     cols = dict(up.columns)
-    _finish_strings(up.host_strings, cols, indexed, device, dist)
+    _finish_strings(up, cols, indexed, device, dist)
     return {n: cols[n] for n in names}, names, pa.schema(fields)
 
 
@@ -627,7 +691,7 @@ def device_rewrite_buckets(session, files: List[str], indexed: List[str], out_pa
                               device_pages=False)
     cols = dict(up.columns)
     bucket = cols.pop(bname).data.to(torch.int32)
-    _finish_strings(up.host_strings, cols, indexed, device, None)
+    _finish_strings(up, cols, indexed, device, None)
     n = up.num_rows
     if deleted_ids:
         # K5: lineage NOT IN deleted -> bitmap probe + stable compaction, fused in one scan kernel

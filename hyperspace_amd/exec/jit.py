@@ -88,6 +88,9 @@ MJ_STEPS = int(os.environ.get("HS_JIT_MJ_STEPS", "1"))   # branch-free walk step
 MJ_STAGE_UNROLL = int(os.environ.get("HS_JIT_MJ_STAGE_UNROLL", "4"))
 MJ_DBUF = os.environ.get("HS_JIT_MJ_DBUF", "0") == "1"
 MJ_PREFETCH = os.environ.get("HS_JIT_MJ_PREFETCH", "0") == "1"
+# workgroup size of the merge join: 64 = one wavefront per workgroup working its own 512-row
+# tiles (own right span, no block barriers), 256 = four wavefronts sharing 2048-row tiles
+MJ_BLOCK = int(os.environ.get("HS_JIT_MJ_BLOCK", "256"))
 MJ_KEY32 = os.environ.get("HS_JIT_MJ_KEY32", "1") == "1"  # 32-bit merge images (_key32_frame)
 # cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
 MJ_EXP = os.environ.get("HS_JIT_MJ_EXP", "")
@@ -1232,6 +1235,7 @@ def merge_join_shape(p: NL.JoinParams, compacts=None, hk=None) -> tuple:
     return ("merge_join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey,
             p.key_is_float, MJ_ITEMS, MJ_LDS_KEYS, MJ_STEPS, BLOCK, WAVE_SYNC,
             _key32_frame(p, compacts) is not None, MJ_EXP, MJ_STAGE_UNROLL, MJ_DBUF, MJ_PREFETCH,
+            MJ_BLOCK,
             hk.shape() if hk is not None else None)
 
 
@@ -1350,6 +1354,7 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
     tile) are searched in HBM.  Reference: the bucketed SortMergeJoin plans of JoinIndexRule
     (JoinIndexRule.scala:63-69), which re-match keys on every query."""
     NI = MJ_ITEMS  # noqa: N806
+    BLOCK = MJ_BLOCK  # noqa: N806 — 64: one wavefront per workgroup, no block barriers
     T = BLOCK * NI  # noqa: N806
     LK = MJ_LDS_KEYS  # noqa: N806
     args = Args()
@@ -1456,7 +1461,7 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
             b.append(f"{ind}{{ const bool kv = act{it} && {okl}; kvb |= kv ? {1 << it}u : 0u; "
                      f"mb |= (kv && {cond}) ? {1 << it}u : 0u; }}")
             b.append(f"{ind}const {KT} k{it} = {limg(it)};")
-        b.append(f"{ind}__syncthreads();")
+        b.append(f"{ind}{_block_sync(BLOCK)}")
 
         def bit(word: str, it: int) -> str:
             return f"(({word} >> {it}) & 1u)"
@@ -1547,7 +1552,7 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
         one_round(i2)
         b.append(f"{ind}}}")
         if NB == 1:   # single span buffer: the next tile's staging must wait for this tile
-            b.append(f"{ind}__syncthreads();")
+            b.append(f"{ind}{_block_sync(BLOCK)}")
 
     loads = _vec_loads(g1, first)
     if MJ_PREFETCH:
@@ -1568,12 +1573,17 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
     b += _deferred_drain(args, cols, split, approx, aggs, grouped, p.group_col, allslots, "  ",
                          final=True, hk=hk)
     if hk is None:
-        b += _flush(aggs, grouped)
+        b += _flush(aggs, grouped, BLOCK)
     src = (_PRELUDE + args.struct_src() +
            f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_merge_join_agg(Args a) {{\n' +
            "\n".join(b) + "\n}\n")
     lds = (len(aggs) * p.num_groups * 32) if grouped else 0
-    return Kernel(src, "hs_jit_merge_join_agg", args, lds)
+    return Kernel(src, "hs_jit_merge_join_agg", args, lds, BLOCK)
+
+
+def _block_sync(block: int) -> str:
+    """Workgroup barrier; a one-wavefront workgroup only needs its LDS accesses ordered."""
+    return _wave_sync(True) if block == 64 else "__syncthreads();"
 
 
 def merge_join_ok(p: NL.JoinParams, compacts=None, rnrows: int = 0, lnrows: int = 0) -> bool:
@@ -1597,13 +1607,13 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
     ``nrows`` = left table rows; ``rdup`` = the right key column may repeat a key
     (``key_has_dups``)."""
     NI = MJ_ITEMS  # noqa: N806
-    T = BLOCK * NI  # noqa: N806
+    T = MJ_BLOCK * NI  # noqa: N806
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
     dev = rstart.device
     max_tiles = nrows // T + 2 * rstart.numel() + 2
     tp, spans = _join_spans(p, rstart, rlen, rbucket, roff, max_tiles, T, cache_spans, align=NI)
     k = kernel_for(merge_join_shape(p, compacts, hk), lambda: gen_merge_join_agg(p, compacts, hk))
-    grid = MJ_GRID
+    grid = MJ_GRID * (256 // MJ_BLOCK)
     if hk is not None:
         v = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
              "spans": spans.data_ptr(), "R": rstart.numel(), "nrows": nrows, "rdup": int(rdup),

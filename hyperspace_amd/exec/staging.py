@@ -24,6 +24,7 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import pyarrow as pa
+import pyarrow.compute as pc
 
 from .device_table import DeviceColumn, is_string, storage_numpy_dtype
 
@@ -220,6 +221,11 @@ def device_decode_enabled() -> bool:
     return os.environ.get("HS_DEVICE_PARQUET", "1") == "1"
 
 
+def device_strings_enabled() -> bool:
+    """Dictionary-encoded string pages decode on the device (``HS_DEVICE_STRINGS=0``: pyarrow)."""
+    return os.environ.get("HS_DEVICE_STRINGS", "1") == "1"
+
+
 def _h2d_async(dst, src: np.ndarray, stream) -> None:
     """Copy ``src`` into device tensor slice ``dst`` via a pinned bounce buffer on ``stream``."""
     import torch
@@ -235,10 +241,70 @@ def _h2d_async(dst, src: np.ndarray, stream) -> None:
 
 
 class UploadResult:
-    def __init__(self, columns: Dict[str, DeviceColumn], num_rows: int, host_strings: dict):
+    def __init__(self, columns: Dict[str, DeviceColumn], num_rows: int, host_strings: dict,
+                 device_strings: Optional[dict] = None, offsets: Optional[np.ndarray] = None):
         self.columns = columns
         self.num_rows = num_rows
-        self.host_strings = host_strings  # name -> list of per-file arrow chunks (in file order)
+        # name -> list of per-file arrow chunks (file order; None where the device decoded the
+        # file's pages): only string columns some file had to decode on the host
+        self.host_strings = host_strings
+        # name -> io.native_parquet.StringCodes: string columns whose codes the device wrote
+        self.device_strings = device_strings or {}
+        self.offsets = offsets              # first row of every file (+ total)
+
+
+def finish_strings(up: "UploadResult", cols: Dict[str, DeviceColumn], device, dist,
+                   raw: Sequence[str] = (), names: Optional[Sequence[str]] = None) -> None:
+    """Turn every string column of an upload into int32 codes over one job-global sorted
+    dictionary (``parallel/dictionary.union_sorted``; ``dist`` None: this process only).
+
+    Device-decoded columns (``up.device_strings``) hold upload-local codes: the dictionary is
+    the union of the parsed dictionary pages plus the values of host-decoded files, and the
+    codes are remapped with one gather on the device; host-decoded files' codes are computed
+    on the host and copied into their row ranges.  Columns named in ``raw`` also keep their
+    bytes (offsets/chars) when they were host-decoded."""
+    import torch
+    from ..ops import kernels as K
+    from ..parallel.dictionary import union_sorted
+    if names is None:
+        names = list(dict.fromkeys(list(up.device_strings) + list(up.host_strings)))
+    for name in names:
+        sc = up.device_strings.get(name)
+        chunks = up.host_strings.get(name) or []
+        if sc is None:
+            chunks = [c for c in chunks if c is not None]
+            arr = pa.chunked_array(chunks, type=chunks[0].type) if chunks else \
+                pa.chunked_array([], pa.string())
+            if pa.types.is_dictionary(arr.type):
+                arr = arr.cast(arr.type.value_type)
+            arr = arr.combine_chunks() if arr.num_chunks != 1 else arr.chunk(0)
+            d = union_sorted(arr, dist)
+            cols[name] = DeviceColumn.from_arrow(arr, device, d, raw_strings=name in raw)
+            continue
+        dc = cols[name]
+        local = sc.concat()
+        host = {i: (c.cast(c.type.value_type) if pa.types.is_dictionary(c.type) else c)
+                for i, c in enumerate(chunks) if c is not None}
+        host = {i: (c.combine_chunks() if isinstance(c, pa.ChunkedArray) else c)
+                for i, c in host.items()}
+        vals = [local] + [c.cast(pa.string()) for c in host.values()]
+        gd = union_sorted(pa.concat_arrays(vals) if vals else local, dist)
+        if len(local):
+            remap = pc.index_in(local.cast(pa.string()), value_set=gd)
+            tab = torch.from_numpy(np.asarray(remap.to_numpy(zero_copy_only=False),
+                                              dtype=np.int32)).to(device)
+            dc.data = K.lookup_i32(tab, dc.data)
+        for i, c in host.items():
+            lo, hi = int(up.offsets[i]), int(up.offsets[i + 1])
+            codes = pc.index_in(c.cast(pa.string()), value_set=gd).fill_null(0)
+            dc.data[lo:hi].copy_(torch.from_numpy(
+                np.asarray(codes.to_numpy(zero_copy_only=False), dtype=np.int32)).to(device))
+            if c.null_count:
+                if dc.valid is None:
+                    dc.valid = torch.ones(up.num_rows, dtype=torch.uint8, device=device)
+                dc.valid[lo:hi].copy_(torch.from_numpy(np.asarray(
+                    c.is_valid().to_numpy(zero_copy_only=False), dtype=np.uint8)).to(device))
+        cols[name] = DeviceColumn(dc.data, dc.valid, pa.string(), gd)
 
 
 def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
@@ -277,9 +343,18 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
     streams = copy_streams(device)
     cols: Dict[str, DeviceColumn] = {}
     strings: Dict[str, list] = {}
+    native = parquet_local is not None and native_decode_enabled()
+    use_device_pages = device_decode_enabled() if device_pages is None else device_pages
+    dev_strings: Dict[str, object] = {}
     for f in schema:
         if is_string(f.type):
             strings[f.name] = [None] * len(files)
+            if native and use_device_pages and device_strings_enabled():
+                from ..io.native_parquet import StringCodes
+                dev_strings[f.name] = StringCodes()
+                # zeroed: rows of host-decoded files are remapped along with the device ones
+                cols[f.name] = DeviceColumn(torch.zeros(n, dtype=torch.int32, device=device),
+                                            None, pa.string())
             continue
         nd = storage_numpy_dtype(f.type)
         cols[f.name] = DeviceColumn(torch.empty(n, dtype=_torch_dtype(nd), device=device), None,
@@ -296,8 +371,6 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
         st.wait_stream(main)  # allocations above happen-before the copies
 
     t_alloc = _t.perf_counter()
-    native = parquet_local is not None and native_decode_enabled()
-    use_device_pages = device_decode_enabled() if device_pages is None else device_pages
     status = None
     if native:
         _warm_decode_kernels()
@@ -313,9 +386,9 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
             flds = [f for f in schema if f.name in cols]
             if use_device_pages:
                 done = native_parquet.upload_file_device(parquet_local[i], flds, cols, lo,
-                                                         stream, device, status)
+                                                         stream, device, status, dev_strings)
                 DEVICE_DECODED.update(done)
-            rest_native = [f for f in flds if f.name not in done]
+            rest_native = [f for f in flds if f.name not in done and f.name not in strings]
             if rest_native:
                 done = done | native_parquet.upload_file(parquet_local[i], rest_native, cols, lo,
                                                          n, stream, device, lock)
@@ -374,7 +447,9 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
         if code:
             raise IOError(f"device Parquet decode failed (status {code}: 1 corrupt page, "
                           f"2 dictionary index out of range) in {len(files)} files")
-    return UploadResult(cols, n, strings)
+    host_strings = {k: v for k, v in strings.items()
+                    if k not in dev_strings or any(c is not None for c in v)}
+    return UploadResult(cols, n, host_strings, dev_strings, offs)
 
 
 def download_buckets(columns: List[DeviceColumn], names: List[str], schema: pa.Schema,

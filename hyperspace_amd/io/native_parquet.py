@@ -51,6 +51,8 @@ class ChunkInfo(C.Structure):
 
 # arrow type -> (Parquet physical type, element bytes) decodable as raw bits into our storage
 def _native_kind(t: pa.DataType):
+    if pa.types.is_string(t) or pa.types.is_large_string(t):
+        return 6, 4                     # BYTE_ARRAY -> int32 dictionary codes (device path only)
     if pa.types.is_int32(t) or pa.types.is_date32(t):
         return 1, 4
     if pa.types.is_int64(t):
@@ -95,6 +97,7 @@ def lib():
                         ("hs_pq_chunk_host_bound", I64, [P, I, I]),
                         ("hs_pq_page_size", I, []),
                         ("hs_pq_snappy_decompress", I64, [P, I64, P, I64]),
+                        ("hs_pq_plain_strings", I64, [P, I64, I64, P, P, I64]),
                         ("hs_pq_set_host_inflate", None, [I])):
                     fn = getattr(L, name)
                     fn.restype = res
@@ -223,7 +226,7 @@ def upload_file(path: str, fields: Sequence[pa.Field], cols: Dict[str, object], 
         plan = []
         for fld in fields:
             kind = _native_kind(fld.type)
-            if kind is None:
+            if kind is None or kind[0] == 6:
                 continue
             c = f.column(fld.name)
             if c < 0:
@@ -384,14 +387,59 @@ def plan_file(f: "PqFile", plan, raw_cap: int, raw_buf_ptr: int, host_cap: int =
     return pages[:npg], chunks, raw_at, dst_at, h_at, skipped
 
 
+class StringCodes:
+    """One string column decoded on the device across the files of an upload.
+
+    Every row-group chunk's dictionary page is parsed on the host (``hs_pq_plain_strings``) and
+    given a range of codes ``[base, base + len)`` in one upload-wide code space (``add``, any
+    thread); the data pages decode on the device to those codes.  ``concat`` is the dictionary
+    of that code space; the caller maps it onto the job-global sorted dictionary with one device
+    gather (``staging.finish_strings``).  ``host`` holds the arrow chunks of files whose pages the
+    device path could not take (PLAIN pages, nulls), by file index."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self.size = 0
+        self.parts: List[tuple] = []
+        self.host: Dict[int, object] = {}
+
+    def add(self, arr: pa.Array) -> int:
+        with self._lock:
+            base = self.size
+            self.size += len(arr)
+            self.parts.append((base, arr))
+            return base
+
+    def concat(self) -> pa.Array:
+        parts = [a for _, a in sorted(self.parts, key=lambda x: x[0])]
+        return pa.concat_arrays(parts) if parts else pa.array([], pa.string())
+
+
+def plain_strings(buf_ptr: int, nbytes: int, n: int) -> pa.Array:
+    """Arrow string array of a PLAIN BYTE_ARRAY stream of ``n`` values at host ``buf_ptr``."""
+    offs = np.empty(n + 1, dtype=np.int32)
+    chars = np.empty(max(nbytes, 1), dtype=np.uint8)
+    got = lib().hs_pq_plain_strings(buf_ptr, nbytes, n, offs.ctypes.data, chars.ctypes.data,
+                                    len(chars))
+    if got < 0:
+        raise IOError("corrupt BYTE_ARRAY dictionary page")
+    return pa.Array.from_buffers(pa.string(), n, [None, pa.py_buffer(offs),
+                                                  pa.py_buffer(chars[:max(got, 1)])])
+
+
 def upload_file_device(path: str, fields: Sequence[pa.Field], cols: Dict[str, object], lo: int,
-                       stream, device, status) -> Set[str]:
+                       stream, device, status, strings: Optional[Dict[str, StringCodes]] = None
+                       ) -> Set[str]:
     """Decode the natively supported, null-free ``fields`` of ``path`` entirely on the GPU into
     ``cols[name].data[lo:...]``: the host preads the raw column chunks into pinned memory and
     lists their pages; one H2D copy moves the compressed bytes and the page table, and two
     launches (``hs_pq_decode_pages``: Snappy inflate, then RLE / bit-packed / PLAIN expansion
     with the dictionary gather) write the values.  Errors accumulate in the device int
-    ``status`` (checked once per build).  Returns the names decoded."""
+    ``status`` (checked once per build).  Returns the names decoded.
+
+    String columns named in ``strings`` decode when every chunk is dictionary-encoded and
+    null-free: the host parses only the (small) dictionary pages, the device expands the index
+    pages through a per-chunk code table (``StringCodes``) into ``cols[name].data`` (int32)."""
     import time
     import torch
     from ..ops import _lib as NL
@@ -408,10 +456,14 @@ def upload_file_device(path: str, fields: Sequence[pa.Field], cols: Dict[str, ob
             kind = _native_kind(fld.type)
             if kind is None:
                 continue
+            if kind[0] == 6 and (strings is None or fld.name not in strings):
+                continue
             c = f.column(fld.name)
             if c < 0:
                 continue
             ptype, _, eb = f.column_info(c)
+            if kind[0] == 6 and ptype == 6:
+                eb = 4
             if eb == 0 or ptype != kind[0]:
                 continue
             plan.append((fld, c, eb))
@@ -455,6 +507,18 @@ def upload_file_device(path: str, fields: Sequence[pa.Field], cols: Dict[str, ob
                                     sbase + pages["dst"])
             dp = pages["dict_page"]
             pages["dict"] = np.where(dp >= 0, pages["dst"][np.maximum(dp, 0)], 0)
+            tabs = _string_code_tables(chunks, pages, pinned.data_ptr() + raw_cap, strings)
+            if tabs is not None:
+                tab_host, fix = tabs
+                tpin = pool.acquire(tab_host.nbytes)
+                tpin.numpy()[:tab_host.nbytes] = tab_host.view(np.uint8)
+                dtab = torch.empty(tab_host.nbytes, dtype=torch.uint8, device=device)
+                dtab.copy_(tpin[:tab_host.nbytes], non_blocking=True)
+                pool.release(tpin, stream)
+                dtab.record_stream(stream)
+                for p0, np_, toff in fix:
+                    seg = pages[p0:p0 + np_]
+                    seg["dict"] = np.where(seg["kind"] != 2, dtab.data_ptr() + 4 * toff, 0)
             ppin = pool.acquire(pages.nbytes)
             ppin.numpy()[:pages.nbytes] = pages.view(np.uint8)
             dpages = torch.empty(pages.nbytes, dtype=torch.uint8, device=device)
@@ -471,6 +535,33 @@ def upload_file_device(path: str, fields: Sequence[pa.Field], cols: Dict[str, ob
         return {fld.name for fld, _, _, _ in chunks}
     finally:
         f.close()
+
+
+def _string_code_tables(chunks, pages, host_base: int, strings):
+    """For the string chunks of a file plan: parse each dictionary page (inflated on the host by
+    the planner, at ``host_base + src``), register it with the column's ``StringCodes`` and lay
+    out the chunk's code table ``[base, base + len)``.  Returns (int32 tables, [(first page,
+    pages, table offset)]) or None when the plan has no string chunk."""
+    if not strings:
+        return None
+    tabs, fix, at = [], [], 0
+    for fld, g, p0, np_ in chunks:
+        sc = strings.get(fld.name)
+        if sc is None:
+            continue
+        seg = pages[p0:p0 + np_]
+        dpg = np.nonzero(seg["kind"] == 2)[0]
+        if len(dpg) != 1 or seg["codec"][dpg[0]] != 2:
+            raise IOError(f"string chunk of {fld.name} without a host-parsed dictionary page")
+        d = seg[dpg[0]]
+        arr = plain_strings(host_base + int(d["src"]), int(d["usize"]), int(d["nvals"]))
+        base = sc.add(arr)
+        tabs.append(np.arange(base, base + len(arr), dtype=np.int32))
+        fix.append((p0, np_, at))
+        at += len(arr)
+    if not fix:
+        return None
+    return (np.concatenate(tabs) if at else np.zeros(1, np.int32)), fix
 
 
 def decode_plan_host(raw: np.ndarray, pages: np.ndarray, outputs: Dict[int, np.ndarray],

@@ -6,6 +6,7 @@ from __future__ import annotations
 
 import numpy as np
 import pyarrow as pa
+import pyarrow.compute as pc
 import pyarrow.parquet as pq
 import pytest
 
@@ -263,7 +264,62 @@ def test_native_parquet_gpu_decode_matches_pyarrow(tmp_path, device):
             assert col.valid is not None
             np.testing.assert_array_equal(col.valid.cpu().numpy().astype(bool), valid)
         np.testing.assert_array_equal(vals[valid], ref.drop_null().to_numpy())
-    assert "s" in up.host_strings  # strings still come back through pyarrow
+    # strings: the dictionary-encoded files decode on the device (codes through the parsed
+    # dictionary pages), the PLAIN-encoded file 1 through pyarrow; one global dictionary
+    assert "s" in staging.DEVICE_DECODED
+    assert [c is not None for c in up.host_strings["s"]] == [False, True, False]
+    cols = dict(up.columns)
+    staging.finish_strings(up, cols, device, None)
+    got = cols["s"].dictionary.take(pa.array(cols["s"].data.cpu().numpy()))
+    assert got.equals(full.column("s").combine_chunks())
+    assert cols["s"].dictionary.equals(pc.unique(full.column("s").combine_chunks()).sort())
+
+
+@pytest.mark.gpu
+def test_device_string_decode_matches_pyarrow(tmp_path, device):
+    """Dictionary-encoded BYTE_ARRAY chunks decode on the device to codes over one global
+    sorted dictionary: v1 and v2 pages, Snappy and uncompressed, many row groups with different
+    dictionaries, a large dictionary, empty strings and multi-byte UTF-8; a file with nulls and
+    one without a dictionary fall back to pyarrow for that file only."""
+    import torch
+    from hyperspace_amd.exec import staging
+    rng = np.random.default_rng(21)
+    words = np.array(["", "a", "zz", "été", "日本", "x" * 300] +
+                     [f"w{i:05d}" for i in range(20_000)], dtype=object)
+    files, tables = [], []
+    specs = [("snappy", True, "1.0", 6), ("none", True, "2.0", 20_006), ("snappy", True, "2.0", 40),
+             ("snappy", False, "1.0", 50), ("snappy", True, "1.0", 9)]
+    for i, (comp, dic, ver, card) in enumerate(specs):
+        n = 25_000 + 1000 * i
+        vals = words[rng.integers(0, card, n)]
+        mask = (rng.random(n) < 0.05) if i == 4 else None
+        t = pa.table({"s": pa.array(list(vals), pa.string(), mask=mask),
+                      "k": pa.array(rng.integers(0, 1 << 40, n))})
+        path = tmp_path / f"s{i}.parquet"
+        pq.write_table(t, path, compression=comp, use_dictionary=dic, data_page_version=ver,
+                       row_group_size=7_000, data_page_size=4096)
+        files.append(str(path))
+        tables.append(t)
+    full = pa.concat_tables(tables)
+
+    def read_file(p, cols=None):
+        return pq.read_table(p, columns=cols)
+    staging.DEVICE_DECODED.clear()
+    up = staging.upload_files(read_file, files, [t.num_rows for t in tables], full.schema,
+                              device, parquet_local=files)
+    torch.cuda.synchronize()
+    assert "s" in staging.DEVICE_DECODED
+    assert [c is not None for c in up.host_strings["s"]] == [False, False, False, True, True]
+    cols = dict(up.columns)
+    staging.finish_strings(up, cols, device, None)
+    c = cols["s"]
+    ref = full.column("s").combine_chunks()
+    assert c.dictionary.equals(pc.unique(ref.drop_null()).sort())
+    valid = np.asarray(ref.is_valid())
+    assert c.valid is not None
+    np.testing.assert_array_equal(c.valid.cpu().numpy().astype(bool), valid)
+    got = c.dictionary.take(pa.array(c.data.cpu().numpy()))
+    assert got.filter(pa.array(valid)).equals(ref.drop_null())
 
 
 @pytest.mark.gpu

@@ -45,7 +45,10 @@ def test_streaming_build_is_byte_identical(tmp_path, device):
                       "d": pa.array(rng.integers(8000, 11000, n).astype(np.int32)),
                       "p": pa.array(np.round(rng.random(n) * 1e4, 2)),
                       "q": pa.array(np.where(rng.random(n) < 0.1, None,
-                                             rng.integers(0, 50, n)).tolist(), pa.int64())})
+                                             rng.integers(0, 50, n)).tolist(), pa.int64()),
+                      # strings: per-file dictionaries differ; file 3 has nulls (host decode)
+                      "s": pa.array([f"s{x}" if i != 3 or x % 9 else None
+                                     for x in rng.integers(0, 40 + 10 * i, n)], pa.string())})
         pq.write_table(t, src / f"part-{i}.parquet", row_group_size=16_000)
 
     def build(name, budget):
@@ -54,7 +57,7 @@ def test_streaming_build_is_byte_identical(tmp_path, device):
                           "spark.hyperspace.mi.execution.device": "gpu",
                           "spark.hyperspace.mi.build.hbmBudgetBytes": str(budget)},
                     warehouse_dir=str(tmp_path / "wh"))
-        Hyperspace(s).createIndex(s.read.parquet(str(src)), IndexConfig(name, ["k"], ["d", "p", "q"]))
+        Hyperspace(s).createIndex(s.read.parquet(str(src)), IndexConfig(name, ["k"], ["d", "p", "q", "s"]))
         stats = dict(device_build.LAST_BUILD_STATS)
         files = {}
         for root, _, fs in os.walk(tmp_path / "ix" / name):

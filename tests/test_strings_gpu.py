@@ -67,7 +67,11 @@ def test_hybrid_scan_join_on_string_key_native(strs):
         s.conf.set(f"spark.hyperspace.index.{k}", v)
     hs = Hyperspace(s)
     fact, dim = s.read.parquet(fpath), s.read.parquet(dpath)
+    from hyperspace_amd.exec import device_build
     hs.createIndex(fact, IndexConfig("f_c3", ["c3"], ["v", "q"]))
+    # the string key's dictionary-encoded pages decoded on the device, not through pyarrow
+    assert "c3" in device_build.LAST_BUILD_STATS["device_decoded"]
+    assert device_build.LAST_BUILD_STATS["host_decoded"] == []
     hs.createIndex(dim, IndexConfig("d_c3", ["c3"], ["w"]))
     # appended files: new keys (not in either index dictionary) and existing ones
     newk = np.array([f"new-{i}" for i in range(300)])
