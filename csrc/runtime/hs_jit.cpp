@@ -30,7 +30,7 @@ struct Entry {
 
 std::mutex g_mu;
 std::unordered_map<std::string, Entry> g_fns;  // key: hash + kernel name
-std::string g_last_error;
+thread_local std::string g_last_error;
 
 uint64_t fnv1a(const std::string& s) {
   uint64_t h = 1469598103934665603ull;
@@ -130,12 +130,16 @@ void* hs_jit_get(const char* src, const char* kernel, const char* arch, const ch
   const std::string s(src);
   const std::string key = hex(fnv1a(s + "|" + arch));
   const std::string mkey = key + ":" + kernel;
-  std::lock_guard<std::mutex> lock(g_mu);
-  auto it = g_fns.find(mkey);
-  if (it != g_fns.end()) {
-    if (compiled) *compiled = 0;
-    return (void*)it->second.fn;
+  {
+    std::lock_guard<std::mutex> lock(g_mu);
+    auto it = g_fns.find(mkey);
+    if (it != g_fns.end()) {
+      if (compiled) *compiled = 0;
+      return (void*)it->second.fn;
+    }
   }
+  // compile / read outside the lock: kernels of one query plan compile concurrently
+  // (hs_jit_prepare from a thread pool); a racing duplicate compile is harmless
   std::vector<char> code;
   const std::string path = cache_dir && *cache_dir ? std::string(cache_dir) + "/" + key + ".co"
                                                    : std::string();
@@ -146,6 +150,12 @@ void* hs_jit_get(const char* src, const char* kernel, const char* arch, const ch
       mkdir(cache_dir, 0755);
       write_file_atomic(path, code);
     }
+  }
+  std::lock_guard<std::mutex> lock(g_mu);
+  auto it = g_fns.find(mkey);
+  if (it != g_fns.end()) {
+    if (compiled) *compiled = 0;
+    return (void*)it->second.fn;
   }
   Entry e;
   hipError_t err = hipModuleLoadData(&e.module, code.data());

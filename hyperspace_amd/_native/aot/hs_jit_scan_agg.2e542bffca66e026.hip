@@ -1,0 +1,436 @@
+
+typedef long long i64;
+typedef unsigned long long u64;
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ i64 wsumi(i64 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wmin(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wmax(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ bool in_set(const i64* s, int n, i64 x) {
+  int lo = 0, hi = n;
+  while (lo < hi) { const int m = (lo + hi) >> 1; if (s[m] < x) lo = m + 1; else hi = m; }
+  return lo < n && s[lo] == x;
+}
+__device__ __forceinline__ bool bit_test(const u64* w, i64 nbits, i64 x) {
+  return x >= 0 && x < nbits && ((w[x >> 6] >> (x & 63)) & 1ull);
+}
+// V consecutive elements starting at an index that is a multiple of V (so the address is
+// aligned to V * sizeof(T) for a 16-byte aligned base): one dwordx4 per 16 bytes
+template <typename T, int V>
+__device__ __forceinline__ void vload(const T* __restrict__ p, long long i, T (&x)[V]) {
+  constexpr int B = (int)sizeof(T) * V;
+  if constexpr (B % 16 == 0) {
+    const uint4* q = reinterpret_cast<const uint4*>(p + i);
+#pragma unroll
+    for (int k = 0; k < B / 16; ++k) reinterpret_cast<uint4*>(x)[k] = q[k];
+  } else if constexpr (B == 8) {
+    *reinterpret_cast<uint2*>(x) = *reinterpret_cast<const uint2*>(p + i);
+  } else if constexpr (B == 4) {
+    *reinterpret_cast<unsigned*>(x) = *reinterpret_cast<const unsigned*>(p + i);
+  } else {
+#pragma unroll
+    for (int k = 0; k < V; ++k) x[k] = p[i + k];
+  }
+}
+__device__ __forceinline__ void lds_min(double* p, double v) {
+  u64* a = (u64*)p; u64 old = *a, as;
+  do { as = old; if (__longlong_as_double((i64)as) <= v) break;
+       old = atomicCAS(a, as, (u64)__double_as_longlong(v)); } while (as != old);
+}
+__device__ __forceinline__ void lds_max(double* p, double v) {
+  u64* a = (u64*)p; u64 old = *a, as;
+  do { as = old; if (__longlong_as_double((i64)as) >= v) break;
+       old = atomicCAS(a, as, (u64)__double_as_longlong(v)); } while (as != old);
+}
+// hash-mode grouping (exec/hash_agg.py, csrc/kernels/hash_agg.hip): probe hash and the bit
+// images of float group keys (-0.0 -> 0.0, one NaN)
+__device__ __forceinline__ u64 hs_mix64(u64 h) {
+  h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull;
+  return h ^ (h >> 33);
+}
+__device__ __forceinline__ u64 hs_f64key(double d) {
+  d = d == 0.0 ? 0.0 : d;
+  return d != d ? 0x7ff8000000000000ull : (u64)__double_as_longlong(d);
+}
+__device__ __forceinline__ u64 hs_f32key(float f) {
+  f = f == 0.0f ? 0.0f : f;
+  return f != f ? 0x7fc00000ull : (u64)(unsigned)__float_as_uint(f);
+}
+struct Args {
+  const long long* rstart;
+  const long long* rlen;
+  const long long* tile_prefix;
+  long long R;
+  double* psum;
+  double* pmin;
+  double* pmax;
+  long long* pcnt;
+  long long nrows;
+  const signed char* c0;
+  const signed char* c1;
+  long long B0;
+  double R0;
+  long long B1;
+  double Q1;
+  long long CL2;
+  long long CH2;
+  long long CL3;
+  long long CH3;
+  long long CL4;
+  long long CH4;
+  const int* c2;
+  long long B2;
+  double R2;
+  double A0_0;
+  double B0_0;
+  double A0_1;
+  double B0_1;
+};
+extern "C" __global__ __launch_bounds__(256) void hs_jit_scan_agg(const Args* __restrict__ ap) {
+  const Args a = *ap;
+  typedef unsigned short crow_t; __shared__ crow_t crow_s[4][512];
+  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  constexpr int NA = 2;
+  double acc0 = 0.0; unsigned cnt0 = 0u;
+  double acc1 = 0.0; unsigned cnt1 = 0u;
+  const i64 ntiles = a.tile_prefix[a.R];
+  const i64 per = (ntiles + gridDim.x - 1) / gridDim.x;
+  const i64 t0 = (i64)blockIdx.x * per;
+  const i64 t1 = ntiles < t0 + per ? ntiles : t0 + per;
+  int r = 0;
+  if (t0 < t1) { int lo = 0, hi = (int)a.R;
+    while (hi - lo > 1) { const int m = (lo + hi) >> 1; if (a.tile_prefix[m] <= t0) lo = m; else hi = m; }
+    r = lo; }
+  i64 rsP = 0, reP = 0, tb0P = 0, g0P = 0; bool fullP = false;
+  signed char x0vP[8];
+  signed char x1vP[8];
+  i64 t = t0;
+  if (t < t1) {
+    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;
+    { const i64 off_ = (t - a.tile_prefix[r]) * 2048;
+      rsP = a.rstart[r]; reP = rsP + a.rlen[r];
+      tb0P = (rsP & ~(i64)7) + off_;
+      g0P = tb0P + (i64)threadIdx.x * 8; }
+    fullP = tb0P + 2048 <= a.nrows;
+    if (fullP) {
+      vload<signed char, 8>(a.c0, g0P, x0vP);
+      vload<signed char, 8>(a.c1, g0P, x1vP);
+    }
+  }
+  for (; t < t1 && fullP; ++t) {
+    const i64 rs = rsP, re = reP, tb0 = tb0P, g0 = g0P;
+    signed char x0v[8]; x0v[0] = x0vP[0]; x0v[1] = x0vP[1]; x0v[2] = x0vP[2]; x0v[3] = x0vP[3]; x0v[4] = x0vP[4]; x0v[5] = x0vP[5]; x0v[6] = x0vP[6]; x0v[7] = x0vP[7];
+    signed char x1v[8]; x1v[0] = x1vP[0]; x1v[1] = x1vP[1]; x1v[2] = x1vP[2]; x1v[3] = x1vP[3]; x1v[4] = x1vP[4]; x1v[5] = x1vP[5]; x1v[6] = x1vP[6]; x1v[7] = x1vP[7];
+    if (t + 1 < t1) {
+      while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= (t + 1)) ++r;
+      { const i64 off_ = ((t + 1) - a.tile_prefix[r]) * 2048;
+        rsP = a.rstart[r]; reP = rsP + a.rlen[r];
+        tb0P = (rsP & ~(i64)7) + off_;
+        g0P = tb0P + (i64)threadIdx.x * 8; }
+      fullP = tb0P + 2048 <= a.nrows;
+      if (fullP) {
+        vload<signed char, 8>(a.c0, g0P, x0vP);
+        vload<signed char, 8>(a.c1, g0P, x1vP);
+      }
+    } else fullP = false;
+    const i64 dlo_ = rs - g0, dhi_ = re - g0;
+    const int alo = dlo_ <= 0 ? 0 : (dlo_ >= 8 ? 8 : (int)dlo_);
+    const int ahi = dhi_ <= 0 ? 0 : (dhi_ >= 8 ? 8 : (int)dhi_);
+    const bool act0 = 0 >= alo && 0 < ahi;
+    const i64 row0 = g0 + 0;
+    const bool act1 = 1 >= alo && 1 < ahi;
+    const i64 row1 = g0 + 1;
+    const bool act2 = 2 >= alo && 2 < ahi;
+    const i64 row2 = g0 + 2;
+    const bool act3 = 3 >= alo && 3 < ahi;
+    const i64 row3 = g0 + 3;
+    const bool act4 = 4 >= alo && 4 < ahi;
+    const i64 row4 = g0 + 4;
+    const bool act5 = 5 >= alo && 5 < ahi;
+    const i64 row5 = g0 + 5;
+    const bool act6 = 6 >= alo && 6 < ahi;
+    const i64 row6 = g0 + 6;
+    const bool act7 = 7 >= alo && 7 < ahi;
+    const i64 row7 = g0 + 7;
+    const int r0_0 = (int)x0v[0];
+    const i64 q0_0 = a.B0 + (i64)x0v[0];
+    const double x0_0 = (double)((double)(a.B0 + (i64)x0v[0]) * a.R0);
+    const int r1_0 = (int)x1v[0];
+    const i64 q1_0 = a.B1 + (i64)x1v[0];
+    const double x1_0 = (double)((double)(a.B1 + (i64)x1v[0]) / a.Q1);
+    const int r0_1 = (int)x0v[1];
+    const i64 q0_1 = a.B0 + (i64)x0v[1];
+    const double x0_1 = (double)((double)(a.B0 + (i64)x0v[1]) * a.R0);
+    const int r1_1 = (int)x1v[1];
+    const i64 q1_1 = a.B1 + (i64)x1v[1];
+    const double x1_1 = (double)((double)(a.B1 + (i64)x1v[1]) / a.Q1);
+    const int r0_2 = (int)x0v[2];
+    const i64 q0_2 = a.B0 + (i64)x0v[2];
+    const double x0_2 = (double)((double)(a.B0 + (i64)x0v[2]) * a.R0);
+    const int r1_2 = (int)x1v[2];
+    const i64 q1_2 = a.B1 + (i64)x1v[2];
+    const double x1_2 = (double)((double)(a.B1 + (i64)x1v[2]) / a.Q1);
+    const int r0_3 = (int)x0v[3];
+    const i64 q0_3 = a.B0 + (i64)x0v[3];
+    const double x0_3 = (double)((double)(a.B0 + (i64)x0v[3]) * a.R0);
+    const int r1_3 = (int)x1v[3];
+    const i64 q1_3 = a.B1 + (i64)x1v[3];
+    const double x1_3 = (double)((double)(a.B1 + (i64)x1v[3]) / a.Q1);
+    const int r0_4 = (int)x0v[4];
+    const i64 q0_4 = a.B0 + (i64)x0v[4];
+    const double x0_4 = (double)((double)(a.B0 + (i64)x0v[4]) * a.R0);
+    const int r1_4 = (int)x1v[4];
+    const i64 q1_4 = a.B1 + (i64)x1v[4];
+    const double x1_4 = (double)((double)(a.B1 + (i64)x1v[4]) / a.Q1);
+    const int r0_5 = (int)x0v[5];
+    const i64 q0_5 = a.B0 + (i64)x0v[5];
+    const double x0_5 = (double)((double)(a.B0 + (i64)x0v[5]) * a.R0);
+    const int r1_5 = (int)x1v[5];
+    const i64 q1_5 = a.B1 + (i64)x1v[5];
+    const double x1_5 = (double)((double)(a.B1 + (i64)x1v[5]) / a.Q1);
+    const int r0_6 = (int)x0v[6];
+    const i64 q0_6 = a.B0 + (i64)x0v[6];
+    const double x0_6 = (double)((double)(a.B0 + (i64)x0v[6]) * a.R0);
+    const int r1_6 = (int)x1v[6];
+    const i64 q1_6 = a.B1 + (i64)x1v[6];
+    const double x1_6 = (double)((double)(a.B1 + (i64)x1v[6]) / a.Q1);
+    const int r0_7 = (int)x0v[7];
+    const i64 q0_7 = a.B0 + (i64)x0v[7];
+    const double x0_7 = (double)((double)(a.B0 + (i64)x0v[7]) * a.R0);
+    const int r1_7 = (int)x1v[7];
+    const i64 q1_7 = a.B1 + (i64)x1v[7];
+    const double x1_7 = (double)((double)(a.B1 + (i64)x1v[7]) / a.Q1);
+    bool pass0 = act0 && ((true)) && ((true)) && ((true && (r0_0 >= (int)a.CL2 && r0_0 <= (int)a.CH2))) && ((true && (r0_0 >= (int)a.CL3 && r0_0 <= (int)a.CH3))) && ((true && (r1_0 >= (int)a.CL4 && r1_0 <= (int)a.CH4)));
+    bool pass1 = act1 && ((true)) && ((true)) && ((true && (r0_1 >= (int)a.CL2 && r0_1 <= (int)a.CH2))) && ((true && (r0_1 >= (int)a.CL3 && r0_1 <= (int)a.CH3))) && ((true && (r1_1 >= (int)a.CL4 && r1_1 <= (int)a.CH4)));
+    bool pass2 = act2 && ((true)) && ((true)) && ((true && (r0_2 >= (int)a.CL2 && r0_2 <= (int)a.CH2))) && ((true && (r0_2 >= (int)a.CL3 && r0_2 <= (int)a.CH3))) && ((true && (r1_2 >= (int)a.CL4 && r1_2 <= (int)a.CH4)));
+    bool pass3 = act3 && ((true)) && ((true)) && ((true && (r0_3 >= (int)a.CL2 && r0_3 <= (int)a.CH2))) && ((true && (r0_3 >= (int)a.CL3 && r0_3 <= (int)a.CH3))) && ((true && (r1_3 >= (int)a.CL4 && r1_3 <= (int)a.CH4)));
+    bool pass4 = act4 && ((true)) && ((true)) && ((true && (r0_4 >= (int)a.CL2 && r0_4 <= (int)a.CH2))) && ((true && (r0_4 >= (int)a.CL3 && r0_4 <= (int)a.CH3))) && ((true && (r1_4 >= (int)a.CL4 && r1_4 <= (int)a.CH4)));
+    bool pass5 = act5 && ((true)) && ((true)) && ((true && (r0_5 >= (int)a.CL2 && r0_5 <= (int)a.CH2))) && ((true && (r0_5 >= (int)a.CL3 && r0_5 <= (int)a.CH3))) && ((true && (r1_5 >= (int)a.CL4 && r1_5 <= (int)a.CH4)));
+    bool pass6 = act6 && ((true)) && ((true)) && ((true && (r0_6 >= (int)a.CL2 && r0_6 <= (int)a.CH2))) && ((true && (r0_6 >= (int)a.CL3 && r0_6 <= (int)a.CH3))) && ((true && (r1_6 >= (int)a.CL4 && r1_6 <= (int)a.CH4)));
+    bool pass7 = act7 && ((true)) && ((true)) && ((true && (r0_7 >= (int)a.CL2 && r0_7 <= (int)a.CH2))) && ((true && (r0_7 >= (int)a.CL3 && r0_7 <= (int)a.CH3))) && ((true && (r1_7 >= (int)a.CL4 && r1_7 <= (int)a.CH4)));
+    int wtot = 0;
+    { const bool pz = pass0; const u64 bm = __ballot(pz);
+      const int pos0 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos0] = (crow_t)(row0 - tb0); }
+      wtot += __popcll(bm); }
+    { const bool pz = pass1; const u64 bm = __ballot(pz);
+      const int pos1 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos1] = (crow_t)(row1 - tb0); }
+      wtot += __popcll(bm); }
+    { const bool pz = pass2; const u64 bm = __ballot(pz);
+      const int pos2 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos2] = (crow_t)(row2 - tb0); }
+      wtot += __popcll(bm); }
+    { const bool pz = pass3; const u64 bm = __ballot(pz);
+      const int pos3 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos3] = (crow_t)(row3 - tb0); }
+      wtot += __popcll(bm); }
+    { const bool pz = pass4; const u64 bm = __ballot(pz);
+      const int pos4 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos4] = (crow_t)(row4 - tb0); }
+      wtot += __popcll(bm); }
+    { const bool pz = pass5; const u64 bm = __ballot(pz);
+      const int pos5 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos5] = (crow_t)(row5 - tb0); }
+      wtot += __popcll(bm); }
+    { const bool pz = pass6; const u64 bm = __ballot(pz);
+      const int pos6 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos6] = (crow_t)(row6 - tb0); }
+      wtot += __popcll(bm); }
+    { const bool pz = pass7; const u64 bm = __ballot(pz);
+      const int pos7 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos7] = (crow_t)(row7 - tb0); }
+      wtot += __popcll(bm); }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int cb = 0; cb < wtot; cb += 64) {
+      const int ce = cb + cln;
+      bool cok = ce < wtot;
+      const i64 crow = tb0 + (cok ? crow_s[wv][ce] : 0);
+      const i64 cj = crow;
+      const int w2_c = a.c2[crow];
+      const int r2_c = (int)w2_c;
+      const i64 q2_c = a.B2 + (i64)w2_c;
+      const double x2_c = (double)((double)(a.B2 + (i64)w2_c) * a.R2);
+      const signed char w0_c = a.c0[crow];
+      const int r0_c = (int)w0_c;
+      const i64 q0_c = a.B0 + (i64)w0_c;
+      const double x0_c = (double)((double)(a.B0 + (i64)w0_c) * a.R0);
+      { const bool ok = cok && true; const double v = ok ? (a.A0_0 + a.B0_0 * (double)x2_c) * (a.A0_1 + a.B0_1 * (double)x0_c) : 0.0;
+        acc0 += v; cnt0 += ok ? 1u : 0u; }
+      { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
+        acc1 += v; cnt1 += ok ? 1u : 0u; }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  for (; t < t1; ++t) {
+    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;
+    const i64 off = (t - a.tile_prefix[r]) * 2048;
+    const i64 rs = a.rstart[r], re = rs + a.rlen[r];
+    const i64 tb0 = (rs & ~(i64)7) + off;
+    const i64 g0 = tb0 + (i64)threadIdx.x * 8;
+    const i64 dlo_ = rs - g0, dhi_ = re - g0;
+    const int alo = dlo_ <= 0 ? 0 : (dlo_ >= 8 ? 8 : (int)dlo_);
+    const int ahi = dhi_ <= 0 ? 0 : (dhi_ >= 8 ? 8 : (int)dhi_);
+    const bool act0 = 0 >= alo && 0 < ahi;
+    const i64 row0 = g0 + 0;
+    const bool act1 = 1 >= alo && 1 < ahi;
+    const i64 row1 = g0 + 1;
+    const bool act2 = 2 >= alo && 2 < ahi;
+    const i64 row2 = g0 + 2;
+    const bool act3 = 3 >= alo && 3 < ahi;
+    const i64 row3 = g0 + 3;
+    const bool act4 = 4 >= alo && 4 < ahi;
+    const i64 row4 = g0 + 4;
+    const bool act5 = 5 >= alo && 5 < ahi;
+    const i64 row5 = g0 + 5;
+    const bool act6 = 6 >= alo && 6 < ahi;
+    const i64 row6 = g0 + 6;
+    const bool act7 = 7 >= alo && 7 < ahi;
+    const i64 row7 = g0 + 7;
+    signed char x0v[8];
+    x0v[0] = act0 ? a.c0[g0 + 0] : (signed char)0; x0v[1] = act1 ? a.c0[g0 + 1] : (signed char)0; x0v[2] = act2 ? a.c0[g0 + 2] : (signed char)0; x0v[3] = act3 ? a.c0[g0 + 3] : (signed char)0; x0v[4] = act4 ? a.c0[g0 + 4] : (signed char)0; x0v[5] = act5 ? a.c0[g0 + 5] : (signed char)0; x0v[6] = act6 ? a.c0[g0 + 6] : (signed char)0; x0v[7] = act7 ? a.c0[g0 + 7] : (signed char)0;
+    signed char x1v[8];
+    x1v[0] = act0 ? a.c1[g0 + 0] : (signed char)0; x1v[1] = act1 ? a.c1[g0 + 1] : (signed char)0; x1v[2] = act2 ? a.c1[g0 + 2] : (signed char)0; x1v[3] = act3 ? a.c1[g0 + 3] : (signed char)0; x1v[4] = act4 ? a.c1[g0 + 4] : (signed char)0; x1v[5] = act5 ? a.c1[g0 + 5] : (signed char)0; x1v[6] = act6 ? a.c1[g0 + 6] : (signed char)0; x1v[7] = act7 ? a.c1[g0 + 7] : (signed char)0;
+    const int r0_0 = (int)x0v[0];
+    const i64 q0_0 = a.B0 + (i64)x0v[0];
+    const double x0_0 = (double)((double)(a.B0 + (i64)x0v[0]) * a.R0);
+    const int r1_0 = (int)x1v[0];
+    const i64 q1_0 = a.B1 + (i64)x1v[0];
+    const double x1_0 = (double)((double)(a.B1 + (i64)x1v[0]) / a.Q1);
+    const int r0_1 = (int)x0v[1];
+    const i64 q0_1 = a.B0 + (i64)x0v[1];
+    const double x0_1 = (double)((double)(a.B0 + (i64)x0v[1]) * a.R0);
+    const int r1_1 = (int)x1v[1];
+    const i64 q1_1 = a.B1 + (i64)x1v[1];
+    const double x1_1 = (double)((double)(a.B1 + (i64)x1v[1]) / a.Q1);
+    const int r0_2 = (int)x0v[2];
+    const i64 q0_2 = a.B0 + (i64)x0v[2];
+    const double x0_2 = (double)((double)(a.B0 + (i64)x0v[2]) * a.R0);
+    const int r1_2 = (int)x1v[2];
+    const i64 q1_2 = a.B1 + (i64)x1v[2];
+    const double x1_2 = (double)((double)(a.B1 + (i64)x1v[2]) / a.Q1);
+    const int r0_3 = (int)x0v[3];
+    const i64 q0_3 = a.B0 + (i64)x0v[3];
+    const double x0_3 = (double)((double)(a.B0 + (i64)x0v[3]) * a.R0);
+    const int r1_3 = (int)x1v[3];
+    const i64 q1_3 = a.B1 + (i64)x1v[3];
+    const double x1_3 = (double)((double)(a.B1 + (i64)x1v[3]) / a.Q1);
+    const int r0_4 = (int)x0v[4];
+    const i64 q0_4 = a.B0 + (i64)x0v[4];
+    const double x0_4 = (double)((double)(a.B0 + (i64)x0v[4]) * a.R0);
+    const int r1_4 = (int)x1v[4];
+    const i64 q1_4 = a.B1 + (i64)x1v[4];
+    const double x1_4 = (double)((double)(a.B1 + (i64)x1v[4]) / a.Q1);
+    const int r0_5 = (int)x0v[5];
+    const i64 q0_5 = a.B0 + (i64)x0v[5];
+    const double x0_5 = (double)((double)(a.B0 + (i64)x0v[5]) * a.R0);
+    const int r1_5 = (int)x1v[5];
+    const i64 q1_5 = a.B1 + (i64)x1v[5];
+    const double x1_5 = (double)((double)(a.B1 + (i64)x1v[5]) / a.Q1);
+    const int r0_6 = (int)x0v[6];
+    const i64 q0_6 = a.B0 + (i64)x0v[6];
+    const double x0_6 = (double)((double)(a.B0 + (i64)x0v[6]) * a.R0);
+    const int r1_6 = (int)x1v[6];
+    const i64 q1_6 = a.B1 + (i64)x1v[6];
+    const double x1_6 = (double)((double)(a.B1 + (i64)x1v[6]) / a.Q1);
+    const int r0_7 = (int)x0v[7];
+    const i64 q0_7 = a.B0 + (i64)x0v[7];
+    const double x0_7 = (double)((double)(a.B0 + (i64)x0v[7]) * a.R0);
+    const int r1_7 = (int)x1v[7];
+    const i64 q1_7 = a.B1 + (i64)x1v[7];
+    const double x1_7 = (double)((double)(a.B1 + (i64)x1v[7]) / a.Q1);
+    bool pass0 = act0 && ((true)) && ((true)) && ((true && (r0_0 >= (int)a.CL2 && r0_0 <= (int)a.CH2))) && ((true && (r0_0 >= (int)a.CL3 && r0_0 <= (int)a.CH3))) && ((true && (r1_0 >= (int)a.CL4 && r1_0 <= (int)a.CH4)));
+    bool pass1 = act1 && ((true)) && ((true)) && ((true && (r0_1 >= (int)a.CL2 && r0_1 <= (int)a.CH2))) && ((true && (r0_1 >= (int)a.CL3 && r0_1 <= (int)a.CH3))) && ((true && (r1_1 >= (int)a.CL4 && r1_1 <= (int)a.CH4)));
+    bool pass2 = act2 && ((true)) && ((true)) && ((true && (r0_2 >= (int)a.CL2 && r0_2 <= (int)a.CH2))) && ((true && (r0_2 >= (int)a.CL3 && r0_2 <= (int)a.CH3))) && ((true && (r1_2 >= (int)a.CL4 && r1_2 <= (int)a.CH4)));
+    bool pass3 = act3 && ((true)) && ((true)) && ((true && (r0_3 >= (int)a.CL2 && r0_3 <= (int)a.CH2))) && ((true && (r0_3 >= (int)a.CL3 && r0_3 <= (int)a.CH3))) && ((true && (r1_3 >= (int)a.CL4 && r1_3 <= (int)a.CH4)));
+    bool pass4 = act4 && ((true)) && ((true)) && ((true && (r0_4 >= (int)a.CL2 && r0_4 <= (int)a.CH2))) && ((true && (r0_4 >= (int)a.CL3 && r0_4 <= (int)a.CH3))) && ((true && (r1_4 >= (int)a.CL4 && r1_4 <= (int)a.CH4)));
+    bool pass5 = act5 && ((true)) && ((true)) && ((true && (r0_5 >= (int)a.CL2 && r0_5 <= (int)a.CH2))) && ((true && (r0_5 >= (int)a.CL3 && r0_5 <= (int)a.CH3))) && ((true && (r1_5 >= (int)a.CL4 && r1_5 <= (int)a.CH4)));
+    bool pass6 = act6 && ((true)) && ((true)) && ((true && (r0_6 >= (int)a.CL2 && r0_6 <= (int)a.CH2))) && ((true && (r0_6 >= (int)a.CL3 && r0_6 <= (int)a.CH3))) && ((true && (r1_6 >= (int)a.CL4 && r1_6 <= (int)a.CH4)));
+    bool pass7 = act7 && ((true)) && ((true)) && ((true && (r0_7 >= (int)a.CL2 && r0_7 <= (int)a.CH2))) && ((true && (r0_7 >= (int)a.CL3 && r0_7 <= (int)a.CH3))) && ((true && (r1_7 >= (int)a.CL4 && r1_7 <= (int)a.CH4)));
+    int wtot = 0;
+    { const bool pz = pass0; const u64 bm = __ballot(pz);
+      const int pos0 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos0] = (crow_t)(row0 - tb0); }
+      wtot += __popcll(bm); }
+    { const bool pz = pass1; const u64 bm = __ballot(pz);
+      const int pos1 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos1] = (crow_t)(row1 - tb0); }
+      wtot += __popcll(bm); }
+    { const bool pz = pass2; const u64 bm = __ballot(pz);
+      const int pos2 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos2] = (crow_t)(row2 - tb0); }
+      wtot += __popcll(bm); }
+    { const bool pz = pass3; const u64 bm = __ballot(pz);
+      const int pos3 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos3] = (crow_t)(row3 - tb0); }
+      wtot += __popcll(bm); }
+    { const bool pz = pass4; const u64 bm = __ballot(pz);
+      const int pos4 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos4] = (crow_t)(row4 - tb0); }
+      wtot += __popcll(bm); }
+    { const bool pz = pass5; const u64 bm = __ballot(pz);
+      const int pos5 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos5] = (crow_t)(row5 - tb0); }
+      wtot += __popcll(bm); }
+    { const bool pz = pass6; const u64 bm = __ballot(pz);
+      const int pos6 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos6] = (crow_t)(row6 - tb0); }
+      wtot += __popcll(bm); }
+    { const bool pz = pass7; const u64 bm = __ballot(pz);
+      const int pos7 = wtot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+      if (pz) { crow_s[wv][pos7] = (crow_t)(row7 - tb0); }
+      wtot += __popcll(bm); }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int cb = 0; cb < wtot; cb += 64) {
+      const int ce = cb + cln;
+      bool cok = ce < wtot;
+      const i64 crow = tb0 + (cok ? crow_s[wv][ce] : 0);
+      const i64 cj = crow;
+      const int w2_c = a.c2[crow];
+      const int r2_c = (int)w2_c;
+      const i64 q2_c = a.B2 + (i64)w2_c;
+      const double x2_c = (double)((double)(a.B2 + (i64)w2_c) * a.R2);
+      const signed char w0_c = a.c0[crow];
+      const int r0_c = (int)w0_c;
+      const i64 q0_c = a.B0 + (i64)w0_c;
+      const double x0_c = (double)((double)(a.B0 + (i64)w0_c) * a.R0);
+      { const bool ok = cok && true; const double v = ok ? (a.A0_0 + a.B0_0 * (double)x2_c) * (a.A0_1 + a.B0_1 * (double)x0_c) : 0.0;
+        acc0 += v; cnt0 += ok ? 1u : 0u; }
+      { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
+        acc1 += v; cnt1 += ok ? 1u : 0u; }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  __shared__ double rv[4][NA]; __shared__ i64 rc[4][NA];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  { const double r = wsum(acc0); const i64 c = wsumi((i64)cnt0); if (lane == 0) { rv[w][0] = r; rc[w][0] = c; } }
+  { const double r = wsum(acc1); const i64 c = wsumi((i64)cnt1); if (lane == 0) { rv[w][1] = r; rc[w][1] = c; } }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    { double t = 0.0; i64 c = 0;
+      for (int k = 0; k < 4; ++k) { t = t + rv[k][0]; c += rc[k][0]; }
+      const i64 o = (i64)blockIdx.x * NA + 0;
+      a.psum[o] = t; a.pcnt[o] = c;
+      a.pmin[o] = __builtin_inf(); a.pmax[o] = -__builtin_inf(); }
+    { double t = 0.0; i64 c = 0;
+      for (int k = 0; k < 4; ++k) { t = t + rv[k][1]; c += rc[k][1]; }
+      const i64 o = (i64)blockIdx.x * NA + 1;
+      a.psum[o] = t; a.pcnt[o] = c;
+      a.pmin[o] = __builtin_inf(); a.pmax[o] = -__builtin_inf(); }
+  }
+}

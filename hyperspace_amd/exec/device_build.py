@@ -1,13 +1,25 @@
 """Index build on MI355X (SURVEY §3.1 hot loop, kernels K1-K4; §7.2 steps 3-4).
 
-1. scan: this rank's share of the source files is decoded on the host (pyarrow, thread pool)
-   and streamed to HBM through pinned staging (K1); lineage ids are a per-file constant (K2);
-2. ``hs_murmur3_bucket``: Spark-compatible bucket id per row (K3);
-3. multi-GPU: rows move to their owner rank (bucket % world) with one RCCL all-to-all per column;
+1. scan (K1, ``staging.upload_files``): this rank's share of the source files is decoded by a
+   thread pool.  Parquet goes through the native page layer: the host preads raw column chunks
+   and plans their pages (``csrc/runtime/hs_parquet.cpp``), the compressed bytes cross PCIe and
+   HIP kernels inflate Snappy and expand RLE / bit-packed / PLAIN / dictionary pages
+   (``csrc/kernels/parquet_decode.hip``).  Dictionary-encoded string chunks decode on the device
+   to codes (the host parses only their dictionary pages).  Chunks the device path does not
+   take (nulls, PLAIN strings, booleans, decimals, other formats) are decoded by pyarrow;
+   lineage ids (K2) are a per-file constant fill;
+2. ``hs_murmur3_bucket``: Spark-compatible bucket id per row (K3; strings hash their dictionary
+   entry's bytes);
+3. multi-GPU: rows move to their owner rank (bucket % world) in one packed all-to-all per batch
+   of files (``_BatchedExchange`` / ``parallel/exchange.RowExchange``: counts, then one payload
+   collective over RCCL), overlapping the decode of the next batch;
 4. ``hs_sort_columns``: one stable LSD radix sort by (bucket, indexed columns...) (K4);
 5. ``hs_gather``: all columns permuted in one launch; bucket offsets from the histogram;
-6. one Parquet file per owned bucket, written by a host thread pool while the GPU is idle.
+6. one Parquet file per owned bucket, encoded on the device (``pq_encode``: dictionary codes,
+   bit packing, Snappy) and written by a host thread pool as each chunk lands.
 String columns use a job-global sorted dictionary so their codes sort and exchange consistently.
+Builds larger than the HBM budget run in bucket-range passes (``_streaming_build``), and the
+sorted bucket columns seed the device index cache (``device_cache.register_seed``).
 """
 from __future__ import annotations
 

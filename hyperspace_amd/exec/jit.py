@@ -172,6 +172,47 @@ class Args:
         return struct.pack(fmt, *vals)
 
 
+# kernels this process compiled with hipRTC / loaded from the on-disk code-object cache
+JIT_STATS = {"compiled": 0, "loaded": 0}
+# committed kernel sources compiled ahead of time by aot_compile() (__graft_entry__.build)
+AOT_DIR = os.path.join(_HERE, "_native", "aot")
+
+
+def _record_source(directory: str, name: str, src: str) -> None:
+    import hashlib
+    os.makedirs(directory, exist_ok=True)
+    h = hashlib.sha1(src.encode()).hexdigest()[:16]
+    path = os.path.join(directory, f"{name}.{h}.hip")
+    if not os.path.exists(path):
+        with open(path, "w") as f:
+            f.write(src)
+
+
+def aot_compile(src_dir: str = AOT_DIR, cache_dir: str = None, workers: int = 8) -> int:
+    """Compile every recorded kernel source in ``src_dir`` (``<kernel>.<hash>.hip``, the exact
+    text the planner generates: HS_JIT_RECORD) into the code-object cache, so the first query
+    of those shapes loads a code object instead of running hipRTC.  Needs no GPU.  Returns the
+    number of sources."""
+    import concurrent.futures as cf
+    cache_dir = cache_dir or CACHE_DIR
+    if not os.path.isdir(src_dir):
+        return 0
+    files = sorted(f for f in os.listdir(src_dir) if f.endswith(".hip"))
+    L = runtime()
+
+    def one(f):
+        with open(os.path.join(src_dir, f)) as fh:
+            src = fh.read()
+        name = f.split(".")[0]
+        rc = L.hs_jit_compile_to_cache(src.encode(), name.encode(), ARCH.encode(),
+                                       cache_dir.encode())
+        if rc != 0:
+            raise RuntimeError(f"AOT compile of {f} failed: {L.hs_jit_last_error().decode()}")
+    with cf.ThreadPoolExecutor(max_workers=max(1, workers)) as ex:
+        list(ex.map(one, files))
+    return len(files)
+
+
 class Kernel:
     def __init__(self, src: str, name: str, args: Args, lds_bytes: int = 0, block: int = 256):
         self.src = src
@@ -210,11 +251,15 @@ class Kernel:
                 h = hashlib.md5(self.src.encode()).hexdigest()[:10]
                 with open(os.path.join(dump, f"{self.name}_{h}.hip"), "w") as f:
                     f.write("#include <hip/hip_runtime.h>\n" + self.src)
+            rec = os.environ.get("HS_JIT_RECORD")
+            if rec:    # kernel sources of a workload, for the ahead-of-time set (aot_compile)
+                _record_source(rec, self.name, self.src)
             compiled = C.c_int(0)
             fn = L.hs_jit_get(self.src.encode(), self.name.encode(), ARCH.encode(),
                               CACHE_DIR.encode(), C.byref(compiled))
             if not fn:
                 raise RuntimeError(f"JIT compile/load failed: {L.hs_jit_last_error().decode()}")
+            JIT_STATS["compiled" if compiled.value == 1 else "loaded"] += 1
             self._fn = fn
         return self._fn
 
