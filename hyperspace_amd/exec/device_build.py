@@ -74,10 +74,10 @@ def _prepare_out_dir(out_path: str, mode: str, dist) -> None:
 
 def _sort_and_write(session, table: Dict[str, DeviceColumn], names: List[str], bucket,
                     indexed: List[str], num_buckets: int, out_path: str, schema: pa.Schema,
-                    task_id: int, presorted: bool = False, seed=None) -> List[str]:
+                    task_id: int, presorted: bool = False, seed=None, perm=None) -> List[str]:
     """Sort rows by (bucket, indexed columns) and write one file per bucket.  ``presorted``:
     the rows already are in that order (a rewrite of single sorted files per bucket), so no
-    sort or gather runs."""
+    sort or gather runs; ``perm``: that order as a row permutation (merged runs, K6)."""
     import torch
     n = int(bucket.numel())
     if n == 0:
@@ -86,7 +86,8 @@ def _sort_and_write(session, table: Dict[str, DeviceColumn], names: List[str], b
     if presorted:
         gathered = [table[c] for c in names]
     else:
-        perm = K.sort_permutation([table[c] for c in indexed], extra_leading=(bucket, 16))
+        if perm is None:
+            perm = K.sort_permutation([table[c] for c in indexed], extra_leading=(bucket, 16))
         gathered = K.gather_columns([table[c] for c in names], perm)
     counts = K.histogram(bucket, num_buckets)
     torch.cuda.synchronize()
@@ -726,11 +727,24 @@ def device_rewrite_buckets(session, files: List[str], indexed: List[str], out_pa
         cols = dict(zip(names, kept[:-1]))
         bucket = kept[-1].data
     presorted = all(len(groups[b]) == 1 for b in mine)
+    perm, how = None, "none" if presorted else "radix"
+    if not presorted and os.environ.get("HS_MERGE_PATH", "1") == "1":
+        # K6: every file is a sorted run; merge the runs of each bucket instead of re-sorting
+        run_off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        if deleted_ids:
+            # runs after the stable compaction: kept rows below each file's first row
+            b_at = torch.from_numpy(run_off).to(device=device, dtype=rows.dtype)
+            run_off = torch.searchsorted(rows.contiguous(), b_at).cpu().numpy().astype(np.int64)
+        perm = K.merge_runs_permutation([cols[c] for c in indexed], run_off,
+                                        np.asarray(file_bucket))
+        if perm is not None:
+            how = "merge-path"
     t1 = time.perf_counter()
     out = _sort_and_write(session, cols, names, bucket, indexed,
                           num_buckets or (max(mine) + 1), out_path, schema, rank,
-                          presorted=presorted)
+                          presorted=presorted, perm=perm)
     LAST_BUILD_STATS.update({"rewrite_read_h2d_s": t1 - t0, "rewrite_presorted": presorted,
+                             "rewrite_sort": how,
                              "rewrite_files": len(paths_in),
                              "rewrite_total_s": time.perf_counter() - t0})
     return out

@@ -82,6 +82,15 @@ class SortKeySpec(C.Structure):
                 ("has_nulls", C.c_int32)]
 
 
+MERGE_MAX_KEYS = 8
+
+
+class MergeKeys(C.Structure):
+    _fields_ = [("col", ColDesc * MERGE_MAX_KEYS), ("kmin", C.c_uint64 * MERGE_MAX_KEYS),
+                ("bits", C.c_int32 * MERGE_MAX_KEYS), ("nullable", C.c_int32 * MERGE_MAX_KEYS),
+                ("nkeys", C.c_int32), ("pad", C.c_int32)]
+
+
 class GatherCol(C.Structure):
     _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("src_valid", C.c_void_p),
                 ("dst_valid", C.c_void_p), ("elem_bytes", C.c_int32), ("pad", C.c_int32)]
@@ -140,7 +149,7 @@ def lib():
     for name, st in (("hs_hash_params_size", HashParams), ("hs_scan_params_size", ScanParams),
                      ("hs_join_params_size", JoinParams), ("hs_sort_key_spec_size", SortKeySpec),
                      ("hs_gather_params_size", GatherParams), ("hs_xch_params_size", XchParams),
-                     ("hs_xch_copy_size", XchCopy)):
+                     ("hs_xch_copy_size", XchCopy), ("hs_merge_keys_size", MergeKeys)):
         f = getattr(L, name)
         f.restype = C.c_int
         if f() != C.sizeof(st):
@@ -149,6 +158,8 @@ def lib():
     _sig(L.hs_murmur3_hash, I, P, I64, P, P)
     _sig(L.hs_sort_workspace_bytes, I64, I64)
     _sig(L.hs_sort_columns, I, P, I, I64, P, I, P, I64, P)
+    _sig(L.hs_merge_make_keys, I, P, I64, P, P)
+    _sig(L.hs_merge_round, I, P, P, P, P, P, I, I64, P)
     _sig(L.hs_scan_tmp_elems, I64, I64)
     _sig(L.hs_exclusive_scan_i64, I, P, P, I64, P, I64, P)
     _sig(L.hs_exclusive_scan_u32, I, P, P, I64, P, I64, P)

@@ -203,6 +203,92 @@ def sort_permutation(key_cols: Sequence, init_perm=None, extra_leading=None):
     return perm
 
 
+def merge_plan(run_off: np.ndarray, run_group: np.ndarray) -> List[np.ndarray]:
+    """Pair tables ({start, mid, end} int64 rows) of the pairwise merge rounds that turn the
+    sorted runs ``[run_off[r], run_off[r + 1])`` into one sorted run per group (runs of a group
+    are adjacent; groups never merge).  Each round merges runs 2i and 2i + 1 of every group; an
+    odd last run is carried as a pair with an empty right half."""
+    groups: List[List[int]] = []
+    for r in range(len(run_off) - 1):
+        if run_off[r + 1] == run_off[r]:
+            continue
+        if groups and groups[-1][0] == run_group[r]:
+            groups[-1][1].append(int(run_off[r + 1]))
+        else:
+            groups.append((run_group[r], [int(run_off[r]), int(run_off[r + 1])]))
+    bounds = [g[1] for g in groups]
+    rounds = []
+    while any(len(b) > 2 for b in bounds):
+        # every round covers all rows (the keys / permutation ping-pong between two buffers):
+        # a group already merged is a copy pair
+        pairs, nb = [], []
+        for b in bounds:
+            nxt = [b[0]]
+            for i in range(0, len(b) - 1, 2):
+                s, m = b[i], b[i + 1]
+                e = b[i + 2] if i + 2 < len(b) else m
+                pairs.append((s, m, e))
+                nxt.append(e)
+            nb.append(nxt)
+        rounds.append(np.asarray(pairs, dtype=np.int64).reshape(-1, 3))
+        bounds = nb
+    return rounds
+
+
+def merge_runs_permutation(key_cols: Sequence, run_off: np.ndarray, run_group: np.ndarray):
+    """Stable ascending (NULLS FIRST) permutation of rows made of runs already sorted by
+    ``key_cols``, grouped by ``run_group`` (e.g. bucket ids; groups stay in place): the order
+    ``sort_permutation([group] + key_cols)`` gives for such input, from ceil(log2(runs)) merge
+    rounds instead of a radix sort (K6).  None when the composite key exceeds 64 bits."""
+    torch = _torch()
+    cols = list(key_cols)
+    n = len(cols[0])
+    dev = cols[0].data.device
+    if len(cols) > NL.MERGE_MAX_KEYS:
+        return None
+    mk = NL.MergeKeys()
+    total = 0
+    for i, c in enumerate(cols):
+        kmin, bits = _sortable_range(c)
+        mk.col[i] = c.desc()
+        mk.kmin[i] = kmin
+        mk.bits[i] = bits
+        mk.nullable[i] = 1 if c.valid is not None else 0
+        total += bits + mk.nullable[i]
+    mk.nkeys = len(cols)
+    if total > 64:
+        return None
+    rounds = merge_plan(np.asarray(run_off, np.int64), np.asarray(run_group))
+    perm = torch.arange(n, dtype=torch.int32, device=dev)
+    if not rounds or n == 0:
+        return perm
+    L = NL.lib()
+    ka = torch.empty(n, dtype=torch.int64, device=dev)
+    kb = torch.empty_like(ka)
+    pb = torch.empty_like(perm)
+    NL.check(L.hs_merge_make_keys(C.byref(mk), n, NL.ptr(ka), NL.stream_ptr()),
+             "hs_merge_make_keys")
+    # the runs must really be sorted in this order (files written by another writer may order
+    # floats or strings differently): otherwise the caller sorts from scratch
+    if n > 1:
+        starts = torch.zeros(n, dtype=torch.bool, device=dev)
+        ro = torch.from_numpy(np.asarray(run_off[:-1], np.int64)).to(dev)
+        starts[ro[ro < n]] = True
+        ks = ka ^ torch.tensor(-(1 << 63), dtype=torch.int64, device=dev)   # unsigned order
+        if bool(((ks[1:] < ks[:-1]) & ~starts[1:]).any()):
+            return None
+    pa_, first = perm, True
+    for pairs in rounds:
+        dp = torch.from_numpy(pairs.reshape(-1)).to(dev)
+        NL.check(L.hs_merge_round(NL.ptr(ka), 0 if first else NL.ptr(pa_), NL.ptr(kb),
+                                  NL.ptr(pb), NL.ptr(dp), len(pairs), n, NL.stream_ptr()),
+                 "hs_merge_round")
+        first = False
+        ka, kb = kb, ka
+        pa_, pb = pb, pa_
+    return pa_
+
+
 def exclusive_scan_i64(x):
     torch = _torch()
     n = x.numel()

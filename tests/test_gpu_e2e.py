@@ -295,6 +295,8 @@ def test_optimize_full_on_device_merges_bucket_files(tpch, tmp_path):
     hs.refreshIndex("li_ok", "incremental")       # appended rows: a second file per bucket
     hs.optimizeIndex("li_ok", "full")
     assert device_build.LAST_BUILD_STATS.get("rewrite_presorted") is False
+    # K6: the bucket's two sorted files are merged (merge path), not radix re-sorted
+    assert device_build.LAST_BUILD_STATS.get("rewrite_sort") == "merge-path"
     assert _bucket_files_sorted(str(tmp_path / "idx" / "li_ok"), "l_orderkey") <= 16
     Hyperspace.enable(s)
     q = s.read.parquet(lpath).filter("l_orderkey > 0").agg(sum_("l_quantity").alias("q"),

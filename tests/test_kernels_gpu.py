@@ -337,3 +337,36 @@ def test_histogram_kernel(device):
         ids = rng.integers(0, B, 1_000_003).astype(np.int32)
         got = K.histogram(torch.from_numpy(ids).to(device), B).cpu().numpy()
         assert np.array_equal(got, np.bincount(ids, minlength=B))
+
+
+@pytest.mark.parametrize("runs_per_bucket", [2, 3, 7])
+def test_merge_runs_permutation_equals_stable_sort(device, runs_per_bucket):
+    """K6 merge path: buckets made of sorted runs (ties across runs, nulls, a two-column key,
+    empty runs) merge to exactly the stable (bucket, keys) sort permutation."""
+    import torch
+    from hyperspace_amd.ops import kernels as K
+    rng = np.random.default_rng(runs_per_bucket)
+    parts_a, parts_b, masks, off, grp = [], [], [], [0], []
+    for bkt in range(37):
+        for r in range(runs_per_bucket):
+            m = int(rng.integers(0, 5000)) if (bkt + r) % 11 else 0
+            a = rng.integers(-300, 300, m).astype(np.int64)
+            b = rng.integers(0, 1000, m).astype(np.int32)
+            mask = rng.random(m) < 0.03
+            key = np.where(mask, np.iinfo(np.int64).min, a)
+            o = np.lexsort((b, key, (~mask).astype(np.int8)))   # a sorted run, nulls first
+            parts_a.append(a[o]); parts_b.append(b[o]); masks.append(mask[o])
+            off.append(off[-1] + m)
+            grp.append(bkt)
+    a, b, mask = np.concatenate(parts_a), np.concatenate(parts_b), np.concatenate(masks)
+    n = len(a)
+    ca = _col(pa.array(a, mask=mask), device)
+    cb = _col(pa.array(b), device)
+    bucket = np.repeat(np.asarray(grp, np.int32), np.diff(off))
+    perm = K.merge_runs_permutation([ca, cb], np.asarray(off), np.asarray(grp))
+    assert perm is not None
+    ref = K.sort_permutation([ca, cb], extra_leading=(torch.from_numpy(bucket).to(device), 8))
+    assert np.array_equal(perm.cpu().numpy(), ref.cpu().numpy()), n
+    # unsorted runs are detected: the caller falls back to the radix sort
+    bad = _col(pa.array(rng.integers(0, 100, n).astype(np.int64)), device)
+    assert K.merge_runs_permutation([bad], np.asarray(off), np.asarray(grp)) is None
