@@ -75,6 +75,10 @@ _CMP = {E.EqualTo: pc.equal, E.NotEqual: pc.not_equal, E.LessThan: pc.less,
 _ARITH = {E.Add: pc.add, E.Subtract: pc.subtract, E.Multiply: pc.multiply}
 
 
+def _is_num(t: pa.DataType) -> bool:
+    return pa.types.is_integer(t) or pa.types.is_floating(t)
+
+
 def eval_expr(e: E.Expression, t: pa.Table):
     if isinstance(e, E.Attribute):
         return t.column(key(e))
@@ -109,10 +113,17 @@ def eval_expr(e: E.Expression, t: pa.Table):
         a, b = _operands(e, t)
         return _ARITH[type(e)](a, b)
     if isinstance(e, E.Divide):
+        # Spark: a double division, NULL for a zero divisor
         a, b = _operands(e, t)
-        return pc.divide(pc.cast(a, pa.float64()), pc.cast(b, pa.float64()))
+        b = pc.cast(b, pa.float64())
+        q = pc.divide(pc.cast(a, pa.float64()), b)
+        return pc.if_else(pc.equal(b, 0.0), pa.scalar(None, pa.float64()), q)
     if isinstance(e, E.Cast):
-        return pc.cast(eval_expr(e.child, t), e.dtype)
+        v = eval_expr(e.child, t)
+        if _is_num(v.type) and _is_num(e.dtype):
+            # Spark's numeric casts truncate toward zero and wrap (non-ANSI)
+            return pc.cast(v, e.dtype, safe=False)
+        return pc.cast(v, e.dtype)
     raise NotImplementedError(f"cannot evaluate {type(e).__name__}")
 
 

@@ -349,6 +349,8 @@ class CpuBackend:
     def _eval_agg_result(self, e, grouping, groups, agg_vals, nrows):
         if isinstance(e, E.AggregateFunction):
             return agg_vals[id(e)]
+        # a named grouping expression matches its own expression (the result column)
+        grouping = [g.child if isinstance(g, E.Alias) else g for g in grouping]
         for gi, g in enumerate(grouping):
             if e.semantic_equals(g) or (isinstance(e, E.Attribute) and isinstance(g, E.Attribute)
                                         and e.expr_id == g.expr_id):

@@ -73,6 +73,8 @@ class DRel:
         # distributed: this rank holds a file split of a non-index relation (rows not yet routed
         # to their bucket owners)
         self.split = split
+        # computed projection columns of this query (exec/project.py), by colmap name
+        self.extra: Dict[str, DeviceColumn] = {}
 
     def col(self, a: E.Attribute) -> DeviceColumn:
         if self.parts:
@@ -80,11 +82,16 @@ class DRel:
         name = self.colmap.get(a.expr_id)
         if name is None:
             raise Unsupported(f"attribute {a.sql()} not available on device")
-        return self.table.columns[name]
+        c = self.extra.get(name)
+        return c if c is not None else self.table.columns[name]
+
+    def is_computed(self, a: E.Attribute) -> bool:
+        return self.colmap.get(a.expr_id) in self.extra
 
     def copy(self, **kw) -> "DRel":
         d = DRel(self.table, dict(self.colmap), list(self.attrs), list(self.conds), self.bucketed,
                  self.sort_attrs, self.bucket_attrs, self.num_buckets, self.parts, self.split)
+        d.extra = dict(self.extra)
         for k, v in kw.items():
             setattr(d, k, v)
         return d
@@ -275,6 +282,7 @@ class GpuBackend:
         if isinstance(p, X.ProjectExec):
             colmap = dict(r.colmap)
             attrs = []
+            computed = []
             for e in p.project_list:
                 if isinstance(e, E.Attribute):
                     attrs.append(e)
@@ -283,9 +291,27 @@ class GpuBackend:
                         raise Unsupported("alias of unknown column")
                     colmap[e.expr_id] = colmap[e.child.expr_id]
                     attrs.append(e.to_attribute())
+                elif isinstance(e, E.Alias):
+                    computed.append(e)
+                    attrs.append(e.to_attribute())
                 else:
-                    raise Unsupported("computed projection")
-            return r.copy(colmap=colmap, attrs=attrs)
+                    raise Unsupported("computed projection without a name")
+            out = r.copy(colmap=colmap, attrs=attrs)
+            if computed:
+                # one generated elementwise kernel over the relation's rows (pending filters
+                # still apply afterwards, on the computed columns too)
+                from . import project
+                refs = {a.expr_id: r.col(a) for e in computed for a in e.child.references()}
+                n = r.table.num_rows if r.table.num_rows is not None else \
+                    len(next(iter(r.table.columns.values())))
+                with stage("project"):
+                    vals = project.evaluate([e.child for e in computed], refs, n, self.device)
+                for e, c in zip(computed, vals):
+                    c.hs_transient = True     # per query: no domain / encoding caches
+                    name = f"__hs_expr_{e.expr_id}"
+                    colmap[e.expr_id] = name
+                    out.extra[name] = c
+            return out
         raise Unsupported(f"operator {p.node_name}")
 
     def _scan(self, p: X.FileSourceScanExec) -> DRel:
@@ -719,7 +745,7 @@ class GpuBackend:
         and run inside the consuming kernel.  Queries with new literals reuse the layout."""
         need = list(dict.fromkeys(list(r.attrs) + list(keys) +
                                   [a for c in r.conds for a in c.references()]))
-        if any(a.expr_id not in r.colmap for a in need):
+        if any(a.expr_id not in r.colmap or r.is_computed(a) for a in need):
             return None
         names = sorted({r.colmap[a.expr_id] for a in need})
         knames = tuple(r.colmap[k.expr_id] for k in keys)
@@ -1046,11 +1072,43 @@ class GpuBackend:
         """Queue a fused aggregate and return ``finish() -> pa.Table``: the dense LDS
         aggregate for one small integer group column, else the hash-mode aggregate
         (``_hash_agg``)."""
+        if any(not isinstance(g, E.Attribute) for g in final.grouping):
+            final, child = self._named_groups(final, child)
         try:
             return self._dense_agg(final, child)
         except _NeedHash as e:
             log.debug("hash-mode aggregate: %s", e)
         return self._hash_agg(final, child, order, limit)
+
+    @staticmethod
+    def _named_groups(final: X.HashAggregateExec, child: X.SparkPlan):
+        """GROUP BY expressions: each named grouping expression becomes a computed column of a
+        projection over the aggregate's input (exec/project.py) and the aggregate groups on
+        that column; result expressions that repeat a grouping expression read the column."""
+        groups, extra = [], []
+        for g in final.grouping:
+            if isinstance(g, E.Attribute):
+                groups.append(g)
+            elif isinstance(g, E.Alias):
+                extra.append(g)
+                groups.append(g.to_attribute())
+            else:
+                raise Unsupported("unnamed group by expression")
+
+        def swap(x):
+            for g in extra:
+                if x.semantic_equals(g.child):
+                    return g.to_attribute()
+            return None
+        aggs = []
+        for e in final.aggregates:
+            hit = next((g for g in extra if g.expr_id == getattr(e, "expr_id", None)), None)
+            if hit is not None:
+                aggs.append(hit.to_attribute())
+            else:
+                aggs.append(e.transform_up(swap))
+        proj = X.ProjectExec(list(child.output) + extra, child)
+        return X.HashAggregateExec(groups, aggs, final.mode, final.child, final.result_attrs), proj
 
     def _dense_agg(self, final: X.HashAggregateExec, child: X.SparkPlan):
         """Queue a fused aggregate and return ``finish() -> pa.Table``.  Nothing here waits on
@@ -1206,7 +1264,7 @@ class GpuBackend:
             base = 0
         else:
             base, G = self._local_domain(c)
-            if multi and gkey is not None:
+            if multi and gkey is not None and not getattr(c, "hs_transient", False):
                 k = (gkey, r.colmap.get(group.expr_id))
                 dom = self._gdomains.get(k)
                 if dom is None:
@@ -1242,6 +1300,7 @@ class GpuBackend:
         hit = self._domains.get(ck)
         if hit is not None and hit[0] is c:
             return hit[1]
+        transient = getattr(c, "hs_transient", False)   # a per-query column: not cached
         import torch
         vals = c.data if c.valid is None else c.data[c.valid.bool()]
         if vals.numel() == 0:
@@ -1249,7 +1308,8 @@ class GpuBackend:
         else:
             lo, hi = torch.aminmax(vals)
             dom = (int(lo.item()), int(hi.item()) - int(lo.item()) + 1)
-        self._domains[ck] = (c, dom)
+        if not transient:
+            self._domains[ck] = (c, dom)
         return dom
 
     def _agg_specs(self, fns, col_info):

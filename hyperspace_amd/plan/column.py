@@ -102,6 +102,17 @@ class Column:
         return Column(E.Alias(self.expr, name))
 
     def cast(self, dtype):
+        """``dtype``: a pyarrow type or a Spark type name ("int", "bigint", "double", ...)."""
+        if isinstance(dtype, str):
+            import pyarrow as pa
+            names = {"byte": pa.int8(), "tinyint": pa.int8(), "short": pa.int16(),
+                     "smallint": pa.int16(), "int": pa.int32(), "integer": pa.int32(),
+                     "long": pa.int64(), "bigint": pa.int64(), "float": pa.float32(),
+                     "double": pa.float64(), "string": pa.string(), "boolean": pa.bool_(),
+                     "date": pa.date32()}
+            if dtype.lower() not in names:
+                raise ValueError(f"unknown type name {dtype!r}")
+            dtype = names[dtype.lower()]
         return Column(E.Cast(self.expr, dtype))
 
     def __repr__(self):

@@ -276,8 +276,12 @@ class DataFrame:
 
 class GroupedData:
     def __init__(self, df: DataFrame, grouping: Sequence[E.Expression]):
+        import re
         self.df = df
-        self.grouping = list(grouping)
+        # an unnamed grouping expression is an output column too: name it like Spark does,
+        # after its SQL text ("(a * 2)")
+        self.grouping = [g if isinstance(g, (E.Attribute, E.Alias)) else
+                         E.Alias(g, re.sub(r"#\d+", "", g.sql())) for g in grouping]
 
     def agg(self, *aggs) -> DataFrame:
         exprs: List[E.Expression] = list(self.grouping)

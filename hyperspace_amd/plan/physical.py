@@ -519,8 +519,11 @@ class HashAggregateExec(UnaryExec):
         return [e if isinstance(e, E.Attribute) else e.to_attribute() for e in self.aggregates]
 
     def partial_output(self):
-        out = [g if isinstance(g, E.Attribute) else E.Attribute(g.sql(), g.data_type, True)
-               for g in self.grouping]
+        # a named grouping expression keeps its alias's id: the exchange above partitions by,
+        # and the final aggregate groups on, these same attributes
+        out = [g if isinstance(g, E.Attribute) else
+               (g.to_attribute() if isinstance(g, E.Alias) else
+                E.Attribute(g.sql(), g.data_type, True)) for g in self.grouping]
         for i, (_, fn) in enumerate(agg_functions(self.aggregates)):
             for j, (nm, dt) in enumerate(_buffer_fields(fn)):
                 out.append(E.Attribute(f"{nm}#{i}_{j}", dt, True, expr_id=-(1000 * (i + 1) + j)))

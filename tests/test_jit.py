@@ -593,3 +593,32 @@ def test_aot_sources_compile_into_cache(rt, tmp_path):
     jit._record_source(str(rec), "hs_jit_x", "int x;")
     (f,) = os.listdir(rec)
     assert f.startswith("hs_jit_x.") and f.endswith(".hip") and (rec / f).read_text() == "int x;"
+
+
+def test_project_kernel_compiles(rt, tmp_path):
+    """exec/project.py: the elementwise kernel of a computed projection (arithmetic with
+    wrapping / division / casts / Kleene logic over nullable columns) compiles for gfx950."""
+    import torch
+    from hyperspace_amd.exec import project
+    from hyperspace_amd.exec.device_table import DeviceColumn
+    jit = rt
+    from hyperspace_amd.plan import expressions as E
+    a = E.Attribute("a", pa.int64())
+    b = E.Attribute("b", pa.int32())
+    x = E.Attribute("x", pa.float64())
+    cols = {a.expr_id: DeviceColumn(torch.zeros(4, dtype=torch.int64),
+                                    torch.ones(4, dtype=torch.uint8), pa.int64()),
+            b.expr_id: DeviceColumn(torch.zeros(4, dtype=torch.int32), None, pa.int32()),
+            x.expr_id: DeviceColumn(torch.zeros(4, dtype=torch.float64), None, pa.float64())}
+    exprs = [E.Add(E.Multiply(a, E.Literal(3)), b), E.Divide(a, b), E.Cast(x, pa.int32()),
+             E.Or(E.And(E.GreaterThan(a, b), E.LessThan(x, E.Literal(2.5))), E.IsNull(a)),
+             E.Subtract(x, E.Cast(b, pa.float64()))]
+    k, values, outs = project.build(exprs, cols, 4, torch.device("cpu"))
+    assert [o.atype for o in outs] == [e.data_type for e in exprs]
+    rc = jit.runtime().hs_jit_compile_to_cache(k.src.encode(), k.name.encode(), b"gfx950",
+                                               str(tmp_path).encode())
+    assert rc == 0, jit.runtime().hs_jit_last_error().decode()
+    # literals are arguments: another literal reuses the kernel
+    exprs[0] = E.Add(E.Multiply(a, E.Literal(7)), b)
+    k2, _, _ = project.build(exprs, cols, 4, torch.device("cpu"))
+    assert k2 is k
