@@ -91,6 +91,8 @@ MJ_PREFETCH = os.environ.get("HS_JIT_MJ_PREFETCH", "0") == "1"
 # workgroup size of the merge join: 64 = one wavefront per workgroup working its own 512-row
 # tiles (own right span, no block barriers), 256 = four wavefronts sharing 2048-row tiles
 MJ_BLOCK = int(os.environ.get("HS_JIT_MJ_BLOCK", "256"))
+# eager aggregate tail (no deferred match lists): _eager_tail
+MJ_EAGER = os.environ.get("HS_JIT_MJ_EAGER", "1") == "1"
 MJ_KEY32 = os.environ.get("HS_JIT_MJ_KEY32", "1") == "1"  # 32-bit merge images (_key32_frame)
 # cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
 MJ_EXP = os.environ.get("HS_JIT_MJ_EXP", "")
@@ -1280,7 +1282,7 @@ def merge_join_shape(p: NL.JoinParams, compacts=None, hk=None) -> tuple:
     return ("merge_join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey,
             p.key_is_float, MJ_ITEMS, MJ_LDS_KEYS, MJ_STEPS, BLOCK, WAVE_SYNC,
             _key32_frame(p, compacts) is not None, MJ_EXP, MJ_STAGE_UNROLL, MJ_DBUF, MJ_PREFETCH,
-            MJ_BLOCK,
+            MJ_BLOCK, MJ_EAGER,
             hk.shape() if hk is not None else None)
 
 
@@ -1434,6 +1436,14 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
     ronly_slots = [x for x in _pred_slots(ronly)]
     mixed_right = [x for x in _pred_slots(mixed) if x >= split]
     stage_slots = list(dict.fromkeys([rk] + ronly_slots))
+    # eager tail: the aggregate inputs of the left side stream with the tile (vector loads) and
+    # the right side's are staged in LDS with the span, so a match accumulates at once - no
+    # deferred (row, j) lists (20 KB of LDS per block) and no dependent gathers
+    tail_slots = list(dict.fromkeys(_agg_slots(aggs) + ([p.group_col] if grouped else [])))
+    eager = MJ_EAGER and hk is None
+    rtail = [x for x in tail_slots if x >= split] if eager else []
+    if eager:
+        first = list(dict.fromkeys(first + [x for x in tail_slots if x < split]))
     allslots = list(dict.fromkeys(first + stage_slots + mixed_right + _agg_slots(aggs) +
                                   ([p.group_col] if grouped else []) + hslots))
     approx = _sum_only_slots(lpreds + rpreds, aggs, p.group_col, cols) - {lk, rk} - set(hslots)
@@ -1445,10 +1455,16 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
     CAP = 64 * NI + 64  # noqa: N806 — list entries: < 64 carried over + one tile's appends
     NB = 2 if MJ_DBUF else 1  # noqa: N806
     b += [f"  __shared__ {KT} skeys_[{NB}][{LK + 1}]; __shared__ unsigned char spass_[{NB}][{LK}];",
-          f"  constexpr int DUMP = {CAP};",
-          f"  __shared__ int lrow_s[{W}][{CAP + 64}]; __shared__ int lj_s[{W}][{CAP + 64}];",
-          "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;",
-          "  int wcnt = 0;   // wavefront-uniform length of this wavefront's (row, j) list"]
+          "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;"]
+    if eager:
+        for x in rtail:
+            b.append(f"  __shared__ {_CTYPE[cols[x][0]]} stv{x}_[{NB}][{LK}];")
+            if cols[x][1]:
+                b.append(f"  __shared__ unsigned char stn{x}_[{NB}][{LK}];")
+    else:
+        b += [f"  constexpr int DUMP = {CAP};",
+              f"  __shared__ int lrow_s[{W}][{CAP + 64}]; __shared__ int lj_s[{W}][{CAP + 64}];",
+              "  int wcnt = 0;   // wavefront-uniform length of this wavefront's (row, j) list"]
     rkv = _valid_expr(g1, rk, "{r}")
 
     def rimg(val: str) -> str:
@@ -1470,6 +1486,11 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
                   f"{ind}const bool staged = ns <= {LK};",
                   f"{ind}{KT}* const skeys = skeys_[{'(int)(t & 1)' if NB == 2 else '0'}];",
                   f"{ind}unsigned char* const spass = spass_[{'(int)(t & 1)' if NB == 2 else '0'}];"])
+        for x in rtail:
+            sel = '(int)(t & 1)' if NB == 2 else '0'
+            b.append(f"{ind}{_CTYPE[cols[x][0]]}* const stv{x} = stv{x}_[{sel}];")
+            if cols[x][1]:
+                b.append(f"{ind}unsigned char* const stn{x} = stn{x}_[{sel}];")
         # (1) stage the right span: key images + right-only predicate pass bytes; each round
         # issues the loads of U rows per thread before any store (one HBM round trip per round
         # instead of one per row)
@@ -1482,7 +1503,7 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
                       f"{ind}  const i64 jr{u} = ss + (sv{u} ? sq{u} : 0);"])
         for u in range(U):
             gs = _Gen(args, cols, split, (f"jr{u}", f"jr{u}"), approx, True)
-            for sl in stage_slots:
+            for sl in list(dict.fromkeys(stage_slots + rtail)):
                 _uload(gs, sl, f"s{u}", b, ind + "  ")
         okk_fmt = f"n{rk}_s{{u}}" if cols[rk][1] else "true"
         for u in range(U):
@@ -1491,7 +1512,12 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
             okk = okk_fmt.format(u=u)
             b.extend([f"{ind}  if (sv{u}) {{ const bool kv = {okk};",
                       f"{ind}    skeys[sq{u}] = kv ? {rimg(f'x{rk}_s{u}')} : ({KT})0;",
-                      f"{ind}    spass[sq{u}] = (kv && {cond}) ? 1 : 0; }}"])
+                      f"{ind}    spass[sq{u}] = (kv && {cond}) ? 1 : 0;"])
+            for x in rtail:
+                b.append(f"{ind}    stv{x}[sq{u}] = x{x}_s{u};")
+                if cols[x][1]:
+                    b.append(f"{ind}    stn{x}[sq{u}] = n{x}_s{u} ? 1 : 0;")
+            b.append(f"{ind}  }}")
         b.extend([f"{ind}}}",
                   f"{ind}if (staged && threadIdx.x == 0) skeys[ns] = {KMAX};   // walk sentinel"])
         # (2) left stream (raw vector arrays come from the tile loop).  Per-item flags live as
@@ -1577,6 +1603,9 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
                     b.append(f"{i2}  pb &= ({cond}) ? ~0u : ~{1 << it}u; }}")
             if "notail" in MJ_EXP:
                 b.append(f"{i2}cnt0 += __popc(pb);")
+            elif eager:
+                b.extend(_eager_tail(args, cols, split, approx, aggs, grouped, p.group_col,
+                                     allslots, rtail, NI, i2))
             else:
                 b.extend(_deferred_append(NI, i2, "((pb >> {it}) & 1u)", "row{it}",
                                           "ss + jl{it}"))
@@ -1615,8 +1644,9 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
         body(b, False)
         b.append(f"{ind}}}")
     b += ["  }"]
-    b += _deferred_drain(args, cols, split, approx, aggs, grouped, p.group_col, allslots, "  ",
-                         final=True, hk=hk)
+    if not eager:
+        b += _deferred_drain(args, cols, split, approx, aggs, grouped, p.group_col, allslots,
+                             "  ", final=True, hk=hk)
     if hk is None:
         b += _flush(aggs, grouped, BLOCK)
     src = (_PRELUDE + args.struct_src() +
@@ -1624,6 +1654,36 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
            "\n".join(b) + "\n}\n")
     lds = (len(aggs) * p.num_groups * 32) if grouped else 0
     return Kernel(src, "hs_jit_merge_join_agg", args, lds, BLOCK)
+
+
+def _eager_tail(args, cols, split, approx, aggs, grouped, group_col, allslots, rtail, NI: int,
+                ind: str) -> List[str]:
+    """Merge-join matches of this round (bit ``it`` of ``pb``) accumulated at once: left inputs
+    are the tile's registers ``x<s>_<it>``, right inputs come from the staged span (``stv<s>``
+    at ``jl<it>``; an unstaged span reads them from HBM)."""
+    b = []
+    for it in range(NI):
+        b.append(f"{ind}{{ bool pe = ((pb >> {it}) & 1u) != 0u; const int je = pe ? jl{it} : 0;")
+        gr = _Gen(args, cols, split, (f"row{it}", "(ss + je)"), approx, True)
+        for x in rtail:
+            ct = _CTYPE[cols[x][0]]
+            b.append(f"{ind}  const {ct} x{x}_{it} = staged ? stv{x}[je] : {gr.value(x, '(ss + je)')};")
+            if cols[x][1]:
+                b.append(f"{ind}  const bool n{x}_{it} = staged ? stn{x}[je] != 0 : "
+                         f"{gr.vptr(x)}[ss + je] != 0;")
+        g = _Gen(args, cols, split, (f"row{it}", "(ss + je)"), approx, True)
+        gvar = f"gi{it}"
+        if grouped:
+            base = args.add("q", "group_base", "long long")
+            ng = args.add("q", "num_groups", "long long")
+            b.append(f"{ind}  const i64 gl = (i64){_rename(f'x{group_col}', allslots, it)} - {base};")
+            b.append(f"{ind}  pe = pe && {_rename(g.ok(group_col), allslots, it)} && "
+                     f"gl >= 0 && gl < {ng};")
+            b.append(f"{ind}  const int {gvar} = pe ? (int)gl : 0;")
+        b += [_rename(x, allslots, it) for x in _accumulate(g, aggs, grouped, "pe", gvar,
+                                                             ind + "  ")]
+        b.append(f"{ind}}}")
+    return b
 
 
 def _block_sync(block: int) -> str:
