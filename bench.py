@@ -12,13 +12,15 @@ TPC-H-shaped (``hyperspace_amd.models.tpch``) and generated once per data dir.  
 timed separately (three covering indexes: lineitem(l_shipdate), lineitem(l_orderkey),
 orders(o_orderkey)); ``index_build_gbps`` = decoded indexed-column bytes / build wall time.
 Index builds shard buckets over ranks (bucket ``b`` -> rank ``b % N``, RCCL all-to-all).  Queries
-run with two placements (``--placement``, default both; ``value`` is the sharded one):
+run with two placements (``--placement``, default both; with N > 1 ``value`` is the replicated
+one):
 
-* ``sharded`` (headline): each rank holds its buckets only; every query runs on all ranks and
-  partial aggregates combine with one all-gather — strong scaling of a single query stream;
-* ``replicated`` (side key ``replicated``): every rank loads all buckets into its HBM (the SF100
-  index set is ~36 GB of a 288 GB MI355X) and serves its own query stream with no collective —
-  read replicas, weak scaling (total queries/s of all ranks).
+* ``replicated`` (headline for N > 1): every rank loads all buckets into its HBM (the SF100
+  index set is ~36 GB of a 288 GB MI355X) and serves its own query stream with no collective -
+  read replicas, weak scaling (``value`` = total queries/s of all ranks);
+* ``sharded`` (side key ``sharded``; the only placement at N = 1): each rank holds its buckets
+  only; every query runs on all ranks and partial aggregates combine with one all-gather -
+  strong scaling of a single query stream.
 
 The timed Q3 re-matches join keys on every query (the co-located sort-merge join kernel,
 ``spark.hyperspace.mi.joinIndex.enabled=false``), as the reference's bucketed SortMergeJoin
@@ -360,7 +362,7 @@ def main():
     log(rank, f"[bench] cold first queries {cold}")
 
     from hyperspace_amd.utils.tracing import TRACER, format_report
-    modes = ["replicated", "sharded"] if world > 1 and args.placement == "both" else \
+    modes = ["sharded", "replicated"] if world > 1 and args.placement == "both" else \
         [args.placement if world > 1 else "sharded"]
     ji_key = "spark.hyperspace.mi.joinIndex.enabled"
     ji_run = None
@@ -477,10 +479,11 @@ def main():
             out["join_index"] = {"value": round(ji_run["qps"], 3),
                                  "ms_per_step": round(ji_run["ms_per_step"], 3),
                                  "note": "Q3 through the cached join index (derived HBM map)"}
-        if "replicated" in runs and final != "replicated":
-            out["replicated"] = {"value": round(runs["replicated"]["qps"], 3),
-                                 "ms_per_step": round(runs["replicated"]["ms_per_step"], 3),
-                                 "scaling": "weak"}
+        for m in runs:
+            if m != final:
+                out[m] = {"value": round(runs[m]["qps"], 3),
+                          "ms_per_step": round(runs[m]["ms_per_step"], 3),
+                          "scaling": "weak" if m == "replicated" else "strong"}
         if base:
             out["cpu_baseline"] = {"value": base["value"], "source": base.get("source")}
         if on_gpu:
