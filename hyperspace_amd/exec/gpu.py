@@ -278,7 +278,31 @@ class GpuBackend:
 
     def _unary(self, p: X.SparkPlan, r: DRel) -> DRel:
         if isinstance(p, X.FilterExec):
-            return r.copy(conds=r.conds + E.split_conjuncts(p.condition))
+            conds = E.split_conjuncts(p.condition)
+            computed = [c for c in conds if _needs_eval(c)]
+            if not computed:
+                return r.copy(conds=r.conds + conds)
+            # conjuncts over computed values (``a * 2 > 500``, pushed below a projection by the
+            # optimizer): one generated kernel evaluates them to 0/1 columns, and the scan
+            # kernels test those like any column
+            from . import project
+            out = r.copy()
+            refs = {a.expr_id: r.col(a) for c in computed for a in c.references()}
+            n = r.table.num_rows if r.table.num_rows is not None else \
+                len(next(iter(r.table.columns.values())))
+            with stage("project"):
+                vals = project.evaluate([E.Cast(c, pa.int8()) for c in computed], refs, n,
+                                        self.device)
+            rest = [c for c in conds if not _needs_eval(c)]
+            for c, v in zip(computed, vals):
+                v.hs_transient = True
+                at = E.Attribute(f"__hs_pred", pa.int8(), True)
+                name = f"__hs_pred_{at.expr_id}"
+                out.colmap[at.expr_id] = name
+                out.extra[name] = v
+                rest.append(E.GreaterThan(at, E.Literal(0)))
+            out.conds = r.conds + rest
+            return out
         if isinstance(p, X.ProjectExec):
             colmap = dict(r.colmap)
             attrs = []
@@ -1899,6 +1923,31 @@ def _combine_aggs(a, b):
     torch.minimum(a[2], b[2], out=a[2])
     torch.maximum(a[3], b[3], out=a[3])
     return a
+
+
+def _needs_eval(c: E.Expression) -> bool:
+    """A predicate over computed values (arithmetic, or a cast that changes a column's values):
+    the scan kernels' predicate compiler takes column / literal comparisons (it looks through
+    value-preserving casts only), so such a conjunct is evaluated as a computed column."""
+    for x in c.iter_tree():
+        if isinstance(x, E.BinaryArithmetic):
+            return True
+        if isinstance(x, E.Cast) and not isinstance(x.child, E.Literal) and \
+                not _lossless_cast(x.child.data_type, x.dtype):
+            return True
+    return False
+
+
+def _lossless_cast(src: pa.DataType, dst: pa.DataType) -> bool:
+    if src == dst:
+        return True
+    if pa.types.is_integer(src) and pa.types.is_integer(dst):
+        return dst.bit_width >= src.bit_width and \
+            pa.types.is_signed_integer(dst) >= pa.types.is_signed_integer(src)
+    if pa.types.is_float64(dst):
+        return pa.types.is_floating(src) or \
+            (pa.types.is_integer(src) and src.bit_width <= 32) or pa.types.is_decimal(src)
+    return False
 
 
 def _prefix_sorted(r: DRel, exprs) -> bool:
