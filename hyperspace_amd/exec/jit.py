@@ -1456,6 +1456,8 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
     NB = 2 if MJ_DBUF else 1  # noqa: N806
     b += [f"  __shared__ {KT} skeys_[{NB}][{LK + 1}]; __shared__ unsigned char spass_[{NB}][{LK}];",
           "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;"]
+    if eager and grouped:
+        b += _run_decls(aggs)
     if eager:
         for x in rtail:
             b.append(f"  __shared__ {_CTYPE[cols[x][0]]} stv{x}_[{NB}][{LK}];")
@@ -1644,6 +1646,8 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
         body(b, False)
         b.append(f"{ind}}}")
     b += ["  }"]
+    if eager and grouped:
+        b += _run_flush(aggs, "  ")
     if not eager:
         b += _deferred_drain(args, cols, split, approx, aggs, grouped, p.group_col, allslots,
                              "  ", final=True, hk=hk)
@@ -1680,10 +1684,58 @@ def _eager_tail(args, cols, split, approx, aggs, grouped, group_col, allslots, r
             b.append(f"{ind}  pe = pe && {_rename(g.ok(group_col), allslots, it)} && "
                      f"gl >= 0 && gl < {ng};")
             b.append(f"{ind}  const int {gvar} = pe ? (int)gl : 0;")
-        b += [_rename(x, allslots, it) for x in _accumulate(g, aggs, grouped, "pe", gvar,
-                                                             ind + "  ")]
+            b += [_rename(x, allslots, it) for x in _run_accumulate(g, aggs, "pe", gvar,
+                                                                    ind + "  ")]
+        else:
+            b += [_rename(x, allslots, it) for x in _accumulate(g, aggs, grouped, "pe", gvar,
+                                                                 ind + "  ")]
         b.append(f"{ind}}}")
     return b
+
+
+def _run_decls(aggs) -> List[str]:
+    """Per-thread run accumulators of grouped eager aggregation (``_run_accumulate``)."""
+    out = ["  int rg_ = -1;"]
+    for i, a in enumerate(aggs):
+        out.append(f"  double rs{i}_ = {_ident(a.kind)}; unsigned long long rc{i}_ = 0ull;")
+    return out
+
+
+def _run_flush(aggs, ind: str) -> List[str]:
+    """Add this thread's run (group ``rg_``) to the block's LDS group table."""
+    out = [f"{ind}if (rg_ >= 0) {{"]
+    for i, a in enumerate(aggs):
+        out.append(f"{ind}  if (rc{i}_) {{ const int s = rg_ * NA + {i};")
+        if a.kind == NL.AK_MIN:
+            out.append(f"{ind}    lds_min(&gmn[s], rs{i}_);")
+        elif a.kind == NL.AK_MAX:
+            out.append(f"{ind}    lds_max(&gmx[s], rs{i}_);")
+        elif a.kind == NL.AK_SUM:
+            out.append(f"{ind}    atomicAdd(&gsum[s], rs{i}_);")
+        out.append(f"{ind}    atomicAdd(&gcnt[s], rc{i}_); }}")
+    out.append(f"{ind}}}")
+    return out
+
+
+def _run_accumulate(gen: _Gen, aggs, pass_var: str, gvar: str, ind: str) -> List[str]:
+    """Grouped accumulation into per-thread registers while consecutive matches of the thread
+    stay in one group (sorted / low-cardinality groups: almost always), flushed to the LDS group
+    table when the group changes - instead of a wavefront-wide peel per row."""
+    out = [f"{ind}if ({pass_var}) {{",
+           f"{ind}  if ({gvar} != rg_) {{"]
+    out += _run_flush(aggs, ind + "    ")
+    out.append(f"{ind}    rg_ = {gvar};")
+    for i, a in enumerate(aggs):
+        out.append(f"{ind}    rs{i}_ = {_ident(a.kind)}; rc{i}_ = 0ull;")
+    out.append(f"{ind}  }}")
+    for i, a in enumerate(aggs):
+        v, ok = gen.agg_value(i, a)
+        upd = {NL.AK_MIN: f"rs{i}_ = fmin(rs{i}_, (double)({v}));",
+               NL.AK_MAX: f"rs{i}_ = fmax(rs{i}_, (double)({v}));"}.get(
+            a.kind, f"rs{i}_ += (double)({v});")
+        out.append(f"{ind}  if ({ok}) {{ {upd} rc{i}_ += 1ull; }}")
+    out.append(f"{ind}}}")
+    return out
 
 
 def _block_sync(block: int) -> str:
