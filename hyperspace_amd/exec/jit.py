@@ -92,7 +92,7 @@ MJ_PREFETCH = os.environ.get("HS_JIT_MJ_PREFETCH", "0") == "1"
 # tiles (own right span, no block barriers), 256 = four wavefronts sharing 2048-row tiles
 MJ_BLOCK = int(os.environ.get("HS_JIT_MJ_BLOCK", "256"))
 # eager aggregate tail (no deferred match lists): _eager_tail
-MJ_EAGER = os.environ.get("HS_JIT_MJ_EAGER", "1") == "1"
+MJ_EAGER = os.environ.get("HS_JIT_MJ_EAGER", "0") == "1"
 MJ_KEY32 = os.environ.get("HS_JIT_MJ_KEY32", "1") == "1"  # 32-bit merge images (_key32_frame)
 # cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
 MJ_EXP = os.environ.get("HS_JIT_MJ_EXP", "")
