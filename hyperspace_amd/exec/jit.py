@@ -93,6 +93,8 @@ MJ_PREFETCH = os.environ.get("HS_JIT_MJ_PREFETCH", "0") == "1"
 MJ_BLOCK = int(os.environ.get("HS_JIT_MJ_BLOCK", "256"))
 # eager aggregate tail (no deferred match lists): _eager_tail
 MJ_EAGER = os.environ.get("HS_JIT_MJ_EAGER", "0") == "1"
+# match-list appends one set match bit per round (_sparse_append) instead of one per item
+MJ_SPARSE = os.environ.get("HS_JIT_MJ_SPARSE", "1") == "1"
 MJ_KEY32 = os.environ.get("HS_JIT_MJ_KEY32", "1") == "1"  # 32-bit merge images (_key32_frame)
 # cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
 MJ_EXP = os.environ.get("HS_JIT_MJ_EXP", "")
@@ -1282,7 +1284,7 @@ def merge_join_shape(p: NL.JoinParams, compacts=None, hk=None) -> tuple:
     return ("merge_join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey,
             p.key_is_float, MJ_ITEMS, MJ_LDS_KEYS, MJ_STEPS, BLOCK, WAVE_SYNC,
             _key32_frame(p, compacts) is not None, MJ_EXP, MJ_STAGE_UNROLL, MJ_DBUF, MJ_PREFETCH,
-            MJ_BLOCK, MJ_EAGER,
+            MJ_BLOCK, MJ_EAGER, MJ_SPARSE,
             hk.shape() if hk is not None else None)
 
 
@@ -1339,6 +1341,29 @@ def _deferred_append(NI: int, ind: str, pass_fmt: str, row_fmt: str, j_fmt: str)
               f"{ind}  lrow_s[wv][wp] = (int)({row_fmt.format(it=it)}); "
               f"lj_s[wv][wp] = (int)({j_fmt.format(it=it)});",
               f"{ind}  wcnt += __popcll(bm); }}"]
+    return b
+
+
+def _sparse_append(NI: int, ind: str, word: str, j_fmt: str) -> List[str]:
+    """``_deferred_append`` for sparse matches: the thread's match bits ``word`` are appended
+    one set bit per round, for as many rounds as the wavefront's busiest lane needs (a join
+    keeping a few percent of its rows: one or two rounds instead of NI).  The item's row is
+    ``g0 + it``; its match index comes from a select chain over the per-item registers."""
+    b = [f"{ind}{{ unsigned pend = {word};",
+         f"{ind}  while (__any(pend != 0u)) {{",
+         f"{ind}    const bool has = pend != 0u;",
+         f"{ind}    const int it = has ? __builtin_ctz(pend) : 0;",
+         f"{ind}    pend &= pend - 1u;",
+         f"{ind}    int jv = {j_fmt.format(it=0)};"]
+    for it in range(1, NI):
+        b.append(f"{ind}    jv = it == {it} ? {j_fmt.format(it=it)} : jv;")
+    b += [f"{ind}    const u64 bm = __ballot(has);",
+          f"{ind}    const int wp = has ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), "
+          f"__builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;",
+          f"{ind}    lrow_s[wv][wp] = (int)(g0 + it); lj_s[wv][wp] = (int)(ss + jv);",
+          f"{ind}    wcnt += __popcll(bm);",
+          f"{ind}  }}",
+          f"{ind}}}"]
     return b
 
 
@@ -1609,8 +1634,11 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
                 b.extend(_eager_tail(args, cols, split, approx, aggs, grouped, p.group_col,
                                      allslots, rtail, NI, i2))
             else:
-                b.extend(_deferred_append(NI, i2, "((pb >> {it}) & 1u)", "row{it}",
-                                          "ss + jl{it}"))
+                if MJ_SPARSE:
+                    b.extend(_sparse_append(NI, i2, "pb", "jl{it}"))
+                else:
+                    b.extend(_deferred_append(NI, i2, "((pb >> {it}) & 1u)", "row{it}",
+                                              "ss + jl{it}"))
                 b.extend(_deferred_drain(args, cols, split, approx, aggs, grouped, p.group_col,
                                          allslots, i2, final=False, hk=hk))
             b.append(f"{i2}}}")
