@@ -11,12 +11,41 @@ import os
 from typing import List, Optional
 
 
+class _PendingCombine:
+    """Partials of one query on their way to the host (pinned, stream-ordered copy)."""
+
+    def __init__(self, packed):
+        import torch
+        self.result = None
+        if packed.is_cuda:
+            self.host = torch.empty(packed.numel(), dtype=torch.uint8, pin_memory=True)
+            self.host.copy_(packed, non_blocking=True)
+            self.event = torch.cuda.Event()
+            self.event.record()
+        else:
+            self.host, self.event = packed.clone(), None
+
+    def wait(self) -> None:
+        if self.event is not None:
+            self.event.synchronize()
+
+
+def _reduce_ranks(x):
+    """(sum, count, min, max) over ranks, in rank order, of ``x``: [world, 4, GA * 8] bytes."""
+    s = x[:, 0].copy().view("<f8").sum(axis=0)
+    c = x[:, 1].copy().view("<i8").sum(axis=0)
+    mn = x[:, 2].copy().view("<f8").min(axis=0)
+    mx = x[:, 3].copy().view("<f8").max(axis=0)
+    return s, c, mn, mx
+
+
 class DistContext:
     def __init__(self, rank: int, world: int, backend: str, device=None):
         self.rank = rank
         self.world = world
         self.backend = backend
         self.device = device
+        self._pending_combines: list = []
 
     @staticmethod
     def from_env(init: bool = True, backend: Optional[str] = None) -> Optional["DistContext"]:
@@ -135,9 +164,18 @@ class DistContext:
             ev = torch.cuda.Event()
             ev.record()
         else:
-            parts = [torch.empty_like(packed, device="cpu") for _ in range(self.world)]
-            dist.all_gather(parts, packed.cpu())
-            h, ev = torch.cat(parts), None
+            # gloo (host-staged): the partials go to pinned memory stream-ordered now, and the
+            # collective waits until a result is asked for; every combine pending at that point
+            # travels in ONE all-gather (ranks submit and fetch in the same program order, so
+            # they coalesce the same entries)
+            ent = _PendingCombine(packed)
+            self._pending_combines.append(ent)
+
+            def fetch_gloo():
+                if ent.result is None:
+                    self._flush_combines()
+                return _reduce_ranks(ent.result.numpy().reshape(self.world, 4, GA * 8))
+            return fetch_gloo
 
         def fetch():
             if ev is not None:
@@ -149,6 +187,23 @@ class DistContext:
             mx = x[:, 3].copy().view(np.float64).max(axis=0)
             return s, c, mn, mx
         return fetch
+
+    def _flush_combines(self) -> None:
+        """One all-gather for every pending (gloo) partial-aggregate combine."""
+        import torch
+        import torch.distributed as dist
+        pend, self._pending_combines = self._pending_combines, []
+        for e in pend:
+            e.wait()
+        flat = torch.cat([e.host for e in pend])
+        parts = [torch.empty_like(flat) for _ in range(self.world)]
+        dist.all_gather(parts, flat)
+        allr = torch.stack(parts)             # [world, total bytes]
+        off = 0
+        for e in pend:
+            nb = e.host.numel()
+            e.result = allr[:, off:off + nb].contiguous()
+            off += nb
 
     def all_gather_rows(self, rows):
         """Concatenation over ranks (in rank order) of each rank's int64 ``[n_r, w]`` numpy
