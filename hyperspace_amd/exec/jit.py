@@ -1344,7 +1344,7 @@ def _deferred_append(NI: int, ind: str, pass_fmt: str, row_fmt: str, j_fmt: str)
     return b
 
 
-def _sparse_append(NI: int, ind: str, word: str, j_fmt: str) -> List[str]:
+def _sparse_append(NI: int, ind: str, word: str, j_fmt: str, drain=()) -> List[str]:
     """``_deferred_append`` for sparse matches: the thread's match bits ``word`` are appended
     one set bit per round, for as many rounds as the wavefront's busiest lane needs (a join
     keeping a few percent of its rows: one or two rounds instead of NI).  The item's row is
@@ -1361,7 +1361,7 @@ def _sparse_append(NI: int, ind: str, word: str, j_fmt: str) -> List[str]:
           f"{ind}    const int wp = has ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), "
           f"__builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;",
           f"{ind}    lrow_s[wv][wp] = (int)(g0 + it); lj_s[wv][wp] = (int)(ss + jv);",
-          f"{ind}    wcnt += __popcll(bm);",
+          f"{ind}    wcnt += __popcll(bm);"] + list(drain) + [
           f"{ind}  }}",
           f"{ind}}}"]
     return b
@@ -1477,7 +1477,9 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
     b: List[str] = []
     b += _acc_decls(aggs, grouped, args)
     W = BLOCK // 64  # noqa: N806
-    CAP = 64 * NI + 64  # noqa: N806 — list entries: < 64 carried over + one tile's appends
+    # list entries: < 64 carried over + one round's appends (all NI items per round, or one
+    # item per round with the sparse appends, which drain between rounds)
+    CAP = 128 if MJ_SPARSE else 64 * NI + 64  # noqa: N806
     NB = 2 if MJ_DBUF else 1  # noqa: N806
     b += [f"  __shared__ {KT} skeys_[{NB}][{LK + 1}]; __shared__ unsigned char spass_[{NB}][{LK}];",
           "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;"]
@@ -1634,13 +1636,17 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
                 b.extend(_eager_tail(args, cols, split, approx, aggs, grouped, p.group_col,
                                      allslots, rtail, NI, i2))
             else:
+                drain = _deferred_drain(args, cols, split, approx, aggs, grouped, p.group_col,
+                                        allslots, i2 + "    ", final=False, hk=hk)
                 if MJ_SPARSE:
-                    b.extend(_sparse_append(NI, i2, "pb", "jl{it}"))
+                    # drained inside the append rounds: the lists never hold more than 63 + 64
+                    # entries, so they take 6 KB of LDS per block instead of 20 KB
+                    b.extend(_sparse_append(NI, i2, "pb", "jl{it}", drain))
                 else:
                     b.extend(_deferred_append(NI, i2, "((pb >> {it}) & 1u)", "row{it}",
                                               "ss + jl{it}"))
-                b.extend(_deferred_drain(args, cols, split, approx, aggs, grouped, p.group_col,
-                                         allslots, i2, final=False, hk=hk))
+                    b.extend(_deferred_drain(args, cols, split, approx, aggs, grouped,
+                                             p.group_col, allslots, i2, final=False, hk=hk))
             b.append(f"{i2}}}")
 
         one_round(ind)
