@@ -94,7 +94,7 @@ MJ_BLOCK = int(os.environ.get("HS_JIT_MJ_BLOCK", "256"))
 # eager aggregate tail (no deferred match lists): _eager_tail
 MJ_EAGER = os.environ.get("HS_JIT_MJ_EAGER", "0") == "1"
 # match-list appends one set match bit per round (_sparse_append) instead of one per item
-MJ_SPARSE = os.environ.get("HS_JIT_MJ_SPARSE", "0") == "1"
+MJ_SPARSE = os.environ.get("HS_JIT_MJ_SPARSE", "1") == "1"
 MJ_KEY32 = os.environ.get("HS_JIT_MJ_KEY32", "1") == "1"  # 32-bit merge images (_key32_frame)
 # cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
 MJ_EXP = os.environ.get("HS_JIT_MJ_EXP", "")
