@@ -104,20 +104,32 @@ struct Args {
   const signed char* c3;
   long long B3;
   double R3;
+  const signed char* c10;
+  long long B10;
+  unsigned long long* hkeys;
+  double* hsum;
+  long long* hcnt;
+  long long HM;
+  long long* hflag;
+  long long HL0;
+  long long HS0;
+  long long HL1;
+  long long HS1;
+  long long HL2;
+  long long HS2;
   double A0_0;
   double B0_0;
   double A0_1;
   double B0_1;
 };
 extern "C" __global__ __launch_bounds__(256) void hs_jit_merge_join_agg(Args a) {
-  constexpr int NA = 3;
+  constexpr int NA = 2;
   double acc0 = 0.0; unsigned cnt0 = 0u;
   double acc1 = 0.0; unsigned cnt1 = 0u;
-  double acc2 = 0.0; unsigned cnt2 = 0u;
   __shared__ unsigned skeys_[1][2049]; __shared__ unsigned char spass_[1][2048];
-  constexpr int DUMP = 576;
-  __shared__ int lrow_s[4][640]; __shared__ int lj_s[4][640];
   const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  constexpr int DUMP = 128;
+  __shared__ int lrow_s[4][192]; __shared__ int lj_s[4][192];
   int wcnt = 0;   // wavefront-uniform length of this wavefront's (row, j) list
   const i64 ntiles = a.tile_prefix[a.R];
   const i64 per = (ntiles + gridDim.x - 1) / gridDim.x;
@@ -201,16 +213,20 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_merge_join_agg(Args a) 
       const int x9_s3 = (int)(a.B9 + (i64)w9_s3);
       if (sv0) { const bool kv = true;
         skeys[sq0] = kv ? ({ const i64 d_ = (i64)(x8_s0) - a.KLO; d_ < 0 ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }) : (unsigned)0;
-        spass[sq0] = (kv && ((true)) && ((true)) && ((true && (r9_s0 >= (int)a.CL4 && r9_s0 <= (int)a.CH4)))) ? 1 : 0; }
+        spass[sq0] = (kv && ((true)) && ((true)) && ((true && (r9_s0 >= (int)a.CL4 && r9_s0 <= (int)a.CH4)))) ? 1 : 0;
+      }
       if (sv1) { const bool kv = true;
         skeys[sq1] = kv ? ({ const i64 d_ = (i64)(x8_s1) - a.KLO; d_ < 0 ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }) : (unsigned)0;
-        spass[sq1] = (kv && ((true)) && ((true)) && ((true && (r9_s1 >= (int)a.CL4 && r9_s1 <= (int)a.CH4)))) ? 1 : 0; }
+        spass[sq1] = (kv && ((true)) && ((true)) && ((true && (r9_s1 >= (int)a.CL4 && r9_s1 <= (int)a.CH4)))) ? 1 : 0;
+      }
       if (sv2) { const bool kv = true;
         skeys[sq2] = kv ? ({ const i64 d_ = (i64)(x8_s2) - a.KLO; d_ < 0 ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }) : (unsigned)0;
-        spass[sq2] = (kv && ((true)) && ((true)) && ((true && (r9_s2 >= (int)a.CL4 && r9_s2 <= (int)a.CH4)))) ? 1 : 0; }
+        spass[sq2] = (kv && ((true)) && ((true)) && ((true && (r9_s2 >= (int)a.CL4 && r9_s2 <= (int)a.CH4)))) ? 1 : 0;
+      }
       if (sv3) { const bool kv = true;
         skeys[sq3] = kv ? ({ const i64 d_ = (i64)(x8_s3) - a.KLO; d_ < 0 ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }) : (unsigned)0;
-        spass[sq3] = (kv && ((true)) && ((true)) && ((true && (r9_s3 >= (int)a.CL4 && r9_s3 <= (int)a.CH4)))) ? 1 : 0; }
+        spass[sq3] = (kv && ((true)) && ((true)) && ((true && (r9_s3 >= (int)a.CL4 && r9_s3 <= (int)a.CH4)))) ? 1 : 0;
+      }
     }
     if (staged && threadIdx.x == 0) skeys[ns] = 0xFFFFFFFFu;   // walk sentinel
     const int r0_0 = (int)x0v[0];
@@ -466,61 +482,90 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_merge_join_agg(Args a) 
         const int x9_7 = (int)(a.B9 + (i64)w9_7);
         pb &= (((true)) && ((true)) && ((true && (r9_7 >= (int)a.CL4 && r9_7 <= (int)a.CH4)))) ? ~0u : ~128u; }
     }
-    { const bool pz = ((pb >> 0) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row0); lj_s[wv][wp] = (int)(ss + jl0);
-      wcnt += __popcll(bm); }
-    { const bool pz = ((pb >> 1) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row1); lj_s[wv][wp] = (int)(ss + jl1);
-      wcnt += __popcll(bm); }
-    { const bool pz = ((pb >> 2) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row2); lj_s[wv][wp] = (int)(ss + jl2);
-      wcnt += __popcll(bm); }
-    { const bool pz = ((pb >> 3) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row3); lj_s[wv][wp] = (int)(ss + jl3);
-      wcnt += __popcll(bm); }
-    { const bool pz = ((pb >> 4) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row4); lj_s[wv][wp] = (int)(ss + jl4);
-      wcnt += __popcll(bm); }
-    { const bool pz = ((pb >> 5) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row5); lj_s[wv][wp] = (int)(ss + jl5);
-      wcnt += __popcll(bm); }
-    { const bool pz = ((pb >> 6) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row6); lj_s[wv][wp] = (int)(ss + jl6);
-      wcnt += __popcll(bm); }
-    { const bool pz = ((pb >> 7) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row7); lj_s[wv][wp] = (int)(ss + jl7);
-      wcnt += __popcll(bm); }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    while (wcnt >= 64) {
-      const int cb = wcnt > 64 ? wcnt - 64 : 0;
-      const int ce = cb + cln;
-      bool cok = ce < wcnt;
-      const i64 crow = (i64)lrow_s[wv][cok ? ce : cb];
-      const i64 cj = (i64)lj_s[wv][cok ? ce : cb];
-      const int w2_c = a.c2[crow];
-      const int r2_c = (int)w2_c;
-      const i64 q2_c = a.B2 + (i64)w2_c;
-      const double x2_c = (double)((double)(a.B2 + (i64)w2_c) * a.R2);
-      const signed char w3_c = a.c3[crow];
-      const int r3_c = (int)w3_c;
-      const i64 q3_c = a.B3 + (i64)w3_c;
-      const double x3_c = (double)((double)(a.B3 + (i64)w3_c) * a.R3);
-      { const bool ok = cok && true; const double v = ok ? (a.A0_0 + a.B0_0 * (double)x2_c) * (a.A0_1 + a.B0_1 * (double)x3_c) : 0.0;
-        acc0 += v; cnt0 += ok ? 1u : 0u; }
-      { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
-        acc1 += v; cnt1 += ok ? 1u : 0u; }
-      { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
-        acc2 += v; cnt2 += ok ? 1u : 0u; }
-      wcnt = cb;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    { unsigned pend = pb;
+      while (__any(pend != 0u)) {
+        const bool has = pend != 0u;
+        const int it = has ? __builtin_ctz(pend) : 0;
+        pend &= pend - 1u;
+        int jv = jl0;
+        jv = it == 1 ? jl1 : jv;
+        jv = it == 2 ? jl2 : jv;
+        jv = it == 3 ? jl3 : jv;
+        jv = it == 4 ? jl4 : jv;
+        jv = it == 5 ? jl5 : jv;
+        jv = it == 6 ? jl6 : jv;
+        jv = it == 7 ? jl7 : jv;
+        const u64 bm = __ballot(has);
+        const int wp = has ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
+        lrow_s[wv][wp] = (int)(g0 + it); lj_s[wv][wp] = (int)(ss + jv);
+        wcnt += __popcll(bm);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        while (wcnt >= 64) {
+          const int cb = wcnt > 64 ? wcnt - 64 : 0;
+          const int ce = cb + cln;
+          bool cok = ce < wcnt;
+          const i64 crow = (i64)lrow_s[wv][cok ? ce : cb];
+          const i64 cj = (i64)lj_s[wv][cok ? ce : cb];
+          const int w2_c = a.c2[crow];
+          const int r2_c = (int)w2_c;
+          const i64 q2_c = a.B2 + (i64)w2_c;
+          const double x2_c = (double)((double)(a.B2 + (i64)w2_c) * a.R2);
+          const signed char w3_c = a.c3[crow];
+          const int r3_c = (int)w3_c;
+          const i64 q3_c = a.B3 + (i64)w3_c;
+          const double x3_c = (double)((double)(a.B3 + (i64)w3_c) * a.R3);
+          const int w0_c = a.c0[crow];
+          const int r0_c = (int)w0_c;
+          const long long x0_c = (long long)(a.B0 + (i64)w0_c);
+          const short w9_c = a.c9[cj];
+          const int r9_c = (int)w9_c;
+          const int x9_c = (int)(a.B9 + (i64)w9_c);
+          const signed char w10_c = a.c10[cj];
+          const int r10_c = (int)w10_c;
+          const int x10_c = (int)(a.B10 + (i64)w10_c);
+          { const int hln = (int)(threadIdx.x & 63u); const bool hok = cok;
+            u64 hk = 0ull; const bool hnul = false;
+            hk |= (u64)((i64)x0_c - a.HL0) << (unsigned)a.HS0;
+            hk |= (u64)((i64)x9_c - a.HL1) << (unsigned)a.HS1;
+            hk |= (u64)((i64)x10_c - a.HL2) << (unsigned)a.HS2;
+            const u64 hkp = __shfl_up(hk, 1u, 64);
+            const int hfp = __shfl_up((hok ? 1 : 0) | (hnul ? 2 : 0), 1u, 64);
+            const bool hsame = hln > 0 && hok && (hfp & 1) != 0 && ((hfp >> 1) & 1) == (hnul ? 1 : 0) && hkp == hk;
+            const u64 hH = __ballot(!hsame);
+            const int hss = 63 - __builtin_clzll(hH & ((2ull << hln) - 1ull));
+            const bool htl = hok && (hln == 63 || ((hH >> ((hln + 1) & 63)) & 1ull) != 0ull);
+            const bool hq0 = hok && true;
+            double hv0 = hq0 ? (double)((a.A0_0 + a.B0_0 * (double)x2_c) * (a.A0_1 + a.B0_1 * (double)x3_c)) : 0.0;
+            #pragma unroll
+            for (int hd = 1; hd < 64; hd <<= 1) {
+              const double u_hv0 = __shfl_up(hv0, (unsigned)hd, 64);
+              if (hln - hd >= hss) {
+                hv0 = hv0 + u_hv0;
+              }
+            }
+            if (htl) {
+              long long hs_ = -1;
+              if (hnul) hs_ = a.HM + 1; else if (hk == ~0ull) hs_ = a.HM; else {
+                u64 hh = hs_mix64(hk) & (u64)(a.HM - 1);
+                for (int pr_ = 0; pr_ < 512; ++pr_) {
+                  const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hk);
+                  if (pv_ == ~0ull || pv_ == hk) { hs_ = (long long)hh; break; }
+                  hh = (hh + 1ull) & (u64)(a.HM - 1);
+                }
+                if (hs_ < 0) a.hflag[0] = 1;
+              }
+              if (hs_ >= 0) {
+                const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
+                const unsigned long long hrn = (unsigned long long)(hln - hss + 1);
+                unsafeAtomicAdd(&a.hsum[0 * hst + hs_], hv0);
+                if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
+              }
+            }
+          }
+          wcnt = cb;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+      }
     }
     }
     if (a.rdup) while (true) {
@@ -625,61 +670,90 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_merge_join_agg(Args a) 
           const int x9_7 = (int)(a.B9 + (i64)w9_7);
           pb &= (((true)) && ((true)) && ((true && (r9_7 >= (int)a.CL4 && r9_7 <= (int)a.CH4)))) ? ~0u : ~128u; }
       }
-      { const bool pz = ((pb >> 0) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row0); lj_s[wv][wp] = (int)(ss + jl0);
-        wcnt += __popcll(bm); }
-      { const bool pz = ((pb >> 1) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row1); lj_s[wv][wp] = (int)(ss + jl1);
-        wcnt += __popcll(bm); }
-      { const bool pz = ((pb >> 2) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row2); lj_s[wv][wp] = (int)(ss + jl2);
-        wcnt += __popcll(bm); }
-      { const bool pz = ((pb >> 3) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row3); lj_s[wv][wp] = (int)(ss + jl3);
-        wcnt += __popcll(bm); }
-      { const bool pz = ((pb >> 4) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row4); lj_s[wv][wp] = (int)(ss + jl4);
-        wcnt += __popcll(bm); }
-      { const bool pz = ((pb >> 5) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row5); lj_s[wv][wp] = (int)(ss + jl5);
-        wcnt += __popcll(bm); }
-      { const bool pz = ((pb >> 6) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row6); lj_s[wv][wp] = (int)(ss + jl6);
-        wcnt += __popcll(bm); }
-      { const bool pz = ((pb >> 7) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row7); lj_s[wv][wp] = (int)(ss + jl7);
-        wcnt += __popcll(bm); }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      while (wcnt >= 64) {
-        const int cb = wcnt > 64 ? wcnt - 64 : 0;
-        const int ce = cb + cln;
-        bool cok = ce < wcnt;
-        const i64 crow = (i64)lrow_s[wv][cok ? ce : cb];
-        const i64 cj = (i64)lj_s[wv][cok ? ce : cb];
-        const int w2_c = a.c2[crow];
-        const int r2_c = (int)w2_c;
-        const i64 q2_c = a.B2 + (i64)w2_c;
-        const double x2_c = (double)((double)(a.B2 + (i64)w2_c) * a.R2);
-        const signed char w3_c = a.c3[crow];
-        const int r3_c = (int)w3_c;
-        const i64 q3_c = a.B3 + (i64)w3_c;
-        const double x3_c = (double)((double)(a.B3 + (i64)w3_c) * a.R3);
-        { const bool ok = cok && true; const double v = ok ? (a.A0_0 + a.B0_0 * (double)x2_c) * (a.A0_1 + a.B0_1 * (double)x3_c) : 0.0;
-          acc0 += v; cnt0 += ok ? 1u : 0u; }
-        { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
-          acc1 += v; cnt1 += ok ? 1u : 0u; }
-        { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
-          acc2 += v; cnt2 += ok ? 1u : 0u; }
-        wcnt = cb;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      { unsigned pend = pb;
+        while (__any(pend != 0u)) {
+          const bool has = pend != 0u;
+          const int it = has ? __builtin_ctz(pend) : 0;
+          pend &= pend - 1u;
+          int jv = jl0;
+          jv = it == 1 ? jl1 : jv;
+          jv = it == 2 ? jl2 : jv;
+          jv = it == 3 ? jl3 : jv;
+          jv = it == 4 ? jl4 : jv;
+          jv = it == 5 ? jl5 : jv;
+          jv = it == 6 ? jl6 : jv;
+          jv = it == 7 ? jl7 : jv;
+          const u64 bm = __ballot(has);
+          const int wp = has ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
+          lrow_s[wv][wp] = (int)(g0 + it); lj_s[wv][wp] = (int)(ss + jv);
+          wcnt += __popcll(bm);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          while (wcnt >= 64) {
+            const int cb = wcnt > 64 ? wcnt - 64 : 0;
+            const int ce = cb + cln;
+            bool cok = ce < wcnt;
+            const i64 crow = (i64)lrow_s[wv][cok ? ce : cb];
+            const i64 cj = (i64)lj_s[wv][cok ? ce : cb];
+            const int w2_c = a.c2[crow];
+            const int r2_c = (int)w2_c;
+            const i64 q2_c = a.B2 + (i64)w2_c;
+            const double x2_c = (double)((double)(a.B2 + (i64)w2_c) * a.R2);
+            const signed char w3_c = a.c3[crow];
+            const int r3_c = (int)w3_c;
+            const i64 q3_c = a.B3 + (i64)w3_c;
+            const double x3_c = (double)((double)(a.B3 + (i64)w3_c) * a.R3);
+            const int w0_c = a.c0[crow];
+            const int r0_c = (int)w0_c;
+            const long long x0_c = (long long)(a.B0 + (i64)w0_c);
+            const short w9_c = a.c9[cj];
+            const int r9_c = (int)w9_c;
+            const int x9_c = (int)(a.B9 + (i64)w9_c);
+            const signed char w10_c = a.c10[cj];
+            const int r10_c = (int)w10_c;
+            const int x10_c = (int)(a.B10 + (i64)w10_c);
+            { const int hln = (int)(threadIdx.x & 63u); const bool hok = cok;
+              u64 hk = 0ull; const bool hnul = false;
+              hk |= (u64)((i64)x0_c - a.HL0) << (unsigned)a.HS0;
+              hk |= (u64)((i64)x9_c - a.HL1) << (unsigned)a.HS1;
+              hk |= (u64)((i64)x10_c - a.HL2) << (unsigned)a.HS2;
+              const u64 hkp = __shfl_up(hk, 1u, 64);
+              const int hfp = __shfl_up((hok ? 1 : 0) | (hnul ? 2 : 0), 1u, 64);
+              const bool hsame = hln > 0 && hok && (hfp & 1) != 0 && ((hfp >> 1) & 1) == (hnul ? 1 : 0) && hkp == hk;
+              const u64 hH = __ballot(!hsame);
+              const int hss = 63 - __builtin_clzll(hH & ((2ull << hln) - 1ull));
+              const bool htl = hok && (hln == 63 || ((hH >> ((hln + 1) & 63)) & 1ull) != 0ull);
+              const bool hq0 = hok && true;
+              double hv0 = hq0 ? (double)((a.A0_0 + a.B0_0 * (double)x2_c) * (a.A0_1 + a.B0_1 * (double)x3_c)) : 0.0;
+              #pragma unroll
+              for (int hd = 1; hd < 64; hd <<= 1) {
+                const double u_hv0 = __shfl_up(hv0, (unsigned)hd, 64);
+                if (hln - hd >= hss) {
+                  hv0 = hv0 + u_hv0;
+                }
+              }
+              if (htl) {
+                long long hs_ = -1;
+                if (hnul) hs_ = a.HM + 1; else if (hk == ~0ull) hs_ = a.HM; else {
+                  u64 hh = hs_mix64(hk) & (u64)(a.HM - 1);
+                  for (int pr_ = 0; pr_ < 512; ++pr_) {
+                    const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hk);
+                    if (pv_ == ~0ull || pv_ == hk) { hs_ = (long long)hh; break; }
+                    hh = (hh + 1ull) & (u64)(a.HM - 1);
+                  }
+                  if (hs_ < 0) a.hflag[0] = 1;
+                }
+                if (hs_ >= 0) {
+                  const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
+                  const unsigned long long hrn = (unsigned long long)(hln - hss + 1);
+                  unsafeAtomicAdd(&a.hsum[0 * hst + hs_], hv0);
+                  if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
+                }
+              }
+            }
+            wcnt = cb;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          }
+        }
       }
       }
     }
@@ -733,16 +807,20 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_merge_join_agg(Args a) 
       const int x9_s3 = (int)(a.B9 + (i64)w9_s3);
       if (sv0) { const bool kv = true;
         skeys[sq0] = kv ? ({ const i64 d_ = (i64)(x8_s0) - a.KLO; d_ < 0 ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }) : (unsigned)0;
-        spass[sq0] = (kv && ((true)) && ((true)) && ((true && (r9_s0 >= (int)a.CL4 && r9_s0 <= (int)a.CH4)))) ? 1 : 0; }
+        spass[sq0] = (kv && ((true)) && ((true)) && ((true && (r9_s0 >= (int)a.CL4 && r9_s0 <= (int)a.CH4)))) ? 1 : 0;
+      }
       if (sv1) { const bool kv = true;
         skeys[sq1] = kv ? ({ const i64 d_ = (i64)(x8_s1) - a.KLO; d_ < 0 ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }) : (unsigned)0;
-        spass[sq1] = (kv && ((true)) && ((true)) && ((true && (r9_s1 >= (int)a.CL4 && r9_s1 <= (int)a.CH4)))) ? 1 : 0; }
+        spass[sq1] = (kv && ((true)) && ((true)) && ((true && (r9_s1 >= (int)a.CL4 && r9_s1 <= (int)a.CH4)))) ? 1 : 0;
+      }
       if (sv2) { const bool kv = true;
         skeys[sq2] = kv ? ({ const i64 d_ = (i64)(x8_s2) - a.KLO; d_ < 0 ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }) : (unsigned)0;
-        spass[sq2] = (kv && ((true)) && ((true)) && ((true && (r9_s2 >= (int)a.CL4 && r9_s2 <= (int)a.CH4)))) ? 1 : 0; }
+        spass[sq2] = (kv && ((true)) && ((true)) && ((true && (r9_s2 >= (int)a.CL4 && r9_s2 <= (int)a.CH4)))) ? 1 : 0;
+      }
       if (sv3) { const bool kv = true;
         skeys[sq3] = kv ? ({ const i64 d_ = (i64)(x8_s3) - a.KLO; d_ < 0 ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }) : (unsigned)0;
-        spass[sq3] = (kv && ((true)) && ((true)) && ((true && (r9_s3 >= (int)a.CL4 && r9_s3 <= (int)a.CH4)))) ? 1 : 0; }
+        spass[sq3] = (kv && ((true)) && ((true)) && ((true && (r9_s3 >= (int)a.CL4 && r9_s3 <= (int)a.CH4)))) ? 1 : 0;
+      }
     }
     if (staged && threadIdx.x == 0) skeys[ns] = 0xFFFFFFFFu;   // walk sentinel
     const int r0_0 = (int)x0v[0];
@@ -998,61 +1076,90 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_merge_join_agg(Args a) 
         const int x9_7 = (int)(a.B9 + (i64)w9_7);
         pb &= (((true)) && ((true)) && ((true && (r9_7 >= (int)a.CL4 && r9_7 <= (int)a.CH4)))) ? ~0u : ~128u; }
     }
-    { const bool pz = ((pb >> 0) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row0); lj_s[wv][wp] = (int)(ss + jl0);
-      wcnt += __popcll(bm); }
-    { const bool pz = ((pb >> 1) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row1); lj_s[wv][wp] = (int)(ss + jl1);
-      wcnt += __popcll(bm); }
-    { const bool pz = ((pb >> 2) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row2); lj_s[wv][wp] = (int)(ss + jl2);
-      wcnt += __popcll(bm); }
-    { const bool pz = ((pb >> 3) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row3); lj_s[wv][wp] = (int)(ss + jl3);
-      wcnt += __popcll(bm); }
-    { const bool pz = ((pb >> 4) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row4); lj_s[wv][wp] = (int)(ss + jl4);
-      wcnt += __popcll(bm); }
-    { const bool pz = ((pb >> 5) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row5); lj_s[wv][wp] = (int)(ss + jl5);
-      wcnt += __popcll(bm); }
-    { const bool pz = ((pb >> 6) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row6); lj_s[wv][wp] = (int)(ss + jl6);
-      wcnt += __popcll(bm); }
-    { const bool pz = ((pb >> 7) & 1u); const u64 bm = __ballot(pz);
-      const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-      lrow_s[wv][wp] = (int)(row7); lj_s[wv][wp] = (int)(ss + jl7);
-      wcnt += __popcll(bm); }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    while (wcnt >= 64) {
-      const int cb = wcnt > 64 ? wcnt - 64 : 0;
-      const int ce = cb + cln;
-      bool cok = ce < wcnt;
-      const i64 crow = (i64)lrow_s[wv][cok ? ce : cb];
-      const i64 cj = (i64)lj_s[wv][cok ? ce : cb];
-      const int w2_c = a.c2[crow];
-      const int r2_c = (int)w2_c;
-      const i64 q2_c = a.B2 + (i64)w2_c;
-      const double x2_c = (double)((double)(a.B2 + (i64)w2_c) * a.R2);
-      const signed char w3_c = a.c3[crow];
-      const int r3_c = (int)w3_c;
-      const i64 q3_c = a.B3 + (i64)w3_c;
-      const double x3_c = (double)((double)(a.B3 + (i64)w3_c) * a.R3);
-      { const bool ok = cok && true; const double v = ok ? (a.A0_0 + a.B0_0 * (double)x2_c) * (a.A0_1 + a.B0_1 * (double)x3_c) : 0.0;
-        acc0 += v; cnt0 += ok ? 1u : 0u; }
-      { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
-        acc1 += v; cnt1 += ok ? 1u : 0u; }
-      { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
-        acc2 += v; cnt2 += ok ? 1u : 0u; }
-      wcnt = cb;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    { unsigned pend = pb;
+      while (__any(pend != 0u)) {
+        const bool has = pend != 0u;
+        const int it = has ? __builtin_ctz(pend) : 0;
+        pend &= pend - 1u;
+        int jv = jl0;
+        jv = it == 1 ? jl1 : jv;
+        jv = it == 2 ? jl2 : jv;
+        jv = it == 3 ? jl3 : jv;
+        jv = it == 4 ? jl4 : jv;
+        jv = it == 5 ? jl5 : jv;
+        jv = it == 6 ? jl6 : jv;
+        jv = it == 7 ? jl7 : jv;
+        const u64 bm = __ballot(has);
+        const int wp = has ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
+        lrow_s[wv][wp] = (int)(g0 + it); lj_s[wv][wp] = (int)(ss + jv);
+        wcnt += __popcll(bm);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        while (wcnt >= 64) {
+          const int cb = wcnt > 64 ? wcnt - 64 : 0;
+          const int ce = cb + cln;
+          bool cok = ce < wcnt;
+          const i64 crow = (i64)lrow_s[wv][cok ? ce : cb];
+          const i64 cj = (i64)lj_s[wv][cok ? ce : cb];
+          const int w2_c = a.c2[crow];
+          const int r2_c = (int)w2_c;
+          const i64 q2_c = a.B2 + (i64)w2_c;
+          const double x2_c = (double)((double)(a.B2 + (i64)w2_c) * a.R2);
+          const signed char w3_c = a.c3[crow];
+          const int r3_c = (int)w3_c;
+          const i64 q3_c = a.B3 + (i64)w3_c;
+          const double x3_c = (double)((double)(a.B3 + (i64)w3_c) * a.R3);
+          const int w0_c = a.c0[crow];
+          const int r0_c = (int)w0_c;
+          const long long x0_c = (long long)(a.B0 + (i64)w0_c);
+          const short w9_c = a.c9[cj];
+          const int r9_c = (int)w9_c;
+          const int x9_c = (int)(a.B9 + (i64)w9_c);
+          const signed char w10_c = a.c10[cj];
+          const int r10_c = (int)w10_c;
+          const int x10_c = (int)(a.B10 + (i64)w10_c);
+          { const int hln = (int)(threadIdx.x & 63u); const bool hok = cok;
+            u64 hk = 0ull; const bool hnul = false;
+            hk |= (u64)((i64)x0_c - a.HL0) << (unsigned)a.HS0;
+            hk |= (u64)((i64)x9_c - a.HL1) << (unsigned)a.HS1;
+            hk |= (u64)((i64)x10_c - a.HL2) << (unsigned)a.HS2;
+            const u64 hkp = __shfl_up(hk, 1u, 64);
+            const int hfp = __shfl_up((hok ? 1 : 0) | (hnul ? 2 : 0), 1u, 64);
+            const bool hsame = hln > 0 && hok && (hfp & 1) != 0 && ((hfp >> 1) & 1) == (hnul ? 1 : 0) && hkp == hk;
+            const u64 hH = __ballot(!hsame);
+            const int hss = 63 - __builtin_clzll(hH & ((2ull << hln) - 1ull));
+            const bool htl = hok && (hln == 63 || ((hH >> ((hln + 1) & 63)) & 1ull) != 0ull);
+            const bool hq0 = hok && true;
+            double hv0 = hq0 ? (double)((a.A0_0 + a.B0_0 * (double)x2_c) * (a.A0_1 + a.B0_1 * (double)x3_c)) : 0.0;
+            #pragma unroll
+            for (int hd = 1; hd < 64; hd <<= 1) {
+              const double u_hv0 = __shfl_up(hv0, (unsigned)hd, 64);
+              if (hln - hd >= hss) {
+                hv0 = hv0 + u_hv0;
+              }
+            }
+            if (htl) {
+              long long hs_ = -1;
+              if (hnul) hs_ = a.HM + 1; else if (hk == ~0ull) hs_ = a.HM; else {
+                u64 hh = hs_mix64(hk) & (u64)(a.HM - 1);
+                for (int pr_ = 0; pr_ < 512; ++pr_) {
+                  const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hk);
+                  if (pv_ == ~0ull || pv_ == hk) { hs_ = (long long)hh; break; }
+                  hh = (hh + 1ull) & (u64)(a.HM - 1);
+                }
+                if (hs_ < 0) a.hflag[0] = 1;
+              }
+              if (hs_ >= 0) {
+                const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
+                const unsigned long long hrn = (unsigned long long)(hln - hss + 1);
+                unsafeAtomicAdd(&a.hsum[0 * hst + hs_], hv0);
+                if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
+              }
+            }
+          }
+          wcnt = cb;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+      }
     }
     }
     if (a.rdup) while (true) {
@@ -1157,61 +1264,90 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_merge_join_agg(Args a) 
           const int x9_7 = (int)(a.B9 + (i64)w9_7);
           pb &= (((true)) && ((true)) && ((true && (r9_7 >= (int)a.CL4 && r9_7 <= (int)a.CH4)))) ? ~0u : ~128u; }
       }
-      { const bool pz = ((pb >> 0) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row0); lj_s[wv][wp] = (int)(ss + jl0);
-        wcnt += __popcll(bm); }
-      { const bool pz = ((pb >> 1) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row1); lj_s[wv][wp] = (int)(ss + jl1);
-        wcnt += __popcll(bm); }
-      { const bool pz = ((pb >> 2) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row2); lj_s[wv][wp] = (int)(ss + jl2);
-        wcnt += __popcll(bm); }
-      { const bool pz = ((pb >> 3) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row3); lj_s[wv][wp] = (int)(ss + jl3);
-        wcnt += __popcll(bm); }
-      { const bool pz = ((pb >> 4) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row4); lj_s[wv][wp] = (int)(ss + jl4);
-        wcnt += __popcll(bm); }
-      { const bool pz = ((pb >> 5) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row5); lj_s[wv][wp] = (int)(ss + jl5);
-        wcnt += __popcll(bm); }
-      { const bool pz = ((pb >> 6) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row6); lj_s[wv][wp] = (int)(ss + jl6);
-        wcnt += __popcll(bm); }
-      { const bool pz = ((pb >> 7) & 1u); const u64 bm = __ballot(pz);
-        const int wp = pz ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
-        lrow_s[wv][wp] = (int)(row7); lj_s[wv][wp] = (int)(ss + jl7);
-        wcnt += __popcll(bm); }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      while (wcnt >= 64) {
-        const int cb = wcnt > 64 ? wcnt - 64 : 0;
-        const int ce = cb + cln;
-        bool cok = ce < wcnt;
-        const i64 crow = (i64)lrow_s[wv][cok ? ce : cb];
-        const i64 cj = (i64)lj_s[wv][cok ? ce : cb];
-        const int w2_c = a.c2[crow];
-        const int r2_c = (int)w2_c;
-        const i64 q2_c = a.B2 + (i64)w2_c;
-        const double x2_c = (double)((double)(a.B2 + (i64)w2_c) * a.R2);
-        const signed char w3_c = a.c3[crow];
-        const int r3_c = (int)w3_c;
-        const i64 q3_c = a.B3 + (i64)w3_c;
-        const double x3_c = (double)((double)(a.B3 + (i64)w3_c) * a.R3);
-        { const bool ok = cok && true; const double v = ok ? (a.A0_0 + a.B0_0 * (double)x2_c) * (a.A0_1 + a.B0_1 * (double)x3_c) : 0.0;
-          acc0 += v; cnt0 += ok ? 1u : 0u; }
-        { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
-          acc1 += v; cnt1 += ok ? 1u : 0u; }
-        { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
-          acc2 += v; cnt2 += ok ? 1u : 0u; }
-        wcnt = cb;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      { unsigned pend = pb;
+        while (__any(pend != 0u)) {
+          const bool has = pend != 0u;
+          const int it = has ? __builtin_ctz(pend) : 0;
+          pend &= pend - 1u;
+          int jv = jl0;
+          jv = it == 1 ? jl1 : jv;
+          jv = it == 2 ? jl2 : jv;
+          jv = it == 3 ? jl3 : jv;
+          jv = it == 4 ? jl4 : jv;
+          jv = it == 5 ? jl5 : jv;
+          jv = it == 6 ? jl6 : jv;
+          jv = it == 7 ? jl7 : jv;
+          const u64 bm = __ballot(has);
+          const int wp = has ? wcnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) : DUMP + cln;
+          lrow_s[wv][wp] = (int)(g0 + it); lj_s[wv][wp] = (int)(ss + jv);
+          wcnt += __popcll(bm);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          while (wcnt >= 64) {
+            const int cb = wcnt > 64 ? wcnt - 64 : 0;
+            const int ce = cb + cln;
+            bool cok = ce < wcnt;
+            const i64 crow = (i64)lrow_s[wv][cok ? ce : cb];
+            const i64 cj = (i64)lj_s[wv][cok ? ce : cb];
+            const int w2_c = a.c2[crow];
+            const int r2_c = (int)w2_c;
+            const i64 q2_c = a.B2 + (i64)w2_c;
+            const double x2_c = (double)((double)(a.B2 + (i64)w2_c) * a.R2);
+            const signed char w3_c = a.c3[crow];
+            const int r3_c = (int)w3_c;
+            const i64 q3_c = a.B3 + (i64)w3_c;
+            const double x3_c = (double)((double)(a.B3 + (i64)w3_c) * a.R3);
+            const int w0_c = a.c0[crow];
+            const int r0_c = (int)w0_c;
+            const long long x0_c = (long long)(a.B0 + (i64)w0_c);
+            const short w9_c = a.c9[cj];
+            const int r9_c = (int)w9_c;
+            const int x9_c = (int)(a.B9 + (i64)w9_c);
+            const signed char w10_c = a.c10[cj];
+            const int r10_c = (int)w10_c;
+            const int x10_c = (int)(a.B10 + (i64)w10_c);
+            { const int hln = (int)(threadIdx.x & 63u); const bool hok = cok;
+              u64 hk = 0ull; const bool hnul = false;
+              hk |= (u64)((i64)x0_c - a.HL0) << (unsigned)a.HS0;
+              hk |= (u64)((i64)x9_c - a.HL1) << (unsigned)a.HS1;
+              hk |= (u64)((i64)x10_c - a.HL2) << (unsigned)a.HS2;
+              const u64 hkp = __shfl_up(hk, 1u, 64);
+              const int hfp = __shfl_up((hok ? 1 : 0) | (hnul ? 2 : 0), 1u, 64);
+              const bool hsame = hln > 0 && hok && (hfp & 1) != 0 && ((hfp >> 1) & 1) == (hnul ? 1 : 0) && hkp == hk;
+              const u64 hH = __ballot(!hsame);
+              const int hss = 63 - __builtin_clzll(hH & ((2ull << hln) - 1ull));
+              const bool htl = hok && (hln == 63 || ((hH >> ((hln + 1) & 63)) & 1ull) != 0ull);
+              const bool hq0 = hok && true;
+              double hv0 = hq0 ? (double)((a.A0_0 + a.B0_0 * (double)x2_c) * (a.A0_1 + a.B0_1 * (double)x3_c)) : 0.0;
+              #pragma unroll
+              for (int hd = 1; hd < 64; hd <<= 1) {
+                const double u_hv0 = __shfl_up(hv0, (unsigned)hd, 64);
+                if (hln - hd >= hss) {
+                  hv0 = hv0 + u_hv0;
+                }
+              }
+              if (htl) {
+                long long hs_ = -1;
+                if (hnul) hs_ = a.HM + 1; else if (hk == ~0ull) hs_ = a.HM; else {
+                  u64 hh = hs_mix64(hk) & (u64)(a.HM - 1);
+                  for (int pr_ = 0; pr_ < 512; ++pr_) {
+                    const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hk);
+                    if (pv_ == ~0ull || pv_ == hk) { hs_ = (long long)hh; break; }
+                    hh = (hh + 1ull) & (u64)(a.HM - 1);
+                  }
+                  if (hs_ < 0) a.hflag[0] = 1;
+                }
+                if (hs_ >= 0) {
+                  const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
+                  const unsigned long long hrn = (unsigned long long)(hln - hss + 1);
+                  unsafeAtomicAdd(&a.hsum[0 * hst + hs_], hv0);
+                  if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
+                }
+              }
+            }
+            wcnt = cb;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          }
+        }
       }
       }
     }
@@ -1233,36 +1369,55 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_merge_join_agg(Args a) 
     const int r3_c = (int)w3_c;
     const i64 q3_c = a.B3 + (i64)w3_c;
     const double x3_c = (double)((double)(a.B3 + (i64)w3_c) * a.R3);
-    { const bool ok = cok && true; const double v = ok ? (a.A0_0 + a.B0_0 * (double)x2_c) * (a.A0_1 + a.B0_1 * (double)x3_c) : 0.0;
-      acc0 += v; cnt0 += ok ? 1u : 0u; }
-    { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
-      acc1 += v; cnt1 += ok ? 1u : 0u; }
-    { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
-      acc2 += v; cnt2 += ok ? 1u : 0u; }
+    const int w0_c = a.c0[crow];
+    const int r0_c = (int)w0_c;
+    const long long x0_c = (long long)(a.B0 + (i64)w0_c);
+    const short w9_c = a.c9[cj];
+    const int r9_c = (int)w9_c;
+    const int x9_c = (int)(a.B9 + (i64)w9_c);
+    const signed char w10_c = a.c10[cj];
+    const int r10_c = (int)w10_c;
+    const int x10_c = (int)(a.B10 + (i64)w10_c);
+    { const int hln = (int)(threadIdx.x & 63u); const bool hok = cok;
+      u64 hk = 0ull; const bool hnul = false;
+      hk |= (u64)((i64)x0_c - a.HL0) << (unsigned)a.HS0;
+      hk |= (u64)((i64)x9_c - a.HL1) << (unsigned)a.HS1;
+      hk |= (u64)((i64)x10_c - a.HL2) << (unsigned)a.HS2;
+      const u64 hkp = __shfl_up(hk, 1u, 64);
+      const int hfp = __shfl_up((hok ? 1 : 0) | (hnul ? 2 : 0), 1u, 64);
+      const bool hsame = hln > 0 && hok && (hfp & 1) != 0 && ((hfp >> 1) & 1) == (hnul ? 1 : 0) && hkp == hk;
+      const u64 hH = __ballot(!hsame);
+      const int hss = 63 - __builtin_clzll(hH & ((2ull << hln) - 1ull));
+      const bool htl = hok && (hln == 63 || ((hH >> ((hln + 1) & 63)) & 1ull) != 0ull);
+      const bool hq0 = hok && true;
+      double hv0 = hq0 ? (double)((a.A0_0 + a.B0_0 * (double)x2_c) * (a.A0_1 + a.B0_1 * (double)x3_c)) : 0.0;
+      #pragma unroll
+      for (int hd = 1; hd < 64; hd <<= 1) {
+        const double u_hv0 = __shfl_up(hv0, (unsigned)hd, 64);
+        if (hln - hd >= hss) {
+          hv0 = hv0 + u_hv0;
+        }
+      }
+      if (htl) {
+        long long hs_ = -1;
+        if (hnul) hs_ = a.HM + 1; else if (hk == ~0ull) hs_ = a.HM; else {
+          u64 hh = hs_mix64(hk) & (u64)(a.HM - 1);
+          for (int pr_ = 0; pr_ < 512; ++pr_) {
+            const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hk);
+            if (pv_ == ~0ull || pv_ == hk) { hs_ = (long long)hh; break; }
+            hh = (hh + 1ull) & (u64)(a.HM - 1);
+          }
+          if (hs_ < 0) a.hflag[0] = 1;
+        }
+        if (hs_ >= 0) {
+          const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
+          const unsigned long long hrn = (unsigned long long)(hln - hss + 1);
+          unsafeAtomicAdd(&a.hsum[0 * hst + hs_], hv0);
+          if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
+        }
+      }
+    }
     wcnt = cb;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-  __shared__ double rv[4][NA]; __shared__ i64 rc[4][NA];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  { const double r = wsum(acc0); const i64 c = wsumi((i64)cnt0); if (lane == 0) { rv[w][0] = r; rc[w][0] = c; } }
-  { const double r = wsum(acc1); const i64 c = wsumi((i64)cnt1); if (lane == 0) { rv[w][1] = r; rc[w][1] = c; } }
-  { const double r = wsum(acc2); const i64 c = wsumi((i64)cnt2); if (lane == 0) { rv[w][2] = r; rc[w][2] = c; } }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    { double t = 0.0; i64 c = 0;
-      for (int k = 0; k < 4; ++k) { t = t + rv[k][0]; c += rc[k][0]; }
-      const i64 o = (i64)blockIdx.x * NA + 0;
-      a.psum[o] = t; a.pcnt[o] = c;
-      a.pmin[o] = __builtin_inf(); a.pmax[o] = -__builtin_inf(); }
-    { double t = 0.0; i64 c = 0;
-      for (int k = 0; k < 4; ++k) { t = t + rv[k][1]; c += rc[k][1]; }
-      const i64 o = (i64)blockIdx.x * NA + 1;
-      a.psum[o] = t; a.pcnt[o] = c;
-      a.pmin[o] = __builtin_inf(); a.pmax[o] = -__builtin_inf(); }
-    { double t = 0.0; i64 c = 0;
-      for (int k = 0; k < 4; ++k) { t = t + rv[k][2]; c += rc[k][2]; }
-      const i64 o = (i64)blockIdx.x * NA + 2;
-      a.psum[o] = t; a.pcnt[o] = c;
-      a.pmin[o] = __builtin_inf(); a.pmax[o] = -__builtin_inf(); }
   }
 }
