@@ -1804,7 +1804,7 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
     max_tiles = nrows // T + 2 * rstart.numel() + 2
     tp, spans = _join_spans(p, rstart, rlen, rbucket, roff, max_tiles, T, cache_spans, align=NI)
     k = kernel_for(merge_join_shape(p, compacts, hk), lambda: gen_merge_join_agg(p, compacts, hk))
-    grid = MJ_GRID * (256 // MJ_BLOCK)
+    grid = max(1, MJ_GRID * 256 // MJ_BLOCK)
     if hk is not None:
         v = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
              "spans": spans.data_ptr(), "R": rstart.numel(), "nrows": nrows, "rdup": int(rdup),
