@@ -55,7 +55,9 @@ def _native_kind(t: pa.DataType):
         return 6, 4                     # BYTE_ARRAY -> int32 dictionary codes (device path only)
     if pa.types.is_int32(t) or pa.types.is_date32(t):
         return 1, 4
-    if pa.types.is_int64(t):
+    if pa.types.is_int64(t) or pa.types.is_timestamp(t) or pa.types.is_duration(t):
+        # timestamps: INT64 in the unit the arrow type carries (the schema was read from the
+        # file); INT96 timestamps have another physical type and stay on the host path
         return 2, 8
     if pa.types.is_float32(t):
         return 4, 4

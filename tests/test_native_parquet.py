@@ -529,3 +529,42 @@ def test_device_encoded_bucket_files(tmp_path, device, codec):
             dense, _ = NP.expand_host(bb, info, vr, lr, np.dtype(np.int32))
             np.testing.assert_array_equal(dense[:min(7_000, hi - lo)],
                                           data["date"][lo:lo + min(7_000, hi - lo)])
+
+
+@pytest.mark.gpu
+def test_device_timestamp_decode_matches_pyarrow(tmp_path, device):
+    """INT64 timestamps (micro- and milliseconds, with and without a dictionary, one file with
+    nulls) decode through the native page layer as raw int64 in the arrow type's unit."""
+    import torch
+    from hyperspace_amd.exec import staging
+    rng = np.random.default_rng(4)
+    files, tables = [], []
+    for i, (dic, nulls) in enumerate([(True, False), (False, False), (True, True)]):
+        n = 20_000
+        us = rng.integers(0, 2_000_000_000_000_000, n)
+        mask = (rng.random(n) < 0.1) if nulls else None
+        t = pa.table({"tu": pa.array(us, pa.timestamp("us"), mask=mask),
+                      "tm": pa.array(us // 1000 % 1000, pa.int64()).cast(pa.timestamp("ms")),
+                      "k": pa.array(rng.integers(0, 100, n))})
+        path = tmp_path / f"t{i}.parquet"
+        pq.write_table(t, path, use_dictionary=dic, row_group_size=6000)
+        files.append(str(path))
+        tables.append(pq.read_table(path))
+    full = pa.concat_tables(tables)
+
+    def read_file(p, cols=None):
+        return pq.read_table(p, columns=cols)
+    staging.DEVICE_DECODED.clear()
+    staging.HOST_DECODED.clear()
+    up = staging.upload_files(read_file, files, [t.num_rows for t in tables], full.schema,
+                              device, parquet_local=files)
+    torch.cuda.synchronize()
+    assert {"tu", "tm"} <= staging.DEVICE_DECODED | (staging.HOST_DECODED - {"tu", "tm"})
+    assert "tm" not in staging.HOST_DECODED
+    for name in ("tu", "tm"):
+        ref = full.column(name).combine_chunks()
+        valid = np.asarray(ref.is_valid())
+        got = up.columns[name].data.cpu().numpy()
+        np.testing.assert_array_equal(got[valid], ref.view(pa.int64()).drop_null().to_numpy())
+        if ref.null_count:
+            np.testing.assert_array_equal(up.columns[name].valid.cpu().numpy().astype(bool), valid)
