@@ -34,20 +34,34 @@ struct ScanParams {
 // Range search: for each selected bucket, [lower, upper) of the sorted key within the bucket.
 // bounds are sortable images (hs_sortable) of the literal; nulls sort first and never match.
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ int64_t lb_sorted(const ColDesc& c, int64_t lo, int64_t hi, uint64_t key,
-                                             bool upper) {
-  while (lo < hi) {
-    const int64_t mid = lo + ((hi - lo) >> 1);
-    bool less;
-    if (!col_valid(c, mid)) {
-      less = true;
-    } else {
-      const uint64_t v = hs_sortable(c, mid);
-      less = upper ? (v <= key) : (v < key);
-    }
-    if (less) lo = mid + 1; else hi = mid;
+// One wavefront per range: lanes 0-31 search the lower bound and lanes 32-63 the upper bound,
+// each half with a 32-ary search (32 pivots per step, one ballot): log32(bucket rows) steps of
+// one coalesced load each instead of ~2 x log2 dependent loads of a thread-per-bucket search
+// (a 3M-row bucket: 5 round trips instead of 44).
+#define RANGE_WAVES 4
+
+// first index in [lo, hi] whose row is NOT "less": less = null (nulls sort first) or, for a
+// valid row, sortable < key (upper: <= key); key_mode 2 = only the null prefix
+__device__ __forceinline__ bool range_less(const ColDesc& c, int64_t r, uint64_t key, int mode) {
+  if (!col_valid(c, r)) return true;
+  if (mode == 2) return false;
+  const uint64_t v = hs_sortable(c, r);
+  return mode == 1 ? (v <= key) : (v < key);
+}
+
+__device__ __forceinline__ int64_t kary_bound(const ColDesc& c, int64_t lo, int64_t hi,
+                                              uint64_t key, int mode, int gl, int half) {
+  while (hi - lo > 32) {
+    const int64_t span = hi - lo;
+    const bool less = range_less(c, lo + span * (gl + 1) / 33, key, mode);
+    const int cnt = __popc((uint32_t)(__ballot(less) >> (half * 32)));
+    const int64_t nlo = cnt == 0 ? lo : lo + span * cnt / 33 + 1;
+    const int64_t nhi = cnt == 32 ? hi : lo + span * (cnt + 1) / 33;
+    lo = nlo;
+    hi = nhi;
   }
-  return lo;
+  const bool less = lo + gl < hi && range_less(c, lo + gl, key, mode);
+  return lo + __popc((uint32_t)(__ballot(less) >> (half * 32)));
 }
 
 __device__ __forceinline__ void range_one(const ColDesc& key, const int64_t* __restrict__ bucket_off,
@@ -55,58 +69,53 @@ __device__ __forceinline__ void range_one(const ColDesc& key, const int64_t* __r
                                           uint64_t lo_key, int lo_incl, int has_hi,
                                           uint64_t hi_key, int hi_incl, int64_t* __restrict__ rstart,
                                           int64_t* __restrict__ rlen, int32_t* __restrict__ rbucket) {
+  const int lane = threadIdx.x & 63, half = lane >> 5, gl = lane & 31;
   const int b = buckets ? buckets[i] : i;
   const int64_t s = bucket_off[b], e = bucket_off[b + 1];
-  int64_t first_valid = s;
-  if (key.valid != nullptr) {
-    int64_t lo = s, hi = e;
-    while (lo < hi) {
-      const int64_t mid = lo + ((hi - lo) >> 1);
-      if (!col_valid(key, mid)) lo = mid + 1; else hi = mid;
-    }
-    first_valid = lo;
-  }
-  int64_t a = first_valid, z = e;
-  if (has_lo) a = lb_sorted(key, first_valid, e, lo_key, !lo_incl);
-  if (has_hi) z = lb_sorted(key, first_valid, e, hi_key, hi_incl);
+  const int64_t first_valid = key.valid != nullptr ? kary_bound(key, s, e, 0, 2, gl, half) : s;
+  int64_t r;
+  if (half == 0) r = has_lo ? kary_bound(key, first_valid, e, lo_key, lo_incl ? 0 : 1, gl, 0)
+                            : first_valid;
+  else r = has_hi ? kary_bound(key, first_valid, e, hi_key, hi_incl ? 1 : 0, gl, 1) : e;
+  const int64_t a = __shfl(r, 0, 64);
+  int64_t z = __shfl(r, 32, 64);
   if (z < a) z = a;
-  rstart[i] = a;
-  rlen[i] = z - a;
-  if (rbucket) rbucket[i] = b;
+  if (lane == 0) {
+    rstart[i] = a;
+    rlen[i] = z - a;
+    if (rbucket) rbucket[i] = b;
+  }
 }
 
-__global__ void hs_range_search_kernel(ColDesc key, const int64_t* __restrict__ bucket_off,
-                                       const int32_t* __restrict__ buckets, int nb, int has_lo,
-                                       uint64_t lo_key, int lo_incl, int has_hi, uint64_t hi_key,
-                                       int hi_incl, int64_t* __restrict__ rstart,
-                                       int64_t* __restrict__ rlen, int32_t* __restrict__ rbucket) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nb) return;
+__global__ __launch_bounds__(64 * RANGE_WAVES) void hs_range_search_kernel(
+    ColDesc key, const int64_t* __restrict__ bucket_off, const int32_t* __restrict__ buckets,
+    int nb, int has_lo, uint64_t lo_key, int lo_incl, int has_hi, uint64_t hi_key, int hi_incl,
+    int64_t* __restrict__ rstart, int64_t* __restrict__ rlen, int32_t* __restrict__ rbucket) {
+  const int i = blockIdx.x * RANGE_WAVES + (threadIdx.x >> 6);
+  if (i >= nb) return;   // wave-uniform
   range_one(key, bucket_off, buckets, i, has_lo, lo_key, lo_incl, has_hi, hi_key, hi_incl, rstart,
             rlen, rbucket);
 }
 
 // Key probes: for probe i, the rows of bucket pbucket[i] whose sorted key equals the sortable
-// image pkey[i] (one binary-search pair per probe).  Drives a join from a small, filtered side
+// image pkey[i] (one bound pair per probe).  Drives a join from a small, filtered side
 // into a large index sorted by the join key: only the matching key runs are scanned.
-__global__ void hs_probe_ranges_kernel(ColDesc key, const int64_t* __restrict__ bucket_off,
-                                       const int32_t* __restrict__ pbucket,
-                                       const uint64_t* __restrict__ pkey, int np,
-                                       int64_t* __restrict__ rstart, int64_t* __restrict__ rlen,
-                                       int32_t* __restrict__ rbucket) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(64 * RANGE_WAVES) void hs_probe_ranges_kernel(
+    ColDesc key, const int64_t* __restrict__ bucket_off, const int32_t* __restrict__ pbucket,
+    const uint64_t* __restrict__ pkey, int np, int64_t* __restrict__ rstart,
+    int64_t* __restrict__ rlen, int32_t* __restrict__ rbucket) {
+  const int i = blockIdx.x * RANGE_WAVES + (threadIdx.x >> 6);
   if (i >= np) return;
   range_one(key, bucket_off, pbucket, i, 1, pkey[i], 1, 1, pkey[i], 1, rstart, rlen, rbucket);
 }
 
 // Bounds read from device memory (int64 x6: has_lo, lo, lo_incl, has_hi, hi, hi_incl), so a
 // captured hipGraph replays with new literals after one H2D of the parameter block.
-__global__ void hs_range_search_dev_kernel(ColDesc key, const int64_t* __restrict__ bucket_off,
-                                           const int32_t* __restrict__ buckets, int nb,
-                                           const int64_t* __restrict__ bp,
-                                           int64_t* __restrict__ rstart,
-                                           int64_t* __restrict__ rlen, int32_t* __restrict__ rbucket) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(64 * RANGE_WAVES) void hs_range_search_dev_kernel(
+    ColDesc key, const int64_t* __restrict__ bucket_off, const int32_t* __restrict__ buckets,
+    int nb, const int64_t* __restrict__ bp, int64_t* __restrict__ rstart,
+    int64_t* __restrict__ rlen, int32_t* __restrict__ rbucket) {
+  const int i = blockIdx.x * RANGE_WAVES + (threadIdx.x >> 6);
   if (i >= nb) return;
   range_one(key, bucket_off, buckets, i, (int)bp[0], (uint64_t)bp[1], (int)bp[2], (int)bp[3],
             (uint64_t)bp[4], (int)bp[5], rstart, rlen, rbucket);
@@ -353,7 +362,8 @@ int hs_range_search_dev(const ColDesc* key, const int64_t* bucket_off, const int
                         int nb, const int64_t* dparams, int64_t* rstart, int64_t* rlen,
                         int32_t* rbucket, void* stream) {
   if (nb <= 0) return 0;
-  hipLaunchKernelGGL(hs_range_search_dev_kernel, dim3((nb + 255) / 256), dim3(256), 0,
+  hipLaunchKernelGGL(hs_range_search_dev_kernel, dim3((nb + RANGE_WAVES - 1) / RANGE_WAVES),
+                     dim3(64 * RANGE_WAVES), 0,
                      (hipStream_t)stream, *key, bucket_off, buckets, nb, dparams, rstart, rlen,
                      rbucket);
   return (int)hipGetLastError();
@@ -363,7 +373,8 @@ int hs_range_search(const ColDesc* key, const int64_t* bucket_off, const int32_t
                     int has_lo, uint64_t lo_key, int lo_incl, int has_hi, uint64_t hi_key,
                     int hi_incl, int64_t* rstart, int64_t* rlen, int32_t* rbucket, void* stream) {
   if (nb <= 0) return 0;
-  hipLaunchKernelGGL(hs_range_search_kernel, dim3((nb + 255) / 256), dim3(256), 0,
+  hipLaunchKernelGGL(hs_range_search_kernel, dim3((nb + RANGE_WAVES - 1) / RANGE_WAVES),
+                     dim3(64 * RANGE_WAVES), 0,
                      (hipStream_t)stream, *key, bucket_off, buckets, nb, has_lo, lo_key, lo_incl,
                      has_hi, hi_key, hi_incl, rstart, rlen, rbucket);
   return (int)hipGetLastError();
@@ -373,7 +384,8 @@ int hs_probe_ranges(const ColDesc* key, const int64_t* bucket_off, const int32_t
                     const uint64_t* pkey, int np, int64_t* rstart, int64_t* rlen, int32_t* rbucket,
                     void* stream) {
   if (np <= 0) return 0;
-  hipLaunchKernelGGL(hs_probe_ranges_kernel, dim3((np + 255) / 256), dim3(256), 0,
+  hipLaunchKernelGGL(hs_probe_ranges_kernel, dim3((np + RANGE_WAVES - 1) / RANGE_WAVES),
+                     dim3(64 * RANGE_WAVES), 0,
                      (hipStream_t)stream, *key, bucket_off, pbucket, pkey, np, rstart, rlen,
                      rbucket);
   return (int)hipGetLastError();
