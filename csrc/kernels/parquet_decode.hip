@@ -331,7 +331,8 @@ __global__ __launch_bounds__(256) void hs_pq_inflate_kernel(
   if (pi >= npages) return;               // wavefront-local from here on: no block barriers
   const HsPqPage p = pages[pi];
   if (p.codec == 2) return;               // inflated on the host (dst = its device copy)
-  const uint8_t* in = raw + p.src;
+  // raw == nullptr: the page table of a batched launch carries absolute source addresses
+  const uint8_t* in = (const uint8_t*)((uintptr_t)raw + (uintptr_t)p.src);
   uint8_t* out = (uint8_t*)p.dst;
   const int lv = p.kind == 1 ? p.levels : 0;   // v2: level streams stored uncompressed first
   if (lv > p.csize || lv > p.usize) { if (lane == 0) atomicOr(status, kErrCorrupt); return; }
@@ -340,7 +341,7 @@ __global__ __launch_bounds__(256) void hs_pq_inflate_kernel(
     for (int i = lv + lane; i < p.csize; i += 64) out[i] = in[i];
     return;
   }
-  snappy_wave(raw, p.src + lv, p.csize - lv, out + lv, p.usize - lv, w, lane, status);
+  snappy_wave(in, lv, p.csize - lv, out + lv, p.usize - lv, w, lane, status);
 }
 
 template <typename T>
@@ -465,9 +466,10 @@ __global__ __launch_bounds__(256) void hs_pq_expand_kernel(
 
 extern "C" {
 
-// Decode the pages of one file planned by hs_pq_plan_chunk: inflate (one wavefront per page)
-// then expand (one workgroup per page) on `stream`.  `raw`, `scratch`, `pages` and `status`
-// are device pointers; errors accumulate as bits in *status.
+// Decode the pages planned by hs_pq_plan_chunk: inflate (one wavefront per page) then expand
+// (one workgroup per page) on `stream`.  `raw`, `scratch`, `pages` and `status` are device
+// pointers; errors accumulate as bits in *status.  With `raw` null the pages' `src` fields are
+// absolute device addresses: one launch then decodes the pages of many files.
 int hs_pq_decode_pages(const uint8_t* raw, uint8_t* scratch, const HsPqPage* pages, int npages,
                        int* status, void* stream) {
   if (npages <= 0) return 0;

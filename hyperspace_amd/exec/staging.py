@@ -221,6 +221,25 @@ def device_decode_enabled() -> bool:
     return os.environ.get("HS_DEVICE_PARQUET", "1") == "1"
 
 
+def batch_decode_bytes() -> int:
+    """Device bytes (compressed + inflated pages) of files whose page decode is batched into
+    one launch (``HS_PQ_BATCH_BYTES``; 0 = one launch per file)."""
+    return int(os.environ.get("HS_PQ_BATCH_BYTES", str(4 << 30)))
+
+
+_DECODE_STREAMS: Dict[int, object] = {}
+
+
+def decode_stream(device):
+    """The stream batched page decodes run on (one per device)."""
+    import torch
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _DECODE_STREAMS.get(idx)
+    if s is None:
+        s = _DECODE_STREAMS[idx] = torch.cuda.Stream(device=device)
+    return s
+
+
 def device_strings_enabled() -> bool:
     """Dictionary-encoded string pages decode on the device (``HS_DEVICE_STRINGS=0``: pyarrow)."""
     return os.environ.get("HS_DEVICE_STRINGS", "1") == "1"
@@ -376,17 +395,21 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
         _warm_decode_kernels()
         status = torch.zeros(1, dtype=torch.int32, device=device)
 
+    batched = native and use_device_pages and batch_decode_bytes() > 0
+
     def work(i: int):
         torch.cuda.set_device(device)
         stream = streams[i % len(streams)]
         lo, hi = int(offs[i]), int(offs[i + 1])
         done = set()
+        defer = [] if batched else None
         if native:
             from ..io import native_parquet
             flds = [f for f in schema if f.name in cols]
             if use_device_pages:
                 done = native_parquet.upload_file_device(parquet_local[i], flds, cols, lo,
-                                                         stream, device, status, dev_strings)
+                                                         stream, device, status, dev_strings,
+                                                         defer)
                 DEVICE_DECODED.update(done)
             rest_native = [f for f in flds if f.name not in done and f.name not in strings]
             if rest_native:
@@ -399,7 +422,7 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
             if lineage_ids is not None:
                 with torch.cuda.stream(stream):
                     cols[lineage_name].data[lo:hi].fill_(int(lineage_ids[i]))
-            return _done_event(stream)
+            return _done_event(stream), (defer[0] if defer else None)
         t = read_file(files[i], [f.name for f in rest]) if native else read_file(files[i])
         if t.num_rows != hi - lo:
             raise RuntimeError(f"row count mismatch for {files[i]}: footer {hi - lo}, read "
@@ -417,7 +440,7 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
         if lineage_ids is not None:
             with torch.cuda.stream(stream):
                 cols[lineage_name].data[lo:hi].fill_(int(lineage_ids[i]))
-        return _done_event(stream)
+        return _done_event(stream), (defer[0] if defer else None)
 
     def _done_event(stream):
         ev = torch.cuda.Event()
@@ -430,15 +453,35 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
     futs = [io_pool().submit(work, i) for i in range(len(files))]
     if file_batches is None:
         file_batches = [(0, len(files))]
+    dec_stream = decode_stream(device) if batched else None
+    if dec_stream is not None:
+        dec_stream.wait_stream(main)   # the destination columns exist before any decode
+    pending: list = []
+    pend_bytes = [0]
+    limit = batch_decode_bytes()
+
+    def flush():
+        if pending:
+            from ..io import native_parquet
+            main.wait_event(native_parquet.decode_batch(pending, device, status, dec_stream))
+            pending.clear()
+            pend_bytes[0] = 0
     for b0, b1 in file_batches:
         for fu in futs[b0:b1]:
-            main.wait_event(fu.result())
+            ev, pend = fu.result()
+            main.wait_event(ev)
+            if pend is not None:
+                pending.append(pend)
+                pend_bytes[0] += pend.nbytes
+                if pend_bytes[0] >= limit:
+                    flush()
+        flush()   # the batch's pages are decoded before on_batch reads its rows
         if on_batch is not None:
             on_batch(cols, int(offs[b0]), int(offs[b1]))
     for fu in futs:
         fu.result()
     t_host = _t.perf_counter()
-    for st in streams:
+    for st in streams + ([dec_stream] if dec_stream is not None else []):
         main.wait_stream(st)
     if status is not None:
         code = int(status.item())

@@ -429,9 +429,54 @@ def plain_strings(buf_ptr: int, nbytes: int, n: int) -> pa.Array:
                                                   pa.py_buffer(chars[:max(got, 1)])])
 
 
+class PendingDecode:
+    """One file's planned pages whose device decode is deferred into a batched launch
+    (``decode_batch``): the page table (absolute device addresses), the device buffers the
+    pages live in, and the event after their H2D copies."""
+
+    def __init__(self, pages: np.ndarray, keep: list, event, nbytes: int):
+        self.pages, self.keep, self.event, self.nbytes = pages, keep, event, nbytes
+
+
+def decode_batch(pend: List["PendingDecode"], device, status, stream):
+    """ONE launch pair decoding the pages of every file in ``pend`` on ``stream`` (after their
+    H2D copies): a per-file launch covers a few hundred pages, too few wavefronts for 256 CUs
+    when the pages are Snappy tag chains; a batch of files fills the chip.  Returns the event
+    marking the decode done."""
+    import torch
+    from ..ops import _lib as NL
+    from ..exec.staging import pinned_pool
+    tables, base = [], 0
+    for p in pend:
+        t = p.pages.copy()
+        t["dict_page"] = np.where(t["dict_page"] >= 0, t["dict_page"] + base, -1)
+        tables.append(t)
+        base += len(t)
+        stream.wait_event(p.event)
+    allp = np.concatenate(tables) if tables else np.zeros(0, PAGE_DTYPE)
+    pool = pinned_pool()
+    with torch.cuda.stream(stream):
+        if len(allp):
+            ppin = pool.acquire(allp.nbytes)
+            ppin.numpy()[:allp.nbytes] = allp.view(np.uint8)
+            dpages = torch.empty(allp.nbytes, dtype=torch.uint8, device=device)
+            dpages.copy_(ppin[:allp.nbytes], non_blocking=True)
+            pool.release(ppin, stream)
+            NL.check(NL.lib().hs_pq_decode_pages(None, None, dpages.data_ptr(), len(allp),
+                                                 status.data_ptr(), stream.cuda_stream),
+                     "hs_pq_decode_pages")
+            dpages.record_stream(stream)
+        for p in pend:
+            for x in p.keep:
+                x.record_stream(stream)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+    return ev
+
+
 def upload_file_device(path: str, fields: Sequence[pa.Field], cols: Dict[str, object], lo: int,
-                       stream, device, status, strings: Optional[Dict[str, StringCodes]] = None
-                       ) -> Set[str]:
+                       stream, device, status, strings: Optional[Dict[str, StringCodes]] = None,
+                       defer: Optional[list] = None) -> Set[str]:
     """Decode the natively supported, null-free ``fields`` of ``path`` entirely on the GPU into
     ``cols[name].data[lo:...]``: the host preads the raw column chunks into pinned memory and
     lists their pages; one H2D copy moves the compressed bytes and the page table, and two
@@ -521,6 +566,18 @@ def upload_file_device(path: str, fields: Sequence[pa.Field], cols: Dict[str, ob
                 for p0, np_, toff in fix:
                     seg = pages[p0:p0 + np_]
                     seg["dict"] = np.where(seg["kind"] != 2, dtab.data_ptr() + 4 * toff, 0)
+            if defer is not None:
+                # batched decode (decode_batch): absolute source addresses, buffers kept alive
+                # by the pending record until the batched launch is queued
+                pages["src"] = np.where(pages["codec"] == 2, pages["src"],
+                                        draw.data_ptr() + pages["src"])
+                keep = [draw, scratch] + ([dtab] if tabs is not None else [])
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                defer.append(PendingDecode(pages, keep, ev, draw.numel() + scratch.numel()))
+                pool.release(pinned, stream)
+                _phase("h2d_enqueue", t)
+                return {fld.name for fld, _, _, _ in chunks}
             ppin = pool.acquire(pages.nbytes)
             ppin.numpy()[:pages.nbytes] = pages.view(np.uint8)
             dpages = torch.empty(pages.nbytes, dtype=torch.uint8, device=device)
