@@ -795,8 +795,13 @@ int plan_chunk(File* f, int rg, int col, uint8_t* raw, int64_t raw_cap, int64_t 
     const int mode = g_host_inflate.load(std::memory_order_relaxed);
     const bool big_dict = p.kind == 2 && p.usize > kHostDictMin;
     const bool str_dict = strings && p.kind == 2;
-    const bool dense = str_dict || (p.codec == 1 && mode > 0 &&
+    bool dense = str_dict || (p.codec == 1 && mode > 0 &&
         (big_dict || (mode > 1 && (int64_t)p.usize * 10 >= (int64_t)p.csize * 11)));
+    // mode 3: every third tag-dense data page stays on the device, so host and device inflate
+    // concurrently (a batched device decode keeps up with about half the host's share)
+    if (mode == 3 && dense && !str_dict && !big_dict && p.kind != 2 &&
+        p.usize <= kDeviceInflateMax && (*npages % 3) == 2)
+      dense = false;
     // one wavefront inflates one page on the device: a multi-MB Snappy page left to it runs for
     // seconds (profiles/cold_load_r2.jsonl: 58 s for an index of 1M-row pages), so such a
     // column goes to the host page layer instead
@@ -862,7 +867,8 @@ int hs_pq_plan_chunk(void* h, int rg, int col, uint8_t* raw, int64_t raw_cap, in
 
 // Bytes that bound what hs_pq_plan_chunk may inflate into the host buffer for this chunk.
 // Which Snappy pages the planner inflates on the host (codec 2): 0 none (every page inflates
-// on the device), 1 large dictionary pages only, 2 those and tag-dense data pages (default).
+// on the device), 1 large dictionary pages only, 2 those and tag-dense data pages (default),
+// 3 as 2 but every third tag-dense data page is left to the device.
 void hs_pq_set_host_inflate(int mode) { g_host_inflate.store(mode, std::memory_order_relaxed); }
 
 int64_t hs_pq_chunk_host_bound(void* h, int rg, int col) {
