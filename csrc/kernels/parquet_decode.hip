@@ -143,7 +143,10 @@ __device__ void snappy_wave(const uint8_t* __restrict__ base, int64_t ib, int n,
                             uint8_t* __restrict__ out, int cap, int w, int lane,
                             int* __restrict__ status) {
   constexpr int WIN = 512, PER = WIN / 64, LOGT = 6;
-  __shared__ int s_next[4][LOGT][WIN];   // pointer-jumping tables: 2^k-th following tag
+  // pointer-jumping tables (2^k-th following tag; window offsets fit 16 bits): 6 KB per
+  // wavefront instead of 12, so three workgroups fit a CU instead of two
+  __shared__ short s_next[4][LOGT][WIN];
+  __shared__ int s_skip[4][WIN];         // exact successor offset (a literal may jump far)
   __shared__ int s_len[4][WIN];          // speculative tag at each window offset: output bytes
   __shared__ int s_srcw[4][WIN];         //   and source (literal: input offset, copy: -offset)
   __shared__ uint8_t s_win[4][WIN + 8];
@@ -204,7 +207,11 @@ __device__ void snappy_wave(const uint8_t* __restrict__ base, int64_t ib, int n,
       ok = ok && i + hl <= WIN && ip + i + hl <= n;
       s_len[w][i] = l;
       s_srcw[w][i] = src;
-      s_next[w][0][i] = ok ? i + hl + (kind == 0 ? l : 0) : i;
+      // a target beyond the window saturates at WIN (16 bits): only "< WIN" is ever tested,
+      // except the last real tag's successor, kept exactly in s_skip
+      const int nx = ok ? i + hl + (kind == 0 ? l : 0) : i;
+      s_next[w][0][i] = (short)(nx < WIN ? nx : WIN);
+      s_skip[w][i] = nx;
     }
     wsync();
     for (int t = 1; t < LOGT; ++t) {
@@ -212,7 +219,7 @@ __device__ void snappy_wave(const uint8_t* __restrict__ base, int64_t ib, int n,
       for (int k = 0; k < PER; ++k) {
         const int i = lane * PER + k;
         const int a = s_next[w][t - 1][i];
-        s_next[w][t][i] = a < WIN ? s_next[w][t - 1][a] : a;
+        s_next[w][t][i] = (short)(a < WIN ? s_next[w][t - 1][a] : a);
       }
       wsync();
     }
@@ -237,7 +244,7 @@ __device__ void snappy_wave(const uint8_t* __restrict__ base, int64_t ib, int n,
     }
     const int st = incl - l;
     const int total = __shfl(incl, cnt - 1, 64);
-    const int nextpos = __shfl(mine ? s_next[w][0][pos] : 0, cnt - 1, 64);
+    const int nextpos = __shfl(mine ? s_skip[w][pos] : 0, cnt - 1, 64);
     // a copy may not reach before the output start; literals must end inside the input
     const bool bad = mine && (src < 0 ? (-src > op + st) : (src + l > n));
     if (__ballot(bad) != 0ull || op + total > cap) {
@@ -287,8 +294,11 @@ __device__ void snappy_wave(const uint8_t* __restrict__ base, int64_t ib, int n,
         if (sr >= 0) out[op + b] = base[ib + sr + (b - s_start[w][lo])];
       }
     }
-    __threadfence();
+    // the wavefront's own global stores must be visible to its own later loads: a
+    // workgroup-scope fence (same CU) instead of a device-wide one
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     // 2. copy bytes
 #pragma unroll 2
     for (int b = lane; b < total; b += 64) {
@@ -316,8 +326,11 @@ __device__ void snappy_wave(const uint8_t* __restrict__ base, int64_t ib, int n,
       }
       out[op + b] = out[op + q];
     }
-    __threadfence();
+    // the wavefront's own global stores must be visible to its own later loads: a
+    // workgroup-scope fence (same CU) instead of a device-wide one
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     op += total;
   }
   if (op != cap && lane == 0) atomicOr(status, kErrCorrupt);
