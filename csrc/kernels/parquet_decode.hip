@@ -121,6 +121,12 @@ struct HsPqPage {
 
 enum : int { kErrCorrupt = 1, kErrDictRange = 2 };
 
+// input bytes one wavefront parses per Snappy batch (up to 64 tags); LDS per workgroup scales
+// with it (profiles/build_sweep_inflate_r3.jsonl)
+#ifndef HS_SNAPPY_WIN
+#define HS_SNAPPY_WIN 128
+#endif
+
 // Snappy raw-block decompression by one wavefront (input at byte offset `ib` of the 4-byte
 // aligned buffer `base`, `n` bytes; output `out`, `cap` bytes).
 //
@@ -142,7 +148,7 @@ enum : int { kErrCorrupt = 1, kErrDictRange = 2 };
 __device__ void snappy_wave(const uint8_t* __restrict__ base, int64_t ib, int n,
                             uint8_t* __restrict__ out, int cap, int w, int lane,
                             int* __restrict__ status) {
-  constexpr int WIN = 512, PER = WIN / 64, LOGT = 6;
+  constexpr int WIN = HS_SNAPPY_WIN, PER = WIN / 64, LOGT = 6;
   // pointer-jumping tables (2^k-th following tag; window offsets fit 16 bits): 6 KB per
   // wavefront instead of 12, so three workgroups fit a CU instead of two
   __shared__ short s_next[4][LOGT][WIN];
