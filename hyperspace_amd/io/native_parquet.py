@@ -4,12 +4,12 @@ HIP kernels (``csrc/kernels/parquet_decode.hip``).
 
 Device path (``upload_file_device``, default for chunks whose statistics say null-free): the
 host only preads the raw column chunks into one pinned block and walks the page headers; the
-compressed bytes cross PCIe and two launches per file decode them — ``hs_pq_inflate_kernel``
-(Snappy, one wavefront per page, data-parallel tag parsing) and ``hs_pq_expand_kernel`` (RLE /
-bit-packed hybrid parsing, dictionary gather or PLAIN copy, one workgroup per page).  Pages that
-Snappy actually compressed are chains of short tags that a wavefront resolves slowly; the
-planner inflates those (and large dictionary pages) on the host into the same pinned block, and
-the device still parses and expands them (measured: profiles/build_decode_r2.jsonl).
+compressed bytes cross PCIe and two launches per batch of files decode them -
+``hs_pq_inflate_kernel`` (Snappy, one wavefront per page, data-parallel tag parsing over
+128-byte windows) and ``hs_pq_expand_kernel`` (RLE / bit-packed hybrid parsing, dictionary
+gather or PLAIN copy, one workgroup per page).  Launches cover ~4 GB of files at once
+(``decode_batch``): a page is one wavefront's serial work, so only many files' pages fill the
+chip.  Large dictionary pages (and string dictionaries) are inflated on the host.
 
 Host-page-layer path (``upload_file``, chunks that may hold nulls):
 per file every natively decodable column chunk is decompressed straight into one pinned
@@ -105,8 +105,11 @@ def lib():
                     fn.restype = res
                     fn.argtypes = args
                 # HS_PQ_HOST_INFLATE: which Snappy pages the planner inflates on the host
-                # (0 none, 1 large dictionaries, 2 + tag-dense data pages)
-                L.hs_pq_set_host_inflate(int(os.environ.get("HS_PQ_HOST_INFLATE", "2")))
+                # (0 none, 1 large dictionaries, 2 + tag-dense data pages, 3 two thirds of
+                # those).  With batched launches and 128-byte windows the device inflates
+                # tag-dense pages faster than 16 host threads (SF100 lineitem read + H2D
+                # 0.34 s vs 0.42 s: profiles/build_sweep_inflate_r3_win128.jsonl)
+                L.hs_pq_set_host_inflate(int(os.environ.get("HS_PQ_HOST_INFLATE", "1")))
                 if L.hs_pq_run_size() != RUN_DTYPE.itemsize or \
                         L.hs_pq_info_size() != C.sizeof(ChunkInfo) or \
                         L.hs_pq_page_size() != PAGE_DTYPE.itemsize:
