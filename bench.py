@@ -353,7 +353,23 @@ def main():
     # the on-disk code-object cache is empty, join-index build) — not part of the timed steps
     s.conf.set("spark.hyperspace.mi.index.placement", "sharded")
     jit0 = dict(jit_mod.JIT_STATS) if jit_mod is not None else {}
+    from hyperspace_amd.utils.tracing import TRACER as _TR, format_report as _fmt
+    _TR.reset()
+    cprof = None
+    if os.environ.get("HS_BENCH_COLD_PROFILE") and rank == 0:
+        import cProfile
+        cprof = cProfile.Profile()
+        cprof.enable()
     cold = {"q6_cold_ms": one_query_ms(q6, 999), "q3_cold_ms": one_query_ms(q3, 999)}
+    if cprof is not None:
+        import io
+        import pstats
+        cprof.disable()
+        buf = io.StringIO()
+        pstats.Stats(cprof, stream=buf).sort_stats("tottime").print_stats(25)
+        log(rank, "[bench] cold queries host profile\n" + buf.getvalue())
+    if _TR.profile:
+        log(rank, "[bench] cold queries stage profile\n" + _fmt(_TR.report()))
     if jit_mod is not None:
         # kernels the cold queries compiled with hipRTC vs loaded from the code-object cache
         # (the AOT set of __graft_entry__.build covers the bench's shapes)

@@ -147,6 +147,7 @@ class GpuBackend:
         staging.copy_streams(self.device)
         if staging.native_decode_enabled():
             staging._warm_decode_kernels()
+        _warm_torch_kernels(self.device)
 
     # ------------------------------------------------------------------------------------------
     @property
@@ -1923,6 +1924,30 @@ def _combine_aggs(a, b):
     torch.minimum(a[2], b[2], out=a[2])
     torch.maximum(a[3], b[3], out=a[3])
     return a
+
+
+def _warm_torch_kernels(device) -> None:
+    """Run the PyTorch elementwise / reduction / scan kernels the query paths use once, on
+    tiny tensors: ROCm loads a kernel's code object on its first launch (tens of ms each),
+    which would otherwise land in the first query that needs it (profiled: floor_divide,
+    cumsum, compare + any of the join setup, ~250 ms of a cold Q3)."""
+    import torch
+    for dt in (torch.int64, torch.int32):
+        x = torch.arange(64, dtype=dt, device=device)
+        y = x.flip(0)
+        (x // 3, x % 3, x + y, x - y, x * y, x == y, x != y, x < y, x <= y, x > y, x >= y,
+         torch.cumsum(x, 0), torch.cumsum((x + 1) // 2, 0, out=torch.empty_like(x)),
+         torch.aminmax(x), x.max(), x.min(), x.sum(), (x == y).any(), (x == y).all(),
+         torch.nonzero(x > 3), x.index_select(0, y.long()), torch.where(x > 3, x, y),
+         x.clamp(0, 9), torch.repeat_interleave(x[:4].long(), 2), x.long(), x.int(),
+         x.to(torch.float64), torch.minimum(x, y), torch.maximum(x, y), x[1:] == x[:-1],
+         (x[1:] != 0) & (x[:-1] != 0), torch.zeros_like(x), torch.full_like(x, 7))
+    v = torch.ones(64, dtype=torch.uint8, device=device)
+    (v.bool(), v & v, v == 0, v.any(), v.sum(), v.bool().any(), torch.nonzero(v))
+    f = torch.linspace(0, 1, 64, dtype=torch.float64, device=device)
+    (f + f, f * f, f / 3, f < 0.5, torch.aminmax(f), f.sum(), torch.minimum(f, f),
+     torch.maximum(f, f), torch.isnan(f), f.to(torch.int64))
+    torch.cuda.synchronize(device)
 
 
 def _needs_eval(c: E.Expression) -> bool:

@@ -169,8 +169,15 @@ class ScanAggGraph:
             g = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream()
             side.wait_stream(cur)
-            with torch.cuda.graph(g, stream=side):
-                self._enqueue(slot, torch.cuda.current_stream().cuda_stream)
+            # capture_begin/end directly: the torch.cuda.graph context manager synchronizes,
+            # runs gc.collect() and empties the caching allocator first (~100 ms, and every
+            # later allocation goes back to hipMalloc); the captured work allocates nothing
+            with torch.cuda.stream(side):
+                g.capture_begin()
+                try:
+                    self._enqueue(slot, side.cuda_stream)
+                finally:
+                    g.capture_end()
             cur.wait_stream(side)
             slot.graph = g
         if not eager:
