@@ -95,6 +95,8 @@ MJ_BLOCK = int(os.environ.get("HS_JIT_MJ_BLOCK", "256"))
 MJ_EAGER = os.environ.get("HS_JIT_MJ_EAGER", "0") == "1"
 # match-list appends one set match bit per round (_sparse_append) instead of one per item
 MJ_SPARSE = os.environ.get("HS_JIT_MJ_SPARSE", "1") == "1"
+# hash-mode merge joins append matches lane-major (row order): _lanemajor_append
+MJ_HASH_LANEMAJOR = os.environ.get("HS_JIT_MJ_HASH_LANEMAJOR", "1") == "1"
 MJ_KEY32 = os.environ.get("HS_JIT_MJ_KEY32", "1") == "1"  # 32-bit merge images (_key32_frame)
 # cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
 MJ_EXP = os.environ.get("HS_JIT_MJ_EXP", "")
@@ -1284,7 +1286,7 @@ def merge_join_shape(p: NL.JoinParams, compacts=None, hk=None) -> tuple:
     return ("merge_join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey,
             p.key_is_float, MJ_ITEMS, MJ_LDS_KEYS, MJ_STEPS, BLOCK, WAVE_SYNC,
             _key32_frame(p, compacts) is not None, MJ_EXP, MJ_STAGE_UNROLL, MJ_DBUF, MJ_PREFETCH,
-            MJ_BLOCK, MJ_EAGER, MJ_SPARSE,
+            MJ_BLOCK, MJ_EAGER, MJ_SPARSE, MJ_HASH_LANEMAJOR,
             hk.shape() if hk is not None else None)
 
 
@@ -1363,6 +1365,30 @@ def _sparse_append(NI: int, ind: str, word: str, j_fmt: str, drain=()) -> List[s
           f"{ind}    lrow_s[wv][wp] = (int)(g0 + it); lj_s[wv][wp] = (int)(ss + jv);",
           f"{ind}    wcnt += __popcll(bm);"] + list(drain) + [
           f"{ind}  }}",
+          f"{ind}}}"]
+    return b
+
+
+def _lanemajor_append(NI: int, ind: str, word: str, j_fmt: str) -> List[str]:
+    """Append the thread's matches (bits of ``word``) to the wavefront's list in row order:
+    lane t's matches go after those of lanes < t (one wave prefix sum of the match counts), so a
+    batch of 64 list entries is 64 consecutive matches of the tile."""
+    b = [f"{ind}{{ unsigned pend = {word};",
+         f"{ind}  const int mc = __popc(pend);",
+         f"{ind}  int mi = mc;",
+         f"{ind}  for (int o = 1; o < 64; o <<= 1) {{ const int y = __shfl_up(mi, (unsigned)o, 64); "
+         f"if (cln >= o) mi += y; }}",
+         f"{ind}  int wp = wcnt + mi - mc;",
+         f"{ind}  const int mt = __shfl(mi, 63, 64);",
+         f"{ind}  while (pend != 0u) {{",
+         f"{ind}    const int it = __builtin_ctz(pend);",
+         f"{ind}    pend &= pend - 1u;",
+         f"{ind}    int jv = {j_fmt.format(it=0)};"]
+    for it in range(1, NI):
+        b.append(f"{ind}    jv = it == {it} ? {j_fmt.format(it=it)} : jv;")
+    b += [f"{ind}    lrow_s[wv][wp] = (int)(g0 + it); lj_s[wv][wp] = (int)(ss + jv); ++wp;",
+          f"{ind}  }}",
+          f"{ind}  wcnt += mt;",
           f"{ind}}}"]
     return b
 
@@ -1479,7 +1505,8 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
     W = BLOCK // 64  # noqa: N806
     # list entries: < 64 carried over + one round's appends (all NI items per round, or one
     # item per round with the sparse appends, which drain between rounds)
-    CAP = 128 if MJ_SPARSE else 64 * NI + 64  # noqa: N806
+    lanemajor = hk is not None and MJ_HASH_LANEMAJOR
+    CAP = 128 if (MJ_SPARSE and not lanemajor) else 64 * NI + 64  # noqa: N806
     NB = 2 if MJ_DBUF else 1  # noqa: N806
     b += [f"  __shared__ {KT} skeys_[{NB}][{LK + 1}]; __shared__ unsigned char spass_[{NB}][{LK}];",
           "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;"]
@@ -1638,7 +1665,13 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
             else:
                 drain = _deferred_drain(args, cols, split, approx, aggs, grouped, p.group_col,
                                         allslots, i2 + "    ", final=False, hk=hk)
-                if MJ_SPARSE:
+                if hk is not None and MJ_HASH_LANEMAJOR:
+                    # hash-mode grouping: matches appended in row order (lane-major), so equal
+                    # keys of a batch are adjacent and merge into one probe per run
+                    b.extend(_lanemajor_append(NI, i2, "pb", "jl{it}"))
+                    b.extend(_deferred_drain(args, cols, split, approx, aggs, grouped,
+                                             p.group_col, allslots, i2, final=False, hk=hk))
+                elif MJ_SPARSE:
                     # drained inside the append rounds: the lists never hold more than 63 + 64
                     # entries, so they take 6 KB of LDS per block instead of 20 KB
                     b.extend(_sparse_append(NI, i2, "pb", "jl{it}", drain))
