@@ -96,7 +96,7 @@ MJ_EAGER = os.environ.get("HS_JIT_MJ_EAGER", "0") == "1"
 # match-list appends one set match bit per round (_sparse_append) instead of one per item
 MJ_SPARSE = os.environ.get("HS_JIT_MJ_SPARSE", "1") == "1"
 # hash-mode merge joins append matches lane-major (row order): _lanemajor_append
-MJ_HASH_LANEMAJOR = os.environ.get("HS_JIT_MJ_HASH_LANEMAJOR", "1") == "1"
+MJ_HASH_LANEMAJOR = os.environ.get("HS_JIT_MJ_HASH_LANEMAJOR", "0") == "1"
 MJ_KEY32 = os.environ.get("HS_JIT_MJ_KEY32", "1") == "1"  # 32-bit merge images (_key32_frame)
 # cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
 MJ_EXP = os.environ.get("HS_JIT_MJ_EXP", "")
