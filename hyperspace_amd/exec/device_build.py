@@ -116,6 +116,11 @@ def _sort_and_write(session, table: Dict[str, DeviceColumn], names: List[str], b
             bucket.device)
     LAST_BUILD_STATS.update({"sort_gather_s": t1 - t0,
                              "d2h_write_s": time.perf_counter() - t1})
+    if paths is not None:
+        from . import pq_encode
+        LAST_BUILD_STATS["write_phases_s"] = {k: round(v, 4) for k, v in
+                                              pq_encode.WRITE_PHASES.items()}
+        pq_encode.WRITE_PHASES.clear()
     if seed is not None and paths:
         # the sorted bucket-major columns are exactly what a query would load back from these
         # files: hand them to the device table cache instead of freeing them

@@ -29,6 +29,7 @@ from __future__ import annotations
 import ctypes as C
 import math
 import os
+import time
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -113,7 +114,10 @@ def snappy_pages(plans, p_first: int, p_end: int, device):
     sizes = torch.empty(total, dtype=torch.int32, device=device)
     NL.check(L.hs_snappy_compress(dtab.data_ptr(), total, slots.data_ptr(), slot,
                                   sizes.data_ptr(), NL.stream_ptr()), "hs_snappy_compress")
+    t_sync = time.perf_counter()
     hsz = sizes.cpu().numpy().astype(np.int64)
+    WRITE_PHASES["snappy_sync_s"] = WRITE_PHASES.get("snappy_sync_s", 0.0) + \
+        time.perf_counter() - t_sync
     dst = np.concatenate([[0], np.cumsum(hsz)]).astype(np.int64)
     zsize = np.add.reduceat(hsz, first[:-1]).reshape(len(plans), npg)
     zoff = dst[first[:-1]].reshape(len(plans), npg)
@@ -122,6 +126,10 @@ def snappy_pages(plans, p_first: int, p_end: int, device):
     NL.check(L.hs_snappy_pack(slots.data_ptr(), slot, sizes.data_ptr(), ddst.data_ptr(), total,
                               out.data_ptr(), NL.stream_ptr()), "hs_snappy_pack")
     return out, zoff, zsize
+
+
+# seconds of the last builds' write phases (reset by device_build per build)
+WRITE_PHASES: Dict[str, float] = {}
 
 
 def _writer():
@@ -290,7 +298,10 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
     pages, files = page_table(bucket_off, rg_rows)
     if not files:
         return []
+    t_plan = time.perf_counter()
     plans = plan_columns(cols, names, schema, pages, device)
+    WRITE_PHASES["plan_columns_s"] = WRITE_PHASES.get("plan_columns_s", 0.0) + \
+        time.perf_counter() - t_plan
     if plans is None:
         return None
     for cp in plans:
@@ -405,6 +416,9 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
             return out
         futs.append(io_pool().submit(write_batch))
     paths = []
+    t_wait = time.perf_counter()
     for fu in futs:
         paths.extend(fu.result())
+    WRITE_PHASES["write_tail_s"] = WRITE_PHASES.get("write_tail_s", 0.0) + \
+        time.perf_counter() - t_wait
     return paths
