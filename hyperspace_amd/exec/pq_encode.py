@@ -55,7 +55,7 @@ class WCol(C.Structure):
 
 CODEC_IDS = {"none": 0, "uncompressed": 0, "snappy": 1}
 # raw encoded bytes compressed per Snappy launch (slots take ~1.17x that in HBM)
-SNAPPY_GROUP_BYTES = 2 << 30
+SNAPPY_GROUP_BYTES = 512 << 20
 SNAPPY_CHUNK_DTYPE = np.dtype([("src", "<u8"), ("len", "<i8")])
 
 
@@ -85,12 +85,18 @@ def snappy_stream_host(raw: np.ndarray) -> np.ndarray:
     return np.concatenate(parts)
 
 
-def snappy_pages(plans, p_first: int, p_end: int, device):
-    """Compress pages [p_first, p_end) of every column on the device (current stream):
-    returns (packed device buffer, offsets [col][page - p_first] into it, compressed sizes of
-    the same shape).  Pages are cut into 64 KiB chunks (one lane each,
-    csrc/kernels/snappy_encode.hip); the chunk sizes come back to the host once, then one pack
-    launch concatenates the used slot bytes page by page."""
+class _SnappyGroup:
+    """Device state of one compressed page group between ``snappy_launch`` and
+    ``snappy_finish``."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def snappy_launch(plans, p_first: int, p_end: int, device) -> _SnappyGroup:
+    """Queue the compression of pages [p_first, p_end) of every column on the current
+    stream (no host wait): pages are cut into 64 KiB chunks, one wavefront each
+    (csrc/kernels/snappy_encode.hip), into fixed-size slots."""
     import torch
     L = NL.lib()
     ch = int(L.hs_snappy_chunk_bytes())
@@ -114,18 +120,54 @@ def snappy_pages(plans, p_first: int, p_end: int, device):
     sizes = torch.empty(total, dtype=torch.int32, device=device)
     NL.check(L.hs_snappy_compress(dtab.data_ptr(), total, slots.data_ptr(), slot,
                                   sizes.data_ptr(), NL.stream_ptr()), "hs_snappy_compress")
+    hsizes = torch.empty(total, dtype=torch.int32, pin_memory=True)
+    hsizes.copy_(sizes, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    return _SnappyGroup(dtab=dtab, slots=slots, sizes=sizes, hsizes=hsizes, event=ev,
+                        first=first, total=total, slot=slot, nplans=len(plans), npg=npg)
+
+
+def snappy_finish(g: _SnappyGroup, device):
+    """Wait for group ``g``'s chunk sizes, then pack the used slot bytes page by page on the
+    current stream: (packed device buffer, offsets [col][page] into it, compressed sizes)."""
+    import torch
+    L = NL.lib()
     t_sync = time.perf_counter()
-    hsz = sizes.cpu().numpy().astype(np.int64)
+    g.event.synchronize()
     WRITE_PHASES["snappy_sync_s"] = WRITE_PHASES.get("snappy_sync_s", 0.0) + \
         time.perf_counter() - t_sync
+    hsz = g.hsizes.numpy().astype(np.int64)
     dst = np.concatenate([[0], np.cumsum(hsz)]).astype(np.int64)
-    zsize = np.add.reduceat(hsz, first[:-1]).reshape(len(plans), npg)
-    zoff = dst[first[:-1]].reshape(len(plans), npg)
+    zsize = np.add.reduceat(hsz, g.first[:-1]).reshape(g.nplans, g.npg)
+    zoff = dst[g.first[:-1]].reshape(g.nplans, g.npg)
     out = torch.empty(max(1, int(dst[-1])), dtype=torch.uint8, device=device)
     ddst = torch.from_numpy(dst[:-1].copy()).to(device)
-    NL.check(L.hs_snappy_pack(slots.data_ptr(), slot, sizes.data_ptr(), ddst.data_ptr(), total,
-                              out.data_ptr(), NL.stream_ptr()), "hs_snappy_pack")
+    NL.check(L.hs_snappy_pack(g.slots.data_ptr(), g.slot, g.sizes.data_ptr(), ddst.data_ptr(),
+                              g.total, out.data_ptr(), NL.stream_ptr()), "hs_snappy_pack")
     return out, zoff, zsize
+
+
+def snappy_pages(plans, p_first: int, p_end: int, device):
+    """Compress pages [p_first, p_end) of every column on the device (current stream):
+    returns (packed device buffer, offsets [col][page - p_first] into it, compressed sizes of
+    the same shape).  The chunk sizes come back to the host once, then one pack launch
+    concatenates the used slot bytes page by page."""
+    return snappy_finish(snappy_launch(plans, p_first, p_end, device), device)
+
+
+_ZSTREAMS: Dict[int, object] = {}
+
+
+def compress_stream(device):
+    """The stream index pages are Snappy-compressed on (one per device), next to the D2H copy
+    stream that drains them."""
+    import torch
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _ZSTREAMS.get(idx)
+    if st is None:
+        st = _ZSTREAMS[idx] = torch.cuda.Stream(device=device)
+    return st
 
 
 # seconds of the last builds' write phases (reset by device_build per build)
@@ -342,6 +384,12 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
             groups.append(g)
     group_of = {bi: gi for gi, g in enumerate(groups) for bi in g}
     zgroup = (-1, None)
+    launched: Dict[int, _SnappyGroup] = {}
+    zs = compress_stream(device) if cid == 1 else None
+
+    def group_range(gi: int) -> Tuple[int, int]:
+        gb0, gb1 = batches[groups[gi][0]], batches[groups[gi][-1]]
+        return gb0[0][1], gb1[-1][1] + gb1[-1][2]
     for bi, batch in enumerate(batches):
         if len(futs) >= max_inflight:
             futs[len(futs) - max_inflight].result()
@@ -353,10 +401,23 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
         with torch.cuda.stream(stream):
             if cid == 1:
                 gi = group_of[bi]
-                gb0, gb1 = batches[groups[gi][0]], batches[groups[gi][-1]]
-                gfirst, gend = gb0[0][1], gb1[-1][1] + gb1[-1][2]
+                gfirst = group_range(gi)[0]
                 if zgroup[0] != gi:
-                    zgroup = (gi, snappy_pages(plans, gfirst, gend, device))
+                    # compress this group (if not yet queued) and the next one on the
+                    # compression stream: group g+1 compresses while g's pages are copied out
+                    # and written
+                    for gg in (gi, gi + 1):
+                        if gg < len(groups) and gg not in launched:
+                            zs.wait_stream(torch.cuda.current_stream(device))
+                            with torch.cuda.stream(zs):
+                                launched[gg] = snappy_launch(plans, *group_range(gg), device)
+                    with torch.cuda.stream(zs):
+                        res = snappy_finish(launched.pop(gi), device)
+                        zev = torch.cuda.Event()
+                        zev.record(zs)
+                    stream.wait_event(zev)
+                    res[0].record_stream(stream)
+                    zgroup = (gi, res)
                 packed, zoff, zsize = zgroup[1]
                 for c in range(len(plans)):
                     lo = int(zoff[c][p_first - gfirst])
