@@ -115,7 +115,11 @@ def snappy_launch(plans, p_first: int, p_end: int, device) -> _SnappyGroup:
     tab["src"] = src_page[page_of] + (k * ch).astype(np.uint64)
     tab["len"] = np.minimum(ch, plen[page_of] - k * ch)
     slot = int(L.hs_snappy_max_compressed(ch))
-    dtab = torch.from_numpy(tab.view(np.uint8)).to(device, non_blocking=False)
+    # pinned source: the chunk-table copy is queued, not waited for (a pageable copy would
+    # block the host until the stream drains, serializing the groups)
+    htab = torch.from_numpy(tab.view(np.uint8)).pin_memory()
+    dtab = torch.empty(htab.numel(), dtype=torch.uint8, device=device)
+    dtab.copy_(htab, non_blocking=True)
     slots = torch.empty(total * slot, dtype=torch.uint8, device=device)
     sizes = torch.empty(total, dtype=torch.int32, device=device)
     NL.check(L.hs_snappy_compress(dtab.data_ptr(), total, slots.data_ptr(), slot,
@@ -142,7 +146,9 @@ def snappy_finish(g: _SnappyGroup, device):
     zsize = np.add.reduceat(hsz, g.first[:-1]).reshape(g.nplans, g.npg)
     zoff = dst[g.first[:-1]].reshape(g.nplans, g.npg)
     out = torch.empty(max(1, int(dst[-1])), dtype=torch.uint8, device=device)
-    ddst = torch.from_numpy(dst[:-1].copy()).to(device)
+    hdst = torch.from_numpy(dst[:-1].copy()).pin_memory()
+    ddst = torch.empty_like(hdst, device=device)
+    ddst.copy_(hdst, non_blocking=True)
     NL.check(L.hs_snappy_pack(g.slots.data_ptr(), g.slot, g.sizes.data_ptr(), ddst.data_ptr(),
                               g.total, out.data_ptr(), NL.stream_ptr()), "hs_snappy_pack")
     return out, zoff, zsize
@@ -172,6 +178,7 @@ def compress_stream(device):
 
 # seconds of the last builds' write phases (reset by device_build per build)
 WRITE_PHASES: Dict[str, float] = {}
+_WP_LOCK = __import__("threading").Lock()
 
 
 def _writer():
@@ -392,7 +399,10 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
         return gb0[0][1], gb1[-1][1] + gb1[-1][2]
     for bi, batch in enumerate(batches):
         if len(futs) >= max_inflight:
+            t_bp = time.perf_counter()
             futs[len(futs) - max_inflight].result()
+            WRITE_PHASES["backpressure_s"] = WRITE_PHASES.get("backpressure_s", 0.0) + \
+                time.perf_counter() - t_bp
         p_first = batch[0][1]
         p_end = batch[-1][1] + batch[-1][2]
         host = []
@@ -437,7 +447,9 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
             ev.record(stream)
 
         def write_batch(batch=batch, host=host, ev=ev, zoff=zoff, zsize=zsize, gfirst=gfirst):
+            t_w = time.perf_counter()
             ev.synchronize()
+            t_s = time.perf_counter()
             out = []
             for b, p0, pn in batch:
                 arr = (WCol * (pn * len(plans)))()
@@ -474,6 +486,11 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
                 out.append(path)
             for h, _ in host:   # written: the blocks can serve the next batch
                 pinned_pool().release(h, torch.cuda.current_stream(device))
+            with _WP_LOCK:
+                WRITE_PHASES["writer_wait_d2h_s"] = WRITE_PHASES.get("writer_wait_d2h_s", 0.0) + \
+                    t_s - t_w
+                WRITE_PHASES["writer_write_s"] = WRITE_PHASES.get("writer_write_s", 0.0) + \
+                    time.perf_counter() - t_s
             return out
         futs.append(io_pool().submit(write_batch))
     paths = []
