@@ -55,7 +55,7 @@ class WCol(C.Structure):
 
 CODEC_IDS = {"none": 0, "uncompressed": 0, "snappy": 1}
 # raw encoded bytes compressed per Snappy launch (slots take ~1.17x that in HBM)
-SNAPPY_GROUP_BYTES = 512 << 20
+SNAPPY_GROUP_BYTES = int(os.environ.get("HS_SNAPPY_GROUP_BYTES", str(2 << 30)))
 SNAPPY_CHUNK_DTYPE = np.dtype([("src", "<u8"), ("len", "<i8")])
 
 
