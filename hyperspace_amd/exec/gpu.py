@@ -1013,7 +1013,55 @@ class GpuBackend:
         runs it."""
         left, right, lk, rk = self._join_inputs(p)
         if left.parts or right.parts:
-            raise Unsupported("row-producing join over a bucket union")
+            return self._join_rel_union(p, left, right, lk, rk)
+        return self._join_rel_pair(p, left, right, lk, rk)
+
+    def _join_rel_union(self, p: X.SortMergeJoinExec, left: DRel, right: DRel, lk, rk) -> DRel:
+        """Inner join rows over BucketUnion inputs (Hybrid Scan: index buckets plus appended
+        rows shuffled by the index bucket spec): an inner join distributes over union, so each
+        (left part, right part) pair runs as its own co-located join and the row sets are
+        concatenated; string columns whose parts carry different dictionaries are re-coded
+        over the union of the dictionaries."""
+        import torch
+        from ..parallel.dictionary import remap_table
+        if p.join_type != "inner":
+            raise Unsupported(f"{p.join_type} join over a bucket union")
+        out_attrs = list(p.output)
+        pieces = [self._join_rel_pair(p, lp, rp, lk, rk)
+                  for lp in (left.parts or [left]) for rp in (right.parts or [right])]
+        cols = {}
+        for a in out_attrs:
+            cs = [x.col(a) for x in pieces]
+            dicts = [c.dictionary for c in cs]
+            gd = None
+            if any(d is not None for d in dicts):
+                gd = dicts[0]
+                if not all(d is not None and d.equals(gd) for d in dicts):
+                    import pyarrow.compute as pc
+                    allv = pa.concat_arrays([d.cast(pa.string()) for d in dicts if d is not None])
+                    gd = pc.unique(allv).sort()
+            datas = []
+            for c in cs:
+                d = c.data
+                if gd is not None and c.dictionary is not None and not c.dictionary.equals(gd) \
+                        and d.numel():
+                    tab = torch.from_numpy(remap_table(c.dictionary, gd)).to(self.device)
+                    d = K.lookup_i32(tab, d)
+                datas.append(d)
+            valid = None
+            if any(c.valid is not None for c in cs):
+                valid = torch.cat([c.valid if c.valid is not None else
+                                   torch.ones(c.data.numel(), dtype=torch.uint8,
+                                              device=self.device) for c in cs])
+            col = DeviceColumn(torch.cat(datas), valid, cs[0].atype, gd)
+            col.hs_transient = True
+            cols[key(a)] = col
+        n = sum(int(x.table.num_rows or 0) for x in pieces)
+        off = np.array([0, n], dtype=np.int64)
+        table = DeviceTable(cols, n, torch.from_numpy(off).to(self.device), off)
+        return DRel(table, {a.expr_id: key(a) for a in out_attrs}, out_attrs)
+
+    def _join_rel_pair(self, p: X.SortMergeJoinExec, left: DRel, right: DRel, lk, rk) -> DRel:
         jt = p.join_type
         out_attrs = list(p.output)
         implied: set = set()

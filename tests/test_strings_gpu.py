@@ -95,6 +95,13 @@ def test_hybrid_scan_join_on_string_key_native(strs):
     g, c, path = _both(s, q2)
     assert path == "native", s.backend().fallback_reason
     _close(g, c)
+    # rows of the join: every (index part, appended part) pair joins on its own, the row sets
+    # concatenate, string columns re-coded over one dictionary
+    q3 = j.filter(col("w") < 20).select(fact["c3"], "v", "w")
+    g, c, path = _both(s, q3)
+    assert path == "native", s.backend().fallback_reason
+    assert g.num_rows > 0
+    _close(g, c)
 
 
 def test_non_index_string_join_device_shuffle(strs):
