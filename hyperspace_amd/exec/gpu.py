@@ -255,6 +255,22 @@ class GpuBackend:
             return self._repartition(self._rel(p.child), p.partitioning)
         if isinstance(p, X.SortMergeJoinExec):
             return self._join_rel(p)
+        if isinstance(p, X.UnionExec):
+            # UNION ALL: every child's rows (its pending filters applied) concatenated into one
+            # flat device relation, columns by position
+            out_attrs = list(p.output)
+            pieces = []
+            for child in p.children:
+                r = self._rel(child)
+                if r.parts:
+                    raise Unsupported("union of a bucket union")
+                got = self._materialize(r, list(child.output))
+                pieces.append([got[a.expr_id] for a in child.output])
+            for ai in range(len(out_attrs)):
+                if len({str(x[ai].atype) for x in pieces}) > 1 or \
+                        len({x[ai].data.dtype for x in pieces}) > 1:
+                    raise Unsupported("union of differently typed columns")
+            return self._concat_rels(pieces, out_attrs)
         if isinstance(p, X.ReusedExchangeExec):
             # the device repartition of a resident table is cached, so the original subtree
             # replays the first exchange's result
@@ -1022,16 +1038,22 @@ class GpuBackend:
         (left part, right part) pair runs as its own co-located join and the row sets are
         concatenated; string columns whose parts carry different dictionaries are re-coded
         over the union of the dictionaries."""
-        import torch
-        from ..parallel.dictionary import remap_table
         if p.join_type != "inner":
             raise Unsupported(f"{p.join_type} join over a bucket union")
         out_attrs = list(p.output)
         pieces = [self._join_rel_pair(p, lp, rp, lk, rk)
                   for lp in (left.parts or [left]) for rp in (right.parts or [right])]
+        return self._concat_rels([[x.col(a) for a in out_attrs] for x in pieces], out_attrs)
+
+    def _concat_rels(self, pieces: List[List[DeviceColumn]], out_attrs) -> DRel:
+        """One flat device relation over ``out_attrs`` from row sets ``pieces`` (per piece the
+        columns in ``out_attrs`` order); string columns with different dictionaries are
+        re-coded over their union."""
+        import torch
+        from ..parallel.dictionary import remap_table
         cols = {}
-        for a in out_attrs:
-            cs = [x.col(a) for x in pieces]
+        for ai, a in enumerate(out_attrs):
+            cs = [x[ai] for x in pieces]
             dicts = [c.dictionary for c in cs]
             gd = None
             if any(d is not None for d in dicts):
@@ -1056,7 +1078,7 @@ class GpuBackend:
             col = DeviceColumn(torch.cat(datas), valid, cs[0].atype, gd)
             col.hs_transient = True
             cols[key(a)] = col
-        n = sum(int(x.table.num_rows or 0) for x in pieces)
+        n = sum(int(x[0].data.numel()) for x in pieces) if out_attrs else 0
         off = np.array([0, n], dtype=np.int64)
         table = DeviceTable(cols, n, torch.from_numpy(off).to(self.device), off)
         return DRel(table, {a.expr_id: key(a) for a in out_attrs}, out_attrs)

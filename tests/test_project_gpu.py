@@ -85,3 +85,18 @@ def test_group_by_expressions_native(tbl):
         g, c, path = _both(s, q)
         assert path == "native", s.backend().fallback_reason
         _close(g, c)
+
+
+def test_union_all_rows_and_aggregates_native(tbl):
+    s, df = tbl
+    lo = df.filter(col("k") < 3000).select("k", "a", "x")
+    hi = df.filter(col("k") > 47_000).select("k", "a", "x")
+    u = lo.union(hi)
+    for q in (u,
+              u.agg(sum_("x").alias("sx"), count("*").alias("n"), sum_("a").alias("sa")),
+              u.groupBy((col("k") / 10_000).cast("int").alias("band"))
+               .agg(count("*").alias("n"), sum_("x").alias("sx"))):
+        g, c, path = _both(s, q)
+        assert path == "native", s.backend().fallback_reason
+        assert g.num_rows > 0
+        _close(g, c)
