@@ -470,6 +470,95 @@ __device__ void expand_page(const HsPqPage& p, const uint8_t* __restrict__ pg,
   }
 }
 
+// BOOLEAN data page -> one byte (0 / 1) per value.  PLAIN: bit-packed LSB first; RLE (enc 3):
+// a 4-byte length, then the RLE / bit-packed hybrid stream at bit width 1.  Runs are resolved
+// per 64-value slice by one lane each (a run header is at most a few bytes), so the whole
+// workgroup writes values.
+__device__ void expand_bool(const HsPqPage& p, const uint8_t* __restrict__ pg,
+                            int* __restrict__ status) {
+  uint8_t* out = (uint8_t*)p.out;
+  const int n = p.usize;
+  int voff = 0;
+  if (p.kind == 0 && p.levels) voff = 4 + (int)load_u32_at(pg, 0);
+  else if (p.kind == 1) voff = p.levels;
+  if (voff < 0 || voff > n) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
+  const int nv = p.nvals;
+  if (p.enc == 0) {
+    if ((nv + 7) / 8 > n - voff) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
+    for (int i = threadIdx.x; i < nv; i += blockDim.x)
+      out[i] = (uint8_t)((pg[voff + (i >> 3)] >> (i & 7)) & 1);
+    return;
+  }
+  if (n - voff < 4) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
+  const int64_t len = (int64_t)load_u32_at(pg, voff);
+  const int64_t s0 = voff + 4, send = s0 + len;
+  if (send > n) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
+  __shared__ int r_start[129];
+  __shared__ int64_t r_src[128];
+  __shared__ int r_kind[128];
+  __shared__ int r_meta[2];
+  int64_t pos = s0;
+  int done = 0;
+  while (done < nv) {
+    if (threadIdx.x == 0) {
+      int k = 0, acc = 0, err = 0;
+      int64_t q = pos;
+      while (k < 128 && done + acc < nv) {
+        uint64_t h = 0;
+        int shift = 0;
+        for (;;) {
+          if (q >= send || shift > 35) { err = 1; break; }
+          const uint8_t b = pg[q++];
+          h |= (uint64_t)(b & 0x7f) << shift;
+          if (!(b & 0x80)) break;
+          shift += 7;
+        }
+        if (err) break;
+        const int left = nv - done - acc;
+        if (h & 1) {                       // bit-packed: groups of 8 values, 1 byte each
+          const int64_t groups = (int64_t)(h >> 1);
+          if (q + groups > send) { err = 1; break; }
+          r_kind[k] = 1;
+          r_src[k] = q;
+          r_start[k] = acc;
+          acc += (int)(groups * 8 < left ? groups * 8 : left);
+          q += groups;
+        } else {                           // RLE: count, then one value byte
+          const int64_t cnt = (int64_t)(h >> 1);
+          if (q + 1 > send) { err = 1; break; }
+          const int v = pg[q++] & 1;
+          if (cnt == 0) continue;
+          r_kind[k] = 0;
+          r_src[k] = v;
+          r_start[k] = acc;
+          acc += (int)(cnt < left ? cnt : left);
+        }
+        ++k;
+      }
+      r_start[k] = acc;
+      r_meta[0] = k;
+      r_meta[1] = err || (k == 0 && done < nv);
+      pos = q;
+    }
+    __syncthreads();
+    const int k = r_meta[0];
+    if (r_meta[1]) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
+    const int total = r_start[k];
+    for (int i = threadIdx.x; i < total; i += blockDim.x) {
+      int lo = 0, hi = k - 1;
+      while (lo < hi) {
+        const int m = (lo + hi + 1) >> 1;
+        if (r_start[m] <= i) lo = m; else hi = m - 1;
+      }
+      const int j = i - r_start[lo];
+      out[done + i] = r_kind[lo] == 0 ? (uint8_t)r_src[lo]
+                                      : (uint8_t)((pg[r_src[lo] + (j >> 3)] >> (j & 7)) & 1);
+    }
+    __syncthreads();
+    done += total;
+  }
+}
+
 __global__ __launch_bounds__(256) void hs_pq_expand_kernel(
     const uint8_t* __restrict__ scratch, const HsPqPage* __restrict__ pages, int npages,
     int* __restrict__ status) {
@@ -480,6 +569,7 @@ __global__ __launch_bounds__(256) void hs_pq_expand_kernel(
   const uint8_t* pg = (const uint8_t*)p.dst;
   if (p.eb == 4) expand_page<uint32_t>(p, pg, pages, status);
   else if (p.eb == 8) expand_page<uint64_t>(p, pg, pages, status);
+  else if (p.eb == 1) expand_bool(p, pg, status);
   else if (threadIdx.x == 0) atomicOr(status, kErrCorrupt);
 }
 

@@ -696,10 +696,10 @@ struct HsPqPage {
   int32_t nvals;    // rows of the page (data pages) / dictionary entries (dictionary page)
   int32_t codec;    // 0 uncompressed, 1 snappy
   int32_t kind;     // 0 data v1, 1 data v2, 2 dictionary
-  int32_t enc;      // 0 PLAIN, 2 / 8 dictionary indices
+  int32_t enc;      // 0 PLAIN, 2 / 8 dictionary indices, 3 RLE (booleans)
   int32_t levels;   // v1: 1 if a length-prefixed definition-level stream precedes the values;
                     // v2: byte length of the (never compressed) level streams
-  int32_t eb;       // element bytes (4 / 8)
+  int32_t eb;       // element bytes (4 / 8; 1: BOOLEAN, one byte per value)
   int32_t dict_page;  // index (within the plan) of the chunk's dictionary page, -1: none
   int32_t pad;
 };
@@ -721,7 +721,9 @@ int plan_chunk(File* f, int rg, int col, uint8_t* raw, int64_t raw_cap, int64_t 
   // caller parses its strings, hs_pq_plain_strings) and the data pages decode on the device to
   // 4-byte dictionary codes through a code table the caller supplies in `dict`.
   const bool strings = m.type == 6;
-  const int eb = strings ? 4 : elem_bytes(m.type);
+  // BOOLEAN: bit-packed PLAIN or length-prefixed RLE (bit width 1) values, one byte per row out
+  const bool boolean = m.type == 0;
+  const int eb = strings ? 4 : (boolean ? 1 : elem_bytes(m.type));
   if (!eb) return HS_PQ_UNSUPPORTED;
   if (strings && !hbuf) return HS_PQ_UNSUPPORTED;
   if (m.codec != 0 && m.codec != 1) return HS_PQ_UNSUPPORTED;
@@ -755,7 +757,7 @@ int plan_chunk(File* f, int rg, int col, uint8_t* raw, int64_t raw_cap, int64_t 
     p.eb = eb;
     p.dict_page = -1;
     if (ph.type == 2) {
-      if (ph.enc != 0 && ph.enc != 2) return HS_PQ_UNSUPPORTED;
+      if (boolean || (ph.enc != 0 && ph.enc != 2)) return HS_PQ_UNSUPPORTED;
       p.kind = 2;
       p.usize = ph.usize;
       p.nvals = ph.dict_nvals;
@@ -763,8 +765,8 @@ int plan_chunk(File* f, int rg, int col, uint8_t* raw, int64_t raw_cap, int64_t 
         return HS_PQ_CORRUPT;
       dict_idx = *npages;
     } else {
-      const bool dict = ph.enc == 2 || ph.enc == 8;
-      if (!dict && ph.enc != 0) return HS_PQ_UNSUPPORTED;
+      const bool dict = !boolean && (ph.enc == 2 || ph.enc == 8);
+      if (!dict && ph.enc != 0 && !(boolean && ph.enc == 3)) return HS_PQ_UNSUPPORTED;
       if (strings && !dict) return HS_PQ_UNSUPPORTED;   // PLAIN strings: decoded another way
       if (dict && dict_idx < 0) return HS_PQ_CORRUPT;
       p.enc = ph.enc;

@@ -53,6 +53,8 @@ class ChunkInfo(C.Structure):
 def _native_kind(t: pa.DataType):
     if pa.types.is_string(t) or pa.types.is_large_string(t):
         return 6, 4                     # BYTE_ARRAY -> int32 dictionary codes (device path only)
+    if pa.types.is_boolean(t):
+        return 0, 1                     # BOOLEAN -> one byte per value (device path only)
     if pa.types.is_int32(t) or pa.types.is_date32(t):
         return 1, 4
     if pa.types.is_int64(t) or pa.types.is_timestamp(t) or pa.types.is_duration(t):
@@ -231,7 +233,7 @@ def upload_file(path: str, fields: Sequence[pa.Field], cols: Dict[str, object], 
         plan = []
         for fld in fields:
             kind = _native_kind(fld.type)
-            if kind is None or kind[0] == 6:
+            if kind is None or kind[0] in (0, 6):
                 continue
             c = f.column(fld.name)
             if c < 0:
@@ -514,6 +516,8 @@ def upload_file_device(path: str, fields: Sequence[pa.Field], cols: Dict[str, ob
             ptype, _, eb = f.column_info(c)
             if kind[0] == 6 and ptype == 6:
                 eb = 4
+            elif kind[0] == 0 and ptype == 0:
+                eb = 1
             if eb == 0 or ptype != kind[0]:
                 continue
             plan.append((fld, c, eb))
@@ -626,6 +630,32 @@ def _string_code_tables(chunks, pages, host_base: int, strings):
     return (np.concatenate(tabs) if at else np.zeros(1, np.int32)), fix
 
 
+def _hybrid_host(s: np.ndarray, bw: int, nv: int) -> np.ndarray:
+    """The ``nv`` values of an RLE / bit-packed hybrid stream ``s`` at bit width ``bw``."""
+    out = np.zeros(nv, dtype=np.int64)
+    q, done = 0, 0
+    while done < nv:
+        h, shift = 0, 0
+        while True:
+            b = int(s[q]); q += 1
+            h |= (b & 0x7F) << shift
+            if not b & 0x80:
+                break
+            shift += 7
+        if h & 1:
+            groups = h >> 1
+            take = min(groups * 8, nv - done)
+            out[done:done + take] = _unpack(s, q, take, bw) if bw else 0
+            q += groups * bw
+        else:
+            vb = (bw + 7) // 8
+            take = min(h >> 1, nv - done)
+            out[done:done + take] = int.from_bytes(bytes(s[q:q + vb]), "little")
+            q += vb
+        done += take
+    return out
+
+
 def decode_plan_host(raw: np.ndarray, pages: np.ndarray, outputs: Dict[int, np.ndarray],
                      host_dicts: Optional[np.ndarray] = None) -> None:
     """Reference (host) consumer of a device page plan — the oracle for hs_pq_decode_pages.
@@ -653,7 +683,7 @@ def decode_plan_host(raw: np.ndarray, pages: np.ndarray, outputs: Dict[int, np.n
         if p["kind"] == 2:
             continue
         pg = scratch[i]
-        dt = np.dtype(np.uint32 if p["eb"] == 4 else np.uint64)
+        dt = np.dtype({1: np.uint8, 4: np.uint32}.get(int(p["eb"]), np.uint64))
         voff = 0
         if p["kind"] == 0 and p["levels"]:
             voff = 4 + int(pg[:4].view(np.uint32)[0])
@@ -661,6 +691,13 @@ def decode_plan_host(raw: np.ndarray, pages: np.ndarray, outputs: Dict[int, np.n
             voff = int(p["levels"])
         nv = int(p["nvals"])
         dst = outputs[int(p["out"])]
+        if p["eb"] == 1:                 # BOOLEAN: PLAIN bits or length-prefixed RLE, width 1
+            if p["enc"] == 0:
+                dst[:nv] = np.unpackbits(pg[voff:voff + (nv + 7) // 8], bitorder="little")[:nv]
+            else:
+                dst[:nv] = _hybrid_host(pg[voff + 4:voff + 4 + int(pg[voff:voff + 4].view(
+                    np.uint32)[0])], 1, nv)
+            continue
         if p["enc"] == 0:
             dst[:nv] = pg[voff:voff + nv * dt.itemsize].view(dt)
             continue

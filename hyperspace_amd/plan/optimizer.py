@@ -181,6 +181,12 @@ def column_pruning(plan, required=None):
 def _prune_child(child, need: set, wrap: bool):
     out = child.output
     keep = [a for a in out if a.expr_id in need]
+    if wrap and not keep and isinstance(child, L.Filter):
+        # COUNT(*) over a filter needs no column of its own: keep one the filter reads anyway,
+        # so the scan below narrows to the filter's columns (Spark's empty Project) and a
+        # covering index over them qualifies (FilterIndexRule.scala:59-65)
+        refs = {a.expr_id for a in child.condition.references()}
+        keep = [a for a in out if a.expr_id in refs][:1]
     if isinstance(child, L.Project):
         plist = [e for e in child.project_list
                  if (e.expr_id if isinstance(e, (E.Attribute, E.Alias)) else None) in need]

@@ -8,7 +8,7 @@ import pyarrow.csv as pacsv
 import pyarrow.json  # noqa: F401
 import pytest
 
-from hyperspace_amd import Hyperspace, IndexConfig, col
+from hyperspace_amd import Hyperspace, IndexConfig, col, count
 from hyperspace_amd.plan import physical as X
 
 from helpers import (count_nodes, index_names_used, make_session, sample_table, scans,
@@ -46,6 +46,17 @@ def test_filter_index_range_predicates_and_sql_string(env):
                        .select("clicks", "Query"), {"fIdx"})
     verify_index_usage(s, lambda: s.read.parquet(src).filter(col("clicks").isin(10, 90))
                        .select("Query"), {"fIdx"})
+
+
+def test_filter_index_used_for_count_star_over_filter(env):
+    # COUNT(*) reads no column of its own: the scan narrows to the filter's columns, which the
+    # index covers
+    s, hs, src = env
+    hs.createIndex(s.read.parquet(src), IndexConfig("fIdx", ["clicks"], ["Query"]))
+    df = verify_index_usage(
+        s, lambda: s.read.parquet(src).filter((col("clicks") >= 30) & (col("Query") != "ibraco"))
+        .agg(count("*").alias("n")), {"fIdx"})
+    assert df.collect()[0].n > 0
 
 
 def test_filter_index_not_used_without_first_indexed_column(env):

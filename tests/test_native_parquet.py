@@ -154,7 +154,9 @@ def _plan_and_decode_host(path, names):
         plan = []
         for name in names:
             c = f.column(name)
-            _, _, eb = f.column_info(c)
+            ptype, _, eb = f.column_info(c)
+            if ptype == 0:               # BOOLEAN: one byte per value on the device path
+                eb = 1
             plan.append((pa.field(name, pa.int64()), c, eb))
         cap = sum(int(f.L.hs_pq_chunk_raw_bytes(f.h, g, c)) + 16
                   for _, c, _ in plan for g in range(f.num_row_groups)) + 64
@@ -167,7 +169,7 @@ def _plan_and_decode_host(path, names):
         assert raw_used <= cap and host_used <= hcap
         rg_off = np.concatenate([[0], np.cumsum([f.row_group_rows(g)
                                                  for g in range(f.num_row_groups)])])
-        out = {fld.name: np.zeros(f.num_rows, dtype=np.uint32 if eb == 4 else np.uint64)
+        out = {fld.name: np.zeros(f.num_rows, dtype={1: np.uint8, 4: np.uint32}.get(eb, np.uint64))
                for fld, _, eb in plan}
         targets = {}
         for fld, g, p0, n in chunks:
@@ -207,6 +209,27 @@ def test_device_page_plan_matches_pyarrow(tmp_path, compression, dictionary, pag
             ref = ref.view(pa.int32())
         nd = ref.to_numpy()
         np.testing.assert_array_equal(vals[name].view(nd.dtype), nd)
+
+
+@pytest.mark.parametrize("compression", ["none", "snappy"])
+@pytest.mark.parametrize("encoding", ["PLAIN", "RLE"])
+@pytest.mark.parametrize("page_version", ["1.0", "2.0"])
+def test_device_page_plan_booleans(tmp_path, compression, encoding, page_version):
+    """BOOLEAN chunks (bit-packed PLAIN and length-prefixed RLE pages, v1 and v2) plan for the
+    device and decode to one byte per value; runs of equal values exercise the RLE runs."""
+    rng = np.random.default_rng(3)
+    n = 50_000
+    runs = np.repeat(rng.random(n // 100) < 0.5, 100)
+    t = pa.table({"b": pa.array(rng.random(n) < 0.3), "r": pa.array(runs),
+                  "k": pa.array(rng.integers(0, 9, n))})
+    path = tmp_path / "b.parquet"
+    pq.write_table(t, path, compression=compression, use_dictionary=False,
+                   column_encoding={"b": encoding, "r": encoding, "k": "PLAIN"},
+                   data_page_version=page_version, row_group_size=20_000, data_page_size=2048)
+    vals, skipped = _plan_and_decode_host(path, ["b", "r", "k"])
+    assert not skipped
+    for name in ("b", "r"):
+        np.testing.assert_array_equal(vals[name], t.column(name).to_numpy().astype(np.uint8))
 
 
 def test_device_page_plan_large_dictionary(tmp_path):
@@ -566,5 +589,46 @@ def test_device_timestamp_decode_matches_pyarrow(tmp_path, device):
         valid = np.asarray(ref.is_valid())
         got = up.columns[name].data.cpu().numpy()
         np.testing.assert_array_equal(got[valid], ref.view(pa.int64()).drop_null().to_numpy())
+        if ref.null_count:
+            np.testing.assert_array_equal(up.columns[name].valid.cpu().numpy().astype(bool), valid)
+
+
+@pytest.mark.gpu
+def test_device_boolean_decode_matches_pyarrow(tmp_path, device):
+    """BOOLEAN columns (PLAIN and RLE pages, v1 and v2, one file with nulls) decode on the device
+    to one byte per row; the file with nulls takes the host page layer."""
+    import torch
+    from hyperspace_amd.exec import staging
+    rng = np.random.default_rng(6)
+    files, tables = [], []
+    for i, (enc, ver, nulls) in enumerate([("PLAIN", "1.0", False), ("RLE", "2.0", False),
+                                           ("RLE", "1.0", False), ("PLAIN", "2.0", True)]):
+        n = 30_000
+        runs = np.repeat(rng.random(n // 50) < 0.5, 50)
+        mask = (rng.random(n) < 0.1) if nulls else None
+        t = pa.table({"b": pa.array(rng.random(n) < 0.4, mask=mask), "r": pa.array(runs),
+                      "k": pa.array(rng.integers(0, 100, n))})
+        path = tmp_path / f"b{i}.parquet"
+        pq.write_table(t, path, use_dictionary=False, row_group_size=12_000,
+                       column_encoding={"b": enc, "r": enc, "k": "PLAIN"},
+                       data_page_version=ver, data_page_size=4096, compression="snappy")
+        files.append(str(path))
+        tables.append(pq.read_table(path))
+    full = pa.concat_tables(tables)
+
+    def read_file(p, cols=None):
+        return pq.read_table(p, columns=cols)
+    staging.DEVICE_DECODED.clear()
+    staging.HOST_DECODED.clear()
+    up = staging.upload_files(read_file, files, [t.num_rows for t in tables], full.schema,
+                              device, parquet_local=files)
+    torch.cuda.synchronize()
+    assert "r" in staging.DEVICE_DECODED and "r" not in staging.HOST_DECODED
+    assert "b" in staging.DEVICE_DECODED
+    for name in ("b", "r"):
+        ref = full.column(name).combine_chunks()
+        valid = np.asarray(ref.is_valid())
+        got = up.columns[name].data.cpu().numpy()
+        np.testing.assert_array_equal(got[valid], ref.drop_null().to_numpy(zero_copy_only=False).astype(np.uint8))
         if ref.null_count:
             np.testing.assert_array_equal(up.columns[name].valid.cpu().numpy().astype(bool), valid)
