@@ -116,7 +116,8 @@ __global__ __launch_bounds__(256) void hs_pq_levels_kernel(
 // into addresses; host-inflated pages, codec 2, point at their own device copy)
 struct HsPqPage {
   int64_t src, dst, out, dict, row;
-  int32_t csize, usize, nvals, codec, kind, enc, levels, eb, dict_page, pad;
+  int32_t csize, usize, nvals, codec, kind, enc, levels, eb, dict_page, nulls;
+  int64_t valid;   // nulls != 0: device address of the page's first validity byte
 };
 
 enum : int { kErrCorrupt = 1, kErrDictRange = 2 };
@@ -365,7 +366,7 @@ __global__ __launch_bounds__(256) void hs_pq_inflate_kernel(
 
 template <typename T>
 __device__ void expand_page(const HsPqPage& p, const uint8_t* __restrict__ pg,
-                            const HsPqPage* __restrict__ pages, int* __restrict__ status) {
+                            const HsPqPage* __restrict__ pages, int nv, int* __restrict__ status) {
   __shared__ int r_start[129];
   __shared__ int64_t r_src[128];
   __shared__ int r_kind[128];
@@ -377,11 +378,11 @@ __device__ void expand_page(const HsPqPage& p, const uint8_t* __restrict__ pg,
   else if (p.kind == 1) voff = p.levels;
   if (voff < 0 || voff > n) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
   if (p.enc == 0) {                   // PLAIN
-    if ((int64_t)p.nvals * (int64_t)sizeof(T) > n - voff) {
+    if ((int64_t)nv * (int64_t)sizeof(T) > n - voff) {
       if (threadIdx.x == 0) atomicOr(status, kErrCorrupt);
       return;
     }
-    for (int i = threadIdx.x; i < p.nvals; i += blockDim.x)
+    for (int i = threadIdx.x; i < nv; i += blockDim.x)
       out[i] = load_elem<T>(pg, voff + (int64_t)i * (int64_t)sizeof(T));
     return;
   }
@@ -395,11 +396,11 @@ __device__ void expand_page(const HsPqPage& p, const uint8_t* __restrict__ pg,
   const int vbytes = (bw + 7) / 8;
   int64_t pos = s0;
   int done = 0;
-  while (done < p.nvals) {
+  while (done < nv) {
     if (threadIdx.x == 0) {
       int k = 0, acc = 0, err = 0;
       int64_t q = pos;
-      while (k < 128 && done + acc < p.nvals) {
+      while (k < 128 && done + acc < nv) {
         uint64_t h = 0;
         int shift = 0;
         for (;;) {
@@ -410,7 +411,7 @@ __device__ void expand_page(const HsPqPage& p, const uint8_t* __restrict__ pg,
           shift += 7;
         }
         if (err) break;
-        const int left = p.nvals - done - acc;
+        const int left = nv - done - acc;
         if (h & 1) {
           const int64_t groups = (int64_t)(h >> 1);
           const int64_t nbytes = groups * bw;
@@ -437,7 +438,7 @@ __device__ void expand_page(const HsPqPage& p, const uint8_t* __restrict__ pg,
       }
       r_start[k] = acc;
       r_meta[0] = k;
-      r_meta[2] = err || (k == 0 && done < p.nvals);
+      r_meta[2] = err || (k == 0 && done < nv);
       pos = q;
     }
     __syncthreads();
@@ -474,7 +475,7 @@ __device__ void expand_page(const HsPqPage& p, const uint8_t* __restrict__ pg,
 // a 4-byte length, then the RLE / bit-packed hybrid stream at bit width 1.  Runs are resolved
 // per 64-value slice by one lane each (a run header is at most a few bytes), so the whole
 // workgroup writes values.
-__device__ void expand_bool(const HsPqPage& p, const uint8_t* __restrict__ pg,
+__device__ void expand_bool(const HsPqPage& p, const uint8_t* __restrict__ pg, int nv,
                             int* __restrict__ status) {
   uint8_t* out = (uint8_t*)p.out;
   const int n = p.usize;
@@ -482,7 +483,6 @@ __device__ void expand_bool(const HsPqPage& p, const uint8_t* __restrict__ pg,
   if (p.kind == 0 && p.levels) voff = 4 + (int)load_u32_at(pg, 0);
   else if (p.kind == 1) voff = p.levels;
   if (voff < 0 || voff > n) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
-  const int nv = p.nvals;
   if (p.enc == 0) {
     if ((nv + 7) / 8 > n - voff) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
     for (int i = threadIdx.x; i < nv; i += blockDim.x)
@@ -559,6 +559,131 @@ __device__ void expand_bool(const HsPqPage& p, const uint8_t* __restrict__ pg,
   }
 }
 
+// Block-wide sum of one int per thread (256 threads: 4 wavefronts).
+__device__ __forceinline__ int block_sum(int v, int* __restrict__ s_part) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return s_part[0] + s_part[1] + s_part[2] + s_part[3];
+}
+
+// Definition levels (max level 1) of a page with nulls -> one validity byte per row at
+// `valid`; returns the page's non-null value count (every thread), or -1 on corruption.  v1
+// pages carry a 4-byte length then the RLE / bit-packed hybrid stream; v2 pages the bare stream
+// of `levels` bytes.  Runs are cut by one lane (headers are a few bytes), rows written by all.
+__device__ int expand_levels(const HsPqPage& p, const uint8_t* __restrict__ pg,
+                             uint8_t* __restrict__ valid) {
+  __shared__ int r_start[129];
+  __shared__ int64_t r_src[128];
+  __shared__ int r_kind[128];
+  __shared__ int r_meta[2];
+  __shared__ int s_part[4];
+  const int n = p.usize, nv = p.nvals;
+  int64_t s0, send;
+  if (p.kind == 0) {
+    if (!p.levels || n < 4) return -1;
+    s0 = 4;
+    send = 4 + (int64_t)load_u32_at(pg, 0);
+  } else {
+    s0 = 0;
+    send = p.levels;
+  }
+  if (send > n) return -1;
+  int64_t pos = s0;
+  int done = 0, ones = 0;
+  while (done < nv) {
+    if (threadIdx.x == 0) {
+      int k = 0, acc = 0, err = 0;
+      int64_t q = pos;
+      while (k < 128 && done + acc < nv) {
+        uint64_t h = 0;
+        int shift = 0;
+        for (;;) {
+          if (q >= send || shift > 35) { err = 1; break; }
+          const uint8_t b = pg[q++];
+          h |= (uint64_t)(b & 0x7f) << shift;
+          if (!(b & 0x80)) break;
+          shift += 7;
+        }
+        if (err) break;
+        const int left = nv - done - acc;
+        if (h & 1) {
+          const int64_t groups = (int64_t)(h >> 1);
+          if (q + groups > send) { err = 1; break; }
+          r_kind[k] = 1;
+          r_src[k] = q;
+          r_start[k] = acc;
+          acc += (int)(groups * 8 < left ? groups * 8 : left);
+          q += groups;
+        } else {
+          const int64_t cnt = (int64_t)(h >> 1);
+          if (q + 1 > send) { err = 1; break; }
+          const int v = pg[q++] & 1;
+          if (cnt == 0) continue;
+          r_kind[k] = 0;
+          r_src[k] = v;
+          r_start[k] = acc;
+          acc += (int)(cnt < left ? cnt : left);
+        }
+        ++k;
+      }
+      r_start[k] = acc;
+      r_meta[0] = k;
+      r_meta[1] = err || (k == 0 && done < nv);
+      pos = q;
+    }
+    __syncthreads();
+    const int k = r_meta[0];
+    if (r_meta[1]) return -1;
+    const int total = r_start[k];
+    for (int i = threadIdx.x; i < total; i += blockDim.x) {
+      int lo = 0, hi = k - 1;
+      while (lo < hi) {
+        const int m = (lo + hi + 1) >> 1;
+        if (r_start[m] <= i) lo = m; else hi = m - 1;
+      }
+      const int j = i - r_start[lo];
+      const uint8_t v = r_kind[lo] == 0 ? (uint8_t)r_src[lo]
+                                        : (uint8_t)((pg[r_src[lo] + (j >> 3)] >> (j & 7)) & 1);
+      valid[done + i] = v;
+      ones += v;
+    }
+    __syncthreads();
+    done += total;
+  }
+  return block_sum(ones, s_part);
+}
+
+// In-place spread of a page's `nonnull` dense values (out[0, nonnull)) to their rows
+// (out[row] for valid rows, 0 for nulls).  Rank(row) <= row, so 256-row chunks are processed
+// from the last: a chunk only overwrites dense slots at or after its first row, which no
+// earlier chunk reads, and within a chunk every source is loaded before any store.
+template <typename T>
+__device__ void spread_nulls(T* __restrict__ out, const uint8_t* __restrict__ valid, int nv,
+                             int nonnull) {
+  __shared__ int s_wave[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int base_end = nonnull;
+  for (int c = ((nv + 255) >> 8) - 1; c >= 0; --c) {
+    const int r = (c << 8) + (int)threadIdx.x;
+    const bool v = r < nv && valid[r] != 0;
+    const uint64_t bal = __ballot(v);
+    const int rank_in_wave = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) s_wave[w] = __popcll(bal);
+    __syncthreads();
+    int before = 0;
+    for (int x = 0; x < w; ++x) before += s_wave[x];
+    const int chunk = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+    const int base = base_end - chunk;
+    const T x = v ? out[base + before + rank_in_wave] : (T)0;
+    __syncthreads();
+    if (r < nv) out[r] = x;
+    base_end = base;
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256) void hs_pq_expand_kernel(
     const uint8_t* __restrict__ scratch, const HsPqPage* __restrict__ pages, int npages,
     int* __restrict__ status) {
@@ -567,10 +692,24 @@ __global__ __launch_bounds__(256) void hs_pq_expand_kernel(
   const HsPqPage p = pages[pi];
   if (p.kind == 2 || p.nvals == 0) return;     // dictionary pages are read by the data pages
   const uint8_t* pg = (const uint8_t*)p.dst;
-  if (p.eb == 4) expand_page<uint32_t>(p, pg, pages, status);
-  else if (p.eb == 8) expand_page<uint64_t>(p, pg, pages, status);
-  else if (p.eb == 1) expand_bool(p, pg, status);
-  else if (threadIdx.x == 0) atomicOr(status, kErrCorrupt);
+  int nv = p.nvals;
+  uint8_t* valid = (uint8_t*)p.valid;
+  if (p.nulls) {                               // levels first, then the non-null values dense
+    if (!valid) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
+    nv = expand_levels(p, pg, valid);
+    if (nv < 0 || nv > p.nvals) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
+  }
+  if (nv > 0) {
+    if (p.eb == 4) expand_page<uint32_t>(p, pg, pages, nv, status);
+    else if (p.eb == 8) expand_page<uint64_t>(p, pg, pages, nv, status);
+    else if (p.eb == 1) expand_bool(p, pg, nv, status);
+    else if (threadIdx.x == 0) atomicOr(status, kErrCorrupt);
+  }
+  if (!p.nulls) return;
+  __syncthreads();
+  if (p.eb == 4) spread_nulls<uint32_t>((uint32_t*)p.out, valid, p.nvals, nv);
+  else if (p.eb == 8) spread_nulls<uint64_t>((uint64_t*)p.out, valid, p.nvals, nv);
+  else if (p.eb == 1) spread_nulls<uint8_t>((uint8_t*)p.out, valid, p.nvals, nv);
 }
 
 extern "C" {

@@ -437,6 +437,7 @@ constexpr int64_t kChunk = 4096;  // split long runs so each GPU work item stays
 constexpr int kHostDictMin = 64 << 10;
 constexpr int64_t kDeviceInflateMax = 2 << 20;   // largest page a wavefront inflates
 std::atomic<int> g_host_inflate{2};   // hs_pq_set_host_inflate
+std::atomic<int> g_device_nulls{1};   // hs_pq_set_device_nulls
 
 // Parse an RLE/bit-packed hybrid stream of `count` values into runs (dst starts at `dst0`).
 // `base` is the stream's byte offset in the chunk buffer.  Returns the number of non-zero
@@ -701,7 +702,9 @@ struct HsPqPage {
                     // v2: byte length of the (never compressed) level streams
   int32_t eb;       // element bytes (4 / 8; 1: BOOLEAN, one byte per value)
   int32_t dict_page;  // index (within the plan) of the chunk's dictionary page, -1: none
-  int32_t pad;
+  int32_t nulls;    // 1: the page may hold nulls - its definition levels decode to validity
+                    // bytes at `valid` and the dense values spread to their rows
+  int64_t valid;    // device address of the page's first validity byte (caller fills it in)
 };
 
 namespace {
@@ -728,8 +731,10 @@ int plan_chunk(File* f, int rg, int col, uint8_t* raw, int64_t raw_cap, int64_t 
   if (strings && !hbuf) return HS_PQ_UNSUPPORTED;
   if (m.codec != 0 && m.codec != 1) return HS_PQ_UNSUPPORTED;
   const bool optional = s.repetition == 1;
-  // the device path writes values at their row index: every row must hold a value
-  if (optional && m.null_count != 0) return HS_PQ_NULLS;
+  // chunks with nulls (or without a null count): the kernels decode the definition levels too,
+  // unless disabled (hs_pq_set_device_nulls), in which case another path decodes the chunk
+  const bool nullable = optional && m.null_count != 0;
+  if (nullable && !g_device_nulls.load(std::memory_order_relaxed)) return HS_PQ_NULLS;
   const int64_t start = m.dict_page_offset > 0 && m.dict_page_offset < m.data_page_offset
                             ? m.dict_page_offset : m.data_page_offset;
   const int64_t len = m.total_compressed;
@@ -772,6 +777,7 @@ int plan_chunk(File* f, int rg, int col, uint8_t* raw, int64_t raw_cap, int64_t 
       p.enc = ph.enc;
       p.nvals = ph.nvals;
       p.row = rows;
+      p.nulls = nullable ? 1 : 0;
       p.dict_page = dict ? dict_idx : -1;
       if (ph.v2) {
         if (ph.v2_rep_len) return HS_PQ_UNSUPPORTED;
@@ -872,6 +878,10 @@ int hs_pq_plan_chunk(void* h, int rg, int col, uint8_t* raw, int64_t raw_cap, in
 // on the device), 1 large dictionary pages only, 2 those and tag-dense data pages (default),
 // 3 as 2 but every third tag-dense data page is left to the device.
 void hs_pq_set_host_inflate(int mode) { g_host_inflate.store(mode, std::memory_order_relaxed); }
+
+// 1 (default): device page plans accept chunks with nulls (levels decoded on the device);
+// 0: such chunks report HS_PQ_NULLS and go through the host page layer.
+void hs_pq_set_device_nulls(int on) { g_device_nulls.store(on, std::memory_order_relaxed); }
 
 int64_t hs_pq_chunk_host_bound(void* h, int rg, int col) {
   const ChunkMeta& m = ((File*)h)->rgs[(size_t)rg].cols[(size_t)col];

@@ -88,6 +88,12 @@ MJ_STEPS = int(os.environ.get("HS_JIT_MJ_STEPS", "1"))   # branch-free walk step
 MJ_STAGE_UNROLL = int(os.environ.get("HS_JIT_MJ_STAGE_UNROLL", "4"))
 MJ_DBUF = os.environ.get("HS_JIT_MJ_DBUF", "0") == "1"
 MJ_PREFETCH = os.environ.get("HS_JIT_MJ_PREFETCH", "0") == "1"
+# right-span prefetch: tile t+1's span bounds and first staging round are loaded into registers
+# at the top of tile t (span bounds of t+2 with them), so staging a tile's right keys is an LDS
+# store instead of two dependent HBM round trips at the head of every tile.  Off by default: it
+# measured 1.63 vs 1.40 ms at SF100 (profiles/mj_sweep_r3_rpf.jsonl; the staging share of the
+# kernel is ~0.22 ms: profiles/mj_decompose_r3.jsonl)
+MJ_RPF = os.environ.get("HS_JIT_MJ_RPF", "0") == "1"
 # workgroup size of the merge join: 64 = one wavefront per workgroup working its own 512-row
 # tiles (own right span, no block barriers), 256 = four wavefronts sharing 2048-row tiles
 MJ_BLOCK = int(os.environ.get("HS_JIT_MJ_BLOCK", "256"))
@@ -1286,7 +1292,7 @@ def merge_join_shape(p: NL.JoinParams, compacts=None, hk=None) -> tuple:
     return ("merge_join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey,
             p.key_is_float, MJ_ITEMS, MJ_LDS_KEYS, MJ_STEPS, BLOCK, WAVE_SYNC,
             _key32_frame(p, compacts) is not None, MJ_EXP, MJ_STAGE_UNROLL, MJ_DBUF, MJ_PREFETCH,
-            MJ_BLOCK, MJ_EAGER, MJ_SPARSE, MJ_HASH_LANEMAJOR,
+            MJ_BLOCK, MJ_EAGER, MJ_SPARSE, MJ_HASH_LANEMAJOR, MJ_RPF and not MJ_PREFETCH,
             hk.shape() if hk is not None else None)
 
 
@@ -1536,9 +1542,40 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
             return _key_expr(f"x{lk}_{it}", fl)
         return f"((unsigned)x{lk}v[{it}] + (unsigned)a.KOF)"
 
+    U = max(1, MJ_STAGE_UNROLL)  # noqa: N806
+    rpf = MJ_RPF and not MJ_PREFETCH
+    pf_slots = list(dict.fromkeys(stage_slots + rtail))
+
+    def pf_issue(b: List[str], i2: str, ssv: str, sev: str) -> None:
+        """Loads of the first staging round of the span [ssv, sev) into the pk/pn registers."""
+        b.append(f"{i2}{{ const int nsq_ = (int)({sev} - {ssv});")
+        for u in range(U):
+            b.append(f"{i2}  const i64 jq{u}_ = {ssv} + ({u * BLOCK} + (int)threadIdx.x < nsq_ ? "
+                     f"{u * BLOCK} + (int)threadIdx.x : 0);")
+        for u in range(U):
+            for sl in pf_slots:
+                b.append(f"{i2}  pk{sl}_{u} = {g1.ptr(sl)}[jq{u}_];")
+                if cols[sl][1]:
+                    b.append(f"{i2}  pn{sl}_{u} = {g1.vptr(sl)}[jq{u}_];")
+        b.append(f"{i2}}}")
+
     def body(b: List[str], full: bool) -> None:
-        b.extend([f"{ind}const i64 ss = a.spans[4 * t + 2], se = a.spans[4 * t + 3];",
-                  f"{ind}const int ns = (int)(se - ss);",
+        if rpf:
+            # this tile's span and first staging round came with the previous tile; issue the
+            # next tile's now (its span bounds were loaded one tile earlier still)
+            b.extend([f"{ind}const i64 ss = ssC, se = seC;"])
+            for u in range(U):
+                for sl in pf_slots:
+                    b.append(f"{ind}const {g1.raw_type(sl)} ck{sl}_{u} = pk{sl}_{u};")
+                    if cols[sl][1]:
+                        b.append(f"{ind}const unsigned char cn{sl}_{u} = pn{sl}_{u};")
+            pf_issue(b, ind, "ssN", "seN")
+            b.extend([f"{ind}i64 ssNN = 0, seNN = 0;",
+                      f"{ind}if (t + 2 < t1) {{ ssNN = a.spans[4 * (t + 2) + 2]; "
+                      f"seNN = a.spans[4 * (t + 2) + 3]; }}"])
+        else:
+            b.append(f"{ind}const i64 ss = a.spans[4 * t + 2], se = a.spans[4 * t + 3];")
+        b.extend([f"{ind}const int ns = (int)(se - ss);",
                   f"{ind}const bool staged = ns <= {LK};",
                   f"{ind}{KT}* const skeys = skeys_[{'(int)(t & 1)' if NB == 2 else '0'}];",
                   f"{ind}unsigned char* const spass = spass_[{'(int)(t & 1)' if NB == 2 else '0'}];"])
@@ -1551,29 +1588,42 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
         # issues the loads of U rows per thread before any store (one HBM round trip per round
         # instead of one per row)
         stg = "staged && false" if "nostage" in MJ_EXP else "staged"
-        U = max(1, MJ_STAGE_UNROLL)  # noqa: N806
-        b.extend([f"{ind}if ({stg}) for (int sqb = 0; sqb < ns; sqb += {BLOCK * U}) {{"])
+        okk_fmt = f"n{rk}_s{{u}}" if cols[rk][1] else "true"
+
+        def stage_stores(i2: str) -> None:
+            for u in range(U):
+                gs = _Gen(args, cols, split, (f"jr{u}", f"jr{u}"), approx, True)
+                cond = _rename(gs.cnf(ronly), allslots, f"s{u}")
+                okk = okk_fmt.format(u=u)
+                b.extend([f"{i2}if (sv{u}) {{ const bool kv = {okk};",
+                          f"{i2}  skeys[sq{u}] = kv ? {rimg(f'x{rk}_s{u}')} : ({KT})0;",
+                          f"{i2}  spass[sq{u}] = (kv && {cond}) ? 1 : 0;"])
+                for x in rtail:
+                    b.append(f"{i2}  stv{x}[sq{u}] = x{x}_s{u};")
+                    if cols[x][1]:
+                        b.append(f"{i2}  stn{x}[sq{u}] = n{x}_s{u} ? 1 : 0;")
+                b.append(f"{i2}}}")
+        if rpf:
+            # round 0 from the prefetched registers
+            b.append(f"{ind}if ({stg}) {{")
+            for u in range(U):
+                b.extend([f"{ind}  const int sq{u} = {u * BLOCK} + (int)threadIdx.x;",
+                          f"{ind}  const bool sv{u} = sq{u} < ns;"])
+                for sl in pf_slots:
+                    _uload_raw(g1, sl, f"s{u}", f"ck{sl}_{u}", f"cn{sl}_{u}", b, ind + "  ")
+            stage_stores(ind + "  ")
+            b.append(f"{ind}}}")
+        sq0 = BLOCK * U if rpf else 0
+        b.extend([f"{ind}if ({stg}) for (int sqb = {sq0}; sqb < ns; sqb += {BLOCK * U}) {{"])
         for u in range(U):
             b.extend([f"{ind}  const int sq{u} = sqb + {u * BLOCK} + (int)threadIdx.x;",
                       f"{ind}  const bool sv{u} = sq{u} < ns;",
                       f"{ind}  const i64 jr{u} = ss + (sv{u} ? sq{u} : 0);"])
         for u in range(U):
             gs = _Gen(args, cols, split, (f"jr{u}", f"jr{u}"), approx, True)
-            for sl in list(dict.fromkeys(stage_slots + rtail)):
+            for sl in pf_slots:
                 _uload(gs, sl, f"s{u}", b, ind + "  ")
-        okk_fmt = f"n{rk}_s{{u}}" if cols[rk][1] else "true"
-        for u in range(U):
-            gs = _Gen(args, cols, split, (f"jr{u}", f"jr{u}"), approx, True)
-            cond = _rename(gs.cnf(ronly), allslots, f"s{u}")
-            okk = okk_fmt.format(u=u)
-            b.extend([f"{ind}  if (sv{u}) {{ const bool kv = {okk};",
-                      f"{ind}    skeys[sq{u}] = kv ? {rimg(f'x{rk}_s{u}')} : ({KT})0;",
-                      f"{ind}    spass[sq{u}] = (kv && {cond}) ? 1 : 0;"])
-            for x in rtail:
-                b.append(f"{ind}    stv{x}[sq{u}] = x{x}_s{u};")
-                if cols[x][1]:
-                    b.append(f"{ind}    stn{x}[sq{u}] = n{x}_s{u} ? 1 : 0;")
-            b.append(f"{ind}  }}")
+        stage_stores(ind + "  ")
         b.extend([f"{ind}}}",
                   f"{ind}if (staged && threadIdx.x == 0) skeys[ns] = {KMAX};   // walk sentinel"])
         # (2) left stream (raw vector arrays come from the tile loop).  Per-item flags live as
@@ -1696,15 +1746,36 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
         b.append(f"{ind}}}")
         if NB == 1:   # single span buffer: the next tile's staging must wait for this tile
             b.append(f"{ind}{_block_sync(BLOCK)}")
+        if rpf:
+            b.append(f"{ind}ssC = ssN; seC = seN; ssN = ssNN; seN = seNN;")
 
     loads = _vec_loads(g1, first)
+    if rpf:
+        # the span registers and the first prefetch (tile t0), before the tile loop
+        pre: List[str] = ["  i64 ssC = 0, seC = 0, ssN = 0, seN = 0;"]
+        for u in range(U):
+            for sl in pf_slots:
+                pre.append(f"  {g1.raw_type(sl)} pk{sl}_{u} = 0;")
+                if cols[sl][1]:
+                    pre.append(f"  unsigned char pn{sl}_{u} = 0;")
+        pre.append("  if (t0 < t1) { ssC = a.spans[4 * t0 + 2]; seC = a.spans[4 * t0 + 3]; }")
+        pre.append("  if (t0 + 1 < t1) { ssN = a.spans[4 * (t0 + 1) + 2]; "
+                   "seN = a.spans[4 * (t0 + 1) + 3]; }")
+        pf_issue(pre, "  ", "ssC", "seC")
+        b += _TILE_HEAD + pre
     if MJ_PREFETCH:
         # software-pipelined: tile t+1's left vectors are in flight during tile t's staging,
         # search and aggregate tail (the kernel waits on memory ~60% of its wave cycles:
         # profiles/pmc_merge_join_r3.txt)
         _vec_tiles(b, T, NI, ind, loads, [], body)
     else:
-        _tile_loop(b, T, NI, 1, ind)
+        if rpf:
+            b += ["  for (i64 t = t0; t < t1; ++t) {",
+                  "    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;",
+                  f"    const i64 off = (t - a.tile_prefix[r]) * {T};"]
+            _vec_rows(b, NI, ind)
+        else:
+            _tile_loop(b, T, NI, 1, ind)
         b.append(f"{ind}if (tb0 + {T} <= a.nrows) {{")
         _vec_issue(b, loads, NI, ind, True)
         body(b, True)
@@ -1950,6 +2021,21 @@ def join_index_agg_shape(p: NL.JoinParams, compacts=None, vec: int = 0, jw: int 
                  for i in range(p.naggs))
     return ("join_index_agg", cols, preds, p.nlp, aggs, p.group_col, JI_ITEMS, vec, BLOCK, jw,
             jlog, JI_COMPACT, WAVE_SYNC, bool(stage and vec), bool(bitmap), VEC_PREFETCH)
+
+
+def _uload_raw(gen: _Gen, slot: int, it, raw: str, vraw: str, out: List[str], ind: str) -> None:
+    """``_uload``'s registers for column ``slot`` / item ``it`` from an already loaded stored
+    element ``raw`` (and validity byte ``vraw``)."""
+    ct = _CTYPE[gen.cols[slot][0]]
+    enc = gen.cols[slot][2]
+    if enc:
+        out.append(f"{ind}const int r{slot}_{it} = (int){raw};")
+        if enc[1]:
+            base = gen.a.add("q", f"B{slot}", "long long")
+            out.append(f"{ind}const i64 q{slot}_{it} = {base} + (i64){raw};")
+    out.append(f"{ind}const {ct} x{slot}_{it} = {gen.decode(slot, raw)};")
+    if gen.cols[slot][1]:
+        out.append(f"{ind}const bool n{slot}_{it} = {vraw} != 0;")
 
 
 def _uload(gen: _Gen, slot: int, it: int, out: List[str], ind: str) -> None:

@@ -409,7 +409,7 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
             if use_device_pages:
                 done = native_parquet.upload_file_device(parquet_local[i], flds, cols, lo,
                                                          stream, device, status, dev_strings,
-                                                         defer)
+                                                         defer, lock)
                 DEVICE_DECODED.update(done)
             rest_native = [f for f in flds if f.name not in done and f.name not in strings]
             if rest_native:

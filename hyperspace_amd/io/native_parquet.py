@@ -2,7 +2,8 @@
 (``csrc/runtime/hs_parquet.cpp``: footer/page-header Thrift parsing, Snappy, run tables) and
 HIP kernels (``csrc/kernels/parquet_decode.hip``).
 
-Device path (``upload_file_device``, default for chunks whose statistics say null-free): the
+Device path (``upload_file_device``, default for source files; definition levels of chunks
+with nulls decode on the device as well): the
 host only preads the raw column chunks into one pinned block and walks the page headers; the
 compressed bytes cross PCIe and two launches per batch of files decode them -
 ``hs_pq_inflate_kernel`` (Snappy, one wavefront per page, data-parallel tag parsing over
@@ -11,7 +12,8 @@ gather or PLAIN copy, one workgroup per page).  Launches cover ~4 GB of files at
 (``decode_batch``): a page is one wavefront's serial work, so only many files' pages fill the
 chip.  Large dictionary pages (and string dictionaries) are inflated on the host.
 
-Host-page-layer path (``upload_file``, chunks that may hold nulls):
+Host-page-layer path (``upload_file``: index bucket files, whose row-group-sized pages are
+too long for one wavefront's inflate, and ``HS_PQ_DEVICE_NULLS=0`` for chunks with nulls):
 per file every natively decodable column chunk is decompressed straight into one pinned
 buffer, its RLE/bit-packed streams are cut into run tables, buffer and run tables cross PCIe
 in two copies on the HIP copy stream, and the expansion kernels write the values into the
@@ -39,7 +41,7 @@ RUN_DTYPE = np.dtype([("dst", "<i8"), ("count", "<i8"), ("src", "<i8"), ("kind",
 PAGE_DTYPE = np.dtype([("src", "<i8"), ("dst", "<i8"), ("out", "<i8"), ("dict", "<i8"),
                        ("row", "<i8"), ("csize", "<i4"), ("usize", "<i4"), ("nvals", "<i4"),
                        ("codec", "<i4"), ("kind", "<i4"), ("enc", "<i4"), ("levels", "<i4"),
-                       ("eb", "<i4"), ("dict_page", "<i4"), ("pad", "<i4")])
+                       ("eb", "<i4"), ("dict_page", "<i4"), ("nulls", "<i4"), ("valid", "<i8")])
 
 
 class ChunkInfo(C.Structure):
@@ -102,7 +104,8 @@ def lib():
                         ("hs_pq_page_size", I, []),
                         ("hs_pq_snappy_decompress", I64, [P, I64, P, I64]),
                         ("hs_pq_plain_strings", I64, [P, I64, I64, P, P, I64]),
-                        ("hs_pq_set_host_inflate", None, [I])):
+                        ("hs_pq_set_host_inflate", None, [I]),
+                        ("hs_pq_set_device_nulls", None, [I])):
                     fn = getattr(L, name)
                     fn.restype = res
                     fn.argtypes = args
@@ -112,6 +115,9 @@ def lib():
                 # tag-dense pages faster than 16 host threads (SF100 lineitem read + H2D
                 # 0.34 s vs 0.42 s: profiles/build_sweep_inflate_r3_win128.jsonl)
                 L.hs_pq_set_host_inflate(int(os.environ.get("HS_PQ_HOST_INFLATE", "1")))
+                # HS_PQ_DEVICE_NULLS=0: chunks with nulls go through the host page layer
+                # (strings: pyarrow) instead of decoding their definition levels on the device
+                L.hs_pq_set_device_nulls(int(os.environ.get("HS_PQ_DEVICE_NULLS", "1")))
                 if L.hs_pq_run_size() != RUN_DTYPE.itemsize or \
                         L.hs_pq_info_size() != C.sizeof(ChunkInfo) or \
                         L.hs_pq_page_size() != PAGE_DTYPE.itemsize:
@@ -394,6 +400,9 @@ def plan_file(f: "PqFile", plan, raw_cap: int, raw_buf_ptr: int, host_cap: int =
     return pages[:npg], chunks, raw_at, dst_at, h_at, skipped
 
 
+_VALID_LOCK = threading.Lock()
+
+
 class StringCodes:
     """One string column decoded on the device across the files of an upload.
 
@@ -402,7 +411,7 @@ class StringCodes:
     thread); the data pages decode on the device to those codes.  ``concat`` is the dictionary
     of that code space; the caller maps it onto the job-global sorted dictionary with one device
     gather (``staging.finish_strings``).  ``host`` holds the arrow chunks of files whose pages the
-    device path could not take (PLAIN pages, nulls), by file index."""
+    device path could not take (PLAIN-encoded pages), by file index."""
 
     def __init__(self):
         self._lock = threading.Lock()
@@ -481,21 +490,26 @@ def decode_batch(pend: List["PendingDecode"], device, status, stream):
 
 def upload_file_device(path: str, fields: Sequence[pa.Field], cols: Dict[str, object], lo: int,
                        stream, device, status, strings: Optional[Dict[str, StringCodes]] = None,
-                       defer: Optional[list] = None) -> Set[str]:
-    """Decode the natively supported, null-free ``fields`` of ``path`` entirely on the GPU into
+                       defer: Optional[list] = None, lock=None) -> Set[str]:
+    """Decode the natively supported ``fields`` of ``path`` entirely on the GPU into
     ``cols[name].data[lo:...]``: the host preads the raw column chunks into pinned memory and
     lists their pages; one H2D copy moves the compressed bytes and the page table, and two
     launches (``hs_pq_decode_pages``: Snappy inflate, then RLE / bit-packed / PLAIN expansion
     with the dictionary gather) write the values.  Errors accumulate in the device int
     ``status`` (checked once per build).  Returns the names decoded.
 
-    String columns named in ``strings`` decode when every chunk is dictionary-encoded and
-    null-free: the host parses only the (small) dictionary pages, the device expands the index
-    pages through a per-chunk code table (``StringCodes``) into ``cols[name].data`` (int32)."""
+    String columns named in ``strings`` decode when every chunk is dictionary-encoded: the host
+    parses only the (small) dictionary pages, the device expands the index pages through a
+    per-chunk code table (``StringCodes``) into ``cols[name].data`` (int32).
+
+    Chunks that may hold nulls decode their definition levels on the device too
+    (``hs_pq_expand_kernel``: levels -> validity bytes, dense values spread to their rows, 0 at
+    nulls); the column's validity mask is created on first need (``staging.ensure_valid`` under
+    ``lock``)."""
     import time
     import torch
     from ..ops import _lib as NL
-    from ..exec.staging import pinned_pool
+    from ..exec.staging import ensure_valid, pinned_pool
     t = time.perf_counter()
     f = PqFile(path)
     try:
@@ -555,6 +569,9 @@ def upload_file_device(path: str, fields: Sequence[pa.Field], cols: Dict[str, ob
                 eb = dc.data.element_size()
                 row0 = lo + int(rg_off[g])
                 seg["out"] = dc.data.data_ptr() + (row0 + seg["row"]) * eb
+                if seg["nulls"].any():
+                    v = ensure_valid(dc, dc.data.shape[0], device, lock or _VALID_LOCK)
+                    seg["valid"] = np.where(seg["nulls"] != 0, v.data_ptr() + row0 + seg["row"], 0)
             # device address of every decompressed page (scratch, or the host-inflated copy)
             hbase = draw.data_ptr() + raw_cap
             pages["dst"] = np.where(pages["codec"] == 2, hbase + pages["src"],
@@ -657,10 +674,13 @@ def _hybrid_host(s: np.ndarray, bw: int, nv: int) -> np.ndarray:
 
 
 def decode_plan_host(raw: np.ndarray, pages: np.ndarray, outputs: Dict[int, np.ndarray],
-                     host_dicts: Optional[np.ndarray] = None) -> None:
+                     host_dicts: Optional[np.ndarray] = None,
+                     valid_outputs: Optional[Dict[int, np.ndarray]] = None) -> None:
     """Reference (host) consumer of a device page plan — the oracle for hs_pq_decode_pages.
     ``outputs`` maps a page's ``out`` value to a numpy array slice receiving its values (the
-    plan is built with ``out`` = synthetic keys here instead of device addresses)."""
+    plan is built with ``out`` = synthetic keys here instead of device addresses);
+    ``valid_outputs`` likewise maps ``valid`` to the validity slice of pages with nulls, whose
+    values are spread to their rows with 0 at nulls (as ``hs_pq_expand_kernel`` does)."""
     L = lib()
     scratch = {}
     for i, p in enumerate(pages):
@@ -683,7 +703,6 @@ def decode_plan_host(raw: np.ndarray, pages: np.ndarray, outputs: Dict[int, np.n
         if p["kind"] == 2:
             continue
         pg = scratch[i]
-        dt = np.dtype({1: np.uint8, 4: np.uint32}.get(int(p["eb"]), np.uint64))
         voff = 0
         if p["kind"] == 0 and p["levels"]:
             voff = 4 + int(pg[:4].view(np.uint32)[0])
@@ -691,41 +710,60 @@ def decode_plan_host(raw: np.ndarray, pages: np.ndarray, outputs: Dict[int, np.n
             voff = int(p["levels"])
         nv = int(p["nvals"])
         dst = outputs[int(p["out"])]
-        if p["eb"] == 1:                 # BOOLEAN: PLAIN bits or length-prefixed RLE, width 1
-            if p["enc"] == 0:
-                dst[:nv] = np.unpackbits(pg[voff:voff + (nv + 7) // 8], bitorder="little")[:nv]
-            else:
-                dst[:nv] = _hybrid_host(pg[voff + 4:voff + 4 + int(pg[voff:voff + 4].view(
-                    np.uint32)[0])], 1, nv)
+        if p["nulls"]:
+            lstream = pg[4:voff] if p["kind"] == 0 else pg[:voff]
+            valid = _hybrid_host(lstream, 1, nv).astype(np.uint8)
+            valid_outputs[int(p["valid"])][:nv] = valid
+            dense = np.zeros(nv, dtype=dst.dtype)
+            nn = int(valid.sum())
+            _decode_values_host(p, pg, voff, nn, dense, scratch, pages)
+            dst[:nv] = 0
+            dst[:nv][valid.astype(bool)] = dense[:nn]
             continue
+        _decode_values_host(p, pg, voff, nv, dst, scratch, pages)
+
+
+def _decode_values_host(p, pg: np.ndarray, voff: int, nv: int, dst: np.ndarray, scratch,
+                        pages) -> None:
+    """The ``nv`` values of data page ``p`` (bytes ``pg``, values at ``voff``) into ``dst``."""
+    dt = np.dtype({1: np.uint8, 4: np.uint32}.get(int(p["eb"]), np.uint64))
+    if nv == 0:
+        return
+    if p["eb"] == 1:                 # BOOLEAN: PLAIN bits or length-prefixed RLE, width 1
         if p["enc"] == 0:
-            dst[:nv] = pg[voff:voff + nv * dt.itemsize].view(dt)
-            continue
-        d = scratch[int(p["dict_page"])]
-        dvals = d[:int(pages[int(p["dict_page"])]["nvals"]) * dt.itemsize].view(dt)
-        bw = int(pg[voff])
-        s = pg[voff + 1:]
-        q, done = 0, 0
-        while done < nv:
-            h, shift = 0, 0
-            while True:
-                b = int(s[q]); q += 1
-                h |= (b & 0x7F) << shift
-                if not b & 0x80:
-                    break
-                shift += 7
-            if h & 1:
-                groups = h >> 1
-                take = min(groups * 8, nv - done)
-                idx = _unpack(s, q, take, bw) if bw else np.zeros(take, np.int64)
-                dst[done:done + take] = dvals[idx]
-                q += groups * bw
-                done += take
-            else:
-                cnt = h >> 1
-                vb = (bw + 7) // 8
-                v = int.from_bytes(bytes(s[q:q + vb]), "little")
-                q += vb
-                take = min(cnt, nv - done)
-                dst[done:done + take] = dvals[v]
-                done += take
+            dst[:nv] = np.unpackbits(pg[voff:voff + (nv + 7) // 8], bitorder="little")[:nv]
+        else:
+            dst[:nv] = _hybrid_host(pg[voff + 4:voff + 4 + int(pg[voff:voff + 4].view(
+                np.uint32)[0])], 1, nv)
+        return
+    if p["enc"] == 0:
+        dst[:nv] = pg[voff:voff + nv * dt.itemsize].view(dt)
+        return
+    d = scratch[int(p["dict_page"])]
+    dvals = d[:int(pages[int(p["dict_page"])]["nvals"]) * dt.itemsize].view(dt)
+    bw = int(pg[voff])
+    s = pg[voff + 1:]
+    q, done = 0, 0
+    while done < nv:
+        h, shift = 0, 0
+        while True:
+            b = int(s[q]); q += 1
+            h |= (b & 0x7F) << shift
+            if not b & 0x80:
+                break
+            shift += 7
+        if h & 1:
+            groups = h >> 1
+            take = min(groups * 8, nv - done)
+            idx = _unpack(s, q, take, bw) if bw else np.zeros(take, np.int64)
+            dst[done:done + take] = dvals[idx]
+            q += groups * bw
+            done += take
+        else:
+            cnt = h >> 1
+            vb = (bw + 7) // 8
+            v = int.from_bytes(bytes(s[q:q + vb]), "little")
+            q += vb
+            take = min(cnt, nv - done)
+            dst[done:done + take] = dvals[v]
+            done += take

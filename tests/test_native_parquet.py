@@ -171,19 +171,24 @@ def _plan_and_decode_host(path, names):
                                                  for g in range(f.num_row_groups)])])
         out = {fld.name: np.zeros(f.num_rows, dtype={1: np.uint8, 4: np.uint32}.get(eb, np.uint64))
                for fld, _, eb in plan}
-        targets = {}
+        valid = {fld.name: np.ones(f.num_rows, dtype=np.uint8) for fld, _, _ in plan}
+        targets, vtargets = {}, {}
         for fld, g, p0, n in chunks:
             for i in range(p0, p0 + n):
                 p = pages[i]
                 pages[i]["out"] = i + 1
                 r0 = int(rg_off[g] + p["row"])
                 targets[i + 1] = out[fld.name][r0:r0 + int(p["nvals"])]
-        NP.decode_plan_host(raw, pages, targets, hd)
+                if p["nulls"]:
+                    pages[i]["valid"] = i + 1
+                    vtargets[i + 1] = valid[fld.name][r0:r0 + int(p["nvals"])]
+        NP.decode_plan_host(raw, pages, targets, hd, vtargets)
         # every data page starts at its row; pages tile the chunk
         for fld, g, p0, n in chunks:
             data = pages[p0:p0 + n][pages[p0:p0 + n]["kind"] != 2]
             assert int(data["nvals"].sum()) == f.row_group_rows(g)
             assert (data["dst"] % 16 == 0).all()
+        _plan_and_decode_host.valid = {k: v for k, v in valid.items() if k not in skipped}
         return {k: v for k, v in out.items() if k not in skipped}, skipped
 
 
@@ -192,7 +197,8 @@ def _plan_and_decode_host(path, names):
 @pytest.mark.parametrize("page_version", ["1.0", "2.0"])
 def test_device_page_plan_matches_pyarrow(tmp_path, compression, dictionary, page_version):
     """The device-decode page plan (host pread + page headers only) decodes to pyarrow's values;
-    chunks that may hold nulls are refused (they take the host page layer)."""
+    chunks with nulls decode their definition levels too (validity bytes, values spread to
+    their rows with 0 at nulls)."""
     rng = np.random.default_rng(8)
     t = _table(23_000, rng, False)
     t = t.append_column("n64", pa.array(np.where(rng.random(t.num_rows) < 0.05, None,
@@ -202,13 +208,60 @@ def test_device_page_plan_matches_pyarrow(tmp_path, compression, dictionary, pag
                    data_page_version=page_version, row_group_size=9_000, data_page_size=4096)
     names = list(np_types) + ["sorted", "n64"]
     vals, skipped = _plan_and_decode_host(path, names)
-    assert skipped == {"n64"}
+    assert not skipped
     for name in names[:-1]:
         ref = t.column(name).combine_chunks()
         if ref.type == pa.date32():
             ref = ref.view(pa.int32())
         nd = ref.to_numpy()
         np.testing.assert_array_equal(vals[name].view(nd.dtype), nd)
+    ref = t.column("n64").combine_chunks()
+    np.testing.assert_array_equal(_plan_and_decode_host.valid["n64"],
+                                  ref.is_valid().to_numpy(zero_copy_only=False).astype(np.uint8))
+    np.testing.assert_array_equal(vals["n64"].view(np.int64),
+                                  ref.fill_null(0).to_numpy().astype(np.int64))
+
+
+def test_device_page_plan_refuses_nulls_when_disabled(tmp_path):
+    """HS_PQ_DEVICE_NULLS=0 (hs_pq_set_device_nulls(0)): chunks with nulls are refused by the
+    device plan and take the host page layer."""
+    rng = np.random.default_rng(12)
+    n = 9_000
+    t = pa.table({"k": pa.array(rng.integers(0, 9, n)),
+                  "n": pa.array(np.where(rng.random(n) < 0.1, None, rng.integers(0, 9, n)))})
+    path = tmp_path / "n.parquet"
+    pq.write_table(t, path)
+    L = NP.lib()
+    L.hs_pq_set_device_nulls(0)
+    try:
+        _, skipped = _plan_and_decode_host(path, ["k", "n"])
+    finally:
+        L.hs_pq_set_device_nulls(1)
+    assert skipped == {"n"}
+
+
+@pytest.mark.parametrize("page_version", ["1.0", "2.0"])
+def test_device_page_plan_nullable_strings_and_bools(tmp_path, page_version):
+    """Nullable dictionary-encoded strings (codes through the chunk's code table) and nullable
+    booleans plan for the device; all-null pages and runs of nulls included."""
+    rng = np.random.default_rng(14)
+    n = 30_000
+    words = np.array(["alpha", "beta", "gamma", "delta", "eps"])
+    nulls = rng.random(n) < 0.2
+    nulls[5_000:9_000] = True                       # whole pages of nulls
+    s = pa.array(np.where(nulls, None, words[rng.integers(0, 5, n)]).tolist(), pa.string())
+    b = pa.array(np.where(rng.random(n) < 0.3, None, rng.random(n) < 0.5).tolist(), pa.bool_())
+    t = pa.table({"s": s, "b": b})
+    path = tmp_path / "s.parquet"
+    pq.write_table(t, path, data_page_version=page_version, row_group_size=12_000,
+                   data_page_size=1024, use_dictionary=["s"])
+    vals, skipped = _plan_and_decode_host(path, ["b"])
+    assert not skipped
+    vb = _plan_and_decode_host.valid["b"]
+    np.testing.assert_array_equal(vb, b.is_valid().to_numpy(zero_copy_only=False).astype(np.uint8))
+    np.testing.assert_array_equal(vals["b"][vb == 1],
+                                  b.drop_null().to_numpy(zero_copy_only=False).astype(np.uint8))
+    assert (vals["b"][vb == 0] == 0).all()
 
 
 @pytest.mark.parametrize("compression", ["none", "snappy"])
@@ -302,8 +355,9 @@ def test_native_parquet_gpu_decode_matches_pyarrow(tmp_path, device):
 def test_device_string_decode_matches_pyarrow(tmp_path, device):
     """Dictionary-encoded BYTE_ARRAY chunks decode on the device to codes over one global
     sorted dictionary: v1 and v2 pages, Snappy and uncompressed, many row groups with different
-    dictionaries, a large dictionary, empty strings and multi-byte UTF-8; a file with nulls and
-    one without a dictionary fall back to pyarrow for that file only."""
+    dictionaries, a large dictionary, empty strings and multi-byte UTF-8, and a file with nulls
+    (definition levels decoded on the device); the file without a dictionary (PLAIN pages) falls
+    back to pyarrow for that file only."""
     import torch
     from hyperspace_amd.exec import staging
     rng = np.random.default_rng(21)
@@ -332,7 +386,7 @@ def test_device_string_decode_matches_pyarrow(tmp_path, device):
                               device, parquet_local=files)
     torch.cuda.synchronize()
     assert "s" in staging.DEVICE_DECODED
-    assert [c is not None for c in up.host_strings["s"]] == [False, False, False, True, True]
+    assert [c is not None for c in up.host_strings["s"]] == [False, False, False, True, False]
     cols = dict(up.columns)
     staging.finish_strings(up, cols, device, None)
     c = cols["s"]
