@@ -10,3 +10,7 @@ if [ -n "$CONFIGS" ]; then
   timeout -k 10 600 python3 scripts/qk_sweep.py --sf ${SF:-100} --reps ${REPS:-12} ${SWEEP_MODE:---only-merge} \
     --configs "${CONFIGS}" > gpurun_out/iter_sweep${TAG}.jsonl 2> gpurun_out/iter_sweep${TAG}.log || exit $?
 fi
+if [ -n "$CONFIGS2" ]; then
+  timeout -k 10 600 python3 scripts/qk_sweep.py --sf ${SF:-100} --reps ${REPS:-12} ${SWEEP_MODE2} \
+    --configs "${CONFIGS2}" > gpurun_out/iter_sweep2${TAG}.jsonl 2> gpurun_out/iter_sweep2${TAG}.log || exit $?
+fi
