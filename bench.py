@@ -275,7 +275,9 @@ def main():
             .orderBy(col("revenue").desc(), col("o_orderdate")).limit(10)
 
     def submit(i):
-        """One step = one Q6 + one Q3, each planned and submitted through the full engine."""
+        """One step = one Q6 + one Q3, each planned and submitted through the full engine (a
+        warm Q6 scan pipeline replays on the engine's side stream, beside the Q3 merge join:
+        spark.hyperspace.mi.sideStreamScans.enabled)."""
         return q6(i).collect_async(), q3(i).collect_async()
 
     def finish(fs):

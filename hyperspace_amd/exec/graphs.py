@@ -110,6 +110,7 @@ class ScanAggGraph:
         self._next = 0
         self._warm = False
         self.replays = 0
+        self.on_side = False   # replays moved to the backend's side stream (exec/gpu.py)
 
     @property
     def graph(self):
@@ -140,6 +141,11 @@ class ScanAggGraph:
                                 NL.ptr(o[3]), stream), "hs_agg_final")
         NL.check(L.hs_memcpy_async(slot.h_out.ptr, o[0].hs_buf.data_ptr(), slot.h_out.nbytes, 2,
                                    stream), "result D2H")
+
+    def buffers(self) -> list:
+        """Device intermediates a replay reads and writes."""
+        return [self.d_params, self.rstart, self.rlen, self.rbk, self.tp, self.bucket_off,
+                *self.parts, self.out[0].hs_buf]
 
     def values_template(self) -> dict:
         return {"rstart": self.rstart.data_ptr(), "rlen": self.rlen.data_ptr(),

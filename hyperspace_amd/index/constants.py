@@ -102,6 +102,10 @@ HBM_COMPRESSION_ENABLED_DEFAULT = "true"
 # replay captured hipGraphs of the scan pipeline (exec/graphs.py)
 HIPGRAPH_ENABLED = "spark.hyperspace.mi.hipGraph.enabled"
 HIPGRAPH_ENABLED_DEFAULT = "true"
+# warm captured scan pipelines replay on a side stream, overlapping the work queued on the
+# query's stream (exec/gpu.py GpuBackend._scan_agg_graph)
+SIDE_STREAM_SCANS = "spark.hyperspace.mi.sideStreamScans.enabled"
+SIDE_STREAM_SCANS_DEFAULT = "true"
 # cached join index (left row -> first matching right row, int32 in HBM) for joins of two
 # device-resident index tables with unique integer right keys: the fused join aggregate becomes a
 # streaming scan of the left table plus a gather, no per-tile span search (exec/join_index.py)

@@ -123,6 +123,10 @@ class HyperspaceConf:
         return _b(conf.get(C.HIPGRAPH_ENABLED, C.HIPGRAPH_ENABLED_DEFAULT))
 
     @staticmethod
+    def side_stream_scans(conf) -> bool:
+        return _b(conf.get(C.SIDE_STREAM_SCANS, C.SIDE_STREAM_SCANS_DEFAULT))
+
+    @staticmethod
     def index_placement(conf) -> str:
         v = str(conf.get(C.INDEX_PLACEMENT, C.INDEX_PLACEMENT_DEFAULT)).lower()
         if v not in ("sharded", "replicated"):

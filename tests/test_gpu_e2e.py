@@ -140,6 +140,51 @@ def test_q6_graph_replays_with_new_literals(tpch):
     _close(g2, g)
 
 
+def test_side_stream_scans_pipelined_with_joins(tpch):
+    """Warm scan pipelines replay on the engine's side stream while merge joins queue on the
+    query stream (several queries in flight, fresh literals each): every result equals the
+    same query run with side-stream scans off, one at a time."""
+    s, lpath, opath = tpch
+    hs = Hyperspace(s)
+    li = s.read.parquet(lpath)
+    od = s.read.parquet(opath)
+    hs.createIndex(li, IndexConfig("li_ship2", ["l_shipdate"],
+                                   ["l_discount", "l_quantity", "l_extendedprice"]))
+    hs.createIndex(li, IndexConfig("li_ok2", ["l_orderkey"],
+                                   ["l_extendedprice", "l_discount", "l_shipdate"]))
+    hs.createIndex(od, IndexConfig("od_ok2", ["o_orderkey"], ["o_orderdate", "o_shippriority"]))
+    Hyperspace.enable(s)
+    s.conf.set("spark.hyperspace.mi.joinIndex.enabled", "false")
+
+    def q6(i):
+        y = 1993 + i % 5
+        return li.filter(f"l_shipdate >= DATE '{y}-01-01' AND l_shipdate < DATE '{y + 1}-01-01'"
+                         f" AND l_discount >= 0.0{i % 5 + 1} AND l_quantity < {20 + i % 7}") \
+            .agg(sum_(col("l_extendedprice") * col("l_discount")).alias("revenue"))
+
+    def q3(i):
+        dd = f"1995-03-{10 + i % 15:02d}"
+        return li.join(od, li["l_orderkey"] == od["o_orderkey"]) \
+            .filter(f"o_orderdate < DATE '{dd}' AND l_shipdate > DATE '{dd}'") \
+            .groupBy("o_shippriority").agg(sum_("l_extendedprice").alias("rev"),
+                                           count("*").alias("n"))
+    backend = s.backend()
+    futs = []
+    for i in range(10):
+        futs.append((q6(i).collect_async(), q3(i).collect_async()))
+    got = [(a.result(), b.result()) for a, b in futs]
+    assert all(g.path == "native" for pair in futs for g in pair), backend.fallback_reason
+    assert any(g.on_side for g in backend.graphs._lru.values())
+    s.conf.set("spark.hyperspace.mi.sideStreamScans.enabled", "false")
+
+    def table(rows):
+        return pa.Table.from_pylist(sorted((r.asDict() for r in rows),
+                                           key=lambda d: tuple(d.values())))
+    for i, (g6, g3) in enumerate(got):
+        _close(table(g6), table(q6(i).collect()))
+        _close(table(g3), table(q3(i).collect()))
+
+
 def test_filter_rows_and_group_by_native(tpch):
     s, lpath, _ = tpch
     hs = Hyperspace(s)
