@@ -1230,6 +1230,10 @@ class GpuBackend:
         if isinstance(sums, _GraphPending) and d is not None and d.world > 1:
             # sharded: combine this rank's partials straight from the graph's device output
             # (stream-ordered after the replay; the next replay is ordered after the collective)
+            if sums.graph.on_side:
+                import torch
+                # the replay ran on the side stream: the collective on this stream waits for it
+                torch.cuda.current_stream().wait_stream(self._side)
             sums, cnts, mins, maxs = sums.graph.out
         if isinstance(sums, _GraphPending):
             fetch = sums.result
