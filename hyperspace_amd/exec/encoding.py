@@ -25,7 +25,7 @@ _MAX_SCALE_DIGITS = 4
 
 
 class Compact:
-    __slots__ = ("codes", "width", "base", "scale", "logical_type", "lo", "hi")
+    __slots__ = ("codes", "width", "base", "scale", "logical_type", "lo", "hi", "g16")
 
     def __init__(self, codes, width: int, base: int, scale: Optional[float], logical_type: int,
                  lo: Optional[int] = None, hi: Optional[int] = None):
@@ -35,13 +35,86 @@ class Compact:
         self.scale = scale          # None for integers, 10**k for decimals
         self.logical_type = logical_type
         self.lo, self.hi = lo, hi   # range of the (integer / scaled) values of valid rows
+        self.g16 = False            # grouped16(): derived 16-bit form (None: not applicable)
 
     def nbytes(self) -> int:
-        return self.codes.numel() * self.width
+        n = self.codes.numel() * self.width
+        return n + (self.g16.nbytes() if self.g16 else 0)
 
     def signature(self) -> tuple:
         """Shape-relevant part (codegen key): literals like base/scale are kernel arguments."""
         return (self.width, self.scale is not None)
+
+
+GROUP_ROWS = 64
+
+
+WIDE_GROUP = -(1 << 31)
+
+
+class GroupedCompact(Compact):
+    """16-bit codes relative to a per-64-row group base: value = base + gbase[row >> 6] +
+    (uint16) code.  Derived from a sorted integer column's 32-bit compact form (an index's
+    bucket-sorted key: neighbouring rows hold close keys), it halves the bytes a merge join
+    streams for the left key (``exec/jit.py`` ``MJ_KEY16``).  A group spanning 2^16 codes or
+    more (one straddling two buckets) is *wide*: its base is ``WIDE_GROUP`` and readers take
+    its 32-bit codes from ``wide`` (the parent compact's codes)."""
+    __slots__ = ("gbase", "wide")
+
+    def __init__(self, codes, gbase, wide, base: int, logical_type: int, lo, hi):
+        super().__init__(codes, 2, base, None, logical_type, lo, hi)
+        self.gbase = gbase          # int32 [ceil(n / 64)]: the group's smallest 32-bit code
+        self.wide = wide            # int32 codes of every row (read for wide groups only)
+
+    def nbytes(self) -> int:
+        return self.codes.numel() * 2 + self.gbase.numel() * 4
+
+    def signature(self) -> tuple:
+        return (2, False, GROUP_ROWS)
+
+
+def grouped16(c: Compact, max_wide: float = 0.01) -> Optional[GroupedCompact]:
+    """The 16-bit grouped form of the 32-bit integer compact ``c`` (computed once, kept on
+    ``c``), or None when more than ``max_wide`` of its 64-row groups are wide."""
+    if c.g16 is not False:
+        return c.g16
+    c.g16 = None
+    if c.scale is not None or c.lo is None or c.width != 4 or c.codes.numel() == 0:
+        return None
+    import torch
+    x = c.codes
+    n = x.numel()
+    pad = (-n) % GROUP_ROWS
+    xp = torch.cat([x, x[-1:].expand(pad)]) if pad else x
+    g = xp.view(-1, GROUP_ROWS)
+    gmin = g.amin(dim=1)
+    wide = ((g.amax(dim=1).long() - gmin.long()) >= (1 << 16)) | (gmin == WIDE_GROUP)
+    if float(wide.float().mean().item()) > max_wide:
+        return None
+    gbase = torch.where(wide, torch.full_like(gmin, WIDE_GROUP), gmin)
+    d = (xp.long() - gmin.long().repeat_interleave(GROUP_ROWS))[:n]
+    d = torch.where(wide.repeat_interleave(GROUP_ROWS)[:n], torch.zeros_like(d), d)
+    codes = torch.where(d >= (1 << 15), d - (1 << 16), d).to(torch.int16)   # uint16 bits
+    c.g16 = GroupedCompact(codes.contiguous(), gbase.contiguous(), x, c.base, c.logical_type,
+                           c.lo, c.hi)
+    return c.g16
+    c.g16 = None
+    if c.scale is not None or c.lo is None or c.codes.numel() == 0:
+        return None
+    import torch
+    x = c.codes.to(torch.int32)
+    n = x.numel()
+    pad = (-n) % GROUP_ROWS
+    xp = torch.cat([x, x[-1:].expand(pad)]) if pad else x
+    g = xp.view(-1, GROUP_ROWS)
+    gmin = g.amin(dim=1)
+    if int((g.amax(dim=1) - gmin).max().item()) >= (1 << 16):
+        return None
+    d = (xp - gmin.repeat_interleave(GROUP_ROWS))[:n]
+    codes = torch.where(d >= (1 << 15), d - (1 << 16), d).to(torch.int16)   # uint16 bits
+    c.g16 = GroupedCompact(codes.contiguous(), gmin.contiguous(), c.base, c.logical_type,
+                           c.lo, c.hi)
+    return c.g16
 
 
 def _width_for(span: int):

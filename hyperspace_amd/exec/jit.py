@@ -104,6 +104,11 @@ MJ_SPARSE = os.environ.get("HS_JIT_MJ_SPARSE", "1") == "1"
 # hash-mode merge joins append matches lane-major (row order): _lanemajor_append
 MJ_HASH_LANEMAJOR = os.environ.get("HS_JIT_MJ_HASH_LANEMAJOR", "0") == "1"
 MJ_KEY32 = os.environ.get("HS_JIT_MJ_KEY32", "1") == "1"  # 32-bit merge images (_key32_frame)
+# left join key streamed as 16-bit codes over a per-64-row group base (encoding.grouped16) when
+# the key is only the join key: 2 bytes per left row instead of 4.  Off by default: exact, but
+# 1.51 vs 1.38 ms at SF100 (profiles/mj_sweep_r3_key16.jsonl) - the kernel is bound by its
+# per-tile dependent round trips, not by the bytes it streams
+MJ_KEY16 = os.environ.get("HS_JIT_MJ_KEY16", "0") == "1"
 # cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
 MJ_EXP = os.environ.get("HS_JIT_MJ_EXP", "")
 # software-pipelined full tiles in the vectorized kernels (_vec_tiles)
@@ -389,9 +394,7 @@ class _Gen:
         return self.rows[1] if slot >= self.split else self.rows[0]
 
     def ptr(self, slot: int) -> str:
-        t, _, enc = self.cols[slot]
-        ct = _CODE_T[enc[0]] if enc else _CTYPE[t]
-        return self.a.add("p", f"c{slot}", f"const {ct}*")
+        return self.a.add("p", f"c{slot}", f"const {self.raw_type(slot)}*")
 
     def vptr(self, slot: int) -> Optional[str]:
         hv = self.cols[slot][1]
@@ -402,8 +405,11 @@ class _Gen:
         return self.decode(slot, f"{self.ptr(slot)}[{row}]")
 
     def raw_type(self, slot: int) -> str:
-        """C type of the stored element (the code type for compact columns)."""
+        """C type of the stored element (the code type for compact columns; grouped 16-bit
+        codes, encoding.GroupedCompact, are unsigned)."""
         t, _, enc = self.cols[slot]
+        if enc and len(enc) > 2:
+            return "unsigned short"
         return _CODE_T[enc[0]] if enc else _CTYPE[t]
 
     def decode(self, slot: int, raw: str) -> str:
@@ -975,6 +981,10 @@ def _fill_common(v: Dict[str, object], cols, preds, aggs, compacts=None) -> None
                 v[f"B{s}"] = c.base
                 v[f"Q{s}"] = c.scale or 1.0
                 v[f"R{s}"] = 1.0 / (c.scale or 1.0)
+                gb = getattr(c, "gbase", None)
+                if gb is not None:
+                    v[f"G{s}"] = gb.data_ptr()
+                    v[f"W{s}"] = c.wide.data_ptr()
     for k, p in preds:
         v[f"L{k}"] = p.ilit
         v[f"F{k}"] = p.flit
@@ -1292,7 +1302,7 @@ def merge_join_shape(p: NL.JoinParams, compacts=None, hk=None) -> tuple:
     return ("merge_join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey,
             p.key_is_float, MJ_ITEMS, MJ_LDS_KEYS, MJ_STEPS, BLOCK, WAVE_SYNC,
             _key32_frame(p, compacts) is not None, MJ_EXP, MJ_STAGE_UNROLL, MJ_DBUF, MJ_PREFETCH,
-            MJ_BLOCK, MJ_EAGER, MJ_SPARSE, MJ_HASH_LANEMAJOR, MJ_RPF and not MJ_PREFETCH,
+            MJ_BLOCK, MJ_EAGER, MJ_SPARSE, MJ_HASH_LANEMAJOR, MJ_RPF and not MJ_PREFETCH, MJ_KEY16,
             hk.shape() if hk is not None else None)
 
 
@@ -1536,10 +1546,18 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
         return (f"({{ const i64 d_ = (i64)({val}) - a.KLO; "
                 f"d_ < 0 ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }})")
 
+    k16 = k32 and cols[lk][2] is not None and len(cols[lk][2]) > 2
+    if k16:
+        args.add("p", f"G{lk}", "const int*")
+        args.add("p", f"W{lk}", "const int*")
+
     def limg(it: int) -> str:
-        """Merge image of left item ``it``."""
+        """Merge image of left item ``it`` (grouped 16-bit keys: the thread's 8-aligned rows lie
+        in one 64-row group, whose base ``gb_`` is loaded once per tile)."""
         if not k32:
             return _key_expr(f"x{lk}_{it}", fl)
+        if k16:
+            return f"(kx_[{it}] + (unsigned)a.KOF)"
         return f"((unsigned)x{lk}v[{it}] + (unsigned)a.KOF)"
 
     U = max(1, MJ_STAGE_UNROLL)  # noqa: N806
@@ -1630,6 +1648,16 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
         # bits of one VGPR word each (kvb: key valid, mb: left predicates, mtb: matched): a bool
         # per item would hold a 64-bit SGPR lane mask, and 8 items x 4 flags exhaust the SGPRs
         _vec_load_slots(b, g1, first, NI, ind)
+        if k16:
+            # 32-bit codes of the thread's rows: group base + 16-bit code, or (a wide group,
+            # one straddling two buckets) the 32-bit codes themselves
+            b.append(f"{ind}const int gbi_ = a.G{lk}[(g0 < a.nrows ? g0 : a.nrows - 1) >> 6];")
+            b.append(f"{ind}unsigned kx_[{NI}];")
+            b.append(f"{ind}" + " ".join(f"kx_[{it}] = (unsigned)gbi_ + (unsigned)x{lk}v[{it}];"
+                                         for it in range(NI)))
+            b.append(f"{ind}if (gbi_ == (int)0x80000000) {{ " + " ".join(
+                f"kx_[{it}] = act{it} ? (unsigned)a.W{lk}[g0 + {it}] : 0u;" for it in range(NI)) +
+                " }")
         b.append(f"{ind}unsigned kvb = 0u, mb = 0u;")
         for it in range(NI):
             gi = _Gen(args, cols, split, (f"row{it}", f"row{it}"), approx, True)
@@ -1906,6 +1934,8 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
     dev = rstart.device
     max_tiles = nrows // T + 2 * rstart.numel() + 2
+    if hk is None:
+        compacts = _with_key16(p, compacts)
     tp, spans = _join_spans(p, rstart, rlen, rbucket, roff, max_tiles, T, cache_spans, align=NI)
     k = kernel_for(merge_join_shape(p, compacts, hk), lambda: gen_merge_join_agg(p, compacts, hk))
     grid = max(1, MJ_GRID * 256 // MJ_BLOCK)
@@ -1934,6 +1964,28 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
         v["KLO"], v["KSP"], v["KOF"] = frame
     k.launch(grid, v, NL.stream_ptr(), GA * 32 if p.group_col >= 0 else 0)
     return _final(parts, grid, GA, dev)
+
+
+def _with_key16(p: NL.JoinParams, compacts):
+    """``compacts`` with the left key's grouped 16-bit form (encoding.grouped16) when the merge
+    join reads that column only as its 32-bit-frame join key (no validity, no predicate,
+    aggregate or group use) and every 64-row group of it spans < 2^16 codes."""
+    from .encoding import grouped16
+    if not (MJ_KEY16 and MJ_ITEMS and 64 % MJ_ITEMS == 0) or _key32_frame(p, compacts) is None:
+        return compacts
+    lk = p.lkey
+    if p.cols[lk].valid:
+        return compacts
+    used = set(_pred_slots([(k, p.preds[k]) for k in range(p.npreds)])) | \
+        set(_agg_slots([p.aggs[i] for i in range(p.naggs)])) | {p.group_col}
+    if lk in used:
+        return compacts
+    g = grouped16(compacts[lk])
+    if g is None:
+        return compacts
+    out = dict(compacts)
+    out[lk] = g
+    return out
 
 
 def _sample_offsets(roff):

@@ -179,6 +179,13 @@ def test_generated_sources_compile_with_compact_columns(rt, tmp_path):
     assert "unsigned skeys" in k32.src and "a.KOF" in k32.src    # 32-bit merge images
     assert "u64 skeys" in ks[-1].src
     ks.append(k32)
+    from hyperspace_amd.exec.encoding import GroupedCompact
+    c16 = dict(c32)
+    c16[0] = GroupedCompact(None, None, None, 1 + (1 << 31), NL.I64, 1, 600_000_000)
+    k16 = jit.gen_merge_join_agg(_q3_params(), c16)
+    assert "const unsigned short* c0" in k16.src and "a.G0[" in k16.src   # 16-bit left keys
+    assert jit.merge_join_shape(_q3_params(), c16) != jit.merge_join_shape(_q3_params(), c32)
+    ks.append(k16)
     assert "st9_s" in ks[0].src          # phase 2 staged through LDS
     assert "a.rbm" in ks[1].src and "a.c9" not in ks[1].src   # phase 2 = bitmap tests
     for k in ks:
@@ -479,6 +486,79 @@ def test_merge_join_agg_numpy_oracle(device):
         jit.MJ_LDS_KEYS = lds_keys
 
 
+@pytest.mark.gpu
+def test_merge_join_key16_matches_oracle(device):
+    """Merge join streaming the left key as grouped 16-bit codes (MJ_KEY16): TPC-H-like sparse
+    unique right keys, 1-7 left rows per key, buckets sorted by key (groups straddling buckets
+    read the 32-bit codes), full and partial tiles; equals the 32-bit-key kernel and numpy."""
+    import torch
+    from hyperspace_amd.exec import jit
+    from hyperspace_amd.exec.encoding import GroupedCompact, encode
+    rng = np.random.default_rng(8)
+    B = 8
+    ok = np.arange(1, 150_001, dtype=np.int64) * 4 + (1 << 20)
+    rb = murmur3.bucket_ids([pa.array(ok)], B)
+    per = rng.integers(1, 8, len(ok))
+    lk = np.repeat(ok, per)
+    lb = np.repeat(rb, per)
+    ro = np.lexsort((ok, rb)); rk, rb = ok[ro], rb[ro]
+    lo_ = np.lexsort((lk, lb)); lk, lb = lk[lo_], lb[lo_]
+    loff = np.searchsorted(lb, np.arange(B + 1)).astype(np.int64)
+    roff = np.searchsorted(rb, np.arange(B + 1)).astype(np.int64)
+    ldate = rng.integers(0, 1000, len(lk)).astype(np.int32)
+    lprice = np.round(rng.random(len(lk)) * 1000, 2)
+    rdate = rng.integers(0, 1000, len(rk)).astype(np.int32)
+    p = NL.JoinParams()
+    cl = [_col(pa.array(lk), device), _col(pa.array(ldate), device), _col(pa.array(lprice), device)]
+    cr = [_col(pa.array(rk), device), _col(pa.array(rdate), device)]
+    for i, c in enumerate(cl):
+        p.cols[i] = c.desc()
+    for i, c in enumerate(cr):
+        p.cols[8 + i] = c.desc()
+    p.preds[0] = NL.Pred(NL.PK_INT_LIT, NL.OP_GT, 1, 0, 0, 0, 300, 0.0, None)
+    p.preds[1] = NL.Pred(NL.PK_INT_LIT, NL.OP_LT, 9, 0, 1, 0, 500, 0.0, None)
+    p.nlp, p.npreds = 1, 2
+    p.aggs[0] = _agg(NL.AK_SUM, [(2, 0.0, 1.0)])
+    p.aggs[1] = _agg(NL.AK_COUNT_STAR)
+    p.naggs, p.lkey, p.rkey, p.key_is_float = 2, 0, 8, 0
+    p.group_col, p.num_groups, p.group_base = -1, 1, 0
+    rpass = dict(zip(rk.tolist(), (rdate < 500).tolist()))
+    m = np.array([rpass[k] for k in lk.tolist()]) & (ldate > 300)
+    allc = dict(enumerate(cl))
+    allc.update({8 + i: c for i, c in enumerate(cr)})
+    comp = {s: e for s, e in ((s, encode(c)) for s, c in allc.items()) if e is not None}
+    assert comp[0].width == 4
+    key16 = jit.MJ_KEY16
+    jit.MJ_KEY16 = True
+    try:
+        assert isinstance(jit._with_key16(p, comp)[0], GroupedCompact)
+    finally:
+        jit.MJ_KEY16 = key16
+    assert int((comp[0].g16.gbase == -(1 << 31)).sum()) >= 1      # groups across buckets
+    for starts, lens, exp in ((loff[:-1], loff[1:] - loff[:-1], m),
+                              (loff[:-1] + 5, loff[1:] - loff[:-1] - 9, None)):
+        if exp is None:
+            exp = np.zeros(len(lk), bool)
+            for b in range(B):
+                exp[starts[b]:starts[b] + lens[b]] = m[starts[b]:starts[b] + lens[b]]
+        rstart = torch.from_numpy(starts.astype(np.int64)).to(device)
+        rlen = torch.from_numpy(lens.astype(np.int64)).to(device)
+        rbk = torch.arange(B, dtype=torch.int32, device=device)
+        roff_t = torch.from_numpy(roff).to(device)
+        res = {}
+        for k16 in (True, False):
+            jit.MJ_KEY16 = k16
+            try:
+                res[k16] = [t.cpu().numpy() for t in
+                            jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, comp, nrows=len(lk),
+                                               rdup=False)]
+            finally:
+                jit.MJ_KEY16 = key16
+        for r in res.values():
+            assert r[1][0] == int(exp.sum())
+            assert abs(r[0][0] - float(lprice[exp].sum())) <= 1e-9 * max(1.0, float(lprice[exp].sum()))
+
+
 def test_code_bounds_match_value_compares():
     """Predicates on compact columns compare stored codes with host-computed int32 bounds; they
     must agree with the compare on the decoded value for every code, op and literal."""
@@ -622,3 +702,28 @@ def test_project_kernel_compiles(rt, tmp_path):
     exprs[0] = E.Add(E.Multiply(a, E.Literal(7)), b)
     k2, _, _ = project.build(exprs, cols, 4, torch.device("cpu"))
     assert k2 is k
+
+
+def test_grouped16_round_trips_sorted_keys():
+    """encoding.grouped16: 16-bit codes over per-64-row group bases reproduce every 32-bit code
+    of a bucket-sorted key column (uint16 bits in int16 storage); groups straddling two buckets
+    are wide (read from the 32-bit codes); too many wide groups make the column ineligible."""
+    import torch
+    from hyperspace_amd.exec.encoding import Compact, grouped16
+    rng = np.random.default_rng(5)
+    runs = []
+    for _ in range(8):              # sorted runs (buckets), restarting low
+        runs.append(np.sort(rng.integers(0, 4_000_000, 20_000)))
+    codes = torch.from_numpy(np.concatenate(runs).astype(np.int32))
+    c = Compact(codes, 4, 100, None, NL.I64, 100, 4_000_100)
+    g = grouped16(c)
+    assert g is not None and g.codes.dtype == torch.int16
+    assert g.gbase.numel() == (codes.numel() + 63) // 64
+    gb = g.gbase.repeat_interleave(64)[:codes.numel()].long()
+    wide = gb == -(1 << 31)
+    assert 0 < int(wide.sum()) <= 8 * 64      # only groups across run boundaries
+    back = torch.where(wide, g.wide.long(), gb + (g.codes.long() & 0xFFFF))
+    assert torch.equal(back, codes.long())
+    assert grouped16(c) is g and c.nbytes() == codes.numel() * 4 + g.nbytes()
+    spread = torch.from_numpy(np.array([0, 1 << 17] * 64, dtype=np.int32))
+    assert grouped16(Compact(spread, 4, 0, None, NL.I64, 0, 1 << 17)) is None
