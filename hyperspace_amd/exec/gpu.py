@@ -1527,6 +1527,7 @@ class GpuBackend:
         if s is None:
             s = self._side = torch.cuda.Stream(device=self.device)
         g.on_side = True
+        g.side_stream = s
         return s
 
     def _compacts(self, descs: Dict[int, DeviceColumn]) -> Optional[dict]:

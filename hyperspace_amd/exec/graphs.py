@@ -111,6 +111,7 @@ class ScanAggGraph:
         self._warm = False
         self.replays = 0
         self.on_side = False   # replays moved to the backend's side stream (exec/gpu.py)
+        self.side_stream = None
 
     @property
     def graph(self):
@@ -230,7 +231,12 @@ class GraphCache:
         with self._lock:
             self._lru[key] = g
             while len(self._lru) > self.capacity:
-                self._lru.popitem(last=False)
+                _, old = self._lru.popitem(last=False)
+                side = getattr(old, "side_stream", None)
+                if side is not None:
+                    # its last replays may still run on the side stream: let them finish before
+                    # the executable graphs are destroyed
+                    side.synchronize()
         return g
 
     def __len__(self):
