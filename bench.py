@@ -277,7 +277,8 @@ def main():
     def submit(i):
         """One step = one Q6 + one Q3, each planned and submitted through the full engine (a
         warm Q6 scan pipeline replays on the engine's side stream, beside the Q3 merge join:
-        spark.hyperspace.mi.sideStreamScans.enabled)."""
+        spark.hyperspace.mi.sideStreamScans.enabled; two Q3 merge joins on two streams at once
+        measured slower, 1.75 vs 1.45 ms per step: profiles/bench_q3_streams_r3.log)."""
         return q6(i).collect_async(), q3(i).collect_async()
 
     def finish(fs):
