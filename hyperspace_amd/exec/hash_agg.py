@@ -26,6 +26,7 @@ runs every operator above them; ``E2EHyperspaceRulesTest.scala:1004-1019`` check
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -36,6 +37,8 @@ from ..ops import _lib as NL
 from .compile import Unsupported
 
 EMPTY = (1 << 64) - 1
+# table slots per group seen on the previous run of a query shape (HS_HAGG_SLOTS_PER_GROUP)
+SLOTS_PER_GROUP = float(os.environ.get("HS_HAGG_SLOTS_PER_GROUP", "2"))
 MIN_SLOTS = 1 << 12
 MAX_SLOTS = 1 << 29
 _INT_TYPES = (NL.I8, NL.I16, NL.I32, NL.I64, NL.U32, NL.BOOL)
@@ -341,9 +344,10 @@ class TablePool:
         return M
 
     def record(self, shape_key, M: int, groups: int) -> None:
-        # next time: at least 2x the groups seen (load <= 0.5), never below what worked
-        self.sizes[shape_key] = max(next_pow2(max(MIN_SLOTS, 2 * groups)),
-                                    min(M, next_pow2(max(MIN_SLOTS, 2 * groups)) * 2))
+        # next time: at least SLOTS_PER_GROUP x the groups seen (load <= 0.5 by default), never
+        # below what worked
+        want = next_pow2(max(MIN_SLOTS, int(SLOTS_PER_GROUP * groups)))
+        self.sizes[shape_key] = max(want, min(M, want * 2))
 
 
 def next_pow2(n: int) -> int:
