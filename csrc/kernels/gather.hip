@@ -46,6 +46,55 @@ __global__ __launch_bounds__(256) void hs_gather_kernel(GatherParams p, const vo
   }
 }
 
+// Packed-row gather for permutations of whole tables (K4's permutation apply).  A random row
+// read of one column fetches a whole memory sector for a few bytes, once per column; packing
+// each row's fields (and validity bytes) into one `row_bytes` record first makes the random
+// phase one sector per row: all fields of a record share it, so the per-column reads after the
+// first hit the cache.  Field byte offsets within a record: GatherCol.pad (values), and
+// `vbase` + column index (validity bytes).
+__global__ __launch_bounds__(256) void hs_pack_rows_kernel(GatherParams p, int row_bytes,
+                                                           int vbase, int64_t n,
+                                                           uint8_t* __restrict__ rows) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint8_t* rec = rows + i * row_bytes;
+    for (int c = 0; c < p.ncols; ++c) {
+      const GatherCol& g = p.cols[c];
+      uint8_t* f = rec + g.pad;
+      switch (g.elem_bytes) {
+        case 1: *f = ((const uint8_t*)g.src)[i]; break;
+        case 2: *(uint16_t*)f = ((const uint16_t*)g.src)[i]; break;
+        case 4: *(uint32_t*)f = ((const uint32_t*)g.src)[i]; break;
+        default: *(uint64_t*)f = ((const uint64_t*)g.src)[i]; break;
+      }
+      if (g.dst_valid) rec[vbase + c] = g.src_valid ? g.src_valid[i] : (uint8_t)1;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void hs_gather_rows_kernel(GatherParams p, int row_bytes,
+                                                             int vbase,
+                                                             const uint8_t* __restrict__ rows,
+                                                             const void* __restrict__ idx,
+                                                             int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t r = p.idx_is_u32 ? (int64_t)((const uint32_t*)idx)[i] : ((const int64_t*)idx)[i];
+    const uint8_t* rec = rows + r * row_bytes;
+    for (int c = 0; c < p.ncols; ++c) {
+      const GatherCol& g = p.cols[c];
+      const uint8_t* f = rec + g.pad;
+      switch (g.elem_bytes) {
+        case 1: ((uint8_t*)g.dst)[i] = *f; break;
+        case 2: ((uint16_t*)g.dst)[i] = *(const uint16_t*)f; break;
+        case 4: ((uint32_t*)g.dst)[i] = *(const uint32_t*)f; break;
+        default: ((uint64_t*)g.dst)[i] = *(const uint64_t*)f; break;
+      }
+      if (g.dst_valid) g.dst_valid[i] = rec[vbase + c];
+    }
+  }
+}
+
 // Bucket offsets from sorted bucket ids: off[b] = first i with bucket[i] >= b  (b in [0, B]).
 __global__ void hs_bucket_offsets_kernel(const int32_t* __restrict__ sorted_bucket, int64_t n,
                                          int B, int64_t* __restrict__ off) {
@@ -183,6 +232,23 @@ int hs_gather(const GatherParams* p, const void* idx, int64_t n, void* stream) {
   if (gx > 2048) gx = 2048;
   hipLaunchKernelGGL(hs_gather_kernel, dim3((unsigned)gx, p->ncols), dim3(256), 0,
                      (hipStream_t)stream, *p, idx, n);
+  return (int)hipGetLastError();
+}
+
+// Packed-row gather (no padding rows): pack every column into `rows` (n_src records of
+// `row_bytes`, 16-byte multiple), then gather the records by `idx` into the destinations.
+int hs_gather_packed(const GatherParams* p, int row_bytes, int vbase, int64_t n_src,
+                     uint8_t* rows, const void* idx, int64_t n, void* stream) {
+  if (n == 0 || p->ncols == 0) return 0;
+  if (row_bytes <= 0 || row_bytes % 16 != 0) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t gp = (n_src + 255) / 256 < 8192 ? (n_src + 255) / 256 : 8192;
+  if (n_src > 0)
+    hipLaunchKernelGGL(hs_pack_rows_kernel, dim3((unsigned)gp), dim3(256), 0, s, *p, row_bytes,
+                       vbase, n_src, rows);
+  const int64_t gg = (n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192;
+  hipLaunchKernelGGL(hs_gather_rows_kernel, dim3((unsigned)gg), dim3(256), 0, s, *p, row_bytes,
+                     vbase, (const uint8_t*)rows, idx, n);
   return (int)hipGetLastError();
 }
 

@@ -164,6 +164,7 @@ def lib():
     _sig(L.hs_exclusive_scan_i64, I, P, P, I64, P, I64, P)
     _sig(L.hs_exclusive_scan_u32, I, P, P, I64, P, I64, P)
     _sig(L.hs_gather, I, P, P, I64, P)
+    _sig(L.hs_gather_packed, I, P, I, I, I64, P, P, I64, P)
     _sig(L.hs_bucket_offsets, I, P, I64, I, P, P)
     _sig(L.hs_scan_tile_rows, I)
     _sig(L.hs_scan_grid, I)

@@ -5,6 +5,7 @@ hipGraph capture).  Kernels never allocate; workspaces are torch allocations mad
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -303,13 +304,52 @@ def exclusive_scan_i64(x):
 # ------------------------------------------------------------------------------------------------
 # Gather
 # ------------------------------------------------------------------------------------------------
+# packed-row gather (hs_gather_packed, opt-in: HS_GATHER_PACKED=1): tables of at least this many
+# rows, records of at most PACKED_MAX_BYTES.  Off by default: at SF100 it cut the li_shipdate
+# build's sort+gather 0.102 -> 0.082 s (a random permutation) but raised li_orderkey's
+# 0.060 -> 0.274 s (a permutation that is nearly sequential within each bucket, where the
+# per-column gather already streams, plus the record buffer's allocation):
+# profiles/build_packed_gather_r3.log
+PACKED_MIN_ROWS = 1 << 20
+PACKED_MAX_BYTES = 64
+
+
+def _packed_layout(cols, want_valid: bool):
+    """(row_bytes, value offsets, validity base) of the packed records of ``cols`` (fields by
+    descending width, so every field is naturally aligned), or None when records would exceed
+    PACKED_MAX_BYTES."""
+    order = sorted(range(len(cols)), key=lambda j: -cols[j].data.element_size())
+    offs = [0] * len(cols)
+    at = 0
+    for j in order:
+        offs[j] = at
+        at += cols[j].data.element_size()
+    vbase = at
+    if any(c.valid is not None and want_valid for c in cols):
+        at += len(cols)
+    rb = (at + 15) // 16 * 16
+    return (rb, offs, vbase) if rb <= PACKED_MAX_BYTES else None
+
+
 def gather_columns(cols: list, idx, want_valid: bool = True, padded: bool = False) -> list:
     """Gather a list of DeviceColumns by ``idx`` (int32 or int64 tensor) in one launch.
     ``padded``: ``idx`` (int64) may hold -1 for outer-join padding rows, which come out NULL
-    (every output column then carries a validity mask)."""
+    (every output column then carries a validity mask).  With ``HS_GATHER_PACKED=1``,
+    permutations of large multi-column tables go through packed records (``hs_gather_packed``):
+    one random sector per row instead of one per column."""
     torch = _torch()
     from ..exec.device_table import DeviceColumn
     n = idx.numel()
+    if (not padded and len(cols) >= 2 and len(cols) <= NL.GATHER_MAX_COLS and
+            n >= PACKED_MIN_ROWS and os.environ.get("HS_GATHER_PACKED", "0") == "1" and
+            len({len(c.data) for c in cols}) == 1):
+        lay = _packed_layout(cols, want_valid)
+        if lay is not None:
+            rb, offs, vbase = lay
+            n_src = len(cols[0].data)
+            free, _ = torch.cuda.mem_get_info(cols[0].data.device)
+            if n_src * rb < free // 2:
+                return _gather_packed(cols, idx, want_valid, rb, offs, vbase, n_src)
     out = []
     for i in range(0, len(cols), NL.GATHER_MAX_COLS):
         chunk = cols[i:i + NL.GATHER_MAX_COLS]
@@ -329,6 +369,30 @@ def gather_columns(cols: list, idx, want_valid: bool = True, padded: bool = Fals
         NL.check(NL.lib().hs_gather(C.byref(p), NL.ptr(idx), n, NL.stream_ptr()), "hs_gather")
         out.extend(res)
     return out
+
+
+def _gather_packed(cols, idx, want_valid, rb: int, offs, vbase: int, n_src: int) -> list:
+    torch = _torch()
+    from ..exec.device_table import DeviceColumn
+    n = idx.numel()
+    dev = cols[0].data.device
+    p = NL.GatherParams()
+    res = []
+    for j, c in enumerate(cols):
+        dst = torch.empty(n, dtype=c.data.dtype, device=dev)
+        dv = torch.empty(n, dtype=torch.uint8, device=dev) \
+            if (c.valid is not None and want_valid) else None
+        p.cols[j] = NL.GatherCol(c.data.data_ptr(), dst.data_ptr(),
+                                 c.valid.data_ptr() if c.valid is not None else 0,
+                                 dv.data_ptr() if dv is not None else 0,
+                                 c.data.element_size(), offs[j])
+        res.append(DeviceColumn(dst, dv, c.atype, c.dictionary))
+    p.ncols = len(cols)
+    p.idx_is_u32 = 1 if idx.dtype == torch.int32 else 0
+    rows = torch.empty(max(n_src, 1) * rb, dtype=torch.uint8, device=dev)
+    NL.check(NL.lib().hs_gather_packed(C.byref(p), rb, vbase, n_src, NL.ptr(rows), NL.ptr(idx),
+                                       n, NL.stream_ptr()), "hs_gather_packed")
+    return res
 
 
 def mark_rows(idx, n: int):

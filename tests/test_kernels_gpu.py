@@ -370,3 +370,45 @@ def test_merge_runs_permutation_equals_stable_sort(device, runs_per_bucket):
     # unsorted runs are detected: the caller falls back to the radix sort
     bad = _col(pa.array(rng.integers(0, 100, n).astype(np.int64)), device)
     assert K.merge_runs_permutation([bad], np.asarray(off), np.asarray(grp)) is None
+
+
+@pytest.mark.parametrize("idx_bits", [32, 64])
+def test_packed_row_gather_matches_per_column_gather(device, idx_bits):
+    """Permutations of large tables through packed records (hs_gather_packed, HS_GATHER_PACKED=1):
+    1-, 2-, 4- and 8-byte columns with and without validity give exactly what the per-column
+    gather and torch indexing give."""
+    import os
+    import torch
+    from hyperspace_amd.exec.device_table import DeviceColumn
+    from hyperspace_amd.ops import kernels as K
+    n = (1 << 20) + 4097
+    g = torch.Generator(device=device)
+    g.manual_seed(3)
+    cols = [DeviceColumn(torch.randint(-2**62, 2**62, (n,), device=device, generator=g),
+                         None, pa.int64()),
+            DeviceColumn(torch.rand(n, device=device, dtype=torch.float64, generator=g),
+                         (torch.rand(n, device=device, generator=g) < 0.9).to(torch.uint8),
+                         pa.float64()),
+            DeviceColumn(torch.randint(0, 2**31 - 1, (n,), device=device, generator=g)
+                         .to(torch.int32), None, pa.int32()),
+            DeviceColumn(torch.randint(0, 30000, (n,), device=device, generator=g)
+                         .to(torch.int16), None, pa.int16()),
+            DeviceColumn(torch.randint(0, 2, (n,), device=device, generator=g).to(torch.uint8),
+                         (torch.rand(n, device=device, generator=g) < 0.5).to(torch.uint8),
+                         pa.bool_())]
+    perm = torch.randperm(n, device=device, generator=g)[: n - 1000]
+    idx = perm.to(torch.int32 if idx_bits == 32 else torch.int64)
+    lay = K._packed_layout(cols, True)
+    assert lay is not None and lay[0] == 32
+    ref = K.gather_columns(cols, idx)
+    os.environ["HS_GATHER_PACKED"] = "1"
+    try:
+        got = K.gather_columns(cols, idx)
+    finally:
+        os.environ.pop("HS_GATHER_PACKED")
+    for c, a, b in zip(cols, got, ref):
+        assert torch.equal(a.data, b.data) and torch.equal(a.data, c.data[perm])
+        if c.valid is None:
+            assert a.valid is None and b.valid is None
+        else:
+            assert torch.equal(a.valid, b.valid) and torch.equal(a.valid, c.valid[perm])
