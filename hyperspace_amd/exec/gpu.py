@@ -1496,6 +1496,11 @@ class GpuBackend:
                          [p.aggs[i] for i in range(p.naggs)], compacts)
         side = self._scan_side_stream(g)
         if side is None:
+            if g.on_side:
+                import torch
+                # side-stream scans were switched off after this pipeline replayed there: its
+                # shared intermediates are free only once those replays are done
+                torch.cuda.current_stream().wait_stream(g.side_stream)
             handle = g.launch(range_bounds(lo, lo_incl, hi, hi_incl), k.args.pack(values))
             return (_GraphPending(g, handle), None, None, None)
         import torch
