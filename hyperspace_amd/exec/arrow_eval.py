@@ -121,10 +121,29 @@ def eval_expr(e: E.Expression, t: pa.Table):
     if isinstance(e, E.Cast):
         v = eval_expr(e.child, t)
         if _is_num(v.type) and _is_num(e.dtype):
+            if pa.types.is_floating(v.type) and pa.types.is_integer(e.dtype):
+                return _float_to_int(v, e.dtype)
             # Spark's numeric casts truncate toward zero and wrap (non-ANSI)
             return pc.cast(v, e.dtype, safe=False)
         return pc.cast(v, e.dtype)
     raise NotImplementedError(f"cannot evaluate {type(e).__name__}")
+
+
+def _float_to_int(v, dtype: pa.DataType):
+    """Spark (non-ANSI) float -> integral cast: truncate toward zero, NaN -> 0, saturate to the
+    long range (d2l) for a long target, to the int range (d2i) otherwise; a short / byte target
+    then wraps (``toInt.toShort``).  Explicit clamps: an out-of-range ``pc.cast`` is undefined."""
+    lo, hi = ((-2.0 ** 63, 2.0 ** 63) if pa.types.is_int64(dtype)
+              else (-2147483648.0, 2147483647.0))
+    f = pc.cast(v, pa.float64())
+    f = pc.if_else(pc.is_nan(f), 0.0, f)
+    f = pc.trunc(pc.min_element_wise(pc.max_element_wise(f, lo, skip_nulls=False), hi,
+                                     skip_nulls=False))
+    if pa.types.is_int64(dtype):
+        big = pc.greater_equal(f, 2.0 ** 63)
+        out = pc.cast(pc.if_else(big, 0.0, f), pa.int64(), safe=False)
+        return pc.if_else(big, pa.scalar(2**63 - 1, pa.int64()), out)
+    return pc.cast(pc.cast(f, pa.int64(), safe=False), dtype, safe=False)
 
 
 def eval_predicate(e: E.Expression, t: pa.Table) -> pa.Table:

@@ -291,6 +291,7 @@ def _streaming_build(session, rel, my_files, columns, indexed, num_buckets, out_
     paths: List[str] = []
     t0 = time.perf_counter()
     decode_s = sort_s = 0.0
+    sent_total = 0
     source_bytes = 0
     schema = names = None
     for pi, (lo, hi) in enumerate(passes):
@@ -337,6 +338,8 @@ def _streaming_build(session, rel, my_files, columns, indexed, num_buckets, out_
         ts = time.perf_counter()
         if multi:
             recv = ex.finish() if ex is not None else None
+            if ex is not None:
+                sent_total += ex.sent_bytes
             vnames = [n for n in names if n in (nullable or set())]
             table = {}
             vi = len(names)
@@ -370,7 +373,7 @@ def _streaming_build(session, rel, my_files, columns, indexed, num_buckets, out_
     if multi:
         dist.barrier()
     LAST_BUILD_STATS.update({"passes": len(passes), "file_groups": len(groups),
-                             "source_bytes": source_bytes,
+                             "source_bytes": source_bytes, "exchange_sent_bytes": sent_total,
                              "pass_decode_s": decode_s, "pass_sort_write_s": sort_s,
                              "total_s": time.perf_counter() - t0})
     return paths

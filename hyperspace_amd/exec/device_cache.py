@@ -167,13 +167,15 @@ def seeded_index(files, columns: List[str], num_buckets: int, rank: int,
     key = (tuple(sorted(owned)), rank, world)
     with _SEED_LOCK:
         e = _SEEDS.get(key)
-        if e is not None:
-            _SEEDS.move_to_end(key)
-    if e is None or e["num_buckets"] != num_buckets or any(c not in e["cols"] for c in columns):
-        return None
+        if e is None or e["num_buckets"] != num_buckets or \
+                any(c not in e["cols"] for c in columns):
+            return None
+        # consumed on its first hit: the device cache owns the table from here on, so the
+        # seed pins no HBM outside the cache budget
+        _SEEDS.pop(key)
+        SEED_STATS["hits"] += 1
     off = e["off"]
     cols = {c: e["cols"][c] for c in columns}
-    SEED_STATS["hits"] += 1
     return DeviceTable(cols, int(off[-1]), e["off_dev"], off)
 
 

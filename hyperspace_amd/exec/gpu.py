@@ -1515,6 +1515,12 @@ class GpuBackend:
             for x in (c.data, c.valid):
                 if x is not None:
                     x.record_stream(side)
+        # the generated kernel reads the compact codes (jit._fill_common) rather than c.data:
+        # those buffers are in use by the side stream too (a device-cache eviction between
+        # this launch and its fetch must not hand their memory to query-stream allocations)
+        for enc in (compacts or {}).values():
+            for x in _compact_buffers(enc):
+                x.record_stream(side)
         for x in g.buffers():
             x.record_stream(side)
         with torch.cuda.stream(side):
@@ -2124,6 +2130,21 @@ def _eval_scalar(e, agg_val, attr_val):
             return a * b
         return None if b == 0 else a / b
     raise Unsupported(f"result expression {type(e).__name__}")
+
+
+def _compact_buffers(enc) -> list:
+    """Device tensors of a compact encoding whose pointers go into a kernel's argument block
+    (codes, and a grouped 16-bit form's group bases and wide codes)."""
+    out = [enc.codes]
+    g = getattr(enc, "g16", None)
+    for e in (enc, g if g else None):
+        if e is None:
+            continue
+        for name in ("gbase", "wide", "codes"):
+            x = getattr(e, name, None)
+            if x is not None and hasattr(x, "record_stream") and all(x is not y for y in out):
+                out.append(x)
+    return out
 
 
 class _GraphPending:

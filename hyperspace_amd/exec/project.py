@@ -198,11 +198,17 @@ class _Gen:
                 self.lines.append(f"const double {v} = (double){a};")
             elif tk == "b":
                 self.lines.append(f"const bool {v} = {a} != 0;")
-            elif ak == "f":
+            elif ak == "f" and pa.types.is_int64(e.dtype):
                 # truncation toward zero; NaN / out of range saturate like the JVM's d2l
                 self.lines.append(f"const long long {v} = {a} != {a} ? 0LL : ({a} >= 9.2233720368547758e18 ? "
                                   f"0x7fffffffffffffffLL : ({a} <= -9.2233720368547758e18 ? "
                                   f"(-0x7fffffffffffffffLL - 1) : (long long){a}));")
+            elif ak == "f":
+                # Spark: d2i saturates to the int range (NaN -> 0); a short / byte target is
+                # toInt then a wrapping narrow, which the store performs
+                self.lines.append(f"const long long {v} = {a} != {a} ? 0LL : ({a} >= 2147483647.0 ? "
+                                  f"2147483647LL : ({a} <= -2147483648.0 ? -2147483648LL : "
+                                  f"(long long){a}));")
             else:
                 self.lines.append(f"const long long {v} = (long long){a};")
             return v, av, tk

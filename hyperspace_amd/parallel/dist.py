@@ -196,6 +196,18 @@ class DistContext:
         for e in pend:
             e.wait()
         flat = torch.cat([e.host for e in pend])
+        # ranks must coalesce the same entries (a rank that abandoned a query between submit
+        # and fetch would shift every later result): agree on (count, total bytes, layout hash)
+        # first and fail loudly on a mismatch instead of hanging or misattributing results
+        lay = 0
+        for e in pend:
+            lay = (lay * 1000003 + int(e.host.numel())) & ((1 << 62) - 1)
+        hdr = torch.tensor([len(pend), int(flat.numel()), lay], dtype=torch.int64)
+        hdrs = [torch.empty_like(hdr) for _ in range(self.world)]
+        dist.all_gather(hdrs, hdr)
+        if any(not torch.equal(h, hdr) for h in hdrs):
+            raise RuntimeError("cross-rank combine mismatch: ranks have different pending "
+                               f"aggregates {[h.tolist() for h in hdrs]}")
         parts = [torch.empty_like(flat) for _ in range(self.world)]
         dist.all_gather(parts, flat)
         allr = torch.stack(parts)             # [world, total bytes]

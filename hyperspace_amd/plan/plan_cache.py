@@ -243,6 +243,34 @@ def _same(a: E.Literal, b: E.Literal) -> bool:
     return type(a.value) is type(b.value) and a.value == b.value and a.dtype == b.dtype
 
 
+class _Entry:
+    """One cached executed plan.  ``prepared`` holds per-backend re-bindable launches of it
+    (exec/prepared.py): a hit runs those with the new literals written into ``old_lits`` for
+    the duration of the launch (under ``lock``), with no substitution and no executor walk."""
+    __slots__ = ("plan", "old_lits", "paths", "refs", "reuse", "prepared", "lock")
+
+    def __init__(self, plan, old_lits, paths, refs, reuse):
+        self.plan, self.old_lits, self.paths, self.refs, self.reuse = \
+            plan, old_lits, paths, refs, reuse
+        self.prepared: Dict[int, object] = {}
+        self.lock = threading.Lock()
+
+    def bind_literals(self, lits) -> list:
+        """Write the new query's literal values into the cached plan's literal objects (caller
+        holds ``lock``); returns what ``restore_literals`` puts back."""
+        saved = []
+        for o, n in zip(self.old_lits, lits):
+            if o is not n:
+                saved.append((o, o.value))
+                o.value = n.value
+        return saved
+
+    @staticmethod
+    def restore_literals(saved) -> None:
+        for o, v in saved:
+            o.value = v
+
+
 class PlanCache:
     def __init__(self, capacity: int = CAPACITY):
         self.capacity = capacity
@@ -264,8 +292,10 @@ class PlanCache:
             snap = id(snap_obj)
         return (id(session), session.conf.version, rules, snap)
 
-    def lookup(self, session, logical) -> Tuple[Optional[object], Optional[tuple], _Ctx]:
-        """(executed plan or None, key, fingerprint context) of ``logical``."""
+    def lookup_entry(self, session, logical):
+        """(entry or None, key, fingerprint context) of ``logical`` - no substitution.  A hit's
+        ``ctx.lits`` are the new query's literals, position for position with
+        ``entry.old_lits``."""
         ctx = _Ctx()
         try:
             key = (self._session_key(session, ctx), _fp(logical, ctx))
@@ -276,24 +306,30 @@ class PlanCache:
             hit = self._lru.get(key)
             if hit is not None:
                 self._lru.move_to_end(key)
-        if hit is None:
+        if hit is None or len(hit.old_lits) != len(ctx.lits):
             self.misses += 1
             return None, key, ctx
-        plan, old_lits, paths, _refs, reuse = hit
-        ctx.reuse = reuse
-        if len(old_lits) != len(ctx.lits):
-            self.misses += 1
-            return None, key, ctx
-        # only literals whose value changed are substituted, along their own paths
-        m = {id(o): n for o, n in zip(old_lits, ctx.lits) if o is not n and not _same(o, n)}
-        new_plan = plan
-        if m:
-            hot = set().union(*(paths[k] for k in m))
-            new_plan = _subst(plan, m, hot, {})
+        ctx.reuse = hit.reuse
         self.hits += 1
-        return new_plan, key, ctx
+        return hit, key, ctx
 
-    def store(self, key, executed, ctx: _Ctx) -> bool:
+    def materialize(self, entry: "_Entry", ctx: _Ctx):
+        """The cached executed plan with the new query's literals (``ctx.lits``): only literals
+        whose value changed are substituted, along their own paths."""
+        m = {id(o): n for o, n in zip(entry.old_lits, ctx.lits) if o is not n and not _same(o, n)}
+        if not m:
+            return entry.plan
+        hot = set().union(*(entry.paths[k] for k in m))
+        return _subst(entry.plan, m, hot, {})
+
+    def lookup(self, session, logical) -> Tuple[Optional[object], Optional[tuple], _Ctx]:
+        """(executed plan or None, key, fingerprint context) of ``logical``."""
+        entry, key, ctx = self.lookup_entry(session, logical)
+        if entry is None:
+            return None, key, ctx
+        return self.materialize(entry, ctx), key, ctx
+
+    def store(self, key, executed, ctx: _Ctx):
         """Cache ``executed`` — the plan *before* exchange reuse — for ``key`` if every literal
         of the analyzed plan reached it.  Exchange reuse compares canonical subtrees including
         literal values (a self-join with equal filter literals shares one exchange, with unequal
@@ -301,7 +337,7 @@ class PlanCache:
         exchanges that could match are flagged and re-run ``reuse_exchanges`` after each
         substitution."""
         if key is None:
-            return False
+            return None
         from . import physical as X
         exch = executed.collect(lambda n: isinstance(n, (X.ShuffleExchangeExec,
                                                          X.BroadcastExchangeExec)))
@@ -314,18 +350,19 @@ class PlanCache:
         ids = {id(x) for x in present}
         if not all(id(x) in ids for x in ctx.lits):
             self.uncacheable += 1
-            return False
+            return None
         paths = {}
         for x in ctx.lits:
             if id(x) not in paths:
                 hot: set = set()
                 _hot_paths(executed, {id(x)}, hot, {})
                 paths[id(x)] = hot
+        entry = _Entry(executed, list(ctx.lits), paths, list(ctx.refs), reuse)
         with self._lock:
-            self._lru[key] = (executed, list(ctx.lits), paths, list(ctx.refs), reuse)
+            self._lru[key] = entry
             while len(self._lru) > self.capacity:
                 self._lru.popitem(last=False)
-        return True
+        return entry
 
     def clear(self):
         with self._lock:

@@ -185,6 +185,40 @@ def test_side_stream_scans_pipelined_with_joins(tpch):
         _close(table(g3), table(q3(i).collect()))
 
 
+def test_side_stream_scan_survives_table_eviction(tpch):
+    """A warm scan pipeline replays on the side stream; the device cache then drops the table
+    (and with it the compact codes the generated kernel reads) before the result is fetched,
+    and the query stream reuses that memory at once.  The replay must still read the old codes:
+    every buffer whose pointer is in the args block is marked in use by the side stream
+    (ADVICE r3)."""
+    import torch
+    s, lpath, _ = tpch
+    hs = Hyperspace(s)
+    li = s.read.parquet(lpath)
+    hs.createIndex(li, IndexConfig("li_ship_ev", ["l_shipdate"],
+                                   ["l_discount", "l_quantity", "l_extendedprice"]))
+    Hyperspace.enable(s)
+
+    def q6(i):
+        y = 1993 + i % 5
+        return li.filter(f"l_shipdate >= DATE '{y}-01-01' AND l_shipdate < DATE '{y + 1}-01-01'"
+                         f" AND l_quantity < {20 + i % 7}") \
+            .agg(sum_(col("l_extendedprice") * col("l_discount")).alias("revenue"),
+                 count("*").alias("n"))
+    backend = s.backend()
+    want = [q6(i).collect() for i in range(4)]      # warm: later replays go to the side stream
+    for i in range(4):
+        f = q6(i).collect_async()
+        backend.cache.clear()                       # drops the table's last references
+        junk = [torch.full((1 << 22,), -7, dtype=torch.int32, device="cuda") for _ in range(16)]
+        got = f.result()
+        del junk
+        assert f.path == "native", backend.fallback_reason
+        assert got[0][1] == want[i][0][1]
+        assert abs(got[0][0] - want[i][0][0]) <= 1e-9 * abs(want[i][0][0])
+    assert any(g.on_side for g in backend.graphs._lru.values())
+
+
 def test_filter_rows_and_group_by_native(tpch):
     s, lpath, _ = tpch
     hs = Hyperspace(s)
@@ -436,3 +470,5 @@ def test_first_query_after_build_uses_the_build_hbm_columns(tpch):
     assert path == "native", s.backend().fallback_reason
     assert DC.SEED_STATS["hits"] == before["hits"] + 1
     _close(g, c)
+    # the seed was consumed by that first hit (it pins no HBM outside the cache budget)
+    assert not any(k[0] and "li_seed" in k[0][0][0] for k in DC._SEEDS)

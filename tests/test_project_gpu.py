@@ -100,3 +100,20 @@ def test_union_all_rows_and_aggregates_native(tbl):
         assert path == "native", s.backend().fallback_reason
         assert g.num_rows > 0
         _close(g, c)
+
+
+def test_float_to_int_casts_saturate_like_spark(tbl):
+    """d2i / d2l saturation (NaN -> 0, +-inf and 3e9 clamp) and the wrapping narrow of a short /
+    byte target, device against the host oracle (the int target used to wrap)."""
+    s, df = tbl
+    f = df.filter(col("k") < 6000)
+    big = col("x") * 1e8                    # up to +-1e10: outside the int range
+    inf = col("x") * 1e307 * 100            # +-inf (0 stays 0)
+    q = f.select(col("k"), big.cast("int").alias("i32"), big.cast("short").alias("i16"),
+                 big.cast("byte").alias("i8"), big.cast("long").alias("i64"),
+                 inf.cast("int").alias("inf32"), inf.cast("long").alias("inf64"))
+    g, c, path = _both(s, q)
+    assert path == "native", s.backend().fallback_reason
+    _close(g, c)
+    i32 = g.column("i32").to_pylist()
+    assert 2147483647 in i32 and -2147483648 in i32

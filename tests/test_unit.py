@@ -366,3 +366,17 @@ def test_negative_zero_float_keys_bucket_like_spark_2_4():
     from hyperspace_amd.utils import murmur3
     b = murmur3.bucket_ids([pa.array([0.0, -0.0])], 200)
     assert int(b[0]) != int(b[1])
+
+
+def test_float_to_int_cast_oracle_matches_spark():
+    """Host oracle of Spark's non-ANSI float -> integral casts (exec/arrow_eval._float_to_int)."""
+    import pyarrow as pa
+    from hyperspace_amd.exec.arrow_eval import _float_to_int
+    v = pa.array([float("nan"), float("inf"), -float("inf"), 3e9, -3e9, 2.9, -2.9, 70000.5, None])
+    assert _float_to_int(v, pa.int32()).to_pylist() == \
+        [0, 2**31 - 1, -2**31, 2**31 - 1, -2**31, 2, -2, 70000, None]
+    # short / byte: toInt then a wrapping narrow
+    assert _float_to_int(v, pa.int16()).to_pylist() == [0, -1, 0, -1, 0, 2, -2, 4464, None]
+    assert _float_to_int(v, pa.int8()).to_pylist() == [0, -1, 0, -1, 0, 2, -2, 112, None]
+    assert _float_to_int(v, pa.int64()).to_pylist() == \
+        [0, 2**63 - 1, -2**63, 3000000000, -3000000000, 2, -2, 70000, None]
