@@ -130,6 +130,9 @@ def main():
     ap.add_argument("--record-baseline", action="store_true",
                     help="with --device cpu: save the JSON line as profiles/cpu_baseline_sf<SF>.json "
                          "(the vs_baseline denominator of later GPU runs)")
+    ap.add_argument("--host-breakdown", type=int, default=0, metavar="N",
+                    help="after the timed steps, time N queries phase by phase on the host "
+                         "(DataFrame build / plan / submit / result), reported as host_breakdown")
     args = ap.parse_args()
 
     import numpy as np
@@ -441,6 +444,8 @@ def main():
         latency("q3_join_index_ms", q3)
         s.conf.set(ji_key, "false")
     lat.update(cold)
+    hb = _host_breakdown(args.host_breakdown, (q6, q3), backend, sync, barrier) \
+        if args.host_breakdown and on_gpu else None
 
     # ---------------------------------------------------------------- cross-check
     check = None
@@ -497,6 +502,8 @@ def main():
                "datagen_s": round(gen_s, 2), "crosscheck": check, "inflight": args.inflight}
         if q3f is not None:
             out["q3_full"] = q3f
+        if hb is not None:
+            out["host_breakdown"] = hb
         if ji_run is not None:
             out["join_index"] = {"value": round(ji_run["qps"], 3),
                                  "ms_per_step": round(ji_run["ms_per_step"], 3),
@@ -520,6 +527,46 @@ def main():
     if dist:
         barrier()
         torch.distributed.destroy_process_group()
+
+
+def _host_breakdown(n, fns, backend, sync, barrier) -> dict:
+    """Host milliseconds per query of each phase of the serving loop (``inflight`` 2): building
+    the DataFrame, planning it (analysis + plan cache / optimizer), submitting it to the device
+    executor, and waiting for its result (the last one includes device time the host did not
+    overlap)."""
+    from collections import deque
+    ph = {"build": 0.0, "plan": 0.0, "submit": 0.0, "result": 0.0}
+    pend = deque()
+    barrier()
+    sync()
+    t_all = time.perf_counter()
+    for i in range(n):
+        for fn in fns:
+            t0 = time.perf_counter()
+            df = fn(5000 + i)
+            t1 = time.perf_counter()
+            plan = df.queryExecution.executed_plan
+            t2 = time.perf_counter()
+            fut = backend.collect_async(plan)
+            t3 = time.perf_counter()
+            ph["build"] += t1 - t0
+            ph["plan"] += t2 - t1
+            ph["submit"] += t3 - t2
+            pend.append(fut)
+        while len(pend) > 2:
+            t4 = time.perf_counter()
+            pend.popleft().result()
+            ph["result"] += time.perf_counter() - t4
+    while pend:
+        t4 = time.perf_counter()
+        pend.popleft().result()
+        ph["result"] += time.perf_counter() - t4
+    sync()
+    nq = n * len(fns)
+    out = {k: round(v / nq * 1000.0, 4) for k, v in ph.items()}
+    out["wall_ms_per_query"] = round((time.perf_counter() - t_all) / nq * 1000.0, 4)
+    out["queries"] = nq
+    return out
 
 
 if __name__ == "__main__":

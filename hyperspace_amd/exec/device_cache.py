@@ -3,7 +3,8 @@
 Index data is immutable per log version, so the executor keeps decoded index columns resident in
 HBM (288 GB per MI355X) and re-reads files only when the index content changes — the "keep
 tensors resident instead of re-reading them" rule.  Entries are keyed by the exact file set
-(path, size, mtime), the projected columns and the rank's bucket ownership; eviction is LRU by
+(path, size, mtime), the projected columns and the rank's bucket ownership (the session's owner
+map, parallel/placement.py); eviction is LRU by
 bytes under ``spark.hyperspace.mi.deviceCacheBytes``.
 
 Index tables are laid out bucket-major with a ``B+1`` offset table; every bucket is sorted by the
@@ -91,8 +92,27 @@ class DeviceTableCache:
                 self._lru[key] = t
                 self._size[key] = nb
                 self._bytes += nb
+                t._hs_cache_key = key
                 self._evict(key)
         return t
+
+    def holds(self, t) -> bool:
+        """Whether ``t`` is still the resident table of its key (then counted as a hit, like
+        ``get``): lets the executor reuse a relation it lowered earlier without rebuilding the
+        key from the file list."""
+        key = getattr(t, "_hs_cache_key", None)
+        if key is None:
+            return False
+        with self._lock:
+            if self._lru.get(key) is not t:
+                return False
+            self._lru.move_to_end(key)
+            self.hits += 1
+            nb = t.resident_bytes()
+            self._bytes += nb - self._size.get(key, nb)
+            self._size[key] = nb
+            self._evict(key)
+            return True
 
     @property
     def resident_bytes(self) -> int:
@@ -152,17 +172,21 @@ def register_seed(session, paths, cols: Dict[str, DeviceColumn], off, rank: int,
 
 
 def seeded_index(files, columns: List[str], num_buckets: int, rank: int,
-                 world: int) -> Optional[DeviceTable]:
-    """The build seed of exactly this rank's share of ``files`` holding ``columns``, as a
-    table view (shared tensors), or None."""
+                 world: int, owned_buckets=None) -> Optional[DeviceTable]:
+    """The build seed of exactly this rank's share of ``files`` (buckets ``owned_buckets``,
+    default ``b % world == rank``) holding ``columns``, as a table view (shared tensors), or
+    None.  A build writes bucket b from rank b % world, so only a query placement that gives
+    this rank those same buckets can take the seed."""
     if not _SEEDS:
         return None
+    mine = set(owned_buckets) if owned_buckets is not None else \
+        {b for b in range(num_buckets) if b % world == rank}
     owned = []
     for f in files:
         b = get_bucket_id(P.get_name(f.path))
         if b is None or b >= num_buckets:
             return None
-        if b % world == rank:
+        if b in mine:
             owned.append((P.to_local(f.path), int(f.length)))
     key = (tuple(sorted(owned)), rank, world)
     with _SEED_LOCK:
@@ -185,8 +209,9 @@ def clear_seeds() -> None:
 
 
 def load_bucketed_index(files, columns: List[str], num_buckets: int, sort_cols: List[str], device,
-                        rank: int = 0, world: int = 1) -> DeviceTable:
-    """Load index files bucket-major for the buckets this rank owns (b % world == rank)."""
+                        rank: int = 0, world: int = 1, owned_buckets=None) -> DeviceTable:
+    """Load index files bucket-major for the buckets this rank owns (``owned_buckets``, default
+    b % world == rank); every other bucket is an empty range of the offset table."""
     import torch
     from ..ops import kernels as K
     by_bucket: Dict[int, list] = {}
@@ -195,7 +220,9 @@ def load_bucketed_index(files, columns: List[str], num_buckets: int, sort_cols: 
         if b is None or b >= num_buckets:
             raise ValueError(f"not an index bucket file: {f.path}")
         by_bucket.setdefault(b, []).append(f.path)
-    owned = [b for b in range(num_buckets) if b % world == rank and b in by_bucket]
+    mine = set(owned_buckets) if owned_buckets is not None else \
+        {b for b in range(num_buckets) if b % world == rank}
+    owned = [b for b in range(num_buckets) if b in mine and b in by_bucket]
     ordered = [(b, p) for b in owned for p in sorted(by_bucket[b])]
     paths = [p for _, p in ordered]
     counts = np.zeros(num_buckets, dtype=np.int64)

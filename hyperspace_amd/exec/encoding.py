@@ -25,7 +25,7 @@ _MAX_SCALE_DIGITS = 4
 
 
 class Compact:
-    __slots__ = ("codes", "width", "base", "scale", "logical_type", "lo", "hi", "g16")
+    __slots__ = ("codes", "width", "base", "scale", "logical_type", "lo", "hi", "g16", "runs")
 
     def __init__(self, codes, width: int, base: int, scale: Optional[float], logical_type: int,
                  lo: Optional[int] = None, hi: Optional[int] = None):
@@ -36,10 +36,12 @@ class Compact:
         self.logical_type = logical_type
         self.lo, self.hi = lo, hi   # range of the (integer / scaled) values of valid rows
         self.g16 = False            # grouped16(): derived 16-bit form (None: not applicable)
+        self.runs = False           # key_runs(): derived run-length form (None: not applicable)
 
     def nbytes(self) -> int:
         n = self.codes.numel() * self.width
-        return n + (self.g16.nbytes() if self.g16 else 0)
+        n += self.g16.nbytes() if self.g16 else 0
+        return n + (self.runs.extra_bytes() if self.runs else 0)
 
     def signature(self) -> tuple:
         """Shape-relevant part (codegen key): literals like base/scale are kernel arguments."""
@@ -98,23 +100,109 @@ def grouped16(c: Compact, max_wide: float = 0.01) -> Optional[GroupedCompact]:
     c.g16 = GroupedCompact(codes.contiguous(), gbase.contiguous(), x, c.base, c.logical_type,
                            c.lo, c.hi)
     return c.g16
-    c.g16 = None
-    if c.scale is not None or c.lo is None or c.codes.numel() == 0:
+
+
+class RunCompact(Compact):
+    """Run-length form of a bucket-sorted 32-bit integer key (csrc/kernels/key_runs.hip): a
+    covering index is sorted by its indexed columns inside each bucket, so its leading key is a
+    sequence of runs of equal values (TPC-H ``l_orderkey``: 1-7 rows per key).  The run-keyed
+    merge join (``exec/jit.py`` ``MJ_RUNS``) reads, per row, only which run holds it:
+
+        gmask[g]   rows of 64-row group g that start a run (uint64 bits)
+        gruns[g]   index of the run holding row 64 * g (int32)
+        runkeys[r] code of run r (int32)
+
+    ~1.2 instead of 4 bytes per row at 4 rows per run.  ``codes`` stays the parent's full 32-bit
+    codes, so every other reader (spans, aggregate tails, group keys) is unchanged."""
+    __slots__ = ("runkeys", "gmask", "gruns", "nruns")
+
+    def __init__(self, parent: Compact, runkeys, gmask, gruns):
+        super().__init__(parent.codes, parent.width, parent.base, parent.scale,
+                         parent.logical_type, parent.lo, parent.hi)
+        self.runkeys, self.gmask, self.gruns = runkeys, gmask, gruns
+        self.nruns = int(runkeys.numel())
+
+    def extra_bytes(self) -> int:
+        return self.runkeys.numel() * 4 + self.gmask.numel() * 8 + self.gruns.numel() * 4
+
+    def nbytes(self) -> int:
+        return self.codes.numel() * self.width + self.extra_bytes()
+
+    def signature(self) -> tuple:
+        return (4, False, "runs")
+
+
+# the run form pays off when a run covers this many rows on average (4 bytes per run + 12 per
+# 64 rows against 4 per row)
+MIN_ROWS_PER_RUN = 1.5
+
+
+def key_runs(c: Compact) -> Optional[RunCompact]:
+    """The run-length form of the 32-bit integer compact ``c`` (computed once, kept on ``c``),
+    or None when it does not apply or its runs are too short to pay off."""
+    if c.runs is not False:
+        return c.runs
+    c.runs = None
+    if c.scale is not None or c.lo is None or c.width != 4 or c.codes.numel() == 0 or \
+            c.codes.numel() >= (1 << 31):
         return None
+    x = c.codes
+    runkeys, gmask, gruns = (_runs_device if x.is_cuda else runs_torch)(x)
+    if runkeys.numel() * MIN_ROWS_PER_RUN > x.numel():
+        return None
+    c.runs = RunCompact(c, runkeys, gmask, gruns)
+    return c.runs
+
+
+def _runs_device(x):
     import torch
-    x = c.codes.to(torch.int32)
+    L = NL.lib()
     n = x.numel()
-    pad = (-n) % GROUP_ROWS
-    xp = torch.cat([x, x[-1:].expand(pad)]) if pad else x
-    g = xp.view(-1, GROUP_ROWS)
-    gmin = g.amin(dim=1)
-    if int((g.amax(dim=1) - gmin).max().item()) >= (1 << 16):
-        return None
-    d = (xp - gmin.repeat_interleave(GROUP_ROWS))[:n]
-    codes = torch.where(d >= (1 << 15), d - (1 << 16), d).to(torch.int16)   # uint16 bits
-    c.g16 = GroupedCompact(codes.contiguous(), gmin.contiguous(), c.base, c.logical_type,
-                           c.lo, c.hi)
-    return c.g16
+    ng = (n + 63) // 64
+    gmask = torch.empty(ng, dtype=torch.int64, device=x.device)
+    gcnt = torch.empty(ng, dtype=torch.int64, device=x.device)
+    NL.check(L.hs_key_runs_mask(x.data_ptr(), n, gmask.data_ptr(), gcnt.data_ptr(),
+                                NL.stream_ptr()), "hs_key_runs_mask")
+    incl = torch.cumsum(gcnt, 0)
+    nruns = int(incl[-1].item())
+    gexcl = incl - gcnt
+    del incl, gcnt
+    gruns = torch.empty(ng, dtype=torch.int32, device=x.device)
+    runkeys = torch.empty(nruns, dtype=torch.int32, device=x.device)
+    NL.check(L.hs_key_runs_fill(x.data_ptr(), n, gmask.data_ptr(), gexcl.data_ptr(),
+                                gruns.data_ptr(), runkeys.data_ptr(), NL.stream_ptr()),
+             "hs_key_runs_fill")
+    return runkeys, gmask, gruns
+
+
+def runs_torch(x):
+    """PyTorch reference of ``hs_key_runs_mask`` + ``hs_key_runs_fill``: (runkeys int32,
+    gmask int64 bit patterns, gruns int32)."""
+    import torch
+    n = x.numel()
+    start = torch.ones(n, dtype=torch.bool, device=x.device)
+    if n > 1:
+        start[1:] = x[1:] != x[:-1]
+    runkeys = x[start].to(torch.int32)
+    ng = (n + 63) // 64
+    sp = torch.zeros(ng * 64, dtype=torch.int64, device=x.device)
+    sp[:n] = start.long()
+    g = sp.view(ng, 64)
+    w = torch.tensor([1 << i for i in range(63)] + [-(1 << 63)], dtype=torch.int64,
+                     device=x.device)
+    gmask = (g * w).sum(1)              # distinct bits: the wrapping sum is their OR
+    cnt = g.sum(1)
+    gexcl = torch.cumsum(cnt, 0) - cnt
+    gruns = (gexcl + g[:, 0] - 1).to(torch.int32)
+    return runkeys, gmask, gruns
+
+
+def run_of(gmask, gruns, row: int) -> int:
+    """Host reference of the kernels' run_of(row)."""
+    g, i = row >> 6, row & 63
+    m = int(gmask[g]) & ((1 << 64) - 1)
+    below = ((2 << i) - 2) & ((1 << 64) - 1)
+    return int(gruns[g]) + bin(m & below).count("1")
 
 
 def _width_for(span: int):

@@ -10,7 +10,8 @@ needs rows, so the hot shapes compile into single fused launches:
 * ``SortMergeJoin``                                 -> ``hs_join_count/emit`` + gathers
 * ``Exchange(hashpartitioning) <- Scan``           -> Murmur3 + radix sort on the device
 
-Under ``torch.distributed`` each rank owns buckets ``b % world == rank`` (co-partitioned, so a
+Under ``torch.distributed`` each rank owns the buckets the session's owner map gives it
+(``parallel/placement.py``: size-balanced, ``b % world`` for equal sizes; co-partitioned, so a
 bucketed join needs no data movement); partial aggregates are combined with one RCCL all-reduce
 and row results with an all-gather.  Shapes outside the kernel templates raise ``Unsupported``
 and the whole query runs on the host oracle (recorded in ``last_path``).
@@ -237,7 +238,7 @@ class GpuBackend:
     # ------------------------------------------------------------------------------------------
     def _rel(self, p: X.SparkPlan) -> DRel:
         if isinstance(p, X.FileSourceScanExec):
-            return self._scan(p)
+            return self._scan_memo(p)
         if isinstance(p, X.BucketUnionExec):
             return self._bucket_union(p)
         if isinstance(p, (X.FilterExec, X.ProjectExec)):
@@ -355,6 +356,26 @@ class GpuBackend:
             return out
         raise Unsupported(f"operator {p.node_name}")
 
+    def _scan_memo(self, p: X.FileSourceScanExec) -> DRel:
+        """``_scan`` of a plan leaf, reused while the device cache still holds its table: a
+        plan-cache hit re-runs the same scan nodes with new literals above them, so the file
+        listing, placement and cache-key work of the scan happen once per (node, placement)."""
+        d = self._dist()
+        tag = (d.rank, d.world, self.session.conf.get(
+            "spark.hyperspace.mi.bucketPlacement", "balanced")) if d is not None else None
+        memo = self.__dict__.setdefault("_scans", {})
+        m = memo.get(id(p))
+        if m is not None and m[0] is p and m[2] == tag and m[1].table is not None and \
+                self.cache.holds(m[1].table):
+            return m[1].copy()
+        r = self._scan(p)
+        if getattr(r.table, "_hs_cache_key", None) is not None:
+            if len(memo) > 256:
+                memo.clear()
+            memo[id(p)] = (p, r, tag)
+            return r.copy()
+        return r
+
     def _scan(self, p: X.FileSourceScanExec) -> DRel:
         rel = p.relation
         files = rel.location.all_files()
@@ -367,11 +388,13 @@ class GpuBackend:
             cols = [ncol[a.name.lower()] for a in p.output]
             sort_cols = [ncol[c.lower()] for c in idx.indexed_columns]
             load_cols = list(dict.fromkeys(cols + sort_cols))
+            owners = self._owner_map(idx.num_buckets, world, files)
+            owned = owners.owned(rank)
             table = self.cache.get(
-                files, load_cols, ("bucketed", rank, world),
-                lambda: seeded_index(files, load_cols, idx.num_buckets, rank, world) or
+                files, load_cols, ("bucketed", rank, world, owners.key),
+                lambda: seeded_index(files, load_cols, idx.num_buckets, rank, world, owned) or
                 load_bucketed_index(files, load_cols, idx.num_buckets, sort_cols, self.device,
-                                    rank, world))
+                                    rank, world, owned))
             # rank-independent identity (every rank scans the same file list)
             table.global_key = ("bucketed", _files_key(files), tuple(load_cols), world)
             colmap = {a.expr_id: c for a, c in zip(p.output, cols)}
@@ -396,6 +419,16 @@ class GpuBackend:
         table.global_key = gkey
         return DRel(table, {a.expr_id: a.name for a in p.output}, list(p.output),
                     split=world > 1)
+
+    def _owner_map(self, num_buckets: int, world: int, files=None):
+        """The session's bucket -> rank map for this bucket count (parallel/placement.py):
+        size-balanced from the first index queried with it, shared by every later index and
+        query-time shuffle with that bucket count (co-partitioned)."""
+        from ..parallel.placement import bucket_weights, session_map
+        if world <= 1:
+            return session_map(self.session, num_buckets, 1)
+        w = bucket_weights(files, num_buckets) if files is not None else None
+        return session_map(self.session, num_buckets, world, w)
 
     @staticmethod
     def _all_bucket_files(location, files, nb) -> bool:
@@ -763,7 +796,8 @@ class GpuBackend:
             bucket, counts = K.murmur3_bucket(kcols, B)
         if d is not None and d.world > 1:
             with stage("shuffle.all_to_all"):
-                cols, bucket = self._exchange_rows(d, cols, bucket)
+                cols, bucket = self._exchange_rows(d, cols, bucket,
+                                                   self._owner_map(B, d.world).dest(bucket))
             kcols = [cols[k.expr_id] for k in keys]
             counts = K.histogram(bucket, B)
         n = int(bucket.numel())
@@ -810,8 +844,9 @@ class GpuBackend:
         colmap = {a.expr_id: r.colmap[a.expr_id] for a in need}
         return DRel(nt, colmap, list(r.attrs), list(r.conds), True, list(keys), list(keys), B)
 
-    def _exchange_rows(self, d, cols: Dict[int, DeviceColumn], bucket):
-        """Route every row to rank ``bucket % world`` with ONE packed all-to-all
+    def _exchange_rows(self, d, cols: Dict[int, DeviceColumn], bucket, dest=None):
+        """Route every row to its bucket's owner rank (``dest``, default ``bucket % world``:
+        parallel/placement.py) with ONE packed all-to-all
         (``parallel/exchange.py``).  Ranks first agree on column layouts: a validity mask exists
         on every rank if it exists on any (one small all-reduce), and string dictionaries are
         unified (raw-buffer all-gather, ``parallel/dictionary.py``) with codes remapped on the
@@ -841,7 +876,7 @@ class GpuBackend:
             dicts.append(gdict)
         send = datas + [v for v in valids if v is not None] + [bucket]
         moved = RowExchange(d, [t.dtype for t in send], self.device)
-        moved.add(send, bucket)
+        moved.add(send, bucket, dest)
         got = moved.finish()
         out = {}
         vi = len(ids)
@@ -1514,15 +1549,15 @@ class GpuBackend:
         for c in list((descs or {}).values()) + [kc]:
             for x in (c.data, c.valid):
                 if x is not None:
-                    x.record_stream(side)
+                    _use_on(x, side)
         # the generated kernel reads the compact codes (jit._fill_common) rather than c.data:
         # those buffers are in use by the side stream too (a device-cache eviction between
         # this launch and its fetch must not hand their memory to query-stream allocations)
         for enc in (compacts or {}).values():
             for x in _compact_buffers(enc):
-                x.record_stream(side)
+                _use_on(x, side)
         for x in g.buffers():
-            x.record_stream(side)
+            _use_on(x, side)
         with torch.cuda.stream(side):
             handle = g.launch(range_bounds(lo, lo_incl, hi, hi_incl), k.args.pack(values))
         return (_GraphPending(g, handle), None, None, None)
@@ -2130,6 +2165,15 @@ def _eval_scalar(e, agg_val, attr_val):
             return a * b
         return None if b == 0 else a / b
     raise Unsupported(f"result expression {type(e).__name__}")
+
+
+def _use_on(x, stream) -> None:
+    """``x.record_stream(stream)`` once per (tensor, stream): the caching allocator keeps the
+    streams a block was used on until the block is freed, and then waits for the work queued
+    on each of them by that time, so one record covers every later use on the stream."""
+    if getattr(x, "_hs_used_on", None) is not stream:
+        x.record_stream(stream)
+        x._hs_used_on = stream
 
 
 def _compact_buffers(enc) -> list:

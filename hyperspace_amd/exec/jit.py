@@ -109,6 +109,10 @@ MJ_KEY32 = os.environ.get("HS_JIT_MJ_KEY32", "1") == "1"  # 32-bit merge images 
 # 1.51 vs 1.38 ms at SF100 (profiles/mj_sweep_r3_key16.jsonl) - the kernel is bound by its
 # per-tile dependent round trips, not by the bytes it streams
 MJ_KEY16 = os.environ.get("HS_JIT_MJ_KEY16", "0") == "1"
+# run-keyed merge join: a left key with a run-length form (encoding.RunCompact) streams which
+# run each row belongs to (gmask / gruns, 0.19 bytes per row) instead of its 4-byte key; the
+# tile's run keys are matched against the staged right span once per run, not once per row
+MJ_RUNS = os.environ.get("HS_JIT_MJ_RUNS", "1") == "1"
 # cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
 MJ_EXP = os.environ.get("HS_JIT_MJ_EXP", "")
 # software-pipelined full tiles in the vectorized kernels (_vec_tiles)
@@ -408,7 +412,7 @@ class _Gen:
         """C type of the stored element (the code type for compact columns; grouped 16-bit
         codes, encoding.GroupedCompact, are unsigned)."""
         t, _, enc = self.cols[slot]
-        if enc and len(enc) > 2:
+        if enc and len(enc) > 2 and enc[2] == 64:
             return "unsigned short"
         return _CODE_T[enc[0]] if enc else _CTYPE[t]
 
@@ -985,6 +989,11 @@ def _fill_common(v: Dict[str, object], cols, preds, aggs, compacts=None) -> None
                 if gb is not None:
                     v[f"G{s}"] = gb.data_ptr()
                     v[f"W{s}"] = c.wide.data_ptr()
+                rk = getattr(c, "runkeys", None)
+                if rk is not None:
+                    v[f"RK{s}"] = rk.data_ptr()
+                    v[f"GM{s}"] = c.gmask.data_ptr()
+                    v[f"GR{s}"] = c.gruns.data_ptr()
     for k, p in preds:
         v[f"L{k}"] = p.ilit
         v[f"F{k}"] = p.flit
@@ -1303,7 +1312,7 @@ def merge_join_shape(p: NL.JoinParams, compacts=None, hk=None) -> tuple:
             p.key_is_float, MJ_ITEMS, MJ_LDS_KEYS, MJ_STEPS, BLOCK, WAVE_SYNC,
             _key32_frame(p, compacts) is not None, MJ_EXP, MJ_STAGE_UNROLL, MJ_DBUF, MJ_PREFETCH,
             MJ_BLOCK, MJ_EAGER, MJ_SPARSE, MJ_HASH_LANEMAJOR, MJ_RPF and not MJ_PREFETCH, MJ_KEY16,
-            hk.shape() if hk is not None else None)
+            hk.shape() if hk is not None else None, MJ_RUNS)
 
 
 def key_has_dups(col) -> bool:
@@ -1490,6 +1499,14 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
         args.add("q", "KLO", "long long")
         args.add("q", "KSP", "long long")
         args.add("q", "KOF", "long long")
+    lenc = cols[lk][2]
+    runs = k32 and lenc is not None and len(lenc) > 2 and lenc[2] == "runs"
+    if runs:
+        assert 64 % NI == 0 and T <= (1 << 16)
+        args.add("p", "TR", "const int*")
+        args.add("p", f"RK{lk}", "const int*")
+        args.add("p", f"GM{lk}", "const unsigned long long*")
+        args.add("p", f"GR{lk}", "const int*")
     lpreds = [(k, p.preds[k]) for k in range(p.nlp)]
     rpreds = [(k, p.preds[k]) for k in range(p.nlp, p.npreds)]
     ronly = [(k, q) for k, q in rpreds if all(x >= split for x in _slots_of(q))]
@@ -1499,7 +1516,7 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
     assert not (grouped and hk is not None)
     hslots = hk.slots if hk is not None else []
     mixed_left = [x for x in _pred_slots(mixed) if x < split]
-    first = list(dict.fromkeys([lk] + _pred_slots(lpreds) + mixed_left))
+    first = list(dict.fromkeys(([] if runs else [lk]) + _pred_slots(lpreds) + mixed_left))
     ronly_slots = [x for x in _pred_slots(ronly)]
     mixed_right = [x for x in _pred_slots(mixed) if x >= split]
     stage_slots = list(dict.fromkeys([rk] + ronly_slots))
@@ -1526,6 +1543,9 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
     NB = 2 if MJ_DBUF else 1  # noqa: N806
     b += [f"  __shared__ {KT} skeys_[{NB}][{LK + 1}]; __shared__ unsigned char spass_[{NB}][{LK}];",
           "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;"]
+    if runs:
+        # the tile's run keys (32-bit images), overwritten in place by each run's span match
+        b.append(f"  __shared__ unsigned lrk_[{T}];")
     if eager and grouped:
         b += _run_decls(aggs)
     if eager:
@@ -1546,7 +1566,7 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
         return (f"({{ const i64 d_ = (i64)({val}) - a.KLO; "
                 f"d_ < 0 ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }})")
 
-    k16 = k32 and cols[lk][2] is not None and len(cols[lk][2]) > 2
+    k16 = k32 and not runs and cols[lk][2] is not None and len(cols[lk][2]) > 2
     if k16:
         args.add("p", f"G{lk}", "const int*")
         args.add("p", f"W{lk}", "const int*")
@@ -1561,7 +1581,7 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
         return f"((unsigned)x{lk}v[{it}] + (unsigned)a.KOF)"
 
     U = max(1, MJ_STAGE_UNROLL)  # noqa: N806
-    rpf = MJ_RPF and not MJ_PREFETCH
+    rpf = MJ_RPF and not MJ_PREFETCH and not runs
     pf_slots = list(dict.fromkeys(stage_slots + rtail))
 
     def pf_issue(b: List[str], i2: str, ssv: str, sev: str) -> None:
@@ -1593,6 +1613,15 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
                       f"seNN = a.spans[4 * (t + 2) + 3]; }}"])
         else:
             b.append(f"{ind}const i64 ss = a.spans[4 * t + 2], se = a.spans[4 * t + 3];")
+        if runs:
+            # the tile's runs (hs_tile_runs), the thread's 64-row group run mask / base, and the
+            # run keys staged as merge images - loads issued with the right span's staging
+            b.extend([f"{ind}const int ra_ = a.TR[2 * t], nl_ = a.TR[2 * t + 1];",
+                      f"{ind}const i64 gi_ = (g0 < a.nrows ? g0 : a.nrows - 1) >> 6;",
+                      f"{ind}const unsigned long long gm_ = a.GM{lk}[gi_];",
+                      f"{ind}const int gr_ = a.GR{lk}[gi_];",
+                      f"{ind}for (int q_ = (int)threadIdx.x; q_ < nl_; q_ += {BLOCK}) "
+                      f"lrk_[q_] = (unsigned)a.RK{lk}[ra_ + q_] + (unsigned)a.KOF;"])
         b.extend([f"{ind}const int ns = (int)(se - ss);",
                   f"{ind}const bool staged = ns <= {LK};",
                   f"{ind}{KT}* const skeys = skeys_[{'(int)(t & 1)' if NB == 2 else '0'}];",
@@ -1662,54 +1691,58 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
         for it in range(NI):
             gi = _Gen(args, cols, split, (f"row{it}", f"row{it}"), approx, True)
             cond = _rename(gi.cnf(lpreds), allslots, it)
-            okl = f"n{lk}_{it}" if cols[lk][1] else "true"
+            okl = f"n{lk}_{it}" if cols[lk][1] and not runs else "true"
             b.append(f"{ind}{{ const bool kv = act{it} && {okl}; kvb |= kv ? {1 << it}u : 0u; "
                      f"mb |= (kv && {cond}) ? {1 << it}u : 0u; }}")
-            b.append(f"{ind}const {KT} k{it} = {limg(it)};")
+            if not runs:
+                b.append(f"{ind}const {KT} k{it} = {limg(it)};")
         b.append(f"{ind}{_block_sync(BLOCK)}")
+        if runs:
+            _runs_match(b, ind, g1, rk, rkv, rimg, NI, BLOCK)
 
         def bit(word: str, it: int) -> str:
             return f"(({word} >> {it}) & 1u)"
-        # (3) merge
-        b.append(f"{ind}{KT} kf = {KMAX};")
-        for it in reversed(range(NI)):
-            b.append(f"{ind}kf = {bit('mb', it)} ? k{it} : kf;")
-        b.append(f"{ind}unsigned mtb = 0u;")
-        for it in range(NI):
-            b.append(f"{ind}int jl{it} = 0;")
-        b.extend([f"{ind}bool slow = !staged;",
-                  f"{ind}int jw0 = 0;",
-                  f"{ind}if (staged) {{",
-                  f"{ind}  int lo = 0;",
-                  f"{ind}  for (int st = ns > 0 ? (1 << (31 - __builtin_clz(ns))) : 0; st > 0; st >>= 1) {{",
-                  f"{ind}    const int c = lo + st; const {KT} sv = skeys[c <= ns ? c - 1 : ns];",
-                  f"{ind}    lo = (c <= ns && sv < kf) ? c : lo; }}",
-                  f"{ind}  jw0 = lo; int jw = lo; {KT} v = skeys[jw];"])
-        for it in range(NI):
-            b.append(f"{ind}  {{ const {KT} ke = {bit('kvb', it)} ? k{it} : ({KT})0;")
-            for _ in range(MJ_STEPS):
-                b.append(f"{ind}    {{ const bool c = v < ke; jw += c ? 1 : 0; v = skeys[jw]; }}")
-            b.extend([f"{ind}    slow = slow || v < ke;",
-                      f"{ind}    mtb |= ({bit('mb', it)} && v == ke && jw < ns) ? {1 << it}u : 0u; "
-                      f"jl{it} = jw; }}"])
-        b.append(f"{ind}}}")
-        if "nowalk" in MJ_EXP:
-            b.append(f"{ind}mtb = mb; slow = false;")
-        b.extend([f"{ind}if (__any(slow)) {{",
-                  f"{ind}  if (slow) {{ int jw = jw0; mtb = 0u;"])
-        for it in range(NI):
-            b.extend([f"{ind}    if ({bit('mb', it)}) {{ bool hit;",
-                      f"{ind}      if (staged) {{ while (jw < ns && skeys[jw] < k{it}) ++jw;",
-                      f"{ind}        hit = jw < ns && skeys[jw] == k{it}; jl{it} = jw; }}",
-                      f"{ind}      else {{ i64 lo = ss, hi = se;",
-                      f"{ind}        while (lo < hi) {{ const i64 md = (lo + hi) >> 1; "
-                      f"const bool nv = {rkv.format(r='md')}; "
-                      f"if (nv || {rimg(g1.value(rk, 'md'))} < k{it}) lo = md + 1; else hi = md; }}",
-                      f"{ind}        hit = lo < se && !({rkv.format(r='lo')}) && "
-                      f"{rimg(g1.value(rk, 'lo'))} == k{it}; jl{it} = (int)(lo - ss); }}",
-                      f"{ind}      mtb |= hit ? {1 << it}u : 0u;",
-                      f"{ind}    }}"])
-        b.extend([f"{ind}  }}", f"{ind}}}"])
+        # (3) merge (the run-keyed form matched runs above instead)
+        if not runs:
+            b.append(f"{ind}{KT} kf = {KMAX};")
+            for it in reversed(range(NI)):
+                b.append(f"{ind}kf = {bit('mb', it)} ? k{it} : kf;")
+            b.append(f"{ind}unsigned mtb = 0u;")
+            for it in range(NI):
+                b.append(f"{ind}int jl{it} = 0;")
+            b.extend([f"{ind}bool slow = !staged;",
+                      f"{ind}int jw0 = 0;",
+                      f"{ind}if (staged) {{",
+                      f"{ind}  int lo = 0;",
+                      f"{ind}  for (int st = ns > 0 ? (1 << (31 - __builtin_clz(ns))) : 0; st > 0; st >>= 1) {{",
+                      f"{ind}    const int c = lo + st; const {KT} sv = skeys[c <= ns ? c - 1 : ns];",
+                      f"{ind}    lo = (c <= ns && sv < kf) ? c : lo; }}",
+                      f"{ind}  jw0 = lo; int jw = lo; {KT} v = skeys[jw];"])
+            for it in range(NI):
+                b.append(f"{ind}  {{ const {KT} ke = {bit('kvb', it)} ? k{it} : ({KT})0;")
+                for _ in range(MJ_STEPS):
+                    b.append(f"{ind}    {{ const bool c = v < ke; jw += c ? 1 : 0; v = skeys[jw]; }}")
+                b.extend([f"{ind}    slow = slow || v < ke;",
+                          f"{ind}    mtb |= ({bit('mb', it)} && v == ke && jw < ns) ? {1 << it}u : 0u; "
+                          f"jl{it} = jw; }}"])
+            b.append(f"{ind}}}")
+            if "nowalk" in MJ_EXP:
+                b.append(f"{ind}mtb = mb; slow = false;")
+            b.extend([f"{ind}if (__any(slow)) {{",
+                      f"{ind}  if (slow) {{ int jw = jw0; mtb = 0u;"])
+            for it in range(NI):
+                b.extend([f"{ind}    if ({bit('mb', it)}) {{ bool hit;",
+                          f"{ind}      if (staged) {{ while (jw < ns && skeys[jw] < k{it}) ++jw;",
+                          f"{ind}        hit = jw < ns && skeys[jw] == k{it}; jl{it} = jw; }}",
+                          f"{ind}      else {{ i64 lo = ss, hi = se;",
+                          f"{ind}        while (lo < hi) {{ const i64 md = (lo + hi) >> 1; "
+                          f"const bool nv = {rkv.format(r='md')}; "
+                          f"if (nv || {rimg(g1.value(rk, 'md'))} < k{it}) lo = md + 1; else hi = md; }}",
+                          f"{ind}        hit = lo < se && !({rkv.format(r='lo')}) && "
+                          f"{rimg(g1.value(rk, 'lo'))} == k{it}; jl{it} = (int)(lo - ss); }}",
+                          f"{ind}      mtb |= hit ? {1 << it}u : 0u;",
+                          f"{ind}    }}"])
+            b.extend([f"{ind}  }}", f"{ind}}}"])
 
         # (4) match rounds: right predicates at j, compacted aggregate tail; right tables with
         # duplicate keys (a.rdup) repeat for the next equal key until no lane has one
@@ -1761,6 +1794,10 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
             b.append(f"{i2}}}")
 
         one_round(ind)
+        if runs:    # unique right keys only (merge_join_agg): no duplicate-key rounds
+            if NB == 1:
+                b.append(f"{ind}{_block_sync(BLOCK)}")
+            return
         b.append(f"{ind}if (a.rdup) while (true) {{")
         i2 = ind + "  "
         for it in range(NI):
@@ -1824,6 +1861,59 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
            "\n".join(b) + "\n}\n")
     lds = (len(aggs) * p.num_groups * 32) if grouped else 0
     return Kernel(src, "hs_jit_merge_join_agg", args, lds, BLOCK)
+
+
+def _runs_match(b: List[str], ind: str, g1: "_Gen", rk: int, rkv: str, rimg, NI: int,
+                BLOCK: int) -> None:  # noqa: N803
+    """Run-keyed merge (MJ_RUNS): each thread matches a contiguous chunk of the tile's runs
+    against the staged right span - one LDS binary search for its first run, then a walk (an FK
+    join moves one right key per run) - and overwrites each run's key in ``lrk_`` with its span
+    index (~0u: no match).  Neighbouring lanes search neighbouring keys, so the search and the
+    walk touch neighbouring LDS words.  Each row then reads its run's entry: run = group base +
+    popcount of the group's run-start bits up to the row."""
+    rv = lambda r: rimg(g1.value(rk, r))  # noqa: E731
+    b.extend([f"{ind}{{ const int c_ = (nl_ + {BLOCK - 1}) / {BLOCK};",
+              f"{ind}  const int q0_ = (int)threadIdx.x * c_;",
+              f"{ind}  const int q1_ = q0_ + c_ < nl_ ? q0_ + c_ : nl_;",
+              f"{ind}  if (staged) {{",
+              f"{ind}    int j_ = 0;",
+              f"{ind}    if (q0_ < q1_) {{ const unsigned key_ = lrk_[q0_]; int lo = 0;",
+              f"{ind}      for (int st = ns > 0 ? (1 << (31 - __builtin_clz(ns))) : 0; st > 0; st >>= 1) {{",
+              f"{ind}        const int c = lo + st; lo = (c <= ns && skeys[c - 1] < key_) ? c : lo; }}",
+              f"{ind}      j_ = lo; }}",
+              f"{ind}    for (int q = q0_; q < q1_; ++q) {{",
+              f"{ind}      const unsigned key_ = lrk_[q];",
+              f"{ind}      if (skeys[j_] < key_) {{ ++j_;",
+              f"{ind}        if (skeys[j_] < key_) {{ int lo = j_ + 1, hi = ns;",
+              f"{ind}          while (lo < hi) {{ const int m = (lo + hi) >> 1; "
+              f"if (skeys[m] < key_) lo = m + 1; else hi = m; }}",
+              f"{ind}          j_ = lo; }} }}",
+              f"{ind}      lrk_[q] = (j_ < ns && skeys[j_] == key_) ? (unsigned)j_ : 0xFFFFFFFFu;",
+              f"{ind}    }}",
+              f"{ind}  }} else {{",
+              f"{ind}    for (int q = q0_; q < q1_; ++q) {{ const unsigned key_ = lrk_[q]; "
+              f"i64 lo = ss, hi = se;",
+              f"{ind}      while (lo < hi) {{ const i64 md = (lo + hi) >> 1; "
+              f"const bool nv = {rkv.format(r='md')}; "
+              f"if (nv || {rv('md')} < key_) lo = md + 1; else hi = md; }}",
+              f"{ind}      lrk_[q] = (lo < se && !({rkv.format(r='lo')}) && {rv('lo')} == key_) ? "
+              f"(unsigned)(lo - ss) : 0xFFFFFFFFu; }}",
+              f"{ind}  }}",
+              f"{ind}}}",
+              f"{ind}__syncthreads();",
+              f"{ind}unsigned mtb = 0u;"])
+    for it in range(NI):
+        b.append(f"{ind}int jl{it} = 0;")
+    b.extend([f"{ind}{{ const int sh_ = (int)(g0 & 63);",
+              f"{ind}  int rq_ = gr_ + (int)__popcll(gm_ & ((2ull << sh_) - 2ull)) - ra_;"])
+    for it in range(NI):
+        if it:
+            b.append(f"{ind}  rq_ += (int)((gm_ >> (sh_ + {it})) & 1ull);")
+        b.extend([f"{ind}  {{ const int ri_ = rq_ < 0 ? 0 : (rq_ < nl_ ? rq_ : (nl_ > 0 ? nl_ - 1 : 0));",
+                  f"{ind}    const unsigned jm_ = lrk_[ri_];",
+                  f"{ind}    const bool h_ = ((mb >> {it}) & 1u) && jm_ != 0xFFFFFFFFu;",
+                  f"{ind}    mtb |= h_ ? {1 << it}u : 0u; jl{it} = h_ ? (int)jm_ : 0; }}"])
+    b.append(f"{ind}}}")
 
 
 def _eager_tail(args, cols, split, approx, aggs, grouped, group_col, allslots, rtail, NI: int,
@@ -1934,15 +2024,20 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
     dev = rstart.device
     max_tiles = nrows // T + 2 * rstart.numel() + 2
-    if hk is None:
+    runs = None
+    if not rdup:
+        compacts, runs = _with_runs(p, compacts)
+    if hk is None and runs is None:
         compacts = _with_key16(p, compacts)
     tp, spans = _join_spans(p, rstart, rlen, rbucket, roff, max_tiles, T, cache_spans, align=NI)
     k = kernel_for(merge_join_shape(p, compacts, hk), lambda: gen_merge_join_agg(p, compacts, hk))
     grid = max(1, MJ_GRID * 256 // MJ_BLOCK)
+    tr = _tile_runs(tp, spans, rstart.numel(), runs, max_tiles, cache_spans) \
+        if runs is not None else None
     if hk is not None:
         v = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
              "spans": spans.data_ptr(), "R": rstart.numel(), "nrows": nrows, "rdup": int(rdup),
-             "psum": 0, "pcnt": 0, "pmin": 0, "pmax": 0}
+             "psum": 0, "pcnt": 0, "pmin": 0, "pmax": 0, "TR": tr.data_ptr() if tr is not None else 0}
         _fill_common(v, p.cols, [(k_, p.preds[k_]) for k_ in range(p.npreds)],
                      [p.aggs[i] for i in range(p.naggs)], compacts)
         frame = _key32_frame(p, compacts)
@@ -1956,7 +2051,8 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
     v = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
          "spans": spans.data_ptr(), "R": rstart.numel(), "nrows": nrows, "rdup": int(rdup),
          "psum": parts[0].data_ptr(), "pcnt": parts[1].data_ptr(), "pmin": parts[2].data_ptr(),
-         "pmax": parts[3].data_ptr(), "num_groups": p.num_groups, "group_base": p.group_base}
+         "pmax": parts[3].data_ptr(), "num_groups": p.num_groups, "group_base": p.group_base,
+         "TR": tr.data_ptr() if tr is not None else 0}
     _fill_common(v, p.cols, [(k_, p.preds[k_]) for k_ in range(p.npreds)],
                  [p.aggs[i] for i in range(p.naggs)], compacts)
     frame = _key32_frame(p, compacts)
@@ -1964,6 +2060,49 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
         v["KLO"], v["KSP"], v["KOF"] = frame
     k.launch(grid, v, NL.stream_ptr(), GA * 32 if p.group_col >= 0 else 0)
     return _final(parts, grid, GA, dev)
+
+
+def _with_runs(p: NL.JoinParams, compacts):
+    """(``compacts`` with the left key's run-length form, that form) when the run-keyed merge
+    join applies: a 32-bit-frame left key without nulls whose runs average at least
+    ``encoding.MIN_ROWS_PER_RUN`` rows; else (``compacts``, None).  Callers use it only for
+    unique right keys."""
+    from .encoding import GroupedCompact, key_runs
+    if not (MJ_RUNS and MJ_ITEMS and 64 % MJ_ITEMS == 0) or _key32_frame(p, compacts) is None:
+        return compacts, None
+    lk = p.lkey
+    c = compacts.get(lk)
+    if p.cols[lk].valid or c is None or isinstance(c, GroupedCompact):
+        return compacts, None
+    r = key_runs(c)
+    if r is None:
+        return compacts, None
+    out = dict(compacts)
+    out[lk] = r
+    return out, r
+
+
+# (spans id, run form id) -> (spans, run form, per-tile (first run, run count) int32 pairs)
+_TRUNS: Dict[tuple, tuple] = {}
+
+
+def _tile_runs(tp, spans, R: int, rc, max_tiles: int, cache: bool):
+    """Per merge-join tile: its first run and run count (csrc/kernels/key_runs.hip)."""
+    import torch
+    key = (id(spans), id(rc))
+    if cache:
+        hit = _TRUNS.get(key)
+        if hit is not None and hit[0] is spans and hit[1] is rc:
+            return hit[2]
+    out = torch.empty(2 * max(int(max_tiles), 1), dtype=torch.int32, device=spans.device)
+    NL.check(NL.lib().hs_tile_runs(tp.data_ptr(), R, spans.data_ptr(), rc.gmask.data_ptr(),
+                                   rc.gruns.data_ptr(), int(max_tiles), out.data_ptr(),
+                                   NL.stream_ptr()), "hs_tile_runs")
+    if cache:
+        if len(_TRUNS) >= 16:
+            _TRUNS.pop(next(iter(_TRUNS)))
+        _TRUNS[key] = (spans, rc, out)
+    return out
 
 
 def _with_key16(p: NL.JoinParams, compacts):

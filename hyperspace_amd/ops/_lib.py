@@ -200,6 +200,9 @@ def lib():
     _sig(L.hs_compact_probe, I, P, P, I64, I, I, P, P, P)
     _sig(L.hs_compact_probe_ws_elems, I64)
     _sig(L.hs_compact_encode, I, P, P, I64, I, I, I64, I64, I, P, P)
+    _sig(L.hs_key_runs_mask, I, P, I64, P, P, P)
+    _sig(L.hs_key_runs_fill, I, P, I64, P, P, P, P, P)
+    _sig(L.hs_tile_runs, I, P, I, P, P, P, I64, P, P)
     _sig(L.hs_snappy_max_compressed, I64, I64)
     _sig(L.hs_snappy_chunk_bytes, I)
     _sig(L.hs_snappy_compress, I, P, I, P, I64, P, P)

@@ -2,7 +2,8 @@
 ``repartition(numBuckets, indexedCols)``, ``CreateActionBase.scala:129-130``; Hybrid Scan's
 appended-row shuffle, ``RuleUtils.scala:519-578``) as ONE uneven all-to-all per batch of rows.
 
-Row ``i`` goes to rank ``bucket[i] % world`` (bucket ``b`` is owned by rank ``b % world``).  Every
+Row ``i`` goes to rank ``dest[i]``: its bucket's owner (``bucket[i] % world`` by default, else the
+session's owner map, ``parallel/placement.py``).  Every
 column of a batch — values, validity bytes, bucket ids — is packed by one kernel
 (``csrc/kernels/exchange.hip``) into a byte buffer with one contiguous segment per destination,
 so a batch costs one counts all-to-all (device tensors, no host round trip before it), one small
@@ -96,8 +97,12 @@ class RowExchange:
         return w if async_op else None
 
     # -- send side -------------------------------------------------------------------------------
-    def add(self, columns: Sequence, bucket) -> None:
-        """Exchange one batch: row ``i`` of every column goes to rank ``bucket[i] % world``."""
+    def add(self, columns: Sequence, bucket, dest=None) -> None:
+        """Exchange one batch: row ``i`` of every column goes to rank ``dest[i]`` (default
+        ``bucket[i] % world``).  The pack kernel routes by ``route % world``, so an owner-map
+        destination (< world) passes through it unchanged."""
+        if dest is not None:
+            bucket = dest.to(bucket.dtype) if dest.dtype != bucket.dtype else dest
         if len(columns) != len(self.dtypes):
             raise ValueError("RowExchange.add: column count mismatch")
         for c, dt in zip(columns, self.dtypes):

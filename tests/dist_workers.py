@@ -244,4 +244,59 @@ def spmd_stream_build(ctx, data_dir):
     return out
 
 
-SCENARIOS = {"spmd_stream_build": spmd_stream_build, "nccl_paths": nccl_paths, "collectives": collectives, "spmd_index": spmd_index, "spmd_gpu": spmd_gpu}
+def balanced_exchange(ctx, data_dir):
+    """Rows routed by a size-balanced owner map (parallel/placement.py) through the packed
+    all-to-all: every row lands on its bucket's owner under that map."""
+    import torch
+    from hyperspace_amd.parallel.exchange import RowExchange
+    from hyperspace_amd.parallel.placement import OwnerMap
+    r, w = ctx.rank, ctx.world
+    B = 16
+    weights = [1000.0] + [10.0] * (B - 1)             # bucket 0 is heavy
+    m = OwnerMap.balanced(weights, w)
+    g = torch.Generator().manual_seed(7 + r)
+    bucket = torch.randint(0, B, (300,), generator=g, dtype=torch.int32)
+    vals = torch.arange(300, dtype=torch.int64) + 10_000 * r
+    ex = RowExchange(ctx, [torch.int64, torch.int32])
+    ex.add([vals, bucket], bucket, m.dest(bucket))
+    rv, rb = ex.finish()
+    return {"owners": m.owners.tolist(), "recv_buckets": rb.tolist(), "recv": rv.tolist(),
+            "sent": vals.tolist(), "sent_b": bucket.tolist()}
+
+
+def spmd_skew(ctx, data_dir):
+    """Device executor over a skewed join key (ranks share cuda:0 over gloo): the same indexes
+    and queries under the modulo and the size-balanced bucket placement give identical results,
+    and the balanced map gives the heavy bucket a rank of its own."""
+    from hyperspace_amd import Hyperspace, IndexConfig, col, count, sum_
+    s = _session(ctx, data_dir, **{"spark.hyperspace.mi.execution.device": "gpu",
+                                   "spark.hyperspace.index.numBuckets": "8",
+                                   "spark.hyperspace.system.path":
+                                       os.path.join(data_dir, "indexes_skew")})
+    hs = Hyperspace(s)
+    t1 = s.read.parquet(os.path.join(data_dir, "s1"))
+    t2 = s.read.parquet(os.path.join(data_dir, "s2"))
+    hs.createIndex(t1, IndexConfig("k1", ["k"], ["v"]))
+    hs.createIndex(t2, IndexConfig("k2", ["k"], ["w"]))
+    Hyperspace.enable(s)
+    out = {"paths": []}
+    for mode in ("modulo", "balanced"):
+        s.conf.set("spark.hyperspace.mi.bucketPlacement", mode)
+        j = t1.join(t2, t1["k"] == t2["k"])
+        qs = {"agg": j.groupBy(t2["w"]).agg(sum_(col("v")).alias("sv"), count("*").alias("n")),
+              "rows": j.filter(col("v") % 97 == 0).select(t1["k"], t1["v"], t2["w"]),
+              "filter": t1.filter(col("k") < 40).groupBy(t1["k"]).agg(count("*").alias("n"))}
+        res = {}
+        for name, df in qs.items():
+            res[name] = sorted((tuple(r.values()) for r in df.to_arrow().to_pylist()), key=repr)
+            out["paths"].append(s.backend().last_path)
+        out[mode] = res
+        maps = s.__dict__.get("_hs_owner_maps", {})
+        m = maps.get((8, ctx.world, mode))
+        out[mode + "_owners"] = m.owners.tolist() if m is not None else None
+    ctx.barrier()
+    return out
+
+
+SCENARIOS = {"spmd_stream_build": spmd_stream_build, "nccl_paths": nccl_paths, "collectives": collectives, "spmd_index": spmd_index, "spmd_gpu": spmd_gpu,
+             "balanced_exchange": balanced_exchange, "spmd_skew": spmd_skew}

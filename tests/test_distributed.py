@@ -288,3 +288,61 @@ def test_multi_rank_streaming_build_is_byte_identical(tmp_path, device):
     assert sorted(one) == sorted(many) and len(one) == 16
     for b in one:
         assert one[b] == many[b], f"bucket {b} differs"
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_balanced_owner_map_routes_rows(tmp_path, world):
+    """The packed all-to-all routes every row to its bucket's owner under a size-balanced map
+    (parallel/placement.py): the heavy bucket's owner holds no other bucket."""
+    res = _spawn("balanced_exchange", tmp_path, str(tmp_path), world=world)
+    owners = res[0]["owners"]
+    assert all(d["owners"] == owners for d in res)
+    heavy = owners[0]
+    assert owners.count(heavy) == 1
+    for r, d in enumerate(res):
+        assert all(owners[b] == r for b in d["recv_buckets"])
+        expect = []
+        for src in res:
+            expect += [v for v, b in zip(src["sent"], src["sent_b"]) if owners[b] == r]
+        assert d["recv"] == expect
+
+
+@pytest.fixture
+def skew_data(tmp_path):
+    rng = np.random.default_rng(9)
+    data = tmp_path / "data"
+    k1 = np.concatenate([np.full(6000, 7, np.int64), rng.integers(0, 400, 4000)])
+    t1 = pa.table({"k": k1, "v": np.arange(len(k1), dtype=np.int64)})
+    k2 = np.arange(400, dtype=np.int64)
+    t2 = pa.table({"k": k2, "w": (k2 % 6).astype(np.int32)})
+    for name, t, parts in (("s1", t1, 4), ("s2", t2, 2)):
+        os.makedirs(data / name)
+        step = (t.num_rows + parts - 1) // parts
+        for i in range(parts):
+            pq.write_table(t.slice(i * step, step), data / name / f"part-{i}.parquet")
+    return data, t1, t2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_balanced_placement_matches_modulo_on_skewed_key(tmp_path, skew_data, device, world):
+    """Ranks share cuda:0 (gloo): a skewed join key (60% of the rows on one key) gives one
+    heavy bucket; the size-balanced placement gives it a rank of its own, and every query
+    (co-located join aggregate, join rows, filter) returns exactly the modulo placement's result
+    and the pyarrow oracle's."""
+    data, t1, t2 = skew_data
+    res = _spawn("spmd_skew", tmp_path, str(data), timeout=600.0, world=world)
+    j = t1.join(t2, "k", join_type="inner")
+    g = j.group_by("w").aggregate([("v", "sum"), ("v", "count")])
+    exp = sorted(zip(g.column("w").to_pylist(), g.column("v_sum").to_pylist(),
+                     g.column("v_count").to_pylist()))
+    for d in res:
+        assert d["paths"] == ["native"] * 6, d["paths"]
+        assert d["modulo"] == d["balanced"]
+        assert [tuple(x) for x in d["balanced"]["agg"]] == exp
+        assert d["modulo_owners"] == [b % world for b in range(8)]
+        ow = d["balanced_owners"]
+        assert ow != d["modulo_owners"]
+        from hyperspace_amd.utils import murmur3
+        heavy = int(murmur3.bucket_ids([pa.array([7], pa.int64())], 8)[0])
+        assert ow.count(ow[heavy]) == 1          # the hot key's bucket alone on its rank

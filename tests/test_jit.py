@@ -186,6 +186,17 @@ def test_generated_sources_compile_with_compact_columns(rt, tmp_path):
     assert "const unsigned short* c0" in k16.src and "a.G0[" in k16.src   # 16-bit left keys
     assert jit.merge_join_shape(_q3_params(), c16) != jit.merge_join_shape(_q3_params(), c32)
     ks.append(k16)
+    import torch
+    from hyperspace_amd.exec.encoding import RunCompact
+    cr = dict(c32)
+    cr[0] = RunCompact(c32[0], torch.zeros(1, dtype=torch.int32), torch.zeros(1, dtype=torch.int64),
+                       torch.zeros(1, dtype=torch.int32))
+    kr = jit.gen_merge_join_agg(_q3_params(), cr)
+    # run-keyed merge join: per-row run lookups, no per-row key stream of slot 0
+    assert "a.GM0[" in kr.src and "a.RK0[" in kr.src and "lrk_[" in kr.src
+    assert "vload<int, 8>(a.c0" not in kr.src and "a.rdup" not in kr.src
+    assert jit.merge_join_shape(_q3_params(), cr) != jit.merge_join_shape(_q3_params(), c32)
+    ks.append(kr)
     assert "st9_s" in ks[0].src          # phase 2 staged through LDS
     assert "a.rbm" in ks[1].src and "a.c9" not in ks[1].src   # phase 2 = bitmap tests
     for k in ks:
@@ -546,14 +557,15 @@ def test_merge_join_key16_matches_oracle(device):
         rbk = torch.arange(B, dtype=torch.int32, device=device)
         roff_t = torch.from_numpy(roff).to(device)
         res = {}
+        runs = jit.MJ_RUNS
         for k16 in (True, False):
-            jit.MJ_KEY16 = k16
+            jit.MJ_KEY16, jit.MJ_RUNS = k16, False
             try:
                 res[k16] = [t.cpu().numpy() for t in
                             jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, comp, nrows=len(lk),
                                                rdup=False)]
             finally:
-                jit.MJ_KEY16 = key16
+                jit.MJ_KEY16, jit.MJ_RUNS = key16, runs
         for r in res.values():
             assert r[1][0] == int(exp.sum())
             assert abs(r[0][0] - float(lprice[exp].sum())) <= 1e-9 * max(1.0, float(lprice[exp].sum()))
@@ -727,3 +739,83 @@ def test_grouped16_round_trips_sorted_keys():
     assert grouped16(c) is g and c.nbytes() == codes.numel() * 4 + g.nbytes()
     spread = torch.from_numpy(np.array([0, 1 << 17] * 64, dtype=np.int32))
     assert grouped16(Compact(spread, 4, 0, None, NL.I64, 0, 1 << 17)) is None
+
+
+@pytest.mark.gpu
+def test_merge_join_runs_matches_oracle(device):
+    """Run-keyed merge join (MJ_RUNS, encoding.RunCompact): TPC-H-like unique right keys, 1-7
+    left rows per key, right keys with no left rows and left keys with no right row, a grouped
+    aggregate over a right column; full buckets and unaligned sub-ranges, staged (2048 LDS keys)
+    and HBM-searched (32) spans; equals the per-row-key kernel and numpy.  The device run form
+    equals the PyTorch reference."""
+    import torch
+    from hyperspace_amd.exec import jit
+    from hyperspace_amd.exec.encoding import encode, key_runs, runs_torch
+    rng = np.random.default_rng(11)
+    B = 8
+    ok = np.arange(1, 120_001, dtype=np.int64) * 4 + (1 << 20)
+    per = rng.integers(1, 8, len(ok))
+    per[rng.random(len(ok)) < 0.05] = 0                         # orders without lines
+    lk = np.repeat(ok, per)
+    orphan = rng.integers(1, 120_001, 3000) * 4 + (1 << 20) + 1  # lines without an order
+    lk = np.concatenate([lk, orphan])
+    rk = ok
+    rb = murmur3.bucket_ids([pa.array(rk)], B)
+    lb = murmur3.bucket_ids([pa.array(lk)], B)
+    ro = np.lexsort((rk, rb)); rk, rb = rk[ro], rb[ro]
+    lo_ = np.lexsort((lk, lb)); lk, lb = lk[lo_], lb[lo_]
+    loff = np.searchsorted(lb, np.arange(B + 1)).astype(np.int64)
+    roff = np.searchsorted(rb, np.arange(B + 1)).astype(np.int64)
+    ldate = rng.integers(0, 1000, len(lk)).astype(np.int32)
+    lprice = np.round(rng.random(len(lk)) * 1000, 2)
+    rdate = rng.integers(0, 1000, len(rk)).astype(np.int32)
+    rprio = rng.integers(0, 3, len(rk)).astype(np.int32)
+    p = NL.JoinParams()
+    cl = [_col(pa.array(lk), device), _col(pa.array(ldate), device), _col(pa.array(lprice), device)]
+    cr = [_col(pa.array(rk), device), _col(pa.array(rdate), device), _col(pa.array(rprio), device)]
+    for i, c in enumerate(cl):
+        p.cols[i] = c.desc()
+    for i, c in enumerate(cr):
+        p.cols[8 + i] = c.desc()
+    p.preds[0] = NL.Pred(NL.PK_INT_LIT, NL.OP_GT, 1, 0, 0, 0, 300, 0.0, None)
+    p.preds[1] = NL.Pred(NL.PK_INT_LIT, NL.OP_LT, 9, 0, 1, 0, 500, 0.0, None)
+    p.nlp, p.npreds = 1, 2
+    p.aggs[0] = _agg(NL.AK_SUM, [(2, 0.0, 1.0)])
+    p.aggs[1] = _agg(NL.AK_COUNT_STAR)
+    p.naggs, p.lkey, p.rkey, p.key_is_float = 2, 0, 8, 0
+    p.group_col, p.num_groups, p.group_base = 10, 3, 0
+    rmap = {k: (d < 500, g) for k, d, g in zip(rk.tolist(), rdate.tolist(), rprio.tolist())}
+    allc = dict(enumerate(cl))
+    allc.update({8 + i: c for i, c in enumerate(cr)})
+    comp = {s: e for s, e in ((s, encode(c)) for s, c in allc.items()) if e is not None}
+    rc = key_runs(comp[0])
+    assert rc is not None and rc.nruns < len(lk) / 2
+    ref = runs_torch(comp[0].codes.cpu())
+    for a, b_ in zip((rc.runkeys, rc.gmask, rc.gruns), ref):
+        assert torch.equal(a.cpu(), b_)
+    lds_keys, runs = jit.MJ_LDS_KEYS, jit.MJ_RUNS
+    try:
+        for starts, lens in ((loff[:-1], loff[1:] - loff[:-1]),
+                             (loff[:-1] + 5, loff[1:] - loff[:-1] - 9)):
+            exp_s, exp_c = np.zeros(3), np.zeros(3, np.int64)
+            for b in range(B):
+                for i in range(starts[b], starts[b] + lens[b]):
+                    m = rmap.get(int(lk[i]))
+                    if m is not None and m[0] and ldate[i] > 300:
+                        exp_s[m[1]] += lprice[i]
+                        exp_c[m[1]] += 1
+            rstart = torch.from_numpy(starts.astype(np.int64)).to(device)
+            rlen = torch.from_numpy(lens.astype(np.int64)).to(device)
+            rbk = torch.arange(B, dtype=torch.int32, device=device)
+            roff_t = torch.from_numpy(roff).to(device)
+            for keys in (lds_keys, 32):
+                for use_runs in (True, False):
+                    jit.MJ_LDS_KEYS, jit.MJ_RUNS = keys, use_runs
+                    got = [t.cpu().numpy() for t in
+                           jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, comp, nrows=len(lk),
+                                              rdup=False)]
+                    s_, c_ = got[0].reshape(3, 2)[:, 0], got[1].reshape(3, 2)[:, 1]
+                    assert (c_ == exp_c).all(), (keys, use_runs, c_, exp_c)
+                    assert np.allclose(s_, exp_s, rtol=1e-12), (keys, use_runs)
+    finally:
+        jit.MJ_LDS_KEYS, jit.MJ_RUNS = lds_keys, runs

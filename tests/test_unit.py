@@ -380,3 +380,31 @@ def test_float_to_int_cast_oracle_matches_spark():
     assert _float_to_int(v, pa.int8()).to_pylist() == [0, -1, 0, -1, 0, 2, -2, 112, None]
     assert _float_to_int(v, pa.int64()).to_pylist() == \
         [0, 2**63 - 1, -2**63, 3000000000, -3000000000, 2, -2, 70000, None]
+
+
+def test_owner_map_lpt_and_sticky_session_map():
+    """parallel/placement.py: equal weights reproduce b % W; a heavy bucket gets a rank of its
+    own; the session keeps the first map it decides per (bucket count, world, mode)."""
+    import types
+    import numpy as np
+    from hyperspace_amd.parallel.placement import OwnerMap, lpt, session_map
+    for w in (1, 2, 3, 8):
+        assert lpt([5.0] * 200, w).tolist() == [b % w for b in range(200)]
+        assert OwnerMap.modulo(200, w).is_modulo()
+    wts = [1.0] * 16
+    wts[5] = 100.0
+    m = OwnerMap.balanced(wts, 4)
+    assert m.owners.tolist().count(m.owner(5)) == 1
+    loads = m.loads(wts)
+    assert loads.max() == 100.0 and loads.min() >= 5.0
+    assert sorted(b for r in range(4) for b in m.owned(r)) == list(range(16))
+    import torch
+    bt = torch.tensor([5, 0, 15, 5], dtype=torch.int32)
+    assert m.dest(bt).tolist() == [m.owner(5), m.owner(0), m.owner(15), m.owner(5)]
+    sess = types.SimpleNamespace(conf={})
+    first = session_map(sess, 16, 4, wts)
+    assert session_map(sess, 16, 4, [1.0] * 16) is first          # sticky
+    assert session_map(sess, 16, 1, wts).owners.tolist() == [0] * 16
+    sess.conf = {"spark.hyperspace.mi.bucketPlacement": "modulo"}
+    assert session_map(sess, 16, 4, wts).is_modulo()
+    assert np.array_equal(first.owners, m.owners)
