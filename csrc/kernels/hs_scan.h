@@ -86,7 +86,7 @@ __device__ __forceinline__ bool hs_eval_pred(const Pred& p, const ColDesc* cols,
       return p.op == OP_EQ ? found : !found;
     }
     case PK_BITMAP: {
-      const int64_t v = load_i64(c, row);
+      const int64_t v = load_i64(c, row) - p.ilit;   // bit (value - base)
       bool found = false;
       if (v >= 0 && v < (int64_t)p.set_len * 64)
         found = (((const uint64_t*)p.set)[v >> 6] >> (v & 63)) & 1ull;

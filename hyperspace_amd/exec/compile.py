@@ -42,7 +42,7 @@ class Leaf:
         self.value, self.values = value, values
 
     def negate(self) -> "Leaf":
-        if self.kind in ("cmp_lit", "cmp_col", "in"):
+        if self.kind in ("cmp_lit", "cmp_col", "in", "bitmap"):
             return Leaf(self.kind, _NEG[self.op], self.attr, self.attr2, self.value, self.values)
         if self.kind == "isnull":
             return Leaf("notnull", 0, self.attr)
@@ -98,7 +98,36 @@ def _to_nnf(e: E.Expression, negate: bool = False):
     return leaf.negate() if negate else leaf
 
 
+class KeyBitmap(E.Expression):
+    """Executor-internal predicate ``attr in <device key bitmap>``: bit (value - base) of
+    ``words`` (int64 tensor, ``nbits`` bits) is set.  Built from a semi-join's build-side keys
+    (GpuBackend._semi_join_agg) and bound as a PK_BITMAP predicate of the probe scan."""
+
+    def __init__(self, attr: E.Attribute, words, base: int, nbits: int):
+        self.attr, self.words, self.base, self.nbits = attr, words, int(base), int(nbits)
+        self.children = (attr,)
+
+    @property
+    def data_type(self):
+        return pa.bool_()
+
+    @property
+    def nullable(self) -> bool:
+        return False
+
+    def with_children(self, children):
+        return KeyBitmap(children[0], self.words, self.base, self.nbits)
+
+    def canonical_key(self):
+        return ("KeyBitmap", self.attr.canonical_key(), id(self.words), self.base, self.nbits)
+
+    def sql(self) -> str:
+        return f"{self.attr.sql()} IN key_bitmap[{self.base}, {self.base + self.nbits})"
+
+
 def _leaf(e: E.Expression) -> Leaf:
+    if isinstance(e, KeyBitmap):
+        return Leaf("bitmap", NL.OP_EQ, e.attr, value=e)
     if isinstance(e, E.Literal) and isinstance(e.value, bool):
         return Leaf("const", 0, None, value=e.value)
     if type(e) in _OPS:
@@ -250,6 +279,13 @@ def bind(clauses: List[List[Leaf]], col_info: Callable[[E.Attribute], ColumnInfo
                                            float(v), None))
                 else:
                     b.preds.append(NL.Pred(NL.PK_INT_LIT, leaf.op, info.slot, 0, group, 0, int(v), 0.0, None))
+            elif leaf.kind == "bitmap":
+                kb = leaf.value
+                if info.dictionary is not None or info.is_float:
+                    raise Unsupported("key bitmap on a non-integer column")
+                b.buffers.append(kb.words)
+                b.preds.append(NL.Pred(NL.PK_BITMAP, leaf.op, info.slot, 0, group,
+                                       kb.words.numel(), kb.base, 0.0, kb.words.data_ptr()))
             elif leaf.kind == "in":
                 vals = [v for v in leaf.values if v is not None]
                 if info.dictionary is not None:

@@ -100,6 +100,9 @@ class DRel:
 
 class GpuBackend:
     name = "gpu"
+    # QueryExecution may submit a plan-cache entry's own plan with a query's literals bound in
+    # place (plan/plan_cache.py): everything literal-dependent is read during collect_async
+    supports_bound_plans = True
 
     def __init__(self, session):
         import torch
@@ -1255,7 +1258,12 @@ class GpuBackend:
         while isinstance(node, X.ProjectExec) and all(isinstance(e, E.Attribute) for e in node.project_list):
             node = node.child
         self._groups_agreed = False
+        res = None
         if isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner":
+            res = self._semi_join_agg(node, fns, group)
+        if res is not None:
+            pass
+        elif isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner":
             res = self._join_agg(node, fns, group)
         else:
             res = self._scan_agg(self._rel(child), fns, group)
@@ -1490,7 +1498,7 @@ class GpuBackend:
             with stage("scan.graph"):
                 out = self._scan_agg_graph(r, p, spec,
                                            p.naggs * (p.num_groups if p.group_col >= 0 else 1),
-                                           descs)
+                                           descs, keep=bound.buffers)
         else:
             with stage("scan.agg_kernel"):
                 tp = K.ranges_to_tiles(rlen)
@@ -1510,7 +1518,7 @@ class GpuBackend:
         conf = self.session.conf
         return HyperspaceConf.codegen_enabled(conf) and HyperspaceConf.hipgraph_enabled(conf)
 
-    def _scan_agg_graph(self, r: DRel, p: NL.ScanParams, spec, GA: int, descs=None):
+    def _scan_agg_graph(self, r: DRel, p: NL.ScanParams, spec, GA: int, descs=None, keep=()):
         kc, lo, lo_incl, hi, hi_incl, _ = spec
         t = r.table
         nb = t.num_buckets
@@ -1558,6 +1566,8 @@ class GpuBackend:
                 _use_on(x, side)
         for x in g.buffers():
             _use_on(x, side)
+        for x in keep:      # per-query predicate buffers (IN sets, key bitmaps)
+            _use_on(x, side)
         with torch.cuda.stream(side):
             handle = g.launch(range_bounds(lo, lo_incl, hi, hi_incl), k.args.pack(values))
         return (_GraphPending(g, handle), None, None, None)
@@ -1595,6 +1605,107 @@ class GpuBackend:
         z = torch.zeros(G * A, dtype=torch.float64, device=self.device)
         zc = torch.zeros(G * A, dtype=torch.int64, device=self.device)
         return z, zc, torch.full_like(z, float("inf")), torch.full_like(z, float("-inf"))
+
+    # ------------------------------------------------------------------------------------------
+    # Semi-join through a key-domain bitmap (csrc/kernels/key_bitmap.hip)
+    # ------------------------------------------------------------------------------------------
+    def _semi_join_agg(self, node: X.SortMergeJoinExec, fns, group):
+        """An inner equi-join whose aggregate reads only one side (the probe) and whose other
+        side (the build) needs an Exchange - it is not co-partitioned with the probe, e.g. the
+        output of another join (TPC-H Q3: (customer x orders) x lineitem; JoinIndexRule cannot
+        rewrite a join whose side is a join, JoinIndexRule.scala:100-105,149-150) - runs as a
+        scan of the probe side filtered by a bitmap of the build keys, when those keys are
+        unique (then the join matches each probe row at most once and multiplies nothing).
+        That replaces the Exchange + Sort of both sides and the merge join.  None when the
+        shape does not qualify (or the build keys repeat): the general join runs instead."""
+        if node.condition is not None or len(node.left_keys) != 1:
+            return None
+        conf = self.session.conf
+        if not HyperspaceConf.codegen_enabled(conf) or \
+                str(conf.get("spark.hyperspace.mi.semiJoinBitmap.enabled", "true")).lower() != "true":
+            return None
+        failed = self.__dict__.setdefault("_semi_failed", {})
+        if failed.get(id(node)) is node:
+            return None
+        need = set()
+        for fn in fns:
+            need.update(a.expr_id for a in fn.references())
+        if group is not None:
+            need.add(group.expr_id)
+        lk, rk = node.left_keys[0], node.right_keys[0]
+        if not (isinstance(lk, E.Attribute) and isinstance(rk, E.Attribute)):
+            return None
+        sides = []
+        for probe, build, pk, bk in ((node.right, node.left, rk, lk), (node.left, node.right, lk, rk)):
+            if not need <= {a.expr_id for a in probe.output}:
+                continue
+            binner = _strip_exchange(build)
+            if binner is None:
+                continue
+            sides.append((_plan_bytes(build), probe, binner, pk, bk))
+        if not sides:
+            return None
+        _, probe, binner, pk, bk = min(sides, key=lambda x: x[0])
+        if not all(pa.types.is_integer(a.data_type) for a in (pk, bk)):
+            return None
+        pinner = _strip_exchange(probe) or probe
+        with stage("semi.build"):
+            brel = self._rel(binner)
+            if brel.parts:
+                return None
+            keys = self._materialize(brel, [bk])[bk.expr_id]
+            bm = self._semi_bitmap(keys)
+        if bm is None:
+            if len(failed) > 256:
+                failed.clear()
+            failed[id(node)] = node
+            return None
+        words, lo, nbits = bm
+        prel = self._rel(pinner)
+        if prel.parts:
+            return None
+        cond = CP.KeyBitmap(pk, words, lo, nbits)
+        self.last_semi_join = {"build_keys": int(keys.data.numel()), "bitmap_bits": nbits}
+        with stage("semi.probe"):
+            return self._scan_agg(prel.copy(conds=prel.conds + [cond]), fns, group)
+
+    def _semi_bitmap(self, keys: DeviceColumn):
+        """(words, lo, nbits) of the build keys over every rank's keys, or None when they are
+        not unique, not integer, empty everywhere or span more than K.MAX_BITMAP_BITS."""
+        import torch
+        d = self._dist()
+        dom = K.key_domain(keys)
+        if d is None or d.world == 1:
+            if dom is None:
+                return None
+            lo, hi, n = dom
+            if hi - lo + 1 > K.MAX_BITMAP_BITS:
+                return None
+            words, dup = K.key_bitmap(keys, lo, hi - lo + 1)
+            return None if dup else (words, lo, hi - lo + 1)
+        # every rank: the global domain (one all-reduce), its own keys' bits, then the OR of all
+        # ranks' bitmaps (all-gather) and a uniqueness check by population count
+        big = 1 << 62
+        lo, hi, n = dom if dom is not None else (big, -big, 0)
+        t = torch.tensor([lo, -hi, 0], dtype=torch.int64, device=self.device)
+        t2 = torch.tensor([n], dtype=torch.int64, device=self.device)
+        d.all_reduce(t, "min")
+        d.all_reduce(t2, "sum")
+        glo, ghi, gn = int(t[0].item()), -int(t[1].item()), int(t2[0].item())
+        if gn == 0 or ghi - glo + 1 > K.MAX_BITMAP_BITS:
+            return None
+        nbits = ghi - glo + 1
+        if dom is not None:
+            words, _ = K.key_bitmap(keys, glo, nbits)
+        else:
+            words = torch.zeros((nbits + 63) // 64, dtype=torch.int64, device=self.device)
+        allw = d.all_gather_tensor(words).view(d.world, -1)
+        words = allw[0].clone()
+        for r in range(1, d.world):
+            words.bitwise_or_(allw[r])
+        if K.bitmap_popcount(words) != gn:
+            return None
+        return words, glo, nbits
 
     def _join_agg(self, node: X.SortMergeJoinExec, fns, group):
         """Fused join + aggregate.  A side that is a BucketUnion (Hybrid Scan: index buckets plus
@@ -2167,6 +2278,28 @@ def _eval_scalar(e, agg_val, attr_val):
     raise Unsupported(f"result expression {type(e).__name__}")
 
 
+def _strip_exchange(p):
+    """The child below a [Sort(local) <-] hash Exchange (a join side Spark would shuffle), or
+    None when ``p`` does not start with one."""
+    if isinstance(p, X.SortExec) and not p.global_sort:
+        p = p.child
+    if isinstance(p, X.ShuffleExchangeExec) and isinstance(p.partitioning, X.HashPartitioning):
+        return p.child
+    return None
+
+
+def _plan_bytes(p) -> int:
+    """Bytes of the files under a physical plan's scans (the build side of a semi-join is the
+    side with fewer)."""
+    n = 0
+    for s in p.collect(lambda x: isinstance(x, X.FileSourceScanExec)):
+        try:
+            n += sum(int(f.length) for f in s.relation.location.all_files())
+        except Exception:  # noqa: BLE001 - a relation without a file listing counts 0
+            pass
+    return n
+
+
 def _use_on(x, stream) -> None:
     """``x.record_stream(stream)`` once per (tensor, stream): the caching allocator keeps the
     streams a block was used on until the block is freed, and then waits for the work queued
@@ -2206,6 +2339,7 @@ class QueryFuture:
 
     def __init__(self, backend, plan, finish, path: str, reason, t0: float):
         self.backend, self.plan = backend, plan
+        self.plan_fn = None         # builds the plan when ``plan`` was a bound cached plan
         self._finish = finish
         self.path, self.reason = path, reason
         self._t0 = t0
@@ -2217,7 +2351,8 @@ class QueryFuture:
             try:
                 self._value = self._finish()
             except Unsupported as e:   # e.g. a result expression the device path cannot finish
-                f = self.backend._fallback(self.plan, e, self._t0)
+                plan = self.plan if self.plan is not None else self.plan_fn()
+                f = self.backend._fallback(plan, e, self._t0)
                 self._value, self.path, self.reason = f.result(), f.path, f.reason
                 self.backend.last_path, self.backend.fallback_reason = self.path, self.reason
             self._done = True

@@ -113,6 +113,8 @@ MJ_KEY16 = os.environ.get("HS_JIT_MJ_KEY16", "0") == "1"
 # run each row belongs to (gmask / gruns, 0.19 bytes per row) instead of its 4-byte key; the
 # tile's run keys are matched against the staged right span once per run, not once per row
 MJ_RUNS = os.environ.get("HS_JIT_MJ_RUNS", "1") == "1"
+MJ_RUNS_ITEMS = int(os.environ.get("HS_JIT_MJ_RUNS_ITEMS", "16"))
+MJ_RUNS_PREFETCH = os.environ.get("HS_JIT_MJ_RUNS_PREFETCH", "0") == "1"
 # cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
 MJ_EXP = os.environ.get("HS_JIT_MJ_EXP", "")
 # software-pipelined full tiles in the vectorized kernels (_vec_tiles)
@@ -482,10 +484,12 @@ class _Gen:
             neg = "" if op == NL.OP_EQ else "!"
             return f"({self.ok(c)} && {neg}in_set({sp}, (int){sn}, (i64)x{c}))"
         if kind == NL.PK_BITMAP:
+            # bit (value - base) of a key-domain bitmap (base = ilit: a semi-join's build keys)
             sp = self.a.add("p", f"S{k}", "const unsigned long long*")
             sn = self.a.add("q", f"N{k}", "long long")
+            base = self.a.add("q", f"L{k}", "long long")
             neg = "" if op == NL.OP_EQ else "!"
-            return f"({self.ok(c)} && {neg}bit_test({sp}, {sn} * 64, (i64)x{c}))"
+            return f"({self.ok(c)} && {neg}bit_test({sp}, {sn} * 64, (i64)x{c} - {base}))"
         raise ValueError(f"pred kind {kind}")
 
     def cnf(self, preds: List[Tuple[int, NL.Pred]]) -> str:
@@ -1312,7 +1316,7 @@ def merge_join_shape(p: NL.JoinParams, compacts=None, hk=None) -> tuple:
             p.key_is_float, MJ_ITEMS, MJ_LDS_KEYS, MJ_STEPS, BLOCK, WAVE_SYNC,
             _key32_frame(p, compacts) is not None, MJ_EXP, MJ_STAGE_UNROLL, MJ_DBUF, MJ_PREFETCH,
             MJ_BLOCK, MJ_EAGER, MJ_SPARSE, MJ_HASH_LANEMAJOR, MJ_RPF and not MJ_PREFETCH, MJ_KEY16,
-            hk.shape() if hk is not None else None, MJ_RUNS)
+            hk.shape() if hk is not None else None, MJ_RUNS, MJ_RUNS_ITEMS, MJ_RUNS_PREFETCH)
 
 
 def key_has_dups(col) -> bool:
@@ -1455,6 +1459,17 @@ def _deferred_drain(args, cols, split, approx, aggs, grouped, group_col, allslot
     return b
 
 
+def _mj_items(runs: bool) -> int:
+    """Rows per thread of the vectorized merge join: the run-keyed form does little work per row
+    and takes longer tiles (MJ_RUNS_ITEMS); ``profiles/mj_micro_r4*.jsonl``."""
+    return MJ_RUNS_ITEMS if runs and MJ_RUNS_ITEMS else MJ_ITEMS
+
+
+def _is_runs(compacts, slot: int) -> bool:
+    c = (compacts or {}).get(slot)
+    return c is not None and c.signature()[2:3] == ("runs",)
+
+
 def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
     """Co-located sort-merge join + aggregate, re-matching keys every query (no cached join
     index).  Left tiles are ``BLOCK * MJ_ITEMS`` rows of one bucket range, aligned so each thread
@@ -1476,7 +1491,7 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
     (profiles/pmc_merge_join_r2.txt).  Spans longer than MJ_LDS_KEYS (many right rows per left
     tile) are searched in HBM.  Reference: the bucketed SortMergeJoin plans of JoinIndexRule
     (JoinIndexRule.scala:63-69), which re-match keys on every query."""
-    NI = MJ_ITEMS  # noqa: N806
+    NI = _mj_items(_is_runs(compacts, p.lkey))  # noqa: N806
     BLOCK = MJ_BLOCK  # noqa: N806 — 64: one wavefront per workgroup, no block barriers
     T = BLOCK * NI  # noqa: N806
     LK = MJ_LDS_KEYS  # noqa: N806
@@ -1582,6 +1597,9 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
 
     U = max(1, MJ_STAGE_UNROLL)  # noqa: N806
     rpf = MJ_RPF and not MJ_PREFETCH and not runs
+    # run-keyed + software pipelining: tile t+1's span bounds, run window, run masks and left
+    # vectors are in flight while tile t stages, matches and drains
+    runs_pf = runs and MJ_RUNS_PREFETCH
     pf_slots = list(dict.fromkeys(stage_slots + rtail))
 
     def pf_issue(b: List[str], i2: str, ssv: str, sev: str) -> None:
@@ -1611,9 +1629,13 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
             b.extend([f"{ind}i64 ssNN = 0, seNN = 0;",
                       f"{ind}if (t + 2 < t1) {{ ssNN = a.spans[4 * (t + 2) + 2]; "
                       f"seNN = a.spans[4 * (t + 2) + 3]; }}"])
-        else:
+        elif not runs_pf:
             b.append(f"{ind}const i64 ss = a.spans[4 * t + 2], se = a.spans[4 * t + 3];")
-        if runs:
+        if runs and runs_pf:
+            # span bounds, run window and run masks came with the previous tile (_vec_tiles)
+            b.append(f"{ind}for (int q_ = (int)threadIdx.x; q_ < nl_; q_ += {BLOCK}) "
+                     f"lrk_[q_] = (unsigned)a.RK{lk}[ra_ + q_] + (unsigned)a.KOF;")
+        elif runs:
             # the tile's runs (hs_tile_runs), the thread's 64-row group run mask / base, and the
             # run keys staged as merge images - loads issued with the right span's staging
             b.extend([f"{ind}const int ra_ = a.TR[2 * t], nl_ = a.TR[2 * t + 1];",
@@ -1749,10 +1771,11 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
         def one_round(i2: str) -> None:
             b.append(f"{i2}{{ unsigned pb = mtb;")
             if ronly:
-                b.append(f"{i2}if (staged) {{")
+                # run-keyed: a staged span's pass bytes were folded into the run matches
+                b.append(f"{i2}if ({'false' if runs else 'staged'}) {{")
                 for it in range(NI):
                     b.append(f"{i2}  pb &= spass[{bit('mtb', it)} ? jl{it} : 0] != 0 ? ~0u : ~{1 << it}u;")
-                b.append(f"{i2}}} else {{")
+                b.append(f"{i2}}} else{' if (!staged)' if runs else ''} {{")
                 for it in range(NI):
                     b.append(f"{i2}  {{ const i64 jq{it} = ss + ({bit('mtb', it)} ? jl{it} : 0);")
                     g2 = _Gen(args, cols, split, (f"row{it}", f"jq{it}"), approx, True)
@@ -1828,7 +1851,14 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
                    "seN = a.spans[4 * (t0 + 1) + 3]; }")
         pf_issue(pre, "  ", "ssC", "seC")
         b += _TILE_HEAD + pre
-    if MJ_PREFETCH:
+    if runs_pf:
+        gi = "((G0 < a.nrows ? G0 : a.nrows - 1) >> 6)"
+        _vec_tiles(b, T, NI, ind, loads,
+                   [("gm_", "unsigned long long", f"a.GM{lk}[{gi}]"),
+                    ("gr_", "int", f"a.GR{lk}[{gi}]")], body,
+                   [("ss", "i64", "a.spans[4 * ({t}) + 2]"), ("se", "i64", "a.spans[4 * ({t}) + 3]"),
+                    ("ra_", "int", "a.TR[2 * ({t})]"), ("nl_", "int", "a.TR[2 * ({t}) + 1]")])
+    elif MJ_PREFETCH:
         # software-pipelined: tile t+1's left vectors are in flight during tile t's staging,
         # search and aggregate tail (the kernel waits on memory ~60% of its wave cycles:
         # profiles/pmc_merge_join_r3.txt)
@@ -1888,7 +1918,7 @@ def _runs_match(b: List[str], ind: str, g1: "_Gen", rk: int, rkv: str, rimg, NI:
               f"{ind}          while (lo < hi) {{ const int m = (lo + hi) >> 1; "
               f"if (skeys[m] < key_) lo = m + 1; else hi = m; }}",
               f"{ind}          j_ = lo; }} }}",
-              f"{ind}      lrk_[q] = (j_ < ns && skeys[j_] == key_) ? (unsigned)j_ : 0xFFFFFFFFu;",
+              f"{ind}      lrk_[q] = (j_ < ns && skeys[j_] == key_ && spass[j_]) ? (unsigned)j_ : 0xFFFFFFFFu;",
               f"{ind}    }}",
               f"{ind}  }} else {{",
               f"{ind}    for (int q = q0_; q < q1_; ++q) {{ const unsigned key_ = lrk_[q]; "
@@ -1904,12 +1934,15 @@ def _runs_match(b: List[str], ind: str, g1: "_Gen", rk: int, rkv: str, rimg, NI:
               f"{ind}unsigned mtb = 0u;"])
     for it in range(NI):
         b.append(f"{ind}int jl{it} = 0;")
+    # the thread's NI rows lie in one 64-row group: their run-start bits, shifted down, fit in
+    # 32 bits, so each row's run is the first row's run plus one popcount (no carried chain)
     b.extend([f"{ind}{{ const int sh_ = (int)(g0 & 63);",
-              f"{ind}  int rq_ = gr_ + (int)__popcll(gm_ & ((2ull << sh_) - 2ull)) - ra_;"])
+              f"{ind}  const int rq0_ = gr_ + (int)__popcll(gm_ & ((2ull << sh_) - 2ull)) - ra_;",
+              f"{ind}  const unsigned gl_ = (unsigned)(gm_ >> sh_);",
+              f"{ind}  const int rmax_ = nl_ > 0 ? nl_ - 1 : 0;"])
     for it in range(NI):
-        if it:
-            b.append(f"{ind}  rq_ += (int)((gm_ >> (sh_ + {it})) & 1ull);")
-        b.extend([f"{ind}  {{ const int ri_ = rq_ < 0 ? 0 : (rq_ < nl_ ? rq_ : (nl_ > 0 ? nl_ - 1 : 0));",
+        rq = "rq0_" if it == 0 else f"(rq0_ + (int)__popc(gl_ & {(2 << it) - 2}u))"
+        b.extend([f"{ind}  {{ const int ri_ = min(max({rq}, 0), rmax_);",
                   f"{ind}    const unsigned jm_ = lrk_[ri_];",
                   f"{ind}    const bool h_ = ((mb >> {it}) & 1u) && jm_ != 0xFFFFFFFFu;",
                   f"{ind}    mtb |= h_ ? {1 << it}u : 0u; jl{it} = h_ ? (int)jm_ : 0; }}"])
@@ -2019,16 +2052,16 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
     """Sort-merge join + aggregate with ``gen_merge_join_agg`` (same outputs as ``join_agg``);
     ``nrows`` = left table rows; ``rdup`` = the right key column may repeat a key
     (``key_has_dups``)."""
-    NI = MJ_ITEMS  # noqa: N806
-    T = MJ_BLOCK * NI  # noqa: N806
-    GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
-    dev = rstart.device
-    max_tiles = nrows // T + 2 * rstart.numel() + 2
     runs = None
     if not rdup:
         compacts, runs = _with_runs(p, compacts)
     if hk is None and runs is None:
         compacts = _with_key16(p, compacts)
+    NI = _mj_items(runs is not None)  # noqa: N806
+    T = MJ_BLOCK * NI  # noqa: N806
+    GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
+    dev = rstart.device
+    max_tiles = nrows // T + 2 * rstart.numel() + 2
     tp, spans = _join_spans(p, rstart, rlen, rbucket, roff, max_tiles, T, cache_spans, align=NI)
     k = kernel_for(merge_join_shape(p, compacts, hk), lambda: gen_merge_join_agg(p, compacts, hk))
     grid = max(1, MJ_GRID * 256 // MJ_BLOCK)
@@ -2068,7 +2101,8 @@ def _with_runs(p: NL.JoinParams, compacts):
     ``encoding.MIN_ROWS_PER_RUN`` rows; else (``compacts``, None).  Callers use it only for
     unique right keys."""
     from .encoding import GroupedCompact, key_runs
-    if not (MJ_RUNS and MJ_ITEMS and 64 % MJ_ITEMS == 0) or _key32_frame(p, compacts) is None:
+    ni = _mj_items(True)
+    if not (MJ_RUNS and ni and 64 % ni == 0) or _key32_frame(p, compacts) is None:
         return compacts, None
     lk = p.lkey
     c = compacts.get(lk)
@@ -2319,7 +2353,8 @@ def _tile_loop(b: List[str], T: int, NI: int, vec: int, ind: str = "    ") -> No
         _vec_rows(b, NI, ind)
 
 
-def _vec_tiles(b: List[str], T: int, NI: int, ind: str, loads, scalars, body) -> None:
+def _vec_tiles(b: List[str], T: int, NI: int, ind: str, loads, scalars, body,
+               tscalars=()) -> None:
     """Tile loops of a vectorized streaming kernel (``body(b, mode)`` emits one tile's work;
     ``loads`` = (name, C type, pointer) vector arrays, ``scalars`` = (name, C type, expression
     over ``G0``) per-thread values loaded with them).
@@ -2333,9 +2368,12 @@ def _vec_tiles(b: List[str], T: int, NI: int, ind: str, loads, scalars, body) ->
     at the top of tile t, before t's predicates, gathers and aggregate tail, so each wavefront
     keeps the next tile's stream in flight across this tile's dependent round trips.  Full
     tiles precede partial ones in a block's run, so the pipelined loop runs first and the
-    element-wise loop finishes the run."""
+    element-wise loop finishes the run.  ``tscalars`` = (name, C type, expression over ``{t}``)
+    per-tile values (span bounds, run windows) prefetched the same way."""
     if not VEC_PREFETCH:
         _tile_loop(b, T, NI, 1, ind)
+        for name, ct, expr in tscalars:
+            b.append(f"{ind}const {ct} {name} = {expr.format(t='t')};")
         b.append(f"{ind}if (tb0 + {T} <= a.nrows) {{")
         _vec_issue(b, loads, NI, ind, True)
         for name, ct, expr in scalars:
@@ -2356,8 +2394,10 @@ def _vec_tiles(b: List[str], T: int, NI: int, ind: str, loads, scalars, body) ->
                   f"{i2}  rsP = a.rstart[r]; reP = rsP + a.rlen[r];",
                   f"{i2}  tb0P = (rsP & ~(i64){NI - 1}) + off_;",
                   f"{i2}  g0P = tb0P + (i64)threadIdx.x * {NI}; }}",
-                  f"{i2}fullP = tb0P + {T} <= a.nrows;",
-                  f"{i2}if (fullP) {{"])
+                  f"{i2}fullP = tb0P + {T} <= a.nrows;"])
+        for name, ct, expr in tscalars:
+            b.append(f"{i2}{name}P = {expr.format(t=texpr)};")
+        b.append(f"{i2}if (fullP) {{")
         for name, ct, ptr in loads:
             b.append(f"{i2}  vload<{ct}, {NI}>({ptr}, g0P, {name}vP);")
         for name, ct, expr in scalars:
@@ -2367,7 +2407,7 @@ def _vec_tiles(b: List[str], T: int, NI: int, ind: str, loads, scalars, body) ->
     b.append("  i64 rsP = 0, reP = 0, tb0P = 0, g0P = 0; bool fullP = false;")
     for name, ct, _ in loads:
         b.append(f"  {ct} {name}vP[{NI}];")
-    for name, ct, _ in scalars:
+    for name, ct, _ in list(scalars) + list(tscalars):
         b.append(f"  {ct} {name}P = ({ct})0;")
     b.append("  i64 t = t0;")
     b.append("  if (t < t1) {")
@@ -2378,7 +2418,7 @@ def _vec_tiles(b: List[str], T: int, NI: int, ind: str, loads, scalars, body) ->
     for name, ct, _ in loads:
         b.append(f"{ind}{ct} {name}v[{NI}]; " +
                  " ".join(f"{name}v[{k}] = {name}vP[{k}];" for k in range(NI)))
-    for name, ct, _ in scalars:
+    for name, ct, _ in list(scalars) + list(tscalars):
         b.append(f"{ind}const {ct} {name} = {name}P;")
     b.append(f"{ind}if (t + 1 < t1) {{")
     geom("(t + 1)", ind + "  ")
@@ -2390,6 +2430,8 @@ def _vec_tiles(b: List[str], T: int, NI: int, ind: str, loads, scalars, body) ->
           "    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;",
           f"    const i64 off = (t - a.tile_prefix[r]) * {T};"]
     _vec_rows(b, NI, ind)
+    for name, ct, expr in tscalars:
+        b.append(f"{ind}const {ct} {name} = {expr.format(t='t')};")
     _vec_issue(b, loads, NI, ind, False)
     for name, ct, expr in scalars:
         b.append(f"{ind}const {ct} {name} = {expr.replace('G0', 'g0')};")

@@ -430,6 +430,57 @@ def histogram(ids, num_bins: int):
     return out
 
 
+MAX_BITMAP_BITS = 1 << 33     # 1 GiB of HBM: a key domain wider than this is not bitmapped
+
+
+def key_domain(col):
+    """(lo, hi, non-null count) of an integer device column, or None when it holds no non-null
+    key or is not an integer column.  One host sync."""
+    torch = _torch()
+    if col.hs_type not in (NL.I8, NL.I16, NL.I32, NL.I64, NL.U32) or col.offsets is not None:
+        return None
+    d = col.data
+    if d.numel() == 0:
+        return None
+    if col.valid is not None:
+        vm = col.valid.bool()
+        x = d.long()
+        st = torch.stack([torch.where(vm, x, torch.iinfo(torch.int64).max).min(),
+                          torch.where(vm, x, torch.iinfo(torch.int64).min).max(),
+                          vm.sum()]).cpu().tolist()
+        if st[2] == 0:
+            return None
+        return int(st[0]), int(st[1]), int(st[2])
+    mm = torch.aminmax(d)
+    lo, hi = (int(v) for v in torch.stack([mm.min.long(), mm.max.long()]).cpu().tolist())
+    return lo, hi, int(d.numel())
+
+
+def key_bitmap(col, lo: int, nbits: int):
+    """(int64 words, duplicate flag) of the non-null integer keys of device column ``col`` as
+    bits (key - lo) of an ``nbits``-bit bitmap (csrc/kernels/key_bitmap.hip).  Every key must
+    lie in [lo, lo + nbits)."""
+    torch = _torch()
+    d = col.data
+    words = torch.zeros(max((nbits + 63) // 64, 1), dtype=torch.int64, device=d.device)
+    flags = torch.zeros(1, dtype=torch.int32, device=d.device)
+    desc = col.desc()
+    NL.check(NL.lib().hs_key_bitmap(C.byref(desc), d.numel(), int(lo), int(nbits), NL.ptr(words),
+                                    NL.ptr(flags), NL.stream_ptr()), "hs_key_bitmap")
+    f = int(flags.item())
+    if f & 2:
+        raise RuntimeError("hs_key_bitmap: key outside its domain")
+    return words, bool(f & 1)
+
+
+def bitmap_popcount(words) -> int:
+    torch = _torch()
+    out = torch.zeros(1, dtype=torch.int64, device=words.device)
+    NL.check(NL.lib().hs_bitmap_popcount(NL.ptr(words), words.numel(), NL.ptr(out),
+                                         NL.stream_ptr()), "hs_bitmap_popcount")
+    return int(out.item())
+
+
 def lookup_i32(table, codes):
     """``table[codes]`` for an int32 table and int32 codes, through the gather kernel."""
     from ..exec.device_table import DeviceColumn

@@ -112,6 +112,24 @@ class DistContext:
             dist.all_reduce(t, op=rop)
         return t
 
+    def all_gather_tensor(self, t):
+        """``[world * n]`` concatenation (rank order) of every rank's 1-D tensor ``t`` (same n
+        on every rank): one RCCL all-gather on device, host-staged for gloo + CUDA tensors."""
+        import torch
+        import torch.distributed as dist
+        if self._staged(t):
+            h = t.cpu()
+            parts = [torch.empty_like(h) for _ in range(self.world)]
+            dist.all_gather(parts, h)
+            return torch.cat(parts).to(t.device)
+        if self.backend == "nccl":
+            out = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
+            dist.all_gather_into_tensor(out, t.contiguous())
+            return out
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(parts, t.contiguous())
+        return torch.cat(parts)
+
     def all_to_all_single(self, out, inp, out_splits=None, in_splits=None):
         import torch.distributed as dist
         if self._staged(inp):

@@ -40,7 +40,11 @@ class QueryExecution:
         if self._executed is None:
             from ..utils.conf import HyperspaceConf
             pc = None
-            if HyperspaceConf.plan_cache_enabled(self.session.conf):
+            pend = getattr(self, "_pending_store", None)
+            if pend is not None:        # _submit_bound already looked the query up: a miss
+                pc, key, ctx = pend
+                self._pending_store = None
+            elif HyperspaceConf.plan_cache_enabled(self.session.conf):
                 from .plan_cache import plan_cache
                 pc = plan_cache(self.session)
                 plan, key, ctx = pc.lookup(self.session, self.logical)
@@ -66,10 +70,42 @@ class QueryExecution:
         device backend returns before its kernels finish (``GpuBackend.collect_async``); the
         host backend runs the query here."""
         backend = self.session.backend()
+        if self._executed is None and getattr(backend, "supports_bound_plans", False):
+            fut = self._submit_bound(backend)
+            if fut is not None:
+                return fut
         plan = self.executed_plan
         if hasattr(backend, "collect_async"):
             return backend.collect_async(plan)
         return _Done(backend.collect(plan), getattr(backend, "last_path", "host"))
+
+    def _submit_bound(self, backend):
+        """Plan-cache hit fast path: submit the cached plan itself with this query's literal
+        values bound into it for the duration of the submission (plan_cache._Entry).  None when
+        the query is not a hit that allows it (then ``executed_plan`` plans / materializes)."""
+        from ..utils.conf import HyperspaceConf
+        if not HyperspaceConf.plan_cache_enabled(self.session.conf):
+            return None
+        from .plan_cache import plan_cache
+        pc = plan_cache(self.session)
+        entry, key, ctx = pc.lookup_entry(self.session, self.logical)
+        if entry is None or ctx.reuse or not entry.inplace_ok:
+            if entry is not None:
+                plan = pc.materialize(entry, ctx)
+                self._executed = reuse_exchanges(plan, self.session) if ctx.reuse else plan
+            else:
+                self._pending_store = (pc, key, ctx)
+            return None
+        with entry.lock:
+            saved = entry.bind_literals(ctx.lits)
+            try:
+                fut = backend.collect_async(entry.plan)
+            finally:
+                entry.restore_literals(saved)
+        # a result fallback later re-runs the query on the host: give it a plan of its own
+        fut.plan = None
+        fut.plan_fn = lambda: pc.materialize(entry, ctx)
+        return fut
 
     def explain_string(self, extended: bool = False) -> str:
         parts = []

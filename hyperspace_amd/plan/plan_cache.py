@@ -238,22 +238,47 @@ def _subst(v, m: Dict[int, E.Literal], hot: set, memo: Dict[int, object]):
     return out
 
 
+def _deferred_literals(plan) -> set:
+    """ids of the literals a backend evaluates after a query's submission returns: those in an
+    aggregate's result expressions outside the aggregate functions' own inputs (the result
+    arithmetic over aggregates runs when the result is fetched)."""
+    from . import physical as X
+    out: set = set()
+
+    def walk(e):
+        if isinstance(e, E.AggregateFunction):
+            return
+        if isinstance(e, E.Literal):
+            out.add(id(e))
+            return
+        for c in getattr(e, "children", ()):
+            walk(c)
+    for n in plan.collect(lambda x: isinstance(x, X.HashAggregateExec)):
+        for e in n.aggregates:
+            walk(e)
+    return out
+
+
 def _same(a: E.Literal, b: E.Literal) -> bool:
     """Same value and type (so the cached plan's literal object can stay)."""
     return type(a.value) is type(b.value) and a.value == b.value and a.dtype == b.dtype
 
 
 class _Entry:
-    """One cached executed plan.  ``prepared`` holds per-backend re-bindable launches of it
-    (exec/prepared.py): a hit runs those with the new literals written into ``old_lits`` for
-    the duration of the launch (under ``lock``), with no substitution and no executor walk."""
-    __slots__ = ("plan", "old_lits", "paths", "refs", "reuse", "prepared", "lock")
+    """One cached executed plan.  Its literal objects are private clones (``old_lits``), so a
+    hit can also run the cached plan itself with the new query's values written into them for
+    the duration of a submission (``bind_literals`` / ``restore_literals`` under ``lock``): no
+    plan copy, and the executor sees the same node objects on every hit (its per-node memos
+    stay warm).  ``inplace_ok`` is False when a literal sits where a submitted query still
+    reads it after the submission returns (a result expression over aggregates, evaluated when
+    the result is fetched); such entries are always materialized."""
+    __slots__ = ("plan", "old_lits", "paths", "refs", "reuse", "lock", "inplace_ok")
 
-    def __init__(self, plan, old_lits, paths, refs, reuse):
+    def __init__(self, plan, old_lits, paths, refs, reuse, inplace_ok=False):
         self.plan, self.old_lits, self.paths, self.refs, self.reuse = \
             plan, old_lits, paths, refs, reuse
-        self.prepared: Dict[int, object] = {}
         self.lock = threading.Lock()
+        self.inplace_ok = inplace_ok
 
     def bind_literals(self, lits) -> list:
         """Write the new query's literal values into the cached plan's literal objects (caller
@@ -357,7 +382,20 @@ class PlanCache:
                 hot: set = set()
                 _hot_paths(executed, {id(x)}, hot, {})
                 paths[id(x)] = hot
-        entry = _Entry(executed, list(ctx.lits), paths, list(ctx.refs), reuse)
+        # the entry's own copy, with private literal objects: the caller keeps running (and may
+        # re-execute) ``executed``, whose literals must never see another query's values
+        clones = {k: copy.copy(x) for k, x in ((id(x), x) for x in ctx.lits)}
+        private = _subst(executed, clones, set().union(*paths.values()) if paths else set(), {})
+        old_lits = [clones[id(x)] for x in ctx.lits]
+        ppaths = {}
+        for x in old_lits:
+            if id(x) not in ppaths:
+                hot = set()
+                _hot_paths(private, {id(x)}, hot, {})
+                ppaths[id(x)] = hot
+        late = _deferred_literals(private)
+        entry = _Entry(private, old_lits, ppaths, list(ctx.refs), reuse,
+                       inplace_ok=not any(id(x) in late for x in old_lits))
         with self._lock:
             self._lru[key] = entry
             while len(self._lru) > self.capacity:

@@ -168,3 +168,68 @@ def test_canonical_string_keeps_literal_text():
     assert X.canonical_string(f1) != X.canonical_string(f2)
     f3 = X.FilterExec(E.EqualTo(a, E.Literal("item#5")), scan)
     assert X.canonical_string(f1) == X.canonical_string(f3)
+
+
+class _BoundBackend:
+    """A backend that accepts bound cached plans (like GpuBackend): it runs the host executor
+    during collect_async, i.e. while the query's literals are bound into the cached plan."""
+    supports_bound_plans = True
+
+    def __init__(self, cpu):
+        self.cpu, self.calls, self.plans = cpu, 0, []
+        self.last_path = "host"
+
+    def collect(self, plan):
+        return self.cpu.collect(plan)
+
+    def collect_async(self, plan):
+        import types
+        self.calls += 1
+        self.plans.append(plan)
+        t = self.cpu.collect(plan)
+        return types.SimpleNamespace(result=lambda: t, path="host", reason=None)
+
+
+def test_bound_literal_submission_matches_fresh_planning(data):
+    """Plan-cache hits submit the entry's own plan with the query's literals bound in place
+    (plan_cache._Entry.bind_literals): same rows as planning from scratch, the entry's literal
+    objects are restored afterwards, and hits see the same plan object (no copy)."""
+    s, _, df, od = data
+    cpu = s.backend()
+    fake = _BoundBackend(cpu)
+    s.backend = lambda: fake
+    pc = plan_cache(s)
+    try:
+        got = []
+        before = None
+        for i in range(6):
+            got.append((sorted(tuple(r) for r in _filter_q(df, i).collect_async().result()),
+                        sorted(tuple(r) for r in _join_q(df, od, i).collect_async().result())))
+            if i == 0:
+                before = {id(e): [x.value for x in e.old_lits] for e in pc._lru.values()}
+    finally:
+        del s.backend
+    entries = list(pc._lru.values())
+    assert any(e.inplace_ok for e in entries)
+    for e in entries:      # every bound literal was restored to the creating query's value
+        assert not e.lock.locked()
+        if id(e) in before:
+            assert [x.value for x in e.old_lits] == before[id(e)]
+    hits = [p for p in fake.plans if any(p is e.plan for e in entries)]
+    assert len(hits) >= 8                # hits ran the cached plans themselves
+    s.conf.set("spark.hyperspace.mi.planCache.enabled", "false")
+    want = [(_rows(_filter_q(df, i)), _rows(_join_q(df, od, i))) for i in range(6)]
+    s.conf.set("spark.hyperspace.mi.planCache.enabled", "true")
+    assert got == want
+
+
+def test_result_literals_force_materialized_hits(data):
+    """A literal in result arithmetic over aggregates is read when the result is fetched, after
+    the submission returned: such entries never run bound in place."""
+    s, _, df, _ = data
+    pc = plan_cache(s)
+    pc.clear()
+    for i in range(3):
+        q = df.filter(col("v") > 0.1 * i).agg((sum_(col("v")) * (2 + i)).alias("x"))
+        q.collect()
+    assert pc._lru and not any(e.inplace_ok for e in pc._lru.values())
