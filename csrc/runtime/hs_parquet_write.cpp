@@ -295,4 +295,253 @@ int hs_pq_write_file(const char* path, int ncols, int nrg, const int64_t* rg_row
   return err;
 }
 
+// ------------------------------------------------------------------ general writer (v2)
+// One data page of a column chunk.  Definition levels (nullable columns) and values arrive as
+// separate device-encoded segments: the level bits of one bit-packed run (1 bit per row, LSB
+// first) and the value payload (PLAIN values of the non-null rows, bit-packed dictionary codes,
+// or bit-packed BOOLEANs).  With codec 1 each segment holds the Snappy elements of its raw bytes
+// (no preamble); the small host parts of the page (level length + run header, dictionary bit
+// width + run header) go in as literal elements.
+struct HsPqWPage {
+  const uint8_t* levels;
+  int64_t levels_bytes;
+  int64_t levels_raw;     // ceil(nvals / 8)
+  const uint8_t* payload;
+  int64_t payload_bytes;
+  int64_t payload_raw;
+  int64_t nvals;          // rows of the page (nulls included)
+  int64_t nonnull;        // non-null rows (= values encoded)
+};
+
+struct HsPqWCol2 {
+  const char* name;
+  int32_t ptype;          // 0 BOOLEAN, 1 INT32, 2 INT64, 4 FLOAT, 5 DOUBLE, 6 BYTE_ARRAY
+  int32_t logical;        // 0 none, 1 DATE, 2 STRING, 3 INT, 4 TIMESTAMP, 5 DECIMAL
+  int32_t lp0;            // INT: bit width | TIMESTAMP: unit 0 ms, 1 us, 2 ns | DECIMAL: precision
+  int32_t lp1;            // INT: signed | TIMESTAMP: adjusted to UTC | DECIMAL: scale
+  int32_t dict;
+  int32_t bit_width;
+  int32_t codec;
+  int32_t nullable;
+  const uint8_t* dict_page;
+  int64_t dict_bytes;
+  int64_t dict_count;
+  int64_t dict_raw_bytes;
+  int64_t null_count;
+  const HsPqWPage* pages;
+  int32_t npages;
+  int32_t pad;
+};
+
+namespace {
+
+void literal(std::vector<uint8_t>& z, const std::vector<uint8_t>& raw) {
+  // Snappy literal element(s) of a small host byte string
+  size_t i = 0;
+  while (i < raw.size()) {
+    const size_t n = std::min<size_t>(raw.size() - i, 60);
+    z.push_back((uint8_t)((n - 1) << 2));
+    z.insert(z.end(), raw.begin() + (long)i, raw.begin() + (long)(i + n));
+    i += n;
+  }
+}
+
+void schema_element(TWriter& w, const HsPqWCol2& col) {
+  w.begin_anon_struct();
+  w.i32(1, col.ptype);
+  w.i32(3, 1);   // OPTIONAL (as Spark writes every column of a DataFrame)
+  w.str(4, col.name);
+  // converted_type (6) for older readers, scale (7) / precision (8) for DECIMAL
+  switch (col.logical) {
+    case 1: w.i32(6, 6); break;                                   // DATE
+    case 2: w.i32(6, 0); break;                                   // UTF8
+    case 3: w.i32(6, (col.lp1 ? 15 : 11) + (col.lp0 == 8 ? 0 : col.lp0 == 16 ? 1 :
+                                             col.lp0 == 32 ? 2 : 3)); break;   // INT_x / UINT_x
+    case 4: if (col.lp0 <= 1) w.i32(6, col.lp0 == 0 ? 9 : 10); break;          // TIMESTAMP_*
+    case 5: w.i32(6, 5); w.i32(7, col.lp1); w.i32(8, col.lp0); break;         // DECIMAL
+    default: break;
+  }
+  if (col.logical) {
+    w.begin_struct(10);               // LogicalType union
+    switch (col.logical) {
+      case 1: w.begin_struct(6); w.end_struct(); break;          // DATE
+      case 2: w.begin_struct(1); w.end_struct(); break;          // STRING
+      case 3:                                                    // INTEGER
+        w.begin_struct(10);
+        w.field(1, 3); w.byte((uint8_t)col.lp0);                 // i8 bitWidth
+        w.field(2, col.lp1 ? 1 : 2);                             // bool isSigned
+        w.end_struct();
+        break;
+      case 4:                                                    // TIMESTAMP
+        w.begin_struct(8);
+        w.field(1, col.lp1 ? 1 : 2);                             // isAdjustedToUTC
+        w.begin_struct(2);                                       // TimeUnit union
+        w.begin_struct(col.lp0 == 0 ? 1 : col.lp0 == 1 ? 2 : 3); w.end_struct();
+        w.end_struct();
+        w.end_struct();
+        break;
+      case 5:                                                    // DECIMAL
+        w.begin_struct(5);
+        w.i32(1, col.lp1);                                       // scale
+        w.i32(2, col.lp0);                                       // precision
+        w.end_struct();
+        break;
+      default: break;
+    }
+    w.end_struct();
+  }
+  w.end_struct();
+}
+
+}  // namespace
+
+// Write one Parquet file: `ncols` columns x `nrg` row groups (cols[rg * ncols + c]), each
+// column chunk one optional dictionary page plus `npages` data pages.  Returns 0 or -errno.
+int hs_pq_write_file2(const char* path, int ncols, int nrg, const int64_t* rg_rows,
+                      const HsPqWCol2* cols, const char* created_by) {
+  const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd < 0) return -errno;
+  int64_t pos = 0;
+  std::vector<std::vector<uint8_t>> keep;
+  std::vector<iovec> iov;
+  static const char magic[4] = {'P', 'A', 'R', '1'};
+  iov.push_back({(void*)magic, 4});
+  int64_t off = 4;
+  std::vector<ColPos> posv((size_t)ncols * nrg);
+  size_t reserve = 4;
+  for (int i = 0; i < ncols * nrg; ++i) reserve += 8 + 6 * (size_t)cols[i].npages;
+  keep.reserve(reserve);   // iovecs point into keep's elements: never reallocate
+  for (int g = 0; g < nrg; ++g) {
+    for (int c = 0; c < ncols; ++c) {
+      const HsPqWCol2& col = cols[(size_t)g * ncols + c];
+      ColPos& p = posv[(size_t)g * ncols + c];
+      const int64_t start = off;
+      const bool snappy = col.codec == 1;
+      if (col.dict) {
+        const int64_t raw = snappy ? col.dict_raw_bytes : col.dict_bytes;
+        keep.push_back(page_header(2, col.dict_bytes, col.dict_count, 0, raw));
+        p.dict_off = off;
+        iov.push_back({keep.back().data(), keep.back().size()});
+        iov.push_back({(void*)col.dict_page, (size_t)col.dict_bytes});
+        off += (int64_t)keep.back().size() + col.dict_bytes;
+        p.raw_total += (int64_t)keep.back().size() + raw;
+      }
+      p.data_off = off;
+      for (int q = 0; q < col.npages; ++q) {
+        const HsPqWPage& pg = col.pages[q];
+        // host parts: level length + run header, value run header
+        std::vector<uint8_t> lpre, vpre;
+        if (col.nullable) {
+          std::vector<uint8_t> run;
+          put_varint(run, ((uint64_t)((pg.nvals + 7) / 8) << 1) | 1);
+          const uint32_t len = (uint32_t)(run.size() + pg.levels_raw);
+          lpre.insert(lpre.end(), (const uint8_t*)&len, (const uint8_t*)&len + 4);
+          lpre.insert(lpre.end(), run.begin(), run.end());
+        } else {
+          def_levels_all_valid(lpre, pg.nvals);   // one RLE run of 1s, no device bytes
+        }
+        if (col.dict) {
+          vpre.push_back((uint8_t)col.bit_width);
+          if (pg.nonnull > 0) put_varint(vpre, ((uint64_t)((pg.nonnull + 7) / 8) << 1) | 1);
+        }
+        const int64_t lraw = col.nullable ? pg.levels_raw : 0;
+        const int64_t raw_size = (int64_t)lpre.size() + lraw + (int64_t)vpre.size() +
+                                 pg.payload_raw;
+        std::vector<uint8_t> head, mid;   // bytes before the level bits / before the payload
+        if (snappy) {
+          put_varint(head, (uint64_t)raw_size);
+          if (!lpre.empty()) literal(head, lpre);
+          if (!vpre.empty()) literal(mid, vpre);
+        } else {
+          head = lpre;
+          mid = vpre;
+        }
+        const int64_t lbytes = col.nullable ? pg.levels_bytes : 0;
+        const int64_t psize = (int64_t)head.size() + lbytes + (int64_t)mid.size() +
+                              pg.payload_bytes;
+        keep.push_back(page_header(0, psize, pg.nvals, col.dict ? 8 : 0, raw_size));
+        iov.push_back({keep.back().data(), keep.back().size()});
+        off += (int64_t)keep.back().size();
+        p.raw_total += (int64_t)keep.back().size() + raw_size;
+        if (!head.empty()) {
+          keep.push_back(std::move(head));
+          iov.push_back({keep.back().data(), keep.back().size()});
+        }
+        if (lbytes) iov.push_back({(void*)pg.levels, (size_t)lbytes});
+        if (!mid.empty()) {
+          keep.push_back(std::move(mid));
+          iov.push_back({keep.back().data(), keep.back().size()});
+        }
+        if (pg.payload_bytes) iov.push_back({(void*)pg.payload, (size_t)pg.payload_bytes});
+        off += psize;
+      }
+      p.total = off - start;
+    }
+  }
+  TWriter w;
+  w.i32(1, 1);
+  w.list(2, 12, ncols + 1);
+  w.begin_anon_struct();
+  w.str(4, "schema");
+  w.i32(5, ncols);
+  w.end_struct();
+  for (int c = 0; c < ncols; ++c) schema_element(w, cols[c]);
+  int64_t total_rows = 0;
+  for (int g = 0; g < nrg; ++g) total_rows += rg_rows[g];
+  w.i64(3, total_rows);
+  w.list(4, 12, nrg);
+  for (int g = 0; g < nrg; ++g) {
+    w.begin_anon_struct();
+    w.list(1, 12, ncols);
+    int64_t rg_bytes = 0;
+    for (int c = 0; c < ncols; ++c) {
+      const HsPqWCol2& col = cols[(size_t)g * ncols + c];
+      const ColPos& p = posv[(size_t)g * ncols + c];
+      rg_bytes += p.raw_total;
+      w.begin_anon_struct();
+      w.i64(2, p.dict_off >= 0 ? p.dict_off : p.data_off);
+      w.begin_struct(3);
+      w.i32(1, col.ptype);
+      if (col.dict) {
+        w.list(2, 5, 3);
+        w.zz(0); w.zz(3); w.zz(8);
+      } else {
+        w.list(2, 5, 2);
+        w.zz(0); w.zz(3);
+      }
+      w.list(3, 8, 1);
+      w.varint(strlen(col.name));
+      w.bin(col.name);
+      w.i32(4, col.codec == 1 ? 1 : 0);
+      w.i64(5, rg_rows[g]);
+      w.i64(6, p.raw_total);
+      w.i64(7, p.total);
+      w.i64(9, p.data_off);
+      if (p.dict_off >= 0) w.i64(11, p.dict_off);
+      w.begin_struct(12);               // Statistics { 3: null_count }
+      w.i64(3, col.null_count);
+      w.end_struct();
+      w.end_struct();
+      w.end_struct();
+    }
+    w.i64(2, rg_bytes);
+    w.i64(3, rg_rows[g]);
+    w.end_struct();
+  }
+  w.str(6, created_by ? created_by : "hyperspace_amd");
+  w.byte(0);
+  keep.push_back(std::move(w.b));
+  const uint32_t flen = (uint32_t)keep.back().size();
+  iov.push_back({keep.back().data(), keep.back().size()});
+  std::vector<uint8_t> tail(8);
+  memcpy(tail.data(), &flen, 4);
+  memcpy(tail.data() + 4, magic, 4);
+  keep.push_back(std::move(tail));
+  iov.push_back({keep.back().data(), 8});
+  const bool ok = write_all(fd, iov, pos);
+  const int err = ok ? 0 : -errno;
+  if (close(fd) != 0 && ok) return -errno;
+  return err;
+}
+
 }  // extern "C"

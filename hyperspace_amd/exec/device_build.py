@@ -109,7 +109,11 @@ def _sort_and_write(session, table: Dict[str, DeviceColumn], names: List[str], b
             dict(zip(names, gathered)), names, schema, off,
             lambda b: os.path.join(local, bucket_file_name(task_id, job, b, codec)), rg,
             bucket.device, codec="none" if codec == "uncompressed" else codec)
+    LAST_BUILD_STATS["writer"] = "device" if paths is not None else "host"
     if paths is None:
+        from . import pq_encode
+        LAST_BUILD_STATS["writer_fallback"] = pq_encode.LAST_FALLBACK.get("reason") or \
+            ("codec " + codec if codec not in ("none", "uncompressed", "snappy") else "disabled")
         paths = staging.download_buckets(
             gathered, names, schema, off,
             lambda t, b: write_bucket_file(t, out_path, task_id, job, b, codec, rg),

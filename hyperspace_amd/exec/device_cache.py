@@ -231,8 +231,14 @@ def load_bucketed_index(files, columns: List[str], num_buckets: int, sort_cols: 
         # footers give every file's row count up front, so files stream straight into their
         # slice of presized HBM columns (staging.upload_files) with no host-side concatenation
         from . import staging
-        rows = list(staging.io_pool().map(
-            lambda p: pq.ParquetFile(P.to_local(p)).metadata.num_rows, paths))
+        from .pq_encode import CREATED_BY
+        metas = list(staging.io_pool().map(
+            lambda p: pq.ParquetFile(P.to_local(p)).metadata, paths))
+        rows = [m.num_rows for m in metas]
+        # files of the paged device writer (pages of at most pq_encode.PAGE_ROWS rows) decode
+        # on the device, pages and all; older row-group-sized pages take the host page layer
+        # (one wavefront inflates one page: profiles/cold_load_r2.jsonl)
+        paged = all((m.created_by or "") == CREATED_BY for m in metas)
         for (b, _), r in zip(ordered, rows):
             multi = multi or counts[b] > 0
             counts[b] += r
@@ -244,7 +250,7 @@ def load_bucketed_index(files, columns: List[str], num_buckets: int, sort_cols: 
                                  use_threads=False)
         up = staging.upload_files(read_file, paths, rows, schema, device,
                                   parquet_local=[P.to_local(p) for p in paths],
-                                  device_pages=False)
+                                  device_pages=paged)
         cols = dict(up.columns)
         for name, chunks in up.host_strings.items():
             arr = pa.chunked_array(chunks, type=chunks[0].type)

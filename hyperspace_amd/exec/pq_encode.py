@@ -20,9 +20,15 @@ writes each bucket file with ``pwritev`` straight from the pinned D2H buffers.
   (``csrc/kernels/snappy_encode.hip``, ``snappy_pages``), so only compressed bytes cross PCIe;
   the small dictionary pages with the host build of the same match finder.
 
-Files are Parquet v1 (data page V1, UNCOMPRESSED or SNAPPY, optional flat columns); anything
-outside that (nulls, booleans, decimals, timestamps, another codec) returns ``None`` so the
-caller writes with pyarrow instead.
+Files are Parquet v1 (data page V1, UNCOMPRESSED or SNAPPY, optional flat columns) with data
+pages of at most ``PAGE_ROWS`` rows (so the device read path inflates one page per wavefront),
+written by ``hs_pq_write_file2``.  Nullable columns carry their definition levels as one
+bit-packed run per page (packed on the device from the validity bytes) and encode only their
+non-null values.  Types: BOOLEAN (bit-packed PLAIN), INT8/INT16 (INT32 + INT logical type),
+INT32, INT64, DATE, TIMESTAMP(ms/us/ns), DECIMAL up to 18 digits (INT64 + DECIMAL), FLOAT,
+DOUBLE and dictionary strings.  Anything else (nested types, seconds timestamps, wider decimals,
+string dictionaries over ``DICT_MAX_STRINGS``, another codec) returns ``None`` with the reason
+in ``LAST_FALLBACK`` and the caller writes with pyarrow (``LAST_BUILD_STATS["writer"]``).
 """
 from __future__ import annotations
 
@@ -181,45 +187,99 @@ WRITE_PHASES: Dict[str, float] = {}
 _WP_LOCK = __import__("threading").Lock()
 
 
+class WPage(C.Structure):
+    _fields_ = [("levels", C.c_void_p), ("levels_bytes", C.c_int64), ("levels_raw", C.c_int64),
+                ("payload", C.c_void_p), ("payload_bytes", C.c_int64), ("payload_raw", C.c_int64),
+                ("nvals", C.c_int64), ("nonnull", C.c_int64)]
+
+
+class WCol2(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("ptype", C.c_int32), ("logical", C.c_int32),
+                ("lp0", C.c_int32), ("lp1", C.c_int32), ("dict", C.c_int32),
+                ("bit_width", C.c_int32), ("codec", C.c_int32), ("nullable", C.c_int32),
+                ("dict_page", C.c_void_p), ("dict_bytes", C.c_int64), ("dict_count", C.c_int64),
+                ("dict_raw_bytes", C.c_int64), ("null_count", C.c_int64),
+                ("pages", C.POINTER(WPage)), ("npages", C.c_int32), ("pad", C.c_int32)]
+
+
 def _writer():
     from .jit import runtime
     L = runtime()
     if not getattr(L, "_hs_pqw", False):
-        L.hs_pq_write_file.restype = C.c_int
-        L.hs_pq_write_file.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_int64),
-                                       C.POINTER(WCol), C.c_char_p]
+        L.hs_pq_write_file2.restype = C.c_int
+        L.hs_pq_write_file2.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_int64),
+                                        C.POINTER(WCol2), C.c_char_p]
         L._hs_pqw = True
     return L
 
 
-def _physical(t: pa.DataType):
-    """(Parquet physical type, logical 0/1 DATE/2 STRING, element bytes) or None."""
+# last reason write_buckets handed a build to the pyarrow writer (None: it wrote on the device)
+LAST_FALLBACK: Dict[str, Optional[str]] = {"reason": None}
+_TS_UNITS = {"ms": 0, "us": 1, "ns": 2}
+
+
+class _Phys:
+    """Parquet physical type, logical annotation and the device conversion of one column."""
+    __slots__ = ("ptype", "logical", "lp0", "lp1", "eb", "conv")
+
+    def __init__(self, ptype, logical=0, lp0=0, lp1=0, eb=0, conv=None):
+        self.ptype, self.logical, self.lp0, self.lp1, self.eb, self.conv = \
+            ptype, logical, lp0, lp1, eb, conv
+
+
+def _physical(t: pa.DataType) -> Optional[_Phys]:
+    """How column type ``t`` is written (physical type 0 BOOLEAN, 1 INT32, 2 INT64, 4 FLOAT,
+    5 DOUBLE, 6 BYTE_ARRAY; logical 1 DATE, 2 STRING, 3 INT, 4 TIMESTAMP, 5 DECIMAL), or None
+    when the device writer does not cover it."""
+    if pa.types.is_boolean(t):
+        return _Phys(0, eb=1, conv="bits")
     if pa.types.is_date32(t):
-        return 1, 1, 4
+        return _Phys(1, 1, eb=4)
     if pa.types.is_int32(t):
-        return 1, 0, 4
+        return _Phys(1, eb=4)
     if pa.types.is_int64(t):
-        return 2, 0, 8
+        return _Phys(2, eb=8)
+    if pa.types.is_int8(t) or pa.types.is_int16(t):
+        return _Phys(1, 3, t.bit_width, 1, eb=4, conv="widen")
     if pa.types.is_float32(t):
-        return 4, 0, 4
+        return _Phys(4, eb=4)
     if pa.types.is_float64(t):
-        return 5, 0, 8
+        return _Phys(5, eb=8)
+    if pa.types.is_timestamp(t) and t.unit in _TS_UNITS:
+        return _Phys(2, 4, _TS_UNITS[t.unit], 1 if t.tz is not None else 0, eb=8)
+    if pa.types.is_decimal(t) and t.precision <= 18 and t.bit_width == 128:
+        return _Phys(2, 5, t.precision, t.scale, eb=8, conv="decimal")
     if is_string(t):
-        return 6, 2, 0
+        return _Phys(6, 2)
     return None
 
 
 class ColPlan:
-    def __init__(self, name: str, ptype: int, logical: int, eb: int):
+    def __init__(self, name: str, ph: _Phys):
         self.name = name
         self.bname = name.encode()
-        self.ptype, self.logical, self.eb = ptype, logical, eb
+        self.ph = ph
+        self.ptype, self.logical, self.eb = ph.ptype, ph.logical, ph.eb
         self.dict = False
         self.bw = 0
         self.dict_page: Optional[np.ndarray] = None
         self.dict_count = 0
-        self.payload = None          # device uint8
+        self.payload = None          # device uint8: the value segment of every page
         self.page_off: Optional[np.ndarray] = None   # byte offset of every page (+ end)
+        self.nullable = False
+        self.levels: Optional["_Seg"] = None          # definition-level bits of every page
+        self.nonnull: Optional[np.ndarray] = None    # non-null rows of every page
+
+    @property
+    def encoded_bytes(self) -> int:
+        return int(self.page_off[-1]) + (self.levels.encoded_bytes if self.levels else 0)
+
+
+class _Seg:
+    """A device byte buffer cut into per-page segments (the shape snappy_launch compresses)."""
+
+    def __init__(self, payload, page_off: np.ndarray):
+        self.payload, self.page_off = payload, page_off
 
     @property
     def encoded_bytes(self) -> int:
@@ -237,14 +297,15 @@ def _string_dict_page(d: pa.Array) -> np.ndarray:
     bufs = a.buffers()
     offs = np.frombuffer(bufs[1], dtype=np.int64)[a.offset:a.offset + len(a) + 1]
     data = np.frombuffer(bufs[2], dtype=np.uint8) if bufs[2] is not None else np.zeros(0, np.uint8)
-    lens = np.diff(offs)
+    lens = np.diff(offs).astype(np.uint32)
     out = np.empty(int(lens.sum()) + 4 * len(a), dtype=np.uint8)
-    pos = 0
-    for i in range(len(a)):   # dictionaries are small (<= DICT_MAX_STRINGS)
-        ln = int(lens[i])
-        out[pos:pos + 4] = np.frombuffer(np.uint32(ln).tobytes(), dtype=np.uint8)
-        out[pos + 4:pos + 4 + ln] = data[offs[i]:offs[i] + ln]
-        pos += 4 + ln
+    # (u32 len, bytes) records: record i starts at its bytes offset plus 4 * i
+    starts = (offs[:-1] - offs[0]) + 4 * np.arange(len(a), dtype=np.int64)
+    hdr = lens.view(np.uint8).reshape(-1, 4)
+    for k in range(4):
+        out[starts + k] = hdr[:, k]
+    body = np.repeat(starts + 4 - (offs[:-1] - offs[0]), lens.astype(np.int64))
+    out[body + np.arange(int(lens.sum()), dtype=np.int64)] = data[offs[0]:offs[-1]]
     return out
 
 
@@ -258,90 +319,159 @@ def _dict_codes(v, eb: int, dbits, device):
     return codes, bool(miss.item())
 
 
+def _pack(codes, rows0: np.ndarray, n: np.ndarray, bw: int, device):
+    """Bit-pack int32 ``codes`` page by page (``hs_pq_pack``): page p packs codes
+    [rows0[p], rows0[p] + n[p]) into ceil(n[p] / 8) * bw bytes; returns (device bytes, page
+    byte offsets + end)."""
+    import torch
+    groups = (n + 7) // 8
+    sizes = groups * bw
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    gpre = np.concatenate([[0], np.cumsum(groups)]).astype(np.int64)
+    tab = np.empty(len(n), dtype=PAGE_DTYPE)
+    tab["row0"], tab["n"], tab["out_off"], tab["gpre"] = rows0, n, off[:-1], gpre[:-1]
+    dtab = torch.from_numpy(tab.view(np.uint8).copy()).to(device)
+    out = torch.empty(int(off[-1]) + 16, dtype=torch.uint8, device=device)
+    if int(gpre[-1]):
+        NL.check(NL.lib().hs_pq_pack(codes.data_ptr(), dtab.data_ptr(), len(tab), int(gpre[-1]),
+                                     bw, out.data_ptr(), NL.stream_ptr()), "hs_pq_pack")
+    return out, off
+
+
+def _values(dc: DeviceColumn, ph: _Phys):
+    """The column's stored values as written: int8/int16 widened to int32, decimals (float64
+    storage) as scaled int64 (exact for the precisions written: <= 18 digits), booleans as
+    int32 0/1 for the bit packer."""
+    import torch
+    v = dc.data
+    if ph.conv == "widen" or ph.conv == "bits":
+        return v.to(torch.int32)
+    if ph.conv == "decimal":
+        return torch.round(v.double() * float(10 ** ph.lp1)).to(torch.int64)
+    if ph.ptype == 6:
+        return v
+    return v.view(torch.int32 if ph.eb == 4 else torch.int64)
+
+
 def plan_columns(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: pa.Schema,
                  pages: np.ndarray, device) -> Optional[List[ColPlan]]:
-    """Encode every column on the device; None if some column needs the pyarrow writer."""
+    """Encode every column's pages on the device; None (reason in ``LAST_FALLBACK``) if some
+    column needs the pyarrow writer.  Nullable columns get definition-level bits per page and
+    only their non-null values encoded (RLE_DICTIONARY codes, PLAIN values or BOOLEAN bits)."""
     import torch
     plans = []
-    np_pages = pages
-    gpre = np.concatenate([[0], np.cumsum((np_pages["n"] + 7) // 8)]).astype(np.int64)
+    n_pg = pages["n"].astype(np.int64)
+    r0_pg = pages["row0"].astype(np.int64)
     for name in names:
         dc = cols[name]
-        phys = _physical(schema.field(name).type)
-        if phys is None:
+        t = schema.field(name).type
+        ph = _physical(t)
+        if ph is None:
+            LAST_FALLBACK["reason"] = f"column {name}: type {t}"
             return None
-        if dc.valid is not None and bool((dc.valid == 0).any().item()):
-            return None
-        ptype, logical, eb = phys
-        cp = ColPlan(name, ptype, logical, eb)
+        cp = ColPlan(name, ph)
+        v = _values(dc, ph)
+        # definition levels: compact the non-null values, page bounds in compacted positions
+        c0, m = r0_pg, n_pg
+        if dc.valid is not None:
+            vb = dc.valid != 0
+            cnt = torch.cumsum(vb.to(torch.int64), 0)
+            bounds = torch.from_numpy(np.concatenate([r0_pg, [r0_pg[-1] + n_pg[-1]]])).to(device)
+            at = torch.where(bounds > 0, cnt.index_select(0, (bounds - 1).clamp(min=0)),
+                             torch.zeros_like(bounds)).cpu().numpy()
+            c0 = at[:-1]
+            m = np.diff(at)
+            if int(m.sum()) < int(n_pg.sum()):
+                cp.nullable = True
+                lev, loff = _pack(vb.to(torch.int32), r0_pg, n_pg, 1, device)
+                cp.levels = _Seg(lev, loff)
+                v = v.index_select(0, torch.nonzero(vb).squeeze(1))
+        cp.nonnull = m
         codes = None
-        if ptype == 6:
+        if ph.ptype == 6:
             d = dc.dictionary
-            if d is None or len(d) == 0 or len(d) > DICT_MAX_STRINGS:
+            if d is None or len(d) > DICT_MAX_STRINGS:
+                LAST_FALLBACK["reason"] = f"column {name}: string dictionary over " \
+                                          f"{DICT_MAX_STRINGS} entries"
                 return None
-            codes = dc.data
-            cp.dict_page = _string_dict_page(d)
+            codes = v
+            cp.dict_page = _string_dict_page(d) if len(d) else np.zeros(0, np.uint8)
             cp.dict_count = len(d)
-        else:
-            v = dc.data.view(torch.int32 if eb == 4 else torch.int64)
-            n = v.numel()
-            step = max(1, n // SAMPLE)
+        elif ph.ptype == 0:
+            out, off = _pack(v, c0, m, 1, device)
+            cp.payload, cp.page_off = out, off
+        elif v.numel():
+            step = max(1, v.numel() // SAMPLE)
             u = torch.unique(v[::step])
             if 0 < u.numel() <= DICT_MAX // 2:
-                codes, missed = _dict_codes(v, eb, u, device)
+                codes, missed = _dict_codes(v, ph.eb, u, device)
                 if missed:
                     u = torch.unique(v)
                     codes = None
                     if u.numel() <= DICT_MAX:
-                        codes, _ = _dict_codes(v, eb, u, device)
+                        codes, _ = _dict_codes(v, ph.eb, u, device)
             if codes is not None:
                 cp.dict_page = u.cpu().numpy().view(np.uint8)
                 cp.dict_count = int(u.numel())
         if codes is not None:
             cp.dict = True
             cp.bw = _bit_width(cp.dict_count)
-            sizes = ((np_pages["n"] + 7) // 8) * cp.bw
-            cp.page_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
-            tab = np_pages.copy()
-            tab["out_off"] = cp.page_off[:-1]
-            tab["gpre"] = gpre[:-1]
-            dtab = torch.from_numpy(tab.view(np.uint8).copy()).to(device)
-            cp.payload = torch.empty(int(cp.page_off[-1]) + 16, dtype=torch.uint8, device=device)
-            NL.check(NL.lib().hs_pq_pack(codes.data_ptr(), dtab.data_ptr(), len(tab),
-                                         int(gpre[-1]), cp.bw, cp.payload.data_ptr(),
-                                         NL.stream_ptr()), "hs_pq_pack")
-        else:
-            cp.payload = dc.data.view(torch.uint8)
-            cp.page_off = np.concatenate([np_pages["row0"], [np_pages["row0"][-1] +
-                                                              np_pages["n"][-1]]]) * eb
+            cp.payload, cp.page_off = _pack(codes.to(torch.int32) if codes.dtype != torch.int32
+                                            else codes, c0, m, cp.bw, device)
+        elif ph.ptype != 0:
+            cp.payload = v.contiguous().view(torch.uint8) if v.numel() else \
+                torch.zeros(16, dtype=torch.uint8, device=device)
+            cp.page_off = np.concatenate([c0, [c0[-1] + m[-1]]]).astype(np.int64) * ph.eb
         plans.append(cp)
+    LAST_FALLBACK["reason"] = None
     return plans
 
 
-def page_table(bucket_off: np.ndarray, rg_rows: int) -> Tuple[np.ndarray, List[Tuple[int, int, int]]]:
-    """Pages (= row groups) of every non-empty bucket and, per bucket, (bucket, first page,
-    page count)."""
+# footer ``created_by`` of the paged writer: readers take the device page decode for such files
+CREATED_BY = "hyperspace_amd 2 (MI355X device-encoded, paged)"
+# rows per data page: ~0.5 MiB of 8-byte PLAIN values, so a compressed page is one
+# wavefront's inflate on the device read path (io/native_parquet.py upload_file_device)
+PAGE_ROWS = int(os.environ.get("HS_PQ_PAGE_ROWS", str(1 << 16)))
+
+
+def page_table(bucket_off: np.ndarray, rg_rows: int, page_rows: Optional[int] = None):
+    """Data pages of every non-empty bucket: (pages, files) with ``files`` = per bucket
+    (bucket, [(first page, page count, rows) per row group]).  Row groups hold ``rg_rows``
+    rows, pages at most ``page_rows``."""
     rows, files = [], []
+    page_rows = max(1, min(page_rows or PAGE_ROWS, rg_rows))
     for b in range(len(bucket_off) - 1):
         lo, hi = int(bucket_off[b]), int(bucket_off[b + 1])
         if hi <= lo:
             continue
-        first = len(rows)
-        for r0 in range(lo, hi, rg_rows):
-            rows.append((r0, min(rg_rows, hi - r0), 0, 0))
-        files.append((b, first, len(rows) - first))
+        rgs = []
+        for g0 in range(lo, hi, rg_rows):
+            g1 = min(g0 + rg_rows, hi)
+            first = len(rows)
+            for r0 in range(g0, g1, page_rows):
+                rows.append((r0, min(page_rows, g1 - r0), 0, 0))
+            rgs.append((first, len(rows) - first, g1 - g0))
+        files.append((b, rgs))
     return np.array(rows, dtype=PAGE_DTYPE), files
+
+
+def _file_pages(f) -> Tuple[int, int]:
+    """(first page, end page) of a file entry of ``page_table``."""
+    rgs = f[1]
+    return rgs[0][0], rgs[-1][0] + rgs[-1][1]
 
 
 def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: pa.Schema,
                   bucket_off: np.ndarray, path_of: Callable[[int], str], rg_rows: int, device,
                   chunk_bytes: int = 96 << 20, codec: str = "none") -> Optional[List[str]]:
     """Encode on the device and write one Parquet file per non-empty bucket; None when the
-    columns need the pyarrow writer.  ``codec`` "snappy" compresses every data page on the
-    device (``snappy_pages``) and dictionary pages on the host."""
+    columns need the pyarrow writer (reason in ``LAST_FALLBACK``).  ``codec`` "snappy"
+    compresses every page segment on the device (``snappy_pages``) and dictionary pages on the
+    host."""
     import torch
     from .staging import copy_stream, io_pool, pinned_pool
     if codec not in CODEC_IDS:
+        LAST_FALLBACK["reason"] = f"codec {codec}"
         return None
     cid = CODEC_IDS[codec]
     pages, files = page_table(bucket_off, rg_rows)
@@ -355,14 +485,21 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
         return None
     for cp in plans:
         cp.dict_z = snappy_stream_host(cp.dict_page) if cid == 1 and cp.dict else None
+    # every device segment: each column's values, then the level bits of nullable columns
+    segs = [cp for cp in plans] + [cp.levels for cp in plans if cp.levels is not None]
+    lev_index = {}
+    k = len(plans)
+    for ci, cp in enumerate(plans):
+        if cp.levels is not None:
+            lev_index[ci] = k
+            k += 1
     L = _writer()
     stream = copy_stream(device)
     stream.wait_stream(torch.cuda.current_stream(device))
-    # group files into ~chunk_bytes of encoded data per D2H batch
     batches, cur, cur_bytes = [], [], 0
     for f in files:
-        _, p0, pn = f
-        nb = sum(int(cp.page_off[p0 + pn] - cp.page_off[p0]) for cp in plans)
+        p0, p1 = _file_pages(f)
+        nb = sum(int(sg.page_off[p1] - sg.page_off[p0]) for sg in segs)
         if cur and cur_bytes + nb > chunk_bytes:
             batches.append(cur)
             cur, cur_bytes = [], 0
@@ -372,16 +509,13 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
         batches.append(cur)
     futs = []
     max_inflight = 2 * min(16, os.cpu_count() or 4)
-    created_by = b"hyperspace_amd (MI355X device-encoded)"
-    # Snappy: batches are compressed in groups of ~SNAPPY_GROUP_BYTES raw bytes, one launch each
-    # (tens of thousands of 64 KiB chunks keep every CU busy); each batch then copies its slice
-    # of the group's packed output
+    created_by = CREATED_BY.encode()
     groups = []
     if cid == 1:
         g, gb = [], 0
         for bi, batch in enumerate(batches):
-            nb = sum(int(cp.page_off[batch[-1][1] + batch[-1][2]] - cp.page_off[batch[0][1]])
-                     for cp in plans)
+            p0, p1 = _file_pages(batch[0])[0], _file_pages(batch[-1])[1]
+            nb = sum(int(sg.page_off[p1] - sg.page_off[p0]) for sg in segs)
             if g and gb + nb > SNAPPY_GROUP_BYTES:
                 groups.append(g)
                 g, gb = [], 0
@@ -395,16 +529,16 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
     zs = compress_stream(device) if cid == 1 else None
 
     def group_range(gi: int) -> Tuple[int, int]:
-        gb0, gb1 = batches[groups[gi][0]], batches[groups[gi][-1]]
-        return gb0[0][1], gb1[-1][1] + gb1[-1][2]
+        return _file_pages(batches[groups[gi][0]][0])[0], \
+            _file_pages(batches[groups[gi][-1]][-1])[1]
     for bi, batch in enumerate(batches):
         if len(futs) >= max_inflight:
             t_bp = time.perf_counter()
             futs[len(futs) - max_inflight].result()
             WRITE_PHASES["backpressure_s"] = WRITE_PHASES.get("backpressure_s", 0.0) + \
                 time.perf_counter() - t_bp
-        p_first = batch[0][1]
-        p_end = batch[-1][1] + batch[-1][2]
+        p_first = _file_pages(batch[0])[0]
+        p_end = _file_pages(batch[-1])[1]
         host = []
         zoff = zsize = None
         gfirst = 0
@@ -413,14 +547,11 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
                 gi = group_of[bi]
                 gfirst = group_range(gi)[0]
                 if zgroup[0] != gi:
-                    # compress this group (if not yet queued) and the next one on the
-                    # compression stream: group g+1 compresses while g's pages are copied out
-                    # and written
                     for gg in (gi, gi + 1):
                         if gg < len(groups) and gg not in launched:
                             zs.wait_stream(torch.cuda.current_stream(device))
                             with torch.cuda.stream(zs):
-                                launched[gg] = snappy_launch(plans, *group_range(gg), device)
+                                launched[gg] = snappy_launch(segs, *group_range(gg), device)
                     with torch.cuda.stream(zs):
                         res = snappy_finish(launched.pop(gi), device)
                         zev = torch.cuda.Event()
@@ -429,7 +560,7 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
                     res[0].record_stream(stream)
                     zgroup = (gi, res)
                 packed, zoff, zsize = zgroup[1]
-                for c in range(len(plans)):
+                for c in range(len(segs)):
                     lo = int(zoff[c][p_first - gfirst])
                     hi = int(zoff[c][p_end - 1 - gfirst] + zsize[c][p_end - 1 - gfirst])
                     h = pinned_pool().acquire(hi - lo)
@@ -437,54 +568,73 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
                         h[:hi - lo].copy_(packed[lo:hi], non_blocking=True)
                     host.append((h, lo))
             else:
-                for cp in plans:
-                    lo, hi = int(cp.page_off[p_first]), int(cp.page_off[p_end])
+                for sg in segs:
+                    lo, hi = int(sg.page_off[p_first]), int(sg.page_off[p_end])
                     h = pinned_pool().acquire(hi - lo)
                     if hi > lo:
-                        h[:hi - lo].copy_(cp.payload[lo:hi], non_blocking=True)
+                        h[:hi - lo].copy_(sg.payload[lo:hi], non_blocking=True)
                     host.append((h, lo))
             ev = torch.cuda.Event()
             ev.record(stream)
+
+        def seg_page(si: int, q: int, host=None, zoff=None, zsize=None, gfirst=0):
+            """(host address, bytes, raw bytes) of segment ``si`` of global page ``q``."""
+            sg = segs[si]
+            raw = int(sg.page_off[q + 1] - sg.page_off[q])
+            h, base = host[si]
+            if cid == 1:
+                j = q - gfirst
+                return h.data_ptr() + int(zoff[si][j]) - base, int(zsize[si][j]), raw
+            return h.data_ptr() + int(sg.page_off[q]) - base, raw, raw
 
         def write_batch(batch=batch, host=host, ev=ev, zoff=zoff, zsize=zsize, gfirst=gfirst):
             t_w = time.perf_counter()
             ev.synchronize()
             t_s = time.perf_counter()
             out = []
-            for b, p0, pn in batch:
-                arr = (WCol * (pn * len(plans)))()
-                rg = (C.c_int64 * pn)()
-                for g in range(pn):
-                    rg[g] = int(pages["n"][p0 + g])
+            for b, rgs in batch:
+                ncols, nrg = len(plans), len(rgs)
+                arr = (WCol2 * (nrg * ncols))()
+                rg = (C.c_int64 * nrg)()
+                keep = []
+                for g, (p0, pn, rows) in enumerate(rgs):
+                    rg[g] = rows
                     for c, cp in enumerate(plans):
-                        w = arr[g * len(plans) + c]
-                        raw = int(cp.page_off[p0 + g + 1] - cp.page_off[p0 + g])
+                        w = arr[g * ncols + c]
                         w.name = cp.bname
-                        w.ptype, w.logical = cp.ptype, cp.logical
+                        ph = cp.ph
+                        w.ptype, w.logical, w.lp0, w.lp1 = ph.ptype, ph.logical, ph.lp0, ph.lp1
                         w.dict, w.bit_width = int(cp.dict), cp.bw
-                        w.codec = cid
+                        w.codec, w.nullable = cid, int(cp.nullable)
                         if cp.dict:
                             dp = cp.dict_z if cid == 1 else cp.dict_page
                             w.dict_page = dp.ctypes.data
                             w.dict_bytes = dp.nbytes
                             w.dict_raw_bytes = cp.dict_page.nbytes
                             w.dict_count = cp.dict_count
-                        if cid == 1:
-                            j = p0 + g - gfirst
-                            h, base = host[c]
-                            w.payload = h.data_ptr() + int(zoff[c][j]) - base
-                            w.payload_bytes = int(zsize[c][j])
-                        else:
-                            h, base = host[c]
-                            w.payload = h.data_ptr() + int(cp.page_off[p0 + g]) - base
-                            w.payload_bytes = raw
-                        w.payload_raw_bytes = raw
+                        pgs = (WPage * pn)()
+                        nulls = 0
+                        for q in range(pn):
+                            pg = pgs[q]
+                            gq = p0 + q
+                            pg.nvals = int(pages["n"][gq])
+                            pg.nonnull = int(cp.nonnull[gq])
+                            nulls += pg.nvals - pg.nonnull
+                            pg.payload, pg.payload_bytes, pg.payload_raw = seg_page(
+                                c, gq, host, zoff, zsize, gfirst)
+                            if cp.levels is not None:
+                                pg.levels, pg.levels_bytes, pg.levels_raw = seg_page(
+                                    lev_index[c], gq, host, zoff, zsize, gfirst)
+                        keep.append(pgs)
+                        w.pages = C.cast(pgs, C.POINTER(WPage))
+                        w.npages = pn
+                        w.null_count = nulls
                 path = path_of(b)
-                rc = L.hs_pq_write_file(path.encode(), len(plans), pn, rg, arr, created_by)
+                rc = L.hs_pq_write_file2(path.encode(), ncols, nrg, rg, arr, created_by)
                 if rc != 0:
                     raise OSError(-rc, f"native Parquet write failed: {path}")
                 out.append(path)
-            for h, _ in host:   # written: the blocks can serve the next batch
+            for h, _ in host:
                 pinned_pool().release(h, torch.cuda.current_stream(device))
             with _WP_LOCK:
                 WRITE_PHASES["writer_wait_d2h_s"] = WRITE_PHASES.get("writer_wait_d2h_s", 0.0) + \
