@@ -1036,8 +1036,9 @@ class GpuBackend:
         return r.copy(table=hit[1])
 
     def _join_params(self, left: DRel, right: DRel, lk, rk, residual, extra_attrs=(),
-                     lconds=None):
-        col_info, descs = self._column_infos([(left, 0), (right, 8)])
+                     lconds=None, slots=None):
+        col_info, descs = slots if slots is not None else \
+            self._column_infos([(left, 0), (right, 8)])
         lslot = col_info(lk).slot
         rslot = col_info(rk).slot
         lb = CP.bind(CP.to_cnf(left.conds if lconds is None else lconds), col_info, self.device, 0)
@@ -1243,6 +1244,57 @@ class GpuBackend:
         proj = X.ProjectExec(list(child.output) + extra, child)
         return X.HashAggregateExec(groups, aggs, final.mode, final.child, final.result_attrs), proj
 
+    def _agg_prep_get(self, final) -> Optional["_ScanPrep"]:
+        """The prepared scan of a fused aggregate node submitted before (plan-cache hits
+        submit the same node objects with new literal values), while its table is resident."""
+        preps = self.__dict__.get("_agg_preps")
+        if not preps:
+            return None
+        pr = preps.get(id(final))
+        if pr is None or pr.final is not final or pr.placement != self._placement_tag() or \
+                not all(self.cache.holds(t) for t in pr.tables()):
+            return None
+        return pr
+
+    def _agg_prep_put(self, final, r: DRel) -> None:
+        """Keep what the fused scan of ``final`` lowered, for its next submission: only for a
+        relation of one resident table with no computed columns (their values are literal
+        dependent) whose lowering completed."""
+        st = getattr(self, "_scan_gs", None)
+        if st is None or r.parts or r.extra or r.split or \
+                getattr(r.table, "_hs_cache_key", None) is None:
+            return
+        col_info, descs, gs, p = st
+        preps = self.__dict__.setdefault("_agg_preps", {})
+        if len(preps) > 256:
+            preps.clear()
+        preps[id(final)] = _ScanPrep(final, r, col_info, descs, gs, p,
+                                     getattr(self, "_last_graph_prep", None),
+                                     self._placement_tag())
+
+    def _join_prep_put(self, final, node, res) -> None:
+        """Keep a co-located merge join aggregate's lowering (one left x right pair over full
+        bucket ranges, resident tables) for its next submission."""
+        rec = getattr(self, "_join_rec", None)
+        self._join_rec = None
+        if rec is None or res is None or rec[6] is None:
+            return
+        left, right, lk, rk, col_info, descs, launcher, specs = rec
+        for t in (left.table, right.table):
+            if getattr(t, "_hs_cache_key", None) is None:
+                return
+        preps = self.__dict__.setdefault("_agg_preps", {})
+        if len(preps) > 256:
+            preps.clear()
+        preps[id(final)] = _JoinPrep(final, node, left, right, lk, rk, col_info, descs,
+                                     launcher, res[4:], self._placement_tag(),
+                                     self._groups_agreed)
+
+    def _placement_tag(self):
+        d = self._dist()
+        return None if d is None else (d.rank, d.world, self.session.conf.get(
+            "spark.hyperspace.mi.bucketPlacement", "balanced"))
+
     def _dense_agg(self, final: X.HashAggregateExec, child: X.SparkPlan):
         """Queue a fused aggregate and return ``finish() -> pa.Table``.  Nothing here waits on
         the device: kernels, the cross-rank combine and the D2H of the tiny result block are
@@ -1259,14 +1311,29 @@ class GpuBackend:
             node = node.child
         self._groups_agreed = False
         res = None
-        if isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner":
+        prep = self._agg_prep_get(final)
+        if prep is not None:
+            try:
+                res = prep.run(self, fns, group)
+            except _Stale:
+                self._agg_preps.pop(id(final), None)
+                res = None
+        if res is not None:
+            pass
+        elif isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner":
             res = self._semi_join_agg(node, fns, group)
         if res is not None:
             pass
         elif isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner":
+            self._join_rec = None
             res = self._join_agg(node, fns, group)
+            self._join_prep_put(final, node, res)
         else:
-            res = self._scan_agg(self._rel(child), fns, group)
+            r = self._rel(child)
+            self._scan_gs = None
+            self._last_graph_prep = None
+            res = self._scan_agg(r, fns, group)
+            self._agg_prep_put(final, r)
         sums, cnts, mins, maxs, G, gbase, gdict, gtype = res
         d = self._dist()
         A = len(fns) + 1  # + implicit count(*)
@@ -1400,6 +1467,13 @@ class GpuBackend:
             raise _NeedHash("float group key")
         d = self._dist()
         multi = d is not None and d.world > 1
+        if c.valid is not None:
+            nulls = self._has_nulls(c)
+            if multi:
+                nulls = d.agree_any([nulls])[0]
+            if nulls:
+                # NULL is a group of its own (Spark): the hash-mode aggregate keys it
+                raise _NeedHash("nullable group key")
         gkey = getattr(r.table, "global_key", None) if r.table is not None else None
         if c.dictionary is not None:
             G = len(c.dictionary)
@@ -1435,6 +1509,19 @@ class GpuBackend:
             return None
         return None, max(G, 1), base, c.dictionary, c.atype
 
+    def _has_nulls(self, c: DeviceColumn) -> bool:
+        """Whether a device column holds a null (cached per resident column)."""
+        memo = self.__dict__.setdefault("_nulls_memo", {})
+        hit = memo.get(id(c))
+        if hit is not None and hit[0] is c:
+            return hit[1]
+        v = bool((c.valid == 0).any().item())
+        if not getattr(c, "hs_transient", False):
+            if len(memo) > 4096:
+                memo.clear()
+            memo[id(c)] = (c, v)
+        return v
+
     def _local_domain(self, c: DeviceColumn):
         """(min, max - min + 1) of an integer column on this rank; tables are immutable, so it
         is computed once per column."""
@@ -1463,8 +1550,17 @@ class GpuBackend:
             raise Unsupported("too many aggregates")
         return specs
 
-    def _scan_agg(self, r: DRel, fns, group):
-        col_info, descs = self._column_infos([(r, 0)])
+    def _scan_agg(self, r: DRel, fns, group, prep: Optional["_ScanPrep"] = None):
+        """Fused scan + filter + aggregate.  ``prep`` (a plan-cache hit submitting the same plan
+        nodes again, ``_dense_agg``) carries what does not depend on literal values - column
+        slots, group domain, compact encodings, the generated kernel, the captured graph and
+        the column argument slots - so only the literal-dependent work runs: range bounds,
+        predicate values, aggregate terms, the args block and the launch."""
+        if prep is None:
+            col_info, descs = self._column_infos([(r, 0)])
+        else:
+            col_info, descs = prep.col_info, prep.descs
+        nd = len(descs)
         implied: set = set()
         spec = self._range_spec(r, r.conds, implied)
         graph = self._graph_eligible(spec, descs)
@@ -1475,30 +1571,40 @@ class GpuBackend:
         bound = CP.bind(CP.to_cnf([c for c in r.conds if id(c) not in implied]), col_info,
                         self.device)
         specs = self._agg_specs(fns, col_info)
-        gs = self._group_spec(r, group, MAX_GROUPS_SCAN)
-        p = NL.ScanParams()
+        if prep is None:
+            gs = self._group_spec(r, group, MAX_GROUPS_SCAN)
+        else:
+            gs = prep.gs
+            if len(descs) != nd or (prep.graph is not None) != graph:
+                raise _Stale()
         if gs is None:  # empty group column
             return (*self._empty_agg(len(specs)), 1, 0, None, None)
         agreed, G, gbase, gdict, gtype = gs
         self._groups_agreed = agreed is True
-        # a single-valued group key runs the register-accumulating (ungrouped) kernel
-        p.group_col = col_info(group).slot if (group is not None and G > 1) else -1
-        p.num_groups, p.group_base = G, gbase
-        for s, c in descs.items():
-            p.cols[s] = c.desc()
+        if prep is None:
+            p = NL.ScanParams()
+            # a single-valued group key runs the register-accumulating (ungrouped) kernel
+            p.group_col = col_info(group).slot if (group is not None and G > 1) else -1
+            p.num_groups, p.group_base = G, gbase
+            for s_, c in descs.items():
+                p.cols[s_] = c.desc()
+        else:
+            p = prep.params
         for i, pr in enumerate(bound.preds):
             p.preds[i] = pr
         p.npreds = len(bound.preds)
         for i, a in enumerate(specs):
             p.aggs[i] = a
         p.naggs = len(specs)
+        self._scan_gs = (col_info, descs, gs, p)
         if bound.always_false:
             out = self._empty_agg(len(specs), G)
         elif graph:
             with stage("scan.graph"):
                 out = self._scan_agg_graph(r, p, spec,
                                            p.naggs * (p.num_groups if p.group_col >= 0 else 1),
-                                           descs, keep=bound.buffers)
+                                           descs, keep=bound.buffers,
+                                           prep=prep.graph if prep is not None else None)
         else:
             with stage("scan.agg_kernel"):
                 tp = K.ranges_to_tiles(rlen)
@@ -1518,25 +1624,16 @@ class GpuBackend:
         conf = self.session.conf
         return HyperspaceConf.codegen_enabled(conf) and HyperspaceConf.hipgraph_enabled(conf)
 
-    def _scan_agg_graph(self, r: DRel, p: NL.ScanParams, spec, GA: int, descs=None, keep=()):
+    def _scan_agg_graph(self, r: DRel, p: NL.ScanParams, spec, GA: int, descs=None, keep=(),
+                        prep: Optional["_GraphPrep"] = None):
         kc, lo, lo_incl, hi, hi_incl, _ = spec
-        t = r.table
-        nb = t.num_buckets
-        grid = jit.SCAN_GRID or NL.lib().hs_scan_grid()
-        compacts = self._compacts(descs or {})
-        vec = jit.scan_vec(p, compacts, t.num_rows)
-        shape = jit.scan_agg_shape(p, compacts, vec)
-        k = jit.kernel_for(shape, lambda: jit.gen_scan_agg(p, compacts, vec))
-        key = (shape, kc.data.data_ptr(), kc.valid.data_ptr() if kc.valid is not None else 0,
-               kc.hs_type, t.bucket_offsets.data_ptr(), nb, grid, GA)
-        shmem = GA * 32 if p.group_col >= 0 else 0
-        g = self.graphs.get(key, lambda: ScanAggGraph(k, kc.desc(), t.bucket_offsets, nb, grid,
-                                                      GA, shmem, self.device, vec))
-        values = g.values_template()
-        values.update({"num_groups": p.num_groups, "group_base": p.group_base,
-                       "nrows": t.num_rows})
-        jit._fill_common(values, p.cols, [(i, p.preds[i]) for i in range(p.npreds)],
-                         [p.aggs[i] for i in range(p.naggs)], compacts)
+        if prep is None or prep.GA != GA or self.graphs.peek(prep.key) is not prep.g:
+            prep = self._graph_prep(r, p, kc, GA, descs)
+            self._last_graph_prep = prep
+        g, k, compacts = prep.g, prep.k, prep.compacts
+        values = dict(prep.values)
+        jit.fill_preds_aggs(values, [(i, p.preds[i]) for i in range(p.npreds)],
+                            [p.aggs[i] for i in range(p.naggs)], compacts)
         side = self._scan_side_stream(g)
         if side is None:
             if g.on_side:
@@ -1571,6 +1668,27 @@ class GpuBackend:
         with torch.cuda.stream(side):
             handle = g.launch(range_bounds(lo, lo_incl, hi, hi_incl), k.args.pack(values))
         return (_GraphPending(g, handle), None, None, None)
+
+    def _graph_prep(self, r: DRel, p: NL.ScanParams, kc, GA: int, descs) -> "_GraphPrep":
+        """The literal-independent part of a graph-replayed scan: kernel, graph, and the args
+        slots of the columns and the graph's own buffers."""
+        t = r.table
+        nb = t.num_buckets
+        grid = jit.SCAN_GRID or NL.lib().hs_scan_grid()
+        compacts = self._compacts(descs or {})
+        vec = jit.scan_vec(p, compacts, t.num_rows)
+        shape = jit.scan_agg_shape(p, compacts, vec)
+        k = jit.kernel_for(shape, lambda: jit.gen_scan_agg(p, compacts, vec))
+        key = (shape, kc.data.data_ptr(), kc.valid.data_ptr() if kc.valid is not None else 0,
+               kc.hs_type, t.bucket_offsets.data_ptr(), nb, grid, GA)
+        shmem = GA * 32 if p.group_col >= 0 else 0
+        g = self.graphs.get(key, lambda: ScanAggGraph(k, kc.desc(), t.bucket_offsets, nb, grid,
+                                                      GA, shmem, self.device, vec))
+        values = g.values_template()
+        values.update({"num_groups": p.num_groups, "group_base": p.group_base,
+                       "nrows": t.num_rows})
+        jit._fill_cols(values, p.cols, compacts)
+        return _GraphPrep(key, g, k, compacts, values, GA)
 
     def _scan_side_stream(self, g):
         """The side stream warm scan pipelines replay on (None: replay on the current stream)."""
@@ -1728,6 +1846,8 @@ class GpuBackend:
             for rp in rparts:
                 part = self._join_agg_pair(node, lp, rp, lk, rk, fns, group, G, gbase)
                 out = part if out is None else _combine_aggs(out, part)
+        if len(lparts) * len(rparts) > 1:
+            self._join_rec = None       # a bucket union: no single replayable launch
         return (*out, G, gbase, gdict, gtype)
 
     def _group_spec_parts(self, parts, group, limit):
@@ -1796,10 +1916,16 @@ class GpuBackend:
                 fr = getattr(left.table, "_full_ranges", None)
                 comp = self._compacts(descs)
                 if jit.merge_join_ok(jp, comp, right.table.num_rows, left.table.num_rows):
-                    return jit.merge_join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets,
-                                              comp, nrows=left.table.num_rows,
-                                              cache_spans=fr is not None and rstart is fr[0],
-                                              rdup=jit.key_has_dups(right.col(rk)))
+                    jit.LAST_MJ_LAUNCHER[0] = None
+                    out = jit.merge_join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets,
+                                             comp, nrows=left.table.num_rows,
+                                             cache_spans=fr is not None and rstart is fr[0],
+                                             rdup=jit.key_has_dups(right.col(rk)))
+                    if fr is not None and rstart is fr[0] and probed is None and not implied:
+                        # full ranges, no probing: the launch can be replayed for this pair
+                        self._join_rec = (left, right, lk, rk, col_info, descs,
+                                          jit.LAST_MJ_LAUNCHER[0], specs)
+                    return out
                 return jit.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles,
                                     self._compacts(descs),
                                     cache_spans=fr is not None and rstart is fr[0])
@@ -2276,6 +2402,76 @@ def _eval_scalar(e, agg_val, attr_val):
             return a * b
         return None if b == 0 else a / b
     raise Unsupported(f"result expression {type(e).__name__}")
+
+
+class _Stale(Exception):
+    """A prepared lowering no longer matches the query (the normal path runs instead)."""
+
+
+class _GraphPrep:
+    __slots__ = ("key", "g", "k", "compacts", "values", "GA")
+
+    def __init__(self, key, g, k, compacts, values, GA):
+        self.key, self.g, self.k, self.compacts, self.values, self.GA = \
+            key, g, k, compacts, values, GA
+
+
+class _ScanPrep:
+    """Literal-independent lowering of a fused scan aggregate (GpuBackend._dense_agg)."""
+    __slots__ = ("final", "r", "col_info", "descs", "gs", "params", "graph", "placement")
+
+    def __init__(self, final, r, col_info, descs, gs, params, graph, placement):
+        self.final, self.r, self.col_info, self.descs, self.gs = final, r, col_info, descs, gs
+        self.params, self.graph, self.placement = params, graph, placement
+
+    def tables(self):
+        return (self.r.table,)
+
+    def run(self, be, fns, group):
+        return be._scan_agg(self.r, fns, group, self)
+
+
+class _JoinPrep:
+    """Literal-independent lowering of a co-located merge-join aggregate: the two resident
+    relations, column slots, group domain and the kernel launcher (jit.MergeJoinLauncher).
+    A submission re-binds the predicates and aggregate terms and launches."""
+    __slots__ = ("final", "node", "left", "right", "lk", "rk", "col_info", "descs", "launcher",
+                 "gtail", "placement", "agreed")
+
+    def __init__(self, final, node, left, right, lk, rk, col_info, descs, launcher, gtail,
+                 placement, agreed):
+        self.final, self.node, self.left, self.right = final, node, left, right
+        self.lk, self.rk, self.col_info, self.descs = lk, rk, col_info, descs
+        self.launcher, self.gtail, self.placement, self.agreed = launcher, gtail, placement, agreed
+
+    def tables(self):
+        return (self.left.table, self.right.table)
+
+    def run(self, be, fns, group):
+        left = self.left
+        if be._range_spec(left, left.conds) is not None:
+            raise _Stale()        # the new literals bound the left key: ranges change
+        nd = len(self.descs)
+        with stage("join.agg_kernel"):
+            jp, col_info, descs, keep = be._join_params(
+                left, self.right, self.lk, self.rk, self.node.condition,
+                slots=(self.col_info, self.descs))
+            specs = be._agg_specs(fns, col_info)
+            G, gbase = self.gtail[0], self.gtail[1]
+            if len(descs) != nd:
+                raise _Stale()
+            if keep[0].always_false or keep[1].always_false:
+                out = be._empty_agg(len(specs), G)
+            else:
+                for i, a in enumerate(specs):
+                    jp.aggs[i] = a
+                jp.naggs = len(specs)
+                if group is not None:
+                    jp.group_col = col_info(group).slot if G > 1 else -1
+                    jp.num_groups, jp.group_base = G, gbase
+                out = self.launcher.launch(jp)
+        be._groups_agreed = self.agreed
+        return (*out, *self.gtail)
 
 
 def _strip_exchange(p):

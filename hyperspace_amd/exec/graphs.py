@@ -239,6 +239,14 @@ class GraphCache:
                     side.synchronize()
         return g
 
+    def peek(self, key: tuple) -> Optional[ScanAggGraph]:
+        """The cached pipeline of ``key`` (touched as most recent), or None."""
+        with self._lock:
+            g = self._lru.get(key)
+            if g is not None:
+                self._lru.move_to_end(key)
+            return g
+
     def __len__(self):
         return len(self._lru)
 

@@ -980,6 +980,13 @@ def int_bounds(op: int, lit: float, scale: float) -> Tuple[int, int]:
 
 
 def _fill_common(v: Dict[str, object], cols, preds, aggs, compacts=None) -> None:
+    _fill_cols(v, cols, compacts)
+    fill_preds_aggs(v, preds, aggs, compacts)
+
+
+def _fill_cols(v: Dict[str, object], cols, compacts=None) -> None:
+    """Column argument slots (pointers, compact bases / scales): fixed for a resident table,
+    so a prepared query fills them once."""
     for s in range(NL.MAX_COLS):
         if cols[s].data:
             c = (compacts or {}).get(s)
@@ -998,6 +1005,10 @@ def _fill_common(v: Dict[str, object], cols, preds, aggs, compacts=None) -> None
                     v[f"RK{s}"] = rk.data_ptr()
                     v[f"GM{s}"] = c.gmask.data_ptr()
                     v[f"GR{s}"] = c.gruns.data_ptr()
+
+
+def fill_preds_aggs(v: Dict[str, object], preds, aggs, compacts=None) -> None:
+    """Literal-dependent argument slots: predicate values / code bounds and aggregate terms."""
     for k, p in preds:
         v[f"L{k}"] = p.ilit
         v[f"F{k}"] = p.flit
@@ -2080,19 +2091,43 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
         v.update(hk.values())
         k.launch(grid, v, NL.stream_ptr(), 0)
         return None
-    parts = _partials(grid, GA, dev)
     v = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
          "spans": spans.data_ptr(), "R": rstart.numel(), "nrows": nrows, "rdup": int(rdup),
-         "psum": parts[0].data_ptr(), "pcnt": parts[1].data_ptr(), "pmin": parts[2].data_ptr(),
-         "pmax": parts[3].data_ptr(), "num_groups": p.num_groups, "group_base": p.group_base,
+         "num_groups": p.num_groups, "group_base": p.group_base,
          "TR": tr.data_ptr() if tr is not None else 0}
-    _fill_common(v, p.cols, [(k_, p.preds[k_]) for k_ in range(p.npreds)],
-                 [p.aggs[i] for i in range(p.naggs)], compacts)
+    _fill_cols(v, p.cols, compacts)
     frame = _key32_frame(p, compacts)
     if frame is not None:
         v["KLO"], v["KSP"], v["KOF"] = frame
-    k.launch(grid, v, NL.stream_ptr(), GA * 32 if p.group_col >= 0 else 0)
-    return _final(parts, grid, GA, dev)
+    launcher = MergeJoinLauncher(k, grid, GA, GA * 32 if p.group_col >= 0 else 0, v, compacts,
+                                 (rstart, rlen, rbucket, roff, tp, spans, tr), dev)
+    LAST_MJ_LAUNCHER[0] = launcher
+    return launcher.launch(p)
+
+
+# the launcher merge_join_agg built last (GpuBackend keeps it for the query's next submission)
+LAST_MJ_LAUNCHER: list = [None]
+
+
+class MergeJoinLauncher:
+    """A merge-join aggregate lowered once - generated kernel, tile spans / run windows and the
+    column argument slots; ``launch(p)`` fills only the literal-dependent slots (predicate
+    values, aggregate terms) of ``p`` and queues the kernel and the partials fold."""
+    __slots__ = ("k", "grid", "GA", "shmem", "values", "compacts", "keep", "dev")
+
+    def __init__(self, k, grid, GA, shmem, values, compacts, keep, dev):
+        self.k, self.grid, self.GA, self.shmem = k, grid, GA, shmem
+        self.values, self.compacts, self.keep, self.dev = values, compacts, keep, dev
+
+    def launch(self, p: NL.JoinParams):
+        parts = _partials(self.grid, self.GA, self.dev)
+        v = dict(self.values)
+        v.update({"psum": parts[0].data_ptr(), "pcnt": parts[1].data_ptr(),
+                  "pmin": parts[2].data_ptr(), "pmax": parts[3].data_ptr()})
+        fill_preds_aggs(v, [(k_, p.preds[k_]) for k_ in range(p.npreds)],
+                        [p.aggs[i] for i in range(p.naggs)], self.compacts)
+        self.k.launch(self.grid, v, NL.stream_ptr(), self.shmem)
+        return _final(parts, self.grid, self.GA, self.dev)
 
 
 def _with_runs(p: NL.JoinParams, compacts):
