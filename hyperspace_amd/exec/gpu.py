@@ -112,6 +112,7 @@ class GpuBackend:
         self.cache = DeviceTableCache(HyperspaceConf.device_cache_bytes(session.conf))
         self.last_path = None
         self.fallback_reason = None
+        self.last_stream_passes = 0      # bucket-range passes of the last aggregate (0: resident)
         self.metrics: Dict[str, float] = {}
         self._cpu = None
         self._domains: Dict[tuple, tuple] = {}
@@ -215,8 +216,24 @@ class GpuBackend:
         if agg is not None:
             finish = self._exec_agg(*agg, order=order, limit=limit)
         else:
-            rel = self._rel(plan)
-            t = self._to_arrow_ranks(rel, plan.output)
+            self.last_stream_passes = 0
+            chunks = self._stream_chunks(plan)
+            if chunks is None:
+                t = self._to_arrow_ranks(self._rel(plan), plan.output)
+            else:
+                # rows of an index larger than the HBM budget: bucket range by bucket range,
+                # in the bucket-major order of the resident run
+                self.last_stream_passes = len(chunks)
+                pieces = []
+                try:
+                    for ch in chunks:
+                        self._bucket_chunk = ch
+                        self._drop_resident()
+                        pieces.append(self._to_arrow_ranks(self._rel(plan), plan.output))
+                finally:
+                    self._bucket_chunk = None
+                    self._drop_resident()
+                t = pa.concat_tables(pieces) if len(pieces) > 1 else pieces[0]
             finish = (lambda: t)
         if order is None and limit is None:
             return finish
@@ -244,6 +261,10 @@ class GpuBackend:
             return self._scan_memo(p)
         if isinstance(p, X.BucketUnionExec):
             return self._bucket_union(p)
+        if isinstance(p, X.ProjectExec):
+            sj = self._semi_project(p)
+            if sj is not None:
+                return sj
         if isinstance(p, (X.FilterExec, X.ProjectExec)):
             r = self._rel(p.child)
             if r.parts:
@@ -366,6 +387,7 @@ class GpuBackend:
         d = self._dist()
         tag = (d.rank, d.world, self.session.conf.get(
             "spark.hyperspace.mi.bucketPlacement", "balanced")) if d is not None else None
+        tag = (tag, getattr(self, "_bucket_chunk", None))
         memo = self.__dict__.setdefault("_scans", {})
         m = memo.get(id(p))
         if m is not None and m[0] is p and m[2] == tag and m[1].table is not None and \
@@ -393,8 +415,12 @@ class GpuBackend:
             load_cols = list(dict.fromkeys(cols + sort_cols))
             owners = self._owner_map(idx.num_buckets, world, files)
             owned = owners.owned(rank)
+            chunk = getattr(self, "_bucket_chunk", None)
+            if chunk is not None:
+                # bucket-range streaming (_streamed_agg): this pass holds buckets [lo, hi) only
+                owned = [b for b in owned if chunk[0] <= b < chunk[1]]
             table = self.cache.get(
-                files, load_cols, ("bucketed", rank, world, owners.key),
+                files, load_cols, ("bucketed", rank, world, owners.key, chunk),
                 lambda: seeded_index(files, load_cols, idx.num_buckets, rank, world, owned) or
                 load_bucketed_index(files, load_cols, idx.num_buckets, sort_cols, self.device,
                                     rank, world, owned))
@@ -1244,6 +1270,171 @@ class GpuBackend:
         proj = X.ProjectExec(list(child.output) + extra, child)
         return X.HashAggregateExec(groups, aggs, final.mode, final.child, final.result_attrs), proj
 
+    # ------------------------------------------------------------------------------------------
+    # Bucket-range streaming: indexes larger than the HBM budget
+    # ------------------------------------------------------------------------------------------
+    def _stream_chunks(self, child) -> Optional[List[tuple]]:
+        """Bucket ranges an aggregate over ``child`` runs in, one resident range at a time, when
+        its index scans would not fit ``deviceCacheBytes`` together; None when they fit or the
+        plan cannot be split by bucket (a non-index scan, indexes of different bucket counts,
+        a Hybrid Scan union, several ranks).  Every index of the plan is cut at the same bucket
+        boundaries, so a co-partitioned join joins bucket range to bucket range
+        (BucketUnionExec.scala:61-74 runs a bucketed plan partition by partition)."""
+        if self._dist() is not None:
+            return None
+        scans = child.collect(lambda x: isinstance(x, X.FileSourceScanExec))
+        # only operators that keep bucket b's rows inside bucket b: an Exchange (a join of
+        # sides bucketed on other keys) or a union would pair rows across bucket ranges
+        if not scans or child.collect(lambda x: not isinstance(
+                x, (X.FileSourceScanExec, X.FilterExec, X.ProjectExec, X.SortExec,
+                    X.SortMergeJoinExec))):
+            return None
+        nbs, per_bucket = set(), None
+        total = 0
+        for sc in scans:
+            rel = sc.relation
+            if not rel.is_index():
+                return None
+            files = rel.location.all_files()
+            nb = rel.index.num_buckets
+            if not self._all_bucket_files(rel.location, files, nb):
+                return None
+            nbs.add(nb)
+            memo = getattr(rel.location, "_hs_bucket_weights", None)
+            if memo is None or memo[0] != nb or memo[1] is not files:
+                from ..parallel.placement import bucket_weights
+                memo = (nb, files, bucket_weights(files, nb) * self.STREAM_EXPANSION)
+                rel.location._hs_bucket_weights = memo
+            w = memo[2]
+            per_bucket = w if per_bucket is None or len(per_bucket) != nb else per_bucket + w
+            total += float(w.sum())
+        budget = HyperspaceConf.device_cache_bytes(self.session.conf)
+        if len(nbs) != 1 or total <= budget:
+            return None
+        cap = max(budget // 2, 1)              # the pass's tables plus what queries derive
+        chunks, lo, acc = [], 0, 0.0
+        for b, wb in enumerate(per_bucket):
+            if acc and acc + wb > cap:
+                chunks.append((lo, b))
+                lo, acc = b, 0.0
+            acc += wb
+        chunks.append((lo, len(per_bucket)))
+        return chunks
+
+    # decoded bytes per byte of a (compressed, dictionary-encoded) index file: the resident
+    # estimate of a bucket for the streaming plan
+    STREAM_EXPANSION = 4.0
+
+    def _streamed_agg(self, final, child, fns, group, chunks):
+        """The aggregate as one pass per bucket range: each pass loads its range of every
+        index (evicting the previous one), runs the fused kernels and brings its partials to
+        the host, where they combine by group value."""
+        import torch
+        A = len(fns) + 1
+        acc: Dict[object, list] = {}
+        gtype = None
+        gdict_all = None
+        self.last_stream_passes = len(chunks)
+        try:
+            for ch in chunks:
+                self._bucket_chunk = ch
+                self._drop_resident()
+                node = child
+                while isinstance(node, X.ProjectExec) and \
+                        all(isinstance(e, E.Attribute) for e in node.project_list):
+                    node = node.child
+                if isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner":
+                    res = self._join_agg(node, fns, group)
+                else:
+                    res = self._scan_agg(self._rel(child), fns, group)
+                sums, cnts, mins, maxs, G, gbase, gdict, gt = res
+                if isinstance(sums, _GraphPending):
+                    host = sums.result()
+                elif isinstance(sums, np.ndarray):
+                    host = (sums, cnts, mins, maxs)
+                else:
+                    host = K.agg_to_host_async(sums, cnts, mins, maxs)()
+                gtype = gt if gt is not None else gtype
+                s_, c_, mn_, mx_ = (np.asarray(x).reshape(G, A) for x in host)
+                for g in range(G):
+                    if c_[g, A - 1] == 0 and group is not None:
+                        continue
+                    key = None
+                    if group is not None:
+                        key = gdict[gbase + g].as_py() if gdict is not None else gbase + g
+                    cur = acc.get(key)
+                    if cur is None:
+                        acc[key] = [s_[g].copy(), c_[g].copy(), mn_[g].copy(), mx_[g].copy()]
+                    else:
+                        cur[0] += s_[g]
+                        cur[1] += c_[g]
+                        cur[2] = np.minimum(cur[2], mn_[g])
+                        cur[3] = np.maximum(cur[3], mx_[g])
+                del res, sums, cnts, mins, maxs
+                torch.cuda.current_stream().synchronize()
+        finally:
+            self._bucket_chunk = None
+            self._drop_resident()
+        if group is None:
+            if None not in acc:
+                acc[None] = [np.zeros(A), np.zeros(A, np.int64), np.full(A, np.inf),
+                             np.full(A, -np.inf)]
+            keys = [None]
+        else:
+            keys = sorted(acc)
+            if gtype is not None and pa.types.is_string(gtype):
+                gdict_all = pa.array(keys, type=pa.string())
+        G = max(len(keys), 1)
+        host = tuple(np.concatenate([acc[k][i] for k in keys]) if keys else
+                     np.zeros(A) for i in range(4))
+        if group is not None and gdict_all is None:
+            # integer group values: lay the rows out over their own domain order
+            gvals = keys
+            gbase = 0
+
+            def finish() -> pa.Table:
+                return self._agg_table_values(final, fns, group, host, G, A, gvals, gtype)
+            return finish
+        gbase = 0
+        gd = gdict_all
+
+        def finish() -> pa.Table:
+            return self._agg_table(final, fns, group, host, G, A, gbase, gd, gtype)
+        return finish
+
+    def _drop_resident(self) -> None:
+        """Release every device table this backend holds: the cache and the per-table memos
+        (scan nodes, null flags, domains, prepared submissions) that keep tables alive."""
+        self.cache.clear()
+        for memo in ("_scans", "_nulls_memo"):
+            self.__dict__.pop(memo, None)
+        self._domains.clear()
+        preps = getattr(self, "_agg_preps", None)
+        if preps:
+            preps.clear()
+        self._join_rec = None
+
+    def _agg_table_values(self, final, fns, group, host, G, A, gvals, gtype) -> pa.Table:
+        """``_agg_table`` over explicit integer group values (row g has group ``gvals[g]``)."""
+        s, c, mn, mx = (x.reshape(G, A) for x in host)
+        rows = [g for g in range(G) if c[g, A - 1] > 0]
+        vals = {}
+        for i, fn in enumerate(fns):
+            vals[id(fn)] = [CP.finalize_value(fn, s[g, i], c[g, i], mn[g, i], mx[g, i]) for g in rows]
+        raw = [gvals[g] for g in rows]
+        if pa.types.is_date32(gtype):
+            gv = pa.array(np.array(raw, dtype=np.int32)).view(pa.date32()).to_pylist()
+        else:
+            gv = raw
+        out_cols = [self._agg_output(e, group, gv, vals, len(rows)) for e in final.aggregates]
+        arrays = []
+        for a, vlist in zip(final.output, out_cols):
+            try:
+                arrays.append(pa.array(vlist, type=a.data_type))
+            except (pa.ArrowInvalid, pa.ArrowTypeError):
+                arrays.append(pa.array(vlist))
+        return pa.Table.from_arrays(arrays, names=[a.name for a in final.output])
+
     def _agg_prep_get(self, final) -> Optional["_ScanPrep"]:
         """The prepared scan of a fused aggregate node submitted before (plan-cache hits
         submit the same node objects with new literal values), while its table is resident."""
@@ -1310,6 +1501,10 @@ class GpuBackend:
         while isinstance(node, X.ProjectExec) and all(isinstance(e, E.Attribute) for e in node.project_list):
             node = node.child
         self._groups_agreed = False
+        self.last_stream_passes = 0
+        chunks = self._stream_chunks(child)
+        if chunks is not None:
+            return self._streamed_agg(final, child, fns, group, chunks)
         res = None
         prep = self._agg_prep_get(final)
         if prep is not None:
@@ -1786,6 +1981,64 @@ class GpuBackend:
         self.last_semi_join = {"build_keys": int(keys.data.numel()), "bitmap_bits": nbits}
         with stage("semi.probe"):
             return self._scan_agg(prel.copy(conds=prel.conds + [cond]), fns, group)
+
+    def _semi_project(self, p: X.ProjectExec) -> Optional[DRel]:
+        """``Project <- Filter* <- inner join`` whose projection and filters read one side only:
+        that side filtered by a bitmap of the other side's (unique) keys - a semi-join, no
+        row pairs materialized (TPC-H Q3's customer x orders feeding the lineitem join).  None
+        when the shape does not qualify or the other side's keys repeat."""
+        filters, node = [], p.child
+        while isinstance(node, X.FilterExec):
+            filters.append(node)
+            node = node.child
+        if not (isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner" and
+                node.condition is None and len(node.left_keys) == 1):
+            return None
+        conf = self.session.conf
+        if not HyperspaceConf.codegen_enabled(conf) or \
+                str(conf.get("spark.hyperspace.mi.semiJoinBitmap.enabled", "true")).lower() != "true":
+            return None
+        failed = self.__dict__.setdefault("_semi_failed", {})
+        if failed.get(id(node)) is node:
+            return None
+        need = set()
+        for e in p.project_list:
+            need.update(a.expr_id for a in e.references())
+        for f in filters:
+            need.update(a.expr_id for a in f.condition.references())
+        lk, rk = node.left_keys[0], node.right_keys[0]
+        if not (isinstance(lk, E.Attribute) and isinstance(rk, E.Attribute)) or \
+                not all(pa.types.is_integer(a.data_type) for a in (lk, rk)):
+            return None
+        cands = []
+        for probe, build, pk, bk in ((node.right, node.left, rk, lk),
+                                     (node.left, node.right, lk, rk)):
+            if need <= {a.expr_id for a in probe.output}:
+                cands.append((_plan_bytes(build), probe, build, pk, bk))
+        if not cands:
+            return None
+        _, probe, build, pk, bk = min(cands, key=lambda x: x[0])
+        binner = _strip_exchange(build) or build
+        pinner = _strip_exchange(probe) or probe
+        with stage("semi.build"):
+            brel = self._rel(binner)
+            if brel.parts:
+                return None
+            keys = self._materialize(brel, [bk])[bk.expr_id]
+            bm = self._semi_bitmap(keys)
+        if bm is None:
+            if len(failed) > 256:
+                failed.clear()
+            failed[id(node)] = node
+            return None
+        words, lo, nbits = bm
+        r = self._rel(pinner)
+        if r.parts:
+            return None
+        r = r.copy(conds=r.conds + [CP.KeyBitmap(pk, words, lo, nbits)])
+        for f in reversed(filters):
+            r = self._unary(f, r)
+        return self._unary(p, r)
 
     def _semi_bitmap(self, keys: DeviceColumn):
         """(words, lo, nbits) of the build keys over every rank's keys, or None when they are
