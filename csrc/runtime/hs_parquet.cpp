@@ -9,9 +9,13 @@
 // csrc/kernels/parquet_decode.hip.  Dictionary-encoded data therefore crosses PCIe at its
 // encoded width (e.g. 6 bits per TPC-H l_quantity instead of 64).
 //
-// Scope: flat schemas (no repetition), physical types INT32 / INT64 / FLOAT / DOUBLE,
-// encodings PLAIN and PLAIN_DICTIONARY / RLE_DICTIONARY, data pages V1 and V2.  Anything else
-// returns HS_PQ_UNSUPPORTED and the Python side reads that column with pyarrow instead.
+// Scope: flat schemas (no repetition), optional or required columns (definition levels), data
+// pages V1 and V2.  Physical types INT32 / INT64 / FLOAT / DOUBLE (PLAIN and dictionary
+// encodings; the INT32 / INT64 logical types DATE, TIMESTAMP, DECIMAL and INT8/16 included),
+// BOOLEAN (bit-packed PLAIN or RLE), BYTE_ARRAY (dictionary-encoded chunks: the dictionary page
+// parses on the host, hs_pq_plain_strings, and the codes decode on the device).  Anything else (INT96,
+// FIXED_LEN_BYTE_ARRAY, DELTA_* encodings, codecs other than SNAPPY / UNCOMPRESSED) returns
+// HS_PQ_UNSUPPORTED and the Python side reads that column with pyarrow instead.
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>

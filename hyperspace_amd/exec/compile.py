@@ -413,7 +413,19 @@ def finalize_value(fn: E.AggregateFunction, s: float, c: int, mn: float, mx: flo
     t = fn.child.data_type
     if isinstance(fn, (E.Min, E.Max)) and pa.types.is_date32(t):
         return datetime.date(1970, 1, 1) + datetime.timedelta(days=int(v))
+    if isinstance(fn, (E.Min, E.Max)) and _int_coded(t):
+        # timestamps / times / durations / date64 aggregate as their int64 counts
+        return pa.array([int(round(v))], pa.int64()).cast(t)[0].as_py()
+    if isinstance(fn, (E.Min, E.Max)) and pa.types.is_decimal(t):
+        import decimal
+        return decimal.Decimal(int(round(v * 10 ** t.scale))).scaleb(-t.scale)
     return float(v)
+
+
+def _int_coded(t: pa.DataType) -> bool:
+    """Arrow types stored as int64 counts of a unit (besides plain integers)."""
+    return (pa.types.is_timestamp(t) or pa.types.is_date64(t) or pa.types.is_time(t) or
+            pa.types.is_duration(t))
 
 
 __all__ = ["Unsupported", "to_cnf", "bind", "ColumnInfo", "agg_spec", "finalize_value",

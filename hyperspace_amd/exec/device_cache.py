@@ -19,7 +19,6 @@ from typing import Dict, List, Optional
 
 import numpy as np
 import pyarrow as pa
-import pyarrow.compute as pc
 import pyarrow.parquet as pq
 
 from ..io.writer import get_bucket_id
@@ -252,10 +251,9 @@ def load_bucketed_index(files, columns: List[str], num_buckets: int, sort_cols: 
                                   parquet_local=[P.to_local(p) for p in paths],
                                   device_pages=paged)
         cols = dict(up.columns)
-        for name, chunks in up.host_strings.items():
-            arr = pa.chunked_array(chunks, type=chunks[0].type)
-            d = pc.unique(arr.combine_chunks().drop_null()).sort()
-            cols[name] = DeviceColumn.from_arrow(arr, device, d)
+        # string columns -> int32 codes over one sorted dictionary: device-decoded files'
+        # upload-local codes are remapped on the device, host-decoded files' are looked up
+        staging.finish_strings(up, cols, device, None)
         cols = {c: cols[c] for c in columns}
     off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
     n = int(off[-1])

@@ -2526,6 +2526,11 @@ def _finalize_array(fn, s, c, mn, mx) -> pa.Array:
     t = fn.child.data_type
     if isinstance(fn, (E.Min, E.Max)) and pa.types.is_date32(t):
         return pa.array(np.rint(v).astype(np.int32), mask=null).view(pa.date32())
+    if isinstance(fn, (E.Min, E.Max)) and CP._int_coded(t):
+        return pa.array(np.rint(v).astype(np.int64), mask=null).cast(t)
+    if isinstance(fn, (E.Min, E.Max)) and pa.types.is_decimal(t):
+        return pa.array([CP.finalize_value(fn, 0.0, 1, x, x) if not nl else None
+                         for x, nl in zip(v, null)], type=t)
     return pa.array(v.astype(np.float64), mask=null)
 
 

@@ -2066,6 +2066,12 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
     runs = None
     if not rdup:
         compacts, runs = _with_runs(p, compacts)
+    if hk is None and runs is not None:
+        from . import jit_runs
+        two = jit_runs.lower(p, rstart, rlen, rbucket, roff, compacts, runs, nrows, cache_spans)
+        if two is not None:
+            LAST_MJ_LAUNCHER[0] = two
+            return two.launch(p)
     if hk is None and runs is None:
         compacts = _with_key16(p, compacts)
     NI = _mj_items(runs is not None)  # noqa: N806
@@ -2508,7 +2514,8 @@ def _vec_aligned_ptrs(ptrs) -> bool:
 
 def _compacted_tail(args, cols, split, approx, aggs, grouped, group_col, third, allslots,
                     NI: int, ind: str, with_j: bool = True, pass_fmt: str = "pass{it}",
-                    j_fmt: str = "j{it}", dump: bool = False, hk=None) -> List[str]:
+                    j_fmt: str = "j{it}", dump: bool = False, hk=None,
+                    jgroup: bool = False) -> List[str]:
     """Phase 3 over the passing rows only.  A join like TPC-H Q3 keeps a few percent of its
     rows, so decoding and accumulating all NI x 64 rows of a wavefront (branch-free) is mostly
     wasted VALU work: instead each lane appends its passing (row, j) pairs to a per-wavefront
@@ -2543,12 +2550,16 @@ def _compacted_tail(args, cols, split, approx, aggs, grouped, group_col, third, 
     g = _Gen(args, cols, split, ("crow", "cj"), approx, True)
     # every slot the aggregates and the group key read, re-loaded at the listed rows (the
     # phase-1/2 registers belong to the original, uncompacted rows)
-    tail = list(dict.fromkeys(_agg_slots(aggs) + ([group_col] if grouped else []) +
+    tail = list(dict.fromkeys(_agg_slots(aggs) + ([group_col] if grouped and not jgroup else []) +
                               (hk.slots if hk is not None else [])))
     for sl in tail:
         _uload(g, sl, "c", b, ind2)
     gvar = "gic"
-    if grouped:
+    if jgroup:
+        # the listed j is the row's group index itself (jit_runs: a right-side group key's code
+        # carried in the run tag)
+        b.append(f"{ind2}const int {gvar} = cok ? (int)cj : 0;")
+    elif grouped:
         base = args.add("q", "group_base", "long long")
         ng = args.add("q", "num_groups", "long long")
         b.append(f"{ind2}const i64 glc = (i64){_rename(f'x{group_col}', allslots, 'c')} - {base};")

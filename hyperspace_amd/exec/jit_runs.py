@@ -1,0 +1,361 @@
+"""Two-phase run-keyed merge join + aggregate (the MI355X form of a co-located bucketed
+SortMergeJoin whose right key is unique: JoinIndexRule.scala:63-69).
+
+The left key is in its run-length form (exec/encoding.RunCompact: per 64-row group a run-start
+mask ``gmask`` and the first row's run ``gruns``, plus one key per run ``runkeys``).  Instead of
+one kernel that stages, matches and aggregates per tile, the join is split by what each phase
+streams:
+
+1. ``hs_jit_run_tags`` - per merge-join tile, the tile's right key span is staged in LDS with
+   the right side's predicates evaluated once per right row; each thread matches a contiguous
+   chunk of the tile's runs (one LDS binary search, then a walk) and writes a W-bit **tag** per
+   run into a bitmap: 0 = no (passing) right row, else 1 (ungrouped / left-grouped) or the
+   right-side group code + 1.  Tags are assembled in LDS and leave as whole 32-bit words (only
+   a tile's two edge words use an atomic OR).  It reads the run keys, the right keys and the
+   right predicate columns once: ~1.5 GB at TPC-H SF100.
+2. ``hs_jit_run_scan`` - a streaming scan of the left rows (vector loads, no LDS staging, no
+   barriers): row -> run index from the group mask by one popcount, tag from the bitmap (the
+   NI rows of a thread touch one or a few adjacent words), left predicates, and the compacted
+   aggregate tail over the passing rows only.
+
+Both phases are plain streams, so each runs near the HBM roofline; the single-kernel form
+(jit.gen_merge_join_agg) keeps a long chain of dependent round trips per tile.  The two-phase
+form applies when no aggregate input comes from the right side, every right predicate reads
+only right columns, and a right-side group key (if any) has at most 255 groups."""
+from __future__ import annotations
+
+from typing import List, Optional
+
+from ..ops import _lib as NL
+from . import jit as J
+
+SPLIT = 8
+RT_UNROLL = 4
+# 2 phases on by default; HS_JIT_MJ_2P=0 keeps the single-kernel merge join
+import os  # noqa: E402
+MJ_2P = os.environ.get("HS_JIT_MJ_2P", "1") == "1"
+RS_ITEMS = int(os.environ.get("HS_JIT_RS_ITEMS", "16"))
+
+
+def tag_width(p: NL.JoinParams) -> int:
+    """Bits per run tag, or 0 when the two-phase form does not apply to ``p``."""
+    if p.group_col >= SPLIT:
+        if p.num_groups > 255:
+            return 0
+        for w in (1, 2, 4, 8):
+            if p.num_groups + 1 <= (1 << w):
+                return w
+    return 1
+
+
+def applies(p: NL.JoinParams) -> bool:
+    if not MJ_2P:
+        return False
+    for i in range(p.naggs):
+        a = p.aggs[i]
+        if any(a.col[t] >= SPLIT for t in range(a.nterms)) and a.kind != NL.AK_COUNT_STAR:
+            return False
+    if not J._right_only(p, SPLIT):
+        return False
+    if p.group_col >= SPLIT and p.cols[p.group_col].valid:
+        return False
+    return tag_width(p) > 0
+
+
+def _rpreds(p):
+    return [(k, p.preds[k]) for k in range(p.nlp, p.npreds)]
+
+
+def _lpreds(p):
+    return [(k, p.preds[k]) for k in range(p.nlp)]
+
+
+def tags_shape(p: NL.JoinParams, compacts, W: int, T: int) -> tuple:
+    cols = tuple(sorted((s, c) for s, c in J._col_specs(p, compacts).items()
+                        if s >= SPLIT or s == p.lkey))
+    preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
+                   p.preds[k].group) for k in range(p.nlp, p.npreds))
+    return ("run_tags", cols, preds, p.nlp, p.lkey, p.rkey, p.group_col >= SPLIT and p.group_col,
+            W, T, J.MJ_LDS_KEYS, RT_UNROLL, J.BLOCK)
+
+
+def gen_run_tags(p: NL.JoinParams, compacts, W: int, T: int) -> J.Kernel:
+    """Phase 1 (module docstring).  ``T`` = left rows per merge-join tile (its runs <= T)."""
+    args = J.Args()
+    for n, ct in (("tile_prefix", "const long long*"), ("spans", "const long long*"),
+                  ("TR", "const int*")):
+        args.add("p", n, ct)
+    lk, rk = p.lkey, p.rkey
+    args.add("p", f"RK{lk}", "const int*")
+    args.add("p", "tags", "unsigned*")
+    args.add("q", "R", "long long")
+    for n in ("KLO", "KSP", "KOF"):
+        args.add("q", n, "long long")
+    cols = J._col_specs(p, compacts)
+    rpreds = _rpreds(p)
+    rgroup = p.group_col >= SPLIT
+    stage_slots = list(dict.fromkeys([rk] + J._pred_slots(rpreds) +
+                                     ([p.group_col] if rgroup else [])))
+    LK = J.MJ_LDS_KEYS  # noqa: N806 — right span keys staged per tile (longer: HBM search)
+    BLOCK = J.BLOCK  # noqa: N806
+    U = RT_UNROLL  # noqa: N806
+    NW = (T * W + 31) // 32 + 2  # noqa: N806 — LDS tag words of one tile
+    MASK = (1 << W) - 1  # noqa: N806
+    g = J._Gen(args, cols, SPLIT, ("row0", "row0"), frozenset(), True)
+    if rgroup:
+        gb = args.add("q", "group_base", "long long")
+        ng = args.add("q", "num_groups", "long long")
+
+    def rimg(val: str) -> str:
+        return (f"({{ const i64 d_ = (i64)({val}) - a.KLO; "
+                f"d_ < 0 ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }})")
+
+    def tag_expr(gen: J._Gen, it, ok: str) -> str:
+        cond = J._rename(gen.cnf(rpreds), stage_slots, it)
+        if not rgroup:
+            return f"(({ok}) && {cond} ? 1u : 0u)"
+        gx = J._rename(f"x{p.group_col}", stage_slots, it)
+        return (f"({{ const i64 gl_ = (i64){gx} - {gb}; (({ok}) && {cond} && gl_ >= 0 && "
+                f"gl_ < {ng}) ? (unsigned)(gl_ + 1) : 0u; }})")
+
+    b: List[str] = [
+        f"  __shared__ unsigned skeys[{LK + 1}]; __shared__ unsigned char stag[{LK}];",
+        f"  __shared__ unsigned lrk_[{T}]; __shared__ unsigned tw_[{NW}];"]
+    b += J._TILE_HEAD
+    b += ["  for (i64 t = t0; t < t1; ++t) {",
+          "    const i64 ss = a.spans[4 * t + 2], se = a.spans[4 * t + 3];",
+          "    const int ra = a.TR[2 * t], nl = a.TR[2 * t + 1];",
+          "    const int ns = (int)(se - ss);",
+          f"    const bool staged = ns <= {LK};",
+          f"    const i64 wlo = ((i64)ra * {W}) >> 5;",
+          f"    const int nw = (int)((((i64)(ra + nl) * {W} + 31) >> 5) - wlo);",
+          f"    for (int q = (int)threadIdx.x; q < nw; q += {BLOCK}) tw_[q] = 0u;",
+          f"    for (int q = (int)threadIdx.x; q < nl; q += {BLOCK}) "
+          f"lrk_[q] = (unsigned)a.RK{lk}[ra + q] + (unsigned)a.KOF;"]
+    ind = "      "
+    rkv = J._valid_expr(g, rk, "{r}")
+    b.append(f"    if (staged) for (int sqb = 0; sqb < ns; sqb += {BLOCK * U}) {{")
+    for u in range(U):
+        b += [f"{ind}const int sq{u} = sqb + {u * BLOCK} + (int)threadIdx.x;",
+              f"{ind}const bool sv{u} = sq{u} < ns;",
+              f"{ind}const i64 jr{u} = ss + (sv{u} ? sq{u} : 0);"]
+    for u in range(U):
+        gs = J._Gen(args, cols, SPLIT, (f"jr{u}", f"jr{u}"), frozenset(), True)
+        for sl in stage_slots:
+            J._uload(gs, sl, f"s{u}", b, ind)
+    for u in range(U):
+        gs = J._Gen(args, cols, SPLIT, (f"jr{u}", f"jr{u}"), frozenset(), True)
+        kv = f"n{rk}_s{u}" if cols[rk][1] else "true"
+        b += [f"{ind}if (sv{u}) {{ const bool kv = {kv};",
+              f"{ind}  skeys[sq{u}] = kv ? {rimg(f'x{rk}_s{u}')} : 0u;",
+              f"{ind}  stag[sq{u}] = (unsigned char){tag_expr(gs, f's{u}', 'kv')}; }}"]
+    b += ["    }",
+          "    if (staged && threadIdx.x == 0) skeys[ns] = 0xFFFFFFFFu;   // walk sentinel",
+          "    __syncthreads();",
+          # each thread: a contiguous chunk of the tile's runs
+          f"    {{ const int c_ = (nl + {BLOCK - 1}) / {BLOCK};",
+          "      const int q0 = (int)threadIdx.x * c_;",
+          "      const int q1 = q0 + c_ < nl ? q0 + c_ : nl;",
+          "      int cw = -1; unsigned cb = 0u;",
+          "      int j_ = 0;",
+          "      if (staged && q0 < q1) { const unsigned key_ = lrk_[q0]; int lo = 0;",
+          "        for (int st = ns > 0 ? (1 << (31 - __builtin_clz(ns))) : 0; st > 0; st >>= 1) {",
+          "          const int c = lo + st; lo = (c <= ns && skeys[c - 1] < key_) ? c : lo; }",
+          "        j_ = lo; }",
+          "      for (int q = q0; q < q1; ++q) {",
+          "        const unsigned key_ = lrk_[q];",
+          "        unsigned tg = 0u;",
+          "        if (staged) {",
+          "          if (skeys[j_] < key_) { ++j_;",
+          "            if (skeys[j_] < key_) { int lo = j_ + 1, hi = ns;",
+          "              while (lo < hi) { const int m = (lo + hi) >> 1; "
+          "if (skeys[m] < key_) lo = m + 1; else hi = m; }",
+          "              j_ = lo; } }",
+          "          tg = (j_ < ns && skeys[j_] == key_) ? (unsigned)stag[j_] : 0u;",
+          "        } else {",
+          "          i64 lo = ss, hi = se;",
+          f"          while (lo < hi) {{ const i64 md = (lo + hi) >> 1; const bool nv = "
+          f"{rkv.format(r='md')};",
+          f"            if (nv || {rimg(g.value(rk, 'md'))} < key_) lo = md + 1; else hi = md; }}",
+          f"          const bool hit = lo < se && !({rkv.format(r='lo')}) && "
+          f"{rimg(g.value(rk, 'lo'))} == key_;",
+          "          const i64 jg = hit ? lo : ss;"]
+    gg = J._Gen(args, cols, SPLIT, ("jg", "jg"), frozenset(), True)
+    for sl in stage_slots:
+        J._uload(gg, sl, "g", b, "          ")
+    b += [f"          tg = {tag_expr(gg, 'g', 'hit')};",
+          "        }",
+          f"        const i64 bit = (i64)(ra + q) * {W};",
+          "        const int wi = (int)((bit >> 5) - wlo);",
+          "        if (wi != cw) { if (cb) atomicOr(&tw_[cw], cb); cw = wi; cb = 0u; }",
+          f"        cb |= (tg & {MASK}u) << (unsigned)(bit & 31);",
+          "      }",
+          "      if (cb) atomicOr(&tw_[cw], cb);",
+          "    }",
+          "    __syncthreads();",
+          # whole words leave with plain stores; the tile's edge words (shared with the
+          # neighbouring tiles' runs) with an OR into the zeroed bitmap
+          f"    for (int q = (int)threadIdx.x; q < nw; q += {BLOCK}) {{",
+          "      const i64 gw = wlo + q; const unsigned v = tw_[q];",
+          f"      const bool whole = gw * 32 >= (i64)ra * {W} && gw * 32 + 32 <= (i64)(ra + nl) * {W};",
+          "      if (whole) a.tags[gw] = v; else if (v) atomicOr(&a.tags[gw], v);",
+          "    }",
+          "    __syncthreads();",
+          "  }"]
+    src = (J._PRELUDE + args.struct_src() +
+           f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_run_tags(Args a) {{\n' +
+           "\n".join(b) + "\n}\n")
+    return J.Kernel(src, "hs_jit_run_tags", args)
+
+
+def scan_shape(p: NL.JoinParams, compacts, W: int, NI: int) -> tuple:
+    cols = tuple(sorted((s, c) for s, c in J._col_specs(p, compacts).items() if s < SPLIT))
+    preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
+                   p.preds[k].group) for k in range(p.nlp))
+    aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
+                 for i in range(p.naggs))
+    return ("run_scan", cols, preds, aggs, p.group_col, p.lkey, W, NI, J.BLOCK, J.WAVE_SYNC,
+            J.VEC_PREFETCH)
+
+
+def gen_run_scan(p: NL.JoinParams, compacts, W: int, NI: int) -> J.Kernel:
+    """Phase 2 (module docstring): the left rows' scan with the run-tag test."""
+    args = J.Args()
+    for n, ct in (("rstart", "const long long*"), ("rlen", "const long long*"),
+                  ("tile_prefix", "const long long*")):
+        args.add("p", n, ct)
+    lk = p.lkey
+    args.add("p", f"GM{lk}", "const unsigned long long*")
+    args.add("p", f"GR{lk}", "const int*")
+    args.add("p", "tags", "const unsigned*")
+    args.add("q", "R", "long long")
+    args.add("q", "nrows", "long long")
+    J._common_args(args)
+    cols = J._col_specs(p, compacts)
+    lpreds = _lpreds(p)
+    aggs = [p.aggs[i] for i in range(p.naggs)]
+    grouped = p.group_col >= 0
+    rgroup = p.group_col >= SPLIT
+    pslots = J._pred_slots(lpreds)
+    tail = J._agg_slots(aggs) + ([p.group_col] if grouped and not rgroup else [])
+    allslots = list(dict.fromkeys(pslots + tail))
+    approx = J._sum_only_slots(lpreds, aggs, -1 if rgroup else p.group_col, cols)
+    BLOCK = J.BLOCK  # noqa: N806
+    T = BLOCK * NI  # noqa: N806
+    MASK = (1 << W) - 1  # noqa: N806
+    KW = ((31 + (NI - 1) * W) >> 5) + 1  # noqa: N806 — tag words a thread's rows can touch
+    ind = "    "
+    g1 = J._Gen(args, cols, SPLIT, ("row0", "row0"), approx, True)
+    b: List[str] = []
+    b += J._acc_decls(aggs, grouped, args)
+
+    def body(b: List[str], full: bool) -> None:
+        J._vec_load_slots(b, g1, pslots, NI, ind)
+        for it in range(NI):
+            gi = J._Gen(args, cols, SPLIT, (f"row{it}", f"row{it}"), approx, True)
+            b.append(f"{ind}bool pass{it} = act{it} && "
+                     f"{J._rename(gi.cnf(lpreds), allslots, it)};")
+        # row -> run: the thread's NI rows lie in one 64-row group (NI | 64, g0 % NI == 0)
+        b += [f"{ind}const int sh_ = (int)(g0 & 63);",
+              f"{ind}const i64 r0_ = (i64)gr_ + (i64)__popcll(gm_ & ((2ull << sh_) - 2ull));",
+              f"{ind}const unsigned gl_ = (unsigned)(gm_ >> sh_);",
+              f"{ind}const i64 b0_ = r0_ * {W};",
+              f"{ind}const i64 w0_ = b0_ >> 5;",
+              f"{ind}" + " ".join(f"const unsigned tw{k}_ = a.tags[w0_ + {k}];" for k in range(KW))]
+        for it in range(NI):
+            ri = "0" if it == 0 else f"(int)__popc(gl_ & {(2 << it) - 2}u)"
+            b.append(f"{ind}{{ const int rel = (int)(b0_ & 31) + {ri} * {W};")
+            sel = f"tw{KW - 1}_"
+            for k in reversed(range(KW - 1)):
+                sel = f"((rel >> 5) == {k} ? tw{k}_ : {sel})"
+            b += [f"{ind}  const unsigned tg = ({sel} >> (unsigned)(rel & 31)) & {MASK}u;",
+                  f"{ind}  pass{it} = pass{it} && tg != 0u;",
+                  f"{ind}  jg{it} = (int)tg - 1; }}"]
+        b.extend(J._compacted_tail(args, cols, SPLIT, approx, aggs, grouped, p.group_col,
+                                   tail, allslots, NI, ind, with_j=rgroup, j_fmt="jg{it}",
+                                   jgroup=rgroup))
+
+    def body_decl(b: List[str], full: bool) -> None:
+        b.append(f"{ind}int " + ", ".join(f"jg{it} = 0" for it in range(NI)) + ";")
+        body(b, full)
+
+    gi = "((G0 < a.nrows ? G0 : a.nrows - 1) >> 6)"
+    J._vec_tiles(b, T, NI, ind, J._vec_loads(g1, pslots),
+                 [("gm_", "unsigned long long", f"a.GM{lk}[{gi}]"),
+                  ("gr_", "int", f"a.GR{lk}[{gi}]")], body_decl)
+    b += ["  }"]
+    b += J._flush(aggs, grouped)
+    Wv = BLOCK // 64  # noqa: N806
+    pre = [f"  typedef {J._crow_t(T)} crow_t; __shared__ crow_t crow_s[{Wv}][{64 * NI}];",
+           "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;"]
+    if rgroup:
+        pre.append(f"  __shared__ int cj_s[{Wv}][{64 * NI}];")
+    src = (J._PRELUDE + args.struct_src() +
+           f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_run_scan(Args a) {{\n' +
+           "\n".join(pre + b) + "\n}\n")
+    lds = (len(aggs) * p.num_groups * 32) if grouped else 0
+    return J.Kernel(src, "hs_jit_run_scan", args, lds)
+
+
+class TwoPhaseLauncher:
+    """Both phases lowered once (kernels, tiles, spans, per-tile run windows, the tag bitmap);
+    ``launch(p)`` fills the literal slots and queues: bitmap clear, tags, scan, partials fold."""
+    __slots__ = ("kt", "ks", "grid_t", "grid_s", "GA", "shmem", "vt", "vs", "compacts", "keep",
+                 "tags", "dev")
+
+    def __init__(self, kt, ks, grid_t, grid_s, GA, shmem, vt, vs, compacts, keep, tags, dev):
+        self.kt, self.ks, self.grid_t, self.grid_s = kt, ks, grid_t, grid_s
+        self.GA, self.shmem, self.vt, self.vs = GA, shmem, vt, vs
+        self.compacts, self.keep, self.tags, self.dev = compacts, keep, tags, dev
+
+    def launch(self, p: NL.JoinParams):
+        preds = [(k_, p.preds[k_]) for k_ in range(p.npreds)]
+        aggs = [p.aggs[i] for i in range(p.naggs)]
+        vt = dict(self.vt)
+        J.fill_preds_aggs(vt, preds, [], self.compacts)
+        self.tags.zero_()
+        st = NL.stream_ptr()
+        self.kt.launch(self.grid_t, vt, st)
+        parts = J._partials(self.grid_s, self.GA, self.dev)
+        vs = dict(self.vs)
+        vs.update({"psum": parts[0].data_ptr(), "pcnt": parts[1].data_ptr(),
+                   "pmin": parts[2].data_ptr(), "pmax": parts[3].data_ptr()})
+        J.fill_preds_aggs(vs, preds, aggs, self.compacts)
+        self.ks.launch(self.grid_s, vs, st, self.shmem)
+        return J._final(parts, self.grid_s, self.GA, self.dev)
+
+
+def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: int,
+          cache_spans: bool) -> Optional[TwoPhaseLauncher]:
+    """The two-phase launcher of a run-keyed merge join, or None when it does not apply."""
+    import torch
+    if not applies(p) or runs is None:
+        return None
+    W = tag_width(p)
+    NI = RS_ITEMS if RS_ITEMS and 64 % RS_ITEMS == 0 else J._mj_items(True)
+    T = J.BLOCK * NI  # noqa: N806
+    dev = rstart.device
+    max_tiles = nrows // T + 2 * rstart.numel() + 2
+    tp, spans = J._join_spans(p, rstart, rlen, rbucket, roff, max_tiles, T, cache_spans, align=NI)
+    tr = J._tile_runs(tp, spans, rstart.numel(), runs, max_tiles, cache_spans)
+    kt = J.kernel_for(tags_shape(p, compacts, W, T), lambda: gen_run_tags(p, compacts, W, T))
+    ks = J.kernel_for(scan_shape(p, compacts, W, NI), lambda: gen_run_scan(p, compacts, W, NI))
+    nruns = int(runs.runkeys.numel())
+    KW = ((31 + (NI - 1) * W) >> 5) + 1  # noqa: N806
+    tags = torch.empty(((nruns * W + 31) >> 5) + KW + 2, dtype=torch.int32, device=dev)
+    frame = J._key32_frame(p, compacts)
+    vt = {"tile_prefix": tp.data_ptr(), "spans": spans.data_ptr(), "TR": tr.data_ptr(),
+          "tags": tags.data_ptr(), "R": rstart.numel(),
+          "num_groups": p.num_groups, "group_base": p.group_base}
+    vt["KLO"], vt["KSP"], vt["KOF"] = frame
+    J._fill_cols(vt, p.cols, compacts)
+    vs = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
+          "tags": tags.data_ptr(), "R": rstart.numel(), "nrows": nrows,
+          "num_groups": p.num_groups, "group_base": p.group_base}
+    J._fill_cols(vs, p.cols, compacts)
+    GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
+    grid_t = max(1, J.MJ_GRID)
+    grid_s = max(1, J.SCAN_GRID or NL.lib().hs_scan_grid())
+    return TwoPhaseLauncher(kt, ks, grid_t, grid_s, GA, GA * 32 if p.group_col >= 0 else 0,
+                            vt, vs, compacts, (rstart, rlen, rbucket, roff, tp, spans, tr, runs),
+                            tags, dev)

@@ -11,6 +11,14 @@ covering-index files the MI355X engine serves from, used the way a CPU engine wo
   hash-joined and partially aggregated by one task of a thread pool, partials merged at the end.
 * The un-indexed alternative (the same queries over the source Parquet files) is measured too,
   and the baseline is the better of the two (VERDICT r2 "what's weak" 5).
+* ``--warm`` (the default since round 4): the same two plans over Arrow tables already RESIDENT
+  in host RAM (the index columns each query reads, loaded once before timing, split into
+  record batches for the thread pool) - the CPU counterpart of the MI355X engine serving
+  HBM-resident columns, with no file read or decode inside the timed queries.  Q6 is Acero's
+  multithreaded filter + project over the in-memory dataset with the same row-group pruning
+  done by the batches' min/max (batches are sorted by l_shipdate inside every bucket); Q3 is the
+  bucketed hash join per resident bucket pair on the thread pool.  The baseline is the best of
+  warm / cold / unindexed per query.
 
 Writes ``profiles/cpu_baseline_sf<SF>.json`` (the ``vs_baseline`` denominator of bench.py).
 Run it where the bench's data and indexes exist (the GPU box, after bench.py), e.g.
@@ -104,6 +112,76 @@ def q3_unindexed(li_ds, od_ds, i: int):
     return dict(zip(g["p"].to_pylist(), zip(g["r_sum"].to_pylist(), g["r_count"].to_pylist())))
 
 
+class WarmQ6:
+    """Resident ``li_shipdate`` columns as record batches with their l_shipdate ranges, so a
+    query touches only batches that can hold its year (the in-memory form of row-group
+    pruning)."""
+
+    COLS = ["l_shipdate", "l_discount", "l_quantity", "l_extendedprice"]
+
+    def __init__(self, files, batch_rows: int = 1 << 20):
+        self.batches = []
+        for f in sorted(files):
+            t = ds.dataset(f, format="parquet").to_table(columns=self.COLS)
+            for b in t.combine_chunks().to_batches(max_chunksize=batch_rows):
+                mm = pc.min_max(b.column(0))
+                self.batches.append((mm["min"].as_py(), mm["max"].as_py(), b))
+
+    def __call__(self, pool, i: int) -> float:
+        lo, hi, dlo, dhi, qty = q6_lits(i)
+
+        def part(b):
+            d = b.column(0)
+            m = pc.and_(pc.and_(pc.greater_equal(d, pa.scalar(lo)), pc.less(d, pa.scalar(hi))),
+                        pc.and_(pc.and_(pc.greater_equal(b.column(1), dlo),
+                                        pc.less_equal(b.column(1), dhi)),
+                                pc.less(b.column(2), qty)))
+            t = b.filter(m)
+            return pc.sum(pc.multiply(t.column(3), t.column(1))).as_py() or 0.0
+        live = [b for mn, mx, b in self.batches if mx is not None and mx >= lo and mn < hi]
+        return sum(pool.map(part, live))
+
+
+class WarmQ3:
+    """Resident bucket pairs of ``li_orderkey`` / ``ord_orderkey`` (the Q3 columns), joined
+    bucket by bucket on the thread pool."""
+
+    def __init__(self, li_buckets, od_buckets):
+        self.pairs = []
+        for b in sorted(li_buckets):
+            if b not in od_buckets:
+                continue
+            li = ds.dataset(li_buckets[b], format="parquet").to_table(
+                columns=["l_orderkey", "l_extendedprice", "l_discount", "l_shipdate"])
+            od = ds.dataset(od_buckets[b], format="parquet").to_table(
+                columns=["o_orderkey", "o_orderdate", "o_shippriority"])
+            self.pairs.append((li.combine_chunks(), od.combine_chunks()))
+
+    @staticmethod
+    def _part(li, od, dd):
+        li = li.filter(pc.greater(li["l_shipdate"], pa.scalar(dd)))
+        od = od.filter(pc.less(od["o_orderdate"], pa.scalar(dd)))
+        if not li.num_rows or not od.num_rows:
+            return {}
+        j = li.select(["l_orderkey", "l_extendedprice", "l_discount"]).join(
+            od.select(["o_orderkey", "o_shippriority"]), keys="l_orderkey",
+            right_keys="o_orderkey", join_type="inner", use_threads=False)
+        rev = pc.multiply(j["l_extendedprice"], pc.subtract(1.0, j["l_discount"]))
+        g = pa.table({"p": j["o_shippriority"], "r": rev}).group_by("p").aggregate(
+            [("r", "sum"), ("r", "count")])
+        return {p: (r, n) for p, r, n in zip(g["p"].to_pylist(), g["r_sum"].to_pylist(),
+                                             g["r_count"].to_pylist())}
+
+    def __call__(self, pool, i: int):
+        dd = q3_date(i)
+        out = {}
+        for part in pool.map(lambda x: self._part(x[0], x[1], dd), self.pairs):
+            for p, (r, n) in part.items():
+                a = out.get(p, (0.0, 0))
+                out[p] = (a[0] + r, a[1] + n)
+        return out
+
+
 def _bucket_files(index_dir: str):
     out = {}
     for f in glob.glob(os.path.join(index_dir, "**", "*.parquet"), recursive=True):
@@ -130,6 +208,8 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--skip-unindexed", action="store_true")
+    ap.add_argument("--no-warm", action="store_true",
+                    help="skip the resident-table (warm) plans")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     pa.set_cpu_count(args.threads)
@@ -156,6 +236,26 @@ def main():
     print(f"[cpu_baseline] q3 indexed {res['q3_indexed_s']:.3f}s", file=sys.stderr, flush=True)
     step = res["q6_indexed_s"] + res["q3_indexed_s"]
     source = "indexed"
+    best6, best3 = res["q6_indexed_s"], res["q3_indexed_s"]
+    if not args.no_warm:
+        t0 = time.perf_counter()
+        w6, w3 = WarmQ6(ship), WarmQ3(li_b, od_b)
+        res["warm_load_s"] = time.perf_counter() - t0
+        with cf.ThreadPoolExecutor(args.threads) as pool:
+            # same answers as the cold plans
+            a6 = q6(ship_ds, 1)
+            assert abs(w6(pool, 1) - a6) <= 1e-9 * max(abs(a6), 1.0)
+            c3 = q3_bucketed(pool, li_b, od_b, 1)
+            g3 = w3(pool, 1)
+            assert sorted(c3) == sorted(g3) and all(
+                c3[k][1] == g3[k][1] and abs(c3[k][0] - g3[k][0]) <= 1e-9 * abs(c3[k][0])
+                for k in c3), (c3, g3)
+            res["q6_warm_s"], _ = _timed(lambda i: w6(pool, i), args.reps)
+            res["q3_warm_s"], _ = _timed(lambda i: w3(pool, i), args.reps)
+        print(f"[cpu_baseline] warm q6 {res['q6_warm_s']:.3f}s q3 {res['q3_warm_s']:.3f}s",
+              file=sys.stderr, flush=True)
+        best6, best3 = min(best6, res["q6_warm_s"]), min(best3, res["q3_warm_s"])
+        del w6, w3
     if not args.skip_unindexed:
         li_ds = ds.dataset(os.path.join(data, "lineitem"), format="parquet")
         od_ds = ds.dataset(os.path.join(data, "orders"), format="parquet")
@@ -175,11 +275,11 @@ def main():
             a3[k][1] == b3[k][1] and abs(a3[k][0] - b3[k][0]) <= 1e-9 * abs(b3[k][0])
             for k in b3), (a3, b3)
         res["results_match"] = True
-        # the better of the two per query
-        q6b = min(res["q6_indexed_s"], res["q6_unindexed_s"])
-        q3b = min(res["q3_indexed_s"], res["q3_unindexed_s"])
-        if q6b + q3b < step:
-            step, source = q6b + q3b, "best of indexed / unindexed per query"
+        best6 = min(best6, res["q6_unindexed_s"])
+        best3 = min(best3, res["q3_unindexed_s"])
+    if best6 + best3 < step:
+        # the best plan per query
+        step, source = best6 + best3, "best of warm-resident / indexed / unindexed per query"
     stop.set()
     out = {"metric": "queries/s (CPU baseline: one Q6 + one Q3 per step)",
            "value": round(2.0 / step, 4), "unit": "queries/s", "ms_per_step": round(step * 1e3, 2),

@@ -95,14 +95,18 @@ def main():
     p.naggs, p.lkey, p.rkey, p.key_is_float, p.group_col = 2, 0, 8, 0, -1
     p.num_groups, p.group_base = 1, 0
     rstart, rlen, rbk = K.full_ranges(loff, dev)
+    from hyperspace_amd.exec import jit_runs
     configs = json.loads(args.configs)
-    base = {k: getattr(jit, k) for cfg in configs for k in cfg}
+
+    def mod(k):     # knobs of the two-phase form live in exec/jit_runs.py
+        return jit_runs if hasattr(jit_runs, k) and not hasattr(jit, k) else jit
+    base = {k: getattr(mod(k), k) for cfg in configs for k in cfg}
     ref = None
     for cfg in configs:
         for k, v in base.items():
-            setattr(jit, k, v)
+            setattr(mod(k), k, v)
         for k, v in cfg.items():
-            setattr(jit, k, v)
+            setattr(mod(k), k, v)
         jit._KERNELS.clear()
 
         def run():
@@ -124,7 +128,7 @@ def main():
         print(json.dumps({"cfg": cfg, "ms": round(ms, 4), "sum": s_, "count": n_, "match": ok}),
               flush=True)
     for k, v in base.items():
-        setattr(jit, k, v)
+        setattr(mod(k), k, v)
 
 
 if __name__ == "__main__":

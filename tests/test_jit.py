@@ -197,6 +197,23 @@ def test_generated_sources_compile_with_compact_columns(rt, tmp_path):
     assert "vload<int, 8>(a.c0" not in kr.src and "a.rdup" not in kr.src
     assert jit.merge_join_shape(_q3_params(), cr) != jit.merge_join_shape(_q3_params(), c32)
     ks.append(kr)
+    # two-phase form (exec/jit_runs.py): run tags, then the left scan with the tag test
+    from hyperspace_amd.exec import jit_runs
+    q3 = _q3_params()
+    assert jit_runs.applies(q3) and jit_runs.tag_width(q3) == 1
+    for g, G, W in ((-1, 1, 1), (10, 1, 1), (10, 3, 2), (10, 200, 8), (1, 4, 1)):
+        q3.group_col, q3.num_groups = g, G
+        if g == 10:
+            q3.cols[10] = _fake(NL.I32)
+        assert jit_runs.tag_width(q3) == W
+        kt = jit_runs.gen_run_tags(q3, cr, W, 4096)
+        kq = jit_runs.gen_run_scan(q3, cr, W, 16)
+        assert "a.tags[gw]" in kt.src and "a.RK0[" in kt.src and "a.c2" not in kt.src
+        assert "a.GM0[" in kq.src and "a.tags[w0_" in kq.src and "a.c8" not in kq.src
+        ks += [kt, kq]
+    q3.group_col, q3.num_groups = 10, 300
+    assert not jit_runs.applies(q3)
+    q3.group_col = -1
     assert "st9_s" in ks[0].src          # phase 2 staged through LDS
     assert "a.rbm" in ks[1].src and "a.c9" not in ks[1].src   # phase 2 = bitmap tests
     for k in ks:
@@ -793,7 +810,8 @@ def test_merge_join_runs_matches_oracle(device):
     ref = runs_torch(comp[0].codes.cpu())
     for a, b_ in zip((rc.runkeys, rc.gmask, rc.gruns), ref):
         assert torch.equal(a.cpu(), b_)
-    lds_keys, runs = jit.MJ_LDS_KEYS, jit.MJ_RUNS
+    from hyperspace_amd.exec import jit_runs
+    lds_keys, runs, two2 = jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P
     try:
         for starts, lens in ((loff[:-1], loff[1:] - loff[:-1]),
                              (loff[:-1] + 5, loff[1:] - loff[:-1] - 9)):
@@ -809,13 +827,15 @@ def test_merge_join_runs_matches_oracle(device):
             rbk = torch.arange(B, dtype=torch.int32, device=device)
             roff_t = torch.from_numpy(roff).to(device)
             for keys in (lds_keys, 32):
-                for use_runs in (True, False):
-                    jit.MJ_LDS_KEYS, jit.MJ_RUNS = keys, use_runs
+                for use_runs, two in ((True, True), (True, False), (False, False)):
+                    jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P = keys, use_runs, two
                     got = [t.cpu().numpy() for t in
                            jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, comp, nrows=len(lk),
                                               rdup=False)]
                     s_, c_ = got[0].reshape(3, 2)[:, 0], got[1].reshape(3, 2)[:, 1]
-                    assert (c_ == exp_c).all(), (keys, use_runs, c_, exp_c)
-                    assert np.allclose(s_, exp_s, rtol=1e-12), (keys, use_runs)
+                    assert (c_ == exp_c).all(), (keys, use_runs, two, c_, exp_c)
+                    assert np.allclose(s_, exp_s, rtol=1e-12), (keys, use_runs, two)
+                    if two:
+                        assert isinstance(jit.LAST_MJ_LAUNCHER[0], jit_runs.TwoPhaseLauncher)
     finally:
-        jit.MJ_LDS_KEYS, jit.MJ_RUNS = lds_keys, runs
+        jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P = lds_keys, runs, two2
