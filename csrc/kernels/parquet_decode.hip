@@ -559,6 +559,54 @@ __device__ void expand_bool(const HsPqPage& p, const uint8_t* __restrict__ pg, i
   }
 }
 
+// PLAIN BYTE_ARRAY data page (eb 16): `nv` length-prefixed values (4-byte little-endian length,
+// then the bytes) -> per value the device address of its first byte (uint64 at p.out) and its
+// length (int32 at p.dict).  The offsets are one dependent chain, so one lane walks it, 1024
+// values per round into LDS, and the workgroup writes them out coalesced; the page's bytes stay
+// where the inflate left them (the caller keeps the scratch alive until the strings are
+// hashed: io/native_parquet.StringCodes.finish_plain).
+__device__ void expand_plain_strings(const HsPqPage& p, const uint8_t* __restrict__ pg, int nv,
+                                     int* __restrict__ status) {
+  __shared__ int s_off[1024];
+  __shared__ int s_len[1024];
+  __shared__ int s_meta[2];
+  uint64_t* optr = (uint64_t*)p.out;
+  int32_t* olen = (int32_t*)p.dict;
+  const int n = p.usize;
+  int voff = 0;
+  if (p.kind == 0 && p.levels) voff = 4 + (int)load_u32_at(pg, 0);
+  else if (p.kind == 1) voff = p.levels;
+  if (voff < 0 || voff > n) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
+  int64_t q = voff;                       // lane 0's walk position
+  int done = 0;
+  while (done < nv) {
+    if (threadIdx.x == 0) {
+      int k = 0, err = 0;
+      while (k < 1024 && done + k < nv) {
+        if (q + 4 > n) { err = 1; break; }
+        const int64_t l = (int64_t)load_u32_at(pg, q);
+        q += 4;
+        if (l > n - q) { err = 1; break; }
+        s_off[k] = (int)q;
+        s_len[k] = (int)l;
+        q += l;
+        ++k;
+      }
+      s_meta[0] = k;
+      s_meta[1] = err;
+    }
+    __syncthreads();
+    const int k = s_meta[0];
+    if (s_meta[1]) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
+    for (int i = threadIdx.x; i < k; i += blockDim.x) {
+      optr[done + i] = (uint64_t)(uintptr_t)(pg + s_off[i]);
+      olen[done + i] = s_len[i];
+    }
+    __syncthreads();
+    done += k;
+  }
+}
+
 // Block-wide sum of one int per thread (256 threads: 4 wavefronts).
 __device__ __forceinline__ int block_sum(int v, int* __restrict__ s_part) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -700,14 +748,18 @@ __global__ __launch_bounds__(256) void hs_pq_expand_kernel(
     if (nv < 0 || nv > p.nvals) { if (threadIdx.x == 0) atomicOr(status, kErrCorrupt); return; }
   }
   if (nv > 0) {
-    if (p.eb == 4) expand_page<uint32_t>(p, pg, pages, nv, status);
+    if (p.eb == 16) expand_plain_strings(p, pg, nv, status);
+    else if (p.eb == 4) expand_page<uint32_t>(p, pg, pages, nv, status);
     else if (p.eb == 8) expand_page<uint64_t>(p, pg, pages, nv, status);
     else if (p.eb == 1) expand_bool(p, pg, nv, status);
     else if (threadIdx.x == 0) atomicOr(status, kErrCorrupt);
   }
   if (!p.nulls) return;
   __syncthreads();
-  if (p.eb == 4) spread_nulls<uint32_t>((uint32_t*)p.out, valid, p.nvals, nv);
+  if (p.eb == 16) {                        // (address, length) pairs; nulls get (0, 0)
+    spread_nulls<uint64_t>((uint64_t*)p.out, valid, p.nvals, nv);
+    spread_nulls<uint32_t>((uint32_t*)p.dict, valid, p.nvals, nv);
+  } else if (p.eb == 4) spread_nulls<uint32_t>((uint32_t*)p.out, valid, p.nvals, nv);
   else if (p.eb == 8) spread_nulls<uint64_t>((uint64_t*)p.out, valid, p.nvals, nv);
   else if (p.eb == 1) spread_nulls<uint8_t>((uint8_t*)p.out, valid, p.nvals, nv);
 }

@@ -12,8 +12,9 @@
 // Scope: flat schemas (no repetition), optional or required columns (definition levels), data
 // pages V1 and V2.  Physical types INT32 / INT64 / FLOAT / DOUBLE (PLAIN and dictionary
 // encodings; the INT32 / INT64 logical types DATE, TIMESTAMP, DECIMAL and INT8/16 included),
-// BOOLEAN (bit-packed PLAIN or RLE), BYTE_ARRAY (dictionary-encoded chunks: the dictionary page
-// parses on the host, hs_pq_plain_strings, and the codes decode on the device).  Anything else (INT96,
+// BOOLEAN (bit-packed PLAIN or RLE), BYTE_ARRAY (dictionary pages parse on the host,
+// hs_pq_plain_strings, and the codes decode on the device; PLAIN data pages decode on the device
+// to value addresses + lengths, hashed into codes afterwards).  Anything else (INT96,
 // FIXED_LEN_BYTE_ARRAY, DELTA_* encodings, codecs other than SNAPPY / UNCOMPRESSED) returns
 // HS_PQ_UNSUPPORTED and the Python side reads that column with pyarrow instead.
 #include <fcntl.h>
@@ -442,6 +443,7 @@ constexpr int kHostDictMin = 64 << 10;
 constexpr int64_t kDeviceInflateMax = 2 << 20;   // largest page a wavefront inflates
 std::atomic<int> g_host_inflate{2};   // hs_pq_set_host_inflate
 std::atomic<int> g_device_nulls{1};   // hs_pq_set_device_nulls
+std::atomic<int> g_plain_strings{1};  // hs_pq_set_plain_strings
 
 // Parse an RLE/bit-packed hybrid stream of `count` values into runs (dst starts at `dst0`).
 // `base` is the stream's byte offset in the chunk buffer.  Returns the number of non-zero
@@ -776,7 +778,13 @@ int plan_chunk(File* f, int rg, int col, uint8_t* raw, int64_t raw_cap, int64_t 
     } else {
       const bool dict = !boolean && (ph.enc == 2 || ph.enc == 8);
       if (!dict && ph.enc != 0 && !(boolean && ph.enc == 3)) return HS_PQ_UNSUPPORTED;
-      if (strings && !dict) return HS_PQ_UNSUPPORTED;   // PLAIN strings: decoded another way
+      // PLAIN strings (eb 16): each value's address and length; the caller hashes them into
+      // codes (io/native_parquet.StringCodes.finish_plain)
+      if (strings && !dict) {
+        if (ph.enc != 0 || !g_plain_strings.load(std::memory_order_relaxed))
+          return HS_PQ_UNSUPPORTED;
+        p.eb = 16;
+      }
       if (dict && dict_idx < 0) return HS_PQ_CORRUPT;
       p.enc = ph.enc;
       p.nvals = ph.nvals;
@@ -886,6 +894,10 @@ void hs_pq_set_host_inflate(int mode) { g_host_inflate.store(mode, std::memory_o
 // 1 (default): device page plans accept chunks with nulls (levels decoded on the device);
 // 0: such chunks report HS_PQ_NULLS and go through the host page layer.
 void hs_pq_set_device_nulls(int on) { g_device_nulls.store(on, std::memory_order_relaxed); }
+
+// 1 (default): PLAIN BYTE_ARRAY data pages plan as eb-16 pages (value addresses + lengths on
+// the device); 0: such chunks report HS_PQ_UNSUPPORTED and are read another way.
+void hs_pq_set_plain_strings(int on) { g_plain_strings.store(on, std::memory_order_relaxed); }
 
 int64_t hs_pq_chunk_host_bound(void* h, int rg, int col) {
   const ChunkMeta& m = ((File*)h)->rgs[(size_t)rg].cols[(size_t)col];

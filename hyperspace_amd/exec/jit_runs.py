@@ -215,7 +215,13 @@ def scan_shape(p: NL.JoinParams, compacts, W: int, NI: int) -> tuple:
     aggs = tuple((p.aggs[i].kind, p.aggs[i].nterms, tuple(p.aggs[i].col[:p.aggs[i].nterms]))
                  for i in range(p.naggs))
     return ("run_scan", cols, preds, aggs, p.group_col, p.lkey, W, NI, J.BLOCK, J.WAVE_SYNC,
-            J.VEC_PREFETCH)
+            J.VEC_PREFETCH, _scan_grouped(p))
+
+
+def _scan_grouped(p: NL.JoinParams) -> bool:
+    """Whether the scan phase keeps a group table: a right-side group key with a single group
+    (a constant column) accumulates like an ungrouped aggregate (same partials layout)."""
+    return p.group_col >= 0 and not (p.group_col >= SPLIT and p.num_groups == 1)
 
 
 def gen_run_scan(p: NL.JoinParams, compacts, W: int, NI: int) -> J.Kernel:
@@ -234,12 +240,12 @@ def gen_run_scan(p: NL.JoinParams, compacts, W: int, NI: int) -> J.Kernel:
     cols = J._col_specs(p, compacts)
     lpreds = _lpreds(p)
     aggs = [p.aggs[i] for i in range(p.naggs)]
-    grouped = p.group_col >= 0
-    rgroup = p.group_col >= SPLIT
+    grouped = _scan_grouped(p)
+    rgroup = grouped and p.group_col >= SPLIT
     pslots = J._pred_slots(lpreds)
     tail = J._agg_slots(aggs) + ([p.group_col] if grouped and not rgroup else [])
     allslots = list(dict.fromkeys(pslots + tail))
-    approx = J._sum_only_slots(lpreds, aggs, -1 if rgroup else p.group_col, cols)
+    approx = J._sum_only_slots(lpreds, aggs, p.group_col if grouped and not rgroup else -1, cols)
     BLOCK = J.BLOCK  # noqa: N806
     T = BLOCK * NI  # noqa: N806
     MASK = (1 << W) - 1  # noqa: N806
@@ -356,6 +362,6 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
     grid_t = max(1, J.MJ_GRID)
     grid_s = max(1, J.SCAN_GRID or NL.lib().hs_scan_grid())
-    return TwoPhaseLauncher(kt, ks, grid_t, grid_s, GA, GA * 32 if p.group_col >= 0 else 0,
+    return TwoPhaseLauncher(kt, ks, grid_t, grid_s, GA, GA * 32 if _scan_grouped(p) else 0,
                             vt, vs, compacts, (rstart, rlen, rbucket, roff, tp, spans, tr, runs),
                             tags, dev)

@@ -301,6 +301,7 @@ def finish_strings(up: "UploadResult", cols: Dict[str, DeviceColumn], device, di
             cols[name] = DeviceColumn.from_arrow(arr, device, d, raw_strings=name in raw)
             continue
         dc = cols[name]
+        sc.finish_plain(dc)          # PLAIN pages' values -> codes (a dictionary part each)
         local = sc.concat()
         host = {i: (c.cast(c.type.value_type) if pa.types.is_dictionary(c.type) else c)
                 for i, c in enumerate(chunks) if c is not None}
@@ -386,6 +387,8 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
             cols[name].valid = torch.ones(n, dtype=torch.uint8, device=device)
     lock = threading.Lock()
     main = torch.cuda.current_stream(device)
+    for sc in dev_strings.values():
+        sc.main = main
     for st in streams:
         st.wait_stream(main)  # allocations above happen-before the copies
 

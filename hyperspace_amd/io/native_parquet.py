@@ -105,7 +105,8 @@ def lib():
                         ("hs_pq_snappy_decompress", I64, [P, I64, P, I64]),
                         ("hs_pq_plain_strings", I64, [P, I64, I64, P, P, I64]),
                         ("hs_pq_set_host_inflate", None, [I]),
-                        ("hs_pq_set_device_nulls", None, [I])):
+                        ("hs_pq_set_device_nulls", None, [I]),
+                        ("hs_pq_set_plain_strings", None, [I])):
                     fn = getattr(L, name)
                     fn.restype = res
                     fn.argtypes = args
@@ -118,6 +119,9 @@ def lib():
                 # HS_PQ_DEVICE_NULLS=0: chunks with nulls go through the host page layer
                 # (strings: pyarrow) instead of decoding their definition levels on the device
                 L.hs_pq_set_device_nulls(int(os.environ.get("HS_PQ_DEVICE_NULLS", "1")))
+                # HS_PQ_PLAIN_STRINGS=0: PLAIN BYTE_ARRAY pages are read by pyarrow instead of
+                # decoding to (address, length) pairs on the device
+                L.hs_pq_set_plain_strings(int(os.environ.get("HS_PQ_PLAIN_STRINGS", "1")))
                 if L.hs_pq_run_size() != RUN_DTYPE.itemsize or \
                         L.hs_pq_info_size() != C.sizeof(ChunkInfo) or \
                         L.hs_pq_page_size() != PAGE_DTYPE.itemsize:
@@ -411,13 +415,87 @@ class StringCodes:
     thread); the data pages decode on the device to those codes.  ``concat`` is the dictionary
     of that code space; the caller maps it onto the job-global sorted dictionary with one device
     gather (``staging.finish_strings``).  ``host`` holds the arrow chunks of files whose pages the
-    device path could not take (PLAIN-encoded pages), by file index."""
+    device path could not take, by file index.
 
-    def __init__(self):
+    PLAIN-encoded data pages decode on the device to each value's address and length
+    (``sptr`` / ``slen``, rows ``plain_rows``; the page buffers they point into are held in
+    ``keep``); ``finish_plain`` hashes them into codes of a dictionary of their distinct values,
+    read back from the device."""
+
+    def __init__(self, main=None):
         self._lock = threading.Lock()
         self.size = 0
         self.parts: List[tuple] = []
         self.host: Dict[int, object] = {}
+        self.main = main                  # the upload's consumer stream (allocations)
+        self.sptr = self.slen = None
+        self.plain_rows: List[tuple] = []
+        self.keep: list = []
+
+    def plain_arrays(self, n: int, device):
+        """The column's (address int64, length int32) arrays, allocated on first need."""
+        import torch
+        with self._lock:
+            if self.sptr is None:
+                st = self.main if self.main is not None else torch.cuda.current_stream(device)
+                with torch.cuda.stream(st):
+                    self.sptr = torch.empty(n, dtype=torch.int64, device=device)
+                    self.slen = torch.empty(n, dtype=torch.int32, device=device)
+            return self.sptr, self.slen
+
+    def add_plain(self, ranges, keep) -> None:
+        with self._lock:
+            self.plain_rows += ranges
+            self.keep += keep
+
+    def finish_plain(self, dc) -> None:
+        """Codes of the PLAIN-page rows into ``dc.data`` (on the current stream, after the
+        decode): a 64-bit hash per value (csrc/kernels/strings.hip), the distinct hashes, one
+        representative value per hash copied to the host as a dictionary part, and a byte
+        compare of every value with its representative - values whose hash collides with a
+        different value's are resolved on the host (their bytes only)."""
+        import torch
+        import pyarrow.compute as pc
+        from ..ops import kernels as K
+        if not self.plain_rows:
+            return
+        dev = dc.data.device
+        rr = np.array(sorted(self.plain_rows), dtype=np.int64).reshape(-1, 2)
+        lens = rr[:, 1] - rr[:, 0]
+        starts = torch.from_numpy(np.repeat(rr[:, 0] - np.concatenate([[0], np.cumsum(lens)[:-1]]),
+                                            lens)).to(dev)
+        idx = torch.arange(int(lens.sum()), dtype=torch.int64, device=dev) + starts
+        if dc.valid is not None:
+            idx = idx[dc.valid.index_select(0, idx) != 0]
+        if idx.numel():
+            ptr, ln = self.sptr.index_select(0, idx), self.slen.index_select(0, idx)
+            h = K.str_hash64(ptr, ln)
+            uh, inv = torch.unique(h, return_inverse=True)
+            first = torch.full((uh.numel(),), idx.numel(), dtype=torch.int64, device=dev)
+            first.scatter_reduce_(0, inv, torch.arange(idx.numel(), device=dev), "amin")
+            rptr, rlen = ptr.index_select(0, first), ln.index_select(0, first)
+            offh, chars = K.str_gather(rptr, rlen)
+            arr = pa.Array.from_buffers(pa.string(), uh.numel(), [
+                None, pa.py_buffer(offh.to(torch.int32).numpy()),
+                pa.py_buffer(chars.cpu().numpy())])
+            codes = inv + self.add(arr)
+            bad = K.str_differ(ptr, ln, rptr.index_select(0, inv), rlen.index_select(0, inv))
+            nb = int(bad.sum().item())
+            if nb:
+                # 64-bit hash collisions: these values get codes of their own
+                sel = torch.nonzero(bad).squeeze(1)
+                boff, bchars = K.str_gather(ptr.index_select(0, sel), ln.index_select(0, sel))
+                vals = pa.Array.from_buffers(pa.string(), nb, [
+                    None, pa.py_buffer(boff.to(torch.int32).numpy()),
+                    pa.py_buffer(bchars.cpu().numpy())])
+                d = pc.unique(vals)
+                base = self.add(d)
+                pos = pc.index_in(vals, value_set=d).to_numpy(zero_copy_only=False)
+                codes[sel] = torch.from_numpy(pos.astype(np.int64) + base).to(dev)
+            dc.data.index_copy_(0, idx, codes.to(torch.int32))
+        self.sptr = self.slen = None
+        self.keep = []
+        self.plain_rows = []
 
     def add(self, arr: pa.Array) -> int:
         with self._lock:
@@ -578,6 +656,7 @@ def upload_file_device(path: str, fields: Sequence[pa.Field], cols: Dict[str, ob
                                     sbase + pages["dst"])
             dp = pages["dict_page"]
             pages["dict"] = np.where(dp >= 0, pages["dst"][np.maximum(dp, 0)], 0)
+            plain = _plain_string_pages(chunks, pages, cols, strings, lo, rg_off, device)
             tabs = _string_code_tables(chunks, pages, pinned.data_ptr() + raw_cap, strings)
             if tabs is not None:
                 tab_host, fix = tabs
@@ -589,13 +668,16 @@ def upload_file_device(path: str, fields: Sequence[pa.Field], cols: Dict[str, ob
                 dtab.record_stream(stream)
                 for p0, np_, toff in fix:
                     seg = pages[p0:p0 + np_]
-                    seg["dict"] = np.where(seg["kind"] != 2, dtab.data_ptr() + 4 * toff, 0)
+                    seg["dict"] = np.where(seg["kind"] == 2, 0, np.where(
+                        seg["eb"] == 16, seg["dict"], dtab.data_ptr() + 4 * toff))
             if defer is not None:
                 # batched decode (decode_batch): absolute source addresses, buffers kept alive
                 # by the pending record until the batched launch is queued
                 pages["src"] = np.where(pages["codec"] == 2, pages["src"],
                                         draw.data_ptr() + pages["src"])
                 keep = [draw, scratch] + ([dtab] if tabs is not None else [])
+                for sc in plain:                # the (address, length) pairs point into these
+                    sc.add_plain([], [draw, scratch])
                 ev = torch.cuda.Event()
                 ev.record(stream)
                 defer.append(PendingDecode(pages, keep, ev, draw.numel() + scratch.numel()))
@@ -614,10 +696,36 @@ def upload_file_device(path: str, fields: Sequence[pa.Field], cols: Dict[str, ob
                                                  stream.cuda_stream), "hs_pq_decode_pages")
             for x in (draw, dpages, scratch):
                 x.record_stream(stream)
+            for sc in plain:
+                sc.add_plain([], [draw, scratch])
             _phase("launch", t)
         return {fld.name for fld, _, _, _ in chunks}
     finally:
         f.close()
+
+
+def _plain_string_pages(chunks, pages, cols, strings, lo: int, rg_off, device) -> list:
+    """Point the PLAIN string pages (eb 16) of a file plan at their rows of the column's
+    (address, length) arrays; returns the StringCodes that received such pages."""
+    out = []
+    if not strings:
+        return out
+    for fld, g, p0, np_ in chunks:
+        sc = strings.get(fld.name)
+        if sc is None:
+            continue
+        seg = pages[p0:p0 + np_]
+        pl = seg["eb"] == 16
+        if not pl.any():
+            continue
+        sptr, slen = sc.plain_arrays(cols[fld.name].data.shape[0], device)
+        rows = lo + int(rg_off[g]) + seg["row"]
+        seg["out"] = np.where(pl, sptr.data_ptr() + rows * 8, seg["out"])
+        seg["dict"] = np.where(pl, slen.data_ptr() + rows * 4, seg["dict"])
+        sc.add_plain([(int(r), int(r) + int(nv)) for r, nv in zip(rows[pl], seg["nvals"][pl])], [])
+        if sc not in out:
+            out.append(sc)
+    return out
 
 
 def _string_code_tables(chunks, pages, host_base: int, strings):
@@ -634,6 +742,8 @@ def _string_code_tables(chunks, pages, host_base: int, strings):
             continue
         seg = pages[p0:p0 + np_]
         dpg = np.nonzero(seg["kind"] == 2)[0]
+        if not len(dpg) and (seg["eb"] == 16).all():
+            continue                            # PLAIN pages only: StringCodes.finish_plain
         if len(dpg) != 1 or seg["codec"][dpg[0]] != 2:
             raise IOError(f"string chunk of {fld.name} without a host-parsed dictionary page")
         d = seg[dpg[0]]

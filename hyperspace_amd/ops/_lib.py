@@ -205,6 +205,9 @@ def lib():
     _sig(L.hs_tile_runs, I, P, I, P, P, P, I64, P, P)
     _sig(L.hs_key_bitmap, I, P, I64, I64, I64, P, P, P)
     _sig(L.hs_bitmap_popcount, I, P, I64, P, P)
+    _sig(L.hs_str_hash64, I, P, P, I64, P, P)
+    _sig(L.hs_str_gather, I, P, P, P, I64, P, P)
+    _sig(L.hs_str_differ, I, P, P, P, P, I64, P, P)
     _sig(L.hs_snappy_max_compressed, I64, I64)
     _sig(L.hs_snappy_chunk_bytes, I)
     _sig(L.hs_snappy_compress, I, P, I, P, I64, P, P)

@@ -481,6 +481,39 @@ def bitmap_popcount(words) -> int:
     return int(out.item())
 
 
+def str_hash64(ptr, ln):
+    """int64 hash per string value given as (device address int64, length int32) tensors
+    (csrc/kernels/strings.hip)."""
+    torch = _torch()
+    out = torch.empty(ptr.numel(), dtype=torch.int64, device=ptr.device)
+    NL.check(NL.lib().hs_str_hash64(NL.ptr(ptr), NL.ptr(ln), ptr.numel(), NL.ptr(out),
+                                    NL.stream_ptr()), "hs_str_hash64")
+    return out
+
+
+def str_gather(ptr, ln):
+    """(int32 offsets [n + 1] on the host, uint8 bytes on the device) of the values
+    (address, length): Arrow string layout of the selection."""
+    torch = _torch()
+    l64 = ln.clamp(min=0).long()
+    off = torch.zeros(ptr.numel() + 1, dtype=torch.int64, device=ptr.device)
+    torch.cumsum(l64, 0, out=off[1:])
+    offh = off.cpu()
+    out = torch.empty(max(int(offh[-1]), 1), dtype=torch.uint8, device=ptr.device)
+    NL.check(NL.lib().hs_str_gather(NL.ptr(ptr), NL.ptr(ln), NL.ptr(off), ptr.numel(),
+                                    NL.ptr(out), NL.stream_ptr()), "hs_str_gather")
+    return offh, out
+
+
+def str_differ(a, alen, b, blen):
+    """bool per value: value i of (a, alen) differs from value i of (b, blen)."""
+    torch = _torch()
+    out = torch.empty(a.numel(), dtype=torch.uint8, device=a.device)
+    NL.check(NL.lib().hs_str_differ(NL.ptr(a), NL.ptr(alen), NL.ptr(b), NL.ptr(blen), a.numel(),
+                                    NL.ptr(out), NL.stream_ptr()), "hs_str_differ")
+    return out.bool()
+
+
 def lookup_i32(table, codes):
     """``table[codes]`` for an int32 table and int32 codes, through the gather kernel."""
     from ..exec.device_table import DeviceColumn
