@@ -220,17 +220,22 @@ def _streaming_plan(session, rel, my_files, columns, lineage_ids, num_buckets, d
         agreed = dist.agree_any([n in may for n in fixed])
         nullable = {n for n, a in zip(fixed, agreed) if a}
         return passes, groups, row_bytes, nullable, _string_dictionaries(rel, my_files, schema,
-                                                                         dist)
+                                                                         dist, device, groups)
     if len(passes) <= 1:
         return None
-    return (passes, plan_file_groups(rows, row_bytes, max(budget // 4, 1)), row_bytes, None,
-            _string_dictionaries(rel, my_files, schema, None))
+    groups = plan_file_groups(rows, row_bytes, max(budget // 4, 1))
+    return (passes, groups, row_bytes, None,
+            _string_dictionaries(rel, my_files, schema, None, device, groups))
 
 
-def _string_dictionaries(rel, my_files, schema, dist) -> Dict[str, pa.Array]:
-    """Job-global sorted dictionary of every string column of a streaming build: the union of
-    the files' Parquet dictionary pages (read as dictionary arrays, no string materialised per
-    row; plain-encoded pages contribute their values) over all ranks."""
+def _string_dictionaries(rel, my_files, schema, dist, device=None,
+                         groups=None) -> Dict[str, pa.Array]:
+    """Job-global sorted dictionary of every string column of a streaming build, over all
+    ranks.  Parquet columns decode on the device, file group by file group (``groups``), and
+    contribute the dictionaries ``staging.finish_strings`` gives them - dictionary pages parsed,
+    PLAIN pages hashed on the device (io/native_parquet.StringCodes) - so no string is decoded
+    on the host; without the device page path the files' dictionary pages are read as
+    dictionary arrays (plain-encoded pages contribute their values)."""
     import pyarrow.parquet as pq
     from ..parallel.dictionary import union_sorted
     from . import staging
@@ -240,6 +245,26 @@ def _string_dictionaries(rel, my_files, schema, dist) -> Dict[str, pa.Array]:
     part_names = {f.name for f in rel.location.partition_spec.columns} \
         if rel.location.partition_spec is not None else set()
     file_cols = [n for n in names if n not in part_names and n in rel.data_schema.names]
+    dev_parts: Dict[str, list] = {}
+    if device is not None and file_cols and staging.native_decode_enabled() and \
+            staging.device_strings_enabled() and my_files:
+        sch = pa.schema([rel.data_schema.field(c) for c in file_cols])
+        for a, b in (groups or [(0, len(my_files))]):
+            fs = my_files[a:b]
+            if not fs:
+                continue
+            rows = list(staging.io_pool().map(
+                lambda f: pq.ParquetFile(P.to_local(f)).metadata.num_rows, fs))
+            up = staging.upload_files(
+                lambda f, cols=None: pq.read_table(P.to_local(f), columns=cols or file_cols),
+                fs, rows, sch, device, parquet_local=[P.to_local(f) for f in fs],
+                device_pages=True)
+            cols = dict(up.columns)
+            staging.finish_strings(up, cols, device, None)
+            for n in file_cols:
+                dev_parts.setdefault(n, []).append(cols[n].dictionary)
+            del up, cols
+        file_cols = []
 
     def values(f):
         out = {}
@@ -251,7 +276,7 @@ def _string_dictionaries(rel, my_files, schema, dist) -> Dict[str, pa.Array]:
                     vals.append(ch.dictionary if pa.types.is_dictionary(ch.type)
                                 else pc.unique(ch))
                 out[n] = vals
-        rest = [n for n in names if n not in file_cols]
+        rest = [n for n in names if n not in file_cols and n not in dev_parts]
         if rest:
             from ..io.reader import read_files
             t = read_files("parquet", [f], rel.data_schema, rel.options,
@@ -259,10 +284,12 @@ def _string_dictionaries(rel, my_files, schema, dist) -> Dict[str, pa.Array]:
             for n in rest:
                 out[n] = [pc.unique(t.column(n).combine_chunks())]
         return out
-    per_file = list(staging.io_pool().map(values, my_files))
+    per_file = list(staging.io_pool().map(values, my_files)) \
+        if len(names) > len(dev_parts) else []
     dicts = {}
     for n in names:
-        parts = [a.cast(pa.string()) for v in per_file for a in v.get(n, [])]
+        parts = [a.cast(pa.string()) for v in per_file for a in v.get(n, [])] + \
+            [a.cast(pa.string()) for a in dev_parts.get(n, [])]
         local = pa.concat_arrays(parts) if parts else pa.array([], pa.string())
         dicts[n] = union_sorted(local, dist)
     return dicts
@@ -376,10 +403,13 @@ def _streaming_build(session, rel, my_files, columns, indexed, num_buckets, out_
         sort_s += time.perf_counter() - ts
     if multi:
         dist.barrier()
+    from . import staging
     LAST_BUILD_STATS.update({"passes": len(passes), "file_groups": len(groups),
                              "source_bytes": source_bytes, "exchange_sent_bytes": sent_total,
                              "pass_decode_s": decode_s, "pass_sort_write_s": sort_s,
-                             "total_s": time.perf_counter() - t0})
+                             "total_s": time.perf_counter() - t0,
+                             "host_decoded": sorted(staging.HOST_DECODED),
+                             "device_decoded": sorted(staging.DEVICE_DECODED)})
     return paths
 
 

@@ -46,10 +46,12 @@ def test_streaming_build_is_byte_identical(tmp_path, device):
                       "p": pa.array(np.round(rng.random(n) * 1e4, 2)),
                       "q": pa.array(np.where(rng.random(n) < 0.1, None,
                                              rng.integers(0, 50, n)).tolist(), pa.int64()),
-                      # strings: per-file dictionaries differ; file 3 has nulls (host decode)
+                      # strings: per-file dictionaries differ; file 3 has nulls
                       "s": pa.array([f"s{x}" if i != 3 or x % 9 else None
                                      for x in rng.integers(0, 40 + 10 * i, n)], pa.string())})
-        pq.write_table(t, src / f"part-{i}.parquet", row_group_size=16_000)
+        # file 4: PLAIN-encoded strings (decoded on the device, no dictionary pages)
+        pq.write_table(t, src / f"part-{i}.parquet", row_group_size=16_000,
+                       use_dictionary=(i != 4))
 
     def build(name, budget):
         s = Session(conf={"spark.hyperspace.system.path": str(tmp_path / "ix"),
@@ -69,6 +71,9 @@ def test_streaming_build_is_byte_identical(tmp_path, device):
     one, s1 = build("one_pass", 1 << 40)
     many, s2 = build("streamed", 600_000)
     assert "passes" not in s1 and s2["passes"] >= 4 and s2["file_groups"] >= 2, s2
+    # every column - dictionary and PLAIN strings, nulls included - decoded on the device, the
+    # streamed build's job-global string dictionary too
+    assert s1.get("host_decoded") == [] and s2.get("host_decoded") == [], (s1, s2)
     assert sorted(one) == sorted(many) and len(one) == 16
     for b in one:
         assert one[b] == many[b], f"bucket {b} differs"
