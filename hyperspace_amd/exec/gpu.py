@@ -1282,6 +1282,18 @@ class GpuBackend:
         (BucketUnionExec.scala:61-74 runs a bucketed plan partition by partition)."""
         if self._dist() is not None:
             return None
+        budget = HyperspaceConf.device_cache_bytes(self.session.conf)
+        memo = self.__dict__.setdefault("_stream_memo", {})
+        hit = memo.get(id(child))
+        if hit is not None and hit[0] is child and hit[1] == budget:
+            return hit[2]       # a plan-cache hit re-submits the same nodes: decided once
+        chunks = self._stream_plan(child, budget)
+        if len(memo) > 256:
+            memo.clear()
+        memo[id(child)] = (child, budget, chunks)
+        return chunks
+
+    def _stream_plan(self, child, budget: int) -> Optional[List[tuple]]:
         scans = child.collect(lambda x: isinstance(x, X.FileSourceScanExec))
         # only operators that keep bucket b's rows inside bucket b: an Exchange (a join of
         # sides bucketed on other keys) or a union would pair rows across bucket ranges
@@ -1308,7 +1320,6 @@ class GpuBackend:
             w = memo[2]
             per_bucket = w if per_bucket is None or len(per_bucket) != nb else per_bucket + w
             total += float(w.sum())
-        budget = HyperspaceConf.device_cache_bytes(self.session.conf)
         if len(nbs) != 1 or total <= budget:
             return None
         cap = max(budget // 2, 1)              # the pass's tables plus what queries derive
@@ -1756,16 +1767,25 @@ class GpuBackend:
         else:
             col_info, descs = prep.col_info, prep.descs
         nd = len(descs)
-        implied: set = set()
-        spec = self._range_spec(r, r.conds, implied)
+        lkey = prep.literal_key() if prep is not None else None
+        low = prep.lowered.get(lkey) if lkey is not None else None
+        if low is None:
+            implied: set = set()
+            spec = self._range_spec(r, r.conds, implied)
+            bound = CP.bind(CP.to_cnf([c for c in r.conds if id(c) not in implied]), col_info,
+                            self.device)
+            specs = self._agg_specs(fns, col_info)
+            if lkey is not None:
+                if len(prep.lowered) >= 1024:
+                    prep.lowered.clear()
+                prep.lowered[lkey] = (spec, bound, specs)
+        else:
+            spec, bound, specs = low
         graph = self._graph_eligible(spec, descs)
         if not graph:
             with stage("scan.ranges"):
                 rstart, rlen, _ = self._ranges(r, r.conds) if spec is not None else \
                     self._full_ranges(r.table)
-        bound = CP.bind(CP.to_cnf([c for c in r.conds if id(c) not in implied]), col_info,
-                        self.device)
-        specs = self._agg_specs(fns, col_info)
         if prep is None:
             gs = self._group_spec(r, group, MAX_GROUPS_SCAN)
         else:
@@ -1799,7 +1819,8 @@ class GpuBackend:
                 out = self._scan_agg_graph(r, p, spec,
                                            p.naggs * (p.num_groups if p.group_col >= 0 else 1),
                                            descs, keep=bound.buffers,
-                                           prep=prep.graph if prep is not None else None)
+                                           prep=prep.graph if prep is not None else None,
+                                           lkey=lkey)
         else:
             with stage("scan.agg_kernel"):
                 tp = K.ranges_to_tiles(rlen)
@@ -1820,15 +1841,24 @@ class GpuBackend:
         return HyperspaceConf.codegen_enabled(conf) and HyperspaceConf.hipgraph_enabled(conf)
 
     def _scan_agg_graph(self, r: DRel, p: NL.ScanParams, spec, GA: int, descs=None, keep=(),
-                        prep: Optional["_GraphPrep"] = None):
+                        prep: Optional["_GraphPrep"] = None, lkey=None):
         kc, lo, lo_incl, hi, hi_incl, _ = spec
         if prep is None or prep.GA != GA or self.graphs.peek(prep.key) is not prep.g:
             prep = self._graph_prep(r, p, kc, GA, descs)
             self._last_graph_prep = prep
         g, k, compacts = prep.g, prep.k, prep.compacts
-        values = dict(prep.values)
-        jit.fill_preds_aggs(values, [(i, p.preds[i]) for i in range(p.npreds)],
-                            [p.aggs[i] for i in range(p.naggs)], compacts)
+        hit = prep.packed.get(lkey) if lkey is not None else None
+        if hit is None:
+            values = dict(prep.values)
+            jit.fill_preds_aggs(values, [(i, p.preds[i]) for i in range(p.npreds)],
+                                [p.aggs[i] for i in range(p.naggs)], compacts)
+            # (the per-query predicate buffers the block points to stay referenced with it)
+            hit = (range_bounds(lo, lo_incl, hi, hi_incl), k.args.pack(values), list(keep))
+            if lkey is not None:
+                if len(prep.packed) >= 1024:
+                    prep.packed.clear()
+                prep.packed[lkey] = hit
+        bounds, packed, _ = hit
         side = self._scan_side_stream(g)
         if side is None:
             if g.on_side:
@@ -1836,7 +1866,7 @@ class GpuBackend:
                 # side-stream scans were switched off after this pipeline replayed there: its
                 # shared intermediates are free only once those replays are done
                 torch.cuda.current_stream().wait_stream(g.side_stream)
-            handle = g.launch(range_bounds(lo, lo_incl, hi, hi_incl), k.args.pack(values))
+            handle = g.launch(bounds, packed)
             return (_GraphPending(g, handle), None, None, None)
         import torch
         # a warm pipeline (replays only: no module load, capture or cache fill left) runs on
@@ -1861,7 +1891,7 @@ class GpuBackend:
         for x in keep:      # per-query predicate buffers (IN sets, key bitmaps)
             _use_on(x, side)
         with torch.cuda.stream(side):
-            handle = g.launch(range_bounds(lo, lo_incl, hi, hi_incl), k.args.pack(values))
+            handle = g.launch(bounds, packed)
         return (_GraphPending(g, handle), None, None, None)
 
     def _graph_prep(self, r: DRel, p: NL.ScanParams, kc, GA: int, descs) -> "_GraphPrep":
@@ -2667,20 +2697,49 @@ class _Stale(Exception):
 
 
 class _GraphPrep:
-    __slots__ = ("key", "g", "k", "compacts", "values", "GA")
+    __slots__ = ("key", "g", "k", "compacts", "values", "GA", "packed")
 
     def __init__(self, key, g, k, compacts, values, GA):
         self.key, self.g, self.k, self.compacts, self.values, self.GA = \
             key, g, k, compacts, values, GA
+        self.packed: Dict[tuple, tuple] = {}     # literal vector -> (range bounds, args block)
+
+
+def _literals(exprs) -> list:
+    """The Literal nodes under ``exprs`` (depth first)."""
+    out = []
+    stack = list(reversed(list(exprs)))
+    while stack:
+        e = stack.pop()
+        if isinstance(e, E.Literal):
+            out.append(e)
+        else:
+            stack.extend(reversed(getattr(e, "children", ()) or ()))
+    return out
 
 
 class _ScanPrep:
-    """Literal-independent lowering of a fused scan aggregate (GpuBackend._dense_agg)."""
-    __slots__ = ("final", "r", "col_info", "descs", "gs", "params", "graph", "placement")
+    """Literal-independent lowering of a fused scan aggregate (GpuBackend._dense_agg), plus
+    the literal-dependent part per literal vector (``lowered``): the plan cache binds a query's
+    literals into the same Literal nodes of the cached plan, so their values key the range
+    bounds, bound predicates and aggregate terms - a repeated parameter set (a dashboard's
+    queries) skips predicate compilation altogether."""
+    __slots__ = ("final", "r", "col_info", "descs", "gs", "params", "graph", "placement",
+                 "lits", "lowered")
 
     def __init__(self, final, r, col_info, descs, gs, params, graph, placement):
         self.final, self.r, self.col_info, self.descs, self.gs = final, r, col_info, descs, gs
         self.params, self.graph, self.placement = params, graph, placement
+        self.lits = _literals(list(r.conds) + list(final.aggregates))
+        self.lowered: Dict[tuple, tuple] = {}
+
+    def literal_key(self):
+        try:
+            k = tuple(x.value for x in self.lits)
+            hash(k)
+            return k
+        except TypeError:
+            return None
 
     def tables(self):
         return (self.r.table,)
@@ -2694,30 +2753,46 @@ class _JoinPrep:
     relations, column slots, group domain and the kernel launcher (jit.MergeJoinLauncher).
     A submission re-binds the predicates and aggregate terms and launches."""
     __slots__ = ("final", "node", "left", "right", "lk", "rk", "col_info", "descs", "launcher",
-                 "gtail", "placement", "agreed")
+                 "gtail", "placement", "agreed", "lits", "lowered")
 
     def __init__(self, final, node, left, right, lk, rk, col_info, descs, launcher, gtail,
                  placement, agreed):
         self.final, self.node, self.left, self.right = final, node, left, right
         self.lk, self.rk, self.col_info, self.descs = lk, rk, col_info, descs
         self.launcher, self.gtail, self.placement, self.agreed = launcher, gtail, placement, agreed
+        conds = list(left.conds) + list(right.conds) + \
+            ([node.condition] if node.condition is not None else [])
+        self.lits = _literals(conds + list(final.aggregates))
+        self.lowered: Dict[tuple, tuple] = {}   # literal vector -> (params, keep, specs)
+
+    literal_key = _ScanPrep.literal_key
 
     def tables(self):
         return (self.left.table, self.right.table)
 
     def run(self, be, fns, group):
         left = self.left
-        if be._range_spec(left, left.conds) is not None:
+        lkey = self.literal_key()
+        low = self.lowered.get(lkey) if lkey is not None else None
+        if low is None and be._range_spec(left, left.conds) is not None:
             raise _Stale()        # the new literals bound the left key: ranges change
         nd = len(self.descs)
         with stage("join.agg_kernel"):
-            jp, col_info, descs, keep = be._join_params(
-                left, self.right, self.lk, self.rk, self.node.condition,
-                slots=(self.col_info, self.descs))
-            specs = be._agg_specs(fns, col_info)
+            if low is None:
+                jp, col_info, descs, keep = be._join_params(
+                    left, self.right, self.lk, self.rk, self.node.condition,
+                    slots=(self.col_info, self.descs))
+                specs = be._agg_specs(fns, col_info)
+                if len(descs) != nd:
+                    raise _Stale()
+                if lkey is not None:
+                    if len(self.lowered) >= 1024:
+                        self.lowered.clear()
+                    self.lowered[lkey] = (jp, keep, specs)
+            else:
+                jp, keep, specs = low
+                col_info = self.col_info
             G, gbase = self.gtail[0], self.gtail[1]
-            if len(descs) != nd:
-                raise _Stale()
             if keep[0].always_false or keep[1].always_false:
                 out = be._empty_agg(len(specs), G)
             else:

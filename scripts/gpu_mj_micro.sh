@@ -20,7 +20,7 @@ while read -r CFG; do
   for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" \
            "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH FETCH_SIZE" ; do
     i=$((i+1))
-    timeout -s KILL 180 rocprofv3 --pmc $P --kernel-include-regex hs_jit_merge --kernel-trace --output-format csv \
+    timeout -s KILL 180 rocprofv3 --pmc $P --kernel-include-regex "hs_jit_(merge|run)" --kernel-trace --output-format csv \
       -d "$OUT/c${j}p$i" -o pmc -- python3 "$REPO/scripts/mj_micro.py" --sf ${SF:-100} --iters 3 \
       --configs "[$CFG]" > "$OUT/c${j}run$i.jsonl" 2> "$OUT/c${j}run$i.log" || exit $?
     find "$OUT/c${j}p$i" -name "*counter_collection.csv" -exec cp {} "$OUT/c${j}counters$i.csv" \;
