@@ -45,6 +45,15 @@ log = logging.getLogger(__name__)
 Unsupported = CP.Unsupported
 MAX_GROUPS_SCAN = 3000
 MAX_GROUPS_JOIN = 2400
+# LDS bytes a dense aggregate's group table may take (32 bytes per group x aggregate: sum, min,
+# max, count) beside the rest of the kernel's LDS (160 KiB per CU on gfx950)
+GROUP_LDS_SCAN = 144 << 10
+GROUP_LDS_JOIN = 112 << 10
+
+
+def _group_limit(limit: int, lds: int, naggs: int) -> int:
+    """Most groups a dense aggregate of ``naggs`` aggregates (+ COUNT(*)) keeps in LDS."""
+    return max(1, min(limit, lds // (32 * (naggs + 1))))
 # a grouped aggregate with more groups than this returns candidates of ORDER BY ... LIMIT from
 # the device top-k instead of copying every group to the host
 TOPK_MIN_GROUPS = 4096
@@ -1787,7 +1796,8 @@ class GpuBackend:
                 rstart, rlen, _ = self._ranges(r, r.conds) if spec is not None else \
                     self._full_ranges(r.table)
         if prep is None:
-            gs = self._group_spec(r, group, MAX_GROUPS_SCAN)
+            gs = self._group_spec(r, group, _group_limit(MAX_GROUPS_SCAN, GROUP_LDS_SCAN,
+                                                         len(fns)))
         else:
             gs = prep.gs
             if len(descs) != nd or (prep.graph is not None) != graph:
@@ -2119,7 +2129,8 @@ class GpuBackend:
         gs = (None, 1, 0, None, None)
         if group is not None:
             side = lparts if any(group.expr_id in x.colmap for x in lparts) else rparts
-            gs = self._group_spec_parts(side, group, MAX_GROUPS_JOIN)
+            gs = self._group_spec_parts(side, group, _group_limit(MAX_GROUPS_JOIN, GROUP_LDS_JOIN,
+                                                                  len(fns)))
             if gs is None:
                 return (*self._empty_agg(len(fns) + 1), 1, 0, None, None)
         agreed, G, gbase, gdict, gtype = gs
