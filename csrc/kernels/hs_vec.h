@@ -179,8 +179,9 @@ __device__ __forceinline__ void veval_pred(const Pred& p, const ColDesc* cols, i
       const int64_t nbits = (int64_t)p.set_len * 64;
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
+        const int64_t v = x[i] - p.ilit;     // bit (value - base), as hs_scan.h
         bool found = false;
-        if (mv[i] && x[i] >= 0 && x[i] < nbits) found = (words[x[i] >> 6] >> (x[i] & 63)) & 1ull;
+        if (mv[i] && v >= 0 && v < nbits) found = (words[v >> 6] >> (v & 63)) & 1ull;
         out[i] = mv[i] && (p.op == OP_EQ ? found : !found);
       }
       return;

@@ -2036,7 +2036,8 @@ class GpuBackend:
             return None
         conf = self.session.conf
         if not HyperspaceConf.codegen_enabled(conf) or \
-                str(conf.get("spark.hyperspace.mi.semiJoinBitmap.enabled", "true")).lower() != "true":
+                str(conf.get("spark.hyperspace.mi.semiJoinBitmap.enabled", "true")).lower() != "true" \
+                or str(conf.get("spark.hyperspace.mi.semiProject.enabled", "true")).lower() != "true":
             return None
         failed = self.__dict__.setdefault("_semi_failed", {})
         if failed.get(id(node)) is node:
