@@ -1331,15 +1331,7 @@ class GpuBackend:
             total += float(w.sum())
         if len(nbs) != 1 or total <= budget:
             return None
-        cap = max(budget // 2, 1)              # the pass's tables plus what queries derive
-        chunks, lo, acc = [], 0, 0.0
-        for b, wb in enumerate(per_bucket):
-            if acc and acc + wb > cap:
-                chunks.append((lo, b))
-                lo, acc = b, 0.0
-            acc += wb
-        chunks.append((lo, len(per_bucket)))
-        return chunks
+        return bucket_chunks(per_bucket, budget)
 
     # decoded bytes per byte of a (compressed, dictionary-encoded) index file: the resident
     # estimate of a bucket for the streaming plan
@@ -2715,6 +2707,21 @@ class _GraphPrep:
         self.key, self.g, self.k, self.compacts, self.values, self.GA = \
             key, g, k, compacts, values, GA
         self.packed: Dict[tuple, tuple] = {}     # literal vector -> (range bounds, args block)
+
+
+def bucket_chunks(per_bucket, budget: int) -> List[tuple]:
+    """Contiguous bucket ranges [lo, hi) whose estimated resident bytes (``per_bucket``, the
+    decoded bytes of every index of a plan per bucket) stay within half of ``budget`` - the
+    pass's tables plus what its kernels derive - one bucket at least per range."""
+    cap = max(budget // 2, 1)
+    chunks, lo, acc = [], 0, 0.0
+    for b, wb in enumerate(per_bucket):
+        if acc and acc + wb > cap:
+            chunks.append((lo, b))
+            lo, acc = b, 0.0
+        acc += float(wb)
+    chunks.append((lo, len(per_bucket)))
+    return chunks
 
 
 def _literals(exprs) -> list:

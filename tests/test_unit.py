@@ -408,3 +408,19 @@ def test_owner_map_lpt_and_sticky_session_map():
     sess.conf = {"spark.hyperspace.mi.bucketPlacement": "modulo"}
     assert session_map(sess, 16, 4, wts).is_modulo()
     assert np.array_equal(first.owners, m.owners)
+
+
+def test_bucket_chunks_cover_buckets_within_budget():
+    """Bucket-range streaming plan (exec/gpu.py bucket_chunks): contiguous ranges covering every
+    bucket once, each within half the budget unless a single bucket alone exceeds it."""
+    from hyperspace_amd.exec.gpu import bucket_chunks
+    rng = np.random.default_rng(4)
+    w = rng.integers(1, 100, 200).astype(float)
+    for budget in (50, 400, 2000, 10**9):
+        ch = bucket_chunks(w, budget)
+        assert ch[0][0] == 0 and ch[-1][1] == 200
+        assert all(a[1] == b[0] for a, b in zip(ch, ch[1:]))
+        for lo, hi in ch:
+            assert hi > lo
+            assert hi - lo == 1 or w[lo:hi].sum() <= budget // 2
+    assert bucket_chunks(w, 10**9) == [(0, 200)]
