@@ -182,6 +182,8 @@ def compress_stream(device):
     return st
 
 
+# copy streams the index pages leave HBM on (HS_PQ_D2H_STREAMS)
+D2H_STREAMS = int(os.environ.get("HS_PQ_D2H_STREAMS", "2"))
 # seconds of the last builds' write phases (reset by device_build per build)
 WRITE_PHASES: Dict[str, float] = {}
 _WP_LOCK = __import__("threading").Lock()
@@ -469,7 +471,7 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
     compresses every page segment on the device (``snappy_pages``) and dictionary pages on the
     host."""
     import torch
-    from .staging import copy_stream, io_pool, pinned_pool
+    from .staging import io_pool, pinned_pool
     if codec not in CODEC_IDS:
         LAST_FALLBACK["reason"] = f"codec {codec}"
         return None
@@ -494,8 +496,12 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
             lev_index[ci] = k
             k += 1
     L = _writer()
-    stream = copy_stream(device)
-    stream.wait_stream(torch.cuda.current_stream(device))
+    from .staging import copy_streams
+    # batches alternate over D2H_STREAMS copy streams: their page copies run on separate DMA
+    # queues instead of queueing behind one another
+    d2h = copy_streams(device)[:max(1, D2H_STREAMS)]
+    for st in d2h:
+        st.wait_stream(torch.cuda.current_stream(device))
     batches, cur, cur_bytes = [], [], 0
     for f in files:
         p0, p1 = _file_pages(f)
@@ -524,7 +530,7 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
         if g:
             groups.append(g)
     group_of = {bi: gi for gi, g in enumerate(groups) for bi in g}
-    zgroup = (-1, None)
+    zgroup = (-1, None, None)
     launched: Dict[int, _SnappyGroup] = {}
     zs = compress_stream(device) if cid == 1 else None
 
@@ -542,6 +548,7 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
         host = []
         zoff = zsize = None
         gfirst = 0
+        stream = d2h[bi % len(d2h)]
         with torch.cuda.stream(stream):
             if cid == 1:
                 gi = group_of[bi]
@@ -556,9 +563,10 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
                         res = snappy_finish(launched.pop(gi), device)
                         zev = torch.cuda.Event()
                         zev.record(zs)
-                    stream.wait_event(zev)
-                    res[0].record_stream(stream)
-                    zgroup = (gi, res)
+                    for st in d2h:
+                        res[0].record_stream(st)
+                    zgroup = (gi, res, zev)
+                stream.wait_event(zgroup[2])
                 packed, zoff, zsize = zgroup[1]
                 for c in range(len(segs)):
                     lo = int(zoff[c][p_first - gfirst])
