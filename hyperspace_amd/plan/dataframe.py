@@ -106,12 +106,24 @@ class DataFrame:
             raise AttributeError(str(e)) from None
 
     def _resolve(self, e: E.Expression, plan: L.LogicalPlan = None) -> E.Expression:
+        """``e`` with its unresolved column names bound to ``plan``'s attributes; subtrees
+        without one are kept as they are (a serving loop builds a fresh expression per query,
+        so this walk is on its host path)."""
         plan = plan or self.plan
-        def fn(x):
-            if isinstance(x, E.UnresolvedAttribute):
+        unresolved = E.UnresolvedAttribute
+
+        def walk(x):
+            if type(x) is unresolved or isinstance(x, unresolved):
                 return self._resolve_name(x.name, plan)
-            return None
-        return e.transform_up(fn)
+            ch = x.children
+            if not ch:
+                return x
+            new = tuple([walk(c) for c in ch])
+            for a, b in zip(new, ch):
+                if a is not b:
+                    return x.with_children(new)
+            return x
+        return walk(e)
 
     def _to_expr(self, c) -> E.Expression:
         if isinstance(c, str):

@@ -90,19 +90,44 @@ def _fields(d: dict) -> tuple:
     return f
 
 
+def _fp_lit(v, ctx: _Ctx):
+    ctx.lits.append(v)
+    return ("L", str(v.dtype), v.value is None)
+
+
+def _fp_attr(v, ctx: _Ctx):
+    return ("A", v.name, str(v.dtype), v.nullable, ctx.eid(v.expr_id), v.qualifier)
+
+
+def _fp_children(v, ctx: _Ctx):
+    d = v.__dict__
+    if len(d) != 1:                     # an instance with more fields: the generic walk
+        return _fp_node(v, type(v), ctx)
+    return (type(v).__name__, (("children", tuple([_fp(x, ctx) for x in d["children"]])),))
+
+
+# per exact type: the fingerprint function the generic dispatch below would reach (the
+# expression trees a serving loop builds per query are mostly these)
+_FAST: Dict[type, object] = {}
+
+
 def _fp(v, ctx: _Ctx):
     t = type(v)
     if t in _PRIMS:
         return v
+    f = _FAST.get(t)
+    if f is not None:
+        return f(v, ctx)
     if t is tuple or t is list:
         return tuple([_fp(x, ctx) for x in v])
     if isinstance(v, E.Literal):
-        ctx.lits.append(v)
-        return ("L", str(v.dtype), v.value is None)
+        _FAST[t] = _fp_lit
+        return _fp_lit(v, ctx)
     if isinstance(v, (E.In, E.InSet)):
         raise _NotCacheable("IN list (OptimizeIn depends on its values)")
     if isinstance(v, E.Attribute):
-        return ("A", v.name, str(v.dtype), v.nullable, ctx.eid(v.expr_id), v.qualifier)
+        _FAST[t] = _fp_attr
+        return _fp_attr(v, ctx)
     if isinstance(v, _PRIMS):
         return v
     if isinstance(v, (list, tuple)):
@@ -144,8 +169,11 @@ def _fp_leaf(v, ctx: _Ctx):
 
 def _fp_node(v, t: type, ctx: _Ctx):
     d = vars(v)
+    fields = _fields(d)
+    if fields == ("children",) and type(d["children"]) is tuple and t not in _FAST:
+        _FAST[t] = _fp_children        # its fingerprint is its type and its children's
     items = []
-    for k in _fields(d):
+    for k in fields:
         x = d[k]
         items.append((k, ctx.eid(x)) if k == "expr_id" else (k, _fp(x, ctx)))
     return (t.__name__, tuple(items))
