@@ -311,6 +311,14 @@ class GpuBackend:
             return self._rel(p.equivalent)
         raise Unsupported(f"operator {p.node_name}")
 
+    def _holds(self, t) -> bool:
+        """Whether resident table ``t`` is still current: in the device cache, or derived from
+        tables that are (a merged Hybrid Scan union, a cached repartition of appended rows)."""
+        src = getattr(t, "_hs_sources", None)
+        if src is not None:
+            return all(self._holds(x) for x in src)
+        return self.cache.holds(t)
+
     def _bucket_union(self, p: X.BucketUnionExec) -> DRel:
         nb = p.bucket_spec.num_buckets
         parts = []
@@ -324,8 +332,89 @@ class GpuBackend:
                     colmap[u.expr_id] = r.colmap[c.expr_id]
             parts.append(r.copy(colmap=colmap))
         first = parts[0]
+        merged = self._merged_union(p, parts)
+        if merged is not None:
+            return merged
         return DRel(None, dict(first.colmap), list(p.output), [], True, first.sort_attrs,
                     first.bucket_attrs, nb, parts)
+
+    def _merged_union(self, p: X.BucketUnionExec, parts: List[DRel]) -> Optional[DRel]:
+        """A Hybrid Scan's bucket union as ONE resident table: the index rows and the appended
+        rows (already bucketed and sorted by the device shuffle) of every bucket merged into
+        bucket-major order sorted by the index key, built once per (index table, appended
+        table) and kept while both stay resident - so queries over an index with appended
+        files take the single-table paths (prepared lowering, graph replays, the run-keyed
+        merge join) instead of one launch per (part, part) pair.  None when the parts carry
+        their own predicates (a deleted-files filter), computed columns, differently encoded
+        columns, or would take more than a quarter of the device cache."""
+        import torch
+        conf = self.session.conf
+        if str(conf.get("spark.hyperspace.mi.hybridMerge.enabled", "true")).lower() != "true":
+            return None
+        d = self._dist()
+        if d is not None and d.world > 1:
+            return None
+        if any(x.table is None or x.conds or x.extra or x.split or x.parts for x in parts):
+            return None
+        first = parts[0]
+        outs = list(p.output)
+        ids = {u.expr_id for u in outs}
+        if not first.sort_attrs or any(a.expr_id not in ids for a in first.sort_attrs):
+            return None
+        key = tuple(id(x.table) for x in parts) + tuple(u.expr_id for u in outs)
+        memo = self.__dict__.setdefault("_unions", {})
+        hit = memo.get(key)
+        if hit is not None and all(a is b for a, b in zip(hit[0], [x.table for x in parts])) \
+                and self._holds(hit[1]):
+            table = hit[1]
+        else:
+            cols = []
+            for u in outs:
+                cs = [x.col(u) for x in parts]
+                c0 = cs[0]
+                if any(c.data.dtype != c0.data.dtype or str(c.atype) != str(c0.atype) or
+                       c.offsets is not None or
+                       (c.dictionary is None) != (c0.dictionary is None) or
+                       (c.dictionary is not None and not c.dictionary.equals(c0.dictionary))
+                       for c in cs):
+                    return None
+                cols.append(cs)
+            nbytes = sum(c.data.numel() * c.data.element_size() for cs in cols for c in cs)
+            if nbytes > HyperspaceConf.device_cache_bytes(conf) // 4:
+                return None
+            nb = first.num_buckets
+            with stage("hybrid.merge"):
+                bucket = torch.cat([torch.repeat_interleave(
+                    torch.arange(nb, dtype=torch.int32, device=self.device),
+                    x.table.bucket_offsets[1:] - x.table.bucket_offsets[:-1]) for x in parts])
+                merged = {}
+                for j, cs in enumerate(cols):
+                    data = torch.cat([c.data for c in cs])
+                    valid = None
+                    if any(c.valid is not None for c in cs):
+                        valid = torch.cat([c.valid if c.valid is not None else
+                                           torch.ones(c.data.shape[0], dtype=torch.uint8,
+                                                      device=self.device) for c in cs])
+                    merged[f"u{j}"] = DeviceColumn(data, valid, cs[0].atype, cs[0].dictionary)
+                pos = {u.expr_id: j for j, u in enumerate(outs)}
+                keys = [merged[f"u{pos[a.expr_id]}"] for a in first.sort_attrs]
+                perm = K.sort_permutation(keys, extra_leading=(bucket, 16))
+                names = list(merged)
+                gathered = K.gather_columns([merged[n] for n in names], perm)
+                off_host = sum(np.asarray(x.table.bucket_offsets_host, dtype=np.int64) for x in parts)
+                n = int(off_host[-1])
+                table = DeviceTable(dict(zip(names, gathered)), n,
+                                    torch.from_numpy(off_host).to(self.device), off_host)
+            table._hs_sources = [x.table for x in parts]
+            table._hs_cache_key = ("hybrid-union",) + key
+            table.global_key = ("hybrid-union",) + tuple(
+                getattr(x.table, "global_key", None) for x in parts)
+            if len(memo) > 8:
+                memo.clear()
+            memo[key] = ([x.table for x in parts], table)
+        colmap = {u.expr_id: f"u{j}" for j, u in enumerate(outs)}
+        return DRel(table, colmap, outs, [], True, first.sort_attrs, first.bucket_attrs,
+                    first.num_buckets)
 
     def _unary(self, p: X.SparkPlan, r: DRel) -> DRel:
         if isinstance(p, X.FilterExec):
@@ -400,7 +489,7 @@ class GpuBackend:
         memo = self.__dict__.setdefault("_scans", {})
         m = memo.get(id(p))
         if m is not None and m[0] is p and m[2] == tag and m[1].table is not None and \
-                self.cache.holds(m[1].table):
+                self._holds(m[1].table):
             return m[1].copy()
         r = self._scan(p)
         if getattr(r.table, "_hs_cache_key", None) is not None:
@@ -878,6 +967,8 @@ class GpuBackend:
             nt = DeviceTable(dict(zip(names, gathered)), t.num_rows,
                              torch.from_numpy(off_host).to(self.device), off_host)
             nt.global_key = ("repartition", t.global_key, ck)
+            nt._hs_sources = [t]      # current while the source table is resident
+            nt._hs_cache_key = nt.global_key
             cache[ck] = nt
         colmap = {a.expr_id: r.colmap[a.expr_id] for a in need}
         return DRel(nt, colmap, list(r.attrs), list(r.conds), True, list(keys), list(keys), B)
@@ -1455,7 +1546,7 @@ class GpuBackend:
             return None
         pr = preps.get(id(final))
         if pr is None or pr.final is not final or pr.placement != self._placement_tag() or \
-                not all(self.cache.holds(t) for t in pr.tables()):
+                not all(self._holds(t) for t in pr.tables()):
             return None
         return pr
 

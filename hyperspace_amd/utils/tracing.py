@@ -158,8 +158,14 @@ def _event():
 TRACER = Tracer()
 
 
+_OFF = contextlib.nullcontext()
+
+
 def stage(name: str, device: bool = True):
-    """``with stage("join.probe"): ...`` — the module-level shortcut used by the executors."""
+    """``with stage("join.probe"): ...`` — the module-level shortcut used by the executors
+    (a shared no-op context while tracing is off: it sits on every query's host path)."""
+    if not (TRACER.roctx or TRACER.profile):
+        return _OFF
     return TRACER.stage(name, device)
 
 

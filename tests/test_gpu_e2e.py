@@ -308,6 +308,17 @@ def test_hybrid_scan_join_and_filter_on_device(tpch, tmp_path):
     g, c, path = _both(s, q2, sort=False)
     assert path == "native", s.backend().fallback_reason
     _close(g, c)
+    # the unions ran as merged single tables (GpuBackend._merged_union); the per-part
+    # lowering gives the same answers
+    assert s.backend().__dict__.get("_unions")
+    s.conf.set("spark.hyperspace.mi.hybridMerge.enabled", "false")
+    try:
+        for qq in (q, q2):
+            g2, c2, path = _both(s, qq, sort=False)
+            assert path == "native", s.backend().fallback_reason
+            _close(g2, c2)
+    finally:
+        s.conf.set("spark.hyperspace.mi.hybridMerge.enabled", "true")
 
 
 def test_incremental_refresh_with_deletes_on_device(tpch, tmp_path):
