@@ -266,6 +266,10 @@ class ColPlan:
         self.bw = 0
         self.dict_page: Optional[np.ndarray] = None
         self.dict_count = 0
+        self.fdict_page: List[np.ndarray] = []   # per file: its dictionary page (PLAIN values)
+        self.fdict_count: List[int] = []
+        self.fbw: List[int] = []                 # per file: code bit width
+        self.fdict_z = None
         self.payload = None          # device uint8: the value segment of every page
         self.page_off: Optional[np.ndarray] = None   # byte offset of every page (+ end)
         self.nullable = False
@@ -321,23 +325,58 @@ def _dict_codes(v, eb: int, dbits, device):
     return codes, bool(miss.item())
 
 
-def _pack(codes, rows0: np.ndarray, n: np.ndarray, bw: int, device):
+def _pack(codes, rows0: np.ndarray, n: np.ndarray, bw, device):
     """Bit-pack int32 ``codes`` page by page (``hs_pq_pack``): page p packs codes
-    [rows0[p], rows0[p] + n[p]) into ceil(n[p] / 8) * bw bytes; returns (device bytes, page
-    byte offsets + end)."""
+    [rows0[p], rows0[p] + n[p]) into ceil(n[p] / 8) * bw bytes (``bw`` an int, or an array of
+    per-page widths); returns (device bytes, page byte offsets + end)."""
     import torch
     groups = (n + 7) // 8
-    sizes = groups * bw
+    per_page = not np.isscalar(bw)
+    sizes = groups * (np.asarray(bw, dtype=np.int64) if per_page else bw)
     off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
     gpre = np.concatenate([[0], np.cumsum(groups)]).astype(np.int64)
     tab = np.empty(len(n), dtype=PAGE_DTYPE)
     tab["row0"], tab["n"], tab["out_off"], tab["gpre"] = rows0, n, off[:-1], gpre[:-1]
     dtab = torch.from_numpy(tab.view(np.uint8).copy()).to(device)
     out = torch.empty(int(off[-1]) + 16, dtype=torch.uint8, device=device)
+    dbw = None
+    if per_page:
+        bwa = np.asarray(bw, dtype=np.int32)
+        if len(bwa) and (bwa.min() < 1 or bwa.max() > 16):
+            raise ValueError("bit widths must be in 1..16")
+        dbw = torch.from_numpy(bwa.copy()).to(device)
     if int(gpre[-1]):
         NL.check(NL.lib().hs_pq_pack(codes.data_ptr(), dtab.data_ptr(), len(tab), int(gpre[-1]),
-                                     bw, out.data_ptr(), NL.stream_ptr()), "hs_pq_pack")
+                                     0 if per_page else bw,
+                                     dbw.data_ptr() if dbw is not None else None,
+                                     out.data_ptr(), NL.stream_ptr()), "hs_pq_pack")
     return out, off
+
+
+def _file_dicts(codes, n_dict: int, fo: np.ndarray, device):
+    """Per-file dictionaries (``hs_pq_dict_mark`` / ``hs_pq_dict_remap``): ``codes`` (int32,
+    into a sorted job-wide dictionary of ``n_dict`` entries, rows of file f at [fo[f],
+    fo[f + 1])) are rewritten in place as codes into the sorted subset file f uses; returns that
+    subset per file (job-dictionary indices).  A file's encoded bytes then depend only on its
+    own rows: one-pass, bucket-range-streamed and multi-rank builds write identical files, as
+    Spark writes a dictionary per column chunk."""
+    import torch
+    L = NL.lib()
+    nf = len(fo) - 1
+    dw = (n_dict + 31) // 32
+    n = int(fo[-1])
+    present = torch.zeros(nf * dw, dtype=torch.int32, device=device)
+    fo_d = torch.from_numpy(np.ascontiguousarray(fo, dtype=np.int64)).to(device)
+    NL.check(L.hs_pq_dict_mark(codes.data_ptr(), fo_d.data_ptr(), nf, n, dw, present.data_ptr(),
+                               NL.stream_ptr()), "hs_pq_dict_mark")
+    bits = np.unpackbits(present.cpu().numpy().view(np.uint8), bitorder="little") \
+        .reshape(nf, dw * 32)
+    cnt = bits.reshape(nf, dw, 32).sum(2, dtype=np.int64)
+    wpre = (np.cumsum(cnt, 1) - cnt).astype(np.int32)
+    wpre_d = torch.from_numpy(wpre.reshape(-1).copy()).to(device)
+    NL.check(L.hs_pq_dict_remap(codes.data_ptr(), fo_d.data_ptr(), nf, n, dw, present.data_ptr(),
+                                wpre_d.data_ptr(), NL.stream_ptr()), "hs_pq_dict_remap")
+    return [np.nonzero(bits[f])[0] for f in range(nf)]
 
 
 def _values(dc: DeviceColumn, ph: _Phys):
@@ -356,14 +395,22 @@ def _values(dc: DeviceColumn, ph: _Phys):
 
 
 def plan_columns(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: pa.Schema,
-                 pages: np.ndarray, device) -> Optional[List[ColPlan]]:
+                 pages: np.ndarray, device, files=None) -> Optional[List[ColPlan]]:
     """Encode every column's pages on the device; None (reason in ``LAST_FALLBACK``) if some
     column needs the pyarrow writer.  Nullable columns get definition-level bits per page and
-    only their non-null values encoded (RLE_DICTIONARY codes, PLAIN values or BOOLEAN bits)."""
+    only their non-null values encoded (RLE_DICTIONARY codes, PLAIN values or BOOLEAN bits).
+    Dictionary columns get one dictionary per file of ``files`` (``page_table``; all pages one
+    file when None): ``ColPlan.fdict_page`` / ``fdict_count`` / ``fbw`` per file index."""
     import torch
     plans = []
     n_pg = pages["n"].astype(np.int64)
     r0_pg = pages["row0"].astype(np.int64)
+    if files is None:
+        files = [(0, [(0, len(pages), int(n_pg.sum()))])]
+    fpg = [_file_pages(f) for f in files]
+    page_file = np.empty(len(pages), dtype=np.int64)
+    for fi, (p0, p1) in enumerate(fpg):
+        page_file[p0:p1] = fi
     for name in names:
         dc = cols[name]
         t = schema.field(name).type
@@ -396,8 +443,8 @@ def plan_columns(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: pa
                 LAST_FALLBACK["reason"] = f"column {name}: string dictionary over " \
                                           f"{DICT_MAX_STRINGS} entries"
                 return None
-            codes = v
-            cp.dict_page = _string_dict_page(d) if len(d) else np.zeros(0, np.uint8)
+            codes = v.to(torch.int32) if v.dtype != torch.int32 else v.clone()
+            cp.dict_page = d
             cp.dict_count = len(d)
         elif ph.ptype == 0:
             out, off = _pack(v, c0, m, 1, device)
@@ -413,13 +460,31 @@ def plan_columns(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: pa
                     if u.numel() <= DICT_MAX:
                         codes, _ = _dict_codes(v, ph.eb, u, device)
             if codes is not None:
-                cp.dict_page = u.cpu().numpy().view(np.uint8)
+                cp.dict_page = u.cpu().numpy()
                 cp.dict_count = int(u.numel())
         if codes is not None:
             cp.dict = True
-            cp.bw = _bit_width(cp.dict_count)
-            cp.payload, cp.page_off = _pack(codes.to(torch.int32) if codes.dtype != torch.int32
-                                            else codes, c0, m, cp.bw, device)
+            codes = codes.to(torch.int32) if codes.dtype != torch.int32 else codes
+            # file row ranges in this column's (non-null) value positions
+            fo = np.array([c0[p0] for p0, _ in fpg] + [c0[fpg[-1][1] - 1] + m[fpg[-1][1] - 1]],
+                          dtype=np.int64)
+            subsets = _file_dicts(codes, cp.dict_count, fo, device) if cp.dict_count else \
+                [np.zeros(0, np.int64)] * len(files)
+            cp.fdict_page, cp.fdict_count, cp.fbw = [], [], []
+            for idx in subsets:
+                if ph.ptype == 6:
+                    page = _string_dict_page(cp.dict_page.take(pa.array(idx, pa.int64()))) \
+                        if len(idx) else _string_dict_page(pa.array([""], pa.string()))
+                else:
+                    # a file whose values are all null still gets a one-entry dictionary
+                    page = cp.dict_page[idx].view(np.uint8) if len(idx) else \
+                        np.zeros(ph.eb, np.uint8)
+                cp.fdict_page.append(np.ascontiguousarray(page))
+                cp.fdict_count.append(max(1, len(idx)))
+                cp.fbw.append(_bit_width(max(1, len(idx))))
+            cp.dict_page = None
+            cp.bw = max(cp.fbw)
+            cp.payload, cp.page_off = _pack(codes, c0, m, np.asarray(cp.fbw)[page_file], device)
         elif ph.ptype != 0:
             cp.payload = v.contiguous().view(torch.uint8) if v.numel() else \
                 torch.zeros(16, dtype=torch.uint8, device=device)
@@ -480,13 +545,15 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
     if not files:
         return []
     t_plan = time.perf_counter()
-    plans = plan_columns(cols, names, schema, pages, device)
+    plans = plan_columns(cols, names, schema, pages, device, files)
     WRITE_PHASES["plan_columns_s"] = WRITE_PHASES.get("plan_columns_s", 0.0) + \
         time.perf_counter() - t_plan
     if plans is None:
         return None
     for cp in plans:
-        cp.dict_z = snappy_stream_host(cp.dict_page) if cid == 1 and cp.dict else None
+        cp.fdict_z = [snappy_stream_host(dp) for dp in cp.fdict_page] \
+            if cid == 1 and cp.dict else None
+    file_index = {f[0]: fi for fi, f in enumerate(files)}
     # every device segment: each column's values, then the level bits of nullable columns
     segs = [cp for cp in plans] + [cp.levels for cp in plans if cp.levels is not None]
     lev_index = {}
@@ -612,14 +679,15 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
                         w.name = cp.bname
                         ph = cp.ph
                         w.ptype, w.logical, w.lp0, w.lp1 = ph.ptype, ph.logical, ph.lp0, ph.lp1
-                        w.dict, w.bit_width = int(cp.dict), cp.bw
+                        fi = file_index[b]
+                        w.dict, w.bit_width = int(cp.dict), cp.fbw[fi] if cp.dict else cp.bw
                         w.codec, w.nullable = cid, int(cp.nullable)
                         if cp.dict:
-                            dp = cp.dict_z if cid == 1 else cp.dict_page
+                            dp = cp.fdict_z[fi] if cid == 1 else cp.fdict_page[fi]
                             w.dict_page = dp.ctypes.data
                             w.dict_bytes = dp.nbytes
-                            w.dict_raw_bytes = cp.dict_page.nbytes
-                            w.dict_count = cp.dict_count
+                            w.dict_raw_bytes = cp.fdict_page[fi].nbytes
+                            w.dict_count = cp.fdict_count[fi]
                         pgs = (WPage * pn)()
                         nulls = 0
                         for q in range(pn):

@@ -186,7 +186,9 @@ def lib():
     _sig(L.hs_join_index, I, P, I, P, P, I, P, P)
     _sig(L.hs_pq_decode_values, I, P, P, I64, I64, I64, I, P, P)
     _sig(L.hs_pq_decode_levels, I, P, P, I64, P, P)
-    _sig(L.hs_pq_pack, I, P, P, I, I64, I, P, P)
+    _sig(L.hs_pq_pack, I, P, P, I, I64, I, P, P, P)
+    _sig(L.hs_pq_dict_mark, I, P, P, I, I64, I, P, P)
+    _sig(L.hs_pq_dict_remap, I, P, P, I, I64, I, P, P, P)
     _sig(L.hs_pq_warmup, I, P)
     _sig(L.hs_pq_decode_pages, I, P, P, P, I, P, P)
     _sig(L.hs_pq_page_struct_size, I)

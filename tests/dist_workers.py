@@ -239,7 +239,8 @@ def spmd_stream_build(ctx, data_dir):
         Hyperspace(s).createIndex(s.read.parquet(os.path.join(data_dir, "src")),
                                   IndexConfig(name, ["k"], ["d", "p", "q"]))
         st = device_build.LAST_BUILD_STATS
-        out[name] = {"passes": st.get("passes"), "groups": st.get("file_groups")}
+        out[name] = {"passes": st.get("passes"), "groups": st.get("file_groups"),
+                     "writer": st.get("writer"), "writer_fallback": st.get("writer_fallback")}
     ctx.barrier()
     return out
 

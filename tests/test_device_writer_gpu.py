@@ -105,3 +105,24 @@ def test_device_writer_covers_nullable_and_typed_columns(mixed, tmp_path):
             assert not ({"k", "x", "b", "ts", "s"} & staging.HOST_DECODED), staging.HOST_DECODED
         want = gr
     assert want
+
+
+def test_file_dicts_match_numpy(device):
+    """Per-file dictionaries (hs_pq_dict_mark / hs_pq_dict_remap): codes into a job-wide
+    dictionary become ranks among the codes each file uses; files of 0 rows, of one row, and
+    spanning several 4096-row mark chunks; a 16-bit wide dictionary."""
+    import torch
+    from hyperspace_amd.exec import pq_encode as PE
+    rng = np.random.default_rng(5)
+    for n_dict, sizes in ((11, [0, 1, 5000, 9000, 3, 4096, 12000]),
+                          (40_000, [70_000, 10, 0, 33_333])):
+        fo = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        codes = rng.integers(0, n_dict, int(fo[-1])).astype(np.int32)
+        d = torch.from_numpy(codes.copy()).to(device)
+        subsets = PE._file_dicts(d, n_dict, fo, device)
+        got = d.cpu().numpy()
+        for f in range(len(sizes)):
+            c = codes[fo[f]:fo[f + 1]]
+            u = np.unique(c)
+            assert np.array_equal(subsets[f], u)
+            assert np.array_equal(got[fo[f]:fo[f + 1]], np.searchsorted(u, c))
