@@ -208,6 +208,221 @@ def gen_run_tags(p: NL.JoinParams, compacts, W: int, T: int) -> J.Kernel:
     return J.Kernel(src, "hs_jit_run_tags", args)
 
 
+# phase 1, direct form: 64-run groups per unrolled iteration of a wavefront
+RT2_UNROLL = int(os.environ.get("HS_JIT_RT2_UNROLL", "4"))
+# 1: phase 1 maps runs to right rows by guess-and-verify (gen_run_tags2); 0: per-tile LDS search
+RT2 = os.environ.get("HS_JIT_RT2", "1") == "1"
+RT2_GRID = int(os.environ.get("HS_JIT_RT2_GRID", "8192"))
+
+
+def tags2_shape(p: NL.JoinParams, compacts, W: int) -> tuple:
+    cols = tuple(sorted((s, c) for s, c in J._col_specs(p, compacts).items()
+                        if s >= SPLIT or s == p.lkey))
+    preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
+                   p.preds[k].group) for k in range(p.nlp, p.npreds))
+    return ("run_tags2", cols, preds, p.nlp, p.lkey, p.rkey, _tags_grouped(p) and p.group_col,
+            W, RT2_UNROLL, J.BLOCK)
+
+
+def _tags_grouped(p: NL.JoinParams) -> bool:
+    """Whether the tags carry a right-side group code: a right group key with more than one
+    group (a single group's domain [group_base, group_base + 1) holds every value of the column,
+    which is non-null here: ``applies``)."""
+    return p.group_col >= SPLIT and p.num_groups > 1
+
+
+def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
+    """Phase 1, direct form: no tiles and no LDS.  Each wavefront owns a contiguous chunk of
+    64-run groups of the left run list (so it owns whole 2W-word stretches of the tag bitmap
+    and stores them without atomics).  Lane l of a group guesses the right row of its run: the
+    previous group's last match + 1 + l (or, at a range start, the range-relative position) -
+    exact for a foreign key whose every right key has left rows, the common case - and verifies
+    it with one compare of the 32-bit key images; a mismatch gallops from the guess to the
+    lower bound (exact for any sorted unique right keys).  The right predicate and group
+    columns are loaded at the guess together with the key, so a verified guess costs one round
+    trip; RT2_UNROLL groups are in flight per iteration.
+
+    Ranges (``RNG``, NRG x 4 int64, sorted by first run): [first run, end run) of each left row
+    range and the right bucket's rows [s0, s1)."""
+    args = J.Args()
+    lk, rk = p.lkey, p.rkey
+    args.add("p", f"RK{lk}", "const int*")
+    args.add("p", "RNG", "const long long*")
+    args.add("p", "tags", "unsigned*")
+    for n in ("NRG", "NRUNS", "KLO", "KSP", "KOF"):
+        args.add("q", n, "long long")
+    cols = J._col_specs(p, compacts)
+    rpreds = _rpreds(p)
+    rgroup = _tags_grouped(p)
+    stage_slots = list(dict.fromkeys([rk] + J._pred_slots(rpreds) +
+                                     ([p.group_col] if rgroup else [])))
+    U = max(1, RT2_UNROLL)  # noqa: N806
+    WV = J.BLOCK // 64  # noqa: N806
+    MASK = (1 << W) - 1  # noqa: N806
+    g = J._Gen(args, cols, SPLIT, ("row_", "row_"), frozenset(), True)
+    rv = J._valid_expr(g, rk, "row_")
+    if rgroup:
+        gb = args.add("q", "group_base", "long long")
+        ng = args.add("q", "num_groups", "long long")
+    img = (f"({rv} ? 0u : ({{ const i64 d_ = (i64)({g.value(rk, 'row_')}) - a.KLO; "
+           f"d_ < 0 ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }}))")
+
+    def tag_expr(gen: J._Gen, it, ok: str) -> str:
+        cond = J._rename(gen.cnf(rpreds), stage_slots, it)
+        if not rgroup:
+            return f"(({ok}) && {cond} ? 1u : 0u)"
+        gx = J._rename(f"x{p.group_col}", stage_slots, it)
+        return (f"({{ const i64 gl_ = (i64){gx} - {gb}; (({ok}) && {cond} && gl_ >= 0 && "
+                f"gl_ < {ng}) ? (unsigned)(gl_ + 1) : 0u; }})")
+
+    b: List[str] = [
+        f"  auto IMG = [&](i64 row_) -> unsigned {{ return {img}; }};",
+        "  const int lane = (int)(threadIdx.x & 63);",
+        "  const i64 G = (a.NRUNS + 63) >> 6;",
+        f"  const i64 nwv = (i64)gridDim.x * {WV};",
+        # wavefront-uniform (scalar registers, scalar loads of the range table)
+        f"  const i64 wv = (i64)blockIdx.x * {WV} + "
+        "(i64)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));",
+        "  const i64 per = (G + nwv - 1) / nwv;",
+        "  const i64 gbeg = wv * per;",
+        "  const i64 gend = G < gbeg + per ? G : gbeg + per;",
+        "  if (gbeg >= gend || a.NRG <= 0) return;",
+        "  const i64* RG = a.RNG;",
+        "  int rg = 0;",
+        "  { int lo = 0, hi = (int)a.NRG; const i64 r0 = gbeg << 6;",
+        "    while (hi - lo > 1) { const int m = (lo + hi) >> 1; "
+        "if (RG[4 * m] <= r0) lo = m; else hi = m; }",
+        "    rg = lo; }",
+        "  i64 lr0 = RG[4 * rg], lr1 = RG[4 * rg + 1], s0 = RG[4 * rg + 2], s1 = RG[4 * rg + 3];",
+        "  i64 nxt0 = rg + 1 < a.NRG ? RG[4 * (rg + 1)] : 0x7fffffffffffffffll;",
+        "  i64 gbase = -1;   // right row of the next group's first run (-1: range-relative)",
+        f"  for (i64 gi = gbeg; gi < gend; gi += {U}) {{",
+        "    while (nxt0 <= (gi << 6)) {",
+        "      ++rg; lr0 = RG[4 * rg]; lr1 = RG[4 * rg + 1]; s0 = RG[4 * rg + 2];",
+        "      s1 = RG[4 * rg + 3]; gbase = -1;",
+        "      nxt0 = rg + 1 < a.NRG ? RG[4 * (rg + 1)] : 0x7fffffffffffffffll; }",
+        # wavefront-uniform: every run of this iteration's groups belongs to range rg (or none)
+        f"    if (((gi + {U}) << 6) <= nxt0) {{"]
+    ind = "      "
+
+    def group(u: int, fast: bool, ind: str) -> None:
+        """Loads and guess of group u: unconditional (clamped) loads in the fast form, so all
+        U groups' loads are in flight together (a load under a per-lane condition makes the
+        compiler wait for it before the branches merge)."""
+        b.extend([f"{ind}const i64 r{u} = ((gi + {u}) << 6) + lane;",
+                  f"{ind}const bool in{u} = gi + {u} < gend;"])
+        if fast:
+            b.append(f"{ind}const i64 l0_{u} = lr0, l1_{u} = lr1, a0_{u} = s0, a1_{u} = s1; "
+                     f"const bool own{u} = true;")
+        else:
+            b.extend([f"{ind}i64 l0_{u} = lr0, l1_{u} = lr1, a0_{u} = s0, a1_{u} = s1; "
+                  f"bool own{u} = true;",
+                  f"{ind}if (r{u} >= nxt0) {{ own{u} = false; int q_ = rg;",
+                  f"{ind}  while (q_ + 1 < (int)a.NRG && RG[4 * (q_ + 1)] <= r{u}) ++q_;",
+                  f"{ind}  l0_{u} = RG[4 * q_]; l1_{u} = RG[4 * q_ + 1]; a0_{u} = RG[4 * q_ + 2]; "
+                  f"a1_{u} = RG[4 * q_ + 3]; }}"])
+        b.extend([f"{ind}const bool act{u} = in{u} && r{u} < a.NRUNS && r{u} >= l0_{u} && "
+              f"r{u} < l1_{u} && a1_{u} > a0_{u};",
+              f"{ind}const unsigned key{u} = (unsigned)a.RK{lk}[act{u} ? r{u} : 0] + "
+              f"(unsigned)a.KOF;",
+              f"{ind}i64 j{u} = (own{u} && gbase >= 0) ? gbase + {u * 64} + lane : "
+              f"a0_{u} + (r{u} - l0_{u});",
+              f"{ind}j{u} = act{u} ? (j{u} < a0_{u} ? a0_{u} : (j{u} >= a1_{u} ? a1_{u} - 1 : j{u}))"
+              f" : 0;",
+              f"{ind}const unsigned k{u} = IMG(j{u});"])
+        gu = J._Gen(args, cols, SPLIT, (f"j{u}", f"j{u}"), frozenset(), True)
+        for sl in stage_slots:
+            J._uload(gu, sl, f"g{u}", b, ind)
+
+    def resolve(u: int, ind: str) -> None:
+        gu = J._Gen(args, cols, SPLIT, (f"j{u}", f"j{u}"), frozenset(), True)
+        b.extend([f"{ind}bool hit{u} = act{u} && k{u} == key{u};",
+                  f"{ind}i64 m{u} = j{u};",
+                  f"{ind}unsigned tg{u} = {tag_expr(gu, f'g{u}', f'hit{u}')};",
+                  f"{ind}if (act{u} && !hit{u}) {{",
+                  # gallop from the guess to the lower bound of key in [a0, a1)
+                  f"{ind}  const unsigned key_ = key{u}; i64 lo_, hi_;",
+                  f"{ind}  if (k{u} > key_) {{",
+                  f"{ind}    hi_ = j{u}; i64 st_ = 1; lo_ = j{u} - 1;",
+                  f"{ind}    while (lo_ > a0_{u} && IMG(lo_) >= key_) {{ hi_ = lo_; st_ <<= 1; "
+                  f"lo_ = hi_ - st_; }}",
+                  f"{ind}    if (lo_ < a0_{u}) lo_ = a0_{u};",
+                  f"{ind}  }} else {{",
+                  f"{ind}    lo_ = j{u} + 1; i64 st_ = 1; hi_ = j{u} + 1;",
+                  f"{ind}    while (hi_ < a1_{u} && IMG(hi_) < key_) {{ lo_ = hi_ + 1; st_ <<= 1; "
+                  f"hi_ = j{u} + st_; }}",
+                  f"{ind}    if (hi_ > a1_{u}) hi_ = a1_{u};",
+                  f"{ind}  }}",
+                  f"{ind}  while (lo_ < hi_) {{ const i64 md_ = (lo_ + hi_) >> 1; "
+                  f"if (IMG(md_) < key_) lo_ = md_ + 1; else hi_ = md_; }}",
+                  f"{ind}  m{u} = lo_;",
+                  f"{ind}  hit{u} = lo_ < a1_{u} && IMG(lo_) == key_;",
+                  f"{ind}  const i64 jm{u} = hit{u} ? lo_ : 0;"])
+        gm = J._Gen(args, cols, SPLIT, (f"jm{u}", f"jm{u}"), frozenset(), True)
+        for sl in stage_slots:
+            J._uload(gm, sl, f"h{u}", b, ind + "  ")
+        b.extend([f"{ind}  tg{u} = {tag_expr(gm, f'h{u}', f'hit{u}')};",
+                  f"{ind}}}"])
+        # the group's 2W tag words: whole words, plain stores
+        if W == 1:
+            b.extend([f"{ind}{{ const u64 bal_ = __ballot(tg{u} != 0u);",
+                      f"{ind}  if (in{u} && lane < 2) a.tags[((gi + {u}) << 1) + lane] = "
+                      f"(unsigned)(bal_ >> (32 * lane)); }}"])
+        else:
+            per_w = 32 // W
+            b.extend([f"{ind}{{ unsigned wd_ = 0u;",
+                      f"{ind}  for (int i_ = 0; i_ < {per_w}; ++i_) {{",
+                      f"{ind}    const int src_ = ((lane * {per_w}) + i_) & 63;",
+                      f"{ind}    wd_ |= (((unsigned)__shfl((int)tg{u}, src_, 64)) & {MASK}u) << "
+                      f"(unsigned)(i_ * {W}); }}",
+                      f"{ind}  if (in{u} && lane < {2 * W}) a.tags[(gi + {u}) * {2 * W} + lane] = "
+                      f"wd_; }}"])
+
+    def iteration(fast: bool, ind: str) -> None:
+        for u in range(U):
+            group(u, fast, ind)
+        for u in range(U):
+            resolve(u, ind)
+        # next iteration's guess: the last group's last lane, when it matched in this range
+        b.extend([f"{ind}{{ const i64 nx_ = __shfl((hit{U - 1} && own{U - 1}) ? m{U - 1} + 1 : "
+                  f"(i64)-1, 63, 64);",
+                  f"{ind}  gbase = nx_; }}"])
+    iteration(True, ind)
+    b.append("    } else {   // a range starts inside this iteration's groups")
+    iteration(False, ind)
+    b += ["    }", "  }"]
+    src = (J._PRELUDE + args.struct_src() +
+           f'extern "C" __global__ __launch_bounds__({J.BLOCK}) void hs_jit_run_tags2(Args a) {{\n' +
+           "\n".join(b) + "\n}\n")
+    return J.Kernel(src, "hs_jit_run_tags2", args)
+
+
+def run_ranges(rstart, rlen, rbucket, roff, runs):
+    """RNG of ``gen_run_tags2``: per non-empty left row range (first run, end run, right bucket
+    rows [s0, s1)), sorted by first run; computed once per lowering (one small D2H)."""
+    import numpy as np
+    import torch
+    rs = rstart.cpu().numpy().astype(np.int64)
+    rl = rlen.cpu().numpy().astype(np.int64)
+    rb = rbucket.cpu().numpy().astype(np.int64)
+    ro = roff.cpu().numpy().astype(np.int64)
+    keep = rl > 0
+    rs, rl, rb = rs[keep], rl[keep], rb[keep]
+    if len(rs) == 0:
+        return np.zeros((0, 4), np.int64)
+    rows = np.concatenate([rs, rs + rl - 1])
+    gi = torch.from_numpy(rows >> 6).to(runs.gmask.device)
+    gm = runs.gmask.index_select(0, gi).cpu().numpy().view(np.uint64)
+    gr = runs.gruns.index_select(0, gi).cpu().numpy().astype(np.int64)
+    full = (1 << 64) - 1
+    # run of a row: the group's first run + run starts among the group's rows 1..i
+    run = np.array([int(g_) + bin(int(m_) & (((2 << int(r_ & 63)) - 2) & full)).count("1")
+                    for g_, m_, r_ in zip(gr, gm, rows)], dtype=np.int64)
+    n = len(rs)
+    out = np.stack([run[:n], run[n:] + 1, ro[rb], ro[rb + 1]], axis=1)
+    return out[np.argsort(out[:, 0], kind="stable")]
+
+
 def scan_shape(p: NL.JoinParams, compacts, W: int, NI: int) -> tuple:
     cols = tuple(sorted((s, c) for s, c in J._col_specs(p, compacts).items() if s < SPLIT))
     preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
@@ -319,7 +534,8 @@ class TwoPhaseLauncher:
         aggs = [p.aggs[i] for i in range(p.naggs)]
         vt = dict(self.vt)
         J.fill_preds_aggs(vt, preds, [], self.compacts)
-        self.tags.zero_()
+        if "RNG" not in vt:   # the tile form ORs into a zeroed bitmap; the direct form stores
+            self.tags.zero_()  # every word of every run group
         st = NL.stream_ptr()
         self.kt.launch(self.grid_t, vt, st)
         parts = J._partials(self.grid_s, self.GA, self.dev)
@@ -343,16 +559,28 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
     dev = rstart.device
     max_tiles = nrows // T + 2 * rstart.numel() + 2
     tp, spans = J._join_spans(p, rstart, rlen, rbucket, roff, max_tiles, T, cache_spans, align=NI)
-    tr = J._tile_runs(tp, spans, rstart.numel(), runs, max_tiles, cache_spans)
-    kt = J.kernel_for(tags_shape(p, compacts, W, T), lambda: gen_run_tags(p, compacts, W, T))
     ks = J.kernel_for(scan_shape(p, compacts, W, NI), lambda: gen_run_scan(p, compacts, W, NI))
     nruns = int(runs.runkeys.numel())
     KW = ((31 + (NI - 1) * W) >> 5) + 1  # noqa: N806
-    tags = torch.empty(((nruns * W + 31) >> 5) + KW + 2, dtype=torch.int32, device=dev)
+    nwords = max((nruns * W + 31) >> 5, ((nruns + 63) >> 6) * 2 * W)
+    tags = torch.empty(nwords + KW + 2, dtype=torch.int32, device=dev)
     frame = J._key32_frame(p, compacts)
-    vt = {"tile_prefix": tp.data_ptr(), "spans": spans.data_ptr(), "TR": tr.data_ptr(),
-          "tags": tags.data_ptr(), "R": rstart.numel(),
-          "num_groups": p.num_groups, "group_base": p.group_base}
+    if RT2 and int(roff[-1].item()) > 0:
+        rng = run_ranges(rstart, rlen, rbucket, roff, runs)
+        rng_d = torch.from_numpy(rng.reshape(-1).copy() if len(rng) else
+                                 __import__("numpy").zeros(4, "int64")).to(dev)
+        kt = J.kernel_for(tags2_shape(p, compacts, W), lambda: gen_run_tags2(p, compacts, W))
+        vt = {"RNG": rng_d.data_ptr(), "NRG": len(rng), "NRUNS": nruns, "tags": tags.data_ptr(),
+              "num_groups": p.num_groups, "group_base": p.group_base}
+        tr = rng_d
+        grid_t = max(1, RT2_GRID)
+    else:
+        tr = J._tile_runs(tp, spans, rstart.numel(), runs, max_tiles, cache_spans)
+        kt = J.kernel_for(tags_shape(p, compacts, W, T), lambda: gen_run_tags(p, compacts, W, T))
+        vt = {"tile_prefix": tp.data_ptr(), "spans": spans.data_ptr(), "TR": tr.data_ptr(),
+              "tags": tags.data_ptr(), "R": rstart.numel(),
+              "num_groups": p.num_groups, "group_base": p.group_base}
+        grid_t = max(1, J.MJ_GRID)
     vt["KLO"], vt["KSP"], vt["KOF"] = frame
     J._fill_cols(vt, p.cols, compacts)
     vs = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
@@ -360,7 +588,6 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
           "num_groups": p.num_groups, "group_base": p.group_base}
     J._fill_cols(vs, p.cols, compacts)
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
-    grid_t = max(1, J.MJ_GRID)
     grid_s = max(1, J.SCAN_GRID or NL.lib().hs_scan_grid())
     return TwoPhaseLauncher(kt, ks, grid_t, grid_s, GA, GA * 32 if _scan_grouped(p) else 0,
                             vt, vs, compacts, (rstart, rlen, rbucket, roff, tp, spans, tr, runs),

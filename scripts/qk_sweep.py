@@ -150,14 +150,19 @@ def main():
         with open(args.configs[1:]) as f:
             args.configs = f.read()
     configs = json.loads(args.configs) if args.configs else DEFAULT
-    base = {k: getattr(jit, k) for c in configs for k in c}
+    from hyperspace_amd.exec import jit_runs
+
+    def owner(k):   # knobs of the two-phase run-keyed join live in exec/jit_runs.py
+        return jit if hasattr(jit, k) else jit_runs
+    base = {k: getattr(owner(k), k) for c in configs for k in c}
     for cfg in configs:
         for k, v in base.items():
-            setattr(jit, k, v)
+            setattr(owner(k), k, v)
         for k, v in cfg.items():
-            setattr(jit, k, v)
+            setattr(owner(k), k, v)
         jit._KERNELS.clear()
         backend.graphs._lru.clear()
+        backend.__dict__.pop("_agg_preps", None)   # prepared lowerings hold launchers
         if args.only_merge:
             s.conf.set("spark.hyperspace.mi.joinIndex.enabled", "false")
             out = {"cfg": cfg, "q3_merge": timed(q3, args.reps)}

@@ -811,7 +811,7 @@ def test_merge_join_runs_matches_oracle(device):
     for a, b_ in zip((rc.runkeys, rc.gmask, rc.gruns), ref):
         assert torch.equal(a.cpu(), b_)
     from hyperspace_amd.exec import jit_runs
-    lds_keys, runs, two2 = jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P
+    lds_keys, runs, two2, rt2 = jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P, jit_runs.RT2
     try:
         for starts, lens in ((loff[:-1], loff[1:] - loff[:-1]),
                              (loff[:-1] + 5, loff[1:] - loff[:-1] - 9)):
@@ -827,8 +827,10 @@ def test_merge_join_runs_matches_oracle(device):
             rbk = torch.arange(B, dtype=torch.int32, device=device)
             roff_t = torch.from_numpy(roff).to(device)
             for keys in (lds_keys, 32):
-                for use_runs, two in ((True, True), (True, False), (False, False)):
+                for use_runs, two, direct in ((True, True, True), (True, True, False),
+                                              (True, False, False), (False, False, False)):
                     jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P = keys, use_runs, two
+                    jit_runs.RT2 = direct
                     got = [t.cpu().numpy() for t in
                            jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, comp, nrows=len(lk),
                                               rdup=False)]
@@ -838,4 +840,4 @@ def test_merge_join_runs_matches_oracle(device):
                     if two:
                         assert isinstance(jit.LAST_MJ_LAUNCHER[0], jit_runs.TwoPhaseLauncher)
     finally:
-        jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P = lds_keys, runs, two2
+        jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P, jit_runs.RT2 = lds_keys, runs, two2, rt2
