@@ -112,6 +112,8 @@ def eval_expr(e: E.Expression, t: pa.Table):
     if type(e) in _ARITH:
         a, b = _operands(e, t)
         return _ARITH[type(e)](a, b)
+    if isinstance(e, E.Remainder):
+        return _remainder(*_operands(e, t))
     if isinstance(e, E.Divide):
         # Spark: a double division, NULL for a zero divisor
         a, b = _operands(e, t)
@@ -127,6 +129,33 @@ def eval_expr(e: E.Expression, t: pa.Table):
             return pc.cast(v, e.dtype, safe=False)
         return pc.cast(v, e.dtype)
     raise NotImplementedError(f"cannot evaluate {type(e).__name__}")
+
+
+def _remainder(a, b):
+    """Spark ``%``: truncated remainder (sign of the dividend), NULL for a zero divisor or a
+    NULL operand; ``fmod`` for floating-point operands; Long.MIN_VALUE % -1 = 0."""
+    import numpy as np
+    a = a if isinstance(a, (pa.Array, pa.ChunkedArray)) else pa.array([a.as_py()] * 1)
+    n = max(len(a), len(b)) if isinstance(b, (pa.Array, pa.ChunkedArray)) else len(a)
+    def arr(x):
+        if isinstance(x, pa.Scalar):
+            return pa.array([x.as_py()] * n, x.type)
+        return x.combine_chunks() if isinstance(x, pa.ChunkedArray) else x
+    a, b = arr(a), arr(b)
+    f = pa.types.is_floating(a.type) or pa.types.is_floating(b.type)
+    out_t = pa.float64() if f else pa.int64()
+    av = np.asarray(pc.fill_null(pc.cast(a, out_t), 0).to_numpy(zero_copy_only=False))
+    bv = np.asarray(pc.fill_null(pc.cast(b, out_t), 0).to_numpy(zero_copy_only=False))
+    bad = np.asarray(pc.or_kleene(pc.is_null(a), pc.is_null(b)).to_numpy(zero_copy_only=False))
+    bad = bad | (bv == 0)
+    if f:
+        with np.errstate(invalid="ignore"):
+            r = np.fmod(av, np.where(bad, 1.0, bv))
+    else:
+        safe = np.where(bad | (bv == -1), 1, bv)
+        r = np.fmod(av, safe)          # C / JVM truncated remainder
+        r = np.where(bv == -1, 0, r)
+    return pa.array(r, out_t, mask=bad)
 
 
 def _float_to_int(v, dtype: pa.DataType):

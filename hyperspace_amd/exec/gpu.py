@@ -349,20 +349,28 @@ class GpuBackend:
         columns, or would take more than a quarter of the device cache."""
         import torch
         conf = self.session.conf
-        if str(conf.get("spark.hyperspace.mi.hybridMerge.enabled", "true")).lower() != "true":
+
+        def skip(why: str):
+            self.metrics["hybrid_merge_skip"] = why
             return None
+        if str(conf.get("spark.hyperspace.mi.hybridMerge.enabled", "true")).lower() != "true":
+            return skip("disabled")
         d = self._dist()
         if d is not None and d.world > 1:
-            return None
-        if any(x.table is None or x.conds or x.extra or x.split or x.parts for x in parts):
-            return None
+            return skip("world > 1")
+        for x in parts:
+            if x.table is None or x.conds or x.extra or x.split or x.parts:
+                return skip("part: " + ", ".join(
+                    n for n, v in (("no table", x.table is None), ("conds", x.conds),
+                                   ("extra", x.extra), ("split", x.split), ("parts", x.parts))
+                    if v))
         first = parts[0]
         outs = list(p.output)
         ids = {u.expr_id for u in outs}
         if not first.sort_attrs or any(a.expr_id not in ids for a in first.sort_attrs):
-            return None
+            return skip("sort attributes not in the output")
         key = tuple(id(x.table) for x in parts) + tuple(u.expr_id for u in outs)
-        memo = self.__dict__.setdefault("_unions", {})
+        memo = self.__dict__.setdefault("_hybrid_unions", {})
         hit = memo.get(key)
         if hit is not None and all(a is b for a, b in zip(hit[0], [x.table for x in parts])) \
                 and self._holds(hit[1]):
@@ -377,11 +385,11 @@ class GpuBackend:
                        (c.dictionary is None) != (c0.dictionary is None) or
                        (c.dictionary is not None and not c.dictionary.equals(c0.dictionary))
                        for c in cs):
-                    return None
+                    return skip(f"column {u.name}: parts differ in type or dictionary")
                 cols.append(cs)
             nbytes = sum(c.data.numel() * c.data.element_size() for cs in cols for c in cs)
             if nbytes > HyperspaceConf.device_cache_bytes(conf) // 4:
-                return None
+                return skip("over a quarter of the device cache")
             nb = first.num_buckets
             with stage("hybrid.merge"):
                 bucket = torch.cat([torch.repeat_interleave(
@@ -412,6 +420,7 @@ class GpuBackend:
             if len(memo) > 8:
                 memo.clear()
             memo[key] = ([x.table for x in parts], table)
+        self.metrics.pop("hybrid_merge_skip", None)
         colmap = {u.expr_id: f"u{j}" for j, u in enumerate(outs)}
         return DRel(table, colmap, outs, [], True, first.sort_attrs, first.bucket_attrs,
                     first.num_buckets)

@@ -137,12 +137,24 @@ class _Gen:
         if isinstance(e, E.Literal):
             return self.lit(e)
         self.shape.append(type(e).__name__)
-        if type(e) in _ARITH or isinstance(e, E.Divide) or type(e) in _CMP:
+        if type(e) in _ARITH or isinstance(e, (E.Divide, E.Remainder)) or type(e) in _CMP:
             (a, av, ak), (b, bv, bk) = self.emit(e.left), self.emit(e.right)
             if "b" in (ak, bk):
                 raise Unsupported("arithmetic / comparison on booleans")
             v, ok = self._var(), self._var()
             f = "f" in (ak, bk)
+            if isinstance(e, E.Remainder):
+                # Spark: sign of the dividend, NULL for a zero divisor; x % -1 = 0 (no trap on
+                # LLONG_MIN % -1)
+                if f:
+                    self.lines.append(f"const bool {ok} = {av} && {bv} && (double){b} != 0.0;")
+                    self.lines.append(f"const double {v} = {ok} ? fmod((double){a}, (double){b})"
+                                      f" : 0.0;")
+                    return v, ok, "f"
+                self.lines.append(f"const bool {ok} = {av} && {bv} && (long long){b} != 0;")
+                self.lines.append(f"const long long {v} = (!{ok} || (long long){b} == -1) ? 0 : "
+                                  f"(long long){a} % (long long){b};")
+                return v, ok, "i"
             if isinstance(e, E.Divide):
                 self.lines.append(f"const bool {ok} = {av} && {bv} && (double){b} != 0.0;")
                 self.lines.append(f"const double {v} = {ok} ? (double){a} / (double){b} : 0.0;")

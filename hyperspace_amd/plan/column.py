@@ -64,6 +64,12 @@ class Column:
     def __rmul__(self, o):
         return Column(E.Multiply(_expr(o), self.expr))
 
+    def __mod__(self, o):
+        return Column(E.Remainder(self.expr, _expr(o)))
+
+    def __rmod__(self, o):
+        return Column(E.Remainder(_expr(o), self.expr))
+
     def __truediv__(self, o):
         return Column(E.Divide(self.expr, _expr(o)))
 

@@ -399,6 +399,12 @@ class Multiply(BinaryArithmetic):
     symbol, op = "*", "mul"
 
 
+class Remainder(BinaryArithmetic):
+    """``a % b``: Spark's (and the JVM's) remainder - the sign follows the dividend, NULL for a
+    zero divisor; ``fmod`` for floating-point operands."""
+    symbol, op = "%", "mod"
+
+
 class Divide(BinaryArithmetic):
     symbol, op = "/", "div"
 

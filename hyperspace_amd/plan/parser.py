@@ -143,6 +143,8 @@ class _Parser:
                 e = E.Multiply(e, self.unary())
             elif self.accept("op", "/"):
                 e = E.Divide(e, self.unary())
+            elif self.accept("op", "%"):
+                e = E.Remainder(e, self.unary())
             else:
                 return e
 

@@ -310,7 +310,7 @@ def test_hybrid_scan_join_and_filter_on_device(tpch, tmp_path):
     _close(g, c)
     # the unions ran as merged single tables (GpuBackend._merged_union); the per-part
     # lowering gives the same answers
-    assert s.backend().__dict__.get("_unions")
+    assert s.backend().__dict__.get("_hybrid_unions"), s.backend().metrics.get("hybrid_merge_skip")
     s.conf.set("spark.hyperspace.mi.hybridMerge.enabled", "false")
     try:
         for qq in (q, q2):
