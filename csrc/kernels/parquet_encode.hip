@@ -103,18 +103,28 @@ __global__ __launch_bounds__(256) void hs_pq_dict_mark_kernel(const int32_t* __r
 
 // Remap: code -> its rank among the file's present codes (wpre = exclusive prefix of the
 // present words' popcounts within each file).
+// One workgroup per CH-row chunk, file segment by file segment (the file search runs once per
+// chunk and segment, not per row); the file's present words and prefixes are read through L1.
 __global__ __launch_bounds__(256) void hs_pq_dict_remap_kernel(int32_t* __restrict__ codes,
                                                                const int64_t* __restrict__ fo,
                                                                int nf, int dw,
                                                                const uint32_t* __restrict__ present,
                                                                const int32_t* __restrict__ wpre) {
   const int64_t n = fo[nf];
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  const int f = file_of(fo, nf, r);
-  const uint32_t c = (uint32_t)codes[r];
-  const int64_t w = (int64_t)f * dw + (c >> 5);
-  codes[r] = wpre[w] + __popc(present[w] & ((1u << (c & 31)) - 1u));
+  const int64_t r0 = (int64_t)blockIdx.x * kDictChunk;
+  if (r0 >= n) return;
+  const int64_t r1 = r0 + kDictChunk < n ? r0 + kDictChunk : n;
+  int f = file_of(fo, nf, r0);
+  for (int64_t s = r0; s < r1; ++f) {
+    const int64_t e = fo[f + 1] < r1 ? fo[f + 1] : r1;
+    const uint32_t* pw = present + (int64_t)f * dw;
+    const int32_t* pp = wpre + (int64_t)f * dw;
+    for (int64_t r = s + threadIdx.x; r < e; r += blockDim.x) {
+      const uint32_t c = (uint32_t)codes[r];
+      codes[r] = pp[c >> 5] + __popc(pw[c >> 5] & ((1u << (c & 31)) - 1u));
+    }
+    s = e;
+  }
 }
 
 // codes[i] = index of bits[i] in the sorted dictionary `dict` (n_dict entries); a value that is
@@ -167,7 +177,8 @@ int hs_pq_dict_remap(int32_t* codes, const int64_t* fo, int nf, int64_t n, int d
                      const uint32_t* present, const int32_t* wpre, void* stream) {
   if (n <= 0 || nf <= 0) return 0;
   (void)hipGetLastError();
-  hipLaunchKernelGGL(hs_pq_dict_remap_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+  hipLaunchKernelGGL(hs_pq_dict_remap_kernel, dim3((unsigned)((n + kDictChunk - 1) / kDictChunk)),
+                     dim3(256), 0,
                      (hipStream_t)stream, codes, fo, nf, dw, present, wpre);
   return (int)hipGetLastError();
 }

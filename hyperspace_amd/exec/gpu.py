@@ -332,13 +332,40 @@ class GpuBackend:
                     colmap[u.expr_id] = r.colmap[c.expr_id]
             parts.append(r.copy(colmap=colmap))
         first = parts[0]
-        merged = self._merged_union(p, parts)
+        merged = self._merged_union(p, parts, [c.output for c in p.children])
         if merged is not None:
             return merged
         return DRel(None, dict(first.colmap), list(p.output), [], True, first.sort_attrs,
                     first.bucket_attrs, nb, parts)
 
-    def _merged_union(self, p: X.BucketUnionExec, parts: List[DRel]) -> Optional[DRel]:
+    @staticmethod
+    def _union_conds(p: X.BucketUnionExec, parts: List[DRel], outputs) -> Optional[list]:
+        """The parts' pending predicates over the union's output attributes when every part
+        carries the same ones (a filter pushed below the union into each child), else None."""
+        keys, conds0 = None, None
+        for x, out in zip(parts, outputs):
+            sub = {c.expr_id: u for u, c in zip(p.output, out)}
+            missing = []
+
+            def ren(e, sub=sub, missing=missing):
+                if isinstance(e, E.Attribute):
+                    u = sub.get(e.expr_id)
+                    if u is None:
+                        missing.append(e)
+                    return u
+                return None
+            conds = [c.transform_up(ren) for c in x.conds]
+            if missing:
+                return None
+            k = sorted(repr(c.canonical_key()) for c in conds)
+            if keys is None:
+                keys, conds0 = k, conds
+            elif k != keys:
+                return None
+        return conds0
+
+    def _merged_union(self, p: X.BucketUnionExec, parts: List[DRel],
+                      outputs=None) -> Optional[DRel]:
         """A Hybrid Scan's bucket union as ONE resident table: the index rows and the appended
         rows (already bucketed and sorted by the device shuffle) of every bucket merged into
         bucket-major order sorted by the index key, built once per (index table, appended
@@ -359,11 +386,15 @@ class GpuBackend:
         if d is not None and d.world > 1:
             return skip("world > 1")
         for x in parts:
-            if x.table is None or x.conds or x.extra or x.split or x.parts:
+            if x.table is None or x.extra or x.split or x.parts:
                 return skip("part: " + ", ".join(
-                    n for n, v in (("no table", x.table is None), ("conds", x.conds),
-                                   ("extra", x.extra), ("split", x.split), ("parts", x.parts))
-                    if v))
+                    n for n, v in (("no table", x.table is None), ("extra", x.extra),
+                                   ("split", x.split), ("parts", x.parts)) if v))
+        # the same filter in every part (pushed below the union) applies to the merged rows
+        conds = self._union_conds(p, parts, outputs) if outputs is not None else \
+            ([] if not any(x.conds for x in parts) else None)
+        if conds is None:
+            return skip("parts carry different predicates")
         first = parts[0]
         outs = list(p.output)
         ids = {u.expr_id for u in outs}
@@ -422,7 +453,7 @@ class GpuBackend:
             memo[key] = ([x.table for x in parts], table)
         self.metrics.pop("hybrid_merge_skip", None)
         colmap = {u.expr_id: f"u{j}" for j, u in enumerate(outs)}
-        return DRel(table, colmap, outs, [], True, first.sort_attrs, first.bucket_attrs,
+        return DRel(table, colmap, outs, conds, True, first.sort_attrs, first.bucket_attrs,
                     first.num_buckets)
 
     def _unary(self, p: X.SparkPlan, r: DRel) -> DRel:
@@ -1582,7 +1613,7 @@ class GpuBackend:
         self._join_rec = None
         if rec is None or res is None or rec[6] is None:
             return
-        left, right, lk, rk, col_info, descs, launcher, specs = rec
+        left, right, lk, rk, col_info, descs, launcher, specs, lconds = rec
         for t in (left.table, right.table):
             if getattr(t, "_hs_cache_key", None) is None:
                 return
@@ -1591,7 +1622,7 @@ class GpuBackend:
             preps.clear()
         preps[id(final)] = _JoinPrep(final, node, left, right, lk, rk, col_info, descs,
                                      launcher, res[4:], self._placement_tag(),
-                                     self._groups_agreed)
+                                     self._groups_agreed, lconds)
 
     def _placement_tag(self):
         d = self._dist()
@@ -2308,10 +2339,13 @@ class GpuBackend:
                                              comp, nrows=left.table.num_rows,
                                              cache_spans=fr is not None and rstart is fr[0],
                                              rdup=jit.key_has_dups(right.col(rk)))
-                    if fr is not None and rstart is fr[0] and probed is None and not implied:
+                    if fr is not None and rstart is fr[0] and probed is None:
                         # full ranges, no probing: the launch can be replayed for this pair
+                        # (``implied`` then holds only isnotnull(key) conjuncts the full ranges
+                        # satisfy; the replay binds the same left conjuncts as this launch)
                         self._join_rec = (left, right, lk, rk, col_info, descs,
-                                          jit.LAST_MJ_LAUNCHER[0], specs)
+                                          jit.LAST_MJ_LAUNCHER[0], specs,
+                                          [c for c in left.conds if id(c) not in implied])
                     return out
                 return jit.join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, max_tiles,
                                     self._compacts(descs),
@@ -2872,13 +2906,15 @@ class _JoinPrep:
     relations, column slots, group domain and the kernel launcher (jit.MergeJoinLauncher).
     A submission re-binds the predicates and aggregate terms and launches."""
     __slots__ = ("final", "node", "left", "right", "lk", "rk", "col_info", "descs", "launcher",
-                 "gtail", "placement", "agreed", "lits", "lowered")
+                 "gtail", "placement", "agreed", "lits", "lowered", "lconds")
 
     def __init__(self, final, node, left, right, lk, rk, col_info, descs, launcher, gtail,
-                 placement, agreed):
+                 placement, agreed, lconds=None):
         self.final, self.node, self.left, self.right = final, node, left, right
         self.lk, self.rk, self.col_info, self.descs = lk, rk, col_info, descs
         self.launcher, self.gtail, self.placement, self.agreed = launcher, gtail, placement, agreed
+        # the left conjuncts the recorded launch bound (same order: predicate slots match)
+        self.lconds = list(left.conds) if lconds is None else list(lconds)
         conds = list(left.conds) + list(right.conds) + \
             ([node.condition] if node.condition is not None else [])
         self.lits = _literals(conds + list(final.aggregates))
@@ -2900,7 +2936,7 @@ class _JoinPrep:
             if low is None:
                 jp, col_info, descs, keep = be._join_params(
                     left, self.right, self.lk, self.rk, self.node.condition,
-                    slots=(self.col_info, self.descs))
+                    lconds=self.lconds, slots=(self.col_info, self.descs))
                 specs = be._agg_specs(fns, col_info)
                 if len(descs) != nd:
                     raise _Stale()
