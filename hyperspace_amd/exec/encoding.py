@@ -25,7 +25,8 @@ _MAX_SCALE_DIGITS = 4
 
 
 class Compact:
-    __slots__ = ("codes", "width", "base", "scale", "logical_type", "lo", "hi", "g16", "runs")
+    __slots__ = ("codes", "width", "base", "scale", "logical_type", "lo", "hi", "g16", "runs",
+                 "_g16_wide")
 
     def __init__(self, codes, width: int, base: int, scale: Optional[float], logical_type: int,
                  lo: Optional[int] = None, hi: Optional[int] = None):
@@ -77,15 +78,30 @@ class GroupedCompact(Compact):
 
 def grouped16(c: Compact, max_wide: float = 0.01) -> Optional[GroupedCompact]:
     """The 16-bit grouped form of the 32-bit integer compact ``c`` (computed once, kept on
-    ``c``), or None when more than ``max_wide`` of its 64-row groups are wide."""
-    if c.g16 is not False:
+    ``c``), or None when more than ``max_wide`` of its 64-row groups are wide (a refusal is
+    re-examined for a more tolerant ``max_wide``)."""
+    if c.g16 is not False and (c.g16 is not None or getattr(c, "_g16_wide", 1.0) >= max_wide):
         return c.g16
     c.g16 = None
+    c._g16_wide = max_wide
     if c.scale is not None or c.lo is None or c.width != 4 or c.codes.numel() == 0:
         return None
+    r = group16(c.codes, max_wide)
+    if r is None:
+        return None
+    c.g16 = GroupedCompact(r[0], r[1], c.codes, c.base, c.logical_type, c.lo, c.hi)
+    return c.g16
+
+
+def group16(x, max_wide: float):
+    """(codes16, gbase) of a sorted-within-groups int32 code array ``x``: per 64-element group
+    its smallest code (``WIDE_GROUP`` when the group spans 2^16 codes or more) and each
+    element's uint16 offset from it (0 in wide groups, whose readers take ``x``); None when more
+    than ``max_wide`` of the groups are wide."""
     import torch
-    x = c.codes
     n = x.numel()
+    if n == 0:
+        return None
     pad = (-n) % GROUP_ROWS
     xp = torch.cat([x, x[-1:].expand(pad)]) if pad else x
     g = xp.view(-1, GROUP_ROWS)
@@ -94,12 +110,10 @@ def grouped16(c: Compact, max_wide: float = 0.01) -> Optional[GroupedCompact]:
     if float(wide.float().mean().item()) > max_wide:
         return None
     gbase = torch.where(wide, torch.full_like(gmin, WIDE_GROUP), gmin)
-    d = (xp.long() - gmin.long().repeat_interleave(GROUP_ROWS))[:n]
-    d = torch.where(wide.repeat_interleave(GROUP_ROWS)[:n], torch.zeros_like(d), d)
+    d = g.long() - gmin.long().unsqueeze(1)
+    d = torch.where(wide.unsqueeze(1), torch.zeros_like(d), d).reshape(-1)[:n]
     codes = torch.where(d >= (1 << 15), d - (1 << 16), d).to(torch.int16)   # uint16 bits
-    c.g16 = GroupedCompact(codes.contiguous(), gbase.contiguous(), x, c.base, c.logical_type,
-                           c.lo, c.hi)
-    return c.g16
+    return codes.contiguous(), gbase.contiguous()
 
 
 class RunCompact(Compact):
@@ -114,16 +128,27 @@ class RunCompact(Compact):
 
     ~1.2 instead of 4 bytes per row at 4 rows per run.  ``codes`` stays the parent's full 32-bit
     codes, so every other reader (spans, aggregate tails, group keys) is unchanged."""
-    __slots__ = ("runkeys", "gmask", "gruns", "nruns")
+    __slots__ = ("runkeys", "gmask", "gruns", "nruns", "k16")
 
     def __init__(self, parent: Compact, runkeys, gmask, gruns):
         super().__init__(parent.codes, parent.width, parent.base, parent.scale,
                          parent.logical_type, parent.lo, parent.hi)
         self.runkeys, self.gmask, self.gruns = runkeys, gmask, gruns
         self.nruns = int(runkeys.numel())
+        self.k16 = False
+
+    def keys16(self, max_wide: float = 0.1):
+        """(runkeys16, group bases) of the run keys, per 64-run group (``group16``; computed
+        once): the run-keyed join's phase 1 reads 2 instead of 4 bytes per run."""
+        if self.k16 is False:
+            self.k16 = group16(self.runkeys, max_wide)
+        return self.k16
 
     def extra_bytes(self) -> int:
-        return self.runkeys.numel() * 4 + self.gmask.numel() * 8 + self.gruns.numel() * 4
+        n = self.runkeys.numel() * 4 + self.gmask.numel() * 8 + self.gruns.numel() * 4
+        if self.k16:
+            n += self.k16[0].numel() * 2 + self.k16[1].numel() * 4
+        return n
 
     def nbytes(self) -> int:
         return self.codes.numel() * self.width + self.extra_bytes()

@@ -213,15 +213,24 @@ RT2_UNROLL = int(os.environ.get("HS_JIT_RT2_UNROLL", "4"))
 # 1: phase 1 maps runs to right rows by guess-and-verify (gen_run_tags2); 0: per-tile LDS search
 RT2 = os.environ.get("HS_JIT_RT2", "1") == "1"
 RT2_GRID = int(os.environ.get("HS_JIT_RT2_GRID", "8192"))
+# 1: phase 1 reads 16-bit grouped run keys and right keys (encoding.group16 / grouped16)
+RT2_K16 = os.environ.get("HS_JIT_RT2_K16", "1") == "1"
+RT2_MAX_WIDE = 0.1   # at most this share of 64-key groups spanning >= 2^16 codes
 
 
-def tags2_shape(p: NL.JoinParams, compacts, W: int) -> tuple:
+def tags2_shape(p: NL.JoinParams, compacts, W: int, k16: bool = False) -> tuple:
     cols = tuple(sorted((s, c) for s, c in J._col_specs(p, compacts).items()
                         if s >= SPLIT or s == p.lkey))
     preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
                    p.preds[k].group) for k in range(p.nlp, p.npreds))
     return ("run_tags2", cols, preds, p.nlp, p.lkey, p.rkey, _tags_grouped(p) and p.group_col,
-            W, RT2_UNROLL, J.BLOCK)
+            W, RT2_UNROLL, J.BLOCK, k16)
+
+
+def _stage_slots(p: NL.JoinParams) -> list:
+    """Right columns phase 1 reads at a matched row: predicate columns and the group key."""
+    return list(dict.fromkeys(J._pred_slots(_rpreds(p)) +
+                              ([p.group_col] if _tags_grouped(p) else [])))
 
 
 def _tags_grouped(p: NL.JoinParams) -> bool:
@@ -231,7 +240,7 @@ def _tags_grouped(p: NL.JoinParams) -> bool:
     return p.group_col >= SPLIT and p.num_groups > 1
 
 
-def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
+def gen_run_tags2(p: NL.JoinParams, compacts, W: int, k16: bool = False) -> J.Kernel:
     """Phase 1, direct form: no tiles and no LDS.  Each wavefront owns a contiguous chunk of
     64-run groups of the left run list (so it owns whole 2W-word stretches of the tag bitmap
     and stores them without atomics).  Lane l of a group guesses the right row of its run: the
@@ -243,10 +252,18 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
     trip; RT2_UNROLL groups are in flight per iteration.
 
     Ranges (``RNG``, NRG x 4 int64, sorted by first run): [first run, end run) of each left row
-    range and the right bucket's rows [s0, s1)."""
+    range and the right bucket's rows [s0, s1).
+
+    ``k16``: the run keys are read as 16-bit offsets from a per-64-run-group base (one scalar
+    load per group; a wide group reads the 32-bit keys), and a right key in its grouped 16-bit
+    form (``encoding.GroupedCompact``: signature (2, False, 64)) likewise - 2 instead of 4 bytes
+    per key on both sides."""
     args = J.Args()
     lk, rk = p.lkey, p.rkey
     args.add("p", f"RK{lk}", "const int*")
+    if k16:
+        args.add("p", f"RKS{lk}", "const unsigned short*")
+        args.add("p", f"RKB{lk}", "const int*")
     args.add("p", "RNG", "const long long*")
     args.add("p", "tags", "unsigned*")
     for n in ("NRG", "NRUNS", "KLO", "KSP", "KOF"):
@@ -254,8 +271,7 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
     cols = J._col_specs(p, compacts)
     rpreds = _rpreds(p)
     rgroup = _tags_grouped(p)
-    stage_slots = list(dict.fromkeys([rk] + J._pred_slots(rpreds) +
-                                     ([p.group_col] if rgroup else [])))
+    stage_slots = _stage_slots(p)
     U = max(1, RT2_UNROLL)  # noqa: N806
     WV = J.BLOCK // 64  # noqa: N806
     MASK = (1 << W) - 1  # noqa: N806
@@ -264,8 +280,31 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
     if rgroup:
         gb = args.add("q", "group_base", "long long")
         ng = args.add("q", "num_groups", "long long")
-    img = (f"({rv} ? 0u : ({{ const i64 d_ = (i64)({g.value(rk, 'row_')}) - a.KLO; "
-           f"d_ < 0 ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }}))")
+    renc = cols[rk][2]
+    if renc and len(renc) > 2 and renc[2] == 64:
+        # grouped 16-bit right key: code = gbase[row >> 6] + offset, or the 32-bit code of a
+        # wide group (both loads unconditional: the wide one hits row 0 otherwise)
+        assert rk not in stage_slots
+        base = args.add("q", f"B{rk}", "long long")
+        gp = args.add("p", f"G{rk}", "const int*")
+        wp = args.add("p", f"W{rk}", "const int*")
+        cp = g.ptr(rk)
+        rval = (f"({{ const int gb_ = {gp}[row_ >> 6]; const bool wd_ = gb_ == (int)0x80000000; "
+                f"const int w_ = {wp}[wd_ ? row_ : 0]; const unsigned short o_ = {cp}[row_]; "
+                f"{base} + (wd_ ? (i64)w_ : (i64)gb_ + (i64)o_); }})")
+        # the guess's image without the dependent wide-group load: 0 (below every left image,
+        # so never a false match) for a wide group; a miss re-reads the exact image
+        fval = (f"({{ const int gb_ = {gp}[row_ >> 6]; const unsigned short o_ = {cp}[row_]; "
+                f"gb_ == (int)0x80000000 ? (i64)-1 : {base} + (i64)gb_ + (i64)o_; }})")
+    else:
+        rval = fval = g.value(rk, "row_")
+
+    def image(val: str, wide0: bool) -> str:
+        guard = "(__v_ == (i64)-1) || " if wide0 else ""
+        return (f"({rv} ? 0u : ({{ const i64 __v_ = (i64)({val}); const i64 d_ = __v_ - a.KLO; "
+                f"({guard}d_ < 0) ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }}))")
+    img = image(rval, False)
+    imgf = image(fval, fval is not rval)
 
     def tag_expr(gen: J._Gen, it, ok: str) -> str:
         cond = J._rename(gen.cnf(rpreds), stage_slots, it)
@@ -277,6 +316,7 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
 
     b: List[str] = [
         f"  auto IMG = [&](i64 row_) -> unsigned {{ return {img}; }};",
+        f"  auto IMGF = [&](i64 row_) -> unsigned {{ return {imgf}; }};",
         "  const int lane = (int)(threadIdx.x & 63);",
         "  const i64 G = (a.NRUNS + 63) >> 6;",
         f"  const i64 nwv = (i64)gridDim.x * {WV};",
@@ -323,13 +363,19 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
                   f"a1_{u} = RG[4 * q_ + 3]; }}"])
         b.extend([f"{ind}const bool act{u} = in{u} && r{u} < a.NRUNS && r{u} >= l0_{u} && "
               f"r{u} < l1_{u} && a1_{u} > a0_{u};",
-              f"{ind}const unsigned key{u} = (unsigned)a.RK{lk}[act{u} ? r{u} : 0] + "
-              f"(unsigned)a.KOF;",
+              (f"{ind}const int kb{u} = a.RKB{lk}[gi + {u} < G ? gi + {u} : G - 1];\n"
+               f"{ind}const bool kw{u} = kb{u} == (int)0x80000000;\n"
+               f"{ind}const unsigned short ks{u} = a.RKS{lk}[act{u} ? r{u} : 0];\n"
+               f"{ind}const int kx{u} = a.RK{lk}[(act{u} && kw{u}) ? r{u} : 0];\n"
+               f"{ind}const unsigned key{u} = (unsigned)(kw{u} ? (i64)kx{u} : "
+               f"(i64)kb{u} + (i64)ks{u}) + (unsigned)a.KOF;") if k16 else
+              (f"{ind}const unsigned key{u} = (unsigned)a.RK{lk}[act{u} ? r{u} : 0] + "
+               f"(unsigned)a.KOF;"),
               f"{ind}i64 j{u} = (own{u} && gbase >= 0) ? gbase + {u * 64} + lane : "
               f"a0_{u} + (r{u} - l0_{u});",
               f"{ind}j{u} = act{u} ? (j{u} < a0_{u} ? a0_{u} : (j{u} >= a1_{u} ? a1_{u} - 1 : j{u}))"
               f" : 0;",
-              f"{ind}const unsigned k{u} = IMG(j{u});"])
+              f"{ind}const unsigned k{u} = IMGF(j{u});"])
         gu = J._Gen(args, cols, SPLIT, (f"j{u}", f"j{u}"), frozenset(), True)
         for sl in stage_slots:
             J._uload(gu, sl, f"g{u}", b, ind)
@@ -342,7 +388,9 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
                   f"{ind}if (act{u} && !hit{u}) {{",
                   # gallop from the guess to the lower bound of key in [a0, a1)
                   f"{ind}  const unsigned key_ = key{u}; i64 lo_, hi_;",
-                  f"{ind}  if (k{u} > key_) {{",
+                  f"{ind}  const unsigned kj_ = IMG(j{u});",
+                  f"{ind}  if (kj_ == key_) {{ lo_ = j{u}; hi_ = j{u}; }}",
+                  f"{ind}  else if (kj_ > key_) {{",
                   f"{ind}    hi_ = j{u}; i64 st_ = 1; lo_ = j{u} - 1;",
                   f"{ind}    while (lo_ > a0_{u} && IMG(lo_) >= key_) {{ hi_ = lo_; st_ <<= 1; "
                   f"lo_ = hi_ - st_; }}",
@@ -565,14 +613,30 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
     nwords = max((nruns * W + 31) >> 5, ((nruns + 63) >> 6) * 2 * W)
     tags = torch.empty(nwords + KW + 2, dtype=torch.int32, device=dev)
     frame = J._key32_frame(p, compacts)
+    tcomp = compacts
     if RT2 and int(roff[-1].item()) > 0:
         rng = run_ranges(rstart, rlen, rbucket, roff, runs)
         rng_d = torch.from_numpy(rng.reshape(-1).copy() if len(rng) else
                                  __import__("numpy").zeros(4, "int64")).to(dev)
-        kt = J.kernel_for(tags2_shape(p, compacts, W), lambda: gen_run_tags2(p, compacts, W))
+        lk16 = runs.keys16(RT2_MAX_WIDE) if RT2_K16 else None
+        if lk16 is not None:
+            from .encoding import GroupedCompact, grouped16
+            rc = compacts.get(p.rkey)
+            if rc is not None and not isinstance(rc, GroupedCompact) and \
+                    p.rkey not in _stage_slots(p):
+                r16 = grouped16(rc, RT2_MAX_WIDE)
+                if r16 is not None:
+                    tcomp = dict(compacts)
+                    tcomp[p.rkey] = r16
+        k16 = lk16 is not None
+        kt = J.kernel_for(tags2_shape(p, tcomp, W, k16),
+                          lambda: gen_run_tags2(p, tcomp, W, k16))
         vt = {"RNG": rng_d.data_ptr(), "NRG": len(rng), "NRUNS": nruns, "tags": tags.data_ptr(),
               "num_groups": p.num_groups, "group_base": p.group_base}
-        tr = rng_d
+        if k16:
+            vt[f"RKS{p.lkey}"] = lk16[0].data_ptr()
+            vt[f"RKB{p.lkey}"] = lk16[1].data_ptr()
+        tr = (rng_d, lk16)
         grid_t = max(1, RT2_GRID)
     else:
         tr = J._tile_runs(tp, spans, rstart.numel(), runs, max_tiles, cache_spans)
@@ -582,7 +646,7 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
               "num_groups": p.num_groups, "group_base": p.group_base}
         grid_t = max(1, J.MJ_GRID)
     vt["KLO"], vt["KSP"], vt["KOF"] = frame
-    J._fill_cols(vt, p.cols, compacts)
+    J._fill_cols(vt, p.cols, tcomp)
     vs = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
           "tags": tags.data_ptr(), "R": rstart.numel(), "nrows": nrows,
           "num_groups": p.num_groups, "group_base": p.group_base}

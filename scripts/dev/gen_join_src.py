@@ -59,7 +59,14 @@ def main(out):
         p, comp, keep = q3_params(ng)
         W = jit_runs.tag_width(p)
         NI = jit_runs.RS_ITEMS
+        from hyperspace_amd.exec.encoding import grouped16
+        t16 = dict(comp)
+        t16[p.rkey] = grouped16(comp[p.rkey], 1.0)
+        comp[0].keys16(1.0)
         ks = [jit_runs.gen_run_tags2(p, comp, W), jit_runs.gen_run_scan(p, comp, W, NI)]
+        k2 = jit_runs.gen_run_tags2(p, t16, W, True)
+        k2.name = "hs_jit_run_tags2_k16"
+        ks.append(k2)
         for k in ks:
             path = os.path.join(out, f"{k.name}_g{ng}.hip")
             with open(path, "w") as f:

@@ -759,7 +759,8 @@ def test_grouped16_round_trips_sorted_keys():
 
 
 @pytest.mark.gpu
-def test_merge_join_runs_matches_oracle(device):
+@pytest.mark.parametrize("layout", ["dense", "jumpy"])
+def test_merge_join_runs_matches_oracle(device, layout):
     """Run-keyed merge join (MJ_RUNS, encoding.RunCompact): TPC-H-like unique right keys, 1-7
     left rows per key, right keys with no left rows and left keys with no right row, a grouped
     aggregate over a right column; full buckets and unaligned sub-ranges, staged (2048 LDS keys)
@@ -771,6 +772,11 @@ def test_merge_join_runs_matches_oracle(device):
     rng = np.random.default_rng(11)
     B = 8
     ok = np.arange(1, 120_001, dtype=np.int64) * 4 + (1 << 20)
+    if layout == "jumpy":
+        # rare large key gaps: a few percent of the 64-key groups span >= 2^16 codes (the 16-bit
+        # grouped key forms read those groups' 32-bit keys)
+        gaps = np.where(rng.random(len(ok)) < 0.0001, 3_000_000, 4)
+        ok = np.cumsum(gaps) + (1 << 20)
     per = rng.integers(1, 8, len(ok))
     per[rng.random(len(ok)) < 0.05] = 0                         # orders without lines
     lk = np.repeat(ok, per)
@@ -812,6 +818,7 @@ def test_merge_join_runs_matches_oracle(device):
         assert torch.equal(a.cpu(), b_)
     from hyperspace_amd.exec import jit_runs
     lds_keys, runs, two2, rt2 = jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P, jit_runs.RT2
+    k16 = jit_runs.RT2_K16
     try:
         for starts, lens in ((loff[:-1], loff[1:] - loff[:-1]),
                              (loff[:-1] + 5, loff[1:] - loff[:-1] - 9)):
@@ -827,10 +834,12 @@ def test_merge_join_runs_matches_oracle(device):
             rbk = torch.arange(B, dtype=torch.int32, device=device)
             roff_t = torch.from_numpy(roff).to(device)
             for keys in (lds_keys, 32):
-                for use_runs, two, direct in ((True, True, True), (True, True, False),
-                                              (True, False, False), (False, False, False)):
+                for use_runs, two, direct, short in (
+                        (True, True, True, True), (True, True, True, False),
+                        (True, True, False, False), (True, False, False, False),
+                        (False, False, False, False)):
                     jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P = keys, use_runs, two
-                    jit_runs.RT2 = direct
+                    jit_runs.RT2, jit_runs.RT2_K16 = direct, short
                     got = [t.cpu().numpy() for t in
                            jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, comp, nrows=len(lk),
                                               rdup=False)]
@@ -841,3 +850,4 @@ def test_merge_join_runs_matches_oracle(device):
                         assert isinstance(jit.LAST_MJ_LAUNCHER[0], jit_runs.TwoPhaseLauncher)
     finally:
         jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P, jit_runs.RT2 = lds_keys, runs, two2, rt2
+        jit_runs.RT2_K16 = k16
