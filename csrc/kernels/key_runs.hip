@@ -79,9 +79,51 @@ __global__ __launch_bounds__(256) void hs_tile_runs_kernel(const int64_t* __rest
   out[2 * t + 1] = nl;
 }
 
+// Run tags (1 bit per run, exec/jit_runs.py phase 1) -> row mask (1 bit per row) over 64-row
+// groups [g0, g1): bit i of out[g] = tag of the run holding row 64 g + i.  One thread per group:
+// T = the tag bits of the group's runs (<= 64 runs from gruns[g]: a 3-word funnel), the change
+// points c_k = T_k ^ T_{k-1} are deposited at the runs' start rows (a software bit deposit over
+// the set bits of the start mask, ~rows/4 iterations) and a prefix XOR spreads each run's tag
+// over its rows.  The streaming scan (phase 2) then reads 8 bytes per 64 rows, prefetched one
+// tile ahead, and skips the predicate loads of rows no tagged run holds.
+__global__ __launch_bounds__(256) void hs_run_rowmask_kernel(const uint64_t* __restrict__ gmask,
+                                                             const int32_t* __restrict__ gruns,
+                                                             const uint32_t* __restrict__ tags,
+                                                             int64_t g0, int64_t g1,
+                                                             uint64_t* __restrict__ out) {
+  const int64_t g = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= g1) return;
+  const uint64_t m = gmask[g] | 1ull;   // row 0 starts (or continues) the group's first run
+  const int64_t r0 = gruns[g];
+  const int64_t w = r0 >> 5;
+  const unsigned sh = (unsigned)(r0 & 31);
+  const uint64_t lo = (uint64_t)tags[w] | ((uint64_t)tags[w + 1] << 32);
+  const uint64_t hi = (uint64_t)tags[w + 2];
+  const uint64_t T = sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
+  const uint64_t c = T ^ (T << 1);      // c_k = T_k ^ T_{k-1}, T_{-1} = 0
+  uint64_t d = 0, mm = m, cc = c;
+  while (mm) {                          // deposit c's low bits at m's set bits, in order
+    const uint64_t low = mm & (0ull - mm);
+    if (cc & 1ull) d |= low;
+    cc >>= 1;
+    mm ^= low;
+  }
+  d ^= d << 1; d ^= d << 2; d ^= d << 4; d ^= d << 8; d ^= d << 16; d ^= d << 32;  // prefix XOR
+  out[g] = d;
+}
+
 }  // namespace
 
 extern "C" {
+
+// tags must hold 2 readable words past the last run's word (phase 1 allocates that slack)
+int hs_run_rowmask(const uint64_t* gmask, const int32_t* gruns, const uint32_t* tags, int64_t g0,
+                   int64_t g1, uint64_t* out, void* stream) {
+  if (g1 > g0)
+    hipLaunchKernelGGL(hs_run_rowmask_kernel, dim3((unsigned)((g1 - g0 + 255) / 256)), dim3(256),
+                       0, (hipStream_t)stream, gmask, gruns, tags, g0, g1, out);
+  return (int)hipGetLastError();
+}
 
 // Pass 1: gmask / per-group run counts of the int32 column x[0, n).
 int hs_key_runs_mask(const int32_t* x, int64_t n, uint64_t* gmask, int64_t* gcnt, void* stream) {

@@ -566,16 +566,93 @@ def gen_run_scan(p: NL.JoinParams, compacts, W: int, NI: int) -> J.Kernel:
     return J.Kernel(src, "hs_jit_run_scan", args, lds)
 
 
+# 1: a 1-bit tag bitmap is expanded to a row mask (hs_run_rowmask) and the scan skips the
+# predicate loads of rows no tagged run holds (gen_run_scan_rows)
+ROWMASK = os.environ.get("HS_JIT_RS_ROWMASK", "1") == "1"
+
+
+def scan_rows_shape(p: NL.JoinParams, compacts, NI: int) -> tuple:
+    return ("run_scan_rows",) + scan_shape(p, compacts, 1, NI)[1:]
+
+
+def gen_run_scan_rows(p: NL.JoinParams, compacts, NI: int) -> J.Kernel:
+    """Phase 2 over a row mask (1-bit tags expanded per row): each thread's NI rows take their
+    mask bits from the 64-bit word of their group (prefetched one tile ahead with the tile
+    geometry), and the left predicate columns are loaded only by threads with a set bit - so the
+    predicate stream shrinks to the rows of matching runs - then the compacted aggregate tail
+    runs over the rows passing both."""
+    args = J.Args()
+    for n, ct in (("rstart", "const long long*"), ("rlen", "const long long*"),
+                  ("tile_prefix", "const long long*")):
+        args.add("p", n, ct)
+    args.add("p", "RM", "const unsigned long long*")
+    args.add("q", "R", "long long")
+    args.add("q", "nrows", "long long")
+    J._common_args(args)
+    cols = J._col_specs(p, compacts)
+    lpreds = _lpreds(p)
+    aggs = [p.aggs[i] for i in range(p.naggs)]
+    grouped = _scan_grouped(p)
+    assert not (grouped and p.group_col >= SPLIT)
+    pslots = J._pred_slots(lpreds)
+    tail = J._agg_slots(aggs) + ([p.group_col] if grouped else [])
+    allslots = list(dict.fromkeys(pslots + tail))
+    approx = J._sum_only_slots(lpreds, aggs, p.group_col if grouped else -1, cols)
+    BLOCK = J.BLOCK  # noqa: N806
+    T = BLOCK * NI  # noqa: N806
+    ind = "    "
+    g1 = J._Gen(args, cols, SPLIT, ("row0", "row0"), approx, True)
+    b: List[str] = []
+    b += J._acc_decls(aggs, grouped, args)
+    loads = J._vec_loads(g1, pslots)
+
+    def body(b: List[str], full: bool) -> None:
+        b.append(f"{ind}const unsigned bits_ = (unsigned)((rm_ >> (unsigned)(g0 & 63)) & "
+                 f"{(1 << NI) - 1}ull);")
+        for name, ct, ptr in loads:
+            b.append(f"{ind}{ct} {name}v[{NI}];")
+            if full:
+                b.append(f"{ind}if (bits_) vload<{ct}, {NI}>({ptr}, g0, {name}v); else " +
+                         " ".join(f"{name}v[{k}] = ({ct})0;" for k in range(NI)))
+            else:
+                b.append(f"{ind}" + " ".join(
+                    f"{name}v[{k}] = (act{k} && ((bits_ >> {k}) & 1u)) ? {ptr}[g0 + {k}] : "
+                    f"({ct})0;" for k in range(NI)))
+        J._vec_load_slots(b, g1, pslots, NI, ind)
+        for it in range(NI):
+            gi = J._Gen(args, cols, SPLIT, (f"row{it}", f"row{it}"), approx, True)
+            b.append(f"{ind}const bool pass{it} = act{it} && ((bits_ >> {it}) & 1u) && "
+                     f"{J._rename(gi.cnf(lpreds), allslots, it)};")
+        b.extend(J._compacted_tail(args, cols, SPLIT, approx, aggs, grouped, p.group_col,
+                                   tail, allslots, NI, ind, with_j=False))
+
+    gw = "((G0 < a.nrows ? G0 : a.nrows - 1) >> 6)"
+    J._vec_tiles(b, T, NI, ind, [], [("rm_", "unsigned long long", f"a.RM[{gw}]")], body)
+    b += ["  }"]
+    b += J._flush(aggs, grouped)
+    Wv = BLOCK // 64  # noqa: N806
+    pre = [f"  typedef {J._crow_t(T)} crow_t; __shared__ crow_t crow_s[{Wv}][{64 * NI}];",
+           "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;"]
+    src = (J._PRELUDE + args.struct_src() +
+           f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_run_scan_rows(Args a) '
+           f'{{\n' + "\n".join(pre + b) + "\n}\n")
+    lds = (len(aggs) * p.num_groups * 32) if grouped else 0
+    return J.Kernel(src, "hs_jit_run_scan_rows", args, lds)
+
+
 class TwoPhaseLauncher:
     """Both phases lowered once (kernels, tiles, spans, per-tile run windows, the tag bitmap);
     ``launch(p)`` fills the literal slots and queues: bitmap clear, tags, scan, partials fold."""
     __slots__ = ("kt", "ks", "grid_t", "grid_s", "GA", "shmem", "vt", "vs", "compacts", "keep",
-                 "tags", "dev")
+                 "tags", "dev", "rows")
 
-    def __init__(self, kt, ks, grid_t, grid_s, GA, shmem, vt, vs, compacts, keep, tags, dev):
+    def __init__(self, kt, ks, grid_t, grid_s, GA, shmem, vt, vs, compacts, keep, tags, dev,
+                 rows=None):
         self.kt, self.ks, self.grid_t, self.grid_s = kt, ks, grid_t, grid_s
         self.GA, self.shmem, self.vt, self.vs = GA, shmem, vt, vs
         self.compacts, self.keep, self.tags, self.dev = compacts, keep, tags, dev
+        # row-mask expansion between the phases: (gmask ptr, gruns ptr, g0, g1, mask tensor)
+        self.rows = rows
 
     def launch(self, p: NL.JoinParams):
         preds = [(k_, p.preds[k_]) for k_ in range(p.npreds)]
@@ -586,6 +663,10 @@ class TwoPhaseLauncher:
             self.tags.zero_()  # every word of every run group
         st = NL.stream_ptr()
         self.kt.launch(self.grid_t, vt, st)
+        if self.rows is not None:
+            gm, gr, g0, g1, rm = self.rows
+            NL.check(NL.lib().hs_run_rowmask(gm, gr, self.tags.data_ptr(), g0, g1, rm.data_ptr(),
+                                             st), "hs_run_rowmask")
         parts = J._partials(self.grid_s, self.GA, self.dev)
         vs = dict(self.vs)
         vs.update({"psum": parts[0].data_ptr(), "pcnt": parts[1].data_ptr(),
@@ -607,7 +688,13 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
     dev = rstart.device
     max_tiles = nrows // T + 2 * rstart.numel() + 2
     tp, spans = J._join_spans(p, rstart, rlen, rbucket, roff, max_tiles, T, cache_spans, align=NI)
-    ks = J.kernel_for(scan_shape(p, compacts, W, NI), lambda: gen_run_scan(p, compacts, W, NI))
+    rowmask = ROWMASK and W == 1 and not (_scan_grouped(p) and p.group_col >= SPLIT)
+    if rowmask:
+        ks = J.kernel_for(scan_rows_shape(p, compacts, NI),
+                          lambda: gen_run_scan_rows(p, compacts, NI))
+    else:
+        ks = J.kernel_for(scan_shape(p, compacts, W, NI),
+                          lambda: gen_run_scan(p, compacts, W, NI))
     nruns = int(runs.runkeys.numel())
     KW = ((31 + (NI - 1) * W) >> 5) + 1  # noqa: N806
     nwords = max((nruns * W + 31) >> 5, ((nruns + 63) >> 6) * 2 * W)
@@ -651,8 +738,20 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
           "tags": tags.data_ptr(), "R": rstart.numel(), "nrows": nrows,
           "num_groups": p.num_groups, "group_base": p.group_base}
     J._fill_cols(vs, p.cols, compacts)
+    rows = None
+    if rowmask:
+        # the 64-row groups the left ranges touch (the mask is read for those only)
+        import numpy as np
+        rs = rstart.cpu().numpy().astype(np.int64)
+        rl = rlen.cpu().numpy().astype(np.int64)
+        nz = rl > 0
+        g0 = int((rs[nz].min() >> 6)) if nz.any() else 0
+        g1 = int((((rs[nz] + rl[nz]).max() + 63) >> 6)) if nz.any() else 0
+        rm = torch.zeros(max((nrows + 63) >> 6, 1), dtype=torch.int64, device=dev)
+        rows = (runs.gmask.data_ptr(), runs.gruns.data_ptr(), g0, g1, rm)
+        vs["RM"] = rm.data_ptr()
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
     grid_s = max(1, J.SCAN_GRID or NL.lib().hs_scan_grid())
     return TwoPhaseLauncher(kt, ks, grid_t, grid_s, GA, GA * 32 if _scan_grouped(p) else 0,
                             vt, vs, compacts, (rstart, rlen, rbucket, roff, tp, spans, tr, runs),
-                            tags, dev)
+                            tags, dev, rows)

@@ -67,6 +67,8 @@ def main(out):
         k2 = jit_runs.gen_run_tags2(p, t16, W, True)
         k2.name = "hs_jit_run_tags2_k16"
         ks.append(k2)
+        if W == 1 and not (p.group_col >= 8 and p.num_groups > 1):
+            ks.append(jit_runs.gen_run_scan_rows(p, comp, NI))
         for k in ks:
             path = os.path.join(out, f"{k.name}_g{ng}.hip")
             with open(path, "w") as f:

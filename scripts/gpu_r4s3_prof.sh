@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 profiling iteration: selected GPU tests (rc 1 does not stop the chain), a rocprofv3
 # kernel-stats pass over the merge-join sweep ($CONFIGS), and the SF100 bench with the host
-# cProfile of the timed steps (HS_BENCH_PROFILE).  Each GPU step has its own time limit.
+# cProfile of the timed steps (HS_BENCH_PROFILE, when HPROF=1).  Each GPU step has its own time limit.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 REPO="$(pwd)"
@@ -16,7 +16,7 @@ if [ -n "${TESTS}" ]; then
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 fi
 if [ -z "$NOBENCH" ]; then
-  HS_BENCH_PROFILE=1 timeout -k 10 600 python bench.py --sf ${SF:-100} --steps ${STEPS:-100} \
+  HS_BENCH_PROFILE=${HPROF} timeout -k 10 600 python bench.py --sf ${SF:-100} --steps ${STEPS:-100} \
     --warmup 5 --host-breakdown 100 > gpurun_out/${TAG}_bench.json \
     2> gpurun_out/${TAG}_bench.log || exit $?
 fi
