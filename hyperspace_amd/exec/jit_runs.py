@@ -214,7 +214,7 @@ RT2_UNROLL = int(os.environ.get("HS_JIT_RT2_UNROLL", "4"))
 RT2 = os.environ.get("HS_JIT_RT2", "1") == "1"
 RT2_GRID = int(os.environ.get("HS_JIT_RT2_GRID", "8192"))
 # 1: phase 1 reads 16-bit grouped run keys and right keys (encoding.group16 / grouped16)
-RT2_K16 = os.environ.get("HS_JIT_RT2_K16", "1") == "1"
+RT2_K16 = os.environ.get("HS_JIT_RT2_K16", "0") == "1"
 RT2_MAX_WIDE = 0.1   # at most this share of 64-key groups spanning >= 2^16 codes
 
 
@@ -612,8 +612,8 @@ def gen_run_scan_rows(p: NL.JoinParams, compacts, NI: int) -> J.Kernel:
         for name, ct, ptr in loads:
             b.append(f"{ind}{ct} {name}v[{NI}];")
             if full:
-                b.append(f"{ind}if (bits_) vload<{ct}, {NI}>({ptr}, g0, {name}v); else " +
-                         " ".join(f"{name}v[{k}] = ({ct})0;" for k in range(NI)))
+                b.append(f"{ind}if (bits_) {{ vload<{ct}, {NI}>({ptr}, g0, {name}v); }} else {{ " +
+                         " ".join(f"{name}v[{k}] = ({ct})0;" for k in range(NI)) + " }")
             else:
                 b.append(f"{ind}" + " ".join(
                     f"{name}v[{k}] = (act{k} && ((bits_ >> {k}) & 1u)) ? {ptr}[g0 + {k}] : "
