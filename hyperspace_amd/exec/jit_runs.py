@@ -640,6 +640,133 @@ def gen_run_scan_rows(p: NL.JoinParams, compacts, NI: int) -> J.Kernel:
     return J.Kernel(src, "hs_jit_run_scan_rows", args, lds)
 
 
+# 1: phase 2 (1-bit tags) visits only the rows of tagged runs (gen_run_sparse_scan)
+SPARSE = os.environ.get("HS_JIT_RS_SPARSE", "1") == "1"
+SPARSE_GRID = int(os.environ.get("HS_JIT_RS_SPARSE_GRID", "4096"))
+
+
+def sparse_shape(p: NL.JoinParams, compacts) -> tuple:
+    return ("run_sparse_scan",) + scan_shape(p, compacts, 1, 64)[1:]
+
+
+def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
+    """Phase 2 for 1-bit tags, visiting only the rows of tagged runs (a few percent of the left
+    rows for a selective right side like TPC-H Q3's o_orderdate window).  A wavefront takes
+    4096-row tiles of the left ranges, lane l the 64-row group l of its tile:
+
+    1. row mask of the group: the tag bits of its runs (gruns / the 3 tag words) deposited at
+       the run starts (gmask) and spread over each run's rows by a prefix XOR (as
+       hs_run_rowmask), limited to the tile's range rows;
+    2. the set rows are appended to a per-wavefront LDS list (offsets from a shuffle scan of
+       the lanes' popcounts);
+    3. the wavefront walks the list 64 rows at a time: left predicate columns and aggregate
+       inputs are loaded at those rows only, predicates evaluated, aggregates accumulated.
+
+    So the per-row VALU work of a dense scan (decode, predicate, compaction ballots for every
+    row) is spent only on tagged rows; the mask work is per 64-row group."""
+    args = J.Args()
+    for n, ct in (("rstart", "const long long*"), ("rlen", "const long long*"),
+                  ("tile_prefix", "const long long*")):
+        args.add("p", n, ct)
+    lk = p.lkey
+    args.add("p", f"GM{lk}", "const unsigned long long*")
+    args.add("p", f"GR{lk}", "const int*")
+    args.add("p", "tags", "const unsigned*")
+    args.add("q", "R", "long long")
+    args.add("q", "nrows", "long long")
+    J._common_args(args)
+    cols = J._col_specs(p, compacts)
+    lpreds = _lpreds(p)
+    aggs = [p.aggs[i] for i in range(p.naggs)]
+    grouped = _scan_grouped(p)
+    assert not (grouped and p.group_col >= SPLIT)
+    pslots = J._pred_slots(lpreds)
+    tail = list(dict.fromkeys(pslots + J._agg_slots(aggs) + ([p.group_col] if grouped else [])))
+    approx = J._sum_only_slots(lpreds, aggs, p.group_col if grouped else -1, cols)
+    BLOCK = J.BLOCK  # noqa: N806
+    WV = BLOCK // 64  # noqa: N806
+    T = 4096  # noqa: N806 — rows per tile: 64 groups, one per lane
+    b: List[str] = []
+    b += J._acc_decls(aggs, grouped, args)
+    CAP = 1024  # noqa: N806 — list entries per wavefront and round (a denser tile takes rounds)
+    b += [f"  __shared__ unsigned short lst_[{WV}][{CAP}];",
+          "  const int ln = (int)(threadIdx.x & 63);",
+          "  const int wq = (int)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));",
+          "  const i64 ntiles = a.tile_prefix[a.R];",
+          f"  const i64 nwv = (i64)gridDim.x * {WV};",
+          f"  const i64 wid = (i64)blockIdx.x * {WV} + wq;",
+          "  const i64 per = (ntiles + nwv - 1) / nwv;",
+          "  const i64 t0 = wid * per;",
+          "  const i64 t1 = ntiles < t0 + per ? ntiles : t0 + per;",
+          "  int r = 0;",
+          "  if (t0 < t1) { int lo = 0, hi = (int)a.R;",
+          "    while (hi - lo > 1) { const int m = (lo + hi) >> 1; "
+          "if (a.tile_prefix[m] <= t0) lo = m; else hi = m; }",
+          "    r = lo; }",
+          "  for (i64 t = t0; t < t1; ++t) {",
+          "    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;",
+          f"    const i64 rs = a.rstart[r], re = rs + a.rlen[r];",
+          f"    const i64 tb0 = (rs & ~(i64)63) + (t - a.tile_prefix[r]) * {T};",
+          "    const i64 row0 = tb0 + 64 * ln;",
+          # rows of this lane's group inside [rs, re)
+          "    const i64 lo_ = rs - row0, hi_ = re - row0;",
+          "    const int alo = lo_ <= 0 ? 0 : (lo_ >= 64 ? 64 : (int)lo_);",
+          "    const int ahi = hi_ <= 0 ? 0 : (hi_ >= 64 ? 64 : (int)hi_);",
+          "    const u64 am = alo >= ahi ? 0ull : ((ahi == 64 ? ~0ull : ((1ull << ahi) - 1ull)) & "
+          "~((1ull << alo) - 1ull));",
+          "    const i64 g = (row0 < a.nrows ? row0 : a.nrows - 1) >> 6;",
+          f"    const u64 m_ = a.GM{lk}[g] | 1ull;",
+          f"    const i64 q0 = a.GR{lk}[g];",
+          "    const i64 w_ = q0 >> 5; const unsigned sh_ = (unsigned)(q0 & 31);",
+          "    const u64 lw_ = (u64)a.tags[w_] | ((u64)a.tags[w_ + 1] << 32);",
+          "    const u64 hw_ = (u64)a.tags[w_ + 2];",
+          "    const u64 T_ = sh_ ? ((lw_ >> sh_) | (hw_ << (64 - sh_))) : lw_;",
+          "    u64 c_ = T_ ^ (T_ << 1), d_ = 0ull, mm_ = am ? m_ : 0ull;",
+          "    while (mm_) { const u64 lb_ = mm_ & (0ull - mm_); if (c_ & 1ull) d_ |= lb_; "
+          "c_ >>= 1; mm_ ^= lb_; }",
+          "    d_ ^= d_ << 1; d_ ^= d_ << 2; d_ ^= d_ << 4; d_ ^= d_ << 8; d_ ^= d_ << 16; "
+          "d_ ^= d_ << 32;",
+          "    d_ &= am;",
+          # exclusive scan of the lanes' row counts
+          "    const int cn_ = __popcll(d_);",
+          "    int inc_ = cn_;",
+          "    for (int o_ = 1; o_ < 64; o_ <<= 1) { const int y_ = __shfl_up(inc_, o_, 64); "
+          "if (ln >= o_) inc_ += y_; }",
+          "    const int tot_ = __shfl(inc_, 63, 64);",
+          f"    for (int wb_ = 0; wb_ < tot_; wb_ += {CAP}) {{",
+          f"    const int wn_ = tot_ - wb_ < {CAP} ? tot_ - wb_ : {CAP};",
+          "    { int pos_ = inc_ - cn_ - wb_; u64 e_ = d_;",
+          "      while (e_) { const int bq_ = __builtin_ctzll(e_); "
+          f"if (pos_ >= 0 && pos_ < {CAP}) lst_[wq][pos_] = (unsigned short)(64 * ln + bq_); "
+          "++pos_; e_ &= e_ - 1ull; } }",
+          f"    {J._wave_sync()}",
+          "    for (int cb = 0; cb < wn_; cb += 64) {",
+          "      const int ce = cb + ln;",
+          "      bool cok = ce < wn_;",
+          "      const i64 crow = tb0 + (cok ? (i64)lst_[wq][ce] : 0);"]
+    ind2 = "      "
+    g = J._Gen(args, cols, SPLIT, ("crow", "crow"), approx, True)
+    for sl in tail:
+        J._uload(g, sl, "c", b, ind2)
+    b.append(f"{ind2}cok = cok && {J._rename(g.cnf(lpreds), tail, 'c')};")
+    gvar = "gic"
+    if grouped:
+        base = args.add("q", "group_base", "long long")
+        ng = args.add("q", "num_groups", "long long")
+        b.append(f"{ind2}const i64 glc = (i64){J._rename(f'x{p.group_col}', tail, 'c')} - {base};")
+        b.append(f"{ind2}cok = cok && {J._rename(g.ok(p.group_col), tail, 'c')} && glc >= 0 && "
+                 f"glc < {ng};")
+        b.append(f"{ind2}const int {gvar} = cok ? (int)glc : 0;")
+    b += [J._rename(x, tail, "c") for x in J._accumulate(g, aggs, grouped, "cok", gvar, ind2)]
+    b += ["    }", f"    {J._wave_sync()}", "    }", "  }"]
+    b += J._flush(aggs, grouped)
+    src = (J._PRELUDE + args.struct_src() +
+           f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_run_sparse_scan(Args a) '
+           f'{{\n' + "\n".join(b) + "\n}\n")
+    lds = (len(aggs) * p.num_groups * 32) if grouped else 0
+    return J.Kernel(src, "hs_jit_run_sparse_scan", args, lds)
+
+
 class TwoPhaseLauncher:
     """Both phases lowered once (kernels, tiles, spans, per-tile run windows, the tag bitmap);
     ``launch(p)`` fills the literal slots and queues: bitmap clear, tags, scan, partials fold."""
@@ -688,8 +815,12 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
     dev = rstart.device
     max_tiles = nrows // T + 2 * rstart.numel() + 2
     tp, spans = J._join_spans(p, rstart, rlen, rbucket, roff, max_tiles, T, cache_spans, align=NI)
-    rowmask = ROWMASK and W == 1 and not (_scan_grouped(p) and p.group_col >= SPLIT)
-    if rowmask:
+    onebit = W == 1 and not (_scan_grouped(p) and p.group_col >= SPLIT)
+    sparse = SPARSE and onebit
+    rowmask = ROWMASK and onebit and not sparse
+    if sparse:
+        ks = J.kernel_for(sparse_shape(p, compacts), lambda: gen_run_sparse_scan(p, compacts))
+    elif rowmask:
         ks = J.kernel_for(scan_rows_shape(p, compacts, NI),
                           lambda: gen_run_scan_rows(p, compacts, NI))
     else:
@@ -752,6 +883,12 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
         vs["RM"] = rm.data_ptr()
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
     grid_s = max(1, J.SCAN_GRID or NL.lib().hs_scan_grid())
+    if sparse:
+        from ..ops import kernels as K
+        tp64 = K.ranges_to_tiles(rlen + (rstart & 63), 4096)   # 64-aligned 4096-row tiles
+        vs["tile_prefix"] = tp64.data_ptr()
+        spans = (spans, tp64)
+        grid_s = max(1, SPARSE_GRID)
     return TwoPhaseLauncher(kt, ks, grid_t, grid_s, GA, GA * 32 if _scan_grouped(p) else 0,
                             vt, vs, compacts, (rstart, rlen, rbucket, roff, tp, spans, tr, runs),
                             tags, dev, rows)

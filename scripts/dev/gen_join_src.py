@@ -69,6 +69,7 @@ def main(out):
         ks.append(k2)
         if W == 1 and not (p.group_col >= 8 and p.num_groups > 1):
             ks.append(jit_runs.gen_run_scan_rows(p, comp, NI))
+            ks.append(jit_runs.gen_run_sparse_scan(p, comp))
         for k in ks:
             path = os.path.join(out, f"{k.name}_g{ng}.hip")
             with open(path, "w") as f:

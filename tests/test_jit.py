@@ -818,7 +818,7 @@ def test_merge_join_runs_matches_oracle(device, layout):
         assert torch.equal(a.cpu(), b_)
     from hyperspace_amd.exec import jit_runs
     lds_keys, runs, two2, rt2 = jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P, jit_runs.RT2
-    k16, rowmask = jit_runs.RT2_K16, jit_runs.ROWMASK
+    k16, rowmask, sparse0 = jit_runs.RT2_K16, jit_runs.ROWMASK, jit_runs.SPARSE
     try:
         for starts, lens in ((loff[:-1], loff[1:] - loff[:-1]),
                              (loff[:-1] + 5, loff[1:] - loff[:-1] - 9)):
@@ -839,24 +839,28 @@ def test_merge_join_runs_matches_oracle(device, layout):
                 G = 3 if grouped else 1
                 es = exp_s if grouped else exp_s.sum(keepdims=True)
                 ec = exp_c if grouped else exp_c.sum(keepdims=True)
-                for use_runs, two, direct, short, rowm in (
-                        (True, True, True, True, True), (True, True, True, False, False),
-                        (True, True, False, False, True), (True, False, False, False, False),
-                        (False, False, False, False, False)):
+                for use_runs, two, direct, short, rowm, sparse in (
+                        (True, True, True, False, False, True),
+                        (True, True, True, True, True, False), (True, True, True, False, False, False),
+                        (True, True, False, False, True, False), (True, True, False, False, False, True),
+                        (True, False, False, False, False, False),
+                        (False, False, False, False, False, False)):
                     jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P = keys, use_runs, two
-                    jit_runs.RT2, jit_runs.RT2_K16, jit_runs.ROWMASK = direct, short, rowm
+                    jit_runs.RT2, jit_runs.RT2_K16 = direct, short
+                    jit_runs.ROWMASK, jit_runs.SPARSE = rowm, sparse
                     got = [t.cpu().numpy() for t in
                            jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, comp, nrows=len(lk),
                                               rdup=False)]
                     s_, c_ = got[0].reshape(G, 2)[:, 0], got[1].reshape(G, 2)[:, 1]
-                    cfg = (keys, grouped, use_runs, two, direct, short, rowm)
+                    cfg = (keys, grouped, use_runs, two, direct, short, rowm, sparse)
                     assert (c_ == ec).all(), (cfg, c_, ec)
                     assert np.allclose(s_, es, rtol=1e-12), cfg
                     if two:
                         launcher = jit.LAST_MJ_LAUNCHER[0]
                         assert isinstance(launcher, jit_runs.TwoPhaseLauncher)
-                        assert (launcher.rows is not None) == (rowm and not grouped), cfg
+                        assert (launcher.rows is not None) == (rowm and not sparse and
+                                                               not grouped), cfg
     finally:
         jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P, jit_runs.RT2 = lds_keys, runs, two2, rt2
-        jit_runs.RT2_K16, jit_runs.ROWMASK = k16, rowmask
+        jit_runs.RT2_K16, jit_runs.ROWMASK, jit_runs.SPARSE = k16, rowmask, sparse0
         p.group_col, p.num_groups = 10, 3
