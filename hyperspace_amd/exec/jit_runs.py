@@ -689,6 +689,16 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
     b: List[str] = []
     b += J._acc_decls(aggs, grouped, args)
     CAP = 1024  # noqa: N806 — list entries per wavefront and round (a denser tile takes rounds)
+    EW = 4  # noqa: N806 — list entries per lane per walk pass, loads all in flight together
+
+    def geom(tv: str, sfx: str) -> List[str]:
+        """Tile ``tv``'s range / row geometry and its group's run-form words (suffix sfx)."""
+        return [f"    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= {tv}) ++r;",
+                f"    rs{sfx} = a.rstart[r]; re{sfx} = rs{sfx} + a.rlen[r];",
+                f"    tb{sfx} = (rs{sfx} & ~(i64)63) + ({tv} - a.tile_prefix[r]) * {T};",
+                f"    {{ const i64 r0_ = tb{sfx} + 64 * ln; "
+                f"const i64 g_ = (r0_ < a.nrows ? r0_ : a.nrows - 1) >> 6;",
+                f"      gm{sfx} = a.GM{lk}[g_] | 1ull; gr{sfx} = a.GR{lk}[g_]; }}"]
     b += [f"  __shared__ unsigned short lst_[{WV}][{CAP}];",
           "  const int ln = (int)(threadIdx.x & 63);",
           "  const int wq = (int)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));",
@@ -703,25 +713,31 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
           "    while (hi - lo > 1) { const int m = (lo + hi) >> 1; "
           "if (a.tile_prefix[m] <= t0) lo = m; else hi = m; }",
           "    r = lo; }",
+          "  i64 rsN = 0, reN = 0, tbN = 0; u64 gmN = 0ull; i64 grN = 0;",
+          "  if (t0 < t1) {"]
+    b += geom("t0", "N")
+    b += ["  }",
           "  for (i64 t = t0; t < t1; ++t) {",
-          "    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t) ++r;",
-          f"    const i64 rs = a.rstart[r], re = rs + a.rlen[r];",
-          f"    const i64 tb0 = (rs & ~(i64)63) + (t - a.tile_prefix[r]) * {T};",
+          "    const i64 rs = rsN, re = reN, tb0 = tbN; const u64 m_ = gmN; const i64 q0 = grN;",
+          # the group's tag words (depend on this tile's gruns), then the next tile's run-form
+          # words, so they are in flight during this tile's mask and walk
+          "    const i64 w_ = q0 >> 5; const unsigned sh_ = (unsigned)(q0 & 31);",
+          "    const u64 lw_ = (u64)a.tags[w_] | ((u64)a.tags[w_ + 1] << 32);",
+          "    const u64 hw_ = (u64)a.tags[w_ + 2];",
+          "    if (t + 1 < t1) {"]
+    b += ["  " + x for x in geom("(t + 1)", "N")]
+    b += ["    }",
           "    const i64 row0 = tb0 + 64 * ln;",
-          # rows of this lane's group inside [rs, re)
           "    const i64 lo_ = rs - row0, hi_ = re - row0;",
           "    const int alo = lo_ <= 0 ? 0 : (lo_ >= 64 ? 64 : (int)lo_);",
           "    const int ahi = hi_ <= 0 ? 0 : (hi_ >= 64 ? 64 : (int)hi_);",
           "    const u64 am = alo >= ahi ? 0ull : ((ahi == 64 ? ~0ull : ((1ull << ahi) - 1ull)) & "
           "~((1ull << alo) - 1ull));",
-          "    const i64 g = (row0 < a.nrows ? row0 : a.nrows - 1) >> 6;",
-          f"    const u64 m_ = a.GM{lk}[g] | 1ull;",
-          f"    const i64 q0 = a.GR{lk}[g];",
-          "    const i64 w_ = q0 >> 5; const unsigned sh_ = (unsigned)(q0 & 31);",
-          "    const u64 lw_ = (u64)a.tags[w_] | ((u64)a.tags[w_ + 1] << 32);",
-          "    const u64 hw_ = (u64)a.tags[w_ + 2];",
           "    const u64 T_ = sh_ ? ((lw_ >> sh_) | (hw_ << (64 - sh_))) : lw_;",
-          "    u64 c_ = T_ ^ (T_ << 1), d_ = 0ull, mm_ = am ? m_ : 0ull;",
+          # only the group's own runs' tags (popc(m) of them) decide whether any row is set
+          "    const int nr_ = __popcll(m_);",
+          "    const u64 Tm_ = nr_ >= 64 ? T_ : (T_ & ((1ull << nr_) - 1ull));",
+          "    u64 c_ = T_ ^ (T_ << 1), d_ = 0ull, mm_ = (am && Tm_) ? m_ : 0ull;",
           "    while (mm_) { const u64 lb_ = mm_ & (0ull - mm_); if (c_ & 1ull) d_ |= lb_; "
           "c_ >>= 1; mm_ ^= lb_; }",
           "    d_ ^= d_ << 1; d_ ^= d_ << 2; d_ ^= d_ << 4; d_ ^= d_ << 8; d_ ^= d_ << 16; "
@@ -740,24 +756,31 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
           f"if (pos_ >= 0 && pos_ < {CAP}) lst_[wq][pos_] = (unsigned short)(64 * ln + bq_); "
           "++pos_; e_ &= e_ - 1ull; } }",
           f"    {J._wave_sync()}",
-          "    for (int cb = 0; cb < wn_; cb += 64) {",
-          "      const int ce = cb + ln;",
-          "      bool cok = ce < wn_;",
-          "      const i64 crow = tb0 + (cok ? (i64)lst_[wq][ce] : 0);"]
+          f"    for (int cb = 0; cb < wn_; cb += {64 * EW}) {{"]
     ind2 = "      "
-    g = J._Gen(args, cols, SPLIT, ("crow", "crow"), approx, True)
-    for sl in tail:
-        J._uload(g, sl, "c", b, ind2)
-    b.append(f"{ind2}cok = cok && {J._rename(g.cnf(lpreds), tail, 'c')};")
-    gvar = "gic"
-    if grouped:
-        base = args.add("q", "group_base", "long long")
-        ng = args.add("q", "num_groups", "long long")
-        b.append(f"{ind2}const i64 glc = (i64){J._rename(f'x{p.group_col}', tail, 'c')} - {base};")
-        b.append(f"{ind2}cok = cok && {J._rename(g.ok(p.group_col), tail, 'c')} && glc >= 0 && "
-                 f"glc < {ng};")
-        b.append(f"{ind2}const int {gvar} = cok ? (int)glc : 0;")
-    b += [J._rename(x, tail, "c") for x in J._accumulate(g, aggs, grouped, "cok", gvar, ind2)]
+    for k in range(EW):
+        b += [f"{ind2}const int ce{k} = cb + {64 * k} + ln;",
+              f"{ind2}bool cok{k} = ce{k} < wn_;",
+              f"{ind2}const i64 crow{k} = tb0 + (cok{k} ? (i64)lst_[wq][ce{k}] : 0);"]
+    gs = [J._Gen(args, cols, SPLIT, (f"crow{k}", f"crow{k}"), approx, True) for k in range(EW)]
+    for k in range(EW):
+        for sl in tail:
+            J._uload(gs[k], sl, f"c{k}", b, ind2)
+    for k in range(EW):
+        g = gs[k]
+        it = f"c{k}"
+        b.append(f"{ind2}{{ bool cok = cok{k} && {J._rename(g.cnf(lpreds), tail, it)};")
+        gvar = "gic"
+        if grouped:
+            base = args.add("q", "group_base", "long long")
+            ng = args.add("q", "num_groups", "long long")
+            b.append(f"{ind2}const i64 glc = (i64){J._rename(f'x{p.group_col}', tail, it)} - "
+                     f"{base};")
+            b.append(f"{ind2}cok = cok && {J._rename(g.ok(p.group_col), tail, it)} && glc >= 0 && "
+                     f"glc < {ng};")
+            b.append(f"{ind2}const int {gvar} = cok ? (int)glc : 0;")
+        b += [J._rename(x, tail, it) for x in J._accumulate(g, aggs, grouped, "cok", gvar, ind2)]
+        b.append(f"{ind2}}}")
     b += ["    }", f"    {J._wave_sync()}", "    }", "  }"]
     b += J._flush(aggs, grouped)
     src = (J._PRELUDE + args.struct_src() +
