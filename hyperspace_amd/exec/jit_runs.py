@@ -640,30 +640,32 @@ def gen_run_scan_rows(p: NL.JoinParams, compacts, NI: int) -> J.Kernel:
     return J.Kernel(src, "hs_jit_run_scan_rows", args, lds)
 
 
-# 1: phase 2 (1-bit tags) visits only the rows of tagged runs (gen_run_sparse_scan)
-SPARSE = os.environ.get("HS_JIT_RS_SPARSE", "1") == "1"
-SPARSE_GRID = int(os.environ.get("HS_JIT_RS_SPARSE_GRID", "4096"))
+# 1: phase 2 for 1-bit tags evaluates its masks 64 rows at a time (gen_run_bits_scan)
+SPARSE = os.environ.get("HS_JIT_RS_BITS", "1") == "1"
+SPARSE_GRID = int(os.environ.get("HS_JIT_RS_BITS_GRID", "8192"))
 
 
 def sparse_shape(p: NL.JoinParams, compacts) -> tuple:
-    return ("run_sparse_scan",) + scan_shape(p, compacts, 1, 64)[1:]
+    return ("run_bits_scan",) + scan_shape(p, compacts, 1, 64)[1:]
 
 
 def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
-    """Phase 2 for 1-bit tags, visiting only the rows of tagged runs (a few percent of the left
-    rows for a selective right side like TPC-H Q3's o_orderdate window).  A wavefront takes
-    4096-row tiles of the left ranges, lane l the 64-row group l of its tile:
+    """Phase 2 for 1-bit tags, bit-parallel: the dense per-row scan spends ~20 VALU
+    instructions per row (decode, predicate, run index by popcount, tag extract, compaction
+    ballot + mbcnt), which bounds it below HBM speed.  Here a wavefront takes 4096-row tiles of
+    the left ranges, lane l the 64-row group l of its tile, and works on 64-bit row masks:
 
-    1. row mask of the group: the tag bits of its runs (gruns / the 3 tag words) deposited at
-       the run starts (gmask) and spread over each run's rows by a prefix XOR (as
-       hs_run_rowmask), limited to the tile's range rows;
-    2. the set rows are appended to a per-wavefront LDS list (offsets from a shuffle scan of
-       the lanes' popcounts);
-    3. the wavefront walks the list 64 rows at a time: left predicate columns and aggregate
-       inputs are loaded at those rows only, predicates evaluated, aggregates accumulated.
+    1. tag mask: the tag bits of the group's runs (gruns / 3 tag words) deposited at the run
+       starts (gmask) and spread over each run's rows by a prefix XOR (as hs_run_rowmask),
+       limited to the tile's range rows - ~1.5 instructions per row;
+    2. predicate mask: the lane's 64 rows of every left predicate column (vector loads, in
+       flight with the tag words), one compare + shift-or per row;
+    3. the rows of (tag mask & predicate mask) - the join's passing rows, a few percent - go to
+       a per-wavefront LDS list (offsets from a shuffle scan of the lanes' popcounts), which the
+       wavefront walks 4 entries per lane per pass: aggregate inputs loaded at those rows only
+       and accumulated.
 
-    So the per-row VALU work of a dense scan (decode, predicate, compaction ballots for every
-    row) is spent only on tagged rows; the mask work is per 64-row group."""
+    The next tile's run-form words are prefetched during the current tile."""
     args = J.Args()
     for n, ct in (("rstart", "const long long*"), ("rlen", "const long long*"),
                   ("tile_prefix", "const long long*")):
@@ -681,11 +683,12 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
     grouped = _scan_grouped(p)
     assert not (grouped and p.group_col >= SPLIT)
     pslots = J._pred_slots(lpreds)
-    tail = list(dict.fromkeys(pslots + J._agg_slots(aggs) + ([p.group_col] if grouped else [])))
+    tail = list(dict.fromkeys(J._agg_slots(aggs) + ([p.group_col] if grouped else [])))
     approx = J._sum_only_slots(lpreds, aggs, p.group_col if grouped else -1, cols)
     BLOCK = J.BLOCK  # noqa: N806
     WV = BLOCK // 64  # noqa: N806
-    T = 4096  # noqa: N806 — rows per tile: 64 groups, one per lane
+    T = 4096  # noqa: N806 — rows per wavefront tile: 64 groups, one per lane
+    NI = 64  # noqa: N806
     b: List[str] = []
     b += J._acc_decls(aggs, grouped, args)
     CAP = 1024  # noqa: N806 — list entries per wavefront and round (a denser tile takes rounds)
@@ -719,20 +722,37 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
     b += ["  }",
           "  for (i64 t = t0; t < t1; ++t) {",
           "    const i64 rs = rsN, re = reN, tb0 = tbN; const u64 m_ = gmN; const i64 q0 = grN;",
-          # the group's tag words (depend on this tile's gruns), then the next tile's run-form
-          # words, so they are in flight during this tile's mask and walk
-          "    const i64 w_ = q0 >> 5; const unsigned sh_ = (unsigned)(q0 & 31);",
-          "    const u64 lw_ = (u64)a.tags[w_] | ((u64)a.tags[w_ + 1] << 32);",
-          "    const u64 hw_ = (u64)a.tags[w_ + 2];",
-          "    if (t + 1 < t1) {"]
-    b += ["  " + x for x in geom("(t + 1)", "N")]
-    b += ["    }",
           "    const i64 row0 = tb0 + 64 * ln;",
           "    const i64 lo_ = rs - row0, hi_ = re - row0;",
           "    const int alo = lo_ <= 0 ? 0 : (lo_ >= 64 ? 64 : (int)lo_);",
           "    const int ahi = hi_ <= 0 ? 0 : (hi_ >= 64 ? 64 : (int)hi_);",
           "    const u64 am = alo >= ahi ? 0ull : ((ahi == 64 ? ~0ull : ((1ull << ahi) - 1ull)) & "
           "~((1ull << alo) - 1ull));",
+          # this tile's tag words and predicate columns in flight together, then the next
+          # tile's run-form words
+          "    const i64 w_ = q0 >> 5; const unsigned sh_ = (unsigned)(q0 & 31);",
+          "    const u64 lw_ = (u64)a.tags[w_] | ((u64)a.tags[w_ + 1] << 32);",
+          "    const u64 hw_ = (u64)a.tags[w_ + 2];",
+          # a whole in-table group reads its columns with vector loads, a partial one (the
+          # table's last group) element-wise
+          f"    const bool vok_ = row0 + {NI} <= a.nrows;"]
+    g1 = J._Gen(args, cols, SPLIT, ("row0", "row0"), approx, True)
+    elem = {}   # array name -> C expression of element (idx) from its packed 32-bit words
+    for name, ct, ptr in J._vec_loads(g1, pslots):
+        es = J._SIZEOF[ct]
+        nw = NI * es // 4
+        per = 4 // es
+        b.append(f"    unsigned {name}w[{nw}];")
+        b.append(f"    if (vok_) {{ vload<unsigned, {nw}>((const unsigned*){ptr}, row0 * {es} / 4, "
+                 f"{name}w); }} else {{ for (int k_ = 0; k_ < {nw}; ++k_) {name}w[k_] = 0u;"
+                 f" for (int k_ = 0; k_ < {NI} && row0 + k_ < a.nrows; ++k_) {{ const unsigned "
+                 f"u_ = (unsigned)({'unsigned char' if es == 1 else ('unsigned short' if es == 2 else 'unsigned')})"
+                 f"{ptr}[row0 + k_]; {name}w[k_ / {per}] |= u_ << ({8 * es} * (k_ % {per})); }} }}")
+        elem[name] = (ct, f"{name}w[({{i}}) / {per}]" if per > 1 else f"{name}w[{{i}}]",
+                      8 * es, per)
+    b += ["    if (t + 1 < t1) {"]
+    b += ["  " + x for x in geom("(t + 1)", "N")]
+    b += ["    }",
           "    const u64 T_ = sh_ ? ((lw_ >> sh_) | (hw_ << (64 - sh_))) : lw_;",
           # only the group's own runs' tags (popc(m) of them) decide whether any row is set
           "    const int nr_ = __popcll(m_);",
@@ -742,8 +762,37 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
           "c_ >>= 1; mm_ ^= lb_; }",
           "    d_ ^= d_ << 1; d_ ^= d_ << 2; d_ ^= d_ << 4; d_ ^= d_ << 8; d_ ^= d_ << 16; "
           "d_ ^= d_ << 32;",
-          "    d_ &= am;",
-          # exclusive scan of the lanes' row counts
+          "    d_ &= am;"]
+    # predicate mask: 64 compares, shift-or into two 32-bit halves (a C loop: each row's
+    # value is decoded where it is compared, not all 64 held decoded at once)
+    b.append("    unsigned plo_ = 0u, phi_ = 0u;")
+    cond = J._rename(g1.cnf(lpreds), pslots, "k")
+    for half, off in (("plo_", 0), ("phi_", 32)):
+        b.append("    #pragma unroll")
+        b.append("    for (int k_ = 0; k_ < 32; ++k_) {")
+        def raw_of(name: str) -> str:
+            et, word, bits, per = elem[name]
+            i = f"{off} + k_"
+            w = word.format(i=i)
+            return f"(({et})({w} >> ({bits} * (({i}) % {per}))))" if per > 1 else f"(({et}){w})"
+        for sl in pslots:
+            ct = J._CTYPE[cols[sl][0]]
+            enc = cols[sl][2]
+            raw = raw_of(f"x{sl}")
+            b.append(f"      const auto xr{sl}_k = {raw};")
+            raw = f"xr{sl}_k"
+            if enc:
+                b.append(f"      const int r{sl}_k = (int){raw};")
+            if enc and enc[1]:
+                bq = args.add("q", f"B{sl}", "long long")
+                b.append(f"      const i64 q{sl}_k = {bq} + (i64){raw};")
+            b.append(f"      const {ct} x{sl}_k = {g1.decode(sl, raw)};")
+            if cols[sl][1]:
+                b.append(f"      const bool n{sl}_k = {raw_of(f'n{sl}')} != 0;")
+        b.append(f"      {half} |= ({cond} ? 1u : 0u) << k_;")
+        b.append("    }")
+    b += ["    d_ &= ((u64)phi_ << 32) | (u64)plo_;",
+          # exclusive scan of the lanes' passing-row counts
           "    const int cn_ = __popcll(d_);",
           "    int inc_ = cn_;",
           "    for (int o_ = 1; o_ < 64; o_ <<= 1) { const int y_ = __shfl_up(inc_, o_, 64); "
@@ -760,7 +809,7 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
     ind2 = "      "
     for k in range(EW):
         b += [f"{ind2}const int ce{k} = cb + {64 * k} + ln;",
-              f"{ind2}bool cok{k} = ce{k} < wn_;",
+              f"{ind2}const bool cok{k} = ce{k} < wn_;",
               f"{ind2}const i64 crow{k} = tb0 + (cok{k} ? (i64)lst_[wq][ce{k}] : 0);"]
     gs = [J._Gen(args, cols, SPLIT, (f"crow{k}", f"crow{k}"), approx, True) for k in range(EW)]
     for k in range(EW):
@@ -769,7 +818,7 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
     for k in range(EW):
         g = gs[k]
         it = f"c{k}"
-        b.append(f"{ind2}{{ bool cok = cok{k} && {J._rename(g.cnf(lpreds), tail, it)};")
+        b.append(f"{ind2}{{ bool cok = cok{k};")
         gvar = "gic"
         if grouped:
             base = args.add("q", "group_base", "long long")
@@ -784,10 +833,10 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
     b += ["    }", f"    {J._wave_sync()}", "    }", "  }"]
     b += J._flush(aggs, grouped)
     src = (J._PRELUDE + args.struct_src() +
-           f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_run_sparse_scan(Args a) '
+           f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_run_bits_scan(Args a) '
            f'{{\n' + "\n".join(b) + "\n}\n")
     lds = (len(aggs) * p.num_groups * 32) if grouped else 0
-    return J.Kernel(src, "hs_jit_run_sparse_scan", args, lds)
+    return J.Kernel(src, "hs_jit_run_bits_scan", args, lds)
 
 
 class TwoPhaseLauncher:
