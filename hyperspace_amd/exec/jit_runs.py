@@ -645,8 +645,63 @@ SPARSE = os.environ.get("HS_JIT_RS_BITS", "1") == "1"
 SPARSE_GRID = int(os.environ.get("HS_JIT_RS_BITS_GRID", "8192"))
 
 
+# 1: the bits scan reads its aggregate inputs from one row-packed 64-bit word per row
+# (pack_layout / packed_tail) when they fit: one scattered fetch per passing row instead of one
+# per column
+PACK_TAIL = os.environ.get("HS_JIT_RS_PACK", "1") == "1"
+
+
+def _tail_slots(p: NL.JoinParams) -> list:
+    grouped = _scan_grouped(p)
+    aggs = [p.aggs[i] for i in range(p.naggs)]
+    return list(dict.fromkeys(J._agg_slots(aggs) + ([p.group_col] if grouped else [])))
+
+
+def pack_layout(p: NL.JoinParams, compacts) -> Optional[tuple]:
+    """((slot, bit offset, code bytes), ...) of the row-packed aggregate inputs of the bits
+    scan: two or more compact-coded tail columns without validity whose codes fit 64 bits."""
+    if not PACK_TAIL:
+        return None
+    slots = _tail_slots(p)
+    if len(slots) < 2:
+        return None
+    out, off = [], 0
+    for sl in slots:
+        c = (compacts or {}).get(sl)
+        if c is None or p.cols[sl].valid or getattr(c, "runs", None) or \
+                type(c).__name__ != "Compact" or c.width not in (1, 2, 4):
+            return None
+        out.append((sl, off, c.width))
+        off += 8 * c.width
+    return tuple(out) if off <= 64 else None
+
+
+# (ids of the packed code tensors) -> (the tensors, packed int64 words): derived per resident
+# table once, like the compact codes themselves
+_PACKS: dict = {}
+
+
+def packed_tail(layout, compacts):
+    """One int64 word per row: each layout column's code at its bit offset (uint bits)."""
+    import torch
+    key = tuple(id(compacts[sl].codes) for sl, _, _ in layout)
+    hit = _PACKS.get(key)
+    if hit is not None and all(a is compacts[sl].codes for a, (sl, _, _) in zip(hit[0], layout)):
+        return hit[1]
+    n = compacts[layout[0][0]].codes.numel()
+    w = torch.zeros(n, dtype=torch.int64, device=compacts[layout[0][0]].codes.device)
+    for sl, off, nb in layout:
+        c = compacts[sl].codes.to(torch.int64) & ((1 << (8 * nb)) - 1)
+        w |= c << off
+        del c
+    if len(_PACKS) >= 8:
+        _PACKS.pop(next(iter(_PACKS)))
+    _PACKS[key] = (tuple(compacts[sl].codes for sl, _, _ in layout), w)
+    return w
+
+
 def sparse_shape(p: NL.JoinParams, compacts) -> tuple:
-    return ("run_bits_scan",) + scan_shape(p, compacts, 1, 64)[1:]
+    return ("run_bits_scan",) + scan_shape(p, compacts, 1, 64)[1:] + (pack_layout(p, compacts),)
 
 
 def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
@@ -812,9 +867,21 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
               f"{ind2}const bool cok{k} = ce{k} < wn_;",
               f"{ind2}const i64 crow{k} = tb0 + (cok{k} ? (i64)lst_[wq][ce{k}] : 0);"]
     gs = [J._Gen(args, cols, SPLIT, (f"crow{k}", f"crow{k}"), approx, True) for k in range(EW)]
+    layout = pack_layout(p, compacts)
+    packed = {sl: (off, nb) for sl, off, nb in layout} if layout else {}
+    if layout:
+        args.add("p", "PK", "const unsigned long long*")
     for k in range(EW):
+        if layout:
+            b.append(f"{ind2}const u64 pk{k}_ = a.PK[crow{k}];")
         for sl in tail:
-            J._uload(gs[k], sl, f"c{k}", b, ind2)
+            if sl in packed:
+                off, nb = packed[sl]
+                ct = gs[k].raw_type(sl)
+                ut = {1: "unsigned char", 2: "unsigned short", 4: "unsigned"}[nb]
+                J._uload_raw(gs[k], sl, f"c{k}", f"(({ct})({ut})(pk{k}_ >> {off}))", "1", b, ind2)
+            else:
+                J._uload(gs[k], sl, f"c{k}", b, ind2)
     for k in range(EW):
         g = gs[k]
         it = f"c{k}"
@@ -959,7 +1026,11 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
         from ..ops import kernels as K
         tp64 = K.ranges_to_tiles(rlen + (rstart & 63), 4096)   # 64-aligned 4096-row tiles
         vs["tile_prefix"] = tp64.data_ptr()
-        spans = (spans, tp64)
+        layout = pack_layout(p, compacts)
+        pk = packed_tail(layout, compacts) if layout else None
+        if pk is not None:
+            vs["PK"] = pk.data_ptr()
+        spans = (spans, tp64, pk)
         grid_s = max(1, SPARSE_GRID)
     return TwoPhaseLauncher(kt, ks, grid_t, grid_s, GA, GA * 32 if _scan_grouped(p) else 0,
                             vt, vs, compacts, (rstart, rlen, rbucket, roff, tp, spans, tr, runs),

@@ -803,7 +803,8 @@ def test_merge_join_runs_matches_oracle(device, layout):
     p.preds[0] = NL.Pred(NL.PK_INT_LIT, NL.OP_GT, 1, 0, 0, 0, 300, 0.0, None)
     p.preds[1] = NL.Pred(NL.PK_INT_LIT, NL.OP_LT, 9, 0, 1, 0, 500, 0.0, None)
     p.nlp, p.npreds = 1, 2
-    p.aggs[0] = _agg(NL.AK_SUM, [(2, 0.0, 1.0)])
+    # two aggregate input columns (price, date): the bits scan reads them row-packed
+    p.aggs[0] = _agg(NL.AK_SUM, [(2, 0.0, 1.0), (1, 1.0, 0.001)])
     p.aggs[1] = _agg(NL.AK_COUNT_STAR)
     p.naggs, p.lkey, p.rkey, p.key_is_float = 2, 0, 8, 0
     p.group_col, p.num_groups, p.group_base = 10, 3, 0
@@ -827,7 +828,7 @@ def test_merge_join_runs_matches_oracle(device, layout):
                 for i in range(starts[b], starts[b] + lens[b]):
                     m = rmap.get(int(lk[i]))
                     if m is not None and m[0] and ldate[i] > 300:
-                        exp_s[m[1]] += lprice[i]
+                        exp_s[m[1]] += lprice[i] * (1.0 + 0.001 * ldate[i])
                         exp_c[m[1]] += 1
             rstart = torch.from_numpy(starts.astype(np.int64)).to(device)
             rlen = torch.from_numpy(lens.astype(np.int64)).to(device)
@@ -860,6 +861,8 @@ def test_merge_join_runs_matches_oracle(device, layout):
                         assert isinstance(launcher, jit_runs.TwoPhaseLauncher)
                         assert (launcher.rows is not None) == (rowm and not sparse and
                                                                not grouped), cfg
+                        if sparse and not grouped:
+                            assert jit_runs.pack_layout(p, comp) is not None
     finally:
         jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P, jit_runs.RT2 = lds_keys, runs, two2, rt2
         jit_runs.RT2_K16, jit_runs.ROWMASK, jit_runs.SPARSE = k16, rowmask, sparse0
