@@ -312,6 +312,32 @@ def exclusive_scan_i64(x):
 # profiles/build_packed_gather_r3.log
 PACKED_MIN_ROWS = 1 << 20
 PACKED_MAX_BYTES = 64
+# HS_GATHER_PACKED=auto (default): packed records only for permutations that jump around - the
+# median distance between the source rows of neighbouring outputs, over an evenly spaced sample,
+# at least PACKED_MIN_JUMP rows (a random permutation: ~n/3; li_orderkey's nearly sequential
+# one: ~1)
+PACKED_MIN_JUMP = 64
+PACKED_SAMPLE = 4096
+
+
+def sample_positions(n: int, k: int, device):
+    """min(k, n - 1) evenly spaced int64 positions in [0, n - 2] (integer arithmetic: a float32
+    linspace rounds positions of large n past the end)."""
+    torch = _torch()
+    k = min(k, n - 1)
+    return torch.arange(k, dtype=torch.int64, device=device) * (n - 2) // max(k - 1, 1)
+
+
+def _random_permutation(idx) -> bool:
+    """Whether ``idx`` reads its sources scattered (one small D2H of a sample of neighbouring
+    index pairs)."""
+    torch = _torch()
+    n = idx.numel()
+    if n < 2:
+        return False
+    pos = sample_positions(n, PACKED_SAMPLE, idx.device)
+    d = (idx.index_select(0, pos + 1).long() - idx.index_select(0, pos).long()).abs()
+    return float(d.float().median().item()) >= PACKED_MIN_JUMP
 
 
 def _packed_layout(cols, want_valid: bool):
@@ -334,15 +360,18 @@ def _packed_layout(cols, want_valid: bool):
 def gather_columns(cols: list, idx, want_valid: bool = True, padded: bool = False) -> list:
     """Gather a list of DeviceColumns by ``idx`` (int32 or int64 tensor) in one launch.
     ``padded``: ``idx`` (int64) may hold -1 for outer-join padding rows, which come out NULL
-    (every output column then carries a validity mask).  With ``HS_GATHER_PACKED=1``,
-    permutations of large multi-column tables go through packed records (``hs_gather_packed``):
-    one random sector per row instead of one per column."""
+    (every output column then carries a validity mask).  Scattered permutations of large
+    multi-column tables (``HS_GATHER_PACKED=auto``: ``_random_permutation``; ``1``: always,
+    ``0``: never) go through packed records (``hs_gather_packed``): one random sector per row
+    instead of one per column."""
     torch = _torch()
     from ..exec.device_table import DeviceColumn
     n = idx.numel()
+    mode = os.environ.get("HS_GATHER_PACKED", "auto")
     if (not padded and len(cols) >= 2 and len(cols) <= NL.GATHER_MAX_COLS and
-            n >= PACKED_MIN_ROWS and os.environ.get("HS_GATHER_PACKED", "0") == "1" and
-            len({len(c.data) for c in cols}) == 1):
+            n >= PACKED_MIN_ROWS and mode in ("1", "auto") and
+            len({len(c.data) for c in cols}) == 1 and
+            (mode == "1" or _random_permutation(idx))):
         lay = _packed_layout(cols, want_valid)
         if lay is not None:
             rb, offs, vbase = lay
