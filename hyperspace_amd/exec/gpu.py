@@ -34,7 +34,7 @@ from ..utils import murmur3
 from ..utils.conf import HyperspaceConf
 from ..utils.tracing import TRACER, stage
 from . import compile as CP
-from . import jit, join_index
+from . import jit, jit_runs, join_index
 from .arrow_eval import key
 from .device_cache import (DeviceTableCache, _files_key, load_bucketed_index, load_flat,
                            seeded_index)
@@ -2957,7 +2957,10 @@ class _JoinPrep:
                 if group is not None:
                     jp.group_col = col_info(group).slot if G > 1 else -1
                     jp.num_groups, jp.group_base = G, gbase
-                out = self.launcher.launch(jp)
+                if isinstance(self.launcher, jit_runs.TwoPhaseLauncher):
+                    out = self.launcher.launch(jp, lkey)
+                else:
+                    out = self.launcher.launch(jp)
         be._groups_agreed = self.agreed
         return (*out, *self.gtail)
 

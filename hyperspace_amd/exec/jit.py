@@ -186,6 +186,10 @@ class Args:
         body = "".join(f"  {ct} {n};\n" for _, n, ct in self.slots)
         return "struct Args {\n" + body + "};\n"
 
+    def offset(self, name: str) -> int:
+        """Byte offset of slot ``name`` in the packed block (every slot is 8 bytes)."""
+        return 8 * self._index[name]
+
     def pack(self, values: Dict[str, object]) -> bytes:
         fmt = "<" + "".join("q" if k in ("p", "q") else "d" for k, _, _ in self.slots)
         vals = []
@@ -285,6 +289,14 @@ class Kernel:
             JIT_STATS["compiled" if compiled.value == 1 else "loaded"] += 1
             self._fn = fn
         return self._fn
+
+    def launch_packed(self, grid: int, buf, stream_ptr: int, shmem: int = 0) -> None:
+        """Launch with an already packed argument block (``Args.pack`` bytes / bytearray)."""
+        cbuf = C.create_string_buffer(bytes(buf), len(buf))
+        rc = runtime().hs_jit_launch(self.function(), grid, self.block, shmem or self.lds_bytes,
+                                     stream_ptr, cbuf, len(buf))
+        if rc != 0:
+            raise RuntimeError(f"JIT launch failed: {runtime().hs_jit_last_error().decode()}")
 
     def launch(self, grid: int, values: Dict[str, object], stream_ptr: int, shmem: int = 0) -> None:
         buf = self.args.pack(values)

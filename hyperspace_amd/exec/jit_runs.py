@@ -910,7 +910,7 @@ class TwoPhaseLauncher:
     """Both phases lowered once (kernels, tiles, spans, per-tile run windows, the tag bitmap);
     ``launch(p)`` fills the literal slots and queues: bitmap clear, tags, scan, partials fold."""
     __slots__ = ("kt", "ks", "grid_t", "grid_s", "GA", "shmem", "vt", "vs", "compacts", "keep",
-                 "tags", "dev", "rows")
+                 "tags", "dev", "rows", "blocks")
 
     def __init__(self, kt, ks, grid_t, grid_s, GA, shmem, vt, vs, compacts, keep, tags, dev,
                  rows=None):
@@ -919,26 +919,40 @@ class TwoPhaseLauncher:
         self.compacts, self.keep, self.tags, self.dev = compacts, keep, tags, dev
         # row-mask expansion between the phases: (gmask ptr, gruns ptr, g0, g1, mask tensor)
         self.rows = rows
+        # literal vector -> (phase-1 block, phase-2 block template): a repeated parameter set
+        # re-packs only the per-launch partials pointers
+        self.blocks: dict = {}
 
-    def launch(self, p: NL.JoinParams):
-        preds = [(k_, p.preds[k_]) for k_ in range(p.npreds)]
-        aggs = [p.aggs[i] for i in range(p.naggs)]
-        vt = dict(self.vt)
-        J.fill_preds_aggs(vt, preds, [], self.compacts)
-        if "RNG" not in vt:   # the tile form ORs into a zeroed bitmap; the direct form stores
-            self.tags.zero_()  # every word of every run group
+    def launch(self, p: NL.JoinParams, key=None):
+        import struct
         st = NL.stream_ptr()
-        self.kt.launch(self.grid_t, vt, st)
+        hit = self.blocks.get(key) if key is not None else None
+        if hit is None:
+            preds = [(k_, p.preds[k_]) for k_ in range(p.npreds)]
+            aggs = [p.aggs[i] for i in range(p.naggs)]
+            vt = dict(self.vt)
+            J.fill_preds_aggs(vt, preds, [], self.compacts)
+            vs = dict(self.vs)
+            vs.update({"psum": 0, "pcnt": 0, "pmin": 0, "pmax": 0})
+            J.fill_preds_aggs(vs, preds, aggs, self.compacts)
+            hit = (self.kt.args.pack(vt), bytearray(self.ks.args.pack(vs)))
+            if key is not None:
+                if len(self.blocks) >= 256:
+                    self.blocks.clear()
+                self.blocks[key] = hit
+        if "RNG" not in self.vt:  # the tile form ORs into a zeroed bitmap; the direct form
+            self.tags.zero_()     # stores every word of every run group
+        self.kt.launch_packed(self.grid_t, hit[0], st)
         if self.rows is not None:
             gm, gr, g0, g1, rm = self.rows
             NL.check(NL.lib().hs_run_rowmask(gm, gr, self.tags.data_ptr(), g0, g1, rm.data_ptr(),
                                              st), "hs_run_rowmask")
         parts = J._partials(self.grid_s, self.GA, self.dev)
-        vs = dict(self.vs)
-        vs.update({"psum": parts[0].data_ptr(), "pcnt": parts[1].data_ptr(),
-                   "pmin": parts[2].data_ptr(), "pmax": parts[3].data_ptr()})
-        J.fill_preds_aggs(vs, preds, aggs, self.compacts)
-        self.ks.launch(self.grid_s, vs, st, self.shmem)
+        bs = bytearray(hit[1])
+        a = self.ks.args
+        for name, t in zip(("psum", "pcnt", "pmin", "pmax"), parts):
+            struct.pack_into("<q", bs, a.offset(name), t.data_ptr())
+        self.ks.launch_packed(self.grid_s, bs, st, self.shmem)
         return J._final(parts, self.grid_s, self.GA, self.dev)
 
 
