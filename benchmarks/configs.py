@@ -236,6 +236,8 @@ def config_hybrid(args):
     TRACER.reset()
     el_h = _timed_loop(step, args.steps, args.device)
     path_h = getattr(s.backend(), "last_path", None)
+    merge_skip = getattr(s.backend(), "metrics", {}).get("hybrid_merge_skip")
+    print(f"[hybrid] merged union skipped: {merge_skip}", file=sys.stderr, flush=True)
     if TRACER.profile:   # HS_PROFILE=1: where the Hybrid Scan steps spend their time
         print("[hybrid] hybrid-scan stage profile\n" + format_report(TRACER.report()),
               file=sys.stderr, flush=True)
@@ -269,6 +271,7 @@ def config_hybrid(args):
             "refreshed_queries_per_s": round(2 * args.steps / el_r, 2),
             "incremental_refresh_s": round(refresh_s, 3), "index_build_s": builds,
             "bucket_union_in_plan": "BucketUnion" in plan, "path": path_h,
+            "hybrid_merge_skip": merge_skip,
             "hybrid_matches_refreshed": bool(match)}
 
 
