@@ -339,18 +339,25 @@ class GpuBackend:
                     first.bucket_attrs, nb, parts)
 
     @staticmethod
-    def _union_conds(p: X.BucketUnionExec, parts: List[DRel], outputs) -> Optional[list]:
-        """The parts' pending predicates over the union's output attributes when every part
-        carries the same ones (a filter pushed below the union into each child), else None."""
+    def _union_conds(p: X.BucketUnionExec, parts: List[DRel], outputs):
+        """(predicates, extra attributes) when every part carries the same pending predicates (a
+        filter pushed below the union into each child), over the union's output attributes plus
+        ``extra``: columns the filter reads that a projection above it dropped, present under
+        the same attribute in every part (a Hybrid Scan's branches share the relation's
+        attributes).  None when the parts' predicates differ."""
         keys, conds0 = None, None
+        extra: Dict[int, E.Attribute] = {}
         for x, out in zip(parts, outputs):
             sub = {c.expr_id: u for u, c in zip(p.output, out)}
             missing = []
 
-            def ren(e, sub=sub, missing=missing):
+            def ren(e, sub=sub, missing=missing, x=x):
                 if isinstance(e, E.Attribute):
                     u = sub.get(e.expr_id)
                     if u is None:
+                        if all(e.expr_id in y.colmap for y in parts):
+                            extra.setdefault(e.expr_id, e)
+                            return e
                         missing.append(e)
                     return u
                 return None
@@ -362,7 +369,7 @@ class GpuBackend:
                 keys, conds0 = k, conds
             elif k != keys:
                 return None
-        return conds0
+        return conds0, list(extra.values())
 
     def _merged_union(self, p: X.BucketUnionExec, parts: List[DRel],
                       outputs=None) -> Optional[DRel]:
@@ -391,12 +398,14 @@ class GpuBackend:
                     n for n, v in (("no table", x.table is None), ("extra", x.extra),
                                    ("split", x.split), ("parts", x.parts)) if v))
         # the same filter in every part (pushed below the union) applies to the merged rows
-        conds = self._union_conds(p, parts, outputs) if outputs is not None else \
-            ([] if not any(x.conds for x in parts) else None)
-        if conds is None:
+        uc = self._union_conds(p, parts, outputs) if outputs is not None else \
+            (([], []) if not any(x.conds for x in parts) else None)
+        if uc is None:
             return skip("parts carry different predicates")
+        conds, extra = uc
         first = parts[0]
-        outs = list(p.output)
+        visible = list(p.output)
+        outs = visible + [a for a in extra if a.expr_id not in {u.expr_id for u in visible}]
         ids = {u.expr_id for u in outs}
         if not first.sort_attrs or any(a.expr_id not in ids for a in first.sort_attrs):
             return skip("sort attributes not in the output")
@@ -453,7 +462,7 @@ class GpuBackend:
             memo[key] = ([x.table for x in parts], table)
         self.metrics.pop("hybrid_merge_skip", None)
         colmap = {u.expr_id: f"u{j}" for j, u in enumerate(outs)}
-        return DRel(table, colmap, outs, conds, True, first.sort_attrs, first.bucket_attrs,
+        return DRel(table, colmap, visible, conds, True, first.sort_attrs, first.bucket_attrs,
                     first.num_buckets)
 
     def _unary(self, p: X.SparkPlan, r: DRel) -> DRel:
