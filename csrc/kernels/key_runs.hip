@@ -112,9 +112,40 @@ __global__ __launch_bounds__(256) void hs_run_rowmask_kernel(const uint64_t* __r
   out[g] = d;
 }
 
+// Semi-join probe over the run form: tag of run r = the build-key bitmap's bit for run r's key
+// (one bitmap test per run instead of per row), 1 bit per run, stored as whole words by the
+// wavefront that owns 64 consecutive runs (ballot), as exec/jit_runs.py phase 1 writes them.
+// key value = code + code_off - lo is the bitmap position; codes out of [0, nbits) miss.
+__global__ __launch_bounds__(256) void hs_run_bitmap_tags_kernel(const int32_t* __restrict__ runkeys,
+                                                                 int64_t nruns, int64_t code_off,
+                                                                 const uint64_t* __restrict__ words,
+                                                                 int64_t nbits,
+                                                                 uint32_t* __restrict__ tags) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  bool t = false;
+  if (r < nruns) {
+    const int64_t v = (int64_t)runkeys[r] + code_off;
+    t = v >= 0 && v < nbits && ((words[v >> 6] >> (v & 63)) & 1ull);
+  }
+  const uint64_t b = __ballot(t);
+  const int64_t g = r >> 6;                 // wavefront-uniform: 64 runs per wavefront
+  if (lane < 2 && (g << 6) < nruns) tags[2 * g + lane] = (uint32_t)(b >> (32 * lane));
+}
+
 }  // namespace
 
 extern "C" {
+
+// tags: at least 2 * ceil(nruns / 64) words
+int hs_run_bitmap_tags(const int32_t* runkeys, int64_t nruns, int64_t code_off,
+                       const uint64_t* words, int64_t nbits, uint32_t* tags, void* stream) {
+  if (nruns > 0)
+    hipLaunchKernelGGL(hs_run_bitmap_tags_kernel, dim3((unsigned)((nruns + 255) / 256)),
+                       dim3(256), 0, (hipStream_t)stream, runkeys, nruns, code_off, words, nbits,
+                       tags);
+  return (int)hipGetLastError();
+}
 
 // tags must hold 2 readable words past the last run's word (phase 1 allocates that slack)
 int hs_run_rowmask(const uint64_t* gmask, const int32_t* gruns, const uint32_t* tags, int64_t g0,

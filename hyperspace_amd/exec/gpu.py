@@ -2150,9 +2150,70 @@ class GpuBackend:
         if prel.parts:
             return None
         cond = CP.KeyBitmap(pk, words, lo, nbits)
-        self.last_semi_join = {"build_keys": int(keys.data.numel()), "bitmap_bits": nbits}
+        self.last_semi_join = {"build_keys": int(keys.data.numel()), "bitmap_bits": nbits,
+                               "probe": "scan"}
         with stage("semi.probe"):
+            out = self._semi_runs(prel, pk, words, lo, nbits, fns, group)
+            if out is not None:
+                self.last_semi_join["probe"] = "runs"
+                return out
             return self._scan_agg(prel.copy(conds=prel.conds + [cond]), fns, group)
+
+    def _semi_runs(self, r: DRel, key, words, lo: int, nbits: int, fns, group):
+        """The semi-join probe over the probe key's run form (``jit_runs.semi_runs_agg``): a
+        resident index relation sorted by the key (an index's bucket-sorted indexed column, so
+        its rows form runs of equal keys) tests the build bitmap once per run and scans its
+        own predicates and aggregates bit-parallel.  None when the shape does not qualify (the
+        plain scan with a per-row bitmap predicate runs instead)."""
+        conf = self.session.conf
+        if not (jit_runs.SPARSE and HyperspaceConf.codegen_enabled(conf)) or \
+                str(conf.get("spark.hyperspace.mi.semiRuns.enabled", "true")).lower() != "true":
+            return None
+        if r.table is None or r.parts or r.extra or r.split or not r.bucketed or \
+                not r.sort_attrs or r.sort_attrs[0].expr_id != key.expr_id:
+            return None
+        col_info, descs = self._column_infos([(r, 0)])
+        kslot = col_info(key).slot
+        implied: set = set()
+        spec = self._range_spec(r, r.conds, implied)
+        bound = CP.bind(CP.to_cnf([c for c in r.conds if id(c) not in implied]), col_info,
+                        self.device)
+        specs = self._agg_specs(fns, col_info)
+        gs = self._group_spec(r, group, _group_limit(MAX_GROUPS_SCAN, GROUP_LDS_SCAN, len(fns)))
+        if gs is None:
+            return None
+        agreed, G, gbase, gdict, gtype = gs
+        gslot = col_info(group).slot if (group is not None and G > 1) else -1
+        if any(sl >= jit_runs.SPLIT for sl in descs) or len(bound.preds) > NL.MAX_PREDS:
+            return None
+        comp = self._compacts(descs)
+        if not comp or kslot not in comp or r.col(key).valid is not None:
+            return None
+        from .encoding import key_runs
+        runs = key_runs(comp[kslot])
+        if runs is None:
+            return None
+        comp = dict(comp)
+        comp[kslot] = runs
+        rstart, rlen, _ = self._ranges(r, r.conds) if spec is not None else \
+            self._full_ranges(r.table)
+        self._groups_agreed = agreed is True
+        if bound.always_false:
+            return (*self._empty_agg(len(specs), G), G, gbase, gdict, gtype)
+        p = NL.JoinParams()
+        for s_, c in descs.items():
+            p.cols[s_] = c.desc()
+        for i, pr in enumerate(bound.preds):
+            p.preds[i] = pr
+        p.nlp = p.npreds = len(bound.preds)
+        for i, a in enumerate(specs):
+            p.aggs[i] = a
+        p.naggs = len(specs)
+        p.lkey, p.rkey, p.key_is_float = kslot, kslot, 0
+        p.group_col, p.num_groups, p.group_base = gslot, G, gbase
+        out = jit_runs.semi_runs_agg(p, rstart, rlen, comp, runs, r.table.num_rows, words, lo,
+                                     nbits)
+        return (*out, G, gbase, gdict, gtype)
 
     def _semi_project(self, p: X.ProjectExec) -> Optional[DRel]:
         """``Project <- Filter* <- inner join`` whose projection and filters read one side only:

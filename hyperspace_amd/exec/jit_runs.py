@@ -1049,3 +1049,46 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
     return TwoPhaseLauncher(kt, ks, grid_t, grid_s, GA, GA * 32 if _scan_grouped(p) else 0,
                             vt, vs, compacts, (rstart, rlen, rbucket, roff, tp, spans, tr, runs),
                             tags, dev, rows)
+
+
+def semi_runs_agg(p: NL.JoinParams, rstart, rlen, compacts, runs, nrows: int, words, lo: int,
+                  nbits: int):
+    """A semi-join probe (``attr in <build-key bitmap>``, GpuBackend._semi_join_agg) over the
+    probe key's run form: one bitmap test per run (``hs_run_bitmap_tags``: 1-bit run tags), then
+    the bit-parallel phase 2 (``gen_run_sparse_scan``) with the probe's own predicates and
+    aggregates - the per-row key read and bitmap test of the plain scan become per-run.  ``p``
+    carries the probe side only (slots < SPLIT, ``p.lkey`` = the key slot, ``p.nlp ==
+    p.npreds``).  Returns the aggregate outputs (sums, counts, mins, maxs)."""
+    import torch
+    from ..ops import kernels as K
+    dev = rstart.device
+    nruns = int(runs.runkeys.numel())
+    G = (nruns + 63) >> 6  # noqa: N806
+    tags = torch.empty(2 * G + 4, dtype=torch.int32, device=dev)
+    st = NL.stream_ptr()
+    NL.check(NL.lib().hs_run_bitmap_tags(runs.runkeys.data_ptr(), nruns, int(runs.base) - int(lo),
+                                         words.data_ptr(), int(nbits), tags.data_ptr(), st),
+             "hs_run_bitmap_tags")
+    ks = J.kernel_for(sparse_shape(p, compacts), lambda: gen_run_sparse_scan(p, compacts))
+    tp64 = K.ranges_to_tiles(rlen + (rstart & 63), 4096)
+    vs = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp64.data_ptr(),
+          "tags": tags.data_ptr(), "R": rstart.numel(), "nrows": nrows,
+          "num_groups": p.num_groups, "group_base": p.group_base}
+    J._fill_cols(vs, p.cols, compacts)
+    layout = pack_layout(p, compacts)
+    pk = packed_tail(layout, compacts) if layout else None
+    if pk is not None:
+        vs["PK"] = pk.data_ptr()
+    GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)  # noqa: N806
+    grid = max(1, SPARSE_GRID)
+    parts = J._partials(grid, GA, dev)
+    vs.update({"psum": parts[0].data_ptr(), "pcnt": parts[1].data_ptr(),
+               "pmin": parts[2].data_ptr(), "pmax": parts[3].data_ptr()})
+    J.fill_preds_aggs(vs, [(k_, p.preds[k_]) for k_ in range(p.npreds)],
+                      [p.aggs[i] for i in range(p.naggs)], compacts)
+    ks.launch(grid, vs, st, GA * 32 if _scan_grouped(p) else 0)
+    out = J._final(parts, grid, GA, dev)
+    for t in (tags, tp64, pk):      # used by the queued kernels: keep until they ran
+        if t is not None:
+            t.record_stream(torch.cuda.current_stream(dev))
+    return out

@@ -206,6 +206,7 @@ def lib():
     _sig(L.hs_key_runs_fill, I, P, I64, P, P, P, P, P)
     _sig(L.hs_tile_runs, I, P, I, P, P, P, I64, P, P)
     _sig(L.hs_run_rowmask, I, P, P, P, I64, I64, P, P)
+    _sig(L.hs_run_bitmap_tags, I, P, I64, I64, P, I64, P, P)
     _sig(L.hs_key_bitmap, I, P, I64, I64, I64, P, P, P)
     _sig(L.hs_bitmap_popcount, I, P, I64, P, P)
     _sig(L.hs_str_hash64, I, P, P, I64, P, P)

@@ -68,7 +68,10 @@ def test_three_way_q3_semi_join_bitmap(q3data):
         g, h, path, be = _run(s, q)
         assert path == "native", be.fallback_reason
         assert be.last_semi_join["build_keys"] > 0
+        # the lineitem index is sorted by l_orderkey: one bitmap test per key run
+        assert be.last_semi_join["probe"] == "runs"
         assert g[0]["lines"] == h[0]["lines"] > 0
+        h0 = h
         assert abs(g[0]["revenue"] - h[0]["revenue"]) <= 1e-9 * abs(h[0]["revenue"])
         # grouped over a probe-side column as well
         s.backend().last_semi_join = None
@@ -81,6 +84,15 @@ def test_three_way_q3_semi_join_bitmap(q3data):
         assert be.last_semi_join is not None
         assert sorted(map(tuple, (r.values() for r in g))) == \
             sorted(map(tuple, (r.values() for r in h)))
+        # the per-row bitmap scan agrees with the run form
+        s.conf.set("spark.hyperspace.mi.semiRuns.enabled", "false")
+        try:
+            g2, _, path2, be = _run(s, q)
+            assert path2 == "native" and be.last_semi_join["probe"] == "scan"
+            assert g2[0]["lines"] == h0[0]["lines"]
+            assert abs(g2[0]["revenue"] - h0[0]["revenue"]) <= 1e-9 * abs(h0[0]["revenue"])
+        finally:
+            s.conf.set("spark.hyperspace.mi.semiRuns.enabled", "true")
 
 
 def test_repeated_build_keys_take_the_general_join(q3data, tmp_path):
