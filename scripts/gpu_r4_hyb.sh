@@ -12,3 +12,10 @@ rc=$?
 echo "tests rc=$rc" >> gpurun_out/${TAG}_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 HS_PROFILE=1 TAG=$TAG PART=configs CONFIGS="${CONFIGS:-hybrid q3_3way}" bash scripts/gpu_r4_side.sh
+rc=$?
+[ $rc -ne 0 ] && exit $rc
+if [ -n "$RECORD" ]; then
+  # kernel sources the bench generates, for the ahead-of-time set (hyperspace_amd/_native/aot)
+  HS_JIT_RECORD=gpurun_out/aot_${TAG} timeout -k 10 600 python bench.py --sf 100 --steps 100 \
+    --warmup 5 > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.log || exit $?
+fi
