@@ -1675,6 +1675,10 @@ class GpuBackend:
             self._join_rec = None
             res = self._join_agg(node, fns, group)
             self._join_prep_put(final, node, res)
+        elif group is None and isinstance(node, X.UnionExec) and \
+                str(self.session.conf.get("spark.hyperspace.mi.unionAgg.enabled", "true")).lower() \
+                == "true":
+            res = self._union_agg(node, fns)
         else:
             r = self._rel(child)
             self._scan_gs = None
@@ -1897,7 +1901,33 @@ class GpuBackend:
             raise Unsupported("too many aggregates")
         return specs
 
-    def _scan_agg(self, r: DRel, fns, group, prep: Optional["_ScanPrep"] = None):
+    def _union_agg(self, node: X.UnionExec, fns):
+        """An ungrouped aggregate over UNION ALL (a Hybrid Scan filter query: the index scan
+        plus the appended files, FilterIndexRule's hybrid union) as one fused scan aggregate
+        per branch - the index branch keeps its key-range pruning - with the partial results
+        combined on the device (an aggregate distributes over UNION ALL), instead of
+        materializing and concatenating every branch's rows first."""
+        import torch
+        res = []
+        for child in node.children:
+            r = self._rel(child)
+            if r.parts or r.table is None:
+                raise Unsupported("union branch is a bucket union")
+            colmap = dict(r.colmap)
+            for u, c in zip(node.output, child.output):
+                if c.expr_id in r.colmap:
+                    colmap[u.expr_id] = r.colmap[c.expr_id]
+            res.append(self._scan_agg(r.copy(colmap=colmap), fns, None, graph_ok=False))
+        sums, cnts, mins, maxs = (t.clone() for t in res[0][:4])
+        for x in res[1:]:
+            sums.add_(x[0])
+            cnts.add_(x[1])
+            torch.minimum(mins, x[2], out=mins)
+            torch.maximum(maxs, x[3], out=maxs)
+        return sums, cnts, mins, maxs, 1, 0, None, None
+
+    def _scan_agg(self, r: DRel, fns, group, prep: Optional["_ScanPrep"] = None,
+                  graph_ok: bool = True):
         """Fused scan + filter + aggregate.  ``prep`` (a plan-cache hit submitting the same plan
         nodes again, ``_dense_agg``) carries what does not depend on literal values - column
         slots, group domain, compact encodings, the generated kernel, the captured graph and
@@ -1922,7 +1952,7 @@ class GpuBackend:
                 prep.lowered[lkey] = (spec, bound, specs)
         else:
             spec, bound, specs = low
-        graph = self._graph_eligible(spec, descs)
+        graph = graph_ok and self._graph_eligible(spec, descs)
         if not graph:
             with stage("scan.ranges"):
                 rstart, rlen, _ = self._ranges(r, r.conds) if spec is not None else \

@@ -319,6 +319,18 @@ def test_hybrid_scan_join_and_filter_on_device(tpch, tmp_path):
             _close(g2, c2)
     finally:
         s.conf.set("spark.hyperspace.mi.hybridMerge.enabled", "true")
+    # the filter query's UNION ALL (index + appended files): per-branch fused aggregates
+    # (GpuBackend._union_agg) equal the materialize-and-concatenate path
+    plan2 = q2.queryExecution.executed_plan.tree_string()
+    if "Union" in plan2 and "BucketUnion" not in plan2:
+        s.conf.set("spark.hyperspace.mi.unionAgg.enabled", "false")
+        try:
+            g3, c3, path = _both(s, q2, sort=False)
+            assert path == "native", s.backend().fallback_reason
+            _close(g3, c3)
+            _close(g3, g)
+        finally:
+            s.conf.set("spark.hyperspace.mi.unionAgg.enabled", "true")
 
 
 def test_incremental_refresh_with_deletes_on_device(tpch, tmp_path):
