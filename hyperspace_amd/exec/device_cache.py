@@ -41,6 +41,9 @@ def _files_key(files) -> tuple:
     return k
 
 
+HOLDS_REACCOUNT = 16
+
+
 class DeviceTableCache:
     """LRU of resident tables under an HBM byte budget.  A table's footprint includes what
     queries derive from it and keep on it (compacted column copies, join indexes, packed /
@@ -107,10 +110,15 @@ class DeviceTableCache:
                 return False
             self._lru.move_to_end(key)
             self.hits += 1
-            nb = t.resident_bytes()
-            self._bytes += nb - self._size.get(key, nb)
-            self._size[key] = nb
-            self._evict(key)
+            # re-account the structures queries derived from the table (compact codes, join
+            # indexes, ...) every HOLDS_REACCOUNT hits, not on every query's check
+            seen = getattr(t, "_hs_holds", 0)
+            t._hs_holds = seen + 1
+            if seen % HOLDS_REACCOUNT == 0:
+                nb = t.resident_bytes()
+                self._bytes += nb - self._size.get(key, nb)
+                self._size[key] = nb
+                self._evict(key)
             return True
 
     @property
