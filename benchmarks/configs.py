@@ -238,6 +238,12 @@ def config_hybrid(args):
     path_h = getattr(s.backend(), "last_path", None)
     merge_skip = getattr(s.backend(), "metrics", {}).get("hybrid_merge_skip")
     print(f"[hybrid] merged union skipped: {merge_skip}", file=sys.stderr, flush=True)
+    if TRACER.profile:   # the filter query's plan and whether its scan pruned key ranges
+        q6p = _q6(li, 0)
+        q6p.collect()
+        print(q6p.queryExecution.executed_plan.tree_string()[:3000], file=sys.stderr, flush=True)
+        print(f"[hybrid] q6 metrics {getattr(s.backend(), 'metrics', {})}", file=sys.stderr,
+              flush=True)
     if TRACER.profile:   # HS_PROFILE=1: where the Hybrid Scan steps spend their time
         print("[hybrid] hybrid-scan stage profile\n" + format_report(TRACER.report()),
               file=sys.stderr, flush=True)

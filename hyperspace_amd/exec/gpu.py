@@ -1953,6 +1953,7 @@ class GpuBackend:
         else:
             spec, bound, specs = low
         graph = graph_ok and self._graph_eligible(spec, descs)
+        self.metrics["scan_key_ranges"] = spec is not None   # leading-key range pruning
         if not graph:
             with stage("scan.ranges"):
                 rstart, rlen, _ = self._ranges(r, r.conds) if spec is not None else \
