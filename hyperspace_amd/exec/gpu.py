@@ -548,13 +548,20 @@ class GpuBackend:
             return r.copy()
         return r
 
-    def _scan(self, p: X.FileSourceScanExec) -> DRel:
+    def _scan(self, p: X.FileSourceScanExec, files=None, bucketed: Optional[bool] = None) -> DRel:
+        """The device relation of a scan leaf: its index bucket files as a bucket-sorted table,
+        anything else as a flat table.  ``files`` / ``bucketed``: a subset of the leaf's files
+        and which path it takes (``_mixed_index_agg``)."""
         rel = p.relation
-        files = rel.location.all_files()
+        if files is None:
+            files = rel.location.all_files()
         d = self._dist()
         rank, world = (d.rank, d.world) if d is not None else (0, 1)
         names = [a.name for a in p.output]
-        if rel.is_index() and self._all_bucket_files(rel.location, files, rel.index.num_buckets):
+        if bucketed is None:
+            bucketed = rel.is_index() and \
+                self._all_bucket_files(rel.location, files, rel.index.num_buckets)
+        if bucketed:
             idx = rel.index
             ncol = {n.lower(): n for n in idx.schema.names}
             cols = [ncol[a.name.lower()] for a in p.output]
@@ -1679,6 +1686,8 @@ class GpuBackend:
                 str(self.session.conf.get("spark.hyperspace.mi.unionAgg.enabled", "true")).lower() \
                 == "true":
             res = self._union_agg(node, fns)
+        elif group is None and (res := self._mixed_index_agg(child, fns)) is not None:
+            pass
         else:
             r = self._rel(child)
             self._scan_gs = None
@@ -1900,6 +1909,56 @@ class GpuBackend:
         if len(specs) > NL.MAX_AGGS:
             raise Unsupported("too many aggregates")
         return specs
+
+    def _mixed_index_agg(self, child: X.SparkPlan, fns):
+        """An ungrouped aggregate over Filter / Project of an index scan whose file list also
+        holds appended source files (FilterIndexRule's Hybrid Scan appends them to the index
+        relation, ``RuleUtils`` same-scan appended files): the index bucket files load as the
+        bucket-sorted table - so the scan keeps its leading-key range pruning - and the appended
+        files as a flat table; one fused scan aggregate each, partials combined on the device.
+        None when the shape does not qualify (one flat table of every file then)."""
+        import torch
+        if str(self.session.conf.get("spark.hyperspace.mi.mixedScanAgg.enabled", "true")).lower() \
+                != "true":
+            return None
+        d = self._dist()
+        if d is not None and d.world > 1:
+            return None
+        chain, node = [], child
+        while isinstance(node, (X.FilterExec, X.ProjectExec)):
+            chain.append(node)
+            node = node.child
+        if not isinstance(node, X.FileSourceScanExec) or not node.relation.is_index():
+            return None
+        rel = node.relation
+        nb = rel.index.num_buckets
+        files = rel.location.all_files()
+        if self._all_bucket_files(rel.location, files, nb):
+            return None
+        from ..io.writer import get_bucket_id
+        from ..utils import path_utils as P
+
+        def is_bucket(f) -> bool:
+            b = get_bucket_id(P.get_name(f.path))
+            return b is not None and b < nb
+        bfiles = [f for f in files if is_bucket(f)]
+        afiles = [f for f in files if not is_bucket(f)]
+        if not bfiles or not afiles:
+            return None
+        res = []
+        for fs, bk in ((bfiles, True), (afiles, False)):
+            r = self._scan(node, fs, bk)
+            for n in reversed(chain):
+                r = self._unary(n, r)
+            res.append(self._scan_agg(r, fns, None, graph_ok=False))
+        sums, cnts, mins, maxs = (t.clone() for t in res[0][:4])
+        x = res[1]
+        sums.add_(x[0])
+        cnts.add_(x[1])
+        torch.minimum(mins, x[2], out=mins)
+        torch.maximum(maxs, x[3], out=maxs)
+        self.metrics["mixed_scan_agg"] = (len(bfiles), len(afiles))
+        return sums, cnts, mins, maxs, 1, 0, None, None
 
     def _union_agg(self, node: X.UnionExec, fns):
         """An ungrouped aggregate over UNION ALL (a Hybrid Scan filter query: the index scan

@@ -322,6 +322,18 @@ def test_hybrid_scan_join_and_filter_on_device(tpch, tmp_path):
     # the filter query's UNION ALL (index + appended files): per-branch fused aggregates
     # (GpuBackend._union_agg) equal the materialize-and-concatenate path
     plan2 = q2.queryExecution.executed_plan.tree_string()
+    if "Union" not in plan2:
+        # same-scan appended files: the index files scan bucket-sorted (key-range pruned), the
+        # appended files flat (GpuBackend._mixed_index_agg); equal to one flat table of all
+        assert s.backend().metrics.get("mixed_scan_agg"), plan2
+        s.conf.set("spark.hyperspace.mi.mixedScanAgg.enabled", "false")
+        try:
+            g3, c3, path = _both(s, q2, sort=False)
+            assert path == "native", s.backend().fallback_reason
+            _close(g3, c3)
+            _close(g3, g)
+        finally:
+            s.conf.set("spark.hyperspace.mi.mixedScanAgg.enabled", "true")
     if "Union" in plan2 and "BucketUnion" not in plan2:
         s.conf.set("spark.hyperspace.mi.unionAgg.enabled", "false")
         try:
