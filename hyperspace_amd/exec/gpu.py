@@ -1951,6 +1951,9 @@ class GpuBackend:
             for n in reversed(chain):
                 r = self._unary(n, r)
             res.append(self._scan_agg(r, fns, None, graph_ok=False))
+            if bk:
+                pruned = self.metrics.get("scan_key_ranges")
+        self.metrics["scan_key_ranges"] = pruned     # the bucket files' scan, not the flat one
         sums, cnts, mins, maxs = (t.clone() for t in res[0][:4])
         x = res[1]
         sums.add_(x[0])
@@ -2532,11 +2535,15 @@ class GpuBackend:
         while isinstance(node, X.ProjectExec) and \
                 all(isinstance(e, E.Attribute) for e in node.project_list):
             node = node.child
+        fd = None
         if isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner":
             left, right, lk, rk = self._join_inputs(node)
             lparts, rparts = left.parts or [left], right.parts or [right]
             rels = lparts + rparts
             launches = [("join", lp, rp) for lp in lparts for rp in rparts]
+            fd = self._fd_grouping(final, grouping, left, right, lk, rk, order, limit)
+            if fd is not None:
+                grouping = fd[0]
         else:
             r = self._rel(child)
             rels = r.parts or [r]
@@ -2587,8 +2594,100 @@ class GpuBackend:
                 src = self._topk_source(final, fns, grouping, hk, order, limit, G)
                 if src is not None:
                     groups, G = H.topk_candidates(groups, G, src, int(limit))
-                return self._hash_table_out(final, fns, grouping, hk, groups.to_host(G), A)
+                extra = None
+                if fd is not None:
+                    def extra(gmap, host):
+                        self._fd_lookup(right, rk, fd[1], gmap[fd[0][0].expr_id], gmap)
+                return self._hash_table_out(final, fns, grouping, hk, groups.to_host(G), A,
+                                            extra)
         return finish
+
+    # keys per functional-dependency lookup launch (one probe per (bucket, key))
+    FD_MAX_KEYS = 8192
+
+    def _fd_grouping(self, final, grouping, left: DRel, right: DRel, lk, rk, order, limit):
+        """GROUP BY (left join key, right columns...) over an inner join whose right key is
+        unique: every right column is a function of the key (TPC-H Q3's ``l_orderkey,
+        o_orderdate, o_shippriority``), so the groups are the left key's and the right columns
+        are looked up for the result groups only (``_fd_lookup``).  The reduced grouping lets
+        the run-keyed two-phase join aggregate into the hash table (jit_runs hash walk).  Returns
+        ([the key attribute], [right attributes]) or None.  Applies when the result is bounded
+        by an ORDER BY <aggregate> LIMIT k (device top-k) on one rank."""
+        if not HyperspaceConf.fd_group_enabled(self.session.conf):
+            return None
+        if left.parts or right.parts or not order or limit is None or \
+                not 0 < int(limit) <= 1024:
+            return None
+        d = self._dist()
+        if d is not None and d.world > 1:
+            return None
+        if (right.table.num_rows or 0) * 64 < (left.table.num_rows or 0):
+            return None          # _join_hash_pair would swap the sides
+        keyg = [g for g in grouping if g.expr_id in (lk.expr_id, rk.expr_id)]
+        rest = [g for g in grouping if g.expr_id not in (lk.expr_id, rk.expr_id)]
+        if len(keyg) != 1 or not rest:
+            return None
+        if any(g.expr_id not in right.colmap or g.expr_id in left.colmap for g in rest):
+            return None
+        lc, rc = left.col(lk), right.col(rk)
+        if lc.is_float or rc.is_float or lc.dictionary is not None or \
+                rc.dictionary is not None or lc.valid is not None or \
+                rc.hs_type not in (NL.I8, NL.I16, NL.I32, NL.I64):
+            return None
+        e = order[0].child
+        if not isinstance(e, E.Attribute):
+            return None
+        ok = False
+        for agg in final.aggregates:
+            a = agg if isinstance(agg, E.Attribute) else agg.to_attribute()
+            if a.expr_id == e.expr_id:
+                inner = agg.child if isinstance(agg, E.Alias) else agg
+                ok = isinstance(inner, E.AggregateFunction)
+        if not ok or jit.key_has_dups(rc):
+            return None
+        g = keyg[0]
+        if g.expr_id != lk.expr_id:      # the right key's attribute: group by the left's
+            g = lk
+        return [g], rest
+
+    def _fd_lookup(self, right: DRel, rk, attrs, keys: pa.Array, gmap: dict) -> None:
+        """``gmap[attr] = right[attr]`` at the right row of each key (unique right keys; the
+        row is found by one equality probe per (bucket, key), as ``_probe_ranges``)."""
+        import torch
+        G = len(keys)
+        if G == 0:
+            for a in attrs:
+                gmap[a.expr_id] = pa.array([], type=a.data_type)
+            return
+        if G > self.FD_MAX_KEYS:
+            raise RuntimeError(f"functional-dependency lookup of {G} keys")
+        rc = right.col(rk)
+        width = {NL.I8: 8, NL.I16: 16, NL.I32: 32, NL.I64: 64}[rc.hs_type]
+        vals = np.asarray(keys.cast(pa.int64()).to_numpy(zero_copy_only=False), dtype=np.int64)
+        if width == 64:
+            img = vals.view(np.uint64) ^ np.uint64(1 << 63)
+        else:
+            img = (vals + (1 << (width - 1))).astype(np.uint64)
+        nb = len(right.table.bucket_offsets_host) - 1
+        pb = torch.from_numpy(np.repeat(np.arange(nb, dtype=np.int32), G)).to(self.device)
+        pk = torch.from_numpy(np.tile(img, nb).view(np.int64)).to(self.device)
+        rstart, rlen, _ = K.probe_ranges(rc, right.table.bucket_offsets, pb, pk)
+        rs, rl = rstart.cpu().numpy(), rlen.cpu().numpy()
+        row = np.full(G, -1, dtype=np.int64)
+        hit = np.nonzero(rl > 0)[0]
+        row[hit % G] = rs[hit]
+        if (row < 0).any():
+            raise RuntimeError("functional-dependency lookup: a group key has no right row")
+        idx = torch.from_numpy(row).to(self.device)
+        cols = K.gather_columns([right.col(a) for a in attrs], idx)
+        for a, c in zip(attrs, cols):
+            arr = c.to_arrow()
+            if not arr.type.equals(a.data_type):
+                try:
+                    arr = arr.cast(a.data_type)
+                except (pa.ArrowInvalid, pa.ArrowNotImplementedError):
+                    pass
+            gmap[a.expr_id] = arr
 
     def _union_domain(self, rels, g: E.Attribute):
         """(lo, span, scale) of group column ``g`` over every part holding it and every rank.
@@ -2805,9 +2904,10 @@ class GpuBackend:
                                  nullable=c.nullable, desc=desc)
         return None
 
-    def _hash_table_out(self, final, fns, grouping, hk, host, A) -> pa.Table:
+    def _hash_table_out(self, final, fns, grouping, hk, host, A, extra=None) -> pa.Table:
         """Result table of a hash-mode aggregate from its host group arrays (vectorized
-        finalize; arithmetic over aggregates with pyarrow.compute)."""
+        finalize; arithmetic over aggregates with pyarrow.compute).  ``extra(gmap, host)`` adds
+        group columns not in the key (``_fd_grouping``)."""
         G = 0 if host is None else len(host["keys"])
         if G and hk is not None and not hk.need_star:
             host["cnts"][:, A - 1] = 1     # COUNT(*) not accumulated: every group has rows
@@ -2818,6 +2918,8 @@ class GpuBackend:
         else:
             for g in grouping:
                 gmap[g.expr_id] = pa.array([], type=g.data_type)
+        if extra is not None:
+            extra(gmap, host)
         vals = {}
         for i, fn in enumerate(fns):
             if G:

@@ -113,6 +113,9 @@ MJ_KEY16 = os.environ.get("HS_JIT_MJ_KEY16", "0") == "1"
 # run each row belongs to (gmask / gruns, 0.19 bytes per row) instead of its 4-byte key; the
 # tile's run keys are matched against the staged right span once per run, not once per row
 MJ_RUNS = os.environ.get("HS_JIT_MJ_RUNS", "1") == "1"
+# hash-mode GROUP BY over a run-keyed merge join whose group keys are left columns (the
+# functionally reduced TPC-H Q3 shape): the two-phase form with a hash walk (jit_runs)
+MJ_RUNS_HASH = os.environ.get("HS_JIT_MJ_RUNS_HASH", "1") == "1"
 MJ_RUNS_ITEMS = int(os.environ.get("HS_JIT_MJ_RUNS_ITEMS", "16"))
 MJ_RUNS_PREFETCH = os.environ.get("HS_JIT_MJ_RUNS_PREFETCH", "0") == "1"
 # cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
@@ -2084,6 +2087,16 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
         if two is not None:
             LAST_MJ_LAUNCHER[0] = two
             return two.launch(p)
+    if hk is not None and runs is not None and MJ_RUNS_HASH:
+        from . import jit_runs
+        two = jit_runs.lower(p, rstart, rlen, rbucket, roff, compacts, runs, nrows, cache_spans,
+                             hk=hk)
+        if two is not None:
+            LAST_MJ_PATH[0] = "runs_hash"
+            two.launch(p, htab=htab)
+            return None
+    if hk is not None:
+        LAST_MJ_PATH[0] = "hash"
     if hk is None and runs is None:
         compacts = _with_key16(p, compacts)
     NI = _mj_items(runs is not None)  # noqa: N806
@@ -2125,6 +2138,8 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
 
 # the launcher merge_join_agg built last (GpuBackend keeps it for the query's next submission)
 LAST_MJ_LAUNCHER: list = [None]
+# which form the last hash-mode merge join took ("runs_hash" / "hash")
+LAST_MJ_PATH: list = [None]
 
 
 class MergeJoinLauncher:

@@ -700,11 +700,12 @@ def packed_tail(layout, compacts):
     return w
 
 
-def sparse_shape(p: NL.JoinParams, compacts) -> tuple:
-    return ("run_bits_scan",) + scan_shape(p, compacts, 1, 64)[1:] + (pack_layout(p, compacts),)
+def sparse_shape(p: NL.JoinParams, compacts, hk=None) -> tuple:
+    return ("run_bits_scan",) + scan_shape(p, compacts, 1, 64)[1:] + \
+        (pack_layout(p, compacts),) + ((hk.shape(),) if hk is not None else ())
 
 
-def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
+def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None) -> J.Kernel:
     """Phase 2 for 1-bit tags, bit-parallel: the dense per-row scan spends ~20 VALU
     instructions per row (decode, predicate, run index by popcount, tag extract, compaction
     ballot + mbcnt), which bounds it below HBM speed.  Here a wavefront takes 4096-row tiles of
@@ -720,7 +721,12 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
        wavefront walks 4 entries per lane per pass: aggregate inputs loaded at those rows only
        and accumulated.
 
-    The next tile's run-form words are prefetched during the current tile."""
+    The next tile's run-form words are prefetched during the current tile.
+
+    With ``hk`` (an exec.hash_agg.KeyPlan over left columns) the walk groups by the hash key
+    instead: each pass's 64 list entries are consecutive passing rows, so a segmented shuffle
+    reduce folds a group's rows (one run = one left join key) before one table probe
+    (``jit._hash_accumulate``); kernel ``hs_jit_run_bits_hash``, no partials."""
     args = J.Args()
     for n, ct in (("rstart", "const long long*"), ("rlen", "const long long*"),
                   ("tile_prefix", "const long long*")):
@@ -738,8 +744,11 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
     grouped = _scan_grouped(p)
     assert not (grouped and p.group_col >= SPLIT)
     pslots = J._pred_slots(lpreds)
-    tail = list(dict.fromkeys(J._agg_slots(aggs) + ([p.group_col] if grouped else [])))
-    approx = J._sum_only_slots(lpreds, aggs, p.group_col if grouped else -1, cols)
+    assert not (grouped and hk is not None)
+    tail = list(dict.fromkeys(J._agg_slots(aggs) + ([p.group_col] if grouped else []) +
+                              (list(hk.slots) if hk is not None else [])))
+    approx = J._sum_only_slots(lpreds, aggs, p.group_col if grouped else -1, cols) - \
+        set(hk.slots if hk is not None else [])
     BLOCK = J.BLOCK  # noqa: N806
     WV = BLOCK // 64  # noqa: N806
     T = 4096  # noqa: N806 — rows per wavefront tile: 64 groups, one per lane
@@ -895,25 +904,31 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts) -> J.Kernel:
             b.append(f"{ind2}cok = cok && {J._rename(g.ok(p.group_col), tail, it)} && glc >= 0 && "
                      f"glc < {ng};")
             b.append(f"{ind2}const int {gvar} = cok ? (int)glc : 0;")
-        b += [J._rename(x, tail, it) for x in J._accumulate(g, aggs, grouped, "cok", gvar, ind2)]
+        if hk is not None:
+            b += [J._rename(x, tail, it) for x in J._hash_accumulate(g, aggs, hk, "cok", ind2)]
+        else:
+            b += [J._rename(x, tail, it)
+                  for x in J._accumulate(g, aggs, grouped, "cok", gvar, ind2)]
         b.append(f"{ind2}}}")
     b += ["    }", f"    {J._wave_sync()}", "    }", "  }"]
-    b += J._flush(aggs, grouped)
+    if hk is None:
+        b += J._flush(aggs, grouped)
+    name = "hs_jit_run_bits_scan" if hk is None else "hs_jit_run_bits_hash"
     src = (J._PRELUDE + args.struct_src() +
-           f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_run_bits_scan(Args a) '
+           f'extern "C" __global__ __launch_bounds__({BLOCK}) void {name}(Args a) '
            f'{{\n' + "\n".join(b) + "\n}\n")
     lds = (len(aggs) * p.num_groups * 32) if grouped else 0
-    return J.Kernel(src, "hs_jit_run_bits_scan", args, lds)
+    return J.Kernel(src, name, args, lds)
 
 
 class TwoPhaseLauncher:
     """Both phases lowered once (kernels, tiles, spans, per-tile run windows, the tag bitmap);
     ``launch(p)`` fills the literal slots and queues: bitmap clear, tags, scan, partials fold."""
     __slots__ = ("kt", "ks", "grid_t", "grid_s", "GA", "shmem", "vt", "vs", "compacts", "keep",
-                 "tags", "dev", "rows", "blocks")
+                 "tags", "dev", "rows", "blocks", "hk")
 
     def __init__(self, kt, ks, grid_t, grid_s, GA, shmem, vt, vs, compacts, keep, tags, dev,
-                 rows=None):
+                 rows=None, hk=None):
         self.kt, self.ks, self.grid_t, self.grid_s = kt, ks, grid_t, grid_s
         self.GA, self.shmem, self.vt, self.vs = GA, shmem, vt, vs
         self.compacts, self.keep, self.tags, self.dev = compacts, keep, tags, dev
@@ -922,10 +937,24 @@ class TwoPhaseLauncher:
         # literal vector -> (phase-1 block, phase-2 block template): a repeated parameter set
         # re-packs only the per-launch partials pointers
         self.blocks: dict = {}
+        # hash-mode phase 2 (a KeyPlan): groups go to a device hash table, no partials
+        self.hk = hk
 
-    def launch(self, p: NL.JoinParams, key=None):
+    def launch(self, p: NL.JoinParams, key=None, htab=None):
         import struct
         st = NL.stream_ptr()
+        if self.hk is not None:
+            preds = [(k_, p.preds[k_]) for k_ in range(p.npreds)]
+            vt = dict(self.vt)
+            J.fill_preds_aggs(vt, preds, [], self.compacts)
+            vs = dict(self.vs)
+            vs.update({"psum": 0, "pcnt": 0, "pmin": 0, "pmax": 0})
+            J.fill_preds_aggs(vs, preds, [p.aggs[i] for i in range(p.naggs)], self.compacts)
+            vs.update(htab.kernel_values())
+            vs.update(self.hk.values())
+            self.kt.launch(self.grid_t, vt, st, 0)
+            self.ks.launch(self.grid_s, vs, st, self.shmem)
+            return None
         hit = self.blocks.get(key) if key is not None else None
         if hit is None:
             preds = [(k_, p.preds[k_]) for k_ in range(p.npreds)]
@@ -957,10 +986,15 @@ class TwoPhaseLauncher:
 
 
 def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: int,
-          cache_spans: bool) -> Optional[TwoPhaseLauncher]:
-    """The two-phase launcher of a run-keyed merge join, or None when it does not apply."""
+          cache_spans: bool, hk=None) -> Optional[TwoPhaseLauncher]:
+    """The two-phase launcher of a run-keyed merge join, or None when it does not apply.
+    ``hk``: group by that hash key plan (left-side key columns only) through the bits scan's
+    hash mode (needs 1-bit tags and the direct phase 1)."""
     import torch
     if not applies(p) or runs is None:
+        return None
+    if hk is not None and (not SPARSE or not RT2 or tag_width(p) != 1 or _scan_grouped(p) or
+                           any(s >= SPLIT for s in hk.slots) or int(roff[-1].item()) <= 0):
         return None
     W = tag_width(p)
     NI = RS_ITEMS if RS_ITEMS and 64 % RS_ITEMS == 0 else J._mj_items(True)
@@ -972,7 +1006,8 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
     sparse = SPARSE and onebit
     rowmask = ROWMASK and onebit and not sparse
     if sparse:
-        ks = J.kernel_for(sparse_shape(p, compacts), lambda: gen_run_sparse_scan(p, compacts))
+        ks = J.kernel_for(sparse_shape(p, compacts, hk),
+                          lambda: gen_run_sparse_scan(p, compacts, hk))
     elif rowmask:
         ks = J.kernel_for(scan_rows_shape(p, compacts, NI),
                           lambda: gen_run_scan_rows(p, compacts, NI))
@@ -1048,7 +1083,7 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
         grid_s = max(1, SPARSE_GRID)
     return TwoPhaseLauncher(kt, ks, grid_t, grid_s, GA, GA * 32 if _scan_grouped(p) else 0,
                             vt, vs, compacts, (rstart, rlen, rbucket, roff, tp, spans, tr, runs),
-                            tags, dev, rows)
+                            tags, dev, rows, hk)
 
 
 def semi_runs_agg(p: NL.JoinParams, rstart, rlen, compacts, runs, nrows: int, words, lo: int,

@@ -119,6 +119,12 @@ class HyperspaceConf:
         return _b(conf.get(C.CODEGEN_ENABLED, C.CODEGEN_ENABLED_DEFAULT))
 
     @staticmethod
+    def fd_group_enabled(conf) -> bool:
+        """GROUP BY (join key, right columns) over a unique right key groups by the key and
+        looks the right columns up for the result groups (exec/gpu.py ``_fd_grouping``)."""
+        return _b(conf.get("spark.hyperspace.mi.fdGroup.enabled", "true"))
+
+    @staticmethod
     def hipgraph_enabled(conf) -> bool:
         return _b(conf.get(C.HIPGRAPH_ENABLED, C.HIPGRAPH_ENABLED_DEFAULT))
 

@@ -70,6 +70,12 @@ def main(out):
         if W == 1 and not (p.group_col >= 8 and p.num_groups > 1):
             ks.append(jit_runs.gen_run_scan_rows(p, comp, NI))
             ks.append(jit_runs.gen_run_sparse_scan(p, comp))
+            # hash walk grouped by the left key (the functionally reduced Q3 GROUP BY)
+            from hyperspace_amd.exec import hash_agg as H
+            ph, _, _ = q3_params(ng)
+            ph.group_col, ph.num_groups = -1, 1
+            hk = H.plan_keys([(0, None, keep[0][0], (4, 80_001))], (False, False), False)
+            ks.append(jit_runs.gen_run_sparse_scan(ph, comp, hk))
         for k in ks:
             path = os.path.join(out, f"{k.name}_g{ng}.hip")
             with open(path, "w") as f:

@@ -67,10 +67,20 @@ def test_tpch_q3_full_shape(tpch):  # noqa: F811
     q = j.groupBy("l_orderkey", "o_orderdate", "o_shippriority") \
         .agg(sum_(col("l_extendedprice") * (1 - col("l_discount"))).alias("revenue")) \
         .orderBy(col("revenue").desc(), col("o_orderdate")).limit(10)
+    from hyperspace_amd.exec import jit
     g, c, path = _both(s, q, sort=False)
     assert path == "native", s.backend().fallback_reason
     assert g.num_rows == 10
     _close(g, c)
+    # the (l_orderkey, o_orderdate, o_shippriority) groups reduce to l_orderkey's (o_orderkey is
+    # unique): the run-keyed two-phase join aggregates into the hash table and the top groups'
+    # orders columns are looked up afterwards
+    assert jit.LAST_MJ_PATH[0] == "runs_hash"
+    s.conf.set("spark.hyperspace.mi.fdGroup.enabled", "false")
+    g2, _, path = _both(s, q, sort=False)
+    s.conf.set("spark.hyperspace.mi.fdGroup.enabled", "true")
+    assert path == "native" and jit.LAST_MJ_PATH[0] == "hash"
+    _close(g2, c)
     # without the LIMIT: every group comes back (multi-column packed key, no top-k)
     q_all = j.groupBy("l_orderkey", "o_orderdate", "o_shippriority") \
         .agg(sum_(col("l_extendedprice") * (1 - col("l_discount"))).alias("revenue"),
