@@ -144,7 +144,9 @@ def main():
         wall = (time.perf_counter() - t) / reps * 1e3
         rep = TRACER.report()
         stages = {k: round(v["device_ms"] / max(v["calls"], 1), 4) for k, v in rep.items()}
-        return {"wall_ms": round(wall, 4), "stages": stages, "res": str(res)[:120]}
+        host = {k: round(v["host_ms"] / max(v["calls"], 1), 4) for k, v in rep.items()}
+        return {"wall_ms": round(wall, 4), "stages": stages, "host_stages": host,
+                "res": str(res)[:120]}
 
     if args.configs and args.configs.startswith("@"):   # @file: JSON list in a file
         with open(args.configs[1:]) as f:
