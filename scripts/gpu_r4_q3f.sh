@@ -7,8 +7,10 @@ REPO="$(pwd)"
 mkdir -p gpurun_out
 export HS_BENCH_DIR=/tmp/hs_bench
 TAG=${TAG:-q3f}
+CFG='[{}]'
+[ -n "$CONFIGS" ] && CFG="$CONFIGS"
 HS_PROFILE=1 timeout -k 10 600 python3 scripts/qk_sweep.py --sf 100 --reps 20 --only-q3-full \
-  --configs "${CONFIGS:-[{}]}" > gpurun_out/${TAG}.jsonl 2> gpurun_out/${TAG}.log || exit $?
+  --configs "$CFG" > gpurun_out/${TAG}.jsonl 2> gpurun_out/${TAG}.log || exit $?
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$REPO/gpurun_out/prof_${TAG}" \
   -o run -- python3 "$REPO/scripts/qk_sweep.py" --sf 100 --reps 20 --only-q3-full --configs '[{}]' \
