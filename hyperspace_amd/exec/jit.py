@@ -2089,11 +2089,21 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
             return two.launch(p)
     if hk is not None and runs is not None and MJ_RUNS_HASH:
         from . import jit_runs
-        two = jit_runs.lower(p, rstart, rlen, rbucket, roff, compacts, runs, nrows, cache_spans,
-                             hk=hk)
+        # over a resident table's cached full ranges the lowering (run ranges, tiles, kernels,
+        # column slots) is fixed: keep it, keyed by the ranges, the column pointers and the shape
+        ck = (id(rstart), id(runs), tuple(p.cols[s].data for s in range(NL.MAX_COLS)),
+              merge_join_shape(p, compacts, hk)) if cache_spans else None
+        two = _RUNS_HASH_LOWERED.get(ck) if ck is not None else None
+        if two is None:
+            two = jit_runs.lower(p, rstart, rlen, rbucket, roff, compacts, runs, nrows,
+                                 cache_spans, hk=hk)
+            if two is not None and ck is not None:
+                if len(_RUNS_HASH_LOWERED) >= 8:
+                    _RUNS_HASH_LOWERED.pop(next(iter(_RUNS_HASH_LOWERED)))
+                _RUNS_HASH_LOWERED[ck] = two
         if two is not None:
             LAST_MJ_PATH[0] = "runs_hash"
-            two.launch(p, htab=htab)
+            two.launch(p, htab=htab, hk=hk)
             return None
     if hk is not None:
         LAST_MJ_PATH[0] = "hash"
@@ -2140,6 +2150,9 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
 LAST_MJ_LAUNCHER: list = [None]
 # which form the last hash-mode merge join took ("runs_hash" / "hash")
 LAST_MJ_PATH: list = [None]
+# cached two-phase hash-mode lowerings (merge_join_agg); each holds its ranges / run form, so
+# the ids in its key stay valid while it is cached
+_RUNS_HASH_LOWERED: Dict[tuple, object] = {}
 
 
 class MergeJoinLauncher:

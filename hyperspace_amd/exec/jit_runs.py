@@ -940,7 +940,7 @@ class TwoPhaseLauncher:
         # hash-mode phase 2 (a KeyPlan): groups go to a device hash table, no partials
         self.hk = hk
 
-    def launch(self, p: NL.JoinParams, key=None, htab=None):
+    def launch(self, p: NL.JoinParams, key=None, htab=None, hk=None):
         import struct
         st = NL.stream_ptr()
         if self.hk is not None:
@@ -951,7 +951,7 @@ class TwoPhaseLauncher:
             vs.update({"psum": 0, "pcnt": 0, "pmin": 0, "pmax": 0})
             J.fill_preds_aggs(vs, preds, [p.aggs[i] for i in range(p.naggs)], self.compacts)
             vs.update(htab.kernel_values())
-            vs.update(self.hk.values())
+            vs.update((hk or self.hk).values())   # this query's key domain
             self.kt.launch(self.grid_t, vt, st, 0)
             self.ks.launch(self.grid_s, vs, st, self.shmem)
             return None
