@@ -113,7 +113,7 @@ def eval_expr(e: E.Expression, t: pa.Table):
         a, b = _operands(e, t)
         return _ARITH[type(e)](a, b)
     if isinstance(e, E.Remainder):
-        return _remainder(*_operands(e, t))
+        return _remainder(*_operands(e, t), t.num_rows, e.data_type)
     if isinstance(e, E.Divide):
         # Spark: a double division, NULL for a zero divisor
         a, b = _operands(e, t)
@@ -131,12 +131,13 @@ def eval_expr(e: E.Expression, t: pa.Table):
     raise NotImplementedError(f"cannot evaluate {type(e).__name__}")
 
 
-def _remainder(a, b):
+def _remainder(a, b, n: int, dtype=None):
     """Spark ``%``: truncated remainder (sign of the dividend), NULL for a zero divisor or a
-    NULL operand; ``fmod`` for floating-point operands; Long.MIN_VALUE % -1 = 0."""
+    NULL operand; ``fmod`` for floating-point operands; Long.MIN_VALUE % -1 = 0.  Either operand
+    may be a scalar (a literal dividend or divisor): both are broadcast to the ``n`` rows first.
+    The result takes the expression's type ``dtype``."""
     import numpy as np
-    a = a if isinstance(a, (pa.Array, pa.ChunkedArray)) else pa.array([a.as_py()] * 1)
-    n = max(len(a), len(b)) if isinstance(b, (pa.Array, pa.ChunkedArray)) else len(a)
+
     def arr(x):
         if isinstance(x, pa.Scalar):
             return pa.array([x.as_py()] * n, x.type)
@@ -155,7 +156,11 @@ def _remainder(a, b):
         safe = np.where(bad | (bv == -1), 1, bv)
         r = np.fmod(av, safe)          # C / JVM truncated remainder
         r = np.where(bv == -1, 0, r)
-    return pa.array(r, out_t, mask=bad)
+    out = pa.array(r, out_t, mask=bad)
+    if dtype is not None and out.type != dtype and (pa.types.is_integer(dtype) or
+                                                    pa.types.is_floating(dtype)):
+        out = pc.cast(out, dtype, safe=False)
+    return out
 
 
 def _float_to_int(v, dtype: pa.DataType):

@@ -2203,7 +2203,8 @@ class GpuBackend:
                 str(conf.get("spark.hyperspace.mi.semiJoinBitmap.enabled", "true")).lower() != "true":
             return None
         failed = self.__dict__.setdefault("_semi_failed", {})
-        if failed.get(id(node)) is node:
+        fkey = _semi_fail_key(node)
+        if failed.get(fkey) is node:
             return None
         need = set()
         for fn in fns:
@@ -2236,7 +2237,7 @@ class GpuBackend:
         if bm is None:
             if len(failed) > 256:
                 failed.clear()
-            failed[id(node)] = node
+            failed[fkey] = node
             return None
         words, lo, nbits = bm
         prel = self._rel(pinner)
@@ -2326,7 +2327,8 @@ class GpuBackend:
                 or str(conf.get("spark.hyperspace.mi.semiProject.enabled", "true")).lower() != "true":
             return None
         failed = self.__dict__.setdefault("_semi_failed", {})
-        if failed.get(id(node)) is node:
+        fkey = _semi_fail_key(node)
+        if failed.get(fkey) is node:
             return None
         need = set()
         for e in p.project_list:
@@ -2356,7 +2358,7 @@ class GpuBackend:
         if bm is None:
             if len(failed) > 256:
                 failed.clear()
-            failed[id(node)] = node
+            failed[fkey] = node
             return None
         words, lo, nbits = bm
         r = self._rel(pinner)
@@ -3090,6 +3092,21 @@ def _eval_scalar(e, agg_val, attr_val):
             return a * b
         return None if b == 0 else a / b
     raise Unsupported(f"result expression {type(e).__name__}")
+
+
+def _semi_fail_key(node) -> tuple:
+    """Memo key of a semi-join whose build keys repeated: the join node AND the literal values
+    under it - a plan-cache hit re-submits the same nodes with other literals, whose filtered
+    build side may well be unique."""
+    from ..plan.plan_cache import _iter_literals
+    lits: list = []
+    _iter_literals(node, lits, set())
+    try:
+        vals = tuple(x.value for x in lits)
+        hash(vals)
+    except TypeError:
+        vals = tuple(id(x) for x in lits)
+    return (id(node), vals)
 
 
 class _Stale(Exception):

@@ -17,6 +17,7 @@ class _PendingCombine:
     def __init__(self, packed):
         import torch
         self.result = None
+        self.error = None      # set on every entry of a flush that failed
         if packed.is_cuda:
             self.host = torch.empty(packed.numel(), dtype=torch.uint8, pin_memory=True)
             self.host.copy_(packed, non_blocking=True)
@@ -190,8 +191,10 @@ class DistContext:
             self._pending_combines.append(ent)
 
             def fetch_gloo():
-                if ent.result is None:
+                if ent.result is None and ent.error is None:
                     self._flush_combines()
+                if ent.error is not None:
+                    raise ent.error
                 return _reduce_ranks(ent.result.numpy().reshape(self.world, 4, GA * 8))
             return fetch_gloo
 
@@ -224,8 +227,11 @@ class DistContext:
         hdrs = [torch.empty_like(hdr) for _ in range(self.world)]
         dist.all_gather(hdrs, hdr)
         if any(not torch.equal(h, hdr) for h in hdrs):
-            raise RuntimeError("cross-rank combine mismatch: ranks have different pending "
+            err = RuntimeError("cross-rank combine mismatch: ranks have different pending "
                                f"aggregates {[h.tolist() for h in hdrs]}")
+            for e in pend:      # every coalesced entry reports the mismatch
+                e.error = err
+            raise err
         parts = [torch.empty_like(flat) for _ in range(self.world)]
         dist.all_gather(parts, flat)
         allr = torch.stack(parts)             # [world, total bytes]

@@ -269,7 +269,9 @@ def _subst(v, m: Dict[int, E.Literal], hot: set, memo: Dict[int, object]):
 def _deferred_literals(plan) -> set:
     """ids of the literals a backend evaluates after a query's submission returns: those in an
     aggregate's result expressions outside the aggregate functions' own inputs (the result
-    arithmetic over aggregates runs when the result is fetched)."""
+    arithmetic over aggregates runs when the result is fetched) and those in a global sort's
+    order expressions (GpuBackend orders the few result rows on the host when the result is
+    fetched, exec/gpu.py ``_collect_native``)."""
     from . import physical as X
     out: set = set()
 
@@ -284,12 +286,10 @@ def _deferred_literals(plan) -> set:
     for n in plan.collect(lambda x: isinstance(x, X.HashAggregateExec)):
         for e in n.aggregates:
             walk(e)
+    for n in plan.collect(lambda x: isinstance(x, X.SortExec) and x.global_sort):
+        for o in n.order:
+            walk(o.child)
     return out
-
-
-def _same(a: E.Literal, b: E.Literal) -> bool:
-    """Same value and type (so the cached plan's literal object can stay)."""
-    return type(a.value) is type(b.value) and a.value == b.value and a.dtype == b.dtype
 
 
 class _Entry:
@@ -367,13 +367,19 @@ class PlanCache:
         return hit, key, ctx
 
     def materialize(self, entry: "_Entry", ctx: _Ctx):
-        """The cached executed plan with the new query's literals (``ctx.lits``): only literals
-        whose value changed are substituted, along their own paths."""
-        m = {id(o): n for o, n in zip(entry.old_lits, ctx.lits) if o is not n and not _same(o, n)}
-        if not m:
-            return entry.plan
-        hot = set().union(*(entry.paths[k] for k in m))
-        return _subst(entry.plan, m, hot, {})
+        """The cached executed plan with the new query's literals (``ctx.lits``) substituted
+        along their paths.  Every literal position is replaced, changed value or not: the
+        entry's own literal objects are rewritten in place by concurrent bound submissions
+        (``_Entry.bind_literals``), so no materialized plan may share them.  Runs
+        under ``entry.lock`` so the entry's paths and literal list are read consistently."""
+        with entry.lock:
+            m = {}
+            for o, n in zip(entry.old_lits, ctx.lits):
+                m[id(o)] = n if n is not o else copy.copy(n)
+            if not m:
+                return entry.plan
+            hot = set().union(*(entry.paths[k] for k in m))
+            return _subst(entry.plan, m, hot, {})
 
     def lookup(self, session, logical) -> Tuple[Optional[object], Optional[tuple], _Ctx]:
         """(executed plan or None, key, fingerprint context) of ``logical``."""

@@ -1,0 +1,108 @@
+#!/bin/bash
+# One parameterized runner for every GPU-box job (gpurun):
+#
+#   gpurun -- 'TAG=x bash scripts/gpu.sh tests smoke bench prof'
+#
+# Steps run in the order given; each GPU step has its own time limit and the chain stops at the
+# first crash / abort / time limit (a plain pytest failure, rc 1, lets later steps run so the
+# record is complete).  Outputs land in gpurun_out/<TAG>_<step>.* (copy what is judged into
+# profiles/).  Knobs (env):
+#   TAG           output prefix (default run)
+#   PYTEST_ARGS   extra pytest args for `tests` (e.g. "-k semi")
+#   BENCH_ARGS    args for `bench` / `prof` / `hostprof` (default SF100, 100 / 40 steps)
+#   SF            scale factor for `pmc`, `configs`, `q3f`, `dist` (defaults 10 / 100 / 100 / 2)
+#   CONFIGS       benchmarks/configs.py configs for `configs` (default "sf10_filter q3_3way hybrid")
+#   PMC_REGEX     kernel-name regex for `pmc` (default hs_jit_)
+#   NPROC         ranks for `dist` (gloo, all on cuda:0; default 4)
+#   HS_PROFILE    1 = per-stage host/device tracer in the bench log
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+REPO="$(pwd)"
+mkdir -p gpurun_out
+export HS_BENCH_DIR=${HS_BENCH_DIR:-/tmp/hs_bench}
+TAG=${TAG:-run}
+O="$REPO/gpurun_out/$TAG"
+
+step_tests() {
+  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -v -m gpu --timeout 240 \
+    --timeout-method thread -x ${PYTEST_ARGS} > "${O}_tests.log" 2>&1
+  local rc=$?
+  echo "tests rc=$rc" >> "${O}_tests.log"
+  [ $rc -eq 0 ] || [ $rc -eq 1 ]
+}
+
+step_smoke() {
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
+    > "${O}_smoke.log" 2>&1
+}
+
+step_bench() {
+  timeout -k 10 ${BENCH_TIMEOUT:-700} python bench.py ${BENCH_ARGS:---sf 100 --steps 100 --warmup 5 --host-breakdown 100} \
+    > "${O}_bench.json" 2> "${O}_bench.log"
+}
+
+step_hostprof() {
+  HS_BENCH_PROFILE=1 timeout -k 10 600 python bench.py ${BENCH_ARGS:---sf 100 --steps 40 --warmup 3 --no-crosscheck} \
+    > "${O}_hostprof.json" 2> "${O}_hostprof.log"
+}
+
+step_prof() {
+  (cd /tmp && export TMPDIR=/tmp &&
+   timeout -k 10 700 rocprofv3 --kernel-trace --stats --output-format csv -d "${O}_prof" -o run \
+     -- python3 "$REPO/bench.py" ${BENCH_ARGS:---sf 100 --steps 40 --warmup 5 --no-crosscheck} \
+     > "${O}_prof.json" 2> "${O}_prof.log") || return $?
+  find "${O}_prof" -name "*kernel_stats.csv" -exec cp {} "${O}_kernel_stats.csv" \;
+}
+
+step_pmc() {
+  local sf=${SF:-10}
+  timeout -k 10 600 python3 scripts/qk_sweep.py --sf $sf --reps 3 --configs '[{}]' \
+    > "${O}_pmc_warm.jsonl" 2> "${O}_pmc_warm.log" || return $?
+  local i=0
+  for P in "FETCH_SIZE" "WRITE_SIZE" \
+           "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU" \
+           "SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU TCP_TOTAL_CACHE_ACCESSES_sum"; do
+    i=$((i+1))
+    (cd /tmp && export TMPDIR=/tmp &&
+     timeout -s KILL 240 rocprofv3 --pmc $P --kernel-include-regex "${PMC_REGEX:-hs_jit_}" --kernel-trace \
+       --output-format csv -d "${O}_pmc/p$i" -o pmc -- python3 "$REPO/scripts/qk_sweep.py" --sf $sf \
+       --reps 3 --configs '[{}]' > "${O}_pmc_run$i.jsonl" 2> "${O}_pmc_run$i.log") || return $?
+    find "${O}_pmc/p$i" -name "*counter_collection.csv" -exec cp {} "${O}_pmc/counters$i.csv" \;
+    rm -rf "${O}_pmc/p$i"
+  done
+  python3 scripts/pmc_summary.py "${O}_pmc"/counters*.csv > "${O}_pmc_summary.txt" 2>&1 || true
+}
+
+step_configs() {
+  for c in ${CONFIGS:-sf10_filter q3_3way hybrid}; do
+    rm -rf "$HS_BENCH_DIR"/indexes_* "$HS_BENCH_DIR"/cfg_* 2>/dev/null
+    timeout -k 10 ${CFG_TIMEOUT:-420} python benchmarks/configs.py --config $c --sf ${SF:-100} \
+      ${CFG_ARGS} >> "${O}_configs.jsonl" 2> "${O}_config_$c.log" || return $?
+  done
+}
+
+step_q3f() {
+  HS_PROFILE=1 timeout -k 10 600 python3 scripts/qk_sweep.py --sf ${SF:-100} --reps 20 --only-q3-full \
+    --configs "${Q3F_CONFIGS:-[{}]}" > "${O}_q3f.jsonl" 2> "${O}_q3f.log"
+}
+
+step_dist() {
+  local n=${NPROC:-4}
+  HS_BENCH_DIR=/tmp/hs_bench_dist HS_DIST_BACKEND=gloo timeout -k 10 700 \
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
+    --master-port 29517 bench.py --gpus $n --sf ${SF:-2} --steps ${DIST_STEPS:-20} --warmup 3 \
+    --buckets 16 ${DIST_ARGS} > "${O}_dist$n.json" 2> "${O}_dist$n.log"
+}
+
+step_cpubase() {
+  timeout -k 10 840 python scripts/cpu_baseline.py --sf ${SF:-100} --threads 16 --reps ${REPS:-3} \
+    --out "${O}_cpu_baseline.json" > "${O}_cpu.log" 2>&1
+}
+
+for s in "$@"; do
+  echo "[gpu.sh] step $s $(date +%T)"
+  "step_$s"
+  rc=$?
+  echo "[gpu.sh] step $s rc=$rc $(date +%T)"
+  [ $rc -eq 0 ] || exit $rc
+done

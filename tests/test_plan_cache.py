@@ -233,3 +233,59 @@ def test_result_literals_force_materialized_hits(data):
         q = df.filter(col("v") > 0.1 * i).agg((sum_(col("v")) * (2 + i)).alias("x"))
         q.collect()
     assert pc._lru and not any(e.inplace_ok for e in pc._lru.values())
+
+
+class _DeferredSortBackend(_BoundBackend):
+    """Like GpuBackend._collect_native: the part below a global sort runs at submission, the
+    ORDER BY / LIMIT of the (few) result rows runs when the result is fetched."""
+
+    def collect_async(self, plan):
+        import types
+        from hyperspace_amd.exec.arrow_eval import key
+        from hyperspace_amd.plan import physical as X
+        self.calls += 1
+        self.plans.append(plan)
+        limit = order = None
+        if isinstance(plan, X.CollectLimitExec):
+            limit, plan = plan.n, plan.child
+        if isinstance(plan, X.SortExec) and plan.global_sort:
+            order, plan = plan.order, plan.child
+        attrs = list(plan.output)
+        t = self.cpu.collect(plan)
+
+        def result():
+            out = t
+            if order is not None:
+                names = out.column_names
+                out = self.cpu._sort_table(out.rename_columns([key(a) for a in attrs]),
+                                           order).rename_columns(names)
+            return out if limit is None else out.slice(0, limit)
+        return types.SimpleNamespace(result=result, path="host", reason=None)
+
+
+def test_order_by_literals_force_materialized_hits(data):
+    """ORDER BY an expression with a literal over an aggregate, with a LIMIT: the
+    order keys are evaluated when the result is fetched, so the cached entry must not run bound
+    in place - every in-flight query sorts by its own literal."""
+    s, _, df, _ = data
+    cpu = s.backend()
+    fake = _DeferredSortBackend(cpu)
+    pc = plan_cache(s)
+    pc.clear()
+
+    def q(p):
+        return df.groupBy("k").agg(sum_(col("v")).alias("s")) \
+            .orderBy((col("s") - p) * (col("s") - p), col("k")).limit(5)
+    ps = [0.5, 3.0, 7.5, 1.25]
+    s.backend = lambda: fake
+    try:
+        futs = [q(p).collect_async() for p in ps]       # all in flight before any result
+        got = [[tuple(r) for r in f.result()] for f in futs]
+    finally:
+        del s.backend
+    assert pc._lru and not any(e.inplace_ok for e in pc._lru.values())
+    s.conf.set("spark.hyperspace.mi.planCache.enabled", "false")
+    want = [[tuple(r) for r in q(p).collect()] for p in ps]
+    s.conf.set("spark.hyperspace.mi.planCache.enabled", "true")
+    assert got == want
+    assert got[0] != got[2]

@@ -117,3 +117,23 @@ def test_float_to_int_casts_saturate_like_spark(tbl):
     _close(g, c)
     i32 = g.column("i32").to_pylist()
     assert 2147483647 in i32 and -2147483648 in i32
+
+
+def test_remainder_matches_host_oracle(tbl):
+    """Spark ``%`` on the device against the host oracle: column % literal,
+    literal % column, negative operands, zero divisors (NULL), LLONG_MIN % -1 and float fmod."""
+    s, df = tbl
+    f = df.filter(col("k") < 5000)
+    q = f.select(col("k"),
+                 (col("a") % 7).alias("a_mod_lit"),
+                 (col("a") % -7).alias("a_mod_neg"),
+                 (1000 % col("b")).alias("lit_mod_b"),        # b has zeros: NULLs
+                 (-1000 % col("b")).alias("neg_lit_mod_b"),
+                 (col("a") % col("b")).alias("a_mod_b"),
+                 ((col("a") * 0 - 9223372036854775807 - 1) % -1).alias("min_mod_m1"),
+                 (col("x") % 3.5).alias("fmod"),
+                 (7.25 % col("x")).alias("lit_fmod"))
+    g, c, path = _both(s, q)
+    assert path == "native", s.backend().fallback_reason
+    assert g.num_rows > 0
+    _close(g, c)
