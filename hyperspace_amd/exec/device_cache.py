@@ -58,6 +58,10 @@ class DeviceTableCache:
         self._lock = threading.Lock()
         self.hits = 0
         self.misses = 0
+        # bumped whenever a table leaves the cache: a prepared submission (exec/gpu.py
+        # _AggProgram) that saw its tables resident at epoch e still holds them while the epoch
+        # is e, without re-checking each table
+        self.epoch = 0
 
     def _key(self, files, columns, extra):
         fk = _files_key(files)
@@ -73,6 +77,7 @@ class DeviceTableCache:
                     break
             self._lru.pop(k)
             self._bytes -= self._size.pop(k, 0)
+            self.epoch += 1
 
     def get(self, files, columns, extra, loader) -> DeviceTable:
         key = self._key(files, columns, extra)
@@ -91,6 +96,8 @@ class DeviceTableCache:
         nb = t.resident_bytes()
         with self._lock:
             if self.budget > 0 and nb <= self.budget:
+                if key in self._lru:         # replaces a concurrently loaded copy
+                    self.epoch += 1
                 self._lru[key] = t
                 self._size[key] = nb
                 self._bytes += nb
@@ -127,6 +134,7 @@ class DeviceTableCache:
 
     def clear(self):
         with self._lock:
+            self.epoch += 1
             self._lru.clear()
             self._size.clear()
             self._bytes = 0

@@ -40,6 +40,7 @@ from .device_cache import (DeviceTableCache, _files_key, load_bucketed_index, lo
                            seeded_index)
 from .device_table import DeviceColumn, DeviceTable
 from .graphs import GraphCache, ScanAggGraph, range_bounds
+from .graphs import GraphPending as _GraphPending, _cbuf
 
 log = logging.getLogger(__name__)
 Unsupported = CP.Unsupported
@@ -129,6 +130,9 @@ class GpuBackend:
         self._unions: Dict[tuple, tuple] = {}     # string join keys: dictionary pair -> union
         self._groups_agreed = False
         self.graphs = GraphCache()
+        # plan object id -> (plan, _AggProgram): prepared re-submission of plan-cache hits
+        self._programs: Dict[int, tuple] = {}
+        self._prog_candidate = None
         from .hash_agg import TablePool
         self.htables = TablePool()
         # engine start: size the pinned staging pool once (pinning GBs is the slow part of a
@@ -189,15 +193,39 @@ class GpuBackend:
         several queries in flight overlaps host planning with device execution.  A shape the
         device cannot run falls back to the host oracle (recorded in ``path``)."""
         t0 = time.perf_counter()
+        hit = self._programs.get(id(plan))
+        if hit is not None and hit[0] is plan:
+            fut = hit[1].submit(self, plan, t0)
+            if fut is not None:
+                self.last_path, self.fallback_reason = "native", None
+                return fut
         TRACER.configure(self.session.conf)
+        self._prog_candidate = None
         try:
             with stage("query"):
                 finish = self._collect_native(plan)
             fut = QueryFuture(self, plan, finish, "native", None, t0)
+            self._register_program(plan)
         except Unsupported as e:
             fut = self._fallback(plan, e, t0)
         self.last_path, self.fallback_reason = fut.path, fut.reason
         return fut
+
+    def _register_program(self, plan) -> None:
+        """After a native submission that ran a prepared lowering (``_ScanPrep`` /
+        ``_JoinPrep``) for the plan's top aggregate, keep an ``_AggProgram`` for the plan
+        object: a plan-cache hit re-submits the same plan with new literals bound into it, and
+        the program replays the prepared kernels / hipGraph directly."""
+        cand = self._prog_candidate
+        self._prog_candidate = None
+        if cand is None or not HyperspaceConf.prepared_submit_enabled(self.session.conf):
+            return
+        m = self._match_agg(plan)
+        if m is None or m[0] is not cand[0]:
+            return
+        if len(self._programs) >= 256:
+            self._programs.clear()
+        self._programs[id(plan)] = (plan, _AggProgram(self, *cand))
 
     def _fallback(self, plan, e, t0) -> "QueryFuture":
         log.info("device executor fallback: %s", e)
@@ -1672,6 +1700,8 @@ class GpuBackend:
             except _Stale:
                 self._agg_preps.pop(id(final), None)
                 res = None
+            if res is not None:
+                self._prog_candidate = (final, fns, group, prep, self.cache.epoch)
         if res is not None:
             pass
         elif isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner":
@@ -1694,6 +1724,12 @@ class GpuBackend:
             self._last_graph_prep = None
             res = self._scan_agg(r, fns, group)
             self._agg_prep_put(final, r)
+        return self._agg_finish(final, fns, group, res)
+
+    def _agg_finish(self, final, fns, group, res):
+        """``finish() -> pa.Table`` of a queued fused aggregate ``res`` = (sums, counts, mins,
+        maxs, G, gbase, gdict, gtype): the cross-rank combine (sharded placement) is queued
+        now, stream-ordered behind the kernels; the result is read when ``finish`` runs."""
         sums, cnts, mins, maxs, G, gbase, gdict, gtype = res
         d = self._dist()
         A = len(fns) + 1  # + implicit count(*)
@@ -2088,7 +2124,8 @@ class GpuBackend:
             jit.fill_preds_aggs(values, [(i, p.preds[i]) for i in range(p.npreds)],
                                 [p.aggs[i] for i in range(p.naggs)], compacts)
             # (the per-query predicate buffers the block points to stay referenced with it)
-            hit = (range_bounds(lo, lo_incl, hi, hi_incl), k.args.pack(values), list(keep))
+            hit = (range_bounds(lo, lo_incl, hi, hi_incl), _cbuf(k.args.pack(values)),
+                   list(keep))
             if lkey is not None:
                 if len(prep.packed) >= 1024:
                     prep.packed.clear()
@@ -2111,18 +2148,21 @@ class GpuBackend:
         # buffers it reads are marked in use by that stream, so memory the caller frees
         # meanwhile is not handed out again before the replay is done.
         side.wait_stream(torch.cuda.current_stream())
-        for c in list((descs or {}).values()) + [kc]:
-            for x in (c.data, c.valid):
-                if x is not None:
+        if prep.marked is not side:
+            for c in list((descs or {}).values()) + [kc]:
+                for x in (c.data, c.valid):
+                    if x is not None:
+                        _use_on(x, side)
+            # the generated kernel reads the compact codes (jit._fill_common) rather than
+            # c.data: those buffers are in use by the side stream too (a device-cache eviction
+            # between this launch and its fetch must not hand their memory to query-stream
+            # allocations).  One record per buffer and stream covers every later replay.
+            for enc in (compacts or {}).values():
+                for x in _compact_buffers(enc):
                     _use_on(x, side)
-        # the generated kernel reads the compact codes (jit._fill_common) rather than c.data:
-        # those buffers are in use by the side stream too (a device-cache eviction between
-        # this launch and its fetch must not hand their memory to query-stream allocations)
-        for enc in (compacts or {}).values():
-            for x in _compact_buffers(enc):
+            for x in g.buffers():
                 _use_on(x, side)
-        for x in g.buffers():
-            _use_on(x, side)
+            prep.marked = side
         for x in keep:      # per-query predicate buffers (IN sets, key bitmaps)
             _use_on(x, side)
         with torch.cuda.stream(side):
@@ -3114,12 +3154,13 @@ class _Stale(Exception):
 
 
 class _GraphPrep:
-    __slots__ = ("key", "g", "k", "compacts", "values", "GA", "packed")
+    __slots__ = ("key", "g", "k", "compacts", "values", "GA", "packed", "marked")
 
     def __init__(self, key, g, k, compacts, values, GA):
         self.key, self.g, self.k, self.compacts, self.values, self.GA = \
             key, g, k, compacts, values, GA
         self.packed: Dict[tuple, tuple] = {}     # literal vector -> (range bounds, args block)
+        self.marked = None    # the side stream every persistent buffer was marked in use by
 
 
 def bucket_chunks(per_bucket, budget: int) -> List[tuple]:
@@ -3179,6 +3220,34 @@ class _ScanPrep:
     def run(self, be, fns, group):
         return be._scan_agg(self.r, fns, group, self)
 
+    def fast(self, be, fns, group):
+        """``run`` for a literal vector whose lowering and graph block are cached, with no
+        re-validation beyond the graph's (``_AggProgram`` checked residency); None otherwise."""
+        gp = self.graph
+        if gp is None:
+            return None
+        lkey = self.literal_key()
+        low = self.lowered.get(lkey) if lkey is not None else None
+        hit = gp.packed.get(lkey) if low is not None else None
+        if hit is None or low[1].always_false or be.graphs.peek(gp.key) is not gp.g:
+            return None
+        g = gp.g
+        side = gp.marked
+        if side is None and (g.on_side or HyperspaceConf.side_stream_scans(be.session.conf)):
+            return None     # the full path moves warm replays to the side stream first
+        agreed, G, gbase, gdict, gtype = self.gs
+        be._groups_agreed = agreed is True
+        if side is None:
+            handle = g.launch(hit[0], hit[1])
+        else:
+            import torch
+            side.wait_stream(torch.cuda.current_stream())
+            for x in hit[2]:
+                _use_on(x, side)
+            with torch.cuda.stream(side):
+                handle = g.launch(hit[0], hit[1])
+        return (_GraphPending(g, handle), None, None, None, G, gbase, gdict, gtype)
+
 
 class _JoinPrep:
     """Literal-independent lowering of a co-located merge-join aggregate: the two resident
@@ -3237,11 +3306,58 @@ class _JoinPrep:
                     jp.group_col = col_info(group).slot if G > 1 else -1
                     jp.num_groups, jp.group_base = G, gbase
                 if isinstance(self.launcher, jit_runs.TwoPhaseLauncher):
-                    out = self.launcher.launch(jp, lkey)
+                    out = self.launcher.launch(
+                        jp, lkey, graph=HyperspaceConf.join_graph_enabled(be.session.conf))
+                    if isinstance(out, _GraphPending):
+                        out = (out, None, None, None)
                 else:
                     out = self.launcher.launch(jp)
         be._groups_agreed = self.agreed
         return (*out, *self.gtail)
+
+    def fast(self, be, fns, group):
+        """``run`` replaying the captured two-phase pipeline for a cached literal vector; None
+        when that does not apply (the full ``run`` / planning path runs instead)."""
+        launcher = self.launcher
+        if not isinstance(launcher, jit_runs.TwoPhaseLauncher) or launcher.graph is None:
+            return None
+        lkey = self.literal_key()
+        low = self.lowered.get(lkey) if lkey is not None else None
+        if low is None or lkey not in launcher.gblocks:
+            return None
+        jp, keep, specs = low
+        if keep[0].always_false or keep[1].always_false:
+            return None
+        out = launcher.launch(jp, lkey, graph=True)
+        be._groups_agreed = self.agreed
+        return (out, None, None, None, *self.gtail)
+
+
+class _AggProgram:
+    """Prepared re-submission of a fused aggregate plan (GpuBackend._register_program): a
+    plan-cache hit binds its literals into the cached plan's nodes and the program replays the
+    prepared lowering of its literal vector - a captured hipGraph (scan: ``ScanAggGraph``;
+    two-phase merge join: ``TwoPhaseGraph``) - and queues the cross-rank combine, skipping the
+    executor's plan walk and every per-query lowering check.  Valid while the device-table
+    cache has evicted nothing since it was made (``epoch``); any miss (new literal vector,
+    eviction, graph dropped) returns None and the full path runs (and re-registers)."""
+    __slots__ = ("final", "fns", "group", "prep", "epoch", "n")
+
+    def __init__(self, be, final, fns, group, prep, epoch):
+        self.final, self.fns, self.group, self.prep, self.epoch = final, fns, group, prep, epoch
+        self.n = 0
+
+    def submit(self, be, plan, t0):
+        if be.cache.epoch != self.epoch:
+            return None
+        self.n += 1
+        if self.n % 64 == 0 and not all(be._holds(t) for t in self.prep.tables()):
+            return None      # (also keeps the tables recent in the cache's LRU)
+        res = self.prep.fast(be, self.fns, self.group)
+        if res is None:
+            return None
+        finish = be._agg_finish(self.final, self.fns, self.group, res)
+        return QueryFuture(be, plan, finish, "native", None, t0)
 
 
 def _strip_exchange(p):
@@ -3288,16 +3404,6 @@ def _compact_buffers(enc) -> list:
             if x is not None and hasattr(x, "record_stream") and all(x is not y for y in out):
                 out.append(x)
     return out
-
-
-class _GraphPending:
-    """A replayed scan pipeline whose result block is still in flight (exec/graphs.py)."""
-
-    def __init__(self, graph, handle):
-        self.graph, self.handle = graph, handle
-
-    def result(self):
-        return self.graph.result(self.handle)
 
 
 class QueryFuture:

@@ -58,16 +58,23 @@ class _Pinned:
 class _Slot:
     """One in-flight instance of a captured pipeline: its own pinned parameter and result
     blocks (the graph's H2D reads the first and its D2H writes the second when the graph
-    EXECUTES, so a query queued behind another must not share them), its own graph, and the
-    event that marks its result ready."""
+    EXECUTES, so a query queued behind another must not share them), its own executable graph
+    (whose kernel arguments are rewritten per launch), and the event that marks its result
+    ready."""
 
     def __init__(self, params_bytes: int, out_bytes: int):
         import torch
-        self.h_params = _Pinned(params_bytes)
+        self.h_params = _Pinned(max(params_bytes, 8))
         self.h_out = _Pinned(out_bytes)
-        self.graph = None
+        self.graph = None          # native handle (csrc/runtime/hs_graph.cpp)
         self.event = torch.cuda.Event()
+        self.launched = False
         self.current = None   # _Launch whose result the slot's h_out holds / will hold
+
+    def __del__(self):
+        if getattr(self, "graph", None):
+            jit.runtime().hs_graph_destroy(self.graph)
+            self.graph = None
 
 
 class _Launch:
@@ -81,32 +88,29 @@ class _Launch:
         self.value = None
 
 
-class ScanAggGraph:
+def _rt_check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what}: {jit.runtime().hs_graph_last_error().decode()}")
+
+
+class _RingGraph:
+    """A captured pipeline with ``RING`` in-flight instances (one pinned parameter block, one
+    pinned result block and one executable graph per slot; device intermediates shared, since
+    replays on one stream execute in order).  Subclasses define ``kernels`` (the generated
+    kernels whose by-value argument blocks change per query), ``_enqueue(slot, stream, blocks)``
+    (the work one query queues, eager or under capture), ``GA`` and ``out`` (the device result
+    block, ``K.agg_outputs``).
+
+    A replay rewrites the captured kernel nodes' argument blocks (``hs_graph_set_args``) and
+    launches the executable graph: the kernels keep their by-value kernarg struct (a struct read
+    from device memory makes every column load a flat load, ~2x slower on gfx950 -
+    ``profiles/graph_byptr_r5.txt``)."""
     # in-flight instances per captured shape: a pipelined query stream (exec/gpu.py
     # collect_async) keeps a few replays of the same shape queued at once
     RING = 4
 
-    def __init__(self, kernel: jit.Kernel, kd: NL.ColDesc, bucket_off, nb: int, grid: int,
-                 GA: int, shmem: int, device, vec: int = 0):
-        import torch
-        from ..ops import kernels as K
-        self.kernel = kernel.by_pointer()
-        self.kd = kd
-        self.bucket_off = bucket_off
-        self.nb, self.grid, self.GA, self.shmem = nb, grid, GA, shmem
-        self.vec = vec   # rows per thread of a vectorized kernel (tiles over aligned ranges)
-        self.tile = jit.BLOCK * (vec or jit.SCAN_ITEMS)
-        self.args_size = 8 * len(kernel.args.slots)
-        # device intermediates are shared: replays on one stream execute in order
-        self.d_params = torch.empty(PARAM_HEAD + self.args_size, dtype=torch.uint8, device=device)
-        self.rstart = torch.empty(nb, dtype=torch.int64, device=device)
-        self.rlen = torch.empty(nb, dtype=torch.int64, device=device)
-        self.rbk = torch.empty(nb, dtype=torch.int32, device=device)
-        self.tp = torch.empty(nb + 1, dtype=torch.int64, device=device)
-        self.parts = jit._partials(grid, GA, device)
-        self.out = K.agg_outputs(GA, device)
-        self.slots = [_Slot(PARAM_HEAD + self.args_size, self.out[0].hs_buf.numel())
-                      for _ in range(self.RING)]
+    def _init_ring(self, params_bytes: int) -> None:
+        self.slots = [_Slot(params_bytes, self.out[0].hs_buf.numel()) for _ in range(self.RING)]
         self._next = 0
         self._warm = False
         self.replays = 0
@@ -117,80 +121,55 @@ class ScanAggGraph:
     def graph(self):
         return self.slots[0].graph
 
-    def _enqueue(self, slot: _Slot, stream: int) -> None:
-        L = jit.runtime()
-        K = NL.lib()
-        NL.check(L.hs_memcpy_async(self.d_params.data_ptr(), slot.h_params.ptr,
-                                   slot.h_params.nbytes, 1, stream), "param H2D")
-        NL.check(K.hs_range_search_dev(C.byref(self.kd), NL.ptr(self.bucket_off), None, self.nb,
-                                       self.d_params.data_ptr(), NL.ptr(self.rstart),
-                                       NL.ptr(self.rlen), NL.ptr(self.rbk), stream),
-                 "hs_range_search_dev")
-        if self.vec:
-            NL.check(K.hs_ranges_to_tiles_aligned(NL.ptr(self.rstart), NL.ptr(self.rlen), self.nb,
-                                                  self.tile, self.vec, NL.ptr(self.tp), stream),
-                     "hs_ranges_to_tiles_aligned")
-        else:
-            NL.check(K.hs_ranges_to_tiles(NL.ptr(self.rlen), self.nb, self.tile,
-                                          NL.ptr(self.tp), stream), "hs_ranges_to_tiles")
-        self.kernel.launch_ptr(self.grid, self.d_params.data_ptr() + PARAM_HEAD, stream,
-                               self.shmem)
-        p = self.parts
-        o = self.out
-        NL.check(K.hs_agg_final(NL.ptr(p[0]), NL.ptr(p[1]), NL.ptr(p[2]), NL.ptr(p[3]),
-                                self.grid, self.GA, NL.ptr(o[0]), NL.ptr(o[1]), NL.ptr(o[2]),
-                                NL.ptr(o[3]), stream), "hs_agg_final")
-        NL.check(L.hs_memcpy_async(slot.h_out.ptr, o[0].hs_buf.data_ptr(), slot.h_out.nbytes, 2,
-                                   stream), "result D2H")
+    def _capture(self, slot: _Slot, blocks, cur) -> None:
+        import torch
+        R = jit.runtime()
+        side = torch.cuda.Stream()
+        side.wait_stream(cur)
+        _rt_check(R.hs_graph_capture_begin(side.cuda_stream), "hs_graph_capture_begin")
+        try:
+            self._enqueue(slot, side.cuda_stream, blocks)
+        finally:
+            fns = [k.function() for k in self.kernels]
+            arr = (C.c_void_p * len(fns))(*fns)
+            h = R.hs_graph_capture_end(side.cuda_stream, arr, len(fns))
+        if not h:
+            raise RuntimeError(f"graph capture: {R.hs_graph_last_error().decode()}")
+        cur.wait_stream(side)
+        slot.graph = h
 
-    def buffers(self) -> list:
-        """Device intermediates a replay reads and writes."""
-        return [self.d_params, self.rstart, self.rlen, self.rbk, self.tp, self.bucket_off,
-                *self.parts, self.out[0].hs_buf]
-
-    def values_template(self) -> dict:
-        return {"rstart": self.rstart.data_ptr(), "rlen": self.rlen.data_ptr(),
-                "tile_prefix": self.tp.data_ptr(), "R": self.nb,
-                "psum": self.parts[0].data_ptr(), "pcnt": self.parts[1].data_ptr(),
-                "pmin": self.parts[2].data_ptr(), "pmax": self.parts[3].data_ptr()}
-
-    def launch(self, bounds: Tuple[int, int, int, int, int, int], args_block: bytes) -> _Launch:
-        """Queue one query on the current stream; ``result(handle)`` waits for it.  A slot
-        still holding an unread earlier result is drained first: wait for it and keep its
-        result on the earlier handle (back-pressure, no lost results)."""
+    def _launch_slot(self, fill, blocks) -> _Launch:
+        """Queue one query on the current stream: ``fill(host_params_view)`` writes its pinned
+        parameter block, ``blocks`` are the packed argument blocks of ``kernels``.  A slot still
+        holding an unread earlier result is drained first (wait for it and keep its result on
+        the earlier handle: back-pressure, no lost results); a slot's graph gets new kernel
+        arguments only once its previous replay has finished."""
         import torch
         slot = self.slots[self._next]
         self._next = (self._next + 1) % len(self.slots)
         prev = slot.current
         if prev is not None and prev.value is None:
             prev.value = self._read(slot)
-        hp = slot.h_params.view()
-        hp[:48] = np.frombuffer(struct.pack("<6q", *bounds), dtype=np.uint8)
-        hp[PARAM_HEAD:PARAM_HEAD + len(args_block)] = np.frombuffer(args_block, dtype=np.uint8)
+        elif slot.launched:
+            slot.event.synchronize()
+        fill(slot.h_params.view())
         cur = torch.cuda.current_stream()
-        eager = not self._warm
-        if eager:
-            self._enqueue(slot, cur.cuda_stream)   # first run of the shape: eager (loads the module)
+        st = cur.cuda_stream
+        if not self._warm:
+            self._enqueue(slot, st, blocks)   # first run of the shape: eager (loads the modules)
             self._warm = True
-        if slot.graph is None:
-            g = torch.cuda.CUDAGraph()
-            side = torch.cuda.Stream()
-            side.wait_stream(cur)
-            # capture_begin/end directly: the torch.cuda.graph context manager synchronizes,
-            # runs gc.collect() and empties the caching allocator first (~100 ms, and every
-            # later allocation goes back to hipMalloc); the captured work allocates nothing
-            with torch.cuda.stream(side):
-                g.capture_begin()
-                try:
-                    self._enqueue(slot, side.cuda_stream)
-                finally:
-                    g.capture_end()
-            cur.wait_stream(side)
-            slot.graph = g
-        if not eager:
-            slot.graph.replay()
+        elif slot.graph is None:
+            self._capture(slot, blocks, cur)
+            _rt_check(jit.runtime().hs_graph_launch(slot.graph, st), "hs_graph_launch")
+            self.replays += 1
+        else:
+            R = jit.runtime()
+            for i, b in enumerate(blocks):
+                _rt_check(R.hs_graph_set_args(slot.graph, i, b, len(b)), "hs_graph_set_args")
+            _rt_check(R.hs_graph_launch(slot.graph, st), "hs_graph_launch")
             self.replays += 1
         slot.event.record(cur)
+        slot.launched = True
         h = _Launch(slot)
         slot.current = h
         return h
@@ -208,9 +187,139 @@ class ScanAggGraph:
         return (h[0:n].view(np.float64).copy(), h[n:2 * n].view(np.int64).copy(),
                 h[2 * n:3 * n].view(np.float64).copy(), h[3 * n:4 * n].view(np.float64).copy())
 
-    def run(self, bounds: Tuple[int, int, int, int, int, int], args_block: bytes):
+    def _final_and_d2h(self, slot: _Slot, stream: int, grid: int) -> None:
+        L = jit.runtime()
+        K = NL.lib()
+        p = self.parts
+        o = self.out
+        NL.check(K.hs_agg_final(NL.ptr(p[0]), NL.ptr(p[1]), NL.ptr(p[2]), NL.ptr(p[3]),
+                                grid, self.GA, NL.ptr(o[0]), NL.ptr(o[1]), NL.ptr(o[2]),
+                                NL.ptr(o[3]), stream), "hs_agg_final")
+        NL.check(L.hs_memcpy_async(slot.h_out.ptr, o[0].hs_buf.data_ptr(), slot.h_out.nbytes, 2,
+                                   stream), "result D2H")
+
+
+def _cbuf(block) -> "C.Array":
+    """A ctypes copy of a packed argument block (kept with the cached block, so a replay passes
+    its address without a per-query copy)."""
+    b = bytes(block)
+    return C.create_string_buffer(b, len(b))
+
+
+class ScanAggGraph(_RingGraph):
+    def __init__(self, kernel: jit.Kernel, kd: NL.ColDesc, bucket_off, nb: int, grid: int,
+                 GA: int, shmem: int, device, vec: int = 0):
+        import torch
+        from ..ops import kernels as K
+        self.kernel = kernel
+        self.kernels = (kernel,)
+        self.kd = kd
+        self.bucket_off = bucket_off
+        self.nb, self.grid, self.GA, self.shmem = nb, grid, GA, shmem
+        self.vec = vec   # rows per thread of a vectorized kernel (tiles over aligned ranges)
+        self.tile = jit.BLOCK * (vec or jit.SCAN_ITEMS)
+        # device intermediates are shared: replays on one stream execute in order
+        self.d_params = torch.empty(PARAM_HEAD, dtype=torch.uint8, device=device)
+        self.rstart = torch.empty(nb, dtype=torch.int64, device=device)
+        self.rlen = torch.empty(nb, dtype=torch.int64, device=device)
+        self.rbk = torch.empty(nb, dtype=torch.int32, device=device)
+        self.tp = torch.empty(nb + 1, dtype=torch.int64, device=device)
+        self.parts = jit._partials(grid, GA, device)
+        self.out = K.agg_outputs(GA, device)
+        self._init_ring(PARAM_HEAD)
+
+    def _enqueue(self, slot: _Slot, stream: int, blocks) -> None:
+        L = jit.runtime()
+        K = NL.lib()
+        NL.check(L.hs_memcpy_async(self.d_params.data_ptr(), slot.h_params.ptr,
+                                   slot.h_params.nbytes, 1, stream), "param H2D")
+        NL.check(K.hs_range_search_dev(C.byref(self.kd), NL.ptr(self.bucket_off), None, self.nb,
+                                       self.d_params.data_ptr(), NL.ptr(self.rstart),
+                                       NL.ptr(self.rlen), NL.ptr(self.rbk), stream),
+                 "hs_range_search_dev")
+        if self.vec:
+            NL.check(K.hs_ranges_to_tiles_aligned(NL.ptr(self.rstart), NL.ptr(self.rlen), self.nb,
+                                                  self.tile, self.vec, NL.ptr(self.tp), stream),
+                     "hs_ranges_to_tiles_aligned")
+        else:
+            NL.check(K.hs_ranges_to_tiles(NL.ptr(self.rlen), self.nb, self.tile,
+                                          NL.ptr(self.tp), stream), "hs_ranges_to_tiles")
+        self.kernel.launch_packed(self.grid, blocks[0], stream, self.shmem)
+        self._final_and_d2h(slot, stream, self.grid)
+
+    def buffers(self) -> list:
+        """Device intermediates a replay reads and writes."""
+        return [self.d_params, self.rstart, self.rlen, self.rbk, self.tp, self.bucket_off,
+                *self.parts, self.out[0].hs_buf]
+
+    def values_template(self) -> dict:
+        return {"rstart": self.rstart.data_ptr(), "rlen": self.rlen.data_ptr(),
+                "tile_prefix": self.tp.data_ptr(), "R": self.nb,
+                "psum": self.parts[0].data_ptr(), "pcnt": self.parts[1].data_ptr(),
+                "pmin": self.parts[2].data_ptr(), "pmax": self.parts[3].data_ptr()}
+
+    def launch(self, bounds: Tuple[int, int, int, int, int, int], args_block) -> _Launch:
+        """Queue one query on the current stream; ``result(handle)`` waits for it.
+        ``args_block``: the scan kernel's packed arguments (bytes or a ``_cbuf``)."""
+        head = np.frombuffer(struct.pack("<6q", *bounds), dtype=np.uint8)
+
+        def fill(hp):
+            hp[:48] = head
+        if not isinstance(args_block, C.Array):
+            args_block = _cbuf(args_block)
+        return self._launch_slot(fill, (args_block,))
+
+    def run(self, bounds: Tuple[int, int, int, int, int, int], args_block):
         """(sum, count, min, max) numpy arrays for one query (launch + wait)."""
         return self.result(self.launch(bounds, args_block))
+
+
+def _nofill(hp) -> None:
+    pass
+
+
+class TwoPhaseGraph(_RingGraph):
+    """The run-keyed two-phase merge-join aggregate (exec/jit_runs.py) captured: phase 1 (run
+    tags), phase 2 (bits scan into the graph's partials), the deterministic final reduction and
+    the result D2H - one replay per query instead of four launches and their host-side argument
+    packing.  The tag bitmap and the run tables are the launcher's (fixed per lowering)."""
+
+    def __init__(self, kt: jit.Kernel, ks: jit.Kernel, grid_t: int, grid_s: int, GA: int,
+                 shmem: int, device):
+        from ..ops import kernels as K
+        self.kt, self.ks = kt, ks
+        self.kernels = (kt, ks)
+        self.grid_t, self.grid_s, self.GA, self.shmem = grid_t, grid_s, GA, shmem
+        self.parts = jit._partials(grid_s, GA, device)
+        self.out = K.agg_outputs(GA, device)
+        self._init_ring(0)
+
+    def _enqueue(self, slot: _Slot, stream: int, blocks) -> None:
+        self.kt.launch_packed(self.grid_t, blocks[0], stream, 0)
+        self.ks.launch_packed(self.grid_s, blocks[1], stream, self.shmem)
+        self._final_and_d2h(slot, stream, self.grid_s)
+
+    def buffers(self) -> list:
+        return [*self.parts, self.out[0].hs_buf]
+
+    def partial_ptrs(self) -> dict:
+        return {"psum": self.parts[0].data_ptr(), "pcnt": self.parts[1].data_ptr(),
+                "pmin": self.parts[2].data_ptr(), "pmax": self.parts[3].data_ptr()}
+
+    def launch(self, block_t, block_s) -> _Launch:
+        """``block_t`` / ``block_s``: ``_cbuf`` argument blocks of the two phases."""
+        return self._launch_slot(_nofill, (block_t, block_s))
+
+
+class GraphPending:
+    """A replayed pipeline whose result block is still in flight."""
+    __slots__ = ("graph", "handle")
+
+    def __init__(self, graph, handle):
+        self.graph, self.handle = graph, handle
+
+    def result(self):
+        return self.graph.result(self.handle)
 
 
 class GraphCache:

@@ -165,6 +165,18 @@ def runtime():
                                               C.c_void_p]
                 L.hs_stream_sync.restype = C.c_int
                 L.hs_stream_sync.argtypes = [C.c_void_p]
+                # captured pipelines with per-replay kernel arguments (csrc/runtime/hs_graph.cpp)
+                L.hs_graph_capture_begin.restype = C.c_int
+                L.hs_graph_capture_begin.argtypes = [C.c_void_p]
+                L.hs_graph_capture_end.restype = C.c_void_p
+                L.hs_graph_capture_end.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.c_int]
+                L.hs_graph_set_args.restype = C.c_int
+                L.hs_graph_set_args.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]
+                L.hs_graph_launch.restype = C.c_int
+                L.hs_graph_launch.argtypes = [C.c_void_p, C.c_void_p]
+                L.hs_graph_destroy.restype = None
+                L.hs_graph_destroy.argtypes = [C.c_void_p]
+                L.hs_graph_last_error.restype = C.c_char_p
                 _rt = L
     return _rt
 
@@ -252,25 +264,6 @@ class Kernel:
         self.block = block
         self._fn = None
 
-    def by_pointer(self) -> "Kernel":
-        """The same kernel taking ``const Args*`` (argument block in device memory): a captured
-        hipGraph replays it with new literals after one H2D of the block."""
-        sig = f"void {self.name}(Args a) {{"
-        assert sig in self.src
-        # copy the block once: a reference would make every field access a memory load the
-        # compiler cannot hoist across the kernel's own stores
-        src = self.src.replace(sig, f"void {self.name}(const Args* __restrict__ ap) {{\n"
-                                    f"  const Args a = *ap;")
-        return Kernel(src, self.name, self.args, self.lds_bytes, self.block)
-
-    def launch_ptr(self, grid: int, dev_args: int, stream_ptr: int, shmem: int = 0) -> None:
-        buf = struct.pack("<q", dev_args)
-        cbuf = C.create_string_buffer(buf, len(buf))
-        rc = runtime().hs_jit_launch(self.function(), grid, self.block, shmem or self.lds_bytes,
-                                     stream_ptr, cbuf, len(buf))
-        if rc != 0:
-            raise RuntimeError(f"JIT launch failed: {runtime().hs_jit_last_error().decode()}")
-
     def function(self):
         if self._fn is None:
             L = runtime()
@@ -294,8 +287,9 @@ class Kernel:
         return self._fn
 
     def launch_packed(self, grid: int, buf, stream_ptr: int, shmem: int = 0) -> None:
-        """Launch with an already packed argument block (``Args.pack`` bytes / bytearray)."""
-        cbuf = C.create_string_buffer(bytes(buf), len(buf))
+        """Launch with an already packed argument block (``Args.pack`` bytes / bytearray, or a
+        ctypes buffer used as is)."""
+        cbuf = buf if isinstance(buf, C.Array) else C.create_string_buffer(bytes(buf), len(buf))
         rc = runtime().hs_jit_launch(self.function(), grid, self.block, shmem or self.lds_bytes,
                                      stream_ptr, cbuf, len(buf))
         if rc != 0:

@@ -925,7 +925,7 @@ class TwoPhaseLauncher:
     """Both phases lowered once (kernels, tiles, spans, per-tile run windows, the tag bitmap);
     ``launch(p)`` fills the literal slots and queues: bitmap clear, tags, scan, partials fold."""
     __slots__ = ("kt", "ks", "grid_t", "grid_s", "GA", "shmem", "vt", "vs", "compacts", "keep",
-                 "tags", "dev", "rows", "blocks", "hk")
+                 "tags", "dev", "rows", "blocks", "hk", "graph", "gblocks")
 
     def __init__(self, kt, ks, grid_t, grid_s, GA, shmem, vt, vs, compacts, keep, tags, dev,
                  rows=None, hk=None):
@@ -939,8 +939,19 @@ class TwoPhaseLauncher:
         self.blocks: dict = {}
         # hash-mode phase 2 (a KeyPlan): groups go to a device hash table, no partials
         self.hk = hk
+        # the captured pipeline (graphs.TwoPhaseGraph) and its per-literal-vector blocks
+        self.graph = None
+        self.gblocks: dict = {}
 
-    def launch(self, p: NL.JoinParams, key=None, htab=None, hk=None):
+    def graphable(self) -> bool:
+        """Whether one query's launches can be captured: the direct phase 1 (no bitmap clear),
+        no row-mask expansion between the phases, partials out (not the hash mode)."""
+        return self.hk is None and self.rows is None and "RNG" in self.vt
+
+    def launch(self, p: NL.JoinParams, key=None, htab=None, hk=None, graph: bool = False):
+        """Queue one query.  Returns the (sum, count, min, max) device outputs, or with
+        ``graph`` (and a literal vector ``key``) a ``graphs.GraphPending`` of one replay of the
+        captured pipeline."""
         import struct
         st = NL.stream_ptr()
         if self.hk is not None:
@@ -969,6 +980,23 @@ class TwoPhaseLauncher:
                 if len(self.blocks) >= 256:
                     self.blocks.clear()
                 self.blocks[key] = hit
+        if graph and key is not None and self.graphable():
+            from .graphs import GraphPending, TwoPhaseGraph, _cbuf
+            g = self.graph
+            if g is None:
+                g = self.graph = TwoPhaseGraph(self.kt, self.ks, self.grid_t, self.grid_s,
+                                               self.GA, self.shmem, self.dev)
+            gb = self.gblocks.get(key)
+            if gb is None:
+                bs = bytearray(hit[1])
+                a = self.ks.args
+                for name, ptr in g.partial_ptrs().items():
+                    struct.pack_into("<q", bs, a.offset(name), ptr)
+                gb = (_cbuf(hit[0]), _cbuf(bs))
+                if len(self.gblocks) >= 256:
+                    self.gblocks.clear()
+                self.gblocks[key] = gb
+            return GraphPending(g, g.launch(*gb))
         if "RNG" not in self.vt:  # the tile form ORs into a zeroed bitmap; the direct form
             self.tags.zero_()     # stores every word of every run group
         self.kt.launch_packed(self.grid_t, hit[0], st)

@@ -106,6 +106,14 @@ HIPGRAPH_ENABLED_DEFAULT = "true"
 # query's stream (exec/gpu.py GpuBackend._scan_agg_graph)
 SIDE_STREAM_SCANS = "spark.hyperspace.mi.sideStreamScans.enabled"
 SIDE_STREAM_SCANS_DEFAULT = "true"
+# replay the run-keyed two-phase merge join (tags, bits scan, fold, result copy) as one captured
+# hipGraph per lowering (graphs.TwoPhaseGraph); needs hipGraph.enabled
+JOIN_GRAPH_ENABLED = "spark.hyperspace.mi.joinGraph.enabled"
+JOIN_GRAPH_ENABLED_DEFAULT = "true"
+# plan-cache hits of a fused aggregate with a known literal vector replay the prepared
+# lowering directly (exec/gpu.py _AggProgram), skipping the executor's plan walk
+PREPARED_SUBMIT_ENABLED = "spark.hyperspace.mi.preparedSubmit.enabled"
+PREPARED_SUBMIT_ENABLED_DEFAULT = "true"
 # cached join index (left row -> first matching right row, int32 in HBM) for joins of two
 # device-resident index tables with unique integer right keys: the fused join aggregate becomes a
 # streaming scan of the left table plus a gather, no per-tile span search (exec/join_index.py)

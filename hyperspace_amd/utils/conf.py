@@ -129,6 +129,15 @@ class HyperspaceConf:
         return _b(conf.get(C.HIPGRAPH_ENABLED, C.HIPGRAPH_ENABLED_DEFAULT))
 
     @staticmethod
+    def join_graph_enabled(conf) -> bool:
+        return HyperspaceConf.hipgraph_enabled(conf) and \
+            _b(conf.get(C.JOIN_GRAPH_ENABLED, C.JOIN_GRAPH_ENABLED_DEFAULT))
+
+    @staticmethod
+    def prepared_submit_enabled(conf) -> bool:
+        return _b(conf.get(C.PREPARED_SUBMIT_ENABLED, C.PREPARED_SUBMIT_ENABLED_DEFAULT))
+
+    @staticmethod
     def side_stream_scans(conf) -> bool:
         return _b(conf.get(C.SIDE_STREAM_SCANS, C.SIDE_STREAM_SCANS_DEFAULT))
 

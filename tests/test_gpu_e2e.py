@@ -185,6 +185,60 @@ def test_side_stream_scans_pipelined_with_joins(tpch):
         _close(table(g3), table(q3(i).collect()))
 
 
+def test_two_phase_join_graph_replays_with_new_literals(tpch):
+    """Plan-cache hits of the run-keyed two-phase merge join replay ONE captured hipGraph
+    (graphs.TwoPhaseGraph: params H2D, tags, bits scan, final fold, D2H) with each query's
+    literals - ungrouped and grouped by a right-side key, several queries in flight - equal to
+    the host oracle and to the eager launches (hipGraph off)."""
+    s, lpath, opath = tpch
+    hs = Hyperspace(s)
+    li = s.read.parquet(lpath)
+    od = s.read.parquet(opath)
+    hs.createIndex(li, IndexConfig("li_ok3", ["l_orderkey"],
+                                   ["l_extendedprice", "l_discount", "l_shipdate"]))
+    hs.createIndex(od, IndexConfig("od_ok3", ["o_orderkey"], ["o_orderdate", "o_shippriority"]))
+    Hyperspace.enable(s)
+    s.conf.set("spark.hyperspace.mi.joinIndex.enabled", "false")
+
+    def q(i, grouped):
+        dd = f"1995-03-{1 + (i * 7) % 28:02d}"
+        j = li.join(od, li["l_orderkey"] == od["o_orderkey"]) \
+            .filter(f"o_orderdate < DATE '{dd}' AND l_shipdate > DATE '{dd}'")
+        aggs = (sum_(col("l_extendedprice") * (1 - col("l_discount"))).alias("rev"),
+                count("*").alias("n"))
+        return j.groupBy("o_shippriority").agg(*aggs) if grouped else j.agg(*aggs)
+    from hyperspace_amd.exec import jit_runs
+    backend = s.backend()
+    for grouped in (False, True):
+        futs = [q(i, grouped).collect_async() for i in range(8)]
+        got = [f.result() for f in futs]
+        assert all(f.path == "native" for f in futs), backend.fallback_reason
+        preps = [pr for pr in backend._agg_preps.values()
+                 if isinstance(getattr(pr, "launcher", None), jit_runs.TwoPhaseLauncher)]
+        assert preps and any(pr.launcher.graph is not None and pr.launcher.graph.replays >= 4
+                             for pr in preps), "two-phase join did not replay a graph"
+        # plan-cache hits with a known literal vector take the prepared program (no plan walk)
+        futs = [q(i, grouped).collect_async() for i in range(8)]
+        again = [f.result() for f in futs]
+        assert any(pg[1].n > 0 for pg in backend._programs.values()), "no prepared submission"
+        for a, b in zip(again, got):    # same literals: equal up to summation order
+            _close(pa.Table.from_pylist(sorted((r.asDict() for r in a), key=lambda d: tuple(d.values()))),
+                   pa.Table.from_pylist(sorted((r.asDict() for r in b), key=lambda d: tuple(d.values()))))
+        s.conf.set("spark.hyperspace.mi.execution.device", "cpu")
+        want = [q(i, grouped).collect() for i in range(8)]
+        s.conf.set("spark.hyperspace.mi.hipGraph.enabled", "false")
+        s.conf.set("spark.hyperspace.mi.execution.device", "gpu")
+        eager = [q(i, grouped).collect() for i in range(8)]
+        s.conf.set("spark.hyperspace.mi.hipGraph.enabled", "true")
+
+        def table(rows):
+            return pa.Table.from_pylist(sorted((r.asDict() for r in rows),
+                                               key=lambda d: tuple(d.values())))
+        for a, b, c in zip(got, want, eager):
+            _close(table(a), table(b))
+            _close(table(c), table(b))
+
+
 def test_side_stream_scan_survives_table_eviction(tpch):
     """A warm scan pipeline replays on the side stream; the device cache then drops the table
     (and with it the compact codes the generated kernel reads) before the result is fetched,
