@@ -119,6 +119,11 @@ class DataFrameWriter:
         self._partition_by = list(cols)
         return self
 
+    def saveAsTable(self, name: str) -> None:
+        """Write the data and record table ``name`` in the session catalog (managed under the
+        warehouse directory, or external at ``option("path", ...)``)."""
+        self.df.session.catalog.save_table(name, self, self._mode)
+
     def save(self, path: str) -> None:
         local = P.to_local(path)
         if os.path.exists(local):

@@ -250,6 +250,15 @@ class DataFrame:
     def hint(self, *_):
         return self
 
+    # -- catalog -------------------------------------------------------------------------------
+    def createOrReplaceTempView(self, name: str) -> None:
+        self.session.catalog.create_temp_view(name, self.plan, replace=True)
+
+    def createTempView(self, name: str) -> None:
+        self.session.catalog.create_temp_view(name, self.plan, replace=False)
+
+    registerTempTable = createOrReplaceTempView
+
     def cache(self):
         return self
 

@@ -63,6 +63,13 @@ class QueryExecution:
 
     def to_arrow(self) -> pa.Table:
         backend = self.session.backend()
+        if self._executed is None and getattr(backend, "supports_bound_plans", False):
+            # a plan-cache hit runs the cached plan with its literals bound in place, the same
+            # path as ``to_arrow_async``: the executor's prepared lowerings (and captured graphs)
+            # are keyed by the cached plan's nodes, which a materialized copy would not share
+            fut = self._submit_bound(backend)
+            if fut is not None:
+                return fut.result()
         return backend.collect(self.executed_plan)
 
     def to_arrow_async(self):

@@ -90,6 +90,24 @@ class Session:
 
     create_dataframe = createDataFrame
 
+    # -- catalog / SQL ----------------------------------------------------------------------------
+    @property
+    def catalog(self):
+        """Temporary views and warehouse tables (hyperspace_amd/catalog.py)."""
+        c = self.__dict__.get("_catalog")
+        if c is None:
+            from .catalog import Catalog
+            c = self._catalog = Catalog(self)
+        return c
+
+    def sql(self, query: str) -> DataFrame:
+        """A DataFrame for a SQL SELECT over temporary views and tables (plan/sql.py)."""
+        from .plan.sql import sql
+        return sql(self, query)
+
+    def table(self, name: str) -> DataFrame:
+        return self.catalog.lookup(name)
+
     @property
     def case_sensitive(self) -> bool:
         return HyperspaceConf.case_sensitive(self.conf)
