@@ -43,6 +43,9 @@ from .graphs import GraphCache, ScanAggGraph, range_bounds
 from .graphs import GraphPending as _GraphPending, _cbuf
 
 log = logging.getLogger(__name__)
+
+# per-wavefront list size of a run top-K aggregate (hash_agg.TopKPlan.K): LIMIT must be below
+H_TOPK_K = 32
 Unsupported = CP.Unsupported
 MAX_GROUPS_SCAN = 3000
 MAX_GROUPS_JOIN = 2400
@@ -2601,13 +2604,19 @@ class GpuBackend:
             span *= max(1, doms[g.expr_id][1]) + 1 if doms[g.expr_id][1] else (1 << 32)
         est = max(1, min(est, span))
         hk_box: list = []
+        tk_box: list = []
+        # ORDER BY <sum / count> LIMIT k over the key-run hash walk: whole keys compete in the
+        # walk's per-wavefront top-K lists and only split keys use the table (TopKPlan)
+        tk_req = self._topk_request(final, fns, order, limit, minmax) if fd is not None else None
 
-        def run(M: int):
+        def run(M: int, use_tk: bool = True):
             table = self.htables.get(M, A, minmax, self.device)
+            tk_box.clear()
             with stage("hagg.kernels"):
                 for kind, a, b in launches:
                     if kind == "join":
-                        self._join_hash_pair(node, a, b, lk, rk, fns, grouping, doms, table, hk_box)
+                        self._join_hash_pair(node, a, b, lk, rk, fns, grouping, doms, table, hk_box,
+                                             tk_req=tk_req if use_tk else None, tk_box=tk_box)
                     else:
                         self._scan_hash(a, fns, grouping, doms, table, hk_box)
             with stage("hagg.extract"):
@@ -2629,6 +2638,27 @@ class GpuBackend:
                     G, over = groups.count()
                 self.htables.record(shape_key, M, G)
                 hk = hk_box[0] if hk_box else None
+                extra = None
+                if fd is not None:
+                    def extra(gmap, host):
+                        self._fd_lookup(right, rk, fd[1], gmap[fd[0][0].expr_id], gmap)
+                tk = tk_box[0] if tk_box and tk_box[0].used else None
+                if tk is not None and hk is not None:
+                    host = self._topk_merge(tk, groups, G, hk, A, int(limit))
+                    if host is not None:
+                        self.metrics["run_topk"] = 1
+                        return self._hash_table_out(final, fns, grouping, hk, host, A, extra)
+                    # a full top-K list may have dropped a tie of the k-th value: exact path
+                    self.metrics["run_topk"] = 0
+                    groups = run(M, use_tk=False)
+                    G, over = groups.count()
+                    while over:
+                        if M >= H.MAX_SLOTS:
+                            raise Unsupported("hash aggregate table too large")
+                        M *= 4
+                        groups = run(M, use_tk=False)
+                        G, over = groups.count()
+                    self.htables.record(shape_key, M, G)
                 if d is not None and d.world > 1:
                     groups, G = self._hash_combine_ranks(d, groups, G, A, minmax)
                 if hk is None or G == 0:
@@ -2636,16 +2666,12 @@ class GpuBackend:
                 src = self._topk_source(final, fns, grouping, hk, order, limit, G)
                 if src is not None:
                     groups, G = H.topk_candidates(groups, G, src, int(limit))
-                extra = None
-                if fd is not None:
-                    def extra(gmap, host):
-                        self._fd_lookup(right, rk, fd[1], gmap[fd[0][0].expr_id], gmap)
                 return self._hash_table_out(final, fns, grouping, hk, groups.to_host(G), A,
                                             extra)
         return finish
 
-    # keys per functional-dependency lookup launch (one probe per (bucket, key))
-    FD_MAX_KEYS = 8192
+    # keys per functional-dependency lookup (one probe per key, in the key's bucket)
+    FD_MAX_KEYS = 1 << 22
 
     def _fd_grouping(self, final, grouping, left: DRel, right: DRel, lk, rk, order, limit):
         """GROUP BY (left join key, right columns...) over an inner join whose right key is
@@ -2694,7 +2720,7 @@ class GpuBackend:
 
     def _fd_lookup(self, right: DRel, rk, attrs, keys: pa.Array, gmap: dict) -> None:
         """``gmap[attr] = right[attr]`` at the right row of each key (unique right keys; the
-        row is found by one equality probe per (bucket, key), as ``_probe_ranges``)."""
+        row is found by one equality probe in the key's bucket, as ``_probe_ranges``)."""
         import torch
         G = len(keys)
         if G == 0:
@@ -2711,13 +2737,13 @@ class GpuBackend:
         else:
             img = (vals + (1 << (width - 1))).astype(np.uint64)
         nb = len(right.table.bucket_offsets_host) - 1
-        pb = torch.from_numpy(np.repeat(np.arange(nb, dtype=np.int32), G)).to(self.device)
-        pk = torch.from_numpy(np.tile(img, nb).view(np.int64)).to(self.device)
+        # each key probes only its own bucket (the index's Murmur3 bucketing of the right key)
+        bids = np.asarray(murmur3.bucket_ids([keys.cast(rk.data_type)], nb), dtype=np.int32)
+        pb = torch.from_numpy(bids).to(self.device)
+        pk = torch.from_numpy(img.view(np.int64)).to(self.device)
         rstart, rlen, _ = K.probe_ranges(rc, right.table.bucket_offsets, pb, pk)
         rs, rl = rstart.cpu().numpy(), rlen.cpu().numpy()
-        row = np.full(G, -1, dtype=np.int64)
-        hit = np.nonzero(rl > 0)[0]
-        row[hit % G] = rs[hit]
+        row = np.where(rl > 0, rs, -1).astype(np.int64)
         if (row < 0).any():
             raise RuntimeError("functional-dependency lookup: a group key has no right row")
         idx = torch.from_numpy(row).to(self.device)
@@ -2824,8 +2850,66 @@ class GpuBackend:
             jit.scan_agg(p, rstart, rlen, tp, self._compacts(descs), nrows=r.table.num_rows,
                          hk=hk, htab=table)
 
+    def _topk_request(self, final, fns, order, limit, minmax):
+        """(aggregate index, by count, descending) when the query orders by one SUM / COUNT
+        aggregate with a small LIMIT (a ``TopKPlan`` can serve it), else None."""
+        if not order or limit is None or minmax or not 0 < int(limit) < H_TOPK_K or \
+                not HyperspaceConf.run_topk_enabled(self.session.conf):
+            return None
+        e = order[0].child
+        if not isinstance(e, E.Attribute):
+            return None
+        for agg in final.aggregates:
+            a = agg if isinstance(agg, E.Attribute) else agg.to_attribute()
+            if a.expr_id != e.expr_id:
+                continue
+            inner = agg.child if isinstance(agg, E.Alias) else agg
+            if not isinstance(inner, (E.Sum, E.Count)):
+                return None
+            i = next((k for k, fn in enumerate(fns) if fn is inner), None)
+            if i is None:
+                return None
+            return (i, isinstance(inner, E.Count), not order[0].ascending)
+        return None
+
+    def _topk_plan(self, req, hk, A: int):
+        """The cached TopKPlan of a request (buffers reused across queries), or None when the
+        order aggregate keeps its own non-null count (a NULL sum has no order value there)."""
+        from . import hash_agg as H
+        i, by_count, desc = req
+        if (hk.own_counts[i] and not by_count) or any(c.nullable for c in hk.cols):
+            return None
+        plans = self.__dict__.setdefault("_tkplans", {})
+        key = (i, by_count, desc, A)
+        tk = plans.get(key)
+        if tk is None:
+            tk = plans[key] = H.TopKPlan(i, by_count, desc, A)
+        return tk
+
+    def _topk_merge(self, tk, groups, G: int, hk, A: int, limit: int):
+        """Host group arrays of the top-``limit`` candidates of a run top-K query: the lists'
+        candidates plus the table's (split keys), or None when a full list's threshold reaches
+        the k-th best value (a dropped tie is possible; the caller re-runs exactly)."""
+        from . import hash_agg as H
+        i = tk.agg
+        cs = i if hk.own_counts[i] else (A - 1 if hk.need_star else -1)
+        src = H.OrderSource(H.SRC_COUNT if tk.src_count else H.SRC_SUM, i, cs, desc=tk.desc)
+        gt, nt, thr = tk.candidates(src, limit)
+        gh, gn = (H.topk_candidates(groups, G, src, limit) if G > limit else (groups, G))
+        ht, hh = gt.to_host(nt), gh.to_host(gn)
+        host = {k: np.concatenate([ht[k], hh[k]]) for k in ht}
+        n = len(host["keys"])
+        if n >= limit:
+            vals = np.sort(tk.image(host["sums"], host["cnts"]))[::-1]
+            kth = float(vals[limit - 1])
+        else:
+            kth = -np.inf
+        if thr >= kth:       # a dropped value may tie the k-th
+            return None
+        return host
+
     def _join_hash_pair(self, node, left: DRel, right: DRel, lk, rk, fns, grouping, doms,
-                        table, hk_box) -> None:
+                        table, hk_box, tk_req=None, tk_box=None) -> None:
         if right.table.num_rows * 64 < left.table.num_rows:
             left, right, lk, rk = right, left, rk, lk
         implied: set = set()
@@ -2856,11 +2940,15 @@ class GpuBackend:
         if not jit.merge_join_ok(jp, comp, right.table.num_rows, left.table.num_rows):
             raise Unsupported("hash aggregate over a join the merge-join kernel cannot run")
         fr = getattr(left.table, "_full_ranges", None)
+        tk = self._topk_plan(tk_req, hk, len(specs)) if tk_req is not None else None
+        if tk is not None:
+            tk.used = False
+            tk_box.append(tk)
         with stage("join.hash_agg_kernel"):
             jit.merge_join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, comp,
                                nrows=left.table.num_rows,
                                cache_spans=fr is not None and rstart is fr[0],
-                               rdup=jit.key_has_dups(right.col(rk)), hk=hk, htab=table)
+                               rdup=jit.key_has_dups(right.col(rk)), hk=hk, htab=table, tk=tk)
 
     def _hash_combine_ranks(self, d, groups, G: int, A: int, minmax: bool):
         """Every rank's groups to every rank (one variable-size all-gather of packed rows, no

@@ -393,6 +393,92 @@ def topk_candidates(g: Groups, G: int, o: OrderSource, k: int) -> Tuple[Groups, 
     return g.take(sel, n), n
 
 
+class TopKPlan:
+    """ORDER BY <SUM or COUNT aggregate> LIMIT k over a key-run walk (jit_runs bits scan, hash
+    mode): keys whose passing rows the walk sees whole keep their final aggregates in a
+    per-wavefront top-``K`` list (registers) instead of a hash-table slot.  Full lists publish
+    their threshold (the K-th best; ``ctl[0]``, an order-preserving integer image, atomicMax)
+    and every wavefront drops values below the best published one - such a value has K > k
+    better ones.  At the end each list appends its entries at or above the final threshold to
+    candidate arrays laid out like ``Groups`` (keys, then per aggregate sums / counts at stride
+    ``cap``; the count in ``ctl[1]``).  Values are compared in the "larger is better" image
+    (negated for an ascending order).
+
+    A value EQUAL to a threshold is dropped too, so when the final threshold reaches the k-th
+    best value overall a tie may be missing: ``exact`` is False and the caller re-runs the
+    table path."""
+    K = 32
+
+    def __init__(self, agg: int, src_count: bool, desc: bool, NA: int):
+        self.agg, self.src_count, self.desc, self.NA = agg, src_count, desc, NA
+        self.nwv = 0
+        self.cap = 0
+        self.keys = self.sums = self.cnts = self.ctl = self._ctl0 = None
+        self.used = False
+
+    def shape(self) -> tuple:
+        return ("topk", self.agg, self.src_count, self.desc, self.K)
+
+    def bind(self, nwv: int, device) -> None:
+        """Buffers for ``nwv`` wavefronts (the bits scan's grid)."""
+        import torch
+        if self.nwv == nwv and self.keys is not None:
+            return
+        self.nwv, self.cap = nwv, nwv * self.K
+        self.keys = torch.empty(self.cap, dtype=torch.int64, device=device)
+        self.sums = torch.empty(self.cap * self.NA, dtype=torch.float64, device=device)
+        self.cnts = torch.empty(self.cap * self.NA, dtype=torch.int64, device=device)
+        # [threshold image of -inf, candidate count 0]
+        neg_inf = np.array([-np.inf]).view(np.int64)[0]
+        img = int(neg_inf) ^ 0x7FFFFFFFFFFFFFFF
+        self._ctl0 = torch.tensor([img, 0], dtype=torch.int64, device=device)
+        self.ctl = torch.empty(2, dtype=torch.int64, device=device)
+
+    def reset(self) -> None:
+        """Stream-ordered, before each launch."""
+        self.ctl.copy_(self._ctl0, non_blocking=True)
+
+    def kernel_values(self) -> Dict[str, int]:
+        return {"TKK": self.keys.data_ptr(), "TKS": self.sums.data_ptr(),
+                "TKC": self.cnts.data_ptr(), "TKG": self.ctl.data_ptr(), "TKCAP": self.cap}
+
+    def read_ctl(self) -> Tuple[float, int]:
+        """(final threshold in the order image, candidate count) - one small D2H."""
+        c = self.ctl.cpu().numpy()
+        v = int(c[0])
+        bits = v if v >= 0 else v ^ 0x7FFFFFFFFFFFFFFF
+        return float(np.array([bits], dtype=np.int64).view(np.float64)[0]), int(c[1])
+
+    def candidates(self, o: "OrderSource", k: int) -> Tuple["Groups", int, float]:
+        """(the appended entries reduced to their top k, ties kept; their count; the final
+        threshold)."""
+        thr, n = self.read_ctl()
+        n = min(n, self.cap)
+        g = Groups(self.NA, self.cap, self.keys.device)
+        g.keys, g.sums, g.cnts = self.keys, self.sums, self.cnts
+        g.nulls = _zeros_u8(self.cap, self.keys.device)
+        g.set_count(n)
+        if n > k:
+            g, n = topk_candidates(g, n, o, k)
+        return g, n, thr
+
+    def image(self, sums, cnts) -> "np.ndarray":
+        """Order values of host group arrays in the kernel's image (larger is better)."""
+        v = cnts[:, self.agg].astype(np.float64) if self.src_count else sums[:, self.agg]
+        return v if self.desc else -v
+
+
+_ZEROS: Dict[tuple, object] = {}
+
+
+def _zeros_u8(n: int, dev):
+    import torch
+    z = _ZEROS.get((n, str(dev)))
+    if z is None:
+        z = _ZEROS[(n, str(dev))] = torch.zeros(n, dtype=torch.uint8, device=dev)
+    return z
+
+
 _TOPK_WS: Dict[object, dict] = {}
 
 
@@ -409,4 +495,4 @@ def _topk_ws(dev) -> dict:
 
 
 __all__ = ["KeyPlan", "KeyCol", "plan_keys", "HashTable", "Groups", "TablePool",
-           "OrderSource", "topk_candidates", "Unsupported"]
+           "OrderSource", "topk_candidates", "TopKPlan", "Unsupported"]

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import re
 import struct
 import threading
 from typing import Dict, List, Optional, Tuple
@@ -366,6 +367,14 @@ __device__ __forceinline__ void lds_max(double* p, double v) {
   do { as = old; if (__longlong_as_double((i64)as) >= v) break;
        old = atomicCAS(a, as, (u64)__double_as_longlong(v)); } while (as != old);
 }
+// order-preserving signed image of a double (top-K thresholds published with atomicMax)
+__device__ __forceinline__ long long hs_dimg(double d) {
+  const long long u = __double_as_longlong(d);
+  return u >= 0 ? u : u ^ 0x7fffffffffffffffll;
+}
+__device__ __forceinline__ double hs_dimg_inv(long long i) {
+  return __longlong_as_double(i >= 0 ? i : i ^ 0x7fffffffffffffffll);
+}
 // hash-mode grouping (exec/hash_agg.py, csrc/kernels/hash_agg.hip): probe hash and the bit
 // images of float group keys (-0.0 -> 0.0, one NaN)
 __device__ __forceinline__ u64 hs_mix64(u64 h) {
@@ -619,14 +628,56 @@ def _accumulate(gen: _Gen, aggs, grouped: bool, pass_var: str, gvar: str, ind: s
 HASH_MAX_PROBE = 512
 
 
-def _hash_accumulate(gen: _Gen, aggs, hk, pass_var: str, ind: str) -> List[str]:
+def _hash_key_lines(gen: _Gen, hk, var: str, sfx: str, ind: str) -> List[str]:
+    """``u64 <var>`` = the packed / raw hash key from the key columns ``x<slot><sfx>``, and
+    ``bool <var>_nul``."""
+    a = gen.a
+    b = []
+    if hk.mode == "packed":
+        b.append(f"{ind}u64 {var} = 0ull; const bool {var}_nul = false;")
+        for j, c in enumerate(hk.cols):
+            lo = a.add("q", f"HL{j}", "long long")
+            sh = a.add("q", f"HS{j}", "long long")
+            s = c.slot
+            x = f"x{s}{sfx}"
+            if c.kind == "f32":
+                val = f"hs_f32key((float){x})"
+            elif c.kind == "dec":
+                sc = a.add("d", f"HQ{j}", "double")
+                val = f"(u64)((i64)__builtin_rint((double){x} * {sc}) - {lo})"
+            else:
+                val = f"(u64)((i64){x} - {lo})"
+            ok = gen.ok(s)
+            if sfx:
+                ok = re.sub(rf"\bn{s}\b", f"n{s}{sfx}", ok)
+            expr = f"({ok} ? {val} + 1ull : 0ull)" if c.nullable else val
+            b.append(f"{ind}{var} |= {expr} << (unsigned){sh};")
+    else:
+        c = hk.cols[0]
+        s = c.slot
+        x = f"x{s}{sfx}"
+        val = f"hs_f64key((double){x})" if hk.mode == "raw_float" else f"(u64)(i64){x}"
+        ok = gen.ok(s)
+        if sfx:
+            ok = re.sub(rf"\bn{s}\b", f"n{s}{sfx}", ok)
+        nul = f"!{ok}" if c.nullable else "false"
+        b.append(f"{ind}const bool {var}_nul = {nul}; const u64 {var} = {var}_nul ? 0ull : {val};")
+    return b
+
+
+def _hash_accumulate(gen: _Gen, aggs, hk, pass_var: str, ind: str, tk=None,
+                     seg: str = None) -> List[str]:
     """Hash-mode grouping (``hk``: an exec.hash_agg.KeyPlan): the wavefront's lanes, in row
     order, are cut into runs of equal group keys (one ballot of the run heads); a segmented
     shuffle scan sums each run's values into its last lane, and only that lane probes the
     global table (linear probing, 64-bit key, atomicCAS insert) and adds the run's partials
     with memory-side atomics.  Inputs sorted by a key prefix (index scans, merge-join output)
     put a group's rows in adjacent lanes, so most groups cost one probe and one atomic per
-    aggregate per 64-row batch.  Variables are ``x<slot>`` / ``n<slot>`` (callers rename)."""
+    aggregate per 64-row batch.  Variables are ``x<slot>`` / ``n<slot>`` (callers rename).
+
+    ``seg``: a per-lane variable that identifies the group within the batch (the key run of
+    the key-run walk): lanes are cut on it, and the key columns are loaded (``_uload``) only
+    by lanes that emit a group (a table probe or a top-K candidate), not for every row."""
     a = gen.a
     kp = a.add("p", "hkeys", "unsigned long long*")
     sp = a.add("p", "hsum", "double*")
@@ -636,35 +687,30 @@ def _hash_accumulate(gen: _Gen, aggs, hk, pass_var: str, ind: str) -> List[str]:
     mxp = a.add("p", "hmax", "double*") if mm else None
     hm = a.add("q", "HM", "long long")
     fl = a.add("p", "hflag", "long long*")
-    na = len(aggs)
     i2 = ind + "  "
     b = [f"{ind}{{ const int hln = (int)(threadIdx.x & 63u); const bool hok = {pass_var};"]
-    if hk.mode == "packed":
-        b.append(f"{i2}u64 hk = 0ull; const bool hnul = false;")
-        for j, c in enumerate(hk.cols):
-            lo = a.add("q", f"HL{j}", "long long")
-            sh = a.add("q", f"HS{j}", "long long")
-            s = c.slot
-            if c.kind == "f32":
-                val = f"hs_f32key((float)x{s})"
-            elif c.kind == "dec":
-                sc = a.add("d", f"HQ{j}", "double")
-                val = f"(u64)((i64)__builtin_rint((double)x{s} * {sc}) - {lo})"
-            else:
-                val = f"(u64)((i64)x{s} - {lo})"
-            expr = f"({gen.ok(s)} ? {val} + 1ull : 0ull)" if c.nullable else val
-            b.append(f"{i2}hk |= {expr} << (unsigned){sh};")
+
+    def lazy_key(cond: str, out: List[str], ind_: str) -> None:
+        """``hk`` / ``hnul`` of lanes where ``cond`` holds, from the key columns loaded there."""
+        out.append(f"{ind_}u64 hk = 0ull; bool hnul = false;")
+        out.append(f"{ind_}if ({cond}) {{")
+        for c in hk.cols:
+            _uload(gen, c.slot, "KK", out, ind_ + "  ")
+        out.extend(_hash_key_lines(gen, hk, "hk_l", "_KK", ind_ + "  "))
+        out.append(f"{ind_}  hk = hk_l; hnul = hk_l_nul; }}")
+    if seg is None:
+        b.extend(_hash_key_lines(gen, hk, "hk", "", i2))
+        b.append(f"{i2}const bool hnul = hk_nul;")
+        b += [f"{i2}const u64 hkp = __shfl_up(hk, 1u, 64);",
+              f"{i2}const int hfp = __shfl_up((hok ? 1 : 0) | (hnul ? 2 : 0), 1u, 64);",
+              f"{i2}const bool hsame = hln > 0 && hok && (hfp & 1) != 0 && "
+              f"((hfp >> 1) & 1) == (hnul ? 1 : 0) && hkp == hk;"]
     else:
-        c = hk.cols[0]
-        s = c.slot
-        val = f"hs_f64key((double)x{s})" if hk.mode == "raw_float" else f"(u64)(i64)x{s}"
-        nul = f"!{gen.ok(s)}" if c.nullable else "false"
-        b.append(f"{i2}const bool hnul = {nul}; const u64 hk = hnul ? 0ull : {val};")
-    b += [f"{i2}const u64 hkp = __shfl_up(hk, 1u, 64);",
-          f"{i2}const int hfp = __shfl_up((hok ? 1 : 0) | (hnul ? 2 : 0), 1u, 64);",
-          f"{i2}const bool hsame = hln > 0 && hok && (hfp & 1) != 0 && "
-          f"((hfp >> 1) & 1) == (hnul ? 1 : 0) && hkp == hk;",
-          f"{i2}const u64 hH = __ballot(!hsame);",
+        b += [f"{i2}const unsigned hsg = (unsigned){seg};",
+              f"{i2}const unsigned hsp = __shfl_up(hsg, 1u, 64);",
+              f"{i2}const int hfp = __shfl_up(hok ? 1 : 0, 1u, 64);",
+              f"{i2}const bool hsame = hln > 0 && hok && hfp != 0 && hsp == hsg;"]
+    b += [f"{i2}const u64 hH = __ballot(!hsame);",
           f"{i2}const int hss = 63 - __builtin_clzll(hH & ((2ull << hln) - 1ull));",
           f"{i2}const bool htl = hok && (hln == 63 || ((hH >> ((hln + 1) & 63)) & 1ull) != 0ull);"]
     own = hk.own_counts
@@ -691,9 +737,24 @@ def _hash_accumulate(gen: _Gen, aggs, hk, pass_var: str, ind: str) -> List[str]:
             b.append(f"{i2}    {var} = " + (f"{op}({var}, u_{var});" if op else f"{var} + u_{var};"))
         b.append(f"{i2}  }}")
         b.append(f"{i2}}}")
+    probe = "htl"
+    if tk is not None:
+        # run top-K mode (hash_agg.TopKPlan): a segment strictly inside the 64-entry window -
+        # a different key on both sides, the next lane valid - holds ALL passing rows of its
+        # key (a key's rows are one contiguous run and the list is in row order), so its sums
+        # are final and go to the wavefront's top-K list instead of the table; only segments
+        # touching a window edge (keys split across windows, passes or tiles) probe the table
+        b += [f"{i2}const u64 hV_ = __ballot(hok);",
+              f"{i2}const bool hcomp = htl && hss > 0 && hln < 63 && "
+              f"((hV_ >> (unsigned)(hln + 1)) & 1ull) != 0ull;"]
+        probe = "htl && !hcomp"
+        b += _topk_value(aggs, hk, tk, i2)
+    if seg is not None:
+        emit = f"({probe})" + (" || (hcomp && tkv_ > tkcut)" if tk is not None else "")
+        lazy_key(emit, b, i2)
     # CAS-first probe: a group's first run inserts with one returning atomic (no load first);
     # later runs of the same group find it on the first CAS of their probe
-    b += [f"{i2}if (htl) {{",
+    b += [f"{i2}if ({probe}) {{",
           f"{i2}  long long hs_ = -1;",
           f"{i2}  if (hnul) hs_ = {hm} + 1; else if (hk == ~0ull) hs_ = {hm}; else {{",
           f"{i2}    u64 hh = hs_mix64(hk) & (u64)({hm} - 1);",
@@ -729,7 +790,119 @@ def _hash_accumulate(gen: _Gen, aggs, hk, pass_var: str, ind: str) -> List[str]:
             b.append(f"{i2}    atomicMax(&{mxp}[{i} * hst + hs_], hv{i});")
         if own[i]:
             b.append(f"{i2}    atomicAdd({tgt}, {cnt});")
-    b += [f"{i2}  }}", f"{i2}}}", f"{ind}}}"]
+    b += [f"{i2}  }}", f"{i2}}}"]
+    if tk is not None:
+        b += _topk_insert(aggs, hk, tk, i2)
+    b.append(f"{ind}}}")
+    return b
+
+
+def _topk_values(aggs, hk):
+    """Per aggregate i: (sum expression, count expression) a complete segment stores, matching
+    what the hash table would hold for that group (counts only where the table keeps them)."""
+    own = hk.own_counts
+    out = []
+    for i, ag in enumerate(aggs):
+        if ag.kind == NL.AK_COUNT_STAR:
+            out.append(("0.0", "hrn_" if hk.need_star else "0ll"))
+        elif ag.kind == NL.AK_COUNT:
+            out.append(("0.0", f"hc{i}" if own[i] else "hrn_"))
+        else:
+            out.append((f"hv{i}", f"hc{i}" if own[i] else "0ll"))
+    return out
+
+
+def _topk_value(aggs, hk, tk, ind: str) -> List[str]:
+    """``tkv_``: the segment's order value in the "larger is better" image."""
+    sv, cv = _topk_values(aggs, hk)[tk.agg]
+    ov = f"(double){cv}" if tk.src_count else sv
+    sign = "" if tk.desc else "-"
+    return [f"{ind}const long long hrn_ = (long long)(hln - hss + 1);",
+            f"{ind}const double tkv_ = {sign}({ov});"]
+
+
+def _topk_decls(aggs, tk, args: "Args") -> List[str]:
+    """Kernel-scope state of the wavefront's top-K list (lane l < K holds entry l), its own
+    threshold ``tkthr`` (the minimum of a full list) and the cut ``tkcut`` = max(own, the
+    global threshold other wavefronts published)."""
+    args.add("p", "TKG", "long long*")
+    b = ["  u64 tkk = ~0ull; double tko = -__builtin_inf(); int tkn = 0;",
+         "  double tkthr = -__builtin_inf(); double tkcut = -__builtin_inf();",
+         "  double tkpub = -__builtin_inf();"]
+    for i in range(len(aggs)):
+        b.append(f"  double tks{i} = 0.0; long long tkc{i} = 0ll;")
+    return b
+
+
+def _topk_sync(tk, ind: str) -> List[str]:
+    """Once per tile: publish a full list's threshold (atomicMax of the order-preserving
+    integer image) and take the best published threshold as this wavefront's cut - a value
+    below the 32nd best of any list cannot reach the top ``limit < 32``."""
+    return [f"{ind}if (tkn >= {tk.K} && tkthr > tkpub) {{",
+            f"{ind}  if ((threadIdx.x & 63u) == 0) atomicMax(a.TKG, hs_dimg(tkthr));",
+            f"{ind}  tkpub = tkthr; }}",
+            f"{ind}tkcut = fmax(tkthr, hs_dimg_inv(__atomic_load_n(a.TKG, __ATOMIC_RELAXED)));"]
+
+
+def _topk_insert(aggs, hk, tk, ind: str) -> List[str]:
+    """Complete segments whose order value beats the cut enter the list one at a time
+    (wavefront-uniform loop over the ballot): the first K fill empty slots, later ones replace
+    the list's minimum; the list's threshold is the minimum of a full list."""
+    K = tk.K
+    vals = _topk_values(aggs, hk)
+    b = [f"{ind}{{ u64 tq_ = __ballot(hcomp && tkv_ > tkcut);",
+         f"{ind}  while (tq_) {{",
+         f"{ind}    const int sl_ = __builtin_ctzll(tq_); tq_ &= tq_ - 1ull;",
+         f"{ind}    const double cv_ = __shfl(tkv_, sl_, 64);",
+         f"{ind}    if (cv_ > tkcut) {{",
+         f"{ind}      const u64 ck_ = __shfl(hk, sl_, 64);"]
+    for i, (sx, cx) in enumerate(vals):
+        b.append(f"{ind}      const double cs{i}_ = __shfl((double)({sx}), sl_, 64); "
+                 f"const long long cc{i}_ = __shfl((long long)({cx}), sl_, 64);")
+    b += [f"{ind}      int slot_ = tkn;",
+          f"{ind}      if (tkn >= {K}) {{",
+          f"{ind}        double m_ = hln < {K} ? tko : __builtin_inf(); int mi_ = hln;",
+          f"{ind}        for (int o_ = 32; o_ > 0; o_ >>= 1) {{",
+          f"{ind}          const double om_ = __shfl_xor(m_, o_, 64); "
+          f"const int oi_ = __shfl_xor(mi_, o_, 64);",
+          f"{ind}          if (om_ < m_ || (om_ == m_ && oi_ < mi_)) {{ m_ = om_; mi_ = oi_; }} }}",
+          f"{ind}        slot_ = mi_;",
+          f"{ind}      }} else {{ ++tkn; }}",
+          f"{ind}      if (hln == slot_) {{ tkk = ck_; tko = cv_;" +
+          "".join(f" tks{i} = cs{i}_; tkc{i} = cc{i}_;" for i in range(len(vals))) + " }",
+          f"{ind}      if (tkn >= {K}) {{",
+          f"{ind}        double m_ = hln < {K} ? tko : __builtin_inf();",
+          f"{ind}        for (int o_ = 32; o_ > 0; o_ >>= 1) m_ = fmin(m_, __shfl_xor(m_, o_, 64));",
+          f"{ind}        tkthr = m_; tkcut = fmax(tkcut, m_);",
+          f"{ind}      }}",
+          f"{ind}    }}",
+          f"{ind}  }}",
+          f"{ind}}}"]
+    return b
+
+
+def _topk_flush(aggs, tk, args: "Args") -> List[str]:
+    """The list entries at or above the final global threshold, appended (one atomic per
+    wavefront) to the candidate arrays (hash_agg.Groups layout: keys, then per aggregate sums /
+    counts at stride TKCAP); the count in TKG[1]."""
+    kk = args.add("p", "TKK", "unsigned long long*")
+    ks = args.add("p", "TKS", "double*")
+    kc = args.add("p", "TKC", "long long*")
+    cap = args.add("q", "TKCAP", "long long")
+    b = ["  { const int tl_ = (int)(threadIdx.x & 63u);",
+         "    const double gt_ = hs_dimg_inv(__atomic_load_n(a.TKG, __ATOMIC_RELAXED));",
+         f"    const bool lv_ = tl_ < {tk.K} && tl_ < tkn && tko >= gt_;",
+         "    const u64 lb_ = __ballot(lv_);",
+         "    long long base_ = 0;",
+         "    if (tl_ == 0 && lb_) base_ = (long long)atomicAdd((unsigned long long*)&a.TKG[1], "
+         "(unsigned long long)__popcll(lb_));",
+         "    base_ = __shfl(base_, 0, 64);",
+         "    if (lv_) {",
+         "      const long long te_ = base_ + __popcll(lb_ & ((1ull << tl_) - 1ull));",
+         f"      if (te_ < {cap}) {{ {kk}[te_] = tkk;"]
+    for i in range(len(aggs)):
+        b.append(f"        {ks}[{i} * {cap} + te_] = tks{i}; {kc}[{i} * {cap} + te_] = tkc{i};")
+    b += ["      }", "    }", "  }"]
     return b
 
 
@@ -2068,7 +2241,7 @@ def merge_join_ok(p: NL.JoinParams, compacts=None, rnrows: int = 0, lnrows: int 
 
 
 def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None, nrows: int = 0,
-                   cache_spans: bool = False, rdup: bool = True, hk=None, htab=None):
+                   cache_spans: bool = False, rdup: bool = True, hk=None, htab=None, tk=None):
     """Sort-merge join + aggregate with ``gen_merge_join_agg`` (same outputs as ``join_agg``);
     ``nrows`` = left table rows; ``rdup`` = the right key column may repeat a key
     (``key_has_dups``)."""
@@ -2086,11 +2259,12 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
         # over a resident table's cached full ranges the lowering (run ranges, tiles, kernels,
         # column slots) is fixed: keep it, keyed by the ranges, the column pointers and the shape
         ck = (id(rstart), id(runs), tuple(p.cols[s].data for s in range(NL.MAX_COLS)),
-              merge_join_shape(p, compacts, hk)) if cache_spans else None
+              merge_join_shape(p, compacts, hk), id(tk),
+              tk.shape() if tk is not None else None) if cache_spans else None
         two = _RUNS_HASH_LOWERED.get(ck) if ck is not None else None
         if two is None:
             two = jit_runs.lower(p, rstart, rlen, rbucket, roff, compacts, runs, nrows,
-                                 cache_spans, hk=hk)
+                                 cache_spans, hk=hk, tk=tk)
             if two is not None and ck is not None:
                 if len(_RUNS_HASH_LOWERED) >= 8:
                     _RUNS_HASH_LOWERED.pop(next(iter(_RUNS_HASH_LOWERED)))

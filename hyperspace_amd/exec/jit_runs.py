@@ -700,12 +700,13 @@ def packed_tail(layout, compacts):
     return w
 
 
-def sparse_shape(p: NL.JoinParams, compacts, hk=None) -> tuple:
+def sparse_shape(p: NL.JoinParams, compacts, hk=None, tk=None) -> tuple:
     return ("run_bits_scan",) + scan_shape(p, compacts, 1, 64)[1:] + \
-        (pack_layout(p, compacts),) + ((hk.shape(),) if hk is not None else ())
+        (pack_layout(p, compacts),) + ((hk.shape(),) if hk is not None else ()) + \
+        ((tk.shape(),) if tk is not None else ())
 
 
-def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None) -> J.Kernel:
+def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kernel:
     """Phase 2 for 1-bit tags, bit-parallel: the dense per-row scan spends ~20 VALU
     instructions per row (decode, predicate, run index by popcount, tag extract, compaction
     ballot + mbcnt), which bounds it below HBM speed.  Here a wavefront takes 4096-row tiles of
@@ -726,7 +727,13 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None) -> J.Kernel:
     With ``hk`` (an exec.hash_agg.KeyPlan over left columns) the walk groups by the hash key
     instead: each pass's 64 list entries are consecutive passing rows, so a segmented shuffle
     reduce folds a group's rows (one run = one left join key) before one table probe
-    (``jit._hash_accumulate``); kernel ``hs_jit_run_bits_hash``, no partials."""
+    (``jit._hash_accumulate``); kernel ``hs_jit_run_bits_hash``, no partials.
+
+    With ``tk`` as well (an exec.hash_agg.TopKPlan: ORDER BY <aggregate> LIMIT k over those
+    groups), a key whose passing rows lie strictly inside one 64-entry window is final there
+    and competes for the wavefront's top-K list (registers, lane l = entry l) instead of
+    probing the table; only keys split across windows / passes / tiles go to the table (kernel
+    ``hs_jit_run_bits_topk``; every wavefront writes its list at the end)."""
     args = J.Args()
     for n, ct in (("rstart", "const long long*"), ("rlen", "const long long*"),
                   ("tile_prefix", "const long long*")):
@@ -745,8 +752,10 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None) -> J.Kernel:
     assert not (grouped and p.group_col >= SPLIT)
     pslots = J._pred_slots(lpreds)
     assert not (grouped and hk is not None)
+    # top-K mode segments the walk by key run (lrn_) and loads the key columns only where a
+    # group is emitted (jit._hash_accumulate ``seg``): they are not part of the per-row tail
     tail = list(dict.fromkeys(J._agg_slots(aggs) + ([p.group_col] if grouped else []) +
-                              (list(hk.slots) if hk is not None else [])))
+                              (list(hk.slots) if hk is not None and tk is None else [])))
     approx = J._sum_only_slots(lpreds, aggs, p.group_col if grouped else -1, cols) - \
         set(hk.slots if hk is not None else [])
     BLOCK = J.BLOCK  # noqa: N806
@@ -755,6 +764,9 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None) -> J.Kernel:
     NI = 64  # noqa: N806
     b: List[str] = []
     b += J._acc_decls(aggs, grouped, args)
+    assert tk is None or hk is not None
+    if tk is not None:
+        b += J._topk_decls(aggs, tk, args)
     CAP = 1024  # noqa: N806 — list entries per wavefront and round (a denser tile takes rounds)
     EW = 4  # noqa: N806 — list entries per lane per walk pass, loads all in flight together
 
@@ -766,6 +778,8 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None) -> J.Kernel:
                 f"    {{ const i64 r0_ = tb{sfx} + 64 * ln; "
                 f"const i64 g_ = (r0_ < a.nrows ? r0_ : a.nrows - 1) >> 6;",
                 f"      gm{sfx} = a.GM{lk}[g_] | 1ull; gr{sfx} = a.GR{lk}[g_]; }}"]
+    if tk is not None:
+        b.append(f"  __shared__ unsigned short lrn_[{WV}][{CAP}];")
     b += [f"  __shared__ unsigned short lst_[{WV}][{CAP}];",
           "  const int ln = (int)(threadIdx.x & 63);",
           "  const int wq = (int)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));",
@@ -785,7 +799,14 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None) -> J.Kernel:
     b += geom("t0", "N")
     b += ["  }",
           "  for (i64 t = t0; t < t1; ++t) {",
-          "    const i64 rs = rsN, re = reN, tb0 = tbN; const u64 m_ = gmN; const i64 q0 = grN;",
+          "    const i64 rs = rsN, re = reN, tb0 = tbN; const u64 m_ = gmN; const i64 q0 = grN;"]
+    if tk is not None:
+        # key run of a list entry, relative to the tile's first run (lrn_); the lists'
+        # threshold exchange once per tile
+        b.append("    const int qr_ = (int)(q0 - __shfl(q0, 0, 64));")
+        b += J._topk_sync(tk, "    ")
+    b += [
+
           "    const i64 row0 = tb0 + 64 * ln;",
           "    const i64 lo_ = rs - row0, hi_ = re - row0;",
           "    const int alo = lo_ <= 0 ? 0 : (lo_ >= 64 ? 64 : (int)lo_);",
@@ -866,8 +887,10 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None) -> J.Kernel:
           f"    const int wn_ = tot_ - wb_ < {CAP} ? tot_ - wb_ : {CAP};",
           "    { int pos_ = inc_ - cn_ - wb_; u64 e_ = d_;",
           "      while (e_) { const int bq_ = __builtin_ctzll(e_); "
-          f"if (pos_ >= 0 && pos_ < {CAP}) lst_[wq][pos_] = (unsigned short)(64 * ln + bq_); "
-          "++pos_; e_ &= e_ - 1ull; } }",
+          f"if (pos_ >= 0 && pos_ < {CAP}) {{ lst_[wq][pos_] = (unsigned short)(64 * ln + bq_); "
+          + ("lrn_[wq][pos_] = (unsigned short)(qr_ + __popcll(m_ & ((2ull << bq_) - 1ull))); "
+             if tk is not None else "") +
+          "} ++pos_; e_ &= e_ - 1ull; } }",
           f"    {J._wave_sync()}",
           f"    for (int cb = 0; cb < wn_; cb += {64 * EW}) {{"]
     ind2 = "      "
@@ -875,6 +898,9 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None) -> J.Kernel:
         b += [f"{ind2}const int ce{k} = cb + {64 * k} + ln;",
               f"{ind2}const bool cok{k} = ce{k} < wn_;",
               f"{ind2}const i64 crow{k} = tb0 + (cok{k} ? (i64)lst_[wq][ce{k}] : 0);"]
+        if tk is not None:
+            b.append(f"{ind2}const unsigned crn{k} = cok{k} ? (unsigned)lrn_[wq][ce{k}] : "
+                     f"0xFFFFFFFFu;")
     gs = [J._Gen(args, cols, SPLIT, (f"crow{k}", f"crow{k}"), approx, True) for k in range(EW)]
     layout = pack_layout(p, compacts)
     packed = {sl: (off, nb) for sl, off, nb in layout} if layout else {}
@@ -905,7 +931,9 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None) -> J.Kernel:
                      f"glc < {ng};")
             b.append(f"{ind2}const int {gvar} = cok ? (int)glc : 0;")
         if hk is not None:
-            b += [J._rename(x, tail, it) for x in J._hash_accumulate(g, aggs, hk, "cok", ind2)]
+            b += [J._rename(x, tail, it)
+                  for x in J._hash_accumulate(g, aggs, hk, "cok", ind2, tk=tk,
+                                              seg=f"crn{k}" if tk is not None else None)]
         else:
             b += [J._rename(x, tail, it)
                   for x in J._accumulate(g, aggs, grouped, "cok", gvar, ind2)]
@@ -913,7 +941,10 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None) -> J.Kernel:
     b += ["    }", f"    {J._wave_sync()}", "    }", "  }"]
     if hk is None:
         b += J._flush(aggs, grouped)
-    name = "hs_jit_run_bits_scan" if hk is None else "hs_jit_run_bits_hash"
+    if tk is not None:
+        b += J._topk_flush(aggs, tk, args)
+    name = "hs_jit_run_bits_scan" if hk is None else \
+        ("hs_jit_run_bits_hash" if tk is None else "hs_jit_run_bits_topk")
     src = (J._PRELUDE + args.struct_src() +
            f'extern "C" __global__ __launch_bounds__({BLOCK}) void {name}(Args a) '
            f'{{\n' + "\n".join(b) + "\n}\n")
@@ -925,10 +956,10 @@ class TwoPhaseLauncher:
     """Both phases lowered once (kernels, tiles, spans, per-tile run windows, the tag bitmap);
     ``launch(p)`` fills the literal slots and queues: bitmap clear, tags, scan, partials fold."""
     __slots__ = ("kt", "ks", "grid_t", "grid_s", "GA", "shmem", "vt", "vs", "compacts", "keep",
-                 "tags", "dev", "rows", "blocks", "hk", "graph", "gblocks")
+                 "tags", "dev", "rows", "blocks", "hk", "graph", "gblocks", "tk")
 
     def __init__(self, kt, ks, grid_t, grid_s, GA, shmem, vt, vs, compacts, keep, tags, dev,
-                 rows=None, hk=None):
+                 rows=None, hk=None, tk=None):
         self.kt, self.ks, self.grid_t, self.grid_s = kt, ks, grid_t, grid_s
         self.GA, self.shmem, self.vt, self.vs = GA, shmem, vt, vs
         self.compacts, self.keep, self.tags, self.dev = compacts, keep, tags, dev
@@ -939,6 +970,7 @@ class TwoPhaseLauncher:
         self.blocks: dict = {}
         # hash-mode phase 2 (a KeyPlan): groups go to a device hash table, no partials
         self.hk = hk
+        self.tk = tk          # run top-K mode of the hash walk (hash_agg.TopKPlan)
         # the captured pipeline (graphs.TwoPhaseGraph) and its per-literal-vector blocks
         self.graph = None
         self.gblocks: dict = {}
@@ -963,6 +995,10 @@ class TwoPhaseLauncher:
             J.fill_preds_aggs(vs, preds, [p.aggs[i] for i in range(p.naggs)], self.compacts)
             vs.update(htab.kernel_values())
             vs.update((hk or self.hk).values())   # this query's key domain
+            if self.tk is not None:
+                vs.update(self.tk.kernel_values())
+                self.tk.reset()
+                self.tk.used = True
             self.kt.launch(self.grid_t, vt, st, 0)
             self.ks.launch(self.grid_s, vs, st, self.shmem)
             return None
@@ -1014,7 +1050,7 @@ class TwoPhaseLauncher:
 
 
 def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: int,
-          cache_spans: bool, hk=None) -> Optional[TwoPhaseLauncher]:
+          cache_spans: bool, hk=None, tk=None) -> Optional[TwoPhaseLauncher]:
     """The two-phase launcher of a run-keyed merge join, or None when it does not apply.
     ``hk``: group by that hash key plan (left-side key columns only) through the bits scan's
     hash mode (needs 1-bit tags and the direct phase 1)."""
@@ -1033,9 +1069,11 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
     onebit = W == 1 and not (_scan_grouped(p) and p.group_col >= SPLIT)
     sparse = SPARSE and onebit
     rowmask = ROWMASK and onebit and not sparse
+    if tk is not None and hk is None:
+        tk = None
     if sparse:
-        ks = J.kernel_for(sparse_shape(p, compacts, hk),
-                          lambda: gen_run_sparse_scan(p, compacts, hk))
+        ks = J.kernel_for(sparse_shape(p, compacts, hk, tk),
+                          lambda: gen_run_sparse_scan(p, compacts, hk, tk))
     elif rowmask:
         ks = J.kernel_for(scan_rows_shape(p, compacts, NI),
                           lambda: gen_run_scan_rows(p, compacts, NI))
@@ -1109,9 +1147,11 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
             vs["PK"] = pk.data_ptr()
         spans = (spans, tp64, pk)
         grid_s = max(1, SPARSE_GRID)
+    if tk is not None:
+        tk.bind(grid_s * (J.BLOCK // 64), dev)
     return TwoPhaseLauncher(kt, ks, grid_t, grid_s, GA, GA * 32 if _scan_grouped(p) else 0,
                             vt, vs, compacts, (rstart, rlen, rbucket, roff, tp, spans, tr, runs),
-                            tags, dev, rows, hk)
+                            tags, dev, rows, hk, tk if sparse else None)
 
 
 def semi_runs_agg(p: NL.JoinParams, rstart, rlen, compacts, runs, nrows: int, words, lo: int,

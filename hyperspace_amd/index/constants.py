@@ -114,6 +114,10 @@ JOIN_GRAPH_ENABLED_DEFAULT = "true"
 # lowering directly (exec/gpu.py _AggProgram), skipping the executor's plan walk
 PREPARED_SUBMIT_ENABLED = "spark.hyperspace.mi.preparedSubmit.enabled"
 PREPARED_SUBMIT_ENABLED_DEFAULT = "true"
+# ORDER BY <sum / count> LIMIT k over the key-run hash walk keeps whole keys in per-wavefront
+# top-K lists instead of hash-table slots (hash_agg.TopKPlan)
+RUN_TOPK_ENABLED = "spark.hyperspace.mi.runTopK.enabled"
+RUN_TOPK_ENABLED_DEFAULT = "true"
 # cached join index (left row -> first matching right row, int32 in HBM) for joins of two
 # device-resident index tables with unique integer right keys: the fused join aggregate becomes a
 # streaming scan of the left table plus a gather, no per-tile span search (exec/join_index.py)

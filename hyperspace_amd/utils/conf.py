@@ -134,6 +134,10 @@ class HyperspaceConf:
             _b(conf.get(C.JOIN_GRAPH_ENABLED, C.JOIN_GRAPH_ENABLED_DEFAULT))
 
     @staticmethod
+    def run_topk_enabled(conf) -> bool:
+        return _b(conf.get(C.RUN_TOPK_ENABLED, C.RUN_TOPK_ENABLED_DEFAULT))
+
+    @staticmethod
     def prepared_submit_enabled(conf) -> bool:
         return _b(conf.get(C.PREPARED_SUBMIT_ENABLED, C.PREPARED_SUBMIT_ENABLED_DEFAULT))
 

@@ -76,6 +76,29 @@ def test_tpch_q3_full_shape(tpch):  # noqa: F811
     # unique): the run-keyed two-phase join aggregates into the hash table and the top groups'
     # orders columns are looked up afterwards
     assert jit.LAST_MJ_PATH[0] == "runs_hash"
+    # whole keys went through the walk's per-wavefront top-K lists (hash_agg.TopKPlan) and the
+    # table kept only keys split across walk windows; same rows as the table-only walk
+    be = s.backend()
+    assert be.metrics.get("run_topk") == 1
+    s.conf.set("spark.hyperspace.mi.runTopK.enabled", "false")
+    g1, _, path = _both(s, q, sort=False)
+    s.conf.set("spark.hyperspace.mi.runTopK.enabled", "true")
+    assert path == "native" and jit.LAST_MJ_PATH[0] == "runs_hash"
+    _close(g1, c)
+    _close(g1, g)
+    # ascending order, a COUNT order key, and several literal vectors (a fresh walk each)
+    for dd, asc in (("1995-03-02", True), ("1995-03-20", False), ("1994-11-30", True)):
+        qa = li.join(od, li["l_orderkey"] == od["o_orderkey"]) \
+            .filter(f"o_orderdate < DATE '{dd}' AND l_shipdate > DATE '{dd}'") \
+            .groupBy("l_orderkey", "o_orderdate", "o_shippriority") \
+            .agg(sum_(col("l_extendedprice") * (1 - col("l_discount"))).alias("revenue"),
+                 count("*").alias("n")) \
+            .orderBy(col("n").asc() if asc else col("revenue").desc(), col("l_orderkey")) \
+            .limit(7)
+        ga, ca, path = _both(s, qa, sort=False)
+        assert path == "native", be.fallback_reason
+        assert be.metrics.get("run_topk") in (0, 1)
+        _close(ga, ca)
     s.conf.set("spark.hyperspace.mi.fdGroup.enabled", "false")
     g2, _, path = _both(s, q, sort=False)
     s.conf.set("spark.hyperspace.mi.fdGroup.enabled", "true")

