@@ -36,95 +36,31 @@ RUNTIME_PATH = os.path.join(_HERE, "_native", "libhs_runtime.so")
 CACHE_DIR = os.environ.get("HS_JIT_CACHE", os.path.join(_HERE, "_native", "jitcache"))
 
 BLOCK = 256
-SCAN_ITEMS = int(os.environ.get("HS_JIT_SCAN_ITEMS", "4"))
-# 512-row join tiles on a 16384-block grid measured best on MI355X (scripts/microbench_join.py,
-# profiles/microbench_join_r1*.jsonl): short per-tile latency chains, many blocks per CU in flight
-JOIN_ITEMS = int(os.environ.get("HS_JIT_JOIN_ITEMS", "2"))
-JOIN_BLOCK = int(os.environ.get("HS_JIT_JOIN_BLOCK", "256"))
-JOIN_LDS_KEYS = int(os.environ.get("HS_JIT_JOIN_LDS_KEYS", "2048"))
-SCAN_GRID = int(os.environ.get("HS_JIT_SCAN_GRID", "8192"))
-JOIN_GRID = int(os.environ.get("HS_JIT_JOIN_GRID", "16384"))
-# eager = load every needed column in the first batch (more bytes, one round trip fewer); the
-# sweep (profiles/microbench_join_r1c.jsonl) favoured lazy loads for both kernels
-JOIN_EAGER = os.environ.get("HS_JIT_JOIN_EAGER", "0") == "1"
-# stage the right side's columns of each tile's key span in LDS with the keys
-JOIN_STAGE_RIGHT = os.environ.get("HS_JIT_JOIN_STAGE_RIGHT", "1") == "1"
-SCAN_EAGER = os.environ.get("HS_JIT_SCAN_EAGER", "0") == "1"
-# rows per thread of the join-index kernel (phase-major: each phase's loads of all items in flight)
-JI_ITEMS = int(os.environ.get("HS_JIT_JI_ITEMS", "4"))
-# > 0: each thread of the join-index kernel owns JI_VEC consecutive rows and loads the streamed
-# left columns (join index, predicate columns) as aligned vectors (dwordx4 for 4 int32 rows)
-JI_VEC = int(os.environ.get("HS_JIT_JI_VEC", "8"))
-# join-index kernel: run the aggregate phase over a per-wavefront list of passing rows only
-JI_COMPACT = os.environ.get("HS_JIT_JI_COMPACT", "1") == "1"
-# join-index kernel phase 2 through a per-wavefront LDS copy of the matched right rows' run
-# (_ji_stage_phase2); measured slower than both alternatives on the Q3 shape, off by default
-JI_STAGE = os.environ.get("HS_JIT_JI_STAGE", "0") == "1"
-# join-index kernel phase 2 as a semi-join bitmap: the right side's predicates are evaluated
-# once per query over the right table into one bit per row (gen_pred_bitmap), and the join
-# kernel tests bits (cache-resident) instead of gathering right columns from HBM.  Off by
-# default: on the SF100 Q3 shape bitmap kernel + join measured no faster than the gathers
-# (profiles/qk_sweep_r2.jsonl)
-JI_BITMAP = os.environ.get("HS_JIT_JI_BITMAP", "0") == "1"
-# scan kernel: same, for the aggregate inputs loaded after the predicates
-SCAN_COMPACT = os.environ.get("HS_JIT_SCAN_COMPACT", "1") == "1"
-# > 0: rows per thread of the vectorized scan kernel (aligned vector loads of predicate columns)
-SCAN_VEC = int(os.environ.get("HS_JIT_SCAN_VEC", "8"))
-# software-pipeline the join's tile loop (next tile's batch loads overlap this tile's work)
-JOIN_PIPELINE = os.environ.get("HS_JIT_JOIN_PIPELINE", "1") == "1"
-# direct-address LDS table for dense integer key spans (one verified lookup instead of a
-# binary search); slots = key values a tile's right span may cover.  Off by default: it measured
-# 5.18 vs 3.98 ms on the SF100 Q3 shape (profiles/microbench_join_r1f_direct.jsonl) — the LDS
-# search is not on this kernel's critical path, the extra table writes and loads are
-JOIN_DIRECT = os.environ.get("HS_JIT_JOIN_DIRECT", "0") == "1"
-JOIN_DIRECT_SLOTS = int(os.environ.get("HS_JIT_JOIN_DIRECT_SLOTS", "2048"))
-# vectorized sort-merge join (gen_merge_join_agg): rows per thread (0 = the strided join_agg
-# kernel), LDS right-key slots per tile, grid
-MJ_ITEMS = int(os.environ.get("HS_JIT_MJ_ITEMS", "8"))
-MJ_LDS_KEYS = int(os.environ.get("HS_JIT_MJ_LDS_KEYS", "2048"))
-MJ_GRID = int(os.environ.get("HS_JIT_MJ_GRID", "8192"))
-MJ_STEPS = int(os.environ.get("HS_JIT_MJ_STEPS", "1"))   # branch-free walk steps per row
-# right-span staging: per-thread rows loaded per round trip (all loads of a round issue before
-# any LDS store), and double-buffered LDS spans (no end-of-tile barrier)
-MJ_STAGE_UNROLL = int(os.environ.get("HS_JIT_MJ_STAGE_UNROLL", "4"))
-MJ_DBUF = os.environ.get("HS_JIT_MJ_DBUF", "0") == "1"
-MJ_PREFETCH = os.environ.get("HS_JIT_MJ_PREFETCH", "0") == "1"
-# right-span prefetch: tile t+1's span bounds and first staging round are loaded into registers
-# at the top of tile t (span bounds of t+2 with them), so staging a tile's right keys is an LDS
-# store instead of two dependent HBM round trips at the head of every tile.  Off by default: it
-# measured 1.63 vs 1.40 ms at SF100 (profiles/mj_sweep_r3_rpf.jsonl; the staging share of the
-# kernel is ~0.22 ms: profiles/mj_decompose_r3.jsonl)
-MJ_RPF = os.environ.get("HS_JIT_MJ_RPF", "0") == "1"
-# workgroup size of the merge join: 64 = one wavefront per workgroup working its own 512-row
-# tiles (own right span, no block barriers), 256 = four wavefronts sharing 2048-row tiles
-MJ_BLOCK = int(os.environ.get("HS_JIT_MJ_BLOCK", "256"))
-# eager aggregate tail (no deferred match lists): _eager_tail
-MJ_EAGER = os.environ.get("HS_JIT_MJ_EAGER", "0") == "1"
-# match-list appends one set match bit per round (_sparse_append) instead of one per item
-MJ_SPARSE = os.environ.get("HS_JIT_MJ_SPARSE", "1") == "1"
-# hash-mode merge joins append matches lane-major (row order): _lanemajor_append
-MJ_HASH_LANEMAJOR = os.environ.get("HS_JIT_MJ_HASH_LANEMAJOR", "0") == "1"
-MJ_KEY32 = os.environ.get("HS_JIT_MJ_KEY32", "1") == "1"  # 32-bit merge images (_key32_frame)
-# left join key streamed as 16-bit codes over a per-64-row group base (encoding.grouped16) when
-# the key is only the join key: 2 bytes per left row instead of 4.  Off by default: exact, but
-# 1.51 vs 1.38 ms at SF100 (profiles/mj_sweep_r3_key16.jsonl) - the kernel is bound by its
-# per-tile dependent round trips, not by the bytes it streams
-MJ_KEY16 = os.environ.get("HS_JIT_MJ_KEY16", "0") == "1"
-# run-keyed merge join: a left key with a run-length form (encoding.RunCompact) streams which
-# run each row belongs to (gmask / gruns, 0.19 bytes per row) instead of its 4-byte key; the
-# tile's run keys are matched against the staged right span once per run, not once per row
-MJ_RUNS = os.environ.get("HS_JIT_MJ_RUNS", "1") == "1"
-# hash-mode GROUP BY over a run-keyed merge join whose group keys are left columns (the
-# functionally reduced TPC-H Q3 shape): the two-phase form with a hash walk (jit_runs)
-MJ_RUNS_HASH = os.environ.get("HS_JIT_MJ_RUNS_HASH", "1") == "1"
-MJ_RUNS_ITEMS = int(os.environ.get("HS_JIT_MJ_RUNS_ITEMS", "16"))
-MJ_RUNS_PREFETCH = os.environ.get("HS_JIT_MJ_RUNS_PREFETCH", "0") == "1"
-# cost-decomposition experiments only (wrong results): "nowalk" / "notail" / "nostage"
-MJ_EXP = os.environ.get("HS_JIT_MJ_EXP", "")
-# software-pipelined full tiles in the vectorized kernels (_vec_tiles)
-VEC_PREFETCH = os.environ.get("HS_JIT_VEC_PREFETCH", "1") == "1"
-# per-wavefront compaction lists ordered by a wavefront barrier instead of __syncthreads
-WAVE_SYNC = os.environ.get("HS_JIT_WAVE_SYNC", "1") == "1"
+# Code-generation tunables: the fields of ONE frozen exec.kernel_config.KernelConfig (defaults,
+# measurements and meaning are documented there), bound into these names by
+# kernel_config.bind(); generated kernel shape keys include them.
+from . import kernel_config as _KC  # noqa: E402
+_CFG = _KC.active()
+SCAN_ITEMS, SCAN_GRID, SCAN_VEC = _CFG.scan_items, _CFG.scan_grid, _CFG.scan_vec
+SCAN_COMPACT, SCAN_EAGER = _CFG.scan_compact, _CFG.scan_eager
+JOIN_ITEMS, JOIN_BLOCK, JOIN_LDS_KEYS, JOIN_GRID = (_CFG.join_items, _CFG.join_block,
+                                                    _CFG.join_lds_keys, _CFG.join_grid)
+JOIN_EAGER, JOIN_STAGE_RIGHT, JOIN_PIPELINE = (_CFG.join_eager, _CFG.join_stage_right,
+                                               _CFG.join_pipeline)
+JOIN_DIRECT, JOIN_DIRECT_SLOTS = _CFG.join_direct, _CFG.join_direct_slots
+JI_ITEMS, JI_VEC, JI_COMPACT, JI_STAGE, JI_BITMAP = (_CFG.ji_items, _CFG.ji_vec, _CFG.ji_compact,
+                                                     _CFG.ji_stage, _CFG.ji_bitmap)
+MJ_ITEMS, MJ_LDS_KEYS, MJ_GRID, MJ_STEPS = (_CFG.mj_items, _CFG.mj_lds_keys, _CFG.mj_grid,
+                                            _CFG.mj_steps)
+MJ_STAGE_UNROLL, MJ_BLOCK = _CFG.mj_stage_unroll, _CFG.mj_block
+MJ_DBUF, MJ_PREFETCH, MJ_RPF, MJ_EAGER = (_CFG.mj_dbuf, _CFG.mj_prefetch, _CFG.mj_rpf,
+                                          _CFG.mj_eager)
+MJ_SPARSE, MJ_HASH_LANEMAJOR = _CFG.mj_sparse, _CFG.mj_hash_lanemajor
+MJ_KEY32, MJ_KEY16 = _CFG.mj_key32, _CFG.mj_key16
+MJ_RUNS, MJ_RUNS_HASH, MJ_RUNS_ITEMS, MJ_RUNS_PREFETCH = (_CFG.mj_runs, _CFG.mj_runs_hash,
+                                                          _CFG.mj_runs_items,
+                                                          _CFG.mj_runs_prefetch)
+VEC_PREFETCH, WAVE_SYNC = _CFG.vec_prefetch, _CFG.wave_sync
 
 _CTYPE = {NL.I8: "signed char", NL.I16: "short", NL.I32: "int", NL.I64: "long long",
           NL.F32: "float", NL.F64: "double", NL.BOOL: "unsigned char", NL.U32: "unsigned int",
@@ -1507,7 +1443,7 @@ def merge_join_shape(p: NL.JoinParams, compacts=None, hk=None) -> tuple:
                  for i in range(p.naggs))
     return ("merge_join_agg", cols, preds, p.nlp, aggs, p.group_col, p.lkey, p.rkey,
             p.key_is_float, MJ_ITEMS, MJ_LDS_KEYS, MJ_STEPS, BLOCK, WAVE_SYNC,
-            _key32_frame(p, compacts) is not None, MJ_EXP, MJ_STAGE_UNROLL, MJ_DBUF, MJ_PREFETCH,
+            _key32_frame(p, compacts) is not None, MJ_STAGE_UNROLL, MJ_DBUF, MJ_PREFETCH,
             MJ_BLOCK, MJ_EAGER, MJ_SPARSE, MJ_HASH_LANEMAJOR, MJ_RPF and not MJ_PREFETCH, MJ_KEY16,
             hk.shape() if hk is not None else None, MJ_RUNS, MJ_RUNS_ITEMS, MJ_RUNS_PREFETCH)
 
@@ -1849,7 +1785,7 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
         # (1) stage the right span: key images + right-only predicate pass bytes; each round
         # issues the loads of U rows per thread before any store (one HBM round trip per round
         # instead of one per row)
-        stg = "staged && false" if "nostage" in MJ_EXP else "staged"
+        stg = "staged"
         okk_fmt = f"n{rk}_s{{u}}" if cols[rk][1] else "true"
 
         def stage_stores(i2: str) -> None:
@@ -1941,8 +1877,6 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
                           f"{ind}    mtb |= ({bit('mb', it)} && v == ke && jw < ns) ? {1 << it}u : 0u; "
                           f"jl{it} = jw; }}"])
             b.append(f"{ind}}}")
-            if "nowalk" in MJ_EXP:
-                b.append(f"{ind}mtb = mb; slow = false;")
             b.extend([f"{ind}if (__any(slow)) {{",
                       f"{ind}  if (slow) {{ int jw = jw0; mtb = 0u;"])
             for it in range(NI):
@@ -1984,9 +1918,7 @@ def gen_merge_join_agg(p: NL.JoinParams, compacts=None, hk=None) -> Kernel:
                         _uload(g2, sl, f"{it}m", b, i2 + "  ")
                     cond = _rename(_rename(g2.cnf(mixed), mixed_right, f"{it}m"), first, it)
                     b.append(f"{i2}  pb &= ({cond}) ? ~0u : ~{1 << it}u; }}")
-            if "notail" in MJ_EXP:
-                b.append(f"{i2}cnt0 += __popc(pb);")
-            elif eager:
+            if eager:
                 b.extend(_eager_tail(args, cols, split, approx, aggs, grouped, p.group_col,
                                      allslots, rtail, NI, i2))
             else:

@@ -30,11 +30,12 @@ from ..ops import _lib as NL
 from . import jit as J
 
 SPLIT = 8
-RT_UNROLL = 4
-# 2 phases on by default; HS_JIT_MJ_2P=0 keeps the single-kernel merge join
-import os  # noqa: E402
-MJ_2P = os.environ.get("HS_JIT_MJ_2P", "1") == "1"
-RS_ITEMS = int(os.environ.get("HS_JIT_RS_ITEMS", "16"))
+# tunables: fields of exec.kernel_config.KernelConfig (bound by kernel_config.bind)
+from . import kernel_config as _KC  # noqa: E402
+_CFG = _KC.active()
+MJ_2P, RS_ITEMS = _CFG.mj_2p, _CFG.rs_items
+RT2_UNROLL, RT2_GRID = _CFG.rt2_unroll, _CFG.rt2_grid
+RS_BITS, RS_BITS_GRID, RS_PACK = _CFG.rs_bits, _CFG.rs_bits_grid, _CFG.rs_pack
 
 
 def tag_width(p: NL.JoinParams) -> int:
@@ -70,161 +71,16 @@ def _lpreds(p):
     return [(k, p.preds[k]) for k in range(p.nlp)]
 
 
-def tags_shape(p: NL.JoinParams, compacts, W: int, T: int) -> tuple:
-    cols = tuple(sorted((s, c) for s, c in J._col_specs(p, compacts).items()
-                        if s >= SPLIT or s == p.lkey))
-    preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
-                   p.preds[k].group) for k in range(p.nlp, p.npreds))
-    return ("run_tags", cols, preds, p.nlp, p.lkey, p.rkey, p.group_col >= SPLIT and p.group_col,
-            W, T, J.MJ_LDS_KEYS, RT_UNROLL, J.BLOCK)
+# phase 1: 64-run groups per unrolled iteration of a wavefront (gen_run_tags2)
 
 
-def gen_run_tags(p: NL.JoinParams, compacts, W: int, T: int) -> J.Kernel:
-    """Phase 1 (module docstring).  ``T`` = left rows per merge-join tile (its runs <= T)."""
-    args = J.Args()
-    for n, ct in (("tile_prefix", "const long long*"), ("spans", "const long long*"),
-                  ("TR", "const int*")):
-        args.add("p", n, ct)
-    lk, rk = p.lkey, p.rkey
-    args.add("p", f"RK{lk}", "const int*")
-    args.add("p", "tags", "unsigned*")
-    args.add("q", "R", "long long")
-    for n in ("KLO", "KSP", "KOF"):
-        args.add("q", n, "long long")
-    cols = J._col_specs(p, compacts)
-    rpreds = _rpreds(p)
-    rgroup = p.group_col >= SPLIT
-    stage_slots = list(dict.fromkeys([rk] + J._pred_slots(rpreds) +
-                                     ([p.group_col] if rgroup else [])))
-    LK = J.MJ_LDS_KEYS  # noqa: N806 — right span keys staged per tile (longer: HBM search)
-    BLOCK = J.BLOCK  # noqa: N806
-    U = RT_UNROLL  # noqa: N806
-    NW = (T * W + 31) // 32 + 2  # noqa: N806 — LDS tag words of one tile
-    MASK = (1 << W) - 1  # noqa: N806
-    g = J._Gen(args, cols, SPLIT, ("row0", "row0"), frozenset(), True)
-    if rgroup:
-        gb = args.add("q", "group_base", "long long")
-        ng = args.add("q", "num_groups", "long long")
-
-    def rimg(val: str) -> str:
-        return (f"({{ const i64 d_ = (i64)({val}) - a.KLO; "
-                f"d_ < 0 ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); }})")
-
-    def tag_expr(gen: J._Gen, it, ok: str) -> str:
-        cond = J._rename(gen.cnf(rpreds), stage_slots, it)
-        if not rgroup:
-            return f"(({ok}) && {cond} ? 1u : 0u)"
-        gx = J._rename(f"x{p.group_col}", stage_slots, it)
-        return (f"({{ const i64 gl_ = (i64){gx} - {gb}; (({ok}) && {cond} && gl_ >= 0 && "
-                f"gl_ < {ng}) ? (unsigned)(gl_ + 1) : 0u; }})")
-
-    b: List[str] = [
-        f"  __shared__ unsigned skeys[{LK + 1}]; __shared__ unsigned char stag[{LK}];",
-        f"  __shared__ unsigned lrk_[{T}]; __shared__ unsigned tw_[{NW}];"]
-    b += J._TILE_HEAD
-    b += ["  for (i64 t = t0; t < t1; ++t) {",
-          "    const i64 ss = a.spans[4 * t + 2], se = a.spans[4 * t + 3];",
-          "    const int ra = a.TR[2 * t], nl = a.TR[2 * t + 1];",
-          "    const int ns = (int)(se - ss);",
-          f"    const bool staged = ns <= {LK};",
-          f"    const i64 wlo = ((i64)ra * {W}) >> 5;",
-          f"    const int nw = (int)((((i64)(ra + nl) * {W} + 31) >> 5) - wlo);",
-          f"    for (int q = (int)threadIdx.x; q < nw; q += {BLOCK}) tw_[q] = 0u;",
-          f"    for (int q = (int)threadIdx.x; q < nl; q += {BLOCK}) "
-          f"lrk_[q] = (unsigned)a.RK{lk}[ra + q] + (unsigned)a.KOF;"]
-    ind = "      "
-    rkv = J._valid_expr(g, rk, "{r}")
-    b.append(f"    if (staged) for (int sqb = 0; sqb < ns; sqb += {BLOCK * U}) {{")
-    for u in range(U):
-        b += [f"{ind}const int sq{u} = sqb + {u * BLOCK} + (int)threadIdx.x;",
-              f"{ind}const bool sv{u} = sq{u} < ns;",
-              f"{ind}const i64 jr{u} = ss + (sv{u} ? sq{u} : 0);"]
-    for u in range(U):
-        gs = J._Gen(args, cols, SPLIT, (f"jr{u}", f"jr{u}"), frozenset(), True)
-        for sl in stage_slots:
-            J._uload(gs, sl, f"s{u}", b, ind)
-    for u in range(U):
-        gs = J._Gen(args, cols, SPLIT, (f"jr{u}", f"jr{u}"), frozenset(), True)
-        kv = f"n{rk}_s{u}" if cols[rk][1] else "true"
-        b += [f"{ind}if (sv{u}) {{ const bool kv = {kv};",
-              f"{ind}  skeys[sq{u}] = kv ? {rimg(f'x{rk}_s{u}')} : 0u;",
-              f"{ind}  stag[sq{u}] = (unsigned char){tag_expr(gs, f's{u}', 'kv')}; }}"]
-    b += ["    }",
-          "    if (staged && threadIdx.x == 0) skeys[ns] = 0xFFFFFFFFu;   // walk sentinel",
-          "    __syncthreads();",
-          # each thread: a contiguous chunk of the tile's runs
-          f"    {{ const int c_ = (nl + {BLOCK - 1}) / {BLOCK};",
-          "      const int q0 = (int)threadIdx.x * c_;",
-          "      const int q1 = q0 + c_ < nl ? q0 + c_ : nl;",
-          "      int cw = -1; unsigned cb = 0u;",
-          "      int j_ = 0;",
-          "      if (staged && q0 < q1) { const unsigned key_ = lrk_[q0]; int lo = 0;",
-          "        for (int st = ns > 0 ? (1 << (31 - __builtin_clz(ns))) : 0; st > 0; st >>= 1) {",
-          "          const int c = lo + st; lo = (c <= ns && skeys[c - 1] < key_) ? c : lo; }",
-          "        j_ = lo; }",
-          "      for (int q = q0; q < q1; ++q) {",
-          "        const unsigned key_ = lrk_[q];",
-          "        unsigned tg = 0u;",
-          "        if (staged) {",
-          "          if (skeys[j_] < key_) { ++j_;",
-          "            if (skeys[j_] < key_) { int lo = j_ + 1, hi = ns;",
-          "              while (lo < hi) { const int m = (lo + hi) >> 1; "
-          "if (skeys[m] < key_) lo = m + 1; else hi = m; }",
-          "              j_ = lo; } }",
-          "          tg = (j_ < ns && skeys[j_] == key_) ? (unsigned)stag[j_] : 0u;",
-          "        } else {",
-          "          i64 lo = ss, hi = se;",
-          f"          while (lo < hi) {{ const i64 md = (lo + hi) >> 1; const bool nv = "
-          f"{rkv.format(r='md')};",
-          f"            if (nv || {rimg(g.value(rk, 'md'))} < key_) lo = md + 1; else hi = md; }}",
-          f"          const bool hit = lo < se && !({rkv.format(r='lo')}) && "
-          f"{rimg(g.value(rk, 'lo'))} == key_;",
-          "          const i64 jg = hit ? lo : ss;"]
-    gg = J._Gen(args, cols, SPLIT, ("jg", "jg"), frozenset(), True)
-    for sl in stage_slots:
-        J._uload(gg, sl, "g", b, "          ")
-    b += [f"          tg = {tag_expr(gg, 'g', 'hit')};",
-          "        }",
-          f"        const i64 bit = (i64)(ra + q) * {W};",
-          "        const int wi = (int)((bit >> 5) - wlo);",
-          "        if (wi != cw) { if (cb) atomicOr(&tw_[cw], cb); cw = wi; cb = 0u; }",
-          f"        cb |= (tg & {MASK}u) << (unsigned)(bit & 31);",
-          "      }",
-          "      if (cb) atomicOr(&tw_[cw], cb);",
-          "    }",
-          "    __syncthreads();",
-          # whole words leave with plain stores; the tile's edge words (shared with the
-          # neighbouring tiles' runs) with an OR into the zeroed bitmap
-          f"    for (int q = (int)threadIdx.x; q < nw; q += {BLOCK}) {{",
-          "      const i64 gw = wlo + q; const unsigned v = tw_[q];",
-          f"      const bool whole = gw * 32 >= (i64)ra * {W} && gw * 32 + 32 <= (i64)(ra + nl) * {W};",
-          "      if (whole) a.tags[gw] = v; else if (v) atomicOr(&a.tags[gw], v);",
-          "    }",
-          "    __syncthreads();",
-          "  }"]
-    src = (J._PRELUDE + args.struct_src() +
-           f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_run_tags(Args a) {{\n' +
-           "\n".join(b) + "\n}\n")
-    return J.Kernel(src, "hs_jit_run_tags", args)
-
-
-# phase 1, direct form: 64-run groups per unrolled iteration of a wavefront
-RT2_UNROLL = int(os.environ.get("HS_JIT_RT2_UNROLL", "4"))
-# 1: phase 1 maps runs to right rows by guess-and-verify (gen_run_tags2); 0: per-tile LDS search
-RT2 = os.environ.get("HS_JIT_RT2", "1") == "1"
-RT2_GRID = int(os.environ.get("HS_JIT_RT2_GRID", "8192"))
-# 1: phase 1 reads 16-bit grouped run keys and right keys (encoding.group16 / grouped16)
-RT2_K16 = os.environ.get("HS_JIT_RT2_K16", "0") == "1"
-RT2_MAX_WIDE = 0.1   # at most this share of 64-key groups spanning >= 2^16 codes
-
-
-def tags2_shape(p: NL.JoinParams, compacts, W: int, k16: bool = False) -> tuple:
+def tags2_shape(p: NL.JoinParams, compacts, W: int) -> tuple:
     cols = tuple(sorted((s, c) for s, c in J._col_specs(p, compacts).items()
                         if s >= SPLIT or s == p.lkey))
     preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
                    p.preds[k].group) for k in range(p.nlp, p.npreds))
     return ("run_tags2", cols, preds, p.nlp, p.lkey, p.rkey, _tags_grouped(p) and p.group_col,
-            W, RT2_UNROLL, J.BLOCK, k16)
+            W, RT2_UNROLL, J.BLOCK)
 
 
 def _stage_slots(p: NL.JoinParams) -> list:
@@ -240,7 +96,7 @@ def _tags_grouped(p: NL.JoinParams) -> bool:
     return p.group_col >= SPLIT and p.num_groups > 1
 
 
-def gen_run_tags2(p: NL.JoinParams, compacts, W: int, k16: bool = False) -> J.Kernel:
+def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
     """Phase 1, direct form: no tiles and no LDS.  Each wavefront owns a contiguous chunk of
     64-run groups of the left run list (so it owns whole 2W-word stretches of the tag bitmap
     and stores them without atomics).  Lane l of a group guesses the right row of its run: the
@@ -252,18 +108,11 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int, k16: bool = False) -> J.Ke
     trip; RT2_UNROLL groups are in flight per iteration.
 
     Ranges (``RNG``, NRG x 4 int64, sorted by first run): [first run, end run) of each left row
-    range and the right bucket's rows [s0, s1).
-
-    ``k16``: the run keys are read as 16-bit offsets from a per-64-run-group base (one scalar
-    load per group; a wide group reads the 32-bit keys), and a right key in its grouped 16-bit
-    form (``encoding.GroupedCompact``: signature (2, False, 64)) likewise - 2 instead of 4 bytes
-    per key on both sides."""
+    range and the right bucket's rows [s0, s1).  (16-bit grouped run keys measured 0.59 vs
+    0.29 ms - more dependent loads per run - and a per-tile LDS form 0.79 ms: both removed.)"""
     args = J.Args()
     lk, rk = p.lkey, p.rkey
     args.add("p", f"RK{lk}", "const int*")
-    if k16:
-        args.add("p", f"RKS{lk}", "const unsigned short*")
-        args.add("p", f"RKB{lk}", "const int*")
     args.add("p", "RNG", "const long long*")
     args.add("p", "tags", "unsigned*")
     for n in ("NRG", "NRUNS", "KLO", "KSP", "KOF"):
@@ -363,14 +212,8 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int, k16: bool = False) -> J.Ke
                   f"a1_{u} = RG[4 * q_ + 3]; }}"])
         b.extend([f"{ind}const bool act{u} = in{u} && r{u} < a.NRUNS && r{u} >= l0_{u} && "
               f"r{u} < l1_{u} && a1_{u} > a0_{u};",
-              (f"{ind}const int kb{u} = a.RKB{lk}[gi + {u} < G ? gi + {u} : G - 1];\n"
-               f"{ind}const bool kw{u} = kb{u} == (int)0x80000000;\n"
-               f"{ind}const unsigned short ks{u} = a.RKS{lk}[act{u} ? r{u} : 0];\n"
-               f"{ind}const int kx{u} = a.RK{lk}[(act{u} && kw{u}) ? r{u} : 0];\n"
-               f"{ind}const unsigned key{u} = (unsigned)(kw{u} ? (i64)kx{u} : "
-               f"(i64)kb{u} + (i64)ks{u}) + (unsigned)a.KOF;") if k16 else
-              (f"{ind}const unsigned key{u} = (unsigned)a.RK{lk}[act{u} ? r{u} : 0] + "
-               f"(unsigned)a.KOF;"),
+              f"{ind}const unsigned key{u} = (unsigned)a.RK{lk}[act{u} ? r{u} : 0] + "
+              f"(unsigned)a.KOF;",
               f"{ind}i64 j{u} = (own{u} && gbase >= 0) ? gbase + {u * 64} + lane : "
               f"a0_{u} + (r{u} - l0_{u});",
               f"{ind}j{u} = act{u} ? (j{u} < a0_{u} ? a0_{u} : (j{u} >= a1_{u} ? a1_{u} - 1 : j{u}))"
@@ -566,89 +409,9 @@ def gen_run_scan(p: NL.JoinParams, compacts, W: int, NI: int) -> J.Kernel:
     return J.Kernel(src, "hs_jit_run_scan", args, lds)
 
 
-# 1: a 1-bit tag bitmap is expanded to a row mask (hs_run_rowmask) and the scan skips the
-# predicate loads of rows no tagged run holds (gen_run_scan_rows)
-ROWMASK = os.environ.get("HS_JIT_RS_ROWMASK", "1") == "1"
-
-
-def scan_rows_shape(p: NL.JoinParams, compacts, NI: int) -> tuple:
-    return ("run_scan_rows",) + scan_shape(p, compacts, 1, NI)[1:]
-
-
-def gen_run_scan_rows(p: NL.JoinParams, compacts, NI: int) -> J.Kernel:
-    """Phase 2 over a row mask (1-bit tags expanded per row): each thread's NI rows take their
-    mask bits from the 64-bit word of their group (prefetched one tile ahead with the tile
-    geometry), and the left predicate columns are loaded only by threads with a set bit - so the
-    predicate stream shrinks to the rows of matching runs - then the compacted aggregate tail
-    runs over the rows passing both."""
-    args = J.Args()
-    for n, ct in (("rstart", "const long long*"), ("rlen", "const long long*"),
-                  ("tile_prefix", "const long long*")):
-        args.add("p", n, ct)
-    args.add("p", "RM", "const unsigned long long*")
-    args.add("q", "R", "long long")
-    args.add("q", "nrows", "long long")
-    J._common_args(args)
-    cols = J._col_specs(p, compacts)
-    lpreds = _lpreds(p)
-    aggs = [p.aggs[i] for i in range(p.naggs)]
-    grouped = _scan_grouped(p)
-    assert not (grouped and p.group_col >= SPLIT)
-    pslots = J._pred_slots(lpreds)
-    tail = J._agg_slots(aggs) + ([p.group_col] if grouped else [])
-    allslots = list(dict.fromkeys(pslots + tail))
-    approx = J._sum_only_slots(lpreds, aggs, p.group_col if grouped else -1, cols)
-    BLOCK = J.BLOCK  # noqa: N806
-    T = BLOCK * NI  # noqa: N806
-    ind = "    "
-    g1 = J._Gen(args, cols, SPLIT, ("row0", "row0"), approx, True)
-    b: List[str] = []
-    b += J._acc_decls(aggs, grouped, args)
-    loads = J._vec_loads(g1, pslots)
-
-    def body(b: List[str], full: bool) -> None:
-        b.append(f"{ind}const unsigned bits_ = (unsigned)((rm_ >> (unsigned)(g0 & 63)) & "
-                 f"{(1 << NI) - 1}ull);")
-        for name, ct, ptr in loads:
-            b.append(f"{ind}{ct} {name}v[{NI}];")
-            if full:
-                b.append(f"{ind}if (bits_) {{ vload<{ct}, {NI}>({ptr}, g0, {name}v); }} else {{ " +
-                         " ".join(f"{name}v[{k}] = ({ct})0;" for k in range(NI)) + " }")
-            else:
-                b.append(f"{ind}" + " ".join(
-                    f"{name}v[{k}] = (act{k} && ((bits_ >> {k}) & 1u)) ? {ptr}[g0 + {k}] : "
-                    f"({ct})0;" for k in range(NI)))
-        J._vec_load_slots(b, g1, pslots, NI, ind)
-        for it in range(NI):
-            gi = J._Gen(args, cols, SPLIT, (f"row{it}", f"row{it}"), approx, True)
-            b.append(f"{ind}const bool pass{it} = act{it} && ((bits_ >> {it}) & 1u) && "
-                     f"{J._rename(gi.cnf(lpreds), allslots, it)};")
-        b.extend(J._compacted_tail(args, cols, SPLIT, approx, aggs, grouped, p.group_col,
-                                   tail, allslots, NI, ind, with_j=False))
-
-    gw = "((G0 < a.nrows ? G0 : a.nrows - 1) >> 6)"
-    J._vec_tiles(b, T, NI, ind, [], [("rm_", "unsigned long long", f"a.RM[{gw}]")], body)
-    b += ["  }"]
-    b += J._flush(aggs, grouped)
-    Wv = BLOCK // 64  # noqa: N806
-    pre = [f"  typedef {J._crow_t(T)} crow_t; __shared__ crow_t crow_s[{Wv}][{64 * NI}];",
-           "  const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;"]
-    src = (J._PRELUDE + args.struct_src() +
-           f'extern "C" __global__ __launch_bounds__({BLOCK}) void hs_jit_run_scan_rows(Args a) '
-           f'{{\n' + "\n".join(pre + b) + "\n}\n")
-    lds = (len(aggs) * p.num_groups * 32) if grouped else 0
-    return J.Kernel(src, "hs_jit_run_scan_rows", args, lds)
-
-
-# 1: phase 2 for 1-bit tags evaluates its masks 64 rows at a time (gen_run_bits_scan)
-SPARSE = os.environ.get("HS_JIT_RS_BITS", "1") == "1"
-SPARSE_GRID = int(os.environ.get("HS_JIT_RS_BITS_GRID", "8192"))
-
-
-# 1: the bits scan reads its aggregate inputs from one row-packed 64-bit word per row
-# (pack_layout / packed_tail) when they fit: one scattered fetch per passing row instead of one
-# per column
-PACK_TAIL = os.environ.get("HS_JIT_RS_PACK", "1") == "1"
+# phase 2 for 1-bit tags: masks 64 rows at a time (gen_run_sparse_scan; RS_BITS), aggregate
+# inputs read row-packed when they fit one 64-bit word (pack_layout / packed_tail; RS_PACK).  (A
+# row-mask expansion between the phases with a gated dense scan measured no faster: removed.)
 
 
 def _tail_slots(p: NL.JoinParams) -> list:
@@ -660,7 +423,7 @@ def _tail_slots(p: NL.JoinParams) -> list:
 def pack_layout(p: NL.JoinParams, compacts) -> Optional[tuple]:
     """((slot, bit offset, code bytes), ...) of the row-packed aggregate inputs of the bits
     scan: two or more compact-coded tail columns without validity whose codes fit 64 bits."""
-    if not PACK_TAIL:
+    if not RS_PACK:
         return None
     slots = _tail_slots(p)
     if len(slots) < 2:
@@ -956,15 +719,13 @@ class TwoPhaseLauncher:
     """Both phases lowered once (kernels, tiles, spans, per-tile run windows, the tag bitmap);
     ``launch(p)`` fills the literal slots and queues: bitmap clear, tags, scan, partials fold."""
     __slots__ = ("kt", "ks", "grid_t", "grid_s", "GA", "shmem", "vt", "vs", "compacts", "keep",
-                 "tags", "dev", "rows", "blocks", "hk", "graph", "gblocks", "tk")
+                 "tags", "dev", "blocks", "hk", "graph", "gblocks", "tk")
 
     def __init__(self, kt, ks, grid_t, grid_s, GA, shmem, vt, vs, compacts, keep, tags, dev,
-                 rows=None, hk=None, tk=None):
+                 hk=None, tk=None):
         self.kt, self.ks, self.grid_t, self.grid_s = kt, ks, grid_t, grid_s
         self.GA, self.shmem, self.vt, self.vs = GA, shmem, vt, vs
         self.compacts, self.keep, self.tags, self.dev = compacts, keep, tags, dev
-        # row-mask expansion between the phases: (gmask ptr, gruns ptr, g0, g1, mask tensor)
-        self.rows = rows
         # literal vector -> (phase-1 block, phase-2 block template): a repeated parameter set
         # re-packs only the per-launch partials pointers
         self.blocks: dict = {}
@@ -976,9 +737,8 @@ class TwoPhaseLauncher:
         self.gblocks: dict = {}
 
     def graphable(self) -> bool:
-        """Whether one query's launches can be captured: the direct phase 1 (no bitmap clear),
-        no row-mask expansion between the phases, partials out (not the hash mode)."""
-        return self.hk is None and self.rows is None and "RNG" in self.vt
+        """Whether one query's launches can be captured: partials out (not the hash mode)."""
+        return self.hk is None
 
     def launch(self, p: NL.JoinParams, key=None, htab=None, hk=None, graph: bool = False):
         """Queue one query.  Returns the (sum, count, min, max) device outputs, or with
@@ -1033,13 +793,8 @@ class TwoPhaseLauncher:
                     self.gblocks.clear()
                 self.gblocks[key] = gb
             return GraphPending(g, g.launch(*gb))
-        if "RNG" not in self.vt:  # the tile form ORs into a zeroed bitmap; the direct form
-            self.tags.zero_()     # stores every word of every run group
+        # (phase 1 stores every word of every run group: no bitmap clear)
         self.kt.launch_packed(self.grid_t, hit[0], st)
-        if self.rows is not None:
-            gm, gr, g0, g1, rm = self.rows
-            NL.check(NL.lib().hs_run_rowmask(gm, gr, self.tags.data_ptr(), g0, g1, rm.data_ptr(),
-                                             st), "hs_run_rowmask")
         parts = J._partials(self.grid_s, self.GA, self.dev)
         bs = bytearray(hit[1])
         a = self.ks.args
@@ -1053,12 +808,12 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
           cache_spans: bool, hk=None, tk=None) -> Optional[TwoPhaseLauncher]:
     """The two-phase launcher of a run-keyed merge join, or None when it does not apply.
     ``hk``: group by that hash key plan (left-side key columns only) through the bits scan's
-    hash mode (needs 1-bit tags and the direct phase 1)."""
+    hash mode (needs 1-bit tags).  None for an empty right side too (nothing to match)."""
     import torch
-    if not applies(p) or runs is None:
+    if not applies(p) or runs is None or int(roff[-1].item()) <= 0:
         return None
-    if hk is not None and (not SPARSE or not RT2 or tag_width(p) != 1 or _scan_grouped(p) or
-                           any(s >= SPLIT for s in hk.slots) or int(roff[-1].item()) <= 0):
+    if hk is not None and (not RS_BITS or tag_width(p) != 1 or _scan_grouped(p) or
+                           any(s >= SPLIT for s in hk.slots)):
         return None
     W = tag_width(p)
     NI = RS_ITEMS if RS_ITEMS and 64 % RS_ITEMS == 0 else J._mj_items(True)
@@ -1067,16 +822,12 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
     max_tiles = nrows // T + 2 * rstart.numel() + 2
     tp, spans = J._join_spans(p, rstart, rlen, rbucket, roff, max_tiles, T, cache_spans, align=NI)
     onebit = W == 1 and not (_scan_grouped(p) and p.group_col >= SPLIT)
-    sparse = SPARSE and onebit
-    rowmask = ROWMASK and onebit and not sparse
+    sparse = RS_BITS and onebit
     if tk is not None and hk is None:
         tk = None
     if sparse:
         ks = J.kernel_for(sparse_shape(p, compacts, hk, tk),
                           lambda: gen_run_sparse_scan(p, compacts, hk, tk))
-    elif rowmask:
-        ks = J.kernel_for(scan_rows_shape(p, compacts, NI),
-                          lambda: gen_run_scan_rows(p, compacts, NI))
     else:
         ks = J.kernel_for(scan_shape(p, compacts, W, NI),
                           lambda: gen_run_scan(p, compacts, W, NI))
@@ -1085,56 +836,20 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
     nwords = max((nruns * W + 31) >> 5, ((nruns + 63) >> 6) * 2 * W)
     tags = torch.empty(nwords + KW + 2, dtype=torch.int32, device=dev)
     frame = J._key32_frame(p, compacts)
-    tcomp = compacts
-    if RT2 and int(roff[-1].item()) > 0:
-        rng = run_ranges(rstart, rlen, rbucket, roff, runs)
-        rng_d = torch.from_numpy(rng.reshape(-1).copy() if len(rng) else
-                                 __import__("numpy").zeros(4, "int64")).to(dev)
-        lk16 = runs.keys16(RT2_MAX_WIDE) if RT2_K16 else None
-        if lk16 is not None:
-            from .encoding import GroupedCompact, grouped16
-            rc = compacts.get(p.rkey)
-            if rc is not None and not isinstance(rc, GroupedCompact) and \
-                    p.rkey not in _stage_slots(p):
-                r16 = grouped16(rc, RT2_MAX_WIDE)
-                if r16 is not None:
-                    tcomp = dict(compacts)
-                    tcomp[p.rkey] = r16
-        k16 = lk16 is not None
-        kt = J.kernel_for(tags2_shape(p, tcomp, W, k16),
-                          lambda: gen_run_tags2(p, tcomp, W, k16))
-        vt = {"RNG": rng_d.data_ptr(), "NRG": len(rng), "NRUNS": nruns, "tags": tags.data_ptr(),
-              "num_groups": p.num_groups, "group_base": p.group_base}
-        if k16:
-            vt[f"RKS{p.lkey}"] = lk16[0].data_ptr()
-            vt[f"RKB{p.lkey}"] = lk16[1].data_ptr()
-        tr = (rng_d, lk16)
-        grid_t = max(1, RT2_GRID)
-    else:
-        tr = J._tile_runs(tp, spans, rstart.numel(), runs, max_tiles, cache_spans)
-        kt = J.kernel_for(tags_shape(p, compacts, W, T), lambda: gen_run_tags(p, compacts, W, T))
-        vt = {"tile_prefix": tp.data_ptr(), "spans": spans.data_ptr(), "TR": tr.data_ptr(),
-              "tags": tags.data_ptr(), "R": rstart.numel(),
-              "num_groups": p.num_groups, "group_base": p.group_base}
-        grid_t = max(1, J.MJ_GRID)
+    rng = run_ranges(rstart, rlen, rbucket, roff, runs)
+    rng_d = torch.from_numpy(rng.reshape(-1).copy() if len(rng) else
+                             __import__("numpy").zeros(4, "int64")).to(dev)
+    kt = J.kernel_for(tags2_shape(p, compacts, W), lambda: gen_run_tags2(p, compacts, W))
+    vt = {"RNG": rng_d.data_ptr(), "NRG": len(rng), "NRUNS": nruns, "tags": tags.data_ptr(),
+          "num_groups": p.num_groups, "group_base": p.group_base}
+    tr = rng_d
+    grid_t = max(1, RT2_GRID)
     vt["KLO"], vt["KSP"], vt["KOF"] = frame
-    J._fill_cols(vt, p.cols, tcomp)
+    J._fill_cols(vt, p.cols, compacts)
     vs = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
           "tags": tags.data_ptr(), "R": rstart.numel(), "nrows": nrows,
           "num_groups": p.num_groups, "group_base": p.group_base}
     J._fill_cols(vs, p.cols, compacts)
-    rows = None
-    if rowmask:
-        # the 64-row groups the left ranges touch (the mask is read for those only)
-        import numpy as np
-        rs = rstart.cpu().numpy().astype(np.int64)
-        rl = rlen.cpu().numpy().astype(np.int64)
-        nz = rl > 0
-        g0 = int((rs[nz].min() >> 6)) if nz.any() else 0
-        g1 = int((((rs[nz] + rl[nz]).max() + 63) >> 6)) if nz.any() else 0
-        rm = torch.zeros(max((nrows + 63) >> 6, 1), dtype=torch.int64, device=dev)
-        rows = (runs.gmask.data_ptr(), runs.gruns.data_ptr(), g0, g1, rm)
-        vs["RM"] = rm.data_ptr()
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)
     grid_s = max(1, J.SCAN_GRID or NL.lib().hs_scan_grid())
     if sparse:
@@ -1146,12 +861,12 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
         if pk is not None:
             vs["PK"] = pk.data_ptr()
         spans = (spans, tp64, pk)
-        grid_s = max(1, SPARSE_GRID)
+        grid_s = max(1, RS_BITS_GRID)
     if tk is not None:
         tk.bind(grid_s * (J.BLOCK // 64), dev)
     return TwoPhaseLauncher(kt, ks, grid_t, grid_s, GA, GA * 32 if _scan_grouped(p) else 0,
                             vt, vs, compacts, (rstart, rlen, rbucket, roff, tp, spans, tr, runs),
-                            tags, dev, rows, hk, tk if sparse else None)
+                            tags, dev, hk, tk if sparse else None)
 
 
 def semi_runs_agg(p: NL.JoinParams, rstart, rlen, compacts, runs, nrows: int, words, lo: int,
@@ -1183,7 +898,7 @@ def semi_runs_agg(p: NL.JoinParams, rstart, rlen, compacts, runs, nrows: int, wo
     if pk is not None:
         vs["PK"] = pk.data_ptr()
     GA = p.naggs * (p.num_groups if p.group_col >= 0 else 1)  # noqa: N806
-    grid = max(1, SPARSE_GRID)
+    grid = max(1, RS_BITS_GRID)
     parts = J._partials(grid, GA, dev)
     vs.update({"psum": parts[0].data_ptr(), "pcnt": parts[1].data_ptr(),
                "pmin": parts[2].data_ptr(), "pmax": parts[3].data_ptr()})

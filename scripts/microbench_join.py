@@ -35,6 +35,8 @@ def main():
     import pyarrow as pa
     import torch
     from hyperspace_amd.exec import jit
+    from hyperspace_amd.exec import kernel_config
+    base = kernel_config.active()
     from hyperspace_amd.exec.device_table import DeviceColumn
     from hyperspace_amd.ops import _lib as NL
     from hyperspace_amd.ops import kernels as K
@@ -111,9 +113,10 @@ def main():
             for block in [int(x) for x in args.blocks.split(",")]:
                 for items in [int(x) for x in args.items.split(",")]:
                     for grid in [int(x) for x in args.grids.split(",")]:
-                        jit.JOIN_ITEMS, jit.JOIN_GRID, jit.JOIN_EAGER = items, grid, eager
-                        jit.JOIN_BLOCK, jit.JOIN_STAGE_RIGHT = block, stage
-                        jit.JOIN_PIPELINE, jit.JOIN_DIRECT = pipe, direct
+                        kernel_config.bind(base.replace(
+                            join_items=items, join_grid=grid, join_eager=eager,
+                            join_block=block, join_stage_right=stage, join_pipeline=pipe,
+                            join_direct=direct))
                         ms, out = timed(lambda: jit.join_agg(p, rstart, rlen, rbk, roff, mt, cm))
                         ok = abs(out[0][0].item() - ref) <= 1e-9 * abs(ref)
                         print(json.dumps({"kernel": "jit_join", "enc": cmode, "eager": eager,
@@ -123,7 +126,7 @@ def main():
                                           "grid": grid, "ms": round(ms, 3),
                                           "GBps_logical": round(nbytes / ms / 1e6, 1),
                                           "match": ok}), flush=True)
-    jit.JOIN_EAGER, jit.JOIN_BLOCK = False, 256
+    kernel_config.bind(base)
     if args.no_scan:
         return
     # scan (Q6 shape) over a shipdate-sorted copy: 1/7 of the rows in range
@@ -162,7 +165,8 @@ def main():
         for eager in (True, False):
             for items in (4, 8):
                 for grid in [int(x) for x in args.grids.split(",")]:
-                    jit.SCAN_ITEMS, jit.SCAN_GRID, jit.SCAN_EAGER = items, grid, eager
+                    kernel_config.bind(base.replace(scan_items=items, scan_grid=grid,
+                                                    scan_eager=eager))
                     ms, out = timed(lambda: jit.scan_agg(sp, rs_, rl_, None, cm))
                     ok = abs(out[0][0].item() - ref) <= 1e-9 * abs(ref)
                     print(json.dumps({"kernel": "jit_scan", "enc": cmode, "eager": eager,

@@ -152,16 +152,11 @@ def main():
         with open(args.configs[1:]) as f:
             args.configs = f.read()
     configs = json.loads(args.configs) if args.configs else DEFAULT
-    from hyperspace_amd.exec import jit_runs
-
-    def owner(k):   # knobs of the two-phase run-keyed join live in exec/jit_runs.py
-        return jit if hasattr(jit, k) else jit_runs
-    base = {k: getattr(owner(k), k) for c in configs for k in c}
+    from hyperspace_amd.exec import kernel_config
+    base = kernel_config.active()
     for cfg in configs:
-        for k, v in base.items():
-            setattr(owner(k), k, v)
-        for k, v in cfg.items():
-            setattr(owner(k), k, v)
+        # a config names KernelConfig fields (upper- or lower-case): {"SCAN_VEC": 16}
+        kernel_config.bind(base.replace(**{k.lower(): v for k, v in cfg.items()}))
         jit._KERNELS.clear()
         backend.graphs._lru.clear()
         backend.__dict__.pop("_agg_preps", None)   # prepared lowerings hold launchers

@@ -206,9 +206,9 @@ def test_generated_sources_compile_with_compact_columns(rt, tmp_path):
         if g == 10:
             q3.cols[10] = _fake(NL.I32)
         assert jit_runs.tag_width(q3) == W
-        kt = jit_runs.gen_run_tags(q3, cr, W, 4096)
+        kt = jit_runs.gen_run_tags2(q3, cr, W)
         kq = jit_runs.gen_run_scan(q3, cr, W, 16)
-        assert "a.tags[gw]" in kt.src and "a.RK0[" in kt.src and "a.c2" not in kt.src
+        assert "a.RNG" in kt.src and "a.RK0[" in kt.src and "a.c2" not in kt.src
         assert "a.GM0[" in kq.src and "a.tags[w0_" in kq.src and "a.c8" not in kq.src
         ks += [kt, kq]
     q3.group_col, q3.num_groups = 10, 300
@@ -423,17 +423,14 @@ def test_jit_join_agg_matches_aot(device):
         np.testing.assert_allclose(cg[0], got[0], rtol=1e-12)
         assert np.array_equal(cg[1], got[1])
         # vectorized sort-merge join: staged spans, and every span searched in HBM
-        lds_keys = jit.MJ_LDS_KEYS
-        try:
-            for keys in (lds_keys, 16):
-                jit.MJ_LDS_KEYS = keys
+        from hyperspace_amd.exec import kernel_config
+        for keys in (kernel_config.active().mj_lds_keys, 16):
+            with kernel_config.use(mj_lds_keys=keys):
                 for cmp in (None, comp):
                     mj = [t.cpu().numpy() for t in
                           jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, cmp, nrows=len(lk))]
                     np.testing.assert_allclose(mj[0], got[0], rtol=1e-12)
                     assert np.array_equal(mj[1], got[1]), (keys, cmp is None)
-        finally:
-            jit.MJ_LDS_KEYS = lds_keys
 
 
 @pytest.mark.gpu
@@ -501,17 +498,14 @@ def test_merge_join_agg_numpy_oracle(device):
     allc = dict(enumerate(cl))
     allc.update({8 + i: c for i, c in enumerate(cr)})
     comp = {s: e for s, e in ((s, encode(c)) for s, c in allc.items()) if e is not None}
-    lds_keys = jit.MJ_LDS_KEYS
-    try:
-        for keys in (lds_keys, 32):
-            jit.MJ_LDS_KEYS = keys
+    from hyperspace_amd.exec import kernel_config
+    for keys in (kernel_config.active().mj_lds_keys, 32):
+        with kernel_config.use(mj_lds_keys=keys):
             for cmp in (None, comp):
                 got = [t.cpu().numpy() for t in
                        jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, cmp, nrows=len(lk))]
                 assert got[1][1] == exp_cnt and got[1][0] == exp_cnt, (keys, got[1], exp_cnt)
                 assert abs(got[0][0] - exp_sum) <= 1e-9 * max(1.0, exp_sum)
-    finally:
-        jit.MJ_LDS_KEYS = lds_keys
 
 
 @pytest.mark.gpu
@@ -556,12 +550,9 @@ def test_merge_join_key16_matches_oracle(device):
     allc.update({8 + i: c for i, c in enumerate(cr)})
     comp = {s: e for s, e in ((s, encode(c)) for s, c in allc.items()) if e is not None}
     assert comp[0].width == 4
-    key16 = jit.MJ_KEY16
-    jit.MJ_KEY16 = True
-    try:
+    from hyperspace_amd.exec import kernel_config
+    with kernel_config.use(mj_key16=True):
         assert isinstance(jit._with_key16(p, comp)[0], GroupedCompact)
-    finally:
-        jit.MJ_KEY16 = key16
     assert int((comp[0].g16.gbase == -(1 << 31)).sum()) >= 1      # groups across buckets
     for starts, lens, exp in ((loff[:-1], loff[1:] - loff[:-1], m),
                               (loff[:-1] + 5, loff[1:] - loff[:-1] - 9, None)):
@@ -574,15 +565,11 @@ def test_merge_join_key16_matches_oracle(device):
         rbk = torch.arange(B, dtype=torch.int32, device=device)
         roff_t = torch.from_numpy(roff).to(device)
         res = {}
-        runs = jit.MJ_RUNS
         for k16 in (True, False):
-            jit.MJ_KEY16, jit.MJ_RUNS = k16, False
-            try:
+            with kernel_config.use(mj_key16=k16, mj_runs=False):
                 res[k16] = [t.cpu().numpy() for t in
                             jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, comp, nrows=len(lk),
                                                rdup=False)]
-            finally:
-                jit.MJ_KEY16, jit.MJ_RUNS = key16, runs
         for r in res.values():
             assert r[1][0] == int(exp.sum())
             assert abs(r[0][0] - float(lprice[exp].sum())) <= 1e-9 * max(1.0, float(lprice[exp].sum()))
@@ -817,9 +804,8 @@ def test_merge_join_runs_matches_oracle(device, layout):
     ref = runs_torch(comp[0].codes.cpu())
     for a, b_ in zip((rc.runkeys, rc.gmask, rc.gruns), ref):
         assert torch.equal(a.cpu(), b_)
-    from hyperspace_amd.exec import jit_runs
-    lds_keys, runs, two2, rt2 = jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P, jit_runs.RT2
-    k16, rowmask, sparse0 = jit_runs.RT2_K16, jit_runs.ROWMASK, jit_runs.SPARSE
+    from hyperspace_amd.exec import jit_runs, kernel_config
+    lds_keys = kernel_config.active().mj_lds_keys
     try:
         for starts, lens in ((loff[:-1], loff[1:] - loff[:-1]),
                              (loff[:-1] + 5, loff[1:] - loff[:-1] - 9)):
@@ -835,37 +821,28 @@ def test_merge_join_runs_matches_oracle(device, layout):
             rbk = torch.arange(B, dtype=torch.int32, device=device)
             roff_t = torch.from_numpy(roff).to(device)
             for keys, grouped in ((lds_keys, True), (32, True), (lds_keys, False)):
-                # ungrouped: 1-bit tags, expanded to a row mask for the gated scan (ROWMASK)
+                # ungrouped: 1-bit tags (bit-parallel phase 2 unless rs_bits is off)
                 p.group_col, p.num_groups = (10, 3) if grouped else (-1, 1)
                 G = 3 if grouped else 1
                 es = exp_s if grouped else exp_s.sum(keepdims=True)
                 ec = exp_c if grouped else exp_c.sum(keepdims=True)
-                for use_runs, two, direct, short, rowm, sparse in (
-                        (True, True, True, False, False, True),
-                        (True, True, True, True, True, False), (True, True, True, False, False, False),
-                        (True, True, False, False, True, False), (True, True, False, False, False, True),
-                        (True, False, False, False, False, False),
-                        (False, False, False, False, False, False)):
-                    jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P = keys, use_runs, two
-                    jit_runs.RT2, jit_runs.RT2_K16 = direct, short
-                    jit_runs.ROWMASK, jit_runs.SPARSE = rowm, sparse
-                    got = [t.cpu().numpy() for t in
-                           jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, comp, nrows=len(lk),
-                                              rdup=False)]
-                    s_, c_ = got[0].reshape(G, 2)[:, 0], got[1].reshape(G, 2)[:, 1]
-                    cfg = (keys, grouped, use_runs, two, direct, short, rowm, sparse)
-                    assert (c_ == ec).all(), (cfg, c_, ec)
-                    assert np.allclose(s_, es, rtol=1e-12), cfg
-                    if two:
-                        launcher = jit.LAST_MJ_LAUNCHER[0]
-                        assert isinstance(launcher, jit_runs.TwoPhaseLauncher)
-                        assert (launcher.rows is not None) == (rowm and not sparse and
-                                                               not grouped), cfg
-                        if sparse and not grouped:
-                            assert jit_runs.pack_layout(p, comp) is not None
+                for use_runs, two, sparse in ((True, True, True), (True, True, False),
+                                              (True, False, False), (False, False, False)):
+                    cfg = (keys, grouped, use_runs, two, sparse)
+                    with kernel_config.use(mj_lds_keys=keys, mj_runs=use_runs, mj_2p=two,
+                                           rs_bits=sparse):
+                        got = [t.cpu().numpy() for t in
+                               jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, comp,
+                                                  nrows=len(lk), rdup=False)]
+                        s_, c_ = got[0].reshape(G, 2)[:, 0], got[1].reshape(G, 2)[:, 1]
+                        assert (c_ == ec).all(), (cfg, c_, ec)
+                        assert np.allclose(s_, es, rtol=1e-12), cfg
+                        if two:
+                            launcher = jit.LAST_MJ_LAUNCHER[0]
+                            assert isinstance(launcher, jit_runs.TwoPhaseLauncher)
+                            if sparse and not grouped:
+                                assert jit_runs.pack_layout(p, comp) is not None
     finally:
-        jit.MJ_LDS_KEYS, jit.MJ_RUNS, jit_runs.MJ_2P, jit_runs.RT2 = lds_keys, runs, two2, rt2
-        jit_runs.RT2_K16, jit_runs.ROWMASK, jit_runs.SPARSE = k16, rowmask, sparse0
         p.group_col, p.num_groups = 10, 3
 
 

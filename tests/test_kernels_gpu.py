@@ -268,16 +268,13 @@ def test_join_many_to_many_with_nulls_and_wide_spans(device):
     # generated kernels (sampled span search + galloping, LDS stage or global fallback),
     # with and without the software-pipelined tile loop / right-column staging
     from hyperspace_amd.exec import jit
-    saved = (jit.JOIN_PIPELINE, jit.JOIN_STAGE_RIGHT)
-    try:
-        for pipe in (True, False):
-            for stage in (True, False):
-                jit.JOIN_PIPELINE, jit.JOIN_STAGE_RIGHT = pipe, stage
+    from hyperspace_amd.exec import kernel_config
+    for pipe in (True, False):
+        for stage in (True, False):
+            with kernel_config.use(join_pipeline=pipe, join_stage_right=stage):
                 js, jc, _, _ = jit.join_agg(p, rstart, rlen, rbk, roff_t, mt)
                 assert jc.cpu().numpy().tolist() == exp_c.tolist(), (pipe, stage)
                 np.testing.assert_allclose(js.cpu().numpy(), exp_s, rtol=1e-9)
-    finally:
-        jit.JOIN_PIPELINE, jit.JOIN_STAGE_RIGHT = saved
 
 
 @pytest.mark.parametrize("world", [1, 3, 8, 64])
