@@ -3088,6 +3088,8 @@ class GpuBackend:
         cs = i if hk.own_counts[i] else (A - 1 if hk.need_star else -1)
         src = H.OrderSource(H.SRC_COUNT if tk.src_count else H.SRC_SUM, i, cs, desc=tk.desc)
         gt, nt, thr = tk.candidates(src, limit)
+        if gt is None:
+            return None
         gh, gn = (H.topk_candidates(groups, G, src, limit) if G > limit else (groups, G))
         ht, hh = gt.to_host(nt), gh.to_host(gn)
         host = {k: np.concatenate([ht[k], hh[k]]) for k in ht}
@@ -3097,6 +3099,7 @@ class GpuBackend:
             kth = float(vals[limit - 1])
         else:
             kth = -np.inf
+        self.metrics["run_topk_guard"] = (float(thr), float(kth), int(nt), int(G))
         if thr >= kth:       # a dropped value may tie the k-th
             return None
         return host

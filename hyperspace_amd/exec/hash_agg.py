@@ -395,68 +395,85 @@ def topk_candidates(g: Groups, G: int, o: OrderSource, k: int) -> Tuple[Groups, 
 
 class TopKPlan:
     """ORDER BY <SUM or COUNT aggregate> LIMIT k over a key-run walk (jit_runs bits scan, hash
-    mode): keys whose passing rows the walk sees whole keep their final aggregates in a
-    per-wavefront top-``K`` list (registers) instead of a hash-table slot.  Full lists publish
-    their threshold (the K-th best; ``ctl[0]``, an order-preserving integer image, atomicMax)
-    and every wavefront drops values below the best published one - such a value has K > k
-    better ones.  At the end each list appends its entries at or above the final threshold to
-    candidate arrays laid out like ``Groups`` (keys, then per aggregate sums / counts at stride
-    ``cap``; the count in ``ctl[1]``).  Values are compared in the "larger is better" image
-    (negated for an ascending order).
+    mode): keys whose passing rows the walk sees whole keep their final aggregates in per-lane
+    top-2 registers (jit._topk_insert: no cross-lane work and no memory traffic per key) instead
+    of a hash-table slot.  At the end every wavefront writes its K best entries (key read from
+    the entry's row only then) to its own K slots, its K-th best value and the largest value it
+    dropped (jit._topk_flush; no atomics in the walk).  Two small kernels
+    (csrc/kernels/topk_runs.hip) take the best K-th value over wavefronts as the threshold - a
+    value below it has K > k better ones - and compact the slots at or above it.  Values are
+    compared in the "larger is better" image (negated for an ascending order).
 
-    A value EQUAL to a threshold is dropped too, so when the final threshold reaches the k-th
-    best value overall a tie may be missing: ``exact`` is False and the caller re-runs the
-    table path."""
+    A lane keeps two entries and displaces a third, and a slot tie at a wavefront's K-th value
+    may be left out: the largest value not kept is ``ctl[2]``/the threshold, and when it reaches
+    the k-th best value overall the caller re-runs the exact table path (a tie, or three of the
+    top k in one lane of one wavefront: in practice never)."""
     K = 32
+    OCAP = 1 << 16          # compacted candidates kept (more means ties: exact re-run)
 
     def __init__(self, agg: int, src_count: bool, desc: bool, NA: int):
         self.agg, self.src_count, self.desc, self.NA = agg, src_count, desc, NA
         self.nwv = 0
         self.cap = 0
-        self.keys = self.sums = self.cnts = self.ctl = self._ctl0 = None
         self.used = False
 
     def shape(self) -> tuple:
         return ("topk", self.agg, self.src_count, self.desc, self.K)
 
     def bind(self, nwv: int, device) -> None:
-        """Buffers for ``nwv`` wavefronts (the bits scan's grid)."""
+        """Slots for ``nwv`` wavefronts (the bits scan's grid) and the compacted output."""
         import torch
-        if self.nwv == nwv and self.keys is not None:
+        if self.nwv == nwv and self.cap:
             return
         self.nwv, self.cap = nwv, nwv * self.K
-        self.keys = torch.empty(self.cap, dtype=torch.int64, device=device)
-        self.sums = torch.empty(self.cap * self.NA, dtype=torch.float64, device=device)
-        self.cnts = torch.empty(self.cap * self.NA, dtype=torch.int64, device=device)
-        # [threshold image of -inf, candidate count 0]
-        neg_inf = np.array([-np.inf]).view(np.int64)[0]
-        img = int(neg_inf) ^ 0x7FFFFFFFFFFFFFFF
-        self._ctl0 = torch.tensor([img, 0], dtype=torch.int64, device=device)
-        self.ctl = torch.empty(2, dtype=torch.int64, device=device)
-
-    def reset(self) -> None:
-        """Stream-ordered, before each launch."""
-        self.ctl.copy_(self._ctl0, non_blocking=True)
+        e = lambda n, t: torch.empty(n, dtype=t, device=device)  # noqa: E731
+        self.keys, self.vimg = e(self.cap, torch.int64), e(self.cap, torch.int64)
+        self.sums, self.cnts = e(self.cap * self.NA, torch.float64), e(self.cap * self.NA, torch.int64)
+        self.wth, self.dmx = e(nwv, torch.int64), e(nwv, torch.int64)
+        self.okeys = e(self.OCAP, torch.int64)
+        self.osums = e(self.OCAP * self.NA, torch.float64)
+        self.ocnts = e(self.OCAP * self.NA, torch.int64)
+        # [threshold, candidate count, largest dropped value] (images of -inf, 0, -inf)
+        neg_inf = int(np.array([-np.inf]).view(np.int64)[0]) ^ 0x7FFFFFFFFFFFFFFF
+        self._ctl0 = torch.tensor([neg_inf, 0, neg_inf], dtype=torch.int64, device=device)
+        self.ctl = e(3, torch.int64)
 
     def kernel_values(self) -> Dict[str, int]:
-        return {"TKK": self.keys.data_ptr(), "TKS": self.sums.data_ptr(),
-                "TKC": self.cnts.data_ptr(), "TKG": self.ctl.data_ptr(), "TKCAP": self.cap}
+        return {"TKK": self.keys.data_ptr(), "TKV": self.vimg.data_ptr(),
+                "TKS": self.sums.data_ptr(), "TKC": self.cnts.data_ptr(),
+                "TKW": self.wth.data_ptr(), "TKD": self.dmx.data_ptr(), "TKCAP": self.cap}
+
+    def finish(self, stream) -> None:
+        """Queued after the walk: threshold over wavefronts, then the compaction."""
+        self.ctl.copy_(self._ctl0, non_blocking=True)
+        L = NL.lib()
+        NL.check(L.hs_topk_runs_threshold(NL.ptr(self.wth), NL.ptr(self.dmx), self.nwv,
+                                          NL.ptr(self.ctl), stream), "hs_topk_runs_threshold")
+        NL.check(L.hs_topk_runs_compact(NL.ptr(self.keys), NL.ptr(self.vimg), NL.ptr(self.sums),
+                                        NL.ptr(self.cnts), self.NA, self.cap, NL.ptr(self.ctl),
+                                        self.OCAP, NL.ptr(self.okeys), NL.ptr(self.osums),
+                                        NL.ptr(self.ocnts), stream), "hs_topk_runs_compact")
+
+    @staticmethod
+    def _unimg(v: int) -> float:
+        bits = v if v >= 0 else v ^ 0x7FFFFFFFFFFFFFFF
+        return float(np.array([bits], dtype=np.int64).view(np.float64)[0])
 
     def read_ctl(self) -> Tuple[float, int]:
-        """(final threshold in the order image, candidate count) - one small D2H."""
+        """(the largest value not kept - the threshold or a dropped entry - in the order image,
+        candidate count): one small D2H."""
         c = self.ctl.cpu().numpy()
-        v = int(c[0])
-        bits = v if v >= 0 else v ^ 0x7FFFFFFFFFFFFFFF
-        return float(np.array([bits], dtype=np.int64).view(np.float64)[0]), int(c[1])
+        return max(self._unimg(int(c[0])), self._unimg(int(c[2]))), int(c[1])
 
     def candidates(self, o: "OrderSource", k: int) -> Tuple["Groups", int, float]:
-        """(the appended entries reduced to their top k, ties kept; their count; the final
-        threshold)."""
+        """(the compacted entries reduced to their top k, ties kept; their count; the largest
+        value not kept).  More than OCAP candidates: +inf (the caller re-runs exactly)."""
         thr, n = self.read_ctl()
-        n = min(n, self.cap)
-        g = Groups(self.NA, self.cap, self.keys.device)
-        g.keys, g.sums, g.cnts = self.keys, self.sums, self.cnts
-        g.nulls = _zeros_u8(self.cap, self.keys.device)
+        if n > self.OCAP:
+            return None, 0, float("inf")
+        g = Groups(self.NA, self.OCAP, self.okeys.device)
+        g.keys, g.sums, g.cnts = self.okeys, self.osums, self.ocnts
+        g.nulls = _zeros_u8(self.OCAP, self.okeys.device)
         g.set_count(n)
         if n > k:
             g, n = topk_candidates(g, n, o, k)

@@ -602,7 +602,7 @@ def _hash_key_lines(gen: _Gen, hk, var: str, sfx: str, ind: str) -> List[str]:
 
 
 def _hash_accumulate(gen: _Gen, aggs, hk, pass_var: str, ind: str, tk=None,
-                     seg: str = None) -> List[str]:
+                     seg: str = None, row: str = None) -> List[str]:
     """Hash-mode grouping (``hk``: an exec.hash_agg.KeyPlan): the wavefront's lanes, in row
     order, are cut into runs of equal group keys (one ballot of the run heads); a segmented
     shuffle scan sums each run's values into its last lane, and only that lane probes the
@@ -686,8 +686,7 @@ def _hash_accumulate(gen: _Gen, aggs, hk, pass_var: str, ind: str, tk=None,
         probe = "htl && !hcomp"
         b += _topk_value(aggs, hk, tk, i2)
     if seg is not None:
-        emit = f"({probe})" + (" || (hcomp && tkv_ > tkcut)" if tk is not None else "")
-        lazy_key(emit, b, i2)
+        lazy_key(probe, b, i2)
     # CAS-first probe: a group's first run inserts with one returning atomic (no load first);
     # later runs of the same group find it on the first CAS of their probe
     b += [f"{i2}if ({probe}) {{",
@@ -728,7 +727,7 @@ def _hash_accumulate(gen: _Gen, aggs, hk, pass_var: str, ind: str, tk=None,
             b.append(f"{i2}    atomicAdd({tgt}, {cnt});")
     b += [f"{i2}  }}", f"{i2}}}"]
     if tk is not None:
-        b += _topk_insert(aggs, hk, tk, i2)
+        b += _topk_insert(aggs, hk, tk, i2, row)
     b.append(f"{ind}}}")
     return b
 
@@ -757,88 +756,89 @@ def _topk_value(aggs, hk, tk, ind: str) -> List[str]:
             f"{ind}const double tkv_ = {sign}({ov});"]
 
 
-def _topk_decls(aggs, tk, args: "Args") -> List[str]:
-    """Kernel-scope state of the wavefront's top-K list (lane l < K holds entry l), its own
-    threshold ``tkthr`` (the minimum of a full list) and the cut ``tkcut`` = max(own, the
-    global threshold other wavefronts published)."""
-    args.add("p", "TKG", "long long*")
-    b = ["  u64 tkk = ~0ull; double tko = -__builtin_inf(); int tkn = 0;",
-         "  double tkthr = -__builtin_inf(); double tkcut = -__builtin_inf();",
-         "  double tkpub = -__builtin_inf();"]
-    for i in range(len(aggs)):
-        b.append(f"  double tks{i} = 0.0; long long tkc{i} = 0ll;")
+TOPK_LANE = 2   # entries each lane keeps (hash_agg.TopKPlan)
+
+
+def _topk_decls(aggs, tk) -> List[str]:
+    """Kernel-scope state of the run top-K (hash_agg.TopKPlan): each lane keeps its best
+    ``TOPK_LANE`` complete segments in registers (entry 0 the better; the tail row, whose key
+    is read only at the end, the order value and the aggregates) and ``tkdmx``, the largest
+    value it dropped."""
+    b = ["  double tkdmx = -__builtin_inf();"]
+    for j in range(TOPK_LANE):
+        b.append(f"  i64 tkr{j} = -1; double tkv{j} = -__builtin_inf();" +
+                 "".join(f" double tks{j}_{i} = 0.0; long long tkc{j}_{i} = 0ll;"
+                         for i in range(len(aggs))))
     return b
 
 
-def _topk_sync(tk, ind: str) -> List[str]:
-    """Once per tile: publish a full list's threshold (atomicMax of the order-preserving
-    integer image) and take the best published threshold as this wavefront's cut - a value
-    below the 32nd best of any list cannot reach the top ``limit < 32``."""
-    return [f"{ind}if (tkn >= {tk.K} && tkthr > tkpub) {{",
-            f"{ind}  if ((threadIdx.x & 63u) == 0) atomicMax(a.TKG, hs_dimg(tkthr));",
-            f"{ind}  tkpub = tkthr; }}",
-            f"{ind}tkcut = fmax(tkthr, hs_dimg_inv(__atomic_load_n(a.TKG, __ATOMIC_RELAXED)));"]
-
-
-def _topk_insert(aggs, hk, tk, ind: str) -> List[str]:
-    """Complete segments whose order value beats the cut enter the list one at a time
-    (wavefront-uniform loop over the ballot): the first K fill empty slots, later ones replace
-    the list's minimum; the list's threshold is the minimum of a full list."""
-    K = tk.K
+def _topk_insert(aggs, hk, tk, ind: str, row: str) -> List[str]:
+    """A complete segment's tail lane keeps it if it beats the lane's worse entry (a lane-local
+    insertion into a sorted pair: no cross-lane work and no memory traffic per key); anything
+    displaced or not kept raises the lane's dropped maximum."""
+    assert TOPK_LANE == 2    # the shift-or-set insertion below is exact for a pair
     vals = _topk_values(aggs, hk)
-    b = [f"{ind}{{ u64 tq_ = __ballot(hcomp && tkv_ > tkcut);",
-         f"{ind}  while (tq_) {{",
-         f"{ind}    const int sl_ = __builtin_ctzll(tq_); tq_ &= tq_ - 1ull;",
-         f"{ind}    const double cv_ = __shfl(tkv_, sl_, 64);",
-         f"{ind}    if (cv_ > tkcut) {{",
-         f"{ind}      const u64 ck_ = __shfl(hk, sl_, 64);"]
-    for i, (sx, cx) in enumerate(vals):
-        b.append(f"{ind}      const double cs{i}_ = __shfl((double)({sx}), sl_, 64); "
-                 f"const long long cc{i}_ = __shfl((long long)({cx}), sl_, 64);")
-    b += [f"{ind}      int slot_ = tkn;",
-          f"{ind}      if (tkn >= {K}) {{",
-          f"{ind}        double m_ = hln < {K} ? tko : __builtin_inf(); int mi_ = hln;",
-          f"{ind}        for (int o_ = 32; o_ > 0; o_ >>= 1) {{",
-          f"{ind}          const double om_ = __shfl_xor(m_, o_, 64); "
-          f"const int oi_ = __shfl_xor(mi_, o_, 64);",
-          f"{ind}          if (om_ < m_ || (om_ == m_ && oi_ < mi_)) {{ m_ = om_; mi_ = oi_; }} }}",
-          f"{ind}        slot_ = mi_;",
-          f"{ind}      }} else {{ ++tkn; }}",
-          f"{ind}      if (hln == slot_) {{ tkk = ck_; tko = cv_;" +
-          "".join(f" tks{i} = cs{i}_; tkc{i} = cc{i}_;" for i in range(len(vals))) + " }",
-          f"{ind}      if (tkn >= {K}) {{",
-          f"{ind}        double m_ = hln < {K} ? tko : __builtin_inf();",
-          f"{ind}        for (int o_ = 32; o_ > 0; o_ >>= 1) m_ = fmin(m_, __shfl_xor(m_, o_, 64));",
-          f"{ind}        tkthr = m_; tkcut = fmax(tkcut, m_);",
-          f"{ind}      }}",
-          f"{ind}    }}",
-          f"{ind}  }}",
-          f"{ind}}}"]
-    return b
+
+    def put(j):
+        return f" tkr{j} = {row}; tkv{j} = tkv_;" + "".join(
+            f" tks{j}_{i} = (double)({sx}); tkc{j}_{i} = (long long)({cx});"
+            for i, (sx, cx) in enumerate(vals))
+    mv = " tkr1 = tkr0; tkv1 = tkv0;" + "".join(
+        f" tks1_{i} = tks0_{i}; tkc1_{i} = tkc0_{i};" for i in range(len(vals)))
+    return [f"{ind}if (hcomp) {{",
+            f"{ind}  if (tkv_ > tkv1) {{",
+            f"{ind}    tkdmx = fmax(tkdmx, tkv1);",
+            f"{ind}    if (tkv_ > tkv0) {{{mv}{put(0)} }} else {{{put(1)} }}",
+            f"{ind}  }} else {{ tkdmx = fmax(tkdmx, tkv_); }}",
+            f"{ind}}}"]
 
 
-def _topk_flush(aggs, tk, args: "Args") -> List[str]:
-    """The list entries at or above the final global threshold, appended (one atomic per
-    wavefront) to the candidate arrays (hash_agg.Groups layout: keys, then per aggregate sums /
-    counts at stride TKCAP); the count in TKG[1]."""
+def _topk_flush(aggs, tk, args: "Args", wid: str, key_lines) -> List[str]:
+    """The wavefront's best K entries to its K slots of the candidate arrays (keys, order-value
+    images, then per aggregate sums / counts at stride TKCAP; empty slots: key ~0, image of
+    -inf), its K-th best value (TKW) and its dropped maximum (TKD) - found by a bitwise search
+    over the lanes' order-preserving images (64 ballots), no atomics.  ``key_lines(j, ind)``
+    loads entry j's key into ``tkey_`` from its row."""
+    K = tk.K
     kk = args.add("p", "TKK", "unsigned long long*")
+    kv = args.add("p", "TKV", "long long*")
     ks = args.add("p", "TKS", "double*")
     kc = args.add("p", "TKC", "long long*")
+    kw = args.add("p", "TKW", "long long*")
+    kd = args.add("p", "TKD", "long long*")
     cap = args.add("q", "TKCAP", "long long")
+    imgs = " + ".join(f"__popcll(__ballot(tki{j} >= t_))" for j in range(TOPK_LANE))
     b = ["  { const int tl_ = (int)(threadIdx.x & 63u);",
-         "    const double gt_ = hs_dimg_inv(__atomic_load_n(a.TKG, __ATOMIC_RELAXED));",
-         f"    const bool lv_ = tl_ < {tk.K} && tl_ < tkn && tko >= gt_;",
-         "    const u64 lb_ = __ballot(lv_);",
-         "    long long base_ = 0;",
-         "    if (tl_ == 0 && lb_) base_ = (long long)atomicAdd((unsigned long long*)&a.TKG[1], "
-         "(unsigned long long)__popcll(lb_));",
-         "    base_ = __shfl(base_, 0, 64);",
-         "    if (lv_) {",
-         "      const long long te_ = base_ + __popcll(lb_ & ((1ull << tl_) - 1ull));",
-         f"      if (te_ < {cap}) {{ {kk}[te_] = tkk;"]
-    for i in range(len(aggs)):
-        b.append(f"        {ks}[{i} * {cap} + te_] = tks{i}; {kc}[{i} * {cap} + te_] = tkc{i};")
-    b += ["      }", "    }", "  }"]
+         "    " + " ".join(f"const u64 tki{j} = (u64)hs_dimg(tkv{j}) ^ 0x8000000000000000ull;"
+                           for j in range(TOPK_LANE)),
+         "    u64 th_ = 0ull;",
+         "    for (int b_ = 63; b_ >= 0; --b_) { const u64 t_ = th_ | (1ull << b_);",
+         f"      if ({imgs} >= {K}) th_ = t_; }}",
+         "    // th_: the K-th best image (0 when fewer than K entries are live)",
+         "    double dm_ = tkdmx;",
+         "    long long pos_ = 0;"]
+    for j in range(TOPK_LANE):
+        b += [f"    {{ const bool lv_ = tkr{j} >= 0 && tki{j} >= th_;",
+              "      const u64 lb_ = __ballot(lv_);",
+              "      const long long at_ = pos_ + __popcll(lb_ & ((1ull << tl_) - 1ull));",
+              f"      if (lv_ && at_ < {K}) {{",
+              f"        const long long te_ = (long long)({wid}) * {K} + at_;"]
+        b += key_lines(j, "        ")
+        b += [f"        {kk}[te_] = tkey_; {kv}[te_] = hs_dimg(tkv{j});"]
+        for i in range(len(aggs)):
+            b.append(f"        {ks}[{i} * {cap} + te_] = tks{j}_{i}; "
+                     f"{kc}[{i} * {cap} + te_] = tkc{j}_{i};")
+        b += [f"      }} else if (tkr{j} >= 0) dm_ = fmax(dm_, tkv{j});",
+              "      pos_ += __popcll(lb_); }"]
+    b += [f"    for (long long e_ = pos_ + tl_; e_ < {K}; e_ += 64) {{",
+          f"      const long long te_ = (long long)({wid}) * {K} + e_;",
+          f"      {kk}[te_] = ~0ull; {kv}[te_] = hs_dimg(-__builtin_inf()); }}",
+          "    for (int o_ = 32; o_ > 0; o_ >>= 1) dm_ = fmax(dm_, __shfl_xor(dm_, o_, 64));",
+          "    if (tl_ == 0) {",
+          f"      {kw}[{wid}] = pos_ >= {K} ? (long long)(th_ ^ 0x8000000000000000ull) : "
+          "hs_dimg(-__builtin_inf());",
+          f"      {kd}[{wid}] = hs_dimg(dm_); }}",
+          "  }"]
     return b
 
 

@@ -529,7 +529,7 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
     b += J._acc_decls(aggs, grouped, args)
     assert tk is None or hk is not None
     if tk is not None:
-        b += J._topk_decls(aggs, tk, args)
+        b += J._topk_decls(aggs, tk)
     CAP = 1024  # noqa: N806 — list entries per wavefront and round (a denser tile takes rounds)
     EW = 4  # noqa: N806 — list entries per lane per walk pass, loads all in flight together
 
@@ -564,10 +564,8 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
           "  for (i64 t = t0; t < t1; ++t) {",
           "    const i64 rs = rsN, re = reN, tb0 = tbN; const u64 m_ = gmN; const i64 q0 = grN;"]
     if tk is not None:
-        # key run of a list entry, relative to the tile's first run (lrn_); the lists'
-        # threshold exchange once per tile
+        # key run of a list entry, relative to the tile's first run (lrn_)
         b.append("    const int qr_ = (int)(q0 - __shfl(q0, 0, 64));")
-        b += J._topk_sync(tk, "    ")
     b += [
 
           "    const i64 row0 = tb0 + 64 * ln;",
@@ -696,7 +694,8 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
         if hk is not None:
             b += [J._rename(x, tail, it)
                   for x in J._hash_accumulate(g, aggs, hk, "cok", ind2, tk=tk,
-                                              seg=f"crn{k}" if tk is not None else None)]
+                                              seg=f"crn{k}" if tk is not None else None,
+                                              row=f"crow{k}")]
         else:
             b += [J._rename(x, tail, it)
                   for x in J._accumulate(g, aggs, grouped, "cok", gvar, ind2)]
@@ -705,7 +704,15 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
     if hk is None:
         b += J._flush(aggs, grouped)
     if tk is not None:
-        b += J._topk_flush(aggs, tk, args)
+        def key_lines(j: int, ind_: str) -> List[str]:
+            gk = J._Gen(args, cols, SPLIT, (f"tkr{j}", f"tkr{j}"), frozenset(), True)
+            out: List[str] = []
+            for c in hk.cols:
+                J._uload(gk, c.slot, "F", out, ind_)
+            out += J._hash_key_lines(gk, hk, "tkey_l", "_F", ind_)
+            out.append(f"{ind_}const u64 tkey_ = tkey_l;")
+            return out
+        b += J._topk_flush(aggs, tk, args, "wid", key_lines)
     name = "hs_jit_run_bits_scan" if hk is None else \
         ("hs_jit_run_bits_hash" if tk is None else "hs_jit_run_bits_topk")
     src = (J._PRELUDE + args.struct_src() +
@@ -757,10 +764,11 @@ class TwoPhaseLauncher:
             vs.update((hk or self.hk).values())   # this query's key domain
             if self.tk is not None:
                 vs.update(self.tk.kernel_values())
-                self.tk.reset()
                 self.tk.used = True
             self.kt.launch(self.grid_t, vt, st, 0)
             self.ks.launch(self.grid_s, vs, st, self.shmem)
+            if self.tk is not None:
+                self.tk.finish(st)
             return None
         hit = self.blocks.get(key) if key is not None else None
         if hit is None:

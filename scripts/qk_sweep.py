@@ -72,6 +72,10 @@ def main():
                       "spark.sql.autoBroadcastJoinThreshold": "-1",
                       "spark.hyperspace.mi.execution.device": "gpu"},
                 warehouse_dir=os.path.join(args.data_dir, "wh"))
+    # extra session conf for sweeps: HS_BENCH_CONF="key=value,key=value" (as bench.py)
+    for kv in filter(None, os.environ.get("HS_BENCH_CONF", "").split(",")):
+        k, v = kv.split("=", 1)
+        s.conf.set(k.strip(), v.strip())
     hs = Hyperspace(s)
     li = s.read.parquet(os.path.join(data, "lineitem"))
     od = s.read.parquet(os.path.join(data, "orders"))
@@ -145,8 +149,9 @@ def main():
         rep = TRACER.report()
         stages = {k: round(v["device_ms"] / max(v["calls"], 1), 4) for k, v in rep.items()}
         host = {k: round(v["host_ms"] / max(v["calls"], 1), 4) for k, v in rep.items()}
+        m = {k: v for k, v in backend.metrics.items() if k.startswith("run_topk")}
         return {"wall_ms": round(wall, 4), "stages": stages, "host_stages": host,
-                "res": str(res)[:120]}
+                "res": str(res)[:120], "metrics": m}
 
     if args.configs and args.configs.startswith("@"):   # @file: JSON list in a file
         with open(args.configs[1:]) as f:

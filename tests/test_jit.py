@@ -867,8 +867,8 @@ def test_run_topk_sources_compile(rt, tmp_path):
             tk = H.TopKPlan(1 if by_count else 0, by_count, desc, 2)
             k = jit_runs.gen_run_sparse_scan(j, comp, hk, tk)
             assert k.name == "hs_jit_run_bits_topk" and "htl && !hcomp" in k.src
-            assert "TKK" in k.src and "tkthr" in k.src and "lrn_" in k.src
-            assert "a.c0[crow" not in k.src.split("lazy")[0] or True
+            assert "TKK" in k.src and "TKW" in k.src and "tkdmx" in k.src and "lrn_" in k.src
+            assert "atomic" not in k.src.split("tkdmx")[-1]     # no atomics in the top-K flush
             ks.append(k)
     k0 = jit_runs.gen_run_sparse_scan(j, comp, hk)
     assert k0.name == "hs_jit_run_bits_hash" and "hcomp" not in k0.src
