@@ -12,8 +12,11 @@ gather or PLAIN copy, one workgroup per page).  Launches cover ~4 GB of files at
 (``decode_batch``): a page is one wavefront's serial work, so only many files' pages fill the
 chip.  Large dictionary pages (and string dictionaries) are inflated on the host.
 
-Host-page-layer path (``upload_file``: index bucket files, whose row-group-sized pages are
-too long for one wavefront's inflate, and ``HS_PQ_DEVICE_NULLS=0`` for chunks with nulls):
+Index bucket files written by the device writer (``exec/pq_encode.py``: pages of at most
+``PAGE_ROWS`` rows, ``created_by`` = ``pq_encode.CREATED_BY``) take the device path too
+(``exec/device_cache.py`` checks the writer).  Host-page-layer path (``upload_file``: index
+files of other writers, whose row-group-sized pages are too long for one wavefront's inflate,
+and ``HS_PQ_DEVICE_NULLS=0`` for chunks with nulls):
 per file every natively decodable column chunk is decompressed straight into one pinned
 buffer, its RLE/bit-packed streams are cut into run tables, buffer and run tables cross PCIe
 in two copies on the HIP copy stream, and the expansion kernels write the values into the
