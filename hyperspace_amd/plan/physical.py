@@ -511,6 +511,9 @@ class HashAggregateExec(UnaryExec):
         self.mode = mode                     # "partial" | "final" | "complete"
         self.children = (child,)
         self.result_attrs = result_attrs
+        # attributes of unnamed grouping expressions (SQL ``GROUP BY a % 7``), made once: the
+        # exchange above partitions by them and the final aggregate reads them by id
+        self._unnamed: dict = {}
 
     @property
     def output(self):
@@ -521,17 +524,26 @@ class HashAggregateExec(UnaryExec):
     def partial_output(self):
         # a named grouping expression keeps its alias's id: the exchange above partitions by,
         # and the final aggregate groups on, these same attributes
-        out = [g if isinstance(g, E.Attribute) else
-               (g.to_attribute() if isinstance(g, E.Alias) else
-                E.Attribute(g.sql(), g.data_type, True)) for g in self.grouping]
+        out = []
+        for i, g in enumerate(self.grouping):
+            if isinstance(g, E.Attribute):
+                out.append(g)
+            elif isinstance(g, E.Alias):
+                out.append(g.to_attribute())
+            else:
+                if i not in self._unnamed:
+                    self._unnamed[i] = E.Attribute(g.sql(), g.data_type, True)
+                out.append(self._unnamed[i])
         for i, (_, fn) in enumerate(agg_functions(self.aggregates)):
             for j, (nm, dt) in enumerate(_buffer_fields(fn)):
                 out.append(E.Attribute(f"{nm}#{i}_{j}", dt, True, expr_id=-(1000 * (i + 1) + j)))
         return out
 
     def with_children(self, children):
-        return HashAggregateExec(self.grouping, self.aggregates, self.mode, children[0],
-                                 self.result_attrs)
+        n = HashAggregateExec(self.grouping, self.aggregates, self.mode, children[0],
+                              self.result_attrs)
+        n._unnamed = self._unnamed
+        return n
 
     @property
     def output_partitioning(self):

@@ -123,6 +123,22 @@ def test_sql_aggregates_order_limit_union(env):
         s.sql("SELECT c1 FROM missing_view")
 
 
+def test_group_by_unnamed_expression(env):
+    """``GROUP BY c5 % 7`` (no alias in the GROUP BY): the partial aggregate's attribute for the
+    expression is made once, so the exchange above and the final aggregate read the same one."""
+    s, _, src = env
+    s.read.parquet(src).createOrReplaceTempView("t")
+    rows = s.sql("SELECT c5 % 7 AS m, count(*) AS n, sum(c4) AS p FROM t WHERE c5 > 0 "
+                 "GROUP BY c5 % 7").collect()
+    want = {}
+    for r in sample_table().to_pylist():
+        if r["clicks"] > 0:
+            a = want.setdefault(r["clicks"] % 7, [0, 0])
+            a[0] += 1
+            a[1] += r["imprs"]
+    assert sorted(tuple(r) for r in rows) == sorted((k, n, p) for k, (n, p) in want.items())
+
+
 def test_temp_view_lifecycle(env):
     s, _, src = env
     df = s.read.parquet(src)
