@@ -2464,6 +2464,9 @@ class GpuBackend:
         if not all(pa.types.is_integer(a.data_type) for a in (pk, bk)):
             return None
         pinner = _strip_exchange(probe) or probe
+        out = self._copart_semi(pinner, pk, binner, bk, fns, group)
+        if out is not None:
+            return out
         with stage("semi.build"):
             brel = self._rel(binner)
             if brel.parts:
@@ -2488,6 +2491,141 @@ class GpuBackend:
                 self.last_semi_join["probe"] = "runs"
                 return out
             return self._scan_agg(prel.copy(conds=prel.conds + [cond]), fns, group)
+
+    def _copart_semi(self, pinner, pk, binner, bk, fns, group):
+        """The semi-join's build as a co-partitioned join: a build ``Project/Filter <- inner
+        join(orders side, customer side)`` whose kept key ``bk`` comes from the orders side
+        (TPC-H Q3: ``(customer x orders) x lineitem``), when another index over the same orders
+        files is bucketed by ``bk`` like the probe index is by ``pk`` and covers the orders
+        side's columns.  Then the probe joins that index bucket by bucket - the two-phase
+        run-keyed merge join of ``_join_agg_pair`` - with the orders side's own filters plus
+        ``o_custkey`` in a bitmap of the (unique) customer keys as right-side predicates: one
+        small bitmap (the customer key domain, L2-resident) instead of the orders-key bitmap
+        (75 MB at SF100, probed at random) and no all-gather of it across ranks.  An inner join
+        with unique customer keys pairs every passing orders row with exactly one customer, so
+        ``(C x O) x L = L x (O where o_custkey in C)``.  None when the shape or the indexes do
+        not qualify."""
+        conf = self.session.conf
+        if str(conf.get("spark.hyperspace.mi.coPartitionedSemiJoin.enabled", "true")).lower() \
+                != "true" or not HyperspaceConf.codegen_enabled(conf):
+            return None
+        above, node = [], binner
+        while isinstance(node, (X.ProjectExec, X.FilterExec)):
+            if isinstance(node, X.ProjectExec) and \
+                    not all(isinstance(e, E.Attribute) for e in node.project_list):
+                return None
+            above.append(node)
+            node = node.child
+        if not (isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner" and
+                node.condition is None and len(node.left_keys) == 1):
+            return None
+        pick = None
+        for o, c, ok, ck in ((node.left, node.right, node.left_keys[0], node.right_keys[0]),
+                             (node.right, node.left, node.right_keys[0], node.left_keys[0])):
+            if any(a.expr_id == bk.expr_id for a in o.output):
+                pick = (o, c, ok, ck)
+        if pick is None:
+            return None
+        oside, cside, ojk, cjk = pick
+        if not all(isinstance(k, E.Attribute) and pa.types.is_integer(k.data_type)
+                   for k in (ojk, cjk)):
+            return None
+        oids = {a.expr_id for a in oside.output}
+        upper = [f for f in above if isinstance(f, X.FilterExec)]
+        if any(not {a.expr_id for a in f.condition.references()} <= oids for f in upper):
+            return None
+        chain, leaf = [], _strip_exchange(oside) or oside
+        while isinstance(leaf, (X.ProjectExec, X.FilterExec)):
+            chain.append(leaf)
+            leaf = leaf.child
+        if not isinstance(leaf, X.FileSourceScanExec) or not leaf.relation.is_index():
+            return None
+        ascan = self._copart_scan(leaf, bk, pinner)
+        if ascan is None:
+            return None
+        prel = self._rel(pinner)
+        if prel.parts or not prel.bucketed or prel.num_buckets != ascan.relation.index.num_buckets \
+                or not prel.sort_attrs or prel.sort_attrs[0].expr_id != pk.expr_id or \
+                pk.data_type != bk.data_type:
+            return None
+        gs = (None, 1, 0, None, None)
+        if group is not None:
+            if group.expr_id not in prel.colmap:
+                return None
+            gs = self._group_spec(prel, group, _group_limit(MAX_GROUPS_JOIN, GROUP_LDS_JOIN,
+                                                            len(fns)))
+            if gs is None:
+                return (*self._empty_agg(len(fns) + 1), 1, 0, None, None)
+        with stage("semi.build"):
+            crel = self._rel(_strip_exchange(cside) or cside)
+            if crel.parts:
+                return None
+            keys = self._materialize(crel, [cjk])[cjk.expr_id]
+            bm = self._semi_bitmap(keys)
+        if bm is None:
+            return None
+        words, lo, nbits = bm
+        orel = self._scan_memo(ascan)
+        for n in reversed(chain):
+            orel = self._unary(n, orel)
+        for f in reversed(upper):
+            orel = self._unary(f, orel)
+        orel = orel.copy(conds=orel.conds + [CP.KeyBitmap(ojk, words, lo, nbits)])
+        self.last_semi_join = {"build_keys": int(keys.data.numel()), "bitmap_bits": nbits,
+                               "probe": "copart", "index": ascan.relation.index.name}
+        agreed, G, gbase, gdict, gtype = gs
+        self._groups_agreed = agreed is True
+        self._join_rec = None
+        with stage("semi.probe"):
+            out = self._join_agg_pair(_NoCondition, prel, orel, pk, bk, fns, group, G, gbase)
+        self._join_rec = None
+        return (*out, G, gbase, gdict, gtype)
+
+    def _copart_scan(self, scan: X.FileSourceScanExec, key, pinner):
+        """A scan of an index over the same source files as ``scan``'s index, bucketed by
+        ``key`` alone with the probe index's bucket count and holding every column ``scan``
+        outputs (``_copart_semi``); the scan node is kept per (scan, index) so the device
+        cache and scan memo see one node.  None when no index qualifies."""
+        from ..hyperspace import get_context
+        from ..actions import states
+        from ..rules import rule_utils as RU
+        from ..index import tags as T
+        from ..plan import logical as L
+        idx = scan.relation.index
+        probe_scans = pinner.collect(lambda x: isinstance(x, X.FileSourceScanExec))
+        if len(probe_scans) != 1 or not probe_scans[0].relation.is_index():
+            return None
+        nb = probe_scans[0].relation.index.num_buckets
+        names = {a.name.lower() for a in scan.output}
+        if C.DATA_FILE_NAME_ID.lower() in names:
+            return None        # lineage ids are per index: a hybrid-scan delete filter stays
+        found = None
+        for e in get_context(self.session).index_collection_manager.get_indexes([states.ACTIVE]):
+            if e.name == idx.name or e.num_buckets != nb or \
+                    [c.lower() for c in e.indexed_columns] != [key.name.lower()] or \
+                    not names <= {n.lower() for n in e.schema.names} or \
+                    e.source_file_info_set != idx.source_file_info_set:
+                continue
+            found = e
+            break
+        if found is None:
+            return None
+        memo = self.__dict__.setdefault("_copart_scans", {})
+        mk = (id(scan), found.name)
+        hit = memo.get(mk)
+        if hit is not None and hit[0] is scan and hit[1] is found:
+            return hit[2]
+        loc = found.with_cached_tag(None, T.INMEMORYFILEINDEX_INDEX_ONLY,
+                                    lambda: RU._index_file_index(found))
+        k, v = C.INDEX_RELATION_IDENTIFIER
+        schema = pa.schema([f for f in found.schema if f.name != C.DATA_FILE_NAME_ID])
+        rel = L.HadoopFsRelation(loc, None, schema, found.bucket_spec, "parquet", {k: v},
+                                 index=found)
+        ascan = X.FileSourceScanExec(rel, list(scan.output), [], [], True)
+        if len(memo) > 64:
+            memo.clear()
+        memo[mk] = (scan, found, ascan)
+        return ascan
 
     def _semi_runs(self, r: DRel, key, words, lo: int, nbits: int, fns, group):
         """The semi-join probe over the probe key's run form (``jit_runs.semi_runs_agg``): a
@@ -3080,18 +3218,26 @@ class GpuBackend:
         return tk
 
     def _topk_merge(self, tk, groups, G: int, hk, A: int, limit: int):
-        """Host group arrays of the top-``limit`` candidates of a run top-K query: the lists'
-        candidates plus the table's (split keys), or None when a full list's threshold reaches
-        the k-th best value (a dropped tie is possible; the caller re-runs exactly)."""
+        """Host group arrays of the top-``limit`` candidates of a run top-K query: the slots'
+        top k plus the table's (split keys), or None when the largest value the slots do not
+        hold reaches the k-th best value (a dropped tie is possible; the caller re-runs
+        exactly)."""
         from . import hash_agg as H
         i = tk.agg
         cs = i if hk.own_counts[i] else (A - 1 if hk.need_star else -1)
         src = H.OrderSource(H.SRC_COUNT if tk.src_count else H.SRC_SUM, i, cs, desc=tk.desc)
-        gt, nt, thr = tk.candidates(src, limit)
-        if gt is None:
-            return None
+        gt, nt, thr = tk.candidates(limit)
         gh, gn = (H.topk_candidates(groups, G, src, limit) if G > limit else (groups, G))
         ht, hh = gt.to_host(nt), gh.to_host(gn)
+        # empty slots (fewer than k live entries): key ~0 with the image of -inf
+        img = gt.vimg.cpu().numpy().view(np.uint64) if nt else np.zeros(0, np.uint64)
+        empty = (ht["keys"] == np.uint64(H.EMPTY)) & (img == np.uint64(tk.empty_image()))
+        if empty.any():
+            live = ~empty
+            ht = {k: v[live] for k, v in ht.items()}
+            nt = int(live.sum())
+            if nt + gn < limit:
+                return None      # a live entry may share the empty pattern: exact path
         host = {k: np.concatenate([ht[k], hh[k]]) for k in ht}
         n = len(host["keys"])
         if n >= limit:
@@ -3642,6 +3788,11 @@ class _AggProgram:
             return None
         finish = be._agg_finish(self.final, self.fns, self.group, res)
         return QueryFuture(be, plan, finish, "native", None, t0)
+
+
+class _NoCondition:
+    """A join node stand-in without a residual condition (``_copart_semi``'s derived join)."""
+    condition = None
 
 
 def _strip_exchange(p):

@@ -399,17 +399,16 @@ class TopKPlan:
     top-2 registers (jit._topk_insert: no cross-lane work and no memory traffic per key) instead
     of a hash-table slot.  At the end every wavefront writes its K best entries (key read from
     the entry's row only then) to its own K slots, its K-th best value and the largest value it
-    dropped (jit._topk_flush; no atomics in the walk).  Two small kernels
-    (csrc/kernels/topk_runs.hip) take the best K-th value over wavefronts as the threshold - a
-    value below it has K > k better ones - and compact the slots at or above it.  Values are
+    dropped (jit._topk_flush; no atomics in the walk).  A small kernel
+    (csrc/kernels/topk_runs.hip) reduces the wavefronts' K-th best and dropped values to the
+    bound of every value the slots do not hold; the radix select of the table path
+    (``topk_candidates``' hs_topk_select) picks the slots' top k from their images.  Values are
     compared in the "larger is better" image (negated for an ascending order).
 
     A lane keeps two entries and displaces a third, and a slot tie at a wavefront's K-th value
-    may be left out: the largest value not kept is ``ctl[2]``/the threshold, and when it reaches
-    the k-th best value overall the caller re-runs the exact table path (a tie, or three of the
-    top k in one lane of one wavefront: in practice never)."""
+    may be left out: when that bound reaches the k-th best value overall the caller re-runs the
+    exact table path (a tie, or three of the top k in one lane of one wavefront)."""
     K = 32
-    OCAP = 1 << 16          # compacted candidates kept (more means ties: exact re-run)
 
     def __init__(self, agg: int, src_count: bool, desc: bool, NA: int):
         self.agg, self.src_count, self.desc, self.NA = agg, src_count, desc, NA
@@ -421,7 +420,7 @@ class TopKPlan:
         return ("topk", self.agg, self.src_count, self.desc, self.K)
 
     def bind(self, nwv: int, device) -> None:
-        """Slots for ``nwv`` wavefronts (the bits scan's grid) and the compacted output."""
+        """Slots for ``nwv`` wavefronts (the bits scan's grid)."""
         import torch
         if self.nwv == nwv and self.cap:
             return
@@ -430,10 +429,7 @@ class TopKPlan:
         self.keys, self.vimg = e(self.cap, torch.int64), e(self.cap, torch.int64)
         self.sums, self.cnts = e(self.cap * self.NA, torch.float64), e(self.cap * self.NA, torch.int64)
         self.wth, self.dmx = e(nwv, torch.int64), e(nwv, torch.int64)
-        self.okeys = e(self.OCAP, torch.int64)
-        self.osums = e(self.OCAP * self.NA, torch.float64)
-        self.ocnts = e(self.OCAP * self.NA, torch.int64)
-        # [threshold, candidate count, largest dropped value] (images of -inf, 0, -inf)
+        # [max K-th best, unused, max dropped value] (images of -inf, 0, -inf)
         neg_inf = int(np.array([-np.inf]).view(np.int64)[0]) ^ 0x7FFFFFFFFFFFFFFF
         self._ctl0 = torch.tensor([neg_inf, 0, neg_inf], dtype=torch.int64, device=device)
         self.ctl = e(3, torch.int64)
@@ -444,40 +440,46 @@ class TopKPlan:
                 "TKW": self.wth.data_ptr(), "TKD": self.dmx.data_ptr(), "TKCAP": self.cap}
 
     def finish(self, stream) -> None:
-        """Queued after the walk: threshold over wavefronts, then the compaction."""
+        """Queued after the walk: the bound over wavefronts."""
         self.ctl.copy_(self._ctl0, non_blocking=True)
-        L = NL.lib()
-        NL.check(L.hs_topk_runs_threshold(NL.ptr(self.wth), NL.ptr(self.dmx), self.nwv,
-                                          NL.ptr(self.ctl), stream), "hs_topk_runs_threshold")
-        NL.check(L.hs_topk_runs_compact(NL.ptr(self.keys), NL.ptr(self.vimg), NL.ptr(self.sums),
-                                        NL.ptr(self.cnts), self.NA, self.cap, NL.ptr(self.ctl),
-                                        self.OCAP, NL.ptr(self.okeys), NL.ptr(self.osums),
-                                        NL.ptr(self.ocnts), stream), "hs_topk_runs_compact")
+        NL.check(NL.lib().hs_topk_runs_threshold(NL.ptr(self.wth), NL.ptr(self.dmx), self.nwv,
+                                                 NL.ptr(self.ctl), stream),
+                 "hs_topk_runs_threshold")
 
     @staticmethod
     def _unimg(v: int) -> float:
         bits = v if v >= 0 else v ^ 0x7FFFFFFFFFFFFFFF
         return float(np.array([bits], dtype=np.int64).view(np.float64)[0])
 
-    def read_ctl(self) -> Tuple[float, int]:
-        """(the largest value not kept - the threshold or a dropped entry - in the order image,
-        candidate count): one small D2H."""
+    def bound(self) -> float:
+        """The largest value the slots do not hold (order image; one small D2H)."""
         c = self.ctl.cpu().numpy()
-        return max(self._unimg(int(c[0])), self._unimg(int(c[2]))), int(c[1])
+        return max(self._unimg(int(c[0])), self._unimg(int(c[2])))
 
-    def candidates(self, o: "OrderSource", k: int) -> Tuple["Groups", int, float]:
-        """(the compacted entries reduced to their top k, ties kept; their count; the largest
-        value not kept).  More than OCAP candidates: +inf (the caller re-runs exactly)."""
-        thr, n = self.read_ctl()
-        if n > self.OCAP:
-            return None, 0, float("inf")
-        g = Groups(self.NA, self.OCAP, self.okeys.device)
-        g.keys, g.sums, g.cnts = self.okeys, self.osums, self.ocnts
-        g.nulls = _zeros_u8(self.OCAP, self.okeys.device)
-        g.set_count(n)
-        if n > k:
-            g, n = topk_candidates(g, n, o, k)
-        return g, n, thr
+    def empty_image(self) -> int:
+        """The slot image of an empty slot (-inf, complemented to smallest-first)."""
+        neg = int(np.array([-np.inf]).view(np.int64)[0]) ^ 0x7FFFFFFFFFFFFFFF
+        return (~(neg ^ (1 << 63))) & ((1 << 64) - 1)
+
+    def candidates(self, k: int) -> Tuple["Groups", int, float]:
+        """(the slots' top k, ties at the select's resolution kept; their count; the largest
+        value the slots do not hold).  Empty slots may be among them when fewer than k live."""
+        import torch
+        L = NL.lib()
+        g = Groups(self.NA, self.cap, self.keys.device)
+        g.keys, g.sums, g.cnts = self.keys, self.sums, self.cnts
+        g.nulls = _zeros_u8(self.cap, self.keys.device)
+        if self.cap <= k:
+            return g, self.cap, self.bound()
+        ws = _topk_ws(g.device)
+        sel = torch.empty(self.cap, dtype=torch.int32, device=g.device)
+        NL.check(L.hs_topk_select(NL.ptr(self.vimg), self.cap, k, NL.ptr(ws["st"]),
+                                  NL.ptr(ws["hist"]), NL.ptr(sel), NL.ptr(ws["count"]),
+                                  NL.stream_ptr()), "hs_topk_select")
+        n = int(ws["count"].item())
+        out = g.take(sel, n)
+        out.vimg = self.vimg[sel[:n].long()] if n else self.vimg[:0]
+        return out, n, self.bound()
 
     def image(self, sums, cnts) -> "np.ndarray":
         """Order values of host group arrays in the kernel's image (larger is better)."""

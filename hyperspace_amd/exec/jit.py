@@ -795,8 +795,9 @@ def _topk_insert(aggs, hk, tk, ind: str, row: str) -> List[str]:
 
 def _topk_flush(aggs, tk, args: "Args", wid: str, key_lines) -> List[str]:
     """The wavefront's best K entries to its K slots of the candidate arrays (keys, order-value
-    images, then per aggregate sums / counts at stride TKCAP; empty slots: key ~0, image of
-    -inf), its K-th best value (TKW) and its dropped maximum (TKD) - found by a bitwise search
+    images - unsigned, smallest first, as hs_topk_select reads them - then per aggregate sums /
+    counts at stride TKCAP; empty slots: key ~0, image of -inf), its K-th best value (TKW,
+    signed image) and its dropped maximum (TKD) - found by a bitwise search
     over the lanes' order-preserving images (64 ballots), no atomics.  ``key_lines(j, ind)``
     loads entry j's key into ``tkey_`` from its row."""
     K = tk.K
@@ -824,7 +825,7 @@ def _topk_flush(aggs, tk, args: "Args", wid: str, key_lines) -> List[str]:
               f"      if (lv_ && at_ < {K}) {{",
               f"        const long long te_ = (long long)({wid}) * {K} + at_;"]
         b += key_lines(j, "        ")
-        b += [f"        {kk}[te_] = tkey_; {kv}[te_] = hs_dimg(tkv{j});"]
+        b += [f"        {kk}[te_] = tkey_; {kv}[te_] = (long long)~tki{j};"]
         for i in range(len(aggs)):
             b.append(f"        {ks}[{i} * {cap} + te_] = tks{j}_{i}; "
                      f"{kc}[{i} * {cap} + te_] = tkc{j}_{i};")
@@ -832,7 +833,8 @@ def _topk_flush(aggs, tk, args: "Args", wid: str, key_lines) -> List[str]:
               "      pos_ += __popcll(lb_); }"]
     b += [f"    for (long long e_ = pos_ + tl_; e_ < {K}; e_ += 64) {{",
           f"      const long long te_ = (long long)({wid}) * {K} + e_;",
-          f"      {kk}[te_] = ~0ull; {kv}[te_] = hs_dimg(-__builtin_inf()); }}",
+          f"      {kk}[te_] = ~0ull; {kv}[te_] = (long long)~((u64)hs_dimg(-__builtin_inf()) ^ "
+          "0x8000000000000000ull); }",
           "    for (int o_ = 32; o_ > 0; o_ >>= 1) dm_ = fmax(dm_, __shfl_xor(dm_, o_, 64));",
           "    if (tl_ == 0) {",
           f"      {kw}[{wid}] = pos_ >= {K} ? (long long)(th_ ^ 0x8000000000000000ull) : "

@@ -111,3 +111,38 @@ def test_repeated_build_keys_take_the_general_join(q3data, tmp_path):
     g, h, path, be = _run(s, q)
     assert g[0]["n"] == h[0]["n"]
     assert abs(g[0]["d"] - h[0]["d"]) <= 1e-9 * max(1.0, abs(h[0]["d"]))
+
+
+def test_three_way_q3_co_partitioned_with_orders_key_index(q3data):
+    """With an orders index bucketed by o_orderkey like the lineitem index (same bucket count,
+    same source files, covering the orders side's columns), the (customer x orders) build
+    becomes right-side predicates of a co-partitioned lineitem x orders merge join: the
+    orders filters plus o_custkey in a bitmap of the customer keys (_copart_semi)."""
+    s, c, o, li = q3data
+    hs = Hyperspace(s)
+    hs.createIndex(o, IndexConfig("ord_ok", ["o_orderkey"], ["o_custkey", "o_orderdate"]))
+    for i, seg in enumerate(["BUILDING", "FURNITURE"]):
+        d = datetime.date(1995, 3, 1) + datetime.timedelta(days=11 * i)
+        q = _q3(c, o, li, seg, d)
+        g, h, path, be = _run(s, q)
+        assert path == "native", be.fallback_reason
+        assert be.last_semi_join["probe"] == "copart" and be.last_semi_join["index"] == "ord_ok"
+        assert g[0]["lines"] == h[0]["lines"] > 0
+        assert abs(g[0]["revenue"] - h[0]["revenue"]) <= 1e-9 * abs(h[0]["revenue"])
+        # grouped by a lineitem column
+        qg = c.join(o, c["c_custkey"] == o["o_custkey"]) \
+            .filter((col("c_mktsegment") == seg) & (col("o_orderdate") < d)) \
+            .join(li, o["o_orderkey"] == li["l_orderkey"]) \
+            .groupBy(li["l_discount"]).agg(count("*").alias("n"))
+        g, h, path, be = _run(s, qg)
+        assert path == "native" and be.last_semi_join["probe"] == "copart"
+        assert sorted(map(tuple, (r.values() for r in g))) == \
+            sorted(map(tuple, (r.values() for r in h)))
+    # switched off: the orders-key bitmap path
+    s.conf.set("spark.hyperspace.mi.coPartitionedSemiJoin.enabled", "false")
+    try:
+        g, h, path, be = _run(s, _q3(c, o, li, "BUILDING", datetime.date(1995, 3, 1)))
+        assert path == "native" and be.last_semi_join["probe"] == "runs"
+        assert g[0]["lines"] == h[0]["lines"]
+    finally:
+        s.conf.set("spark.hyperspace.mi.coPartitionedSemiJoin.enabled", "true")
