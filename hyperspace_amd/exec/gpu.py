@@ -2960,36 +2960,45 @@ class GpuBackend:
         def finish() -> pa.Table:
             nonlocal groups, M
             with stage("hagg.result"):
+                hk = hk_box[0] if hk_box else None
+                tk = tk_box[0] if tk_box and tk_box[0].used else None
+                if tk is not None and hk is not None:
+                    # run top-K: candidates, the table's size and the candidates' right
+                    # columns in one copy (_topk_fast, _fd_device)
+                    fdd = self._fd_device(hk, right, rk, fd) if fd is not None else None
+                    st, host, G = self._topk_fast(tk, groups, hk, A, int(limit), fdd)
+                    while st == "over":
+                        if M >= H.MAX_SLOTS:
+                            raise Unsupported("hash aggregate table too large")
+                        M *= 4
+                        groups = run(M)
+                        st, host, G = self._topk_fast(tk_box[0], groups, hk, A, int(limit), fdd)
+                    self.htables.record(shape_key, M, G)
+                    if st == "ok":
+                        self.metrics["run_topk"] = 1
+                        ex = None
+                        if fd is not None and "fd" in host:
+                            def ex(gmap, host):
+                                _fd_columns(fd[1], fdd["cols"], host["fd"], gmap)
+                        elif fd is not None:
+                            def ex(gmap, host):
+                                self._fd_lookup(right, rk, fd[1], gmap[fd[0][0].expr_id], gmap)
+                        return self._hash_table_out(final, fns, grouping, hk, host, A, ex)
+                    # a dropped value may tie the k-th one (or ties flood the copy): exact path
+                    self.metrics["run_topk"] = 0
+                    groups = run(M, use_tk=False)
                 G, over = groups.count()
                 while over:
                     if M >= H.MAX_SLOTS:
                         raise Unsupported("hash aggregate table too large")
                     M *= 4
-                    groups = run(M)
+                    groups = run(M, use_tk=False)
                     G, over = groups.count()
                 self.htables.record(shape_key, M, G)
-                hk = hk_box[0] if hk_box else None
                 extra = None
                 if fd is not None:
                     def extra(gmap, host):
                         self._fd_lookup(right, rk, fd[1], gmap[fd[0][0].expr_id], gmap)
-                tk = tk_box[0] if tk_box and tk_box[0].used else None
-                if tk is not None and hk is not None:
-                    host = self._topk_merge(tk, groups, G, hk, A, int(limit))
-                    if host is not None:
-                        self.metrics["run_topk"] = 1
-                        return self._hash_table_out(final, fns, grouping, hk, host, A, extra)
-                    # a full top-K list may have dropped a tie of the k-th value: exact path
-                    self.metrics["run_topk"] = 0
-                    groups = run(M, use_tk=False)
-                    G, over = groups.count()
-                    while over:
-                        if M >= H.MAX_SLOTS:
-                            raise Unsupported("hash aggregate table too large")
-                        M *= 4
-                        groups = run(M, use_tk=False)
-                        G, over = groups.count()
-                    self.htables.record(shape_key, M, G)
                 if d is not None and d.world > 1:
                     groups, G = self._hash_combine_ranks(d, groups, G, A, minmax)
                 if hk is None or G == 0:
@@ -3070,15 +3079,16 @@ class GpuBackend:
         nb = len(right.table.bucket_offsets_host) - 1
         # each key probes only its own bucket (the index's Murmur3 bucketing of the right key)
         bids = np.asarray(murmur3.bucket_ids([keys.cast(rk.data_type)], nb), dtype=np.int32)
-        pb = torch.from_numpy(bids).to(self.device)
-        pk = torch.from_numpy(img.view(np.int64)).to(self.device)
+        # one upload (bucket ids and key images), rows picked on the device, one check after
+        # the gathers are queued: the lookup synchronizes once before its column copies
+        both = torch.from_numpy(np.concatenate([bids.astype(np.int64), img.view(np.int64)]))
+        both = both.to(self.device)
+        pb, pk = both[:G].to(torch.int32), both[G:]
         rstart, rlen, _ = K.probe_ranges(rc, right.table.bucket_offsets, pb, pk)
-        rs, rl = rstart.cpu().numpy(), rlen.cpu().numpy()
-        row = np.where(rl > 0, rs, -1).astype(np.int64)
-        if (row < 0).any():
-            raise RuntimeError("functional-dependency lookup: a group key has no right row")
-        idx = torch.from_numpy(row).to(self.device)
+        idx = torch.where(rlen > 0, rstart, torch.zeros_like(rstart))
         cols = K.gather_columns([right.col(a) for a in attrs], idx)
+        if int((rlen <= 0).sum().item()):
+            raise RuntimeError("functional-dependency lookup: a group key has no right row")
         for a, c in zip(attrs, cols):
             arr = c.to_arrow()
             if not arr.type.equals(a.data_type):
@@ -3217,38 +3227,58 @@ class GpuBackend:
             tk = plans[key] = H.TopKPlan(i, by_count, desc, A)
         return tk
 
-    def _topk_merge(self, tk, groups, G: int, hk, A: int, limit: int):
-        """Host group arrays of the top-``limit`` candidates of a run top-K query: the slots'
-        top k plus the table's (split keys), or None when the largest value the slots do not
-        hold reaches the k-th best value (a dropped tie is possible; the caller re-runs
-        exactly)."""
+    def _fd_device(self, hk, right: DRel, rk, fd) -> Optional[dict]:
+        """The device functional-dependency lookup of run top-K candidates
+        (``TopKPlan.gather``'s ``fd``): a single non-null integer key column and at most
+        ``TopKPlan.FD_COLS`` fixed-width right columns; None otherwise (``_fd_lookup``)."""
         from . import hash_agg as H
+        if len(hk.cols) != 1 or hk.mode not in ("packed", "raw_int") or len(fd[1]) > \
+                H.TopKPlan.FD_COLS:
+            return None
+        c = hk.cols[0]
+        if c.kind != "int" or c.nullable or c.dictionary is not None:
+            return None
+        key = right.col(rk)
+        if key.hs_type not in (NL.I8, NL.I16, NL.I32, NL.I64) or key.valid is not None or \
+                right.table.bucket_offsets is None:
+            return None
+        cols = [right.col(a) for a in fd[1]]
+        if any(x.offsets is not None for x in cols):
+            return None
+        raw = hk.mode == "raw_int"
+        mask = ((1 << c.bits) - 1) if c.bits < 64 else (1 << 64) - 1
+        return {"raw": raw, "lo": 0 if raw else int(c.lo), "shift": 0 if raw else int(c.shift),
+                "mask": mask, "key": key, "off": right.table.bucket_offsets,
+                "nb": len(right.table.bucket_offsets_host) - 1, "cols": cols}
+
+    def _topk_fast(self, tk, groups, hk, A: int, limit: int, fdd: Optional[dict] = None):
+        """(status, host group arrays, table groups) of a run top-K query from one packed copy
+        (``TopKPlan.gather``): "ok" with the top-``limit`` candidates of the slots and the
+        table (split keys); "over" when the table overflowed (grow and re-run); "exact" when
+        the largest value the slots do not hold reaches the k-th best value (a dropped tie is
+        possible) or ties of the k-th value overflow the copy (the caller re-runs exactly)."""
         i = tk.agg
         cs = i if hk.own_counts[i] else (A - 1 if hk.need_star else -1)
-        src = H.OrderSource(H.SRC_COUNT if tk.src_count else H.SRC_SUM, i, cs, desc=tk.desc)
-        gt, nt, thr = tk.candidates(limit)
-        gh, gn = (H.topk_candidates(groups, G, src, limit) if G > limit else (groups, G))
-        ht, hh = gt.to_host(nt), gh.to_host(gn)
-        # empty slots (fewer than k live entries): key ~0 with the image of -inf
-        img = gt.vimg.cpu().numpy().view(np.uint64) if nt else np.zeros(0, np.uint64)
-        empty = (ht["keys"] == np.uint64(H.EMPTY)) & (img == np.uint64(tk.empty_image()))
-        if empty.any():
-            live = ~empty
-            ht = {k: v[live] for k, v in ht.items()}
-            nt = int(live.sum())
-            if nt + gn < limit:
-                return None      # a live entry may share the empty pattern: exact path
-        host = {k: np.concatenate([ht[k], hh[k]]) for k in ht}
+        r = tk.unpack(tk.gather(groups, cs, limit, fdd), len(fdd["cols"]) if fdd else 0)
+        if r["over"]:
+            return "over", None, r["G"]
+        host = r["host"]
+        if host is None:
+            return "exact", None, r["G"]
         n = len(host["keys"])
+        if r["empty"] and n < limit:
+            return "exact", None, r["G"]     # a live entry may share the empty pattern
         if n >= limit:
             vals = np.sort(tk.image(host["sums"], host["cnts"]))[::-1]
             kth = float(vals[limit - 1])
         else:
             kth = -np.inf
-        self.metrics["run_topk_guard"] = (float(thr), float(kth), int(nt), int(G))
-        if thr >= kth:       # a dropped value may tie the k-th
-            return None
-        return host
+        self.metrics["run_topk_guard"] = (float(r["bound"]), kth, n, r["G"])
+        if r["bound"] >= kth:
+            return "exact", None, r["G"]
+        if "fd" in r:
+            host["fd"] = r["fd"]
+        return "ok", host, r["G"]
 
     def _join_hash_pair(self, node, left: DRel, right: DRel, lk, rk, fns, grouping, doms,
                         table, hk_box, tk_req=None, tk_box=None) -> None:
@@ -3788,6 +3818,27 @@ class _AggProgram:
             return None
         finish = be._agg_finish(self.final, self.fns, self.group, res)
         return QueryFuture(be, plan, finish, "native", None, t0)
+
+
+def _fd_columns(attrs, cols, fd, gmap: dict) -> None:
+    """``gmap[attr]`` from the device functional-dependency lookup (``TopKPlan.unpack``'s
+    rows, 64-bit values and validity per right column)."""
+    import torch
+    rows, vals, valid = fd
+    if (rows < 0).any():
+        raise RuntimeError("functional-dependency lookup: a group key has no right row")
+    for a, c, v, ok in zip(attrs, cols, vals, valid):
+        nd = np.dtype(str(c.data.dtype).replace("torch.", ""))
+        x = v.view(np.float64).astype(nd) if c.is_float else v.astype(nd)
+        dc = DeviceColumn(torch.from_numpy(x), None if ok.all() else
+                          torch.from_numpy(ok.astype(np.uint8)), c.atype, c.dictionary)
+        arr = dc.to_arrow()
+        if not arr.type.equals(a.data_type):
+            try:
+                arr = arr.cast(a.data_type)
+            except (pa.ArrowInvalid, pa.ArrowNotImplementedError):
+                pass
+        gmap[a.expr_id] = arr
 
 
 class _NoCondition:

@@ -451,35 +451,95 @@ class TopKPlan:
         bits = v if v >= 0 else v ^ 0x7FFFFFFFFFFFFFFF
         return float(np.array([bits], dtype=np.int64).view(np.float64)[0])
 
-    def bound(self) -> float:
-        """The largest value the slots do not hold (order image; one small D2H)."""
-        c = self.ctl.cpu().numpy()
-        return max(self._unimg(int(c[0])), self._unimg(int(c[2])))
+    OUT = 256       # candidates copied to the host (more: ties of the k-th value, exact path)
 
     def empty_image(self) -> int:
         """The slot image of an empty slot (-inf, complemented to smallest-first)."""
         neg = int(np.array([-np.inf]).view(np.int64)[0]) ^ 0x7FFFFFFFFFFFFFFF
         return (~(neg ^ (1 << 63))) & ((1 << 64) - 1)
 
-    def candidates(self, k: int) -> Tuple["Groups", int, float]:
-        """(the slots' top k, ties at the select's resolution kept; their count; the largest
-        value the slots do not hold).  Empty slots may be among them when fewer than k live."""
+    FD_COLS = 4     # right columns a device functional-dependency lookup returns
+
+    def gather(self, g: "Groups", cnt_slot: int, k: int, fd: Optional[dict] = None) -> np.ndarray:
+        """Queue the selection of the top ``k`` over the slots and the table's dense groups
+        ``g`` (count on the device) - one image array, one radix select - and the packed copy
+        of the candidates and bounds (csrc/kernels/topk_runs.hip); returns the host block (the
+        query's one synchronization).  ``fd``: the functional-dependency lookup of the
+        candidates' keys in the right table ({"raw", "lo", "shift", "mask", "key", "off", "nb",
+        "cols"}, exec/gpu.py ``_fd_device``), queued before the copy into the same block."""
         import torch
         L = NL.lib()
-        g = Groups(self.NA, self.cap, self.keys.device)
-        g.keys, g.sums, g.cnts = self.keys, self.sums, self.cnts
-        g.nulls = _zeros_u8(self.cap, self.keys.device)
-        if self.cap <= k:
-            return g, self.cap, self.bound()
-        ws = _topk_ws(g.device)
-        sel = torch.empty(self.cap, dtype=torch.int32, device=g.device)
-        NL.check(L.hs_topk_select(NL.ptr(self.vimg), self.cap, k, NL.ptr(ws["st"]),
-                                  NL.ptr(ws["hist"]), NL.ptr(sel), NL.ptr(ws["count"]),
-                                  NL.stream_ptr()), "hs_topk_select")
-        n = int(ws["count"].item())
-        out = g.take(sel, n)
-        out.vimg = self.vimg[sel[:n].long()] if n else self.vimg[:0]
-        return out, n, self.bound()
+        dev = self.keys.device
+        n = self.cap + g.cap
+        if getattr(self, "_img", None) is None or self._img.numel() < n:
+            self._img = torch.empty(n, dtype=torch.int64, device=dev)
+            self._sel = torch.empty(n, dtype=torch.int32, device=dev)
+        if getattr(self, "_out", None) is None:
+            self._out = torch.empty(self._fd_base() + self.OUT * (1 + 2 * self.FD_COLS),
+                                    dtype=torch.int64, device=dev)
+            self._host = torch.empty(self._out.numel(), dtype=torch.int64, pin_memory=True)
+        ws = _topk_ws(dev)
+        st = NL.stream_ptr()
+        empty = C.c_uint64(self.empty_image())
+        NL.check(L.hs_topk_runs_images(NL.ptr(self.vimg), NL.ptr(self.sums), NL.ptr(self.cnts),
+                                       self.cap, empty, NL.ptr(g.sums), NL.ptr(g.cnts),
+                                       NL.ptr(g.total), g.cap, self.agg, cnt_slot,
+                                       int(self.src_count), int(self.desc), NL.ptr(self._img),
+                                       st), "hs_topk_runs_images")
+        NL.check(L.hs_topk_select(NL.ptr(self._img), n, k, NL.ptr(ws["st"]), NL.ptr(ws["hist"]),
+                                  NL.ptr(self._sel), NL.ptr(ws["count"]), st), "hs_topk_select")
+        NL.check(L.hs_topk_runs_gather(NL.ptr(self._sel), NL.ptr(ws["count"]), self.OUT,
+                                       NL.ptr(self.keys), NL.ptr(self.vimg), NL.ptr(self.sums),
+                                       NL.ptr(self.cnts), self.cap, empty, NL.ptr(g.keys),
+                                       NL.ptr(g.nulls), NL.ptr(g.sums), NL.ptr(g.cnts), g.cap,
+                                       NL.ptr(g.total), NL.ptr(self.ctl), self.NA,
+                                       NL.ptr(self._out), st), "hs_topk_runs_gather")
+        if fd is not None:
+            cols = fd["cols"]
+            descs = (NL.ColDesc * max(len(cols), 1))(*[c.desc() for c in cols])
+            kd = fd["key"].desc()
+            NL.check(L.hs_topk_runs_fd(NL.ptr(self._out), self.OUT, int(fd["raw"]), fd["lo"],
+                                       fd["shift"], C.c_uint64(fd["mask"]), C.byref(kd),
+                                       NL.ptr(fd["off"]), fd["nb"], descs, len(cols),
+                                       self._out.data_ptr() + 8 * self._fd_base(), st),
+                     "hs_topk_runs_fd")
+        self._host.copy_(self._out, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        return self._host.numpy()
+
+    def _fd_base(self) -> int:
+        return 8 + self.OUT * (2 + 2 * self.NA)
+
+    def unpack(self, blk: np.ndarray, nfd: int = 0) -> dict:
+        """The host block of ``gather``: {"n" candidates selected, "bound" (the largest value
+        the slots do not hold), "G" table groups, "over" table overflow, "host" group arrays of
+        the live candidates (None when more than OUT), "empty" empty slots among them}."""
+        O, NA = self.OUT, self.NA
+        n = int(blk[0])
+        out = {"n": n, "bound": max(self._unimg(int(blk[1])), self._unimg(int(blk[2]))),
+               "G": int(blk[3]), "over": bool(blk[4]), "host": None, "empty": 0}
+        if n > O:
+            return out
+        flag = blk[8 + O:8 + O + n]
+        live = (flag & 2) == 0
+        sums = np.stack([blk[8 + (2 + a) * O:8 + (2 + a) * O + n] for a in range(NA)], axis=1)
+        cnts = np.stack([blk[8 + (2 + NA + a) * O:8 + (2 + NA + a) * O + n]
+                         for a in range(NA)], axis=1)
+        m = int(live.sum())
+        out["empty"] = n - m
+        out["host"] = {"keys": blk[8:8 + n][live].view(np.uint64).copy(),
+                       "nulls": (flag[live] & 1).astype(np.uint8),
+                       "sums": sums[live].view(np.float64).copy(),
+                       "cnts": cnts[live].copy(),
+                       "mins": np.full((m, NA), np.inf), "maxs": np.full((m, NA), -np.inf)}
+        if nfd:
+            b = self._fd_base()
+            out["fd"] = (blk[b:b + n][live].copy(),
+                         [blk[b + (1 + a) * O:b + (1 + a) * O + n][live].copy()
+                          for a in range(nfd)],
+                         [blk[b + (1 + nfd + a) * O:b + (1 + nfd + a) * O + n][live] != 0
+                          for a in range(nfd)])
+        return out
 
     def image(self, sums, cnts) -> "np.ndarray":
         """Order values of host group arrays in the kernel's image (larger is better)."""

@@ -493,10 +493,11 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
     (``jit._hash_accumulate``); kernel ``hs_jit_run_bits_hash``, no partials.
 
     With ``tk`` as well (an exec.hash_agg.TopKPlan: ORDER BY <aggregate> LIMIT k over those
-    groups), a key whose passing rows lie strictly inside one 64-entry window is final there
-    and competes for the wavefront's top-K list (registers, lane l = entry l) instead of
-    probing the table; only keys split across windows / passes / tiles go to the table (kernel
-    ``hs_jit_run_bits_topk``; every wavefront writes its list at the end)."""
+    groups), the windows are walked in row order with the last segment of each carried into
+    the next (``jit._topk_accumulate``): a key is final when the walk leaves it and competes
+    for the wavefront's top-K registers instead of probing the table; only keys that may
+    continue into the neighbouring wavefronts' tiles (at most two per wavefront) go to the
+    table (kernel ``hs_jit_run_bits_topk``; every wavefront writes its list at the end)."""
     args = J.Args()
     for n, ct in (("rstart", "const long long*"), ("rlen", "const long long*"),
                   ("tile_prefix", "const long long*")):
@@ -565,7 +566,7 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
           "    const i64 rs = rsN, re = reN, tb0 = tbN; const u64 m_ = gmN; const i64 q0 = grN;"]
     if tk is not None:
         # key run of a list entry, relative to the tile's first run (lrn_)
-        b.append("    const int qr_ = (int)(q0 - __shfl(q0, 0, 64));")
+        b.append("    const i64 qb_ = __shfl(q0, 0, 64); const int qr_ = (int)(q0 - qb_);")
     b += [
 
           "    const i64 row0 = tb0 + 64 * ln;",
@@ -678,6 +679,8 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
                 J._uload_raw(gs[k], sl, f"c{k}", f"(({ct})({ut})(pk{k}_ >> {off}))", "1", b, ind2)
             else:
                 J._uload(gs[k], sl, f"c{k}", b, ind2)
+    carry_gen = J._Gen(args, cols, SPLIT, ("tcw_", "tcw_"), frozenset(), True) \
+        if tk is not None else None
     for k in range(EW):
         g = gs[k]
         it = f"c{k}"
@@ -695,7 +698,8 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
             b += [J._rename(x, tail, it)
                   for x in J._hash_accumulate(g, aggs, hk, "cok", ind2, tk=tk,
                                               seg=f"crn{k}" if tk is not None else None,
-                                              row=f"crow{k}")]
+                                              row=f"crow{k}", run=f"qb_ + (i64)crn{k}",
+                                              carry_gen=carry_gen)]
         else:
             b += [J._rename(x, tail, it)
                   for x in J._accumulate(g, aggs, grouped, "cok", gvar, ind2)]
@@ -704,6 +708,8 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
     if hk is None:
         b += J._flush(aggs, grouped)
     if tk is not None:
+        b += J._topk_carry_final(aggs, hk, tk, "  ", carry_gen)
+
         def key_lines(j: int, ind_: str) -> List[str]:
             gk = J._Gen(args, cols, SPLIT, (f"tkr{j}", f"tkr{j}"), frozenset(), True)
             out: List[str] = []

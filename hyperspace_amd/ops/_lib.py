@@ -229,6 +229,10 @@ def lib():
     _sig(L.hs_topk_images, I, P, P, P, P, P, P, I64, I64, I, I, I, I, U64, I, I, P, P)
     _sig(L.hs_topk_select, I, P, I64, I64, P, P, P, P, P)
     _sig(L.hs_topk_runs_threshold, I, P, P, I64, P, P)
+    _sig(L.hs_topk_runs_fd, I, P, I, I, I64, I, U64, P, P, I, P, I, P, P)
+    _sig(L.hs_topk_runs_images, I, P, P, P, I64, U64, P, P, P, I64, I, I, I, I, P, P)
+    _sig(L.hs_topk_runs_gather, I, P, P, I, P, P, P, P, I64, U64, P, P, P, P, I64, P, P, I, P,
+         P)
     _sig(L.hs_hagg_take, I, P, I64, P, P, P, P, P, P, I, I64, I64, P, P, P, P, P, P, P)
     _lib = L
     return L

@@ -15,6 +15,7 @@
 #   CONFIGS       benchmarks/configs.py configs for `configs` (default "sf10_filter q3_3way hybrid")
 #   PMC_REGEX     kernel-name regex for `pmc` (default hs_jit_)
 #   QK_ARGS       extra scripts/qk_sweep.py args for `pmc` (e.g. --only-q3-full)
+#   Q3F_ARGS      extra scripts/qk_sweep.py args for `q3f` (e.g. --no-profile --cprofile=20)
 #   NPROC         ranks for `dist` (gloo, all on cuda:0; default 4)
 #   HS_PROFILE    1 = per-stage host/device tracer in the bench log
 set -o pipefail
@@ -88,8 +89,8 @@ step_configs() {
 step_q3f() {
   local cfg="$Q3F_CONFIGS"
   [ -z "$cfg" ] && cfg='[{}]'
-  HS_PROFILE=1 timeout -k 10 600 python3 scripts/qk_sweep.py --sf ${SF:-100} --reps 20 --only-q3-full \
-    --configs "$cfg" > "${O}_q3f.jsonl" 2> "${O}_q3f.log"
+  timeout -k 10 600 python3 scripts/qk_sweep.py --sf ${SF:-100} --reps 20 --only-q3-full \
+    --configs "$cfg" ${Q3F_ARGS} > "${O}_q3f.jsonl" 2> "${O}_q3f.log"
 }
 
 step_dist() {

@@ -44,8 +44,14 @@ def main():
                     help="print every resident column's compact HBM encoding after the runs")
     ap.add_argument("--decompose", action="store_true",
                     help="also time Q3 variants without the right predicate / aggregate tail")
+    ap.add_argument("--no-profile", action="store_true",
+                    help="wall times without the per-stage tracer (its HIP events cost time)")
+    ap.add_argument("--cprofile", type=int, default=0,
+                    help="also run N queries of each kind under cProfile (top functions to "
+                         "stderr)")
     args = ap.parse_args()
-    os.environ["HS_PROFILE"] = "1"
+    if not args.no_profile:
+        os.environ["HS_PROFILE"] = "1"
     # heartbeat: long silent phases (data load under a profiler) must still show progress
     import threading
     t_start = time.time()
@@ -150,6 +156,22 @@ def main():
         stages = {k: round(v["device_ms"] / max(v["calls"], 1), 4) for k, v in rep.items()}
         host = {k: round(v["host_ms"] / max(v["calls"], 1), 4) for k, v in rep.items()}
         m = {k: v for k, v in backend.metrics.items() if k.startswith("run_topk")}
+        if args.cprofile:
+            import cProfile
+            import io
+            import pstats
+            pr = cProfile.Profile()
+            pr.enable()
+            for i in range(args.cprofile):
+                fn(i).collect()
+            torch.cuda.synchronize()
+            pr.disable()
+            buf = io.StringIO()
+            st = pstats.Stats(pr, stream=buf)
+            st.sort_stats("tottime").print_stats(45)
+            st.sort_stats("cumulative").print_stats(60)
+            print(f"[qk_sweep] cProfile {fn.__name__} x{args.cprofile}\n{buf.getvalue()}",
+                  file=sys.stderr, flush=True)
         return {"wall_ms": round(wall, 4), "stages": stages, "host_stages": host,
                 "res": str(res)[:120], "metrics": m}
 

@@ -849,7 +849,8 @@ def test_merge_join_runs_matches_oracle(device, layout):
 def test_run_topk_sources_compile(rt, tmp_path):
     """The key-run bits walk in hash mode (TPC-H Q3 full shape: GROUP BY l_orderkey) with and
     without the per-wavefront top-K lists (hash_agg.TopKPlan) compiles for gfx950, and the top-K
-    form keeps the table probe only for split keys."""
+    form carries segments across windows and keeps the table probe only for keys that may
+    continue into another wavefront's tiles."""
     import types
     from hyperspace_amd.exec import hash_agg as H
     from hyperspace_amd.exec import jit_runs
@@ -866,7 +867,7 @@ def test_run_topk_sources_compile(rt, tmp_path):
         for by_count in (False, True):
             tk = H.TopKPlan(1 if by_count else 0, by_count, desc, 2)
             k = jit_runs.gen_run_sparse_scan(j, comp, hk, tk)
-            assert k.name == "hs_jit_run_bits_topk" and "htl && !hcomp" in k.src
+            assert k.name == "hs_jit_run_bits_topk" and "hprb_" in k.src and "tcr_" in k.src
             assert "TKK" in k.src and "TKW" in k.src and "tkdmx" in k.src and "lrn_" in k.src
             assert "atomic" not in k.src.split("tkdmx")[-1]     # no atomics in the top-K flush
             ks.append(k)
