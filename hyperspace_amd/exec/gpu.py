@@ -2958,6 +2958,15 @@ class GpuBackend:
         d = self._dist()
 
         def finish() -> pa.Table:
+            if fd is not None and d is not None and d.world > 1:
+                # keys partitioned by bucket: this rank's top candidates, then result rows
+                # from every rank (one exchange; the caller sorts and cuts)
+                t = local()
+                with stage("hagg.gather_rows"):
+                    return _gather_tables(d, t)
+            return local()
+
+        def local() -> pa.Table:
             nonlocal groups, M
             with stage("hagg.result"):
                 hk = hk_box[0] if hk_box else None
@@ -2999,7 +3008,7 @@ class GpuBackend:
                 if fd is not None:
                     def extra(gmap, host):
                         self._fd_lookup(right, rk, fd[1], gmap[fd[0][0].expr_id], gmap)
-                if d is not None and d.world > 1:
+                if d is not None and d.world > 1 and fd is None:
                     groups, G = self._hash_combine_ranks(d, groups, G, A, minmax)
                 if hk is None or G == 0:
                     return self._hash_table_out(final, fns, grouping, hk, None, A)
@@ -3020,7 +3029,11 @@ class GpuBackend:
         are looked up for the result groups only (``_fd_lookup``).  The reduced grouping lets
         the run-keyed two-phase join aggregate into the hash table (jit_runs hash walk).  Returns
         ([the key attribute], [right attributes]) or None.  Applies when the result is bounded
-        by an ORDER BY <aggregate> LIMIT k (device top-k) on one rank."""
+        by an ORDER BY <aggregate> LIMIT k (device top-k).  Sharded across ranks the key is
+        both sides' bucket key, so every key's groups live on one rank: each rank finishes its
+        own top candidates and the ranks exchange result rows only (``_gather_tables``); the
+        table-dependent checks are agreed once per table pair, so every rank takes the same
+        path."""
         if not HyperspaceConf.fd_group_enabled(self.session.conf):
             return None
         if left.parts or right.parts or not order or limit is None or \
@@ -3028,8 +3041,24 @@ class GpuBackend:
             return None
         d = self._dist()
         if d is not None and d.world > 1:
-            return None
-        if (right.table.num_rows or 0) * 64 < (left.table.num_rows or 0):
+            gk = (getattr(left.table, "global_key", None), getattr(right.table, "global_key", None),
+                  lk.name, rk.name, tuple(g.name for g in grouping))
+            if gk[0] is None or gk[1] is None:
+                return None
+            memo = self.__dict__.setdefault("_fd_agreed", {})
+            ok = memo.get(gk)
+            if ok is None:
+                local = self._fd_grouping_local(final, grouping, left, right, lk, rk, order)
+                ok = not d.agree_any([local is None])[0]
+                memo[gk] = ok
+            return self._fd_grouping_local(final, grouping, left, right, lk, rk, order,
+                                           check=False) if ok else None
+        return self._fd_grouping_local(final, grouping, left, right, lk, rk, order)
+
+    def _fd_grouping_local(self, final, grouping, left: DRel, right: DRel, lk, rk, order,
+                           check: bool = True):
+        """``_fd_grouping`` on this rank's tables (``check``: the data-dependent checks too)."""
+        if check and (right.table.num_rows or 0) * 64 < (left.table.num_rows or 0):
             return None          # _join_hash_pair would swap the sides
         keyg = [g for g in grouping if g.expr_id in (lk.expr_id, rk.expr_id)]
         rest = [g for g in grouping if g.expr_id not in (lk.expr_id, rk.expr_id)]
@@ -3051,7 +3080,7 @@ class GpuBackend:
             if a.expr_id == e.expr_id:
                 inner = agg.child if isinstance(agg, E.Alias) else agg
                 ok = isinstance(inner, E.AggregateFunction)
-        if not ok or jit.key_has_dups(rc):
+        if not ok or (check and jit.key_has_dups(rc)):
             return None
         g = keyg[0]
         if g.expr_id != lk.expr_id:      # the right key's attribute: group by the left's
@@ -3192,8 +3221,8 @@ class GpuBackend:
                          hk=hk, htab=table)
 
     def _topk_request(self, final, fns, order, limit, minmax):
-        """(aggregate index, by count, descending) when the query orders by one SUM / COUNT
-        aggregate with a small LIMIT (a ``TopKPlan`` can serve it), else None."""
+        """(aggregate index, by count, descending, limit) when the query orders by one SUM /
+        COUNT aggregate with a small LIMIT (a ``TopKPlan`` can serve it), else None."""
         if not order or limit is None or minmax or not 0 < int(limit) < H_TOPK_K or \
                 not HyperspaceConf.run_topk_enabled(self.session.conf):
             return None
@@ -3210,21 +3239,22 @@ class GpuBackend:
             i = next((k for k, fn in enumerate(fns) if fn is inner), None)
             if i is None:
                 return None
-            return (i, isinstance(inner, E.Count), not order[0].ascending)
+            return (i, isinstance(inner, E.Count), not order[0].ascending, int(limit))
         return None
 
     def _topk_plan(self, req, hk, A: int):
         """The cached TopKPlan of a request (buffers reused across queries), or None when the
         order aggregate keeps its own non-null count (a NULL sum has no order value there)."""
         from . import hash_agg as H
-        i, by_count, desc = req
+        i, by_count, desc, limit = req
         if (hk.own_counts[i] and not by_count) or any(c.nullable for c in hk.cols):
             return None
         plans = self.__dict__.setdefault("_tkplans", {})
-        key = (i, by_count, desc, A)
+        K = 16 if limit <= 16 else 32
+        key = (i, by_count, desc, A, K)
         tk = plans.get(key)
         if tk is None:
-            tk = plans[key] = H.TopKPlan(i, by_count, desc, A)
+            tk = plans[key] = H.TopKPlan(i, by_count, desc, A, K)
         return tk
 
     def _fd_device(self, hk, right: DRel, rk, fd) -> Optional[dict]:
@@ -3818,6 +3848,28 @@ class _AggProgram:
             return None
         finish = be._agg_finish(self.final, self.fns, self.group, res)
         return QueryFuture(be, plan, finish, "native", None, t0)
+
+
+def _gather_tables(d, t: pa.Table) -> pa.Table:
+    """Every rank's (small) result table, concatenated in rank order: Arrow IPC bytes through
+    one row all-gather (``DistContext.all_gather_rows``), no pickling."""
+    import pyarrow.ipc as ipc
+    sink = pa.BufferOutputStream()
+    with ipc.new_stream(sink, t.schema) as w:
+        w.write_table(t)
+    b = sink.getvalue().to_pybytes()
+    n = len(b)
+    words = np.frombuffer(b + b"\0" * ((-n) % 8), dtype=np.int64)
+    allr = d.all_gather_rows(np.concatenate([[n], words]).astype(np.int64).reshape(-1, 1))
+    allr = allr.reshape(-1)
+    out, i = [], 0
+    while i < len(allr):
+        nb = int(allr[i])
+        nw = (nb + 7) // 8
+        out.append(ipc.open_stream(pa.py_buffer(allr[i + 1:i + 1 + nw].tobytes()[:nb])).read_all())
+        i += 1 + nw
+    out = [x if x.schema.equals(t.schema) else x.cast(t.schema) for x in out]
+    return pa.concat_tables(out)
 
 
 def _fd_columns(attrs, cols, fd, gmap: dict) -> None:

@@ -408,10 +408,12 @@ class TopKPlan:
     A lane keeps two entries and displaces a third, and a slot tie at a wavefront's K-th value
     may be left out: when that bound reaches the k-th best value overall the caller re-runs the
     exact table path (a tie, or three of the top k in one lane of one wavefront)."""
-    K = 32
+    K = 32          # slots per wavefront (16 for LIMIT <= 16: half the select's input)
 
-    def __init__(self, agg: int, src_count: bool, desc: bool, NA: int):
+    def __init__(self, agg: int, src_count: bool, desc: bool, NA: int, K: int = 32):
+        assert K in (16, 32)
         self.agg, self.src_count, self.desc, self.NA = agg, src_count, desc, NA
+        self.K = K
         self.nwv = 0
         self.cap = 0
         self.used = False

@@ -154,10 +154,15 @@ def spmd_gpu(ctx, data_dir):
         "topk": j.groupBy(t1["k"]).agg(sum_(col("v")).alias("sv"))
                  .orderBy(col("sv").desc(), col("k")).limit(5),
         "left_outer": t1.join(t2.filter(col("w") < 3), t1["k"] == t2["k"], "left")
-                        .select(t1["k"], t2["w"])})
+                        .select(t1["k"], t2["w"]),
+        # GROUP BY (join key, right column) over a unique right key + ORDER BY ... LIMIT:
+        # functional-dependency grouping, each rank's own top rows exchanged
+        "fd_topk": t2.join(t1, t2["k"] == t1["k"]).groupBy(t2["k"], t1["v"])
+                     .agg(sum_(col("w")).alias("sw")).orderBy(col("sw").desc(), t2["k"])
+                     .limit(5)})
     for name, df in q.items():
         rows = [tuple(r.values()) for r in df.to_arrow().to_pylist()]
-        out[name] = rows if name == "topk" else sorted(rows, key=repr)
+        out[name] = rows if name in ("topk", "fd_topk") else sorted(rows, key=repr)
         out["paths"].append(s.backend().last_path)
         out[name + "_plan"] = df.queryExecution.executed_plan.tree_string()
     # steady state: the same queries again make no pickled (object) collective

@@ -165,8 +165,13 @@ def test_spmd_device_executor(tmp_path, spmd_data, device):
         for x, y in zip(a, b):
             for u, v in zip(x, y):
                 assert (abs(u - v) <= 1e-9 * max(1.0, abs(v))) if isinstance(v, float) else u == v
+    jf = t2.join(t1, "k", join_type="inner")
+    gf = jf.group_by(["k", "v"]).aggregate([("w", "sum")])
+    exp_fd = sorted(zip(gf.column("k").to_pylist(), gf.column("v").to_pylist(),
+                        gf.column("w_sum").to_pylist()), key=lambda x: (-x[2], x[0]))[:5]
     for d in res:
-        assert d["paths"] == ["native"] * 8, d["paths"]
+        assert d["paths"] == ["native"] * 9, d["paths"]
+        assert [tuple(x) for x in d["fd_topk"]] == exp_fd
         assert [tuple(x) for x in d["nonindex_join"]] == exp_s
         assert [tuple(x) for x in d["join_w"]] == exp_w
         assert [tuple(x) for x in d["join_s"]] == exp_sm

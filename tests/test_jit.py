@@ -865,7 +865,7 @@ def test_run_topk_sources_compile(rt, tmp_path):
     ks = []
     for desc in (True, False):
         for by_count in (False, True):
-            tk = H.TopKPlan(1 if by_count else 0, by_count, desc, 2)
+            tk = H.TopKPlan(1 if by_count else 0, by_count, desc, 2, 16 if desc else 32)
             k = jit_runs.gen_run_sparse_scan(j, comp, hk, tk)
             assert k.name == "hs_jit_run_bits_topk" and "hprb_" in k.src and "tcr_" in k.src
             assert "TKK" in k.src and "TKW" in k.src and "tkdmx" in k.src and "lrn_" in k.src
