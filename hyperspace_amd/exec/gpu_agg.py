@@ -1,0 +1,856 @@
+"""Fused aggregates: dense (LDS) grouped and ungrouped scan aggregates, their prepared lowerings
+and captured graphs, union / mixed-index aggregates, bucket-range streaming, the cross-rank
+combine and group-domain agreement."""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import numpy as np
+import pyarrow as pa
+
+from ..ops import _lib as NL, kernels as K
+from ..plan import expressions as E, physical as X
+from ..utils.conf import HyperspaceConf
+from ..utils.tracing import stage
+from . import compile as CP, jit
+from .arrow_eval import key
+from .device_table import DeviceColumn
+from .graphs import _cbuf, GraphPending as _GraphPending, range_bounds, ScanAggGraph
+from .gpu_common import (_compact_buffers, _eval_scalar, _GraphPrep, _group_limit, _JoinPrep,
+                         _NeedHash, _ScanPrep, _Stale, _use_on, bucket_chunks, DRel,
+                         GROUP_LDS_SCAN, log, MAX_GROUPS_SCAN, Unsupported)
+
+
+class AggOps:
+    """Aggregate operators of ``GpuBackend`` (exec/gpu.py)."""
+
+    # ------------------------------------------------------------------------------------------
+    # Aggregation
+    # ------------------------------------------------------------------------------------------
+    def _match_agg(self, plan):
+        if not (isinstance(plan, X.HashAggregateExec) and plan.mode == "final"):
+            return None
+        ex = plan.child
+        if not isinstance(ex, X.ShuffleExchangeExec):
+            return None
+        partial = ex.child
+        if not (isinstance(partial, X.HashAggregateExec) and partial.mode == "partial"):
+            return None
+        return plan, partial.child
+
+    def _exec_agg(self, final: X.HashAggregateExec, child: X.SparkPlan, order=None,
+                  limit=None):
+        """Queue a fused aggregate and return ``finish() -> pa.Table``: the dense LDS
+        aggregate for one small integer group column, else the hash-mode aggregate
+        (``_hash_agg``)."""
+        if any(not isinstance(g, E.Attribute) for g in final.grouping):
+            final, child = self._named_groups(final, child)
+        try:
+            return self._dense_agg(final, child)
+        except _NeedHash as e:
+            log.debug("hash-mode aggregate: %s", e)
+        return self._hash_agg(final, child, order, limit)
+
+    @staticmethod
+    def _named_groups(final: X.HashAggregateExec, child: X.SparkPlan):
+        """GROUP BY expressions: each named grouping expression becomes a computed column of a
+        projection over the aggregate's input (exec/project.py) and the aggregate groups on
+        that column; result expressions that repeat a grouping expression read the column."""
+        groups, extra = [], []
+        for gi, g in enumerate(final.grouping):
+            if isinstance(g, E.Attribute):
+                groups.append(g)
+            elif isinstance(g, E.Alias):
+                extra.append(g)
+                groups.append(g.to_attribute())
+            else:
+                # an unnamed grouping expression (SQL ``GROUP BY a % 3``): a hidden computed
+                # column; result expressions repeating it read that column (swap below)
+                a = E.Alias(g, f"__hs_g{gi}")
+                extra.append(a)
+                groups.append(a.to_attribute())
+
+        def swap(x):
+            for g in extra:
+                if x.semantic_equals(g.child):
+                    return g.to_attribute()
+            return None
+        aggs = []
+        for e in final.aggregates:
+            hit = next((g for g in extra if g.expr_id == getattr(e, "expr_id", None)), None)
+            if hit is not None:
+                aggs.append(hit.to_attribute())
+            else:
+                aggs.append(e.transform_up(swap))
+        proj = X.ProjectExec(list(child.output) + extra, child)
+        return X.HashAggregateExec(groups, aggs, final.mode, final.child, final.result_attrs), proj
+
+    # ------------------------------------------------------------------------------------------
+    # Bucket-range streaming: indexes larger than the HBM budget
+    # ------------------------------------------------------------------------------------------
+    def _stream_chunks(self, child) -> Optional[List[tuple]]:
+        """Bucket ranges an aggregate over ``child`` runs in, one resident range at a time, when
+        its index scans would not fit ``deviceCacheBytes`` together; None when they fit or the
+        plan cannot be split by bucket (a non-index scan, indexes of different bucket counts,
+        a Hybrid Scan union, several ranks).  Every index of the plan is cut at the same bucket
+        boundaries, so a co-partitioned join joins bucket range to bucket range
+        (BucketUnionExec.scala:61-74 runs a bucketed plan partition by partition)."""
+        if self._dist() is not None:
+            return None
+        budget = HyperspaceConf.device_cache_bytes(self.session.conf)
+        memo = self.__dict__.setdefault("_stream_memo", {})
+        hit = memo.get(id(child))
+        if hit is not None and hit[0] is child and hit[1] == budget:
+            return hit[2]       # a plan-cache hit re-submits the same nodes: decided once
+        chunks = self._stream_plan(child, budget)
+        if len(memo) > 256:
+            memo.clear()
+        memo[id(child)] = (child, budget, chunks)
+        return chunks
+
+    def _stream_plan(self, child, budget: int) -> Optional[List[tuple]]:
+        scans = child.collect(lambda x: isinstance(x, X.FileSourceScanExec))
+        # only operators that keep bucket b's rows inside bucket b: an Exchange (a join of
+        # sides bucketed on other keys) or a union would pair rows across bucket ranges
+        if not scans or child.collect(lambda x: not isinstance(
+                x, (X.FileSourceScanExec, X.FilterExec, X.ProjectExec, X.SortExec,
+                    X.SortMergeJoinExec))):
+            return None
+        nbs, per_bucket = set(), None
+        total = 0
+        for sc in scans:
+            rel = sc.relation
+            if not rel.is_index():
+                return None
+            files = rel.location.all_files()
+            nb = rel.index.num_buckets
+            if not self._all_bucket_files(rel.location, files, nb):
+                return None
+            nbs.add(nb)
+            memo = getattr(rel.location, "_hs_bucket_weights", None)
+            if memo is None or memo[0] != nb or memo[1] is not files:
+                from ..parallel.placement import bucket_weights
+                memo = (nb, files, bucket_weights(files, nb) * self.STREAM_EXPANSION)
+                rel.location._hs_bucket_weights = memo
+            w = memo[2]
+            per_bucket = w if per_bucket is None or len(per_bucket) != nb else per_bucket + w
+            total += float(w.sum())
+        if len(nbs) != 1 or total <= budget:
+            return None
+        return bucket_chunks(per_bucket, budget)
+
+    # decoded bytes per byte of a (compressed, dictionary-encoded) index file: the resident
+    # estimate of a bucket for the streaming plan
+    STREAM_EXPANSION = 4.0
+
+    def _streamed_agg(self, final, child, fns, group, chunks):
+        """The aggregate as one pass per bucket range: each pass loads its range of every
+        index (evicting the previous one), runs the fused kernels and brings its partials to
+        the host, where they combine by group value."""
+        import torch
+        A = len(fns) + 1
+        acc: Dict[object, list] = {}
+        gtype = None
+        gdict_all = None
+        self.last_stream_passes = len(chunks)
+        try:
+            for ch in chunks:
+                self._bucket_chunk = ch
+                self._drop_resident()
+                node = child
+                while isinstance(node, X.ProjectExec) and \
+                        all(isinstance(e, E.Attribute) for e in node.project_list):
+                    node = node.child
+                if isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner":
+                    res = self._join_agg(node, fns, group)
+                else:
+                    res = self._scan_agg(self._rel(child), fns, group)
+                sums, cnts, mins, maxs, G, gbase, gdict, gt = res
+                if isinstance(sums, _GraphPending):
+                    host = sums.result()
+                elif isinstance(sums, np.ndarray):
+                    host = (sums, cnts, mins, maxs)
+                else:
+                    host = K.agg_to_host_async(sums, cnts, mins, maxs)()
+                gtype = gt if gt is not None else gtype
+                s_, c_, mn_, mx_ = (np.asarray(x).reshape(G, A) for x in host)
+                for g in range(G):
+                    if c_[g, A - 1] == 0 and group is not None:
+                        continue
+                    key = None
+                    if group is not None:
+                        key = gdict[gbase + g].as_py() if gdict is not None else gbase + g
+                    cur = acc.get(key)
+                    if cur is None:
+                        acc[key] = [s_[g].copy(), c_[g].copy(), mn_[g].copy(), mx_[g].copy()]
+                    else:
+                        cur[0] += s_[g]
+                        cur[1] += c_[g]
+                        cur[2] = np.minimum(cur[2], mn_[g])
+                        cur[3] = np.maximum(cur[3], mx_[g])
+                del res, sums, cnts, mins, maxs
+                torch.cuda.current_stream().synchronize()
+        finally:
+            self._bucket_chunk = None
+            self._drop_resident()
+        if group is None:
+            if None not in acc:
+                acc[None] = [np.zeros(A), np.zeros(A, np.int64), np.full(A, np.inf),
+                             np.full(A, -np.inf)]
+            keys = [None]
+        else:
+            keys = sorted(acc)
+            if gtype is not None and pa.types.is_string(gtype):
+                gdict_all = pa.array(keys, type=pa.string())
+        G = max(len(keys), 1)
+        host = tuple(np.concatenate([acc[k][i] for k in keys]) if keys else
+                     np.zeros(A) for i in range(4))
+        if group is not None and gdict_all is None:
+            # integer group values: lay the rows out over their own domain order
+            gvals = keys
+            gbase = 0
+
+            def finish() -> pa.Table:
+                return self._agg_table_values(final, fns, group, host, G, A, gvals, gtype)
+            return finish
+        gbase = 0
+        gd = gdict_all
+
+        def finish() -> pa.Table:
+            return self._agg_table(final, fns, group, host, G, A, gbase, gd, gtype)
+        return finish
+
+    def _drop_resident(self) -> None:
+        """Release every device table this backend holds: the cache and the per-table memos
+        (scan nodes, null flags, domains, prepared submissions) that keep tables alive."""
+        self.cache.clear()
+        for memo in ("_scans", "_nulls_memo"):
+            self.__dict__.pop(memo, None)
+        self._domains.clear()
+        preps = getattr(self, "_agg_preps", None)
+        if preps:
+            preps.clear()
+        self._join_rec = None
+
+    def _agg_table_values(self, final, fns, group, host, G, A, gvals, gtype) -> pa.Table:
+        """``_agg_table`` over explicit integer group values (row g has group ``gvals[g]``)."""
+        s, c, mn, mx = (x.reshape(G, A) for x in host)
+        rows = [g for g in range(G) if c[g, A - 1] > 0]
+        vals = {}
+        for i, fn in enumerate(fns):
+            vals[id(fn)] = [CP.finalize_value(fn, s[g, i], c[g, i], mn[g, i], mx[g, i]) for g in rows]
+        raw = [gvals[g] for g in rows]
+        if pa.types.is_date32(gtype):
+            gv = pa.array(np.array(raw, dtype=np.int32)).view(pa.date32()).to_pylist()
+        else:
+            gv = raw
+        out_cols = [self._agg_output(e, group, gv, vals, len(rows)) for e in final.aggregates]
+        arrays = []
+        for a, vlist in zip(final.output, out_cols):
+            try:
+                arrays.append(pa.array(vlist, type=a.data_type))
+            except (pa.ArrowInvalid, pa.ArrowTypeError):
+                arrays.append(pa.array(vlist))
+        return pa.Table.from_arrays(arrays, names=[a.name for a in final.output])
+
+    def _agg_prep_get(self, final) -> Optional["_ScanPrep"]:
+        """The prepared scan of a fused aggregate node submitted before (plan-cache hits
+        submit the same node objects with new literal values), while its table is resident."""
+        preps = self.__dict__.get("_agg_preps")
+        if not preps:
+            return None
+        pr = preps.get(id(final))
+        if pr is None or pr.final is not final or pr.placement != self._placement_tag() or \
+                not all(self._holds(t) for t in pr.tables()):
+            return None
+        return pr
+
+    def _agg_prep_put(self, final, r: DRel) -> None:
+        """Keep what the fused scan of ``final`` lowered, for its next submission: only for a
+        relation of one resident table with no computed columns (their values are literal
+        dependent) whose lowering completed."""
+        st = getattr(self, "_scan_gs", None)
+        if st is None or r.parts or r.extra or r.split or \
+                getattr(r.table, "_hs_cache_key", None) is None:
+            return
+        col_info, descs, gs, p = st
+        preps = self.__dict__.setdefault("_agg_preps", {})
+        if len(preps) > 256:
+            preps.clear()
+        preps[id(final)] = _ScanPrep(final, r, col_info, descs, gs, p,
+                                     getattr(self, "_last_graph_prep", None),
+                                     self._placement_tag())
+
+    def _join_prep_put(self, final, node, res) -> None:
+        """Keep a co-located merge join aggregate's lowering (one left x right pair over full
+        bucket ranges, resident tables) for its next submission."""
+        rec = getattr(self, "_join_rec", None)
+        self._join_rec = None
+        if rec is None or res is None or rec[6] is None:
+            return
+        left, right, lk, rk, col_info, descs, launcher, specs, lconds = rec
+        for t in (left.table, right.table):
+            if getattr(t, "_hs_cache_key", None) is None:
+                return
+        preps = self.__dict__.setdefault("_agg_preps", {})
+        if len(preps) > 256:
+            preps.clear()
+        preps[id(final)] = _JoinPrep(final, node, left, right, lk, rk, col_info, descs,
+                                     launcher, res[4:], self._placement_tag(),
+                                     self._groups_agreed, lconds)
+
+    def _placement_tag(self):
+        d = self._dist()
+        return None if d is None else (d.rank, d.world, self.session.conf.get(
+            "spark.hyperspace.mi.bucketPlacement", "balanced"))
+
+    def _dense_agg(self, final: X.HashAggregateExec, child: X.SparkPlan):
+        """Queue a fused aggregate and return ``finish() -> pa.Table``.  Nothing here waits on
+        the device: kernels, the cross-rank combine and the D2H of the tiny result block are
+        stream-ordered, so the host can plan and submit the next query while this one runs
+        (``collect_async``)."""
+        fns = [fn for _, fn in X.agg_functions(final.aggregates)]
+        if len(final.grouping) > 1:
+            raise _NeedHash("multi-column group by")
+        group = final.grouping[0] if final.grouping else None
+        if group is not None and not isinstance(group, E.Attribute):
+            raise Unsupported("group by expression")
+        node = child
+        while isinstance(node, X.ProjectExec) and all(isinstance(e, E.Attribute) for e in node.project_list):
+            node = node.child
+        self._groups_agreed = False
+        self.last_stream_passes = 0
+        chunks = self._stream_chunks(child)
+        if chunks is not None:
+            return self._streamed_agg(final, child, fns, group, chunks)
+        res = None
+        prep = self._agg_prep_get(final)
+        if prep is not None:
+            try:
+                res = prep.run(self, fns, group)
+            except _Stale:
+                self._agg_preps.pop(id(final), None)
+                res = None
+            if res is not None:
+                self._prog_candidate = (final, fns, group, prep, self.cache.epoch)
+        if res is not None:
+            pass
+        elif isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner":
+            res = self._semi_join_agg(node, fns, group)
+        if res is not None:
+            pass
+        elif isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner":
+            self._join_rec = None
+            res = self._join_agg(node, fns, group)
+            self._join_prep_put(final, node, res)
+        elif group is None and isinstance(node, X.UnionExec) and \
+                str(self.session.conf.get("spark.hyperspace.mi.unionAgg.enabled", "true")).lower() \
+                == "true":
+            res = self._union_agg(node, fns)
+        elif group is None and (res := self._mixed_index_agg(child, fns)) is not None:
+            pass
+        else:
+            r = self._rel(child)
+            self._scan_gs = None
+            self._last_graph_prep = None
+            res = self._scan_agg(r, fns, group)
+            self._agg_prep_put(final, r)
+        return self._agg_finish(final, fns, group, res)
+
+    def _agg_finish(self, final, fns, group, res):
+        """``finish() -> pa.Table`` of a queued fused aggregate ``res`` = (sums, counts, mins,
+        maxs, G, gbase, gdict, gtype): the cross-rank combine (sharded placement) is queued
+        now, stream-ordered behind the kernels; the result is read when ``finish`` runs."""
+        sums, cnts, mins, maxs, G, gbase, gdict, gtype = res
+        d = self._dist()
+        A = len(fns) + 1  # + implicit count(*)
+        if isinstance(sums, _GraphPending) and d is not None and d.world > 1:
+            # sharded: combine this rank's partials straight from the graph's device output
+            # (stream-ordered after the replay; the next replay is ordered after the collective)
+            if sums.graph.on_side:
+                import torch
+                # the replay ran on the side stream: the collective on this stream waits for it
+                torch.cuda.current_stream().wait_stream(self._side)
+            sums, cnts, mins, maxs = sums.graph.out
+        if isinstance(sums, _GraphPending):
+            fetch = sums.result
+        elif d is not None and d.world > 1:
+            with stage("agg.combine_ranks"):
+                if group is not None and not self._groups_agreed:
+                    sums, cnts, mins, maxs, G, gbase, gdict, gtype = self._agree_groups(
+                        d, sums, cnts, mins, maxs, G, gbase, gdict, gtype, A)
+                fetch = d.combine_aggs_async(sums, cnts, mins, maxs)
+        elif isinstance(sums, np.ndarray):
+            host = (sums, cnts, mins, maxs)
+            fetch = (lambda: host)
+        else:
+            fetch = K.agg_to_host_async(sums, cnts, mins, maxs)
+
+        def finish() -> pa.Table:
+            with stage("agg.result"):
+                host = fetch()
+            return self._agg_table(final, fns, group, host, G, A, gbase, gdict, gtype)
+        return finish
+
+    def _agg_table(self, final, fns, group, host, G, A, gbase, gdict, gtype) -> pa.Table:
+        s, c, mn, mx = (x.reshape(G, A) for x in host)
+        rows = [g for g in range(G) if c[g, A - 1] > 0] if group is not None else [0]
+        vals = {}
+        for i, fn in enumerate(fns):
+            vals[id(fn)] = [CP.finalize_value(fn, s[g, i], c[g, i], mn[g, i], mx[g, i]) for g in rows]
+        gvals = None
+        if group is not None:
+            raw = [gbase + g for g in rows]
+            if gdict is not None:
+                gvals = [gdict[int(v)].as_py() for v in raw]
+            elif pa.types.is_date32(gtype):
+                gvals = pa.array(np.array(raw, dtype=np.int32)).view(pa.date32()).to_pylist()
+            else:
+                gvals = raw
+        out_cols = []
+        for e in final.aggregates:
+            out_cols.append(self._agg_output(e, group, gvals, vals, len(rows)))
+        arrays = []
+        for a, vlist in zip(final.output, out_cols):
+            try:
+                arrays.append(pa.array(vlist, type=a.data_type))
+            except (pa.ArrowInvalid, pa.ArrowTypeError):
+                arrays.append(pa.array(vlist))
+        return pa.Table.from_arrays(arrays, names=[a.name for a in final.output])
+
+    def _agree_groups(self, d, sums, cnts, mins, maxs, G, gbase, gdict, gtype, A):
+        """Re-key grouped partials onto the union group domain of all ranks.
+
+        Every rank aggregated only its own buckets (index) or files (non-index), so its [G, A]
+        partials are laid out over its *local* domain — integer range ``[gbase, gbase+G)`` or the
+        rank's own string dictionary.  The ranks exchange those domains with tensor collectives
+        (an all-gather of (G, base, live) and, for string keys, the raw-buffer dictionary union
+        of ``parallel/dictionary.py`` — nothing is pickled), scatter their rows into the union
+        layout, and only then run the element-wise all-reduce.  Ranks that saw no rows do not
+        contribute an integer domain."""
+        import torch
+        from ..parallel.dictionary import union_sorted
+        from ..parallel.gather import _all_gather_flat
+        live_here = bool(cnts.view(G, A)[:, A - 1].sum().item() > 0)
+        cdev = d.device if d.backend == "nccl" else torch.device("cpu")
+        info = torch.tensor([G, gbase, 1 if live_here else 0, 1 if gdict is not None else 0],
+                            dtype=torch.int64, device=cdev)
+        allinfo = _all_gather_flat(d, info).view(d.world, 4).cpu().numpy()
+        live = [x for x in allinfo if x[2]]
+        if any(x[3] for x in allinfo):
+            local = gdict if (live_here and gdict is not None) else pa.array([], pa.string())
+            new_dict = union_sorted(local, d)       # collective: every rank calls it
+            if not live:
+                z = self._empty_agg(A, 1)
+                return (*z, 1, 0, None, gtype)
+            Gg, base = max(len(new_dict), 1), 0
+            if live_here and gdict is not None and len(gdict):
+                import pyarrow.compute as pc
+                idx = pc.index_in(gdict.cast(pa.string()), value_set=new_dict).to_numpy(
+                    zero_copy_only=False).astype(np.int64).tolist()
+            else:
+                idx = []
+        else:
+            if not live:
+                z = self._empty_agg(A, 1)
+                return (*z, 1, 0, None, gtype)
+            base = int(min(x[1] for x in live))
+            Gg = int(max(x[1] + x[0] for x in live)) - base
+            new_dict = None
+            idx = list(range(gbase - base, gbase - base + G)) if live_here else []
+        s2, c2, mn2, mx2 = self._empty_agg(A, Gg)
+        if idx:
+            it = torch.tensor(idx, dtype=torch.int64, device=self.device)
+            for dst, src in ((s2, sums), (c2, cnts), (mn2, mins), (mx2, maxs)):
+                dst.view(Gg, A)[it] = src.view(G, A)[:len(idx)]
+        return s2, c2, mn2, mx2, Gg, base, new_dict, gtype
+
+    def _agg_output(self, e, group, gvals, vals, nrows):
+        inner = e.child if isinstance(e, E.Alias) else e
+        if isinstance(inner, E.AggregateFunction):
+            return vals[id(inner)]
+        if group is not None and isinstance(inner, E.Attribute) and inner.expr_id == group.expr_id:
+            return gvals
+        # arithmetic over aggregates (e.g. sum(a)/count(b)) evaluated on the host
+        out = []
+        for r in range(nrows):
+            out.append(_eval_scalar(inner, lambda fn: vals[id(fn)][r],
+                                    lambda a: gvals[r] if group is not None and a.expr_id == group.expr_id
+                                    else None))
+        return out
+
+    def _group_spec(self, r: DRel, group, limit):
+        """(agreed, G, base, dictionary, arrow type) of a group column, or None when empty.
+
+        ``agreed`` is True when ``[base, base+G)`` is the domain over ALL ranks: partials laid
+        out over it combine with a plain element-wise reduction, no per-query domain exchange.
+        It is agreed once per (table identity, column) — a key every rank computes identically,
+        unlike device-cache residency — and cached, so steady-state queries run no collective
+        here."""
+        if group is None:
+            return -1, 1, 0, None, None
+        c = r.col(group)
+        if c.is_float:
+            raise _NeedHash("float group key")
+        d = self._dist()
+        multi = d is not None and d.world > 1
+        if c.valid is not None:
+            nulls = self._has_nulls(c)
+            if multi:
+                nulls = d.agree_any([nulls])[0]
+            if nulls:
+                # NULL is a group of its own (Spark): the hash-mode aggregate keys it
+                raise _NeedHash("nullable group key")
+        gkey = getattr(r.table, "global_key", None) if r.table is not None else None
+        if c.dictionary is not None:
+            G = len(c.dictionary)
+            base = 0
+        else:
+            base, G = self._local_domain(c)
+            if multi and gkey is not None and not getattr(c, "hs_transient", False):
+                k = (gkey, r.colmap.get(group.expr_id))
+                dom = self._gdomains.get(k)
+                if dom is None:
+                    # (min, max) over ranks with one small all-reduce (no object collective)
+                    import torch
+                    cdev = d.device if d.backend == "nccl" else torch.device("cpu")
+                    big = 1 << 62
+                    t = torch.tensor([-base if G > 0 else -big, base + G - 1 if G > 0 else -big],
+                                     dtype=torch.int64, device=cdev)
+                    d.all_reduce(t, "max")
+                    lo, hi = -int(t[0].item()), int(t[1].item())
+                    dom = (lo, hi - lo + 1) if hi >= lo else (0, 0)
+                    self._gdomains[k] = dom
+                base, G = dom
+                # identical on every rank, so the fallback decision is unanimous by construction
+                if G > limit:
+                    raise _NeedHash("group domain too large for LDS aggregation")
+                return (True, G, base, None, c.atype) if G > 0 else None
+        too_big = G > limit
+        if multi:
+            # data-dependent fallbacks must be unanimous, or ranks diverge in their collectives
+            too_big = d.agree_any([too_big])[0]
+        if too_big:
+            raise _NeedHash("group domain too large for LDS aggregation")
+        if G == 0:
+            return None
+        return None, max(G, 1), base, c.dictionary, c.atype
+
+    def _has_nulls(self, c: DeviceColumn) -> bool:
+        """Whether a device column holds a null (cached per resident column)."""
+        memo = self.__dict__.setdefault("_nulls_memo", {})
+        hit = memo.get(id(c))
+        if hit is not None and hit[0] is c:
+            return hit[1]
+        v = bool((c.valid == 0).any().item())
+        if not getattr(c, "hs_transient", False):
+            if len(memo) > 4096:
+                memo.clear()
+            memo[id(c)] = (c, v)
+        return v
+
+    def _local_domain(self, c: DeviceColumn):
+        """(min, max - min + 1) of an integer column on this rank; tables are immutable, so it
+        is computed once per column."""
+        ck = id(c)
+        hit = self._domains.get(ck)
+        if hit is not None and hit[0] is c:
+            return hit[1]
+        transient = getattr(c, "hs_transient", False)   # a per-query column: not cached
+        import torch
+        vals = c.data if c.valid is None else c.data[c.valid.bool()]
+        if vals.numel() == 0:
+            dom = (0, 0)
+        else:
+            lo, hi = torch.aminmax(vals)
+            dom = (int(lo.item()), int(hi.item()) - int(lo.item()) + 1)
+        if not transient:
+            self._domains[ck] = (c, dom)
+        return dom
+
+    def _agg_specs(self, fns, col_info):
+        specs = [CP.agg_spec(fn, lambda a: col_info(a).slot) for fn in fns]
+        star = NL.AggSpec()
+        star.kind, star.nterms = NL.AK_COUNT_STAR, 0
+        specs.append(star)
+        if len(specs) > NL.MAX_AGGS:
+            raise Unsupported("too many aggregates")
+        return specs
+
+    def _mixed_index_agg(self, child: X.SparkPlan, fns):
+        """An ungrouped aggregate over Filter / Project of an index scan whose file list also
+        holds appended source files (FilterIndexRule's Hybrid Scan appends them to the index
+        relation, ``RuleUtils`` same-scan appended files): the index bucket files load as the
+        bucket-sorted table - so the scan keeps its leading-key range pruning - and the appended
+        files as a flat table; one fused scan aggregate each, partials combined on the device.
+        None when the shape does not qualify (one flat table of every file then)."""
+        import torch
+        if str(self.session.conf.get("spark.hyperspace.mi.mixedScanAgg.enabled", "true")).lower() \
+                != "true":
+            return None
+        d = self._dist()
+        if d is not None and d.world > 1:
+            return None
+        chain, node = [], child
+        while isinstance(node, (X.FilterExec, X.ProjectExec)):
+            chain.append(node)
+            node = node.child
+        if not isinstance(node, X.FileSourceScanExec) or not node.relation.is_index():
+            return None
+        rel = node.relation
+        nb = rel.index.num_buckets
+        files = rel.location.all_files()
+        if self._all_bucket_files(rel.location, files, nb):
+            return None
+        from ..io.writer import get_bucket_id
+        from ..utils import path_utils as P
+
+        def is_bucket(f) -> bool:
+            b = get_bucket_id(P.get_name(f.path))
+            return b is not None and b < nb
+        bfiles = [f for f in files if is_bucket(f)]
+        afiles = [f for f in files if not is_bucket(f)]
+        if not bfiles or not afiles:
+            return None
+        res = []
+        for fs, bk in ((bfiles, True), (afiles, False)):
+            r = self._scan(node, fs, bk)
+            for n in reversed(chain):
+                r = self._unary(n, r)
+            res.append(self._scan_agg(r, fns, None, graph_ok=False))
+            if bk:
+                pruned = self.metrics.get("scan_key_ranges")
+        self.metrics["scan_key_ranges"] = pruned     # the bucket files' scan, not the flat one
+        sums, cnts, mins, maxs = (t.clone() for t in res[0][:4])
+        x = res[1]
+        sums.add_(x[0])
+        cnts.add_(x[1])
+        torch.minimum(mins, x[2], out=mins)
+        torch.maximum(maxs, x[3], out=maxs)
+        self.metrics["mixed_scan_agg"] = (len(bfiles), len(afiles))
+        return sums, cnts, mins, maxs, 1, 0, None, None
+
+    def _union_agg(self, node: X.UnionExec, fns):
+        """An ungrouped aggregate over UNION ALL (a Hybrid Scan filter query: the index scan
+        plus the appended files, FilterIndexRule's hybrid union) as one fused scan aggregate
+        per branch - the index branch keeps its key-range pruning - with the partial results
+        combined on the device (an aggregate distributes over UNION ALL), instead of
+        materializing and concatenating every branch's rows first."""
+        import torch
+        res = []
+        for child in node.children:
+            r = self._rel(child)
+            if r.parts or r.table is None:
+                raise Unsupported("union branch is a bucket union")
+            colmap = dict(r.colmap)
+            for u, c in zip(node.output, child.output):
+                if c.expr_id in r.colmap:
+                    colmap[u.expr_id] = r.colmap[c.expr_id]
+            res.append(self._scan_agg(r.copy(colmap=colmap), fns, None, graph_ok=False))
+        sums, cnts, mins, maxs = (t.clone() for t in res[0][:4])
+        for x in res[1:]:
+            sums.add_(x[0])
+            cnts.add_(x[1])
+            torch.minimum(mins, x[2], out=mins)
+            torch.maximum(maxs, x[3], out=maxs)
+        return sums, cnts, mins, maxs, 1, 0, None, None
+
+    def _scan_agg(self, r: DRel, fns, group, prep: Optional["_ScanPrep"] = None,
+                  graph_ok: bool = True):
+        """Fused scan + filter + aggregate.  ``prep`` (a plan-cache hit submitting the same plan
+        nodes again, ``_dense_agg``) carries what does not depend on literal values - column
+        slots, group domain, compact encodings, the generated kernel, the captured graph and
+        the column argument slots - so only the literal-dependent work runs: range bounds,
+        predicate values, aggregate terms, the args block and the launch."""
+        if prep is None:
+            col_info, descs = self._column_infos([(r, 0)])
+        else:
+            col_info, descs = prep.col_info, prep.descs
+        nd = len(descs)
+        lkey = prep.literal_key() if prep is not None else None
+        low = prep.lowered.get(lkey) if lkey is not None else None
+        if low is None:
+            implied: set = set()
+            spec = self._range_spec(r, r.conds, implied)
+            bound = CP.bind(CP.to_cnf([c for c in r.conds if id(c) not in implied]), col_info,
+                            self.device)
+            specs = self._agg_specs(fns, col_info)
+            if lkey is not None:
+                if len(prep.lowered) >= 1024:
+                    prep.lowered.clear()
+                prep.lowered[lkey] = (spec, bound, specs)
+        else:
+            spec, bound, specs = low
+        graph = graph_ok and self._graph_eligible(spec, descs)
+        self.metrics["scan_key_ranges"] = spec is not None   # leading-key range pruning
+        if not graph:
+            with stage("scan.ranges"):
+                rstart, rlen, _ = self._ranges(r, r.conds) if spec is not None else \
+                    self._full_ranges(r.table)
+        if prep is None:
+            gs = self._group_spec(r, group, _group_limit(MAX_GROUPS_SCAN, GROUP_LDS_SCAN,
+                                                         len(fns)))
+        else:
+            gs = prep.gs
+            if len(descs) != nd or (prep.graph is not None) != graph:
+                raise _Stale()
+        if gs is None:  # empty group column
+            return (*self._empty_agg(len(specs)), 1, 0, None, None)
+        agreed, G, gbase, gdict, gtype = gs
+        self._groups_agreed = agreed is True
+        if prep is None:
+            p = NL.ScanParams()
+            # a single-valued group key runs the register-accumulating (ungrouped) kernel
+            p.group_col = col_info(group).slot if (group is not None and G > 1) else -1
+            p.num_groups, p.group_base = G, gbase
+            for s_, c in descs.items():
+                p.cols[s_] = c.desc()
+        else:
+            p = prep.params
+        for i, pr in enumerate(bound.preds):
+            p.preds[i] = pr
+        p.npreds = len(bound.preds)
+        for i, a in enumerate(specs):
+            p.aggs[i] = a
+        p.naggs = len(specs)
+        self._scan_gs = (col_info, descs, gs, p)
+        if bound.always_false:
+            out = self._empty_agg(len(specs), G)
+        elif graph:
+            with stage("scan.graph"):
+                out = self._scan_agg_graph(r, p, spec,
+                                           p.naggs * (p.num_groups if p.group_col >= 0 else 1),
+                                           descs, keep=bound.buffers,
+                                           prep=prep.graph if prep is not None else None,
+                                           lkey=lkey)
+        else:
+            with stage("scan.agg_kernel"):
+                tp = K.ranges_to_tiles(rlen)
+                if HyperspaceConf.codegen_enabled(self.session.conf):
+                    out = jit.scan_agg(p, rstart, rlen, tp, self._compacts(descs),
+                                       nrows=r.table.num_rows)
+                else:
+                    out = K.scan_agg(p, rstart, rlen, tp)
+        return (*out, G, gbase, gdict, gtype)
+
+    def _graph_eligible(self, spec, descs) -> bool:
+        """Replay a captured hipGraph for this scan (exec/graphs.py): generated kernels and a
+        range search over all of this rank's buckets (equality bucket pruning changes the
+        launch shape)."""
+        if spec is None or spec[5] is not None:
+            return False
+        conf = self.session.conf
+        return HyperspaceConf.codegen_enabled(conf) and HyperspaceConf.hipgraph_enabled(conf)
+
+    def _scan_agg_graph(self, r: DRel, p: NL.ScanParams, spec, GA: int, descs=None, keep=(),
+                        prep: Optional["_GraphPrep"] = None, lkey=None):
+        kc, lo, lo_incl, hi, hi_incl, _ = spec
+        if prep is None or prep.GA != GA or self.graphs.peek(prep.key) is not prep.g:
+            prep = self._graph_prep(r, p, kc, GA, descs)
+            self._last_graph_prep = prep
+        g, k, compacts = prep.g, prep.k, prep.compacts
+        hit = prep.packed.get(lkey) if lkey is not None else None
+        if hit is None:
+            values = dict(prep.values)
+            jit.fill_preds_aggs(values, [(i, p.preds[i]) for i in range(p.npreds)],
+                                [p.aggs[i] for i in range(p.naggs)], compacts)
+            # (the per-query predicate buffers the block points to stay referenced with it)
+            hit = (range_bounds(lo, lo_incl, hi, hi_incl), _cbuf(k.args.pack(values)),
+                   list(keep))
+            if lkey is not None:
+                if len(prep.packed) >= 1024:
+                    prep.packed.clear()
+                prep.packed[lkey] = hit
+        bounds, packed, _ = hit
+        side = self._scan_side_stream(g)
+        if side is None:
+            if g.on_side:
+                import torch
+                # side-stream scans were switched off after this pipeline replayed there: its
+                # shared intermediates are free only once those replays are done
+                torch.cuda.current_stream().wait_stream(g.side_stream)
+            handle = g.launch(bounds, packed)
+            return (_GraphPending(g, handle), None, None, None)
+        import torch
+        # a warm pipeline (replays only: no module load, capture or cache fill left) runs on
+        # the side stream, after everything queued so far, so it overlaps the queries queued
+        # next on this stream (a Q6 scan beside a Q3 merge join: profiles/bench_side_stream_r3).
+        # Every replay of the pipeline goes there (its intermediates stay ordered); the
+        # buffers it reads are marked in use by that stream, so memory the caller frees
+        # meanwhile is not handed out again before the replay is done.
+        side.wait_stream(torch.cuda.current_stream())
+        if prep.marked is not side:
+            for c in list((descs or {}).values()) + [kc]:
+                for x in (c.data, c.valid):
+                    if x is not None:
+                        _use_on(x, side)
+            # the generated kernel reads the compact codes (jit._fill_common) rather than
+            # c.data: those buffers are in use by the side stream too (a device-cache eviction
+            # between this launch and its fetch must not hand their memory to query-stream
+            # allocations).  One record per buffer and stream covers every later replay.
+            for enc in (compacts or {}).values():
+                for x in _compact_buffers(enc):
+                    _use_on(x, side)
+            for x in g.buffers():
+                _use_on(x, side)
+            prep.marked = side
+        for x in keep:      # per-query predicate buffers (IN sets, key bitmaps)
+            _use_on(x, side)
+        with torch.cuda.stream(side):
+            handle = g.launch(bounds, packed)
+        return (_GraphPending(g, handle), None, None, None)
+
+    def _graph_prep(self, r: DRel, p: NL.ScanParams, kc, GA: int, descs) -> "_GraphPrep":
+        """The literal-independent part of a graph-replayed scan: kernel, graph, and the args
+        slots of the columns and the graph's own buffers."""
+        t = r.table
+        nb = t.num_buckets
+        grid = jit.SCAN_GRID or NL.lib().hs_scan_grid()
+        compacts = self._compacts(descs or {})
+        vec = jit.scan_vec(p, compacts, t.num_rows)
+        shape = jit.scan_agg_shape(p, compacts, vec)
+        k = jit.kernel_for(shape, lambda: jit.gen_scan_agg(p, compacts, vec))
+        key = (shape, kc.data.data_ptr(), kc.valid.data_ptr() if kc.valid is not None else 0,
+               kc.hs_type, t.bucket_offsets.data_ptr(), nb, grid, GA)
+        shmem = GA * 32 if p.group_col >= 0 else 0
+        g = self.graphs.get(key, lambda: ScanAggGraph(k, kc.desc(), t.bucket_offsets, nb, grid,
+                                                      GA, shmem, self.device, vec))
+        values = g.values_template()
+        values.update({"num_groups": p.num_groups, "group_base": p.group_base,
+                       "nrows": t.num_rows})
+        jit._fill_cols(values, p.cols, compacts)
+        return _GraphPrep(key, g, k, compacts, values, GA)
+
+    def _scan_side_stream(self, g):
+        """The side stream warm scan pipelines replay on (None: replay on the current stream)."""
+        if not HyperspaceConf.side_stream_scans(self.session.conf):
+            return None
+        if not (g.on_side or g.replays > 0):
+            return None
+        import torch
+        s = getattr(self, "_side", None)
+        if s is None:
+            s = self._side = torch.cuda.Stream(device=self.device)
+        g.on_side = True
+        g.side_stream = s
+        return s
+
+    def _compacts(self, descs: Dict[int, DeviceColumn]) -> Optional[dict]:
+        """Compact HBM encodings (exec/encoding.py) the generated kernels read instead."""
+        if not HyperspaceConf.hbm_compression_enabled(self.session.conf):
+            return None
+        from .encoding import compact_of
+        out = {}
+        for s, c in descs.items():
+            if getattr(c, "hs_transient", False):
+                continue    # a per-query intermediate: analysing it costs more than it saves
+            enc = compact_of(c)
+            if enc is not None:
+                out[s] = enc
+        return out
+
+    def _empty_agg(self, A, G=1):
+        import torch
+        z = torch.zeros(G * A, dtype=torch.float64, device=self.device)
+        zc = torch.zeros(G * A, dtype=torch.int64, device=self.device)
+        return z, zc, torch.full_like(z, float("inf")), torch.full_like(z, float("-inf"))

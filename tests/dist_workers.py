@@ -160,8 +160,14 @@ def spmd_gpu(ctx, data_dir):
         "fd_topk": t2.join(t1, t2["k"] == t1["k"]).groupBy(t2["k"], t1["v"])
                      .agg(sum_(col("w")).alias("sw")).orderBy(col("sw").desc(), t2["k"])
                      .limit(5)})
+    # semi-join: t3 (no index, behind a hash Exchange, unique keys) x the t1 index
+    t3 = s.read.parquet(os.path.join(data_dir, "t3"))
+    q["semi_keys"] = t3.join(t1, t3["k"] == t1["k"]).agg(sum_(col("v")).alias("sv"),
+                                                          count("*").alias("n"))
     for name, df in q.items():
         rows = [tuple(r.values()) for r in df.to_arrow().to_pylist()]
+        if name == "semi_keys":
+            out["semi_exchange"] = getattr(s.backend(), "last_semi_exchange", None)
         out[name] = rows if name in ("topk", "fd_topk") else sorted(rows, key=repr)
         out["paths"].append(s.backend().last_path)
         out[name + "_plan"] = df.queryExecution.executed_plan.tree_string()
@@ -178,6 +184,78 @@ def spmd_gpu(ctx, data_dir):
     ctx.all_gather_object = orig
     out["steady_object_collectives"] = calls["n"]
     ctx.barrier()
+    return out
+
+
+def sync_count(ctx, data_dir):
+    """Host synchronizations of warm sharded queries over RCCL (world 1 on a 1-GPU box): a
+    plan-cache hit of the indexed filter and join aggregates must submit without one (no
+    ``.item()`` / blocking copy / stream or event wait: counted by torch's sync debug mode and
+    by wrapping the explicit waits), and reading the result costs one."""
+    import datetime  # noqa: F401
+    import warnings
+    import torch
+    from hyperspace_amd import Hyperspace, IndexConfig, col, count, sum_
+    assert ctx.backend == "nccl", ctx.backend
+    s = _session(ctx, data_dir, **{"spark.hyperspace.mi.execution.device": "gpu",
+                                   "spark.hyperspace.system.path":
+                                       os.path.join(data_dir, "indexes_sync")})
+    hs = Hyperspace(s)
+    t1 = s.read.parquet(os.path.join(data_dir, "t1"))
+    t2 = s.read.parquet(os.path.join(data_dir, "t2"))
+    hs.createIndex(t1, IndexConfig("i1", ["k"], ["v"]))
+    hs.createIndex(t2, IndexConfig("i2", ["k"], ["w", "s"]))
+    Hyperspace.enable(s)
+    be = s.backend()
+
+    def filt(i):
+        return t1.filter((col("v") >= 10 + i) & (col("v") < 300 - i)) \
+            .agg(sum_(col("v")).alias("sv"), count("*").alias("n"))
+
+    def join(i):
+        return t1.join(t2, t1["k"] == t2["k"]).filter(col("w") < 3 + i % 2) \
+            .groupBy(t2["w"]).agg(sum_(col("v")).alias("sv"))
+
+    counts = {"wait": 0}
+    waits = []
+    for obj, name in ((torch.cuda, "synchronize"), (torch.cuda.Stream, "synchronize"),
+                      (torch.cuda.Event, "synchronize")):
+        orig = getattr(obj, name)
+
+        def wrapped(*a, _orig=orig, **k):
+            counts["wait"] += 1
+            return _orig(*a, **k)
+        waits.append((obj, name, orig))
+        setattr(obj, name, wrapped)
+    out = {}
+    try:
+        for qname, q in (("filter", filt), ("join", join)):
+            for i in range(3):                      # warm: lowering, kernels, program
+                q(i % 2).collect()
+            torch.cuda.synchronize()
+            per = []
+            for i in range(4):
+                df = q(i % 2)
+                counts["wait"] = 0
+                with warnings.catch_warnings(record=True) as w:
+                    warnings.simplefilter("always")
+                    torch.cuda.set_sync_debug_mode("warn")
+                    fut = be.collect_async(df.queryExecution.executed_plan)
+                    torch.cuda.set_sync_debug_mode("default")
+                submit = counts["wait"] + sum("synchroniz" in str(x.message) for x in w)
+                counts["wait"] = 0
+                with warnings.catch_warnings(record=True) as w:
+                    warnings.simplefilter("always")
+                    torch.cuda.set_sync_debug_mode("warn")
+                    res = fut.result()
+                    torch.cuda.set_sync_debug_mode("default")
+                read = counts["wait"] + sum("synchroniz" in str(x.message) for x in w)
+                per.append((submit, read, be.last_path, res.num_rows))
+            out[qname] = per
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+        for obj, name, orig in waits:
+            setattr(obj, name, orig)
     return out
 
 
@@ -304,5 +382,7 @@ def spmd_skew(ctx, data_dir):
     return out
 
 
-SCENARIOS = {"spmd_stream_build": spmd_stream_build, "nccl_paths": nccl_paths, "collectives": collectives, "spmd_index": spmd_index, "spmd_gpu": spmd_gpu,
-             "balanced_exchange": balanced_exchange, "spmd_skew": spmd_skew}
+SCENARIOS = {"spmd_stream_build": spmd_stream_build, "nccl_paths": nccl_paths,
+             "collectives": collectives, "spmd_index": spmd_index, "spmd_gpu": spmd_gpu,
+             "balanced_exchange": balanced_exchange, "spmd_skew": spmd_skew,
+             "sync_count": sync_count}

@@ -85,7 +85,9 @@ def spmd_data(tmp_path):
     k2 = np.repeat(np.arange(100, dtype=np.int64), 2)
     t2 = pa.table({"k": k2, "w": (k2 % 5).astype(np.int32),
                    "s": pa.array([f"s{x % 7}" for x in k2])})
-    for name, t, parts in (("t1", t1, 3), ("t2", t2, 2)):
+    # unique, sparse keys over a wide domain: the sharded semi-join exchanges keys, not bitmaps
+    t3 = pa.table({"k": np.concatenate([np.arange(0, 200, 3), [10_000_000]]).astype(np.int64)})
+    for name, t, parts in (("t1", t1, 3), ("t2", t2, 2), ("t3", t3, 2)):
         os.makedirs(data / name)
         step = (t.num_rows + parts - 1) // parts
         for i in range(parts):
@@ -169,8 +171,12 @@ def test_spmd_device_executor(tmp_path, spmd_data, device):
     gf = jf.group_by(["k", "v"]).aggregate([("w", "sum")])
     exp_fd = sorted(zip(gf.column("k").to_pylist(), gf.column("v").to_pylist(),
                         gf.column("w_sum").to_pylist()), key=lambda x: (-x[2], x[0]))[:5]
+    k3 = set(range(0, 200, 3))
+    exp_semi = [(sum(2 * k for k in k3), len(k3))]
     for d in res:
-        assert d["paths"] == ["native"] * 9, d["paths"]
+        assert d["paths"] == ["native"] * 10, d["paths"]
+        assert [tuple(x) for x in d["semi_keys"]] == exp_semi
+        assert d["semi_exchange"] == "keys"
         assert [tuple(x) for x in d["fd_topk"]] == exp_fd
         assert [tuple(x) for x in d["nonindex_join"]] == exp_s
         assert [tuple(x) for x in d["join_w"]] == exp_w
@@ -230,6 +236,21 @@ def test_rccl_branches_single_rank(tmp_path, device):
     world-size-1 RCCL process group: runs on any 1-GPU MI355X box."""
     res = _spawn("nccl_paths", tmp_path, str(tmp_path), world=1, backend="nccl", timeout=300)
     _check_nccl_paths(res, 1)
+
+
+@pytest.mark.gpu
+def test_warm_sharded_queries_submit_without_host_syncs(tmp_path, spmd_data, device):
+    """A warm sharded query (plan-cache hit of the indexed filter / join aggregate over an
+    RCCL process group) submits with no host synchronization; reading its result is the one
+    wait (torch's sync debug mode plus wrapped stream / event / device waits count them)."""
+    data, t1, t2 = spmd_data
+    res = _spawn("sync_count", tmp_path, str(data), world=1, backend="nccl", timeout=300)
+    d = res[0]
+    for q in ("filter", "join"):
+        for submit, read, path, rows in d[q]:
+            assert path == "native" and rows > 0
+            assert submit == 0, d
+            assert read <= 1, d
 
 
 def _gpu_count() -> int:
