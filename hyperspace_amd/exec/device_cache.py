@@ -224,9 +224,12 @@ def clear_seeds() -> None:
 
 
 def load_bucketed_index(files, columns: List[str], num_buckets: int, sort_cols: List[str], device,
-                        rank: int = 0, world: int = 1, owned_buckets=None) -> DeviceTable:
+                        rank: int = 0, world: int = 1, owned_buckets=None,
+                        cuts=None) -> DeviceTable:
     """Load index files bucket-major for the buckets this rank owns (``owned_buckets``, default
-    b % world == rank); every other bucket is an empty range of the offset table."""
+    b % world == rank); every other bucket is an empty range of the offset table.  ``cuts``:
+    {bucket: (lo, hi)} - of those buckets this rank keeps only the rows whose leading sort key
+    lies in ``[lo, hi)`` (None: open; a heavy bucket cut across ranks, parallel/placement.py)."""
     import torch
     from ..ops import kernels as K
     by_bucket: Dict[int, list] = {}
@@ -286,7 +289,42 @@ def load_bucketed_index(files, columns: List[str], num_buckets: int, sort_cols: 
         names = list(table.columns)
         gathered = K.gather_columns([table.columns[c] for c in names], perm)
         table = DeviceTable(dict(zip(names, gathered)), n, table.bucket_offsets, off)
+    if cuts and n:
+        table = _cut_buckets(table, sort_cols[0], cuts, device)
     return table
+
+
+def _cut_buckets(table: DeviceTable, key: str, cuts, device) -> DeviceTable:
+    """The table without the rows of cut buckets outside this rank's key range (each bucket's
+    rows are sorted by ``key``, so a range is one slice, found by binary search)."""
+    import torch
+    from ..ops import kernels as K
+    off = np.asarray(table.bucket_offsets_host, dtype=np.int64)
+    kc = table.columns[key]
+    if kc.valid is not None or kc.is_float or kc.dictionary is not None:
+        raise ValueError(f"heavy-bucket cut on a non-integer or nullable key {key}")
+    keep_lo, keep_hi = off[:-1].copy(), off[1:].copy()
+    for b, (lo, hi) in cuts.items():
+        a0, a1 = int(off[b]), int(off[b + 1])
+        if a1 <= a0:
+            continue
+        seg = kc.data[a0:a1].long()
+        s = a0 + (int(torch.searchsorted(seg, torch.tensor([lo], device=seg.device))[0])
+                  if lo is not None else 0)
+        e = a0 + (int(torch.searchsorted(seg, torch.tensor([hi], device=seg.device))[0])
+                  if hi is not None else a1 - a0)
+        keep_lo[b], keep_hi[b] = s, max(s, e)
+    counts = keep_hi - keep_lo
+    idx = torch.cat([torch.arange(int(a), int(c), dtype=torch.int64, device=device)
+                     for a, c in zip(keep_lo, keep_hi) if c > a] or
+                    [torch.empty(0, dtype=torch.int64, device=device)])
+    names = list(table.columns)
+    cols = K.gather_columns([table.columns[c] for c in names], idx) if idx.numel() else \
+        [DeviceColumn(table.columns[c].data[:0], None, table.columns[c].atype,
+                      table.columns[c].dictionary) for c in names]
+    noff = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    return DeviceTable(dict(zip(names, cols)), int(noff[-1]), torch.from_numpy(noff).to(device),
+                       noff)
 
 
 def load_flat(files, fmt: str, columns: List[str], data_schema, options, partition_spec,

@@ -625,17 +625,19 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
             cols = [ncol[a.name.lower()] for a in p.output]
             sort_cols = [ncol[c.lower()] for c in idx.indexed_columns]
             load_cols = list(dict.fromkeys(cols + sort_cols))
-            owners = self._owner_map(idx.num_buckets, world, files)
+            owners = self._owner_map(idx.num_buckets, world, files, sort_cols[0])
             owned = owners.owned(rank)
+            cuts = owners.ranges(rank)      # key ranges of heavy buckets cut across ranks
             chunk = getattr(self, "_bucket_chunk", None)
             if chunk is not None:
                 # bucket-range streaming (_streamed_agg): this pass holds buckets [lo, hi) only
                 owned = [b for b in owned if chunk[0] <= b < chunk[1]]
             table = self.cache.get(
                 files, load_cols, ("bucketed", rank, world, owners.key, chunk),
-                lambda: seeded_index(files, load_cols, idx.num_buckets, rank, world, owned) or
+                lambda: (None if cuts else
+                         seeded_index(files, load_cols, idx.num_buckets, rank, world, owned)) or
                 load_bucketed_index(files, load_cols, idx.num_buckets, sort_cols, self.device,
-                                    rank, world, owned))
+                                    rank, world, owned, cuts))
             # rank-independent identity (every rank scans the same file list)
             table.global_key = ("bucketed", _files_key(files), tuple(load_cols), world)
             colmap = {a.expr_id: c for a, c in zip(p.output, cols)}
@@ -661,15 +663,17 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
         return DRel(table, {a.expr_id: a.name for a in p.output}, list(p.output),
                     split=world > 1)
 
-    def _owner_map(self, num_buckets: int, world: int, files=None):
+    def _owner_map(self, num_buckets: int, world: int, files=None, key: str = None):
         """The session's bucket -> rank map for this bucket count (parallel/placement.py):
-        size-balanced from the first index queried with it, shared by every later index and
-        query-time shuffle with that bucket count (co-partitioned)."""
-        from ..parallel.placement import bucket_weights, session_map
+        size-balanced from the first index queried with it (heavy buckets cut into key ranges
+        of its leading indexed column ``key``), shared by every later index and query-time
+        shuffle with that bucket count (co-partitioned)."""
+        from ..parallel.placement import bucket_bounds, bucket_weights, session_map
         if world <= 1:
             return session_map(self.session, num_buckets, 1)
         w = bucket_weights(files, num_buckets) if files is not None else None
-        return session_map(self.session, num_buckets, world, w)
+        bounds = bucket_bounds(files, num_buckets, key) if files is not None and key else None
+        return session_map(self.session, num_buckets, world, w, bounds)
 
     @staticmethod
     def _all_bucket_files(location, files, nb) -> bool:

@@ -154,8 +154,9 @@ class JoinOps:
             bucket, counts = K.murmur3_bucket(kcols, B)
         if d is not None and d.world > 1:
             with stage("shuffle.all_to_all"):
-                cols, bucket = self._exchange_rows(d, cols, bucket,
-                                                   self._owner_map(B, d.world).dest(bucket))
+                om = self._owner_map(B, d.world)
+                cols, bucket = self._exchange_rows(
+                    d, cols, bucket, om.dest(bucket, kcols[0].data if om.splits else None))
             kcols = [cols[k.expr_id] for k in keys]
             counts = K.histogram(bucket, B)
         n = int(bucket.numel())

@@ -288,9 +288,6 @@ class DistContext:
         self.all_reduce(t, "sum")
         return float(t.item())
 
-    def owns(self, bucket: int) -> bool:
-        return bucket % self.world == self.rank
-
 
 def attach(session, ctx: Optional[DistContext]) -> None:
     session.dist = ctx

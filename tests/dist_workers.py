@@ -382,7 +382,58 @@ def spmd_skew(ctx, data_dir):
     return out
 
 
+def spmd_split(ctx, data_dir):
+    """A heavy bucket of many distinct keys (ranks share cuda:0 over gloo): the balanced map
+    cuts it into key ranges on several ranks (parallel/placement.py split_heavy) and the
+    co-located join / filter aggregates still match the
+    modulo placement; every rank's rows of that bucket lie in its key range."""
+    from hyperspace_amd import Hyperspace, IndexConfig, col, count, sum_
+    s = _session(ctx, data_dir, **{"spark.hyperspace.mi.execution.device": "gpu",
+                                   "spark.hyperspace.index.numBuckets": "16",
+                                   "spark.hyperspace.system.path":
+                                       os.path.join(data_dir, "indexes_split")})
+    hs = Hyperspace(s)
+    t3 = s.read.parquet(os.path.join(data_dir, "s3"))
+    t2 = s.read.parquet(os.path.join(data_dir, "s2"))
+    hs.createIndex(t3, IndexConfig("k3", ["k"], ["v"]))
+    hs.createIndex(t2, IndexConfig("k2s", ["k"], ["w"]))
+    Hyperspace.enable(s)
+    out = {"paths": []}
+    for mode in ("modulo", "balanced"):
+        s.conf.set("spark.hyperspace.mi.bucketPlacement", mode)
+        j = t3.join(t2, t3["k"] == t2["k"])
+        qs = {"agg": j.groupBy(t2["w"]).agg(sum_(col("v")).alias("sv"), count("*").alias("n")),
+              "filter": t3.filter(col("v") % 3 == 0).agg(sum_(col("v")).alias("sv"),
+                                                          count("*").alias("n"))}
+        res = {}
+        for name, df in qs.items():
+            res[name] = sorted((tuple(r.values()) for r in df.to_arrow().to_pylist()), key=repr)
+            out["paths"].append(s.backend().last_path)
+        out[mode] = res
+        m = s.__dict__.get("_hs_owner_maps", {}).get((16, ctx.world, mode))
+        out[mode + "_splits"] = {str(b): [r.tolist(), k.tolist()]
+                                 for b, (r, k) in (m.splits.items() if m is not None else [])}
+    # the resident index table of this rank: rows of each cut bucket within its key range
+    be = s.backend()
+    m = s.__dict__["_hs_owner_maps"][(16, ctx.world, "balanced")]
+    cuts = m.ranges(ctx.rank)
+    ok = True
+    for key, t in list(be.cache._lru.items()):
+        if "k" not in t.columns or t.num_buckets != 16 or key[2][0] != "bucketed" or \
+                key[2][3] != m.key:
+            continue
+        off = t.bucket_offsets_host
+        kk = t.columns["k"].data.cpu().numpy()
+        for b, (lo, hi) in cuts.items():
+            seg = kk[off[b]:off[b + 1]]
+            ok = ok and (lo is None or (seg >= lo).all()) and (hi is None or (seg < hi).all())
+    out["cut_rows_in_range"] = bool(ok)
+    out["cuts"] = {str(b): [lo, hi] for b, (lo, hi) in cuts.items()}
+    ctx.barrier()
+    return out
+
+
 SCENARIOS = {"spmd_stream_build": spmd_stream_build, "nccl_paths": nccl_paths,
              "collectives": collectives, "spmd_index": spmd_index, "spmd_gpu": spmd_gpu,
              "balanced_exchange": balanced_exchange, "spmd_skew": spmd_skew,
-             "sync_count": sync_count}
+             "sync_count": sync_count, "spmd_split": spmd_split}

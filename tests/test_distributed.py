@@ -352,12 +352,45 @@ def skew_data(tmp_path):
     t1 = pa.table({"k": k1, "v": np.arange(len(k1), dtype=np.int64)})
     k2 = np.arange(400, dtype=np.int64)
     t2 = pa.table({"k": k2, "w": (k2 % 6).astype(np.int32)})
-    for name, t, parts in (("s1", t1, 4), ("s2", t2, 2)):
+    # s3: 70% of the rows in one bucket of 16 (many distinct keys < 400), the rest spread
+    from hyperspace_amd.utils import murmur3
+    cand = np.arange(400, dtype=np.int64)
+    bid = np.asarray(murmur3.bucket_ids([pa.array(cand)], 16))
+    hot = cand[bid == 5]
+    k3 = np.concatenate([np.repeat(hot, 7000 // len(hot) + 1)[:7000],
+                         rng.integers(0, 400, 3000)])
+    t3 = pa.table({"k": k3, "v": np.arange(len(k3), dtype=np.int64)})
+    for name, t, parts in (("s1", t1, 4), ("s2", t2, 2), ("s3", t3, 4)):
         os.makedirs(data / name)
         step = (t.num_rows + parts - 1) // parts
         for i in range(parts):
             pq.write_table(t.slice(i * step, step), data / name / f"part-{i}.parquet")
     return data, t1, t2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_heavy_bucket_cut_into_key_ranges(tmp_path, skew_data, device, world):
+    """A bucket holding 70% of the rows over many keys is cut into key ranges on distinct ranks
+    (parallel/placement.py split_heavy); the co-located join aggregate and a filter aggregate
+    return the modulo placement's (and the oracle's) result, and every rank's resident rows of
+    the cut bucket lie in its range."""
+    data, _, t2 = skew_data
+    t3 = pq.read_table(data / "s3")
+    res = _spawn("spmd_split", tmp_path, str(data), timeout=600.0, world=world)
+    j = t3.join(t2, "k", join_type="inner")
+    g = j.group_by("w").aggregate([("v", "sum"), ("v", "count")])
+    exp = sorted(zip(g.column("w").to_pylist(), g.column("v_sum").to_pylist(),
+                     g.column("v_count").to_pylist()))
+    for d in res:
+        assert d["paths"] == ["native"] * 4, d["paths"]
+        assert d["modulo"] == d["balanced"]
+        assert [tuple(x) for x in d["balanced"]["agg"]] == exp
+        assert d["modulo_splits"] == {}
+        sp = d["balanced_splits"]
+        assert "5" in sp and len(sp["5"][0]) == len(set(sp["5"][0])) >= 2, sp
+        assert d["cut_rows_in_range"]
+    assert sum(1 for d in res if "5" in d["cuts"]) == len(res[0]["balanced_splits"]["5"][0])
 
 
 @pytest.mark.gpu
