@@ -347,7 +347,7 @@ class AggOps:
                 str(self.session.conf.get("spark.hyperspace.mi.unionAgg.enabled", "true")).lower() \
                 == "true":
             res = self._union_agg(node, fns)
-        elif group is None and (res := self._mixed_index_agg(child, fns)) is not None:
+        elif group is None and (res := self._mixed_index_agg(child, fns, final)) is not None:
             pass
         else:
             r = self._rel(child)
@@ -577,7 +577,7 @@ class AggOps:
             raise Unsupported("too many aggregates")
         return specs
 
-    def _mixed_index_agg(self, child: X.SparkPlan, fns):
+    def _mixed_index_agg(self, child: X.SparkPlan, fns, final=None):
         """An ungrouped aggregate over Filter / Project of an index scan whose file list also
         holds appended source files (FilterIndexRule's Hybrid Scan appends them to the index
         relation, ``RuleUtils`` same-scan appended files): the index bucket files load as the
@@ -626,13 +626,39 @@ class AggOps:
             if len(memo) > 64:
                 memo.clear()
             memo[id(node)] = (node, [x.copy() for x in scans], (nbf, naf))
+        # each part's literal-independent lowering is kept per aggregate node (``_ScanPrep``):
+        # a plan-cache hit rebinds only the literals of both scans
+        preps = self.__dict__.setdefault("_mixed_preps", {})
+        pp = preps.get(id(final)) if final is not None else None
+        if pp is not None and (pp[0] is not final or pp[2] != self._placement_tag() or
+                               not all(self._holds(x.r.table) for x in pp[1])):
+            pp = None
         res = []
-        for r, bk in zip(scans, (True, False)):
+        pruned = None
+        if pp is not None:
+            try:
+                for x, bk in zip(pp[1], (True, False)):
+                    res.append(self._scan_agg(x.r, fns, None, prep=x, graph_ok=False))
+                    if bk:
+                        pruned = self.metrics.get("scan_key_ranges")
+            except _Stale:
+                preps.pop(id(final), None)
+                res = []
+        made = []
+        for r, bk in zip(scans, (True, False)) if not res else ():
             for n in reversed(chain):
                 r = self._unary(n, r)
+            self._scan_gs = None
             res.append(self._scan_agg(r, fns, None, graph_ok=False))
+            st = self._scan_gs
+            if st is not None and final is not None and not r.extra:
+                made.append(_ScanPrep(final, r, *st, None, self._placement_tag()))
             if bk:
                 pruned = self.metrics.get("scan_key_ranges")
+        if len(made) == 2:
+            if len(preps) > 64:
+                preps.clear()
+            preps[id(final)] = (final, made, self._placement_tag())
         self.metrics["scan_key_ranges"] = pruned     # the bucket files' scan, not the flat one
         sums, cnts, mins, maxs = (t.clone() for t in res[0][:4])
         x = res[1]
