@@ -28,6 +28,7 @@ from typing import List, Optional
 
 from ..ops import _lib as NL
 from . import jit as J
+from . import jit_hash as JH
 
 SPLIT = 8
 # tunables: fields of exec.kernel_config.KernelConfig (bound by kernel_config.bind)
@@ -490,11 +491,11 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
     With ``hk`` (an exec.hash_agg.KeyPlan over left columns) the walk groups by the hash key
     instead: each pass's 64 list entries are consecutive passing rows, so a segmented shuffle
     reduce folds a group's rows (one run = one left join key) before one table probe
-    (``jit._hash_accumulate``); kernel ``hs_jit_run_bits_hash``, no partials.
+    (``jit_hash._hash_accumulate``); kernel ``hs_jit_run_bits_hash``, no partials.
 
     With ``tk`` as well (an exec.hash_agg.TopKPlan: ORDER BY <aggregate> LIMIT k over those
     groups), the windows are walked in row order with the last segment of each carried into
-    the next (``jit._topk_accumulate``): a key is final when the walk leaves it and competes
+    the next (``jit_hash._topk_accumulate``): a key is final when the walk leaves it and competes
     for the wavefront's top-K registers instead of probing the table; only keys that may
     continue into the neighbouring wavefronts' tiles (at most two per wavefront) go to the
     table (kernel ``hs_jit_run_bits_topk``; every wavefront writes its list at the end)."""
@@ -517,7 +518,7 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
     pslots = J._pred_slots(lpreds)
     assert not (grouped and hk is not None)
     # top-K mode segments the walk by key run (lrn_) and loads the key columns only where a
-    # group is emitted (jit._hash_accumulate ``seg``): they are not part of the per-row tail
+    # group is emitted (jit_hash._hash_accumulate ``seg``): they are not part of the per-row tail
     tail = list(dict.fromkeys(J._agg_slots(aggs) + ([p.group_col] if grouped else []) +
                               (list(hk.slots) if hk is not None and tk is None else [])))
     approx = J._sum_only_slots(lpreds, aggs, p.group_col if grouped else -1, cols) - \
@@ -530,7 +531,7 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
     b += J._acc_decls(aggs, grouped, args)
     assert tk is None or hk is not None
     if tk is not None:
-        b += J._topk_decls(aggs, tk)
+        b += JH._topk_decls(aggs, tk)
     CAP = 1024  # noqa: N806 — list entries per wavefront and round (a denser tile takes rounds)
     EW = 4  # noqa: N806 — list entries per lane per walk pass, loads all in flight together
 
@@ -696,7 +697,7 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
             b.append(f"{ind2}const int {gvar} = cok ? (int)glc : 0;")
         if hk is not None:
             b += [J._rename(x, tail, it)
-                  for x in J._hash_accumulate(g, aggs, hk, "cok", ind2, tk=tk,
+                  for x in JH._hash_accumulate(g, aggs, hk, "cok", ind2, tk=tk,
                                               seg=f"crn{k}" if tk is not None else None,
                                               row=f"crow{k}", run=f"qb_ + (i64)crn{k}",
                                               carry_gen=carry_gen)]
@@ -708,17 +709,17 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
     if hk is None:
         b += J._flush(aggs, grouped)
     if tk is not None:
-        b += J._topk_carry_final(aggs, hk, tk, "  ", carry_gen)
+        b += JH._topk_carry_final(aggs, hk, tk, "  ", carry_gen)
 
         def key_lines(j: int, ind_: str) -> List[str]:
             gk = J._Gen(args, cols, SPLIT, (f"tkr{j}", f"tkr{j}"), frozenset(), True)
             out: List[str] = []
             for c in hk.cols:
                 J._uload(gk, c.slot, "F", out, ind_)
-            out += J._hash_key_lines(gk, hk, "tkey_l", "_F", ind_)
+            out += JH._hash_key_lines(gk, hk, "tkey_l", "_F", ind_)
             out.append(f"{ind_}const u64 tkey_ = tkey_l;")
             return out
-        b += J._topk_flush(aggs, tk, args, "wid", key_lines)
+        b += JH._topk_flush(aggs, tk, args, "wid", key_lines)
     name = "hs_jit_run_bits_scan" if hk is None else \
         ("hs_jit_run_bits_hash" if tk is None else "hs_jit_run_bits_topk")
     src = (J._PRELUDE + args.struct_src() +
