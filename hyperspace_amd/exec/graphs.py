@@ -150,8 +150,8 @@ class _RingGraph:
         prev = slot.current
         if prev is not None and prev.value is None:
             prev.value = self._read(slot)
-        elif slot.launched:
-            slot.event.synchronize()
+        elif slot.launched and not slot.event.query():
+            slot.event.synchronize()    # back-pressure: the slot's replay is still running
         fill(slot.h_params.view())
         cur = torch.cuda.current_stream()
         st = cur.cuda_stream

@@ -160,10 +160,12 @@ def lpt(weights: Sequence[float], world: int) -> np.ndarray:
 
 def split_heavy(weights: Sequence[float], world: int,
                 bounds_of: Callable[[int, int], Optional[Sequence[int]]],
-                slack: float = 1.05) -> OwnerMap:
+                slack: float = 1.05, max_piece: float = 0.75) -> OwnerMap:
     """LPT over whole buckets and the key-range pieces of heavy ones: a bucket heavier than
-    ``slack`` x total/W asks ``bounds_of(b, m)`` for ``m - 1`` increasing split keys (None: it
-    cannot be cut) and its ``m`` pieces go to distinct ranks."""
+    ``slack`` x total/W asks ``bounds_of(b, m)`` for ``m - 1`` increasing split keys - or
+    (keys, each piece's fraction of the rows) - and its pieces go to distinct ranks, weighted
+    by their fractions.  None, or a piece keeping more than ``max_piece`` of the rows (a hot
+    key), leaves the bucket whole."""
     w = np.asarray(weights, dtype=np.float64)
     world = max(int(world), 1)
     cap = float(w.sum()) / world
@@ -171,15 +173,19 @@ def split_heavy(weights: Sequence[float], world: int,
     cuts: Dict[int, np.ndarray] = {}
     for b in range(len(w)):
         m = min(world, int(math.ceil(w[b] / cap))) if cap > 0 and w[b] > slack * cap else 1
-        bounds = bounds_of(b, m) if m > 1 else None
+        got = bounds_of(b, m) if m > 1 else None
+        bounds, frac = got if isinstance(got, tuple) else (got, None)
         if bounds is not None and len(bounds):
-            bounds = np.unique(np.asarray(bounds, dtype=np.int64))
+            bounds = np.asarray(bounds, dtype=np.int64)
             m = len(bounds) + 1
+            frac = np.full(m, 1.0 / m) if frac is None else np.asarray(frac, dtype=np.float64)
+            if frac.max() > max_piece:
+                m = 1          # one key range keeps most rows (a hot key): not worth a cut
         else:
             m = 1
         if m > 1:
             cuts[b] = bounds
-            items += [(w[b] / m, b, i, m) for i in range(m)]
+            items += [(w[b] * frac[i], b, i, m) for i in range(m)]
         else:
             items.append((w[b], b, 0, 1))
     owners = np.zeros(len(w), dtype=np.int32)
@@ -234,6 +240,7 @@ def bucket_bounds(files, num_buckets: int, key: str) -> Callable[[int, int], Opt
         if not paths:
             return None
         starts = from_stats(paths)
+        vals = None
         if starts is not None:
             starts.sort()
             total = sum(n for _, n in starts)
@@ -254,7 +261,17 @@ def bucket_bounds(files, num_buckets: int, key: str) -> Callable[[int, int], Opt
         for k in cands:
             if k > lo and (not out or k > out[-1]):
                 out.append(int(k))
-        return out or None
+        if not out:
+            return None
+        # each piece's share of the rows: exact from the key column, else from the row groups
+        if vals is not None:
+            cnt = np.diff(np.concatenate([[0], np.searchsorted(vals, out), [len(vals)]]))
+        else:
+            ks = np.array([k for k, _ in starts], dtype=np.int64)
+            rows = np.array([n for _, n in starts], dtype=np.float64)
+            piece = np.searchsorted(np.asarray(out, dtype=np.int64), ks, side="right")
+            cnt = np.bincount(piece, weights=rows, minlength=len(out) + 1)
+        return out, (cnt / max(float(cnt.sum()), 1.0)).tolist()
     return bounds_of
 
 

@@ -187,6 +187,12 @@ def spmd_gpu(ctx, data_dir):
     return out
 
 
+def _is_sync_warning(w) -> bool:
+    """A torch sync-debug-mode report of a synchronizing operation (not the mode's own notice
+    that it is a prototype)."""
+    return "called a synchronizing" in str(w.message)
+
+
 def sync_count(ctx, data_dir):
     """Host synchronizations of warm sharded queries over RCCL (world 1 on a 1-GPU box): a
     plan-cache hit of the indexed filter and join aggregates must submit without one (no
@@ -222,8 +228,12 @@ def sync_count(ctx, data_dir):
                       (torch.cuda.Event, "synchronize")):
         orig = getattr(obj, name)
 
-        def wrapped(*a, _orig=orig, **k):
+        def wrapped(*a, _orig=orig, _name=f"{getattr(obj, '__name__', obj)}.{name}", **k):
             counts["wait"] += 1
+            import traceback
+            counts.setdefault("where", []).append(
+                [_name] + [f"{f.filename.rsplit('/', 1)[-1]}:{f.lineno}:{f.name}"
+                           for f in traceback.extract_stack()[-6:-1]])
             return _orig(*a, **k)
         waits.append((obj, name, orig))
         setattr(obj, name, wrapped)
@@ -237,20 +247,26 @@ def sync_count(ctx, data_dir):
             for i in range(4):
                 df = q(i % 2)
                 counts["wait"] = 0
+                counts["where"] = []
                 with warnings.catch_warnings(record=True) as w:
                     warnings.simplefilter("always")
                     torch.cuda.set_sync_debug_mode("warn")
-                    fut = be.collect_async(df.queryExecution.executed_plan)
+                    fut = df.queryExecution.to_arrow_async()   # the bench's submission
                     torch.cuda.set_sync_debug_mode("default")
-                submit = counts["wait"] + sum("synchroniz" in str(x.message) for x in w)
+                submit = counts["wait"] + sum(_is_sync_warning(x) for x in w)
+                if submit:
+                    out.setdefault("submit_syncs", []).append(
+                        [str(x.message)[:200] + " @ " + f"{x.filename}:{x.lineno}" for x in w
+                         if _is_sync_warning(x)] + counts.get("where", []))
+                counts["where"] = []
                 counts["wait"] = 0
                 with warnings.catch_warnings(record=True) as w:
                     warnings.simplefilter("always")
                     torch.cuda.set_sync_debug_mode("warn")
                     res = fut.result()
                     torch.cuda.set_sync_debug_mode("default")
-                read = counts["wait"] + sum("synchroniz" in str(x.message) for x in w)
-                per.append((submit, read, be.last_path, res.num_rows))
+                read = counts["wait"] + sum(_is_sync_warning(x) for x in w)
+                per.append((submit, read, fut.path, res.num_rows))
             out[qname] = per
     finally:
         torch.cuda.set_sync_debug_mode("default")

@@ -75,10 +75,11 @@ def _bucket_files(tmp_path, b, keys, stats: bool, rg: int):
 def test_bucket_bounds_at_row_quantiles(tmp_path, stats):
     keys = np.repeat(np.arange(1000, dtype=np.int64), 4)           # 4000 rows, 1000 keys
     files = _bucket_files(tmp_path, 3, keys, stats, 100)
-    bounds = PL.bucket_bounds(files, 8, "k")(3, 4)
+    bounds, frac = PL.bucket_bounds(files, 8, "k")(3, 4)
     assert len(bounds) == 3 and bounds == sorted(bounds)
     for got, q in zip(bounds, (250, 500, 750)):
         assert abs(got - q) <= 25
+    assert len(frac) == 4 and abs(sum(frac) - 1) < 1e-9 and max(frac) < 0.3
     assert PL.bucket_bounds(files, 8, "k")(5, 4) is None            # no such bucket
     one = _bucket_files(tmp_path / ".." / tmp_path.name, 6, np.full(500, 9), stats, 100)
     assert PL.bucket_bounds(one, 8, "k")(6, 3) is None              # one key: cannot cut
@@ -94,3 +95,13 @@ def test_session_map_split_switch(tmp_path):
         m = PL.session_map(s, 4, 2, w, PL.bucket_bounds(files, 4, "k"))
         assert bool(m.splits) == expect_split
         assert PL.session_map(s, 4, 2) is m                          # sticky
+
+
+def test_hot_key_bucket_is_not_cut(tmp_path):
+    """90% of the bucket's rows on one key: any cut leaves one piece with most rows, so the
+    bucket stays whole (the plain balanced map gives it a rank of its own)."""
+    keys = np.concatenate([np.full(9000, 500), np.arange(1000)]).astype(np.int64)
+    files = _bucket_files(tmp_path, 0, keys, False, 1000)
+    w = [10000.0, 300.0, 300.0, 300.0]
+    m = PL.split_heavy(w, 2, PL.bucket_bounds(files, 4, "k"))
+    assert not m.splits and (m.owners == PL.lpt(w, 2)).all()
