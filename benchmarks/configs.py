@@ -320,6 +320,7 @@ def config_q3_3way(args):
     from hyperspace_amd.utils.tracing import TRACER, format_report
     TRACER.reset()
     el = _timed_loop(lambda i: q(i).collect(), k, args.device)
+    semi = getattr(s.backend(), "last_semi_join", None)
     if TRACER.profile:   # HS_PROFILE=1: where the 3-way join's time goes
         print("[q3_3way] stage profile\n" + format_report(TRACER.report()), file=sys.stderr,
               flush=True)
@@ -336,7 +337,7 @@ def config_q3_3way(args):
             "no_index_query_s": round(noidx_s, 3), "index_build_s": builds,
             "indexes_in_plan": [n for n in ("cust", "ord_cust", "li_orderkey") if n in plan],
             "path": path, "fallback_reason": reason, "match": _close(got, ref),
-            "semi_join": getattr(s.backend(), "last_semi_join", None)}
+            "semi_join": semi}
 
 
 # ------------------------------------------------------------------------------------ TPC-DS

@@ -721,6 +721,7 @@ class JoinOps:
         max_tiles = K.join_max_tiles(left.table.num_rows, rlen.numel())
         conf = self.session.conf
         if HyperspaceConf.codegen_enabled(conf) and HyperspaceConf.join_index_enabled(conf) and \
+                not getattr(self, "_merge_join_only", False) and \
                 getattr(left.table, "global_key", None) is not None and \
                 getattr(right.table, "global_key", None) is not None and \
                 join_index.eligible(left.table, right.table, left.col(lk), right.col(rk)):

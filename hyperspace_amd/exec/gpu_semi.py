@@ -12,7 +12,7 @@ from ..ops import _lib as NL, kernels as K
 from ..plan import expressions as E, physical as X
 from ..utils.conf import HyperspaceConf
 from ..utils.tracing import stage
-from . import compile as CP, jit_runs
+from . import compile as CP, jit, jit_runs
 from .arrow_eval import key
 from .device_table import DeviceColumn
 from .gpu_common import (_group_limit, _NoCondition, _plan_bytes, _semi_fail_key, _strip_exchange,
@@ -163,7 +163,9 @@ class SemiJoinOps:
             if crel.parts:
                 return None
             keys = self._materialize(crel, [cjk])[cjk.expr_id]
-            bm = self._semi_bitmap(keys)
+            src = crel.col(cjk) if crel.bucketed and crel.sort_attrs and \
+                crel.sort_attrs[0].expr_id == cjk.expr_id and not crel.is_computed(cjk) else None
+            bm = self._semi_bitmap(keys, src)
         if bm is None:
             return None
         words, lo, nbits = bm
@@ -178,8 +180,14 @@ class SemiJoinOps:
         agreed, G, gbase, gdict, gtype = gs
         self._groups_agreed = agreed is True
         self._join_rec = None
-        with stage("semi.probe"):
-            out = self._join_agg_pair(_NoCondition, prel, orel, pk, bk, fns, group, G, gbase)
+        # the two-phase run-keyed merge join tests the orders predicates once per lineitem key
+        # run; a join index would gather o_custkey per lineitem row (at random)
+        self._merge_join_only = True
+        try:
+            with stage("semi.probe"):
+                out = self._join_agg_pair(_NoCondition, prel, orel, pk, bk, fns, group, G, gbase)
+        finally:
+            self._merge_join_only = False
         self._join_rec = None
         return (*out, G, gbase, gdict, gtype)
 
@@ -345,11 +353,22 @@ class SemiJoinOps:
             r = self._unary(f, r)
         return self._unary(p, r)
 
-    def _semi_bitmap(self, keys: DeviceColumn):
+    def _semi_bitmap(self, keys: DeviceColumn, src: Optional[DeviceColumn] = None):
         """(words, lo, nbits) of the build keys over every rank's keys, or None when they are
-        not unique, not integer, empty everywhere or span more than K.MAX_BITMAP_BITS."""
+        not unique, not integer, empty everywhere or span more than K.MAX_BITMAP_BITS.
+        ``src``: the resident, sorted index key column the keys were selected from - its
+        (cached) domain bounds them and, when it repeats no key, so is every selection of it:
+        the bitmap is built with no host synchronization."""
         import torch
         d = self._dist()
+        if (d is None or d.world == 1) and src is not None and src.valid is None and \
+                not getattr(src, "hs_transient", False) and \
+                src.hs_type in (NL.I8, NL.I16, NL.I32, NL.I64) and not jit.key_has_dups(src):
+            lo, span = self._local_domain(src)
+            if span == 0 or span > K.MAX_BITMAP_BITS:
+                return None
+            words, _ = K.key_bitmap(keys, lo, span, check=False)
+            return words, lo, span
         dom = K.key_domain(keys)
         if d is None or d.world == 1:
             if dom is None:

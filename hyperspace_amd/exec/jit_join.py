@@ -760,7 +760,18 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
         compacts, runs = _with_runs(p, compacts)
     if hk is None and runs is not None:
         from . import jit_runs
-        two = jit_runs.lower(p, rstart, rlen, rbucket, roff, compacts, runs, nrows, cache_spans)
+        # over a resident table's cached full ranges the lowering is fixed (as in hash mode
+        # below): a caller without a prepared launcher (the co-partitioned semi-join) reuses it
+        ck = (id(rstart), id(runs), tuple(p.cols[s].data for s in range(NL.MAX_COLS)),
+              merge_join_shape(p, compacts)) if cache_spans else None
+        two = _RUNS_LOWERED.get(ck) if ck is not None else None
+        if two is None:
+            two = jit_runs.lower(p, rstart, rlen, rbucket, roff, compacts, runs, nrows,
+                                 cache_spans)
+            if two is not None and ck is not None:
+                if len(_RUNS_LOWERED) >= 8:
+                    _RUNS_LOWERED.pop(next(iter(_RUNS_LOWERED)))
+                _RUNS_LOWERED[ck] = two
         if two is not None:
             LAST_MJ_LAUNCHER[0] = two
             return two.launch(p)
@@ -831,6 +842,7 @@ LAST_MJ_PATH: list = [None]
 # cached two-phase hash-mode lowerings (merge_join_agg); each holds its ranges / run form, so
 # the ids in its key stay valid while it is cached
 _RUNS_HASH_LOWERED: Dict[tuple, object] = {}
+_RUNS_LOWERED: Dict[tuple, object] = {}
 
 
 class MergeJoinLauncher:
@@ -994,6 +1006,7 @@ def join_agg_values(p: NL.JoinParams, tile_prefix, spans, parts,
 
 
 __all__ = ['LAST_MJ_LAUNCHER', 'LAST_MJ_PATH', 'MergeJoinLauncher', '_RUNS_HASH_LOWERED',
+           '_RUNS_LOWERED',
            '_SPANS', '_TRUNS', '_block_sync', '_deferred_append', '_deferred_drain',
            '_eager_tail', '_is_runs', '_join_spans', '_key32_frame', '_lanemajor_append',
            '_mj_items', '_run_accumulate', '_run_decls', '_run_flush', '_runs_match',

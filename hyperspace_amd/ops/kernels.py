@@ -485,10 +485,11 @@ def key_domain(col):
     return lo, hi, int(d.numel())
 
 
-def key_bitmap(col, lo: int, nbits: int):
+def key_bitmap(col, lo: int, nbits: int, check: bool = True):
     """(int64 words, duplicate flag) of the non-null integer keys of device column ``col`` as
     bits (key - lo) of an ``nbits``-bit bitmap (csrc/kernels/key_bitmap.hip).  Every key must
-    lie in [lo, lo + nbits)."""
+    lie in [lo, lo + nbits).  ``check=False``: the caller knows the keys are unique and in the
+    domain - no flag read, no host synchronization (the flag is None)."""
     torch = _torch()
     d = col.data
     words = torch.zeros(max((nbits + 63) // 64, 1), dtype=torch.int64, device=d.device)
@@ -496,6 +497,8 @@ def key_bitmap(col, lo: int, nbits: int):
     desc = col.desc()
     NL.check(NL.lib().hs_key_bitmap(C.byref(desc), d.numel(), int(lo), int(nbits), NL.ptr(words),
                                     NL.ptr(flags), NL.stream_ptr()), "hs_key_bitmap")
+    if not check:
+        return words, None
     f = int(flags.item())
     if f & 2:
         raise RuntimeError("hs_key_bitmap: key outside its domain")
