@@ -59,7 +59,22 @@ def _timed_loop(fn, n, device):
     for i in range(n):
         fn(i)
     _sync(device)
-    return time.perf_counter() - t0
+    el = time.perf_counter() - t0
+    if os.environ.get("HS_CFG_CPROFILE"):     # where the host time of the loop goes
+        import cProfile
+        import io
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for i in range(n):
+            fn(i)
+        _sync(device)
+        pr.disable()
+        buf = io.StringIO()
+        pstats.Stats(pr, stream=buf).sort_stats("cumulative").print_stats(45)
+        print(f"[cprofile] {getattr(fn, '__name__', fn)} x{n}\n{buf.getvalue()}",
+              file=sys.stderr, flush=True)
+    return el
 
 
 def _rows(df):

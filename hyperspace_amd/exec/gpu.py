@@ -592,7 +592,8 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
         d = self._dist()
         tag = (d.rank, d.world, self.session.conf.get(
             "spark.hyperspace.mi.bucketPlacement", "balanced")) if d is not None else None
-        tag = (tag, getattr(self, "_bucket_chunk", None))
+        tag = (tag, getattr(self, "_bucket_chunk", None),
+               self.session.conf.get("spark.hyperspace.mi.hybridScanMerge.enabled", "true"))
         memo = self.__dict__.setdefault("_scans", {})
         m = memo.get(id(p))
         if m is not None and m[0] is p and m[2] == tag and m[1].table is not None and \
@@ -619,6 +620,10 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
         if bucketed is None:
             bucketed = rel.is_index() and \
                 self._all_bucket_files(rel.location, files, rel.index.num_buckets)
+            if not bucketed and rel.is_index() and world == 1:
+                hy = self._hybrid_scan(p, files)
+                if hy is not None:
+                    return hy
         if bucketed:
             idx = rel.index
             ncol = {n.lower(): n for n in idx.schema.names}
@@ -662,6 +667,89 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
         table.global_key = gkey
         return DRel(table, {a.expr_id: a.name for a in p.output}, list(p.output),
                     split=world > 1)
+
+    def _hybrid_split(self, p: X.FileSourceScanExec, files):
+        """(bucket files, appended files, load columns, sort columns, output columns) of an
+        index scan whose file list also holds appended source files (FilterIndexRule's Hybrid
+        Scan), or None when they cannot share one device table (string columns: every load has
+        its own dictionary; a column missing from the index)."""
+        if str(self.session.conf.get("spark.hyperspace.mi.hybridScanMerge.enabled", "true")) \
+                .lower() != "true":
+            return None
+        from ..io.writer import get_bucket_id
+        from ..utils import path_utils as P
+        from .device_table import is_string
+        idx = p.relation.index
+        nb = idx.num_buckets
+        bfiles, afiles = [], []
+        for f in files:
+            b = get_bucket_id(P.get_name(f.path))
+            (bfiles if b is not None and b < nb else afiles).append(f)
+        if not bfiles or not afiles:
+            return None
+        ncol = {n.lower(): n for n in idx.schema.names}
+        cols = [ncol.get(a.name.lower()) for a in p.output]
+        if any(c is None for c in cols):
+            return None
+        sort_cols = [ncol[c.lower()] for c in idx.indexed_columns]
+        load_cols = list(dict.fromkeys(cols + sort_cols))
+        types = {f.name: f.type for f in idx.schema}
+        if any(is_string(types[c]) for c in load_cols):
+            return None
+        return bfiles, afiles, load_cols, sort_cols, cols
+
+    def _hybrid_scan(self, p: X.FileSourceScanExec, files) -> Optional[DRel]:
+        """An index scan with same-scan appended files (Hybrid Scan) as ONE resident table: the
+        index buckets as loaded (bucket-sorted), then the appended rows sorted once by the
+        indexed columns as one more bucket range.  Every bucket range is sorted by the key,
+        so a filter's key-range search prunes the appended rows too, and the query takes the
+        single-table paths (prepared lowering, captured graph) like a refreshed index.  The
+        extra range carries no bucket identity (``bucket_attrs`` empty): no equality-bucket
+        pruning and no co-partitioned join read it as a hash partition."""
+        sp = self._hybrid_split(p, files)
+        if sp is None:
+            return None
+        bfiles, afiles, load_cols, sort_cols, cols = sp
+        rel = p.relation
+        idx = rel.index
+        nb = idx.num_buckets
+        dev = self.device
+
+        def load():
+            import torch
+            bt = load_bucketed_index(bfiles, load_cols, nb, sort_cols, dev)
+            at = load_flat(afiles, "parquet", load_cols, rel.data_schema, rel.options,
+                           rel.location.partition_spec, dev)
+            perm = K.sort_permutation([at.columns[c] for c in sort_cols]) if at.num_rows else None
+            ag = K.gather_columns([at.columns[c] for c in load_cols], perm) if perm is not None \
+                else [at.columns[c] for c in load_cols]
+            merged = {}
+            for c, a in zip(load_cols, ag):
+                b = bt.columns[c]
+                if b.data.dtype != a.data.dtype:
+                    raise Unsupported(f"hybrid scan: column {c} differs in type")
+                valid = None
+                if b.valid is not None or a.valid is not None:
+                    ones = lambda x: torch.ones(x.data.shape[0], dtype=torch.uint8,  # noqa: E731
+                                                device=dev)
+                    valid = torch.cat([b.valid if b.valid is not None else ones(b),
+                                       a.valid if a.valid is not None else ones(a)])
+                merged[c] = DeviceColumn(torch.cat([b.data, a.data]), valid, b.atype, None)
+            off = np.concatenate([np.asarray(bt.bucket_offsets_host, dtype=np.int64),
+                                  [bt.num_rows + at.num_rows]]).astype(np.int64)
+            return DeviceTable(merged, int(off[-1]), torch.from_numpy(off).to(dev), off)
+        table = self.cache.get(files, load_cols, ("hybrid-scan", nb), load)
+        table.global_key = ("hybrid-scan", _files_key(files), tuple(load_cols))
+        colmap = {a.expr_id: c for a, c in zip(p.output, cols)}
+        sort_attrs = []
+        for c in sort_cols:
+            a = next((x for x in p.output if x.name.lower() == c.lower()), None)
+            if a is None:
+                a = E.Attribute(c, idx.schema.field(c).type)
+                colmap[a.expr_id] = c
+            sort_attrs.append(a)
+        self.metrics["hybrid_scan_merged"] = (len(bfiles), len(afiles))
+        return DRel(table, colmap, list(p.output), [], True, sort_attrs, [], nb + 1)
 
     def _owner_map(self, num_buckets: int, world: int, files=None, key: str = None):
         """The session's bucket -> rank map for this bucket count (parallel/placement.py):

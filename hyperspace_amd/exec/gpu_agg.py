@@ -597,6 +597,8 @@ class AggOps:
             node = node.child
         if not isinstance(node, X.FileSourceScanExec) or not node.relation.is_index():
             return None
+        if self._hybrid_split(node, node.relation.location.all_files()) is not None:
+            return None     # one merged table instead (GpuBackend._hybrid_scan)
         # the file split and both resident relations are kept per scan node (a plan-cache hit
         # re-runs the same node with new literals above it): no listing, bucket-id parsing or
         # cache-key hashing per query while the device cache holds both tables
@@ -621,7 +623,16 @@ class AggOps:
             afiles = [f for f in files if not is_bucket(f)]
             if not bfiles or not afiles:
                 return None
-            scans = [self._scan(node, bfiles, True), self._scan(node, afiles, False)]
+            appended = self._scan(node, afiles, False)
+            # the appended rows sorted once by the index key (a one-bucket layout cached on
+            # their table, as a Hybrid Scan shuffle is): the scan prunes them by key range too
+            ikey = rel.index.indexed_columns[0].lower()
+            ka = next((a for a in node.output if a.name.lower() == ikey), None)
+            if ka is not None:
+                srt = self._repartition_cached(appended, [ka], 1)
+                if srt is not None:
+                    appended = srt
+            scans = [self._scan(node, bfiles, True), appended]
             nbf, naf = len(bfiles), len(afiles)
             if len(memo) > 64:
                 memo.clear()

@@ -404,6 +404,20 @@ class PlanCache:
                    getattr(getattr(e, "partitioning", None), "num_partitions", None))
                   for e in exch]
         reuse = len(shapes) != len(set(shapes))
+        if reuse:
+            # two exchanges can only ever be reused when they read the same data: exchanges of
+            # one shape over different scans (a Hybrid Scan join's two appended-file shuffles)
+            # never match, whatever the literals - no reuse pass per hit for them
+            def data_id(e):
+                return tuple(sorted(
+                    (type(n.relation.location).__name__,
+                     hash(tuple(sorted(repr(f) for f in n.relation.location.all_files()))))
+                    if isinstance(n, X.FileSourceScanExec) else
+                    (("local", id(n.table)) if isinstance(n, X.LocalTableScanExec)
+                     else (type(n).__name__,))
+                    for n in e.collect(lambda m: not m.children)))
+            keyed = [(sh, data_id(e)) for sh, e in zip(shapes, exch)]
+            reuse = len(keyed) != len(set(keyed))
         present: List[E.Literal] = []
         _iter_literals(executed, present, set())
         ids = {id(x) for x in present}

@@ -377,17 +377,26 @@ def test_hybrid_scan_join_and_filter_on_device(tpch, tmp_path):
     # (GpuBackend._union_agg) equal the materialize-and-concatenate path
     plan2 = q2.queryExecution.executed_plan.tree_string()
     if "Union" not in plan2:
-        # same-scan appended files: the index files scan bucket-sorted (key-range pruned), the
-        # appended files flat (GpuBackend._mixed_index_agg); equal to one flat table of all
-        assert s.backend().metrics.get("mixed_scan_agg"), plan2
-        s.conf.set("spark.hyperspace.mi.mixedScanAgg.enabled", "false")
+        # same-scan appended files: one resident table of the index buckets plus the appended
+        # rows sorted by the key as one more range (GpuBackend._hybrid_scan); without it the
+        # index files scan bucket-sorted and the appended files flat
+        # (GpuBackend._mixed_index_agg); both equal one flat table of all the files
+        assert s.backend().metrics.get("hybrid_scan_merged"), plan2
+        s.conf.set("spark.hyperspace.mi.hybridScanMerge.enabled", "false")
         try:
+            g4, c4, path = _both(s, q2, sort=False)
+            assert path == "native", s.backend().fallback_reason
+            assert s.backend().metrics.get("mixed_scan_agg"), plan2
+            _close(g4, c4)
+            _close(g4, g)
+            s.conf.set("spark.hyperspace.mi.mixedScanAgg.enabled", "false")
             g3, c3, path = _both(s, q2, sort=False)
             assert path == "native", s.backend().fallback_reason
             _close(g3, c3)
             _close(g3, g)
         finally:
             s.conf.set("spark.hyperspace.mi.mixedScanAgg.enabled", "true")
+            s.conf.set("spark.hyperspace.mi.hybridScanMerge.enabled", "true")
     if "Union" in plan2 and "BucketUnion" not in plan2:
         s.conf.set("spark.hyperspace.mi.unionAgg.enabled", "false")
         try:
