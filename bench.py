@@ -122,9 +122,11 @@ def main():
                          "sharded = buckets b %% N per rank, every query on all ranks + one "
                          "all-gather; replicated = every rank holds all buckets and serves its "
                          "own query stream; both = time sharded, then replicated (reported)")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=4,
                     help="query steps kept in flight (DataFrame.collect_async): 1 = each query "
-                         "finishes before the next is planned")
+                         "finishes before the next is planned.  4: a sharded run's cross-rank "
+                         "combines of the steps in flight travel together (one collective per "
+                         "flush); one GPU measures the same with 2 or 4")
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
                     help="cpu = the pyarrow host engine (measured baseline, BASELINE.md)")
     ap.add_argument("--record-baseline", action="store_true",
