@@ -528,6 +528,19 @@ def _file_pages(f) -> Tuple[int, int]:
     return rgs[0][0], rgs[-1][0] + rgs[-1][1]
 
 
+DMA_ALIGN = 256
+
+
+def _dma_span(lo: int, hi: int, n: int) -> Tuple[int, int]:
+    """[lo, hi) widened to DMA_ALIGN boundaries inside a device buffer of ``n`` bytes: a copy
+    with an unaligned device offset goes through a blit kernel on the compute units (which
+    then queues behind the compressor's waves) instead of an SDMA engine; the extra bytes are
+    never read on the host (page addresses are taken relative to the returned ``lo``)."""
+    if hi <= lo:
+        return lo, hi
+    return lo - lo % DMA_ALIGN, min(n, -(-hi // DMA_ALIGN) * DMA_ALIGN)
+
+
 def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: pa.Schema,
                   bucket_off: np.ndarray, path_of: Callable[[int], str], rg_rows: int, device,
                   chunk_bytes: int = 96 << 20, codec: str = "none") -> Optional[List[str]]:
@@ -638,6 +651,7 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
                 for c in range(len(segs)):
                     lo = int(zoff[c][p_first - gfirst])
                     hi = int(zoff[c][p_end - 1 - gfirst] + zsize[c][p_end - 1 - gfirst])
+                    lo, hi = _dma_span(lo, hi, packed.numel())
                     h = pinned_pool().acquire(hi - lo)
                     if hi > lo:
                         h[:hi - lo].copy_(packed[lo:hi], non_blocking=True)
@@ -645,6 +659,7 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
             else:
                 for sg in segs:
                     lo, hi = int(sg.page_off[p_first]), int(sg.page_off[p_end])
+                    lo, hi = _dma_span(lo, hi, sg.payload.numel())
                     h = pinned_pool().acquire(hi - lo)
                     if hi > lo:
                         h[:hi - lo].copy_(sg.payload[lo:hi], non_blocking=True)
