@@ -57,6 +57,14 @@ __device__ __forceinline__ void lds_max(double* p, double v) {
   do { as = old; if (__longlong_as_double((i64)as) >= v) break;
        old = atomicCAS(a, as, (u64)__double_as_longlong(v)); } while (as != old);
 }
+// order-preserving signed image of a double (top-K thresholds published with atomicMax)
+__device__ __forceinline__ long long hs_dimg(double d) {
+  const long long u = __double_as_longlong(d);
+  return u >= 0 ? u : u ^ 0x7fffffffffffffffll;
+}
+__device__ __forceinline__ double hs_dimg_inv(long long i) {
+  return __longlong_as_double(i >= 0 ? i : i ^ 0x7fffffffffffffffll);
+}
 // hash-mode grouping (exec/hash_agg.py, csrc/kernels/hash_agg.hip): probe hash and the bit
 // images of float group keys (-0.0 -> 0.0, one NaN)
 __device__ __forceinline__ u64 hs_mix64(u64 h) {
@@ -93,24 +101,16 @@ struct Args {
   double R2;
   long long B3;
   double R3;
-  const int* c0;
-  long long B0;
-  unsigned long long* hkeys;
-  double* hsum;
-  long long* hcnt;
-  long long HM;
-  long long* hflag;
-  long long HL0;
-  long long HS0;
   double A0_0;
   double B0_0;
   double A0_1;
   double B0_1;
 };
-extern "C" __global__ __launch_bounds__(256) void hs_jit_run_bits_hash(Args a) {
-  constexpr int NA = 2;
+extern "C" __global__ __launch_bounds__(256) void hs_jit_run_bits_scan(Args a) {
+  constexpr int NA = 3;
   double acc0 = 0.0; unsigned cnt0 = 0u;
   double acc1 = 0.0; unsigned cnt1 = 0u;
+  double acc2 = 0.0; unsigned cnt2 = 0u;
   __shared__ unsigned short lst_[4][1024];
   const int ln = (int)(threadIdx.x & 63);
   const int wq = (int)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -182,7 +182,7 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_bits_hash(Args a) {
     for (int wb_ = 0; wb_ < tot_; wb_ += 1024) {
     const int wn_ = tot_ - wb_ < 1024 ? tot_ - wb_ : 1024;
     { int pos_ = inc_ - cn_ - wb_; u64 e_ = d_;
-      while (e_) { const int bq_ = __builtin_ctzll(e_); if (pos_ >= 0 && pos_ < 1024) lst_[wq][pos_] = (unsigned short)(64 * ln + bq_); ++pos_; e_ &= e_ - 1ull; } }
+      while (e_) { const int bq_ = __builtin_ctzll(e_); if (pos_ >= 0 && pos_ < 1024) { lst_[wq][pos_] = (unsigned short)(64 * ln + bq_); } ++pos_; e_ &= e_ - 1ull; } }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     for (int cb = 0; cb < wn_; cb += 256) {
       const int ce0 = cb + 0 + ln;
@@ -204,9 +204,6 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_bits_hash(Args a) {
       const int r3_c0 = (int)((signed char)(unsigned char)(pk0_ >> 32));
       const i64 q3_c0 = a.B3 + (i64)((signed char)(unsigned char)(pk0_ >> 32));
       const double x3_c0 = (double)((double)(a.B3 + (i64)((signed char)(unsigned char)(pk0_ >> 32))) * a.R3);
-      const int w0_c0 = a.c0[crow0];
-      const int r0_c0 = (int)w0_c0;
-      const long long x0_c0 = (long long)(a.B0 + (i64)w0_c0);
       const u64 pk1_ = a.PK[crow1];
       const int r2_c1 = (int)((int)(unsigned)(pk1_ >> 0));
       const i64 q2_c1 = a.B2 + (i64)((int)(unsigned)(pk1_ >> 0));
@@ -214,9 +211,6 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_bits_hash(Args a) {
       const int r3_c1 = (int)((signed char)(unsigned char)(pk1_ >> 32));
       const i64 q3_c1 = a.B3 + (i64)((signed char)(unsigned char)(pk1_ >> 32));
       const double x3_c1 = (double)((double)(a.B3 + (i64)((signed char)(unsigned char)(pk1_ >> 32))) * a.R3);
-      const int w0_c1 = a.c0[crow1];
-      const int r0_c1 = (int)w0_c1;
-      const long long x0_c1 = (long long)(a.B0 + (i64)w0_c1);
       const u64 pk2_ = a.PK[crow2];
       const int r2_c2 = (int)((int)(unsigned)(pk2_ >> 0));
       const i64 q2_c2 = a.B2 + (i64)((int)(unsigned)(pk2_ >> 0));
@@ -224,9 +218,6 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_bits_hash(Args a) {
       const int r3_c2 = (int)((signed char)(unsigned char)(pk2_ >> 32));
       const i64 q3_c2 = a.B3 + (i64)((signed char)(unsigned char)(pk2_ >> 32));
       const double x3_c2 = (double)((double)(a.B3 + (i64)((signed char)(unsigned char)(pk2_ >> 32))) * a.R3);
-      const int w0_c2 = a.c0[crow2];
-      const int r0_c2 = (int)w0_c2;
-      const long long x0_c2 = (long long)(a.B0 + (i64)w0_c2);
       const u64 pk3_ = a.PK[crow3];
       const int r2_c3 = (int)((int)(unsigned)(pk3_ >> 0));
       const i64 q2_c3 = a.B2 + (i64)((int)(unsigned)(pk3_ >> 0));
@@ -234,167 +225,63 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_bits_hash(Args a) {
       const int r3_c3 = (int)((signed char)(unsigned char)(pk3_ >> 32));
       const i64 q3_c3 = a.B3 + (i64)((signed char)(unsigned char)(pk3_ >> 32));
       const double x3_c3 = (double)((double)(a.B3 + (i64)((signed char)(unsigned char)(pk3_ >> 32))) * a.R3);
-      const int w0_c3 = a.c0[crow3];
-      const int r0_c3 = (int)w0_c3;
-      const long long x0_c3 = (long long)(a.B0 + (i64)w0_c3);
       { bool cok = cok0;
-      { const int hln = (int)(threadIdx.x & 63u); const bool hok = cok;
-        u64 hk = 0ull; const bool hnul = false;
-        hk |= (u64)((i64)x0_c0 - a.HL0) << (unsigned)a.HS0;
-        const u64 hkp = __shfl_up(hk, 1u, 64);
-        const int hfp = __shfl_up((hok ? 1 : 0) | (hnul ? 2 : 0), 1u, 64);
-        const bool hsame = hln > 0 && hok && (hfp & 1) != 0 && ((hfp >> 1) & 1) == (hnul ? 1 : 0) && hkp == hk;
-        const u64 hH = __ballot(!hsame);
-        const int hss = 63 - __builtin_clzll(hH & ((2ull << hln) - 1ull));
-        const bool htl = hok && (hln == 63 || ((hH >> ((hln + 1) & 63)) & 1ull) != 0ull);
-        const bool hq0 = hok && true;
-        double hv0 = hq0 ? (double)((a.A0_0 + a.B0_0 * (double)x2_c0) * (a.A0_1 + a.B0_1 * (double)x3_c0)) : 0.0;
-        #pragma unroll
-        for (int hd = 1; hd < 64; hd <<= 1) {
-          const double u_hv0 = __shfl_up(hv0, (unsigned)hd, 64);
-          if (hln - hd >= hss) {
-            hv0 = hv0 + u_hv0;
-          }
-        }
-        if (htl) {
-          long long hs_ = -1;
-          if (hnul) hs_ = a.HM + 1; else if (hk == ~0ull) hs_ = a.HM; else {
-            u64 hh = hs_mix64(hk) & (u64)(a.HM - 1);
-            for (int pr_ = 0; pr_ < 512; ++pr_) {
-              const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hk);
-              if (pv_ == ~0ull || pv_ == hk) { hs_ = (long long)hh; break; }
-              hh = (hh + 1ull) & (u64)(a.HM - 1);
-            }
-            if (hs_ < 0) a.hflag[0] = 1;
-          }
-          if (hs_ >= 0) {
-            const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
-            const unsigned long long hrn = (unsigned long long)(hln - hss + 1);
-            unsafeAtomicAdd(&a.hsum[0 * hst + hs_], hv0);
-            if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
-          }
-        }
-      }
+      { const bool ok = cok && true; const double v = ok ? (a.A0_0 + a.B0_0 * (double)x2_c0) * (a.A0_1 + a.B0_1 * (double)x3_c0) : 0.0;
+        acc0 += v; cnt0 += ok ? 1u : 0u; }
+      { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
+        acc1 += v; cnt1 += ok ? 1u : 0u; }
+      { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
+        acc2 += v; cnt2 += ok ? 1u : 0u; }
       }
       { bool cok = cok1;
-      { const int hln = (int)(threadIdx.x & 63u); const bool hok = cok;
-        u64 hk = 0ull; const bool hnul = false;
-        hk |= (u64)((i64)x0_c1 - a.HL0) << (unsigned)a.HS0;
-        const u64 hkp = __shfl_up(hk, 1u, 64);
-        const int hfp = __shfl_up((hok ? 1 : 0) | (hnul ? 2 : 0), 1u, 64);
-        const bool hsame = hln > 0 && hok && (hfp & 1) != 0 && ((hfp >> 1) & 1) == (hnul ? 1 : 0) && hkp == hk;
-        const u64 hH = __ballot(!hsame);
-        const int hss = 63 - __builtin_clzll(hH & ((2ull << hln) - 1ull));
-        const bool htl = hok && (hln == 63 || ((hH >> ((hln + 1) & 63)) & 1ull) != 0ull);
-        const bool hq0 = hok && true;
-        double hv0 = hq0 ? (double)((a.A0_0 + a.B0_0 * (double)x2_c1) * (a.A0_1 + a.B0_1 * (double)x3_c1)) : 0.0;
-        #pragma unroll
-        for (int hd = 1; hd < 64; hd <<= 1) {
-          const double u_hv0 = __shfl_up(hv0, (unsigned)hd, 64);
-          if (hln - hd >= hss) {
-            hv0 = hv0 + u_hv0;
-          }
-        }
-        if (htl) {
-          long long hs_ = -1;
-          if (hnul) hs_ = a.HM + 1; else if (hk == ~0ull) hs_ = a.HM; else {
-            u64 hh = hs_mix64(hk) & (u64)(a.HM - 1);
-            for (int pr_ = 0; pr_ < 512; ++pr_) {
-              const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hk);
-              if (pv_ == ~0ull || pv_ == hk) { hs_ = (long long)hh; break; }
-              hh = (hh + 1ull) & (u64)(a.HM - 1);
-            }
-            if (hs_ < 0) a.hflag[0] = 1;
-          }
-          if (hs_ >= 0) {
-            const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
-            const unsigned long long hrn = (unsigned long long)(hln - hss + 1);
-            unsafeAtomicAdd(&a.hsum[0 * hst + hs_], hv0);
-            if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
-          }
-        }
-      }
+      { const bool ok = cok && true; const double v = ok ? (a.A0_0 + a.B0_0 * (double)x2_c1) * (a.A0_1 + a.B0_1 * (double)x3_c1) : 0.0;
+        acc0 += v; cnt0 += ok ? 1u : 0u; }
+      { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
+        acc1 += v; cnt1 += ok ? 1u : 0u; }
+      { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
+        acc2 += v; cnt2 += ok ? 1u : 0u; }
       }
       { bool cok = cok2;
-      { const int hln = (int)(threadIdx.x & 63u); const bool hok = cok;
-        u64 hk = 0ull; const bool hnul = false;
-        hk |= (u64)((i64)x0_c2 - a.HL0) << (unsigned)a.HS0;
-        const u64 hkp = __shfl_up(hk, 1u, 64);
-        const int hfp = __shfl_up((hok ? 1 : 0) | (hnul ? 2 : 0), 1u, 64);
-        const bool hsame = hln > 0 && hok && (hfp & 1) != 0 && ((hfp >> 1) & 1) == (hnul ? 1 : 0) && hkp == hk;
-        const u64 hH = __ballot(!hsame);
-        const int hss = 63 - __builtin_clzll(hH & ((2ull << hln) - 1ull));
-        const bool htl = hok && (hln == 63 || ((hH >> ((hln + 1) & 63)) & 1ull) != 0ull);
-        const bool hq0 = hok && true;
-        double hv0 = hq0 ? (double)((a.A0_0 + a.B0_0 * (double)x2_c2) * (a.A0_1 + a.B0_1 * (double)x3_c2)) : 0.0;
-        #pragma unroll
-        for (int hd = 1; hd < 64; hd <<= 1) {
-          const double u_hv0 = __shfl_up(hv0, (unsigned)hd, 64);
-          if (hln - hd >= hss) {
-            hv0 = hv0 + u_hv0;
-          }
-        }
-        if (htl) {
-          long long hs_ = -1;
-          if (hnul) hs_ = a.HM + 1; else if (hk == ~0ull) hs_ = a.HM; else {
-            u64 hh = hs_mix64(hk) & (u64)(a.HM - 1);
-            for (int pr_ = 0; pr_ < 512; ++pr_) {
-              const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hk);
-              if (pv_ == ~0ull || pv_ == hk) { hs_ = (long long)hh; break; }
-              hh = (hh + 1ull) & (u64)(a.HM - 1);
-            }
-            if (hs_ < 0) a.hflag[0] = 1;
-          }
-          if (hs_ >= 0) {
-            const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
-            const unsigned long long hrn = (unsigned long long)(hln - hss + 1);
-            unsafeAtomicAdd(&a.hsum[0 * hst + hs_], hv0);
-            if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
-          }
-        }
-      }
+      { const bool ok = cok && true; const double v = ok ? (a.A0_0 + a.B0_0 * (double)x2_c2) * (a.A0_1 + a.B0_1 * (double)x3_c2) : 0.0;
+        acc0 += v; cnt0 += ok ? 1u : 0u; }
+      { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
+        acc1 += v; cnt1 += ok ? 1u : 0u; }
+      { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
+        acc2 += v; cnt2 += ok ? 1u : 0u; }
       }
       { bool cok = cok3;
-      { const int hln = (int)(threadIdx.x & 63u); const bool hok = cok;
-        u64 hk = 0ull; const bool hnul = false;
-        hk |= (u64)((i64)x0_c3 - a.HL0) << (unsigned)a.HS0;
-        const u64 hkp = __shfl_up(hk, 1u, 64);
-        const int hfp = __shfl_up((hok ? 1 : 0) | (hnul ? 2 : 0), 1u, 64);
-        const bool hsame = hln > 0 && hok && (hfp & 1) != 0 && ((hfp >> 1) & 1) == (hnul ? 1 : 0) && hkp == hk;
-        const u64 hH = __ballot(!hsame);
-        const int hss = 63 - __builtin_clzll(hH & ((2ull << hln) - 1ull));
-        const bool htl = hok && (hln == 63 || ((hH >> ((hln + 1) & 63)) & 1ull) != 0ull);
-        const bool hq0 = hok && true;
-        double hv0 = hq0 ? (double)((a.A0_0 + a.B0_0 * (double)x2_c3) * (a.A0_1 + a.B0_1 * (double)x3_c3)) : 0.0;
-        #pragma unroll
-        for (int hd = 1; hd < 64; hd <<= 1) {
-          const double u_hv0 = __shfl_up(hv0, (unsigned)hd, 64);
-          if (hln - hd >= hss) {
-            hv0 = hv0 + u_hv0;
-          }
-        }
-        if (htl) {
-          long long hs_ = -1;
-          if (hnul) hs_ = a.HM + 1; else if (hk == ~0ull) hs_ = a.HM; else {
-            u64 hh = hs_mix64(hk) & (u64)(a.HM - 1);
-            for (int pr_ = 0; pr_ < 512; ++pr_) {
-              const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hk);
-              if (pv_ == ~0ull || pv_ == hk) { hs_ = (long long)hh; break; }
-              hh = (hh + 1ull) & (u64)(a.HM - 1);
-            }
-            if (hs_ < 0) a.hflag[0] = 1;
-          }
-          if (hs_ >= 0) {
-            const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
-            const unsigned long long hrn = (unsigned long long)(hln - hss + 1);
-            unsafeAtomicAdd(&a.hsum[0 * hst + hs_], hv0);
-            if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
-          }
-        }
-      }
+      { const bool ok = cok && true; const double v = ok ? (a.A0_0 + a.B0_0 * (double)x2_c3) * (a.A0_1 + a.B0_1 * (double)x3_c3) : 0.0;
+        acc0 += v; cnt0 += ok ? 1u : 0u; }
+      { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
+        acc1 += v; cnt1 += ok ? 1u : 0u; }
+      { const bool ok = cok && true; const double v = ok ? 1.0 : 0.0;
+        acc2 += v; cnt2 += ok ? 1u : 0u; }
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+  }
+  __shared__ double rv[4][NA]; __shared__ i64 rc[4][NA];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  { const double r = wsum(acc0); const i64 c = wsumi((i64)cnt0); if (lane == 0) { rv[w][0] = r; rc[w][0] = c; } }
+  { const double r = wsum(acc1); const i64 c = wsumi((i64)cnt1); if (lane == 0) { rv[w][1] = r; rc[w][1] = c; } }
+  { const double r = wsum(acc2); const i64 c = wsumi((i64)cnt2); if (lane == 0) { rv[w][2] = r; rc[w][2] = c; } }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    { double t = 0.0; i64 c = 0;
+      for (int k = 0; k < 4; ++k) { t = t + rv[k][0]; c += rc[k][0]; }
+      const i64 o = (i64)blockIdx.x * NA + 0;
+      a.psum[o] = t; a.pcnt[o] = c;
+      a.pmin[o] = __builtin_inf(); a.pmax[o] = -__builtin_inf(); }
+    { double t = 0.0; i64 c = 0;
+      for (int k = 0; k < 4; ++k) { t = t + rv[k][1]; c += rc[k][1]; }
+      const i64 o = (i64)blockIdx.x * NA + 1;
+      a.psum[o] = t; a.pcnt[o] = c;
+      a.pmin[o] = __builtin_inf(); a.pmax[o] = -__builtin_inf(); }
+    { double t = 0.0; i64 c = 0;
+      for (int k = 0; k < 4; ++k) { t = t + rv[k][2]; c += rc[k][2]; }
+      const i64 o = (i64)blockIdx.x * NA + 2;
+      a.psum[o] = t; a.pcnt[o] = c;
+      a.pmin[o] = __builtin_inf(); a.pmax[o] = -__builtin_inf(); }
   }
 }

@@ -1,0 +1,776 @@
+
+typedef long long i64;
+typedef unsigned long long u64;
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ i64 wsumi(i64 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wmin(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wmax(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ bool in_set(const i64* s, int n, i64 x) {
+  int lo = 0, hi = n;
+  while (lo < hi) { const int m = (lo + hi) >> 1; if (s[m] < x) lo = m + 1; else hi = m; }
+  return lo < n && s[lo] == x;
+}
+__device__ __forceinline__ bool bit_test(const u64* w, i64 nbits, i64 x) {
+  return x >= 0 && x < nbits && ((w[x >> 6] >> (x & 63)) & 1ull);
+}
+// V consecutive elements starting at an index that is a multiple of V (so the address is
+// aligned to V * sizeof(T) for a 16-byte aligned base): one dwordx4 per 16 bytes
+template <typename T, int V>
+__device__ __forceinline__ void vload(const T* __restrict__ p, long long i, T (&x)[V]) {
+  constexpr int B = (int)sizeof(T) * V;
+  if constexpr (B % 16 == 0) {
+    const uint4* q = reinterpret_cast<const uint4*>(p + i);
+#pragma unroll
+    for (int k = 0; k < B / 16; ++k) reinterpret_cast<uint4*>(x)[k] = q[k];
+  } else if constexpr (B == 8) {
+    *reinterpret_cast<uint2*>(x) = *reinterpret_cast<const uint2*>(p + i);
+  } else if constexpr (B == 4) {
+    *reinterpret_cast<unsigned*>(x) = *reinterpret_cast<const unsigned*>(p + i);
+  } else {
+#pragma unroll
+    for (int k = 0; k < V; ++k) x[k] = p[i + k];
+  }
+}
+__device__ __forceinline__ void lds_min(double* p, double v) {
+  u64* a = (u64*)p; u64 old = *a, as;
+  do { as = old; if (__longlong_as_double((i64)as) <= v) break;
+       old = atomicCAS(a, as, (u64)__double_as_longlong(v)); } while (as != old);
+}
+__device__ __forceinline__ void lds_max(double* p, double v) {
+  u64* a = (u64*)p; u64 old = *a, as;
+  do { as = old; if (__longlong_as_double((i64)as) >= v) break;
+       old = atomicCAS(a, as, (u64)__double_as_longlong(v)); } while (as != old);
+}
+// order-preserving signed image of a double (top-K thresholds published with atomicMax)
+__device__ __forceinline__ long long hs_dimg(double d) {
+  const long long u = __double_as_longlong(d);
+  return u >= 0 ? u : u ^ 0x7fffffffffffffffll;
+}
+__device__ __forceinline__ double hs_dimg_inv(long long i) {
+  return __longlong_as_double(i >= 0 ? i : i ^ 0x7fffffffffffffffll);
+}
+// hash-mode grouping (exec/hash_agg.py, csrc/kernels/hash_agg.hip): probe hash and the bit
+// images of float group keys (-0.0 -> 0.0, one NaN)
+__device__ __forceinline__ u64 hs_mix64(u64 h) {
+  h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull;
+  return h ^ (h >> 33);
+}
+__device__ __forceinline__ u64 hs_f64key(double d) {
+  d = d == 0.0 ? 0.0 : d;
+  return d != d ? 0x7ff8000000000000ull : (u64)__double_as_longlong(d);
+}
+__device__ __forceinline__ u64 hs_f32key(float f) {
+  f = f == 0.0f ? 0.0f : f;
+  return f != f ? 0x7fc00000ull : (u64)(unsigned)__float_as_uint(f);
+}
+struct Args {
+  const long long* rstart;
+  const long long* rlen;
+  const long long* tile_prefix;
+  const unsigned long long* GM0;
+  const int* GR0;
+  const unsigned* tags;
+  long long R;
+  long long nrows;
+  double* psum;
+  double* pmin;
+  double* pmax;
+  long long* pcnt;
+  const short* c1;
+  long long CL1;
+  long long CH1;
+  long long B1;
+  const unsigned long long* PK;
+  long long B2;
+  double R2;
+  long long B3;
+  double R3;
+  double A0_0;
+  double B0_0;
+  double A0_1;
+  double B0_1;
+  const int* c0;
+  long long B0;
+  long long HL0;
+  long long HS0;
+  unsigned long long* hkeys;
+  double* hsum;
+  long long* hcnt;
+  long long HM;
+  long long* hflag;
+  unsigned long long* TKK;
+  long long* TKV;
+  double* TKS;
+  long long* TKC;
+  long long* TKW;
+  long long* TKD;
+  long long TKCAP;
+};
+extern "C" __global__ __launch_bounds__(256) void hs_jit_run_bits_topk(Args a) {
+  constexpr int NA = 2;
+  double acc0 = 0.0; unsigned cnt0 = 0u;
+  double acc1 = 0.0; unsigned cnt1 = 0u;
+  double tkdmx = -__builtin_inf();
+  long long tcr_ = -1, tcw_ = 0, tcn_ = 0; bool tco_ = false;
+  double tcv0 = 0.0; long long tcc0 = 0ll; double tcv1 = 0.0; long long tcc1 = 0ll;
+  i64 tkr0 = -1; double tkv0 = -__builtin_inf(); double tks0_0 = 0.0; long long tkc0_0 = 0ll; double tks0_1 = 0.0; long long tkc0_1 = 0ll;
+  i64 tkr1 = -1; double tkv1 = -__builtin_inf(); double tks1_0 = 0.0; long long tkc1_0 = 0ll; double tks1_1 = 0.0; long long tkc1_1 = 0ll;
+  __shared__ unsigned short lrn_[4][1024];
+  __shared__ unsigned short lst_[4][1024];
+  const int ln = (int)(threadIdx.x & 63);
+  const int wq = (int)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const i64 ntiles = a.tile_prefix[a.R];
+  const i64 nwv = (i64)gridDim.x * 4;
+  const i64 wid = (i64)blockIdx.x * 4 + wq;
+  const i64 per = (ntiles + nwv - 1) / nwv;
+  const i64 t0 = wid * per;
+  const i64 t1 = ntiles < t0 + per ? ntiles : t0 + per;
+  int r = 0;
+  if (t0 < t1) { int lo = 0, hi = (int)a.R;
+    while (hi - lo > 1) { const int m = (lo + hi) >> 1; if (a.tile_prefix[m] <= t0) lo = m; else hi = m; }
+    r = lo; }
+  i64 rsN = 0, reN = 0, tbN = 0; u64 gmN = 0ull; i64 grN = 0;
+  if (t0 < t1) {
+    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= t0) ++r;
+    rsN = a.rstart[r]; reN = rsN + a.rlen[r];
+    tbN = (rsN & ~(i64)63) + (t0 - a.tile_prefix[r]) * 4096;
+    { const i64 r0_ = tbN + 64 * ln; const i64 g_ = (r0_ < a.nrows ? r0_ : a.nrows - 1) >> 6;
+      gmN = a.GM0[g_] | 1ull; grN = a.GR0[g_]; }
+  }
+  for (i64 t = t0; t < t1; ++t) {
+    const i64 rs = rsN, re = reN, tb0 = tbN; const u64 m_ = gmN; const i64 q0 = grN;
+    const i64 qb_ = __shfl(q0, 0, 64); const int qr_ = (int)(q0 - qb_);
+    const i64 row0 = tb0 + 64 * ln;
+    const i64 lo_ = rs - row0, hi_ = re - row0;
+    const int alo = lo_ <= 0 ? 0 : (lo_ >= 64 ? 64 : (int)lo_);
+    const int ahi = hi_ <= 0 ? 0 : (hi_ >= 64 ? 64 : (int)hi_);
+    const u64 am = alo >= ahi ? 0ull : ((ahi == 64 ? ~0ull : ((1ull << ahi) - 1ull)) & ~((1ull << alo) - 1ull));
+    const i64 w_ = q0 >> 5; const unsigned sh_ = (unsigned)(q0 & 31);
+    const u64 lw_ = (u64)a.tags[w_] | ((u64)a.tags[w_ + 1] << 32);
+    const u64 hw_ = (u64)a.tags[w_ + 2];
+    const bool vok_ = row0 + 64 <= a.nrows;
+    unsigned x1w[32];
+    if (vok_) { vload<unsigned, 32>((const unsigned*)a.c1, row0 * 2 / 4, x1w); } else { for (int k_ = 0; k_ < 32; ++k_) x1w[k_] = 0u; for (int k_ = 0; k_ < 64 && row0 + k_ < a.nrows; ++k_) { const unsigned u_ = (unsigned)(unsigned short)a.c1[row0 + k_]; x1w[k_ / 2] |= u_ << (16 * (k_ % 2)); } }
+    if (t + 1 < t1) {
+      while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= (t + 1)) ++r;
+      rsN = a.rstart[r]; reN = rsN + a.rlen[r];
+      tbN = (rsN & ~(i64)63) + ((t + 1) - a.tile_prefix[r]) * 4096;
+      { const i64 r0_ = tbN + 64 * ln; const i64 g_ = (r0_ < a.nrows ? r0_ : a.nrows - 1) >> 6;
+        gmN = a.GM0[g_] | 1ull; grN = a.GR0[g_]; }
+    }
+    const u64 T_ = sh_ ? ((lw_ >> sh_) | (hw_ << (64 - sh_))) : lw_;
+    const int nr_ = __popcll(m_);
+    const u64 Tm_ = nr_ >= 64 ? T_ : (T_ & ((1ull << nr_) - 1ull));
+    u64 c_ = T_ ^ (T_ << 1), d_ = 0ull, mm_ = (am && Tm_) ? m_ : 0ull;
+    while (mm_) { const u64 lb_ = mm_ & (0ull - mm_); if (c_ & 1ull) d_ |= lb_; c_ >>= 1; mm_ ^= lb_; }
+    d_ ^= d_ << 1; d_ ^= d_ << 2; d_ ^= d_ << 4; d_ ^= d_ << 8; d_ ^= d_ << 16; d_ ^= d_ << 32;
+    d_ &= am;
+    unsigned plo_ = 0u, phi_ = 0u;
+    #pragma unroll
+    for (int k_ = 0; k_ < 32; ++k_) {
+      const auto xr1_k = ((short)(x1w[(0 + k_) / 2] >> (16 * ((0 + k_) % 2))));
+      const int r1_k = (int)xr1_k;
+      const int x1_k = (int)(a.B1 + (i64)xr1_k);
+      plo_ |= (((true)) && ((true && (r1_k >= (int)a.CL1 && r1_k <= (int)a.CH1))) ? 1u : 0u) << k_;
+    }
+    #pragma unroll
+    for (int k_ = 0; k_ < 32; ++k_) {
+      const auto xr1_k = ((short)(x1w[(32 + k_) / 2] >> (16 * ((32 + k_) % 2))));
+      const int r1_k = (int)xr1_k;
+      const int x1_k = (int)(a.B1 + (i64)xr1_k);
+      phi_ |= (((true)) && ((true && (r1_k >= (int)a.CL1 && r1_k <= (int)a.CH1))) ? 1u : 0u) << k_;
+    }
+    d_ &= ((u64)phi_ << 32) | (u64)plo_;
+    const int cn_ = __popcll(d_);
+    int inc_ = cn_;
+    for (int o_ = 1; o_ < 64; o_ <<= 1) { const int y_ = __shfl_up(inc_, o_, 64); if (ln >= o_) inc_ += y_; }
+    const int tot_ = __shfl(inc_, 63, 64);
+    for (int wb_ = 0; wb_ < tot_; wb_ += 1024) {
+    const int wn_ = tot_ - wb_ < 1024 ? tot_ - wb_ : 1024;
+    { int pos_ = inc_ - cn_ - wb_; u64 e_ = d_;
+      while (e_) { const int bq_ = __builtin_ctzll(e_); if (pos_ >= 0 && pos_ < 1024) { lst_[wq][pos_] = (unsigned short)(64 * ln + bq_); lrn_[wq][pos_] = (unsigned short)(qr_ + __popcll(m_ & ((2ull << bq_) - 1ull))); } ++pos_; e_ &= e_ - 1ull; } }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int cb = 0; cb < wn_; cb += 256) {
+      const int ce0 = cb + 0 + ln;
+      const bool cok0 = ce0 < wn_;
+      const i64 crow0 = tb0 + (cok0 ? (i64)lst_[wq][ce0] : 0);
+      const unsigned crn0 = cok0 ? (unsigned)lrn_[wq][ce0] : 0xFFFFFFFFu;
+      const int ce1 = cb + 64 + ln;
+      const bool cok1 = ce1 < wn_;
+      const i64 crow1 = tb0 + (cok1 ? (i64)lst_[wq][ce1] : 0);
+      const unsigned crn1 = cok1 ? (unsigned)lrn_[wq][ce1] : 0xFFFFFFFFu;
+      const int ce2 = cb + 128 + ln;
+      const bool cok2 = ce2 < wn_;
+      const i64 crow2 = tb0 + (cok2 ? (i64)lst_[wq][ce2] : 0);
+      const unsigned crn2 = cok2 ? (unsigned)lrn_[wq][ce2] : 0xFFFFFFFFu;
+      const int ce3 = cb + 192 + ln;
+      const bool cok3 = ce3 < wn_;
+      const i64 crow3 = tb0 + (cok3 ? (i64)lst_[wq][ce3] : 0);
+      const unsigned crn3 = cok3 ? (unsigned)lrn_[wq][ce3] : 0xFFFFFFFFu;
+      const u64 pk0_ = a.PK[crow0];
+      const int r2_c0 = (int)((int)(unsigned)(pk0_ >> 0));
+      const i64 q2_c0 = a.B2 + (i64)((int)(unsigned)(pk0_ >> 0));
+      const double x2_c0 = (double)((double)(a.B2 + (i64)((int)(unsigned)(pk0_ >> 0))) * a.R2);
+      const int r3_c0 = (int)((signed char)(unsigned char)(pk0_ >> 32));
+      const i64 q3_c0 = a.B3 + (i64)((signed char)(unsigned char)(pk0_ >> 32));
+      const double x3_c0 = (double)((double)(a.B3 + (i64)((signed char)(unsigned char)(pk0_ >> 32))) * a.R3);
+      const u64 pk1_ = a.PK[crow1];
+      const int r2_c1 = (int)((int)(unsigned)(pk1_ >> 0));
+      const i64 q2_c1 = a.B2 + (i64)((int)(unsigned)(pk1_ >> 0));
+      const double x2_c1 = (double)((double)(a.B2 + (i64)((int)(unsigned)(pk1_ >> 0))) * a.R2);
+      const int r3_c1 = (int)((signed char)(unsigned char)(pk1_ >> 32));
+      const i64 q3_c1 = a.B3 + (i64)((signed char)(unsigned char)(pk1_ >> 32));
+      const double x3_c1 = (double)((double)(a.B3 + (i64)((signed char)(unsigned char)(pk1_ >> 32))) * a.R3);
+      const u64 pk2_ = a.PK[crow2];
+      const int r2_c2 = (int)((int)(unsigned)(pk2_ >> 0));
+      const i64 q2_c2 = a.B2 + (i64)((int)(unsigned)(pk2_ >> 0));
+      const double x2_c2 = (double)((double)(a.B2 + (i64)((int)(unsigned)(pk2_ >> 0))) * a.R2);
+      const int r3_c2 = (int)((signed char)(unsigned char)(pk2_ >> 32));
+      const i64 q3_c2 = a.B3 + (i64)((signed char)(unsigned char)(pk2_ >> 32));
+      const double x3_c2 = (double)((double)(a.B3 + (i64)((signed char)(unsigned char)(pk2_ >> 32))) * a.R3);
+      const u64 pk3_ = a.PK[crow3];
+      const int r2_c3 = (int)((int)(unsigned)(pk3_ >> 0));
+      const i64 q2_c3 = a.B2 + (i64)((int)(unsigned)(pk3_ >> 0));
+      const double x2_c3 = (double)((double)(a.B2 + (i64)((int)(unsigned)(pk3_ >> 0))) * a.R2);
+      const int r3_c3 = (int)((signed char)(unsigned char)(pk3_ >> 32));
+      const i64 q3_c3 = a.B3 + (i64)((signed char)(unsigned char)(pk3_ >> 32));
+      const double x3_c3 = (double)((double)(a.B3 + (i64)((signed char)(unsigned char)(pk3_ >> 32))) * a.R3);
+      { bool cok = cok0;
+      { const int hln = (int)(threadIdx.x & 63u); const bool hok = cok;
+        const u64 hV_ = __ballot(hok);
+        if (hV_ != 0ull) {
+          const unsigned hsg = (unsigned)crn0;
+          const unsigned hsp = __shfl_up(hsg, 1u, 64);
+          const int hfp = __shfl_up(hok ? 1 : 0, 1u, 64);
+          const bool hsame = hln > 0 && hok && hfp != 0 && hsp == hsg;
+          const u64 hH = __ballot(!hsame);
+          const int hss = 63 - __builtin_clzll(hH & ((2ull << hln) - 1ull));
+          const bool htl = hok && (hln == 63 || ((hH >> ((hln + 1) & 63)) & 1ull) != 0ull);
+          const int hlast_ = 63 - __builtin_clzll(hV_);
+          const long long hrun_ = hok ? (long long)(qb_ + (i64)crn0) : -1ll;
+          const long long hr0_ = __shfl(hrun_, 0, 64);
+          const bool hmg_ = tcr_ == hr0_;
+          const bool hol_ = hmg_ ? tco_ : (tcr_ < 0);
+          const bool hq0 = hok && true;
+          double hv0 = hq0 ? (double)((a.A0_0 + a.B0_0 * (double)x2_c0) * (a.A0_1 + a.B0_1 * (double)x3_c0)) : 0.0;
+          #pragma unroll
+          for (int hd = 1; hd < 64; hd <<= 1) {
+            const double u_hv0 = __shfl_up(hv0, (unsigned)hd, 64);
+            if (hln - hd >= hss) {
+              hv0 = hv0 + u_hv0;
+            }
+          }
+          long long hrn_ = (long long)(hln - hss + 1);
+          if (hmg_ && hss == 0) { hrn_ += tcn_; hv0 += tcv0; }
+          const bool hopen_ = hss == 0 && hol_;
+          const bool hlst_ = htl && hln == hlast_;
+          const bool hcomp = htl && !hlst_ && !hopen_;
+          const bool hprb_ = htl && !hlst_ && hopen_;
+          const double tkv_ = (hv0);
+          u64 hk = 0ull; bool hnul = false;
+          if (hprb_) {
+            const int w0_KK = a.c0[crow0];
+            const int r0_KK = (int)w0_KK;
+            const long long x0_KK = (long long)(a.B0 + (i64)w0_KK);
+            u64 hk_l = 0ull; const bool hk_l_nul = false;
+            hk_l |= (u64)((i64)x0_KK - a.HL0) << (unsigned)a.HS0;
+            hk = hk_l; hnul = hk_l_nul; }
+          if (hprb_) {
+            long long hs_ = -1;
+            if (hnul) hs_ = a.HM + 1; else if (hk == ~0ull) hs_ = a.HM; else {
+              u64 hh = hs_mix64(hk) & (u64)(a.HM - 1);
+              for (int pr_ = 0; pr_ < 512; ++pr_) {
+                const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hk);
+                if (pv_ == ~0ull || pv_ == hk) { hs_ = (long long)hh; break; }
+                hh = (hh + 1ull) & (u64)(a.HM - 1);
+              }
+              if (hs_ < 0) a.hflag[0] = 1;
+            }
+            if (hs_ >= 0) {
+              const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
+              const unsigned long long hrn = (unsigned long long)hrn_;
+              unsafeAtomicAdd(&a.hsum[0 * hst + hs_], hv0);
+              if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
+            }
+          }
+          if (hcomp) {
+            if (tkv_ > tkv1) {
+              tkdmx = fmax(tkdmx, tkv1);
+              if (tkv_ > tkv0) { tkr1 = tkr0; tkv1 = tkv0; tks1_0 = tks0_0; tkc1_0 = tkc0_0; tks1_1 = tks0_1; tkc1_1 = tkc0_1; tkr0 = crow0; tkv0 = tkv_; tks0_0 = (double)(hv0); tkc0_0 = (long long)(0ll); tks0_1 = (double)(0.0); tkc0_1 = (long long)(0ll); } else { tkr1 = crow0; tkv1 = tkv_; tks1_0 = (double)(hv0); tkc1_0 = (long long)(0ll); tks1_1 = (double)(0.0); tkc1_1 = (long long)(0ll); }
+            } else { tkdmx = fmax(tkdmx, tkv_); }
+          }
+          if (tcr_ >= 0 && !hmg_) {
+            const bool hce_ = hln == 0;
+            const bool hct_ = hce_ && !tco_;
+            const bool hcp_ = hce_ && tco_;
+            const double tcv_ = (tcv0);
+            u64 hck_ = 0ull; bool hcn_ = false;
+            if (hcp_) {
+              const int w0_KK = a.c0[tcw_];
+              const int r0_KK = (int)w0_KK;
+              const long long x0_KK = (long long)(a.B0 + (i64)w0_KK);
+              u64 hk_l = 0ull; const bool hk_l_nul = false;
+              hk_l |= (u64)((i64)x0_KK - a.HL0) << (unsigned)a.HS0;
+              hck_ = hk_l; hcn_ = hk_l_nul; }
+            if (hcp_) {
+              long long hs_ = -1;
+              if (hcn_) hs_ = a.HM + 1; else if (hck_ == ~0ull) hs_ = a.HM; else {
+                u64 hh = hs_mix64(hck_) & (u64)(a.HM - 1);
+                for (int pr_ = 0; pr_ < 512; ++pr_) {
+                  const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hck_);
+                  if (pv_ == ~0ull || pv_ == hck_) { hs_ = (long long)hh; break; }
+                  hh = (hh + 1ull) & (u64)(a.HM - 1);
+                }
+                if (hs_ < 0) a.hflag[0] = 1;
+              }
+              if (hs_ >= 0) {
+                const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
+                const unsigned long long hrn = (unsigned long long)tcn_;
+                unsafeAtomicAdd(&a.hsum[0 * hst + hs_], tcv0);
+                if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
+              }
+            }
+            if (hct_) {
+              if (tcv_ > tkv1) {
+                tkdmx = fmax(tkdmx, tkv1);
+                if (tcv_ > tkv0) { tkr1 = tkr0; tkv1 = tkv0; tks1_0 = tks0_0; tkc1_0 = tkc0_0; tks1_1 = tks0_1; tkc1_1 = tkc0_1; tkr0 = tcw_; tkv0 = tcv_; tks0_0 = (double)(tcv0); tkc0_0 = (long long)(0ll); tks0_1 = (double)(0.0); tkc0_1 = (long long)(0ll); } else { tkr1 = tcw_; tkv1 = tcv_; tks1_0 = (double)(tcv0); tkc1_0 = (long long)(0ll); tks1_1 = (double)(0.0); tkc1_1 = (long long)(0ll); }
+              } else { tkdmx = fmax(tkdmx, tcv_); }
+            }
+          }
+          tcr_ = __shfl(hrun_, hlast_, 64);
+          tco_ = __shfl(hopen_ ? 1 : 0, hlast_, 64) != 0;
+          tcw_ = __shfl((long long)(crow0), hlast_, 64);
+          tcn_ = __shfl(hrn_, hlast_, 64);
+          tcv0 = __shfl(hv0, hlast_, 64);
+        }
+      }
+      }
+      { bool cok = cok1;
+      { const int hln = (int)(threadIdx.x & 63u); const bool hok = cok;
+        const u64 hV_ = __ballot(hok);
+        if (hV_ != 0ull) {
+          const unsigned hsg = (unsigned)crn1;
+          const unsigned hsp = __shfl_up(hsg, 1u, 64);
+          const int hfp = __shfl_up(hok ? 1 : 0, 1u, 64);
+          const bool hsame = hln > 0 && hok && hfp != 0 && hsp == hsg;
+          const u64 hH = __ballot(!hsame);
+          const int hss = 63 - __builtin_clzll(hH & ((2ull << hln) - 1ull));
+          const bool htl = hok && (hln == 63 || ((hH >> ((hln + 1) & 63)) & 1ull) != 0ull);
+          const int hlast_ = 63 - __builtin_clzll(hV_);
+          const long long hrun_ = hok ? (long long)(qb_ + (i64)crn1) : -1ll;
+          const long long hr0_ = __shfl(hrun_, 0, 64);
+          const bool hmg_ = tcr_ == hr0_;
+          const bool hol_ = hmg_ ? tco_ : (tcr_ < 0);
+          const bool hq0 = hok && true;
+          double hv0 = hq0 ? (double)((a.A0_0 + a.B0_0 * (double)x2_c1) * (a.A0_1 + a.B0_1 * (double)x3_c1)) : 0.0;
+          #pragma unroll
+          for (int hd = 1; hd < 64; hd <<= 1) {
+            const double u_hv0 = __shfl_up(hv0, (unsigned)hd, 64);
+            if (hln - hd >= hss) {
+              hv0 = hv0 + u_hv0;
+            }
+          }
+          long long hrn_ = (long long)(hln - hss + 1);
+          if (hmg_ && hss == 0) { hrn_ += tcn_; hv0 += tcv0; }
+          const bool hopen_ = hss == 0 && hol_;
+          const bool hlst_ = htl && hln == hlast_;
+          const bool hcomp = htl && !hlst_ && !hopen_;
+          const bool hprb_ = htl && !hlst_ && hopen_;
+          const double tkv_ = (hv0);
+          u64 hk = 0ull; bool hnul = false;
+          if (hprb_) {
+            const int w0_KK = a.c0[crow1];
+            const int r0_KK = (int)w0_KK;
+            const long long x0_KK = (long long)(a.B0 + (i64)w0_KK);
+            u64 hk_l = 0ull; const bool hk_l_nul = false;
+            hk_l |= (u64)((i64)x0_KK - a.HL0) << (unsigned)a.HS0;
+            hk = hk_l; hnul = hk_l_nul; }
+          if (hprb_) {
+            long long hs_ = -1;
+            if (hnul) hs_ = a.HM + 1; else if (hk == ~0ull) hs_ = a.HM; else {
+              u64 hh = hs_mix64(hk) & (u64)(a.HM - 1);
+              for (int pr_ = 0; pr_ < 512; ++pr_) {
+                const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hk);
+                if (pv_ == ~0ull || pv_ == hk) { hs_ = (long long)hh; break; }
+                hh = (hh + 1ull) & (u64)(a.HM - 1);
+              }
+              if (hs_ < 0) a.hflag[0] = 1;
+            }
+            if (hs_ >= 0) {
+              const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
+              const unsigned long long hrn = (unsigned long long)hrn_;
+              unsafeAtomicAdd(&a.hsum[0 * hst + hs_], hv0);
+              if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
+            }
+          }
+          if (hcomp) {
+            if (tkv_ > tkv1) {
+              tkdmx = fmax(tkdmx, tkv1);
+              if (tkv_ > tkv0) { tkr1 = tkr0; tkv1 = tkv0; tks1_0 = tks0_0; tkc1_0 = tkc0_0; tks1_1 = tks0_1; tkc1_1 = tkc0_1; tkr0 = crow1; tkv0 = tkv_; tks0_0 = (double)(hv0); tkc0_0 = (long long)(0ll); tks0_1 = (double)(0.0); tkc0_1 = (long long)(0ll); } else { tkr1 = crow1; tkv1 = tkv_; tks1_0 = (double)(hv0); tkc1_0 = (long long)(0ll); tks1_1 = (double)(0.0); tkc1_1 = (long long)(0ll); }
+            } else { tkdmx = fmax(tkdmx, tkv_); }
+          }
+          if (tcr_ >= 0 && !hmg_) {
+            const bool hce_ = hln == 0;
+            const bool hct_ = hce_ && !tco_;
+            const bool hcp_ = hce_ && tco_;
+            const double tcv_ = (tcv0);
+            u64 hck_ = 0ull; bool hcn_ = false;
+            if (hcp_) {
+              const int w0_KK = a.c0[tcw_];
+              const int r0_KK = (int)w0_KK;
+              const long long x0_KK = (long long)(a.B0 + (i64)w0_KK);
+              u64 hk_l = 0ull; const bool hk_l_nul = false;
+              hk_l |= (u64)((i64)x0_KK - a.HL0) << (unsigned)a.HS0;
+              hck_ = hk_l; hcn_ = hk_l_nul; }
+            if (hcp_) {
+              long long hs_ = -1;
+              if (hcn_) hs_ = a.HM + 1; else if (hck_ == ~0ull) hs_ = a.HM; else {
+                u64 hh = hs_mix64(hck_) & (u64)(a.HM - 1);
+                for (int pr_ = 0; pr_ < 512; ++pr_) {
+                  const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hck_);
+                  if (pv_ == ~0ull || pv_ == hck_) { hs_ = (long long)hh; break; }
+                  hh = (hh + 1ull) & (u64)(a.HM - 1);
+                }
+                if (hs_ < 0) a.hflag[0] = 1;
+              }
+              if (hs_ >= 0) {
+                const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
+                const unsigned long long hrn = (unsigned long long)tcn_;
+                unsafeAtomicAdd(&a.hsum[0 * hst + hs_], tcv0);
+                if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
+              }
+            }
+            if (hct_) {
+              if (tcv_ > tkv1) {
+                tkdmx = fmax(tkdmx, tkv1);
+                if (tcv_ > tkv0) { tkr1 = tkr0; tkv1 = tkv0; tks1_0 = tks0_0; tkc1_0 = tkc0_0; tks1_1 = tks0_1; tkc1_1 = tkc0_1; tkr0 = tcw_; tkv0 = tcv_; tks0_0 = (double)(tcv0); tkc0_0 = (long long)(0ll); tks0_1 = (double)(0.0); tkc0_1 = (long long)(0ll); } else { tkr1 = tcw_; tkv1 = tcv_; tks1_0 = (double)(tcv0); tkc1_0 = (long long)(0ll); tks1_1 = (double)(0.0); tkc1_1 = (long long)(0ll); }
+              } else { tkdmx = fmax(tkdmx, tcv_); }
+            }
+          }
+          tcr_ = __shfl(hrun_, hlast_, 64);
+          tco_ = __shfl(hopen_ ? 1 : 0, hlast_, 64) != 0;
+          tcw_ = __shfl((long long)(crow1), hlast_, 64);
+          tcn_ = __shfl(hrn_, hlast_, 64);
+          tcv0 = __shfl(hv0, hlast_, 64);
+        }
+      }
+      }
+      { bool cok = cok2;
+      { const int hln = (int)(threadIdx.x & 63u); const bool hok = cok;
+        const u64 hV_ = __ballot(hok);
+        if (hV_ != 0ull) {
+          const unsigned hsg = (unsigned)crn2;
+          const unsigned hsp = __shfl_up(hsg, 1u, 64);
+          const int hfp = __shfl_up(hok ? 1 : 0, 1u, 64);
+          const bool hsame = hln > 0 && hok && hfp != 0 && hsp == hsg;
+          const u64 hH = __ballot(!hsame);
+          const int hss = 63 - __builtin_clzll(hH & ((2ull << hln) - 1ull));
+          const bool htl = hok && (hln == 63 || ((hH >> ((hln + 1) & 63)) & 1ull) != 0ull);
+          const int hlast_ = 63 - __builtin_clzll(hV_);
+          const long long hrun_ = hok ? (long long)(qb_ + (i64)crn2) : -1ll;
+          const long long hr0_ = __shfl(hrun_, 0, 64);
+          const bool hmg_ = tcr_ == hr0_;
+          const bool hol_ = hmg_ ? tco_ : (tcr_ < 0);
+          const bool hq0 = hok && true;
+          double hv0 = hq0 ? (double)((a.A0_0 + a.B0_0 * (double)x2_c2) * (a.A0_1 + a.B0_1 * (double)x3_c2)) : 0.0;
+          #pragma unroll
+          for (int hd = 1; hd < 64; hd <<= 1) {
+            const double u_hv0 = __shfl_up(hv0, (unsigned)hd, 64);
+            if (hln - hd >= hss) {
+              hv0 = hv0 + u_hv0;
+            }
+          }
+          long long hrn_ = (long long)(hln - hss + 1);
+          if (hmg_ && hss == 0) { hrn_ += tcn_; hv0 += tcv0; }
+          const bool hopen_ = hss == 0 && hol_;
+          const bool hlst_ = htl && hln == hlast_;
+          const bool hcomp = htl && !hlst_ && !hopen_;
+          const bool hprb_ = htl && !hlst_ && hopen_;
+          const double tkv_ = (hv0);
+          u64 hk = 0ull; bool hnul = false;
+          if (hprb_) {
+            const int w0_KK = a.c0[crow2];
+            const int r0_KK = (int)w0_KK;
+            const long long x0_KK = (long long)(a.B0 + (i64)w0_KK);
+            u64 hk_l = 0ull; const bool hk_l_nul = false;
+            hk_l |= (u64)((i64)x0_KK - a.HL0) << (unsigned)a.HS0;
+            hk = hk_l; hnul = hk_l_nul; }
+          if (hprb_) {
+            long long hs_ = -1;
+            if (hnul) hs_ = a.HM + 1; else if (hk == ~0ull) hs_ = a.HM; else {
+              u64 hh = hs_mix64(hk) & (u64)(a.HM - 1);
+              for (int pr_ = 0; pr_ < 512; ++pr_) {
+                const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hk);
+                if (pv_ == ~0ull || pv_ == hk) { hs_ = (long long)hh; break; }
+                hh = (hh + 1ull) & (u64)(a.HM - 1);
+              }
+              if (hs_ < 0) a.hflag[0] = 1;
+            }
+            if (hs_ >= 0) {
+              const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
+              const unsigned long long hrn = (unsigned long long)hrn_;
+              unsafeAtomicAdd(&a.hsum[0 * hst + hs_], hv0);
+              if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
+            }
+          }
+          if (hcomp) {
+            if (tkv_ > tkv1) {
+              tkdmx = fmax(tkdmx, tkv1);
+              if (tkv_ > tkv0) { tkr1 = tkr0; tkv1 = tkv0; tks1_0 = tks0_0; tkc1_0 = tkc0_0; tks1_1 = tks0_1; tkc1_1 = tkc0_1; tkr0 = crow2; tkv0 = tkv_; tks0_0 = (double)(hv0); tkc0_0 = (long long)(0ll); tks0_1 = (double)(0.0); tkc0_1 = (long long)(0ll); } else { tkr1 = crow2; tkv1 = tkv_; tks1_0 = (double)(hv0); tkc1_0 = (long long)(0ll); tks1_1 = (double)(0.0); tkc1_1 = (long long)(0ll); }
+            } else { tkdmx = fmax(tkdmx, tkv_); }
+          }
+          if (tcr_ >= 0 && !hmg_) {
+            const bool hce_ = hln == 0;
+            const bool hct_ = hce_ && !tco_;
+            const bool hcp_ = hce_ && tco_;
+            const double tcv_ = (tcv0);
+            u64 hck_ = 0ull; bool hcn_ = false;
+            if (hcp_) {
+              const int w0_KK = a.c0[tcw_];
+              const int r0_KK = (int)w0_KK;
+              const long long x0_KK = (long long)(a.B0 + (i64)w0_KK);
+              u64 hk_l = 0ull; const bool hk_l_nul = false;
+              hk_l |= (u64)((i64)x0_KK - a.HL0) << (unsigned)a.HS0;
+              hck_ = hk_l; hcn_ = hk_l_nul; }
+            if (hcp_) {
+              long long hs_ = -1;
+              if (hcn_) hs_ = a.HM + 1; else if (hck_ == ~0ull) hs_ = a.HM; else {
+                u64 hh = hs_mix64(hck_) & (u64)(a.HM - 1);
+                for (int pr_ = 0; pr_ < 512; ++pr_) {
+                  const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hck_);
+                  if (pv_ == ~0ull || pv_ == hck_) { hs_ = (long long)hh; break; }
+                  hh = (hh + 1ull) & (u64)(a.HM - 1);
+                }
+                if (hs_ < 0) a.hflag[0] = 1;
+              }
+              if (hs_ >= 0) {
+                const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
+                const unsigned long long hrn = (unsigned long long)tcn_;
+                unsafeAtomicAdd(&a.hsum[0 * hst + hs_], tcv0);
+                if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
+              }
+            }
+            if (hct_) {
+              if (tcv_ > tkv1) {
+                tkdmx = fmax(tkdmx, tkv1);
+                if (tcv_ > tkv0) { tkr1 = tkr0; tkv1 = tkv0; tks1_0 = tks0_0; tkc1_0 = tkc0_0; tks1_1 = tks0_1; tkc1_1 = tkc0_1; tkr0 = tcw_; tkv0 = tcv_; tks0_0 = (double)(tcv0); tkc0_0 = (long long)(0ll); tks0_1 = (double)(0.0); tkc0_1 = (long long)(0ll); } else { tkr1 = tcw_; tkv1 = tcv_; tks1_0 = (double)(tcv0); tkc1_0 = (long long)(0ll); tks1_1 = (double)(0.0); tkc1_1 = (long long)(0ll); }
+              } else { tkdmx = fmax(tkdmx, tcv_); }
+            }
+          }
+          tcr_ = __shfl(hrun_, hlast_, 64);
+          tco_ = __shfl(hopen_ ? 1 : 0, hlast_, 64) != 0;
+          tcw_ = __shfl((long long)(crow2), hlast_, 64);
+          tcn_ = __shfl(hrn_, hlast_, 64);
+          tcv0 = __shfl(hv0, hlast_, 64);
+        }
+      }
+      }
+      { bool cok = cok3;
+      { const int hln = (int)(threadIdx.x & 63u); const bool hok = cok;
+        const u64 hV_ = __ballot(hok);
+        if (hV_ != 0ull) {
+          const unsigned hsg = (unsigned)crn3;
+          const unsigned hsp = __shfl_up(hsg, 1u, 64);
+          const int hfp = __shfl_up(hok ? 1 : 0, 1u, 64);
+          const bool hsame = hln > 0 && hok && hfp != 0 && hsp == hsg;
+          const u64 hH = __ballot(!hsame);
+          const int hss = 63 - __builtin_clzll(hH & ((2ull << hln) - 1ull));
+          const bool htl = hok && (hln == 63 || ((hH >> ((hln + 1) & 63)) & 1ull) != 0ull);
+          const int hlast_ = 63 - __builtin_clzll(hV_);
+          const long long hrun_ = hok ? (long long)(qb_ + (i64)crn3) : -1ll;
+          const long long hr0_ = __shfl(hrun_, 0, 64);
+          const bool hmg_ = tcr_ == hr0_;
+          const bool hol_ = hmg_ ? tco_ : (tcr_ < 0);
+          const bool hq0 = hok && true;
+          double hv0 = hq0 ? (double)((a.A0_0 + a.B0_0 * (double)x2_c3) * (a.A0_1 + a.B0_1 * (double)x3_c3)) : 0.0;
+          #pragma unroll
+          for (int hd = 1; hd < 64; hd <<= 1) {
+            const double u_hv0 = __shfl_up(hv0, (unsigned)hd, 64);
+            if (hln - hd >= hss) {
+              hv0 = hv0 + u_hv0;
+            }
+          }
+          long long hrn_ = (long long)(hln - hss + 1);
+          if (hmg_ && hss == 0) { hrn_ += tcn_; hv0 += tcv0; }
+          const bool hopen_ = hss == 0 && hol_;
+          const bool hlst_ = htl && hln == hlast_;
+          const bool hcomp = htl && !hlst_ && !hopen_;
+          const bool hprb_ = htl && !hlst_ && hopen_;
+          const double tkv_ = (hv0);
+          u64 hk = 0ull; bool hnul = false;
+          if (hprb_) {
+            const int w0_KK = a.c0[crow3];
+            const int r0_KK = (int)w0_KK;
+            const long long x0_KK = (long long)(a.B0 + (i64)w0_KK);
+            u64 hk_l = 0ull; const bool hk_l_nul = false;
+            hk_l |= (u64)((i64)x0_KK - a.HL0) << (unsigned)a.HS0;
+            hk = hk_l; hnul = hk_l_nul; }
+          if (hprb_) {
+            long long hs_ = -1;
+            if (hnul) hs_ = a.HM + 1; else if (hk == ~0ull) hs_ = a.HM; else {
+              u64 hh = hs_mix64(hk) & (u64)(a.HM - 1);
+              for (int pr_ = 0; pr_ < 512; ++pr_) {
+                const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hk);
+                if (pv_ == ~0ull || pv_ == hk) { hs_ = (long long)hh; break; }
+                hh = (hh + 1ull) & (u64)(a.HM - 1);
+              }
+              if (hs_ < 0) a.hflag[0] = 1;
+            }
+            if (hs_ >= 0) {
+              const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
+              const unsigned long long hrn = (unsigned long long)hrn_;
+              unsafeAtomicAdd(&a.hsum[0 * hst + hs_], hv0);
+              if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
+            }
+          }
+          if (hcomp) {
+            if (tkv_ > tkv1) {
+              tkdmx = fmax(tkdmx, tkv1);
+              if (tkv_ > tkv0) { tkr1 = tkr0; tkv1 = tkv0; tks1_0 = tks0_0; tkc1_0 = tkc0_0; tks1_1 = tks0_1; tkc1_1 = tkc0_1; tkr0 = crow3; tkv0 = tkv_; tks0_0 = (double)(hv0); tkc0_0 = (long long)(0ll); tks0_1 = (double)(0.0); tkc0_1 = (long long)(0ll); } else { tkr1 = crow3; tkv1 = tkv_; tks1_0 = (double)(hv0); tkc1_0 = (long long)(0ll); tks1_1 = (double)(0.0); tkc1_1 = (long long)(0ll); }
+            } else { tkdmx = fmax(tkdmx, tkv_); }
+          }
+          if (tcr_ >= 0 && !hmg_) {
+            const bool hce_ = hln == 0;
+            const bool hct_ = hce_ && !tco_;
+            const bool hcp_ = hce_ && tco_;
+            const double tcv_ = (tcv0);
+            u64 hck_ = 0ull; bool hcn_ = false;
+            if (hcp_) {
+              const int w0_KK = a.c0[tcw_];
+              const int r0_KK = (int)w0_KK;
+              const long long x0_KK = (long long)(a.B0 + (i64)w0_KK);
+              u64 hk_l = 0ull; const bool hk_l_nul = false;
+              hk_l |= (u64)((i64)x0_KK - a.HL0) << (unsigned)a.HS0;
+              hck_ = hk_l; hcn_ = hk_l_nul; }
+            if (hcp_) {
+              long long hs_ = -1;
+              if (hcn_) hs_ = a.HM + 1; else if (hck_ == ~0ull) hs_ = a.HM; else {
+                u64 hh = hs_mix64(hck_) & (u64)(a.HM - 1);
+                for (int pr_ = 0; pr_ < 512; ++pr_) {
+                  const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hck_);
+                  if (pv_ == ~0ull || pv_ == hck_) { hs_ = (long long)hh; break; }
+                  hh = (hh + 1ull) & (u64)(a.HM - 1);
+                }
+                if (hs_ < 0) a.hflag[0] = 1;
+              }
+              if (hs_ >= 0) {
+                const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
+                const unsigned long long hrn = (unsigned long long)tcn_;
+                unsafeAtomicAdd(&a.hsum[0 * hst + hs_], tcv0);
+                if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
+              }
+            }
+            if (hct_) {
+              if (tcv_ > tkv1) {
+                tkdmx = fmax(tkdmx, tkv1);
+                if (tcv_ > tkv0) { tkr1 = tkr0; tkv1 = tkv0; tks1_0 = tks0_0; tkc1_0 = tkc0_0; tks1_1 = tks0_1; tkc1_1 = tkc0_1; tkr0 = tcw_; tkv0 = tcv_; tks0_0 = (double)(tcv0); tkc0_0 = (long long)(0ll); tks0_1 = (double)(0.0); tkc0_1 = (long long)(0ll); } else { tkr1 = tcw_; tkv1 = tcv_; tks1_0 = (double)(tcv0); tkc1_0 = (long long)(0ll); tks1_1 = (double)(0.0); tkc1_1 = (long long)(0ll); }
+              } else { tkdmx = fmax(tkdmx, tcv_); }
+            }
+          }
+          tcr_ = __shfl(hrun_, hlast_, 64);
+          tco_ = __shfl(hopen_ ? 1 : 0, hlast_, 64) != 0;
+          tcw_ = __shfl((long long)(crow3), hlast_, 64);
+          tcn_ = __shfl(hrn_, hlast_, 64);
+          tcv0 = __shfl(hv0, hlast_, 64);
+        }
+      }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  if (tcr_ >= 0) {
+    const int hln = (int)(threadIdx.x & 63u);
+    const bool hcp_ = hln == 0;
+    u64 hck_ = 0ull; bool hcn_ = false;
+    if (hcp_) {
+      const int w0_KK = a.c0[tcw_];
+      const int r0_KK = (int)w0_KK;
+      const long long x0_KK = (long long)(a.B0 + (i64)w0_KK);
+      u64 hk_l = 0ull; const bool hk_l_nul = false;
+      hk_l |= (u64)((i64)x0_KK - a.HL0) << (unsigned)a.HS0;
+      hck_ = hk_l; hcn_ = hk_l_nul; }
+    if (hcp_) {
+      long long hs_ = -1;
+      if (hcn_) hs_ = a.HM + 1; else if (hck_ == ~0ull) hs_ = a.HM; else {
+        u64 hh = hs_mix64(hck_) & (u64)(a.HM - 1);
+        for (int pr_ = 0; pr_ < 512; ++pr_) {
+          const u64 pv_ = atomicCAS(&a.hkeys[hh], ~0ull, hck_);
+          if (pv_ == ~0ull || pv_ == hck_) { hs_ = (long long)hh; break; }
+          hh = (hh + 1ull) & (u64)(a.HM - 1);
+        }
+        if (hs_ < 0) a.hflag[0] = 1;
+      }
+      if (hs_ >= 0) {
+        const long long hst = a.HM + 2;   // SoA: aggregate i of slot s at i * (M + 2) + s
+        const unsigned long long hrn = (unsigned long long)tcn_;
+        unsafeAtomicAdd(&a.hsum[0 * hst + hs_], tcv0);
+        if (hs_ >= a.HM) atomicAdd((unsigned long long*)&a.hcnt[1 * hst + hs_], hrn);
+      }
+    }
+  }
+  { const int tl_ = (int)(threadIdx.x & 63u);
+    const u64 tki0 = (u64)hs_dimg(tkv0) ^ 0x8000000000000000ull; const u64 tki1 = (u64)hs_dimg(tkv1) ^ 0x8000000000000000ull;
+    u64 th_ = 0ull;
+    for (int b_ = 63; b_ >= 0; --b_) { const u64 t_ = th_ | (1ull << b_);
+      if (__popcll(__ballot(tki0 >= t_)) + __popcll(__ballot(tki1 >= t_)) >= 16) th_ = t_; }
+    // th_: the K-th best image (0 when fewer than K entries are live)
+    double dm_ = tkdmx;
+    long long pos_ = 0;
+    { const bool lv_ = tkr0 >= 0 && tki0 >= th_;
+      const u64 lb_ = __ballot(lv_);
+      const long long at_ = pos_ + __popcll(lb_ & ((1ull << tl_) - 1ull));
+      if (lv_ && at_ < 16) {
+        const long long te_ = (long long)(wid) * 16 + at_;
+        const int w0_F = a.c0[tkr0];
+        const int r0_F = (int)w0_F;
+        const long long x0_F = (long long)(a.B0 + (i64)w0_F);
+        u64 tkey_l = 0ull; const bool tkey_l_nul = false;
+        tkey_l |= (u64)((i64)x0_F - a.HL0) << (unsigned)a.HS0;
+        const u64 tkey_ = tkey_l;
+        a.TKK[te_] = tkey_; a.TKV[te_] = (long long)~tki0;
+        a.TKS[0 * a.TKCAP + te_] = tks0_0; a.TKC[0 * a.TKCAP + te_] = tkc0_0;
+        a.TKS[1 * a.TKCAP + te_] = tks0_1; a.TKC[1 * a.TKCAP + te_] = tkc0_1;
+      } else if (tkr0 >= 0) dm_ = fmax(dm_, tkv0);
+      pos_ += __popcll(lb_); }
+    { const bool lv_ = tkr1 >= 0 && tki1 >= th_;
+      const u64 lb_ = __ballot(lv_);
+      const long long at_ = pos_ + __popcll(lb_ & ((1ull << tl_) - 1ull));
+      if (lv_ && at_ < 16) {
+        const long long te_ = (long long)(wid) * 16 + at_;
+        const int w0_F = a.c0[tkr1];
+        const int r0_F = (int)w0_F;
+        const long long x0_F = (long long)(a.B0 + (i64)w0_F);
+        u64 tkey_l = 0ull; const bool tkey_l_nul = false;
+        tkey_l |= (u64)((i64)x0_F - a.HL0) << (unsigned)a.HS0;
+        const u64 tkey_ = tkey_l;
+        a.TKK[te_] = tkey_; a.TKV[te_] = (long long)~tki1;
+        a.TKS[0 * a.TKCAP + te_] = tks1_0; a.TKC[0 * a.TKCAP + te_] = tkc1_0;
+        a.TKS[1 * a.TKCAP + te_] = tks1_1; a.TKC[1 * a.TKCAP + te_] = tkc1_1;
+      } else if (tkr1 >= 0) dm_ = fmax(dm_, tkv1);
+      pos_ += __popcll(lb_); }
+    for (long long e_ = pos_ + tl_; e_ < 16; e_ += 64) {
+      const long long te_ = (long long)(wid) * 16 + e_;
+      a.TKK[te_] = ~0ull; a.TKV[te_] = (long long)~((u64)hs_dimg(-__builtin_inf()) ^ 0x8000000000000000ull); }
+    for (int o_ = 32; o_ > 0; o_ >>= 1) dm_ = fmax(dm_, __shfl_xor(dm_, o_, 64));
+    if (tl_ == 0) {
+      a.TKW[wid] = pos_ >= 16 ? (long long)(th_ ^ 0x8000000000000000ull) : hs_dimg(-__builtin_inf());
+      a.TKD[wid] = hs_dimg(dm_); }
+  }
+}

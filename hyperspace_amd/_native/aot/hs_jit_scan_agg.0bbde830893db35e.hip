@@ -57,6 +57,14 @@ __device__ __forceinline__ void lds_max(double* p, double v) {
   do { as = old; if (__longlong_as_double((i64)as) >= v) break;
        old = atomicCAS(a, as, (u64)__double_as_longlong(v)); } while (as != old);
 }
+// order-preserving signed image of a double (top-K thresholds published with atomicMax)
+__device__ __forceinline__ long long hs_dimg(double d) {
+  const long long u = __double_as_longlong(d);
+  return u >= 0 ? u : u ^ 0x7fffffffffffffffll;
+}
+__device__ __forceinline__ double hs_dimg_inv(long long i) {
+  return __longlong_as_double(i >= 0 ? i : i ^ 0x7fffffffffffffffll);
+}
 // hash-mode grouping (exec/hash_agg.py, csrc/kernels/hash_agg.hip): probe hash and the bit
 // images of float group keys (-0.0 -> 0.0, one NaN)
 __device__ __forceinline__ u64 hs_mix64(u64 h) {
@@ -101,8 +109,7 @@ struct Args {
   double A0_1;
   double B0_1;
 };
-extern "C" __global__ __launch_bounds__(256) void hs_jit_scan_agg(const Args* __restrict__ ap) {
-  const Args a = *ap;
+extern "C" __global__ __launch_bounds__(256) void hs_jit_scan_agg(Args a) {
   typedef unsigned short crow_t; __shared__ crow_t crow_s[4][512];
   const int cln = threadIdx.x & 63, wv = threadIdx.x >> 6;
   constexpr int NA = 2;
