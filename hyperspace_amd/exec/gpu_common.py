@@ -447,6 +447,39 @@ class _JoinPrep:
         return (out, None, None, None, *self.gtail)
 
 
+class _HashPrep:
+    """Literal-independent setup of a hash-mode join aggregate (GpuBackend._hash_agg): the
+    co-partitioned relations, functional-dependency grouping, group domains and top-K request,
+    plus per literal vector the lowering ``_join_hash_pair`` made (join parameters, hash key
+    plan, ranges) - the plan cache binds a query's literals into the same Literal nodes of the
+    cached plan, so their values key it."""
+    __slots__ = ("final", "order", "limit", "node", "tables", "setup", "placement", "epoch",
+                 "lits", "lowered")
+
+    def __init__(self, final, order, limit, node, tables, setup, placement, epoch):
+        self.final, self.order, self.limit, self.node = final, order, limit, node
+        self.tables, self.setup, self.placement, self.epoch = tables, setup, placement, epoch
+        left, right = setup[0], setup[1]
+        conds = list(left.conds if left is not None else []) + \
+            list(right.conds if right is not None else []) + \
+            ([node.condition] if getattr(node, "condition", None) is not None else [])
+        self.lits = _literals(conds + list(final.aggregates))
+        self.lowered: Dict[tuple, tuple] = {}
+
+    def literal_key(self, extra=None):
+        try:
+            k = (tuple(x.value for x in self.lits), extra)
+            hash(k)
+            return k
+        except TypeError:
+            return None
+
+    def keep_lowered(self, key, low) -> None:
+        if len(self.lowered) >= 1024:
+            self.lowered.clear()
+        self.lowered[key] = low
+
+
 class _AggProgram:
     """Prepared re-submission of a fused aggregate plan (GpuBackend._register_program): a
     plan-cache hit binds its literals into the cached plan's nodes and the program replays the

@@ -15,7 +15,7 @@ from ..utils.conf import HyperspaceConf
 from ..utils.tracing import stage
 from . import compile as CP, jit
 from .arrow_eval import key
-from .gpu_common import (_eval_vec, _fd_columns, _finalize_array, _gather_tables, DRel, H_TOPK_K,
+from .gpu_common import (_HashPrep, _eval_vec, _fd_columns, _finalize_array, _gather_tables, DRel, H_TOPK_K,
                          TOPK_MIN_GROUPS, Unsupported)
 
 
@@ -42,34 +42,47 @@ class HashAggOps:
         while isinstance(node, X.ProjectExec) and \
                 all(isinstance(e, E.Attribute) for e in node.project_list):
             node = node.child
-        fd = None
-        if isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner":
-            left, right, lk, rk = self._join_inputs(node)
-            lparts, rparts = left.parts or [left], right.parts or [right]
-            rels = lparts + rparts
-            launches = [("join", lp, rp) for lp in lparts for rp in rparts]
-            fd = self._fd_grouping(final, grouping, left, right, lk, rk, order, limit)
-            if fd is not None:
-                grouping = fd[0]
+        # a plan-cache hit re-submits the same plan nodes with new literals: the relations,
+        # grouping, domains and top-K request are kept per aggregate node (``_HashPrep``), and
+        # the lowering of each literal vector (join parameters, key plan, ranges) with them
+        prep = self._hash_prep_get(final, order, limit)
+        if prep is not None:
+            (left, right, lk, rk, rels, launches, fd, grouping, doms, A, minmax, shape_key, est,
+             tk_req) = prep.setup
         else:
-            r = self._rel(child)
-            rels = r.parts or [r]
-            launches = [("scan", x, None) for x in rels]
-        doms = {g.expr_id: self._union_domain(rels, g) for g in grouping}
-        A = len(fns) + 1
-        minmax = any(isinstance(fn, (E.Min, E.Max)) for fn in fns)
-        shape_key = (tuple(g.name for g in grouping), tuple(fn.sql() for fn in fns),
-                     tuple(id(x.table) for x in rels))
-        est = min(sum(x.table.num_rows or 0 for x in rels), 1 << 40)
-        span = 1
-        for g in grouping:
-            span *= max(1, doms[g.expr_id][1]) + 1 if doms[g.expr_id][1] else (1 << 32)
-        est = max(1, min(est, span))
+            fd = None
+            left = right = lk = rk = None
+            if isinstance(node, X.SortMergeJoinExec) and node.join_type == "inner":
+                left, right, lk, rk = self._join_inputs(node)
+                lparts, rparts = left.parts or [left], right.parts or [right]
+                rels = lparts + rparts
+                launches = [("join", lp, rp) for lp in lparts for rp in rparts]
+                fd = self._fd_grouping(final, grouping, left, right, lk, rk, order, limit)
+                if fd is not None:
+                    grouping = fd[0]
+            else:
+                r = self._rel(child)
+                rels = r.parts or [r]
+                launches = [("scan", x, None) for x in rels]
+            doms = {g.expr_id: self._union_domain(rels, g) for g in grouping}
+            A = len(fns) + 1
+            minmax = any(isinstance(fn, (E.Min, E.Max)) for fn in fns)
+            shape_key = (tuple(g.name for g in grouping), tuple(fn.sql() for fn in fns),
+                         tuple(id(x.table) for x in rels))
+            est = min(sum(x.table.num_rows or 0 for x in rels), 1 << 40)
+            span = 1
+            for g in grouping:
+                span *= max(1, doms[g.expr_id][1]) + 1 if doms[g.expr_id][1] else (1 << 32)
+            est = max(1, min(est, span))
+            # ORDER BY <sum / count> LIMIT k over the key-run hash walk: whole keys compete in
+            # the walk's per-wavefront top-K lists and only split keys use the table (TopKPlan)
+            tk_req = self._topk_request(final, fns, order, limit, minmax) \
+                if fd is not None else None
+            prep = self._hash_prep_put(final, order, limit, node, launches, (
+                left, right, lk, rk, rels, launches, fd, grouping, doms, A, minmax, shape_key,
+                est, tk_req))
         hk_box: list = []
         tk_box: list = []
-        # ORDER BY <sum / count> LIMIT k over the key-run hash walk: whole keys compete in the
-        # walk's per-wavefront top-K lists and only split keys use the table (TopKPlan)
-        tk_req = self._topk_request(final, fns, order, limit, minmax) if fd is not None else None
 
         def run(M: int, use_tk: bool = True):
             table = self.htables.get(M, A, minmax, self.device)
@@ -78,7 +91,8 @@ class HashAggOps:
                 for kind, a, b in launches:
                     if kind == "join":
                         self._join_hash_pair(node, a, b, lk, rk, fns, grouping, doms, table, hk_box,
-                                             tk_req=tk_req if use_tk else None, tk_box=tk_box)
+                                             tk_req=tk_req if use_tk else None, tk_box=tk_box,
+                                             prep=prep)
                     else:
                         self._scan_hash(a, fns, grouping, doms, table, hk_box)
             with stage("hagg.extract"):
@@ -441,8 +455,56 @@ class HashAggOps:
             host["fd"] = r["fd"]
         return "ok", host, r["G"]
 
+    def _hash_prep_get(self, final, order, limit):
+        """The kept setup of a hash-mode aggregate node submitted before, while its tables are
+        resident (``_HashPrep``), or None."""
+        hp = self.__dict__.get("_hash_preps", {}).get(id(final))
+        if hp is None or hp.final is not final or hp.order is not order or hp.limit != limit \
+                or hp.placement != self._placement_tag() or hp.epoch != self.cache.epoch or \
+                not all(self._holds(t) for t in hp.tables):
+            return None
+        return hp
+
+    def _hash_prep_put(self, final, order, limit, node, launches, setup):
+        """Keep a hash-mode join aggregate's setup for its next submission: one join launch
+        over resident tables (no bucket-union parts, no computed columns)."""
+        if len(launches) != 1 or launches[0][0] != "join":
+            return None
+        _, a, b = launches[0]
+        if a.parts or b.parts or a.extra or b.extra or a.split or b.split or \
+                getattr(a.table, "_hs_cache_key", None) is None or \
+                getattr(b.table, "_hs_cache_key", None) is None:
+            return None
+        preps = self.__dict__.setdefault("_hash_preps", {})
+        if len(preps) > 64:
+            preps.clear()
+        hp = _HashPrep(final, order, limit, node, (a.table, b.table), setup,
+                       self._placement_tag(), self.cache.epoch)
+        preps[id(final)] = hp
+        return hp
+
     def _join_hash_pair(self, node, left: DRel, right: DRel, lk, rk, fns, grouping, doms,
-                        table, hk_box, tk_req=None, tk_box=None) -> None:
+                        table, hk_box, tk_req=None, tk_box=None, prep=None) -> None:
+        lkey = prep.literal_key(tk_req) if prep is not None else None
+        low = prep.lowered.get(lkey) if lkey is not None else None
+        if low is not None:
+            # this literal vector was lowered before: bind nothing, launch
+            jp, hk, nspecs, comp, rstart, rlen, rbk, left, right, lk, rk, empty = low
+            if not hk_box:
+                hk_box.append(hk)
+            if empty:
+                return
+            tk = self._topk_plan(tk_req, hk, nspecs) if tk_req is not None else None
+            if tk is not None:
+                tk.used = False
+                tk_box.append(tk)
+            fr = getattr(left.table, "_full_ranges", None)
+            with stage("join.hash_agg_kernel"):
+                jit.merge_join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, comp,
+                                   nrows=left.table.num_rows,
+                                   cache_spans=fr is not None and rstart is fr[0],
+                                   rdup=jit.key_has_dups(right.col(rk)), hk=hk, htab=table, tk=tk)
+            return
         if right.table.num_rows * 64 < left.table.num_rows:
             left, right, lk, rk = right, left, rk, lk
         implied: set = set()
@@ -468,10 +530,16 @@ class HashAggOps:
         jp.naggs = len(specs)
         if keep[0].always_false or keep[1].always_false or left.table.num_rows == 0 or \
                 right.table.num_rows == 0:
+            if lkey is not None:
+                prep.keep_lowered(lkey, (jp, hk, len(specs), None, None, None, None, left, right,
+                                         lk, rk, True))
             return
         comp = self._compacts(descs)
         if not jit.merge_join_ok(jp, comp, right.table.num_rows, left.table.num_rows):
             raise Unsupported("hash aggregate over a join the merge-join kernel cannot run")
+        if lkey is not None:
+            prep.keep_lowered(lkey, (jp, hk, len(specs), comp, rstart, rlen, rbk, left, right,
+                                     lk, rk, False))
         fr = getattr(left.table, "_full_ranges", None)
         tk = self._topk_plan(tk_req, hk, len(specs)) if tk_req is not None else None
         if tk is not None:

@@ -93,6 +93,22 @@ step_q3f() {
     --configs "$cfg" ${Q3F_ARGS} > "${O}_q3f.jsonl" 2> "${O}_q3f.log"
 }
 
+step_q3fprof() {
+  local cfg="$Q3F_CONFIGS"
+  [ -z "$cfg" ] && cfg='[{}]'
+  (cd /tmp && export TMPDIR=/tmp &&
+   timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d "${O}_q3fprof" -o run \
+     -- python3 "$REPO/scripts/qk_sweep.py" --sf ${SF:-100} --reps 20 --only-q3-full \
+     --configs "$cfg" --no-profile ${Q3F_ARGS} > "${O}_q3fprof.jsonl" 2> "${O}_q3fprof.log") \
+    || return $?
+  # the timed queries are the trace's tail (the head is data generation and index builds)
+  local f
+  f=$(find "${O}_q3fprof" -name "*kernel_trace.csv" | head -n 1)
+  python3 -c "import sys; L=open(sys.argv[1]).readlines(); open(sys.argv[2], 'w').writelines(L[:1] + L[-3000:])" \
+    "$f" "${O}_q3f_kernel_trace.csv"
+  rm -rf "${O}_q3fprof"
+}
+
 step_dist() {
   local n=${NPROC:-4}
   HS_BENCH_DIR=/tmp/hs_bench_dist HS_DIST_BACKEND=gloo timeout -k 10 700 \
