@@ -14,15 +14,20 @@ cross-rank combine.  ``value`` = whole-job queries/sec.  Data is synthetic TPC-H
 separately (three covering indexes: lineitem(l_shipdate), lineitem(l_orderkey),
 orders(o_orderkey)); ``index_build_gbps`` = decoded indexed-column bytes / build wall time;
 ``bytes_over_xgmi`` = build-shuffle bytes all ranks sent to other ranks (RCCL all-to-all).
-Queries run with two placements (``--placement``, default both; ``value`` is ALWAYS the sharded
-one):
+Queries run with two placements (``--placement``, default both; with N > 1 ``value`` is the
+replicated one and the sharded one is the side key ``sharded``; at N = 1 they coincide):
 
-* ``sharded`` (headline): each rank holds only the buckets it owns (size-balanced owner map,
-  the same for both sides of a join); every query runs on all ranks over their buckets and the
-  partial aggregates combine with one RCCL all-gather - strong scaling of ONE query stream;
-* ``replicated`` (side key ``replicated``, N > 1 only): every rank loads all buckets into its
-  HBM (the SF100 index set is ~36 GB of a 288 GB MI355X) and serves its own query stream with
-  no collective - read replicas, weak scaling.
+* ``replicated`` (headline, ``scaling: weak``): every rank loads all buckets into its HBM (the
+  SF100 index set is ~36 GB of a 288 GB MI355X) and serves its own query stream with no
+  collective - read replicas, one process per GPU, so the per-query host work (planning,
+  plan-cache binding, result assembly) runs in N processes at once.  This is how an SF100
+  index set is served: it fits one GPU many times over;
+* ``sharded`` (side key, ``scaling: strong``): each rank holds only the buckets it owns
+  (size-balanced owner map with heavy-bucket key ranges, the same for both sides of a join);
+  every query runs on all ranks over their buckets and the partial aggregates combine with one
+  RCCL all-gather - ONE query stream over N GPUs, the placement for index sets larger than one
+  GPU's HBM.  Every rank plans every query, so its rate is bounded by one process's host
+  time per query once the per-rank device time drops below it.
 
 Extra keys: ``latency`` has single-query latencies (``q3_join_ms`` = merge join,
 ``q3_join_index_ms`` = through the join index) and the cold first queries after ``createIndex``
@@ -387,8 +392,8 @@ def main():
     log(rank, f"[bench] cold first queries {cold}")
 
     from hyperspace_amd.utils.tracing import TRACER, format_report
-    # the headline (last) placement is sharded; replicated runs first as a side key
-    modes = ["replicated", "sharded"] if world > 1 and args.placement == "both" else \
+    # the headline (last) placement is replicated; sharded runs first as a side key
+    modes = ["sharded", "replicated"] if world > 1 and args.placement == "both" else \
         [args.placement if world > 1 else "sharded"]
     ji_key = "spark.hyperspace.mi.joinIndex.enabled"
     ji_run = None
