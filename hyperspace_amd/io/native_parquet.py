@@ -352,6 +352,16 @@ PHASES: Dict[str, float] = {}
 _PH_LOCK = threading.Lock()
 
 
+DMA_ALIGN = 256
+
+
+def _dma_up(n: int) -> int:
+    """``n`` rounded up to a DMA_ALIGN multiple: an H2D copy whose length or offsets are not
+    256-byte aligned runs as a blit kernel on the compute queue instead of on an SDMA engine
+    (``pq_encode._dma_span`` does the same for the encoded pages' D2H)."""
+    return -(-int(n) // DMA_ALIGN) * DMA_ALIGN
+
+
 def _phase(name: str, t0: float) -> float:
     import time
     t1 = time.perf_counter()
@@ -619,8 +629,8 @@ def upload_file_device(path: str, fields: Sequence[pa.Field], cols: Dict[str, ob
         if not plan:
             return set()
         nrg = f.num_row_groups
-        raw_cap = sum((int(L.hs_pq_chunk_raw_bytes(f.h, g, c)) + 15) // 16 * 16
-                      for _, c, _ in plan for g in range(nrg)) + 64
+        raw_cap = _dma_up(sum((int(L.hs_pq_chunk_raw_bytes(f.h, g, c)) + 15) // 16 * 16
+                              for _, c, _ in plan for g in range(nrg)) + 64)
         host_cap = sum(int(L.hs_pq_chunk_host_bound(f.h, g, c)) + 16
                        for _, c, _ in plan for g in range(nrg))
         pool = pinned_pool()
@@ -639,11 +649,16 @@ def upload_file_device(path: str, fields: Sequence[pa.Field], cols: Dict[str, ob
             sbase = scratch.data_ptr()
             # device copy of the pinned block's used parts: raw chunks at 0, host-inflated
             # pages (tag-dense pages, large dictionaries) at raw_cap
-            draw = torch.empty(raw_cap + host_used + 64, dtype=torch.uint8, device=device)
-            draw[:raw_used].copy_(pinned[:raw_used], non_blocking=True)
+            # both copies start and end on DMA_ALIGN boundaries (SDMA, not a blit kernel that
+            # would queue behind the decode waves); the padding bytes are never read
+            raw_n = min(_dma_up(raw_used), raw_cap)
+            host_n = min(_dma_up(host_used), pinned.numel() - raw_cap)
+            draw = torch.empty(raw_cap + _dma_up(host_used) + 64, dtype=torch.uint8,
+                               device=device)
+            draw[:raw_n].copy_(pinned[:raw_n], non_blocking=True)
             if host_used:
-                draw[raw_cap:raw_cap + host_used].copy_(pinned[raw_cap:raw_cap + host_used],
-                                                        non_blocking=True)
+                draw[raw_cap:raw_cap + host_n].copy_(pinned[raw_cap:raw_cap + host_n],
+                                                     non_blocking=True)
             for fld, g, p0, np_ in chunks:
                 seg = pages[p0:p0 + np_]
                 dc = cols[fld.name]

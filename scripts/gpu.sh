@@ -117,6 +117,39 @@ step_dist() {
     --buckets 16 ${DIST_ARGS} > "${O}_dist$n.json" 2> "${O}_dist$n.log"
 }
 
+step_build() {
+  timeout -k 10 600 python scripts/build_bench.py --sf ${SF:-100} --codec ${CODEC:-snappy} \
+    --repeat ${REPS:-2} > "${O}_build.jsonl" 2> "${O}_build.log"
+}
+
+step_buildprof() {
+  (cd /tmp && export TMPDIR=/tmp &&
+   timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
+     -d "${O}_buildprof" -o run -- python3 "$REPO/scripts/build_bench.py" --sf ${SF:-100} \
+     --codec ${CODEC:-snappy} > "${O}_buildprof.jsonl" 2> "${O}_buildprof.log") || return $?
+  find "${O}_buildprof" -name "*kernel_stats.csv" -exec cp {} "${O}_build_kernel_stats.csv" \;
+  find "${O}_buildprof" -name "*memory_copy_stats.csv" -exec cp {} "${O}_build_copy_stats.csv" \;
+  # blit copies (grid size ~ bytes) and the SDMA copies, with timestamps, for the timeline
+  local f
+  f=$(find "${O}_buildprof" -name "*kernel_trace.csv" | head -n 1)
+  [ -n "$f" ] && python3 -c "import sys; L=open(sys.argv[1]).readlines(); open(sys.argv[2], 'w').writelines(L[:1] + [l for l in L[1:] if 'copyBuffer' in l or 'snappy' in l or 'inflate' in l or 'gather' in l or 'rs_' in l])" "$f" "${O}_build_ktrace.csv"
+  f=$(find "${O}_buildprof" -name "*memory_copy_trace.csv" | head -n 1)
+  [ -n "$f" ] && cp "$f" "${O}_build_ctrace.csv"
+  rm -rf "${O}_buildprof"
+}
+
+step_d2hprobe() {
+  (cd /tmp && export TMPDIR=/tmp &&
+   timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
+     -d "${O}_d2h" -o run -- python3 "$REPO/scripts/diag/d2h_probe.py" \
+     > "${O}_d2hprobe.jsonl" 2> "${O}_d2hprobe.log") || return $?
+  find "${O}_d2h" -name "*kernel_stats.csv" -exec cp {} "${O}_d2h_kernel_stats.csv" \;
+  find "${O}_d2h" -name "*memory_copy_stats.csv" -exec cp {} "${O}_d2h_copy_stats.csv" \;
+  find "${O}_d2h" -name "*kernel_trace.csv" -exec cp {} "${O}_d2h_ktrace.csv" \;
+  find "${O}_d2h" -name "*memory_copy_trace.csv" -exec cp {} "${O}_d2h_ctrace.csv" \;
+  rm -rf "${O}_d2h"
+}
+
 step_cpubase() {
   timeout -k 10 840 python scripts/cpu_baseline.py --sf ${SF:-100} --threads 16 --reps ${REPS:-3} \
     --out "${O}_cpu_baseline.json" > "${O}_cpu.log" 2>&1
