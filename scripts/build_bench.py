@@ -24,6 +24,10 @@ def main():
     ap.add_argument("--index", action="append", default=None)
     ap.add_argument("--codec", default="none")
     ap.add_argument("--repeat", type=int, default=1)
+    ap.add_argument("--cprofile", action="store_true",
+                    help="main-thread cProfile of each build (top functions to stderr)")
+    ap.add_argument("--conf", action="append", default=[],
+                    help="extra session conf key=value (e.g. spark.hyperspace.mi.build.copyCUs=0)")
     args = ap.parse_args()
     import torch
     from hyperspace_amd import Hyperspace, IndexConfig, Session
@@ -37,7 +41,8 @@ def main():
     s = Session(conf={"spark.hyperspace.system.path": idx_root,
                       "spark.hyperspace.index.numBuckets": str(args.buckets),
                       "spark.hyperspace.mi.execution.device": "gpu",
-                      "spark.hyperspace.mi.index.codec": args.codec},
+                      "spark.hyperspace.mi.index.codec": args.codec,
+                      **dict(kv.split("=", 1) for kv in args.conf)},
                 warehouse_dir=os.path.join(args.data_dir, "wh"))
     hs = Hyperspace(s)
     s.backend()             # engine start outside the timed builds (as bench.py)
@@ -55,12 +60,25 @@ def main():
             if args.index and cfg.indexName not in args.index:
                 continue
             torch.cuda.synchronize()
+            prof = None
+            if args.cprofile:
+                import cProfile
+                prof = cProfile.Profile()
+                prof.enable()
             t = time.perf_counter()
             hs.createIndex(df, cfg)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t
+            if prof is not None:
+                import io
+                import pstats
+                prof.disable()
+                buf = io.StringIO()
+                pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(25)
+                print(f"[build_bench] {cfg.indexName} cProfile\n{buf.getvalue()}", file=sys.stderr)
             st = dict(device_build.LAST_BUILD_STATS)
-            print(json.dumps({"index": cfg.indexName, "rep": rep, "s": round(dt, 3),
+            print(json.dumps({"index": cfg.indexName, "rep": rep, "conf": args.conf,
+                              "s": round(dt, 3),
                               "gbps": round(st.get("source_bytes", 0) / dt / 1e9, 3),
                               "stats": st}), flush=True)
 

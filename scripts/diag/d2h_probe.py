@@ -83,6 +83,42 @@ def main():
                                 ctypes.c_void_p(side.cuda_stream))
         assert rc == 0, rc
     timeit("hipHostRegister D2H", r, n)
+    # H2D while host threads copy memory (the build's preads into pinned blocks run beside its
+    # uploads), and two H2D copies on two streams at once
+    import threading
+    import numpy as np
+    stop = threading.Event()
+    srcs = [np.ones(64 << 20, np.uint8) for _ in range(8)]
+    dsts = [np.empty(64 << 20, np.uint8) for _ in range(8)]
+
+    def churn(k):
+        while not stop.is_set():
+            np.copyto(dsts[k], srcs[k])
+    for threads in (4, 8):
+        stop.clear()
+        th = [threading.Thread(target=churn, args=(k,)) for k in range(threads)]
+        for t in th:
+            t.start()
+        timeit(f"torch_h2d_pinned with {threads} host memcpy threads",
+               lambda: src[:n].copy_(pin[:n], non_blocking=True), n)
+        stop.set()
+        for t in th:
+            t.join()
+    side2 = torch.cuda.Stream(device=dev)
+    pin2 = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    dst2 = torch.empty(n, dtype=torch.uint8, device=dev)
+
+    def two():
+        ev = torch.cuda.Event()
+        ev.record(side)
+        side2.wait_event(ev)
+        src[:n].copy_(pin[:n], non_blocking=True)
+        with torch.cuda.stream(side2):
+            dst2.copy_(pin2, non_blocking=True)
+        ev2 = torch.cuda.Event()
+        ev2.record(side2)
+        side.wait_event(ev2)
+    timeit("torch_h2d_pinned two streams at once (bytes = both)", two, 2 * n)
     torch.cuda.synchronize()
     hip.hipHostUnregister(ctypes.c_void_p(reg.data_ptr()))
     hip.hipHostFree(hp)

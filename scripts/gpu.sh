@@ -57,6 +57,26 @@ step_prof() {
   find "${O}_prof" -name "*kernel_stats.csv" -exec cp {} "${O}_kernel_stats.csv" \;
 }
 
+step_benchtrace() {
+  # kernel trace of the whole bench (name, start, end, queue, stream per dispatch); the timed
+  # steps are the run of tags / bits-scan / scan kernels after the join-index side run
+  (cd /tmp && export TMPDIR=/tmp &&
+   timeout -k 10 700 rocprofv3 --kernel-trace --output-format csv -d "${O}_btrace" -o run \
+     -- python3 "$REPO/bench.py" ${BENCH_ARGS:---sf 100 --steps 60 --warmup 5 --no-crosscheck} \
+     > "${O}_benchtrace.json" 2> "${O}_benchtrace.log") || return $?
+  local f
+  f=$(find "${O}_btrace" -name "*kernel_trace.csv" | head -n 1)
+  python3 -c "
+import csv, sys
+r = csv.DictReader(open(sys.argv[1]))
+w = csv.writer(open(sys.argv[2], 'w'))
+w.writerow(['name', 'start', 'end', 'queue', 'stream'])
+for x in r:
+    w.writerow([x['Kernel_Name'][:60], x['Start_Timestamp'], x['End_Timestamp'], x['Queue_Id'], x['Stream_Id']])
+" "$f" "${O}_bench_ktrace.csv"
+  rm -rf "${O}_btrace"
+}
+
 step_pmc() {
   local sf=${SF:-10}
   timeout -k 10 600 python3 scripts/qk_sweep.py --sf $sf --reps 3 --configs '[{}]' ${QK_ARGS} \
@@ -119,14 +139,14 @@ step_dist() {
 
 step_build() {
   timeout -k 10 600 python scripts/build_bench.py --sf ${SF:-100} --codec ${CODEC:-snappy} \
-    --repeat ${REPS:-2} > "${O}_build.jsonl" 2> "${O}_build.log"
+    --repeat ${REPS:-2} ${BUILD_ARGS} >> "${O}_build.jsonl" 2>> "${O}_build.log"
 }
 
 step_buildprof() {
   (cd /tmp && export TMPDIR=/tmp &&
    timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
      -d "${O}_buildprof" -o run -- python3 "$REPO/scripts/build_bench.py" --sf ${SF:-100} \
-     --codec ${CODEC:-snappy} > "${O}_buildprof.jsonl" 2> "${O}_buildprof.log") || return $?
+     --codec ${CODEC:-snappy} ${BUILD_ARGS} > "${O}_buildprof.jsonl" 2> "${O}_buildprof.log") || return $?
   find "${O}_buildprof" -name "*kernel_stats.csv" -exec cp {} "${O}_build_kernel_stats.csv" \;
   find "${O}_buildprof" -name "*memory_copy_stats.csv" -exec cp {} "${O}_build_copy_stats.csv" \;
   # blit copies (grid size ~ bytes) and the SDMA copies, with timestamps, for the timeline
