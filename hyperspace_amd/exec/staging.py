@@ -45,6 +45,11 @@ def copy_stream(device):
     return copy_streams(device)[0]
 
 
+# streams the H2D copies of a batched device-decode upload go through (0 = one per file, round
+# robin over copy_streams)
+UPLOAD_H2D_STREAMS = 1
+
+
 def copy_streams(device, k: int = 4) -> list:
     """``k`` staging streams per device (the box exposes 4 hardware queues per process):
     uploads of different files run their H2D copies and decode kernels concurrently."""
@@ -361,6 +366,14 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
     offs = np.concatenate([[0], np.cumsum(np.asarray(row_counts, dtype=np.int64))])
     n = int(offs[-1])
     streams = copy_streams(device)
+    batched = parquet_local is not None and native_decode_enabled() and \
+        (device_decode_enabled() if device_pages is None else device_pages) and \
+        batch_decode_bytes() > 0
+    # batched device decode: the per-file streams carry only H2D copies, so they share
+    # UPLOAD_H2D_STREAMS streams (two SDMA copies at once move 35 GB/s in total, one alone 56:
+    # profiles/d2h_probe_r5.jsonl); the batched decode runs on decode_stream
+    up_streams = [streams[k % len(streams)] for k in range(UPLOAD_H2D_STREAMS)] \
+        if batched and UPLOAD_H2D_STREAMS > 0 else streams
     cols: Dict[str, DeviceColumn] = {}
     strings: Dict[str, list] = {}
     native = parquet_local is not None and native_decode_enabled()
@@ -398,11 +411,9 @@ def upload_files(read_file: Callable[..., pa.Table], files: Sequence[str],
         _warm_decode_kernels()
         status = torch.zeros(1, dtype=torch.int32, device=device)
 
-    batched = native and use_device_pages and batch_decode_bytes() > 0
-
     def work(i: int):
         torch.cuda.set_device(device)
-        stream = streams[i % len(streams)]
+        stream = up_streams[i % len(up_streams)]
         lo, hi = int(offs[i]), int(offs[i + 1])
         done = set()
         defer = [] if batched else None

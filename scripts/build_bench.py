@@ -24,6 +24,10 @@ def main():
     ap.add_argument("--index", action="append", default=None)
     ap.add_argument("--codec", default="none")
     ap.add_argument("--repeat", type=int, default=1)
+    ap.add_argument("--h2d-streams", type=int, default=None,
+                    help="staging.UPLOAD_H2D_STREAMS for this run (0 = one stream per file)")
+    ap.add_argument("--d2h-priority", type=int, default=None,
+                    help="pq_encode.D2H_PRIORITY for this run (0 = ordinary copy streams)")
     ap.add_argument("--cprofile", action="store_true",
                     help="main-thread cProfile of each build (top functions to stderr)")
     ap.add_argument("--conf", action="append", default=[],
@@ -34,6 +38,12 @@ def main():
     from hyperspace_amd.exec import device_build
     from hyperspace_amd.models import tpch
     torch.cuda.set_device(0)
+    if args.h2d_streams is not None:
+        from hyperspace_amd.exec import staging
+        staging.UPLOAD_H2D_STREAMS = args.h2d_streams
+    if args.d2h_priority is not None:
+        from hyperspace_amd.exec import pq_encode
+        pq_encode.D2H_PRIORITY = bool(args.d2h_priority)
     nfiles = max(8, int(round(args.sf * 1.28)))
     data = os.path.join(args.data_dir, f"tpch_sf{args.sf:g}_f{nfiles}")
     tpch.generate(data, args.sf, nfiles, workers=16)
@@ -78,6 +88,7 @@ def main():
                 print(f"[build_bench] {cfg.indexName} cProfile\n{buf.getvalue()}", file=sys.stderr)
             st = dict(device_build.LAST_BUILD_STATS)
             print(json.dumps({"index": cfg.indexName, "rep": rep, "conf": args.conf,
+                              "h2d_streams": args.h2d_streams, "d2h_priority": args.d2h_priority,
                               "s": round(dt, 3),
                               "gbps": round(st.get("source_bytes", 0) / dt / 1e9, 3),
                               "stats": st}), flush=True)

