@@ -184,6 +184,11 @@ def compress_stream(device):
 
 # copy streams the index pages leave HBM on (HS_PQ_D2H_STREAMS)
 D2H_STREAMS = int(os.environ.get("HS_PQ_D2H_STREAMS", "2"))
+# Snappy pages: copy them out on the compressor's own stream.  D2H copies on this ROCm are blit
+# kernels on the CUs (profiles/d2h_probe_r5.jsonl); queued beside the compressor they waited for
+# its waves and moved ~18 GB/s (profiles/build_timeline_r5.txt), in line behind it each runs
+# alone at the link's rate
+D2H_ON_COMPRESS_STREAM = True
 # seconds of the last builds' write phases (reset by device_build per build)
 WRITE_PHASES: Dict[str, float] = {}
 _WP_LOCK = __import__("threading").Lock()
@@ -580,6 +585,8 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
     # batches alternate over D2H_STREAMS copy streams: their page copies run on separate DMA
     # queues instead of queueing behind one another
     d2h = copy_streams(device)[:max(1, D2H_STREAMS)]
+    if cid == 1 and D2H_ON_COMPRESS_STREAM:
+        d2h = [compress_stream(device)]
     for st in d2h:
         st.wait_stream(torch.cuda.current_stream(device))
     batches, cur, cur_bytes = [], [], 0

@@ -28,6 +28,8 @@ def main():
                     help="staging.UPLOAD_H2D_STREAMS for this run (0 = one stream per file)")
     ap.add_argument("--d2h-priority", type=int, default=None,
                     help="pq_encode.D2H_PRIORITY for this run (0 = ordinary copy streams)")
+    ap.add_argument("--d2h-serial", type=int, default=None,
+                    help="pq_encode.D2H_ON_COMPRESS_STREAM for this run")
     ap.add_argument("--cprofile", action="store_true",
                     help="main-thread cProfile of each build (top functions to stderr)")
     ap.add_argument("--conf", action="append", default=[],
@@ -41,6 +43,9 @@ def main():
     if args.h2d_streams is not None:
         from hyperspace_amd.exec import staging
         staging.UPLOAD_H2D_STREAMS = args.h2d_streams
+    if args.d2h_serial is not None:
+        from hyperspace_amd.exec import pq_encode
+        pq_encode.D2H_ON_COMPRESS_STREAM = bool(args.d2h_serial)
     if args.d2h_priority is not None:
         from hyperspace_amd.exec import pq_encode
         pq_encode.D2H_PRIORITY = bool(args.d2h_priority)
@@ -88,7 +93,7 @@ def main():
                 print(f"[build_bench] {cfg.indexName} cProfile\n{buf.getvalue()}", file=sys.stderr)
             st = dict(device_build.LAST_BUILD_STATS)
             print(json.dumps({"index": cfg.indexName, "rep": rep, "conf": args.conf,
-                              "h2d_streams": args.h2d_streams, "d2h_priority": args.d2h_priority,
+                              "h2d_streams": args.h2d_streams, "d2h_serial": args.d2h_serial, "d2h_priority": args.d2h_priority,
                               "s": round(dt, 3),
                               "gbps": round(st.get("source_bytes", 0) / dt / 1e9, 3),
                               "stats": st}), flush=True)
