@@ -44,12 +44,21 @@ def _spawn(scenario: str, tmp_path, data_dir: str, timeout: float = 240.0, world
         p.kill()
         p.join()
     assert not alive, f"{scenario}: ranks hung"
-    res = []
-    for r in range(world):
-        with open(out / f"rank{r}.json") as f:
+    res, errs = [], []
+    for r, p in enumerate(procs):
+        path = out / f"rank{r}.json"
+        if not path.exists():
+            errs.append(f"rank {r}: no result, exit code {p.exitcode}")
+            res.append(None)
+            continue
+        with open(path) as f:
             d = json.load(f)
-        assert "error" not in d, d["error"]
+        if "error" in d:
+            errs.append(f"rank {r} (exit code {p.exitcode}): {d['error']}")
         res.append(d)
+    # every rank's outcome, so a rank that died (signal, OOM) is named, not just the peer that
+    # saw its connection close
+    assert not errs, "\n".join(errs)
     return res
 
 
