@@ -101,16 +101,25 @@ class PinnedPool:
                 keep.append((t, ev))
         self._pending = keep
 
+    def _best_fit(self, nbytes: int):
+        best, best_n = None, 0
+        cap = max(4 * nbytes, RESERVE_BLOCK)
+        for i, t in enumerate(self._free):
+            n = t.hs_nbytes
+            if nbytes <= n <= cap and (best is None or n < best_n):
+                best, best_n = i, n
+        return best
+
     def acquire(self, nbytes: int):
         import torch
         nbytes = max(int(nbytes), 1)
         with self._lock:
-            self._reclaim()
-            best = None
-            for i, t in enumerate(self._free):
-                if nbytes <= t.numel() <= max(4 * nbytes, RESERVE_BLOCK) and \
-                        (best is None or t.numel() < self._free[best].numel()):
-                    best = i
+            # free blocks first; the event queries of the pending ones (one HIP call each,
+            # under the lock every reader thread takes) only when nothing free fits
+            best = self._best_fit(nbytes)
+            if best is None:
+                self._reclaim()
+                best = self._best_fit(nbytes)
             if best is not None:
                 return self._free.pop(best)
             size = (nbytes + (8 << 20) - 1) // (8 << 20) * (8 << 20)
@@ -119,6 +128,7 @@ class PinnedPool:
                 self._held += size
         t = torch.empty(size if pooled else nbytes, dtype=torch.uint8, pin_memory=True)
         t.hs_pooled = pooled
+        t.hs_nbytes = t.numel()
         return t
 
     def release(self, t, stream) -> None:
