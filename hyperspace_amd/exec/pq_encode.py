@@ -184,10 +184,10 @@ def compress_stream(device):
 
 # copy streams the index pages leave HBM on (HS_PQ_D2H_STREAMS)
 D2H_STREAMS = int(os.environ.get("HS_PQ_D2H_STREAMS", "2"))
-# Snappy pages: copy them out on the compressor's own stream.  D2H copies on this ROCm are blit
-# kernels on the CUs (profiles/d2h_probe_r5.jsonl); queued beside the compressor they waited for
-# its waves and moved ~18 GB/s (profiles/build_timeline_r5.txt), in line behind it each runs
-# alone at the link's rate
+# Snappy pages: copy them out on the compressor's own stream.  Issued on the copy streams the
+# D2H copies ran as blit kernels on the CUs beside the compressor's waves (~18 GB/s,
+# profiles/build_timeline_r5.txt); queued behind the compressor they run on the SDMA engines
+# (profiles/build_copy_stats_sf100_r5_d2h_serial.csv)
 D2H_ON_COMPRESS_STREAM = True
 # seconds of the last builds' write phases (reset by device_build per build)
 WRITE_PHASES: Dict[str, float] = {}
