@@ -14,20 +14,29 @@ cross-rank combine.  ``value`` = whole-job queries/sec.  Data is synthetic TPC-H
 separately (three covering indexes: lineitem(l_shipdate), lineitem(l_orderkey),
 orders(o_orderkey)); ``index_build_gbps`` = decoded indexed-column bytes / build wall time;
 ``bytes_over_xgmi`` = build-shuffle bytes all ranks sent to other ranks (RCCL all-to-all).
-Queries run with two placements (``--placement``, default both; with N > 1 ``value`` is the
-replicated one and the sharded one is the side key ``sharded``; at N = 1 they coincide):
+Queries run with two placements (``--placement``, default both; ``value`` is always the
+sharded one - ONE query stream over the N GPUs, ``scaling: strong`` at every N, so a 1->8 curve
+compares like with like - and with N > 1 the replicated one is the side key ``replicated``; at
+N = 1 they coincide).  (Round 5 reported the replicated placement as ``value`` at N > 1; from
+round 6 it is a side key again, so multi-GPU records of round 5 are not comparable.)
 
-* ``replicated`` (headline, ``scaling: weak``): every rank loads all buckets into its HBM (the
-  SF100 index set is ~36 GB of a 288 GB MI355X) and serves its own query stream with no
-  collective - read replicas, one process per GPU, so the per-query host work (planning,
-  plan-cache binding, result assembly) runs in N processes at once.  This is how an SF100
-  index set is served: it fits one GPU many times over;
-* ``sharded`` (side key, ``scaling: strong``): each rank holds only the buckets it owns
+* ``sharded`` (headline, ``scaling: strong``): each rank holds only the buckets it owns
   (size-balanced owner map with heavy-bucket key ranges, the same for both sides of a join);
   every query runs on all ranks over their buckets and the partial aggregates combine with one
-  RCCL all-gather - ONE query stream over N GPUs, the placement for index sets larger than one
-  GPU's HBM.  Every rank plans every query, so its rate is bounded by one process's host
-  time per query once the per-rank device time drops below it.
+  RCCL all-gather - the placement for index sets larger than one GPU's HBM, and BASELINE
+  config #3's bucket-parallel JoinIndexRule over RCCL.  Every rank plans every query, so its
+  rate is bounded by one process's host time per query once the per-rank device time drops
+  below it;
+* ``replicated`` (side key, ``scaling: weak``): every rank loads all buckets into its HBM (the
+  SF100 index set is ~36 GB of a 288 GB MI355X) and serves its own query stream with no
+  collective - read replicas, one process per GPU.
+
+At N = 1 two more side keys run the BASELINE configs' real query shapes through the same engine,
+each checked against the host oracle (``benchmarks/configs.py``): ``q3_3way`` (TPC-H Q3's
+customer x orders x lineitem join with the ``c_mktsegment`` filter over four covering indexes)
+and ``hybrid`` (the SF index set + 10% appended Parquet files through Hybrid Scan, then after an
+incremental refresh: ``hybrid_vs_refreshed`` = Hybrid Scan q/s / refreshed q/s).  A side key
+that fails records its error instead of stopping the headline record.
 
 Extra keys: ``latency`` has single-query latencies (``q3_join_ms`` = merge join,
 ``q3_join_index_ms`` = through the join index) and the cold first queries after ``createIndex``
@@ -137,6 +146,8 @@ def main():
     ap.add_argument("--record-baseline", action="store_true",
                     help="with --device cpu: save the JSON line as profiles/cpu_baseline_sf<SF>.json "
                          "(the vs_baseline denominator of later GPU runs)")
+    ap.add_argument("--no-side", action="store_true",
+                    help="skip the N = 1 side configs (q3_3way, hybrid)")
     ap.add_argument("--host-breakdown", type=int, default=0, metavar="N",
                     help="after the timed steps, time N queries phase by phase on the host "
                          "(DataFrame build / plan / submit / result), reported as host_breakdown")
@@ -392,8 +403,9 @@ def main():
     log(rank, f"[bench] cold first queries {cold}")
 
     from hyperspace_amd.utils.tracing import TRACER, format_report
-    # the headline (last) placement is replicated; sharded runs first as a side key
-    modes = ["sharded", "replicated"] if world > 1 and args.placement == "both" else \
+    # the headline (last) placement is sharded (one query stream over the N GPUs); replicated
+    # runs first as a side key
+    modes = ["replicated", "sharded"] if world > 1 and args.placement == "both" else \
         [args.placement if world > 1 else "sharded"]
     ji_key = "spark.hyperspace.mi.joinIndex.enabled"
     ji_run = None
@@ -453,6 +465,7 @@ def main():
     lat.update(cold)
     hb = _host_breakdown(args.host_breakdown, (q6, q3), backend, sync, barrier) \
         if args.host_breakdown and on_gpu else None
+    side = _side_configs(args, sf) if on_gpu and world == 1 and not args.no_side else {}
 
     # ---------------------------------------------------------------- cross-check
     check = None
@@ -511,6 +524,7 @@ def main():
             out["q3_full"] = q3f
         if hb is not None:
             out["host_breakdown"] = hb
+        out.update(side)
         if ji_run is not None:
             out["join_index"] = {"value": round(ji_run["qps"], 3),
                                  "ms_per_step": round(ji_run["ms_per_step"], 3),
@@ -534,6 +548,43 @@ def main():
     if dist:
         barrier()
         torch.distributed.destroy_process_group()
+
+
+def _side_configs(args, sf) -> dict:
+    """BASELINE configs #3-#4's real query shapes at N = 1, through ``benchmarks/configs.py``
+    (own sessions over the same generated data, each result checked against the host oracle
+    with Hyperspace disabled): ``q3_3way`` and ``hybrid``.  Errors are recorded, not raised."""
+    import argparse as _ap
+    import traceback
+    sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
+    import configs as CF
+    ns = _ap.Namespace(data_dir=args.data_dir, device="gpu", buckets=args.buckets,
+                       steps=max(args.steps, 10), sf=sf)
+    out = {}
+    for name, fn in (("q3_3way", CF.config_q3_3way), ("hybrid", CF.config_hybrid)):
+        t0 = time.perf_counter()
+        try:
+            r = fn(ns)
+            if name == "q3_3way":
+                out[name] = {"q3_3way_ms": r["q3_3way_ms"], "value": r["queries_per_s"],
+                             "path": r["path"], "match": r["match"],
+                             "indexes_in_plan": r["indexes_in_plan"],
+                             "semi_join": r.get("semi_join")}
+            else:
+                out[name] = {"hybrid_qps": r["hybrid_queries_per_s"],
+                             "refreshed_qps": r["refreshed_queries_per_s"],
+                             "hybrid_vs_refreshed": round(r["hybrid_queries_per_s"] /
+                                                          r["refreshed_queries_per_s"], 3),
+                             "appended_files": r["appended_files"],
+                             "incremental_refresh_s": r["incremental_refresh_s"],
+                             "path": r["path"], "match": r["hybrid_matches_refreshed"],
+                             "bucket_union_in_plan": r["bucket_union_in_plan"]}
+        except Exception as e:  # noqa: BLE001 — a side key never stops the headline record
+            out[name] = {"error": f"{type(e).__name__}: {e}",
+                         "trace": traceback.format_exc()[-1500:]}
+        out[name]["wall_s"] = round(time.perf_counter() - t0, 2)
+        print(f"[bench] side config {name}: {out[name]}", file=sys.stderr, flush=True)
+    return out
 
 
 def _host_breakdown(n, fns, backend, sync, barrier) -> dict:

@@ -18,12 +18,16 @@ from __future__ import annotations
 
 import json
 import os
+import re
 import shutil
 import threading
 from typing import Dict, List, Optional
 
 from .exceptions import HyperspaceException
 from .index import constants as C
+
+
+_IDENT = re.compile(r"^[A-Za-z_][A-Za-z0-9_]*$")
 
 
 class Catalog:
@@ -42,6 +46,13 @@ class Catalog:
     def _meta_path(self, name: str) -> str:
         return os.path.join(self._warehouse(), "_catalog", f"{name.lower()}.json")
 
+    @staticmethod
+    def _check_name(name: str) -> None:
+        """Table names are identifiers: a managed table's data directory and its catalog record
+        are built from the name, and drop / overwrite delete that directory."""
+        if not isinstance(name, str) or not _IDENT.match(name):
+            raise HyperspaceException(f"Invalid table name '{name}' (expected an identifier)")
+
     # -- temporary views ---------------------------------------------------------------------
     def create_temp_view(self, name: str, plan, replace: bool) -> None:
         with self._lock:
@@ -59,6 +70,8 @@ class Catalog:
 
     # -- tables ------------------------------------------------------------------------------
     def table_meta(self, name: str) -> Optional[dict]:
+        if not isinstance(name, str) or not _IDENT.match(name):
+            return None
         p = self._meta_path(name)
         if not os.path.exists(p):
             return None
@@ -67,6 +80,7 @@ class Catalog:
 
     def save_table(self, name: str, writer, mode: str) -> None:
         """``DataFrameWriter.saveAsTable``: write the data and record the table."""
+        self._check_name(name)
         meta = self.table_meta(name)
         if meta is not None:
             if mode in ("errorifexists", "error"):
@@ -79,6 +93,11 @@ class Catalog:
             path = os.path.join(self._warehouse(), name.lower())
         if meta is not None and mode == "overwrite" and meta.get("managed") and \
                 os.path.exists(meta["path"]):
+            if writer.reads_from(meta["path"]):
+                # e.g. spark.table('t').filter(..).write.mode('overwrite').saveAsTable('t'): the
+                # data is computed inside save, after this delete (Spark refuses it as well)
+                raise HyperspaceException(
+                    f"Cannot overwrite table '{name}' that is also being read from")
             shutil.rmtree(meta["path"])
         writer.save(path)
         os.makedirs(os.path.dirname(self._meta_path(name)), exist_ok=True)
@@ -91,6 +110,7 @@ class Catalog:
         os.replace(tmp, self._meta_path(name))
 
     def dropTable(self, name: str) -> bool:
+        self._check_name(name)
         meta = self.table_meta(name)
         if meta is None:
             return False

@@ -164,12 +164,15 @@ def plan_file_groups(rows: List[int], row_bytes: int, group_budget: int) -> List
 
 
 def _build_budget(session, device) -> int:
-    b = HyperspaceConf.build_hbm_budget_bytes(session.conf)
-    if b > 0:
-        return b
+    """The build's HBM budget: ``build.hbmBudgetBytes`` (0 = 60% of the free HBM now), capped
+    by this rank's share of the device when ranks share it (exec/hbm_budget.py)."""
     import torch
-    free, _ = torch.cuda.mem_get_info(device)
-    return int(free * 0.6)
+    from .hbm_budget import rank_budget
+    b = HyperspaceConf.build_hbm_budget_bytes(session.conf)
+    free = 0
+    if b <= 0:
+        free, _ = torch.cuda.mem_get_info(device)
+    return rank_budget(session.conf, device).build(b, free)
 
 
 def _streaming_plan(session, rel, my_files, columns, lineage_ids, num_buckets, device, world):

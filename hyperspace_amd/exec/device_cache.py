@@ -153,8 +153,8 @@ SEED_STATS = {"registered": 0, "hits": 0}
 
 
 def _seed_budget(session) -> int:
-    from ..utils.conf import HyperspaceConf
-    return HyperspaceConf.device_cache_bytes(session.conf) // 2
+    from .hbm_budget import rank_budget
+    return rank_budget(session.conf).cache // 2
 
 
 def register_seed(session, paths, cols: Dict[str, DeviceColumn], off, rank: int, world: int,
@@ -301,18 +301,22 @@ def _cut_buckets(table: DeviceTable, key: str, cuts, device) -> DeviceTable:
     from ..ops import kernels as K
     off = np.asarray(table.bucket_offsets_host, dtype=np.int64)
     kc = table.columns[key]
-    if kc.valid is not None or kc.is_float or kc.dictionary is not None:
-        raise ValueError(f"heavy-bucket cut on a non-integer or nullable key {key}")
+    if kc.is_float or kc.dictionary is not None:
+        # the loader passes cuts for integer keys only (placement.routes_by_key)
+        raise ValueError(f"heavy-bucket cut on a non-integer key {key}")
     keep_lo, keep_hi = off[:-1].copy(), off[1:].copy()
     for b, (lo, hi) in cuts.items():
         a0, a1 = int(off[b]), int(off[b + 1])
         if a1 <= a0:
             continue
-        seg = kc.data[a0:a1].long()
-        s = a0 + (int(torch.searchsorted(seg, torch.tensor([lo], device=seg.device))[0])
-                  if lo is not None else 0)
-        e = a0 + (int(torch.searchsorted(seg, torch.tensor([hi], device=seg.device))[0])
-                  if hi is not None else a1 - a0)
+        # a bucket's null keys sort first: they belong to its first piece (lo None), like a
+        # shuffled row with a null key (OwnerMap.dest); the cut searches the non-null keys
+        nn = 0 if kc.valid is None else int((kc.valid[a0:a1] == 0).sum().item())
+        seg = kc.data[a0 + nn:a1].long()
+        s = a0 + nn + int(torch.searchsorted(seg, torch.tensor([lo], device=seg.device))[0]) \
+            if lo is not None else a0
+        e = a0 + nn + (int(torch.searchsorted(seg, torch.tensor([hi], device=seg.device))[0])
+                       if hi is not None else a1 - a0 - nn)
         keep_lo[b], keep_hi[b] = s, max(s, e)
     counts = keep_hi - keep_lo
     idx = torch.cat([torch.arange(int(a), int(c), dtype=torch.int64, device=device)

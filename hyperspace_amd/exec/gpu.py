@@ -31,6 +31,7 @@ import pyarrow as pa
 
 from ..ops import _lib as NL, kernels as K
 from ..plan import expressions as E, physical as X
+from ..parallel.placement import routes_by_key
 from ..utils import murmur3
 from ..utils.conf import HyperspaceConf
 from ..utils.tracing import stage, TRACER
@@ -40,6 +41,8 @@ from .device_cache import (_files_key, DeviceTableCache, load_bucketed_index, lo
                            seeded_index)
 from .device_table import DeviceColumn, DeviceTable
 from .graphs import GraphCache
+from .hbm_budget import rank_budget
+from .staging import RESERVE_BLOCK as _RESERVE_BLOCK
 from .gpu_common import (_AggProgram, _needs_eval, _prefix_sorted, _warm_torch_kernels, DRel, log,
                          QueryFuture, Unsupported)
 from .gpu_agg import AggOps
@@ -67,7 +70,10 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
         if cfg != kernel_config.active():
             kernel_config.bind(cfg)
         self.device = torch.device("cuda", torch.cuda.current_device())
-        self.cache = DeviceTableCache(HyperspaceConf.device_cache_bytes(session.conf))
+        # HBM / pinned budgets of this rank: its share of the device when ranks share one
+        # (exec/hbm_budget.py), the configured values otherwise
+        self.budget = rank_budget(session.conf, self.device)
+        self.cache = DeviceTableCache(self.budget.cache)
         self.last_path = None
         self.fallback_reason = None
         self.last_stream_passes = 0      # bucket-range passes of the last aggregate (0: resident)
@@ -86,7 +92,9 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
         # engine start: size the pinned staging pool once (pinning GBs is the slow part of a
         # cold build), as the HBM side is sized by the device table cache
         from .staging import pinned_pool
-        pinned_pool().reserve()
+        pool = pinned_pool()
+        pool.limit = min(pool.limit, self.budget.pinned)
+        pool.reserve(count=max(1, min(32, pool.limit // (2 * _RESERVE_BLOCK))))
         self._engine_start()
 
     def _engine_start(self) -> None:
@@ -101,7 +109,7 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
         import pyarrow.compute  # noqa: F401
         import pyarrow.dataset  # noqa: F401
         import pyarrow.parquet  # noqa: F401
-        reserve = HyperspaceConf.hbm_reserve_bytes(self.session.conf)
+        reserve = self.budget.arena
         if reserve > 0:
             free, _ = torch.cuda.mem_get_info(self.device)
             reserve = min(reserve, int(free * 0.8))
@@ -486,7 +494,7 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
                     return skip(f"column {u.name}: parts differ in type or dictionary")
                 cols.append(cs)
             nbytes = sum(c.data.numel() * c.data.element_size() for cs in cols for c in cs)
-            if nbytes > HyperspaceConf.device_cache_bytes(conf) // 4:
+            if nbytes > rank_budget(conf, self.device).cache // 4:
                 return skip("over a quarter of the device cache")
             nb = first.num_buckets
             with stage("hybrid.merge"):
@@ -631,6 +639,8 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
             sort_cols = [ncol[c.lower()] for c in idx.indexed_columns]
             load_cols = list(dict.fromkeys(cols + sort_cols))
             owners = self._owner_map(idx.num_buckets, world, files, sort_cols[0])
+            if owners.splits and not routes_by_key(idx.schema.field(sort_cols[0]).type):
+                owners = owners.unsplit()   # cut keys are integer values (placement.py)
             owned = owners.owned(rank)
             cuts = owners.ranges(rank)      # key ranges of heavy buckets cut across ranks
             chunk = getattr(self, "_bucket_chunk", None)

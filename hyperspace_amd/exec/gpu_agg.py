@@ -97,7 +97,8 @@ class AggOps:
         (BucketUnionExec.scala:61-74 runs a bucketed plan partition by partition)."""
         if self._dist() is not None:
             return None
-        budget = HyperspaceConf.device_cache_bytes(self.session.conf)
+        from .hbm_budget import rank_budget
+        budget = rank_budget(self.session.conf, self.device).cache   # the live conf
         memo = self.__dict__.setdefault("_stream_memo", {})
         hit = memo.get(id(child))
         if hit is not None and hit[0] is child and hit[1] == budget:

@@ -14,6 +14,7 @@ from ..utils.conf import HyperspaceConf
 from ..utils.tracing import stage
 from . import compile as CP, jit, join_index
 from .arrow_eval import key
+from ..parallel.placement import routes_by_key
 from .device_table import DeviceColumn, DeviceTable
 from .gpu_common import (_combine_aggs, _group_limit, _NeedHash, _prefix_sorted, DRel,
                          GROUP_LDS_JOIN, MAX_GROUPS_JOIN, Unsupported)
@@ -128,7 +129,8 @@ class JoinOps:
     def _repartition(self, r: DRel, part: X.HashPartitioning) -> DRel:
         """Hash Exchange (K3) on the device: Spark-compatible Murmur3 bucket ids, then one
         (bucket, keys) sort so the result is bucketed and sorted like an index.  With several
-        ranks, rows first move to their bucket's owner (``b % world``) with RCCL all-to-all, so
+        ranks, rows first move to their bucket's owner (the owner map, ``parallel/placement.py``) with
+        RCCL all-to-all, so
         the output is co-partitioned with the index tables of the same bucket count."""
         d = self._dist()
         if not all(isinstance(e, E.Attribute) for e in part.expressions):
@@ -155,8 +157,14 @@ class JoinOps:
         if d is not None and d.world > 1:
             with stage("shuffle.all_to_all"):
                 om = self._owner_map(B, d.world)
+                k0 = kcols[0]
+                if om.splits and not (routes_by_key(k0.atype) and k0.dictionary is None):
+                    om = om.unsplit()       # only integer keys follow the key-range cuts
+                # (a null key goes to its bucket's first piece, where the loader keeps an
+                # index's nulls: they sort first)
                 cols, bucket = self._exchange_rows(
-                    d, cols, bucket, om.dest(bucket, kcols[0].data if om.splits else None))
+                    d, cols, bucket, om.dest(bucket, k0.data if om.splits else None,
+                                             k0.valid if om.splits else None))
             kcols = [cols[k.expr_id] for k in keys]
             counts = K.histogram(bucket, B)
         n = int(bucket.numel())

@@ -382,13 +382,18 @@ class SemiJoinOps:
         # moves fewer bytes over xGMI: the keys themselves (32-bit offsets from the global low
         # key when the domain allows; every rank builds the whole bitmap and checks uniqueness
         # itself), or each rank's bitmap of its own keys, OR-ed, with a uniqueness check by
-        # population count.  Every rank sees the same counts, so all take the same branch.
+        # population count.  Every rank sees the same counts and the same "any rank's keys carry
+        # a validity mask" flag (a rank materializes one only when its split has nulls), so all
+        # take the same branch - the keys route ships raw values, so it needs no nulls anywhere.
         from ..parallel.gather import _all_gather_flat
         big = 1 << 62
         lo, hi, n = dom if dom is not None else (big, -big, 0)
         cdev = d.device if d.backend == "nccl" else torch.device("cpu")
-        info = torch.tensor([lo, hi, n], dtype=torch.int64, device=cdev)
-        allinfo = _all_gather_flat(d, info).view(d.world, 3).cpu().numpy()
+        info = torch.tensor([lo, hi, n, int(keys.valid is not None)], dtype=torch.int64,
+                            device=cdev)
+        allinfo = _all_gather_flat(d, info).view(d.world, 4).cpu().numpy()
+        any_valid = bool(allinfo[:, 3].any())
+        allinfo = allinfo[:, :3]
         ns = allinfo[:, 2]
         gn = int(ns.sum())
         if gn == 0:
@@ -401,8 +406,9 @@ class SemiJoinOps:
         wide = nbits > (1 << 31) - 1
         key_bytes = gn * (8 if wide else 4)
         bitmap_bytes = (d.world - 1) * ((nbits + 63) // 64) * 8
-        self.last_semi_exchange = "keys" if key_bytes < bitmap_bytes else "bitmap"
-        if key_bytes < bitmap_bytes and keys.valid is None:
+        self.last_semi_exchange = "keys" if key_bytes < bitmap_bytes and not any_valid else \
+            "bitmap"
+        if key_bytes < bitmap_bytes and not any_valid:
             nmax = int(ns.max())
             dt = torch.int64 if wide else torch.int32
             buf = torch.zeros(nmax, dtype=dt, device=self.device)

@@ -293,6 +293,32 @@ __device__ __forceinline__ void vload(const T* __restrict__ p, long long i, T (&
     for (int k = 0; k < V; ++k) x[k] = p[i + k];
   }
 }
+// NW dwords of a wavefront-uniform window through a raw buffer resource: the base is uniform
+// (scalar registers), the range check of the buffer unit returns 0 for bytes at or past
+// ``nbytes`` - so the table's last, partial group loads with the same dwordx4s as a full one
+// instead of a per-element edge path (which doubled the kernel's register footprint)
+typedef unsigned hs_v4u __attribute__((ext_vector_type(4)));
+// a code bound clamped to +-2^20: narrow (<= 16-bit) codes against it never overflow int32
+__device__ __forceinline__ int hs_c20(long long v) {
+  return (int)(v < -1048576ll ? -1048576ll : (v > 1048576ll ? 1048576ll : v));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t hs_rsrc(const void* base, long long nbytes) {
+  const u64 a_ = (u64)base;
+  const unsigned lo_ = __builtin_amdgcn_readfirstlane((unsigned)a_);
+  const unsigned hi_ = __builtin_amdgcn_readfirstlane((unsigned)(a_ >> 32));
+  const long long n_ = nbytes < 0 ? 0 : (nbytes > 0x7fffffffll ? 0x7fffffffll : nbytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((u64)hi_ << 32) | lo_), (short)0,
+                                           __builtin_amdgcn_readfirstlane((int)n_), 0x00020000);
+}
+template <int NW>
+__device__ __forceinline__ void bload(__amdgpu_buffer_rsrc_t r, unsigned off, unsigned (&x)[NW]) {
+  static_assert(NW % 4 == 0, "bload: whole dwordx4s");
+#pragma unroll
+  for (int k = 0; k < NW / 4; ++k) {
+    const hs_v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * k, 0, 0);
+    x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+  }
+}
 __device__ __forceinline__ void lds_min(double* p, double v) {
   u64* a = (u64*)p; u64 old = *a, as;
   do { as = old; if (__longlong_as_double((i64)as) <= v) break;
@@ -445,6 +471,49 @@ class _Gen:
             neg = "" if op == NL.OP_EQ else "!"
             return f"({self.ok(c)} && {neg}bit_test({sp}, {sn} * 64, (i64)x{c} - {base}))"
         raise ValueError(f"pred kind {kind}")
+
+    def sign_leaf(self, k: int, p: NL.Pred) -> Optional[str]:
+        """``leaf`` as an int32 whose sign bit is set iff the row fails it, with no compare
+        (no lane-mask registers, no select of per-bit constants): a range test of a narrow
+        compact code is ``(r - lo) | (hi - r)``.  None when the leaf has no such form."""
+        kind, op = p.kind, p.op
+        if kind == NL.PK_TRUE:
+            return "0"
+        c = p.col
+        hv = self.cols[c][1]
+        if kind == NL.PK_IS_NULL:
+            return f"(-(int){self.ok(c)})" if hv else "(-1)"
+        if kind == NL.PK_NOT_NULL:
+            return f"((int){self.ok(c)} - 1)" if hv else "0"
+        enc = self.cols[c][2]
+        if not (self.intpred and enc and (kind == NL.PK_INT_LIT and not enc[1] or
+                                          kind == NL.PK_FLT_LIT and enc[1])):
+            return None
+        if _SIZEOF.get(self.raw_type(c), 8) > 2:
+            return None
+        lo = self.a.add("q", f"CL{k}", "long long")
+        hi = self.a.add("q", f"CH{k}", "long long")
+        s = f"((r{c} - hs_c20({lo})) | (hs_c20({hi}) - r{c}))"
+        if op == NL.OP_NE:
+            s = f"(~{s})"
+        return f"({s} | ((int){self.ok(c)} - 1))" if hv else s
+
+    def cnf_sign(self, preds: List[Tuple[int, NL.Pred]]) -> Optional[str]:
+        """``cnf`` as a sign word (negative iff the row fails), or None: a group (OR) fails
+        when every leaf fails (AND of the words), the conjunction when any group fails (OR)."""
+        if not preds:
+            return "0"
+        groups: Dict[int, List[str]] = {}
+        order: List[int] = []
+        for k, p in preds:
+            leaf = self.sign_leaf(k, p)
+            if leaf is None:
+                return None
+            if p.group not in groups:
+                groups[p.group] = []
+                order.append(p.group)
+            groups[p.group].append(leaf)
+        return "(" + " | ".join("(" + " & ".join(groups[g]) + ")" for g in order) + ")"
 
     def cnf(self, preds: List[Tuple[int, NL.Pred]]) -> str:
         if not preds:

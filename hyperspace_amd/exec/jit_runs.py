@@ -37,6 +37,7 @@ _CFG = _KC.active()
 MJ_2P, RS_ITEMS = _CFG.mj_2p, _CFG.rs_items
 RT2_UNROLL, RT2_GRID = _CFG.rt2_unroll, _CFG.rt2_grid
 RS_BITS, RS_BITS_GRID, RS_PACK = _CFG.rs_bits, _CFG.rs_bits_grid, _CFG.rs_pack
+RS_PIPE, RS_WALK = _CFG.rs_pipe, _CFG.rs_walk
 
 
 def tag_width(p: NL.JoinParams) -> int:
@@ -465,7 +466,7 @@ def packed_tail(layout, compacts):
 
 
 def sparse_shape(p: NL.JoinParams, compacts, hk=None, tk=None) -> tuple:
-    return ("run_bits_scan",) + scan_shape(p, compacts, 1, 64)[1:] + \
+    return ("run_bits_scan", RS_PIPE, RS_WALK) + scan_shape(p, compacts, 1, 64)[1:] + \
         (pack_layout(p, compacts),) + ((hk.shape(),) if hk is not None else ()) + \
         ((tk.shape(),) if tk is not None else ())
 
@@ -533,16 +534,18 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
     if tk is not None:
         b += JH._topk_decls(aggs, tk)
     CAP = 1024  # noqa: N806 — list entries per wavefront and round (a denser tile takes rounds)
-    EW = 4  # noqa: N806 — list entries per lane per walk pass, loads all in flight together
+    EW = max(1, RS_WALK)  # noqa: N806 — list entries per lane per walk pass, loads in flight together
 
     def geom(tv: str, sfx: str) -> List[str]:
-        """Tile ``tv``'s range / row geometry and its group's run-form words (suffix sfx)."""
+        """Tile ``tv``'s range / row geometry and its group's run-form words (suffix sfx).  The
+        words stay in their loaded types (no OR / widening here): an operation on a loaded value
+        makes the compiler wait for the load on the spot, and these are prefetched a tile ahead."""
         return [f"    while (r + 1 < (int)a.R && a.tile_prefix[r + 1] <= {tv}) ++r;",
                 f"    rs{sfx} = a.rstart[r]; re{sfx} = rs{sfx} + a.rlen[r];",
                 f"    tb{sfx} = (rs{sfx} & ~(i64)63) + ({tv} - a.tile_prefix[r]) * {T};",
                 f"    {{ const i64 r0_ = tb{sfx} + 64 * ln; "
                 f"const i64 g_ = (r0_ < a.nrows ? r0_ : a.nrows - 1) >> 6;",
-                f"      gm{sfx} = a.GM{lk}[g_] | 1ull; gr{sfx} = a.GR{lk}[g_]; }}"]
+                f"      gm{sfx} = a.GM{lk}[g_]; gr{sfx} = a.GR{lk}[g_]; }}"]
     if tk is not None:
         b.append(f"  __shared__ unsigned short lrn_[{WV}][{CAP}];")
     b += [f"  __shared__ unsigned short lst_[{WV}][{CAP}];",
@@ -559,65 +562,92 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
           "    while (hi - lo > 1) { const int m = (lo + hi) >> 1; "
           "if (a.tile_prefix[m] <= t0) lo = m; else hi = m; }",
           "    r = lo; }",
-          "  i64 rsN = 0, reN = 0, tbN = 0; u64 gmN = 0ull; i64 grN = 0;",
-          "  if (t0 < t1) {"]
-    b += geom("t0", "N")
-    b += ["  }",
-          "  for (i64 t = t0; t < t1; ++t) {",
-          "    const i64 rs = rsN, re = reN, tb0 = tbN; const u64 m_ = gmN; const i64 q0 = grN;"]
-    if tk is not None:
-        # key run of a list entry, relative to the tile's first run (lrn_)
-        b.append("    const i64 qb_ = __shfl(q0, 0, 64); const int qr_ = (int)(q0 - qb_);")
-    b += [
-
-          "    const i64 row0 = tb0 + 64 * ln;",
-          "    const i64 lo_ = rs - row0, hi_ = re - row0;",
-          "    const int alo = lo_ <= 0 ? 0 : (lo_ >= 64 ? 64 : (int)lo_);",
-          "    const int ahi = hi_ <= 0 ? 0 : (hi_ >= 64 ? 64 : (int)hi_);",
-          "    const u64 am = alo >= ahi ? 0ull : ((ahi == 64 ? ~0ull : ((1ull << ahi) - 1ull)) & "
-          "~((1ull << alo) - 1ull));",
-          # this tile's tag words and predicate columns in flight together, then the next
-          # tile's run-form words
-          "    const i64 w_ = q0 >> 5; const unsigned sh_ = (unsigned)(q0 & 31);",
-          "    const u64 lw_ = (u64)a.tags[w_] | ((u64)a.tags[w_ + 1] << 32);",
-          "    const u64 hw_ = (u64)a.tags[w_ + 2];",
-          # a whole in-table group reads its columns with vector loads, a partial one (the
-          # table's last group) element-wise
-          f"    const bool vok_ = row0 + {NI} <= a.nrows;"]
+          # software pipeline (RS_PIPE), one exposed memory round trip per tile: tile t's tag
+          # words and predicate columns were issued during tile t-1 (after its masks were
+          # formed, before its list walk, so the walk's aggregate-input loads wait on them
+          # together) and the run-form words of tile t+1 one tile earlier still (the tag words'
+          # address needs them).  The tile loop is unrolled by two over two named buffers (A, B):
+          # a loop-carried array is copied register to register at the back edge otherwise,
+          # after a wait for its loads, and held twice.
+          "  i64 rsC = 0, reC = 0, tbC = 0; u64 gmC = 0ull; int grC = 0;",
+          "  i64 rsN = 0, reN = 0, tbN = 0; u64 gmN = 0ull; int grN = 0;",
+          "  unsigned tw0A_ = 0u, tw1A_ = 0u, tw2A_ = 0u, tw0B_ = 0u, tw1B_ = 0u, tw2B_ = 0u;"]
     g1 = J._Gen(args, cols, SPLIT, ("row0", "row0"), approx, True)
     elem = {}   # array name -> C expression of element (idx) from its packed 32-bit words
+    issue = []  # the current tile's (C) tag-word and predicate-column loads into buffer @S@
+    issue.append("    { const i64 w_ = (i64)grC >> 5; tw0@S@_ = a.tags[w_]; "
+                 "tw1@S@_ = a.tags[w_ + 1]; tw2@S@_ = a.tags[w_ + 2]; }")
     for name, ct, ptr in J._vec_loads(g1, pslots):
         es = J._SIZEOF[ct]
         nw = NI * es // 4
         per = 4 // es
-        b.append(f"    unsigned {name}w[{nw}];")
-        b.append(f"    if (vok_) {{ vload<unsigned, {nw}>((const unsigned*){ptr}, row0 * {es} / 4, "
-                 f"{name}w); }} else {{ for (int k_ = 0; k_ < {nw}; ++k_) {name}w[k_] = 0u;"
-                 f" for (int k_ = 0; k_ < {NI} && row0 + k_ < a.nrows; ++k_) {{ const unsigned "
-                 f"u_ = (unsigned)({'unsigned char' if es == 1 else ('unsigned short' if es == 2 else 'unsigned')})"
-                 f"{ptr}[row0 + k_]; {name}w[k_ / {per}] |= u_ << ({8 * es} * (k_ % {per})); }} }}")
-        elem[name] = (ct, f"{name}w[({{i}}) / {per}]" if per > 1 else f"{name}w[{{i}}]",
+        b.append(f"  unsigned {name}wA[{nw}], {name}wB[{nw}];")
+        # the group's rows past the table end read as 0 (buffer range check); they are outside
+        # every row range, so the range mask drops them
+        issue.append(f"    bload<{nw}>(hs_rsrc((const char*){ptr} + tbC * {es}, "
+                     f"@LIVE@(a.nrows - tbC) * {es}), (unsigned)(64 * ln * {es}), {name}w@S@);")
+        elem[name] = (ct, f"{name}w@S@[({{i}}) / {per}]" if per > 1 else f"{name}w@S@[{{i}}]",
                       8 * es, per)
-    b += ["    if (t + 1 < t1) {"]
-    b += ["  " + x for x in geom("(t + 1)", "N")]
-    b += ["    }",
-          "    const u64 T_ = sh_ ? ((lw_ >> sh_) | (hw_ << (64 - sh_))) : lw_;",
-          # only the group's own runs' tags (popc(m) of them) decide whether any row is set
-          "    const int nr_ = __popcll(m_);",
-          "    const u64 Tm_ = nr_ >= 64 ? T_ : (T_ & ((1ull << nr_) - 1ull));",
-          "    u64 c_ = T_ ^ (T_ << 1), d_ = 0ull, mm_ = (am && Tm_) ? m_ : 0ull;",
-          "    while (mm_) { const u64 lb_ = mm_ & (0ull - mm_); if (c_ & 1ull) d_ |= lb_; "
-          "c_ >>= 1; mm_ ^= lb_; }",
-          "    d_ ^= d_ << 1; d_ ^= d_ << 2; d_ ^= d_ << 4; d_ ^= d_ << 8; d_ ^= d_ << 16; "
-          "d_ ^= d_ << 32;",
-          "    d_ &= am;"]
+
+    def buf(lines: List[str], sfx: str) -> List[str]:
+        return [x.replace("@S@", sfx).replace("@LIVE@", "") for x in lines]
+
+    b.append("  if (t0 < t1) {")
+    if RS_PIPE:
+        b += geom("t0", "C")
+        b += buf(issue, "A")
+        b += ["    if (t0 + 1 < t1) {"]
+        b += ["  " + x for x in geom("(t0 + 1)", "N")]
+        b += ["    }"]
+    else:
+        b += geom("t0", "N")
+    b += ["  }"]
+    body: List[str] = []   # one tile (@T@), its buffer @S@, the next tile's buffer @O@
+    if not RS_PIPE:
+        # this tile's loads, then the next tile's run-form words: two round trips per tile (the
+        # column stream, then the walk's aggregate inputs), fewer registers
+        body += ["    rsC = rsN; reC = reN; tbC = tbN; gmC = gmN; grC = grN;"]
+        body += [x.replace("@LIVE@", "") for x in issue]
+        body += ["    if (@T@ + 1 < t1) {"]
+        body += ["  " + x for x in geom("(@T@ + 1)", "N")]
+        body += ["    }"]
+    body += ["    const i64 rs = rsC, re = reC, tb0 = tbC; const u64 m_ = gmC | 1ull; "
+             "const i64 q0 = (i64)grC;"]
+    if tk is not None:
+        # key run of a list entry, relative to the tile's first run (lrn_)
+        body.append("    const i64 qb_ = __shfl(q0, 0, 64); const int qr_ = (int)(q0 - qb_);")
+    body += ["    const i64 row0 = tb0 + 64 * ln;",
+             "    const i64 lo_ = rs - row0, hi_ = re - row0;",
+             "    const int alo = lo_ <= 0 ? 0 : (lo_ >= 64 ? 64 : (int)lo_);",
+             "    const int ahi = hi_ <= 0 ? 0 : (hi_ >= 64 ? 64 : (int)hi_);",
+             "    const u64 am = alo >= ahi ? 0ull : ((ahi == 64 ? ~0ull : ((1ull << ahi) - 1ull)) & "
+             "~((1ull << alo) - 1ull));",
+             "    const unsigned sh_ = (unsigned)(q0 & 31);",
+             "    const u64 lw_ = (u64)tw0@S@_ | ((u64)tw1@S@_ << 32);",
+             "    const u64 hw_ = (u64)tw2@S@_;",
+             "    const u64 T_ = sh_ ? ((lw_ >> sh_) | (hw_ << (64 - sh_))) : lw_;",
+             # only the group's own runs' tags (popc(m) of them) decide whether any row is set
+             "    const int nr_ = __popcll(m_);",
+             "    const u64 Tm_ = nr_ >= 64 ? T_ : (T_ & ((1ull << nr_) - 1ull));",
+             "    u64 c_ = T_ ^ (T_ << 1), d_ = 0ull, mm_ = (am && Tm_) ? m_ : 0ull;",
+             "    while (mm_) { const u64 lb_ = mm_ & (0ull - mm_); if (c_ & 1ull) d_ |= lb_; "
+             "c_ >>= 1; mm_ ^= lb_; }",
+             "    d_ ^= d_ << 1; d_ ^= d_ << 2; d_ ^= d_ << 4; d_ ^= d_ << 8; d_ ^= d_ << 16; "
+             "d_ ^= d_ << 32;",
+             "    d_ &= am;"]
     # predicate mask: 64 compares, shift-or into two 32-bit halves (a C loop: each row's
     # value is decoded where it is compared, not all 64 held decoded at once)
-    b.append("    unsigned plo_ = 0u, phi_ = 0u;")
+    body.append("    unsigned plo_ = 0u, phi_ = 0u;")
     cond = J._rename(g1.cnf(lpreds), pslots, "k")
+    # narrow compact-code ranges: fail bits from a sign word (no compares, no constants held in
+    # registers for the select), else the generic condition's pass bits
+    sign = g1.cnf_sign(lpreds)
+    if sign is not None:
+        sign = J._rename(sign, pslots, "k")
     for half, off in (("plo_", 0), ("phi_", 32)):
-        b.append("    #pragma unroll")
-        b.append("    for (int k_ = 0; k_ < 32; ++k_) {")
+        body.append("    #pragma unroll")
+        body.append("    for (int k_ = 0; k_ < 32; ++k_) {")
+
         def raw_of(name: str) -> str:
             et, word, bits, per = elem[name]
             i = f"{off} + k_"
@@ -627,19 +657,41 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
             ct = J._CTYPE[cols[sl][0]]
             enc = cols[sl][2]
             raw = raw_of(f"x{sl}")
-            b.append(f"      const auto xr{sl}_k = {raw};")
+            body.append(f"      const auto xr{sl}_k = {raw};")
             raw = f"xr{sl}_k"
             if enc:
-                b.append(f"      const int r{sl}_k = (int){raw};")
+                body.append(f"      const int r{sl}_k = (int){raw};")
             if enc and enc[1]:
                 bq = args.add("q", f"B{sl}", "long long")
-                b.append(f"      const i64 q{sl}_k = {bq} + (i64){raw};")
-            b.append(f"      const {ct} x{sl}_k = {g1.decode(sl, raw)};")
+                body.append(f"      const i64 q{sl}_k = {bq} + (i64){raw};")
+            body.append(f"      const {ct} x{sl}_k = {g1.decode(sl, raw)};")
             if cols[sl][1]:
-                b.append(f"      const bool n{sl}_k = {raw_of(f'n{sl}')} != 0;")
-        b.append(f"      {half} |= ({cond} ? 1u : 0u) << k_;")
-        b.append("    }")
-    b += ["    d_ &= ((u64)phi_ << 32) | (u64)plo_;",
+                body.append(f"      const bool n{sl}_k = {raw_of(f'n{sl}')} != 0;")
+        if sign is not None:
+            body.append(f"      {half} |= ((unsigned)({sign}) >> 31) << k_;")
+        else:
+            body.append(f"      {half} |= ({cond} ? 1u : 0u) << k_;")
+        body.append("    }")
+    if sign is not None:
+        body += ["    d_ &= ~(((u64)phi_ << 32) | (u64)plo_);"]
+    else:
+        body += ["    d_ &= ((u64)phi_ << 32) | (u64)plo_;"]
+    if RS_PIPE:
+        # this tile's column words are consumed: the next tile's loads go out now
+        # (the scheduler must not hoist the next tile's loads above this tile's masks: both
+        # buffers would be live at once)
+        # The loads are unconditional - a load under a condition keeps the buffer's previous
+        # contents live through the whole tile - and past the wavefront's last tile they read
+        # an empty buffer range (no memory traffic; the tag words re-read this tile's).
+        body += ["    __builtin_amdgcn_sched_barrier(0);",
+                 "    { const bool nx_ = @T@ + 1 < t1;",
+                 "      if (nx_) { rsC = rsN; reC = reN; tbC = tbN; gmC = gmN; grC = grN; }"]
+        body += ["  " + x.replace("@S@", "@O@").replace("@LIVE@", "!nx_ ? 0ll : ")
+                 for x in issue]
+        body += ["      if (@T@ + 2 < t1) {"]
+        body += ["    " + x for x in geom("(@T@ + 2)", "N")]
+        body += ["      }", "    }"]
+    body += [
           # exclusive scan of the lanes' passing-row counts
           "    const int cn_ = __popcll(d_);",
           "    int inc_ = cn_;",
@@ -656,56 +708,79 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
           "} ++pos_; e_ &= e_ - 1ull; } }",
           f"    {J._wave_sync()}",
           f"    for (int cb = 0; cb < wn_; cb += {64 * EW}) {{"]
+    layout = pack_layout(p, compacts)
+    if layout:
+        body.append("      const u64* PKt_ = a.PK + tb0;")
     ind2 = "      "
     for k in range(EW):
-        b += [f"{ind2}const int ce{k} = cb + {64 * k} + ln;",
-              f"{ind2}const bool cok{k} = ce{k} < wn_;",
-              f"{ind2}const i64 crow{k} = tb0 + (cok{k} ? (i64)lst_[wq][ce{k}] : 0);"]
+        body += [f"{ind2}const int ce{k} = cb + {64 * k} + ln;",
+                 f"{ind2}const bool cok{k} = ce{k} < wn_;",
+                 f"{ind2}const int cof{k} = cok{k} ? (int)lst_[wq][ce{k}] : 0;",
+                 f"{ind2}const i64 crow{k} = tb0 + (i64)cof{k};"]
         if tk is not None:
-            b.append(f"{ind2}const unsigned crn{k} = cok{k} ? (unsigned)lrn_[wq][ce{k}] : "
-                     f"0xFFFFFFFFu;")
+            body.append(f"{ind2}const unsigned crn{k} = cok{k} ? (unsigned)lrn_[wq][ce{k}] : "
+                        f"0xFFFFFFFFu;")
     gs = [J._Gen(args, cols, SPLIT, (f"crow{k}", f"crow{k}"), approx, True) for k in range(EW)]
-    layout = pack_layout(p, compacts)
     packed = {sl: (off, nb) for sl, off, nb in layout} if layout else {}
     if layout:
         args.add("p", "PK", "const unsigned long long*")
     for k in range(EW):
         if layout:
-            b.append(f"{ind2}const u64 pk{k}_ = a.PK[crow{k}];")
+            # the tile's rows through a uniform base: 32-bit lane offsets
+            body.append(f"{ind2}const u64 pk{k}_ = PKt_[cof{k}];")
         for sl in tail:
             if sl in packed:
                 off, nb = packed[sl]
                 ct = gs[k].raw_type(sl)
                 ut = {1: "unsigned char", 2: "unsigned short", 4: "unsigned"}[nb]
-                J._uload_raw(gs[k], sl, f"c{k}", f"(({ct})({ut})(pk{k}_ >> {off}))", "1", b, ind2)
+                J._uload_raw(gs[k], sl, f"c{k}", f"(({ct})({ut})(pk{k}_ >> {off}))", "1", body,
+                             ind2)
             else:
-                J._uload(gs[k], sl, f"c{k}", b, ind2)
+                J._uload(gs[k], sl, f"c{k}", body, ind2)
     carry_gen = J._Gen(args, cols, SPLIT, ("tcw_", "tcw_"), frozenset(), True) \
         if tk is not None else None
     for k in range(EW):
         g = gs[k]
         it = f"c{k}"
-        b.append(f"{ind2}{{ bool cok = cok{k};")
+        body.append(f"{ind2}{{ bool cok = cok{k};")
         gvar = "gic"
         if grouped:
             base = args.add("q", "group_base", "long long")
             ng = args.add("q", "num_groups", "long long")
-            b.append(f"{ind2}const i64 glc = (i64){J._rename(f'x{p.group_col}', tail, it)} - "
-                     f"{base};")
-            b.append(f"{ind2}cok = cok && {J._rename(g.ok(p.group_col), tail, it)} && glc >= 0 && "
-                     f"glc < {ng};")
-            b.append(f"{ind2}const int {gvar} = cok ? (int)glc : 0;")
+            body.append(f"{ind2}const i64 glc = (i64){J._rename(f'x{p.group_col}', tail, it)} - "
+                        f"{base};")
+            body.append(f"{ind2}cok = cok && {J._rename(g.ok(p.group_col), tail, it)} && "
+                        f"glc >= 0 && glc < {ng};")
+            body.append(f"{ind2}const int {gvar} = cok ? (int)glc : 0;")
         if hk is not None:
-            b += [J._rename(x, tail, it)
-                  for x in JH._hash_accumulate(g, aggs, hk, "cok", ind2, tk=tk,
-                                              seg=f"crn{k}" if tk is not None else None,
-                                              row=f"crow{k}", run=f"qb_ + (i64)crn{k}",
-                                              carry_gen=carry_gen)]
+            body += [J._rename(x, tail, it)
+                     for x in JH._hash_accumulate(g, aggs, hk, "cok", ind2, tk=tk,
+                                                 seg=f"crn{k}" if tk is not None else None,
+                                                 row=f"crow{k}", run=f"qb_ + (i64)crn{k}",
+                                                 carry_gen=carry_gen)]
         else:
-            b += [J._rename(x, tail, it)
-                  for x in J._accumulate(g, aggs, grouped, "cok", gvar, ind2)]
-        b.append(f"{ind2}}}")
-    b += ["    }", f"    {J._wave_sync()}", "    }", "  }"]
+            body += [J._rename(x, tail, it)
+                     for x in J._accumulate(g, aggs, grouped, "cok", gvar, ind2)]
+        body.append(f"{ind2}}}")
+    body += ["    }", f"    {J._wave_sync()}", "    }"]
+
+    def tile(tv: str, cur: str, nxt: str) -> List[str]:
+        return ["   {"] + [x.replace("@T@", tv).replace("@S@", cur).replace("@O@", nxt)
+                          for x in body] + ["   }"]
+    if RS_PIPE == 2:
+        b += ["  for (i64 t = t0; t < t1; t += 2) {"]
+        b += tile("t", "A", "B")
+        b += ["    if (t + 1 >= t1) break;"]
+        b += tile("(t + 1)", "B", "A")
+        b += ["  }"]
+    elif RS_PIPE:
+        b += ["  for (i64 t = t0; t < t1; ++t) {"]
+        b += tile("t", "A", "A")
+        b += ["  }"]
+    else:
+        b += ["  for (i64 t = t0; t < t1; ++t) {"]
+        b += tile("t", "A", "A")
+        b += ["  }"]
     if hk is None:
         b += J._flush(aggs, grouped)
     if tk is not None:

@@ -77,6 +77,9 @@ class KernelConfig:
     rs_bits: bool = True         # phase 2 bit-parallel for 1-bit tags (gen_run_sparse_scan)
     rs_bits_grid: int = 8192
     rs_pack: bool = True         # bits scan reads its aggregate inputs row-packed
+    rs_pipe: int = 1             # bits scan software pipeline: 0 off (two round trips per tile,
+                                 # fewest registers), 1 one buffer, 2 two named buffers (unroll 2)
+    rs_walk: int = 4             # bits scan list entries per lane per walk pass
     # --- shared ------------------------------------------------------------------------------
     vec_prefetch: bool = True    # software-pipelined full tiles of the vectorized kernels
     wave_sync: bool = True       # per-wavefront lists ordered by a wavefront barrier

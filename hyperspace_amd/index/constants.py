@@ -124,7 +124,8 @@ RUN_TOPK_ENABLED_DEFAULT = "true"
 JOIN_INDEX_ENABLED = "spark.hyperspace.mi.joinIndex.enabled"
 JOIN_INDEX_ENABLED_DEFAULT = "true"
 # Query-time placement of index buckets across the ranks of a torch.distributed job:
-#  "sharded"    bucket b is resident on rank b % world only; every query runs on all ranks and
+#  "sharded"    each bucket (or key-range piece of a heavy bucket) is resident on one rank only
+#               (the owner map of parallel/placement.py); every query runs on all ranks and
 #               partial results combine with one RCCL all-gather (strong scaling of one query);
 #  "replicated" every rank holds all buckets in its HBM (an SF100 index set is ~36 GB of a
 #               288 GB MI355X) and answers queries alone, with no collective (read replicas:

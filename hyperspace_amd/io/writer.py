@@ -124,6 +124,22 @@ class DataFrameWriter:
         warehouse directory, or external at ``option("path", ...)``)."""
         self.df.session.catalog.save_table(name, self, self._mode)
 
+    def reads_from(self, path: str) -> bool:
+        """Whether the DataFrame being written reads files at or under ``path``: the data is
+        only computed inside ``save``, so overwriting such a path would delete the input first."""
+        from ..plan import logical as L
+        root = os.path.abspath(P.to_local(path)).rstrip(os.sep) + os.sep
+        plan = self.df.queryExecution.analyzed
+        for lr in plan.collect(lambda n: isinstance(n, L.LogicalRelation)):
+            loc = getattr(lr.relation, "location", None)
+            paths = list(getattr(loc, "root_paths", []) or [])
+            for f in (loc.all_files() if loc is not None else []):
+                paths.append(f.path)
+            for q in paths:
+                if (os.path.abspath(P.to_local(q)).rstrip(os.sep) + os.sep).startswith(root):
+                    return True
+        return False
+
     def save(self, path: str) -> None:
         local = P.to_local(path)
         if os.path.exists(local):
@@ -132,6 +148,10 @@ class DataFrameWriter:
             if self._mode == "ignore":
                 return
             if self._mode == "overwrite":
+                if self.reads_from(local):
+                    # Spark refuses this too (the input would be deleted before it is read)
+                    raise HyperspaceException(
+                        f"Cannot overwrite a path that is also being read from: {path}")
                 import shutil
                 shutil.rmtree(local)
         os.makedirs(local, exist_ok=True)

@@ -1,9 +1,12 @@
 """Process-group context: one process per GPU, ``torch.distributed`` over RCCL (xGMI) on MI355X
 or gloo on CPU (tests).
 
-Bucket ownership is static: bucket ``b`` lives on rank ``b % world``.  Two bucketed indexes with
-equal bucket counts are therefore co-partitioned and a JoinIndexRule join moves no data between
-GPUs; only index builds (and non-index shuffles) exchange rows, with all-to-all.
+Bucket ownership follows the session's owner map for each bucket count
+(``parallel/placement.py``: size-balanced LPT, ``b % world`` when bucket sizes are equal, heavy
+buckets of an integer key cut into key ranges across ranks).  Every index and query-time shuffle
+with that bucket count uses the same map, so two bucketed indexes with equal bucket counts are
+co-partitioned and a JoinIndexRule join moves no data between GPUs; only index builds (and
+non-index shuffles) exchange rows, with all-to-all.
 """
 from __future__ import annotations
 

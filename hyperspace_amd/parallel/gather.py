@@ -1,6 +1,6 @@
 """Row results of a sharded query to every rank, on the device, without pickling.
 
-A row-producing query over bucket-sharded indexes (each rank holds buckets ``b % world``) ends
+A row-producing query over bucket-sharded indexes (each rank holds the buckets its owner map gives it, ``parallel/placement.py``) ends
 with every rank holding the result rows of its own buckets as device columns.  The reference's
 driver collect (PlanAnalyzer.scala:217 and Spark's ``collect``) becomes here:
 

@@ -47,7 +47,7 @@ class OwnerMap:
     the ``len(ranks) - 1`` increasing split keys) for a bucket cut across ranks - piece i holds
     the keys in ``[bounds[i - 1], bounds[i])``, open at both ends - and ``owners[b]`` is then
     its first piece's rank."""
-    __slots__ = ("owners", "world", "key", "_luts", "splits")
+    __slots__ = ("owners", "world", "key", "_luts", "splits", "_unsplit")
 
     def __init__(self, owners: Sequence[int], world: int,
                  splits: Optional[Dict[int, Tuple[Sequence[int], Sequence[int]]]] = None):
@@ -67,6 +67,19 @@ class OwnerMap:
         self.key = (self.world, self.owners.tobytes(),
                     tuple((b, r.tobytes(), k.tobytes()) for b, (r, k) in self.splits.items()))
         self._luts: Dict[str, object] = {}
+        self._unsplit: Optional["OwnerMap"] = None
+
+    def unsplit(self) -> "OwnerMap":
+        """This map without key-range cuts: a split bucket lives whole on its first piece's rank.
+        The split keys are values of the integer key the cuts were computed from, so a table or
+        shuffle whose leading key is of another type (string codes are rank-local, float values
+        would truncate) must not route by them; it uses this map instead (``routes_by_key``) -
+        every table keyed by that type agrees on it, so joins on such keys stay co-located."""
+        if not self.splits:
+            return self
+        if self._unsplit is None:
+            self._unsplit = OwnerMap(self.owners.copy(), self.world)
+        return self._unsplit
 
     @property
     def num_buckets(self) -> int:
@@ -123,9 +136,11 @@ class OwnerMap:
             self._luts[k] = t
         return t
 
-    def dest(self, bucket, key=None):
+    def dest(self, bucket, key=None, valid=None):
         """Destination rank of every row of an int32 bucket-id tensor; rows of a split bucket
-        go by their (leading bucketing) key, ``key`` (an integer tensor of the same rows)."""
+        go by their (leading bucketing) key, ``key`` (an integer tensor of the same rows), and a
+        row whose key is null (``valid`` == 0) to the bucket's first piece - nulls sort first,
+        so an index's null keys are in that piece's key range (``device_cache._cut_buckets``)."""
         if self.is_modulo():
             return bucket % self.world if self.world > 1 else bucket * 0
         out = self.lut(bucket.device).index_select(0, bucket.long())
@@ -134,12 +149,24 @@ class OwnerMap:
             if key is None:
                 raise ValueError("OwnerMap.dest: a split bucket routes rows by key")
             k = key.long()
+            nonnull = valid.bool() if valid is not None else None
             for b, (ranks, bounds) in self.splits.items():
                 m = bucket == b
+                if nonnull is not None:
+                    m = m & nonnull
                 piece = torch.bucketize(k, torch.from_numpy(bounds).to(k.device), right=True)
                 r = torch.from_numpy(ranks.astype(np.int64)).to(k.device)[piece].to(out.dtype)
                 out = torch.where(m, r, out)
         return out
+
+
+def routes_by_key(atype) -> bool:
+    """Whether rows keyed by a column of arrow type ``atype`` follow a map's key-range cuts:
+    integer keys only (the domain split keys are taken from, ``bucket_bounds``)."""
+    import pyarrow as pa
+    if pa.types.is_dictionary(atype):
+        return False
+    return pa.types.is_integer(atype)
 
 
 def lpt(weights: Sequence[float], world: int) -> np.ndarray:

@@ -9,6 +9,8 @@ from __future__ import annotations
 
 from typing import List, Tuple
 
+import numpy as np
+
 
 def exchange(columns: List, dest, world: int, ctx=None) -> Tuple[List, "object"]:
     """Returns (received columns, per-source receive counts)."""
@@ -19,7 +21,10 @@ def exchange(columns: List, dest, world: int, ctx=None) -> Tuple[List, "object"]
     if ctx is not None and ex.world != world:
         raise ValueError(f"exchange: world {world} != process group size {ex.world}")
     ex.add(live, dest.to(torch.int32))
-    counts = torch.from_numpy(ex.batches[0].counts.copy())
+    # a device batch is deferred until its counts copy lands (RowExchange._add_device):
+    # received_rows() issues it, so its receive counts exist before finish() consumes the batch
+    ex.received_rows()
+    counts = torch.from_numpy(np.asarray(ex.batches[0].counts, dtype=np.int64).copy())
     got = iter(ex.finish())
     return [None if c is None else next(got) for c in columns], counts
 

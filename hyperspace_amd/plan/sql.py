@@ -96,17 +96,62 @@ class SqlPlanner(_Parser):
             raise SyntaxError(f"unexpected token {self.peek()[1]!r}")
         return p
 
+    def _union_ahead(self) -> bool:
+        """Whether a UNION follows at this nesting level (before the closing parenthesis or
+        the end): then a trailing ORDER BY / LIMIT belongs to the whole union, as in Spark."""
+        depth = 0
+        for kind, t in self.toks[self.i:]:
+            if kind == "eof":
+                return False
+            if kind == "op" and t == "(":
+                depth += 1
+            elif kind == "op" and t == ")":
+                if depth == 0:
+                    return False
+                depth -= 1
+            elif depth == 0 and kind == "kw" and t == "UNION":
+                return True
+        return False
+
     def query(self) -> L.LogicalPlan:
-        p = self.select()
+        if not self._union_ahead():
+            return self.select()
+        p = self.select(tail=False)
         while self.accept("kw", "UNION"):
             all_ = self.accept("kw", "ALL")
-            p = L.Union([p, self.select()])
+            p = L.Union([p, self.select(tail=False)])
             if not all_:
                 p = _distinct(p)
+        orders, limit = self.order_limit()
+        if orders:
+            # names resolve against the union's output (the first branch's column names)
+            scope = _Scope(self.session.case_sensitive)
+            scope.add(None, p.output)
+            p = L.Sort([L.SortOrder(self.resolve(e, scope), a) for e, a in orders], True, p)
+        if limit is not None:
+            p = L.Limit(limit, p)
         return p
 
+    def order_limit(self):
+        """A trailing ``ORDER BY ... [LIMIT n]``: ([(expression, ascending)], limit or None)."""
+        orders = []
+        if self.accept("kw", "ORDER"):
+            self.expect("kw", "BY")
+            orders = [self.order_item()]
+            while self.accept("op", ","):
+                orders.append(self.order_item())
+        limit = None
+        if self.accept("kw", "LIMIT"):
+            kind, t = self.take()
+            if kind != "num":
+                raise SyntaxError("LIMIT needs a number")
+            limit = int(t)
+        return orders, limit
+
     # -- SELECT ------------------------------------------------------------------------------
-    def select(self) -> L.LogicalPlan:
+    def select(self, tail: bool = True) -> L.LogicalPlan:
+        """One SELECT; ``tail``: with its ORDER BY / LIMIT (False inside a UNION chain, whose
+        trailing ORDER BY / LIMIT ``query`` applies to the whole union)."""
         if self.accept("op", "("):
             p = self.query()
             self.expect("op", ")")
@@ -130,18 +175,7 @@ class SqlPlanner(_Parser):
         having = None
         if self.accept("kw", "HAVING"):
             having = self.or_expr()
-        orders = []
-        if self.accept("kw", "ORDER"):
-            self.expect("kw", "BY")
-            orders = [self.order_item()]
-            while self.accept("op", ","):
-                orders.append(self.order_item())
-        limit = None
-        if self.accept("kw", "LIMIT"):
-            kind, t = self.take()
-            if kind != "num":
-                raise SyntaxError("LIMIT needs a number")
-            limit = int(t)
+        orders, limit = self.order_limit() if tail else ([], None)
         plan = self.project(plan, scope, items, grouping, having, orders, distinct)
         if limit is not None:
             plan = L.Limit(limit, plan)
@@ -179,8 +213,18 @@ class SqlPlanner(_Parser):
         else:
             self.accept("kw", "ASC")
         if self.accept("kw", "NULLS"):
-            if not (self.accept("kw", "FIRST") or self.accept("kw", "LAST")):
+            if self.accept("kw", "FIRST"):
+                first = True
+            elif self.accept("kw", "LAST"):
+                first = False
+            else:
                 raise SyntaxError("NULLS FIRST | LAST")
+            # SortOrder carries Spark's default null ordering only (ASC NULLS FIRST, DESC NULLS
+            # LAST): an explicit other one must not be silently dropped
+            if first != asc:
+                raise HyperspaceException(
+                    f"ORDER BY ... {'ASC' if asc else 'DESC'} NULLS {'FIRST' if first else 'LAST'}"
+                    f" is not supported (only the default null ordering)")
         return e, asc
 
     # -- FROM --------------------------------------------------------------------------------

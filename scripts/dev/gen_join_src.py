@@ -59,16 +59,8 @@ def main(out):
         p, comp, keep = q3_params(ng)
         W = jit_runs.tag_width(p)
         NI = jit_runs.RS_ITEMS
-        from hyperspace_amd.exec.encoding import grouped16
-        t16 = dict(comp)
-        t16[p.rkey] = grouped16(comp[p.rkey], 1.0)
-        comp[0].keys16(1.0)
         ks = [jit_runs.gen_run_tags2(p, comp, W), jit_runs.gen_run_scan(p, comp, W, NI)]
-        k2 = jit_runs.gen_run_tags2(p, t16, W, True)
-        k2.name = "hs_jit_run_tags2_k16"
-        ks.append(k2)
         if W == 1 and not (p.group_col >= 8 and p.num_groups > 1):
-            ks.append(jit_runs.gen_run_scan_rows(p, comp, NI))
             ks.append(jit_runs.gen_run_sparse_scan(p, comp))
             # hash walk grouped by the left key (the functionally reduced Q3 GROUP BY)
             from hyperspace_amd.exec import hash_agg as H

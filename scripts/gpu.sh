@@ -106,6 +106,38 @@ step_configs() {
   done
 }
 
+step_qk() {
+  # query-kernel sweep: QK_CONFIGS (JSON list of kernel_config fields), QK_ARGS (e.g. --only-merge)
+  local cfg="$QK_CONFIGS"
+  [ -z "$cfg" ] && cfg='[{}]'
+  timeout -k 10 ${QK_TIMEOUT:-600} python3 scripts/qk_sweep.py --sf ${SF:-100} --reps ${REPS:-20} \
+    --configs "$cfg" ${QK_ARGS} > "${O}_qk.jsonl" 2> "${O}_qk.log"
+}
+
+step_qkprof() {
+  # kernel trace of a query-kernel sweep (QK_CONFIGS, QK_ARGS); per-kernel durations of the
+  # hs_jit_ kernels in dispatch order (config i's dispatches follow config i-1's)
+  local cfg="$QK_CONFIGS"
+  [ -z "$cfg" ] && cfg='[{}]'
+  case "$cfg" in @/*) ;; @*) cfg="@$REPO/${cfg#@}" ;; esac   # the profiler runs from /tmp
+  (cd /tmp && export TMPDIR=/tmp &&
+   timeout -k 10 ${QK_TIMEOUT:-600} rocprofv3 --kernel-trace --output-format csv -d "${O}_qkprof" \
+     -o run -- python3 "$REPO/scripts/qk_sweep.py" --sf ${SF:-100} --reps ${REPS:-20} \
+     --configs "$cfg" --no-profile ${QK_ARGS} > "${O}_qkprof.jsonl" 2> "${O}_qkprof.log") || return $?
+  local f
+  f=$(find "${O}_qkprof" -name "*kernel_trace.csv" | head -n 1)
+  python3 -c "
+import csv, sys
+w = csv.writer(open(sys.argv[2], 'w'))
+w.writerow(['name', 'start', 'end', 'vgpr', 'lds', 'grid'])
+for x in csv.DictReader(open(sys.argv[1])):
+    if x['Kernel_Name'].startswith('hs_'):
+        w.writerow([x['Kernel_Name'][:48], x['Start_Timestamp'], x['End_Timestamp'],
+                    x.get('VGPR_Count', ''), x.get('LDS_Block_Size', ''), x.get('Grid_Size', '')])
+" "$f" "${O}_qk_ktrace.csv"
+  rm -rf "${O}_qkprof"
+}
+
 step_q3f() {
   local cfg="$Q3F_CONFIGS"
   [ -z "$cfg" ] && cfg='[{}]'

@@ -201,10 +201,10 @@ def test_spmd_device_executor(tmp_path, spmd_data, device):
 
 def test_bench_two_ranks_reports_both_placements(tmp_path):
     """bench.py under torch.distributed (2 gloo ranks, host engine, tiny scale factor): one JSON
-    line from rank 0 with the replicated (weak scaling: one query stream per rank over read
-    replicas) headline value and the sharded numbers (strong scaling: one query stream over
-    co-partitioned buckets) as a side key, and the indexed results cross-checked against the
-    un-indexed plan."""
+    line from rank 0 with the sharded (strong scaling: one query stream over co-partitioned
+    buckets, the same placement and label as at N = 1) headline value and the replicated numbers
+    (weak scaling: one query stream per rank over read replicas) as a side key, and the indexed
+    results cross-checked against the un-indexed plan."""
     import json
     import subprocess
     import sys
@@ -219,9 +219,9 @@ def test_bench_two_ranks_reports_both_placements(tmp_path):
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
-    assert out["config"]["placement"] == "replicated" and out["scaling"] == "weak"
+    assert out["config"]["placement"] == "sharded" and out["scaling"] == "strong"
     assert out["config"]["parallelism"] == "cpu-host"
-    assert out["sharded"]["scaling"] == "strong" and out["sharded"]["value"] > 0
+    assert out["replicated"]["scaling"] == "weak" and out["replicated"]["value"] > 0
     assert "bytes_over_xgmi" in out
     assert out["steps"] == 2 and out["crosscheck"]["index_vs_full_scan_match"]
 

@@ -150,3 +150,36 @@ def test_temp_view_lifecycle(env):
     assert "v" in s.catalog.listTables()
     assert s.catalog.dropTempView("V")
     assert not s.catalog.tableExists("v")
+
+
+def test_union_order_by_limit_apply_to_the_whole_union(env):
+    """A trailing ORDER BY / LIMIT after a UNION chain orders and limits the union's rows (as in
+    Spark), not the last branch; a parenthesized branch keeps its own ORDER BY / LIMIT."""
+    s, _, src = env
+    t = s.read.parquet(src)
+    t.createOrReplaceTempView("t")
+    full = sample_table().to_pylist()
+    clicks = sorted((r["clicks"] for r in full), reverse=True)
+    got = s.sql("SELECT c5 FROM t WHERE c5 < 300 UNION ALL SELECT c5 FROM t WHERE c5 >= 300 "
+                "ORDER BY c5 DESC LIMIT 4").collect()
+    assert [r[0] for r in got] == clicks[:4]
+    inner = s.sql("SELECT c5 FROM t UNION ALL (SELECT c5 FROM t ORDER BY c5 LIMIT 1)").collect()
+    assert len(inner) == len(full) + 1
+    # only Spark's default null ordering is representable: a different one is refused, not lost
+    assert s.sql("SELECT c5 FROM t ORDER BY c5 ASC NULLS FIRST LIMIT 1").collect()
+    with pytest.raises(HyperspaceException):
+        s.sql("SELECT c5 FROM t ORDER BY c5 ASC NULLS LAST")
+
+
+def test_overwrite_of_a_table_read_by_the_written_data_is_refused(env):
+    s, _, src = env
+    s.read.parquet(src).select("c1", "c5").write.saveAsTable("t1")
+    n = len(s.table("t1").collect())
+    with pytest.raises(HyperspaceException):
+        s.table("t1").filter("c5 > 0").write.mode("overwrite").saveAsTable("t1")
+    assert len(s.table("t1").collect()) == n          # the table survived
+    with pytest.raises(HyperspaceException):
+        s.read.parquet(src).write.saveAsTable("../escape")
+    with pytest.raises(HyperspaceException):
+        s.catalog.dropTable("a/b")
+    assert not s.catalog.tableExists("../escape")
