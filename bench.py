@@ -561,9 +561,12 @@ def _side_configs(args, sf) -> dict:
     ns = _ap.Namespace(data_dir=args.data_dir, device="gpu", buckets=args.buckets,
                        steps=max(args.steps, 10), sf=sf)
     out = {}
+    from hyperspace_amd.exec.gpu import release_process_device_memory
     for name, fn in (("q3_3way", CF.config_q3_3way), ("hybrid", CF.config_hybrid)):
         t0 = time.perf_counter()
         try:
+            # each config runs in sessions of its own: free what the earlier ones hold in HBM
+            release_process_device_memory()
             r = fn(ns)
             if name == "q3_3way":
                 out[name] = {"q3_3way_ms": r["q3_3way_ms"], "value": r["queries_per_s"],

@@ -18,6 +18,8 @@ against the same query with Hyperspace disabled (the reference's correctness ora
   refreshed index.
 * ``q3_3way`` — the TPC-H Q3 three-way join customer ⋈ orders ⋈ lineitem (JoinIndexRule on the
   customer/orders join, device shuffle of the intermediate onto the lineitem index layout).
+* ``streamed`` — the SF-N index set built and queried under small HBM budgets (default 8 GB)
+  against the resident run: bucket-range build passes and streamed queries.
 * ``tpcds_3way`` — BASELINE config #5: TPC-DS-shaped ``store_sales`` ⋈ ``item`` ⋈ ``date_dim``
   (``hyperspace_amd.models.tpcds``, SF300 = 864M fact rows by default, ``--tpcds-sf``) with
   covering indexes on all three tables; queries, then +10% appended fact files and an
@@ -355,6 +357,75 @@ def config_q3_3way(args):
             "semi_join": semi}
 
 
+def config_streamed(args):
+    """SURVEY §5.7 / BASELINE config #5's "beyond one GPU's HBM": the bench's SF-N index set
+    built and queried under small HBM budgets (``--hbm-budget-gb``, default 8 GB for the build
+    working set, ``build.hbmBudgetBytes``, and for resident index tables, ``deviceCacheBytes``)
+    against the resident run on the same files: a build in bucket-range passes (GB/s), then Q6
+    and Q3 that stream their index scans bucket range by bucket range (q/s).  Every streamed
+    result must equal the resident one (itself the engine's oracle-checked path)."""
+    from hyperspace_amd import Hyperspace, IndexConfig
+    sf = args.sf
+    data, _ = _tpch(args, sf)
+    budget = int(args.hbm_budget_gb * (1 << 30))
+    li_cfgs = (IndexConfig("li_shipdate", ["l_shipdate"],
+                           ["l_discount", "l_quantity", "l_extendedprice"]),
+               IndexConfig("li_orderkey", ["l_orderkey"],
+                           ["l_extendedprice", "l_discount", "l_shipdate"]))
+    od_cfg = IndexConfig("ord_orderkey", ["o_orderkey"], ["o_orderdate", "o_shippriority"])
+    out = {"config": "streamed", "device": args.device, "sf": sf,
+           "hbm_budget_gb": args.hbm_budget_gb}
+    results = {}
+    for mode in ("resident", "streamed"):
+        root = os.path.join(args.data_dir, f"cfg_stream_{mode}")
+        shutil.rmtree(root, ignore_errors=True)
+        extra = {}
+        if mode == "streamed":
+            extra = {"spark.hyperspace.mi.build.hbmBudgetBytes": str(budget)}
+        s = _session(root, args.device, args.buckets, **extra)
+        hs = Hyperspace(s)
+        li = s.read.parquet(os.path.join(data, "lineitem"))
+        od = s.read.parquet(os.path.join(data, "orders"))
+        from hyperspace_amd.exec import device_build
+        bt, bb, passes = 0.0, 0, {}
+        for df, cfg in ((li, li_cfgs[0]), (li, li_cfgs[1]), (od, od_cfg)):
+            dt, nb = _build(hs, df, cfg, args.device)
+            bt += dt
+            bb += nb
+            passes[cfg.indexName] = device_build.LAST_BUILD_STATS.get("passes", 1)
+        if mode == "streamed":
+            s.conf.set("spark.hyperspace.mi.deviceCacheBytes", str(budget))
+        Hyperspace.enable(s)
+
+        def step(i):
+            _q6(li, i).collect()
+            _q3(li, od, i).collect()
+        for i in range(2):
+            step(1000 + i)
+        be = s.backend()
+        el = _timed_loop(step, args.steps, args.device)
+        res = [(_q6(li, i).collect()[0][0], _rows(_q3(li, od, i))) for i in range(3)]
+        results[mode] = res
+        out[mode] = {"queries_per_s": round(2 * args.steps / el, 2),
+                     "index_build_s": round(bt, 3),
+                     "index_build_gbps": round(bb / bt / 1e9, 3) if bb else None,
+                     "build_passes": passes, "path": getattr(be, "last_path", None),
+                     "stream_passes": getattr(be, "last_stream_passes", None)}
+        # the next mode's session starts from an empty device
+        del s, hs, be
+        if args.device == "gpu":
+            from hyperspace_amd.exec.gpu import release_process_device_memory
+            release_process_device_memory()
+    a, b = results["resident"], results["streamed"]
+    out["match"] = all(abs(x[0] - y[0]) <= 1e-9 * abs(x[0]) and _close(x[1], y[1])
+                       for x, y in zip(a, b))
+    out["streamed_vs_resident_qps"] = round(out["streamed"]["queries_per_s"] /
+                                            out["resident"]["queries_per_s"], 3)
+    out["streamed_vs_resident_build"] = round(out["resident"]["index_build_s"] /
+                                              out["streamed"]["index_build_s"], 3)
+    return out
+
+
 # ------------------------------------------------------------------------------------ TPC-DS
 def _tpcds_query(ss, it, dd, i):
     """TPC-DS Q3-shaped star join: one manufacturer's items sold in one month of the year."""
@@ -449,7 +520,8 @@ def config_tpcds_3way(args):
 
 
 CONFIGS = {"csv10k": config_csv10k, "sf10_filter": config_sf10_filter, "hybrid": config_hybrid,
-           "q3_3way": config_q3_3way, "tpcds_3way": config_tpcds_3way}
+           "q3_3way": config_q3_3way, "tpcds_3way": config_tpcds_3way,
+           "streamed": config_streamed}
 
 
 def main():
@@ -461,6 +533,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--data-dir", default=os.environ.get("HS_BENCH_DIR", "/tmp/hs_bench"))
     ap.add_argument("--tpcds-sf", type=float, default=300.0)
+    ap.add_argument("--hbm-budget-gb", type=float, default=8.0,
+                    help="streamed: the build and resident-table HBM budgets")
     args = ap.parse_args()
     if args.device == "gpu":
         import torch

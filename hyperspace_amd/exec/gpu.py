@@ -24,6 +24,7 @@ keeps the query entry points, relations, scans and row output."""
 from __future__ import annotations
 
 import time
+import weakref
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -53,6 +54,29 @@ from .gpu_semi import SemiJoinOps
 from .gpu_common import _strip_exchange, bucket_chunks  # noqa: F401
 
 
+# every live backend of the process (release_process_device_memory)
+_BACKENDS: "weakref.WeakSet" = weakref.WeakSet()
+
+
+def release_process_device_memory() -> None:
+    """``GpuBackend.release_device_memory`` for every backend of the process plus the
+    process-wide derived caches (build seeds, cached two-phase lowerings, row-packed aggregate
+    inputs), then the caching allocator's free blocks: sessions created one after another in
+    one process (e.g. ``bench.py``'s side configs) each size their cache for the whole device."""
+    import torch
+    from . import device_cache, jit_join, jit_runs
+    for be in list(_BACKENDS):
+        be.release_device_memory()
+    device_cache.clear_seeds()
+    jit_join._RUNS_LOWERED.clear()
+    jit_join._RUNS_HASH_LOWERED.clear()
+    jit_runs._PACKS.clear()
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
 class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
     name = "gpu"
     # QueryExecution may submit a plan-cache entry's own plan with a query's literals bound in
@@ -63,6 +87,7 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
         import torch
         NL.lib()  # fail loudly if the kernels are not built
         self.session = session
+        _BACKENDS.add(self)
         # the generated kernels' tunables: spark.hyperspace.mi.kernel.* over HS_JIT_* over the
         # measured defaults (exec/kernel_config.py)
         from . import kernel_config
@@ -96,6 +121,20 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
         pool.limit = min(pool.limit, self.budget.pinned)
         pool.reserve(count=max(1, min(32, pool.limit // (2 * _RESERVE_BLOCK))))
         self._engine_start()
+
+    def release_device_memory(self) -> None:
+        """Drop everything this backend keeps resident in HBM - index tables, derived join
+        indexes and packed columns (with the tables), captured graphs, prepared lowerings - so
+        another session of the same process can use the device.  The next query reloads."""
+        import torch
+        torch.cuda.synchronize(self.device)
+        self.cache.clear()
+        self._programs.clear()
+        self.graphs._lru.clear()
+        for k in ("_agg_preps", "_stream_memo", "_side"):
+            self.__dict__.pop(k, None)
+        from .hash_agg import TablePool
+        self.htables = TablePool()
 
     def _engine_start(self) -> None:
         """Bring the engine up once, outside any query or build: the HBM arena (one large
@@ -1008,4 +1047,4 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
         return pa.Table.from_arrays(arrays, names=[a.name for a in out_attrs])
 
 
-__all__ = ["GpuBackend", "QueryFuture", "DRel", "bucket_chunks"]
+__all__ = ["GpuBackend", "QueryFuture", "DRel", "bucket_chunks", "release_process_device_memory"]

@@ -881,7 +881,9 @@ class AggOps:
         import torch
         s = getattr(self, "_side", None)
         if s is None:
-            s = self._side = torch.cuda.Stream(device=self.device)
+            s = self._side = torch.cuda.Stream(
+                device=self.device,
+                priority=HyperspaceConf.side_stream_priority(self.session.conf))
         g.on_side = True
         g.side_stream = s
         return s

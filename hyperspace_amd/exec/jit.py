@@ -319,6 +319,38 @@ __device__ __forceinline__ void bload(__amdgpu_buffer_rsrc_t r, unsigned off, un
     x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
   }
 }
+// the same window read lane-coalesced: instruction k of the wavefront covers 1 KB contiguous
+// (lane l: 16 bytes at (64 k + l) * 16), so lane l holds 16-byte chunks of other lanes' rows;
+// hs_lds_t then moves every chunk to its owner through the wavefront's LDS slab (chunk j of
+// lane g at slot g * NJ + (j ^ (g % NJ)): both the stores and the loads hit distinct banks)
+template <int NW>
+__device__ __forceinline__ void bload_t(__amdgpu_buffer_rsrc_t r, int ln, unsigned (&x)[NW]) {
+  static_assert(NW % 4 == 0, "bload_t: whole dwordx4s");
+#pragma unroll
+  for (int k = 0; k < NW / 4; ++k) {
+    const hs_v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)((64 * k + ln) * 16), 0, 0);
+    x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+  }
+}
+template <int NW>
+__device__ __forceinline__ void hs_lds_t(hs_v4u* slab, int ln, unsigned (&x)[NW]) {
+  constexpr int NJ = NW / 4;
+#pragma unroll
+  for (int k = 0; k < NJ; ++k) {
+    const int c = 64 * k + ln, g = c / NJ, j = c % NJ;
+    hs_v4u v; v.x = x[4 * k]; v.y = x[4 * k + 1]; v.z = x[4 * k + 2]; v.w = x[4 * k + 3];
+    slab[g * NJ + (j ^ (g % NJ))] = v;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const hs_v4u v = slab[ln * NJ + (j ^ (ln % NJ))];
+    x[4 * j] = v.x; x[4 * j + 1] = v.y; x[4 * j + 2] = v.z; x[4 * j + 3] = v.w;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 __device__ __forceinline__ void lds_min(double* p, double v) {
   u64* a = (u64*)p; u64 old = *a, as;
   do { as = old; if (__longlong_as_double((i64)as) <= v) break;

@@ -37,7 +37,7 @@ _CFG = _KC.active()
 MJ_2P, RS_ITEMS = _CFG.mj_2p, _CFG.rs_items
 RT2_UNROLL, RT2_GRID = _CFG.rt2_unroll, _CFG.rt2_grid
 RS_BITS, RS_BITS_GRID, RS_PACK = _CFG.rs_bits, _CFG.rs_bits_grid, _CFG.rs_pack
-RS_PIPE, RS_WALK = _CFG.rs_pipe, _CFG.rs_walk
+RS_PIPE, RS_WALK, RS_LDS = _CFG.rs_pipe, _CFG.rs_walk, _CFG.rs_lds
 
 
 def tag_width(p: NL.JoinParams) -> int:
@@ -466,7 +466,7 @@ def packed_tail(layout, compacts):
 
 
 def sparse_shape(p: NL.JoinParams, compacts, hk=None, tk=None) -> tuple:
-    return ("run_bits_scan", RS_PIPE, RS_WALK) + scan_shape(p, compacts, 1, 64)[1:] + \
+    return ("run_bits_scan", RS_PIPE, RS_WALK, RS_LDS) + scan_shape(p, compacts, 1, 64)[1:] + \
         (pack_layout(p, compacts),) + ((hk.shape(),) if hk is not None else ()) + \
         ((tk.shape(),) if tk is not None else ())
 
@@ -575,6 +575,8 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
     g1 = J._Gen(args, cols, SPLIT, ("row0", "row0"), approx, True)
     elem = {}   # array name -> C expression of element (idx) from its packed 32-bit words
     issue = []  # the current tile's (C) tag-word and predicate-column loads into buffer @S@
+    xpose = []  # RS_LDS: the loaded columns' chunks moved to their rows' lanes
+    slab = 0    # RS_LDS: 16-byte LDS slots per wavefront
     issue.append("    { const i64 w_ = (i64)grC >> 5; tw0@S@_ = a.tags[w_]; "
                  "tw1@S@_ = a.tags[w_ + 1]; tw2@S@_ = a.tags[w_ + 2]; }")
     for name, ct, ptr in J._vec_loads(g1, pslots):
@@ -584,8 +586,15 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
         b.append(f"  unsigned {name}wA[{nw}], {name}wB[{nw}];")
         # the group's rows past the table end read as 0 (buffer range check); they are outside
         # every row range, so the range mask drops them
-        issue.append(f"    bload<{nw}>(hs_rsrc((const char*){ptr} + tbC * {es}, "
-                     f"@LIVE@(a.nrows - tbC) * {es}), (unsigned)(64 * ln * {es}), {name}w@S@);")
+        if RS_LDS:
+            issue.append(f"    bload_t<{nw}>(hs_rsrc((const char*){ptr} + tbC * {es}, "
+                         f"@LIVE@(a.nrows - tbC) * {es}), ln, {name}w@S@);")
+            xpose.append(f"    hs_lds_t<{nw}>(&xt_[wq][0], ln, {name}w@S@);")
+            slab = max(slab, nw // 4 * 64)
+        else:
+            issue.append(f"    bload<{nw}>(hs_rsrc((const char*){ptr} + tbC * {es}, "
+                         f"@LIVE@(a.nrows - tbC) * {es}), (unsigned)(64 * ln * {es}), "
+                         f"{name}w@S@);")
         elem[name] = (ct, f"{name}w@S@[({{i}}) / {per}]" if per > 1 else f"{name}w@S@[{{i}}]",
                       8 * es, per)
 
@@ -635,6 +644,16 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
              "    d_ ^= d_ << 1; d_ ^= d_ << 2; d_ ^= d_ << 4; d_ ^= d_ << 8; d_ ^= d_ << 16; "
              "d_ ^= d_ << 32;",
              "    d_ &= am;"]
+    if xpose:
+        # the transpose slab and the passing-row list share the LDS: a tile's list is built
+        # after its columns left the slab, and walked before the next tile's transpose
+        lst_i = next(i for i, x in enumerate(b) if "__shared__ unsigned short lst_" in x)
+        nslot = max(slab, (CAP * 2 + 15) // 16)
+        # lst_[w] = wavefront w's own slab, seen as 16-bit entries
+        b[lst_i:lst_i + 1] = [
+            f"  __shared__ hs_v4u xt_[{WV}][{nslot}];",
+            f"  unsigned short (*lst_)[{nslot * 8}] = (unsigned short (*)[{nslot * 8}])&xt_[0][0];"]
+        body += xpose
     # predicate mask: 64 compares, shift-or into two 32-bit halves (a C loop: each row's
     # value is decoded where it is compared, not all 64 held decoded at once)
     body.append("    unsigned plo_ = 0u, phi_ = 0u;")

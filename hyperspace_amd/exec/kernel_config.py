@@ -77,9 +77,12 @@ class KernelConfig:
     rs_bits: bool = True         # phase 2 bit-parallel for 1-bit tags (gen_run_sparse_scan)
     rs_bits_grid: int = 8192
     rs_pack: bool = True         # bits scan reads its aggregate inputs row-packed
-    rs_pipe: int = 1             # bits scan software pipeline: 0 off (two round trips per tile,
-                                 # fewest registers), 1 one buffer, 2 two named buffers (unroll 2)
+    rs_pipe: int = 0             # bits scan software pipeline: 0 off (two round trips per tile,
+                                 # fewest registers), 1 one buffer, 2 two named buffers (unroll 2);
+                                 # SF100: 358 / 363 / 391 us (profiles/bits_scan_variants_r6.txt)
     rs_walk: int = 4             # bits scan list entries per lane per walk pass
+    rs_lds: bool = False         # bits scan predicate columns loaded lane-coalesced, then moved
+                                 # to their rows' lanes through LDS (else one 128 B run per lane)
     # --- shared ------------------------------------------------------------------------------
     vec_prefetch: bool = True    # software-pipelined full tiles of the vectorized kernels
     wave_sync: bool = True       # per-wavefront lists ordered by a wavefront barrier
@@ -137,13 +140,17 @@ def bind(cfg: KernelConfig) -> None:
     names) are set from it.  Compiled kernels are keyed by shape tuples that include those
     constants, so switching needs no cache flush for correctness."""
     global _active
-    from . import jit, jit_runs
+    from . import jit, jit_join, jit_runs
     with _lock:
         for name, v in dataclasses.asdict(cfg).items():
             up = name.upper()
             for mod in (jit, jit_runs):
                 if up in mod.__dict__:
                     setattr(mod, up, v)
+        if cfg != _active:
+            # lowerings cached by query shape hold the previous configuration's kernels
+            jit_join._RUNS_LOWERED.clear()
+            jit_join._RUNS_HASH_LOWERED.clear()
         _active = cfg
 
 

@@ -256,7 +256,8 @@ class DistContext:
         cnt = torch.tensor([n], dtype=torch.int64, device=dev)
         counts = [torch.zeros_like(cnt) for _ in range(self.world)]
         dist.all_gather(counts, cnt)
-        counts = [int(c.item()) for c in counts]
+        # one device -> host read of all the counts (not one ``.item()`` sync per rank)
+        counts = torch.cat(counts).cpu().tolist()
         mx = max(counts)
         if mx == 0:
             return np.zeros((0, w), dtype=np.int64)

@@ -146,6 +146,14 @@ class HyperspaceConf:
         return _b(conf.get(C.SIDE_STREAM_SCANS, C.SIDE_STREAM_SCANS_DEFAULT))
 
     @staticmethod
+    def side_stream_priority(conf) -> int:
+        """torch stream priority of the scan side stream (-1 high, 0 normal)."""
+        v = str(conf.get(C.SIDE_STREAM_PRIORITY, C.SIDE_STREAM_PRIORITY_DEFAULT)).lower()
+        if v not in ("high", "normal"):
+            raise ValueError(f"{C.SIDE_STREAM_PRIORITY} must be high or normal, got {v}")
+        return -1 if v == "high" else 0
+
+    @staticmethod
     def index_placement(conf) -> str:
         v = str(conf.get(C.INDEX_PLACEMENT, C.INDEX_PLACEMENT_DEFAULT)).lower()
         if v not in ("sharded", "replicated"):

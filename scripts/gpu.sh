@@ -138,6 +138,19 @@ for x in csv.DictReader(open(sys.argv[1])):
   rm -rf "${O}_qkprof"
 }
 
+step_pmcbench() {
+  # one counter pass (PMC_COUNTERS) over the SF100 bench, counters on PMC_REGEX kernels only
+  (cd /tmp && export TMPDIR=/tmp &&
+   timeout -s KILL ${PMC_TIMEOUT:-600} rocprofv3 --pmc ${PMC_COUNTERS:-FETCH_SIZE} \
+     --kernel-include-regex "${PMC_REGEX:-hs_jit_run_bits_scan}" --kernel-trace --output-format csv \
+     -d "${O}_pmcb" -o pmc -- python3 "$REPO/bench.py" --sf ${SF:-100} --steps 2 --warmup 1 \
+     --no-crosscheck --no-side > "${O}_pmcb.json" 2> "${O}_pmcb.log") || return $?
+  find "${O}_pmcb" -name "*counter_collection.csv" -exec cp {} "${O}_pmcb_counters.csv" \;
+  find "${O}_pmcb" -name "*kernel_trace.csv" -exec cp {} "${O}_pmcb_trace.csv" \;
+  rm -rf "${O}_pmcb"
+  python3 scripts/pmc_summary.py "${O}_pmcb_counters.csv" "${O}_pmcb_trace.csv" > "${O}_pmcb_summary.txt" 2>&1 || true
+}
+
 step_q3f() {
   local cfg="$Q3F_CONFIGS"
   [ -z "$cfg" ] && cfg='[{}]'
