@@ -298,6 +298,32 @@ __device__ __forceinline__ void vload(const T* __restrict__ p, long long i, T (&
 // ``nbytes`` - so the table's last, partial group loads with the same dwordx4s as a full one
 // instead of a per-element edge path (which doubled the kernel's register footprint)
 typedef unsigned hs_v4u __attribute__((ext_vector_type(4)));
+// two 16-bit codes' range test at once: per half, (x - lo) | (hi - x) with saturation (the
+// sign survives clamping), so bits 15 and 31 are the two rows' fail bits
+typedef short hs_s2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned hs_rng2(unsigned x, int lo, int hi) {
+  const hs_s2 v = __builtin_bit_cast(hs_s2, x);
+  const hs_s2 l = {(short)lo, (short)lo}, h = {(short)hi, (short)hi};
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(v, l)) |
+         __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(h, v));
+}
+// [lo, hi] clamped to int16 for hs_rng2: a range wholly outside int16 becomes the empty
+// (32767, -32768), which every code fails (clamping it bound by bound would keep an endpoint)
+__device__ __forceinline__ int hs_c16lo(long long lo, long long hi) {
+  return (hi < -32768ll || lo > 32767ll) ? 32767 : (int)(lo < -32768ll ? -32768ll : lo);
+}
+__device__ __forceinline__ int hs_c16hi(long long lo, long long hi) {
+  return (hi < -32768ll || lo > 32767ll) ? -32768 : (int)(hi > 32767ll ? 32767ll : hi);
+}
+// bits 0..15 of x to the even, 16..31 to the odd positions (row order of a 2-rows-per-word mask)
+__device__ __forceinline__ unsigned hs_unzip16(unsigned x) {
+  unsigned a = x & 0xFFFFu, b = x >> 16;
+  a = (a | (a << 8)) & 0x00FF00FFu; a = (a | (a << 4)) & 0x0F0F0F0Fu;
+  a = (a | (a << 2)) & 0x33333333u; a = (a | (a << 1)) & 0x55555555u;
+  b = (b | (b << 8)) & 0x00FF00FFu; b = (b | (b << 4)) & 0x0F0F0F0Fu;
+  b = (b | (b << 2)) & 0x33333333u; b = (b | (b << 1)) & 0x55555555u;
+  return a | (b << 1);
+}
 // a code bound clamped to +-2^20: narrow (<= 16-bit) codes against it never overflow int32
 __device__ __forceinline__ int hs_c20(long long v) {
   return (int)(v < -1048576ll ? -1048576ll : (v > 1048576ll ? 1048576ll : v));
@@ -529,6 +555,43 @@ class _Gen:
         if op == NL.OP_NE:
             s = f"(~{s})"
         return f"({s} | ((int){self.ok(c)} - 1))" if hv else s
+
+    def cnf_sign2(self, preds: List[Tuple[int, NL.Pred]], word: str) -> Optional[str]:
+        """``cnf_sign`` over two rows at once for 16-bit signed codes without validity: the
+        dword ``word.format(slot)`` holds both rows' codes, the result's bits 15 / 31 are their
+        fail bits (``hs_rng2``).  None when a leaf has no such form."""
+        groups: Dict[int, List[str]] = {}
+        order: List[int] = []
+        for k, p in preds:
+            kind, op = p.kind, p.op
+            if kind == NL.PK_TRUE:
+                leaf = "0u"
+            else:
+                c = p.col
+                if self.cols[c][1] or self.raw_type(c) != "short":
+                    return None
+                enc = self.cols[c][2]
+                if kind == NL.PK_NOT_NULL:
+                    leaf = "0u"
+                elif kind == NL.PK_IS_NULL:
+                    leaf = "0xFFFFFFFFu"
+                elif self.intpred and enc and (kind == NL.PK_INT_LIT and not enc[1] or
+                                               kind == NL.PK_FLT_LIT and enc[1]):
+                    lo = self.a.add("q", f"CL{k}", "long long")
+                    hi = self.a.add("q", f"CH{k}", "long long")
+                    leaf = (f"hs_rng2({word.format(c)}, hs_c16lo({lo}, {hi}), "
+                            f"hs_c16hi({lo}, {hi}))")
+                    if op == NL.OP_NE:
+                        leaf = f"(~{leaf})"
+                else:
+                    return None
+            if p.group not in groups:
+                groups[p.group] = []
+                order.append(p.group)
+            groups[p.group].append(leaf)
+        if not order:
+            return "0u"
+        return "(" + " | ".join("(" + " & ".join(groups[g]) + ")" for g in order) + ")"
 
     def cnf_sign(self, preds: List[Tuple[int, NL.Pred]]) -> Optional[str]:
         """``cnf`` as a sign word (negative iff the row fails), or None: a group (OR) fails

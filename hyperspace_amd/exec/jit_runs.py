@@ -35,9 +35,10 @@ SPLIT = 8
 from . import kernel_config as _KC  # noqa: E402
 _CFG = _KC.active()
 MJ_2P, RS_ITEMS = _CFG.mj_2p, _CFG.rs_items
-RT2_UNROLL, RT2_GRID = _CFG.rt2_unroll, _CFG.rt2_grid
+RT2_UNROLL, RT2_GRID, RT2_I32 = _CFG.rt2_unroll, _CFG.rt2_grid, _CFG.rt2_i32
 RS_BITS, RS_BITS_GRID, RS_PACK = _CFG.rs_bits, _CFG.rs_bits_grid, _CFG.rs_pack
-RS_PIPE, RS_WALK, RS_LDS = _CFG.rs_pipe, _CFG.rs_walk, _CFG.rs_lds
+RS_PIPE, RS_WALK, RS_LDS, RS_LUT = _CFG.rs_pipe, _CFG.rs_walk, _CFG.rs_lds, _CFG.rs_lut
+RS_PK16 = _CFG.rs_pk16
 
 
 def tag_width(p: NL.JoinParams) -> int:
@@ -76,13 +77,13 @@ def _lpreds(p):
 # phase 1: 64-run groups per unrolled iteration of a wavefront (gen_run_tags2)
 
 
-def tags2_shape(p: NL.JoinParams, compacts, W: int) -> tuple:
+def tags2_shape(p: NL.JoinParams, compacts, W: int, ix32: bool = False) -> tuple:
     cols = tuple(sorted((s, c) for s, c in J._col_specs(p, compacts).items()
                         if s >= SPLIT or s == p.lkey))
     preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
                    p.preds[k].group) for k in range(p.nlp, p.npreds))
     return ("run_tags2", cols, preds, p.nlp, p.lkey, p.rkey, _tags_grouped(p) and p.group_col,
-            W, RT2_UNROLL, J.BLOCK)
+            W, RT2_UNROLL, J.BLOCK, ix32)
 
 
 def _stage_slots(p: NL.JoinParams) -> list:
@@ -98,7 +99,7 @@ def _tags_grouped(p: NL.JoinParams) -> bool:
     return p.group_col >= SPLIT and p.num_groups > 1
 
 
-def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
+def gen_run_tags2(p: NL.JoinParams, compacts, W: int, ix32: bool = False) -> J.Kernel:
     """Phase 1, direct form: no tiles and no LDS.  Each wavefront owns a contiguous chunk of
     64-run groups of the left run list (so it owns whole 2W-word stretches of the tag bitmap
     and stores them without atomics).  Lane l of a group guesses the right row of its run: the
@@ -111,7 +112,13 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
 
     Ranges (``RNG``, NRG x 4 int64, sorted by first run): [first run, end run) of each left row
     range and the right bucket's rows [s0, s1).  (16-bit grouped run keys measured 0.59 vs
-    0.29 ms - more dependent loads per run - and a per-tile LDS form 0.79 ms: both removed.)"""
+    0.29 ms - more dependent loads per run - and a per-tile LDS form 0.79 ms: both removed.)
+
+    ``ix32``: run and right-row indices fit int32 (the lowering checks the table sizes), so the
+    index arithmetic, range clamps and gallop run in 32-bit registers and the column loads
+    address through a scalar base plus a 32-bit lane offset - the 64-bit index math was most of
+    the kernel's VALU instructions (``profiles/pmc_query_kernels_sf100_r6.txt``)."""
+    IX = "int" if ix32 else "i64"  # noqa: N806 — run / right-row index type
     args = J.Args()
     lk, rk = p.lkey, p.rkey
     args.add("p", f"RK{lk}", "const int*")
@@ -166,8 +173,8 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
                 f"gl_ < {ng}) ? (unsigned)(gl_ + 1) : 0u; }})")
 
     b: List[str] = [
-        f"  auto IMG = [&](i64 row_) -> unsigned {{ return {img}; }};",
-        f"  auto IMGF = [&](i64 row_) -> unsigned {{ return {imgf}; }};",
+        f"  auto IMG = [&]({IX} row_) -> unsigned {{ return {img}; }};",
+        f"  auto IMGF = [&]({IX} row_) -> unsigned {{ return {imgf}; }};",
         "  const int lane = (int)(threadIdx.x & 63);",
         "  const i64 G = (a.NRUNS + 63) >> 6;",
         f"  const i64 nwv = (i64)gridDim.x * {WV};",
@@ -184,13 +191,14 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
         "    while (hi - lo > 1) { const int m = (lo + hi) >> 1; "
         "if (RG[4 * m] <= r0) lo = m; else hi = m; }",
         "    rg = lo; }",
-        "  i64 lr0 = RG[4 * rg], lr1 = RG[4 * rg + 1], s0 = RG[4 * rg + 2], s1 = RG[4 * rg + 3];",
+        f"  {IX} lr0 = ({IX})RG[4 * rg], lr1 = ({IX})RG[4 * rg + 1], s0 = ({IX})RG[4 * rg + 2], "
+        f"s1 = ({IX})RG[4 * rg + 3];",
         "  i64 nxt0 = rg + 1 < a.NRG ? RG[4 * (rg + 1)] : 0x7fffffffffffffffll;",
-        "  i64 gbase = -1;   // right row of the next group's first run (-1: range-relative)",
+        f"  {IX} gbase = -1;   // right row of the next group's first run (-1: range-relative)",
         f"  for (i64 gi = gbeg; gi < gend; gi += {U}) {{",
         "    while (nxt0 <= (gi << 6)) {",
-        "      ++rg; lr0 = RG[4 * rg]; lr1 = RG[4 * rg + 1]; s0 = RG[4 * rg + 2];",
-        "      s1 = RG[4 * rg + 3]; gbase = -1;",
+        f"      ++rg; lr0 = ({IX})RG[4 * rg]; lr1 = ({IX})RG[4 * rg + 1]; s0 = ({IX})RG[4 * rg + 2];",
+        f"      s1 = ({IX})RG[4 * rg + 3]; gbase = -1;",
         "      nxt0 = rg + 1 < a.NRG ? RG[4 * (rg + 1)] : 0x7fffffffffffffffll; }",
         # wavefront-uniform: every run of this iteration's groups belongs to range rg (or none)
         f"    if (((gi + {U}) << 6) <= nxt0) {{"]
@@ -200,23 +208,23 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
         """Loads and guess of group u: unconditional (clamped) loads in the fast form, so all
         U groups' loads are in flight together (a load under a per-lane condition makes the
         compiler wait for it before the branches merge)."""
-        b.extend([f"{ind}const i64 r{u} = ((gi + {u}) << 6) + lane;",
+        b.extend([f"{ind}const {IX} r{u} = ({IX})(((gi + {u}) << 6) + lane);",
                   f"{ind}const bool in{u} = gi + {u} < gend;"])
         if fast:
-            b.append(f"{ind}const i64 l0_{u} = lr0, l1_{u} = lr1, a0_{u} = s0, a1_{u} = s1; "
+            b.append(f"{ind}const {IX} l0_{u} = lr0, l1_{u} = lr1, a0_{u} = s0, a1_{u} = s1; "
                      f"const bool own{u} = true;")
         else:
-            b.extend([f"{ind}i64 l0_{u} = lr0, l1_{u} = lr1, a0_{u} = s0, a1_{u} = s1; "
+            b.extend([f"{ind}{IX} l0_{u} = lr0, l1_{u} = lr1, a0_{u} = s0, a1_{u} = s1; "
                   f"bool own{u} = true;",
                   f"{ind}if (r{u} >= nxt0) {{ own{u} = false; int q_ = rg;",
                   f"{ind}  while (q_ + 1 < (int)a.NRG && RG[4 * (q_ + 1)] <= r{u}) ++q_;",
-                  f"{ind}  l0_{u} = RG[4 * q_]; l1_{u} = RG[4 * q_ + 1]; a0_{u} = RG[4 * q_ + 2]; "
-                  f"a1_{u} = RG[4 * q_ + 3]; }}"])
+                  f"{ind}  l0_{u} = ({IX})RG[4 * q_]; l1_{u} = ({IX})RG[4 * q_ + 1]; "
+                  f"a0_{u} = ({IX})RG[4 * q_ + 2]; a1_{u} = ({IX})RG[4 * q_ + 3]; }}"])
         b.extend([f"{ind}const bool act{u} = in{u} && r{u} < a.NRUNS && r{u} >= l0_{u} && "
               f"r{u} < l1_{u} && a1_{u} > a0_{u};",
               f"{ind}const unsigned key{u} = (unsigned)a.RK{lk}[act{u} ? r{u} : 0] + "
               f"(unsigned)a.KOF;",
-              f"{ind}i64 j{u} = (own{u} && gbase >= 0) ? gbase + {u * 64} + lane : "
+              f"{ind}{IX} j{u} = (own{u} && gbase >= 0) ? gbase + {u * 64} + lane : "
               f"a0_{u} + (r{u} - l0_{u});",
               f"{ind}j{u} = act{u} ? (j{u} < a0_{u} ? a0_{u} : (j{u} >= a1_{u} ? a1_{u} - 1 : j{u}))"
               f" : 0;",
@@ -228,29 +236,29 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
     def resolve(u: int, ind: str) -> None:
         gu = J._Gen(args, cols, SPLIT, (f"j{u}", f"j{u}"), frozenset(), True)
         b.extend([f"{ind}bool hit{u} = act{u} && k{u} == key{u};",
-                  f"{ind}i64 m{u} = j{u};",
+                  f"{ind}{IX} m{u} = j{u};",
                   f"{ind}unsigned tg{u} = {tag_expr(gu, f'g{u}', f'hit{u}')};",
                   f"{ind}if (act{u} && !hit{u}) {{",
                   # gallop from the guess to the lower bound of key in [a0, a1)
-                  f"{ind}  const unsigned key_ = key{u}; i64 lo_, hi_;",
+                  f"{ind}  const unsigned key_ = key{u}; {IX} lo_, hi_;",
                   f"{ind}  const unsigned kj_ = IMG(j{u});",
                   f"{ind}  if (kj_ == key_) {{ lo_ = j{u}; hi_ = j{u}; }}",
                   f"{ind}  else if (kj_ > key_) {{",
-                  f"{ind}    hi_ = j{u}; i64 st_ = 1; lo_ = j{u} - 1;",
+                  f"{ind}    hi_ = j{u}; {IX} st_ = 1; lo_ = j{u} - 1;",
                   f"{ind}    while (lo_ > a0_{u} && IMG(lo_) >= key_) {{ hi_ = lo_; st_ <<= 1; "
                   f"lo_ = hi_ - st_; }}",
                   f"{ind}    if (lo_ < a0_{u}) lo_ = a0_{u};",
                   f"{ind}  }} else {{",
-                  f"{ind}    lo_ = j{u} + 1; i64 st_ = 1; hi_ = j{u} + 1;",
+                  f"{ind}    lo_ = j{u} + 1; {IX} st_ = 1; hi_ = j{u} + 1;",
                   f"{ind}    while (hi_ < a1_{u} && IMG(hi_) < key_) {{ lo_ = hi_ + 1; st_ <<= 1; "
                   f"hi_ = j{u} + st_; }}",
                   f"{ind}    if (hi_ > a1_{u}) hi_ = a1_{u};",
                   f"{ind}  }}",
-                  f"{ind}  while (lo_ < hi_) {{ const i64 md_ = (lo_ + hi_) >> 1; "
+                  f"{ind}  while (lo_ < hi_) {{ const {IX} md_ = (lo_ + hi_) >> 1; "
                   f"if (IMG(md_) < key_) lo_ = md_ + 1; else hi_ = md_; }}",
                   f"{ind}  m{u} = lo_;",
                   f"{ind}  hit{u} = lo_ < a1_{u} && IMG(lo_) == key_;",
-                  f"{ind}  const i64 jm{u} = hit{u} ? lo_ : 0;"])
+                  f"{ind}  const {IX} jm{u} = hit{u} ? lo_ : 0;"])
         gm = J._Gen(args, cols, SPLIT, (f"jm{u}", f"jm{u}"), frozenset(), True)
         for sl in stage_slots:
             J._uload(gm, sl, f"h{u}", b, ind + "  ")
@@ -277,8 +285,8 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
         for u in range(U):
             resolve(u, ind)
         # next iteration's guess: the last group's last lane, when it matched in this range
-        b.extend([f"{ind}{{ const i64 nx_ = __shfl((hit{U - 1} && own{U - 1}) ? m{U - 1} + 1 : "
-                  f"(i64)-1, 63, 64);",
+        b.extend([f"{ind}{{ const {IX} nx_ = __shfl((hit{U - 1} && own{U - 1}) ? m{U - 1} + 1 : "
+                  f"({IX})-1, 63, 64);",
                   f"{ind}  gbase = nx_; }}"])
     iteration(True, ind)
     b.append("    } else {   // a range starts inside this iteration's groups")
@@ -466,7 +474,7 @@ def packed_tail(layout, compacts):
 
 
 def sparse_shape(p: NL.JoinParams, compacts, hk=None, tk=None) -> tuple:
-    return ("run_bits_scan", RS_PIPE, RS_WALK, RS_LDS) + scan_shape(p, compacts, 1, 64)[1:] + \
+    return ("run_bits_scan", RS_PIPE, RS_WALK, RS_LDS, RS_LUT, RS_PK16) + scan_shape(p, compacts, 1, 64)[1:] + \
         (pack_layout(p, compacts),) + ((hk.shape(),) if hk is not None else ()) + \
         ((tk.shape(),) if tk is not None else ())
 
@@ -548,6 +556,15 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
                 f"      gm{sfx} = a.GM{lk}[g_]; gr{sfx} = a.GR{lk}[g_]; }}"]
     if tk is not None:
         b.append(f"  __shared__ unsigned short lrn_[{WV}][{CAP}];")
+    if RS_LUT:
+        # dlut_[m | w << 4]: the 4 row tags of a nibble with run-start bits m, tag window w
+        b += ["  __shared__ unsigned char dlut_[512];",
+              f"  for (int e_ = (int)threadIdx.x; e_ < 512; e_ += {BLOCK}) {{",
+              "    unsigned k_ = 0u, o_ = 0u;",
+              "    for (int j_ = 0; j_ < 4; ++j_) { k_ += (e_ >> j_) & 1; "
+              "o_ |= (((unsigned)e_ >> (4u + k_)) & 1u) << j_; }",
+              "    dlut_[e_] = (unsigned char)o_; }",
+              "  __syncthreads();"]
     b += [f"  __shared__ unsigned short lst_[{WV}][{CAP}];",
           "  const int ln = (int)(threadIdx.x & 63);",
           "  const int wq = (int)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));",
@@ -635,6 +652,24 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
              "    const u64 lw_ = (u64)tw0@S@_ | ((u64)tw1@S@_ << 32);",
              "    const u64 hw_ = (u64)tw2@S@_;",
              "    const u64 T_ = sh_ ? ((lw_ >> sh_) | (hw_ << (64 - sh_))) : lw_;",
+             ]
+    if RS_LUT:
+        # row tags by nibble: rows 4i..4i+3 take their tags from a 5-run window of T (the run
+        # covering row 4i-1, then the runs starting in the nibble) through a 512-entry LDS
+        # table indexed by (nibble of run starts, window) - 16 fixed steps instead of a loop
+        # over the group's run starts (~15 VALU per start, ~20-28 starts for the slowest lane)
+        body += ["    u64 d_ = (u64)dlut_[((unsigned)m_ & 15u) | ((((unsigned)T_ << 1) & 31u) << 4)];",
+                 "    unsigned P_ = (unsigned)__popc((unsigned)m_ & 15u);",
+                 "    #pragma unroll",
+                 "    for (int i_ = 1; i_ < 16; ++i_) {",
+                 "      const unsigned mn_ = (unsigned)(m_ >> (4 * i_)) & 15u;",
+                 "      const unsigned ix_ = mn_ | (((unsigned)(T_ >> (P_ - 1u)) & 31u) << 4);",
+                 "      d_ |= (u64)dlut_[ix_] << (4 * i_);",
+                 "      P_ += (unsigned)__popc(mn_);",
+                 "    }",
+                 "    d_ &= am;"]
+    else:
+        body += [
              # only the group's own runs' tags (popc(m) of them) decide whether any row is set
              "    const int nr_ = __popcll(m_);",
              "    const u64 Tm_ = nr_ >= 64 ? T_ : (T_ & ((1ull << nr_) - 1ull));",
@@ -663,7 +698,19 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
     sign = g1.cnf_sign(lpreds)
     if sign is not None:
         sign = J._rename(sign, pslots, "k")
-    for half, off in (("plo_", 0), ("phi_", 32)):
+    # two rows per 32-bit word (16-bit signed codes): packed saturating range tests, fail bits
+    # gathered in even/odd order per 32-row half, then unzipped (2.5 VALU per row instead of 5)
+    sign2 = g1.cnf_sign2(lpreds, "x{}w@S@[w_]") if RS_PK16 and sign is not None and \
+        all(J._SIZEOF.get(g1.raw_type(sl)) == 2 for sl in pslots) else None
+    if sign2 is not None:
+        for half, off in (("plo_", 0), ("phi_", 16)):
+            body += ["    #pragma unroll",
+                     "    for (int w_ = 0; w_ < 16; ++w_) {",
+                     f"      const unsigned s2_ = {sign2.replace('[w_]', f'[w_ + {off}]')};",
+                     f"      {half} |= (s2_ >> (15 - w_)) & ((1u << w_) | (1u << (w_ + 16)));",
+                     "    }",
+                     f"    {half} = hs_unzip16({half});"]
+    for half, off in ((("plo_", 0), ("phi_", 32)) if sign2 is None else ()):
         body.append("    #pragma unroll")
         body.append("    for (int k_ = 0; k_ < 32; ++k_) {")
 
@@ -948,7 +995,10 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
     rng = run_ranges(rstart, rlen, rbucket, roff, runs)
     rng_d = torch.from_numpy(rng.reshape(-1).copy() if len(rng) else
                              __import__("numpy").zeros(4, "int64")).to(dev)
-    kt = J.kernel_for(tags2_shape(p, compacts, W), lambda: gen_run_tags2(p, compacts, W))
+    # 32-bit run / right-row indices when both fit (with slack for the gallop's overshoot)
+    ix32 = RT2_I32 and nruns < (1 << 31) - (1 << 20) and int(roff[-1].item()) < (1 << 31) - (1 << 20)
+    kt = J.kernel_for(tags2_shape(p, compacts, W, ix32),
+                      lambda: gen_run_tags2(p, compacts, W, ix32))
     vt = {"RNG": rng_d.data_ptr(), "NRG": len(rng), "NRUNS": nruns, "tags": tags.data_ptr(),
           "num_groups": p.num_groups, "group_base": p.group_base}
     tr = rng_d

@@ -74,6 +74,7 @@ class KernelConfig:
     rs_items: int = 16           # rows per thread of the dense phase-2 scan (W > 1 tags)
     rt2_unroll: int = 4          # phase-1 64-run groups in flight per wavefront iteration
     rt2_grid: int = 8192
+    rt2_i32: bool = True         # phase-1 run / right-row index math in 32 bits when tables fit
     rs_bits: bool = True         # phase 2 bit-parallel for 1-bit tags (gen_run_sparse_scan)
     rs_bits_grid: int = 8192
     rs_pack: bool = True         # bits scan reads its aggregate inputs row-packed
@@ -81,6 +82,9 @@ class KernelConfig:
                                  # fewest registers), 1 one buffer, 2 two named buffers (unroll 2);
                                  # SF100: 358 / 363 / 391 us (profiles/bits_scan_variants_r6.txt)
     rs_walk: int = 4             # bits scan list entries per lane per walk pass
+    rs_pk16: bool = True         # bits scan range tests of 16-bit codes two rows per packed op
+    rs_lut: bool = True          # bits scan row tags by nibble through an LDS table (else a loop
+                                 # over each group's run starts + prefix XOR)
     rs_lds: bool = False         # bits scan predicate columns loaded lane-coalesced, then moved
                                  # to their rows' lanes through LDS (else one 128 B run per lane)
     # --- shared ------------------------------------------------------------------------------

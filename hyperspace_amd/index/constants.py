@@ -106,10 +106,11 @@ HIPGRAPH_ENABLED_DEFAULT = "true"
 # query's stream (exec/gpu.py GpuBackend._scan_agg_graph)
 SIDE_STREAM_SCANS = "spark.hyperspace.mi.sideStreamScans.enabled"
 SIDE_STREAM_SCANS_DEFAULT = "true"
-# the side stream's queue priority: "high" lets the scan pipeline's one-workgroup kernels (range
-# search, tile prefix, final reduction) dispatch ahead of the join kernels' queued waves
+# the side stream's queue priority: "high" lets the scan pipeline's kernels dispatch ahead of the
+# join kernels' queued waves - measured slower at SF100 (1875 vs 2489 q/s: the scan's waves then
+# take the CUs the critical-path join needs, profiles/bench_side_priority_r6.jsonl)
 SIDE_STREAM_PRIORITY = "spark.hyperspace.mi.sideStreamScans.priority"
-SIDE_STREAM_PRIORITY_DEFAULT = "high"
+SIDE_STREAM_PRIORITY_DEFAULT = "normal"
 # replay the run-keyed two-phase merge join (tags, bits scan, fold, result copy) as one captured
 # hipGraph per lowering (graphs.TwoPhaseGraph); needs hipGraph.enabled
 JOIN_GRAPH_ENABLED = "spark.hyperspace.mi.joinGraph.enabled"

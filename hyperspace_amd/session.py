@@ -110,7 +110,12 @@ class Session:
 
     @property
     def case_sensitive(self) -> bool:
-        return HyperspaceConf.case_sensitive(self.conf)
+        # read on every name resolution of every DataFrame built: memoized per conf version
+        c = self.conf
+        memo = self.__dict__.get("_cs_memo")
+        if memo is None or memo[0] is not c or memo[1] != c.version:
+            memo = self.__dict__["_cs_memo"] = (c, c.version, HyperspaceConf.case_sensitive(c))
+        return memo[2]
 
     # -- execution ------------------------------------------------------------------------------
     def gpu_available(self) -> bool:

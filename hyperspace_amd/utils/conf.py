@@ -40,8 +40,16 @@ class RuntimeConf:
         return dict(self._m)
 
 
+_BOOLS: dict = {}
+
+
 def _b(v: str) -> bool:
-    return str(v).strip().lower() == "true"
+    r = _BOOLS.get(v)
+    if r is None:
+        r = str(v).strip().lower() == "true"
+        if isinstance(v, str) and len(_BOOLS) < 1024:
+            _BOOLS[v] = r
+    return r
 
 
 class HyperspaceConf:

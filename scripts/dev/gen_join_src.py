@@ -59,7 +59,7 @@ def main(out):
         p, comp, keep = q3_params(ng)
         W = jit_runs.tag_width(p)
         NI = jit_runs.RS_ITEMS
-        ks = [jit_runs.gen_run_tags2(p, comp, W), jit_runs.gen_run_scan(p, comp, W, NI)]
+        ks = [jit_runs.gen_run_tags2(p, comp, W, jit_runs.RT2_I32), jit_runs.gen_run_scan(p, comp, W, NI)]
         if W == 1 and not (p.group_col >= 8 and p.num_groups > 1):
             ks.append(jit_runs.gen_run_sparse_scan(p, comp))
             # hash walk grouped by the left key (the functionally reduced Q3 GROUP BY)

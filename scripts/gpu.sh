@@ -151,6 +151,11 @@ step_pmcbench() {
   python3 scripts/pmc_summary.py "${O}_pmcb_counters.csv" "${O}_pmcb_trace.csv" > "${O}_pmcb_summary.txt" 2>&1 || true
 }
 
+step_hbm() {
+  (rocm-smi --showclocks --showmemuse > "${O}_smi.txt" 2>&1 || true)
+  timeout -k 10 120 python3 scripts/diag/hbm_probe.py 4 > "${O}_hbm.json" 2> "${O}_hbm.log"
+}
+
 step_q3f() {
   local cfg="$Q3F_CONFIGS"
   [ -z "$cfg" ] && cfg='[{}]'
