@@ -17,7 +17,9 @@
 #define SF_ITEMS 8
 #define SF_TILE (SF_BLOCK * SF_ITEMS)
 #define SF_GRID 2048
-#define FIN_BLOCK 1024  // final reduction: 16 waves, so each lane sums only grid/1024 partials
+#define FIN_BLOCK 256   // final reduction: 4 waves (each lane sums grid/256 partials) - a block
+                        // needing 16 free wave slots on one CU waited behind a concurrent
+                        // join's waves (~110 us per final in the SF100 step timeline, r6)
 
 struct ScanParams {
   ColDesc cols[HS_MAX_COLS];
@@ -121,46 +123,34 @@ __global__ __launch_bounds__(64 * RANGE_WAVES) void hs_range_search_dev_kernel(
             (uint64_t)bp[4], (int)bp[5], rstart, rlen, rbucket);
 }
 
-// ranges -> tile prefix (single block, R arbitrary): tile_prefix[R] = total tiles.
+// ranges -> tile prefix (ONE wavefront, R arbitrary): tile_prefix[R] = total tiles.
 // rstart != nullptr: each range is widened down to a multiple of `align` rows first (the tiling of
 // the vectorized generated kernels, which load `align` consecutive rows per thread).
-__global__ __launch_bounds__(1024) void hs_ranges_to_tiles_kernel(const int64_t* __restrict__ rlen,
-                                                                  int R, int tile_rows,
-                                                                  int64_t* __restrict__ tile_prefix,
-                                                                  const int64_t* __restrict__ rstart,
-                                                                  int64_t align) {
-  __shared__ int64_t wsum[16];
-  __shared__ int64_t carry;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (int base = 0; base < R; base += blockDim.x) {
-    const int i = base + threadIdx.x;
+// A single wavefront, no LDS and no barriers: this kernel sits in the middle of the scan
+// pipeline's graph, and while a concurrent join's waves fill the device a 1024-thread block had to
+// wait for 16 free wave slots on one CU (~185 us in the SF100 step timeline, r6) - one wave slot
+// frees up at once.
+__global__ __launch_bounds__(64) void hs_ranges_to_tiles_kernel(const int64_t* __restrict__ rlen,
+                                                                int R, int tile_rows,
+                                                                int64_t* __restrict__ tile_prefix,
+                                                                const int64_t* __restrict__ rstart,
+                                                                int64_t align) {
+  const int lane = threadIdx.x & 63;
+  int64_t carry = 0;
+  for (int base = 0; base < R; base += 64) {
+    const int i = base + lane;
     const int64_t len = i < R ? rlen[i] + (rstart != nullptr ? (rstart[i] & (align - 1)) : 0) : 0;
     const int64_t t = (len + tile_rows - 1) / tile_rows;
     int64_t x = t;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-      int64_t y = __shfl_up(x, off, 64);
+      const int64_t y = __shfl_up(x, off, 64);
       if (lane >= off) x += y;
     }
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int64_t run = 0;
-      for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
-        int64_t v = wsum[k];
-        wsum[k] = run;
-        run += v;
-      }
-    }
-    __syncthreads();
-    const int64_t incl = x + wsum[w] + carry;
-    if (i < R) tile_prefix[i] = incl - t;
-    __syncthreads();
-    if (threadIdx.x == blockDim.x - 1) carry = incl;
-    __syncthreads();
+    if (i < R) tile_prefix[i] = carry + x - t;
+    carry += __shfl(x, 63, 64);
   }
-  if (threadIdx.x == 0) tile_prefix[R] = carry;
+  if (lane == 0) tile_prefix[R] = carry;
 }
 
 // Walks a block's contiguous tile chunk, yielding (row0, rows) per tile.
@@ -393,14 +383,14 @@ int hs_probe_ranges(const ColDesc* key, const int64_t* bucket_off, const int32_t
 
 int hs_ranges_to_tiles(const int64_t* rlen, int R, int tile_rows, int64_t* tile_prefix,
                        void* stream) {
-  hipLaunchKernelGGL(hs_ranges_to_tiles_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rlen,
+  hipLaunchKernelGGL(hs_ranges_to_tiles_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, rlen,
                      R, tile_rows, tile_prefix, (const int64_t*)nullptr, (int64_t)1);
   return (int)hipGetLastError();
 }
 
 int hs_ranges_to_tiles_aligned(const int64_t* rstart, const int64_t* rlen, int R, int tile_rows,
                                int64_t align, int64_t* tile_prefix, void* stream) {
-  hipLaunchKernelGGL(hs_ranges_to_tiles_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rlen,
+  hipLaunchKernelGGL(hs_ranges_to_tiles_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, rlen,
                      R, tile_rows, tile_prefix, rstart, align);
   return (int)hipGetLastError();
 }

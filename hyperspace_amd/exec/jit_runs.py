@@ -38,7 +38,7 @@ MJ_2P, RS_ITEMS = _CFG.mj_2p, _CFG.rs_items
 RT2_UNROLL, RT2_GRID, RT2_I32 = _CFG.rt2_unroll, _CFG.rt2_grid, _CFG.rt2_i32
 RS_BITS, RS_BITS_GRID, RS_PACK = _CFG.rs_bits, _CFG.rs_bits_grid, _CFG.rs_pack
 RS_PIPE, RS_WALK, RS_LDS, RS_LUT = _CFG.rs_pipe, _CFG.rs_walk, _CFG.rs_lds, _CFG.rs_lut
-RS_PK16 = _CFG.rs_pk16
+RS_PK16, RS_WAVES = _CFG.rs_pk16, _CFG.rs_waves
 
 
 def tag_width(p: NL.JoinParams) -> int:
@@ -474,7 +474,7 @@ def packed_tail(layout, compacts):
 
 
 def sparse_shape(p: NL.JoinParams, compacts, hk=None, tk=None) -> tuple:
-    return ("run_bits_scan", RS_PIPE, RS_WALK, RS_LDS, RS_LUT, RS_PK16) + scan_shape(p, compacts, 1, 64)[1:] + \
+    return ("run_bits_scan", RS_PIPE, RS_WALK, RS_LDS, RS_LUT, RS_PK16, RS_WAVES) + scan_shape(p, compacts, 1, 64)[1:] + \
         (pack_layout(p, compacts),) + ((hk.shape(),) if hk is not None else ()) + \
         ((tk.shape(),) if tk is not None else ())
 
@@ -863,8 +863,9 @@ def gen_run_sparse_scan(p: NL.JoinParams, compacts, hk=None, tk=None) -> J.Kerne
         b += JH._topk_flush(aggs, tk, args, "wid", key_lines)
     name = "hs_jit_run_bits_scan" if hk is None else \
         ("hs_jit_run_bits_hash" if tk is None else "hs_jit_run_bits_topk")
+    occ = f" __attribute__((amdgpu_waves_per_eu({RS_WAVES}, {RS_WAVES})))" if RS_WAVES else ""
     src = (J._PRELUDE + args.struct_src() +
-           f'extern "C" __global__ __launch_bounds__({BLOCK}) void {name}(Args a) '
+           f'extern "C" __global__ __launch_bounds__({BLOCK}){occ} void {name}(Args a) '
            f'{{\n' + "\n".join(b) + "\n}\n")
     lds = (len(aggs) * p.num_groups * 32) if grouped else 0
     return J.Kernel(src, name, args, lds)

@@ -83,6 +83,7 @@ class KernelConfig:
                                  # SF100: 358 / 363 / 391 us (profiles/bits_scan_variants_r6.txt)
     rs_walk: int = 4             # bits scan list entries per lane per walk pass
     rs_pk16: bool = True         # bits scan range tests of 16-bit codes two rows per packed op
+    rs_waves: int = 0            # bits scan waves per SIMD the compiler must fit (0: its choice)
     rs_lut: bool = True          # bits scan row tags by nibble through an LDS table (else a loop
                                  # over each group's run starts + prefix XOR)
     rs_lds: bool = False         # bits scan predicate columns loaded lane-coalesced, then moved
