@@ -71,6 +71,7 @@ def release_process_device_memory() -> None:
     jit_join._RUNS_LOWERED.clear()
     jit_join._RUNS_HASH_LOWERED.clear()
     jit_runs._PACKS.clear()
+    jit_runs._P12.clear()
     import gc
     gc.collect()
     torch.cuda.synchronize()

@@ -556,7 +556,8 @@ class _Gen:
             s = f"(~{s})"
         return f"({s} | ((int){self.ok(c)} - 1))" if hv else s
 
-    def cnf_sign2(self, preds: List[Tuple[int, NL.Pred]], word: str) -> Optional[str]:
+    def cnf_sign2(self, preds: List[Tuple[int, NL.Pred]], word: str,
+                  offset: Optional[str] = None) -> Optional[str]:
         """``cnf_sign`` over two rows at once for 16-bit signed codes without validity: the
         dword ``word.format(slot)`` holds both rows' codes, the result's bits 15 / 31 are their
         fail bits (``hs_rng2``).  None when a leaf has no such form."""
@@ -579,6 +580,9 @@ class _Gen:
                                                kind == NL.PK_FLT_LIT and enc[1]):
                     lo = self.a.add("q", f"CL{k}", "long long")
                     hi = self.a.add("q", f"CH{k}", "long long")
+                    if offset is not None:      # the words hold code - offset
+                        o = offset.format(c)
+                        lo, hi = f"({lo} - {o})", f"({hi} - {o})"
                     leaf = (f"hs_rng2({word.format(c)}, hs_c16lo({lo}, {hi}), "
                             f"hs_c16hi({lo}, {hi}))")
                     if op == NL.OP_NE:

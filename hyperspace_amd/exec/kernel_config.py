@@ -84,6 +84,8 @@ class KernelConfig:
     rs_walk: int = 4             # bits scan list entries per lane per walk pass
     rs_pk16: bool = True         # bits scan range tests of 16-bit codes two rows per packed op
     rs_waves: int = 0            # bits scan waves per SIMD the compiler must fit (0: its choice)
+    rs_pack12: bool = True       # bits scan reads 16-bit predicate codes within [0, 4095] from a
+                                 # 12-bit packed copy (25% fewer bytes of its row stream)
     rs_lut: bool = True          # bits scan row tags by nibble through an LDS table (else a loop
                                  # over each group's run starts + prefix XOR)
     rs_lds: bool = False         # bits scan predicate columns loaded lane-coalesced, then moved

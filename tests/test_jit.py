@@ -826,11 +826,15 @@ def test_merge_join_runs_matches_oracle(device, layout):
                 G = 3 if grouped else 1
                 es = exp_s if grouped else exp_s.sum(keepdims=True)
                 ec = exp_c if grouped else exp_c.sum(keepdims=True)
-                for use_runs, two, sparse in ((True, True, True), (True, True, False),
-                                              (True, False, False), (False, False, False)):
-                    cfg = (keys, grouped, use_runs, two, sparse)
+                for use_runs, two, sparse, pk12 in ((True, True, True, True),
+                                                    (True, True, True, False),
+                                                    (True, True, False, True),
+                                                    (True, False, False, True),
+                                                    (False, False, False, True)):
+                    # pk12: the date predicate reads the 12-bit packed copy (codes span < 4096)
+                    cfg = (keys, grouped, use_runs, two, sparse, pk12)
                     with kernel_config.use(mj_lds_keys=keys, mj_runs=use_runs, mj_2p=two,
-                                           rs_bits=sparse):
+                                           rs_bits=sparse, rs_pack12=pk12):
                         got = [t.cpu().numpy() for t in
                                jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, comp,
                                                   nrows=len(lk), rdup=False)]
@@ -844,6 +848,46 @@ def test_merge_join_runs_matches_oracle(device, layout):
                                 assert jit_runs.pack_layout(p, comp) is not None
     finally:
         p.group_col, p.num_groups = 10, 3
+
+
+def test_pack12_layout_decodes_like_the_kernel():
+    """The 12-bit packed predicate copy (jit_runs.packed12, RS_PACK12): 8 codes per 3 dwords,
+    stored relative to the column's smallest code; decoding with the generated kernel's shifts
+    and masks gives back every code, and the packed 16-bit range test (hs_rng2 with the
+    pair-clamped bounds shifted by the same offset) selects exactly the rows of the value
+    compare, for ranges inside, across and outside the column's span."""
+    import torch
+    from hyperspace_amd.exec.encoding import Compact
+    from hyperspace_amd.exec import jit_runs
+    rng = np.random.default_rng(5)
+    vals = rng.integers(8000, 10000, 1000).astype(np.int64)
+    base = 8000 + 32768
+    c = Compact(torch.from_numpy((vals - base).astype(np.int16)), 2, base, None, NL.I32,
+                8000, 9999)
+    assert jit_runs.pack12_ok(c)
+    assert not jit_runs.pack12_ok(Compact(c.codes, 2, base, None, NL.I32, 8000, 8000 + 4096))
+    w = jit_runs.packed12(c).numpy().view(np.uint32).astype(np.uint64)
+    assert w.size == (1000 + 63) // 64 * 24
+    a, b, cc = w[0::3], w[1::3], w[2::3]
+    m = np.uint64(0xFFF)
+    dec = np.stack([a & m, (a >> 12) & m, ((a >> 24) | (b << 8)) & m, (b >> 4) & m,
+                    (b >> 16) & m, ((b >> 28) | (cc << 4)) & m, (cc >> 8) & m,
+                    (cc >> 20) & m], axis=1).reshape(-1)[:1000].astype(np.int64)
+    off = 8000 - base
+    assert off == -32768 and np.array_equal(dec + off, vals - base)
+
+    def sat16(x):
+        return np.clip(x, -32768, 32767)
+
+    def c16(lo, hi):        # hs_c16lo / hs_c16hi: ranges outside int16 never match
+        if hi < -32768 or lo > 32767:
+            return 32767, -32768
+        return max(lo, -32768), min(hi, 32767)
+    for vlo, vhi in ((8500, 9000), (7000, 8100), (9990, 12000), (100, 200), (20000, 30000),
+                     (9000, 8000), (8000, 9999)):
+        lo, hi = c16(vlo - base - off, vhi - base - off)
+        fail = (sat16(dec - lo) < 0) | (sat16(hi - dec) < 0)    # sign of sub_sat | sub_sat
+        assert np.array_equal(~fail, (vals >= vlo) & (vals <= vhi)), (vlo, vhi)
 
 
 def test_run_topk_sources_compile(rt, tmp_path):
