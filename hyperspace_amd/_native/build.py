@@ -6,6 +6,8 @@ snapshot to the GPU box):
 * ``libhs_runtime.so`` — host C++ runtime (``csrc/runtime/*.cpp``): hipRTC whole-stage codegen
   (compile, code-object cache, module launch) and roctx pipeline-stage markers.  Host-only C++
   against the HIP runtime, built with hipcc.
+* ``_hs_host*.so`` — CPython extension for the query front end's host hot paths
+  (``csrc/host/hs_host.cpp``), built with g++.
 
 Usage: ``python -m hyperspace_amd._native.build [--force]``.
 """
@@ -91,7 +93,31 @@ def build_runtime(force: bool = False) -> str:
     return RUNTIME_LIB
 
 
+def host_ext_path() -> str:
+    import sysconfig
+    return os.path.join(HERE, "_hs_host" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+
+
+def build_host(force: bool = False) -> str:
+    """``_hs_host``: CPython extension for the query front end's host hot paths
+    (``csrc/host/hs_host.cpp``: the plan cache's fingerprint walk), plain g++."""
+    import sysconfig
+    src = os.path.join(CSRC, "host", "hs_host.cpp")
+    out = host_ext_path()
+    if not os.path.exists(src):
+        return ""
+    if not force and not _newer(out, [src]):
+        return out
+    cxx = os.environ.get("CXX") or shutil.which("g++") or "c++"
+    tmp = out + ".tmp"
+    _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-fno-strict-aliasing",
+          f"-I{sysconfig.get_paths()['include']}", src, "-o", tmp])
+    os.replace(tmp, out)
+    return out
+
+
 def build_all(force: bool = False):
+    build_host(force)
     return build_kernels(force), build_runtime(force)
 
 

@@ -20,6 +20,67 @@ from .parser import parse_expression
 _RESOLVED: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 
 
+def _name_map(plan, cs: bool) -> dict:
+    """name -> first output attribute of that name (lower-cased names when not case
+    sensitive), built once per plan: a serving loop resolves the same names against the same
+    base relations on every query (plans are immutable; the weak map dies with the plan)."""
+    memo = _RESOLVED.get(plan)
+    if memo is None:
+        memo = _RESOLVED[plan] = {}
+    m = memo.get(cs)
+    if m is None:
+        t = type(plan)
+        if t is L.Filter or t is L.Sort:         # output = the child's output
+            m = _name_map(plan.children[0], cs)
+        elif t is L.Join and plan.join_type == "inner":
+            # left's attributes first, then right's (the order of Join.output)
+            m = dict(_name_map(plan.children[0], cs))
+            for k, a in _name_map(plan.children[1], cs).items():
+                m.setdefault(k, a)
+        else:
+            m = {}
+            for a in plan.output:
+                m.setdefault(a.name if cs else a.name.lower(), a)
+        memo[cs] = m
+    return m
+
+
+def _resolve_name(cs: bool, name: str, plan) -> E.Attribute:
+    a = _name_map(plan, cs).get(name if cs else name.lower())
+    if a is None:
+        raise HyperspaceException(
+            f"cannot resolve '{name}' given input columns: [{', '.join(x.name for x in plan.output)}]")
+    return a
+
+
+def _native_resolve():
+    from .plan_cache import _NATIVE
+    return _NATIVE.resolve if _NATIVE is not None else None
+
+
+_NATIVE_RESOLVE = _native_resolve()
+
+
+def _resolve_walk(x, names: dict, cs: bool, plan):
+    """``x`` with every UnresolvedAttribute replaced by its attribute in ``names``
+    (``_name_map``)."""
+    if isinstance(x, E.UnresolvedAttribute):
+        a = names.get(x.name if cs else x.name.lower())
+        if a is None:
+            raise HyperspaceException(
+                f"cannot resolve '{x.name}' given input columns: "
+                f"[{', '.join(y.name for y in plan.output)}]")
+        return a
+    ch = x.children
+    if not ch:
+        return x
+    new = tuple([_resolve_walk(c, names, cs, plan) for c in ch])
+    for a, b in zip(new, ch):
+        if a is not b:
+            return x.with_children(new)
+    return x
+
+
 class Row(tuple):
     """Result row: tuple with attribute / key access, like ``pyspark.sql.Row``."""
 
@@ -70,27 +131,7 @@ class DataFrame:
         return QueryExecution(self.session, self.plan)
 
     def _resolve_name(self, name: str, plan: L.LogicalPlan = None) -> E.Attribute:
-        plan = plan or self.plan
-        cs = self.session.case_sensitive
-        # per-plan memo: a serving loop resolves the same names against the same base relation
-        # on every query (plans are immutable; the weak map dies with the plan)
-        memo = _RESOLVED.get(plan)
-        if memo is None:
-            memo = _RESOLVED[plan] = {}
-        hit = memo.get((name, cs))
-        if hit is not None:
-            return hit
-        if cs:
-            matches = [a for a in plan.output if a.name == name]
-        else:
-            lname = name.lower()
-            matches = [a for a in plan.output if a.name.lower() == lname]
-        if matches:
-            memo[(name, cs)] = matches[0]
-        if not matches:
-            raise HyperspaceException(
-                f"cannot resolve '{name}' given input columns: [{', '.join(a.name for a in plan.output)}]")
-        return matches[0]
+        return _resolve_name(self.session.case_sensitive, name, plan or self.plan)
 
     def __getitem__(self, name) -> Column:
         if isinstance(name, str):
@@ -110,20 +151,12 @@ class DataFrame:
         without one are kept as they are (a serving loop builds a fresh expression per query,
         so this walk is on its host path)."""
         plan = plan or self.plan
-        unresolved = E.UnresolvedAttribute
-
-        def walk(x):
-            if type(x) is unresolved or isinstance(x, unresolved):
-                return self._resolve_name(x.name, plan)
-            ch = x.children
-            if not ch:
-                return x
-            new = tuple([walk(c) for c in ch])
-            for a, b in zip(new, ch):
-                if a is not b:
-                    return x.with_children(new)
-            return x
-        return walk(e)
+        cs = self.session.case_sensitive
+        names = _name_map(plan, cs)
+        if _NATIVE_RESOLVE is not None:
+            return _NATIVE_RESOLVE(e, names, cs, E.UnresolvedAttribute,
+                                   lambda n: _resolve_name(cs, n, plan))
+        return _resolve_walk(e, names, cs, plan)
 
     def _to_expr(self, c) -> E.Expression:
         if isinstance(c, str):

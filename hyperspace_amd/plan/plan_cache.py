@@ -179,6 +179,76 @@ def _fp_node(v, t: type, ctx: _Ctx):
     return (t.__name__, tuple(items))
 
 
+# Native walk (csrc/host/hs_host.cpp, same output as ``_fp``): per exact type a (code, name)
+# pair - 0 generic node, 1 literal, 2 attribute, 3 children-only node, 4 the Python ``_fp``
+_KINDS: Dict[type, tuple] = {}
+
+
+def _classify(t: type) -> tuple:
+    if issubclass(t, E.Literal):
+        k = 1
+    elif issubclass(t, (E.In, E.InSet)):
+        k = 4
+    elif issubclass(t, E.Attribute):
+        k = 2
+    elif t is L.LogicalRelation:
+        k = 5
+    elif issubclass(t, _PRIMS + (list, tuple, set, frozenset, dict, pa.DataType, pa.Schema,
+                                 pa.Field)) or not _own_type(t):
+        k = 4
+    else:
+        k = 3
+    out = _KINDS[t] = (k, t.__name__)
+    return out
+
+
+_HOST_ABI = 2      # csrc/host/hs_host.cpp ``ABI``
+
+
+def _native():
+    try:
+        import importlib.util
+        from .._native.build import host_ext_path
+        path = host_ext_path()
+        spec = importlib.util.spec_from_file_location("_hs_host", path)
+        if spec is None or not __import__("os").path.exists(path):
+            return None
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        return mod if getattr(mod, "ABI", None) == _HOST_ABI else None
+    except (ImportError, OSError):
+        return None
+
+
+_NATIVE = _native()
+_NATIVE_FP = _NATIVE.fingerprint if _NATIVE is not None else None
+
+
+def _leaf_memo(v):
+    """(fingerprint in local numbering, expr ids, refs) of base relation ``v`` (``_fp_leaf``'s
+    memo), or None when it holds literals (no memo: the Python walk handles it)."""
+    hit = _LEAF_FP.get(v)
+    if hit is None:
+        lctx = _Ctx()
+        lfp = _fp_node(v, type(v), lctx)
+        if lctx.lits:
+            return None
+        hit = _LEAF_FP[v] = (lfp, tuple(lctx.ids), tuple(lctx.refs))
+    return hit
+
+
+def fingerprint(logical, ctx: _Ctx, native: Optional[bool] = None):
+    """The plan-cache fingerprint of ``logical`` (``_fp``), through the native walk when it is
+    built (``native`` None) or as asked."""
+    f = _NATIVE_FP if native is not False else None
+    if native and f is None:
+        raise RuntimeError("_hs_host extension not built")
+    if f is None:
+        return _fp(logical, ctx)
+    return f(logical, ctx.ids, ctx.lits, ctx.refs, _KINDS, _classify, _fields,
+             lambda v: _fp(v, ctx), _leaf_memo)
+
+
 def _iter_literals(v, out: List[E.Literal], seen: set):
     """Every Literal object reachable from a plan (through our own node/container types)."""
     if isinstance(v, E.Literal):
@@ -351,7 +421,7 @@ class PlanCache:
         ``entry.old_lits``."""
         ctx = _Ctx()
         try:
-            key = (self._session_key(session, ctx), _fp(logical, ctx))
+            key = (self._session_key(session, ctx), fingerprint(logical, ctx))
         except _NotCacheable:
             self.uncacheable += 1
             return None, None, ctx

@@ -289,3 +289,58 @@ def test_order_by_literals_force_materialized_hits(data):
     s.conf.set("spark.hyperspace.mi.planCache.enabled", "true")
     assert got == want
     assert got[0] != got[2]
+
+
+def test_native_fingerprint_matches_python_walk(data):
+    """The native fingerprint walk (csrc/host/hs_host.cpp, ``plan_cache.fingerprint``) builds the
+    same key, literal list and attribute numbering as the interpreted ``_fp`` for filter, join,
+    grouped, ordered, string-literal and null-literal plans; IN lists stay uncacheable."""
+    from hyperspace_amd.plan import plan_cache as PC
+    from hyperspace_amd import lit
+    if PC._NATIVE_FP is None:
+        from hyperspace_amd._native.build import build_host
+        build_host()
+        PC._NATIVE_FP = PC._native()
+    assert PC._NATIVE_FP is not None
+    s, _, df, od = data
+    plans = [_filter_q(df, 3), _join_q(df, od, 2),
+             df.filter(col("s") == "s3").select("k", "v").orderBy(col("v").desc()).limit(5),
+             df.filter(col("k").isNull() | (col("v") > lit(None).cast("double"))).select("k"),
+             df.join(od, df["k"] == od["ok"]).join(df.select("k", "d"), "k")]
+    for q in plans:
+        logical = q.queryExecution.logical
+        a, b = PC._Ctx(), PC._Ctx()
+        fa = PC.fingerprint(logical, a, native=False)
+        fb = PC.fingerprint(logical, b, native=True)
+        assert fa == fb
+        assert [id(x) for x in a.lits] == [id(x) for x in b.lits] and a.ids == b.ids
+        assert [id(x) for x in a.refs] == [id(x) for x in b.refs]
+    q = df.filter(col("k").isin(1, 2, 3))
+    for native in (False, True):
+        with pytest.raises(PC._NotCacheable):
+            PC.fingerprint(q.queryExecution.logical, PC._Ctx(), native=native)
+
+
+def test_native_resolve_matches_python_walk(data):
+    """Expression name binding through the native walk (``dataframe._NATIVE_RESOLVE``) returns
+    the Python walk's tree (same attributes, untouched subtrees shared) and raises the same
+    error for an unknown column, case-insensitive by default."""
+    from hyperspace_amd.plan import dataframe as D
+    from hyperspace_amd.plan import expressions as E
+    from hyperspace_amd.exceptions import HyperspaceException
+    assert D._NATIVE_RESOLVE is not None
+    s, _, df, od = data
+    j = df.join(od, df["k"] == od["ok"])
+    e = ((col("D") >= datetime.date(1993, 1, 1)) & (col("od") < 5)) | col("v").isNull()
+    e = e.expr
+    names = D._name_map(j.plan, False)
+    a = D._resolve_walk(e, names, False, j.plan)
+    b = D._NATIVE_RESOLVE(e, names, False, E.UnresolvedAttribute,
+                          lambda n: D._resolve_name(False, n, j.plan))
+    assert a.sql() == b.sql() and type(a) is type(b)
+    same = col("v").expr
+    done = D._NATIVE_RESOLVE(D._resolve_walk(same, names, False, j.plan), names, False,
+                             E.UnresolvedAttribute, lambda n: None)
+    assert done is names["v"]
+    with pytest.raises(HyperspaceException):
+        j.filter(col("nope") > 1)
