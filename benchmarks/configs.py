@@ -55,13 +55,23 @@ def _sync(device):
         torch.cuda.synchronize()
 
 
+def _mark(device):
+    """HS_CFG_MARK=1: a short spin kernel (``torch.cuda._sleep``) that brackets each timed loop
+    in a kernel trace (gpu.sh cfgprof)."""
+    if device == "gpu" and os.environ.get("HS_CFG_MARK"):
+        import torch
+        torch.cuda._sleep(1000)
+
+
 def _timed_loop(fn, n, device):
+    _mark(device)
     _sync(device)
     t0 = time.perf_counter()
     for i in range(n):
         fn(i)
     _sync(device)
     el = time.perf_counter() - t0
+    _mark(device)
     if os.environ.get("HS_CFG_CPROFILE"):     # where the host time of the loop goes
         import cProfile
         import io

@@ -106,6 +106,27 @@ step_configs() {
   done
 }
 
+step_cfgprof() {
+  # kernel trace of one benchmarks/configs.py config (CONFIG, default hybrid); each timed loop
+  # is bracketed by a spin kernel (HS_CFG_MARK): the kernels between two marks are one loop
+  rm -rf "$HS_BENCH_DIR"/indexes_* "$HS_BENCH_DIR"/cfg_* 2>/dev/null
+  (cd /tmp && export TMPDIR=/tmp && export HS_CFG_MARK=1 &&
+   timeout -k 10 ${CFG_TIMEOUT:-500} rocprofv3 --kernel-trace --output-format csv -d "${O}_cfgprof" -o run \
+     -- python3 "$REPO/benchmarks/configs.py" --config ${CONFIG:-hybrid} --sf ${SF:-100} ${CFG_ARGS} \
+     > "${O}_cfgprof.jsonl" 2> "${O}_cfgprof.log") || return $?
+  local f
+  f=$(find "${O}_cfgprof" -name "*kernel_trace.csv" | head -n 1)
+  python3 - "$f" "${O}_cfg_ktrace.csv" <<'PYEOF'
+import csv, sys
+r = csv.DictReader(open(sys.argv[1]))
+w = csv.writer(open(sys.argv[2], 'w'))
+w.writerow(['name', 'start', 'end', 'queue'])
+for x in r:
+    w.writerow([x['Kernel_Name'][:60], x['Start_Timestamp'], x['End_Timestamp'], x['Queue_Id']])
+PYEOF
+  rm -rf "${O}_cfgprof"
+}
+
 step_qk() {
   # query-kernel sweep: QK_CONFIGS (JSON list of kernel_config fields), QK_ARGS (e.g. --only-merge)
   local cfg="$QK_CONFIGS"
