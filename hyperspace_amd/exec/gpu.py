@@ -221,7 +221,11 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
             return
         if len(self._programs) >= 256:
             self._programs.clear()
+        new_shape = id(plan) not in self._programs
         self._programs[id(plan)] = (plan, _AggProgram(self, *cand))
+        if new_shape and HyperspaceConf.gc_freeze_enabled(self.session.conf):
+            from ..utils import hostgc
+            hostgc.settle()
 
     def _fallback(self, plan, e, t0) -> "QueryFuture":
         log.info("device executor fallback: %s", e)

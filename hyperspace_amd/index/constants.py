@@ -119,6 +119,12 @@ JOIN_GRAPH_ENABLED_DEFAULT = "true"
 # lowering directly (exec/gpu.py _AggProgram), skipping the executor's plan walk
 PREPARED_SUBMIT_ENABLED = "spark.hyperspace.mi.preparedSubmit.enabled"
 PREPARED_SUBMIT_ENABLED_DEFAULT = "true"
+# when a new prepared program is registered (warm-up of a query shape), move every object
+# alive at that point out of the cyclic GC's scans (gc.freeze after a young-generation collect):
+# a full collection over the engine's long-lived state (plans, lowerings, Arrow / torch objects)
+# costs tens of ms of host time in the middle of a serving loop (utils/hostgc.py)
+GC_FREEZE_ENABLED = "spark.hyperspace.mi.host.gcFreeze.enabled"
+GC_FREEZE_ENABLED_DEFAULT = "true"
 # ORDER BY <sum / count> LIMIT k over the key-run hash walk keeps whole keys in per-wavefront
 # top-K lists instead of hash-table slots (hash_agg.TopKPlan)
 RUN_TOPK_ENABLED = "spark.hyperspace.mi.runTopK.enabled"

@@ -150,6 +150,10 @@ class HyperspaceConf:
         return _b(conf.get(C.PREPARED_SUBMIT_ENABLED, C.PREPARED_SUBMIT_ENABLED_DEFAULT))
 
     @staticmethod
+    def gc_freeze_enabled(conf) -> bool:
+        return _b(conf.get(C.GC_FREEZE_ENABLED, C.GC_FREEZE_ENABLED_DEFAULT))
+
+    @staticmethod
     def side_stream_scans(conf) -> bool:
         return _b(conf.get(C.SIDE_STREAM_SCANS, C.SIDE_STREAM_SCANS_DEFAULT))
 

@@ -22,6 +22,10 @@ def main():
     ap.add_argument("--device", default="cpu", choices=["cpu", "gpu"])
     ap.add_argument("--n", type=int, default=2000)
     ap.add_argument("--profile", action="store_true", help="cProfile the build + lookup loops")
+    ap.add_argument("--phases", action="store_true",
+                    help="time the submission's phases (wrapped functions) and the GC passes")
+    ap.add_argument("--gc-freeze", action="store_true",
+                    help="gc.freeze() after warm-up (objects alive then leave the GC's scans)")
     ap.add_argument("--data-dir", default=os.environ.get("HS_BENCH_DIR", "/tmp/hs_bench"))
     args = ap.parse_args()
     from hyperspace_amd import Hyperspace, IndexConfig, Session, col, count, sum_
@@ -72,6 +76,21 @@ def main():
 
     pc = plan_cache(s)
     out = {"sf": args.sf, "device": args.device, "n": args.n}
+    acc = {}
+    if args.phases:
+        import gc
+        _wrap_phases(acc)
+        gct = {}
+
+        def gccb(phase, info):
+            if phase == "start":
+                gct["t"] = time.perf_counter_ns()
+            else:
+                k = f"gc{info['generation']}"
+                acc[k] = acc.get(k, [0, 0])
+                acc[k][0] += time.perf_counter_ns() - gct["t"]
+                acc[k][1] += 1
+        gc.callbacks.append(gccb)
     for name, fn in (("q6", q6), ("q3", q3)):
         for i in range(40):                     # warm: every literal vector planned once
             fn(i).collect()
@@ -80,6 +99,11 @@ def main():
             import cProfile
             prof = cProfile.Profile()
             prof.enable()
+        if args.gc_freeze:
+            import gc
+            gc.collect()
+            gc.freeze()
+        acc.clear()
         # best of rounds of 250 queries (the container's CPU is shared: the minimum is the cost)
         bld, lkp = [], []
         for r in range(max(args.n // 250, 1)):
@@ -126,7 +150,41 @@ def main():
                 import pstats
                 pstats.Stats(sprof, stream=sys.stderr).sort_stats("tottime").print_stats(40)
         out[name] = {k: round(v, 1) for k, v in res.items()}
+        if args.phases:
+            nq = max(args.n // 250, 1) * 250 + 300
+            out[name]["phases_us_per_query"] = {k: round(v[0] / 1e3 / nq, 2)
+                                                for k, v in sorted(acc.items())}
+            out[name]["phase_calls"] = {k: v[1] for k, v in sorted(acc.items())}
     print(json.dumps(out), flush=True)
+
+
+def _wrap_phases(acc: dict) -> None:
+    """Accumulate wall ns and calls of the submission path's stages into ``acc``."""
+    from hyperspace_amd.exec import gpu_agg, gpu_common, graphs, jit
+    from hyperspace_amd.plan import execution, plan_cache
+
+    def wrap(owner, name, key):
+        f = getattr(owner, name)
+
+        def w(*a, **k):
+            t = time.perf_counter_ns()
+            try:
+                return f(*a, **k)
+            finally:
+                e = acc.setdefault(key, [0, 0])
+                e[0] += time.perf_counter_ns() - t
+                e[1] += 1
+        setattr(owner, name, w)
+    wrap(execution.QueryExecution, "_submit_bound", "a_submit_bound")
+    wrap(plan_cache.PlanCache, "lookup_entry", "b_lookup_entry")
+    wrap(gpu_common._AggProgram, "submit", "c_program_submit")
+    wrap(gpu_common._ScanPrep, "fast", "d_scan_fast")
+    wrap(gpu_common._JoinPrep, "fast", "d_join_fast")
+    wrap(graphs._RingGraph, "_launch_slot", "e_launch_slot")
+    wrap(gpu_agg.AggOps, "_agg_finish", "f_agg_finish")
+    rt = jit.runtime()
+    for fn in ("hs_graph_launch", "hs_graph_set_args"):
+        wrap(rt, fn, "g_" + fn)
 
 
 if __name__ == "__main__":

@@ -209,8 +209,10 @@ def sync_count(ctx, data_dir):
     hs = Hyperspace(s)
     t1 = s.read.parquet(os.path.join(data_dir, "t1"))
     t2 = s.read.parquet(os.path.join(data_dir, "t2"))
+    t3 = s.read.parquet(os.path.join(data_dir, "t3"))
     hs.createIndex(t1, IndexConfig("i1", ["k"], ["v"]))
     hs.createIndex(t2, IndexConfig("i2", ["k"], ["w", "s"]))
+    hs.createIndex(t3, IndexConfig("i3", ["k"], []))
     Hyperspace.enable(s)
     be = s.backend()
 
@@ -221,6 +223,18 @@ def sync_count(ctx, data_dir):
     def join(i):
         return t1.join(t2, t1["k"] == t2["k"]).filter(col("w") < 3 + i % 2) \
             .groupBy(t2["w"]).agg(sum_(col("v")).alias("sv"))
+
+    def join3(i):
+        # three indexed relations (TPC-H Q3's customer x orders x lineitem shape): the third
+        # joins as a key semi-join
+        return t1.join(t2, t1["k"] == t2["k"]).join(t3, t1["k"] == t3["k"]) \
+            .filter(col("w") < 3 + i % 2).groupBy(t2["w"]).agg(sum_(col("v")).alias("sv"))
+
+    def full(i):
+        # Q3's full result shape: GROUP BY the join key, ORDER BY the aggregate, LIMIT
+        return t1.join(t2, t1["k"] == t2["k"]).filter(col("w") < 3 + i % 2) \
+            .groupBy(t1["k"], t2["w"]).agg(sum_(col("v")).alias("sv")) \
+            .orderBy(col("sv").desc(), col("k")).limit(5)
 
     counts = {"wait": 0}
     waits = []
@@ -239,7 +253,7 @@ def sync_count(ctx, data_dir):
         setattr(obj, name, wrapped)
     out = {}
     try:
-        for qname, q in (("filter", filt), ("join", join)):
+        for qname, q in (("filter", filt), ("join", join), ("join3", join3), ("full", full)):
             for i in range(3):                      # warm: lowering, kernels, program
                 q(i % 2).collect()
             torch.cuda.synchronize()

@@ -251,17 +251,19 @@ def test_rccl_branches_single_rank(tmp_path, device):
 
 @pytest.mark.gpu
 def test_warm_sharded_queries_submit_without_host_syncs(tmp_path, spmd_data, device):
-    """A warm sharded query (plan-cache hit of the indexed filter / join aggregate over an
-    RCCL process group) submits with no host synchronization; reading its result is the one
-    wait (torch's sync debug mode plus wrapped stream / event / device waits count them)."""
+    """A warm sharded query (plan-cache hit of the indexed filter / join aggregate, the 3-way
+    join with a key semi-join, and the grouped-by-key ORDER BY / LIMIT shape over an RCCL
+    process group) submits with no host synchronization; reading its result is the one wait
+    (torch's sync debug mode plus wrapped stream / event / device waits count them)."""
     data, t1, t2 = spmd_data
     res = _spawn("sync_count", tmp_path, str(data), world=1, backend="nccl", timeout=300)
     d = res[0]
-    for q in ("filter", "join"):
+    print({q: d[q] for q in ("filter", "join", "join3", "full")}, d.get("submit_syncs"))
+    for q in ("filter", "join", "join3", "full"):
         for submit, read, path, rows in d[q]:
-            assert path == "native" and rows > 0
-            assert submit == 0, d
-            assert read <= 1, d
+            assert path == "native" and rows > 0, (q, d[q])
+            assert submit == 0, (q, d)
+            assert read <= 1, (q, d)
 
 
 def _gpu_count() -> int:

@@ -424,3 +424,18 @@ def test_bucket_chunks_cover_buckets_within_budget():
             assert hi > lo
             assert hi - lo == 1 or w[lo:hi].sum() <= budget // 2
     assert bucket_chunks(w, 10**9) == [(0, 200)]
+
+
+def test_hostgc_settle_freezes_live_objects():
+    """utils/hostgc.settle: young garbage collected, everything alive moved to the permanent
+    generation (gc.freeze) so later full collections skip it."""
+    import gc
+    from hyperspace_amd.utils import hostgc
+    keep = [[i] for i in range(1000)]
+    n0 = hostgc.STATS["settles"]
+    hostgc.settle()
+    try:
+        assert gc.get_freeze_count() >= len(keep)
+        assert hostgc.STATS["settles"] == n0 + 1
+    finally:
+        gc.unfreeze()
