@@ -14,7 +14,14 @@
 //   hs_graph_capture_end(stream, funcs, nfuncs) -> handle   (kernel node i = first node of funcs[i])
 //   hs_graph_set_args(handle, i, args, size)                 (next launches use these arguments)
 //   hs_graph_launch(handle, stream)
+//   hs_graph_replay(handle, nblocks, blocks, stream, after, done)
+//       one query's replay in one call: optionally order ``stream`` after ``after``'s queued
+//       work, rewrite the first nblocks kernel nodes' argument blocks, launch, and record the
+//       slot's ``done`` event (the Python side's per-call overhead was several torch stream /
+//       event calls per query)
 //   hs_graph_destroy(handle)
+//   hs_event_create() / hs_event_record(ev, stream) / hs_event_query(ev) / hs_event_sync(ev) /
+//   hs_event_destroy(ev)       (timing-disabled events of the replay slots)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -29,6 +36,7 @@ thread_local std::string g_err;
 struct HsGraph {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
+  hipEvent_t join = nullptr;               // hs_graph_replay's ``after`` ordering event
   std::vector<hipGraphNode_t> nodes;       // the kernel node of funcs[i]
   std::vector<hipKernelNodeParams> params;  // its captured launch configuration
 };
@@ -127,9 +135,78 @@ int hs_graph_launch(void* handle, void* stream) {
   return e == hipSuccess ? 0 : fail("hipGraphLaunch", e);
 }
 
+int hs_graph_replay(void* handle, int nblocks, void** blocks, void* stream, void* after,
+                    void* done) {
+  auto* g = (HsGraph*)handle;
+  if (nblocks < 0 || (size_t)nblocks > g->nodes.size()) {
+    g_err = "hs_graph_replay: bad block count";
+    return -1;
+  }
+  hipError_t e;
+  if (after != nullptr && after != stream) {
+    if (g->join == nullptr) {
+      e = hipEventCreateWithFlags(&g->join, hipEventDisableTiming);
+      if (e != hipSuccess) return fail("hipEventCreateWithFlags", e);
+    }
+    e = hipEventRecord(g->join, (hipStream_t)after);
+    if (e != hipSuccess) return fail("hipEventRecord", e);
+    e = hipStreamWaitEvent((hipStream_t)stream, g->join, 0);
+    if (e != hipSuccess) return fail("hipStreamWaitEvent", e);
+  }
+  for (int i = 0; i < nblocks; ++i) {
+    if (blocks[i] == nullptr) continue;
+    hipKernelNodeParams p = g->params[i];
+    void* kp[1] = {blocks[i]};
+    p.kernelParams = kp;
+    p.extra = nullptr;
+    e = hipGraphExecKernelNodeSetParams(g->exec, g->nodes[i], &p);
+    if (e != hipSuccess) return fail("hipGraphExecKernelNodeSetParams", e);
+  }
+  e = hipGraphLaunch(g->exec, (hipStream_t)stream);
+  if (e != hipSuccess) return fail("hipGraphLaunch", e);
+  if (done != nullptr) {
+    e = hipEventRecord((hipEvent_t)done, (hipStream_t)stream);
+    if (e != hipSuccess) return fail("hipEventRecord", e);
+  }
+  return 0;
+}
+
+void* hs_event_create() {
+  hipEvent_t ev = nullptr;
+  const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    fail("hipEventCreateWithFlags", e);
+    return nullptr;
+  }
+  return ev;
+}
+
+int hs_event_record(void* ev, void* stream) {
+  const hipError_t e = hipEventRecord((hipEvent_t)ev, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : fail("hipEventRecord", e);
+}
+
+// 0: complete, 1: not ready, < 0: error
+int hs_event_query(void* ev) {
+  const hipError_t e = hipEventQuery((hipEvent_t)ev);
+  if (e == hipSuccess) return 0;
+  if (e == hipErrorNotReady) return 1;
+  return -fail("hipEventQuery", e);
+}
+
+int hs_event_sync(void* ev) {
+  const hipError_t e = hipEventSynchronize((hipEvent_t)ev);
+  return e == hipSuccess ? 0 : fail("hipEventSynchronize", e);
+}
+
+void hs_event_destroy(void* ev) {
+  if (ev != nullptr) hipEventDestroy((hipEvent_t)ev);
+}
+
 void hs_graph_destroy(void* handle) {
   auto* g = (HsGraph*)handle;
   if (g == nullptr) return;
+  if (g->join) hipEventDestroy(g->join);
   if (g->exec) hipGraphExecDestroy(g->exec);
   if (g->graph) hipGraphDestroy(g->graph);
   delete g;

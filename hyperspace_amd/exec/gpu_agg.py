@@ -847,8 +847,7 @@ class AggOps:
             prep.marked = side
         for x in keep:      # per-query predicate buffers (IN sets, key bitmaps)
             _use_on(x, side)
-        with torch.cuda.stream(side):
-            handle = g.launch(bounds, packed)
+        handle = g.launch(bounds, packed, stream=side)
         return (_GraphPending(g, handle), None, None, None)
 
     def _graph_prep(self, r: DRel, p: NL.ScanParams, kc, GA: int, descs) -> "_GraphPrep":

@@ -355,11 +355,10 @@ class _ScanPrep:
             handle = g.launch(hit[0], hit[1])
         else:
             import torch
-            side.wait_stream(torch.cuda.current_stream())
             for x in hit[2]:
                 _use_on(x, side)
-            with torch.cuda.stream(side):
-                handle = g.launch(hit[0], hit[1])
+            # on the side stream, ordered after this stream's queued work (one native call)
+            handle = g.launch(hit[0], hit[1], stream=side, after=torch.cuda.current_stream())
         return (_GraphPending(g, handle), None, None, None, G, gbase, gdict, gtype)
 
 

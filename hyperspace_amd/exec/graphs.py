@@ -47,7 +47,10 @@ class _Pinned:
             raise MemoryError(f"hipHostMalloc({nbytes}) failed")
 
     def view(self) -> np.ndarray:
-        return np.ctypeslib.as_array((C.c_uint8 * self.nbytes).from_address(self.ptr))
+        v = getattr(self, "_view", None)
+        if v is None:       # the block never moves: one numpy view for its lifetime
+            v = self._view = np.ctypeslib.as_array((C.c_uint8 * self.nbytes).from_address(self.ptr))
+        return v
 
     def __del__(self):
         if getattr(self, "ptr", None):
@@ -63,18 +66,33 @@ class _Slot:
     ready."""
 
     def __init__(self, params_bytes: int, out_bytes: int):
-        import torch
         self.h_params = _Pinned(max(params_bytes, 8))
         self.h_out = _Pinned(out_bytes)
         self.graph = None          # native handle (csrc/runtime/hs_graph.cpp)
-        self.event = torch.cuda.Event()
+        # native timing-disabled event: recorded by hs_graph_replay in the same call as the
+        # launch (a torch.cuda.Event costs a few Python-level calls per query)
+        self.event = jit.runtime().hs_event_create()
+        if not self.event:
+            raise RuntimeError(f"hs_event_create: {jit.runtime().hs_graph_last_error().decode()}")
         self.launched = False
         self.current = None   # _Launch whose result the slot's h_out holds / will hold
 
+    def done(self) -> bool:
+        rc = jit.runtime().hs_event_query(self.event)
+        _rt_check(rc if rc < 0 else 0, "hs_event_query")
+        return rc == 0
+
+    def wait(self) -> None:
+        _rt_check(jit.runtime().hs_event_sync(self.event), "hs_event_sync")
+
     def __del__(self):
+        R = jit.runtime()
         if getattr(self, "graph", None):
-            jit.runtime().hs_graph_destroy(self.graph)
+            R.hs_graph_destroy(self.graph)
             self.graph = None
+        if getattr(self, "event", None):
+            R.hs_event_destroy(self.event)
+            self.event = None
 
 
 class _Launch:
@@ -138,37 +156,43 @@ class _RingGraph:
         cur.wait_stream(side)
         slot.graph = h
 
-    def _launch_slot(self, fill, blocks) -> _Launch:
-        """Queue one query on the current stream: ``fill(host_params_view)`` writes its pinned
-        parameter block, ``blocks`` are the packed argument blocks of ``kernels``.  A slot still
-        holding an unread earlier result is drained first (wait for it and keep its result on
-        the earlier handle: back-pressure, no lost results); a slot's graph gets new kernel
-        arguments only once its previous replay has finished."""
+    def _launch_slot(self, fill, blocks, stream=None, after=None) -> _Launch:
+        """Queue one query on ``stream`` (default: the current stream), ordered after the work
+        queued on ``after`` when given: ``fill(host_params)`` writes its pinned parameter block
+        (a ``_Pinned``), ``blocks`` are the packed argument blocks (``_cbuf``) of ``kernels``.
+        A slot still holding an unread earlier result is drained first (wait for it and keep
+        its result on the earlier handle: back-pressure, no lost results); a slot's graph gets
+        new kernel arguments only once its previous replay has finished.  A replay is one native
+        call (``hs_graph_replay``: ordering, argument rewrite, launch, completion event)."""
         import torch
         slot = self.slots[self._next]
         self._next = (self._next + 1) % len(self.slots)
         prev = slot.current
         if prev is not None and prev.value is None:
             prev.value = self._read(slot)
-        elif slot.launched and not slot.event.query():
-            slot.event.synchronize()    # back-pressure: the slot's replay is still running
-        fill(slot.h_params.view())
-        cur = torch.cuda.current_stream()
+        elif slot.launched and not slot.done():
+            slot.wait()    # back-pressure: the slot's replay is still running
+        fill(slot.h_params)
+        cur = stream if stream is not None else torch.cuda.current_stream()
         st = cur.cuda_stream
-        if not self._warm:
-            self._enqueue(slot, st, blocks)   # first run of the shape: eager (loads the modules)
-            self._warm = True
-        elif slot.graph is None:
-            self._capture(slot, blocks, cur)
-            _rt_check(jit.runtime().hs_graph_launch(slot.graph, st), "hs_graph_launch")
+        R = jit.runtime()
+        if slot.graph is not None:
+            ptrs = (C.c_void_p * len(blocks))(*[C.addressof(b) for b in blocks])
+            _rt_check(R.hs_graph_replay(slot.graph, len(blocks), ptrs, st,
+                                        after.cuda_stream if after is not None else None,
+                                        slot.event), "hs_graph_replay")
             self.replays += 1
         else:
-            R = jit.runtime()
-            for i, b in enumerate(blocks):
-                _rt_check(R.hs_graph_set_args(slot.graph, i, b, len(b)), "hs_graph_set_args")
-            _rt_check(R.hs_graph_launch(slot.graph, st), "hs_graph_launch")
-            self.replays += 1
-        slot.event.record(cur)
+            if after is not None:
+                cur.wait_stream(after)
+            if not self._warm:
+                self._enqueue(slot, st, blocks)   # first run of the shape: eager (loads modules)
+                self._warm = True
+            else:
+                self._capture(slot, blocks, cur)
+                _rt_check(R.hs_graph_launch(slot.graph, st), "hs_graph_launch")
+                self.replays += 1
+            _rt_check(R.hs_event_record(slot.event, st), "hs_event_record")
         slot.launched = True
         h = _Launch(slot)
         slot.current = h
@@ -181,7 +205,7 @@ class _RingGraph:
         return h.value
 
     def _read(self, slot: _Slot):
-        slot.event.synchronize()
+        slot.wait()
         h = slot.h_out.view()
         n = 8 * self.GA
         return (h[0:n].view(np.float64).copy(), h[n:2 * n].view(np.int64).copy(),
@@ -258,16 +282,18 @@ class ScanAggGraph(_RingGraph):
                 "psum": self.parts[0].data_ptr(), "pcnt": self.parts[1].data_ptr(),
                 "pmin": self.parts[2].data_ptr(), "pmax": self.parts[3].data_ptr()}
 
-    def launch(self, bounds: Tuple[int, int, int, int, int, int], args_block) -> _Launch:
-        """Queue one query on the current stream; ``result(handle)`` waits for it.
-        ``args_block``: the scan kernel's packed arguments (bytes or a ``_cbuf``)."""
-        head = np.frombuffer(struct.pack("<6q", *bounds), dtype=np.uint8)
+    def launch(self, bounds: Tuple[int, int, int, int, int, int], args_block, stream=None,
+               after=None) -> _Launch:
+        """Queue one query on ``stream`` (default current), after ``after``'s queued work when
+        given; ``result(handle)`` waits for it.  ``args_block``: the scan kernel's packed
+        arguments (bytes or a ``_cbuf``)."""
+        head = struct.pack("<6q", *bounds)
 
         def fill(hp):
-            hp[:48] = head
+            C.memmove(hp.ptr, head, 48)
         if not isinstance(args_block, C.Array):
             args_block = _cbuf(args_block)
-        return self._launch_slot(fill, (args_block,))
+        return self._launch_slot(fill, (args_block,), stream, after)
 
     def run(self, bounds: Tuple[int, int, int, int, int, int], args_block):
         """(sum, count, min, max) numpy arrays for one query (launch + wait)."""

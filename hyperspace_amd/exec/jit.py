@@ -113,6 +113,19 @@ def runtime():
                 L.hs_graph_launch.argtypes = [C.c_void_p, C.c_void_p]
                 L.hs_graph_destroy.restype = None
                 L.hs_graph_destroy.argtypes = [C.c_void_p]
+                L.hs_graph_replay.restype = C.c_int
+                L.hs_graph_replay.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                              C.c_void_p, C.c_void_p]
+                L.hs_event_create.restype = C.c_void_p
+                L.hs_event_create.argtypes = []
+                L.hs_event_record.restype = C.c_int
+                L.hs_event_record.argtypes = [C.c_void_p, C.c_void_p]
+                L.hs_event_query.restype = C.c_int
+                L.hs_event_query.argtypes = [C.c_void_p]
+                L.hs_event_sync.restype = C.c_int
+                L.hs_event_sync.argtypes = [C.c_void_p]
+                L.hs_event_destroy.restype = None
+                L.hs_event_destroy.argtypes = [C.c_void_p]
                 L.hs_graph_last_error.restype = C.c_char_p
                 _rt = L
     return _rt
