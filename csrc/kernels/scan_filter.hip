@@ -342,6 +342,38 @@ __global__ __launch_bounds__(SF_BLOCK) void hs_scan_select_kernel(
   }
 }
 
+// Filter -> key bitmap: bit (key - base) of the key column ``key_slot`` for every row that
+// passes the predicate.  A semi-join's build side (TPC-H Q3's customers of one market segment)
+// goes from its filtered scan straight into the bitmap the probe tests: no row-id compaction,
+// so no selected-row count has to reach the host to size a buffer, and the query submits
+// without a synchronization.  Keys outside [base, base + nbits) and null keys set no bit.
+__global__ __launch_bounds__(SF_BLOCK) void hs_scan_bitmap_kernel(
+    ScanParams p, const int64_t* __restrict__ rstart, const int64_t* __restrict__ rlen, int R,
+    const int64_t* __restrict__ tile_prefix, int key_slot, int64_t base, int64_t nbits,
+    unsigned long long* __restrict__ words) {
+  int64_t t0, t1;
+  block_tile_chunk(tile_prefix[R], t0, t1);
+  if (t0 >= t1) return;
+  const ColDesc kc = p.cols[key_slot];
+  TileWalker tw{tile_prefix, rstart, rlen, R, 0};
+  tw.init(t0);
+  for (int64_t t = t0; t < t1; ++t) {
+    int64_t row0, rows;
+    tw.at(t, row0, rows);
+    int64_t r[SF_ITEMS];
+    bool act[SF_ITEMS], pass[SF_ITEMS];
+    tile_rows(row0, rows, r, act);
+    veval_cnf(p.preds, 0, p.npreds, p.cols, HS_MAX_COLS, r, r, act, pass);
+#pragma unroll
+    for (int i = 0; i < SF_ITEMS; ++i) {
+      if (!pass[i] || !col_valid(kc, r[i])) continue;
+      const int64_t v = load_i64(kc, r[i]) - base;
+      if (v < 0 || v >= nbits) continue;
+      atomicOr(&words[v >> 6], 1ull << (v & 63));
+    }
+  }
+}
+
 extern "C" {
 
 int hs_scan_params_size() { return (int)sizeof(ScanParams); }
@@ -429,6 +461,15 @@ int hs_scan_count(const ScanParams* p, const int64_t* rstart, const int64_t* rle
                   const int64_t* tile_prefix, int grid, int64_t* tile_counts, void* stream) {
   hipLaunchKernelGGL(hs_scan_count_kernel, dim3(grid), dim3(SF_BLOCK), 0, (hipStream_t)stream, *p,
                      rstart, rlen, R, tile_prefix, tile_counts);
+  return (int)hipGetLastError();
+}
+
+int hs_scan_bitmap(const ScanParams* p, const int64_t* rstart, const int64_t* rlen, int R,
+                   const int64_t* tile_prefix, int grid, int key_slot, int64_t base, int64_t nbits,
+                   unsigned long long* words, void* stream) {
+  if (key_slot < 0 || key_slot >= HS_MAX_COLS) return -1;
+  hipLaunchKernelGGL(hs_scan_bitmap_kernel, dim3(grid), dim3(SF_BLOCK), 0, (hipStream_t)stream, *p,
+                     rstart, rlen, R, tile_prefix, key_slot, base, nbits, words);
   return (int)hipGetLastError();
 }
 

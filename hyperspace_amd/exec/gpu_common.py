@@ -248,13 +248,25 @@ def _eval_scalar(e, agg_val, attr_val):
     raise Unsupported(f"result expression {type(e).__name__}")
 
 
+_SEMI_LITS: dict = {}
+
+
 def _semi_fail_key(node) -> tuple:
     """Memo key of a semi-join whose build keys repeated: the join node AND the literal values
     under it - a plan-cache hit re-submits the same nodes with other literals, whose filtered
     build side may well be unique."""
-    from ..plan.plan_cache import _iter_literals
-    lits: list = []
-    _iter_literals(node, lits, set())
+    hit = _SEMI_LITS.get(id(node))
+    if hit is not None and hit[0] is node:
+        lits = hit[1]
+    else:
+        # the literal OBJECTS under a node are fixed (a bound plan-cache hit rewrites their
+        # values in place): walk the subtree once per node, read the values per query
+        from ..plan.plan_cache import _iter_literals
+        lits = []
+        _iter_literals(node, lits, set())
+        if len(_SEMI_LITS) >= 256:
+            _SEMI_LITS.clear()
+        _SEMI_LITS[id(node)] = (node, lits)
     try:
         vals = tuple(x.value for x in lits)
         hash(vals)
@@ -564,9 +576,23 @@ def _strip_exchange(p):
     return None
 
 
+_PLAN_BYTES: dict = {}
+
+
 def _plan_bytes(p) -> int:
     """Bytes of the files under a physical plan's scans (the build side of a semi-join is the
-    side with fewer)."""
+    side with fewer); memoized per plan node (its file listings are fixed)."""
+    hit = _PLAN_BYTES.get(id(p))
+    if hit is not None and hit[0] is p:
+        return hit[1]
+    n = _plan_bytes_walk(p)
+    if len(_PLAN_BYTES) >= 256:
+        _PLAN_BYTES.clear()
+    _PLAN_BYTES[id(p)] = (p, n)
+    return n
+
+
+def _plan_bytes_walk(p) -> int:
     n = 0
     for s in p.collect(lambda x: isinstance(x, X.FileSourceScanExec)):
         try:

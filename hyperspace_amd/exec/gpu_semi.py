@@ -162,10 +162,14 @@ class SemiJoinOps:
             crel = self._rel(_strip_exchange(cside) or cside)
             if crel.parts:
                 return None
-            keys = self._materialize(crel, [cjk])[cjk.expr_id]
             src = crel.col(cjk) if crel.bucketed and crel.sort_attrs and \
                 crel.sort_attrs[0].expr_id == cjk.expr_id and not crel.is_computed(cjk) else None
-            bm = self._semi_bitmap(keys, src)
+            bm = self._filtered_bitmap(crel, cjk, src)
+            nkeys = None
+            if bm is None:
+                keys = self._materialize(crel, [cjk])[cjk.expr_id]
+                nkeys = int(keys.data.numel())
+                bm = self._semi_bitmap(keys, src)
         if bm is None:
             return None
         words, lo, nbits = bm
@@ -175,8 +179,9 @@ class SemiJoinOps:
         for f in reversed(upper):
             orel = self._unary(f, orel)
         orel = orel.copy(conds=orel.conds + [CP.KeyBitmap(ojk, words, lo, nbits)])
-        self.last_semi_join = {"build_keys": int(keys.data.numel()), "bitmap_bits": nbits,
-                               "probe": "copart", "index": ascan.relation.index.name}
+        self.last_semi_join = {"build_keys": nkeys, "bitmap_bits": nbits, "probe": "copart",
+                               "index": ascan.relation.index.name,
+                               "build": "materialized" if nkeys is not None else "fused"}
         agreed, G, gbase, gdict, gtype = gs
         self._groups_agreed = agreed is True
         self._join_rec = None
@@ -352,6 +357,44 @@ class SemiJoinOps:
         for f in reversed(filters):
             r = self._unary(f, r)
         return self._unary(p, r)
+
+    def _filtered_bitmap(self, r: DRel, key: E.Attribute, src: Optional[DeviceColumn]):
+        """(words, lo, nbits) of the keys of ``r``'s rows passing its predicates, built by one
+        filter-to-bitmap launch (``K.scan_bitmap``) - no selected-row materialization, so no
+        host synchronization - when ``src`` is the resident, sorted index key column those rows
+        come from, single rank, with a cached domain that fits the bitmap and no repeated key
+        (then every selection of it is unique too).  None when that does not hold (the
+        materializing path runs)."""
+        d = self._dist()
+        if (d is not None and d.world > 1) or src is None or src.valid is not None or \
+                getattr(src, "hs_transient", False) or \
+                src.hs_type not in (NL.I8, NL.I16, NL.I32, NL.I64) or r.table is None or \
+                r.split or r.extra or jit.key_has_dups(src):
+            return None
+        lo, span = self._local_domain(src)
+        if span == 0 or span > K.MAX_BITMAP_BITS:
+            return None
+        implied: set = set()
+        rstart, rlen, _ = self._ranges(r, r.conds, implied)
+        col_info, descs = self._column_infos([(r, 0)])
+        bound = CP.bind(CP.to_cnf([c for c in r.conds if id(c) not in implied]), col_info,
+                        self.device)
+        kslot = col_info(key).slot
+        if len(bound.preds) > NL.MAX_PREDS:
+            return None
+        if bound.always_false:
+            import torch
+            return torch.zeros(max((span + 63) // 64, 1), dtype=torch.int64,
+                               device=self.device), lo, span
+        p = NL.ScanParams()
+        for s_, c in descs.items():
+            p.cols[s_] = c.desc()
+        for i, pr in enumerate(bound.preds):
+            p.preds[i] = pr
+        p.npreds = len(bound.preds)
+        p.naggs, p.group_col = 0, -1
+        words = K.scan_bitmap(p, rstart, rlen, K.ranges_to_tiles(rlen), kslot, lo, span)
+        return words, lo, span
 
     def _semi_bitmap(self, keys: DeviceColumn, src: Optional[DeviceColumn] = None):
         """(words, lo, nbits) of the build keys over every rank's keys, or None when they are

@@ -176,6 +176,7 @@ def lib():
     _sig(L.hs_scan_agg, I, P, P, P, I, P, I, P, P, P, P, P, P, P, P, P)
     _sig(L.hs_scan_count, I, P, P, P, I, P, I, P, P)
     _sig(L.hs_scan_select, I, P, P, P, I, P, P, I, P, P)
+    _sig(L.hs_scan_bitmap, I, P, P, P, I, P, I, I, I64, I64, P, P)
     _sig(L.hs_join_agg, I, P, P, P, P, P, I, P, I64, P, I, P, P, P, P, P, P, P, P, P)
     _sig(L.hs_agg_final, I, P, P, P, P, I, I, P, P, P, P, P)
     _sig(L.hs_join_count, I, P, P, P, P, P, I, P, I64, P, I, P, P)

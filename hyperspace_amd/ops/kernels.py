@@ -703,6 +703,20 @@ def scan_agg(params: NL.ScanParams, rstart, rlen, tile_prefix, grid: int = None)
     return os_, oc, omn, omx
 
 
+def scan_bitmap(params: NL.ScanParams, rstart, rlen, tile_prefix, key_slot: int, lo: int,
+                nbits: int):
+    """int64 words of an ``nbits``-bit bitmap with bit (key - lo) set for the key column
+    ``key_slot`` of every row passing the predicate (csrc/kernels/scan_filter.hip
+    ``hs_scan_bitmap``): filter and bitmap build in one launch, no host synchronization."""
+    torch = _torch()
+    L = NL.lib()
+    words = torch.zeros(max((nbits + 63) // 64, 1), dtype=torch.int64, device=rstart.device)
+    NL.check(L.hs_scan_bitmap(C.byref(params), NL.ptr(rstart), NL.ptr(rlen), rstart.numel(),
+                              NL.ptr(tile_prefix), L.hs_scan_grid(), int(key_slot), int(lo),
+                              int(nbits), NL.ptr(words), NL.stream_ptr()), "hs_scan_bitmap")
+    return words
+
+
 def scan_select(params: NL.ScanParams, rstart, rlen, tile_prefix, max_tiles: int):
     """Row ids (int64, ascending within each range) of rows passing the predicate."""
     torch = _torch()

@@ -212,6 +212,7 @@ def sync_count(ctx, data_dir):
     t3 = s.read.parquet(os.path.join(data_dir, "t3"))
     hs.createIndex(t1, IndexConfig("i1", ["k"], ["v"]))
     hs.createIndex(t2, IndexConfig("i2", ["k"], ["w", "s"]))
+    hs.createIndex(t2, IndexConfig("i2w", ["w"], ["k"]))
     hs.createIndex(t3, IndexConfig("i3", ["k"], []))
     Hyperspace.enable(s)
     be = s.backend()
@@ -225,10 +226,11 @@ def sync_count(ctx, data_dir):
             .groupBy(t2["w"]).agg(sum_(col("v")).alias("sv"))
 
     def join3(i):
-        # three indexed relations (TPC-H Q3's customer x orders x lineitem shape): the third
-        # joins as a key semi-join
-        return t1.join(t2, t1["k"] == t2["k"]).join(t3, t1["k"] == t3["k"]) \
-            .filter(col("w") < 3 + i % 2).groupBy(t2["w"]).agg(sum_(col("v")).alias("sv"))
+        # TPC-H Q3's 3-way shape (customer x orders on custkey, filtered, then x lineitem on
+        # orderkey): t3 plays customer, t2.w o_custkey, t2.k o_orderkey, t1 lineitem
+        co = t3.join(t2, t3["k"] == t2["w"]).filter(t2["w"] < 3 + i % 2)
+        return co.join(t1, t2["k"] == t1["k"]).agg(sum_(t1["v"]).alias("sv"),
+                                                   count("*").alias("n"))
 
     def full(i):
         # Q3's full result shape: GROUP BY the join key, ORDER BY the aggregate, LIMIT
@@ -280,8 +282,13 @@ def sync_count(ctx, data_dir):
                     res = fut.result()
                     torch.cuda.set_sync_debug_mode("default")
                 read = counts["wait"] + sum(_is_sync_warning(x) for x in w)
+                if read > 1:
+                    out.setdefault("read_syncs", {}).setdefault(qname, [
+                        str(x.message)[:60] + " @ " + f"{x.filename}:{x.lineno}" for x in w
+                        if _is_sync_warning(x)] + counts.get("where", []))
                 per.append((submit, read, fut.path, res.num_rows))
             out[qname] = per
+            out.setdefault("semi", {})[qname] = getattr(be, "last_semi_join", None)
     finally:
         torch.cuda.set_sync_debug_mode("default")
         for obj, name, orig in waits:
