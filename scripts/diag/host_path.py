@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--profile", action="store_true", help="cProfile the build + lookup loops")
     ap.add_argument("--phases", action="store_true",
                     help="time the submission's phases (wrapped functions) and the GC passes")
+    ap.add_argument("--fresh", action="store_true",
+                    help="every timed query has a literal vector not seen before (the path a "
+                         "short bench run mostly takes: lowering + argument packing per query)")
     ap.add_argument("--gc-freeze", action="store_true",
                     help="gc.freeze() after warm-up (objects alive then leave the GC's scans)")
     ap.add_argument("--data-dir", default=os.environ.get("HS_BENCH_DIR", "/tmp/hs_bench"))
@@ -74,8 +77,26 @@ def main():
             sum_(col("l_extendedprice") * (1 - col("l_discount"))).alias("revenue"),
             count("*").alias("lines"))
 
+    if args.fresh:
+        base6, base3 = q6, q3
+
+        def q6(i):      # noqa: F811 - a new l_quantity bound per query
+            return li.filter((col("l_shipdate") >= datetime.date(1994, 1, 1)) &
+                             (col("l_shipdate") < datetime.date(1995, 1, 1)) &
+                             (col("l_discount") >= 0.05) & (col("l_discount") <= 0.07) &
+                             (col("l_quantity") < 24.0 + (i % 100000) * 1e-4)) \
+                .agg(sum_(col("l_extendedprice") * col("l_discount")).alias("revenue"))
+
+        def q3(i):      # noqa: F811 - a new date per query
+            dd = datetime.date(1990, 1, 1) + datetime.timedelta(days=i % 4000)
+            j = li.join(od, li["l_orderkey"] == od["o_orderkey"]) \
+                .filter((col("o_orderdate") < dd) & (col("l_shipdate") > dd))
+            return j.groupBy("o_shippriority").agg(
+                sum_(col("l_extendedprice") * (1 - col("l_discount"))).alias("revenue"),
+                count("*").alias("lines"))
+        del base6, base3
     pc = plan_cache(s)
-    out = {"sf": args.sf, "device": args.device, "n": args.n}
+    out = {"sf": args.sf, "device": args.device, "n": args.n, "fresh": args.fresh}
     acc = {}
     if args.phases:
         import gc
@@ -123,7 +144,7 @@ def main():
         if args.device == "gpu":
             # submission alone: the device is idle at each submit (no ring back-pressure)
             import torch
-            dfs = [fn(i) for i in range(300)]
+            dfs = [fn(i + (5000 if args.fresh else 0)) for i in range(300)]
             sub, fin = [], []
             sprof = None
             if args.profile:
