@@ -148,6 +148,9 @@ class Session:
     def enableHyperspace(self) -> "Session":
         from .rules import enable
         enable(self)
+        if HyperspaceConf.gc_freeze_enabled(self.conf) and self.device_kind() == "gpu":
+            from .utils import hostgc
+            hostgc.settle(full=True)      # a serving phase starts: freeze the settled heap
         return self
 
     def disableHyperspace(self) -> "Session":

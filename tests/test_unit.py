@@ -437,5 +437,18 @@ def test_hostgc_settle_freezes_live_objects():
     try:
         assert gc.get_freeze_count() >= len(keep)
         assert hostgc.STATS["settles"] == n0 + 1
+        # a full settle reclaims cyclic garbage frozen by an earlier one
+        import weakref
+
+        class Node:
+            pass
+        a, b = Node(), Node()
+        a.b, b.a = b, a
+        ref = weakref.ref(a)
+        hostgc.settle()
+        del a, b
+        assert ref() is not None           # frozen: the young passes never see it
+        hostgc.settle(full=True)
+        assert ref() is None
     finally:
         gc.unfreeze()
