@@ -82,11 +82,18 @@ def plan(total_bytes: int, share: int, arena_conf: int, cache_conf: int) -> Rank
 
 
 _CACHED: dict = {}
+# (conf, conf version, device) -> budget: the query path asks per query (gpu_agg._stream_chunks)
+# and the rank's environment and the device's size do not change within a process
+_FAST: dict = {}
 
 
 def rank_budget(conf, device=None) -> RankBudget:
     """This process's budgets for ``device`` (the current one by default), from the session
     conf (arena and cache keys) and the device's total memory."""
+    fk = (id(conf), getattr(conf, "version", None), device)
+    hit = _FAST.get(fk)
+    if hit is not None and hit[0] is conf:
+        return hit[1]
     from ..utils.conf import HyperspaceConf
     import torch
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -97,4 +104,8 @@ def rank_budget(conf, device=None) -> RankBudget:
     b = _CACHED.get(key)
     if b is None:
         b = _CACHED[key] = plan(total, share, key[3], key[4])
+    if device is not None:      # (the current device may change between calls)
+        if len(_FAST) >= 64:
+            _FAST.clear()
+        _FAST[fk] = (conf, b)
     return b
