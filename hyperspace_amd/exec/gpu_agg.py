@@ -802,12 +802,14 @@ class AggOps:
         g, k, compacts = prep.g, prep.k, prep.compacts
         hit = prep.packed.get(lkey) if lkey is not None else None
         if hit is None:
-            values = dict(prep.values)
+            if prep.tpl is None:
+                prep.tpl = bytes(k.args.pack(prep.values, default=0))
+            values: dict = {}
             jit.fill_preds_aggs(values, [(i, p.preds[i]) for i in range(p.npreds)],
                                 [p.aggs[i] for i in range(p.naggs)], compacts)
             # (the per-query predicate buffers the block points to stay referenced with it)
-            hit = (range_bounds(lo, lo_incl, hi, hi_incl), _cbuf(k.args.pack(values)),
-                   list(keep))
+            hit = (range_bounds(lo, lo_incl, hi, hi_incl),
+                   _cbuf(k.args.patch(bytearray(prep.tpl), values)), list(keep))
             if lkey is not None:
                 if len(prep.packed) >= 1024:
                     prep.packed.clear()

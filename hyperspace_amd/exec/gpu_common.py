@@ -280,11 +280,12 @@ class _Stale(Exception):
 
 
 class _GraphPrep:
-    __slots__ = ("key", "g", "k", "compacts", "values", "GA", "packed", "marked")
+    __slots__ = ("key", "g", "k", "compacts", "values", "GA", "packed", "marked", "tpl")
 
     def __init__(self, key, g, k, compacts, values, GA):
         self.key, self.g, self.k, self.compacts, self.values, self.GA = \
             key, g, k, compacts, values, GA
+        self.tpl = None     # packed block of the literal-independent slots (Args.patch)
         self.packed: Dict[tuple, tuple] = {}     # literal vector -> (range bounds, args block)
         self.marked = None    # the side stream every persistent buffer was marked in use by
 

@@ -140,11 +140,13 @@ class Args:
     def __init__(self):
         self.slots: List[Tuple[str, str, str]] = []
         self._index: Dict[str, int] = {}
+        self._layout = None    # (struct format, [(name, is_double)]) once the slots are final
 
     def add(self, kind: str, name: str, ctype: str) -> str:
         if name not in self._index:
             self._index[name] = len(self.slots)
             self.slots.append((kind, name, ctype))
+            self._layout = None
         return f"a.{name}"
 
     def struct_src(self) -> str:
@@ -155,13 +157,39 @@ class Args:
         """Byte offset of slot ``name`` in the packed block (every slot is 8 bytes)."""
         return 8 * self._index[name]
 
-    def pack(self, values: Dict[str, object]) -> bytes:
-        fmt = "<" + "".join("q" if k in ("p", "q") else "d" for k, _, _ in self.slots)
-        vals = []
-        for k, n, _ in self.slots:
-            v = values[n]
-            vals.append(float(v) if k == "d" else int(v or 0))
+    def _lay(self):
+        lay = self._layout
+        if lay is None:
+            lay = self._layout = (
+                "<" + "".join("q" if k in ("p", "q") else "d" for k, _, _ in self.slots),
+                [(n, k == "d") for k, n, _ in self.slots])
+        return lay
+
+    def pack(self, values: Dict[str, object], default=None) -> bytes:
+        """The argument block of ``values`` (every slot; ``default`` fills missing ones)."""
+        fmt, names = self._lay()
+        if default is None:
+            vals = [float(values[n]) if d else int(values[n] or 0) for n, d in names]
+        else:
+            vals = [float(values.get(n, default)) if d else int(values.get(n, default) or 0)
+                    for n, d in names]
         return struct.pack(fmt, *vals)
+
+    def patch(self, block: bytearray, values: Dict[str, object]) -> bytearray:
+        """``block`` (a packed template) with the slots named in ``values`` rewritten (names
+        that are not slots of this kernel are skipped): a new literal vector re-packs only its
+        literal slots."""
+        idx = self._index
+        slots = self.slots
+        for n, v in values.items():
+            i = idx.get(n)
+            if i is None:
+                continue
+            if slots[i][0] == "d":
+                struct.pack_into("<d", block, 8 * i, float(v))
+            else:
+                struct.pack_into("<q", block, 8 * i, int(v or 0))
+        return block
 
 
 # kernels this process compiled with hipRTC / loaded from the on-disk code-object cache

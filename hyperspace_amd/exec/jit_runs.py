@@ -991,7 +991,7 @@ class TwoPhaseLauncher:
     """Both phases lowered once (kernels, tiles, spans, per-tile run windows, the tag bitmap);
     ``launch(p)`` fills the literal slots and queues: bitmap clear, tags, scan, partials fold."""
     __slots__ = ("kt", "ks", "grid_t", "grid_s", "GA", "shmem", "vt", "vs", "compacts", "keep",
-                 "tags", "dev", "blocks", "hk", "graph", "gblocks", "tk")
+                 "tags", "dev", "blocks", "hk", "graph", "gblocks", "tk", "tpl")
 
     def __init__(self, kt, ks, grid_t, grid_s, GA, shmem, vt, vs, compacts, keep, tags, dev,
                  hk=None, tk=None):
@@ -1007,6 +1007,9 @@ class TwoPhaseLauncher:
         # the captured pipeline (graphs.TwoPhaseGraph) and its per-literal-vector blocks
         self.graph = None
         self.gblocks: dict = {}
+        # packed argument blocks of the literal-independent slots: a new literal vector patches
+        # only its literal slots into copies of these
+        self.tpl = None
 
     def graphable(self) -> bool:
         """Whether one query's launches can be captured: partials out (not the hash mode)."""
@@ -1039,12 +1042,17 @@ class TwoPhaseLauncher:
         if hit is None:
             preds = [(k_, p.preds[k_]) for k_ in range(p.npreds)]
             aggs = [p.aggs[i] for i in range(p.naggs)]
-            vt = dict(self.vt)
-            J.fill_preds_aggs(vt, preds, [], self.compacts)
-            vs = dict(self.vs)
-            vs.update({"psum": 0, "pcnt": 0, "pmin": 0, "pmax": 0})
-            J.fill_preds_aggs(vs, preds, aggs, self.compacts)
-            hit = (self.kt.args.pack(vt), bytearray(self.ks.args.pack(vs)))
+            if self.tpl is None:
+                vs0 = dict(self.vs)
+                vs0.update({"psum": 0, "pcnt": 0, "pmin": 0, "pmax": 0})
+                self.tpl = (bytes(self.kt.args.pack(self.vt, default=0)),
+                            bytes(self.ks.args.pack(vs0, default=0)))
+            lt: dict = {}
+            J.fill_preds_aggs(lt, preds, [], self.compacts)
+            ls: dict = {}
+            J.fill_preds_aggs(ls, preds, aggs, self.compacts)
+            hit = (bytes(self.kt.args.patch(bytearray(self.tpl[0]), lt)),
+                   self.ks.args.patch(bytearray(self.tpl[1]), ls))
             if key is not None:
                 if len(self.blocks) >= 256:
                     self.blocks.clear()

@@ -923,3 +923,22 @@ def test_run_topk_sources_compile(rt, tmp_path):
         rc = jit.runtime().hs_jit_compile_to_cache(k.src.encode(), k.name.encode(), b"gfx950",
                                                    str(tmp_path).encode())
         assert rc == 0, jit.runtime().hs_jit_last_error().decode()
+
+
+def test_args_template_patch_equals_full_pack():
+    """A new literal vector's argument block packed as template + patched literal slots
+    (``Args.patch``: TwoPhaseLauncher / scan graph fresh path) equals packing every slot."""
+    from hyperspace_amd.exec.jit import Args
+    a = Args()
+    for kind, name in (("p", "RK0"), ("q", "L0"), ("d", "F0"), ("q", "CL0"), ("q", "NRUNS"),
+                       ("d", "A0_0"), ("p", "psum")):
+        a.add(kind, name, "long long" if kind != "d" else "double")
+    base = {"RK0": 1 << 40, "NRUNS": 123, "psum": 0, "L0": 5, "F0": 1.5, "CL0": -7,
+            "A0_0": 2.0}
+    lits = {"L0": 9, "F0": -0.25, "CL0": 3, "A0_0": 0.5, "X_not_a_slot": 1}
+    full = dict(base)
+    full.update({k: v for k, v in lits.items() if k != "X_not_a_slot"})
+    tpl = bytearray(a.pack(base, default=0))
+    assert bytes(a.patch(tpl, lits)) == a.pack(full)
+    assert a.pack({"RK0": 1}, default=0) == a.pack({"RK0": 1, "L0": 0, "F0": 0.0, "CL0": 0,
+                                                    "NRUNS": 0, "A0_0": 0.0, "psum": 0})
