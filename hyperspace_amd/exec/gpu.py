@@ -430,6 +430,25 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
         return self.cache.holds(t)
 
     def _bucket_union(self, p: X.BucketUnionExec) -> DRel:
+        """The device relation of a BucketUnion (Hybrid Scan): its parts, or one merged table
+        (``_merged_union``).  A merged result is kept per union node while its tables stay
+        resident: a plan-cache hit re-submits the same node with its literals rebound in place
+        (the kept predicates hold those same literal objects), so the parts' relations, the
+        predicate check across parts and the merge lookup run once per node."""
+        memo = self.__dict__.setdefault("_union_memo", {})
+        tag = self._placement_tag()
+        hit = memo.get(id(p))
+        if hit is not None and hit[0] is p and hit[2] == tag and self._holds(hit[1].table):
+            return hit[1].copy()
+        r = self._bucket_union_eval(p)
+        if r.table is not None and getattr(r.table, "_hs_sources", None) is not None:
+            if len(memo) > 64:
+                memo.clear()
+            memo[id(p)] = (p, r, tag)
+            return r.copy()
+        return r
+
+    def _bucket_union_eval(self, p: X.BucketUnionExec) -> DRel:
         nb = p.bucket_spec.num_buckets
         parts = []
         for child in p.children:
