@@ -28,6 +28,7 @@ _NP_TO_HS = {np.dtype(np.int8): NL.I8, np.dtype(np.int16): NL.I16, np.dtype(np.i
              np.dtype(np.int64): NL.I64, np.dtype(np.float32): NL.F32,
              np.dtype(np.float64): NL.F64, np.dtype(np.uint8): NL.BOOL,
              np.dtype(np.uint32): NL.U32, np.dtype(np.uint64): NL.U64}
+_HS_OF_TORCH: dict = {}     # torch dtype -> HS type (DeviceColumn.hs_type)
 
 
 def storage_numpy_dtype(t: pa.DataType) -> np.dtype:
@@ -81,7 +82,11 @@ class DeviceColumn:
 
     @property
     def hs_type(self) -> int:
-        return _NP_TO_HS[np.dtype(str(self.data.dtype).replace("torch.", ""))]
+        dt = self.data.dtype
+        t = _HS_OF_TORCH.get(dt)      # on every lowering's path: one dict hit per call
+        if t is None:
+            t = _HS_OF_TORCH[dt] = _NP_TO_HS[np.dtype(str(dt).replace("torch.", ""))]
+        return t
 
     @property
     def is_float(self) -> bool:

@@ -173,16 +173,17 @@ class _RingGraph:
         elif slot.launched and not slot.done():
             slot.wait()    # back-pressure: the slot's replay is still running
         fill(slot.h_params)
-        cur = stream if stream is not None else torch.cuda.current_stream()
-        st = cur.cuda_stream
         R = jit.runtime()
         if slot.graph is not None:
+            st = stream.cuda_stream if stream is not None else NL.raw_stream()
             ptrs = (C.c_void_p * len(blocks))(*[C.addressof(b) for b in blocks])
             _rt_check(R.hs_graph_replay(slot.graph, len(blocks), ptrs, st,
                                         after.cuda_stream if after is not None else None,
                                         slot.event), "hs_graph_replay")
             self.replays += 1
         else:
+            cur = stream if stream is not None else torch.cuda.current_stream()
+            st = cur.cuda_stream
             if after is not None:
                 cur.wait_stream(after)
             if not self._warm:

@@ -244,9 +244,15 @@ def check(rc: int, what: str) -> None:
         raise RuntimeError(f"{what} failed with code {rc}")
 
 
-def stream_ptr():
+def raw_stream() -> int:
+    """The current HIP stream of the current device as an integer handle, without building a
+    ``torch.cuda.Stream`` (every kernel launch and graph replay asks for it)."""
     import torch
-    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
+
+
+def stream_ptr():
+    return C.c_void_p(raw_stream())
 
 
 def ptr(t):
