@@ -497,9 +497,11 @@ class _AggProgram:
     plan-cache hit binds its literals into the cached plan's nodes and the program replays the
     prepared lowering of its literal vector - a captured hipGraph (scan: ``ScanAggGraph``;
     two-phase merge join: ``TwoPhaseGraph``) - and queues the cross-rank combine, skipping the
-    executor's plan walk and every per-query lowering check.  Valid while the device-table
-    cache has evicted nothing since it was made (``epoch``); any miss (new literal vector,
-    eviction, graph dropped) returns None and the full path runs (and re-registers)."""
+    executor's plan walk and every per-query lowering check.  A literal vector it has not seen
+    is lowered by the prep itself (``prep.run``, still no plan walk).  Valid while the
+    device-table cache has evicted nothing since it was made (``epoch``); any other miss
+    (eviction, placement change, a prep gone stale, graph dropped) returns None and the full
+    path runs (and re-registers)."""
     __slots__ = ("final", "fns", "group", "prep", "epoch", "n")
 
     def __init__(self, be, final, fns, group, prep, epoch):
@@ -514,7 +516,18 @@ class _AggProgram:
             return None      # (also keeps the tables recent in the cache's LRU)
         res = self.prep.fast(be, self.fns, self.group)
         if res is None:
-            return None
+            # a literal vector this program has not lowered yet: its literal-dependent lowering
+            # runs here (what the executor's _dense_agg would run for this prep) instead of
+            # after a walk of the plan; anything the prep cannot take returns to that path
+            if self.prep.placement != be._placement_tag():
+                return None
+            be._groups_agreed = False
+            try:
+                res = self.prep.run(be, self.fns, self.group)
+            except _Stale:
+                return None
+            if res is None:
+                return None
         finish = be._agg_finish(self.final, self.fns, self.group, res)
         return QueryFuture(be, plan, finish, "native", None, t0)
 
