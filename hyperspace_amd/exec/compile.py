@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import bisect
 import datetime
-from typing import Callable, Dict, List, Tuple
+from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
 import pyarrow as pa
@@ -35,15 +35,17 @@ _FLIP = {NL.OP_EQ: NL.OP_EQ, NL.OP_NE: NL.OP_NE, NL.OP_LT: NL.OP_GT, NL.OP_LE: N
 # Leaf representation before slot binding
 # ------------------------------------------------------------------------------------------------
 class Leaf:
-    __slots__ = ("kind", "op", "attr", "attr2", "value", "values")
+    __slots__ = ("kind", "op", "attr", "attr2", "value", "values", "lit")
 
-    def __init__(self, kind, op, attr, attr2=None, value=None, values=None):
+    def __init__(self, kind, op, attr, attr2=None, value=None, values=None, lit=None):
         self.kind, self.op, self.attr, self.attr2 = kind, op, attr, attr2
         self.value, self.values = value, values
+        self.lit = lit      # cmp_lit: the Literal node ``value`` came from (``rebind``)
 
     def negate(self) -> "Leaf":
         if self.kind in ("cmp_lit", "cmp_col", "in", "bitmap"):
-            return Leaf(self.kind, _NEG[self.op], self.attr, self.attr2, self.value, self.values)
+            return Leaf(self.kind, _NEG[self.op], self.attr, self.attr2, self.value, self.values,
+                        self.lit)
         if self.kind == "isnull":
             return Leaf("notnull", 0, self.attr)
         if self.kind == "notnull":
@@ -138,9 +140,9 @@ def _leaf(e: E.Expression) -> Leaf:
         if isinstance(r, E.Cast):
             r = r.child
         if isinstance(l, E.Attribute) and isinstance(r, E.Literal):
-            return Leaf("cmp_lit", op, l, value=_lit_value(r.value, l.data_type))
+            return Leaf("cmp_lit", op, l, value=_lit_value(r.value, l.data_type), lit=r)
         if isinstance(r, E.Attribute) and isinstance(l, E.Literal):
-            return Leaf("cmp_lit", _FLIP[op], r, value=_lit_value(l.value, r.data_type))
+            return Leaf("cmp_lit", _FLIP[op], r, value=_lit_value(l.value, r.data_type), lit=l)
         if isinstance(l, E.Attribute) and isinstance(r, E.Attribute):
             return Leaf("cmp_col", op, l, r)
         raise Unsupported(f"comparison {e.sql()}")
@@ -204,12 +206,17 @@ class ColumnInfo:
 
 
 class Bound:
-    """Kernel-ready predicates plus keep-alive buffers (IN sets)."""
+    """Kernel-ready predicates plus keep-alive buffers (IN sets).  ``lits``: for every
+    predicate whose literal came from a Literal node, (predicate index, Literal, column type,
+    float?) - what ``rebind`` rewrites for a new literal vector; ``rebindable`` is False when a
+    predicate's shape depends on its value (dictionary codes, IN sets, string dates, NULLs)."""
 
     def __init__(self):
         self.preds: List[NL.Pred] = []
         self.buffers: list = []
         self.always_false = False
+        self.lits: list = []
+        self.rebindable = True
 
 
 def _dict_code_bound(info: ColumnInfo, op: int, v: str) -> Tuple[str, int, int]:
@@ -256,7 +263,13 @@ def bind(clauses: List[List[Leaf]], col_info: Callable[[E.Attribute], ColumnInfo
             elif leaf.kind == "cmp_lit":
                 v = leaf.value
                 if v is None:
+                    b.rebindable = False
                     continue  # comparison with NULL is never true
+                if info.dictionary is not None or isinstance(v, str) or leaf.lit is None:
+                    b.rebindable = False
+                else:
+                    b.lits.append((len(b.preds), leaf.lit, leaf.attr.data_type,
+                                   bool(info.is_float or isinstance(v, float))))
                 if info.dictionary is not None:
                     if not isinstance(v, str):
                         raise Unsupported("non-string literal vs string column")
@@ -280,6 +293,7 @@ def bind(clauses: List[List[Leaf]], col_info: Callable[[E.Attribute], ColumnInfo
                 else:
                     b.preds.append(NL.Pred(NL.PK_INT_LIT, leaf.op, info.slot, 0, group, 0, int(v), 0.0, None))
             elif leaf.kind == "bitmap":
+                b.rebindable = False
                 kb = leaf.value
                 if info.dictionary is not None or info.is_float:
                     raise Unsupported("key bitmap on a non-integer column")
@@ -287,6 +301,7 @@ def bind(clauses: List[List[Leaf]], col_info: Callable[[E.Attribute], ColumnInfo
                 b.preds.append(NL.Pred(NL.PK_BITMAP, leaf.op, info.slot, 0, group,
                                        kb.words.numel(), kb.base, 0.0, kb.words.data_ptr()))
             elif leaf.kind == "in":
+                b.rebindable = False
                 vals = [v for v in leaf.values if v is not None]
                 if info.dictionary is not None:
                     d = {s: i for i, s in enumerate(info.dictionary.to_pylist())}
@@ -322,6 +337,33 @@ def bind(clauses: List[List[Leaf]], col_info: Callable[[E.Attribute], ColumnInfo
     if len(b.preds) > NL.MAX_PREDS:
         raise Unsupported("too many predicates")
     return b
+
+
+def rebind(b: Bound) -> Optional[Bound]:
+    """``b`` (a bound predicate list of a prepared lowering) with every literal predicate's
+    value re-read from its Literal node - a plan-cache hit writes the new query's values into
+    the cached plan's Literal nodes - so a new literal vector skips the CNF conversion and
+    column binding; None when the new values could change the predicates' shape (a NULL, a
+    type change) or ``b`` is not rebindable (the full ``bind`` runs instead)."""
+    if not b.rebindable or b.always_false:
+        return None
+    out = Bound()
+    out.preds = [NL.Pred.from_buffer_copy(p) for p in b.preds]
+    out.buffers = b.buffers
+    out.lits = b.lits
+    for i, lit, dtype, flt in b.lits:
+        v = lit.value
+        if v is None or isinstance(v, (str, bool)):
+            return None
+        v = _lit_value(v, dtype)
+        p = out.preds[i]
+        if flt:
+            p.flit = float(v)
+        else:
+            if isinstance(v, float) and not v.is_integer():
+                return None
+            p.ilit = int(v)
+    return out
 
 
 # ------------------------------------------------------------------------------------------------

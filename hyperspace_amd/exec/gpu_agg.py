@@ -723,8 +723,15 @@ class AggOps:
         if low is None:
             implied: set = set()
             spec = self._range_spec(r, r.conds, implied)
-            bound = CP.bind(CP.to_cnf([c for c in r.conds if id(c) not in implied]), col_info,
-                            self.device)
+            bound = None
+            tb = prep.tbound if prep is not None else None
+            if tb is not None and tb[0] == implied:
+                bound = CP.rebind(tb[1])     # same predicates, this query's literal values
+            if bound is None:
+                bound = CP.bind(CP.to_cnf([c for c in r.conds if id(c) not in implied]),
+                                col_info, self.device)
+                if prep is not None and bound.rebindable:
+                    prep.tbound = (frozenset(implied), bound)
             specs = self._agg_specs(fns, col_info)
             if lkey is not None:
                 if len(prep.lowered) >= 1024:

@@ -325,13 +325,16 @@ class _ScanPrep:
     bounds, bound predicates and aggregate terms - a repeated parameter set (a dashboard's
     queries) skips predicate compilation altogether."""
     __slots__ = ("final", "r", "col_info", "descs", "gs", "params", "graph", "placement",
-                 "lits", "lowered")
+                 "lits", "lowered", "tbound")
 
     def __init__(self, final, r, col_info, descs, gs, params, graph, placement):
         self.final, self.r, self.col_info, self.descs, self.gs = final, r, col_info, descs, gs
         self.params, self.graph, self.placement = params, graph, placement
         self.lits = _literals(list(r.conds) + list(final.aggregates))
         self.lowered: Dict[tuple, tuple] = {}
+        # (implied condition ids, bound predicates) of a lowering whose literals CP.rebind can
+        # re-read: a new literal vector skips the CNF conversion and column binding
+        self.tbound = None
 
     def literal_key(self):
         try:
@@ -380,7 +383,7 @@ class _JoinPrep:
     relations, column slots, group domain and the kernel launcher (jit.MergeJoinLauncher).
     A submission re-binds the predicates and aggregate terms and launches."""
     __slots__ = ("final", "node", "left", "right", "lk", "rk", "col_info", "descs", "launcher",
-                 "gtail", "placement", "agreed", "lits", "lowered", "lconds")
+                 "gtail", "placement", "agreed", "lits", "lowered", "lconds", "tjoin")
 
     def __init__(self, final, node, left, right, lk, rk, col_info, descs, launcher, gtail,
                  placement, agreed, lconds=None):
@@ -393,6 +396,7 @@ class _JoinPrep:
             ([node.condition] if node.condition is not None else [])
         self.lits = _literals(conds + list(final.aggregates))
         self.lowered: Dict[tuple, tuple] = {}   # literal vector -> (params, keep, specs)
+        self.tjoin = None     # (join params, (left, right) bound predicates) to CP.rebind
 
     literal_key = _ScanPrep.literal_key
 
@@ -408,9 +412,22 @@ class _JoinPrep:
         nd = len(self.descs)
         with stage("join.agg_kernel"):
             if low is None:
-                jp, col_info, descs, keep = be._join_params(
-                    left, self.right, self.lk, self.rk, self.node.condition,
-                    lconds=self.lconds, slots=(self.col_info, self.descs))
+                jp = None
+                col_info, descs = self.col_info, self.descs
+                if self.tjoin is not None:
+                    tjp, (tlb, trb) = self.tjoin
+                    lb, rb = CP.rebind(tlb), CP.rebind(trb)
+                    if lb is not None and rb is not None:
+                        jp = NL.JoinParams.from_buffer_copy(tjp)
+                        for i, pr in enumerate(lb.preds + rb.preds):
+                            jp.preds[i] = pr
+                        keep = (lb, rb)
+                if jp is None:
+                    jp, col_info, descs, keep = be._join_params(
+                        left, self.right, self.lk, self.rk, self.node.condition,
+                        lconds=self.lconds, slots=(self.col_info, self.descs))
+                    if keep[0].rebindable and keep[1].rebindable:
+                        self.tjoin = (NL.JoinParams.from_buffer_copy(jp), keep)
                 specs = be._agg_specs(fns, col_info)
                 if len(descs) != nd:
                     raise _Stale()

@@ -942,3 +942,39 @@ def test_args_template_patch_equals_full_pack():
     assert bytes(a.patch(tpl, lits)) == a.pack(full)
     assert a.pack({"RK0": 1}, default=0) == a.pack({"RK0": 1, "L0": 0, "F0": 0.0, "CL0": 0,
                                                     "NRUNS": 0, "A0_0": 0.0, "psum": 0})
+
+
+def test_rebind_matches_fresh_bind():
+    """``compile.rebind``: a bound predicate list re-reads its literals from their Literal nodes
+    (a plan-cache hit rewrites those in place) and equals a fresh CNF + bind of the same
+    conditions; NULLs, strings and IN sets are not rebindable."""
+    import datetime as dt
+    from hyperspace_amd.exec import compile as CP
+    from hyperspace_amd.plan import expressions as E
+    d = E.Attribute("d", pa.date32())
+    q = E.Attribute("q", pa.int64())
+    x = E.Attribute("x", pa.float64())
+    infos = {d.expr_id: CP.ColumnInfo(0, NL.I32, pa.date32()),
+             q.expr_id: CP.ColumnInfo(1, NL.I64, pa.int64()),
+             x.expr_id: CP.ColumnInfo(2, NL.F64, pa.float64())}
+    lo, hi = E.Literal(dt.date(1994, 1, 1)), E.Literal(dt.date(1995, 1, 1))
+    lq, lx = E.Literal(24), E.Literal(0.05)
+    conds = [E.GreaterThanOrEqual(d, lo), E.LessThan(d, hi),
+             E.Or(E.LessThan(q, lq), E.GreaterThan(lx, x)), E.Not(E.EqualTo(q, E.Literal(7)))]
+
+    def fresh():
+        return CP.bind(CP.to_cnf(conds), lambda a: infos[a.expr_id], None)
+
+    def key(b):
+        return [(p.kind, p.op, p.col, p.group, p.ilit, p.flit) for p in b.preds]
+    b0 = fresh()
+    assert b0.rebindable and len(b0.lits) == 5
+    lo.value, hi.value, lq.value, lx.value = dt.date(1996, 3, 2), dt.date(1997, 1, 1), 25, 0.07
+    rb = CP.rebind(b0)
+    assert rb is not None and key(rb) == key(fresh()) and key(rb) != key(b0)
+    lq.value = None
+    assert CP.rebind(b0) is None
+    s = E.Attribute("s", pa.string())
+    infos[s.expr_id] = CP.ColumnInfo(3, NL.I32, pa.string(), pa.array(["a", "b"]))
+    bs = CP.bind(CP.to_cnf([E.EqualTo(s, E.Literal("b"))]), lambda a: infos[a.expr_id], None)
+    assert not bs.rebindable and CP.rebind(bs) is None
