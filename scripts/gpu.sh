@@ -204,7 +204,7 @@ step_dist() {
   local n=${NPROC:-4}
   HS_BENCH_DIR=/tmp/hs_bench_dist HS_DIST_BACKEND=gloo timeout -k 10 700 \
     python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
-    --master-port 29517 bench.py --gpus $n --sf ${SF:-2} --steps ${DIST_STEPS:-20} --warmup 3 \
+    --master-port 29517 bench.py --gpus $n --sf ${SF:-2} --steps ${DIST_STEPS:-100} --warmup 3 \
     --buckets 16 ${DIST_ARGS} > "${O}_dist$n.json" 2> "${O}_dist$n.log"
 }
 
