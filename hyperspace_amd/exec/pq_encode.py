@@ -188,7 +188,7 @@ D2H_STREAMS = int(os.environ.get("HS_PQ_D2H_STREAMS", "2"))
 # D2H copies ran as blit kernels on the CUs beside the compressor's waves (~18 GB/s,
 # profiles/build_timeline_r5.txt); queued behind the compressor they run on the SDMA engines
 # (profiles/build_copy_stats_sf100_r5_d2h_serial.csv)
-D2H_ON_COMPRESS_STREAM = True
+D2H_ON_COMPRESS_STREAM = os.environ.get("HS_PQ_D2H_ON_COMPRESS", "1") == "1"
 # seconds of the last builds' write phases (reset by device_build per build)
 WRITE_PHASES: Dict[str, float] = {}
 _WP_LOCK = __import__("threading").Lock()
