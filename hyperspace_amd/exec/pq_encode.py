@@ -168,17 +168,22 @@ def snappy_pages(plans, p_first: int, p_end: int, device):
     return snappy_finish(snappy_launch(plans, p_first, p_end, device), device)
 
 
-_ZSTREAMS: Dict[int, object] = {}
+_ZSTREAMS: Dict[tuple, object] = {}
+# compress streams the Snappy groups alternate over: group g is compressed AND copied out on
+# stream g % Z, so one group's D2H (on the SDMA engines: a copy queued behind the kernel that
+# produced it on the same stream) runs while the next group compresses on the other stream -
+# with one stream the two serialize (profiles/build_timeline_r6.txt)
+COMPRESS_STREAMS = max(1, int(os.environ.get("HS_PQ_ZSTREAMS", "2")))
 
 
-def compress_stream(device):
-    """The stream index pages are Snappy-compressed on (one per device), next to the D2H copy
-    stream that drains them."""
+def compress_stream(device, k: int = 0):
+    """Compress stream ``k`` of the device: index pages are Snappy-compressed on it and, with
+    ``D2H_ON_COMPRESS_STREAM``, copied out on it too."""
     import torch
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    st = _ZSTREAMS.get(idx)
+    st = _ZSTREAMS.get((idx, k))
     if st is None:
-        st = _ZSTREAMS[idx] = torch.cuda.Stream(device=device)
+        st = _ZSTREAMS[(idx, k)] = torch.cuda.Stream(device=device)
     return st
 
 
@@ -585,9 +590,10 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
     # batches alternate over D2H_STREAMS copy streams: their page copies run on separate DMA
     # queues instead of queueing behind one another
     d2h = copy_streams(device)[:max(1, D2H_STREAMS)]
+    zsl = [compress_stream(device, k) for k in range(COMPRESS_STREAMS)] if cid == 1 else []
     if cid == 1 and D2H_ON_COMPRESS_STREAM:
-        d2h = [compress_stream(device)]
-    for st in d2h:
+        d2h = zsl
+    for st in d2h + zsl:
         st.wait_stream(torch.cuda.current_stream(device))
     batches, cur, cur_bytes = [], [], 0
     for f in files:
@@ -619,7 +625,9 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
     group_of = {bi: gi for gi, g in enumerate(groups) for bi in g}
     zgroup = (-1, None, None)
     launched: Dict[int, _SnappyGroup] = {}
-    zs = compress_stream(device) if cid == 1 else None
+
+    def zs_of(g: int):
+        return zsl[g % len(zsl)]
 
     def group_range(gi: int) -> Tuple[int, int]:
         return _file_pages(batches[groups[gi][0]][0])[0], \
@@ -636,6 +644,8 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
         zoff = zsize = None
         gfirst = 0
         stream = d2h[bi % len(d2h)]
+        if cid == 1 and D2H_ON_COMPRESS_STREAM:
+            stream = zs_of(group_of[bi])     # the group's own compress stream (SDMA copies)
         with torch.cuda.stream(stream):
             if cid == 1:
                 gi = group_of[bi]
@@ -643,9 +653,9 @@ def write_buckets(cols: Dict[str, DeviceColumn], names: Sequence[str], schema: p
                 if zgroup[0] != gi:
                     for gg in (gi, gi + 1):
                         if gg < len(groups) and gg not in launched:
-                            zs.wait_stream(torch.cuda.current_stream(device))
-                            with torch.cuda.stream(zs):
+                            with torch.cuda.stream(zs_of(gg)):
                                 launched[gg] = snappy_launch(segs, *group_range(gg), device)
+                    zs = zs_of(gi)
                     with torch.cuda.stream(zs):
                         res = snappy_finish(launched.pop(gi), device)
                         zev = torch.cuda.Event()
