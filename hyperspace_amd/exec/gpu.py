@@ -44,8 +44,8 @@ from .device_table import DeviceColumn, DeviceTable
 from .graphs import GraphCache
 from .hbm_budget import rank_budget
 from .staging import RESERVE_BLOCK as _RESERVE_BLOCK
-from .gpu_common import (_AggProgram, _needs_eval, _prefix_sorted, _warm_torch_kernels, DRel, log,
-                         QueryFuture, Unsupported)
+from .gpu_common import (arrow_table, _AggProgram, _needs_eval, _prefix_sorted,
+                         _warm_torch_kernels, DRel, log, QueryFuture, Unsupported)
 from .gpu_agg import AggOps
 from .gpu_hash import HashAggOps
 from .gpu_join import JoinOps
@@ -1018,7 +1018,7 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
                 except (pa.ArrowInvalid, pa.ArrowNotImplementedError):
                     pass
             fixed.append(arr)
-        return pa.Table.from_arrays(fixed, names=[a.name for a in out_attrs])
+        return arrow_table(fixed, [a.name for a in out_attrs])
 
     def _to_arrow_ranks(self, r: DRel, out_attrs: List[E.Attribute]) -> pa.Table:
         """Rows of ``r`` from every rank (sharded placement): this rank's rows are materialized
@@ -1068,7 +1068,7 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
                 except (pa.ArrowInvalid, pa.ArrowNotImplementedError):
                     pass
             arrays.append(arr)
-        return pa.Table.from_arrays(arrays, names=[a.name for a in out_attrs])
+        return arrow_table(arrays, [a.name for a in out_attrs])
 
 
 __all__ = ["GpuBackend", "QueryFuture", "DRel", "bucket_chunks", "release_process_device_memory"]

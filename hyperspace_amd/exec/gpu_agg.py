@@ -16,8 +16,8 @@ from . import compile as CP, jit
 from .arrow_eval import key
 from .device_table import DeviceColumn
 from .graphs import _cbuf, GraphPending as _GraphPending, range_bounds, ScanAggGraph
-from .gpu_common import (_compact_buffers, _eval_scalar, _GraphPrep, _group_limit, _JoinPrep,
-                         _NeedHash, _ScanPrep, _Stale, _use_on, bucket_chunks, DRel,
+from .gpu_common import (arrow_table, _compact_buffers, _eval_scalar, _GraphPrep, _group_limit,
+                         _JoinPrep, _NeedHash, _ScanPrep, _Stale, _use_on, bucket_chunks, DRel,
                          GROUP_LDS_SCAN, log, MAX_GROUPS_SCAN, Unsupported)
 
 
@@ -252,7 +252,7 @@ class AggOps:
                 arrays.append(pa.array(vlist, type=a.data_type))
             except (pa.ArrowInvalid, pa.ArrowTypeError):
                 arrays.append(pa.array(vlist))
-        return pa.Table.from_arrays(arrays, names=[a.name for a in final.output])
+        return arrow_table(arrays, [a.name for a in final.output])
 
     def _agg_prep_get(self, final) -> Optional["_ScanPrep"]:
         """The prepared scan of a fused aggregate node submitted before (plan-cache hits
@@ -417,7 +417,7 @@ class AggOps:
                 arrays.append(pa.array(vlist, type=a.data_type))
             except (pa.ArrowInvalid, pa.ArrowTypeError):
                 arrays.append(pa.array(vlist))
-        return pa.Table.from_arrays(arrays, names=[a.name for a in final.output])
+        return arrow_table(arrays, [a.name for a in final.output])
 
     def _agree_groups(self, d, sums, cnts, mins, maxs, G, gbase, gdict, gtype, A):
         """Re-key grouped partials onto the union group domain of all ranks.

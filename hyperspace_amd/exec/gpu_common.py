@@ -96,6 +96,21 @@ class DRel:
         return d
 
 
+_SCHEMAS: dict = {}
+
+
+def arrow_table(arrays, names) -> pa.Table:
+    """``pa.Table.from_arrays(arrays, names=names)`` through a cached schema: building the
+    schema from names costs several times the table itself, on every query result."""
+    key = (tuple(names), tuple(a.type for a in arrays))
+    sch = _SCHEMAS.get(key)
+    if sch is None:
+        if len(_SCHEMAS) >= 512:
+            _SCHEMAS.clear()
+        sch = _SCHEMAS[key] = pa.schema([pa.field(n, a.type) for n, a in zip(names, arrays)])
+    return pa.Table.from_arrays(arrays, schema=sch)
+
+
 def _finalize_array(fn, s, c, mn, mx) -> pa.Array:
     """Vectorized ``CP.finalize_value`` over the groups of a hash-mode aggregate."""
     c = np.asarray(c, dtype=np.int64)

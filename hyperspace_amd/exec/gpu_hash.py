@@ -15,8 +15,8 @@ from ..utils.conf import HyperspaceConf
 from ..utils.tracing import stage
 from . import compile as CP, jit
 from .arrow_eval import key
-from .gpu_common import (_HashPrep, _eval_vec, _fd_columns, _finalize_array, _gather_tables, DRel, H_TOPK_K,
-                         TOPK_MIN_GROUPS, Unsupported)
+from .gpu_common import (arrow_table, _HashPrep, _eval_vec, _fd_columns, _finalize_array,
+                         _gather_tables, DRel, H_TOPK_K, TOPK_MIN_GROUPS, Unsupported)
 
 
 class HashAggOps:
@@ -668,4 +668,4 @@ class HashAggOps:
                 except (pa.ArrowInvalid, pa.ArrowNotImplementedError):
                     pass
             arrays.append(arr)
-        return pa.Table.from_arrays(arrays, names=[a.name for a in final.output])
+        return arrow_table(arrays, [a.name for a in final.output])
