@@ -278,7 +278,16 @@ def config_hybrid(args):
     hyb = (_q6(li, 0).collect()[0][0], _rows(_q3(li, od, 0)))
     tr = time.perf_counter()
     for name in ("li_orderkey", "ord_orderkey", "li_shipdate"):
+        t1 = time.perf_counter()
         hs.refreshIndex(name, "incremental")
+        _sync(args.device)
+        st = {}
+        if args.device == "gpu":
+            from hyperspace_amd.exec import device_build
+            st = {k: v for k, v in device_build.LAST_BUILD_STATS.items()
+                  if isinstance(v, (int, float, str))}
+        print(f"[hybrid] refresh {name}: {time.perf_counter() - t1:.3f}s {st}", file=sys.stderr,
+              flush=True)
     _sync(args.device)
     refresh_s = time.perf_counter() - tr
     li, od = s.read.parquet(lpath), s.read.parquet(opath)
