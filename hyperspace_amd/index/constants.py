@@ -131,9 +131,12 @@ RUN_TOPK_ENABLED = "spark.hyperspace.mi.runTopK.enabled"
 RUN_TOPK_ENABLED_DEFAULT = "true"
 # cached join index (left row -> first matching right row, int32 in HBM) for joins of two
 # device-resident index tables with unique integer right keys: the fused join aggregate becomes a
-# streaming scan of the left table plus a gather, no per-tile span search (exec/join_index.py)
+# streaming scan of the left table plus a gather, no per-tile span search (exec/join_index.py).
+# Off by default: the run-keyed two-phase merge join is faster on the TPC-H Q3 shape (0.74 vs
+# 0.93-1.53 ms per query at SF100, bench.py's join_index side key) and replays as a prepared
+# program; the join index stays available per session
 JOIN_INDEX_ENABLED = "spark.hyperspace.mi.joinIndex.enabled"
-JOIN_INDEX_ENABLED_DEFAULT = "true"
+JOIN_INDEX_ENABLED_DEFAULT = "false"
 # Query-time placement of index buckets across the ranks of a torch.distributed job:
 #  "sharded"    each bucket (or key-range piece of a heavy bucket) is resident on one rank only
 #               (the owner map of parallel/placement.py); every query runs on all ranks and
