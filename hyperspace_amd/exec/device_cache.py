@@ -43,6 +43,27 @@ def _files_key(files) -> tuple:
 
 HOLDS_REACCOUNT = 16
 
+# Device buffers that lowered queries derive and keep outside any table (the recorded run matches
+# of exec/jit_runs.py, ...): live bytes, released by each buffer's finalizer.  Every cache's
+# budget shrinks by them, so tables plus derived buffers stay within the planned HBM share.
+_DERIVED = [0]
+
+
+def track_derived(t) -> None:
+    """Count device tensor ``t`` against every table cache's budget while it lives."""
+    import weakref
+    nb = int(t.numel()) * int(t.element_size())
+    _DERIVED[0] += nb
+    weakref.finalize(t, _untrack, nb)
+
+
+def _untrack(nb: int) -> None:
+    _DERIVED[0] -= nb
+
+
+def derived_bytes() -> int:
+    return _DERIVED[0]
+
 
 class DeviceTableCache:
     """LRU of resident tables under an HBM byte budget.  A table's footprint includes what
@@ -68,7 +89,7 @@ class DeviceTableCache:
         return (fk, tuple(columns), extra)
 
     def _evict(self, keep) -> None:
-        while self._bytes > self.budget and len(self._lru) > 1:
+        while self._bytes > self.budget - _DERIVED[0] and len(self._lru) > 1:
             k, _ = next(iter(self._lru.items()))
             if k == keep:
                 self._lru.move_to_end(k)

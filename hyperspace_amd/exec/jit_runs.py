@@ -36,6 +36,7 @@ from . import kernel_config as _KC  # noqa: E402
 _CFG = _KC.active()
 MJ_2P, RS_ITEMS = _CFG.mj_2p, _CFG.rs_items
 RT2_UNROLL, RT2_GRID, RT2_I32 = _CFG.rt2_unroll, _CFG.rt2_grid, _CFG.rt2_i32
+RT2_MATCH = _CFG.rt2_match
 RS_BITS, RS_BITS_GRID, RS_PACK = _CFG.rs_bits, _CFG.rs_bits_grid, _CFG.rs_pack
 RS_PIPE, RS_WALK, RS_LDS, RS_LUT = _CFG.rs_pipe, _CFG.rs_walk, _CFG.rs_lds, _CFG.rs_lut
 RS_PK16, RS_WAVES, RS_PACK12 = _CFG.rs_pk16, _CFG.rs_waves, _CFG.rs_pack12
@@ -77,13 +78,13 @@ def _lpreds(p):
 # phase 1: 64-run groups per unrolled iteration of a wavefront (gen_run_tags2)
 
 
-def tags2_shape(p: NL.JoinParams, compacts, W: int, ix32: bool = False) -> tuple:
+def tags2_shape(p: NL.JoinParams, compacts, W: int, ix32: bool = False, mode: str = "") -> tuple:
     cols = tuple(sorted((s, c) for s, c in J._col_specs(p, compacts).items()
                         if s >= SPLIT or s == p.lkey))
     preds = tuple((p.preds[k].kind, p.preds[k].op, p.preds[k].col, p.preds[k].col2,
                    p.preds[k].group) for k in range(p.nlp, p.npreds))
     return ("run_tags2", cols, preds, p.nlp, p.lkey, p.rkey, _tags_grouped(p) and p.group_col,
-            W, RT2_UNROLL, J.BLOCK, ix32)
+            W, RT2_UNROLL, J.BLOCK, ix32, mode)
 
 
 def _stage_slots(p: NL.JoinParams) -> list:
@@ -99,7 +100,8 @@ def _tags_grouped(p: NL.JoinParams) -> bool:
     return p.group_col >= SPLIT and p.num_groups > 1
 
 
-def gen_run_tags2(p: NL.JoinParams, compacts, W: int, ix32: bool = False) -> J.Kernel:
+def gen_run_tags2(p: NL.JoinParams, compacts, W: int, ix32: bool = False,
+                  mode: str = "") -> J.Kernel:
     """Phase 1, direct form: no tiles and no LDS.  Each wavefront owns a contiguous chunk of
     64-run groups of the left run list (so it owns whole 2W-word stretches of the tag bitmap
     and stores them without atomics).  Lane l of a group guesses the right row of its run: the
@@ -117,9 +119,16 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int, ix32: bool = False) -> J.K
     ``ix32``: run and right-row indices fit int32 (the lowering checks the table sizes), so the
     index arithmetic, range clamps and gallop run in 32-bit registers and the column loads
     address through a scalar base plus a 32-bit lane offset - the 64-bit index math was most of
-    the kernel's VALU instructions (``profiles/pmc_query_kernels_sf100_r6.txt``)."""
+    the kernel's VALU instructions (``profiles/pmc_query_kernels_sf100_r6.txt``).
+
+    ``mode``: "rec" also stores each run's matched right row (or -1) into ``MOUT``; "match"
+    reads that record (``MATCH``, one int32 per run, -1 padded to whole 64-run groups) instead of
+    the left run keys, the right key images and the range table - it depends only on the
+    lowering's ranges and the key columns, not on the literals (``record_matches``)."""
     IX = "int" if ix32 else "i64"  # noqa: N806 — run / right-row index type
     args = J.Args()
+    if mode == "match":
+        return _gen_tags2_match(p, compacts, W)
     lk, rk = p.lkey, p.rkey
     args.add("p", f"RK{lk}", "const int*")
     args.add("p", "RNG", "const long long*")
@@ -133,6 +142,9 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int, ix32: bool = False) -> J.K
     U = max(1, RT2_UNROLL)  # noqa: N806
     WV = J.BLOCK // 64  # noqa: N806
     MASK = (1 << W) - 1  # noqa: N806
+    if mode == "rec":
+        assert ix32
+        args.add("p", "MOUT", "int*")
     g = J._Gen(args, cols, SPLIT, ("row_", "row_"), frozenset(), True)
     rv = J._valid_expr(g, rk, "row_")
     if rgroup:
@@ -278,6 +290,8 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int, ix32: bool = False) -> J.K
                       f"(unsigned)(i_ * {W}); }}",
                       f"{ind}  if (in{u} && lane < {2 * W}) a.tags[(gi + {u}) * {2 * W} + lane] = "
                       f"wd_; }}"])
+        if mode == "rec":
+            b.append(f"{ind}if (in{u} && r{u} < a.NRUNS) a.MOUT[r{u}] = hit{u} ? (int)m{u} : -1;")
 
     def iteration(fast: bool, ind: str) -> None:
         for u in range(U):
@@ -296,6 +310,96 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int, ix32: bool = False) -> J.K
            f'extern "C" __global__ __launch_bounds__({J.BLOCK}) void hs_jit_run_tags2(Args a) {{\n' +
            "\n".join(b) + "\n}\n")
     return J.Kernel(src, "hs_jit_run_tags2", args)
+
+
+def _tag_stores(b: List[str], u: int, W: int, ind: str) -> None:
+    """The 2W tag words of 64-run group ``gi + u`` from the lanes' tags ``tg<u>``: whole words,
+    plain stores."""
+    if W == 1:
+        b.extend([f"{ind}{{ const u64 bal_ = __ballot(tg{u} != 0u);",
+                  f"{ind}  if (in{u} && lane < 2) a.tags[((gi + {u}) << 1) + lane] = "
+                  f"(unsigned)(bal_ >> (32 * lane)); }}"])
+        return
+    per_w = 32 // W
+    b.extend([f"{ind}{{ unsigned wd_ = 0u;",
+              f"{ind}  for (int i_ = 0; i_ < {per_w}; ++i_) {{",
+              f"{ind}    const int src_ = ((lane * {per_w}) + i_) & 63;",
+              f"{ind}    wd_ |= (((unsigned)__shfl((int)tg{u}, src_, 64)) & {(1 << W) - 1}u) << "
+              f"(unsigned)(i_ * {W}); }}",
+              f"{ind}  if (in{u} && lane < {2 * W}) a.tags[(gi + {u}) * {2 * W} + lane] = wd_; }}"])
+
+
+def _gen_tags2_match(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
+    """Phase 1 over a recorded match (``gen_run_tags2`` mode "match"): per run one int32 load
+    of its right row (-1: no match, or the run is outside the lowering's ranges), then the right
+    predicate / group columns at that row.  No key images, no range table, no gallop: the
+    record already resolved them (``record_matches``), so the phase reads 4 bytes per run plus
+    the staged right columns (monotone rows: coalesced)."""
+    args = J.Args()
+    args.add("p", "MATCH", "const int*")
+    args.add("p", "tags", "unsigned*")
+    args.add("q", "NRUNS", "long long")
+    cols = J._col_specs(p, compacts)
+    rpreds = _rpreds(p)
+    rgroup = _tags_grouped(p)
+    stage_slots = _stage_slots(p)
+    if rgroup:
+        gb = args.add("q", "group_base", "long long")
+        ng = args.add("q", "num_groups", "long long")
+    U = max(1, RT2_UNROLL)  # noqa: N806
+    WV = J.BLOCK // 64  # noqa: N806
+    ind = "    "
+    b: List[str] = [
+        "  const int lane = (int)(threadIdx.x & 63);",
+        "  const i64 G = (a.NRUNS + 63) >> 6;",
+        f"  const i64 nwv = (i64)gridDim.x * {WV};",
+        f"  const i64 wv = (i64)blockIdx.x * {WV} + "
+        "(i64)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));",
+        "  const i64 per = (G + nwv - 1) / nwv;",
+        "  const i64 gbeg = wv * per;",
+        "  const i64 gend = G < gbeg + per ? G : gbeg + per;",
+        f"  for (i64 gi = gbeg; gi < gend; gi += {U}) {{"]
+    for u in range(U):
+        # the record is padded to whole groups: an in-range group's 64 lanes all read it
+        b.extend([f"{ind}const bool in{u} = gi + {u} < gend;",
+                  f"{ind}const int mt{u} = a.MATCH[in{u} ? (((gi + {u}) << 6) + lane) : lane];"])
+    for u in range(U):
+        b.extend([f"{ind}const bool hit{u} = in{u} && mt{u} >= 0;",
+                  f"{ind}const int j{u} = hit{u} ? mt{u} : 0;"])
+        gu = J._Gen(args, cols, SPLIT, (f"j{u}", f"j{u}"), frozenset(), True)
+        for sl in stage_slots:
+            J._uload(gu, sl, f"g{u}", b, ind)
+    for u in range(U):
+        gu = J._Gen(args, cols, SPLIT, (f"j{u}", f"j{u}"), frozenset(), True)
+        cond = J._rename(gu.cnf(rpreds), stage_slots, f"g{u}")
+        if rgroup:
+            gx = J._rename(f"x{p.group_col}", stage_slots, f"g{u}")
+            b.append(f"{ind}const unsigned tg{u} = ({{ const i64 gl_ = (i64){gx} - {gb}; "
+                     f"(hit{u} && {cond} && gl_ >= 0 && gl_ < {ng}) ? (unsigned)(gl_ + 1) : 0u; }});")
+        else:
+            b.append(f"{ind}const unsigned tg{u} = (hit{u} && {cond}) ? 1u : 0u;")
+        _tag_stores(b, u, W, ind)
+    b.append("  }")
+    src = (J._PRELUDE + args.struct_src() +
+           f'extern "C" __global__ __launch_bounds__({J.BLOCK}) void hs_jit_run_tags2(Args a) {{\n' +
+           "\n".join(b) + "\n}\n")
+    return J.Kernel(src, "hs_jit_run_tags2", args)
+
+
+def record_matches(p: NL.JoinParams, compacts, W: int, vt: dict, nruns: int, grid: int, dev):
+    """Each run's matched right row under the lowering's ranges (or -1), padded with -1 to whole
+    64-run groups: one launch of the verifying phase 1 in mode "rec" at lowering time (queued on
+    the current stream).  Literal-independent: the ranges, key frame and key columns are fixed
+    for the launcher, and the record mode stores the match before any right predicate."""
+    import torch
+    m = torch.full((((nruns + 63) >> 6) * 64,), -1, dtype=torch.int32, device=dev)
+    kr = J.kernel_for(tags2_shape(p, compacts, W, True, "rec"),
+                      lambda: gen_run_tags2(p, compacts, W, True, "rec"))
+    v = dict(vt)
+    v["MOUT"] = m.data_ptr()
+    J.fill_preds_aggs(v, [(k_, p.preds[k_]) for k_ in range(p.npreds)], [], compacts)
+    kr.launch(grid, v, NL.stream_ptr(), 0)
+    return m
 
 
 def run_ranges(rstart, rlen, rbucket, roff, runs):
@@ -991,7 +1095,8 @@ class TwoPhaseLauncher:
     """Both phases lowered once (kernels, tiles, spans, per-tile run windows, the tag bitmap);
     ``launch(p)`` fills the literal slots and queues: bitmap clear, tags, scan, partials fold."""
     __slots__ = ("kt", "ks", "grid_t", "grid_s", "GA", "shmem", "vt", "vs", "compacts", "keep",
-                 "tags", "dev", "blocks", "hk", "graph", "gblocks", "tk", "tpl")
+                 "tags", "dev", "blocks", "hk", "graph", "gblocks", "tk", "tpl", "match",
+                 "launches")
 
     def __init__(self, kt, ks, grid_t, grid_s, GA, shmem, vt, vs, compacts, keep, tags, dev,
                  hk=None, tk=None):
@@ -1010,6 +1115,35 @@ class TwoPhaseLauncher:
         # packed argument blocks of the literal-independent slots: a new literal vector patches
         # only its literal slots into copies of these
         self.tpl = None
+        # (W, runs, lowered parameters) while phase 1 may still switch to a recorded match
+        # (RT2_MATCH): on the launcher's second launch - a lowering that is reused - ``_record``
+        self.match = None
+        self.launches = 0
+
+    def _record(self) -> None:
+        """Switch phase 1 to the recorded-match form: one verifying launch stores each run's
+        right row (``record_matches``), later launches read it.  Skipped when the record would
+        not fit the device's free memory with a margin; the record counts against the table
+        caches' budgets while it lives (``device_cache.track_derived``)."""
+        import torch
+        from .device_cache import track_derived
+        W, nruns, p = self.match
+        self.match = None
+        need = ((nruns + 63) >> 6) * 256
+        free, _ = torch.cuda.mem_get_info(self.dev)
+        free += torch.cuda.memory_reserved(self.dev) - torch.cuda.memory_allocated(self.dev)
+        if free < need + (8 << 30):
+            return
+        m = record_matches(p, self.compacts, W, self.vt, nruns, self.grid_t, self.dev)
+        track_derived(m)
+        self.kt = J.kernel_for(tags2_shape(p, self.compacts, W, True, "match"),
+                               lambda: gen_run_tags2(p, self.compacts, W, True, "match"))
+        self.vt = dict(self.vt, MATCH=m.data_ptr())
+        self.keep = self.keep + (m,)
+        # every packed phase-1 block and the captured pipeline name the verifying kernel
+        self.tpl, self.graph = None, None
+        self.blocks.clear()
+        self.gblocks.clear()
 
     def graphable(self) -> bool:
         """Whether one query's launches can be captured: partials out (not the hash mode)."""
@@ -1020,6 +1154,9 @@ class TwoPhaseLauncher:
         ``graph`` (and a literal vector ``key``) a ``graphs.GraphPending`` of one replay of the
         captured pipeline."""
         import struct
+        self.launches += 1
+        if self.match is not None and self.launches == 2:
+            self._record()
         st = NL.stream_ptr()
         if self.hk is not None:
             preds = [(k_, p.preds[k_]) for k_ in range(p.npreds)]
@@ -1148,9 +1285,13 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
         grid_s = max(1, RS_BITS_GRID)
     if tk is not None:
         tk.bind(grid_s * (J.BLOCK // 64), dev)
-    return TwoPhaseLauncher(kt, ks, grid_t, grid_s, GA, GA * 32 if _scan_grouped(p) else 0,
-                            vt, vs, compacts, (rstart, rlen, rbucket, roff, tp, spans, tr, runs),
-                            tags, dev, hk, tk if sparse else None)
+    lz = TwoPhaseLauncher(kt, ks, grid_t, grid_s, GA, GA * 32 if _scan_grouped(p) else 0,
+                          vt, vs, compacts, (rstart, rlen, rbucket, roff, tp, spans, tr, runs),
+                          tags, dev, hk, tk if sparse else None)
+    if RT2_MATCH and ix32:
+        # the lowering's own parameters: a later launch's may bind other column slots
+        lz.match = (W, nruns, NL.JoinParams.from_buffer_copy(p))
+    return lz
 
 
 def semi_runs_agg(p: NL.JoinParams, rstart, rlen, compacts, runs, nrows: int, words, lo: int,

@@ -75,6 +75,8 @@ class KernelConfig:
     rt2_unroll: int = 4          # phase-1 64-run groups in flight per wavefront iteration
     rt2_grid: int = 8192
     rt2_i32: bool = True         # phase-1 run / right-row index math in 32 bits when tables fit
+    rt2_match: bool = True       # phase 1 reads a per-run matched right row recorded at lowering
+    #                              (literal-independent) instead of re-verifying the key match
     rs_bits: bool = True         # phase 2 bit-parallel for 1-bit tags (gen_run_sparse_scan)
     rs_bits_grid: int = 8192
     rs_pack: bool = True         # bits scan reads its aggregate inputs row-packed

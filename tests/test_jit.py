@@ -211,6 +211,13 @@ def test_generated_sources_compile_with_compact_columns(rt, tmp_path):
         assert "a.RNG" in kt.src and "a.RK0[" in kt.src and "a.c2" not in kt.src
         assert "a.GM0[" in kq.src and "a.tags[w0_" in kq.src and "a.c8" not in kq.src
         ks += [kt, kq]
+        # recorded-match phase 1: the verifying form stores the match, the match form reads it
+        # (no run keys, no right key images, no range table)
+        kr_ = jit_runs.gen_run_tags2(q3, cr, W, True, "rec")
+        km = jit_runs.gen_run_tags2(q3, cr, W, True, "match")
+        assert "a.MOUT[" in kr_.src and "a.MATCH[" in km.src
+        assert "a.RK0[" not in km.src and "a.RNG" not in km.src and "a.c8" not in km.src
+        ks += [kr_, km]
     q3.group_col, q3.num_groups = 10, 300
     assert not jit_runs.applies(q3)
     q3.group_col = -1
@@ -826,15 +833,17 @@ def test_merge_join_runs_matches_oracle(device, layout):
                 G = 3 if grouped else 1
                 es = exp_s if grouped else exp_s.sum(keepdims=True)
                 ec = exp_c if grouped else exp_c.sum(keepdims=True)
-                for use_runs, two, sparse, pk12 in ((True, True, True, True),
-                                                    (True, True, True, False),
-                                                    (True, True, False, True),
-                                                    (True, False, False, True),
-                                                    (False, False, False, True)):
-                    # pk12: the date predicate reads the 12-bit packed copy (codes span < 4096)
-                    cfg = (keys, grouped, use_runs, two, sparse, pk12)
+                for use_runs, two, sparse, pk12, match in ((True, True, True, True, True),
+                                                           (True, True, True, True, False),
+                                                           (True, True, True, False, True),
+                                                           (True, True, False, True, True),
+                                                           (True, False, False, True, True),
+                                                           (False, False, False, True, True)):
+                    # pk12: the date predicate reads the 12-bit packed copy (codes span < 4096);
+                    # match: phase 1 reads the recorded per-run match (rt2_match)
+                    cfg = (keys, grouped, use_runs, two, sparse, pk12, match)
                     with kernel_config.use(mj_lds_keys=keys, mj_runs=use_runs, mj_2p=two,
-                                           rs_bits=sparse, rs_pack12=pk12):
+                                           rs_bits=sparse, rs_pack12=pk12, rt2_match=match):
                         got = [t.cpu().numpy() for t in
                                jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, comp,
                                                   nrows=len(lk), rdup=False)]
@@ -844,6 +853,12 @@ def test_merge_join_runs_matches_oracle(device, layout):
                         if two:
                             launcher = jit.LAST_MJ_LAUNCHER[0]
                             assert isinstance(launcher, jit_runs.TwoPhaseLauncher)
+                            # the second launch of a lowering records the match (rt2_match)
+                            got = [t.cpu().numpy() for t in launcher.launch(p)]
+                            assert ("a.MATCH[" in launcher.kt.src) == match, cfg
+                            s_, c_ = got[0].reshape(G, 2)[:, 0], got[1].reshape(G, 2)[:, 1]
+                            assert (c_ == ec).all(), (cfg, "relaunch", c_, ec)
+                            assert np.allclose(s_, es, rtol=1e-12), cfg
                             if sparse and not grouped:
                                 assert jit_runs.pack_layout(p, comp) is not None
     finally:

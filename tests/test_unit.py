@@ -452,3 +452,18 @@ def test_hostgc_settle_freezes_live_objects():
         assert ref() is None
     finally:
         gc.unfreeze()
+
+
+def test_derived_buffers_shrink_the_table_cache_budget():
+    """Buffers a lowering keeps outside any table (device_cache.track_derived: the recorded run
+    matches of exec/jit_runs.py) count against the cache budget while they live."""
+    import gc
+    import torch
+    from hyperspace_amd.exec import device_cache as DC
+    base = DC.derived_bytes()
+    t = torch.empty(1000, dtype=torch.int32)
+    DC.track_derived(t)
+    assert DC.derived_bytes() == base + 4000
+    del t
+    gc.collect()
+    assert DC.derived_bytes() == base
