@@ -587,6 +587,7 @@ def _side_configs(args, sf) -> dict:
                          "trace": traceback.format_exc()[-1500:]}
         out[name]["wall_s"] = round(time.perf_counter() - t0, 2)
         print(f"[bench] side config {name}: {out[name]}", file=sys.stderr, flush=True)
+    release_process_device_memory()   # the cross-check's un-indexed scans need the room
     return out
 
 

@@ -72,8 +72,11 @@ def release_process_device_memory() -> None:
     jit_join._RUNS_HASH_LOWERED.clear()
     jit_runs._PACKS.clear()
     jit_runs._P12.clear()
-    import gc
-    gc.collect()
+    jit_join.LAST_MJ_LAUNCHER[0] = None
+    # a plain gc.collect() skips what utils/hostgc.py froze: the released sessions' cycles
+    # (and the device tensors they hold) are only found after an unfreeze
+    from ..utils import hostgc
+    hostgc.settle(full=True)
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
 

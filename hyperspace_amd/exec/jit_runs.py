@@ -36,7 +36,7 @@ from . import kernel_config as _KC  # noqa: E402
 _CFG = _KC.active()
 MJ_2P, RS_ITEMS = _CFG.mj_2p, _CFG.rs_items
 RT2_UNROLL, RT2_GRID, RT2_I32 = _CFG.rt2_unroll, _CFG.rt2_grid, _CFG.rt2_i32
-RT2_MATCH = _CFG.rt2_match
+RT2_MATCH, RT2_COPY = _CFG.rt2_match, _CFG.rt2_copy
 RS_BITS, RS_BITS_GRID, RS_PACK = _CFG.rs_bits, _CFG.rs_bits_grid, _CFG.rs_pack
 RS_PIPE, RS_WALK, RS_LDS, RS_LUT = _CFG.rs_pipe, _CFG.rs_walk, _CFG.rs_lds, _CFG.rs_lut
 RS_PK16, RS_WAVES, RS_PACK12 = _CFG.rs_pk16, _CFG.rs_waves, _CFG.rs_pack12
@@ -127,8 +127,8 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int, ix32: bool = False,
     lowering's ranges and the key columns, not on the literals (``record_matches``)."""
     IX = "int" if ix32 else "i64"  # noqa: N806 — run / right-row index type
     args = J.Args()
-    if mode == "match":
-        return _gen_tags2_match(p, compacts, W)
+    if mode in ("match", "copy"):
+        return _gen_tags2_match(p, compacts, W, mode == "copy")
     lk, rk = p.lkey, p.rkey
     args.add("p", f"RK{lk}", "const int*")
     args.add("p", "RNG", "const long long*")
@@ -329,14 +329,33 @@ def _tag_stores(b: List[str], u: int, W: int, ind: str) -> None:
               f"{ind}  if (in{u} && lane < {2 * W}) a.tags[(gi + {u}) * {2 * W} + lane] = wd_; }}"])
 
 
-def _gen_tags2_match(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
+def copy_ok(p: NL.JoinParams, compacts) -> bool:
+    """Whether phase 1 can read per-run copies of its right columns (mode "copy"): every staged
+    column is stored plainly or as a one-array compact code (not the grouped 16-bit form)."""
+    cols = J._col_specs(p, compacts)
+    for sl in _stage_slots(p):
+        enc = cols[sl][2]
+        if enc and len(enc) > 2 and enc[2] == 64:
+            return False
+    return True
+
+
+def _gen_tags2_match(p: NL.JoinParams, compacts, W: int, copy: bool = False) -> J.Kernel:
     """Phase 1 over a recorded match (``gen_run_tags2`` mode "match"): per run one int32 load
     of its right row (-1: no match, or the run is outside the lowering's ranges), then the right
     predicate / group columns at that row.  No key images, no range table, no gallop: the
     record already resolved them (``record_matches``), so the phase reads 4 bytes per run plus
-    the staged right columns (monotone rows: coalesced)."""
+    the staged right columns (monotone rows: coalesced).
+
+    ``copy`` (mode "copy"): the right columns were gathered into run order at the record
+    (``S<slot>`` / ``SV<slot>``, ``gen_match_gather``) and the match is one bit per run
+    (``HIT``, one 64-bit word per 64-run group, read once per wavefront): the phase reads the
+    stored codes of its predicate columns per run and nothing at right rows."""
     args = J.Args()
-    args.add("p", "MATCH", "const int*")
+    if copy:
+        args.add("p", "HIT", "const u64*")
+    else:
+        args.add("p", "MATCH", "const int*")
     args.add("p", "tags", "unsigned*")
     args.add("q", "NRUNS", "long long")
     cols = J._col_specs(p, compacts)
@@ -361,9 +380,26 @@ def _gen_tags2_match(p: NL.JoinParams, compacts, W: int) -> J.Kernel:
         f"  for (i64 gi = gbeg; gi < gend; gi += {U}) {{"]
     for u in range(U):
         # the record is padded to whole groups: an in-range group's 64 lanes all read it
-        b.extend([f"{ind}const bool in{u} = gi + {u} < gend;",
-                  f"{ind}const int mt{u} = a.MATCH[in{u} ? (((gi + {u}) << 6) + lane) : lane];"])
+        b.append(f"{ind}const bool in{u} = gi + {u} < gend;")
+        if copy:
+            b.extend([f"{ind}const int r{u} = in{u} ? (int)(((gi + {u}) << 6) + lane) : lane;",
+                      f"{ind}const u64 hb{u} = a.HIT[in{u} ? gi + {u} : 0];"])
+            for sl in stage_slots:
+                gt = J._Gen(args, cols, SPLIT, ("r_", "r_"), frozenset(), True)
+                sp = args.add("p", f"S{sl}", f"const {gt.raw_type(sl)}*")
+                b.append(f"{ind}const {gt.raw_type(sl)} w{sl}_g{u} = {sp}[r{u}];")
+                if cols[sl][1]:
+                    vp = args.add("p", f"SV{sl}", "const unsigned char*")
+                    b.append(f"{ind}const unsigned char u{sl}_g{u} = {vp}[r{u}];")
+        else:
+            b.append(f"{ind}const int mt{u} = a.MATCH[in{u} ? (((gi + {u}) << 6) + lane) : lane];")
     for u in range(U):
+        if copy:
+            b.append(f"{ind}const bool hit{u} = in{u} && ((hb{u} >> lane) & 1ull);")
+            gu = J._Gen(args, cols, SPLIT, (f"r{u}", f"r{u}"), frozenset(), True)
+            for sl in stage_slots:
+                J._uload_raw(gu, sl, f"g{u}", f"w{sl}_g{u}", f"u{sl}_g{u}", b, ind)
+            continue
         b.extend([f"{ind}const bool hit{u} = in{u} && mt{u} >= 0;",
                   f"{ind}const int j{u} = hit{u} ? mt{u} : 0;"])
         gu = J._Gen(args, cols, SPLIT, (f"j{u}", f"j{u}"), frozenset(), True)
@@ -400,6 +436,57 @@ def record_matches(p: NL.JoinParams, compacts, W: int, vt: dict, nruns: int, gri
     J.fill_preds_aggs(v, [(k_, p.preds[k_]) for k_ in range(p.npreds)], [], compacts)
     kr.launch(grid, v, NL.stream_ptr(), 0)
     return m
+
+
+def gen_match_gather(p: NL.JoinParams, compacts) -> J.Kernel:
+    """The right columns phase 1 reads, gathered into run order at the recorded match
+    (``S<slot>`` stored elements, ``SV<slot>`` validity bytes; row 0 for a run without one - its
+    HIT bit is clear): one pass at record time for the "copy" form of phase 1."""
+    args = J.Args()
+    args.add("p", "MATCH", "const int*")
+    args.add("q", "N", "long long")
+    cols = J._col_specs(p, compacts)
+    g = J._Gen(args, cols, SPLIT, ("j_", "j_"), frozenset(), True)
+    b = [f"  for (i64 i = (i64)blockIdx.x * {J.BLOCK} + threadIdx.x; i < a.N; "
+         f"i += (i64)gridDim.x * {J.BLOCK}) {{",
+         "    const int m_ = a.MATCH[i]; const int j_ = m_ >= 0 ? m_ : 0;"]
+    for sl in _stage_slots(p):
+        sp = args.add("p", f"S{sl}", f"{g.raw_type(sl)}*")
+        b.append(f"    {sp}[i] = {g.ptr(sl)}[j_];")
+        if cols[sl][1]:
+            vp = args.add("p", f"SV{sl}", "unsigned char*")
+            b.append(f"    {vp}[i] = {g.vptr(sl)}[j_];")
+    b.append("  }")
+    src = (J._PRELUDE + args.struct_src() +
+           f'extern "C" __global__ __launch_bounds__({J.BLOCK}) void hs_jit_match_gather(Args a) '
+           "{\n" + "\n".join(b) + "\n}\n")
+    return J.Kernel(src, "hs_jit_match_gather", args)
+
+
+def copy_matches(p: NL.JoinParams, compacts, m, vt: dict, dev) -> tuple:
+    """From a recorded match ``m``: the HIT words (bit l of word g: run 64 g + l has a right
+    row) and the gathered right columns; returns (tensors to keep, their argument values)."""
+    import torch
+    n = int(m.numel())
+    hit = ((m.view(-1, 64) >= 0).to(torch.int64) <<
+           torch.arange(64, device=dev, dtype=torch.int64)).sum(1)  # distinct bits: sum == OR
+    keep, vals = [hit], {"HIT": hit.data_ptr()}
+    cols = J._col_specs(p, compacts)
+    g = J._Gen(J.Args(), cols, SPLIT, ("j_", "j_"), frozenset(), True)
+    for sl in _stage_slots(p):
+        t = torch.empty(n * J._SIZEOF[g.raw_type(sl)], dtype=torch.uint8, device=dev)
+        keep.append(t)
+        vals[f"S{sl}"] = t.data_ptr()
+        if cols[sl][1]:
+            v = torch.empty(n, dtype=torch.uint8, device=dev)
+            keep.append(v)
+            vals[f"SV{sl}"] = v.data_ptr()
+    kg = J.kernel_for(("match_gather", tags2_shape(p, compacts, 1)[1], tuple(_stage_slots(p)),
+                       J.BLOCK),
+                      lambda: gen_match_gather(p, compacts))
+    a = dict(vt, MATCH=m.data_ptr(), N=n, **vals)
+    kg.launch(max(1, min(8192, (n + J.BLOCK - 1) // J.BLOCK)), a, NL.stream_ptr(), 0)
+    return keep, vals
 
 
 def run_ranges(rstart, rlen, rbucket, roff, runs):
@@ -1129,17 +1216,27 @@ class TwoPhaseLauncher:
         from .device_cache import track_derived
         W, nruns, p = self.match
         self.match = None
-        need = ((nruns + 63) >> 6) * 256
+        need = ((nruns + 63) >> 6) * 64 * 16
         free, _ = torch.cuda.mem_get_info(self.dev)
         free += torch.cuda.memory_reserved(self.dev) - torch.cuda.memory_allocated(self.dev)
         if free < need + (8 << 30):
             return
-        m = record_matches(p, self.compacts, W, self.vt, nruns, self.grid_t, self.dev)
-        track_derived(m)
-        self.kt = J.kernel_for(tags2_shape(p, self.compacts, W, True, "match"),
-                               lambda: gen_run_tags2(p, self.compacts, W, True, "match"))
-        self.vt = dict(self.vt, MATCH=m.data_ptr())
-        self.keep = self.keep + (m,)
+        try:
+            m = record_matches(p, self.compacts, W, self.vt, nruns, self.grid_t, self.dev)
+            mode = "copy" if RT2_COPY and copy_ok(p, self.compacts) else "match"
+            if mode == "copy":
+                held, vals = copy_matches(p, self.compacts, m, self.vt, self.dev)
+                # (the match record itself is dropped once the gather ran: stream-ordered frees)
+            else:
+                held, vals = [m], {"MATCH": m.data_ptr()}
+        except torch.OutOfMemoryError:
+            return      # an optional copy: the verifying form stays
+        for t in held:
+            track_derived(t)
+        self.kt = J.kernel_for(tags2_shape(p, self.compacts, W, True, mode),
+                               lambda: gen_run_tags2(p, self.compacts, W, True, mode))
+        self.vt = dict(self.vt, **vals)
+        self.keep = self.keep + tuple(held)
         # every packed phase-1 block and the captured pipeline name the verifying kernel
         self.tpl, self.graph = None, None
         self.blocks.clear()

@@ -77,6 +77,8 @@ class KernelConfig:
     rt2_i32: bool = True         # phase-1 run / right-row index math in 32 bits when tables fit
     rt2_match: bool = True       # phase 1 reads a per-run matched right row recorded at lowering
     #                              (literal-independent) instead of re-verifying the key match
+    rt2_copy: bool = True        # ... and the right predicate / group columns gathered into run
+    #                              order with it (one hit bit per run): nothing read at right rows
     rs_bits: bool = True         # phase 2 bit-parallel for 1-bit tags (gen_run_sparse_scan)
     rs_bits_grid: int = 8192
     rs_pack: bool = True         # bits scan reads its aggregate inputs row-packed

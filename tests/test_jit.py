@@ -217,7 +217,13 @@ def test_generated_sources_compile_with_compact_columns(rt, tmp_path):
         km = jit_runs.gen_run_tags2(q3, cr, W, True, "match")
         assert "a.MOUT[" in kr_.src and "a.MATCH[" in km.src
         assert "a.RK0[" not in km.src and "a.RNG" not in km.src and "a.c8" not in km.src
-        ks += [kr_, km]
+        # copy form: hit bits and run-order copies of the right columns, nothing at right rows
+        kc = jit_runs.gen_run_tags2(q3, cr, W, True, "copy")
+        kgat = jit_runs.gen_match_gather(q3, cr)
+        assert jit_runs.copy_ok(q3, cr) and "a.HIT[" in kc.src and "a.S9[" in kc.src
+        assert "a.c9" not in kc.src and "a.MATCH" not in kc.src
+        assert "a.S9[i] = a.c9[j_]" in kgat.src
+        ks += [kr_, km, kc, kgat]
     q3.group_col, q3.num_groups = 10, 300
     assert not jit_runs.applies(q3)
     q3.group_col = -1
@@ -840,10 +846,13 @@ def test_merge_join_runs_matches_oracle(device, layout):
                                                            (True, False, False, True, True),
                                                            (False, False, False, True, True)):
                     # pk12: the date predicate reads the 12-bit packed copy (codes span < 4096);
-                    # match: phase 1 reads the recorded per-run match (rt2_match)
+                    # match: phase 1 reads the recorded per-run match (rt2_match), the first
+                    # config with the right columns copied into run order (rt2_copy), the second
+                    # through the match
                     cfg = (keys, grouped, use_runs, two, sparse, pk12, match)
                     with kernel_config.use(mj_lds_keys=keys, mj_runs=use_runs, mj_2p=two,
-                                           rs_bits=sparse, rs_pack12=pk12, rt2_match=match):
+                                           rs_bits=sparse, rs_pack12=pk12, rt2_match=match,
+                                           rt2_copy=pk12):
                         got = [t.cpu().numpy() for t in
                                jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, comp,
                                                   nrows=len(lk), rdup=False)]
@@ -855,7 +864,8 @@ def test_merge_join_runs_matches_oracle(device, layout):
                             assert isinstance(launcher, jit_runs.TwoPhaseLauncher)
                             # the second launch of a lowering records the match (rt2_match)
                             got = [t.cpu().numpy() for t in launcher.launch(p)]
-                            assert ("a.MATCH[" in launcher.kt.src) == match, cfg
+                            assert ("a.MATCH[" in launcher.kt.src or
+                                    "a.HIT[" in launcher.kt.src) == match, cfg
                             s_, c_ = got[0].reshape(G, 2)[:, 0], got[1].reshape(G, 2)[:, 1]
                             assert (c_ == ec).all(), (cfg, "relaunch", c_, ec)
                             assert np.allclose(s_, es, rtol=1e-12), cfg
