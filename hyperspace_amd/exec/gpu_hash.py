@@ -503,7 +503,8 @@ class HashAggOps:
                 jit.merge_join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, comp,
                                    nrows=left.table.num_rows,
                                    cache_spans=fr is not None and rstart is fr[0],
-                                   rdup=jit.key_has_dups(right.col(rk)), hk=hk, htab=table, tk=tk)
+                                   rdup=jit.key_has_dups(right.col(rk)), hk=hk, htab=table, tk=tk,
+                                   record=HyperspaceConf.join_index_enabled(self.session.conf))
             return
         if right.table.num_rows * 64 < left.table.num_rows:
             left, right, lk, rk = right, left, rk, lk
@@ -549,7 +550,8 @@ class HashAggOps:
             jit.merge_join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets, comp,
                                nrows=left.table.num_rows,
                                cache_spans=fr is not None and rstart is fr[0],
-                               rdup=jit.key_has_dups(right.col(rk)), hk=hk, htab=table, tk=tk)
+                               rdup=jit.key_has_dups(right.col(rk)), hk=hk, htab=table, tk=tk,
+                               record=HyperspaceConf.join_index_enabled(self.session.conf))
 
     def _hash_combine_ranks(self, d, groups, G: int, A: int, minmax: bool):
         """Every rank's groups to every rank (one variable-size all-gather of packed rows, no

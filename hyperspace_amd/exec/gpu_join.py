@@ -695,6 +695,22 @@ class JoinOps:
             raise _NeedHash("group domain too large for LDS aggregation")
         return (True if all(s[0] is True for s in specs) else None), hi - lo, lo, None, specs[0][4]
 
+    def _run_match_ok(self, jp, left: DRel, right: DRel, rk, descs, rstart) -> bool:
+        """Whether this join takes the run-keyed two-phase form over the left table's full
+        ranges with unique right keys - the form whose launcher can keep its key match
+        (``jit_runs.TwoPhaseLauncher._record``) when join indexes are enabled."""
+        from . import jit_join, jit_runs
+        if not HyperspaceConf.codegen_enabled(self.session.conf) or not jit_runs.RT2_MATCH:
+            return False
+        fr = getattr(left.table, "_full_ranges", None)
+        if fr is None or rstart is not fr[0] or jit.key_has_dups(right.col(rk)):
+            return False
+        comp = self._compacts(descs)
+        if not jit.merge_join_ok(jp, comp, right.table.num_rows, left.table.num_rows) or \
+                not jit_runs.applies(jp):
+            return False
+        return jit_join._with_runs(jp, comp)[1] is not None
+
     def _join_agg_pair(self, node, left: DRel, right: DRel, lk, rk, fns, group, G, gbase):
         # drive the kernel from a much smaller side (the appended part of a hybrid scan).  Only
         # then: one work item per driving row is cheapest when each finds few matches, so a
@@ -728,7 +744,12 @@ class JoinOps:
             return self._empty_agg(len(specs), G)
         max_tiles = K.join_max_tiles(left.table.num_rows, rlen.numel())
         conf = self.session.conf
-        if HyperspaceConf.codegen_enabled(conf) and HyperspaceConf.join_index_enabled(conf) and \
+        jindex = HyperspaceConf.join_index_enabled(conf)
+        if jindex and self._run_match_ok(jp, left, right, rk, descs, rstart):
+            # a unique-key run-keyed join keeps its key match in run form instead (the two-phase
+            # launcher records it on its second launch): the faster join index
+            jindex = False
+        if HyperspaceConf.codegen_enabled(conf) and jindex and \
                 not getattr(self, "_merge_join_only", False) and \
                 getattr(left.table, "global_key", None) is not None and \
                 getattr(right.table, "global_key", None) is not None and \
@@ -751,7 +772,8 @@ class JoinOps:
                     out = jit.merge_join_agg(jp, rstart, rlen, rbk, right.table.bucket_offsets,
                                              comp, nrows=left.table.num_rows,
                                              cache_spans=fr is not None and rstart is fr[0],
-                                             rdup=jit.key_has_dups(right.col(rk)))
+                                             rdup=jit.key_has_dups(right.col(rk)),
+                                             record=HyperspaceConf.join_index_enabled(conf))
                     if fr is not None and rstart is fr[0] and probed is None:
                         # full ranges, no probing: the launch can be replayed for this pair
                         # (``implied`` then holds only isnotnull(key) conjuncts the full ranges

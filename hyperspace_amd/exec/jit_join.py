@@ -751,10 +751,13 @@ def merge_join_ok(p: NL.JoinParams, compacts=None, rnrows: int = 0, lnrows: int 
 
 
 def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None, nrows: int = 0,
-                   cache_spans: bool = False, rdup: bool = True, hk=None, htab=None, tk=None):
+                   cache_spans: bool = False, rdup: bool = True, hk=None, htab=None, tk=None,
+                   record: bool = False):
     """Sort-merge join + aggregate with ``gen_merge_join_agg`` (same outputs as ``join_agg``);
     ``nrows`` = left table rows; ``rdup`` = the right key column may repeat a key
-    (``key_has_dups``)."""
+    (``key_has_dups``).  ``record``: a reused two-phase lowering may keep its key match
+    (``jit_runs.TwoPhaseLauncher._record``: a join index in run form) - only where join indexes
+    are enabled; otherwise every launch re-matches the keys."""
     runs = None
     if not rdup:
         compacts, runs = _with_runs(p, compacts)
@@ -763,11 +766,11 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
         # over a resident table's cached full ranges the lowering is fixed (as in hash mode
         # below): a caller without a prepared launcher (the co-partitioned semi-join) reuses it
         ck = (id(rstart), id(runs), tuple(p.cols[s].data for s in range(NL.MAX_COLS)),
-              merge_join_shape(p, compacts)) if cache_spans else None
+              merge_join_shape(p, compacts), record) if cache_spans else None
         two = _RUNS_LOWERED.get(ck) if ck is not None else None
         if two is None:
             two = jit_runs.lower(p, rstart, rlen, rbucket, roff, compacts, runs, nrows,
-                                 cache_spans)
+                                 cache_spans, record=record)
             if two is not None and ck is not None:
                 if len(_RUNS_LOWERED) >= 8:
                     _RUNS_LOWERED.pop(next(iter(_RUNS_LOWERED)))
@@ -781,11 +784,11 @@ def merge_join_agg(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts=None,
         # column slots) is fixed: keep it, keyed by the ranges, the column pointers and the shape
         ck = (id(rstart), id(runs), tuple(p.cols[s].data for s in range(NL.MAX_COLS)),
               merge_join_shape(p, compacts, hk), id(tk),
-              tk.shape() if tk is not None else None) if cache_spans else None
+              tk.shape() if tk is not None else None, record) if cache_spans else None
         two = _RUNS_HASH_LOWERED.get(ck) if ck is not None else None
         if two is None:
             two = jit_runs.lower(p, rstart, rlen, rbucket, roff, compacts, runs, nrows,
-                                 cache_spans, hk=hk, tk=tk)
+                                 cache_spans, hk=hk, tk=tk, record=record)
             if two is not None and ck is not None:
                 if len(_RUNS_HASH_LOWERED) >= 8:
                     _RUNS_HASH_LOWERED.pop(next(iter(_RUNS_HASH_LOWERED)))

@@ -1320,7 +1320,7 @@ class TwoPhaseLauncher:
 
 
 def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: int,
-          cache_spans: bool, hk=None, tk=None) -> Optional[TwoPhaseLauncher]:
+          cache_spans: bool, hk=None, tk=None, record: bool = False) -> Optional[TwoPhaseLauncher]:
     """The two-phase launcher of a run-keyed merge join, or None when it does not apply.
     ``hk``: group by that hash key plan (left-side key columns only) through the bits scan's
     hash mode (needs 1-bit tags).  None for an empty right side too (nothing to match)."""
@@ -1385,7 +1385,7 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
     lz = TwoPhaseLauncher(kt, ks, grid_t, grid_s, GA, GA * 32 if _scan_grouped(p) else 0,
                           vt, vs, compacts, (rstart, rlen, rbucket, roff, tp, spans, tr, runs),
                           tags, dev, hk, tk if sparse else None)
-    if RT2_MATCH and ix32:
+    if record and RT2_MATCH and ix32:
         # the lowering's own parameters: a later launch's may bind other column slots
         lz.match = (W, nruns, NL.JoinParams.from_buffer_copy(p))
     return lz

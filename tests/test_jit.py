@@ -855,7 +855,7 @@ def test_merge_join_runs_matches_oracle(device, layout):
                                            rt2_copy=pk12):
                         got = [t.cpu().numpy() for t in
                                jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, comp,
-                                                  nrows=len(lk), rdup=False)]
+                                                  nrows=len(lk), rdup=False, record=match)]
                         s_, c_ = got[0].reshape(G, 2)[:, 0], got[1].reshape(G, 2)[:, 1]
                         assert (c_ == ec).all(), (cfg, c_, ec)
                         assert np.allclose(s_, es, rtol=1e-12), cfg
