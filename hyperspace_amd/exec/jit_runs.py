@@ -36,7 +36,7 @@ from . import kernel_config as _KC  # noqa: E402
 _CFG = _KC.active()
 MJ_2P, RS_ITEMS = _CFG.mj_2p, _CFG.rs_items
 RT2_UNROLL, RT2_GRID, RT2_I32 = _CFG.rt2_unroll, _CFG.rt2_grid, _CFG.rt2_i32
-RT2_MATCH, RT2_COPY = _CFG.rt2_match, _CFG.rt2_copy
+RT2_MATCH, RT2_COPY, RT2_LO16 = _CFG.rt2_match, _CFG.rt2_copy, _CFG.rt2_lo16
 RS_BITS, RS_BITS_GRID, RS_PACK = _CFG.rs_bits, _CFG.rs_bits_grid, _CFG.rs_pack
 RS_PIPE, RS_WALK, RS_LDS, RS_LUT = _CFG.rs_pipe, _CFG.rs_walk, _CFG.rs_lds, _CFG.rs_lut
 RS_PK16, RS_WAVES, RS_PACK12 = _CFG.rs_pk16, _CFG.rs_waves, _CFG.rs_pack12
@@ -145,6 +145,12 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int, ix32: bool = False,
     if mode == "rec":
         assert ix32
         args.add("p", "MOUT", "int*")
+    lo16 = mode in ("lo16", "lo16prep")
+    if lo16:
+        assert ix32
+        cst = "" if mode == "lo16prep" else "const "
+        args.add("p", "LL", f"{cst}unsigned short*")
+        args.add("p", "RL", f"{cst}unsigned short*")
     g = J._Gen(args, cols, SPLIT, ("row_", "row_"), frozenset(), True)
     rv = J._valid_expr(g, rk, "row_")
     if rgroup:
@@ -183,6 +189,20 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int, ix32: bool = False,
         gx = J._rename(f"x{p.group_col}", stage_slots, it)
         return (f"({{ const i64 gl_ = (i64){gx} - {gb}; (({ok}) && {cond} && gl_ >= 0 && "
                 f"gl_ < {ng}) ? (unsigned)(gl_ + 1) : 0u; }})")
+
+    if mode == "lo16prep":
+        # the low 16 bits of every left run key image and right key image (``lo16_keys``)
+        args.add("q", "NRIGHT", "long long")
+        body = [f"  auto IMG = [&]({IX} row_) -> unsigned {{ return {img}; }};",
+                f"  const i64 t_ = (i64)blockIdx.x * {J.BLOCK} + threadIdx.x, "
+                f"n_ = (i64)gridDim.x * {J.BLOCK};",
+                f"  for (i64 i = t_; i < a.NRUNS; i += n_) "
+                f"a.LL[i] = (unsigned short)((unsigned)a.RK{lk}[i] + (unsigned)a.KOF);",
+                "  for (i64 i = t_; i < a.NRIGHT; i += n_) a.RL[i] = (unsigned short)IMG((int)i);"]
+        src = (J._PRELUDE + args.struct_src() +
+               f'extern "C" __global__ __launch_bounds__({J.BLOCK}) void hs_jit_key_lo16(Args a) '
+               "{\n" + "\n".join(body) + "\n}\n")
+        return J.Kernel(src, "hs_jit_key_lo16", args)
 
     b: List[str] = [
         f"  auto IMG = [&]({IX} row_) -> unsigned {{ return {img}; }};",
@@ -234,25 +254,51 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int, ix32: bool = False,
                   f"a0_{u} = ({IX})RG[4 * q_ + 2]; a1_{u} = ({IX})RG[4 * q_ + 3]; }}"])
         b.extend([f"{ind}const bool act{u} = in{u} && r{u} < a.NRUNS && r{u} >= l0_{u} && "
               f"r{u} < l1_{u} && a1_{u} > a0_{u};",
-              f"{ind}const unsigned key{u} = (unsigned)a.RK{lk}[act{u} ? r{u} : 0] + "
-              f"(unsigned)a.KOF;",
               f"{ind}{IX} j{u} = (own{u} && gbase >= 0) ? gbase + {u * 64} + lane : "
               f"a0_{u} + (r{u} - l0_{u});",
               f"{ind}j{u} = act{u} ? (j{u} < a0_{u} ? a0_{u} : (j{u} >= a1_{u} ? a1_{u} - 1 : j{u}))"
-              f" : 0;",
-              f"{ind}const unsigned k{u} = IMGF(j{u});"])
+              f" : 0;"])
+        if lo16 and fast:
+            # 16-bit key halves per lane; the full images of the group's two end pairs (lanes
+            # 0 / 1 load them for lane 0 / lane 63) decide in ``resolve`` whether halves suffice
+            b.extend([f"{ind}const unsigned key{u} = (unsigned)a.LL[act{u} ? r{u} : 0];",
+                      f"{ind}const unsigned k{u} = (unsigned)a.RL[j{u}];",
+                      f"{ind}const int j0_{u} = __builtin_amdgcn_readlane((int)j{u}, 0), "
+                      f"j63_{u} = __builtin_amdgcn_readlane((int)j{u}, 63);",
+                      f"{ind}const int re_{u} = (int)((gi + {u}) << 6) + ((lane & 1) ? 63 : 0);",
+                      f"{ind}const unsigned fk{u} = (unsigned)a.RK{lk}[re_{u} < a.NRUNS ? re_{u} : 0]"
+                      f" + (unsigned)a.KOF;",
+                      f"{ind}const unsigned fi{u} = IMGF((lane & 1) ? j63_{u} : j0_{u});"])
+        else:
+            b.extend([f"{ind}const unsigned key{u} = (unsigned)a.RK{lk}[act{u} ? r{u} : 0] + "
+                      f"(unsigned)a.KOF;",
+                      f"{ind}const unsigned k{u} = IMGF(j{u});"])
         gu = J._Gen(args, cols, SPLIT, (f"j{u}", f"j{u}"), frozenset(), True)
         for sl in stage_slots:
             J._uload(gu, sl, f"g{u}", b, ind)
 
-    def resolve(u: int, ind: str) -> None:
+    def resolve(u: int, ind: str, lo: bool = False) -> None:
         gu = J._Gen(args, cols, SPLIT, (f"j{u}", f"j{u}"), frozenset(), True)
-        b.extend([f"{ind}bool hit{u} = act{u} && k{u} == key{u};",
-                  f"{ind}{IX} m{u} = j{u};",
+        # (a checked group's keys are low halves: a miss gallops with the full left key)
+        kfull = f"(unsigned)a.RK{lk}[r{u}] + (unsigned)a.KOF" if lo else f"key{u}"
+        if lo:
+            # halves decide when every lane is active, the guesses are consecutive and both end
+            # pairs match in full with a key span below 2^16: any lane's two keys then differ by
+            # less than 2^16.  Otherwise every lane takes the full-key path below.
+            b.extend([f"{ind}const unsigned fk0_{u} = (unsigned)__builtin_amdgcn_readlane((int)fk{u}, 0), "
+                      f"fk1_{u} = (unsigned)__builtin_amdgcn_readlane((int)fk{u}, 1);",
+                      f"{ind}const bool cl{u} = __ballot(act{u}) == ~0ull && j63_{u} - j0_{u} == 63 && "
+                      f"fk0_{u} == (unsigned)__builtin_amdgcn_readlane((int)fi{u}, 0) && "
+                      f"fk1_{u} == (unsigned)__builtin_amdgcn_readlane((int)fi{u}, 1) && "
+                      f"fk1_{u} - fk0_{u} < 65536u;",
+                      f"{ind}bool hit{u} = act{u} && cl{u} && k{u} == key{u};"])
+        else:
+            b.append(f"{ind}bool hit{u} = act{u} && k{u} == key{u};")
+        b.extend([f"{ind}{IX} m{u} = j{u};",
                   f"{ind}unsigned tg{u} = {tag_expr(gu, f'g{u}', f'hit{u}')};",
                   f"{ind}if (act{u} && !hit{u}) {{",
                   # gallop from the guess to the lower bound of key in [a0, a1)
-                  f"{ind}  const unsigned key_ = key{u}; {IX} lo_, hi_;",
+                  f"{ind}  const unsigned key_ = {kfull}; {IX} lo_, hi_;",
                   f"{ind}  const unsigned kj_ = IMG(j{u});",
                   f"{ind}  if (kj_ == key_) {{ lo_ = j{u}; hi_ = j{u}; }}",
                   f"{ind}  else if (kj_ > key_) {{",
@@ -297,7 +343,7 @@ def gen_run_tags2(p: NL.JoinParams, compacts, W: int, ix32: bool = False,
         for u in range(U):
             group(u, fast, ind)
         for u in range(U):
-            resolve(u, ind)
+            resolve(u, ind, lo16 and fast)
         # next iteration's guess: the last group's last lane, when it matched in this range
         b.extend([f"{ind}{{ const {IX} nx_ = __shfl((hit{U - 1} && own{U - 1}) ? m{U - 1} + 1 : "
                   f"({IX})-1, 63, 64);",
@@ -487,6 +533,27 @@ def copy_matches(p: NL.JoinParams, compacts, m, vt: dict, dev) -> tuple:
     a = dict(vt, MATCH=m.data_ptr(), N=n, **vals)
     kg.launch(max(1, min(8192, (n + J.BLOCK - 1) // J.BLOCK)), a, NL.stream_ptr(), 0)
     return keep, vals
+
+
+def lo16_keys(p: NL.JoinParams, compacts, W: int, vt: dict, nruns: int, nright: int, grid: int,
+              dev):
+    """The low 16 bits of the left run key images and the right key images (phase 1's checked
+    groups compare these: ``gen_run_tags2`` mode "lo16"), computed once per reused lowering;
+    None when the right key has nulls (a null's image 0 could alias a left key's low half).
+    Literal-independent encodings of the key columns: every query still matches its keys."""
+    import torch
+    from .device_cache import track_derived
+    if J._col_specs(p, compacts)[p.rkey][1]:
+        return None
+    ll = torch.empty(max(nruns, 1), dtype=torch.int16, device=dev)
+    rl = torch.empty(max(nright, 1), dtype=torch.int16, device=dev)
+    kp = J.kernel_for(tags2_shape(p, compacts, W, True, "lo16prep"),
+                      lambda: gen_run_tags2(p, compacts, W, True, "lo16prep"))
+    kp.launch(grid, dict(vt, LL=ll.data_ptr(), RL=rl.data_ptr(), NRIGHT=nright),
+              NL.stream_ptr(), 0)
+    track_derived(ll)
+    track_derived(rl)
+    return ll, rl
 
 
 def run_ranges(rstart, rlen, rbucket, roff, runs):
@@ -1364,6 +1431,13 @@ def lower(p: NL.JoinParams, rstart, rlen, rbucket, roff, compacts, runs, nrows: 
     grid_t = max(1, RT2_GRID)
     vt["KLO"], vt["KSP"], vt["KOF"] = frame
     J._fill_cols(vt, p.cols, compacts)
+    lo = lo16_keys(p, compacts, W, vt, nruns, int(roff[-1].item()), grid_t, dev) \
+        if RT2_LO16 and ix32 and cache_spans else None
+    if lo is not None:
+        kt = J.kernel_for(tags2_shape(p, compacts, W, ix32, "lo16"),
+                          lambda: gen_run_tags2(p, compacts, W, ix32, "lo16"))
+        vt["LL"], vt["RL"] = lo[0].data_ptr(), lo[1].data_ptr()
+        tr = (rng_d, lo)
     vs = {"rstart": rstart.data_ptr(), "rlen": rlen.data_ptr(), "tile_prefix": tp.data_ptr(),
           "tags": tags.data_ptr(), "R": rstart.numel(), "nrows": nrows,
           "num_groups": p.num_groups, "group_base": p.group_base}

@@ -79,6 +79,9 @@ class KernelConfig:
     #                              (literal-independent) instead of re-verifying the key match
     rt2_copy: bool = True        # ... and the right predicate / group columns gathered into run
     #                              order with it (one hit bit per run): nothing read at right rows
+    rt2_lo16: bool = False       # phase 1 compares 16-bit key halves in groups whose end keys
+    #                              matched in full with a key span < 2^16 (reused lowerings):
+    #                              correct, but 303 -> 465 us at SF100 (profiles/tags2_lo16_r6.txt)
     rs_bits: bool = True         # phase 2 bit-parallel for 1-bit tags (gen_run_sparse_scan)
     rs_bits_grid: int = 8192
     rs_pack: bool = True         # bits scan reads its aggregate inputs row-packed

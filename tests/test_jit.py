@@ -218,6 +218,10 @@ def test_generated_sources_compile_with_compact_columns(rt, tmp_path):
         assert "a.MOUT[" in kr_.src and "a.MATCH[" in km.src
         assert "a.RK0[" not in km.src and "a.RNG" not in km.src and "a.c8" not in km.src
         # copy form: hit bits and run-order copies of the right columns, nothing at right rows
+        klo = jit_runs.gen_run_tags2(q3, cr, W, True, "lo16")
+        kpr = jit_runs.gen_run_tags2(q3, cr, W, True, "lo16prep")
+        assert "a.LL[act" in klo.src and "cl0" in klo.src and "a.RL[i] =" in kpr.src
+        ks += [klo, kpr]
         kc = jit_runs.gen_run_tags2(q3, cr, W, True, "copy")
         kgat = jit_runs.gen_match_gather(q3, cr)
         assert jit_runs.copy_ok(q3, cr) and "a.HIT[" in kc.src and "a.S9[" in kc.src
@@ -819,6 +823,7 @@ def test_merge_join_runs_matches_oracle(device, layout):
         assert torch.equal(a.cpu(), b_)
     from hyperspace_amd.exec import jit_runs, kernel_config
     lds_keys = kernel_config.active().mj_lds_keys
+    alive = []
     try:
         for starts, lens in ((loff[:-1], loff[1:] - loff[:-1]),
                              (loff[:-1] + 5, loff[1:] - loff[:-1] - 9)):
@@ -833,6 +838,7 @@ def test_merge_join_runs_matches_oracle(device, layout):
             rlen = torch.from_numpy(lens.astype(np.int64)).to(device)
             rbk = torch.arange(B, dtype=torch.int32, device=device)
             roff_t = torch.from_numpy(roff).to(device)
+            alive.append((rstart, rlen, rbk, roff_t))   # cached lowerings key by tensor ids
             for keys, grouped in ((lds_keys, True), (32, True), (lds_keys, False)):
                 # ungrouped: 1-bit tags (bit-parallel phase 2 unless rs_bits is off)
                 p.group_col, p.num_groups = (10, 3) if grouped else (-1, 1)
@@ -852,16 +858,19 @@ def test_merge_join_runs_matches_oracle(device, layout):
                     cfg = (keys, grouped, use_runs, two, sparse, pk12, match)
                     with kernel_config.use(mj_lds_keys=keys, mj_runs=use_runs, mj_2p=two,
                                            rs_bits=sparse, rs_pack12=pk12, rt2_match=match,
-                                           rt2_copy=pk12):
+                                           rt2_copy=pk12, rt2_lo16=match):
                         got = [t.cpu().numpy() for t in
                                jit.merge_join_agg(p, rstart, rlen, rbk, roff_t, comp,
-                                                  nrows=len(lk), rdup=False, record=match)]
+                                                  nrows=len(lk), rdup=False, record=match,
+                                                  cache_spans=match)]
                         s_, c_ = got[0].reshape(G, 2)[:, 0], got[1].reshape(G, 2)[:, 1]
                         assert (c_ == ec).all(), (cfg, c_, ec)
                         assert np.allclose(s_, es, rtol=1e-12), cfg
                         if two:
                             launcher = jit.LAST_MJ_LAUNCHER[0]
                             assert isinstance(launcher, jit_runs.TwoPhaseLauncher)
+                            # a reused (cached) lowering compares 16-bit key halves (rt2_lo16)
+                            assert ("a.LL[" in launcher.kt.src) == match, cfg
                             # the second launch of a lowering records the match (rt2_match)
                             got = [t.cpu().numpy() for t in launcher.launch(p)]
                             assert ("a.MATCH[" in launcher.kt.src or
