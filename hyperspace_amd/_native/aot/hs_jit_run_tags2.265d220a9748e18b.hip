@@ -174,15 +174,10 @@ struct Args {
   long long KOF;
   const int* c8;
   long long B8;
-  const int* c9;
+  const short* c9;
   long long B9;
-  const short* c10;
-  long long B10;
   long long CL4;
   long long CH4;
-  const unsigned long long* S6;
-  long long N6;
-  long long L6;
 };
 extern "C" __global__ __launch_bounds__(256) void hs_jit_run_tags2(Args a) {
   auto IMG = [&](int row_) -> unsigned { return (false ? 0u : ({ const i64 __v_ = (i64)((long long)(a.B8 + (i64)a.c8[row_])); const i64 d_ = __v_ - a.KLO; (d_ < 0) ? 0u : (d_ > a.KSP ? 0xFFFFFFFFu : (unsigned)(d_ + 1)); })); };
@@ -213,73 +208,61 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_tags2(Args a) {
       const bool in0 = gi + 0 < gend;
       const int l0_0 = lr0, l1_0 = lr1, a0_0 = s0, a1_0 = s1; const bool own0 = true;
       const bool act0 = in0 && r0 < a.NRUNS && r0 >= l0_0 && r0 < l1_0 && a1_0 > a0_0;
-      const unsigned key0 = (unsigned)a.RK0[act0 ? r0 : 0] + (unsigned)a.KOF;
       int j0 = (own0 && gbase >= 0) ? gbase + 0 + lane : a0_0 + (r0 - l0_0);
       j0 = act0 ? (j0 < a0_0 ? a0_0 : (j0 >= a1_0 ? a1_0 - 1 : j0)) : 0;
+      const unsigned key0 = (unsigned)a.RK0[act0 ? r0 : 0] + (unsigned)a.KOF;
       const unsigned k0 = IMGF(j0);
-      const int w9_g0 = a.c9[j0];
-      const int r9_g0 = (int)w9_g0;
-      const long long x9_g0 = (long long)(a.B9 + (i64)w9_g0);
-      const short w10_g0 = a.c10[j0];
-      const int r10_g0 = (int)w10_g0;
-      const int x10_g0 = (int)(a.B10 + (i64)w10_g0);
       const int w8_g0 = a.c8[j0];
       const int r8_g0 = (int)w8_g0;
       const long long x8_g0 = (long long)(a.B8 + (i64)w8_g0);
+      const short w9_g0 = a.c9[j0];
+      const int r9_g0 = (int)w9_g0;
+      const int x9_g0 = (int)(a.B9 + (i64)w9_g0);
       const int r1 = (int)(((gi + 1) << 6) + lane);
       const bool in1 = gi + 1 < gend;
       const int l0_1 = lr0, l1_1 = lr1, a0_1 = s0, a1_1 = s1; const bool own1 = true;
       const bool act1 = in1 && r1 < a.NRUNS && r1 >= l0_1 && r1 < l1_1 && a1_1 > a0_1;
-      const unsigned key1 = (unsigned)a.RK0[act1 ? r1 : 0] + (unsigned)a.KOF;
       int j1 = (own1 && gbase >= 0) ? gbase + 64 + lane : a0_1 + (r1 - l0_1);
       j1 = act1 ? (j1 < a0_1 ? a0_1 : (j1 >= a1_1 ? a1_1 - 1 : j1)) : 0;
+      const unsigned key1 = (unsigned)a.RK0[act1 ? r1 : 0] + (unsigned)a.KOF;
       const unsigned k1 = IMGF(j1);
-      const int w9_g1 = a.c9[j1];
-      const int r9_g1 = (int)w9_g1;
-      const long long x9_g1 = (long long)(a.B9 + (i64)w9_g1);
-      const short w10_g1 = a.c10[j1];
-      const int r10_g1 = (int)w10_g1;
-      const int x10_g1 = (int)(a.B10 + (i64)w10_g1);
       const int w8_g1 = a.c8[j1];
       const int r8_g1 = (int)w8_g1;
       const long long x8_g1 = (long long)(a.B8 + (i64)w8_g1);
+      const short w9_g1 = a.c9[j1];
+      const int r9_g1 = (int)w9_g1;
+      const int x9_g1 = (int)(a.B9 + (i64)w9_g1);
       const int r2 = (int)(((gi + 2) << 6) + lane);
       const bool in2 = gi + 2 < gend;
       const int l0_2 = lr0, l1_2 = lr1, a0_2 = s0, a1_2 = s1; const bool own2 = true;
       const bool act2 = in2 && r2 < a.NRUNS && r2 >= l0_2 && r2 < l1_2 && a1_2 > a0_2;
-      const unsigned key2 = (unsigned)a.RK0[act2 ? r2 : 0] + (unsigned)a.KOF;
       int j2 = (own2 && gbase >= 0) ? gbase + 128 + lane : a0_2 + (r2 - l0_2);
       j2 = act2 ? (j2 < a0_2 ? a0_2 : (j2 >= a1_2 ? a1_2 - 1 : j2)) : 0;
+      const unsigned key2 = (unsigned)a.RK0[act2 ? r2 : 0] + (unsigned)a.KOF;
       const unsigned k2 = IMGF(j2);
-      const int w9_g2 = a.c9[j2];
-      const int r9_g2 = (int)w9_g2;
-      const long long x9_g2 = (long long)(a.B9 + (i64)w9_g2);
-      const short w10_g2 = a.c10[j2];
-      const int r10_g2 = (int)w10_g2;
-      const int x10_g2 = (int)(a.B10 + (i64)w10_g2);
       const int w8_g2 = a.c8[j2];
       const int r8_g2 = (int)w8_g2;
       const long long x8_g2 = (long long)(a.B8 + (i64)w8_g2);
+      const short w9_g2 = a.c9[j2];
+      const int r9_g2 = (int)w9_g2;
+      const int x9_g2 = (int)(a.B9 + (i64)w9_g2);
       const int r3 = (int)(((gi + 3) << 6) + lane);
       const bool in3 = gi + 3 < gend;
       const int l0_3 = lr0, l1_3 = lr1, a0_3 = s0, a1_3 = s1; const bool own3 = true;
       const bool act3 = in3 && r3 < a.NRUNS && r3 >= l0_3 && r3 < l1_3 && a1_3 > a0_3;
-      const unsigned key3 = (unsigned)a.RK0[act3 ? r3 : 0] + (unsigned)a.KOF;
       int j3 = (own3 && gbase >= 0) ? gbase + 192 + lane : a0_3 + (r3 - l0_3);
       j3 = act3 ? (j3 < a0_3 ? a0_3 : (j3 >= a1_3 ? a1_3 - 1 : j3)) : 0;
+      const unsigned key3 = (unsigned)a.RK0[act3 ? r3 : 0] + (unsigned)a.KOF;
       const unsigned k3 = IMGF(j3);
-      const int w9_g3 = a.c9[j3];
-      const int r9_g3 = (int)w9_g3;
-      const long long x9_g3 = (long long)(a.B9 + (i64)w9_g3);
-      const short w10_g3 = a.c10[j3];
-      const int r10_g3 = (int)w10_g3;
-      const int x10_g3 = (int)(a.B10 + (i64)w10_g3);
       const int w8_g3 = a.c8[j3];
       const int r8_g3 = (int)w8_g3;
       const long long x8_g3 = (long long)(a.B8 + (i64)w8_g3);
+      const short w9_g3 = a.c9[j3];
+      const int r9_g3 = (int)w9_g3;
+      const int x9_g3 = (int)(a.B9 + (i64)w9_g3);
       bool hit0 = act0 && k0 == key0;
       int m0 = j0;
-      unsigned tg0 = ((hit0) && ((true)) && ((true)) && ((true && (r10_g0 >= (int)a.CL4 && r10_g0 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_g0 - a.L6))) ? 1u : 0u);
+      unsigned tg0 = ((hit0) && ((true)) && ((true)) && ((true && (r9_g0 >= (int)a.CL4 && r9_g0 <= (int)a.CH4))) ? 1u : 0u);
       if (act0 && !hit0) {
         const unsigned key_ = key0; int lo_, hi_;
         const unsigned kj_ = IMG(j0);
@@ -297,22 +280,19 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_tags2(Args a) {
         m0 = lo_;
         hit0 = lo_ < a1_0 && IMG(lo_) == key_;
         const int jm0 = hit0 ? lo_ : 0;
-        const int w9_h0 = a.c9[jm0];
-        const int r9_h0 = (int)w9_h0;
-        const long long x9_h0 = (long long)(a.B9 + (i64)w9_h0);
-        const short w10_h0 = a.c10[jm0];
-        const int r10_h0 = (int)w10_h0;
-        const int x10_h0 = (int)(a.B10 + (i64)w10_h0);
         const int w8_h0 = a.c8[jm0];
         const int r8_h0 = (int)w8_h0;
         const long long x8_h0 = (long long)(a.B8 + (i64)w8_h0);
-        tg0 = ((hit0) && ((true)) && ((true)) && ((true && (r10_h0 >= (int)a.CL4 && r10_h0 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_h0 - a.L6))) ? 1u : 0u);
+        const short w9_h0 = a.c9[jm0];
+        const int r9_h0 = (int)w9_h0;
+        const int x9_h0 = (int)(a.B9 + (i64)w9_h0);
+        tg0 = ((hit0) && ((true)) && ((true)) && ((true && (r9_h0 >= (int)a.CL4 && r9_h0 <= (int)a.CH4))) ? 1u : 0u);
       }
       { const u64 bal_ = __ballot(tg0 != 0u);
         if (in0 && lane < 2) a.tags[((gi + 0) << 1) + lane] = (unsigned)(bal_ >> (32 * lane)); }
       bool hit1 = act1 && k1 == key1;
       int m1 = j1;
-      unsigned tg1 = ((hit1) && ((true)) && ((true)) && ((true && (r10_g1 >= (int)a.CL4 && r10_g1 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_g1 - a.L6))) ? 1u : 0u);
+      unsigned tg1 = ((hit1) && ((true)) && ((true)) && ((true && (r9_g1 >= (int)a.CL4 && r9_g1 <= (int)a.CH4))) ? 1u : 0u);
       if (act1 && !hit1) {
         const unsigned key_ = key1; int lo_, hi_;
         const unsigned kj_ = IMG(j1);
@@ -330,22 +310,19 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_tags2(Args a) {
         m1 = lo_;
         hit1 = lo_ < a1_1 && IMG(lo_) == key_;
         const int jm1 = hit1 ? lo_ : 0;
-        const int w9_h1 = a.c9[jm1];
-        const int r9_h1 = (int)w9_h1;
-        const long long x9_h1 = (long long)(a.B9 + (i64)w9_h1);
-        const short w10_h1 = a.c10[jm1];
-        const int r10_h1 = (int)w10_h1;
-        const int x10_h1 = (int)(a.B10 + (i64)w10_h1);
         const int w8_h1 = a.c8[jm1];
         const int r8_h1 = (int)w8_h1;
         const long long x8_h1 = (long long)(a.B8 + (i64)w8_h1);
-        tg1 = ((hit1) && ((true)) && ((true)) && ((true && (r10_h1 >= (int)a.CL4 && r10_h1 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_h1 - a.L6))) ? 1u : 0u);
+        const short w9_h1 = a.c9[jm1];
+        const int r9_h1 = (int)w9_h1;
+        const int x9_h1 = (int)(a.B9 + (i64)w9_h1);
+        tg1 = ((hit1) && ((true)) && ((true)) && ((true && (r9_h1 >= (int)a.CL4 && r9_h1 <= (int)a.CH4))) ? 1u : 0u);
       }
       { const u64 bal_ = __ballot(tg1 != 0u);
         if (in1 && lane < 2) a.tags[((gi + 1) << 1) + lane] = (unsigned)(bal_ >> (32 * lane)); }
       bool hit2 = act2 && k2 == key2;
       int m2 = j2;
-      unsigned tg2 = ((hit2) && ((true)) && ((true)) && ((true && (r10_g2 >= (int)a.CL4 && r10_g2 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_g2 - a.L6))) ? 1u : 0u);
+      unsigned tg2 = ((hit2) && ((true)) && ((true)) && ((true && (r9_g2 >= (int)a.CL4 && r9_g2 <= (int)a.CH4))) ? 1u : 0u);
       if (act2 && !hit2) {
         const unsigned key_ = key2; int lo_, hi_;
         const unsigned kj_ = IMG(j2);
@@ -363,22 +340,19 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_tags2(Args a) {
         m2 = lo_;
         hit2 = lo_ < a1_2 && IMG(lo_) == key_;
         const int jm2 = hit2 ? lo_ : 0;
-        const int w9_h2 = a.c9[jm2];
-        const int r9_h2 = (int)w9_h2;
-        const long long x9_h2 = (long long)(a.B9 + (i64)w9_h2);
-        const short w10_h2 = a.c10[jm2];
-        const int r10_h2 = (int)w10_h2;
-        const int x10_h2 = (int)(a.B10 + (i64)w10_h2);
         const int w8_h2 = a.c8[jm2];
         const int r8_h2 = (int)w8_h2;
         const long long x8_h2 = (long long)(a.B8 + (i64)w8_h2);
-        tg2 = ((hit2) && ((true)) && ((true)) && ((true && (r10_h2 >= (int)a.CL4 && r10_h2 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_h2 - a.L6))) ? 1u : 0u);
+        const short w9_h2 = a.c9[jm2];
+        const int r9_h2 = (int)w9_h2;
+        const int x9_h2 = (int)(a.B9 + (i64)w9_h2);
+        tg2 = ((hit2) && ((true)) && ((true)) && ((true && (r9_h2 >= (int)a.CL4 && r9_h2 <= (int)a.CH4))) ? 1u : 0u);
       }
       { const u64 bal_ = __ballot(tg2 != 0u);
         if (in2 && lane < 2) a.tags[((gi + 2) << 1) + lane] = (unsigned)(bal_ >> (32 * lane)); }
       bool hit3 = act3 && k3 == key3;
       int m3 = j3;
-      unsigned tg3 = ((hit3) && ((true)) && ((true)) && ((true && (r10_g3 >= (int)a.CL4 && r10_g3 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_g3 - a.L6))) ? 1u : 0u);
+      unsigned tg3 = ((hit3) && ((true)) && ((true)) && ((true && (r9_g3 >= (int)a.CL4 && r9_g3 <= (int)a.CH4))) ? 1u : 0u);
       if (act3 && !hit3) {
         const unsigned key_ = key3; int lo_, hi_;
         const unsigned kj_ = IMG(j3);
@@ -396,16 +370,13 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_tags2(Args a) {
         m3 = lo_;
         hit3 = lo_ < a1_3 && IMG(lo_) == key_;
         const int jm3 = hit3 ? lo_ : 0;
-        const int w9_h3 = a.c9[jm3];
-        const int r9_h3 = (int)w9_h3;
-        const long long x9_h3 = (long long)(a.B9 + (i64)w9_h3);
-        const short w10_h3 = a.c10[jm3];
-        const int r10_h3 = (int)w10_h3;
-        const int x10_h3 = (int)(a.B10 + (i64)w10_h3);
         const int w8_h3 = a.c8[jm3];
         const int r8_h3 = (int)w8_h3;
         const long long x8_h3 = (long long)(a.B8 + (i64)w8_h3);
-        tg3 = ((hit3) && ((true)) && ((true)) && ((true && (r10_h3 >= (int)a.CL4 && r10_h3 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_h3 - a.L6))) ? 1u : 0u);
+        const short w9_h3 = a.c9[jm3];
+        const int r9_h3 = (int)w9_h3;
+        const int x9_h3 = (int)(a.B9 + (i64)w9_h3);
+        tg3 = ((hit3) && ((true)) && ((true)) && ((true && (r9_h3 >= (int)a.CL4 && r9_h3 <= (int)a.CH4))) ? 1u : 0u);
       }
       { const u64 bal_ = __ballot(tg3 != 0u);
         if (in3 && lane < 2) a.tags[((gi + 3) << 1) + lane] = (unsigned)(bal_ >> (32 * lane)); }
@@ -419,19 +390,16 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_tags2(Args a) {
         while (q_ + 1 < (int)a.NRG && RG[4 * (q_ + 1)] <= r0) ++q_;
         l0_0 = (int)RG[4 * q_]; l1_0 = (int)RG[4 * q_ + 1]; a0_0 = (int)RG[4 * q_ + 2]; a1_0 = (int)RG[4 * q_ + 3]; }
       const bool act0 = in0 && r0 < a.NRUNS && r0 >= l0_0 && r0 < l1_0 && a1_0 > a0_0;
-      const unsigned key0 = (unsigned)a.RK0[act0 ? r0 : 0] + (unsigned)a.KOF;
       int j0 = (own0 && gbase >= 0) ? gbase + 0 + lane : a0_0 + (r0 - l0_0);
       j0 = act0 ? (j0 < a0_0 ? a0_0 : (j0 >= a1_0 ? a1_0 - 1 : j0)) : 0;
+      const unsigned key0 = (unsigned)a.RK0[act0 ? r0 : 0] + (unsigned)a.KOF;
       const unsigned k0 = IMGF(j0);
-      const int w9_g0 = a.c9[j0];
-      const int r9_g0 = (int)w9_g0;
-      const long long x9_g0 = (long long)(a.B9 + (i64)w9_g0);
-      const short w10_g0 = a.c10[j0];
-      const int r10_g0 = (int)w10_g0;
-      const int x10_g0 = (int)(a.B10 + (i64)w10_g0);
       const int w8_g0 = a.c8[j0];
       const int r8_g0 = (int)w8_g0;
       const long long x8_g0 = (long long)(a.B8 + (i64)w8_g0);
+      const short w9_g0 = a.c9[j0];
+      const int r9_g0 = (int)w9_g0;
+      const int x9_g0 = (int)(a.B9 + (i64)w9_g0);
       const int r1 = (int)(((gi + 1) << 6) + lane);
       const bool in1 = gi + 1 < gend;
       int l0_1 = lr0, l1_1 = lr1, a0_1 = s0, a1_1 = s1; bool own1 = true;
@@ -439,19 +407,16 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_tags2(Args a) {
         while (q_ + 1 < (int)a.NRG && RG[4 * (q_ + 1)] <= r1) ++q_;
         l0_1 = (int)RG[4 * q_]; l1_1 = (int)RG[4 * q_ + 1]; a0_1 = (int)RG[4 * q_ + 2]; a1_1 = (int)RG[4 * q_ + 3]; }
       const bool act1 = in1 && r1 < a.NRUNS && r1 >= l0_1 && r1 < l1_1 && a1_1 > a0_1;
-      const unsigned key1 = (unsigned)a.RK0[act1 ? r1 : 0] + (unsigned)a.KOF;
       int j1 = (own1 && gbase >= 0) ? gbase + 64 + lane : a0_1 + (r1 - l0_1);
       j1 = act1 ? (j1 < a0_1 ? a0_1 : (j1 >= a1_1 ? a1_1 - 1 : j1)) : 0;
+      const unsigned key1 = (unsigned)a.RK0[act1 ? r1 : 0] + (unsigned)a.KOF;
       const unsigned k1 = IMGF(j1);
-      const int w9_g1 = a.c9[j1];
-      const int r9_g1 = (int)w9_g1;
-      const long long x9_g1 = (long long)(a.B9 + (i64)w9_g1);
-      const short w10_g1 = a.c10[j1];
-      const int r10_g1 = (int)w10_g1;
-      const int x10_g1 = (int)(a.B10 + (i64)w10_g1);
       const int w8_g1 = a.c8[j1];
       const int r8_g1 = (int)w8_g1;
       const long long x8_g1 = (long long)(a.B8 + (i64)w8_g1);
+      const short w9_g1 = a.c9[j1];
+      const int r9_g1 = (int)w9_g1;
+      const int x9_g1 = (int)(a.B9 + (i64)w9_g1);
       const int r2 = (int)(((gi + 2) << 6) + lane);
       const bool in2 = gi + 2 < gend;
       int l0_2 = lr0, l1_2 = lr1, a0_2 = s0, a1_2 = s1; bool own2 = true;
@@ -459,19 +424,16 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_tags2(Args a) {
         while (q_ + 1 < (int)a.NRG && RG[4 * (q_ + 1)] <= r2) ++q_;
         l0_2 = (int)RG[4 * q_]; l1_2 = (int)RG[4 * q_ + 1]; a0_2 = (int)RG[4 * q_ + 2]; a1_2 = (int)RG[4 * q_ + 3]; }
       const bool act2 = in2 && r2 < a.NRUNS && r2 >= l0_2 && r2 < l1_2 && a1_2 > a0_2;
-      const unsigned key2 = (unsigned)a.RK0[act2 ? r2 : 0] + (unsigned)a.KOF;
       int j2 = (own2 && gbase >= 0) ? gbase + 128 + lane : a0_2 + (r2 - l0_2);
       j2 = act2 ? (j2 < a0_2 ? a0_2 : (j2 >= a1_2 ? a1_2 - 1 : j2)) : 0;
+      const unsigned key2 = (unsigned)a.RK0[act2 ? r2 : 0] + (unsigned)a.KOF;
       const unsigned k2 = IMGF(j2);
-      const int w9_g2 = a.c9[j2];
-      const int r9_g2 = (int)w9_g2;
-      const long long x9_g2 = (long long)(a.B9 + (i64)w9_g2);
-      const short w10_g2 = a.c10[j2];
-      const int r10_g2 = (int)w10_g2;
-      const int x10_g2 = (int)(a.B10 + (i64)w10_g2);
       const int w8_g2 = a.c8[j2];
       const int r8_g2 = (int)w8_g2;
       const long long x8_g2 = (long long)(a.B8 + (i64)w8_g2);
+      const short w9_g2 = a.c9[j2];
+      const int r9_g2 = (int)w9_g2;
+      const int x9_g2 = (int)(a.B9 + (i64)w9_g2);
       const int r3 = (int)(((gi + 3) << 6) + lane);
       const bool in3 = gi + 3 < gend;
       int l0_3 = lr0, l1_3 = lr1, a0_3 = s0, a1_3 = s1; bool own3 = true;
@@ -479,22 +441,19 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_tags2(Args a) {
         while (q_ + 1 < (int)a.NRG && RG[4 * (q_ + 1)] <= r3) ++q_;
         l0_3 = (int)RG[4 * q_]; l1_3 = (int)RG[4 * q_ + 1]; a0_3 = (int)RG[4 * q_ + 2]; a1_3 = (int)RG[4 * q_ + 3]; }
       const bool act3 = in3 && r3 < a.NRUNS && r3 >= l0_3 && r3 < l1_3 && a1_3 > a0_3;
-      const unsigned key3 = (unsigned)a.RK0[act3 ? r3 : 0] + (unsigned)a.KOF;
       int j3 = (own3 && gbase >= 0) ? gbase + 192 + lane : a0_3 + (r3 - l0_3);
       j3 = act3 ? (j3 < a0_3 ? a0_3 : (j3 >= a1_3 ? a1_3 - 1 : j3)) : 0;
+      const unsigned key3 = (unsigned)a.RK0[act3 ? r3 : 0] + (unsigned)a.KOF;
       const unsigned k3 = IMGF(j3);
-      const int w9_g3 = a.c9[j3];
-      const int r9_g3 = (int)w9_g3;
-      const long long x9_g3 = (long long)(a.B9 + (i64)w9_g3);
-      const short w10_g3 = a.c10[j3];
-      const int r10_g3 = (int)w10_g3;
-      const int x10_g3 = (int)(a.B10 + (i64)w10_g3);
       const int w8_g3 = a.c8[j3];
       const int r8_g3 = (int)w8_g3;
       const long long x8_g3 = (long long)(a.B8 + (i64)w8_g3);
+      const short w9_g3 = a.c9[j3];
+      const int r9_g3 = (int)w9_g3;
+      const int x9_g3 = (int)(a.B9 + (i64)w9_g3);
       bool hit0 = act0 && k0 == key0;
       int m0 = j0;
-      unsigned tg0 = ((hit0) && ((true)) && ((true)) && ((true && (r10_g0 >= (int)a.CL4 && r10_g0 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_g0 - a.L6))) ? 1u : 0u);
+      unsigned tg0 = ((hit0) && ((true)) && ((true)) && ((true && (r9_g0 >= (int)a.CL4 && r9_g0 <= (int)a.CH4))) ? 1u : 0u);
       if (act0 && !hit0) {
         const unsigned key_ = key0; int lo_, hi_;
         const unsigned kj_ = IMG(j0);
@@ -512,22 +471,19 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_tags2(Args a) {
         m0 = lo_;
         hit0 = lo_ < a1_0 && IMG(lo_) == key_;
         const int jm0 = hit0 ? lo_ : 0;
-        const int w9_h0 = a.c9[jm0];
-        const int r9_h0 = (int)w9_h0;
-        const long long x9_h0 = (long long)(a.B9 + (i64)w9_h0);
-        const short w10_h0 = a.c10[jm0];
-        const int r10_h0 = (int)w10_h0;
-        const int x10_h0 = (int)(a.B10 + (i64)w10_h0);
         const int w8_h0 = a.c8[jm0];
         const int r8_h0 = (int)w8_h0;
         const long long x8_h0 = (long long)(a.B8 + (i64)w8_h0);
-        tg0 = ((hit0) && ((true)) && ((true)) && ((true && (r10_h0 >= (int)a.CL4 && r10_h0 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_h0 - a.L6))) ? 1u : 0u);
+        const short w9_h0 = a.c9[jm0];
+        const int r9_h0 = (int)w9_h0;
+        const int x9_h0 = (int)(a.B9 + (i64)w9_h0);
+        tg0 = ((hit0) && ((true)) && ((true)) && ((true && (r9_h0 >= (int)a.CL4 && r9_h0 <= (int)a.CH4))) ? 1u : 0u);
       }
       { const u64 bal_ = __ballot(tg0 != 0u);
         if (in0 && lane < 2) a.tags[((gi + 0) << 1) + lane] = (unsigned)(bal_ >> (32 * lane)); }
       bool hit1 = act1 && k1 == key1;
       int m1 = j1;
-      unsigned tg1 = ((hit1) && ((true)) && ((true)) && ((true && (r10_g1 >= (int)a.CL4 && r10_g1 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_g1 - a.L6))) ? 1u : 0u);
+      unsigned tg1 = ((hit1) && ((true)) && ((true)) && ((true && (r9_g1 >= (int)a.CL4 && r9_g1 <= (int)a.CH4))) ? 1u : 0u);
       if (act1 && !hit1) {
         const unsigned key_ = key1; int lo_, hi_;
         const unsigned kj_ = IMG(j1);
@@ -545,22 +501,19 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_tags2(Args a) {
         m1 = lo_;
         hit1 = lo_ < a1_1 && IMG(lo_) == key_;
         const int jm1 = hit1 ? lo_ : 0;
-        const int w9_h1 = a.c9[jm1];
-        const int r9_h1 = (int)w9_h1;
-        const long long x9_h1 = (long long)(a.B9 + (i64)w9_h1);
-        const short w10_h1 = a.c10[jm1];
-        const int r10_h1 = (int)w10_h1;
-        const int x10_h1 = (int)(a.B10 + (i64)w10_h1);
         const int w8_h1 = a.c8[jm1];
         const int r8_h1 = (int)w8_h1;
         const long long x8_h1 = (long long)(a.B8 + (i64)w8_h1);
-        tg1 = ((hit1) && ((true)) && ((true)) && ((true && (r10_h1 >= (int)a.CL4 && r10_h1 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_h1 - a.L6))) ? 1u : 0u);
+        const short w9_h1 = a.c9[jm1];
+        const int r9_h1 = (int)w9_h1;
+        const int x9_h1 = (int)(a.B9 + (i64)w9_h1);
+        tg1 = ((hit1) && ((true)) && ((true)) && ((true && (r9_h1 >= (int)a.CL4 && r9_h1 <= (int)a.CH4))) ? 1u : 0u);
       }
       { const u64 bal_ = __ballot(tg1 != 0u);
         if (in1 && lane < 2) a.tags[((gi + 1) << 1) + lane] = (unsigned)(bal_ >> (32 * lane)); }
       bool hit2 = act2 && k2 == key2;
       int m2 = j2;
-      unsigned tg2 = ((hit2) && ((true)) && ((true)) && ((true && (r10_g2 >= (int)a.CL4 && r10_g2 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_g2 - a.L6))) ? 1u : 0u);
+      unsigned tg2 = ((hit2) && ((true)) && ((true)) && ((true && (r9_g2 >= (int)a.CL4 && r9_g2 <= (int)a.CH4))) ? 1u : 0u);
       if (act2 && !hit2) {
         const unsigned key_ = key2; int lo_, hi_;
         const unsigned kj_ = IMG(j2);
@@ -578,22 +531,19 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_tags2(Args a) {
         m2 = lo_;
         hit2 = lo_ < a1_2 && IMG(lo_) == key_;
         const int jm2 = hit2 ? lo_ : 0;
-        const int w9_h2 = a.c9[jm2];
-        const int r9_h2 = (int)w9_h2;
-        const long long x9_h2 = (long long)(a.B9 + (i64)w9_h2);
-        const short w10_h2 = a.c10[jm2];
-        const int r10_h2 = (int)w10_h2;
-        const int x10_h2 = (int)(a.B10 + (i64)w10_h2);
         const int w8_h2 = a.c8[jm2];
         const int r8_h2 = (int)w8_h2;
         const long long x8_h2 = (long long)(a.B8 + (i64)w8_h2);
-        tg2 = ((hit2) && ((true)) && ((true)) && ((true && (r10_h2 >= (int)a.CL4 && r10_h2 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_h2 - a.L6))) ? 1u : 0u);
+        const short w9_h2 = a.c9[jm2];
+        const int r9_h2 = (int)w9_h2;
+        const int x9_h2 = (int)(a.B9 + (i64)w9_h2);
+        tg2 = ((hit2) && ((true)) && ((true)) && ((true && (r9_h2 >= (int)a.CL4 && r9_h2 <= (int)a.CH4))) ? 1u : 0u);
       }
       { const u64 bal_ = __ballot(tg2 != 0u);
         if (in2 && lane < 2) a.tags[((gi + 2) << 1) + lane] = (unsigned)(bal_ >> (32 * lane)); }
       bool hit3 = act3 && k3 == key3;
       int m3 = j3;
-      unsigned tg3 = ((hit3) && ((true)) && ((true)) && ((true && (r10_g3 >= (int)a.CL4 && r10_g3 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_g3 - a.L6))) ? 1u : 0u);
+      unsigned tg3 = ((hit3) && ((true)) && ((true)) && ((true && (r9_g3 >= (int)a.CL4 && r9_g3 <= (int)a.CH4))) ? 1u : 0u);
       if (act3 && !hit3) {
         const unsigned key_ = key3; int lo_, hi_;
         const unsigned kj_ = IMG(j3);
@@ -611,16 +561,13 @@ extern "C" __global__ __launch_bounds__(256) void hs_jit_run_tags2(Args a) {
         m3 = lo_;
         hit3 = lo_ < a1_3 && IMG(lo_) == key_;
         const int jm3 = hit3 ? lo_ : 0;
-        const int w9_h3 = a.c9[jm3];
-        const int r9_h3 = (int)w9_h3;
-        const long long x9_h3 = (long long)(a.B9 + (i64)w9_h3);
-        const short w10_h3 = a.c10[jm3];
-        const int r10_h3 = (int)w10_h3;
-        const int x10_h3 = (int)(a.B10 + (i64)w10_h3);
         const int w8_h3 = a.c8[jm3];
         const int r8_h3 = (int)w8_h3;
         const long long x8_h3 = (long long)(a.B8 + (i64)w8_h3);
-        tg3 = ((hit3) && ((true)) && ((true)) && ((true && (r10_h3 >= (int)a.CL4 && r10_h3 <= (int)a.CH4))) && ((true)) && ((true && bit_test(a.S6, a.N6 * 64, (i64)x9_h3 - a.L6))) ? 1u : 0u);
+        const short w9_h3 = a.c9[jm3];
+        const int r9_h3 = (int)w9_h3;
+        const int x9_h3 = (int)(a.B9 + (i64)w9_h3);
+        tg3 = ((hit3) && ((true)) && ((true)) && ((true && (r9_h3 >= (int)a.CL4 && r9_h3 <= (int)a.CH4))) ? 1u : 0u);
       }
       { const u64 bal_ = __ballot(tg3 != 0u);
         if (in3 && lane < 2) a.tags[((gi + 3) << 1) + lane] = (unsigned)(bal_ >> (32 * lane)); }
