@@ -157,8 +157,13 @@ class GpuBackend(AggOps, JoinOps, SemiJoinOps, HashAggOps):
             free, _ = torch.cuda.mem_get_info(self.device)
             reserve = min(reserve, int(free * 0.8))
             if reserve > (1 << 30):
-                block = torch.empty(reserve, dtype=torch.uint8, device=self.device)
-                del block   # stays cached in the allocator as one segment
+                try:
+                    block = torch.empty(reserve, dtype=torch.uint8, device=self.device)
+                    del block   # stays cached in the allocator as one segment
+                except torch.OutOfMemoryError:
+                    # ranks sharing the device reserve at the same time: the free memory read
+                    # above may already be gone - the arena is only a head start, go without
+                    pass
         pool = staging.io_pool()
         list(pool.map(lambda _: None, range(pool._max_workers)))   # spawn the workers now
         staging.copy_streams(self.device)
